@@ -1,0 +1,257 @@
+/*
+ * wsgpu.h — C ABI of the MI355X-native RFC 6455 frame codec (libwsgpu.so).
+ *
+ * This is the drop-in boundary for snf4j-websocket's frame codec stages.  A JNI
+ * shim binds these entry points from Java; nothing here
+ * depends on jni.h, torch or any C++ type.  All functions return an int status
+ * (0 = success, <0 = API error); protocol errors found in the data are NOT API
+ * errors — they are reported per session in wsg_session_result, exactly like
+ * the reference reports them per session by throwing InvalidFrameException.
+ *
+ * Reference interfaces replaced (paths relative to the snf4j tree):
+ *   FrameDecoder        snf4j-websocket/.../websocket/frame/FrameDecoder.java:41-403
+ *                       (IBaseDecoder<ByteBuffer,Frame>, core/codec/IBaseDecoder.java:49-94)
+ *   FrameUtf8Validator  snf4j-websocket/.../websocket/frame/FrameUtf8Validator.java:40-100
+ *   Utf8 (DFA)          snf4j-websocket/.../websocket/frame/Utf8.java:28-102
+ *   FrameEncoder        snf4j-websocket/.../websocket/frame/FrameEncoder.java:41-136
+ *                       (IEncoder<Frame,ByteBuffer>, core/codec/IEncoder.java:44-67)
+ * Install point kept unchanged: IWebSocketSessionConfig.switchDecoders/switchEncoders
+ *   (IWebSocketSessionConfig.java:123,133; DefaultWebSocketSessionConfig.java:271-281),
+ *   pipeline keys "ws-decoder"/"ws-encoder"/"ws-utf8-validator" (IWebSocketSessionConfig.java:61-75).
+ */
+#ifndef WSGPU_H
+#define WSGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WSG_ABI_VERSION 1
+
+/* ------------------------------------------------------------------------ */
+/* Per-frame / per-session status codes.                                     */
+/* Each code names the exact InvalidFrameException message the reference     */
+/* throws (FrameDecoder.java / FrameUtf8Validator.java line cited); the      */
+/* numeric argument of the message is wsg_session_result.detail.             */
+/* ------------------------------------------------------------------------ */
+typedef enum wsg_status {
+    WSG_OK = 0,
+    WSG_E_OPCODE = 1,          /* "Unexpected opcode value (%d)"                      FrameDecoder.java:200 */
+    WSG_E_RSV = 2,             /* "Unexpected non-zero RSV bits (%d)"                 :207 */
+    WSG_E_MASKING = 3,         /* "Unexpected payload masking"                        :215 */
+    WSG_E_FRAG_CONTROL = 4,    /* "Fragmented control frame"                          :220 */
+    WSG_E_CONTROL_LEN = 5,     /* "Invalid payload length (%d) in control frame"      :223 */
+    WSG_E_CLOSE_LEN = 6,       /* "Invalid payload length (%d) in close frame"        :226 */
+    WSG_E_CONT_OUTSIDE = 7,    /* "Continuation frame outside fragmented message"     :231 */
+    WSG_E_NONCONT_INSIDE = 8,  /* "Non-continuation frame while inside fragmented massage" :235 */
+    WSG_E_MIN_LEN = 9,         /* "Invalid minimal payload length"                    :241,250 */
+    WSG_E_MAX_PAYLOAD = 10,    /* "Invalid maximum payload length"                    :247 */
+    WSG_E_TOO_LONG = 11,       /* "Maximum frame length (%d) has been exceeded"       :255 */
+    WSG_E_CLOSE_STATUS = 12,   /* "Invalid close frame status code (%d)"              :127 */
+    WSG_E_CLOSE_REASON = 13,   /* "Invalid close frame reason value: bytes are not UTF-8" :131 (1007) */
+    WSG_E_TEXT_UTF8 = 14,      /* "Invalid text frame payload: bytes are not UTF-8"   FrameUtf8Validator.java:31 (1007) */
+    WSG_E_NEG_LEN = 15,        /* "Negative payload length (%d)"        FrameDecoder.available :390 */
+    WSG_E_EXT_LEN = 16,        /* "Extended payload length (%d) > %d"   FrameDecoder.available :393
+                                  (detail = plen, detail2 = Integer.MAX_VALUE - need) */
+    WSG_E_BATCH = 17           /* frame extent in the batch does not match its header
+                                  (a caller bug: never produced by the reference) */
+} wsg_status;
+
+/* API return codes (<0). */
+#define WSG_API_OK 0
+#define WSG_API_EINVAL (-1)
+#define WSG_API_EHIP (-2)
+#define WSG_API_ENOMEM (-3)
+#define WSG_API_ERANGE (-4)
+
+/* Close codes the reference writes with writenf(new CloseFrame(code)). */
+#define WSG_CLOSE_PROTOCOL_ERROR 1002  /* CloseFrame.PROTOCOL_ERROR */
+#define WSG_CLOSE_NON_UTF8 1007        /* CloseFrame.NON_UTF8 */
+
+/* RFC 6455 opcodes (Opcode.java:33-98). */
+#define WSG_OP_CONTINUATION 0
+#define WSG_OP_TEXT 1
+#define WSG_OP_BINARY 2
+#define WSG_OP_CLOSE 8
+#define WSG_OP_PING 9
+#define WSG_OP_PONG 10
+
+/* Decoder configuration: the FrameDecoder constructor arguments
+ * (FrameDecoder.java:76) plus whether the "ws-utf8-validator" stage
+ * (FrameUtf8Validator) is fused into the decode pass. */
+typedef struct wsg_decoder_cfg {
+    int32_t client_mode;       /* FrameDecoder.clientMode: 1 = expect unmasked frames */
+    int32_t allow_extensions;  /* FrameDecoder.allowExtensions: RSV bits allowed */
+    int64_t max_payload_len;   /* FrameDecoder.maxPayloadLen */
+    int32_t validate_utf8;     /* 1 = FrameUtf8Validator runs after the decoder */
+    int32_t reserved;
+} wsg_decoder_cfg;
+
+/* Per-session carry state, passed explicitly in and out of every batch.
+ * It is the part of FrameDecoder / FrameUtf8Validator state that survives a
+ * complete frame (FrameDecoder.java:49,63; FrameUtf8Validator.java:42):
+ *   fragmentation : FrameDecoder.fragmentation
+ *   text_open     : FrameUtf8Validator.context != null (inside a text message)
+ *   closed        : FrameDecoder.closed (all further input is swallowed)
+ *   tail[0..tail_len) : the last (<=3) payload bytes of the open text message,
+ *                   which determine the UTF-8 DFA state carried across fragments.
+ * Partial frames never enter a batch: the host buffers them (FrameDecoder.java:276-283). */
+typedef struct wsg_session_state {
+    uint8_t fragmentation;
+    uint8_t text_open;
+    uint8_t closed;
+    uint8_t tail_len;
+    uint8_t tail[3];
+    uint8_t reserved;
+} wsg_session_state; /* 8 bytes */
+
+/* One decoded frame (the device-side form of Frame, Frame.java:33-143). */
+typedef struct wsg_frame_desc {
+    uint64_t payload_off;  /* byte offset of the unmasked payload in payload_out (16-B aligned) */
+    uint32_t payload_len;  /* payload length */
+    uint8_t opcode;        /* Opcode value */
+    uint8_t flags;         /* bit7 = FIN, bits4..6 = RSV (Frame.getRsvBits()<<4), bit0 = was masked */
+    uint16_t status;       /* wsg_status of this frame (meaningful up to the session's first error) */
+} wsg_frame_desc; /* 16 bytes */
+
+/* Per-session outcome of one batch. Frames [first, first+n_delivered) of the
+ * session are delivered to the handler in order; if error != 0, frame
+ * first+n_delivered failed with that error, the session wrote
+ * CloseFrame(close_code) and latched closed (FrameDecoder.java:92-102). */
+typedef struct wsg_session_result {
+    uint32_t n_delivered;
+    uint16_t error;       /* wsg_status */
+    uint16_t close_code;  /* 1002, 1007, or 0 */
+    int64_t detail;       /* numeric argument of the exception message */
+} wsg_session_result; /* 16 bytes */
+
+/* One frame to encode (FrameEncoder.encode input: a Frame + its mask key). */
+typedef struct wsg_encode_frame {
+    uint64_t payload_off;  /* offset of the (unmasked) payload in the payload buffer */
+    uint32_t payload_len;
+    uint8_t opcode;
+    uint8_t flags;         /* bit7 = FIN, bits4..6 = RSV */
+    uint8_t reserved[2];
+    uint8_t mask[4];       /* mask key (client mode); the reference draws it from
+                              java.util.Random (FrameEncoder.java:43,111) — here it is injected */
+    uint32_t reserved2;
+} wsg_encode_frame; /* 24 bytes */
+
+typedef struct wsg_ctx wsg_ctx;
+
+/* ---------------- context ---------------- */
+int wsg_version(void);
+/* Open a context on HIP device `device`. `stream` is a hipStream_t (NULL = the
+ * context creates its own non-blocking stream). */
+int wsg_open(int device, void* stream, wsg_ctx** out);
+int wsg_close(wsg_ctx* ctx);
+int wsg_set_stream(wsg_ctx* ctx, void* stream);
+const char* wsg_last_error(wsg_ctx* ctx);
+/* Pre-size device workspace so later batch calls do no allocation (graph-capture safe). */
+int wsg_reserve(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions);
+int wsg_sync(wsg_ctx* ctx);
+
+/* Kernel timing (hipEvents recorded around each kernel on the ctx stream). */
+int wsg_set_timing(wsg_ctx* ctx, int enable);
+/* out_ms[i] = accumulated milliseconds of kernel i since the last reset, out_count[i] = launches.
+ * Kernel ids: see wsg_kernel_name(). Syncs the stream. */
+int wsg_get_timing(wsg_ctx* ctx, double* out_ms, uint64_t* out_count, int max_kernels);
+int wsg_reset_timing(wsg_ctx* ctx);
+const char* wsg_kernel_name(int kernel_id);
+int wsg_num_kernels(void);
+
+/* ---------------- decode (FrameDecoder [+ FrameUtf8Validator]) ---------------- */
+/* Upper bound of payload_out bytes for a batch. */
+uint64_t wsg_decode_payload_bound(uint64_t wire_len, uint64_t n_frames);
+
+/* Device-resident batch decode; every pointer is a device pointer; the work is
+ * enqueued on the ctx stream and the call returns without synchronising.
+ *   wire[0..wire_len)            concatenated wire bytes of all sessions
+ *   frame_off[0..n_frames]       frame k occupies wire[frame_off[k], frame_off[k+1]),
+ *                                ascending; each entry is what FrameDecoder.available()
+ *                                returned for a complete frame (FrameDecoder.java:357-401)
+ *   session_first[0..n_sessions] session s owns frames [session_first[s], session_first[s+1])
+ *   state[n_sessions]            carry state in / out
+ *   payload_out                  unmasked payloads, 16-B aligned slot per frame
+ *   desc_out[n_frames], result_out[n_sessions]
+ * Equivalent to calling FrameDecoder.decode (FrameDecoder.java:180-288) once per
+ * frame per session, followed by FrameUtf8Validator.decode (FrameUtf8Validator.java:59-98). */
+int wsg_decode_batch_device(wsg_ctx* ctx, const wsg_decoder_cfg* cfg,
+                            const uint8_t* wire, uint64_t wire_len,
+                            const uint64_t* frame_off, uint64_t n_frames,
+                            const uint32_t* session_first, uint32_t n_sessions,
+                            wsg_session_state* state,
+                            uint8_t* payload_out, uint64_t payload_cap,
+                            wsg_frame_desc* desc_out, wsg_session_result* result_out);
+
+/* Same contract with host pointers (pinned or pageable): H2D, decode, D2H,
+ * synchronise. This is the end-to-end (PCIe-inclusive) path of the JNI shim. */
+int wsg_decode_batch_host(wsg_ctx* ctx, const wsg_decoder_cfg* cfg,
+                          const uint8_t* wire, uint64_t wire_len,
+                          const uint64_t* frame_off, uint64_t n_frames,
+                          const uint32_t* session_first, uint32_t n_sessions,
+                          wsg_session_state* state,
+                          uint8_t* payload_out, uint64_t payload_cap,
+                          wsg_frame_desc* desc_out, wsg_session_result* result_out);
+
+/* FrameDecoder.available(ISession, byte[], off, len) for a decoder with no
+ * pending partial payload (FrameDecoder.java:357-401): returns 0 if the header
+ * is incomplete, the full frame length if available, otherwise len.  On the
+ * u64-length errors it returns -1 and sets *err (WSG_E_NEG_LEN / WSG_E_EXT_LEN)
+ * and *detail / *detail2.  Host-only, no device work. */
+int64_t wsg_frame_available(const uint8_t* buf, uint64_t len, int32_t* err,
+                            int64_t* detail, int64_t* detail2);
+
+/* Header-rule check of one (possibly partial) frame whose header is complete:
+ * applies FrameDecoder.decode's rules that need only the header
+ * (FrameDecoder.java:197-256) given the fragmentation flag. Returns wsg_status,
+ * sets *detail.  Used by the host to fail early on partial frames, as the
+ * reference does, before the payload is complete. Host-only. */
+int32_t wsg_check_header(const wsg_decoder_cfg* cfg, int fragmentation,
+                         const uint8_t* buf, uint64_t len, int64_t* detail);
+
+/* ---------------- encode (FrameEncoder) ---------------- */
+/* Exact wire length of a frame (FrameEncoder.length(), FrameEncoder.java:122-135). */
+uint64_t wsg_encoded_length(uint32_t payload_len, int client_mode);
+
+/* Device-resident batch encode (FrameEncoder.encode, FrameEncoder.java:69-120).
+ *   payload[...]                 unmasked payload bytes, frames reference them by offset
+ *   frames[n_frames]             frames in session order
+ *   session_first[0..n_sessions] session s owns frames [session_first[s], session_first[s+1])
+ *   closed[n_sessions]           FrameEncoder.closed carry in / out (a CLOSE frame latches it
+ *                                and every later frame of the session is dropped, :71-76)
+ *   wire_out                     concatenated wire bytes (no padding between frames)
+ *   wire_off[0..n_frames]        frame k occupies wire_out[wire_off[k], wire_off[k+1]);
+ *                                a dropped frame has an empty range
+ *   client_mode                  1 = mask with frames[k].mask (clientMode)  */
+int wsg_encode_batch_device(wsg_ctx* ctx, int client_mode,
+                            const uint8_t* payload, uint64_t payload_len,
+                            const wsg_encode_frame* frames, uint64_t n_frames,
+                            const uint32_t* session_first, uint32_t n_sessions,
+                            uint8_t* closed,
+                            uint8_t* wire_out, uint64_t wire_cap, uint64_t* wire_off);
+
+int wsg_encode_batch_host(wsg_ctx* ctx, int client_mode,
+                          const uint8_t* payload, uint64_t payload_len,
+                          const wsg_encode_frame* frames, uint64_t n_frames,
+                          const uint32_t* session_first, uint32_t n_sessions,
+                          uint8_t* closed,
+                          uint8_t* wire_out, uint64_t wire_cap, uint64_t* wire_off);
+
+/* ---------------- synthetic workloads (bench / tests only) ---------------- */
+/* Fill a device batch of uniform frames: n_frames frames of payload_len bytes,
+ * frame k at k*frame_len in wire (frame_len = wsg_encoded_length(payload_len, masked)),
+ * opcode/fin/masked as given, payload bytes from splitmix64(seed ^ session) where
+ * session = k / frames_per_session; text = 1 generates valid UTF-8 (mixed 1-4 byte
+ * code points, ~70% ASCII bytes).  Also fills frame_off and session_first. */
+int wsg_synth_uniform(wsg_ctx* ctx, uint64_t seed, uint64_t n_frames, uint32_t payload_len,
+                      uint32_t frames_per_session, int opcode, int masked, int text,
+                      uint8_t* wire, uint64_t* frame_off, uint32_t* session_first);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WSGPU_H */

@@ -1,0 +1,445 @@
+"""Generate the golden fixtures for the frame codec from the reference's own tests.
+
+Every vector below transcribes one assertion of snf4j-websocket's JUnit tests
+(paths relative to snf4j-websocket/src/test/java/org/snf4j/websocket/): the
+input bytes are rebuilt with the same frame-description mini-language the
+reference tests use (FrameDecoderTest.frame(), :117-173) and the expected
+outcome is the value the reference test asserts.  The reference itself cannot
+run here (pure Java, no JDK), so these assertions are what pins the oracle.
+
+Run:  python tests/golden/make_golden.py   (writes tests/golden/*.json)
+"""
+from __future__ import annotations
+
+import base64
+import json
+import os
+import struct
+import zlib
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+MASK = (1, 2, 3, 4)  # FrameDecoderTest.mask, :49
+
+
+def fill_bytes(c: str, n: int, masked: bool) -> bytearray:
+    """FrameDecoderTest.bytes(c, len, masked), :96-113."""
+    b = bytearray(n)
+    for i in range(n):
+        b[i] = (i & 0xFF) if c == "*" else ord(c)
+        if masked:
+            b[i] ^= MASK[i % 4]
+    return b
+
+
+def frame(text: str, off: int = 0) -> bytes:
+    """FrameDecoderTest.frame(text, off), :117-173: "FRRR<op>|<len>|<M|m>|<fill>|"."""
+    s = text.split("|")
+    out = bytearray(b"\xff" * off)
+    s0 = s[0]
+    b = 0
+    if s0[0] == "F":
+        b |= 0x80
+    if s0[1] == "R":
+        b |= 0x40
+    if s0[2] == "R":
+        b |= 0x20
+    if s0[3] == "R":
+        b |= 0x10
+    op = int(s0[4:])
+    b |= op
+    out.append(b)
+    ln = int(s[1])
+    m = 0x80 if s[2][0] == "M" else 0
+    if ln < 126:
+        out.append(ln | m)
+    elif ln <= 0xFFFF:
+        out.append(126 | m)
+        out += struct.pack(">H", ln)
+    else:
+        out.append(127 | m)
+        out += struct.pack(">Q", ln & 0xFFFFFFFFFFFFFFFF)
+    if m:
+        out += bytes(MASK)
+    c = s[3][0]
+    if c != "-":
+        payload = fill_bytes(c, ln, bool(m))
+        if op == 8 and len(payload) > 1:
+            payload[0] = 3
+            payload[1] = 0xE8
+            if m:
+                payload[0] ^= MASK[0]
+                payload[1] ^= MASK[1]
+        out += payload
+    return bytes(out)
+
+
+def frame_len(ln: int, mask: bool) -> int:
+    """FrameDecoderTest.frameLen, :57-71."""
+    n = 2 + (4 if mask else 0)
+    if ln > 0xFFFF:
+        n += 8
+    elif ln > 125:
+        n += 2
+    return n + ln
+
+
+def hx(b: bytes) -> str:
+    """Byte strings: hex up to 128 bytes, else "z:" + base64(zlib) (see fixtures.unhex)."""
+    b = bytes(b)
+    if len(b) <= 128:
+        return b.hex()
+    return "z:" + base64.b64encode(zlib.compress(b, 9)).decode()
+
+
+def expect_frame(op, fin, rsv, payload: bytes):
+    return {"frame": {"opcode": op, "fin": fin, "rsv": rsv, "payload": hx(payload)}}
+
+
+def expect_error(msg, close_code=1002):
+    return {"error": msg, "close_code": close_code}
+
+
+OPS = {"CONTINUATION": 0, "TEXT": 1, "BINARY": 2, "CLOSE": 8, "PING": 9, "PONG": 10}
+SRC_DEC = "frame/FrameDecoderTest.java"
+
+
+def builder_kats():
+    """FrameDecoderTest.testFrame, :189-219 — pins the frame() restatement itself."""
+    cases = [
+        ("FRRR1|0|M|*|", [0xf1, 0x80, 1, 2, 3, 4]),
+        ("fRRR1|0|m|*|", [0x71, 0]),
+        ("frRR15|0|m|*|", [0x3f, 0]),
+        ("fRrR0|0|m|*|", [0x50, 0]),
+        ("fRRr15|0|m|*|", [0x6f, 0]),
+        ("fRRr2|1|m|*|", [0x62, 1, 0]),
+        ("fRRr2|1|M|*|", [0x62, 0x81, 1, 2, 3, 4, 0 ^ 1]),
+        ("fRRr2|2|M|*|", [0x62, 0x82, 1, 2, 3, 4, 0 ^ 1, 1 ^ 2]),
+        ("fRRr2|3|M|*|", [0x62, 0x83, 1, 2, 3, 4, 0 ^ 1, 1 ^ 2, 2 ^ 3]),
+        ("fRRr2|4|M|*|", [0x62, 0x84, 1, 2, 3, 4, 0 ^ 1, 1 ^ 2, 2 ^ 3, 3 ^ 4]),
+        ("fRRr2|5|M|*|", [0x62, 0x85, 1, 2, 3, 4, 0 ^ 1, 1 ^ 2, 2 ^ 3, 3 ^ 4, 4 ^ 1]),
+        ("fRRr2|2|m|*|", [0x62, 2, 0, 1]),
+        ("fRRr2|5|m|*|", [0x62, 5, 0, 1, 2, 3, 4]),
+        ("fRRr2|125|m|-|", [0x62, 0x7d]),
+        ("fRRr2|125|M|-|", [0x62, 0xfd, 1, 2, 3, 4]),
+        ("fRRr2|126|m|-|", [0x62, 0x7e, 0, 0x7e]),
+        ("fRRr2|126|M|-|", [0x62, 0xfe, 0, 0x7e, 1, 2, 3, 4]),
+        ("fRRr2|65535|m|-|", [0x62, 0x7e, 0xff, 0xff]),
+        ("fRRr2|65535|M|-|", [0x62, 0xfe, 0xff, 0xff, 1, 2, 3, 4]),
+        ("fRRr2|65536|m|-|", [0x62, 0x7f, 0, 0, 0, 0, 0, 1, 0, 0]),
+        ("fRRr2|65536|M|-|", [0x62, 0xff, 0, 0, 0, 0, 0, 1, 0, 0, 1, 2, 3, 4]),
+        ("fRRr2|9223372036854775807|m|-|", [0x62, 0x7f, 0x7f, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff]),
+        ("fRRr2|9223372036854775807|M|-|",
+         [0x62, 0xff, 0x7f, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 0xff, 1, 2, 3, 4]),
+    ]
+    out = []
+    for t, exp in cases:
+        got = frame(t)
+        assert list(got) == exp, (t, list(got), exp)
+        out.append({"src": SRC_DEC + ":189-219", "spec": t, "bytes": hx(got)})
+    return out
+
+
+def decode_kats():
+    """Sequences of decode() calls on one decoder, with the asserted outcome of each."""
+    V = []
+
+    def seq(src, cm, ext, maxp, steps):
+        V.append({"src": src, "client_mode": cm, "allow_extensions": ext, "max_payload": maxp,
+                  "steps": steps})
+
+    def one(src, data, expected, cm, ext=True, maxp=0x20000):
+        seq(src, cm, ext, maxp, [{"data": hx(data), **expected}])
+
+    z = b""
+    # testDecodeFinRsv :397-426
+    s = SRC_DEC + ":397-426"
+    one(s, frame("FRRR1|0|m|-|"), expect_frame(1, True, 7, z), True)
+    one(s, frame("fRRR1|0|m|-|"), expect_frame(1, False, 7, z), True)
+    one(s, frame("FrRR1|0|m|-|"), expect_frame(1, True, 3, z), True)
+    one(s, frame("FrrR1|0|m|-|"), expect_frame(1, True, 1, z), True)
+    one(s, frame("frrr1|0|m|-|"), expect_frame(1, False, 0, z), True)
+    for op in (8, 9, 10):
+        one(s, frame(f"frrr{op}|0|m|-|"), expect_error("Fragmented control frame"), True)
+    seq(s, True, True, 0x20000, [
+        {"data": hx(frame("FRRR1|0|m|-|")), **expect_frame(1, True, 7, z)},
+        {"data": hx(frame("Frrr1|0|m|-|")), **expect_frame(1, True, 0, z)}])
+    seq(s, True, False, 0x20000, [
+        {"data": hx(frame("Frrr1|0|m|-|")), **expect_frame(1, True, 0, z)}])
+    one(s, frame("FRrr1|0|m|-|"), expect_error("Unexpected non-zero RSV bits (4)"), True, ext=False)
+
+    # testDecodeOpcode :428-446
+    s = SRC_DEC + ":428-446"
+    seq(s, True, True, 0x20000, [
+        {"data": hx(frame("fRrR1|0|m|-|")), **expect_frame(1, False, 5, z)},
+        {"data": hx(frame("fRrR0|0|m|-|")), **expect_frame(0, False, 5, z)}])
+    one(s, frame("FrrR2|0|m|-|"), expect_frame(2, True, 1, z), True)
+    one(s, frame("FrrR8|0|m|-|"), expect_frame(8, True, 1, z), True)
+    one(s, frame("FRrR9|0|m|-|"), expect_frame(9, True, 5, z), True)
+    one(s, frame("FRRR10|0|m|-|"), expect_frame(10, True, 7, z), True)
+    for i in list(range(3, 8)) + list(range(11, 16)):
+        one(s, frame(f"FRRR{i}|0|m|-|"), expect_error(f"Unexpected opcode value ({i})"), True)
+
+    # testDecodeLengthMask :448-513
+    s = SRC_DEC + ":448-513"
+
+    def star(n):
+        return bytes(i & 0xFF for i in range(n))
+
+    for n in (0, 1, 125, 126, 65535, 65536):
+        fill = "-" if n == 0 else "*"
+        one(s, frame(f"FRRR2|{n}|M|{fill}|"), expect_frame(2, True, 7, star(n)), False)
+        one(s, frame(f"FRRR2|{n}|m|{fill}|"), expect_frame(2, True, 7, star(n)), True)
+    one(s, frame("FRRR2|0|M|*|"), expect_error("Unexpected payload masking"), True)
+    one(s, frame("FRRR2|0|m|*|"), expect_error("Unexpected payload masking"), False)
+    one(s, frame("FRRR8|0|M|*|"), expect_frame(8, True, 7, z), False)
+    one(s, frame("FRRR8|1|M|*|"), expect_error("Invalid payload length (1) in close frame"), False)
+    one(s, frame("FRRR8|2|M|*|"), expect_frame(8, True, 7, bytes([3, 0xe8])), False)
+    b = bytearray(star(125))
+    b[0], b[1] = 3, 0xE8
+    one(s, frame("FRRR8|125|M|*|"), expect_frame(8, True, 7, bytes(b)), False)
+    one(s, frame("FRRR9|125|M|*|"), expect_frame(9, True, 7, star(125)), False)
+    one(s, frame("FRRR10|125|M|*|"), expect_frame(10, True, 7, star(125)), False)
+    for i in (8, 9, 10):
+        one(s, frame(f"FRRR{i}|126|M|-|"), expect_error("Invalid payload length (126) in control frame"),
+            False)
+    one(s, bytes([0xf2, 126, 0, 125]), expect_error("Invalid minimal payload length"), True)
+    one(s, bytes([0xf2, 127, 0, 0, 0, 0, 0, 0, 0, 125]), expect_error("Invalid minimal payload length"),
+        True)
+    one(s, bytes([0xf2, 127, 0, 0, 0, 0, 0, 0, 0xff, 0xff]),
+        expect_error("Invalid minimal payload length"), True)
+    for hi in ([0xff] * 8, [0x80] + [0xff] * 7, [0x7f] + [0xff] * 7, [0, 0, 0, 0, 0x80, 0xff, 0xff, 0xff]):
+        one(s, bytes([0xf2, 127] + hi), expect_error("Invalid maximum payload length"), True)
+    one(s, bytes([0xf2, 127, 0, 0, 0, 0, 0, 2, 0, 1]),
+        expect_error("Maximum frame length (131072) has been exceeded"), True)
+    one(s, frame("FRRR2|131072|m|*|"), expect_frame(2, True, 7, star(131072)), True)
+
+    # testDecodeFragemntation :566-617  (decoder: FrameDecoder(true, true, 0x20000))
+    s = SRC_DEC + ":566-617"
+
+    def frag(op, fin, err=None):
+        name = (("F" if fin else "f") + "RRR" + str(OPS[op]) + "|0|m|-|")
+        st = {"data": hx(frame(name))}
+        if err:
+            st.update(expect_error(err))
+        else:
+            st.update(expect_frame(OPS[op], fin, 7, z))
+        return st
+
+    ctl = [frag("CLOSE", True), frag("PING", True), frag("PONG", True)]
+    COUT = "Continuation frame outside fragmented message"
+    NINS = "Non-continuation frame while inside fragmented massage"
+    seq(s, True, True, 0x20000,
+        [frag("TEXT", True), frag("BINARY", True)] + ctl + [frag("CONTINUATION", True, COUT)])
+    for second in (("TEXT", True), ("BINARY", True), ("TEXT", False), ("BINARY", False)):
+        seq(s, True, True, 0x20000, [frag("TEXT", False), frag(second[0], second[1], NINS)])
+    seq(s, True, True, 0x20000, [frag("TEXT", False)] + ctl)
+    seq(s, True, True, 0x20000,
+        [frag("TEXT", False), frag("CONTINUATION", False)] + ctl + [frag("TEXT", True, NINS)])
+    for second in (("BINARY", True), ("TEXT", False), ("BINARY", False)):
+        seq(s, True, True, 0x20000,
+            [frag("TEXT", False), frag("CONTINUATION", False), frag(second[0], second[1], NINS)])
+    seq(s, True, True, 0x20000,
+        [frag("TEXT", False), frag("CONTINUATION", False), frag("CONTINUATION", True),
+         frag("TEXT", True), frag("BINARY", True)] + ctl)
+
+    # testSplittedFrame :633-676 (partial frames across decode() calls)
+    s = SRC_DEC + ":633-676"
+    b = frame("FRRR2|100|m|*|")
+    b2 = b[50:]
+    b3, b4 = b2[: len(b2) // 2], b2[len(b2) // 2:]
+    seq(s, True, True, 0x20000, [
+        {"data": hx(b[:50]), "none": True},
+        {"data": hx(b2), **expect_frame(2, True, 7, star(100))},
+        {"data": hx(frame("FRRR2|1|m|*|")), **expect_frame(2, True, 7, star(1))},
+        {"data": hx(b[:50]), "none": True},
+        {"data": hx(b3), "none": True},
+        {"data": hx(b4), **expect_frame(2, True, 7, star(100))},
+        {"data": hx(frame("FRRR2|1|m|*|")), **expect_frame(2, True, 7, star(1))}])
+    b = frame("FRRR2|100|M|*|")
+    seq(s, False, True, 0x20000, [
+        {"data": hx(b[:50]), "none": True},
+        {"data": hx(b[50:]), **expect_frame(2, True, 7, star(100))},
+        {"data": hx(frame("FRRR2|1|M|*|")), **expect_frame(2, True, 7, star(1))}])
+
+    # testCloseFrame :698-740
+    s = SRC_DEC + ":698-740"
+    one(s, frame("FRRR8|0|m|*|"), expect_frame(8, True, 7, z), True)
+    base = bytearray(frame("FRRR8|2|m|*|"))
+    i = len(base) - 2
+    for st0, st1, res in ((0, 0, "Invalid close frame status code (0)"),
+                          (0xff, 0xff, "Invalid close frame status code (65535)"),
+                          (3, 0xe7, "Invalid close frame status code (999)"),
+                          (3, 0xe8, None), (3, 0xe9, None), (0x13, 0x87, None),
+                          (0x13, 0x88, "Invalid close frame status code (5000)")):
+        f = bytearray(base)
+        f[i], f[i + 1] = st0, st1
+        one(s, bytes(f), expect_error(res) if res else expect_frame(8, True, 7, bytes([st0, st1])), True)
+    f = bytearray(frame("FRRR8|5|m|*|"))
+    i = len(f) - 5
+    f[i:i + 5] = bytes([3, 0xe8, 0xdf, 0xdf, 0xbf])
+    one(s, bytes(f), expect_error("Invalid close frame reason value: bytes are not UTF-8", 1007), True)
+
+    # testClosedDecoder :742-762
+    s = SRC_DEC + ":742-762"
+    f = bytearray(frame("FRRR8|2|m|*|"))
+    f[-2], f[-1] = 0, 0
+    seq(s, True, True, 0x20000, [
+        {"data": hx(f), **expect_error("Invalid close frame status code (0)")},
+        {"data": hx(f), "none": True},
+        {"available": hx(bytes(f) + bytes(len(f))), "expect": 2 * len(f)}])
+    return V
+
+
+def available_kats():
+    """FrameDecoderTest.testAvailableArray :282-367 and testSplittedFrameAvailable :678-696."""
+    s = SRC_DEC + ":282-367"
+    cases = []
+    for off in (0, 5):
+        for n in (0, 1, 125, 126, 65535, 65536):
+            for m in ("M", "m"):
+                data = frame(f"FRRR1|{n}|{m}|-|", off)
+                cases.append({"src": s, "data_spec": f"FRRR1|{n}|{m}|-|", "off": off,
+                              "expected_len": frame_len(n, m == "M"), "payload_len": n})
+    big = []
+    d = frame_len(0x7FFFFFFF, True) - 0x7FFFFFFF  # 14
+    big.append({"src": s, "data": hx(frame(f"FRRR1|{0x7FFFFFFF - d}|M|-|")),
+                "len": frame_len(0x7FFFFFFF - d, True), "expect": frame_len(0x7FFFFFFF - d, True)})
+    big.append({"src": s, "data": hx(frame(f"FRRR1|{0x7FFFFFFF - d}|M|-|")),
+                "len": 0x7FFFFFFF, "expect": 0x7FFFFFFF})
+    big.append({"src": s, "data": hx(frame(f"FRRR1|{0x7FFFFFFF - d + 1}|M|-|")),
+                "len": 0x7FFFFFFF, "error": "Extended payload length (2147483634) > 2147483633"})
+    big.append({"src": s, "data": hx(frame(f"FRRR1|{0x7FFFFFFFFFFFFFFF - d}|M|-|")),
+                "len": 0x7FFFFFFF,
+                "error": "Extended payload length (9223372036854775793) > 2147483633"})
+    f = bytearray(frame(f"FRRR1|{0x7FFFFFFFFFFFFFFF}|M|-|"))
+    f[2] = 0xFF
+    big.append({"src": s, "data": hx(f), "len": 0x7FFFFFFF, "error": "Negative payload length (-1)"})
+    # Java long/int overflow in available(): need += plen wraps to 0 (FrameDecoder.java:392-395)
+    big.append({"src": s, "data": hx(frame(f"FRRR1|{0x7FFFFFFFFFFFFFFF - d + 1}|M|-|")),
+                "len": 0x7FFFFFFF, "expect": 0})
+
+    # testSplittedFrameAvailable :678-696 (decoder in client mode, pending payload)
+    s2 = SRC_DEC + ":678-696"
+    b = frame("FRRR2|100|m|*|")
+    sp1 = (b[: len(b) // 2], b[len(b) // 2:])
+    sp2 = (sp1[0][: len(sp1[0]) // 2], sp1[0][len(sp1[0]) // 2:])
+    split = {"src": s2, "first": hx(sp1[0]),
+             "checks": [{"data": hx(sp1[0]), "expect_before": len(sp1[0])},
+                        {"data": "00", "expect": 1},
+                        {"data": hx(sp2[0]), "expect": len(sp2[0])},
+                        {"data": hx(sp1[1]), "expect": len(sp1[1])},
+                        {"data": hx(bytes(len(sp1[1]) + 1)), "expect": len(sp1[1])}]}
+    return {"frames": cases, "big": big, "split": split}
+
+
+def validator_kats():
+    """FrameUtf8ValidatorTest.testDecode :81-133 — the validator stage alone."""
+    s = "frame/FrameUtf8ValidatorTest.java:81-133"
+    NON, OKU, INC, TAIL = "dfdf", "dfbf", "df", "bf"
+    E = "Invalid text frame payload: bytes are not UTF-8"
+
+    def f(op, fin, p, err=None):
+        d = {"opcode": OPS[op], "fin": fin, "payload": p}
+        if err:
+            d["error"] = E
+        return d
+
+    seqs = [
+        [f("CONTINUATION", True, NON), f("BINARY", True, NON), f("CLOSE", True, NON), f("PING", True, NON),
+         f("PONG", True, NON), f("TEXT", True, OKU), f("CONTINUATION", True, NON)],
+        [f("TEXT", True, NON, 1)],
+        [f("TEXT", True, INC, 1)],
+        [f("CONTINUATION", False, NON), f("BINARY", False, NON), f("TEXT", False, INC), f("BINARY", True, NON),
+         f("CLOSE", True, NON), f("PING", True, NON), f("PONG", True, NON), f("CONTINUATION", True, TAIL),
+         f("CONTINUATION", True, NON), f("TEXT", False, INC), f("CONTINUATION", False, TAIL),
+         f("BINARY", True, NON), f("CLOSE", True, NON), f("PING", True, NON), f("PONG", True, NON),
+         f("CONTINUATION", False, INC), f("CONTINUATION", False, ""), f("CONTINUATION", True, TAIL),
+         f("CONTINUATION", True, NON), f("TEXT", False, INC), f("CONTINUATION", True, "", 1)],
+        [f("TEXT", False, INC), f("CONTINUATION", False, ""), f("CONTINUATION", False, OKU, 1)],
+    ]
+    return [{"src": s, "frames": q} for q in seqs]
+
+
+def encoder_kats():
+    """FrameEncoderTest.testEncode :136-207: header layout strings."""
+    s = "frame/FrameEncoderTest.java:136-207"
+
+    def bytes_fill(n, c):  # FrameEncoderTest.bytes(length, fill), :128-134
+        b = bytearray([ord(c)] * n)
+        b[0] = ord(c) + 1
+        b[-1] = ord(c) + 2
+        return bytes(b)
+
+    rows = [(0, True, 0, b""), (0, True, 0, b"A"), (0, True, 0, b"ABCDEFGH"),
+            (7, True, 0, bytes_fill(125, "D")), (4, True, 0, bytes_fill(126, "E")),
+            (2, True, 0, bytes_fill(127, "E")), (0, True, 0, bytes_fill(0xFFFE, "C")),
+            (0, True, 0, bytes_fill(0xFFFF, "C")), (0, True, 0, bytes_fill(0x10000, "D")),
+            (1, False, 0, bytes_fill(100000, "D"))]
+    exp_masked = ["Frrr2M|0|M(4)=", "Frrr2M|1|M(4)=A", "Frrr2M|8|M(4)=ABCDEFGH",
+                  "FRRR2M|125|M(4)=EDDDDDDDDD...DDDDDDDDDF", "FRrr2M|126|126(2)M(4)=FEEEEEEEEE...EEEEEEEEEG",
+                  "FrRr2M|126|127(2)M(4)=FEEEEEEEEE...EEEEEEEEEG",
+                  "Frrr2M|126|65534(2)M(4)=DCCCCCCCCC...CCCCCCCCCE",
+                  "Frrr2M|126|65535(2)M(4)=DCCCCCCCCC...CCCCCCCCCE",
+                  "Frrr2M|127|65536(8)M(4)=EDDDDDDDDD...DDDDDDDDDF",
+                  "frrR2M|127|100000(8)M(4)=EDDDDDDDDD...DDDDDDDDDF"]
+    out = []
+    for cm in (True, False):
+        for (rsv, fin, _, payload), em in zip(rows, exp_masked):
+            e = em if cm else em.replace("M|", "m|", 1).replace("M(4)", "")
+            out.append({"src": s, "client_mode": cm, "opcode": 2, "fin": fin, "rsv": rsv,
+                        "payload": hx(payload), "expect": e})
+    return out
+
+
+def session_kats():
+    """WebSocketSessionTest stream cases (a client decoding server frames: unmasked)."""
+    s = "WebSocketSessionTest.java"
+    out = []
+    out.append({"src": s + ":568-575", "client_mode": True, "max_payload": 65536,
+                "chunks": [hx(bytes([0x82, 0x0A, ord("A")])), hx(b"BCDEFGHI"), hx(b"J")],
+                "frames": [{"opcode": 2, "fin": True, "rsv": 0, "payload": hx(b"ABCDEFGHIJ")}]})
+    out.append({"src": s + ":595-599", "client_mode": True, "max_payload": 65536,
+                "chunks": [hx(bytes([0x80, 0x00]))], "frames": [],
+                "error": "Continuation frame outside fragmented message", "close_code": 1002})
+    out.append({"src": s + ":605-610", "client_mode": True, "max_payload": 65536,
+                "chunks": [hx(bytes([0x80, 0x7F] + [0xFF] * 8))], "frames": [],
+                "error": "Negative payload length (-1)", "close_code": 1002})
+    out.append({"src": s + ":627-631", "client_mode": True, "max_payload": 65536,
+                "chunks": [hx(bytes([0x81, 0x02, 0xDF, 0xDF]))], "frames": [],
+                "error": "Invalid text frame payload: bytes are not UTF-8", "close_code": 1007})
+    out.append({"src": s + ":636-642", "client_mode": True, "max_payload": 65536,
+                "chunks": [hx(bytes([0x88, 0x04, 3, 0xE8, 0xDF, 0xDF]))], "frames": [],
+                "error": "Invalid close frame reason value: bytes are not UTF-8", "close_code": 1007})
+    for maxp, n_ok in ((65536, 65536), (512, 512)):
+        ok = bytes([0x82]) + (bytes([126]) + struct.pack(">H", n_ok) if n_ok <= 0xFFFF
+                              else bytes([127]) + struct.pack(">Q", n_ok)) + bytes(n_ok)
+        n_bad = n_ok + 1
+        bad = bytes([0x82]) + (bytes([126]) + struct.pack(">H", n_bad) if n_bad <= 0xFFFF
+                               else bytes([127]) + struct.pack(">Q", n_bad)) + bytes(n_bad)
+        out.append({"src": s + ":676-708", "client_mode": True, "max_payload": maxp,
+                    "chunks": [hx(ok)], "frames": [{"opcode": 2, "fin": True, "rsv": 0,
+                                                    "payload": hx(bytes(n_ok))}]})
+        out.append({"src": s + ":676-708", "client_mode": True, "max_payload": maxp,
+                    "chunks": [hx(bad)], "frames": [],
+                    "error": f"Maximum frame length ({maxp}) has been exceeded", "close_code": 1002})
+    return out
+
+
+def main():
+    data = {
+        "builder": builder_kats(),
+        "decode": decode_kats(),
+        "available": available_kats(),
+        "validator": validator_kats(),
+        "encoder": encoder_kats(),
+        "session": session_kats(),
+    }
+    for name, obj in data.items():
+        with open(os.path.join(HERE, f"{name}_kat.json"), "w") as fh:
+            json.dump(obj, fh, indent=0, separators=(",", ":"))
+    sizes = {k: os.path.getsize(os.path.join(HERE, f"{k}_kat.json")) for k in data}
+    print(sizes)
+
+
+if __name__ == "__main__":
+    main()
