@@ -1,0 +1,237 @@
+"""Benchmark: device-resident WebSocket frame decode (unmask + UTF-8 validation)
+on MI355X, one process per GPU, sessions sharded across GPUs with no collective.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--payload P]
+
+A step = one pass of the decode pipeline (libwsgpu's HIP kernels) over one batch
+of F synthetic masked frames per GPU resident in HBM.  Default workload: the
+north-star 1-GPU case, 1 M x 4 KiB masked TEXT frames (valid UTF-8, ~70 % ASCII
+bytes) in 1024 sessions, validation on.  Prints ONE JSON line (rank 0).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "WebSocket frame decode GiB/s device-resident at 1/2/4/8 MI355X; % HBM peak"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU")
+    ap.add_argument("--payload", type=int, default=4096)
+    ap.add_argument("--sessions", type=int, default=1024, help="sessions per GPU")
+    ap.add_argument("--binary", action="store_true", help="BINARY frames (unmask only, no UTF-8 work)")
+    ap.add_argument("--no-validate", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
+    ap.add_argument("--e2e", action="store_true", help="also time the pinned host->device->host path")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, seconds):
+    """The oracle (single-threaded C restatement of the reference codec) on a bounded
+    sample of the same workload; test infrastructure, timed beside the GPU."""
+    import numpy as np
+    from oracle import pyoracle
+    pyoracle.build()
+    n = min(args.frames, 16384)
+    fps = max(1, args.frames // args.sessions)
+    wire, off, sf = pyoracle.synth_uniform(1234, n, args.payload, min(fps, n), opcode=2 if args.binary else 1,
+                                           masked=True, text=not args.binary)
+    n_s = len(sf) - 1
+    done, t = 0, 0.0
+    while t < seconds:
+        b = pyoracle.Batch(False, False, 65536, not args.no_validate, n_s)
+        t0 = time.perf_counter()
+        _, _, res = b.decode(wire, off, sf)
+        t += time.perf_counter() - t0
+        assert int(res["error"].max()) == 0
+        done += 1
+    gib = done * int(off[-1]) / t / 2**30
+    return {"value": round(gib, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{n} frames x {args.payload} B ({int(off[-1]) / 1e6:.1f} MB wire) decoded {done}x "
+                      f"in {t:.1f} s by the C restatement of FrameDecoder+FrameUtf8Validator (oracle/, 1 thread; "
+                      f"no JDK on the box, the Java reference is not runnable)"}
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        # the data path has no collective; gloo carries only the barrier and the timing max
+        dist.init_process_group("gloo")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    import snf4j_amd
+    from snf4j_amd._lib import RESULT_DTYPE
+
+    stream = torch.cuda.current_stream(dev)
+    ctx = snf4j_amd.Context(local, stream=stream)
+    F, P = args.frames, args.payload
+    flen = snf4j_amd.encoded_length(P, True)
+    fps = max(1, F // args.sessions)
+    n_s = (F + fps - 1) // fps
+    text = 0 if args.binary else 1
+    opcode = 2 if args.binary else 1
+    wire = torch.empty(F * flen + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(F + 1, dtype=torch.int64, device=dev)
+    sf = torch.empty(n_s + 1, dtype=torch.int32, device=dev)
+    # sessions of rank r are global sessions [r*n_s, (r+1)*n_s): shard by session, own seed
+    ctx.synth_uniform(0x5EED ^ (rank * 0x1000003), F, P, fps, opcode, True, text, wire, off, sf)
+    payload_cap = F * flen + 16 * F + 16
+    payload = torch.empty(payload_cap, dtype=torch.uint8, device=dev)
+    desc = torch.empty(F * 16, dtype=torch.uint8, device=dev)
+    res = torch.empty(n_s * 16, dtype=torch.uint8, device=dev)
+    state = torch.zeros(n_s * 8, dtype=torch.uint8, device=dev)
+    cfg = snf4j_amd.decoder_cfg(False, False, 65536, not args.no_validate)
+    ctx.reserve(F, n_s)
+    wire_bytes = F * flen
+
+    def step():
+        ctx.decode_device(cfg, wire, off, sf, state, payload, desc, res, wire_len=wire_bytes)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    r = res.cpu().numpy().view(RESULT_DTYPE)
+    assert int(r["error"].max()) == 0 and int(r["n_delivered"].sum()) == F, "decode of the synthetic batch failed"
+
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize(dev)
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    ctx.set_timing(False)
+    elapsed = t1 - t0
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    timing = ctx.timing()
+
+    # dominant kernel: k_unmask reads each frame's wire bytes and writes its payload
+    unmask_ms, unmask_n = timing["k_unmask"]
+    avg_unmask_s = unmask_ms / 1e3 / max(1, unmask_n)
+    alg_bytes = wire_bytes + F * P  # per launch: wire read + payload written
+    achieved = alg_bytes / avg_unmask_s / 1e9
+    traffic = None
+    if os.path.exists(args.pmc_json):
+        try:
+            with open(args.pmc_json) as fh:
+                pmc = json.load(fh)
+            key = f"{'binary' if args.binary else 'text'}_{F}x{P}"
+            traffic = pmc.get(key, {}).get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    e2e = None
+    if args.e2e:
+        e2e = e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev)
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args, args.cpu_seconds)
+
+    if rank == 0:
+        total_wire = wire_bytes * world
+        value = total_wire * args.steps / elapsed / 2**30
+        pipe = {k: round(v[0] / max(1, v[1]), 4) for k, v in timing.items() if v[1]}
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic",
+            "config": {
+                "workload": (f"{F} x {P} B masked {'BINARY' if args.binary else 'TEXT'} frames per GPU, "
+                             f"{n_s} sessions per GPU, unmask{'' if args.binary or args.no_validate else ' + UTF-8 validation'}"
+                             f", server-side decode (FrameDecoder+FrameUtf8Validator)"),
+                "frames_per_gpu": F,
+                "payload_bytes": P,
+                "wire_bytes_per_gpu": wire_bytes,
+                "sessions_per_gpu": n_s,
+                "parallelism": f"sessions sharded over {world} GPU(s), one process per GPU, no data-path collective",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": "k_unmask",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes,
+                "avg_launch_ms": round(avg_unmask_s * 1e3, 4),
+            },
+            "pipeline_ms": pipe,
+            "cpu_baseline": cpu,
+        }
+        if e2e:
+            out["e2e_pinned"] = e2e
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+def e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev, reps=5):
+    """Host-resident batch -> pinned H2D -> decode -> D2H of payload+desc: GiB/s of wire."""
+    import torch
+    h_wire = torch.empty(wire_bytes, dtype=torch.uint8).pin_memory()
+    h_wire.copy_(wire[:wire_bytes])
+    h_pay = torch.empty(wire_bytes + 16 * F, dtype=torch.uint8).pin_memory()
+    d_pay = torch.empty(wire_bytes + 16 * F + 16, dtype=torch.uint8, device=dev)
+    d_desc = torch.empty(F * 16, dtype=torch.uint8, device=dev)
+    h_desc = torch.empty(F * 16, dtype=torch.uint8).pin_memory()
+    d_res = torch.empty(n_s * 16, dtype=torch.uint8, device=dev)
+    d_state = torch.zeros(n_s * 8, dtype=torch.uint8, device=dev)
+    d_wire = wire
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        d_wire[:wire_bytes].copy_(h_wire, non_blocking=True)
+        ctx.decode_device(cfg, d_wire, off, sf, d_state, d_pay, d_desc, d_res, wire_len=wire_bytes)
+        h_pay.copy_(d_pay[:h_pay.numel()], non_blocking=True)
+        h_desc.copy_(d_desc, non_blocking=True)
+    torch.cuda.synchronize(dev)
+    t = (time.perf_counter() - t0) / reps
+    return {"GiB_per_s": round(wire_bytes / t / 2**30, 3), "ms_per_batch": round(t * 1e3, 3),
+            "path": "pinned host -> H2D -> decode -> D2H payload+descriptors"}
+
+
+if __name__ == "__main__":
+    main()

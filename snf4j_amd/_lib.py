@@ -1,0 +1,118 @@
+"""ctypes binding of libwsgpu.so (include/wsgpu.h).
+
+The product path is the HIP library: if it is missing this module raises at
+import time — there is no CPU fallback anywhere in snf4j_amd.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import re
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libwsgpu.so")
+HEADER = os.path.join(os.path.dirname(HERE), "include", "wsgpu.h")
+
+
+class WsgError(RuntimeError):
+    pass
+
+
+class DecoderCfg(C.Structure):
+    _fields_ = [("client_mode", C.c_int32), ("allow_extensions", C.c_int32),
+                ("max_payload_len", C.c_int64), ("validate_utf8", C.c_int32), ("reserved", C.c_int32)]
+
+
+class SessionState(C.Structure):
+    _fields_ = [("fragmentation", C.c_uint8), ("text_open", C.c_uint8), ("closed", C.c_uint8),
+                ("tail_len", C.c_uint8), ("tail", C.c_uint8 * 3), ("reserved", C.c_uint8)]
+
+
+class FrameDesc(C.Structure):
+    _fields_ = [("payload_off", C.c_uint64), ("payload_len", C.c_uint32), ("opcode", C.c_uint8),
+                ("flags", C.c_uint8), ("status", C.c_uint16)]
+
+
+class SessionResult(C.Structure):
+    _fields_ = [("n_delivered", C.c_uint32), ("error", C.c_uint16), ("close_code", C.c_uint16),
+                ("detail", C.c_int64)]
+
+
+class EncodeFrame(C.Structure):
+    _fields_ = [("payload_off", C.c_uint64), ("payload_len", C.c_uint32), ("opcode", C.c_uint8),
+                ("flags", C.c_uint8), ("reserved", C.c_uint8 * 2), ("mask", C.c_uint8 * 4),
+                ("reserved2", C.c_uint32)]
+
+
+assert C.sizeof(SessionState) == 8 and C.sizeof(FrameDesc) == 16
+assert C.sizeof(SessionResult) == 16 and C.sizeof(EncodeFrame) == 24
+
+# numpy views of the same records
+try:
+    import numpy as np
+
+    STATE_DTYPE = np.dtype([("fragmentation", "u1"), ("text_open", "u1"), ("closed", "u1"),
+                            ("tail_len", "u1"), ("tail", "u1", (3,)), ("reserved", "u1")])
+    DESC_DTYPE = np.dtype([("payload_off", "<u8"), ("payload_len", "<u4"), ("opcode", "u1"),
+                           ("flags", "u1"), ("status", "<u2")])
+    RESULT_DTYPE = np.dtype([("n_delivered", "<u4"), ("error", "<u2"), ("close_code", "<u2"),
+                             ("detail", "<i8")])
+    ENCODE_DTYPE = np.dtype([("payload_off", "<u8"), ("payload_len", "<u4"), ("opcode", "u1"),
+                             ("flags", "u1"), ("reserved", "u1", (2,)), ("mask", "u1", (4,)),
+                             ("reserved2", "<u4")])
+except ImportError:  # pragma: no cover
+    np = None
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libwsgpu.so not built ({LIB_PATH}); run snf4j_amd.build.build() — "
+                          "the HIP extension is required, there is no CPU fallback")
+    L = C.CDLL(LIB_PATH)
+    p, i32, i64, u32, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint32, C.c_uint64
+    P = C.POINTER
+    sig = {
+        "wsg_version": ([], i32),
+        "wsg_open": ([i32, p, P(p)], i32),
+        "wsg_close": ([p], i32),
+        "wsg_set_stream": ([p, p], i32),
+        "wsg_last_error": ([p], C.c_char_p),
+        "wsg_reserve": ([p, u64, u32], i32),
+        "wsg_sync": ([p], i32),
+        "wsg_set_timing": ([p, i32], i32),
+        "wsg_get_timing": ([p, P(C.c_double), P(u64), i32], i32),
+        "wsg_reset_timing": ([p], i32),
+        "wsg_kernel_name": ([i32], C.c_char_p),
+        "wsg_num_kernels": ([], i32),
+        "wsg_decode_payload_bound": ([u64, u64], u64),
+        "wsg_decode_batch_device": ([p, P(DecoderCfg), p, u64, p, u64, p, u32, p, p, u64, p, p], i32),
+        "wsg_decode_batch_host": ([p, P(DecoderCfg), p, u64, p, u64, p, u32, p, p, u64, p, p], i32),
+        "wsg_frame_available": ([p, u64, P(i32), P(i64), P(i64)], i64),
+        "wsg_check_header": ([P(DecoderCfg), i32, p, u64, P(i64)], i32),
+        "wsg_encoded_length": ([u32, i32], u64),
+        "wsg_encode_batch_device": ([p, i32, p, u64, p, u64, p, u32, p, p, u64, p], i32),
+        "wsg_encode_batch_host": ([p, i32, p, u64, p, u64, p, u32, p, p, u64, p], i32),
+        "wsg_synth_uniform": ([p, u64, u64, u32, u32, i32, i32, i32, p, p, p], i32),
+    }
+    for name, (args, res) in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    return L
+
+
+lib = _load()
+
+
+def header_symbols() -> list[str]:
+    """Every function the C ABI header declares."""
+    with open(HEADER) as fh:
+        text = fh.read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(wsg_[a-z0-9_]+)\s*\(", text)))
+
+
+def check(rc: int, ctx=None):
+    if rc != 0:
+        msg = lib.wsg_last_error(ctx).decode() if ctx else ""
+        raise WsgError(f"libwsgpu error {rc}: {msg}")

@@ -1,0 +1,277 @@
+"""The drop-in codec stages: FrameDecoder / FrameEncoder with the reference's
+interface (same names, argument meaning and error behaviour), executed by the
+HIP kernels of libwsgpu through its C ABI, plus the cross-session batcher that
+feeds many sessions' frames to one GPU launch.
+
+Reference (snf4j-websocket/src/main/java/org/snf4j/websocket/frame/):
+  FrameDecoder.java:41-403       IBaseDecoder<ByteBuffer,Frame>: available() + decode()
+  FrameUtf8Validator.java:40-100 fused into the decode pass (validate_utf8=True)
+  FrameEncoder.java:41-136       IEncoder<Frame,ByteBuffer>
+Errors: the stage writes CloseFrame(code) to the session and raises
+InvalidFrameException(message) exactly where the reference does
+(FrameDecoder.java:92-102, FrameUtf8Validator.java:54-57).
+"""
+from __future__ import annotations
+
+import os
+import struct
+
+import numpy as np
+
+from ._lib import ENCODE_DTYPE, STATE_DTYPE
+from .context import Context, check_header, decoder_cfg, error_message, frame_available
+from .frame import CloseFrame, Frame, InvalidFrameException, Opcode, make_frame
+
+_CLOSE_FOR = {13: CloseFrame.NON_UTF8, 14: CloseFrame.NON_UTF8}
+
+
+def _close_code(err: int) -> int:
+    return _CLOSE_FOR.get(err, CloseFrame.PROTOCOL_ERROR)
+
+
+def _header_len(buf: bytes) -> int:
+    b1 = buf[1]
+    n = 2 + (4 if b1 & 0x80 else 0)
+    ln = b1 & 0x7F
+    return n + (2 if ln == 126 else 8 if ln == 127 else 0)
+
+
+def _frame_total(buf) -> int:
+    """Header + payload length of the frame starting at buf[0] (header complete)."""
+    ln = buf[1] & 0x7F
+    hl = _header_len(buf)
+    if ln == 126:
+        ln = struct.unpack(">H", bytes(buf[2:4]))[0]
+    elif ln == 127:
+        ln = struct.unpack(">Q", bytes(buf[2:10]))[0]
+    return hl + ln
+
+
+def _writenf(session, frame):
+    if session is not None and hasattr(session, "writenf"):
+        session.writenf(frame)
+
+
+def _release(session, data):
+    if session is not None and hasattr(session, "release"):
+        session.release(data)
+
+
+_default_ctx = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+class FrameDecoder:
+    """GPU-backed FrameDecoder (+ the fused "ws-utf8-validator" stage).
+
+    decode() of a complete frame runs one batch on the GPU; for throughput use
+    SessionBatcher, which puts many sessions' frames into one launch.
+    """
+
+    def __init__(self, clientMode: bool, allowExtensions: bool, maxPayloadLen: int, validate_utf8: bool = True,
+                 ctx: Context | None = None):
+        self.cfg = decoder_cfg(clientMode, allowExtensions, maxPayloadLen, validate_utf8)
+        self.ctx = ctx
+        self.state = np.zeros(1, dtype=STATE_DTYPE)
+        self._pending = None  # bytearray of a frame whose payload is incomplete
+        self._need = 0
+
+    def getInboundType(self):
+        return bytes
+
+    def getOutboundType(self):
+        return Frame
+
+    @property
+    def closed(self) -> bool:
+        return bool(self.state[0]["closed"])
+
+    def _protocol_error(self, session, err, detail=0, detail2=0):
+        self.state[0]["closed"] = 1
+        _writenf(session, CloseFrame.of_status(_close_code(err)))
+        return InvalidFrameException(error_message(err, detail, detail2))
+
+    # FrameDecoder.available(ISession, byte[], off, len), :357-401
+    def available(self, session, buffer, off: int = 0, length: int | None = None) -> int:
+        buf = bytes(buffer)[off:]
+        n = len(buf) if length is None else int(length)
+        if self.closed:
+            return n
+        if self._pending is not None:
+            return min(n, self._need - len(self._pending))
+        r, err, d1, d2 = frame_available(buf, n)
+        if r < 0:
+            raise self._protocol_error(session, err, d1, d2)
+        return r
+
+    # FrameDecoder.decode(ISession, ByteBuffer, List<Frame>), :180-288
+    def decode(self, session, data, out: list):
+        data = bytes(data)
+        try:
+            if self.closed:
+                return
+            if self._pending is not None:
+                self._pending += data
+                if len(self._pending) < self._need:
+                    return
+                frame, self._pending = bytes(self._pending), None
+            else:
+                hl = _header_len(data) if len(data) >= 2 else 2
+                if len(data) < hl:
+                    raise ValueError("incomplete frame header (reference: BufferUnderflowException)")
+                err, det = check_header(self.cfg, bool(self.state[0]["fragmentation"]), data[:hl])
+                if err:
+                    raise self._protocol_error(session, err, det)
+                total = _frame_total(data)
+                if len(data) < total:
+                    self._pending, self._need = bytearray(data), total
+                    return
+                frame = data
+            self._run(session, frame, out)
+        finally:
+            _release(session, data)
+
+    def _run(self, session, frame: bytes, out: list):
+        ctx = self.ctx or default_context()
+        wire = np.frombuffer(frame, dtype=np.uint8)
+        payload, desc, result = ctx.decode_host(self.cfg, wire, np.array([0, len(frame)], np.uint64),
+                                                np.array([0, 1], np.uint32), self.state)
+        r = result[0]
+        if r["n_delivered"] == 1:
+            d = desc[0]
+            off, ln = int(d["payload_off"]), int(d["payload_len"])
+            out.append(make_frame(int(d["opcode"]), bool(d["flags"] & 0x80), (int(d["flags"]) >> 4) & 7,
+                                  payload[off:off + ln].tobytes()))
+        elif r["error"]:
+            _writenf(session, CloseFrame.of_status(int(r["close_code"])))
+            raise InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
+
+
+class FrameEncoder:
+    """GPU-backed FrameEncoder. The mask key comes from `mask_source()` (default:
+    os.urandom, standing in for the reference's java.util.Random, FrameEncoder.java:43)."""
+
+    def __init__(self, clientMode: bool, ctx: Context | None = None, mask_source=None):
+        self.clientMode = bool(clientMode)
+        self.ctx = ctx
+        self.mask_source = mask_source or (lambda: os.urandom(4))
+        self.closed = np.zeros(1, dtype=np.uint8)
+
+    def getInboundType(self):
+        return Frame
+
+    def getOutboundType(self):
+        return bytes
+
+    def length(self, frame: Frame) -> int:
+        from .context import encoded_length
+        return encoded_length(frame.getPayloadLength(), self.clientMode)
+
+    def encode(self, session, frame: Frame, out: list):
+        if self.closed[0]:
+            return
+        ctx = self.ctx or default_context()
+        payload = np.frombuffer(frame.getPayload(), dtype=np.uint8)
+        fr = np.zeros(1, dtype=ENCODE_DTYPE)
+        fr[0]["payload_off"] = 0
+        fr[0]["payload_len"] = len(payload)
+        fr[0]["opcode"] = int(frame.getOpcode())
+        fr[0]["flags"] = (0x80 if frame.isFinalFragment() else 0) | ((frame.getRsvBits() & 7) << 4)
+        if self.clientMode:
+            fr[0]["mask"] = np.frombuffer(bytes(self.mask_source()), dtype=np.uint8)
+        wire, _ = ctx.encode_host(self.clientMode, payload, fr, np.array([0, 1], np.uint32), self.closed)
+        buf = wire.tobytes()
+        if session is not None and hasattr(session, "allocate"):
+            b = session.allocate(len(buf))
+            b[:] = buf
+            buf = b
+        out.append(buf)
+
+
+class SessionBatcher:
+    """Cross-session batching: bytes from many sessions' socket reads are framed on
+    the host (the session loop's available() calls, StreamSession.java:798-854),
+    complete frames are queued, and flush() decodes all queued frames of all
+    sessions in ONE device batch.  Per-session state (fragmentation, UTF-8 carry,
+    closed) persists across flushes.  Header rules are applied as soon as a
+    header is complete, so a frame announcing a too-long payload fails without
+    waiting for its bytes, as in the reference (FrameDecoder.java:238-256)."""
+
+    def __init__(self, n_sessions: int, clientMode: bool = False, allowExtensions: bool = False,
+                 maxPayloadLen: int = 65536, validate_utf8: bool = True, ctx: Context | None = None):
+        self.cfg = decoder_cfg(clientMode, allowExtensions, maxPayloadLen, validate_utf8)
+        self.ctx = ctx
+        self.n = n_sessions
+        self.state = np.zeros(n_sessions, dtype=STATE_DTYPE)
+        self.inbuf = [bytearray() for _ in range(n_sessions)]
+        self.queue = [[] for _ in range(n_sessions)]
+        self.host_error = [None] * n_sessions
+        self._frag_host = np.zeros(n_sessions, dtype=bool)  # fragmentation as of the queued frames
+
+    def feed(self, sid: int, data: bytes):
+        if self.state[sid]["closed"] or self.host_error[sid] is not None:
+            return
+        buf = self.inbuf[sid]
+        buf += data
+        pos = 0
+        while True:
+            r, err, d1, d2 = frame_available(bytes(buf[pos:pos + 14]), len(buf) - pos)
+            if r < 0:
+                self.host_error[sid] = (err, d1, d2)
+                break
+            if r == 0:
+                break
+            hl = _header_len(buf[pos:pos + 2]) if len(buf) - pos >= 2 else 2
+            e, det = check_header(self.cfg, bool(self._frag_host[sid]), bytes(buf[pos:pos + hl]))
+            if e and e != 17:  # a header rule fails: report it now (the frame may never complete)
+                self.host_error[sid] = (e, det, 0)
+                break
+            total = _frame_total(buf[pos:pos + hl])
+            if len(buf) - pos < total:
+                break
+            op = buf[pos] & 0x0F
+            if op <= 2:
+                self._frag_host[sid] = not (buf[pos] & 0x80)
+            self.queue[sid].append(bytes(buf[pos:pos + total]))
+            pos += total
+        del buf[:pos]
+
+    def flush(self):
+        """Decode everything queued. Returns [(frames, InvalidFrameException | None)] per session."""
+        ctx = self.ctx or default_context()
+        frames_all, first, off = [], [0], [0]
+        for q in self.queue:
+            for f in q:
+                frames_all.append(f)
+                off.append(off[-1] + len(f))
+            first.append(len(frames_all))
+        wire = np.frombuffer(b"".join(frames_all), dtype=np.uint8) if frames_all else np.zeros(0, np.uint8)
+        payload, desc, result = ctx.decode_host(self.cfg, wire, np.array(off, np.uint64),
+                                                np.array(first, np.uint32), self.state)
+        out = []
+        for s in range(self.n):
+            r = result[s]
+            frames = []
+            for k in range(first[s], first[s] + int(r["n_delivered"])):
+                d = desc[k]
+                o, ln = int(d["payload_off"]), int(d["payload_len"])
+                frames.append(make_frame(int(d["opcode"]), bool(d["flags"] & 0x80), (int(d["flags"]) >> 4) & 7,
+                                         payload[o:o + ln].tobytes()))
+            exc = None
+            if r["error"]:
+                exc = InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
+                exc.close_code = int(r["close_code"])
+            elif self.host_error[s] is not None and not self.state[s]["closed"]:
+                e, d1, d2 = self.host_error[s]
+                exc = InvalidFrameException(error_message(e, d1, d2))
+                exc.close_code = _close_code(e)
+                self.state[s]["closed"] = 1
+            out.append((frames, exc))
+            self.queue[s] = []
+        return out

@@ -1,0 +1,192 @@
+"""Context: a libwsgpu context on one GPU, with device-resident and host batch calls.
+
+Device buffers are torch tensors (plumbing only: HIP allocations + the stream);
+all work runs in libwsgpu's HIP kernels.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import DESC_DTYPE, ENCODE_DTYPE, RESULT_DTYPE, STATE_DTYPE, DecoderCfg, check, lib
+
+MESSAGES = {
+    1: "Unexpected opcode value ({d})",
+    2: "Unexpected non-zero RSV bits ({d})",
+    3: "Unexpected payload masking",
+    4: "Fragmented control frame",
+    5: "Invalid payload length ({d}) in control frame",
+    6: "Invalid payload length ({d}) in close frame",
+    7: "Continuation frame outside fragmented message",
+    8: "Non-continuation frame while inside fragmented massage",
+    9: "Invalid minimal payload length",
+    10: "Invalid maximum payload length",
+    11: "Maximum frame length ({d}) has been exceeded",
+    12: "Invalid close frame status code ({d})",
+    13: "Invalid close frame reason value: bytes are not UTF-8",
+    14: "Invalid text frame payload: bytes are not UTF-8",
+    15: "Negative payload length ({d})",
+    16: "Extended payload length ({d}) > {d2}",
+    17: "Malformed batch (frame extent does not match its header)",
+}
+
+
+def error_message(code: int, detail: int = 0, detail2: int = 0) -> str:
+    """The InvalidFrameException message the reference builds for a wsg_status
+    (FrameDecoder.java:200-255, :390-393; FrameUtf8Validator.java:31)."""
+    return MESSAGES[int(code)].format(d=int(detail), d2=int(detail2))
+
+
+def decoder_cfg(client_mode: bool, allow_extensions: bool, max_payload_len: int,
+                validate_utf8: bool = True) -> DecoderCfg:
+    return DecoderCfg(int(bool(client_mode)), int(bool(allow_extensions)), int(max_payload_len),
+                      int(bool(validate_utf8)), 0)
+
+
+def _p(a) -> int:
+    """Device pointer of a torch tensor, host pointer of a numpy array."""
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()
+
+
+class Context:
+    def __init__(self, device: int = 0, stream=None):
+        h = C.c_void_p()
+        s = None
+        if stream is not None:
+            s = C.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
+        rc = lib.wsg_open(int(device), s, C.byref(h))
+        if rc != 0:
+            raise _lib.WsgError(f"wsg_open(device={device}) failed: {rc} (no HIP device?)")
+        self._h = h
+        self.device = device
+
+    # -------------------------------------------------------------- plumbing
+    def close(self):
+        if getattr(self, "_h", None):
+            lib.wsg_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def set_stream(self, stream):
+        check(lib.wsg_set_stream(self._h, C.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)),
+              self._h)
+
+    def sync(self):
+        check(lib.wsg_sync(self._h), self._h)
+
+    def reserve(self, max_frames: int, max_sessions: int):
+        check(lib.wsg_reserve(self._h, int(max_frames), int(max_sessions)), self._h)
+
+    def set_timing(self, on: bool = True):
+        check(lib.wsg_set_timing(self._h, int(on)), self._h)
+
+    def reset_timing(self):
+        check(lib.wsg_reset_timing(self._h), self._h)
+
+    def timing(self) -> dict:
+        n = lib.wsg_num_kernels()
+        ms = (C.c_double * n)()
+        cnt = (C.c_uint64 * n)()
+        lib.wsg_get_timing(self._h, ms, cnt, n)
+        return {lib.wsg_kernel_name(i).decode(): (ms[i], cnt[i]) for i in range(n)}
+
+    # -------------------------------------------------------------- decode
+    def decode_device(self, cfg: DecoderCfg, wire, frame_off, session_first, state, payload_out, desc_out,
+                      result_out, wire_len: int | None = None):
+        """Enqueue a device-resident batch decode (all arguments cuda tensors)."""
+        n_frames = frame_off.numel() - 1
+        n_sessions = session_first.numel() - 1
+        wl = wire.numel() if wire_len is None else int(wire_len)
+        check(lib.wsg_decode_batch_device(self._h, C.byref(cfg), _p(wire), wl, _p(frame_off), n_frames,
+                                          _p(session_first), n_sessions, _p(state), _p(payload_out),
+                                          payload_out.numel(), _p(desc_out), _p(result_out)), self._h)
+
+    def decode_host(self, cfg: DecoderCfg, wire: np.ndarray, frame_off: np.ndarray, session_first: np.ndarray,
+                    state: np.ndarray):
+        """Host batch decode (H2D, kernels, D2H). `state` (STATE_DTYPE) is updated in place.
+        Returns (payload, desc, result)."""
+        wire = np.ascontiguousarray(wire, dtype=np.uint8)
+        frame_off = np.ascontiguousarray(frame_off, dtype=np.uint64)
+        session_first = np.ascontiguousarray(session_first, dtype=np.uint32)
+        assert state.dtype == STATE_DTYPE and state.flags.c_contiguous
+        n_frames = len(frame_off) - 1
+        n_sessions = len(session_first) - 1
+        cap = int(lib.wsg_decode_payload_bound(wire.size, n_frames))
+        payload = np.zeros(cap, dtype=np.uint8)
+        desc = np.zeros(max(1, n_frames), dtype=DESC_DTYPE)
+        result = np.zeros(max(1, n_sessions), dtype=RESULT_DTYPE)
+        w = wire if wire.size else np.zeros(1, np.uint8)
+        check(lib.wsg_decode_batch_host(self._h, C.byref(cfg), w.ctypes.data, wire.size, frame_off.ctypes.data,
+                                        n_frames, session_first.ctypes.data, n_sessions, state.ctypes.data,
+                                        payload.ctypes.data, cap, desc.ctypes.data, result.ctypes.data), self._h)
+        return payload, desc[:n_frames], result[:n_sessions]
+
+    # -------------------------------------------------------------- encode
+    def encode_device(self, client_mode: bool, payload, frames, session_first, closed, wire_out, wire_off):
+        n_frames = frames.numel() // ENCODE_DTYPE.itemsize if frames.dtype.itemsize == 1 else frames.shape[0]
+        n_sessions = session_first.numel() - 1
+        check(lib.wsg_encode_batch_device(self._h, int(client_mode), _p(payload), payload.numel(), _p(frames),
+                                          n_frames, _p(session_first), n_sessions, _p(closed), _p(wire_out),
+                                          wire_out.numel(), _p(wire_off)), self._h)
+
+    def encode_host(self, client_mode: bool, payload: np.ndarray, frames: np.ndarray, session_first: np.ndarray,
+                    closed: np.ndarray):
+        """Host batch encode; `closed` (uint8 per session) updated in place.
+        Returns (wire, wire_off)."""
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        frames = np.ascontiguousarray(frames, dtype=ENCODE_DTYPE)
+        session_first = np.ascontiguousarray(session_first, dtype=np.uint32)
+        n_frames, n_sessions = len(frames), len(session_first) - 1
+        cap = int(sum(int(lib.wsg_encoded_length(int(f), int(client_mode))) for f in frames["payload_len"])) + 16
+        wire = np.zeros(cap, dtype=np.uint8)
+        wire_off = np.zeros(n_frames + 1, dtype=np.uint64)
+        p = payload if payload.size else np.zeros(1, np.uint8)
+        fr = frames if n_frames else np.zeros(1, ENCODE_DTYPE)
+        check(lib.wsg_encode_batch_host(self._h, int(client_mode), p.ctypes.data, payload.size, fr.ctypes.data,
+                                        n_frames, session_first.ctypes.data, n_sessions, closed.ctypes.data,
+                                        wire.ctypes.data, cap, wire_off.ctypes.data), self._h)
+        return wire[:int(wire_off[-1])], wire_off
+
+    # -------------------------------------------------------------- synthetic data
+    def synth_uniform(self, seed, n_frames, payload_len, frames_per_session, opcode, masked, text, wire,
+                      frame_off, session_first):
+        check(lib.wsg_synth_uniform(self._h, int(seed), int(n_frames), int(payload_len), int(frames_per_session),
+                                    int(opcode), int(masked), int(text), _p(wire), _p(frame_off),
+                                    _p(session_first)), self._h)
+
+
+def frame_available(buf: bytes, length: int | None = None):
+    """wsg_frame_available: FrameDecoder.available(session, byte[], off, len) without
+    a pending payload. Returns (n, err, detail, detail2)."""
+    b = bytes(buf) + bytes(16)
+    n = len(buf) if length is None else int(length)
+    a = np.frombuffer(b, dtype=np.uint8)
+    err, d1, d2 = C.c_int32(0), C.c_int64(0), C.c_int64(0)
+    r = lib.wsg_frame_available(a.ctypes.data, n, C.byref(err), C.byref(d1), C.byref(d2))
+    return int(r), int(err.value), int(d1.value), int(d2.value)
+
+
+def check_header(cfg: DecoderCfg, fragmentation: bool, buf: bytes):
+    a = np.frombuffer(bytes(buf) + bytes(16), dtype=np.uint8)
+    d = C.c_int64(0)
+    e = lib.wsg_check_header(C.byref(cfg), int(bool(fragmentation)), a.ctypes.data, len(buf), C.byref(d))
+    return int(e), int(d.value)
+
+
+def encoded_length(payload_len: int, client_mode: bool) -> int:
+    return int(lib.wsg_encoded_length(int(payload_len), int(bool(client_mode))))

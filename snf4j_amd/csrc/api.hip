@@ -1,0 +1,504 @@
+// api.hip — the C ABI of libwsgpu.so (include/wsgpu.h): context, workspace,
+// kernel timing, device/host batch entry points, host-side framing helpers.
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "wsgpu_internal.h"
+
+using namespace ws;
+
+namespace {
+
+const char* const kKernelNames[K_COUNT] = {"k_parse",    "k_scan",     "k_link",     "k_unmask",    "k_final",
+                                           "k_enc_len",  "k_enc_scan", "k_enc_emit", "k_enc_final", "k_synth"};
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    size_t want = bytes < 256 ? 256 : bytes;
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess) n = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+struct EventPair {
+  int kid;
+  hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct wsg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  std::string err;
+  // decode workspace
+  DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total;
+  // encode workspace
+  DevBuf esess, elast_close;
+  // host-path device buffers
+  DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
+  // timing
+  bool timing = false;
+  std::vector<EventPair> pending;
+  std::vector<hipEvent_t> free_events;
+  double ms[K_COUNT] = {};
+  uint64_t count[K_COUNT] = {};
+};
+
+static int set_err(wsg_ctx* c, int code, const char* fmt, ...) {
+  if (c) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    c->err = buf;
+  }
+  return code;
+}
+
+#define HIP_TRY(c, expr)                                                                        \
+  do {                                                                                          \
+    hipError_t _e = (expr);                                                                     \
+    if (_e != hipSuccess) return set_err((c), WSG_API_EHIP, "%s: %s", #expr, hipGetErrorString(_e)); \
+  } while (0)
+
+static hipEvent_t get_event(wsg_ctx* c) {
+  if (!c->free_events.empty()) {
+    hipEvent_t e = c->free_events.back();
+    c->free_events.pop_back();
+    return e;
+  }
+  hipEvent_t e = nullptr;
+  (void)hipEventCreate(&e);
+  return e;
+}
+
+static void drain_timing(wsg_ctx* c) {
+  for (auto& p : c->pending) {
+    (void)hipEventSynchronize(p.b);
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, p.a, p.b) == hipSuccess) {
+      c->ms[p.kid] += t;
+      c->count[p.kid] += 1;
+    }
+    c->free_events.push_back(p.a);
+    c->free_events.push_back(p.b);
+  }
+  c->pending.clear();
+}
+
+template <typename F>
+static void timed(wsg_ctx* c, int kid, F&& f) {
+  if (!c->timing) {
+    f();
+    return;
+  }
+  if (c->pending.size() > 4096) drain_timing(c);
+  EventPair p{kid, get_event(c), get_event(c)};
+  (void)hipEventRecord(p.a, c->stream);
+  f();
+  (void)hipEventRecord(p.b, c->stream);
+  c->pending.push_back(p);
+}
+
+extern "C" {
+
+int wsg_version(void) { return WSG_ABI_VERSION; }
+
+int wsg_num_kernels(void) { return K_COUNT; }
+
+const char* wsg_kernel_name(int kid) { return (kid >= 0 && kid < K_COUNT) ? kKernelNames[kid] : ""; }
+
+int wsg_open(int device, void* stream, wsg_ctx** out) {
+  if (!out) return WSG_API_EINVAL;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return WSG_API_EHIP;
+  if (device < 0 || device >= n) return WSG_API_EINVAL;
+  if (hipSetDevice(device) != hipSuccess) return WSG_API_EHIP;
+  wsg_ctx* c = new wsg_ctx();
+  c->device = device;
+  if (stream) {
+    c->stream = (hipStream_t)stream;
+  } else {
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+      delete c;
+      return WSG_API_EHIP;
+    }
+    c->own_stream = true;
+  }
+  *out = c;
+  return WSG_API_OK;
+}
+
+int wsg_close(wsg_ctx* c) {
+  if (!c) return WSG_API_EINVAL;
+  (void)hipSetDevice(c->device);
+  (void)hipStreamSynchronize(c->stream);
+  drain_timing(c);
+  for (auto e : c->free_events) (void)hipEventDestroy(e);
+  DevBuf* bufs[] = {&c->rec,     &c->prev,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
+                    &c->total,   &c->esess,   &c->elast_close, &c->h_wire, &c->h_off,    &c->h_sf,
+                    &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
+                    &c->h_wire_off};
+  for (DevBuf* b : bufs) b->release();
+  if (c->own_stream) (void)hipStreamDestroy(c->stream);
+  delete c;
+  return WSG_API_OK;
+}
+
+int wsg_set_stream(wsg_ctx* c, void* stream) {
+  if (!c) return WSG_API_EINVAL;
+  if (c->own_stream) {
+    (void)hipStreamSynchronize(c->stream);
+    (void)hipStreamDestroy(c->stream);
+    c->own_stream = false;
+  }
+  c->stream = (hipStream_t)stream;
+  return WSG_API_OK;
+}
+
+const char* wsg_last_error(wsg_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+int wsg_sync(wsg_ctx* c) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return WSG_API_OK;
+}
+
+int wsg_set_timing(wsg_ctx* c, int enable) {
+  if (!c) return WSG_API_EINVAL;
+  c->timing = enable != 0;
+  return WSG_API_OK;
+}
+
+int wsg_get_timing(wsg_ctx* c, double* out_ms, uint64_t* out_count, int max_kernels) {
+  if (!c) return WSG_API_EINVAL;
+  drain_timing(c);
+  for (int i = 0; i < K_COUNT && i < max_kernels; ++i) {
+    if (out_ms) out_ms[i] = c->ms[i];
+    if (out_count) out_count[i] = c->count[i];
+  }
+  return K_COUNT;
+}
+
+int wsg_reset_timing(wsg_ctx* c) {
+  if (!c) return WSG_API_EINVAL;
+  drain_timing(c);
+  memset(c->ms, 0, sizeof c->ms);
+  memset(c->count, 0, sizeof c->count);
+  return WSG_API_OK;
+}
+
+static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions) {
+  const uint64_t F = n_frames ? n_frames : 1;
+  const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
+  HIP_TRY(c, c->rec.ensure(F * sizeof(FrameRec)));
+  HIP_TRY(c, c->prev.ensure(3 * F * sizeof(int32_t)));
+  HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));
+  HIP_TRY(c, c->blk_sum.ensure(nblk * sizeof(uint64_t)));
+  HIP_TRY(c, c->blk_max.ensure(3 * nblk * sizeof(int32_t)));
+  HIP_TRY(c, c->sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t)));
+  HIP_TRY(c, c->total.ensure(sizeof(uint64_t)));
+  return WSG_API_OK;
+}
+
+static int ensure_encode_ws(wsg_ctx* c, uint64_t n_frames) {
+  const uint64_t F = n_frames ? n_frames : 1;
+  const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
+  HIP_TRY(c, c->esess.ensure(F * sizeof(uint32_t)));
+  HIP_TRY(c, c->elast_close.ensure(F * sizeof(int32_t)));
+  HIP_TRY(c, c->blk_sum.ensure(nblk * sizeof(uint64_t)));
+  HIP_TRY(c, c->blk_max.ensure(3 * nblk * sizeof(int32_t)));
+  return WSG_API_OK;
+}
+
+int wsg_reserve(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = ensure_decode_ws(c, max_frames, max_sessions);
+  if (rc) return rc;
+  return ensure_encode_ws(c, max_frames);
+}
+
+uint64_t wsg_decode_payload_bound(uint64_t wire_len, uint64_t n_frames) { return wire_len + 16 * n_frames + 16; }
+
+static uint32_t stream_grid(uint64_t n_frames) {
+  // one wave per frame, 4 waves per workgroup; enough workgroups to keep
+  // 8 per CU resident on the 256 CUs, the rest grid-strided
+  uint64_t g = (n_frames + 3) / 4;
+  if (g > 2048) g = 2048;
+  return (uint32_t)(g ? g : 1);
+}
+
+int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t* wire, uint64_t wire_len,
+                            const uint64_t* frame_off, uint64_t n_frames, const uint32_t* session_first,
+                            uint32_t n_sessions, wsg_session_state* state, uint8_t* payload_out,
+                            uint64_t payload_cap, wsg_frame_desc* desc_out, wsg_session_result* result_out) {
+  if (!c || !cfg) return WSG_API_EINVAL;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  if (n_frames >= 0x7fffffffull) return set_err(c, WSG_API_ERANGE, "too many frames in one batch");
+  if (((uintptr_t)wire & 3) || ((uintptr_t)payload_out & 15))
+    return set_err(c, WSG_API_EINVAL, "wire must be 4-B aligned and payload_out 16-B aligned");
+  if (payload_cap < wire_len + 16 * n_frames)
+    return set_err(c, WSG_API_ERANGE, "payload_cap below wsg_decode_payload_bound()");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = ensure_decode_ws(c, n_frames, n_sessions);
+  if (rc) return rc;
+  DecodeArgs a;
+  a.wire = wire;
+  a.wire_len = wire_len;
+  a.frame_off = frame_off;
+  a.n_frames = n_frames;
+  a.session_first = session_first;
+  a.n_sessions = n_sessions;
+  a.client_mode = cfg->client_mode != 0;
+  a.allow_ext = cfg->allow_extensions != 0;
+  a.validate = cfg->validate_utf8 != 0;
+  a.max_payload = cfg->max_payload_len;
+  a.state = state;
+  a.payload_out = payload_out;
+  a.desc = desc_out;
+  a.result = result_out;
+  a.rec = (FrameRec*)c->rec.p;
+  a.prev = (int32_t*)c->prev.p;
+  a.edge = (uint32_t*)c->edge.p;
+  a.blk_sum = (uint64_t*)c->blk_sum.p;
+  a.blk_max = (int32_t*)c->blk_max.p;
+  a.sess_err = (uint64_t*)c->sess_err.p;
+  a.total = (uint64_t*)c->total.p;
+  a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  HIP_TRY(c, hipMemsetAsync(a.sess_err, 0xff, (size_t)n_sessions * sizeof(uint64_t), c->stream));
+  if (n_frames) {
+    timed(c, K_PARSE, [&] { launch_parse(a, c->stream); });
+    timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
+    timed(c, K_LINK, [&] { launch_link(a, c->stream); });
+    timed(c, K_UNMASK, [&] { launch_unmask(a, c->stream, stream_grid(n_frames)); });
+  }
+  timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_decode_batch_host(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t* wire, uint64_t wire_len,
+                          const uint64_t* frame_off, uint64_t n_frames, const uint32_t* session_first,
+                          uint32_t n_sessions, wsg_session_state* state, uint8_t* payload_out, uint64_t payload_cap,
+                          wsg_frame_desc* desc_out, wsg_session_result* result_out) {
+  if (!c || !cfg) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t bound = wire_len + 16 * n_frames + 16;
+  HIP_TRY(c, c->h_wire.ensure(wire_len + 32));
+  HIP_TRY(c, c->h_off.ensure((n_frames + 1) * sizeof(uint64_t)));
+  HIP_TRY(c, c->h_sf.ensure(((uint64_t)n_sessions + 1) * sizeof(uint32_t)));
+  HIP_TRY(c, c->h_state.ensure(((uint64_t)n_sessions + 1) * sizeof(wsg_session_state)));
+  HIP_TRY(c, c->h_payload.ensure(bound));
+  HIP_TRY(c, c->h_desc.ensure((n_frames + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, c->h_result.ensure(((uint64_t)n_sessions + 1) * sizeof(wsg_session_result)));
+  hipStream_t s = c->stream;
+  if (wire_len) HIP_TRY(c, hipMemcpyAsync(c->h_wire.p, wire, wire_len, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_off.p, frame_off, (n_frames + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_sf.p, session_first, ((uint64_t)n_sessions + 1) * sizeof(uint32_t),
+                            hipMemcpyHostToDevice, s));
+  if (n_sessions)
+    HIP_TRY(c, hipMemcpyAsync(c->h_state.p, state, (uint64_t)n_sessions * sizeof(wsg_session_state),
+                              hipMemcpyHostToDevice, s));
+  int rc = wsg_decode_batch_device(c, cfg, (const uint8_t*)c->h_wire.p, wire_len, (const uint64_t*)c->h_off.p,
+                                   n_frames, (const uint32_t*)c->h_sf.p, n_sessions,
+                                   (wsg_session_state*)c->h_state.p, (uint8_t*)c->h_payload.p, bound,
+                                   (wsg_frame_desc*)c->h_desc.p, (wsg_session_result*)c->h_result.p);
+  if (rc) return rc;
+  uint64_t total = 0;
+  if (n_frames) {
+    HIP_TRY(c, hipMemcpyAsync(&total, c->total.p, sizeof total, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipStreamSynchronize(s));
+    if (total > payload_cap) return set_err(c, WSG_API_ERANGE, "payload_cap %llu < %llu", (unsigned long long)payload_cap,
+                                            (unsigned long long)total);
+    if (total) HIP_TRY(c, hipMemcpyAsync(payload_out, c->h_payload.p, total, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(desc_out, c->h_desc.p, n_frames * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, s));
+  }
+  if (n_sessions) {
+    HIP_TRY(c, hipMemcpyAsync(result_out, c->h_result.p, (uint64_t)n_sessions * sizeof(wsg_session_result),
+                              hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(state, c->h_state.p, (uint64_t)n_sessions * sizeof(wsg_session_state),
+                              hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
+
+// FrameDecoder.available(session, byte[], off, len), FrameDecoder.java:357-401,
+// with the JVM's int/long arithmetic (the u64 branch can wrap).
+int64_t wsg_frame_available(const uint8_t* buf, uint64_t len_u, int32_t* err, int64_t* detail, int64_t* detail2) {
+  if (err) *err = 0;
+  const int64_t len = (int64_t)len_u;
+  int32_t need = 2;
+  if (len < need) return 0;
+  if (buf[1] & 0x80) {
+    need += 4;
+    if (len < need) return 0;
+  }
+  int64_t plen = buf[1] & 0x7f;
+  if (plen < 126) {
+    need += (int32_t)plen;
+  } else if (plen == 126) {
+    need += 2;
+    if (len < need) return 0;
+    need += (int32_t)(((uint32_t)buf[2] << 8) | buf[3]);
+  } else {
+    need += 8;
+    if (len < need) return 0;
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | buf[2 + i];
+    plen = (int64_t)v;
+    if (plen < 0) {
+      if (err) *err = WSG_E_NEG_LEN;
+      if (detail) *detail = plen;
+      if (detail2) *detail2 = 0;
+      return -1;
+    }
+    if ((int64_t)((uint64_t)plen + (uint64_t)(int64_t)need) > (int64_t)0x7fffffff) {
+      if (err) *err = WSG_E_EXT_LEN;
+      if (detail) *detail = plen;
+      if (detail2) *detail2 = (int64_t)0x7fffffff - need;
+      return -1;
+    }
+    need = (int32_t)(uint32_t)((uint64_t)(int64_t)need + (uint64_t)plen);
+  }
+  return len > need ? need : len;
+}
+
+int32_t wsg_check_header(const wsg_decoder_cfg* cfg, int fragmentation, const uint8_t* buf, uint64_t len,
+                         int64_t* detail) {
+  Header h;
+  if (detail) *detail = 0;
+  if (!parse_header(buf, len, h)) return WSG_E_BATCH;
+  uint32_t e = rules_pre(h, cfg->client_mode, cfg->allow_extensions);
+  if (!e) e = rules_frag(h.opcode, fragmentation != 0);
+  if (!e) e = rules_post(h, cfg->max_payload_len);
+  if (detail) {
+    switch (e) {
+      case WSG_E_OPCODE: *detail = h.opcode; break;
+      case WSG_E_RSV: *detail = h.rsv; break;
+      case WSG_E_CONTROL_LEN:
+      case WSG_E_CLOSE_LEN: *detail = h.len7; break;
+      case WSG_E_TOO_LONG: *detail = cfg->max_payload_len; break;
+      default: break;
+    }
+  }
+  return (int32_t)e;
+}
+
+uint64_t wsg_encoded_length(uint32_t len, int client_mode) {
+  uint64_t n = len;
+  if (len > 0xffffu) n += 8;
+  else if (len > 125u) n += 2;
+  if (client_mode) n += 4;
+  return n + 2;
+}
+
+int wsg_encode_batch_device(wsg_ctx* c, int client_mode, const uint8_t* payload, uint64_t payload_len,
+                            const wsg_encode_frame* frames, uint64_t n_frames, const uint32_t* session_first,
+                            uint32_t n_sessions, uint8_t* closed, uint8_t* wire_out, uint64_t wire_cap,
+                            uint64_t* wire_off) {
+  if (!c) return WSG_API_EINVAL;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  if (n_frames >= 0x7fffffffull) return set_err(c, WSG_API_ERANGE, "too many frames in one batch");
+  if ((uintptr_t)wire_out & 15) return set_err(c, WSG_API_EINVAL, "wire_out must be 16-B aligned");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = ensure_encode_ws(c, n_frames);
+  if (rc) return rc;
+  EncodeArgs a;
+  a.client_mode = client_mode != 0;
+  a.payload = payload;
+  a.payload_len = payload_len;
+  a.frames = frames;
+  a.n_frames = n_frames;
+  a.session_first = session_first;
+  a.n_sessions = n_sessions;
+  a.closed = closed;
+  a.wire_out = wire_out;
+  a.wire_cap = wire_cap;
+  a.wire_off = wire_off;
+  a.sess = (uint32_t*)c->esess.p;
+  a.blk_sum = (uint64_t*)c->blk_sum.p;
+  a.blk_max = (int32_t*)c->blk_max.p;
+  a.last_close = (int32_t*)c->elast_close.p;
+  a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  if (n_frames) {
+    timed(c, K_ENC_LEN, [&] { launch_enc_len(a, c->stream); });
+    timed(c, K_ENC_SCAN, [&] { launch_enc_scan(a, c->stream); });
+    timed(c, K_ENC_EMIT, [&] { launch_enc_emit(a, c->stream, stream_grid(n_frames)); });
+    timed(c, K_ENC_FINAL, [&] { launch_enc_final(a, c->stream); });
+  } else {
+    HIP_TRY(c, hipMemsetAsync(wire_off, 0, sizeof(uint64_t), c->stream));
+  }
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_encode_batch_host(wsg_ctx* c, int client_mode, const uint8_t* payload, uint64_t payload_len,
+                          const wsg_encode_frame* frames, uint64_t n_frames, const uint32_t* session_first,
+                          uint32_t n_sessions, uint8_t* closed, uint8_t* wire_out, uint64_t wire_cap,
+                          uint64_t* wire_off) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  uint64_t need = 0;
+  for (uint64_t k = 0; k < n_frames; ++k) need += wsg_encoded_length(frames[k].payload_len, client_mode);
+  HIP_TRY(c, c->h_payload.ensure(payload_len + 32));
+  HIP_TRY(c, c->h_frames.ensure((n_frames + 1) * sizeof(wsg_encode_frame)));
+  HIP_TRY(c, c->h_sf.ensure(((uint64_t)n_sessions + 1) * sizeof(uint32_t)));
+  HIP_TRY(c, c->h_closed.ensure((uint64_t)n_sessions + 1));
+  HIP_TRY(c, c->h_wire.ensure(need + 32));
+  HIP_TRY(c, c->h_wire_off.ensure((n_frames + 1) * sizeof(uint64_t)));
+  hipStream_t s = c->stream;
+  if (payload_len) HIP_TRY(c, hipMemcpyAsync(c->h_payload.p, payload, payload_len, hipMemcpyHostToDevice, s));
+  if (n_frames)
+    HIP_TRY(c, hipMemcpyAsync(c->h_frames.p, frames, n_frames * sizeof(wsg_encode_frame), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_sf.p, session_first, ((uint64_t)n_sessions + 1) * sizeof(uint32_t),
+                            hipMemcpyHostToDevice, s));
+  if (n_sessions) HIP_TRY(c, hipMemcpyAsync(c->h_closed.p, closed, n_sessions, hipMemcpyHostToDevice, s));
+  int rc = wsg_encode_batch_device(c, client_mode, (const uint8_t*)c->h_payload.p, payload_len,
+                                   (const wsg_encode_frame*)c->h_frames.p, n_frames, (const uint32_t*)c->h_sf.p,
+                                   n_sessions, (uint8_t*)c->h_closed.p, (uint8_t*)c->h_wire.p, need + 32,
+                                   (uint64_t*)c->h_wire_off.p);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(wire_off, c->h_wire_off.p, (n_frames + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const uint64_t total = wire_off[n_frames];
+  if (total > wire_cap) return set_err(c, WSG_API_ERANGE, "wire_cap too small");
+  if (total) HIP_TRY(c, hipMemcpyAsync(wire_out, c->h_wire.p, total, hipMemcpyDeviceToHost, s));
+  if (n_sessions) HIP_TRY(c, hipMemcpyAsync(closed, c->h_closed.p, n_sessions, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
+
+int wsg_synth_uniform(wsg_ctx* c, uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode,
+                      int masked, int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first) {
+  if (!c || fps == 0) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  timed(c, K_SYNTH, [&] {
+    launch_synth(seed, n_frames, payload_len, fps, opcode, masked, text, wire, frame_off, session_first, c->stream);
+  });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+}  // extern "C"

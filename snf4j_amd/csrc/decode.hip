@@ -1,0 +1,439 @@
+// decode.hip — the frame decode pipeline on gfx950 (FrameDecoder + FrameUtf8Validator).
+//
+//   k_parse   thread per frame: header parse + the per-frame rules of
+//             FrameDecoder.decode (:197-256), close status/reason (:121-136),
+//             first/last payload bytes; block aggregates for the scans.
+//   k_scan    one workgroup: exclusive scan of the block aggregates
+//             (payload slot bytes = the length prefix-scan; last data / message
+//             start / nonempty frame indices = max-scans).
+//   k_link    thread per frame: payload slot offset, the fragmentation rule
+//             (:229-236) from the previous data frame's FIN, text-message
+//             membership for the validator (FrameUtf8Validator.java:59-70).
+//   k_unmask  one wave per frame: coalesced 16-B loads, 4-byte XOR unmask
+//             (:268-273), 16-B stores into the frame's aligned slot, per-lane
+//             SWAR UTF-8 rule with the 3-byte carry taken from the neighbour
+//             lane (DPP/bpermute) and the verdict folded by wavefront ballot;
+//             the fragment-boundary bytes are checked against the carry of the
+//             previous fragments; the first failing frame per session via atomicMin.
+//   k_final   thread per session: wsg_session_result + carry-out state.
+#include "wsgpu_internal.h"
+#include "wsgpu_scan.h"
+
+namespace ws {
+
+// UTF-8 validity of a short byte run (close reason), by the per-byte rule
+__device__ bool utf8_valid_run(const uint8_t* wire, uint64_t off, uint32_t n, uint32_t mask, uint32_t phase0) {
+  uint32_t p1 = 0, p2 = 0, p3 = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    uint32_t b = wire[off + i] ^ ((mask >> (8 * ((phase0 + i) & 3))) & 0xffu);
+    if (utf8_err_byte(p3, p2, p1, b)) return false;
+    p3 = p2; p2 = p1; p1 = b;
+  }
+  return !utf8_incomplete(p3, p2, p1);
+}
+
+// ------------------------------------------------------------------ k_parse
+__global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  Agg v = AGG_ID;
+  if (k < a.n_frames) {
+    const uint32_t s = find_session(a.session_first, a.n_sessions, k);
+    const uint64_t o = a.frame_off[k], e = a.frame_off[k + 1];
+    const uint64_t ext = e > o ? e - o : 0;
+    uint8_t h[16];
+    const uint64_t a4 = o & ~3ull;
+    if (a4 + 20 <= a.wire_len) {
+      const uint32_t* p = (const uint32_t*)(a.wire + a4);
+      uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+      const uint32_t sh = (uint32_t)(o & 3);
+      uint32_t w[4] = {alignbyte(d1, d0, sh), alignbyte(d2, d1, sh), alignbyte(d3, d2, sh), alignbyte(d4, d3, sh)};
+#pragma unroll
+      for (int i = 0; i < 16; ++i) h[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+    } else {
+      for (int i = 0; i < 16; ++i) h[i] = (o + i < a.wire_len) ? a.wire[o + i] : 0;
+    }
+    Header hd;
+    uint32_t pre = 0, post = 0, len = 0;
+    uint64_t src = o;
+    if (!parse_header(h, ext, hd)) {
+      pre = WSG_E_BATCH;
+      hd.opcode = h[0] & 15u; hd.fin = h[0] >> 7; hd.rsv = (h[0] >> 4) & 7u; hd.masked = 0; hd.mask = 0;
+    } else {
+      pre = rules_pre(hd, a.client_mode, a.allow_ext);
+      post = rules_post(hd, a.max_payload);
+      if (!pre && !post && (uint64_t)hd.hdr_len + hd.plen != ext) pre = WSG_E_BATCH;
+      if (!pre && !post) {
+        len = (uint32_t)hd.plen;
+        src = o + hd.hdr_len;
+        if (hd.opcode == WSG_OP_CLOSE && len >= 2) {  // createFrame, FrameDecoder.java:121-136
+          uint32_t b0 = a.wire[src] ^ (hd.mask & 0xffu);
+          uint32_t b1 = a.wire[src + 1] ^ ((hd.mask >> 8) & 0xffu);
+          if (!close_status_ok((b0 << 8) | b1)) post = WSG_E_CLOSE_STATUS;
+          else if (len > 2 && !utf8_valid_run(a.wire, src + 2, len - 2, hd.mask, 2)) post = WSG_E_CLOSE_REASON;
+        }
+        if (hd.opcode <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry
+          uint32_t f3 = 0, l3 = 0;
+          const uint32_t nf = len < 3 ? len : 3;
+          for (uint32_t i = 0; i < nf; ++i) {
+            f3 |= (uint32_t)(a.wire[src + i] ^ ((hd.mask >> (8 * (i & 3))) & 0xffu)) << (8 * i);
+            const uint32_t j = len - 1 - i;
+            l3 |= (uint32_t)(a.wire[src + j] ^ ((hd.mask >> (8 * (j & 3))) & 0xffu)) << (8 * (2 - i));
+          }
+          a.edge[k] = f3;
+          a.edge[a.n_frames + k] = l3;
+        }
+      }
+    }
+    if (pre || post) len = 0;
+    FrameRec r;
+    r.src = src;
+    r.out_off = 0;
+    r.len = len;
+    r.mask = hd.mask;
+    r.code = (pre << CODE_PRE_SHIFT) | (post << CODE_POST_SHIFT) | (hd.fin ? CODE_FIN : 0u) |
+             (hd.rsv << CODE_RSV_SHIFT) | (hd.masked ? CODE_MASKED : 0u) | (hd.opcode << CODE_OP_SHIFT);
+    r.sess = s;
+    a.rec[k] = r;
+    v.sum = (uint64_t)((len + 15u) & ~15u);
+    const bool data = code_is_data(r.code);
+    v.m0 = data ? (int32_t)k : -1;
+    v.m1 = code_is_start(r.code) ? (int32_t)k : -1;
+    v.m2 = (data && len) ? (int32_t)k : -1;
+  }
+  Agg tot;
+  block_excl_scan(v, &tot);
+  if (threadIdx.x == 0) {
+    a.blk_sum[blockIdx.x] = tot.sum;
+    a.blk_max[blockIdx.x] = tot.m0;
+    a.blk_max[a.nblk + blockIdx.x] = tot.m1;
+    a.blk_max[2 * a.nblk + blockIdx.x] = tot.m2;
+  }
+}
+
+// ------------------------------------------------------------------ k_scan
+__global__ __launch_bounds__(1024) void k_scan(DecodeArgs a) {
+  Agg carry = AGG_ID;
+  for (uint32_t base = 0; base < a.nblk; base += 1024) {
+    const uint32_t b = base + threadIdx.x;
+    Agg v = AGG_ID;
+    if (b < a.nblk) {
+      v.sum = a.blk_sum[b];
+      v.m0 = a.blk_max[b];
+      v.m1 = a.blk_max[a.nblk + b];
+      v.m2 = a.blk_max[2 * a.nblk + b];
+    }
+    Agg tot;
+    Agg ex = agg_op(carry, block_excl_scan(v, &tot));
+    if (b < a.nblk) {
+      a.blk_sum[b] = ex.sum;
+      a.blk_max[b] = ex.m0;
+      a.blk_max[a.nblk + b] = ex.m1;
+      a.blk_max[2 * a.nblk + b] = ex.m2;
+    }
+    carry = agg_op(carry, tot);
+  }
+  if (threadIdx.x == 0) *a.total = carry.sum;
+}
+
+// ------------------------------------------------------------------ k_link
+__global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = k < a.n_frames;
+  FrameRec r;
+  Agg v = AGG_ID;
+  if (live) {
+    r = a.rec[k];
+    v.sum = (uint64_t)((r.len + 15u) & ~15u);
+    const bool data = code_is_data(r.code);
+    v.m0 = data ? (int32_t)k : -1;
+    v.m1 = code_is_start(r.code) ? (int32_t)k : -1;
+    v.m2 = (data && r.len) ? (int32_t)k : -1;
+  }
+  Agg tot;
+  Agg ex = block_excl_scan(v, &tot);
+  if (!live) return;
+  Agg bp;
+  bp.sum = a.blk_sum[blockIdx.x];
+  bp.m0 = a.blk_max[blockIdx.x];
+  bp.m1 = a.blk_max[a.nblk + blockIdx.x];
+  bp.m2 = a.blk_max[2 * a.nblk + blockIdx.x];
+  ex = agg_op(bp, ex);
+  a.prev[k] = ex.m0;
+  a.prev[a.n_frames + k] = ex.m1;
+  a.prev[2 * a.n_frames + k] = ex.m2;
+
+  const uint32_t s = r.sess;
+  const int32_t sf = (int32_t)a.session_first[s];
+  const wsg_session_state st = a.state[s];
+  const uint32_t op = code_op(r.code);
+  uint32_t extra = 0;
+  if (!code_pre(r.code)) {
+    // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
+    const int32_t j = ex.m0;
+    const bool frag = j >= sf ? !(a.rec[j].code & CODE_FIN) : (st.fragmentation != 0);
+    extra |= rules_frag(op, frag) << CODE_FRAG_SHIFT;
+    if (a.validate) {
+      bool text = op == WSG_OP_TEXT;
+      if (op == WSG_OP_CONTINUATION) {
+        const int32_t ms = ex.m1;
+        text = ms >= sf ? code_op(a.rec[ms].code) == WSG_OP_TEXT : (st.text_open != 0);
+      }
+      if (text) extra |= CODE_VALIDATE;
+    }
+  }
+  a.rec[k].out_off = ex.sum;
+  a.rec[k].code = r.code | extra;
+  wsg_frame_desc d;
+  d.payload_off = ex.sum;
+  d.payload_len = r.len;
+  d.opcode = (uint8_t)op;
+  d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
+                      ((r.code & CODE_MASKED) ? 1u : 0u));
+  d.status = 0;
+  a.desc[k] = d;
+}
+
+// ------------------------------------------------------------------ k_unmask
+// Carry bytes of the text message before frame k (<= 3, oldest first).
+__device__ uint32_t message_carry(const DecodeArgs& a, uint64_t k, uint32_t op, uint32_t sess, uint8_t c[3]) {
+  if (op != WSG_OP_CONTINUATION) return 0;  // a TEXT frame starts its message
+  const int32_t sf = (int32_t)a.session_first[sess];
+  const int32_t ms = a.prev[a.n_frames + k];
+  const bool in_batch = ms >= sf;
+  const int32_t lo = in_batch ? ms : sf;
+  uint8_t rev[3];  // newest first
+  uint32_t n = 0;
+  int32_t j = a.prev[2 * a.n_frames + k];
+  while (n < 3 && j >= lo) {
+    const uint32_t lj = a.rec[j].len;
+    const uint32_t l3 = a.edge[a.n_frames + j];
+    const uint32_t have = lj < 3 ? lj : 3;
+    for (uint32_t i = 0; i < have && n < 3; ++i) rev[n++] = (uint8_t)(l3 >> (8 * (2 - i)));
+    j = a.prev[2 * a.n_frames + j];
+  }
+  if (n < 3 && !in_batch) {
+    const wsg_session_state st = a.state[sess];
+    for (uint32_t i = 0; i < st.tail_len && n < 3; ++i) rev[n++] = st.tail[st.tail_len - 1 - i];
+  }
+  for (uint32_t i = 0; i < n; ++i) c[i] = rev[n - 1 - i];
+  return n;
+}
+
+// UTF-8 verdict of the first (<=3) bytes of the frame after the carry, and of
+// the message end (FIN): FrameUtf8Validator.java:78-96 at the fragment seams.
+__device__ bool edge_utf8_error(const DecodeArgs& a, uint64_t k, const FrameRec& r) {
+  uint8_t s[6];
+  const uint32_t op = code_op(r.code);
+  uint32_t n = message_carry(a, k, op, r.sess, s);
+  const uint32_t nc = n;
+  const uint32_t f3 = a.edge[k], l3 = a.edge[a.n_frames + k];
+  const uint32_t nh = r.len < 3 ? r.len : 3;
+  for (uint32_t i = 0; i < nh; ++i) s[n++] = (uint8_t)(f3 >> (8 * i));
+  for (uint32_t i = nc; i < n; ++i) {
+    const uint32_t p1 = i >= 1 ? s[i - 1] : 0, p2 = i >= 2 ? s[i - 2] : 0, p3 = i >= 3 ? s[i - 3] : 0;
+    if (utf8_err_byte(p3, p2, p1, s[i])) return true;
+  }
+  if (r.code & CODE_FIN) {
+    uint32_t t1, t2, t3;
+    if (r.len >= 3) {
+      t1 = (l3 >> 16) & 0xffu; t2 = (l3 >> 8) & 0xffu; t3 = l3 & 0xffu;
+    } else {
+      t1 = n >= 1 ? s[n - 1] : 0; t2 = n >= 2 ? s[n - 2] : 0; t3 = n >= 3 ? s[n - 3] : 0;
+    }
+    if (utf8_incomplete(t3, t2, t1)) return true;
+  }
+  return false;
+}
+
+template <int U>
+__global__ __launch_bounds__(256) void k_unmask(DecodeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
+  const uint32_t nw = gridDim.x * 4u;
+  const FrameRec* __restrict__ recs = a.rec;
+  for (uint64_t k = wave0; k < a.n_frames; k += nw) {
+    const FrameRec r = recs[k];
+    const uint32_t pre = code_pre(r.code), post = code_post(r.code), frag = code_frag(r.code);
+    uint32_t status = pre ? pre : (frag ? frag : post);
+    if (status == 0) {
+      const bool validate = (r.code & CODE_VALIDATE) != 0;
+      uint32_t errf = 0;
+      if (r.len) {
+        const uint64_t a4 = r.src & ~3ull;
+        const uint32_t sh = (uint32_t)r.src & 3u;
+        const uint64_t avail = a.wire_len - a4;
+        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
+            (void*)(a.wire + a4), 0, (int)(avail > 0x7fffffffull ? 0x7fffffffull : avail), 0x00020000);
+        const uint32_t slot = (r.len + 15u) & ~15u;
+        const __amdgpu_buffer_rsrc_t rout =
+            __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload_out + r.out_off), 0, (int)slot, 0x00020000);
+        const uint32_t m = r.mask;
+        const uint32_t nch = (r.len + 15u) >> 4;
+        const uint32_t rem = r.len & 15u;
+        uint32_t carry = 0;
+        for (uint32_t c0 = 0; c0 < nch; c0 += 64u * U) {
+          u32x4 q[U];
+          uint32_t t[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * 64u + lane;
+            if (c < nch) {
+              q[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, c * 16u, 0, 0);
+              t[u] = __builtin_amdgcn_raw_buffer_load_b32(rin, c * 16u + 16u, 0, 0);
+            } else {
+              q[u] = (u32x4){0u, 0u, 0u, 0u};
+              t[u] = 0u;
+            }
+          }
+          uint32_t w[U][4];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const uint32_t c = c0 + u * 64u + lane;
+            w[u][0] = alignbyte(q[u].y, q[u].x, sh) ^ m;
+            w[u][1] = alignbyte(q[u].z, q[u].y, sh) ^ m;
+            w[u][2] = alignbyte(q[u].w, q[u].z, sh) ^ m;
+            w[u][3] = alignbyte(t[u], q[u].w, sh) ^ m;
+            if (c + 1 == nch && rem) {  // zero the slot padding past the payload
+#pragma unroll
+              for (int i = 0; i < 4; ++i) {
+                const int keep = (int)rem - 4 * i;
+                w[u][i] = keep >= 4 ? w[u][i] : (keep <= 0 ? 0u : (w[u][i] & ((1u << (8 * keep)) - 1u)));
+              }
+            }
+            if (c < nch)
+              __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[u][0], w[u][1], w[u][2], w[u][3]}, rout,
+                                                     c * 16u, 0, 0);
+          }
+          if (validate) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+              const uint32_t c = c0 + u * 64u + lane;
+              uint32_t p = (uint32_t)__shfl_up((int)w[u][3], 1, 64);
+              const uint32_t from_prev = u == 0 ? carry : (uint32_t)__builtin_amdgcn_readlane((int)w[u - 1][3], 63);
+              if (lane == 0) p = from_prev;
+              uint32_t e0 = utf8_err_word(w[u][0], p);
+              uint32_t e1 = utf8_err_word(w[u][1], w[u][0]);
+              uint32_t e2 = utf8_err_word(w[u][2], w[u][1]);
+              uint32_t e3 = utf8_err_word(w[u][3], w[u][2]);
+              if (c == 0) e0 &= 0x80000000u;  // bytes 0..2 are checked against the fragment carry
+              if (c + 1 == nch && rem) {
+                const uint32_t keep[4] = {rem >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - rem))),
+                                          rem >= 8 ? 0x80808080u : (rem <= 4 ? 0u : (0x80808080u >> (8 * (8 - rem)))),
+                                          rem >= 12 ? 0x80808080u : (rem <= 8 ? 0u : (0x80808080u >> (8 * (12 - rem)))),
+                                          rem <= 12 ? 0u : (0x80808080u >> (8 * (16 - rem)))};
+                e0 &= keep[0]; e1 &= keep[1]; e2 &= keep[2]; e3 &= keep[3];
+              }
+              if (c < nch) errf |= e0 | e1 | e2 | e3;
+            }
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)w[U - 1][3], 63);
+          }
+        }
+      }
+      bool bad = __any(errf != 0);
+      if (validate && !bad) bad = edge_utf8_error(a, k, r);
+      if (bad) status = WSG_E_TEXT_UTF8;
+    }
+    if (lane == 0) {
+      a.desc[k].status = (uint16_t)status;
+      if (status) atomicMin((unsigned long long*)&a.sess_err[r.sess], (unsigned long long)k);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ k_final
+__device__ int64_t error_detail(const DecodeArgs& a, uint64_t k, uint32_t err) {
+  const uint64_t o = a.frame_off[k];
+  const uint32_t b0 = a.wire[o], b1 = a.wire[o + 1];
+  switch (err) {
+    case WSG_E_OPCODE: return b0 & 15;
+    case WSG_E_RSV: return (b0 >> 4) & 7;
+    case WSG_E_CONTROL_LEN:
+    case WSG_E_CLOSE_LEN: return b1 & 0x7f;
+    case WSG_E_TOO_LONG: return a.max_payload;
+    case WSG_E_CLOSE_STATUS: {
+      const FrameRec r = a.rec[k];
+      const uint32_t s0 = a.wire[r.src] ^ (r.mask & 0xffu), s1 = a.wire[r.src + 1] ^ ((r.mask >> 8) & 0xffu);
+      return (int64_t)((s0 << 8) | s1);
+    }
+    default: return 0;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_final(DecodeArgs a) {
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s >= a.n_sessions) return;
+  wsg_session_state st = a.state[s];
+  wsg_session_result res = {0u, 0u, 0u, 0};
+  const uint32_t sf = a.session_first[s], se = a.session_first[s + 1];
+  if (st.closed) {  // FrameDecoder.closed: all further input is swallowed (:185-187)
+    a.result[s] = res;
+    return;
+  }
+  const uint64_t fe = a.sess_err[s];
+  if (fe != ~0ull) {
+    const uint32_t err = a.desc[fe].status;
+    res.n_delivered = (uint32_t)(fe - sf);
+    res.error = (uint16_t)err;
+    res.close_code = close_code_of(err);
+    res.detail = error_detail(a, fe, err);
+    st.closed = 1;
+  } else {
+    res.n_delivered = se - sf;
+    if (se > sf) {
+      const uint64_t last = se - 1;
+      const uint32_t cl = a.rec[last].code;
+      const int32_t ld = code_is_data(cl) ? (int32_t)last : a.prev[last];
+      if (ld >= (int32_t)sf) {
+        const bool frag = !(a.rec[ld].code & CODE_FIN);
+        st.fragmentation = frag;
+        bool text = false;
+        int32_t ls = -1;
+        if (a.validate && frag) {
+          ls = code_is_start(cl) ? (int32_t)last : a.prev[a.n_frames + last];
+          text = ls >= (int32_t)sf ? code_op(a.rec[ls].code) == WSG_OP_TEXT : (st.text_open != 0);
+        }
+        if (text) {  // tail = last <= 3 bytes of the open text message
+          uint8_t rev[3];
+          uint32_t n = 0;
+          const bool in_batch = ls >= (int32_t)sf;
+          const int32_t lo = in_batch ? ls : (int32_t)sf;
+          int32_t j = (code_is_data(cl) && a.rec[last].len) ? (int32_t)last : a.prev[2 * a.n_frames + last];
+          while (n < 3 && j >= lo) {
+            const uint32_t lj = a.rec[j].len, l3 = a.edge[a.n_frames + j];
+            const uint32_t have = lj < 3 ? lj : 3;
+            for (uint32_t i = 0; i < have && n < 3; ++i) rev[n++] = (uint8_t)(l3 >> (8 * (2 - i)));
+            j = a.prev[2 * a.n_frames + j];
+          }
+          if (n < 3 && !in_batch)
+            for (uint32_t i = 0; i < st.tail_len && n < 3; ++i) rev[n++] = st.tail[st.tail_len - 1 - i];
+          st.tail_len = (uint8_t)n;
+          for (uint32_t i = 0; i < n; ++i) st.tail[i] = rev[n - 1 - i];
+        } else {
+          st.tail_len = 0;
+        }
+        st.text_open = text;
+      }
+    }
+  }
+  a.state[s] = st;
+  a.result[s] = res;
+}
+
+// ------------------------------------------------------------------ launchers
+void launch_parse(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_parse, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+}
+void launch_scan(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, a);
+}
+void launch_link(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+}
+void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid) {
+  hipLaunchKernelGGL(k_unmask<4>, dim3(grid), dim3(256), 0, s, a);
+}
+void launch_final(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);
+}
+
+}  // namespace ws

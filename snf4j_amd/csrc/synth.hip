@@ -1,0 +1,123 @@
+// synth.hip — synthetic frame batches generated in HBM (bench / tests only).
+// Byte-identical to the oracle's or_synth_uniform (oracle/ws_oracle.c), so a
+// sample copied back can be checked on the host.
+#include "wsgpu_internal.h"
+
+namespace ws {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// 16 bytes of valid UTF-8 whose code points never straddle the chunk.
+__device__ void synth_text16(uint64_t h, uint8_t out[16]) {
+  int i = 0, draws = 0;
+  uint64_t r = h;
+  while (i < 16) {
+    if (draws == 8) { r = splitmix64(r); draws = 0; }
+    const unsigned v = (unsigned)(r & 0xff);
+    r >>= 8;
+    ++draws;
+    const int room = 16 - i;
+    const unsigned kind = v % 10;
+    if (kind <= 6 || room < 2) {
+      out[i++] = (uint8_t)(0x20 + (v % 95));
+    } else if (kind == 7 || room < 3) {
+      const unsigned cp = 0x80 + (v * 7u) % (0x800 - 0x80);
+      out[i++] = (uint8_t)(0xC0 | (cp >> 6));
+      out[i++] = (uint8_t)(0x80 | (cp & 0x3f));
+    } else if (kind == 8 || room < 4) {
+      unsigned cp = 0x800 + (v * 211u) % (0x10000 - 0x800);
+      if (cp >= 0xD800 && cp <= 0xDFFF) cp += 0x800;
+      out[i++] = (uint8_t)(0xE0 | (cp >> 12));
+      out[i++] = (uint8_t)(0x80 | ((cp >> 6) & 0x3f));
+      out[i++] = (uint8_t)(0x80 | (cp & 0x3f));
+    } else {
+      const unsigned cp = 0x10000 + (v * 4099u) % (0x110000 - 0x10000);
+      out[i++] = (uint8_t)(0xF0 | (cp >> 18));
+      out[i++] = (uint8_t)(0x80 | ((cp >> 12) & 0x3f));
+      out[i++] = (uint8_t)(0x80 | ((cp >> 6) & 0x3f));
+      out[i++] = (uint8_t)(0x80 | (cp & 0x3f));
+    }
+  }
+}
+
+__device__ __forceinline__ uint32_t hdr_len(uint32_t len, int masked) {
+  return 2u + (len > 0xffffu ? 8u : (len > 125u ? 2u : 0u)) + (masked ? 4u : 0u);
+}
+
+__global__ __launch_bounds__(256) void k_synth_payload(uint64_t seed, uint64_t n_frames, uint32_t payload_len,
+                                                       uint32_t fps, int masked, int text, uint8_t* wire) {
+  const uint32_t hl = hdr_len(payload_len, masked);
+  const uint64_t flen = hl + (uint64_t)payload_len;
+  const uint64_t nch = (payload_len + 15u) / 16u;
+  const uint64_t total = n_frames * nch;
+  for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256) {
+    const uint64_t k = t / nch, c = t - k * nch;
+    const uint64_t sseed = seed ^ (k / fps);
+    const uint64_t fh = splitmix64(sseed ^ (k * 0x9E3779B97F4A7C15ull));
+    const uint64_t h = splitmix64(fh + c);
+    uint8_t tmp[16];
+    if (text) {
+      synth_text16(h, tmp);
+    } else {
+      const uint64_t h2 = splitmix64(h);
+      for (int i = 0; i < 8; ++i) { tmp[i] = (uint8_t)(h >> (8 * i)); tmp[8 + i] = (uint8_t)(h2 >> (8 * i)); }
+    }
+    const uint32_t n = payload_len - c * 16 < 16 ? (uint32_t)(payload_len - c * 16) : 16u;
+    if (text && n < 16) {
+      uint32_t cut = n;
+      while (cut > 0 && (tmp[cut] & 0xC0) == 0x80) --cut;
+      for (uint32_t i = cut; i < n; ++i) tmp[i] = 'a';
+    }
+    uint8_t* pl = wire + k * flen + hl + c * 16;
+    for (uint32_t i = 0; i < n; ++i) pl[i] = masked ? (uint8_t)(tmp[i] ^ (uint8_t)(fh >> (8 * (i & 3)))) : tmp[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_synth_header(uint64_t seed, uint64_t n_frames, uint32_t payload_len,
+                                                      uint32_t fps, int opcode, int masked, uint8_t* wire,
+                                                      uint64_t* frame_off, uint32_t* session_first) {
+  const uint32_t hl = hdr_len(payload_len, masked);
+  const uint64_t flen = hl + (uint64_t)payload_len;
+  const uint64_t n_sessions = (n_frames + fps - 1) / fps;
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k <= n_frames; k += (uint64_t)gridDim.x * 256) {
+    frame_off[k] = k * flen;
+    if (k <= n_sessions) {
+      const uint64_t f = k * fps;
+      session_first[k] = (uint32_t)(f < n_frames ? f : n_frames);
+    }
+    if (k == n_frames) continue;
+    const uint64_t fh = splitmix64((seed ^ (k / fps)) ^ (k * 0x9E3779B97F4A7C15ull));
+    uint8_t* w = wire + k * flen;
+    uint32_t p = 0;
+    w[p++] = (uint8_t)(0x80 | (opcode & 0x0f));
+    const uint8_t b1 = masked ? 0x80 : 0;
+    if (payload_len > 0xffffu) {
+      w[p++] = b1 | 127;
+      for (int i = 7; i >= 0; --i) w[p++] = (uint8_t)((uint64_t)payload_len >> (8 * i));
+    } else if (payload_len > 125u) {
+      w[p++] = b1 | 126;
+      w[p++] = (uint8_t)(payload_len >> 8);
+      w[p++] = (uint8_t)payload_len;
+    } else {
+      w[p++] = b1 | (uint8_t)payload_len;
+    }
+    if (masked)
+      for (int i = 0; i < 4; ++i) w[p++] = (uint8_t)(fh >> (8 * i));
+  }
+}
+
+void launch_synth(uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode, int masked,
+                  int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first, hipStream_t s) {
+  hipLaunchKernelGGL(k_synth_header, dim3(2048), dim3(256), 0, s, seed, n_frames, payload_len, fps, opcode, masked,
+                     wire, frame_off, session_first);
+  if (payload_len)
+    hipLaunchKernelGGL(k_synth_payload, dim3(8192), dim3(256), 0, s, seed, n_frames, payload_len, fps, masked, text,
+                       wire);
+}
+
+}  // namespace ws

@@ -1,0 +1,172 @@
+// ws_rules.h — RFC 6455 header rules and the UTF-8 position rule, shared by the
+// HIP kernels and the host side of libwsgpu (wsg_check_header / wsg_frame_available).
+//
+// Semantics follow snf4j-websocket (paths under .../websocket/frame/):
+//   header rules and their order ........ FrameDecoder.java:197-256
+//   available() framing ................. FrameDecoder.java:357-401
+//   close status / reason ............... FrameDecoder.java:121-136
+//   UTF-8 verdicts ...................... Utf8.java:73-92 (Hoehrmann DFA)
+#pragma once
+#include <stdint.h>
+
+#include "../../include/wsgpu.h"
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define WS_HD __host__ __device__ __forceinline__
+#else  // plain C++ host build of the rules (tests/cpp: exhaustive rule-vs-DFA check)
+#define WS_HD static inline
+#endif
+
+namespace ws {
+
+// Opcode.findByValue(v) != null (Opcode.java:48-50)
+WS_HD bool known_opcode(uint32_t v) { return v <= 2u || (v >= 8u && v <= 10u); }
+WS_HD bool is_control(uint32_t v) { return v >= 8u; }
+
+// Parsed frame header.
+struct Header {
+  uint32_t opcode, fin, rsv, masked, len7;
+  uint32_t hdr_len;  // 2 + ext + (masked ? 4 : 0)
+  uint64_t plen;     // payload length as read (u16 / u64 big-endian)
+  uint32_t mask;     // mask key as a little-endian u32 of the 4 wire bytes
+};
+
+// Parse the header from the first n (<= 14 used) bytes; returns false when the
+// header is not complete within n bytes.
+WS_HD bool parse_header(const uint8_t* h, uint64_t n, Header& o) {
+  if (n < 2) return false;
+  uint32_t b0 = h[0], b1 = h[1];
+  o.opcode = b0 & 0x0fu;
+  o.fin = b0 >> 7;
+  o.rsv = (b0 >> 4) & 7u;
+  o.masked = b1 >> 7;
+  o.len7 = b1 & 0x7fu;
+  uint32_t ext = o.len7 == 126 ? 2u : (o.len7 == 127 ? 8u : 0u);
+  o.hdr_len = 2u + ext + (o.masked ? 4u : 0u);
+  if (n < o.hdr_len) return false;
+  if (ext == 0) {
+    o.plen = o.len7;
+  } else if (ext == 2) {
+    o.plen = ((uint64_t)h[2] << 8) | h[3];
+  } else {
+    uint64_t v = 0;
+    for (int i = 0; i < 8; ++i) v = (v << 8) | h[2 + i];
+    o.plen = v;
+  }
+  if (o.masked) {
+    const uint8_t* m = h + 2 + ext;
+    o.mask = (uint32_t)m[0] | ((uint32_t)m[1] << 8) | ((uint32_t)m[2] << 16) | ((uint32_t)m[3] << 24);
+  } else {
+    o.mask = 0;
+  }
+  return true;
+}
+
+// The header checks of FrameDecoder.decode that run before the fragmentation
+// test (:197-228): opcode, RSV, masking, control-frame rules.
+WS_HD uint32_t rules_pre(const Header& h, int client_mode, int allow_ext) {
+  if (!known_opcode(h.opcode)) return WSG_E_OPCODE;
+  if (h.rsv != 0 && !allow_ext) return WSG_E_RSV;
+  if ((int)h.masked == (client_mode ? 1 : 0)) return WSG_E_MASKING;
+  if (is_control(h.opcode)) {
+    if (!h.fin) return WSG_E_FRAG_CONTROL;
+    if (h.len7 > 125) return WSG_E_CONTROL_LEN;
+    if (h.opcode == WSG_OP_CLOSE && h.len7 == 1) return WSG_E_CLOSE_LEN;
+  }
+  return WSG_OK;
+}
+
+// Fragmentation test (:229-236) given FrameDecoder.fragmentation before the frame.
+WS_HD uint32_t rules_frag(uint32_t opcode, bool fragmentation) {
+  if (opcode == WSG_OP_CONTINUATION) return fragmentation ? WSG_OK : WSG_E_CONT_OUTSIDE;
+  if (opcode == WSG_OP_TEXT || opcode == WSG_OP_BINARY) return fragmentation ? WSG_E_NONCONT_INSIDE : WSG_OK;
+  return WSG_OK;
+}
+
+// Length checks after the fragmentation test (:238-256).
+WS_HD uint32_t rules_post(const Header& h, int64_t max_payload) {
+  if (h.len7 == 126) {
+    if (h.plen < 126) return WSG_E_MIN_LEN;
+  } else if (h.len7 == 127) {
+    int64_t v = (int64_t)h.plen;
+    if (v < 0 || v > 0x7fffffffLL) return WSG_E_MAX_PAYLOAD;
+    if (v <= 0xffff) return WSG_E_MIN_LEN;
+  }
+  if ((int64_t)h.plen > max_payload) return WSG_E_TOO_LONG;
+  return WSG_OK;
+}
+
+// Close status range (:124-128).
+WS_HD bool close_status_ok(uint32_t status) { return status > 999u && status <= 4999u; }
+
+WS_HD uint16_t close_code_of(uint32_t err) {
+  if (err == WSG_OK) return 0;
+  return (err == WSG_E_CLOSE_REASON || err == WSG_E_TEXT_UTF8) ? WSG_CLOSE_NON_UTF8 : WSG_CLOSE_PROTOCOL_ERROR;
+}
+
+// ---------------------------------------------------------------------------
+// UTF-8.  The Hoehrmann DFA (Utf8.java) rejects at byte p exactly when, with
+// the bytes before p a valid prefix, byte p is not allowed after the last <=3
+// bytes.  That condition needs only the 3 preceding bytes, so every byte can be
+// checked independently; the first flagged byte is the DFA's REJECT byte
+// (proved exhaustively against the DFA in tests/test_utf8_rule.py).
+// All masks below carry one flag per byte in bit 7 (0x80 lanes of a u32).
+// ---------------------------------------------------------------------------
+WS_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbyte(hi, lo, s);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * (s & 3u)));
+#endif
+}
+
+constexpr uint32_t H80 = 0x80808080u;
+
+// Error flags of the 4 bytes of `w` (little-endian: byte 0 first) given the
+// word `p` holding the 4 bytes before it.
+WS_HD uint32_t utf8_err_word(uint32_t w, uint32_t p) {
+  const uint32_t w2 = w << 2, w3 = w << 3;
+  const uint32_t hw = w & H80;
+  const uint32_t cw = hw & (w << 1);  // byte >= C0
+  const uint32_t gw = cw & w2;        // byte >= E0
+  const uint32_t fw = gw & w3;        // byte >= F0
+  const uint32_t hp = p & H80;
+  const uint32_t cp = hp & (p << 1);
+  const uint32_t gp = cp & (p << 2);
+  const uint32_t fp = gp & (p << 3);
+  // a continuation byte is expected after a lead within the last 1/2/3 bytes
+  const uint32_t expect = alignbyte(cw, cp, 3) | alignbyte(gw, gp, 2) | alignbyte(fw, fp, 1);
+  const uint32_t cont = hw ^ cw;  // 10xxxxxx
+  uint32_t err = expect ^ cont;
+  // C0, C1 (overlong 2-byte leads) and F5..FF are rejected at the byte itself
+  err |= cw & ~((w & 0x3E3E3E3Eu) + 0x7F7F7F7Fu);
+  err |= ((w & 0x7F7F7F7Fu) + 0x0B0B0B0Bu) & hw;
+  // second-byte ranges after E0 (A0..BF), ED (80..9F), F0 (90..BF), F4 (80..8F)
+  const uint32_t g1 = alignbyte(gw, gp, 3);  // previous byte >= E0
+  if (g1) {
+    const uint32_t p1 = alignbyte(w, p, 3);
+    const uint32_t n = p1 & 0x0F0F0F0Fu;
+    const uint32_t n0 = ~(n + 0x7F7F7F7Fu);
+    const uint32_t nd = ~((n ^ 0x0D0D0D0Du) + 0x7F7F7F7Fu);
+    const uint32_t n4 = ~((n ^ 0x04040404u) + 0x7F7F7F7Fu);
+    const uint32_t isf = p1 << 3;  // previous byte >= F0 (given >= E0)
+    const uint32_t b5 = w2, b54 = w2 | w3;
+    err |= g1 & ((n0 & ~isf & ~b5) | (nd & ~isf & b5) | (n0 & isf & ~b54) | (n4 & isf & b54));
+  }
+  return err & H80;
+}
+
+// Error flag of a single byte b given its 3 predecessors (p1 nearest).
+WS_HD bool utf8_err_byte(uint32_t p3, uint32_t p2, uint32_t p1, uint32_t b) {
+  uint32_t p = (p3 << 8) | (p2 << 16) | (p1 << 24);
+  return (utf8_err_word(b, p) & 0x80u) != 0;
+}
+
+// DFA state after a valid prefix is not ACCEPT (a continuation is still due),
+// from the last 3 bytes (l1 = last).
+WS_HD bool utf8_incomplete(uint32_t l3, uint32_t l2, uint32_t l1) {
+  return l1 >= 0xC0u || l2 >= 0xE0u || l3 >= 0xF0u;
+}
+
+}  // namespace ws

@@ -1,0 +1,112 @@
+// wsgpu_internal.h — device workspace layout and launch interface shared by the
+// kernels (decode.hip, encode.hip, synth.hip) and the C ABI (api.hip).
+#pragma once
+#include <stdint.h>
+
+#include <hip/hip_runtime.h>
+
+#include "ws_rules.h"
+
+namespace ws {
+
+// Per-frame record of the decode pipeline (32 B, one scalar load per frame).
+struct FrameRec {
+  uint64_t src;      // absolute wire offset of the payload
+  uint64_t out_off;  // payload slot offset in payload_out (16-B aligned), set by k_link
+  uint32_t len;      // payload length (0 when the header failed a rule)
+  uint32_t mask;     // mask key, little-endian u32 of the 4 wire bytes
+  uint32_t code;     // packed: see CODE_*
+  uint32_t sess;     // owning session
+};
+
+// FrameRec.code packing
+constexpr uint32_t CODE_PRE_SHIFT = 0;      // 5 bits: rule error before the fragmentation test
+constexpr uint32_t CODE_POST_SHIFT = 5;     // 5 bits: length / close rules after it
+constexpr uint32_t CODE_FRAG_SHIFT = 10;    // 5 bits: fragmentation error (k_link)
+constexpr uint32_t CODE_VALIDATE = 1u << 15;  // frame belongs to a text message (k_link)
+constexpr uint32_t CODE_FIN = 1u << 16;
+constexpr uint32_t CODE_RSV_SHIFT = 17;     // 3 bits
+constexpr uint32_t CODE_MASKED = 1u << 20;
+constexpr uint32_t CODE_OP_SHIFT = 24;      // 4 bits
+
+__host__ __device__ inline uint32_t code_pre(uint32_t c) { return (c >> CODE_PRE_SHIFT) & 31u; }
+__host__ __device__ inline uint32_t code_post(uint32_t c) { return (c >> CODE_POST_SHIFT) & 31u; }
+__host__ __device__ inline uint32_t code_frag(uint32_t c) { return (c >> CODE_FRAG_SHIFT) & 31u; }
+__host__ __device__ inline uint32_t code_op(uint32_t c) { return (c >> CODE_OP_SHIFT) & 15u; }
+__host__ __device__ inline bool code_is_data(uint32_t c) { return code_op(c) <= 2u && !code_pre(c); }
+__host__ __device__ inline bool code_is_start(uint32_t c) {
+  return (code_op(c) == 1u || code_op(c) == 2u) && !code_pre(c);
+}
+
+constexpr int BLOCK = 256;  // frames per block in the parse / link passes
+
+struct DecodeArgs {
+  // inputs
+  const uint8_t* wire;
+  uint64_t wire_len;
+  const uint64_t* frame_off;
+  uint64_t n_frames;
+  const uint32_t* session_first;
+  uint32_t n_sessions;
+  int32_t client_mode, allow_ext, validate;
+  int64_t max_payload;
+  // in/out
+  wsg_session_state* state;
+  // outputs
+  uint8_t* payload_out;
+  wsg_frame_desc* desc;
+  wsg_session_result* result;
+  // workspace
+  FrameRec* rec;
+  int32_t* prev;       // [3][n_frames]: last data / last TEXT|BINARY / last nonempty data frame before k
+  uint32_t* edge;      // [2][n_frames]: first 3 / last 3 payload bytes (unmasked)
+  uint64_t* blk_sum;   // [nblk] slot-bytes per block -> exclusive prefix
+  int32_t* blk_max;    // [3][nblk] per-block max indices -> exclusive prefix max
+  uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
+  uint64_t* total;     // [1] total payload slot bytes
+  uint32_t nblk;
+};
+
+struct EncodeArgs {
+  int32_t client_mode;
+  const uint8_t* payload;
+  uint64_t payload_len;
+  const wsg_encode_frame* frames;
+  uint64_t n_frames;
+  const uint32_t* session_first;
+  uint32_t n_sessions;
+  uint8_t* closed;
+  uint8_t* wire_out;
+  uint64_t wire_cap;
+  uint64_t* wire_off;  // [n_frames+1]
+  // workspace
+  uint32_t* sess;      // [n_frames]
+  uint64_t* blk_sum;   // [nblk]
+  int32_t* blk_max;    // [nblk] last CLOSE frame index
+  int32_t* last_close; // [n_frames] last CLOSE frame before k
+  uint32_t nblk;
+};
+
+// kernel ids for timing
+enum KernelId {
+  K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_COUNT
+};
+
+// launchers (enqueue on `s`; the timing hook wraps each one)
+void launch_parse(const DecodeArgs& a, hipStream_t s);
+void launch_scan(const DecodeArgs& a, hipStream_t s);
+void launch_link(const DecodeArgs& a, hipStream_t s);
+void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid);
+void launch_final(const DecodeArgs& a, hipStream_t s);
+
+void launch_enc_len(const EncodeArgs& a, hipStream_t s);
+void launch_enc_scan(const EncodeArgs& a, hipStream_t s);
+void launch_enc_emit(const EncodeArgs& a, hipStream_t s, uint32_t grid);
+void launch_enc_final(const EncodeArgs& a, hipStream_t s);
+
+void launch_synth(uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode,
+                  int masked, int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first,
+                  hipStream_t s);
+
+}  // namespace ws

@@ -1,0 +1,84 @@
+// wsgpu_scan.h — wave/block scans of the per-frame aggregates used by the decode
+// and encode pipelines: the payload-length prefix sum and the "last frame of a
+// kind before k" max-scans that replace the reference's sequential per-session
+// state (FrameDecoder.fragmentation, FrameUtf8Validator.context, FrameEncoder.closed).
+#pragma once
+#include "wsgpu_internal.h"
+
+namespace ws {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, int d) {
+  uint32_t lo = __shfl_up((unsigned)v, d, 64), hi = __shfl_up((unsigned)(v >> 32), d, 64);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// Inclusive block scan (256 threads) of {sum, max a, max b, max c}; returns the
+// thread's EXCLUSIVE values and the block totals.
+struct Agg {
+  uint64_t sum;
+  int32_t m0, m1, m2;
+};
+
+__device__ __forceinline__ Agg agg_op(const Agg& x, const Agg& y) {
+  Agg r;
+  r.sum = x.sum + y.sum;
+  r.m0 = x.m0 > y.m0 ? x.m0 : y.m0;
+  r.m1 = x.m1 > y.m1 ? x.m1 : y.m1;
+  r.m2 = x.m2 > y.m2 ? x.m2 : y.m2;
+  return r;
+}
+
+__device__ __forceinline__ Agg wave_incl_scan(Agg v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    Agg t;
+    t.sum = shfl_up_u64(v.sum, d);
+    t.m0 = __shfl_up(v.m0, d, 64);
+    t.m1 = __shfl_up(v.m1, d, 64);
+    t.m2 = __shfl_up(v.m2, d, 64);
+    if (lane >= d) v = agg_op(t, v);
+  }
+  return v;
+}
+
+constexpr Agg AGG_ID = {0ull, -1, -1, -1};
+
+// Block-wide exclusive scan; nthreads = blockDim.x (multiple of 64, <= 1024).
+__device__ inline Agg block_excl_scan(Agg v, Agg* total) {
+  __shared__ Agg wsum[16];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  Agg inc = wave_incl_scan(v);
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  Agg pre = AGG_ID, tot = AGG_ID;
+  for (int i = 0; i < nw; ++i) {
+    if (i < wid) pre = agg_op(pre, wsum[i]);
+    tot = agg_op(tot, wsum[i]);
+  }
+  __syncthreads();
+  // exclusive within the wave: inclusive of lane-1
+  Agg ex;
+  ex.sum = shfl_up_u64(inc.sum, 1);
+  ex.m0 = __shfl_up(inc.m0, 1, 64);
+  ex.m1 = __shfl_up(inc.m1, 1, 64);
+  ex.m2 = __shfl_up(inc.m2, 1, 64);
+  if (lane == 0) ex = AGG_ID;
+  *total = tot;
+  return agg_op(pre, ex);
+}
+
+// session owning frame k: largest s with session_first[s] <= k
+__device__ __forceinline__ uint32_t find_session(const uint32_t* sf, uint32_t n_sessions, uint64_t k) {
+  uint32_t lo = 0, hi = n_sessions ? n_sessions - 1 : 0;
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if ((uint64_t)sf[mid] <= k) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+}  // namespace ws

@@ -1,0 +1,92 @@
+"""GPU parity of the encode path (FrameEncoder) against the oracle and the
+reference's FrameEncoderTest layouts; encode -> decode round trips."""
+import numpy as np
+import pytest
+
+from tests.golden import fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from snf4j_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _frames(specs):
+    from snf4j_amd._lib import ENCODE_DTYPE
+    fr = np.zeros(len(specs), dtype=ENCODE_DTYPE)
+    payload = []
+    off = 0
+    for i, (op, fin, rsv, p, mask) in enumerate(specs):
+        fr[i]["payload_off"] = off
+        fr[i]["payload_len"] = len(p)
+        fr[i]["opcode"] = op
+        fr[i]["flags"] = (0x80 if fin else 0) | (rsv << 4)
+        fr[i]["mask"] = mask
+        payload.append(p)
+        off += len(p)
+    return np.frombuffer(b"".join(payload), dtype=np.uint8).copy() if off else np.zeros(0, np.uint8), fr
+
+
+def test_encoder_kat(ctx):
+    from tests.test_oracle_golden import _encoder_layout
+    for i, v in enumerate(fixtures.load("encoder")):
+        payload = fixtures.unhex(v["payload"])
+        mask = (0x11 * (i % 7 + 1), 0x5A, 0xA5, i & 0xFF)
+        pl, fr = _frames([(v["opcode"], v["fin"], v["rsv"], payload, mask)])
+        closed = np.zeros(1, np.uint8)
+        wire, off = ctx.encode_host(v["client_mode"], pl, fr, np.array([0, 1], np.uint32), closed)
+        assert _encoder_layout(wire.tobytes()) == v["expect"]
+
+
+@pytest.mark.parametrize("cm", [True, False])
+def test_random_encode_batches(ctx, oracle, cm):
+    rng = np.random.default_rng(31 + cm)
+    specs, first = [], [0]
+    exp = []
+    for s in range(150):
+        enc = oracle.Encoder(cm)
+        for _ in range(int(rng.integers(0, 9))):
+            r = rng.random()
+            op = 8 if r < 0.05 else 9 if r < 0.1 else int(rng.choice([0, 1, 2]))
+            n = int(rng.integers(0, 125 if op >= 8 else 70000 if rng.random() < 0.1 else 300))
+            p = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            fin, rsv = bool(rng.integers(0, 2)) or op >= 8, int(rng.integers(0, 8))
+            mask = tuple(int(x) for x in rng.integers(0, 256, 4))
+            specs.append((op, fin, rsv, p, mask))
+            exp.append(enc.encode(op, fin, rsv, p, mask))
+        first.append(len(specs))
+    pl, fr = _frames(specs)
+    closed = np.zeros(len(first) - 1, np.uint8)
+    wire, off = ctx.encode_host(cm, pl, fr, np.array(first, np.uint32), closed)
+    for k in range(len(specs)):
+        assert wire[int(off[k]):int(off[k + 1])].tobytes() == exp[k], k
+    # the close latch carried out: sessions that sent CLOSE are closed
+    for s in range(len(first) - 1):
+        assert closed[s] == any(specs[k][0] == 8 for k in range(first[s], first[s + 1]))
+
+
+def test_encode_decode_round_trip(ctx, oracle):
+    """16 MiB messages fragmented into 64 KiB frames (BASELINE config 5 at reduced count)."""
+    from snf4j_amd import decoder_cfg
+    from snf4j_amd._lib import STATE_DTYPE
+    rng = np.random.default_rng(2)
+    msg = rng.integers(0, 256, 1 << 22, dtype=np.uint8).tobytes()
+    specs = []
+    for i in range(0, len(msg), 65536):
+        specs.append((2 if i == 0 else 0, i + 65536 >= len(msg), 0, msg[i:i + 65536],
+                      tuple(int(x) for x in rng.integers(0, 256, 4))))
+    pl, fr = _frames(specs)
+    closed = np.zeros(1, np.uint8)
+    wire, off = ctx.encode_host(True, pl, fr, np.array([0, len(specs)], np.uint32), closed)
+    state = np.zeros(1, dtype=STATE_DTYPE)
+    payload, desc, res = ctx.decode_host(decoder_cfg(False, False, 65536), wire, off, np.array([0, len(specs)],
+                                                                                                np.uint32), state)
+    assert res[0]["n_delivered"] == len(specs) and res[0]["error"] == 0
+    got = b"".join(payload[int(d["payload_off"]):int(d["payload_off"]) + int(d["payload_len"])].tobytes()
+                   for d in desc)
+    assert got == msg

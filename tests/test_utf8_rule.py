@@ -1,0 +1,17 @@
+"""The per-byte UTF-8 rule used by the kernels (snf4j_amd/csrc/ws_rules.h) flags
+exactly the byte at which the reference DFA (Utf8.java) rejects — exhaustively
+over every DFA class and range boundary up to length 5, all 2-byte strings and
+random strings — and its end-of-message test equals "state != ACCEPT"."""
+import os
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_rule_equals_dfa(tmp_path):
+    exe = str(tmp_path / "utf8_rule_check")
+    subprocess.run(["g++", "-O2", "-std=c++17", "-o", exe, os.path.join(ROOT, "tests/cpp/utf8_rule_check.cpp"),
+                    "-x", "c", os.path.join(ROOT, "oracle/ws_oracle.c")], check=True)
+    r = subprocess.run([exe, "5", "300000"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "0 mismatches" in r.stdout
