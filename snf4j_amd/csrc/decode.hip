@@ -277,9 +277,15 @@ __global__ __launch_bounds__(256) void k_unmask(DecodeArgs a) {
 #pragma unroll
           for (int u = 0; u < U; ++u) {
             const uint32_t c = c0 + u * 64u + lane;
-            if (c < nch) {
+            if (c < nch && (uint64_t)c * 16u + 20u <= avail) {
               q[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, c * 16u, 0, 0);
               t[u] = __builtin_amdgcn_raw_buffer_load_b32(rin, c * 16u + 16u, 0, 0);
+            } else if (c < nch) {  // the last bytes of the wire: byte loads (the range check is per dword)
+              uint32_t d[5] = {0u, 0u, 0u, 0u, 0u};
+              for (uint32_t i = 0; i < 20u && (uint64_t)c * 16u + i < avail; ++i)
+                d[i >> 2] |= (uint32_t)a.wire[a4 + c * 16u + i] << (8 * (i & 3));
+              q[u] = (u32x4){d[0], d[1], d[2], d[3]};
+              t[u] = d[4];
             } else {
               q[u] = (u32x4){0u, 0u, 0u, 0u};
               t[u] = 0u;

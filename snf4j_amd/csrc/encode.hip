@@ -157,8 +157,18 @@ __global__ __launch_bounds__(256) void k_enc_emit(EncodeArgs a) {
         const uint64_t rel = (ps & 3) + j0;
         const uint32_t sh = (uint32_t)(rel & 3);
         const uint32_t off = (uint32_t)(rel & ~3ull);
-        const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
-        const uint32_t t = __builtin_amdgcn_raw_buffer_load_b32(rin, off + 16, 0, 0);
+        u32x4 q;
+        uint32_t t;
+        if ((uint64_t)off + 20u <= pavail) {
+          q = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
+          t = __builtin_amdgcn_raw_buffer_load_b32(rin, off + 16, 0, 0);
+        } else {  // the last bytes of the payload buffer: byte loads
+          uint32_t d[5] = {0u, 0u, 0u, 0u, 0u};
+          for (uint32_t i = 0; i < 20u && (uint64_t)off + i < pavail; ++i)
+            d[i >> 2] |= (uint32_t)a.payload[pa4 + off + i] << (8 * (i & 3));
+          q = (u32x4){d[0], d[1], d[2], d[3]};
+          t = d[4];
+        }
         const uint32_t ph = (uint32_t)(j0 & 3);
         const uint32_t mr = ph ? ((m >> (8 * ph)) | (m << (32 - 8 * ph))) : m;
         u32x4 o;
