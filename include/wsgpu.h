@@ -151,7 +151,7 @@ int wsg_close(wsg_ctx* ctx);
 int wsg_set_stream(wsg_ctx* ctx, void* stream);
 const char* wsg_last_error(wsg_ctx* ctx);
 /* Pre-size device workspace so later batch calls do no allocation (graph-capture safe). */
-int wsg_reserve(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions);
+int wsg_reserve(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len);
 int wsg_sync(wsg_ctx* ctx);
 
 /* Kernel timing (hipEvents recorded around each kernel on the ctx stream). */
@@ -250,6 +250,10 @@ int wsg_encode_batch_host(wsg_ctx* ctx, int client_mode,
 int wsg_synth_uniform(wsg_ctx* ctx, uint64_t seed, uint64_t n_frames, uint32_t payload_len,
                       uint32_t frames_per_session, int opcode, int masked, int text,
                       uint8_t* wire, uint64_t* frame_off, uint32_t* session_first);
+
+/* Measured streaming ceiling of this device: best-of-`reps` nontemporal 16-B
+ * copy of `bytes` from src to dst (device pointers), in GB/s of read+write. */
+int wsg_copy_ceiling(wsg_ctx* ctx, const void* src, void* dst, uint64_t bytes, int reps, double* gbs);
 
 #ifdef __cplusplus
 }

@@ -77,7 +77,7 @@ def _load():
         "wsg_close": ([p], i32),
         "wsg_set_stream": ([p, p], i32),
         "wsg_last_error": ([p], C.c_char_p),
-        "wsg_reserve": ([p, u64, u32], i32),
+        "wsg_reserve": ([p, u64, u32, u64], i32),
         "wsg_sync": ([p], i32),
         "wsg_set_timing": ([p, i32], i32),
         "wsg_get_timing": ([p, P(C.c_double), P(u64), i32], i32),
@@ -93,6 +93,7 @@ def _load():
         "wsg_encode_batch_device": ([p, i32, p, u64, p, u64, p, u32, p, p, u64, p], i32),
         "wsg_encode_batch_host": ([p, i32, p, u64, p, u64, p, u32, p, p, u64, p], i32),
         "wsg_synth_uniform": ([p, u64, u64, u32, u32, i32, i32, i32, p, p, p], i32),
+        "wsg_copy_ceiling": ([p, p, p, u64, i32, P(C.c_double)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

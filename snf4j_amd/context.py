@@ -89,8 +89,8 @@ class Context:
     def sync(self):
         check(lib.wsg_sync(self._h), self._h)
 
-    def reserve(self, max_frames: int, max_sessions: int):
-        check(lib.wsg_reserve(self._h, int(max_frames), int(max_sessions)), self._h)
+    def reserve(self, max_frames: int, max_sessions: int, max_wire_len: int = 0):
+        check(lib.wsg_reserve(self._h, int(max_frames), int(max_sessions), int(max_wire_len)), self._h)
 
     def set_timing(self, on: bool = True):
         check(lib.wsg_set_timing(self._h, int(on)), self._h)
@@ -161,6 +161,12 @@ class Context:
                                         n_frames, session_first.ctypes.data, n_sessions, closed.ctypes.data,
                                         wire.ctypes.data, cap, wire_off.ctypes.data), self._h)
         return wire[:int(wire_off[-1])], wire_off
+
+    def copy_ceiling(self, src, dst, nbytes: int, reps: int = 5) -> float:
+        """GB/s (read+write) of the device's best streaming copy over nbytes (tensors)."""
+        g = C.c_double(0)
+        check(lib.wsg_copy_ceiling(self._h, _p(src), _p(dst), int(nbytes), int(reps), C.byref(g)), self._h)
+        return float(g.value)
 
     # -------------------------------------------------------------- synthetic data
     def synth_uniform(self, seed, n_frames, payload_len, frames_per_session, opcode, masked, text, wire,

@@ -13,8 +13,9 @@ using namespace ws;
 
 namespace {
 
-const char* const kKernelNames[K_COUNT] = {"k_parse",    "k_scan",     "k_link",     "k_unmask",    "k_final",
-                                           "k_enc_len",  "k_enc_scan", "k_enc_emit", "k_enc_final", "k_synth"};
+const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_pieces",
+                                           "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
+                                           "k_enc_emit", "k_enc_final", "k_synth"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -49,7 +50,7 @@ struct wsg_ctx {
   bool own_stream = false;
   std::string err;
   // decode workspace
-  DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total;
+  DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total, pieces, utf8_err;
   // encode workspace
   DevBuf esess, elast_close;
   // host-path device buffers
@@ -156,7 +157,7 @@ int wsg_close(wsg_ctx* c) {
   drain_timing(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->rec,     &c->prev,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
-                    &c->total,   &c->esess,   &c->elast_close, &c->h_wire, &c->h_off,    &c->h_sf,
+                    &c->total,   &c->pieces, &c->utf8_err, &c->esess,   &c->elast_close, &c->h_wire, &c->h_off,    &c->h_sf,
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
@@ -208,9 +209,11 @@ int wsg_reset_timing(wsg_ctx* c) {
   return WSG_API_OK;
 }
 
-static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions) {
+static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, uint64_t wire_len) {
   const uint64_t F = n_frames ? n_frames : 1;
   const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
+  HIP_TRY(c, c->pieces.ensure(piece_bound(wire_len, F) * sizeof(PieceDesc)));
+  HIP_TRY(c, c->utf8_err.ensure(F * sizeof(uint32_t)));
   HIP_TRY(c, c->rec.ensure(F * sizeof(FrameRec)));
   HIP_TRY(c, c->prev.ensure(3 * F * sizeof(int32_t)));
   HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));
@@ -231,10 +234,10 @@ static int ensure_encode_ws(wsg_ctx* c, uint64_t n_frames) {
   return WSG_API_OK;
 }
 
-int wsg_reserve(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions) {
+int wsg_reserve(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len) {
   if (!c) return WSG_API_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
-  int rc = ensure_decode_ws(c, max_frames, max_sessions);
+  int rc = ensure_decode_ws(c, max_frames, max_sessions, max_wire_len);
   if (rc) return rc;
   return ensure_encode_ws(c, max_frames);
 }
@@ -261,7 +264,7 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   if (payload_cap < wire_len + 16 * n_frames)
     return set_err(c, WSG_API_ERANGE, "payload_cap below wsg_decode_payload_bound()");
   HIP_TRY(c, hipSetDevice(c->device));
-  int rc = ensure_decode_ws(c, n_frames, n_sessions);
+  int rc = ensure_decode_ws(c, n_frames, n_sessions, wire_len);
   if (rc) return rc;
   DecodeArgs a;
   a.wire = wire;
@@ -285,13 +288,17 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.blk_max = (int32_t*)c->blk_max.p;
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
+  a.pieces = (PieceDesc*)c->pieces.p;
+  a.utf8_err = (uint32_t*)c->utf8_err.p;
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
   HIP_TRY(c, hipMemsetAsync(a.sess_err, 0xff, (size_t)n_sessions * sizeof(uint64_t), c->stream));
   if (n_frames) {
+    HIP_TRY(c, hipMemsetAsync(a.utf8_err, 0, (size_t)n_frames * sizeof(uint32_t), c->stream));
     timed(c, K_PARSE, [&] { launch_parse(a, c->stream); });
     timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
     timed(c, K_LINK, [&] { launch_link(a, c->stream); });
-    timed(c, K_UNMASK, [&] { launch_unmask(a, c->stream, stream_grid(n_frames)); });
+    timed(c, K_UNMASK, [&] { launch_pieces(a, c->stream, piece_bound(wire_len, n_frames)); });
+    timed(c, K_MERGE, [&] { launch_merge(a, c->stream); });
   }
   timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());
@@ -487,6 +494,28 @@ int wsg_encode_batch_host(wsg_ctx* c, int client_mode, const uint8_t* payload, u
   if (total) HIP_TRY(c, hipMemcpyAsync(wire_out, c->h_wire.p, total, hipMemcpyDeviceToHost, s));
   if (n_sessions) HIP_TRY(c, hipMemcpyAsync(closed, c->h_closed.p, n_sessions, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
+
+int wsg_copy_ceiling(wsg_ctx* c, const void* src, void* dst, uint64_t bytes, int reps, double* gbs) {
+  if (!c || !gbs || reps <= 0) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  hipEvent_t e0, e1;
+  HIP_TRY(c, hipEventCreate(&e0));
+  HIP_TRY(c, hipEventCreate(&e1));
+  float best = 1e30f;
+  for (int r = 0; r <= reps; ++r) {
+    HIP_TRY(c, hipEventRecord(e0, c->stream));
+    launch_copy_ceiling(src, dst, bytes, c->stream);
+    HIP_TRY(c, hipEventRecord(e1, c->stream));
+    HIP_TRY(c, hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
+    if (r > 0 && ms < best) best = ms;  // first run warms up
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  *gbs = 2.0 * (double)(bytes / 16 * 16) / (best * 1e-3) / 1e9;
   return WSG_API_OK;
 }
 

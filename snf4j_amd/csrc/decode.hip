@@ -183,6 +183,24 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   }
   a.rec[k].out_off = ex.sum;
   a.rec[k].code = r.code | extra;
+  // descriptors of the pieces whose first output byte falls in this frame's slot
+  const uint64_t slot = (uint64_t)((r.len + 15u) & ~15u);
+  if (slot) {
+    const uint64_t total = *a.total, slot_end = ex.sum + slot;
+    const uint64_t flags = ((extra & CODE_VALIDATE) ? PD_VALIDATE : 0ull);
+    for (uint64_t pc = (ex.sum + PIECE - 1) / PIECE; pc * PIECE < slot_end; ++pc) {
+      const uint64_t ps = pc * PIECE;
+      const uint32_t j0 = (uint32_t)(ps - ex.sum);
+      const uint32_t left = r.len - j0;
+      const bool single = slot_end >= ps + PIECE || slot_end == total;
+      PieceDesc d;
+      d.info = ((r.src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) | flags |
+               (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI);
+      d.mask = r.mask;
+      d.frame = (uint32_t)k;
+      a.pieces[pc] = d;
+    }
+  }
   wsg_frame_desc d;
   d.payload_off = ex.sum;
   d.payload_len = r.len;
@@ -233,6 +251,8 @@ __device__ bool edge_utf8_error(const DecodeArgs& a, uint64_t k, const FrameRec&
     const uint32_t p1 = i >= 1 ? s[i - 1] : 0, p2 = i >= 2 ? s[i - 2] : 0, p3 = i >= 3 ? s[i - 3] : 0;
     if (utf8_err_byte(p3, p2, p1, s[i])) return true;
   }
+  // k_pieces' pair rule flags a lone invalid lead one byte late: test the last byte here
+  if (r.len && utf8_bad_last((l3 >> 16) & 0xffu)) return true;
   if (r.code & CODE_FIN) {
     uint32_t t1, t2, t3;
     if (r.len >= 3) {
@@ -346,6 +366,196 @@ __global__ __launch_bounds__(256) void k_unmask(DecodeArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ k_pieces
+// One wave per 1 KiB piece of the payload OUTPUT (16-B aligned frame slots laid
+// end to end): lane i owns output bytes [1024p + 16i, +16).  The grid size is
+// known on the host (piece_bound), every store is an aligned full-line store,
+// and a wave's footprint is 1 KiB in and 1 KiB out — the streaming shape that
+// reaches the chip's copy ceiling.  A piece inside one frame (the common case)
+// reads 16-B ALIGNED source blocks and builds the misaligned payload bytes with
+// a wave-shift DPP funnel; a piece spanning frame slots takes the general path.
+__device__ __forceinline__ uint32_t dpp_from_next(uint32_t v, uint32_t old) {
+  // lane i <- lane i+1 (wave_shl:1); lane 63 keeps `old`
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
+}
+__device__ __forceinline__ uint32_t dpp_from_prev(uint32_t v, uint32_t old) {
+  // lane i <- lane i-1 (wave_shr:1); lane 0 keeps `old`
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int keep) {
+  return keep >= 4 ? w : (keep <= 0 ? 0u : (w & ((1u << (8 * keep)) - 1u)));
+}
+__device__ __forceinline__ uint32_t keep_flags(int keep) {  // UTF-8 flag mask of the first `keep` bytes
+  return keep >= 4 ? 0x80808080u : (keep <= 0 ? 0u : (0x80808080u >> (8 * (4 - keep))));
+}
+
+// 4 source bytes ending right before wire offset `pos`, unmasked (payload phase 0)
+__device__ __forceinline__ uint32_t prev_word(const DecodeArgs& a, uint64_t pos, uint32_t mask) {
+  uint32_t w = 0;
+  for (int i = 0; i < 4; ++i) w |= (uint32_t)a.wire[pos - 4 + i] << (8 * i);
+  return w ^ mask;
+}
+
+// Fast path: the piece is payload of ONE frame.  Every lane loads one 16-B
+// ALIGNED source block; output dword j of lane i is bytes sh+4j.. of
+// (block i ++ block i+1), the next block arriving by a wave-shift DPP move
+// (block 64 by a scalar load).  Returns the lane's UTF-8 error flags.
+template <int NT>
+__device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceDesc d, uint64_t pstart, int lane) {
+  const uint32_t aux = NT ? 2 : 0;
+  const uint64_t s = d.info & PD_SRC_MASK;
+  const uint32_t nb = (uint32_t)(d.info >> PD_NB_SHIFT) & 2047u;
+  const uint64_t a16 = s & ~15ull;
+  const uint32_t sh = (uint32_t)(s & 15u);
+  const uint32_t boff = (uint32_t)lane * 16u;
+  const __amdgpu_buffer_rsrc_t rout =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload_out + pstart), 0, (int)PIECE, 0x00020000);
+  // the 4 payload bytes before the piece (UTF-8 carry from the previous piece of the
+  // same frame): scalar loads issued up front, beside the payload load
+  const uint32_t b = sh & 3u;
+  const uint64_t pva = a16 >= 16u ? a16 - 16u : 0u;  // bytes a16-16 .. a16+15
+  const uint32_t i0 = 3u + (sh >> 2);                 // dword holding byte (s - 4)
+  // (kept in VGPRs: a readfirstlane here would force a wait before the payload load)
+  const uint32_t pv_lo = ((const uint32_t*)(a.wire + pva))[i0];
+  const uint32_t pv_hi = ((const uint32_t*)(a.wire + pva))[i0 + 1];
+  u32x4 A;
+  uint32_t e0, e1, e2, e3;
+  if (a16 + PIECE + 16u <= a.wire_len) {  // wave-uniform: the usual case
+    const __amdgpu_buffer_rsrc_t rin =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.wire + a16), 0, (int)(PIECE + 16u), 0x00020000);
+    A = __builtin_amdgcn_raw_buffer_load_b128(rin, boff, 0, aux);
+    const u32x4 nx = *(const u32x4*)(a.wire + a16 + PIECE);  // block 64 (lane 63's next block)
+    e0 = nx.x; e1 = nx.y; e2 = nx.z; e3 = nx.w;
+  } else {  // the wire's last KiB: byte loads (the buffer range check is per dword)
+    uint32_t dd[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < 16u; ++i)
+      if (a16 + boff + i < a.wire_len) dd[i >> 2] |= (uint32_t)a.wire[a16 + boff + i] << (8 * (i & 3));
+    A = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+    uint32_t ee[4] = {0u, 0u, 0u, 0u};
+    for (uint32_t i = 0; i < 16u; ++i)
+      if (a16 + PIECE + i < a.wire_len) ee[i >> 2] |= (uint32_t)a.wire[a16 + PIECE + i] << (8 * (i & 3));
+    e0 = ee[0]; e1 = ee[1]; e2 = ee[2]; e3 = ee[3];
+  }
+  const uint32_t W0 = A.x, W1 = A.y, W2 = A.z, W3 = A.w;
+  const uint32_t W4 = dpp_from_next(A.x, e0), W5 = dpp_from_next(A.y, e1);
+  const uint32_t W6 = dpp_from_next(A.z, e2), W7 = dpp_from_next(A.w, e3);
+  uint32_t w[4];
+  switch (sh >> 2) {  // wave-uniform
+    case 0: w[0] = alignbyte(W1, W0, b); w[1] = alignbyte(W2, W1, b); w[2] = alignbyte(W3, W2, b); w[3] = alignbyte(W4, W3, b); break;
+    case 1: w[0] = alignbyte(W2, W1, b); w[1] = alignbyte(W3, W2, b); w[2] = alignbyte(W4, W3, b); w[3] = alignbyte(W5, W4, b); break;
+    case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
+    default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
+  }
+  const int keep = (int)nb - lane * 16;  // payload bytes in this lane's chunk
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = keep_bytes(w[i] ^ d.mask, keep - 4 * i);
+  if (keep > 0) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
+  if (!(d.info & PD_VALIDATE)) return 0u;
+  const uint32_t first_prev = (d.info & PD_FIRST) ? 0u : (alignbyte(pv_hi, pv_lo, b) ^ d.mask);
+  const uint32_t pw = dpp_from_prev(w[3], first_prev);
+  uint32_t f0 = utf8_err_word_fast(w[0], pw), f1 = utf8_err_word_fast(w[1], w[0]);
+  uint32_t f2 = utf8_err_word_fast(w[2], w[1]), f3 = utf8_err_word_fast(w[3], w[2]);
+  if (lane == 0 && (d.info & PD_FIRST)) f0 &= 0x80000000u;  // bytes 0..2: checked against the fragment carry
+  f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
+  return f0 | f1 | f2 | f3;
+}
+
+// Workgroups are dealt round-robin to the 8 XCDs (blocks b and b+8 share one);
+// give each XCD a contiguous run of pieces so the source lines two neighbouring
+// pieces share (funnel block, UTF-8 carry word) meet in the same L2.  Bijective
+// for any grid (cdna_hip_programming.md §5.5 T1).
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
+  const uint32_t q = n / 8u, r = n % 8u, x = b % 8u, i = b / 8u;
+  return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + i;
+}
+
+template <int NT, int WPB, int XCD>
+__global__ __launch_bounds__(64 * WPB) void k_pieces(DecodeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t p = (uint64_t)__builtin_amdgcn_readfirstlane(blk * (uint32_t)WPB + (threadIdx.x >> 6));
+  const PieceDesc d = a.pieces[p];
+  const uint64_t total = *a.total;
+  // keep both scalar loads in flight together (the exit test below would
+  // otherwise let the compiler wait for `total` before issuing the descriptor load)
+  asm volatile("" ::"s"(d.info), "s"(d.mask), "s"(d.frame), "s"(total));
+  const uint64_t pstart = p * PIECE;
+  if (pstart >= total) return;
+  if (!(d.info & PD_MULTI)) {
+    const uint32_t err = piece_fast<NT>(a, d, pstart, lane);
+    if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d.frame], 1u);
+    return;
+  }
+  // ---- general path: the piece spans several frame slots (small frames)
+  const uint32_t aux = NT ? 2 : 0;
+  const __amdgpu_buffer_rsrc_t rout =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload_out + pstart), 0, (int)PIECE, 0x00020000);
+  const uint64_t pend = pstart + PIECE < total ? pstart + PIECE : total;
+  const uint64_t my = pstart + (uint64_t)lane * 16u;
+  const bool live = my < pend;
+  uint32_t kk = d.frame, lk = d.frame;
+  FrameRec rr = a.rec[kk];
+  FrameRec lr = rr;
+  uint64_t send = rr.out_off + ((rr.len + 15u) & ~15u);
+  for (;;) {
+    const bool beyond = live && my >= send;
+    if (!__any(beyond)) break;
+    ++kk;
+    rr = a.rec[kk];
+    if (beyond) { lk = kk; lr = rr; }
+    send = rr.out_off + ((rr.len + 15u) & ~15u);
+  }
+  const uint32_t j = (uint32_t)(my - lr.out_off);
+  const int keep = live ? (int)lr.len - (int)j : 0;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  if (live) {
+    const uint64_t s = lr.src + j;
+    const uint64_t a4 = s & ~3ull;
+    const uint32_t sh = (uint32_t)(s & 3u);
+    uint32_t dd[5];
+    if (a4 + 20u <= a.wire_len) {
+      const uint32_t* q = (const uint32_t*)(a.wire + a4);
+      dd[0] = q[0]; dd[1] = q[1]; dd[2] = q[2]; dd[3] = q[3]; dd[4] = q[4];
+    } else {
+      for (int i = 0; i < 5; ++i) dd[i] = 0u;
+      for (uint32_t i = 0; i < 20u && a4 + i < a.wire_len; ++i) dd[i >> 2] |= (uint32_t)a.wire[a4 + i] << (8 * (i & 3));
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = keep_bytes(alignbyte(dd[i + 1], dd[i], sh) ^ lr.mask, keep - 4 * i);
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, (uint32_t)lane * 16u, 0, aux);
+  }
+  const bool lval = live && (lr.code & CODE_VALIDATE);
+  if (__any(lval)) {
+    uint32_t pw = dpp_from_prev(w[3], 0u);
+    const uint32_t prev_k = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffffu, (int)lk, 0x138, 0xf, 0xf, false);
+    if (j == 0) pw = 0u;
+    else if (prev_k != lk) pw = prev_word(a, lr.src + j, lr.mask);  // lane 0 inside a frame
+    if (lval) {
+      uint32_t e0 = utf8_err_word_fast(w[0], pw), e1 = utf8_err_word_fast(w[1], w[0]);
+      uint32_t e2 = utf8_err_word_fast(w[2], w[1]), e3 = utf8_err_word_fast(w[3], w[2]);
+      if (j == 0) e0 &= 0x80000000u;
+      e0 &= keep_flags(keep); e1 &= keep_flags(keep - 4); e2 &= keep_flags(keep - 8); e3 &= keep_flags(keep - 12);
+      if (e0 | e1 | e2 | e3) atomicOr(&a.utf8_err[lk], 1u);
+    }
+  }
+}
+
+// ------------------------------------------------------------------ k_merge
+// Per frame: the first error in the reference's check order (header rules,
+// fragmentation, lengths/close, then the validator), and the first failing
+// frame per session.
+__global__ __launch_bounds__(256) void k_merge(DecodeArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= a.n_frames) return;
+  const FrameRec r = a.rec[k];
+  const uint32_t pre = code_pre(r.code), post = code_post(r.code), frag = code_frag(r.code);
+  uint32_t status = pre ? pre : (frag ? frag : post);
+  if (!status && (r.code & CODE_VALIDATE) && (a.utf8_err[k] || edge_utf8_error(a, k, r))) status = WSG_E_TEXT_UTF8;
+  a.desc[k].status = (uint16_t)status;
+  if (status) atomicMin((unsigned long long*)&a.sess_err[r.sess], (unsigned long long)k);
+}
+
 // ------------------------------------------------------------------ k_final
 __device__ int64_t error_detail(const DecodeArgs& a, uint64_t k, uint32_t err) {
   const uint64_t o = a.frame_off[k];
@@ -437,6 +647,13 @@ void launch_link(const DecodeArgs& a, hipStream_t s) {
 }
 void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid) {
   hipLaunchKernelGGL(k_unmask<4>, dim3(grid), dim3(256), 0, s, a);
+}
+void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
+  // one 64-lane workgroup per piece, nontemporal loads/stores (fastest in tools/ubench_unmask)
+  hipLaunchKernelGGL((k_pieces<1, 1, 1>), dim3((uint32_t)n_pieces_bound), dim3(64), 0, s, a);
+}
+void launch_merge(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_merge, dim3((uint32_t)((a.n_frames + 255) / 256)), dim3(256), 0, s, a);
 }
 void launch_final(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);

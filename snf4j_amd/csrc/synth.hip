@@ -111,6 +111,22 @@ __global__ __launch_bounds__(256) void k_synth_header(uint64_t seed, uint64_t n_
   }
 }
 
+// Streaming copy of `n16` 16-B blocks with the chip's best copy pattern (one
+// 64-lane workgroup per KiB, nontemporal): the measured read+write ceiling the
+// decode kernel is compared with (bench.py roofline.copy_ceiling_GBs).
+typedef unsigned int cu32x4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(64) void k_copy_ceiling(const cu32x4* __restrict__ s, cu32x4* __restrict__ d,
+                                                     uint64_t n16) {
+  const uint64_t i = (uint64_t)blockIdx.x * 64 + threadIdx.x;
+  if (i < n16) __builtin_nontemporal_store(__builtin_nontemporal_load(&s[i]), &d[i]);
+}
+
+void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s) {
+  const uint64_t n16 = bytes / 16;
+  hipLaunchKernelGGL(k_copy_ceiling, dim3((uint32_t)((n16 + 63) / 64)), dim3(64), 0, s, (const cu32x4*)src,
+                     (cu32x4*)dst, n16);
+}
+
 void launch_synth(uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode, int masked,
                   int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first, hipStream_t s) {
   hipLaunchKernelGGL(k_synth_header, dim3(2048), dim3(256), 0, s, seed, n_frames, payload_len, fps, opcode, masked,

@@ -157,6 +157,53 @@ WS_HD uint32_t utf8_err_word(uint32_t w, uint32_t p) {
   return err & H80;
 }
 
+// v_perm_b32 byte permute: each selector byte 0..7 picks byte of {hi:lo}.
+WS_HD uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_perm(hi, lo, sel);
+#else
+  const uint64_t t = ((uint64_t)hi << 32) | lo;
+  uint32_t r = 0;
+  for (int i = 0; i < 4; ++i) r |= (uint32_t)((t >> (8 * ((sel >> (8 * i)) & 7))) & 0xffu) << (8 * i);
+  return r;
+#endif
+}
+
+// The kernels' UTF-8 rule (k_pieces): the continuation count is checked at the
+// byte itself exactly as utf8_err_word does; the lead-specific rules (C0/C1,
+// F5..FF, and the second-byte ranges after E0/ED/F0/F4) are checked on the
+// (previous byte, byte) pair with three v_perm nibble-table lookups and are
+// flagged on the SECOND byte of the pair.  So an invalid lead (C0, C1, F5..FF)
+// is flagged one byte late; the frame-level verdict stays exact because the
+// last byte of every validated frame is also tested with utf8_bad_last
+// (k_merge).  Exhaustively checked against the DFA in tests/cpp/utf8_rule_check.cpp.
+WS_HD uint32_t utf8_err_word_fast(uint32_t w, uint32_t p) {
+  const uint32_t w2 = w << 2, w3 = w << 3;
+  const uint32_t hw = w & H80;
+  const uint32_t cw = hw & (w << 1);
+  const uint32_t gw = cw & w2;
+  const uint32_t fw = gw & w3;
+  const uint32_t hp = p & H80;
+  const uint32_t cp = hp & (p << 1);
+  const uint32_t gp = cp & (p << 2);
+  const uint32_t fp = gp & (p << 3);
+  const uint32_t c1 = alignbyte(cw, cp, 3);  // previous byte >= C0
+  const uint32_t expect = c1 | alignbyte(gw, gp, 2) | alignbyte(fw, fp, 1);
+  uint32_t err = expect ^ (hw ^ cw);
+  // pair tables: bits A=1 C0/C1, B=2 F5..F7, C=4 E0, D=8 ED, E=16 F0, F=32 F4, G=64 F8..FF
+  const uint32_t p1 = alignbyte(w, p, 3);
+  const uint32_t ih = ((p1 >> 4) & 0x03030303u) | ((p1 >> 1) & 0x04040404u);  // C/D/E/F x low-nibble bit 3
+  const uint32_t th = perm_bytes(0x40080000u, 0x32040001u, ih);
+  const uint32_t tl = perm_bytes(0x42424A60u, 0x40404155u, p1 & 0x07070707u);
+  const uint32_t tb = perm_bytes(0u, 0x6B6B6757u, (w >> 4) & 0x03030303u);  // second byte 80/90/A0/B0 class
+  err |= ((th & tl & tb) + 0x7F7F7F7Fu) & c1;
+  return err & H80;
+}
+
+// Last byte of a frame is a lead the DFA rejects on its own (C0, C1, F5..FF):
+// the pair rule above would flag it only at the next byte.
+WS_HD bool utf8_bad_last(uint32_t b) { return b == 0xC0u || b == 0xC1u || b >= 0xF5u; }
+
 // Error flag of a single byte b given its 3 predecessors (p1 nearest).
 WS_HD bool utf8_err_byte(uint32_t p3, uint32_t p2, uint32_t p1, uint32_t b) {
   uint32_t p = (p3 << 8) | (p2 << 16) | (p1 << 24);

@@ -39,6 +39,26 @@ __host__ __device__ inline bool code_is_start(uint32_t c) {
 }
 
 constexpr int BLOCK = 256;  // frames per block in the parse / link passes
+constexpr uint32_t PIECE = 1024;  // payload-output bytes per wave in k_pieces (64 lanes x 16 B)
+
+// Pieces needed for a batch, bounded from host-known sizes: the 16-B aligned
+// payload slots total sum(align16(len)) <= wire_len - 2F + 15F.
+__host__ __device__ inline uint64_t piece_bound(uint64_t wire_len, uint64_t n_frames) {
+  return (wire_len + 16 * n_frames) / PIECE + 1;
+}
+
+// One 1 KiB piece of the payload output (16 B, one scalar load per wave).
+struct PieceDesc {
+  uint64_t info;  // bits 0-47: wire offset of the piece's first payload byte; 48-58: payload bytes in
+                  // the piece (1..1024); 59: validate; 60: piece starts its frame; 61: spans several slots
+  uint32_t mask;  // frame mask key (payload phase 0 at the piece start)
+  uint32_t frame; // frame index
+};
+constexpr uint64_t PD_SRC_MASK = (1ull << 48) - 1;
+constexpr uint32_t PD_NB_SHIFT = 48;
+constexpr uint64_t PD_VALIDATE = 1ull << 59;
+constexpr uint64_t PD_FIRST = 1ull << 60;
+constexpr uint64_t PD_MULTI = 1ull << 61;
 
 struct DecodeArgs {
   // inputs
@@ -64,6 +84,8 @@ struct DecodeArgs {
   int32_t* blk_max;    // [3][nblk] per-block max indices -> exclusive prefix max
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
   uint64_t* total;     // [1] total payload slot bytes
+  struct PieceDesc* pieces;  // [piece_bound]: per-piece work descriptor (k_link)
+  uint32_t* utf8_err;  // [n_frames]: a piece found a UTF-8 error inside the frame (k_pieces)
   uint32_t nblk;
 };
 
@@ -89,7 +111,7 @@ struct EncodeArgs {
 
 // kernel ids for timing
 enum KernelId {
-  K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
+  K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
   K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_COUNT
 };
 
@@ -97,7 +119,9 @@ enum KernelId {
 void launch_parse(const DecodeArgs& a, hipStream_t s);
 void launch_scan(const DecodeArgs& a, hipStream_t s);
 void launch_link(const DecodeArgs& a, hipStream_t s);
-void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid);
+void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid);  // wave per frame (reference kernel)
+void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
+void launch_merge(const DecodeArgs& a, hipStream_t s);
 void launch_final(const DecodeArgs& a, hipStream_t s);
 
 void launch_enc_len(const EncodeArgs& a, hipStream_t s);
@@ -105,6 +129,7 @@ void launch_enc_scan(const EncodeArgs& a, hipStream_t s);
 void launch_enc_emit(const EncodeArgs& a, hipStream_t s, uint32_t grid);
 void launch_enc_final(const EncodeArgs& a, hipStream_t s);
 
+void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 void launch_synth(uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode,
                   int masked, int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first,
                   hipStream_t s);
