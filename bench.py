@@ -84,6 +84,7 @@ def main():
 
     import snf4j_amd
     from snf4j_amd._lib import RESULT_DTYPE
+    from snf4j_amd.shard import rank_seed, time_steps
 
     stream = torch.cuda.current_stream(dev)
     ctx = snf4j_amd.Context(local, stream=stream)
@@ -97,7 +98,7 @@ def main():
     off = torch.empty(F + 1, dtype=torch.int64, device=dev)
     sf = torch.empty(n_s + 1, dtype=torch.int32, device=dev)
     # sessions of rank r are global sessions [r*n_s, (r+1)*n_s): shard by session, own seed
-    ctx.synth_uniform(0x5EED ^ (rank * 0x1000003), F, P, fps, opcode, True, text, wire, off, sf)
+    ctx.synth_uniform(rank_seed(0x5EED, rank), F, P, fps, opcode, True, text, wire, off, sf)
     payload_cap = F * flen + 16 * F + 16
     payload = torch.empty(payload_cap, dtype=torch.uint8, device=dev)
     desc = torch.empty(F * 16, dtype=torch.uint8, device=dev)
@@ -118,22 +119,8 @@ def main():
 
     ctx.reset_timing()
     ctx.set_timing(True)
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize(dev)
-    if dist:
-        dist.barrier()
-    t1 = time.perf_counter()
+    elapsed = time_steps(step, args.steps, sync=lambda: torch.cuda.synchronize(dev), dist=dist)
     ctx.set_timing(False)
-    elapsed = t1 - t0
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
     timing = ctx.timing()
 
     # dominant kernel: k_pieces reads each frame's payload bytes off the wire and writes them unmasked
