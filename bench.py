@@ -37,6 +37,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
     ap.add_argument("--e2e", action="store_true", help="also time the pinned host->device->host path")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the secondary BASELINE configs (measured at N=1 only)")
+    ap.add_argument("--extra-steps", type=int, default=10)
     return ap.parse_args()
 
 
@@ -143,6 +146,12 @@ def main():
     if args.e2e:
         e2e = e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev)
 
+    extras = None
+    if world == 1 and not args.no_extras:
+        del wire, payload, desc, res, state, off, sf
+        torch.cuda.empty_cache()
+        extras = measure_extras(ctx, dev, args)
+
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_seconds)
@@ -192,10 +201,134 @@ def main():
         }
         if e2e:
             out["e2e_pinned"] = e2e
+        if extras:
+            out["configs_measured"] = extras
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+def _timed(ctx, step, steps, warmup, dev, kernel):
+    import torch
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    ctx.reset_timing()
+    ctx.set_timing(True)
+    from snf4j_amd.shard import time_steps
+    el = time_steps(step, steps, sync=lambda: torch.cuda.synchronize(dev))
+    ctx.set_timing(False)
+    tm = ctx.timing()
+    kms, kn = tm[kernel]
+    return el, kms / max(1, kn), {k: round(v[0] / max(1, v[1]), 4) for k, v in tm.items() if v[1]}
+
+
+def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps, warmup, expect_errors=None):
+    """Decode GiB/s (wire) + k_pieces roofline of one device-resident batch."""
+    import numpy as np
+    import torch
+    from snf4j_amd import decoder_cfg
+    from snf4j_amd._lib import RESULT_DTYPE, lib
+    cap = int(lib.wsg_decode_payload_bound(wl, n))
+    payload = torch.empty(cap, dtype=torch.uint8, device=dev)
+    desc = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    res = torch.empty(n_s * 16, dtype=torch.uint8, device=dev)
+    state = torch.zeros(n_s * 8, dtype=torch.uint8, device=dev)
+    cfg = decoder_cfg(False, False, 65536, True)
+    ctx.reserve(n, n_s, wl)
+
+    def step():
+        state.zero_()  # every step decodes the same batch from a fresh session state
+        ctx.decode_device(cfg, wire, off, sf, state, payload, desc, res, wire_len=wl)
+
+    step()
+    torch.cuda.synchronize(dev)
+    r = res.cpu().numpy().view(RESULT_DTYPE)
+    n_err = int((r["error"] != 0).sum())
+    if expect_errors is not None:
+        assert n_err == expect_errors, (name, n_err, expect_errors)
+    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_pieces")
+    alg = wl + payload_bytes
+    ach = alg / (kms / 1e3) / 1e9
+    return {"config": name, "value": round(wl * steps / el / 2**30, 3), "unit": "GiB/s (wire)",
+            "ms_per_step": round(el / steps * 1e3, 4), "frames": n, "sessions": n_s, "wire_bytes": wl,
+            "sessions_with_error": n_err,
+            "roofline": {"kernel": "k_pieces", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": round(kms, 4)},
+            "pipeline_ms": pipe}
+
+
+def measure_extras(ctx, dev, args):
+    """The other 1-GPU configurations of BASELINE.json, each a device-resident batch."""
+    import numpy as np
+    import torch
+    from snf4j_amd import encoded_length
+    from snf4j_amd._lib import ENCODE_DTYPE
+    from snf4j_amd.synth import mixed_plan
+    out = []
+    K, W = args.extra_steps, 2
+    # configs[1]: 1 M masked BINARY frames, 1 KiB payload, 256 sessions (unmask only)
+    F, P, S = 1 << 20, 1024, 256
+    flen = encoded_length(P, True)
+    wire = torch.empty(F * flen + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(F + 1, dtype=torch.int64, device=dev)
+    sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    ctx.synth_uniform(0xC0F2, F, P, F // S, 2, True, 0, wire, off, sf)
+    out.append(_decode_line(ctx, dev, "configs[1]: 1M x 1 KiB masked BINARY, 256 sessions", wire, F * flen, off, sf,
+                            F, S, F * P, K, W, expect_errors=0))
+    del wire, off, sf
+    torch.cuda.empty_cache()
+    # configs[2]: mixed text+binary 64 B-64 KiB, UTF-8 on, 1 K sessions, >= 4 GiB wire
+    t, offh, sfh, wl, info = mixed_plan(0xC0F3, 1024, 4 << 30)
+    tab = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
+    wire = torch.zeros(wl + 64, dtype=torch.uint8, device=dev)
+    ctx.synth_frames(tab, wire)
+    del tab
+    line = _decode_line(ctx, dev, "configs[2]: mixed TEXT+BINARY 64 B-64 KiB log-uniform, 10% fragmented, "
+                        "1% of text messages with invalid UTF-8, 1024 sessions", wire, wl,
+                        torch.from_numpy(offh.astype(np.int64)).to(dev), torch.from_numpy(sfh.astype(np.int32)).to(dev),
+                        len(t), 1024, info["payload_bytes"], K, W, expect_errors=len(info["bad_sessions"]))
+    line["mix"] = {k: v for k, v in info.items() if k != "bad_sessions"}
+    out.append(line)
+    del wire
+    torch.cuda.empty_cache()
+    # configs[4]: client-side encode, 64 messages x 16 MiB in 64 KiB frames (header emit + mask)
+    M, FR, FP = 64, 256, 65536
+    n = M * FR
+    payload = torch.randint(0, 256, (M * FR * FP,), dtype=torch.uint8, device=dev)
+    fr = np.zeros(n, dtype=ENCODE_DTYPE)
+    fr["payload_off"] = np.arange(n, dtype=np.uint64) * FP
+    fr["payload_len"] = FP
+    j = np.arange(n) % FR
+    fr["opcode"] = np.where(j == 0, 2, 0)
+    fr["flags"] = np.where(j == FR - 1, 0x80, 0)
+    fr["mask"] = np.random.default_rng(5).integers(0, 256, (n, 4), dtype=np.uint8)
+    frames = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
+    sfe = torch.from_numpy((np.arange(M + 1) * FR).astype(np.int32)).to(dev)
+    closed = torch.zeros(M, dtype=torch.uint8, device=dev)
+    elen = encoded_length(FP, True)
+    wire_out = torch.empty(n * elen + 16, dtype=torch.uint8, device=dev)
+    wire_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+    def enc():
+        ctx.encode_device(True, payload, frames, sfe, closed, wire_out, wire_off)
+
+    enc()
+    torch.cuda.synchronize(dev)
+    assert int(wire_off[-1].item()) == n * elen
+    el, kms, pipe = _timed(ctx, enc, K, W, dev, "k_enc_emit")
+    alg = M * FR * FP + n * elen
+    ach = alg / (kms / 1e3) / 1e9
+    out.append({"config": "configs[4]: client encode, 64 x 16 MiB messages in 64 KiB frames (header + mask)",
+                "value": round(n * elen * K / el / 2**30, 3), "unit": "GiB/s (wire out)",
+                "ms_per_step": round(el / K * 1e3, 4), "frames": n,
+                "roofline": {"kernel": "k_enc_emit", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                             "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                             "avg_launch_ms": round(kms, 4)},
+                "pipeline_ms": pipe})
+    return out
 
 
 def e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev, reps=5):

@@ -60,6 +60,10 @@ try:
     ENCODE_DTYPE = np.dtype([("payload_off", "<u8"), ("payload_len", "<u4"), ("opcode", "u1"),
                              ("flags", "u1"), ("reserved", "u1", (2,)), ("mask", "u1", (4,)),
                              ("reserved2", "<u4")])
+    SYNTH_DTYPE = np.dtype([("wire_off", "<u8"), ("msg_seed", "<u8"), ("payload_len", "<u4"), ("msg_pos", "<u4"),
+                            ("msg_len", "<u4"), ("mask", "<u4"), ("inject_pos", "<i4"), ("opcode", "u1"),
+                            ("flags", "u1"), ("text", "u1"), ("inject_kind", "u1")])
+    assert SYNTH_DTYPE.itemsize == 40
 except ImportError:  # pragma: no cover
     np = None
 
@@ -94,6 +98,7 @@ def _load():
         "wsg_encode_batch_host": ([p, i32, p, u64, p, u64, p, u32, p, p, u64, p], i32),
         "wsg_synth_uniform": ([p, u64, u64, u32, u32, i32, i32, i32, p, p, p], i32),
         "wsg_copy_ceiling": ([p, p, p, u64, i32, P(C.c_double)], i32),
+        "wsg_synth_frames": ([p, p, u64, p], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -52,17 +52,31 @@ def _p(a) -> int:
     return a.data_ptr()
 
 
+def _stream_handle(stream) -> int:
+    return int(stream) if isinstance(stream, int) else int(stream.cuda_stream)
+
+
 class Context:
-    def __init__(self, device: int = 0, stream=None):
+    """A libwsgpu context on one device.
+
+    stream: "torch" (default) = torch's current stream on `device`, so the codec's
+    kernels are ordered with the torch operations that fill and free the device
+    buffers; "own" = a private non-blocking stream; or a hipStream_t handle /
+    torch.cuda.Stream.  Torch's default stream has handle 0, which is passed on
+    with wsg_set_stream (wsg_open(NULL) would create a private stream instead)."""
+
+    def __init__(self, device: int = 0, stream="torch"):
         h = C.c_void_p()
-        s = None
-        if stream is not None:
-            s = C.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)
-        rc = lib.wsg_open(int(device), s, C.byref(h))
+        rc = lib.wsg_open(int(device), None, C.byref(h))
         if rc != 0:
             raise _lib.WsgError(f"wsg_open(device={device}) failed: {rc} (no HIP device?)")
         self._h = h
         self.device = device
+        if isinstance(stream, str) and stream == "torch":
+            import torch
+            stream = torch.cuda.current_stream(device)
+        if not (isinstance(stream, str) and stream == "own"):
+            self.set_stream(stream)
 
     # -------------------------------------------------------------- plumbing
     def close(self):
@@ -83,8 +97,7 @@ class Context:
         self.close()
 
     def set_stream(self, stream):
-        check(lib.wsg_set_stream(self._h, C.c_void_p(stream if isinstance(stream, int) else stream.cuda_stream)),
-              self._h)
+        check(lib.wsg_set_stream(self._h, C.c_void_p(_stream_handle(stream))), self._h)
 
     def sync(self):
         check(lib.wsg_sync(self._h), self._h)
@@ -174,6 +187,13 @@ class Context:
         check(lib.wsg_synth_uniform(self._h, int(seed), int(n_frames), int(payload_len), int(frames_per_session),
                                     int(opcode), int(masked), int(text), _p(wire), _p(frame_off),
                                     _p(session_first)), self._h)
+
+
+    def synth_frames(self, table, wire):
+        """Table-driven synthetic batch (wsg_synth_frames); `table` is a device
+        uint8 tensor holding SYNTH_DTYPE records (snf4j_amd/synth.py)."""
+        n = table.numel() // 40
+        check(lib.wsg_synth_frames(self._h, _p(table), int(n), _p(wire)), self._h)
 
 
 def frame_available(buf: bytes, length: int | None = None):

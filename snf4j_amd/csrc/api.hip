@@ -530,4 +530,12 @@ int wsg_synth_uniform(wsg_ctx* c, uint64_t seed, uint64_t n_frames, uint32_t pay
   return WSG_API_OK;
 }
 
+int wsg_synth_frames(wsg_ctx* c, const wsg_synth_frame* table, uint64_t n_frames, uint8_t* wire) {
+  if (!c || (n_frames && (!table || !wire))) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  timed(c, K_SYNTH, [&] { launch_synth_frames(table, n_frames, wire, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
 }  // extern "C"

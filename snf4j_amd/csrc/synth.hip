@@ -111,6 +111,79 @@ __global__ __launch_bounds__(256) void k_synth_header(uint64_t seed, uint64_t n_
   }
 }
 
+// Table-driven batches (wsg_synth_frames): one workgroup per frame; thread 0
+// writes the header, the threads generate the message's 16-B chunks that
+// overlap this fragment and store the fragment's bytes (masked).
+__device__ __forceinline__ void msg_chunk(const wsg_synth_frame& f, uint64_t c, uint8_t tmp[16]) {
+  const uint64_t h = splitmix64(f.msg_seed + c);
+  if (f.text) {
+    synth_text16(h, tmp);
+    const uint32_t n = f.msg_len - c * 16 < 16 ? (uint32_t)(f.msg_len - c * 16) : 16u;
+    if (n < 16) {  // message end: never cut a code point
+      uint32_t cut = n;
+      while (cut > 0 && (tmp[cut] & 0xC0) == 0x80) --cut;
+      for (uint32_t i = cut; i < n; ++i) tmp[i] = 'a';
+    }
+    if (f.inject_pos >= 0) {
+      const uint8_t seqs[5][4] = {{0xC0, 0x80}, {0xED, 0xA0, 0x80}, {0xF4, 0x90, 0x80, 0x80}, {0xE2, 0x82, 'a'},
+                                  {0xFF}};
+      const uint32_t lens[5] = {2, 3, 4, 3, 1};
+      const uint32_t kind = f.inject_kind < 5 ? f.inject_kind : 0;
+      for (uint32_t i = 0; i < lens[kind]; ++i) {
+        const int64_t m = (int64_t)f.inject_pos + i - (int64_t)(c * 16);
+        if (m >= 0 && m < 16 && (uint64_t)f.inject_pos + i < f.msg_len) tmp[m] = seqs[kind][i];
+      }
+    }
+  } else {
+    const uint64_t h2 = splitmix64(h);
+    for (int i = 0; i < 8; ++i) { tmp[i] = (uint8_t)(h >> (8 * i)); tmp[8 + i] = (uint8_t)(h2 >> (8 * i)); }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_synth_frames(const wsg_synth_frame* __restrict__ t, uint64_t n,
+                                                      uint8_t* wire) {
+  for (uint64_t k = blockIdx.x; k < n; k += gridDim.x) {
+    const wsg_synth_frame f = t[k];
+    const int masked = f.flags & 1;
+    uint8_t* w = wire + f.wire_off;
+    const uint32_t hl = hdr_len(f.payload_len, masked);
+    if (threadIdx.x == 0) {
+      uint32_t p = 0;
+      w[p++] = (uint8_t)((f.flags & 0x80) | (f.opcode & 0x0f));
+      const uint8_t b1 = masked ? 0x80 : 0;
+      if (f.payload_len > 0xffffu) {
+        w[p++] = b1 | 127;
+        for (int i = 7; i >= 0; --i) w[p++] = (uint8_t)((uint64_t)f.payload_len >> (8 * i));
+      } else if (f.payload_len > 125u) {
+        w[p++] = b1 | 126;
+        w[p++] = (uint8_t)(f.payload_len >> 8);
+        w[p++] = (uint8_t)f.payload_len;
+      } else {
+        w[p++] = b1 | (uint8_t)f.payload_len;
+      }
+      if (masked)
+        for (int i = 0; i < 4; ++i) w[p++] = (uint8_t)(f.mask >> (8 * i));
+    }
+    if (!f.payload_len) continue;
+    uint8_t* pl = w + hl;
+    const uint64_t m0 = f.msg_pos, m1 = (uint64_t)f.msg_pos + f.payload_len;
+    for (uint64_t c = m0 / 16 + threadIdx.x; c < (m1 + 15) / 16; c += 256) {
+      uint8_t tmp[16];
+      msg_chunk(f, c, tmp);
+      for (uint32_t i = 0; i < 16; ++i) {
+        const uint64_t m = c * 16 + i;
+        if (m < m0 || m >= m1) continue;
+        const uint64_t j = m - m0;
+        pl[j] = masked ? (uint8_t)(tmp[i] ^ (uint8_t)(f.mask >> (8 * (j & 3)))) : tmp[i];
+      }
+    }
+  }
+}
+
+void launch_synth_frames(const wsg_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_synth_frames, dim3((uint32_t)(n < 65536 ? n : 65536)), dim3(256), 0, s, t, n, wire);
+}
+
 // Streaming copy of `n16` 16-B blocks with the chip's best copy pattern (one
 // 64-lane workgroup per KiB, nontemporal): the measured read+write ceiling the
 // decode kernel is compared with (bench.py roofline.copy_ceiling_GBs).

@@ -130,6 +130,7 @@ void launch_enc_emit(const EncodeArgs& a, hipStream_t s, uint32_t grid);
 void launch_enc_final(const EncodeArgs& a, hipStream_t s);
 
 void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s);
+void launch_synth_frames(const wsg_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s);
 void launch_synth(uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode,
                   int masked, int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first,
                   hipStream_t s);

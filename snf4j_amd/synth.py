@@ -1,0 +1,90 @@
+"""Host planner of synthetic mixed batches (BASELINE.json configs[2]; SURVEY.md §8d
+"Config 3"): the host decides message sizes, text/binary, fragmentation, session
+placement and injected invalid UTF-8; wsg_synth_frames writes the bytes on the
+device.  Bench and test infrastructure only — the decode path never calls it.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from ._lib import SYNTH_DTYPE
+
+
+def header_len(payload_len, masked: bool):
+    """FrameEncoder.length() header part (FrameEncoder.java:122-135), vectorised."""
+    pl = np.asarray(payload_len, dtype=np.int64)
+    return 2 + np.where(pl > 0xFFFF, 8, np.where(pl > 125, 2, 0)) + (4 if masked else 0)
+
+
+def mixed_plan(seed: int, n_sessions: int, target_wire_bytes: int, min_len: int = 64, max_len: int = 65536,
+               text_frac: float = 0.5, frag_frac: float = 0.1, bad_frac: float = 0.01, max_frags: int = 4,
+               masked: bool = True):
+    """Messages with log-uniform sizes in [min_len, max_len], `text_frac` TEXT (valid
+    UTF-8, ~70 % ASCII bytes) else BINARY; `frag_frac` of them fragmented into 2..max_frags
+    frames cut at arbitrary bytes (code points split across fragments); `bad_frac` of the
+    text messages carry one injected invalid sequence.  Sessions own contiguous frames.
+
+    Returns (table[SYNTH_DTYPE], frame_off u64[n+1], session_first u32[n_sessions+1], wire_len,
+    info dict)."""
+    rng = np.random.default_rng(seed)
+    lo, hi = np.log(min_len), np.log(max_len + 1)
+    mean = (max_len - min_len) / (hi - lo)
+    n_msgs = max(n_sessions, int(target_wire_bytes / (mean + 10)) + 1)
+    L = np.exp(rng.uniform(lo, hi, n_msgs)).astype(np.int64).clip(min_len, max_len)
+    approx = np.cumsum(L + 10)
+    n_msgs = max(min(n_msgs, int(np.searchsorted(approx, target_wire_bytes)) + 1), 1)
+    L = L[:n_msgs]
+    is_text = rng.random(n_msgs) < text_frac
+    nfrag = np.where(rng.random(n_msgs) < frag_frac, rng.integers(2, max_frags + 1, n_msgs), 1)
+    nfrag = np.minimum(nfrag, L)  # every fragment >= 1 byte
+    bad = is_text & (rng.random(n_msgs) < bad_frac)
+    inject_pos = np.where(bad, (rng.random(n_msgs) * np.maximum(L - 1, 1)).astype(np.int64), -1)
+    inject_kind = rng.integers(0, 5, n_msgs)
+    msg_seed = rng.integers(0, 2**63, n_msgs, dtype=np.int64).astype(np.uint64)
+    sess = rng.integers(0, n_sessions, n_msgs)
+    order = np.argsort(sess, kind="stable")  # a session's messages stay in generation order
+
+    # fragments, in session order
+    m_of_f = np.repeat(order, nfrag[order])
+    n_frames = len(m_of_f)
+    pos = np.zeros(n_frames, dtype=np.int64)
+    plen = L[m_of_f].copy()
+    first = np.ones(n_frames, dtype=bool)
+    fin = np.ones(n_frames, dtype=bool)
+    starts = np.concatenate([[0], np.cumsum(nfrag[order])[:-1]])
+    for i in np.nonzero(nfrag[order] > 1)[0]:
+        m = order[i]
+        k = int(nfrag[m])
+        while True:
+            cuts = np.unique(rng.integers(1, int(L[m]), k - 1))
+            if len(cuts) == k - 1:
+                break
+        edges = np.concatenate([[0], cuts, [int(L[m])]])
+        f0 = int(starts[i])
+        pos[f0:f0 + k] = edges[:-1]
+        plen[f0:f0 + k] = np.diff(edges)
+        first[f0 + 1:f0 + k] = False
+        fin[f0:f0 + k - 1] = False
+
+    t = np.zeros(n_frames, dtype=SYNTH_DTYPE)
+    flen = header_len(plen, masked) + plen
+    off = np.zeros(n_frames + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(flen)
+    t["wire_off"] = off[:-1]
+    t["msg_seed"] = msg_seed[m_of_f]
+    t["payload_len"] = plen
+    t["msg_pos"] = pos
+    t["msg_len"] = L[m_of_f]
+    t["mask"] = rng.integers(0, 2**32, n_frames, dtype=np.int64).astype(np.uint32)
+    t["inject_pos"] = inject_pos[m_of_f]
+    t["opcode"] = np.where(first, np.where(is_text[m_of_f], 1, 2), 0)
+    t["flags"] = np.where(fin, 0x80, 0) | (1 if masked else 0)
+    t["text"] = is_text[m_of_f]
+    t["inject_kind"] = inject_kind[m_of_f]
+    counts = np.bincount(sess, weights=nfrag, minlength=n_sessions).astype(np.int64)
+    sf = np.zeros(n_sessions + 1, dtype=np.uint32)
+    sf[1:] = np.cumsum(counts)
+    info = {"messages": int(n_msgs), "frames": int(n_frames), "text_messages": int(is_text.sum()),
+            "fragmented_messages": int((nfrag > 1).sum()), "bad_messages": int(bad.sum()),
+            "payload_bytes": int(plen.sum()), "bad_sessions": sorted(set(sess[bad].tolist()))}
+    return t, off, sf, int(off[-1]), info

@@ -14,9 +14,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.fixture(scope="module")
 def L():
-    from snf4j_amd import build
-    build.build()
-    from snf4j_amd import _lib
+    from snf4j_amd import _lib  # built by conftest.pytest_configure
     return _lib
 
 
