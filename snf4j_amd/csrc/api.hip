@@ -15,20 +15,22 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_pieces",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_emit", "k_enc_final", "k_synth"};
+                                           "k_enc_pieces", "k_enc_final", "k_synth"};
 
 struct DevBuf {
   void* p = nullptr;
   size_t n = 0;
-  hipError_t ensure(size_t bytes) {
+  // (re)allocate to >= bytes; a fresh allocation is filled with `fill` (>= 0) on stream s
+  hipError_t ensure(size_t bytes, int fill = -1, hipStream_t s = nullptr) {
     if (bytes <= n && p) return hipSuccess;
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
     size_t want = bytes < 256 ? 256 : bytes;
     hipError_t e = hipMalloc(&p, want);
-    if (e == hipSuccess) n = want;
-    return e;
+    if (e != hipSuccess) return e;
+    n = want;
+    return fill >= 0 ? hipMemsetAsync(p, fill, want, s) : hipSuccess;
   }
   void release() {
     if (p) (void)hipFree(p);
@@ -52,7 +54,7 @@ struct wsg_ctx {
   // decode workspace
   DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total, pieces, utf8_err;
   // encode workspace
-  DevBuf esess, elast_close;
+  DevBuf esess, elast_close, epieces;
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // timing
@@ -157,7 +159,7 @@ int wsg_close(wsg_ctx* c) {
   drain_timing(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->rec,     &c->prev,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
-                    &c->total,   &c->pieces, &c->utf8_err, &c->esess,   &c->elast_close, &c->h_wire, &c->h_off,    &c->h_sf,
+                    &c->total,   &c->pieces, &c->utf8_err, &c->esess,   &c->elast_close, &c->epieces, &c->h_wire, &c->h_off,    &c->h_sf,
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
@@ -213,13 +215,15 @@ static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, 
   const uint64_t F = n_frames ? n_frames : 1;
   const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
   HIP_TRY(c, c->pieces.ensure(piece_bound(wire_len, F) * sizeof(PieceDesc)));
-  HIP_TRY(c, c->utf8_err.ensure(F * sizeof(uint32_t)));
+  // utf8_err / sess_err are kept in their idle state between batches (k_merge and
+  // k_final reset what they read), so no per-batch memset is needed
+  HIP_TRY(c, c->utf8_err.ensure(F * sizeof(uint32_t), 0, c->stream));
   HIP_TRY(c, c->rec.ensure(F * sizeof(FrameRec)));
   HIP_TRY(c, c->prev.ensure(3 * F * sizeof(int32_t)));
   HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));
   HIP_TRY(c, c->blk_sum.ensure(nblk * sizeof(uint64_t)));
   HIP_TRY(c, c->blk_max.ensure(3 * nblk * sizeof(int32_t)));
-  HIP_TRY(c, c->sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t)));
+  HIP_TRY(c, c->sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t), 0xff, c->stream));
   HIP_TRY(c, c->total.ensure(sizeof(uint64_t)));
   return WSG_API_OK;
 }
@@ -244,13 +248,6 @@ int wsg_reserve(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t
 
 uint64_t wsg_decode_payload_bound(uint64_t wire_len, uint64_t n_frames) { return wire_len + 16 * n_frames + 16; }
 
-static uint32_t stream_grid(uint64_t n_frames) {
-  // one wave per frame, 4 waves per workgroup; enough workgroups to keep
-  // 8 per CU resident on the 256 CUs, the rest grid-strided
-  uint64_t g = (n_frames + 3) / 4;
-  if (g > 2048) g = 2048;
-  return (uint32_t)(g ? g : 1);
-}
 
 int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t* wire, uint64_t wire_len,
                             const uint64_t* frame_off, uint64_t n_frames, const uint32_t* session_first,
@@ -291,9 +288,7 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.pieces = (PieceDesc*)c->pieces.p;
   a.utf8_err = (uint32_t*)c->utf8_err.p;
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
-  HIP_TRY(c, hipMemsetAsync(a.sess_err, 0xff, (size_t)n_sessions * sizeof(uint64_t), c->stream));
   if (n_frames) {
-    HIP_TRY(c, hipMemsetAsync(a.utf8_err, 0, (size_t)n_frames * sizeof(uint32_t), c->stream));
     timed(c, K_PARSE, [&] { launch_parse(a, c->stream); });
     timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
     timed(c, K_LINK, [&] { launch_link(a, c->stream); });
@@ -449,10 +444,14 @@ int wsg_encode_batch_device(wsg_ctx* c, int client_mode, const uint8_t* payload,
   a.blk_max = (int32_t*)c->blk_max.p;
   a.last_close = (int32_t*)c->elast_close.p;
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  // pieces of wire_out: bounded by the caller's capacity (the total is only known on the device)
+  a.n_pieces = wire_cap / PIECE + 1;
+  if (n_frames) HIP_TRY(c, c->epieces.ensure(a.n_pieces * sizeof(PieceDesc)));
+  a.pieces = (PieceDesc*)c->epieces.p;
   if (n_frames) {
     timed(c, K_ENC_LEN, [&] { launch_enc_len(a, c->stream); });
     timed(c, K_ENC_SCAN, [&] { launch_enc_scan(a, c->stream); });
-    timed(c, K_ENC_EMIT, [&] { launch_enc_emit(a, c->stream, stream_grid(n_frames)); });
+    timed(c, K_ENC_EMIT, [&] { launch_enc_pieces(a, c->stream); });
     timed(c, K_ENC_FINAL, [&] { launch_enc_final(a, c->stream); });
   } else {
     HIP_TRY(c, hipMemsetAsync(wire_off, 0, sizeof(uint64_t), c->stream));

@@ -40,17 +40,19 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
     const uint32_t s = find_session(a.session_first, a.n_sessions, k);
     const uint64_t o = a.frame_off[k], e = a.frame_off[k + 1];
     const uint64_t ext = e > o ? e - o : 0;
-    uint8_t h[16];
+    uint8_t hb[20];  // wire bytes o .. o+16 (and up to 3 more), zero past the wire end
+    const uint8_t* h = hb;
     const uint64_t a4 = o & ~3ull;
-    if (a4 + 20 <= a.wire_len) {
+    if (a4 + 24 <= a.wire_len) {
       const uint32_t* p = (const uint32_t*)(a.wire + a4);
-      uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4];
+      uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4], d5 = p[5];
       const uint32_t sh = (uint32_t)(o & 3);
-      uint32_t w[4] = {alignbyte(d1, d0, sh), alignbyte(d2, d1, sh), alignbyte(d3, d2, sh), alignbyte(d4, d3, sh)};
+      uint32_t w[5] = {alignbyte(d1, d0, sh), alignbyte(d2, d1, sh), alignbyte(d3, d2, sh), alignbyte(d4, d3, sh),
+                       alignbyte(d5, d4, sh)};
 #pragma unroll
-      for (int i = 0; i < 16; ++i) h[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+      for (int i = 0; i < 20; ++i) hb[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
     } else {
-      for (int i = 0; i < 16; ++i) h[i] = (o + i < a.wire_len) ? a.wire[o + i] : 0;
+      for (int i = 0; i < 20; ++i) hb[i] = (o + i < a.wire_len) ? a.wire[o + i] : 0;
     }
     Header hd;
     uint32_t pre = 0, post = 0, len = 0;
@@ -72,12 +74,31 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
           else if (len > 2 && !utf8_valid_run(a.wire, src + 2, len - 2, hd.mask, 2)) post = WSG_E_CLOSE_REASON;
         }
         if (hd.opcode <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry
+          // first 3 payload bytes: within the header's 20 loaded bytes (hdr_len <= 14)
           uint32_t f3 = 0, l3 = 0;
           const uint32_t nf = len < 3 ? len : 3;
-          for (uint32_t i = 0; i < nf; ++i) {
-            f3 |= (uint32_t)(a.wire[src + i] ^ ((hd.mask >> (8 * (i & 3))) & 0xffu)) << (8 * i);
-            const uint32_t j = len - 1 - i;
-            l3 |= (uint32_t)(a.wire[src + j] ^ ((hd.mask >> (8 * (j & 3))) & 0xffu)) << (8 * (2 - i));
+          for (uint32_t i = 0; i < nf; ++i) f3 |= (uint32_t)hb[hd.hdr_len + i] << (8 * i);
+          f3 ^= hd.mask & (nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : (nf == 1 ? 0xffu : 0u)));
+          if (nf) {  // last 3 payload bytes: two aligned dwords
+            const uint64_t e3 = src + len - nf;  // first of the last nf bytes
+            const uint64_t q = e3 & ~3ull;
+            uint32_t lo, hi;
+            if (q + 8 <= a.wire_len) {
+              lo = *(const uint32_t*)(a.wire + q);
+              hi = *(const uint32_t*)(a.wire + q + 4);
+            } else {
+              lo = hi = 0;
+              for (uint32_t i = 0; i < 8 && q + i < a.wire_len; ++i)
+                (i < 4 ? lo : hi) |= (uint32_t)a.wire[q + i] << (8 * (i & 3));
+            }
+            const uint32_t t = alignbyte(hi, lo, (uint32_t)(e3 & 3));  // bytes e3.. e3+3
+            const uint32_t ph = (uint32_t)(len - nf) & 3u;            // mask phase of byte e3
+            const uint32_t m = (hd.mask >> (8 * ph)) | (ph ? hd.mask << (32 - 8 * ph) : 0u);
+            const uint32_t u = t ^ m;                                  // unmasked bytes e3..e3+3
+            for (uint32_t i = 0; i < nf; ++i) {  // byte len-1-i (newest first) -> bits 16-8i
+              const uint32_t j = nf - 1 - i;     // its index in u
+              l3 |= ((u >> (8 * j)) & 0xffu) << (8 * (2 - i));
+            }
           }
           a.edge[k] = f3;
           a.edge[a.n_frames + k] = l3;
@@ -551,7 +572,9 @@ __global__ __launch_bounds__(256) void k_merge(DecodeArgs a) {
   const FrameRec r = a.rec[k];
   const uint32_t pre = code_pre(r.code), post = code_post(r.code), frag = code_frag(r.code);
   uint32_t status = pre ? pre : (frag ? frag : post);
-  if (!status && (r.code & CODE_VALIDATE) && (a.utf8_err[k] || edge_utf8_error(a, k, r))) status = WSG_E_TEXT_UTF8;
+  const uint32_t ue = a.utf8_err[k];
+  if (ue) a.utf8_err[k] = 0u;  // back to the idle state for the next batch
+  if (!status && (r.code & CODE_VALIDATE) && (ue || edge_utf8_error(a, k, r))) status = WSG_E_TEXT_UTF8;
   a.desc[k].status = (uint16_t)status;
   if (status) atomicMin((unsigned long long*)&a.sess_err[r.sess], (unsigned long long)k);
 }
@@ -581,11 +604,12 @@ __global__ __launch_bounds__(256) void k_final(DecodeArgs a) {
   wsg_session_state st = a.state[s];
   wsg_session_result res = {0u, 0u, 0u, 0};
   const uint32_t sf = a.session_first[s], se = a.session_first[s + 1];
+  const uint64_t fe = a.sess_err[s];
+  if (fe != ~0ull) a.sess_err[s] = ~0ull;  // back to the idle state for the next batch
   if (st.closed) {  // FrameDecoder.closed: all further input is swallowed (:185-187)
     a.result[s] = res;
     return;
   }
-  const uint64_t fe = a.sess_err[s];
   if (fe != ~0ull) {
     const uint32_t err = a.desc[fe].status;
     res.n_delivered = (uint32_t)(fe - sf);

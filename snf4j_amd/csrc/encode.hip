@@ -5,9 +5,9 @@
 //               or of an already closed encoder, are dropped); block aggregates.
 //   k_enc_scan  one workgroup: exclusive scan of the block aggregates.
 //   k_enc_link  thread per frame: wire offset of each frame (prefix sum).
-//   k_enc_emit  one wave per frame: header bytes (:80-106) and the payload XOR
-//               the injected mask key (:107-117), written with aligned 16-B
-//               stores over the frame's interior and byte stores at its seams.
+//   k_enc_fix   final wire offsets + one descriptor per 1 KiB piece of wire_out.
+//   k_enc_pieces one wave per 1 KiB of wire_out: header bytes (:80-106) and the
+//               payload XOR the injected mask key (:107-117), aligned 16-B stores.
 //   k_enc_final thread per session: FrameEncoder.closed carry-out.
 #include "wsgpu_internal.h"
 #include "wsgpu_scan.h"
@@ -105,96 +105,183 @@ __global__ __launch_bounds__(1024) void k_enc_scan_sum(EncodeArgs a) {
   if (threadIdx.x == 0) a.wire_off[a.n_frames] = carry.sum;
 }
 
+// Final wire offsets, and the descriptors of the 1 KiB pieces of wire_out whose
+// first byte falls in this frame (k_enc_pieces).  A piece entirely inside the
+// frame's payload (or ending the output there) takes the fast path.
 __global__ __launch_bounds__(BLOCK) void k_enc_fix(EncodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  if (k < a.n_frames) a.wire_off[k] += a.blk_sum[blockIdx.x];
+  if (k >= a.n_frames) return;
+  const uint64_t wo = a.wire_off[k] + a.blk_sum[blockIdx.x];
+  a.wire_off[k] = wo;
+  if (!a.pieces) return;
+  const uint32_t s = a.sess[k];
+  if (a.closed[s] || a.last_close[k] >= (int32_t)a.session_first[s]) return;  // dropped
+  const wsg_encode_frame f = a.frames[k];
+  const uint32_t hl = enc_header_len(f.payload_len, a.client_mode);
+  const uint64_t total = a.wire_off[a.n_frames];
+  const uint64_t end = wo + hl + f.payload_len, pay0 = wo + hl;
+  const uint32_t m = (uint32_t)f.mask[0] | ((uint32_t)f.mask[1] << 8) | ((uint32_t)f.mask[2] << 16) |
+                     ((uint32_t)f.mask[3] << 24);
+  for (uint64_t pc = (wo + PIECE - 1) / PIECE; pc * PIECE < end && pc < a.n_pieces; ++pc) {
+    const uint64_t ps = pc * PIECE;
+    const bool single = ps >= pay0 && (ps + PIECE <= end || end == total);
+    PieceDesc d;
+    d.frame = (uint32_t)k;
+    if (single) {
+      const uint64_t j0 = ps - pay0;  // payload index of the piece's first byte
+      const uint32_t ph = (uint32_t)(j0 & 3);
+      const uint32_t mr = a.client_mode ? (ph ? (m >> (8 * ph)) | (m << (32 - 8 * ph)) : m) : 0u;
+      const uint64_t nb = end - ps < PIECE ? end - ps : PIECE;
+      d.info = ((f.payload_off + j0) & PD_SRC_MASK) | (nb << PD_NB_SHIFT);
+      d.mask = mr;
+    } else {
+      d.info = PD_MULTI;
+      d.mask = 0;
+    }
+    a.pieces[pc] = d;
+  }
 }
 
-__global__ __launch_bounds__(256) void k_enc_emit(EncodeArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-  const uint32_t nw = gridDim.x * 4u;
-  for (uint64_t k = wave0; k < a.n_frames; k += nw) {
-    const uint64_t wo = a.wire_off[k], we = a.wire_off[k + 1];
-    if (we == wo) continue;  // dropped by the close latch
-    const wsg_encode_frame f = a.frames[k];
-    const uint32_t len = f.payload_len;
-    const uint32_t hl = enc_header_len(len, a.client_mode);
-    // header bytes (FrameEncoder.java:80-106)
-    uint8_t hb[14];
-    hb[0] = (uint8_t)(((f.flags >> 4) & 7u) << 4 | (f.flags & 0x80u) | (f.opcode & 15u));
-    const uint8_t mb = a.client_mode ? 0x80 : 0;
-    uint32_t p = 1;
-    if (len > 0xffffu) {
-      hb[p++] = mb | 127;
-      for (int i = 7; i >= 0; --i) hb[p++] = (uint8_t)((uint64_t)len >> (8 * i));
-    } else if (len > 125u) {
-      hb[p++] = mb | 126;
-      hb[p++] = (uint8_t)(len >> 8);
-      hb[p++] = (uint8_t)len;
-    } else {
-      hb[p++] = mb | (uint8_t)len;
+// ------------------------------------------------------------------ k_enc_pieces
+// One wave per 1 KiB of wire_out, lane i owning bytes [1024p + 16i, +16): the
+// decode kernel's shape (decode.hip k_pieces) with source and sink swapped.
+__device__ __forceinline__ uint32_t enc_dpp_from_next(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+// header byte r (< hl) of frame f (FrameEncoder.java:80-106)
+__device__ __forceinline__ uint8_t enc_header_byte(const wsg_encode_frame& f, uint32_t r, int client) {
+  const uint32_t len = f.payload_len;
+  if (r == 0) return (uint8_t)((((f.flags >> 4) & 7u) << 4) | (f.flags & 0x80u) | (f.opcode & 15u));
+  const uint8_t mb = client ? 0x80 : 0;
+  uint32_t lb;  // bytes of extended length
+  if (len > 0xffffu) {
+    if (r == 1) return mb | 127;
+    lb = 8;
+  } else if (len > 125u) {
+    if (r == 1) return mb | 126;
+    lb = 2;
+  } else {
+    if (r == 1) return mb | (uint8_t)len;
+    lb = 0;
+  }
+  if (r < 2 + lb) return (uint8_t)((uint64_t)len >> (8 * (lb - 1 - (r - 2))));
+  return f.mask[r - 2 - lb];  // client mode only
+}
+
+__global__ __launch_bounds__(64) void k_enc_pieces(EncodeArgs a) {
+  const int lane = threadIdx.x;
+  const uint64_t p = (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x);
+  const PieceDesc d = a.pieces[p];
+  const uint64_t total = a.wire_off[a.n_frames];
+  asm volatile("" ::"s"(d.info), "s"(d.mask), "s"(d.frame), "s"(total));
+  const uint64_t ps = p * PIECE;
+  const uint64_t lim = total < a.wire_cap ? total : a.wire_cap;
+  if (ps >= lim) return;
+  const uint32_t boff = (uint32_t)lane * 16u;
+  const uint64_t o = ps + boff;
+  uint32_t w[4];
+  if (!(d.info & PD_MULTI)) {
+    // ---- fast path: the piece is payload of one frame
+    const uint64_t s = d.info & PD_SRC_MASK;
+    const uint32_t nb = (uint32_t)(d.info >> PD_NB_SHIFT) & 2047u;
+    const uint64_t a16 = s & ~15ull;
+    const uint32_t sh = (uint32_t)(s & 15u), b = sh & 3u;
+    u32x4 A;
+    uint32_t e0, e1, e2, e3;
+    if (a16 + PIECE + 16u <= a.payload_len) {
+      const __amdgpu_buffer_rsrc_t rin =
+          __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload + a16), 0, (int)(PIECE + 16u), 0x00020000);
+      A = __builtin_amdgcn_raw_buffer_load_b128(rin, boff, 0, 2);
+      const u32x4 nx = *(const u32x4*)(a.payload + a16 + PIECE);
+      e0 = nx.x; e1 = nx.y; e2 = nx.z; e3 = nx.w;
+    } else {  // the payload buffer's last KiB: byte loads
+      uint32_t dd[4] = {0u, 0u, 0u, 0u}, ee[4] = {0u, 0u, 0u, 0u};
+      for (uint32_t i = 0; i < 16u; ++i) {
+        if (a16 + boff + i < a.payload_len) dd[i >> 2] |= (uint32_t)a.payload[a16 + boff + i] << (8 * (i & 3));
+        if (a16 + PIECE + i < a.payload_len) ee[i >> 2] |= (uint32_t)a.payload[a16 + PIECE + i] << (8 * (i & 3));
+      }
+      A = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+      e0 = ee[0]; e1 = ee[1]; e2 = ee[2]; e3 = ee[3];
     }
-    uint32_t m = 0;
-    if (a.client_mode) {
-      for (int i = 0; i < 4; ++i) hb[p++] = f.mask[i];
-      m = (uint32_t)f.mask[0] | ((uint32_t)f.mask[1] << 8) | ((uint32_t)f.mask[2] << 16) | ((uint32_t)f.mask[3] << 24);
+    const uint32_t W0 = A.x, W1 = A.y, W2 = A.z, W3 = A.w;
+    const uint32_t W4 = enc_dpp_from_next(A.x, e0), W5 = enc_dpp_from_next(A.y, e1);
+    const uint32_t W6 = enc_dpp_from_next(A.z, e2), W7 = enc_dpp_from_next(A.w, e3);
+    switch (sh >> 2) {  // wave-uniform
+      case 0: w[0] = alignbyte(W1, W0, b); w[1] = alignbyte(W2, W1, b); w[2] = alignbyte(W3, W2, b); w[3] = alignbyte(W4, W3, b); break;
+      case 1: w[0] = alignbyte(W2, W1, b); w[1] = alignbyte(W3, W2, b); w[2] = alignbyte(W4, W3, b); w[3] = alignbyte(W5, W4, b); break;
+      case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
+      default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
     }
-    // output chunks: aligned 16-B blocks covering [wo, we)
-    const uint64_t A0 = wo & ~15ull;
-    const uint64_t nchunk = ((we + 15) & ~15ull) - A0 >> 4;
-    const uint64_t ps = f.payload_off;  // payload byte j lives at payload[ps + j]
-    const uint64_t pa4 = ps & ~3ull;
-    const uint64_t pavail = a.payload_len - pa4;
-    const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
-        (void*)(a.payload + pa4), 0, (int)(pavail > 0x7fffffffull ? 0x7fffffffull : pavail), 0x00020000);
-    const uint64_t pay0 = wo + hl;  // wire offset of payload byte 0
-    for (uint64_t c = lane; c < nchunk; c += 64) {
-      const uint64_t A = A0 + c * 16;
-      if (A >= pay0 && A + 16 <= we) {
-        // interior: payload bytes j0..j0+15, unaligned source, rotated mask
-        const uint64_t j0 = A - pay0;
-        const uint64_t rel = (ps & 3) + j0;
-        const uint32_t sh = (uint32_t)(rel & 3);
-        const uint32_t off = (uint32_t)(rel & ~3ull);
-        u32x4 q;
-        uint32_t t;
-        if ((uint64_t)off + 20u <= pavail) {
-          q = __builtin_amdgcn_raw_buffer_load_b128(rin, off, 0, 0);
-          t = __builtin_amdgcn_raw_buffer_load_b32(rin, off + 16, 0, 0);
-        } else {  // the last bytes of the payload buffer: byte loads
-          uint32_t d[5] = {0u, 0u, 0u, 0u, 0u};
-          for (uint32_t i = 0; i < 20u && (uint64_t)off + i < pavail; ++i)
-            d[i >> 2] |= (uint32_t)a.payload[pa4 + off + i] << (8 * (i & 3));
-          q = (u32x4){d[0], d[1], d[2], d[3]};
-          t = d[4];
-        }
-        const uint32_t ph = (uint32_t)(j0 & 3);
-        const uint32_t mr = ph ? ((m >> (8 * ph)) | (m << (32 - 8 * ph))) : m;
-        u32x4 o;
-        o.x = alignbyte(q.y, q.x, sh) ^ mr;
-        o.y = alignbyte(q.z, q.y, sh) ^ mr;
-        o.z = alignbyte(q.w, q.z, sh) ^ mr;
-        o.w = alignbyte(t, q.w, sh) ^ mr;
-        *(u32x4*)(a.wire_out + A) = o;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] ^= d.mask;
+    if (boff >= nb) return;
+  } else {
+    // ---- general path: headers and frame seams inside the piece
+    if (o >= lim) return;
+    uint32_t k = d.frame;
+    uint64_t fe = a.wire_off[k + 1];
+    while (o >= fe) fe = a.wire_off[++k + 1];
+    wsg_encode_frame f = a.frames[k];
+    uint64_t fo = a.wire_off[k];
+    uint32_t hl = enc_header_len(f.payload_len, a.client_mode);
+    uint32_t m = a.client_mode ? ((uint32_t)f.mask[0] | ((uint32_t)f.mask[1] << 8) | ((uint32_t)f.mask[2] << 16) |
+                                  ((uint32_t)f.mask[3] << 24))
+                               : 0u;
+    if (o >= fo + hl && o + 16 <= fe) {  // the lane's 16 bytes are payload of one frame
+      const uint64_t j0 = o - fo - hl;
+      const uint64_t src = f.payload_off + j0;
+      const uint64_t a4 = src & ~3ull;
+      const uint32_t sh = (uint32_t)(src & 3u);
+      uint32_t dd[5] = {0u, 0u, 0u, 0u, 0u};
+      if (a4 + 20u <= a.payload_len) {
+        const uint32_t* q = (const uint32_t*)(a.payload + a4);
+        dd[0] = q[0]; dd[1] = q[1]; dd[2] = q[2]; dd[3] = q[3]; dd[4] = q[4];
       } else {
-        // seam chunk: header bytes and/or shared with a neighbouring frame
-        for (uint32_t i = 0; i < 16; ++i) {
-          const uint64_t x = A + i;
-          if (x < wo || x >= we) continue;
-          const uint64_t r = x - wo;
-          uint8_t b;
-          if (r < hl) {
-            b = hb[r];
-          } else {
-            const uint64_t j = r - hl;
-            b = a.payload[ps + j] ^ (uint8_t)(m >> (8 * (j & 3)));
+        for (uint32_t i = 0; i < 20u && a4 + i < a.payload_len; ++i) dd[i >> 2] |= (uint32_t)a.payload[a4 + i] << (8 * (i & 3));
+      }
+      const uint32_t ph = (uint32_t)(j0 & 3);
+      const uint32_t mr = ph ? (m >> (8 * ph)) | (m << (32 - 8 * ph)) : m;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = alignbyte(dd[i + 1], dd[i], sh) ^ mr;
+    } else {
+      w[0] = w[1] = w[2] = w[3] = 0u;
+      for (uint32_t i = 0; i < 16u; ++i) {
+        const uint64_t x = o + i;
+        if (x >= lim) break;
+        while (x >= fe) {  // next frame (dropped frames have an empty extent)
+          ++k;
+          fo = fe;
+          fe = a.wire_off[k + 1];
+          if (x < fe) {
+            f = a.frames[k];
+            hl = enc_header_len(f.payload_len, a.client_mode);
+            m = a.client_mode ? ((uint32_t)f.mask[0] | ((uint32_t)f.mask[1] << 8) | ((uint32_t)f.mask[2] << 16) |
+                                 ((uint32_t)f.mask[3] << 24))
+                              : 0u;
           }
-          a.wire_out[x] = b;
         }
+        const uint64_t r = x - fo;
+        uint32_t byte;
+        if (r < hl) {
+          byte = enc_header_byte(f, (uint32_t)r, a.client_mode);
+        } else {
+          const uint64_t j = r - hl;
+          byte = a.payload[f.payload_off + j] ^ ((m >> (8 * (j & 3))) & 0xffu);
+        }
+        w[i >> 2] |= byte << (8 * (i & 3));
       }
     }
   }
+  if (o + 16 <= lim) {
+    __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (u32x4*)(a.wire_out + o));
+  } else {  // the output's last bytes: wire_out is not padded
+    for (uint32_t i = 0; i < 16u && o + i < lim; ++i) a.wire_out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
+void launch_enc_pieces(const EncodeArgs& a, hipStream_t s) {
+  if (a.n_pieces) hipLaunchKernelGGL(k_enc_pieces, dim3((uint32_t)a.n_pieces), dim3(64), 0, s, a);
 }
 
 __global__ __launch_bounds__(256) void k_enc_final(EncodeArgs a) {
@@ -217,9 +304,6 @@ void launch_enc_scan(const EncodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_enc_kept, dim3(a.nblk), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_enc_scan_sum, dim3(1), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_enc_fix, dim3(a.nblk), dim3(BLOCK), 0, s, a);
-}
-void launch_enc_emit(const EncodeArgs& a, hipStream_t s, uint32_t grid) {
-  hipLaunchKernelGGL(k_enc_emit, dim3(grid), dim3(256), 0, s, a);
 }
 void launch_enc_final(const EncodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_enc_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);

@@ -106,6 +106,8 @@ struct EncodeArgs {
   uint64_t* blk_sum;   // [nblk]
   int32_t* blk_max;    // [nblk] last CLOSE frame index
   int32_t* last_close; // [n_frames] last CLOSE frame before k
+  struct PieceDesc* pieces;  // [n_pieces]: 1 KiB pieces of wire_out (k_enc_fix -> k_enc_pieces)
+  uint64_t n_pieces;
   uint32_t nblk;
 };
 
@@ -126,7 +128,7 @@ void launch_final(const DecodeArgs& a, hipStream_t s);
 
 void launch_enc_len(const EncodeArgs& a, hipStream_t s);
 void launch_enc_scan(const EncodeArgs& a, hipStream_t s);
-void launch_enc_emit(const EncodeArgs& a, hipStream_t s, uint32_t grid);
+void launch_enc_pieces(const EncodeArgs& a, hipStream_t s);
 void launch_enc_final(const EncodeArgs& a, hipStream_t s);
 
 void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s);
