@@ -126,8 +126,8 @@ def main():
     ctx.set_timing(False)
     timing = ctx.timing()
 
-    # dominant kernel: k_pieces reads each frame's payload bytes off the wire and writes them unmasked
-    unmask_ms, unmask_n = timing["k_pieces"]
+    # dominant kernel: k_piecesN reads each frame's payload bytes off the wire and writes them unmasked
+    unmask_ms, unmask_n = timing["k_piecesN"]
     avg_unmask_s = unmask_ms / 1e3 / max(1, unmask_n)
     alg_bytes = wire_bytes + F * P  # per launch: wire read + payload written
     copy = ctx.copy_ceiling(wire, payload, wire_bytes)
@@ -185,7 +185,7 @@ def main():
             },
             "roofline": {
                 "bound": "hbm",
-                "kernel": "k_pieces",
+                "kernel": "k_piecesN",
                 "achieved": round(achieved, 1),
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
@@ -225,7 +225,7 @@ def _timed(ctx, step, steps, warmup, dev, kernel):
 
 
 def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps, warmup, expect_errors=None):
-    """Decode GiB/s (wire) + k_pieces roofline of one device-resident batch."""
+    """Decode GiB/s (wire) + k_piecesN roofline of one device-resident batch."""
     import numpy as np
     import torch
     from snf4j_amd import decoder_cfg
@@ -248,13 +248,13 @@ def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps
     n_err = int((r["error"] != 0).sum())
     if expect_errors is not None:
         assert n_err == expect_errors, (name, n_err, expect_errors)
-    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_pieces")
+    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_piecesN")
     alg = wl + payload_bytes
     ach = alg / (kms / 1e3) / 1e9
     return {"config": name, "value": round(wl * steps / el / 2**30, 3), "unit": "GiB/s (wire)",
             "ms_per_step": round(el / steps * 1e3, 4), "frames": n, "sessions": n_s, "wire_bytes": wl,
             "sessions_with_error": n_err,
-            "roofline": {"kernel": "k_pieces", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "roofline": {"kernel": "k_piecesN", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
                          "avg_launch_ms": round(kms, 4)},
             "pipeline_ms": pipe}

@@ -46,7 +46,7 @@ def main():
     ap.add_argument("--round", required=True)
     ap.add_argument("--key", required=True)
     ap.add_argument("--src", default=os.path.join(ROOT, "gpurun_out"))
-    ap.add_argument("--kernel", default="k_pieces")
+    ap.add_argument("--kernel", default="k_piecesN")
     ap.add_argument("--alg-bytes", type=float, default=None, help="algorithmic bytes per launch (for the ratio)")
     a = ap.parse_args()
     out_dir = os.path.join(ROOT, "profiles")

@@ -13,7 +13,7 @@ using namespace ws;
 
 namespace {
 
-const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_pieces",
+const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
                                            "k_enc_pieces", "k_enc_final", "k_synth"};
 
@@ -214,7 +214,8 @@ int wsg_reset_timing(wsg_ctx* c) {
 static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, uint64_t wire_len) {
   const uint64_t F = n_frames ? n_frames : 1;
   const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
-  HIP_TRY(c, c->pieces.ensure(piece_bound(wire_len, F) * sizeof(PieceDesc)));
+  // + PIECES_PER_WAVE: k_piecesN reads its descriptors in groups
+  HIP_TRY(c, c->pieces.ensure((piece_bound(wire_len, F) + PIECES_PER_WAVE) * sizeof(PieceDesc)));
   // utf8_err / sess_err are kept in their idle state between batches (k_merge and
   // k_final reset what they read), so no per-batch memset is needed
   HIP_TRY(c, c->utf8_err.ensure(F * sizeof(uint32_t), 0, c->stream));

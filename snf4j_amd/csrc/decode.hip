@@ -468,17 +468,26 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
     case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
     default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
   }
+  const bool full = nb >= PIECE;        // wave-uniform: every lane holds 16 payload bytes
   const int keep = (int)nb - lane * 16;  // payload bytes in this lane's chunk
 #pragma unroll
-  for (int i = 0; i < 4; ++i) w[i] = keep_bytes(w[i] ^ d.mask, keep - 4 * i);
-  if (keep > 0) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
+  for (int i = 0; i < 4; ++i) w[i] ^= d.mask;
+  if (full) {
+    __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
+  } else {  // the frame's last piece: zero the slot padding past the payload
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = keep_bytes(w[i], keep - 4 * i);
+    if (keep > 0) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
+  }
   if (!(d.info & PD_VALIDATE)) return 0u;
   const uint32_t first_prev = (d.info & PD_FIRST) ? 0u : (alignbyte(pv_hi, pv_lo, b) ^ d.mask);
   const uint32_t pw = dpp_from_prev(w[3], first_prev);
   uint32_t f0 = utf8_err_word_fast(w[0], pw), f1 = utf8_err_word_fast(w[1], w[0]);
   uint32_t f2 = utf8_err_word_fast(w[2], w[1]), f3 = utf8_err_word_fast(w[3], w[2]);
   if (lane == 0 && (d.info & PD_FIRST)) f0 &= 0x80000000u;  // bytes 0..2: checked against the fragment carry
-  f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
+  if (!full) {
+    f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
+  }
   return f0 | f1 | f2 | f3;
 }
 
@@ -491,24 +500,12 @@ __device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
   return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + i;
 }
 
-template <int NT, int WPB, int XCD>
-__global__ __launch_bounds__(64 * WPB) void k_pieces(DecodeArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint64_t p = (uint64_t)__builtin_amdgcn_readfirstlane(blk * (uint32_t)WPB + (threadIdx.x >> 6));
-  const PieceDesc d = a.pieces[p];
-  const uint64_t total = *a.total;
-  // keep both scalar loads in flight together (the exit test below would
-  // otherwise let the compiler wait for `total` before issuing the descriptor load)
-  asm volatile("" ::"s"(d.info), "s"(d.mask), "s"(d.frame), "s"(total));
-  const uint64_t pstart = p * PIECE;
-  if (pstart >= total) return;
-  if (!(d.info & PD_MULTI)) {
-    const uint32_t err = piece_fast<NT>(a, d, pstart, lane);
-    if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d.frame], 1u);
-    return;
-  }
-  // ---- general path: the piece spans several frame slots (small frames)
+// General path: the piece spans several frame slots (small frames).  Each lane
+// finds the frame owning its 16 output bytes by walking the records from the
+// piece's first frame; the UTF-8 carry is taken per lane.
+template <int NT>
+__device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDesc d, uint64_t pstart, uint64_t total,
+                                              int lane) {
   const uint32_t aux = NT ? 2 : 0;
   const __amdgpu_buffer_rsrc_t rout =
       __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload_out + pstart), 0, (int)PIECE, 0x00020000);
@@ -558,6 +555,161 @@ __global__ __launch_bounds__(64 * WPB) void k_pieces(DecodeArgs a) {
       if (j == 0) e0 &= 0x80000000u;
       e0 &= keep_flags(keep); e1 &= keep_flags(keep - 4); e2 &= keep_flags(keep - 8); e3 &= keep_flags(keep - 12);
       if (e0 | e1 | e2 | e3) atomicOr(&a.utf8_err[lk], 1u);
+    }
+  }
+}
+
+template <int NT, int WPB, int XCD>
+__global__ __launch_bounds__(64 * WPB) void k_pieces(DecodeArgs a) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t p = (uint64_t)__builtin_amdgcn_readfirstlane(blk * (uint32_t)WPB + (threadIdx.x >> 6));
+  const PieceDesc d = a.pieces[p];
+  const uint64_t total = *a.total;
+  // keep both scalar loads in flight together (the exit test below would
+  // otherwise let the compiler wait for `total` before issuing the descriptor load)
+  asm volatile("" ::"s"(d.info), "s"(d.mask), "s"(d.frame), "s"(total));
+  const uint64_t pstart = p * PIECE;
+  if (pstart >= total) return;
+  if (!(d.info & PD_MULTI)) {
+    const uint32_t err = piece_fast<NT>(a, d, pstart, lane);
+    if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d.frame], 1u);
+    return;
+  }
+  piece_general<NT>(a, d, pstart, total, lane);
+}
+
+// output dwords of a lane from its aligned source block (W0..W3) and the next
+// lane's (W4..W7): bytes sh.. of the 32-byte window (sh wave-uniform)
+__device__ __forceinline__ void funnel16(uint32_t sh, uint32_t W0, uint32_t W1, uint32_t W2, uint32_t W3, uint32_t W4,
+                                         uint32_t W5, uint32_t W6, uint32_t W7, uint32_t w[4]) {
+  const uint32_t b = sh & 3u;
+  switch (sh >> 2) {
+    case 0: w[0] = alignbyte(W1, W0, b); w[1] = alignbyte(W2, W1, b); w[2] = alignbyte(W3, W2, b); w[3] = alignbyte(W4, W3, b); break;
+    case 1: w[0] = alignbyte(W2, W1, b); w[1] = alignbyte(W3, W2, b); w[2] = alignbyte(W4, W3, b); w[3] = alignbyte(W5, W4, b); break;
+    case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
+    default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
+  }
+}
+
+// N consecutive pieces of one frame per wave (N KiB in flight per wave).  All
+// but the last piece are full, so the source is contiguous: block 64 of piece i
+// is lane 0's block of piece i+1 (readlane), the last piece's block 64 is one
+// extra load, and the UTF-8 carry of piece i+1 is lane 63's last word of piece i.
+template <int NT, int N>
+__device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const PieceDesc d, const uint32_t nb_last,
+                                                uint64_t pstart, int lane) {
+  const uint32_t aux = NT ? 2 : 0;
+  const uint64_t s = d.info & PD_SRC_MASK;
+  const uint64_t a16 = s & ~15ull;
+  const uint32_t sh = (uint32_t)(s & 15u);
+  const uint32_t boff = (uint32_t)lane * 16u;
+  const __amdgpu_buffer_rsrc_t rout =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload_out + pstart), 0, (int)(N * PIECE), 0x00020000);
+  const uint32_t b = sh & 3u;
+  const uint64_t pva = a16 >= 16u ? a16 - 16u : 0u;
+  const uint32_t i0 = 3u + (sh >> 2);
+  const uint32_t pv_lo = ((const uint32_t*)(a.wire + pva))[i0];
+  const uint32_t pv_hi = ((const uint32_t*)(a.wire + pva))[i0 + 1];
+  u32x4 A[N];
+  u32x4 nx;
+  if (a16 + N * PIECE + 16u <= a.wire_len) {
+    const __amdgpu_buffer_rsrc_t rin =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.wire + a16), 0, (int)(N * PIECE + 16u), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < N; ++i) A[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, boff + i * PIECE, 0, aux);
+    nx = *(const u32x4*)(a.wire + a16 + N * PIECE);
+  } else {  // the wire's last bytes: byte loads (the buffer range check is per dword)
+#pragma unroll
+    for (int i = 0; i <= N; ++i) {
+      uint32_t dd[4] = {0u, 0u, 0u, 0u};
+      const uint64_t base = a16 + (uint64_t)i * PIECE + (i < N ? boff : 0u);
+      for (uint32_t k = 0; k < 16u; ++k)
+        if (base + k < a.wire_len) dd[k >> 2] |= (uint32_t)a.wire[base + k] << (8 * (k & 3));
+      if (i < N) A[i] = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+      else nx = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+    }
+  }
+  uint32_t w[N][4];
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    u32x4 n;
+    if (i + 1 < N) {
+      n.x = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].x, 0);
+      n.y = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].y, 0);
+      n.z = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].z, 0);
+      n.w = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].w, 0);
+    } else {
+      n = nx;
+    }
+    funnel16(sh, A[i].x, A[i].y, A[i].z, A[i].w, dpp_from_next(A[i].x, n.x), dpp_from_next(A[i].y, n.y),
+             dpp_from_next(A[i].z, n.z), dpp_from_next(A[i].w, n.w), w[i]);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) w[i][k] ^= d.mask;
+  }
+  const bool full = nb_last >= PIECE;
+  const int keep = (int)nb_last - lane * 16;
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    if (i + 1 < N || full) {
+      __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[i][0], w[i][1], w[i][2], w[i][3]}, rout, boff + i * PIECE, 0,
+                                             aux);
+    } else {  // the frame's last piece: zero the slot padding past the payload
+      uint32_t v[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) v[k] = keep_bytes(w[i][k], keep - 4 * k);
+      if (keep > 0) __builtin_amdgcn_raw_buffer_store_b128((u32x4){v[0], v[1], v[2], v[3]}, rout, boff + i * PIECE, 0, aux);
+    }
+  }
+  if (!(d.info & PD_VALIDATE)) return 0u;
+  uint32_t err = 0;
+  uint32_t carry = (d.info & PD_FIRST) ? 0u : (alignbyte(pv_hi, pv_lo, b) ^ d.mask);
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    const uint32_t pw = dpp_from_prev(w[i][3], carry);
+    uint32_t f0 = utf8_err_word_fast(w[i][0], pw), f1 = utf8_err_word_fast(w[i][1], w[i][0]);
+    uint32_t f2 = utf8_err_word_fast(w[i][2], w[i][1]), f3 = utf8_err_word_fast(w[i][3], w[i][2]);
+    if (i == 0 && lane == 0 && (d.info & PD_FIRST)) f0 &= 0x80000000u;  // bytes 0..2: the fragment carry's
+    if (i + 1 == N && !full) {
+      f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
+    }
+    err |= f0 | f1 | f2 | f3;
+    if (i + 1 < N) carry = (uint32_t)__builtin_amdgcn_readlane((int)w[i][3], 63);
+  }
+  return err;
+}
+
+template <int NT, int XCD, int N>
+__global__ __launch_bounds__(64) void k_piecesN(DecodeArgs a) {
+  const int lane = threadIdx.x;
+  const uint32_t blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(blk);
+  PieceDesc d[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = a.pieces[p + i];
+  const uint64_t total = *a.total;
+  asm volatile("" ::"s"(d[0].info), "s"(d[0].mask), "s"(d[0].frame), "s"(d[N - 1].info), "s"(d[N - 1].frame),
+               "s"(total));
+  const uint64_t pstart = p * PIECE;
+  if (pstart >= total) return;
+  // fast: all N pieces exist and are payload of the same frame (then all but the last are full)
+  bool fast = pstart + (uint64_t)(N - 1) * PIECE < total && d[0].frame == d[N - 1].frame;
+#pragma unroll
+  for (int i = 0; i < N; ++i) fast = fast && !(d[i].info & PD_MULTI);
+  if (fast) {
+    const uint32_t nb_last = (uint32_t)(d[N - 1].info >> PD_NB_SHIFT) & 2047u;
+    const uint32_t err = piece_fastN<NT, N>(a, d[0], nb_last, pstart, lane);
+    if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d[0].frame], 1u);
+    return;
+  }
+  for (int i = 0; i < N; ++i) {
+    const uint64_t ps = pstart + (uint64_t)i * PIECE;
+    if (ps >= total) return;
+    if (!(d[i].info & PD_MULTI)) {
+      const uint32_t err = piece_fast<NT>(a, d[i], ps, lane);
+      if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d[i].frame], 1u);
+    } else {
+      piece_general<NT>(a, d[i], ps, total, lane);
     }
   }
 }
@@ -673,8 +825,10 @@ void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid) {
   hipLaunchKernelGGL(k_unmask<4>, dim3(grid), dim3(256), 0, s, a);
 }
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
-  // one 64-lane workgroup per piece, nontemporal loads/stores (fastest in tools/ubench_unmask)
-  hipLaunchKernelGGL((k_pieces<1, 1, 1>), dim3((uint32_t)n_pieces_bound), dim3(64), 0, s, a);
+  // one 64-lane workgroup per two pieces, nontemporal loads/stores, XCD-aware
+  // (fastest in tools/ubench_unmask: 2 KiB in flight per wave)
+  hipLaunchKernelGGL((k_piecesN<1, 1, PIECES_PER_WAVE>),
+                     dim3((uint32_t)((n_pieces_bound + PIECES_PER_WAVE - 1) / PIECES_PER_WAVE)), dim3(64), 0, s, a);
 }
 void launch_merge(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_merge, dim3((uint32_t)((a.n_frames + 255) / 256)), dim3(256), 0, s, a);

@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&a.blk_sum, a.nblk * 8)); CK(hipMalloc(&a.blk_max, 3 * a.nblk * 4));
   CK(hipMalloc(&a.sess_err, S * 8)); CK(hipMalloc(&a.total, 8));
   const uint64_t npb = ws::piece_bound(wire_len, F);
-  CK(hipMalloc(&a.pieces, npb * sizeof(ws::PieceDesc))); CK(hipMalloc(&a.utf8_err, F * 4));
+  CK(hipMalloc(&a.pieces, (npb + 8) * sizeof(ws::PieceDesc))); CK(hipMalloc(&a.utf8_err, F * 4));
   CK(hipMemsetAsync(a.sess_err, 0xff, S * 8, st));
   CK(hipMemsetAsync(a.utf8_err, 0, F * 4, st));
   ws::launch_parse(a, st); ws::launch_scan(a, st); ws::launch_link(a, st);
@@ -72,8 +72,8 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   struct V { const char* name; int kind; uint32_t grid; };
   std::vector<V> vs = {
-      {"copy16 g=8192", 0, 8192},        {"unmask U4 g=F/4", 4, (uint32_t)(F / 4)},
-      {"unmask U1 g=F/16", 1, (uint32_t)(F / 16)}, {"pieces nt W1", 13, 0}, {"pieces nt W1 xcd", 14, 0}, {"pieces W1 xcd", 15, 0}, {"pieces nt W4 xcd", 16, 0},
+      {"copy16 g=8192", 0, 8192}, {"pieces nt W1", 13, 0}, {"pieces nt W1 xcd", 14, 0},
+      {"piecesN2 xcd", 18, 0}, {"piecesN4 xcd", 19, 0}, {"piecesN3 xcd", 24, 0}, {"piecesN4", 25, 0},
       {"parse", 20, 0}, {"scan", 23, 0}, {"link", 21, 0}, {"merge", 22, 0},  // pipeline order: scan is in place
   };
   std::vector<double> best(vs.size(), 1e30), sum(vs.size(), 0);
@@ -100,6 +100,14 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((ws::k_pieces<0, 1, 1>), dim3((uint32_t)npb), dim3(64), 0, st, a);
       } else if (vs[i].kind == 16) {
         hipLaunchKernelGGL((ws::k_pieces<1, 4, 1>), dim3((uint32_t)((npb + 3) / 4)), dim3(256), 0, st, a);
+      } else if (vs[i].kind == 18) {
+        hipLaunchKernelGGL((ws::k_piecesN<1, 1, 2>), dim3((uint32_t)((npb + 1) / 2)), dim3(64), 0, st, a);
+      } else if (vs[i].kind == 19) {
+        hipLaunchKernelGGL((ws::k_piecesN<1, 1, 4>), dim3((uint32_t)((npb + 3) / 4)), dim3(64), 0, st, a);
+      } else if (vs[i].kind == 24) {
+        hipLaunchKernelGGL((ws::k_piecesN<1, 1, 3>), dim3((uint32_t)((npb + 2) / 3)), dim3(64), 0, st, a);
+      } else if (vs[i].kind == 25) {
+        hipLaunchKernelGGL((ws::k_piecesN<1, 0, 4>), dim3((uint32_t)((npb + 3) / 4)), dim3(64), 0, st, a);
       } else if (vs[i].kind == 20) {
         ws::launch_parse(a, st);
       } else if (vs[i].kind == 21) {
