@@ -16,5 +16,5 @@ step() {  # step <name> <seconds> <cmd...>
 step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?; ok $rc || exit $rc
 step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; ok $rc || exit $rc
 step bench_small 300 python bench.py --frames 262144 --steps 5 --warmup 2 --no-cpu-baseline; rc=$?; ok $rc || exit $rc
-step bench 600 python bench.py; rc=$?; ok $rc || exit $rc
+step bench 600 python bench.py --e2e; rc=$?; ok $rc || exit $rc
 echo ALL_DONE
