@@ -82,6 +82,10 @@ def main():
         import torch.distributed as dist
         # the data path has no collective; gloo carries only the barrier and the timing max
         dist.init_process_group("gloo")
+    # WSG_BENCH_ONE_DEVICE=1 puts every rank on device 0: a rehearsal of the N>1
+    # code path (barrier, max over ranks) on a 1-GPU box, never a reported number
+    if os.environ.get("WSG_BENCH_ONE_DEVICE") == "1":
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -318,13 +322,13 @@ def measure_extras(ctx, dev, args):
     enc()
     torch.cuda.synchronize(dev)
     assert int(wire_off[-1].item()) == n * elen
-    el, kms, pipe = _timed(ctx, enc, K, W, dev, "k_enc_pieces")
+    el, kms, pipe = _timed(ctx, enc, K, W, dev, "k_enc_piecesN")
     alg = M * FR * FP + n * elen
     ach = alg / (kms / 1e3) / 1e9
     out.append({"config": "configs[4]: client encode, 64 x 16 MiB messages in 64 KiB frames (header + mask)",
                 "value": round(n * elen * K / el / 2**30, 3), "unit": "GiB/s (wire out)",
                 "ms_per_step": round(el / K * 1e3, 4), "frames": n,
-                "roofline": {"kernel": "k_enc_pieces", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "roofline": {"kernel": "k_enc_piecesN", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                              "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
                              "avg_launch_ms": round(kms, 4)},
                 "pipeline_ms": pipe})

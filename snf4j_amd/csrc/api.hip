@@ -15,7 +15,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_pieces", "k_enc_final", "k_synth"};
+                                           "k_enc_piecesN", "k_enc_final", "k_synth"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -447,7 +447,7 @@ int wsg_encode_batch_device(wsg_ctx* c, int client_mode, const uint8_t* payload,
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
   // pieces of wire_out: bounded by the caller's capacity (the total is only known on the device)
   a.n_pieces = wire_cap / PIECE + 1;
-  if (n_frames) HIP_TRY(c, c->epieces.ensure(a.n_pieces * sizeof(PieceDesc)));
+  if (n_frames) HIP_TRY(c, c->epieces.ensure((a.n_pieces + PIECES_PER_WAVE) * sizeof(PieceDesc)));
   a.pieces = (PieceDesc*)c->epieces.p;
   if (n_frames) {
     timed(c, K_ENC_LEN, [&] { launch_enc_len(a, c->stream); });

@@ -6,7 +6,7 @@
 //   k_enc_scan  one workgroup: exclusive scan of the block aggregates.
 //   k_enc_link  thread per frame: wire offset of each frame (prefix sum).
 //   k_enc_fix   final wire offsets + one descriptor per 1 KiB piece of wire_out.
-//   k_enc_pieces one wave per 1 KiB of wire_out: header bytes (:80-106) and the
+//   k_enc_piecesN one wave per 1 KiB of wire_out: header bytes (:80-106) and the
 //               payload XOR the injected mask key (:107-117), aligned 16-B stores.
 //   k_enc_final thread per session: FrameEncoder.closed carry-out.
 #include "wsgpu_internal.h"
@@ -169,15 +169,10 @@ __device__ __forceinline__ uint8_t enc_header_byte(const wsg_encode_frame& f, ui
   return f.mask[r - 2 - lb];  // client mode only
 }
 
-__global__ __launch_bounds__(64) void k_enc_pieces(EncodeArgs a) {
-  const int lane = threadIdx.x;
-  const uint64_t p = (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x);
-  const PieceDesc d = a.pieces[p];
-  const uint64_t total = a.wire_off[a.n_frames];
-  asm volatile("" ::"s"(d.info), "s"(d.mask), "s"(d.frame), "s"(total));
+// One piece (fast single-frame path or the general path with headers/seams).
+__device__ __forceinline__ void enc_piece(const EncodeArgs& a, const PieceDesc d, uint64_t p, uint64_t lim,
+                                          int lane) {
   const uint64_t ps = p * PIECE;
-  const uint64_t lim = total < a.wire_cap ? total : a.wire_cap;
-  if (ps >= lim) return;
   const uint32_t boff = (uint32_t)lane * 16u;
   const uint64_t o = ps + boff;
   uint32_t w[4];
@@ -280,8 +275,98 @@ __global__ __launch_bounds__(64) void k_enc_pieces(EncodeArgs a) {
   }
 }
 
+// N consecutive pieces of one frame's payload per wave: all loads issued before
+// any store (N KiB in flight per wave); lane 63's next block of piece i is lane
+// 0's block of piece i+1.  The mask phase is the same for every piece (1024 = 0 mod 4).
+template <int N>
+__device__ __forceinline__ void enc_fastN(const EncodeArgs& a, const PieceDesc d, uint32_t nb_last, uint64_t ps,
+                                          uint64_t lim, int lane) {
+  const uint64_t s = d.info & PD_SRC_MASK;
+  const uint64_t a16 = s & ~15ull;
+  const uint32_t sh = (uint32_t)(s & 15u), b = sh & 3u;
+  const uint32_t boff = (uint32_t)lane * 16u;
+  u32x4 A[N], nx;
+  if (a16 + N * PIECE + 16u <= a.payload_len) {
+    const __amdgpu_buffer_rsrc_t rin =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload + a16), 0, (int)(N * PIECE + 16u), 0x00020000);
+#pragma unroll
+    for (int i = 0; i < N; ++i) A[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, boff + i * PIECE, 0, 2);
+    nx = *(const u32x4*)(a.payload + a16 + N * PIECE);
+  } else {
+#pragma unroll
+    for (int i = 0; i <= N; ++i) {
+      uint32_t dd[4] = {0u, 0u, 0u, 0u};
+      const uint64_t base = a16 + (uint64_t)i * PIECE + (i < N ? boff : 0u);
+      for (uint32_t k = 0; k < 16u; ++k)
+        if (base + k < a.payload_len) dd[k >> 2] |= (uint32_t)a.payload[base + k] << (8 * (k & 3));
+      if (i < N) A[i] = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+      else nx = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    u32x4 n;
+    if (i + 1 < N) {
+      n.x = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].x, 0);
+      n.y = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].y, 0);
+      n.z = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].z, 0);
+      n.w = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].w, 0);
+    } else {
+      n = nx;
+    }
+    const uint32_t W0 = A[i].x, W1 = A[i].y, W2 = A[i].z, W3 = A[i].w;
+    const uint32_t W4 = enc_dpp_from_next(A[i].x, n.x), W5 = enc_dpp_from_next(A[i].y, n.y);
+    const uint32_t W6 = enc_dpp_from_next(A[i].z, n.z), W7 = enc_dpp_from_next(A[i].w, n.w);
+    uint32_t w[4];
+    switch (sh >> 2) {
+      case 0: w[0] = alignbyte(W1, W0, b); w[1] = alignbyte(W2, W1, b); w[2] = alignbyte(W3, W2, b); w[3] = alignbyte(W4, W3, b); break;
+      case 1: w[0] = alignbyte(W2, W1, b); w[1] = alignbyte(W3, W2, b); w[2] = alignbyte(W4, W3, b); w[3] = alignbyte(W5, W4, b); break;
+      case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
+      default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
+    }
+    const uint64_t o = ps + (uint64_t)i * PIECE + boff;
+    if (i + 1 == N && boff >= nb_last) continue;
+    const u32x4 v = (u32x4){w[0] ^ d.mask, w[1] ^ d.mask, w[2] ^ d.mask, w[3] ^ d.mask};
+    if (o + 16 <= lim) {
+      __builtin_nontemporal_store(v, (u32x4*)(a.wire_out + o));
+    } else {  // the output's last bytes: wire_out is not padded
+      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
+      for (uint32_t k = 0; k < 16u && o + k < lim; ++k) a.wire_out[o + k] = (uint8_t)(vv[k >> 2] >> (8 * (k & 3)));
+    }
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(64) void k_enc_piecesN(EncodeArgs a) {
+  const int lane = threadIdx.x;
+  const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x);
+  PieceDesc d[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = a.pieces[p + i];
+  const uint64_t total = a.wire_off[a.n_frames];
+  asm volatile("" ::"s"(d[0].info), "s"(d[0].mask), "s"(d[0].frame), "s"(d[N - 1].info), "s"(d[N - 1].frame),
+               "s"(total));
+  const uint64_t ps = p * PIECE;
+  const uint64_t lim = total < a.wire_cap ? total : a.wire_cap;
+  if (ps >= lim) return;
+  bool fast = ps + (uint64_t)(N - 1) * PIECE < lim && d[0].frame == d[N - 1].frame;
+#pragma unroll
+  for (int i = 0; i < N; ++i) fast = fast && !(d[i].info & PD_MULTI);
+  if (fast) {
+    enc_fastN<N>(a, d[0], (uint32_t)(d[N - 1].info >> PD_NB_SHIFT) & 2047u, ps, lim, lane);
+    return;
+  }
+  for (int i = 0; i < N; ++i) {
+    if (ps + (uint64_t)i * PIECE >= lim) return;
+    enc_piece(a, d[i], p + i, lim, lane);
+  }
+}
+
 void launch_enc_pieces(const EncodeArgs& a, hipStream_t s) {
-  if (a.n_pieces) hipLaunchKernelGGL(k_enc_pieces, dim3((uint32_t)a.n_pieces), dim3(64), 0, s, a);
+  if (a.n_pieces)
+    hipLaunchKernelGGL(k_enc_piecesN<ENC_PIECES_PER_WAVE>,
+                       dim3((uint32_t)((a.n_pieces + ENC_PIECES_PER_WAVE - 1) / ENC_PIECES_PER_WAVE)), dim3(64), 0,
+                       s, a);
 }
 
 __global__ __launch_bounds__(256) void k_enc_final(EncodeArgs a) {
