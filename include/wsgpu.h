@@ -199,6 +199,25 @@ int wsg_decode_batch_host(wsg_ctx* ctx, const wsg_decoder_cfg* cfg,
                           uint8_t* payload_out, uint64_t payload_cap,
                           wsg_frame_desc* desc_out, wsg_session_result* result_out);
 
+/* Pipelined form for a continuous flow of host batches: enqueues the uploads on
+ * the context's copy-in stream, the kernels on its stream and the downloads on
+ * its copy-out stream, through one of two device staging slots, and returns.
+ * Successive calls overlap: batch i's download runs beside batch i+1's upload
+ * (PCIe is full duplex; each direction needs its own stream).  A batch whose
+ * slot is still busy waits (host side) for that slot's previous batch.
+ * Host buffers must stay valid (and should be pinned, or the copies serialise)
+ * until wsg_sync(ctx).  The carry state of batch i+1 is uploaded only after
+ * batch i's state came back, so successive batches may share sessions and one
+ * host state array.  payload_cap >= wire_len + 16 * n_frames: the whole payload
+ * region is copied back, its used size being known only on the device. */
+int wsg_decode_batch_host_async(wsg_ctx* ctx, const wsg_decoder_cfg* cfg,
+                                const uint8_t* wire, uint64_t wire_len,
+                                const uint64_t* frame_off, uint64_t n_frames,
+                                const uint32_t* session_first, uint32_t n_sessions,
+                                wsg_session_state* state,
+                                uint8_t* payload_out, uint64_t payload_cap,
+                                wsg_frame_desc* desc_out, wsg_session_result* result_out);
+
 /* FrameDecoder.available(ISession, byte[], off, len) for a decoder with no
  * pending partial payload (FrameDecoder.java:357-401): returns 0 if the header
  * is incomplete, the full frame length if available, otherwise len.  On the

@@ -91,6 +91,7 @@ def _load():
         "wsg_decode_payload_bound": ([u64, u64], u64),
         "wsg_decode_batch_device": ([p, P(DecoderCfg), p, u64, p, u64, p, u32, p, p, u64, p, p], i32),
         "wsg_decode_batch_host": ([p, P(DecoderCfg), p, u64, p, u64, p, u32, p, p, u64, p, p], i32),
+        "wsg_decode_batch_host_async": ([p, P(DecoderCfg), p, u64, p, u64, p, u32, p, p, u64, p, p], i32),
         "wsg_frame_available": ([p, u64, P(i32), P(i64), P(i64)], i64),
         "wsg_check_header": ([P(DecoderCfg), i32, p, u64, P(i64)], i32),
         "wsg_encoded_length": ([u32, i32], u64),

@@ -149,6 +149,18 @@ class Context:
                                         payload.ctypes.data, cap, desc.ctypes.data, result.ctypes.data), self._h)
         return payload, desc[:n_frames], result[:n_sessions]
 
+    def decode_host_async(self, cfg: DecoderCfg, wire, frame_off, session_first, state, payload, desc, result,
+                          wire_len: int | None = None):
+        """Enqueue H2D + decode + D2H of a host batch and return (wsg_decode_batch_host_async).
+        All buffers are host tensors/arrays (pinned for real overlap) that must stay alive
+        until sync(); `payload` holds >= wire_len + 16 * n_frames bytes."""
+        n_frames = int(np.prod(frame_off.shape)) - 1
+        n_sessions = int(np.prod(session_first.shape)) - 1
+        wl = int(np.prod(wire.shape)) if wire_len is None else int(wire_len)
+        check(lib.wsg_decode_batch_host_async(self._h, C.byref(cfg), _p(wire), wl, _p(frame_off), n_frames,
+                                              _p(session_first), n_sessions, _p(state), _p(payload),
+                                              int(np.prod(payload.shape)), _p(desc), _p(result)), self._h)
+
     # -------------------------------------------------------------- encode
     def encode_device(self, client_mode: bool, payload, frames, session_first, closed, wire_out, wire_off):
         n_frames = frames.numel() // ENCODE_DTYPE.itemsize if frames.dtype.itemsize == 1 else frames.shape[0]

@@ -44,6 +44,13 @@ struct EventPair {
   hipEvent_t a, b;
 };
 
+// One staging slot of the pipelined host path (wsg_decode_batch_host_async).
+struct HostSlot {
+  DevBuf wire, off, sf, state, payload, desc, result;
+  hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_state = nullptr, ev_out = nullptr;
+  bool used = false;
+};
+
 }  // namespace
 
 struct wsg_ctx {
@@ -57,6 +64,11 @@ struct wsg_ctx {
   DevBuf esess, elast_close, epieces;
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
+  // pipelined host path: copy-in / copy-out streams and two staging slots
+  hipStream_t s_in = nullptr, s_out = nullptr;
+  HostSlot slot[2];
+  int next_slot = 0;
+  hipEvent_t ev_prev_state = nullptr;  // state download of the previous async batch
   // timing
   bool timing = false;
   std::vector<EventPair> pending;
@@ -155,7 +167,9 @@ int wsg_open(int device, void* stream, wsg_ctx** out) {
 int wsg_close(wsg_ctx* c) {
   if (!c) return WSG_API_EINVAL;
   (void)hipSetDevice(c->device);
+  if (c->s_in) (void)hipStreamSynchronize(c->s_in);
   (void)hipStreamSynchronize(c->stream);
+  if (c->s_out) (void)hipStreamSynchronize(c->s_out);
   drain_timing(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->rec,     &c->prev,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
@@ -163,6 +177,15 @@ int wsg_close(wsg_ctx* c) {
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
+  for (HostSlot& hs : c->slot) {
+    DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
+    for (DevBuf* b : sb) b->release();
+    hipEvent_t evs[] = {hs.ev_in, hs.ev_k, hs.ev_state, hs.ev_out};
+    for (hipEvent_t e : evs)
+      if (e) (void)hipEventDestroy(e);
+  }
+  if (c->s_in) (void)hipStreamDestroy(c->s_in);
+  if (c->s_out) (void)hipStreamDestroy(c->s_out);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return WSG_API_OK;
@@ -183,7 +206,9 @@ const char* wsg_last_error(wsg_ctx* c) { return c ? c->err.c_str() : "null conte
 
 int wsg_sync(wsg_ctx* c) {
   if (!c) return WSG_API_EINVAL;
+  if (c->s_in) HIP_TRY(c, hipStreamSynchronize(c->s_in));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (c->s_out) HIP_TRY(c, hipStreamSynchronize(c->s_out));
   return WSG_API_OK;
 }
 
@@ -301,10 +326,12 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   return WSG_API_OK;
 }
 
-int wsg_decode_batch_host(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t* wire, uint64_t wire_len,
-                          const uint64_t* frame_off, uint64_t n_frames, const uint32_t* session_first,
-                          uint32_t n_sessions, wsg_session_state* state, uint8_t* payload_out, uint64_t payload_cap,
-                          wsg_frame_desc* desc_out, wsg_session_result* result_out) {
+// H2D, decode, D2H on the ctx stream, then wait; exactly the payload bytes used
+// are copied back.
+static int decode_host_impl(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t* wire, uint64_t wire_len,
+                            const uint64_t* frame_off, uint64_t n_frames, const uint32_t* session_first,
+                            uint32_t n_sessions, wsg_session_state* state, uint8_t* payload_out, uint64_t payload_cap,
+                            wsg_frame_desc* desc_out, wsg_session_result* result_out) {
   if (!c || !cfg) return WSG_API_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
   const uint64_t bound = wire_len + 16 * n_frames + 16;
@@ -328,12 +355,13 @@ int wsg_decode_batch_host(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t*
                                    (wsg_session_state*)c->h_state.p, (uint8_t*)c->h_payload.p, bound,
                                    (wsg_frame_desc*)c->h_desc.p, (wsg_session_result*)c->h_result.p);
   if (rc) return rc;
-  uint64_t total = 0;
   if (n_frames) {
+    uint64_t total;
     HIP_TRY(c, hipMemcpyAsync(&total, c->total.p, sizeof total, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipStreamSynchronize(s));
-    if (total > payload_cap) return set_err(c, WSG_API_ERANGE, "payload_cap %llu < %llu", (unsigned long long)payload_cap,
-                                            (unsigned long long)total);
+    if (total > payload_cap)
+      return set_err(c, WSG_API_ERANGE, "payload_cap %llu < %llu", (unsigned long long)payload_cap,
+                     (unsigned long long)total);
     if (total) HIP_TRY(c, hipMemcpyAsync(payload_out, c->h_payload.p, total, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipMemcpyAsync(desc_out, c->h_desc.p, n_frames * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, s));
   }
@@ -344,6 +372,84 @@ int wsg_decode_batch_host(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t*
                               hipMemcpyDeviceToHost, s));
   }
   HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
+
+int wsg_decode_batch_host(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t* wire, uint64_t wire_len,
+                          const uint64_t* frame_off, uint64_t n_frames, const uint32_t* session_first,
+                          uint32_t n_sessions, wsg_session_state* state, uint8_t* payload_out, uint64_t payload_cap,
+                          wsg_frame_desc* desc_out, wsg_session_result* result_out) {
+  return decode_host_impl(c, cfg, wire, wire_len, frame_off, n_frames, session_first, n_sessions, state, payload_out,
+                          payload_cap, desc_out, result_out);
+}
+
+// Pipelined host batch: uploads on s_in, kernels on the ctx stream, downloads on
+// s_out (each copy direction needs its own stream to overlap), two staging slots
+// used alternately.  Event edges:
+//   slot reuse   upload(i+2) waits kernels(i); kernels(i+2) waits downloads(i)
+//   carry state  state upload(i+1) waits state download(i), so batches that share
+//                sessions (and one host state array) chain correctly while the
+//                wire upload of batch i+1 still overlaps the kernels of batch i
+int wsg_decode_batch_host_async(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_t* wire, uint64_t wire_len,
+                                const uint64_t* frame_off, uint64_t n_frames, const uint32_t* session_first,
+                                uint32_t n_sessions, wsg_session_state* state, uint8_t* payload_out,
+                                uint64_t payload_cap, wsg_frame_desc* desc_out, wsg_session_result* result_out) {
+  if (!c || !cfg) return WSG_API_EINVAL;
+  if (n_frames && payload_cap < wire_len + 16 * n_frames)
+    return set_err(c, WSG_API_ERANGE, "payload_cap below wire_len + 16 * n_frames");
+  HIP_TRY(c, hipSetDevice(c->device));
+  if (!c->s_in) HIP_TRY(c, hipStreamCreateWithFlags(&c->s_in, hipStreamNonBlocking));
+  if (!c->s_out) HIP_TRY(c, hipStreamCreateWithFlags(&c->s_out, hipStreamNonBlocking));
+  HostSlot& h = c->slot[c->next_slot];
+  c->next_slot ^= 1;
+  hipEvent_t* evs[] = {&h.ev_in, &h.ev_k, &h.ev_state, &h.ev_out};
+  for (hipEvent_t* e : evs)
+    if (!*e) HIP_TRY(c, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  const uint64_t bound = wire_len + 16 * n_frames + 16;
+  if (h.used) {  // buffers may be re-allocated below: drain this slot's last batch first
+    HIP_TRY(c, hipEventSynchronize(h.ev_out));
+  }
+  HIP_TRY(c, h.wire.ensure(wire_len + 32));
+  HIP_TRY(c, h.off.ensure((n_frames + 1) * sizeof(uint64_t)));
+  HIP_TRY(c, h.sf.ensure(((uint64_t)n_sessions + 1) * sizeof(uint32_t)));
+  HIP_TRY(c, h.state.ensure(((uint64_t)n_sessions + 1) * sizeof(wsg_session_state)));
+  HIP_TRY(c, h.payload.ensure(bound));
+  HIP_TRY(c, h.desc.ensure((n_frames + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, h.result.ensure(((uint64_t)n_sessions + 1) * sizeof(wsg_session_result)));
+  // uploads
+  if (wire_len) HIP_TRY(c, hipMemcpyAsync(h.wire.p, wire, wire_len, hipMemcpyHostToDevice, c->s_in));
+  HIP_TRY(c, hipMemcpyAsync(h.off.p, frame_off, (n_frames + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, c->s_in));
+  HIP_TRY(c, hipMemcpyAsync(h.sf.p, session_first, ((uint64_t)n_sessions + 1) * sizeof(uint32_t),
+                            hipMemcpyHostToDevice, c->s_in));
+  if (c->ev_prev_state) HIP_TRY(c, hipStreamWaitEvent(c->s_in, c->ev_prev_state, 0));
+  if (n_sessions)
+    HIP_TRY(c, hipMemcpyAsync(h.state.p, state, (uint64_t)n_sessions * sizeof(wsg_session_state),
+                              hipMemcpyHostToDevice, c->s_in));
+  HIP_TRY(c, hipEventRecord(h.ev_in, c->s_in));
+  // kernels
+  HIP_TRY(c, hipStreamWaitEvent(c->stream, h.ev_in, 0));
+  int rc = wsg_decode_batch_device(c, cfg, (const uint8_t*)h.wire.p, wire_len, (const uint64_t*)h.off.p, n_frames,
+                                   (const uint32_t*)h.sf.p, n_sessions, (wsg_session_state*)h.state.p,
+                                   (uint8_t*)h.payload.p, bound, (wsg_frame_desc*)h.desc.p,
+                                   (wsg_session_result*)h.result.p);
+  if (rc) return rc;
+  HIP_TRY(c, hipEventRecord(h.ev_k, c->stream));
+  // downloads: the carry state first (the next batch's state upload waits for it)
+  HIP_TRY(c, hipStreamWaitEvent(c->s_out, h.ev_k, 0));
+  if (n_sessions)
+    HIP_TRY(c, hipMemcpyAsync(state, h.state.p, (uint64_t)n_sessions * sizeof(wsg_session_state),
+                              hipMemcpyDeviceToHost, c->s_out));
+  HIP_TRY(c, hipEventRecord(h.ev_state, c->s_out));
+  c->ev_prev_state = h.ev_state;
+  if (n_sessions)
+    HIP_TRY(c, hipMemcpyAsync(result_out, h.result.p, (uint64_t)n_sessions * sizeof(wsg_session_result),
+                              hipMemcpyDeviceToHost, c->s_out));
+  if (n_frames) {
+    HIP_TRY(c, hipMemcpyAsync(desc_out, h.desc.p, n_frames * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, c->s_out));
+    HIP_TRY(c, hipMemcpyAsync(payload_out, h.payload.p, wire_len + 16 * n_frames, hipMemcpyDeviceToHost, c->s_out));
+  }
+  HIP_TRY(c, hipEventRecord(h.ev_out, c->s_out));
+  h.used = true;
   return WSG_API_OK;
 }
 

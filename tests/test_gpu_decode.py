@@ -271,3 +271,41 @@ def test_empty_and_closed_sessions(ctx, oracle):
     wire, off, sf = wsgen.make_batch(sessions)
     p, d, r = ctx.decode_host(_cfg(False, False, 65536), wire, off, sf, state)
     assert list(r["n_delivered"]) == [1, 0, 1] and (r["error"] == 0).all()
+
+
+def test_host_async_matches_sync(ctx, oracle):
+    """wsg_decode_batch_host_async (pipelined host path): two back-to-back batches that
+    share sessions and one host state array == the sync host path batch by batch."""
+    import torch
+    from snf4j_amd import Context
+    from snf4j_amd._lib import DESC_DTYPE, RESULT_DTYPE, STATE_DTYPE
+    rng = np.random.default_rng(77)
+    sessions = [wsgen.session_frames(rng, int(rng.integers(0, 14)),
+                                     inject=wsgen.INJECT_KINDS[i % len(wsgen.INJECT_KINDS)] if i % 4 == 0 else None)
+                for i in range(40)]
+    cuts = [int(rng.integers(0, len(fr) + 1)) for fr in sessions]
+    batches = [wsgen.make_batch([fr[:c] for fr, c in zip(sessions, cuts)]),
+               wsgen.make_batch([fr[c:] for fr, c in zip(sessions, cuts)])]
+    cfg = _cfg(False, False, 65536)
+    n_s = len(sessions)
+    st_sync = np.zeros(n_s, dtype=STATE_DTYPE)
+    want = [ctx.decode_host(cfg, w, o, f, st_sync) for w, o, f in batches]
+    c2 = Context(0, stream=torch.cuda.Stream())
+    st = np.zeros(n_s, dtype=STATE_DTYPE)
+    got = []
+    try:
+        for w, o, f in batches:
+            n = len(o) - 1
+            pay = np.zeros(w.size + 16 * n + 16, np.uint8)
+            desc = np.zeros(max(1, n), DESC_DTYPE)
+            res = np.zeros(n_s, RESULT_DTYPE)
+            c2.decode_host_async(cfg, w if w.size else np.zeros(1, np.uint8), o, f, st, pay, desc, res,
+                                 wire_len=w.size)
+            got.append((pay, desc[:n], res))
+        c2.sync()
+    finally:
+        c2.close()
+    assert np.array_equal(st, st_sync)
+    for (gp, gd, gr), (wp, wd, wr), (w, o, f) in zip(got, want, batches):
+        assert np.array_equal(gr, wr) and np.array_equal(gd, wd)
+        compare((gp, gd, gr), (wp, wd, wr), f, "async")
