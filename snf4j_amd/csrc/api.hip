@@ -281,7 +281,7 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
                             uint64_t payload_cap, wsg_frame_desc* desc_out, wsg_session_result* result_out) {
   if (!c || !cfg) return WSG_API_EINVAL;
   if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
-  if (n_frames >= 0x7fffffffull) return set_err(c, WSG_API_ERANGE, "too many frames in one batch");
+  if (n_frames >= (1ull << 30)) return set_err(c, WSG_API_ERANGE, "too many frames in one batch (max 2^30 - 1)");
   if (((uintptr_t)wire & 3) || ((uintptr_t)payload_out & 15))
     return set_err(c, WSG_API_EINVAL, "wire must be 4-B aligned and payload_out 16-B aligned");
   if (payload_cap < wire_len + 16 * n_frames)

@@ -32,6 +32,20 @@ __device__ bool utf8_valid_run(const uint8_t* wire, uint64_t off, uint32_t n, ui
   return !utf8_incomplete(p3, p2, p1);
 }
 
+// Per-frame scan input: payload slot bytes, and the "last frame of a kind" max
+// fields as (k << 1) | bit carrying what k_link needs about that frame (FIN of
+// the last data frame, TEXT-ness of the last message start), so k_link never
+// reads another frame's record.  Frame indices < 2^30 (wsg_decode_batch_device).
+__device__ __forceinline__ Agg frame_agg(uint64_t k, const FrameRec& r) {
+  Agg v;
+  v.sum = (uint64_t)((r.len + 15u) & ~15u);
+  const bool data = code_is_data(r.code);
+  v.m0 = data ? (int32_t)((k << 1) | ((r.code & CODE_FIN) ? 1u : 0u)) : -1;
+  v.m1 = code_is_start(r.code) ? (int32_t)((k << 1) | (code_op(r.code) == WSG_OP_TEXT ? 1u : 0u)) : -1;
+  v.m2 = (data && r.len) ? (int32_t)(k << 1) : -1;
+  return v;
+}
+
 // ------------------------------------------------------------------ k_parse
 __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
@@ -115,11 +129,7 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
              (hd.rsv << CODE_RSV_SHIFT) | (hd.masked ? CODE_MASKED : 0u) | (hd.opcode << CODE_OP_SHIFT);
     r.sess = s;
     a.rec[k] = r;
-    v.sum = (uint64_t)((len + 15u) & ~15u);
-    const bool data = code_is_data(r.code);
-    v.m0 = data ? (int32_t)k : -1;
-    v.m1 = code_is_start(r.code) ? (int32_t)k : -1;
-    v.m2 = (data && len) ? (int32_t)k : -1;
+    v = frame_agg(k, r);
   }
   Agg tot;
   block_excl_scan(v, &tot);
@@ -132,24 +142,37 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
 }
 
 // ------------------------------------------------------------------ k_scan
+// One workgroup: exclusive scan of the block aggregates in place, 4 entries per
+// thread per pass (one block scan per 4096 blocks).
 __global__ __launch_bounds__(1024) void k_scan(DecodeArgs a) {
   Agg carry = AGG_ID;
-  for (uint32_t base = 0; base < a.nblk; base += 1024) {
-    const uint32_t b = base + threadIdx.x;
-    Agg v = AGG_ID;
-    if (b < a.nblk) {
-      v.sum = a.blk_sum[b];
-      v.m0 = a.blk_max[b];
-      v.m1 = a.blk_max[a.nblk + b];
-      v.m2 = a.blk_max[2 * a.nblk + b];
+  for (uint32_t base = 0; base < a.nblk; base += 4096) {
+    const uint32_t b0 = base + threadIdx.x * 4;
+    Agg e[4], t = AGG_ID;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t b = b0 + i;
+      e[i] = AGG_ID;
+      if (b < a.nblk) {
+        e[i].sum = a.blk_sum[b];
+        e[i].m0 = a.blk_max[b];
+        e[i].m1 = a.blk_max[a.nblk + b];
+        e[i].m2 = a.blk_max[2 * a.nblk + b];
+      }
+      t = agg_op(t, e[i]);
     }
     Agg tot;
-    Agg ex = agg_op(carry, block_excl_scan(v, &tot));
-    if (b < a.nblk) {
-      a.blk_sum[b] = ex.sum;
-      a.blk_max[b] = ex.m0;
-      a.blk_max[a.nblk + b] = ex.m1;
-      a.blk_max[2 * a.nblk + b] = ex.m2;
+    Agg ex = agg_op(carry, block_excl_scan(t, &tot));
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const uint32_t b = b0 + i;
+      if (b < a.nblk) {
+        a.blk_sum[b] = ex.sum;
+        a.blk_max[b] = ex.m0;
+        a.blk_max[a.nblk + b] = ex.m1;
+        a.blk_max[2 * a.nblk + b] = ex.m2;
+      }
+      ex = agg_op(ex, e[i]);
     }
     carry = agg_op(carry, tot);
   }
@@ -164,11 +187,7 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   Agg v = AGG_ID;
   if (live) {
     r = a.rec[k];
-    v.sum = (uint64_t)((r.len + 15u) & ~15u);
-    const bool data = code_is_data(r.code);
-    v.m0 = data ? (int32_t)k : -1;
-    v.m1 = code_is_start(r.code) ? (int32_t)k : -1;
-    v.m2 = (data && r.len) ? (int32_t)k : -1;
+    v = frame_agg(k, r);
   }
   Agg tot;
   Agg ex = block_excl_scan(v, &tot);
@@ -179,9 +198,10 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   bp.m1 = a.blk_max[a.nblk + blockIdx.x];
   bp.m2 = a.blk_max[2 * a.nblk + blockIdx.x];
   ex = agg_op(bp, ex);
-  a.prev[k] = ex.m0;
-  a.prev[a.n_frames + k] = ex.m1;
-  a.prev[2 * a.n_frames + k] = ex.m2;
+  const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
+  a.prev[k] = jd;
+  a.prev[a.n_frames + k] = jm;
+  a.prev[2 * a.n_frames + k] = ex.m2 >> 1;
 
   const uint32_t s = r.sess;
   const int32_t sf = (int32_t)a.session_first[s];
@@ -190,15 +210,11 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   uint32_t extra = 0;
   if (!code_pre(r.code)) {
     // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
-    const int32_t j = ex.m0;
-    const bool frag = j >= sf ? !(a.rec[j].code & CODE_FIN) : (st.fragmentation != 0);
+    const bool frag = jd >= sf ? !(ex.m0 & 1) : (st.fragmentation != 0);
     extra |= rules_frag(op, frag) << CODE_FRAG_SHIFT;
     if (a.validate) {
       bool text = op == WSG_OP_TEXT;
-      if (op == WSG_OP_CONTINUATION) {
-        const int32_t ms = ex.m1;
-        text = ms >= sf ? code_op(a.rec[ms].code) == WSG_OP_TEXT : (st.text_open != 0);
-      }
+      if (op == WSG_OP_CONTINUATION) text = jm >= sf ? (ex.m1 & 1) != 0 : (st.text_open != 0);
       if (text) extra |= CODE_VALIDATE;
     }
   }
