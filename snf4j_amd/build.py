@@ -12,7 +12,11 @@ OUT = os.path.join(HERE, "libwsgpu.so")
 SOURCES = ["decode.hip", "encode.hip", "synth.hip", "api.hip"]
 HEADERS = ["ws_rules.h", "wsgpu_internal.h", "wsgpu_scan.h", "../../include/wsgpu.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function"]
+# -disable-promote-alloca-to-lds: a dynamically indexed local array must not turn
+# into an LDS allocation, which slows the dispatch of the piece kernels' millions
+# of one-wave workgroups (measured: k_piecesN -10%)
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-function",
+         "-mllvm", "-disable-promote-alloca-to-lds"]
 
 
 def _stale() -> bool:

@@ -54,26 +54,32 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
     const uint32_t s = find_session(a.session_first, a.n_sessions, k);
     const uint64_t o = a.frame_off[k], e = a.frame_off[k + 1];
     const uint64_t ext = e > o ? e - o : 0;
-    uint8_t hb[20];  // wire bytes o .. o+16 (and up to 3 more), zero past the wire end
-    const uint8_t* h = hb;
+    // wire bytes o .. o+19 as five words, zero past the wire end
+    uint32_t w0, w1, w2, w3, w4;
     const uint64_t a4 = o & ~3ull;
     if (a4 + 24 <= a.wire_len) {
       const uint32_t* p = (const uint32_t*)(a.wire + a4);
-      uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4], d5 = p[5];
+      const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4], d5 = p[5];
       const uint32_t sh = (uint32_t)(o & 3);
-      uint32_t w[5] = {alignbyte(d1, d0, sh), alignbyte(d2, d1, sh), alignbyte(d3, d2, sh), alignbyte(d4, d3, sh),
-                       alignbyte(d5, d4, sh)};
-#pragma unroll
-      for (int i = 0; i < 20; ++i) hb[i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+      w0 = alignbyte(d1, d0, sh); w1 = alignbyte(d2, d1, sh); w2 = alignbyte(d3, d2, sh);
+      w3 = alignbyte(d4, d3, sh); w4 = alignbyte(d5, d4, sh);
     } else {
-      for (int i = 0; i < 20; ++i) hb[i] = (o + i < a.wire_len) ? a.wire[o + i] : 0;
+      uint64_t lo = 0, mid = 0, hi = 0;
+#pragma unroll
+      for (int i = 0; i < 20; ++i) {
+        const uint64_t b = (o + i < a.wire_len) ? a.wire[o + i] : 0u;
+        if (i < 8) lo |= b << (8 * i);
+        else if (i < 16) mid |= b << (8 * (i - 8));
+        else hi |= b << (8 * (i - 16));
+      }
+      w0 = (uint32_t)lo; w1 = (uint32_t)(lo >> 32); w2 = (uint32_t)mid; w3 = (uint32_t)(mid >> 32); w4 = (uint32_t)hi;
     }
     Header hd;
     uint32_t pre = 0, post = 0, len = 0;
     uint64_t src = o;
-    if (!parse_header(h, ext, hd)) {
+    if (!parse_header_words(w0, w1, w2, w3, w4, ext, hd)) {
       pre = WSG_E_BATCH;
-      hd.opcode = h[0] & 15u; hd.fin = h[0] >> 7; hd.rsv = (h[0] >> 4) & 7u; hd.masked = 0; hd.mask = 0;
+      hd.opcode = w0 & 15u; hd.fin = (w0 >> 7) & 1u; hd.rsv = (w0 >> 4) & 7u; hd.masked = 0; hd.mask = 0;
     } else {
       pre = rules_pre(hd, a.client_mode, a.allow_ext);
       post = rules_post(hd, a.max_payload);
@@ -89,10 +95,10 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
         }
         if (hd.opcode <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry
           // first 3 payload bytes: within the header's 20 loaded bytes (hdr_len <= 14)
-          uint32_t f3 = 0, l3 = 0;
+          uint32_t l3 = 0;
           const uint32_t nf = len < 3 ? len : 3;
-          for (uint32_t i = 0; i < nf; ++i) f3 |= (uint32_t)hb[hd.hdr_len + i] << (8 * i);
-          f3 ^= hd.mask & (nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : (nf == 1 ? 0xffu : 0u)));
+          const uint32_t keep3 = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : (nf == 1 ? 0xffu : 0u));
+          const uint32_t f3 = (bytes_at(w0, w1, w2, w3, w4, hd.hdr_len) ^ hd.mask) & keep3;
           if (nf) {  // last 3 payload bytes: two aligned dwords
             const uint64_t e3 = src + len - nf;  // first of the last nf bytes
             const uint64_t q = e3 & ~3ull;
@@ -102,8 +108,9 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
               hi = *(const uint32_t*)(a.wire + q + 4);
             } else {
               lo = hi = 0;
-              for (uint32_t i = 0; i < 8 && q + i < a.wire_len; ++i)
-                (i < 4 ? lo : hi) |= (uint32_t)a.wire[q + i] << (8 * (i & 3));
+#pragma unroll
+              for (uint32_t i = 0; i < 8; ++i)
+                if (q + i < a.wire_len) (i < 4 ? lo : hi) |= (uint32_t)a.wire[q + i] << (8 * (i & 3));
             }
             const uint32_t t = alignbyte(hi, lo, (uint32_t)(e3 & 3));  // bytes e3.. e3+3
             const uint32_t ph = (uint32_t)(len - nf) & 3u;            // mask phase of byte e3
@@ -528,17 +535,39 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
   const uint64_t pend = pstart + PIECE < total ? pstart + PIECE : total;
   const uint64_t my = pstart + (uint64_t)lane * 16u;
   const bool live = my < pend;
-  uint32_t kk = d.frame, lk = d.frame;
-  FrameRec rr = a.rec[kk];
-  FrameRec lr = rr;
-  uint64_t send = rr.out_off + ((rr.len + 15u) & ~15u);
-  for (;;) {
-    const bool beyond = live && my >= send;
-    if (!__any(beyond)) break;
-    ++kk;
-    rr = a.rec[kk];
-    if (beyond) { lk = kk; lr = rr; }
-    send = rr.out_off + ((rr.len + 15u) & ~15u);
+  uint32_t lk = d.frame;  // frame owning this lane's 16 output bytes
+  FrameRec lr;
+  {
+    // lane-parallel lookup: lane l takes record d.frame + l and the 16-B chunk of the
+    // piece where that frame's slot starts (0 for the piece's first frame, 64 past
+    // the piece end); the chunks are non-decreasing over the lanes, so the owner of
+    // chunk i is the last lane whose chunk is <= i: a 6-step search over shuffles
+    const uint64_t fl = (uint64_t)d.frame + (uint64_t)lane;
+    const bool have = fl < a.n_frames;
+    const uint64_t fs = have ? a.rec[fl].out_off : ~0ull;
+    const uint64_t fslot = have ? (uint64_t)((a.rec[fl].len + 15u) & ~15u) : 0ull;
+    if (__any(have && fslot && fs + fslot >= pend)) {  // the 64 records reach the piece end
+      const int c = fs >= pend ? 64 : (fs <= pstart ? 0 : (int)((fs - pstart) >> 4));
+      int pos = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1)
+        if (__shfl(c, pos + step, 64) <= lane) pos += step;
+      lk = d.frame + (uint32_t)pos;
+      lr = a.rec[lk];  // just loaded by lane pos: a cache hit
+    } else {  // more than 64 frames (empty ones) in the piece: walk the records
+      uint32_t kk = d.frame;
+      FrameRec rr = a.rec[kk];
+      lr = rr;
+      uint64_t send = rr.out_off + ((rr.len + 15u) & ~15u);
+      for (;;) {
+        const bool beyond = live && my >= send;
+        if (!__any(beyond)) break;
+        ++kk;
+        rr = a.rec[kk];
+        if (beyond) { lk = kk; lr = rr; }
+        send = rr.out_off + ((rr.len + 15u) & ~15u);
+      }
+    }
   }
   const uint32_t j = (uint32_t)(my - lr.out_off);
   const int keep = live ? (int)lr.len - (int)j : 0;
@@ -553,7 +582,9 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
       dd[0] = q[0]; dd[1] = q[1]; dd[2] = q[2]; dd[3] = q[3]; dd[4] = q[4];
     } else {
       for (int i = 0; i < 5; ++i) dd[i] = 0u;
-      for (uint32_t i = 0; i < 20u && a4 + i < a.wire_len; ++i) dd[i >> 2] |= (uint32_t)a.wire[a4 + i] << (8 * (i & 3));
+#pragma unroll
+      for (uint32_t i = 0; i < 20u; ++i)  // constant indices: dd stays in registers
+        if (a4 + i < a.wire_len) dd[i >> 2] |= (uint32_t)a.wire[a4 + i] << (8 * (i & 3));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = keep_bytes(alignbyte(dd[i + 1], dd[i], sh) ^ lr.mask, keep - 4 * i);
@@ -718,6 +749,7 @@ __global__ __launch_bounds__(64) void k_piecesN(DecodeArgs a) {
     if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d[0].frame], 1u);
     return;
   }
+#pragma unroll
   for (int i = 0; i < N; ++i) {
     const uint64_t ps = pstart + (uint64_t)i * PIECE;
     if (ps >= total) return;

@@ -166,7 +166,9 @@ __device__ __forceinline__ uint8_t enc_header_byte(const wsg_encode_frame& f, ui
     lb = 0;
   }
   if (r < 2 + lb) return (uint8_t)((uint64_t)len >> (8 * (lb - 1 - (r - 2))));
-  return f.mask[r - 2 - lb];  // client mode only
+  const uint32_t m = (uint32_t)f.mask[0] | ((uint32_t)f.mask[1] << 8) | ((uint32_t)f.mask[2] << 16) |
+                     ((uint32_t)f.mask[3] << 24);
+  return (uint8_t)(m >> (8 * (r - 2 - lb)));  // client mode only
 }
 
 // One piece (fast single-frame path or the general path with headers/seams).
@@ -233,14 +235,16 @@ __device__ __forceinline__ void enc_piece(const EncodeArgs& a, const PieceDesc d
         const uint32_t* q = (const uint32_t*)(a.payload + a4);
         dd[0] = q[0]; dd[1] = q[1]; dd[2] = q[2]; dd[3] = q[3]; dd[4] = q[4];
       } else {
-        for (uint32_t i = 0; i < 20u && a4 + i < a.payload_len; ++i) dd[i >> 2] |= (uint32_t)a.payload[a4 + i] << (8 * (i & 3));
+#pragma unroll
+        for (uint32_t i = 0; i < 20u; ++i)  // constant indices: dd stays in registers
+          if (a4 + i < a.payload_len) dd[i >> 2] |= (uint32_t)a.payload[a4 + i] << (8 * (i & 3));
       }
       const uint32_t ph = (uint32_t)(j0 & 3);
       const uint32_t mr = ph ? (m >> (8 * ph)) | (m << (32 - 8 * ph)) : m;
 #pragma unroll
       for (int i = 0; i < 4; ++i) w[i] = alignbyte(dd[i + 1], dd[i], sh) ^ mr;
     } else {
-      w[0] = w[1] = w[2] = w[3] = 0u;
+      uint64_t blo = 0, bhi = 0;  // the 16 bytes (no dynamically indexed array: registers only)
       for (uint32_t i = 0; i < 16u; ++i) {
         const uint64_t x = o + i;
         if (x >= lim) break;
@@ -264,14 +268,18 @@ __device__ __forceinline__ void enc_piece(const EncodeArgs& a, const PieceDesc d
           const uint64_t j = r - hl;
           byte = a.payload[f.payload_off + j] ^ ((m >> (8 * (j & 3))) & 0xffu);
         }
-        w[i >> 2] |= byte << (8 * (i & 3));
+        if (i < 8) blo |= (uint64_t)byte << (8 * i);
+        else bhi |= (uint64_t)byte << (8 * (i - 8));
       }
+      w[0] = (uint32_t)blo; w[1] = (uint32_t)(blo >> 32); w[2] = (uint32_t)bhi; w[3] = (uint32_t)(bhi >> 32);
     }
   }
   if (o + 16 <= lim) {
     __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (u32x4*)(a.wire_out + o));
   } else {  // the output's last bytes: wire_out is not padded
-    for (uint32_t i = 0; i < 16u && o + i < lim; ++i) a.wire_out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+#pragma unroll
+    for (uint32_t i = 0; i < 16u; ++i)
+      if (o + i < lim) a.wire_out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
   }
 }
 
@@ -330,8 +338,10 @@ __device__ __forceinline__ void enc_fastN(const EncodeArgs& a, const PieceDesc d
     if (o + 16 <= lim) {
       __builtin_nontemporal_store(v, (u32x4*)(a.wire_out + o));
     } else {  // the output's last bytes: wire_out is not padded
-      const uint32_t vv[4] = {v.x, v.y, v.z, v.w};
-      for (uint32_t k = 0; k < 16u && o + k < lim; ++k) a.wire_out[o + k] = (uint8_t)(vv[k >> 2] >> (8 * (k & 3)));
+      const uint64_t vlo = ((uint64_t)v.y << 32) | v.x, vhi = ((uint64_t)v.w << 32) | v.z;
+#pragma unroll
+      for (uint32_t k = 0; k < 16u; ++k)
+        if (o + k < lim) a.wire_out[o + k] = (uint8_t)((k < 8 ? vlo : vhi) >> (8 * (k & 7)));
     }
   }
 }
@@ -356,6 +366,7 @@ __global__ __launch_bounds__(64) void k_enc_piecesN(EncodeArgs a) {
     enc_fastN<N>(a, d[0], (uint32_t)(d[N - 1].info >> PD_NB_SHIFT) & 2047u, ps, lim, lane);
     return;
   }
+#pragma unroll
   for (int i = 0; i < N; ++i) {
     if (ps + (uint64_t)i * PIECE >= lim) return;
     enc_piece(a, d[i], p + i, lim, lane);

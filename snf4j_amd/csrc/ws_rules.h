@@ -34,33 +34,65 @@ struct Header {
 
 // Parse the header from the first n (<= 14 used) bytes; returns false when the
 // header is not complete within n bytes.
-WS_HD bool parse_header(const uint8_t* h, uint64_t n, Header& o) {
+// ---------------------------------------------------------------------------
+// UTF-8.  The Hoehrmann DFA (Utf8.java) rejects at byte p exactly when, with
+// the bytes before p a valid prefix, byte p is not allowed after the last <=3
+// bytes.  That condition needs only the 3 preceding bytes, so every byte can be
+// checked independently; the first flagged byte is the DFA's REJECT byte
+// (proved exhaustively against the DFA in tests/test_utf8_rule.py).
+// All masks below carry one flag per byte in bit 7 (0x80 lanes of a u32).
+// ---------------------------------------------------------------------------
+WS_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_alignbyte(hi, lo, s);
+#else
+  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * (s & 3u)));
+#endif
+}
+
+// The 4 bytes at byte offset off (0..16) of the 20-byte window w0..w4 (little
+// endian): word selects + one funnel shift, no indexed array (a device-side
+// indexed array would live in scratch).
+WS_HD uint32_t bytes_at(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, uint32_t off) {
+  const uint32_t q = off >> 2;
+  const uint32_t lo = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : (q == 3 ? w3 : w4)));
+  const uint32_t hi = q == 0 ? w1 : (q == 1 ? w2 : (q == 2 ? w3 : w4));
+  return alignbyte(hi, lo, off & 3u);
+}
+
+WS_HD uint32_t bswap32(uint32_t v) {
+  return (v >> 24) | ((v >> 8) & 0xff00u) | ((v << 8) & 0xff0000u) | (v << 24);
+}
+
+// RFC 6455 header from the first 20 wire bytes of a frame (w0..w4, zero past the
+// data); n = bytes available.  FrameDecoder.java:189-262 header reads.
+WS_HD bool parse_header_words(uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, uint32_t w4, uint64_t n,
+                              Header& o) {
   if (n < 2) return false;
-  uint32_t b0 = h[0], b1 = h[1];
+  const uint32_t b0 = w0 & 0xffu, b1 = (w0 >> 8) & 0xffu;
   o.opcode = b0 & 0x0fu;
   o.fin = b0 >> 7;
   o.rsv = (b0 >> 4) & 7u;
   o.masked = b1 >> 7;
   o.len7 = b1 & 0x7fu;
-  uint32_t ext = o.len7 == 126 ? 2u : (o.len7 == 127 ? 8u : 0u);
+  const uint32_t ext = o.len7 == 126 ? 2u : (o.len7 == 127 ? 8u : 0u);
   o.hdr_len = 2u + ext + (o.masked ? 4u : 0u);
   if (n < o.hdr_len) return false;
   if (ext == 0) {
     o.plen = o.len7;
   } else if (ext == 2) {
-    o.plen = ((uint64_t)h[2] << 8) | h[3];
-  } else {
-    uint64_t v = 0;
-    for (int i = 0; i < 8; ++i) v = (v << 8) | h[2 + i];
-    o.plen = v;
+    o.plen = ((w0 >> 8) & 0xff00u) | (w0 >> 24);  // bytes 2, 3 big-endian
+  } else {                                         // bytes 2..9 big-endian
+    o.plen = ((uint64_t)bswap32(alignbyte(w1, w0, 2)) << 32) | bswap32(alignbyte(w2, w1, 2));
   }
-  if (o.masked) {
-    const uint8_t* m = h + 2 + ext;
-    o.mask = (uint32_t)m[0] | ((uint32_t)m[1] << 8) | ((uint32_t)m[2] << 16) | ((uint32_t)m[3] << 24);
-  } else {
-    o.mask = 0;
-  }
+  o.mask = o.masked ? bytes_at(w0, w1, w2, w3, w4, 2u + ext) : 0u;
   return true;
+}
+
+WS_HD bool parse_header(const uint8_t* h, uint64_t n, Header& o) {
+  uint32_t w[5] = {0u, 0u, 0u, 0u, 0u};
+  for (int i = 0; i < 20 && (uint64_t)i < n; ++i) w[i >> 2] |= (uint32_t)h[i] << (8 * (i & 3));
+  return parse_header_words(w[0], w[1], w[2], w[3], w[4], n, o);
 }
 
 // The header checks of FrameDecoder.decode that run before the fragmentation
@@ -105,21 +137,6 @@ WS_HD uint16_t close_code_of(uint32_t err) {
   return (err == WSG_E_CLOSE_REASON || err == WSG_E_TEXT_UTF8) ? WSG_CLOSE_NON_UTF8 : WSG_CLOSE_PROTOCOL_ERROR;
 }
 
-// ---------------------------------------------------------------------------
-// UTF-8.  The Hoehrmann DFA (Utf8.java) rejects at byte p exactly when, with
-// the bytes before p a valid prefix, byte p is not allowed after the last <=3
-// bytes.  That condition needs only the 3 preceding bytes, so every byte can be
-// checked independently; the first flagged byte is the DFA's REJECT byte
-// (proved exhaustively against the DFA in tests/test_utf8_rule.py).
-// All masks below carry one flag per byte in bit 7 (0x80 lanes of a u32).
-// ---------------------------------------------------------------------------
-WS_HD uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  return __builtin_amdgcn_alignbyte(hi, lo, s);
-#else
-  return (uint32_t)((((uint64_t)hi << 32) | lo) >> (8u * (s & 3u)));
-#endif
-}
 
 constexpr uint32_t H80 = 0x80808080u;
 

@@ -309,3 +309,30 @@ def test_host_async_matches_sync(ctx, oracle):
     for (gp, gd, gr), (wp, wd, wr), (w, o, f) in zip(got, want, batches):
         assert np.array_equal(gr, wr) and np.array_equal(gd, wd)
         compare((gp, gd, gr), (wp, wd, wr), f, "async")
+
+
+@pytest.mark.parametrize("empties", [0, 70, 300])
+def test_dense_small_frames(ctx, oracle, empties):
+    """Pieces holding many frames: tiny text/binary frames (the lane-parallel frame
+    lookup of the multi-frame piece path) and runs of zero-length frames longer
+    than a wave (its walking fallback), with UTF-8 split across tiny fragments."""
+    rng = np.random.default_rng(500 + empties)
+    sessions = []
+    for s in range(24):
+        fr = []
+        for m in range(int(rng.integers(20, 60))):
+            if rng.random() < 0.5:
+                body = wsgen.rand_text(rng, int(rng.integers(0, 12)))
+                pts = wsgen.split_points(rng, len(body), int(rng.integers(1, 4)))
+                for i in range(len(pts) - 1):
+                    fr.append(wsgen.build_frame(1 if i == 0 else 0, i == len(pts) - 2, 0, body[pts[i]:pts[i + 1]], True,
+                                                tuple(int(x) for x in rng.integers(0, 256, 4))))
+            else:
+                fr.append(wsgen.build_frame(2, True, 0, rng.integers(0, 256, int(rng.integers(0, 40)),
+                                                                       dtype=np.uint8).tobytes(), True, (9, 8, 7, 6)))
+            if empties and rng.random() < 0.05:
+                fr.extend(wsgen.build_frame(9, True, 0, b"", True, (1, 1, 1, 1)) for _ in range(empties))
+        if s % 5 == 0:
+            fr.insert(len(fr) // 2, wsgen.bad_frame(rng, "utf8", True, 65536))
+        sessions.append(fr)
+    run_parity(ctx, oracle, sessions, rng=rng, n_batches=2, tag=f"dense {empties}")
