@@ -69,6 +69,14 @@ except ImportError:  # pragma: no cover
 
 
 def _load():
+    # torch (when installed) bundles its own libamdhip64.so.7, the soname libwsgpu.so
+    # links against: load torch first so the process has ONE HIP runtime (torch's) and
+    # device pointers / streams pass between them; loaded the other way round, torch
+    # would bind to the system runtime and fail to initialise.
+    try:
+        import torch  # noqa: F401
+    except ImportError:  # pragma: no cover  (a JNI/ctypes host without torch uses the system runtime)
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libwsgpu.so not built ({LIB_PATH}); run snf4j_amd.build.build() — "
                           "the HIP extension is required, there is no CPU fallback")

@@ -514,14 +514,6 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
   return f0 | f1 | f2 | f3;
 }
 
-// Workgroups are dealt round-robin to the 8 XCDs (blocks b and b+8 share one);
-// give each XCD a contiguous run of pieces so the source lines two neighbouring
-// pieces share (funnel block, UTF-8 carry word) meet in the same L2.  Bijective
-// for any grid (cdna_hip_programming.md §5.5 T1).
-__device__ __forceinline__ uint32_t xcd_remap(uint32_t b, uint32_t n) {
-  const uint32_t q = n / 8u, r = n % 8u, x = b % 8u, i = b / 8u;
-  return (x < r ? x * (q + 1u) : r * (q + 1u) + (x - r) * q) + i;
-}
 
 // General path: the piece spans several frame slots (small frames).  Each lane
 // finds the frame owning its 16 output bytes by walking the records from the

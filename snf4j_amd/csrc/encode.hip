@@ -349,7 +349,7 @@ __device__ __forceinline__ void enc_fastN(const EncodeArgs& a, const PieceDesc d
 template <int N>
 __global__ __launch_bounds__(64) void k_enc_piecesN(EncodeArgs a) {
   const int lane = threadIdx.x;
-  const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(blockIdx.x);
+  const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, gridDim.x));
   PieceDesc d[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) d[i] = a.pieces[p + i];

@@ -41,7 +41,7 @@ __host__ __device__ inline bool code_is_start(uint32_t c) {
 constexpr int BLOCK = 256;  // frames per block in the parse / link passes
 constexpr uint32_t PIECE = 1024;  // payload-output bytes per wave in k_pieces (64 lanes x 16 B)
 constexpr int PIECES_PER_WAVE = 2; // pieces one k_piecesN wave takes (tools/ubench_unmask)
-constexpr int ENC_PIECES_PER_WAVE = 1;  // k_enc_piecesN: 2 per wave measured slower (62.9% vs 71.6% of HBM)
+constexpr int ENC_PIECES_PER_WAVE = 2;  // k_enc_piecesN (1 and 2 within 1% once no array is promoted to LDS)
 
 // Pieces needed for a batch, bounded from host-known sizes: the 16-B aligned
 // payload slots total sum(align16(len)) <= wire_len - 2F + 15F.
