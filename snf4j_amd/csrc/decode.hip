@@ -189,6 +189,7 @@ __global__ __launch_bounds__(1024) void k_scan(DecodeArgs a) {
 // ------------------------------------------------------------------ k_link
 __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const bool live = k < a.n_frames;
   FrameRec r;
   Agg v = AGG_ID;
@@ -198,61 +199,91 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   }
   Agg tot;
   Agg ex = block_excl_scan(v, &tot);
-  if (!live) return;
-  Agg bp;
-  bp.sum = a.blk_sum[blockIdx.x];
-  bp.m0 = a.blk_max[blockIdx.x];
-  bp.m1 = a.blk_max[a.nblk + blockIdx.x];
-  bp.m2 = a.blk_max[2 * a.nblk + blockIdx.x];
-  ex = agg_op(bp, ex);
-  const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
-  a.prev[k] = jd;
-  a.prev[a.n_frames + k] = jm;
-  a.prev[2 * a.n_frames + k] = ex.m2 >> 1;
-
-  const uint32_t s = r.sess;
-  const int32_t sf = (int32_t)a.session_first[s];
-  const wsg_session_state st = a.state[s];
-  const uint32_t op = code_op(r.code);
   uint32_t extra = 0;
-  if (!code_pre(r.code)) {
-    // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
-    const bool frag = jd >= sf ? !(ex.m0 & 1) : (st.fragmentation != 0);
-    extra |= rules_frag(op, frag) << CODE_FRAG_SHIFT;
-    if (a.validate) {
-      bool text = op == WSG_OP_TEXT;
-      if (op == WSG_OP_CONTINUATION) text = jm >= sf ? (ex.m1 & 1) != 0 : (st.text_open != 0);
-      if (text) extra |= CODE_VALIDATE;
+  if (live) {
+    Agg bp;
+    bp.sum = a.blk_sum[blockIdx.x];
+    bp.m0 = a.blk_max[blockIdx.x];
+    bp.m1 = a.blk_max[a.nblk + blockIdx.x];
+    bp.m2 = a.blk_max[2 * a.nblk + blockIdx.x];
+    ex = agg_op(bp, ex);
+    const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
+    a.prev[k] = jd;
+    a.prev[a.n_frames + k] = jm;
+    a.prev[2 * a.n_frames + k] = ex.m2 >> 1;
+    const uint32_t s = r.sess;
+    const int32_t sf = (int32_t)a.session_first[s];
+    const wsg_session_state st = a.state[s];
+    const uint32_t op = code_op(r.code);
+    if (!code_pre(r.code)) {
+      // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
+      const bool frag = jd >= sf ? !(ex.m0 & 1) : (st.fragmentation != 0);
+      extra |= rules_frag(op, frag) << CODE_FRAG_SHIFT;
+      if (a.validate) {
+        bool text = op == WSG_OP_TEXT;
+        if (op == WSG_OP_CONTINUATION) text = jm >= sf ? (ex.m1 & 1) != 0 : (st.text_open != 0);
+        if (text) extra |= CODE_VALIDATE;
+      }
     }
+    a.rec[k].out_off = ex.sum;
+    a.rec[k].code = r.code | extra;
+    wsg_frame_desc d;
+    d.payload_off = ex.sum;
+    d.payload_len = r.len;
+    d.opcode = (uint8_t)op;
+    d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
+                        ((r.code & CODE_MASKED) ? 1u : 0u));
+    d.status = 0;
+    a.desc[k] = d;
   }
-  a.rec[k].out_off = ex.sum;
-  a.rec[k].code = r.code | extra;
-  // descriptors of the pieces whose first output byte falls in this frame's slot
-  const uint64_t slot = (uint64_t)((r.len + 15u) & ~15u);
-  if (slot) {
-    const uint64_t total = *a.total, slot_end = ex.sum + slot;
-    const uint64_t flags = ((extra & CODE_VALIDATE) ? PD_VALIDATE : 0ull);
-    for (uint64_t pc = (ex.sum + PIECE - 1) / PIECE; pc * PIECE < slot_end; ++pc) {
-      const uint64_t ps = pc * PIECE;
-      const uint32_t j0 = (uint32_t)(ps - ex.sum);
-      const uint32_t left = r.len - j0;
-      const bool single = slot_end >= ps + PIECE || slot_end == total;
-      PieceDesc d;
-      d.info = ((r.src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) | flags |
-               (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI);
-      d.mask = r.mask;
-      d.frame = (uint32_t)k;
-      a.pieces[pc] = d;
-    }
+  // Descriptors of the pieces whose first output byte falls in a frame's slot,
+  // written cooperatively: the wave's pieces are contiguous, lane i writes the
+  // wave's pieces i, i+64, ... (coalesced 16-B stores) after finding the owning
+  // frame with a shuffle search over the exclusive piece counts.
+  const uint64_t slot = live ? (uint64_t)((r.len + 15u) & ~15u) : 0ull;
+  const uint64_t slot_end = ex.sum + slot;
+  const uint32_t pc0 = (uint32_t)((ex.sum + PIECE - 1) / PIECE);
+  const uint32_t cnt = slot ? (uint32_t)((slot_end + PIECE - 1) / PIECE) - pc0 : 0u;
+  uint32_t cum = cnt;  // inclusive wave scan of the counts
+#pragma unroll
+  for (int sd = 1; sd < 64; sd <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)cum, sd, 64);
+    if (lane >= sd) cum += t;
   }
-  wsg_frame_desc d;
-  d.payload_off = ex.sum;
-  d.payload_len = r.len;
-  d.opcode = (uint8_t)op;
-  d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
-                      ((r.code & CODE_MASKED) ? 1u : 0u));
-  d.status = 0;
-  a.desc[k] = d;
+  const uint32_t T = (uint32_t)__shfl((int)cum, 63, 64);
+  cum -= cnt;  // exclusive
+  if (!T) return;
+  const uint64_t total = *a.total;
+  // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31
+  const uint32_t fk = (uint32_t)k | ((extra & CODE_VALIDATE) ? 0x80000000u : 0u);
+  for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
+    int o = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+      if ((uint32_t)__shfl((int)cum, o + step, 64) <= t) o += step;
+    const uint32_t o_cum = (uint32_t)__shfl((int)cum, o, 64);
+    const uint32_t o_pc0 = (uint32_t)__shfl((int)pc0, o, 64);
+    const uint64_t o_out = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex.sum >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)ex.sum, o, 64);
+    const uint64_t o_src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(r.src >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)r.src, o, 64);
+    const uint32_t o_len = (uint32_t)__shfl((int)(live ? r.len : 0u), o, 64);
+    const uint32_t o_mask = (uint32_t)__shfl((int)(live ? r.mask : 0u), o, 64);
+    const uint32_t o_fk = (uint32_t)__shfl((int)fk, o, 64);
+    if (t >= T) continue;
+    const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
+    const uint64_t ps = pc * PIECE;
+    const uint64_t o_end = o_out + ((o_len + 15u) & ~15u);
+    const uint32_t j0 = (uint32_t)(ps - o_out);
+    const uint32_t left = o_len - j0;
+    const bool single = o_end >= ps + PIECE || o_end == total;
+    PieceDesc d;
+    d.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) |
+             ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI);
+    d.mask = o_mask;
+    d.frame = o_fk & 0x7fffffffu;
+    a.pieces[pc] = d;
+  }
 }
 
 // ------------------------------------------------------------------ k_unmask

@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
   std::vector<V> vs = {
       {"copy16 g=8192", 0, 8192}, {"pieces nt W1", 13, 0}, {"pieces nt W1 xcd", 14, 0},
       {"piecesN2 xcd", 18, 0}, {"piecesN4 xcd", 19, 0}, {"piecesN3 xcd", 24, 0}, {"piecesN4", 25, 0},
-      {"parse", 20, 0}, {"scan", 23, 0}, {"link", 21, 0}, {"merge", 22, 0},  // pipeline order: scan is in place
+      {"parse", 20, 0}, {"scan", 23, 0}, {"link", 21, 0}, {"merge", 22, 0},  // pipeline order
   };
   std::vector<double> best(vs.size(), 1e30), sum(vs.size(), 0);
   const int rounds = 8;
