@@ -156,7 +156,9 @@ const char* wsg_last_error(wsg_ctx* ctx);
 int wsg_reserve(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len);
 int wsg_sync(wsg_ctx* ctx);
 
-/* Kernel timing (hipEvents recorded around each kernel on the ctx stream). */
+/* Kernel timing (hipEvents recorded around each kernel on the ctx stream).
+ * enable: 0 off, 1 every kernel, 2 only the streaming kernels (k_piecesN,
+ * k_enc_piecesN) — each event pair adds queue time, so a timed step uses 2. */
 int wsg_set_timing(wsg_ctx* ctx, int enable);
 /* out_ms[i] = accumulated milliseconds of kernel i since the last reset, out_count[i] = launches.
  * Kernel ids: see wsg_kernel_name(). Syncs the stream. */

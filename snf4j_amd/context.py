@@ -105,8 +105,10 @@ class Context:
     def reserve(self, max_frames: int, max_sessions: int, max_wire_len: int = 0):
         check(lib.wsg_reserve(self._h, int(max_frames), int(max_sessions), int(max_wire_len)), self._h)
 
-    def set_timing(self, on: bool = True):
-        check(lib.wsg_set_timing(self._h, int(on)), self._h)
+    def set_timing(self, on=True):
+        """True: time every kernel; "hot": only the streaming kernels (an event pair
+        costs queue time, so timed steps bracket only the kernel the roofline needs)."""
+        check(lib.wsg_set_timing(self._h, 2 if on == "hot" else int(bool(on))), self._h)
 
     def reset_timing(self):
         check(lib.wsg_reset_timing(self._h), self._h)

@@ -15,7 +15,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_synth"};
+                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -61,7 +61,7 @@ struct wsg_ctx {
   // decode workspace
   DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total, pieces, utf8_err;
   // encode workspace
-  DevBuf esess, elast_close, epieces;
+  DevBuf esess, elast_close, epieces, epidx;
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -70,7 +70,7 @@ struct wsg_ctx {
   int next_slot = 0;
   hipEvent_t ev_prev_state = nullptr;  // state download of the previous async batch
   // timing
-  bool timing = false;
+  int timing = 0;  // 0 off, 1 every kernel, 2 the streaming kernels only (WSG_TIMING_*)
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> free_events;
   double ms[K_COUNT] = {};
@@ -122,7 +122,9 @@ static void drain_timing(wsg_ctx* c) {
 
 template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
-  if (!c->timing) {
+  // an event pair costs a few microseconds of queue time: mode 2 brackets only the
+  // streaming kernels, so a timed step keeps the side kernels back to back
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT)) {
     f();
     return;
   }
@@ -173,7 +175,7 @@ int wsg_close(wsg_ctx* c) {
   drain_timing(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->rec,     &c->prev,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
-                    &c->total,   &c->pieces, &c->utf8_err, &c->esess,   &c->elast_close, &c->epieces, &c->h_wire, &c->h_off,    &c->h_sf,
+                    &c->total,   &c->pieces, &c->utf8_err, &c->esess,   &c->elast_close, &c->epieces, &c->epidx, &c->h_wire, &c->h_off,    &c->h_sf,
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
@@ -214,7 +216,7 @@ int wsg_sync(wsg_ctx* c) {
 
 int wsg_set_timing(wsg_ctx* c, int enable) {
   if (!c) return WSG_API_EINVAL;
-  c->timing = enable != 0;
+  c->timing = enable == 2 ? 2 : (enable != 0 ? 1 : 0);
   return WSG_API_OK;
 }
 
@@ -553,11 +555,17 @@ int wsg_encode_batch_device(wsg_ctx* c, int client_mode, const uint8_t* payload,
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
   // pieces of wire_out: bounded by the caller's capacity (the total is only known on the device)
   a.n_pieces = wire_cap / PIECE + 1;
-  if (n_frames) HIP_TRY(c, c->epieces.ensure((a.n_pieces + PIECES_PER_WAVE) * sizeof(PieceDesc)));
+  a.n_idx = a.n_pieces / 64 + 2;
+  if (n_frames) {
+    HIP_TRY(c, c->epieces.ensure((a.n_pieces + PIECES_PER_WAVE) * sizeof(PieceDesc)));
+    HIP_TRY(c, c->epidx.ensure(a.n_idx * sizeof(uint32_t)));
+  }
   a.pieces = (PieceDesc*)c->epieces.p;
+  a.pidx = (uint32_t*)c->epidx.p;
   if (n_frames) {
     timed(c, K_ENC_LEN, [&] { launch_enc_len(a, c->stream); });
     timed(c, K_ENC_SCAN, [&] { launch_enc_scan(a, c->stream); });
+    timed(c, K_ENC_DESC, [&] { launch_enc_desc(a, c->stream); });
     timed(c, K_ENC_EMIT, [&] { launch_enc_pieces(a, c->stream); });
     timed(c, K_ENC_FINAL, [&] { launch_enc_final(a, c->stream); });
   } else {

@@ -9,12 +9,13 @@
 //   k_link    thread per frame: payload slot offset, the fragmentation rule
 //             (:229-236) from the previous data frame's FIN, text-message
 //             membership for the validator (FrameUtf8Validator.java:59-70).
-//   k_unmask  one wave per frame: coalesced 16-B loads, 4-byte XOR unmask
-//             (:268-273), 16-B stores into the frame's aligned slot, per-lane
-//             SWAR UTF-8 rule with the 3-byte carry taken from the neighbour
-//             lane (DPP/bpermute) and the verdict folded by wavefront ballot;
-//             the fragment-boundary bytes are checked against the carry of the
-//             previous fragments; the first failing frame per session via atomicMin.
+//   k_piecesN one wave per 2 KiB of payload output: coalesced 16-B loads, 4-byte
+//             XOR unmask (:268-273), aligned 16-B stores into the frame slots,
+//             per-lane SWAR UTF-8 rule with the 3-byte carry taken from the
+//             neighbour lane (DPP) and the verdict folded by wavefront ballot.
+//   k_merge   thread per frame: status in the reference's check order, the
+//             fragment-seam UTF-8 bytes against the message carry, wsg_frame_desc,
+//             the first failing frame per session (atomicMin).
 //   k_final   thread per session: wsg_session_result + carry-out state.
 #include "wsgpu_internal.h"
 #include "wsgpu_scan.h"
@@ -99,7 +100,10 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
           const uint32_t nf = len < 3 ? len : 3;
           const uint32_t keep3 = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : (nf == 1 ? 0xffu : 0u));
           const uint32_t f3 = (bytes_at(w0, w1, w2, w3, w4, hd.hdr_len) ^ hd.mask) & keep3;
-          if (nf) {  // last 3 payload bytes: two aligned dwords
+          // last 3 payload bytes: only a non-FIN fragment's are needed (the carry into the
+          // next fragment or batch); a frame's own last-byte and end-of-message tests
+          // run in k_pieces on bytes it holds, so a FIN frame costs no second line here
+          if (nf && !hd.fin) {
             const uint64_t e3 = src + len - nf;  // first of the last nf bytes
             const uint64_t q = e3 & ~3ull;
             uint32_t lo, hi;
@@ -226,15 +230,7 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
       }
     }
     a.rec[k].out_off = ex.sum;
-    a.rec[k].code = r.code | extra;
-    wsg_frame_desc d;
-    d.payload_off = ex.sum;
-    d.payload_len = r.len;
-    d.opcode = (uint8_t)op;
-    d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
-                        ((r.code & CODE_MASKED) ? 1u : 0u));
-    d.status = 0;
-    a.desc[k] = d;
+    a.rec[k].code = r.code | extra;  // (wsg_frame_desc is written whole by k_merge)
   }
   // Descriptors of the pieces whose first output byte falls in a frame's slot,
   // written cooperatively: the wave's pieces are contiguous, lane i writes the
@@ -255,7 +251,8 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   if (!T) return;
   const uint64_t total = *a.total;
   // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31
-  const uint32_t fk = (uint32_t)k | ((extra & CODE_VALIDATE) ? 0x80000000u : 0u);
+  const uint32_t fk = (uint32_t)k | ((extra & CODE_VALIDATE) ? 0x80000000u : 0u) |
+                     ((live && (r.code & CODE_FIN)) ? 0x40000000u : 0u);
   for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
     int o = 0;
 #pragma unroll
@@ -279,14 +276,15 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
     const bool single = o_end >= ps + PIECE || o_end == total;
     PieceDesc d;
     d.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) |
-             ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI);
+             ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI) |
+             (left <= PIECE ? PD_LAST : 0ull) | ((o_fk & 0x40000000u) ? PD_FIN : 0ull);
     d.mask = o_mask;
-    d.frame = o_fk & 0x7fffffffu;
+    d.frame = o_fk & 0x3fffffffu;
     a.pieces[pc] = d;
   }
 }
 
-// ------------------------------------------------------------------ k_unmask
+// ------------------------------------------------------------------ UTF-8 seams
 // Carry bytes of the text message before frame k (<= 3, oldest first).
 __device__ uint32_t message_carry(const DecodeArgs& a, uint64_t k, uint32_t op, uint32_t sess, uint8_t c[3]) {
   if (op != WSG_OP_CONTINUATION) return 0;  // a TEXT frame starts its message
@@ -319,126 +317,20 @@ __device__ bool edge_utf8_error(const DecodeArgs& a, uint64_t k, const FrameRec&
   const uint32_t op = code_op(r.code);
   uint32_t n = message_carry(a, k, op, r.sess, s);
   const uint32_t nc = n;
-  const uint32_t f3 = a.edge[k], l3 = a.edge[a.n_frames + k];
+  const uint32_t f3 = a.edge[k];
   const uint32_t nh = r.len < 3 ? r.len : 3;
   for (uint32_t i = 0; i < nh; ++i) s[n++] = (uint8_t)(f3 >> (8 * i));
   for (uint32_t i = nc; i < n; ++i) {
     const uint32_t p1 = i >= 1 ? s[i - 1] : 0, p2 = i >= 2 ? s[i - 2] : 0, p3 = i >= 3 ? s[i - 3] : 0;
     if (utf8_err_byte(p3, p2, p1, s[i])) return true;
   }
-  // k_pieces' pair rule flags a lone invalid lead one byte late: test the last byte here
-  if (r.len && utf8_bad_last((l3 >> 16) & 0xffu)) return true;
-  if (r.code & CODE_FIN) {
-    uint32_t t1, t2, t3;
-    if (r.len >= 3) {
-      t1 = (l3 >> 16) & 0xffu; t2 = (l3 >> 8) & 0xffu; t3 = l3 & 0xffu;
-    } else {
-      t1 = n >= 1 ? s[n - 1] : 0; t2 = n >= 2 ? s[n - 2] : 0; t3 = n >= 3 ? s[n - 3] : 0;
-    }
+  // the frame's last byte, and the end of a FIN message of >= 3 bytes in this frame,
+  // are tested by k_pieces (tail_error); a shorter FIN frame ends on the carry
+  if ((r.code & CODE_FIN) && r.len < 3) {
+    const uint32_t t1 = n >= 1 ? s[n - 1] : 0, t2 = n >= 2 ? s[n - 2] : 0, t3 = n >= 3 ? s[n - 3] : 0;
     if (utf8_incomplete(t3, t2, t1)) return true;
   }
   return false;
-}
-
-template <int U>
-__global__ __launch_bounds__(256) void k_unmask(DecodeArgs a) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t wave0 = __builtin_amdgcn_readfirstlane(blockIdx.x * 4u + (threadIdx.x >> 6));
-  const uint32_t nw = gridDim.x * 4u;
-  const FrameRec* __restrict__ recs = a.rec;
-  for (uint64_t k = wave0; k < a.n_frames; k += nw) {
-    const FrameRec r = recs[k];
-    const uint32_t pre = code_pre(r.code), post = code_post(r.code), frag = code_frag(r.code);
-    uint32_t status = pre ? pre : (frag ? frag : post);
-    if (status == 0) {
-      const bool validate = (r.code & CODE_VALIDATE) != 0;
-      uint32_t errf = 0;
-      if (r.len) {
-        const uint64_t a4 = r.src & ~3ull;
-        const uint32_t sh = (uint32_t)r.src & 3u;
-        const uint64_t avail = a.wire_len - a4;
-        const __amdgpu_buffer_rsrc_t rin = __builtin_amdgcn_make_buffer_rsrc(
-            (void*)(a.wire + a4), 0, (int)(avail > 0x7fffffffull ? 0x7fffffffull : avail), 0x00020000);
-        const uint32_t slot = (r.len + 15u) & ~15u;
-        const __amdgpu_buffer_rsrc_t rout =
-            __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload_out + r.out_off), 0, (int)slot, 0x00020000);
-        const uint32_t m = r.mask;
-        const uint32_t nch = (r.len + 15u) >> 4;
-        const uint32_t rem = r.len & 15u;
-        uint32_t carry = 0;
-        for (uint32_t c0 = 0; c0 < nch; c0 += 64u * U) {
-          u32x4 q[U];
-          uint32_t t[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + u * 64u + lane;
-            if (c < nch && (uint64_t)c * 16u + 20u <= avail) {
-              q[u] = __builtin_amdgcn_raw_buffer_load_b128(rin, c * 16u, 0, 0);
-              t[u] = __builtin_amdgcn_raw_buffer_load_b32(rin, c * 16u + 16u, 0, 0);
-            } else if (c < nch) {  // the last bytes of the wire: byte loads (the range check is per dword)
-              uint32_t d[5] = {0u, 0u, 0u, 0u, 0u};
-              for (uint32_t i = 0; i < 20u && (uint64_t)c * 16u + i < avail; ++i)
-                d[i >> 2] |= (uint32_t)a.wire[a4 + c * 16u + i] << (8 * (i & 3));
-              q[u] = (u32x4){d[0], d[1], d[2], d[3]};
-              t[u] = d[4];
-            } else {
-              q[u] = (u32x4){0u, 0u, 0u, 0u};
-              t[u] = 0u;
-            }
-          }
-          uint32_t w[U][4];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const uint32_t c = c0 + u * 64u + lane;
-            w[u][0] = alignbyte(q[u].y, q[u].x, sh) ^ m;
-            w[u][1] = alignbyte(q[u].z, q[u].y, sh) ^ m;
-            w[u][2] = alignbyte(q[u].w, q[u].z, sh) ^ m;
-            w[u][3] = alignbyte(t[u], q[u].w, sh) ^ m;
-            if (c + 1 == nch && rem) {  // zero the slot padding past the payload
-#pragma unroll
-              for (int i = 0; i < 4; ++i) {
-                const int keep = (int)rem - 4 * i;
-                w[u][i] = keep >= 4 ? w[u][i] : (keep <= 0 ? 0u : (w[u][i] & ((1u << (8 * keep)) - 1u)));
-              }
-            }
-            if (c < nch)
-              __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[u][0], w[u][1], w[u][2], w[u][3]}, rout,
-                                                     c * 16u, 0, 0);
-          }
-          if (validate) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) {
-              const uint32_t c = c0 + u * 64u + lane;
-              uint32_t p = (uint32_t)__shfl_up((int)w[u][3], 1, 64);
-              const uint32_t from_prev = u == 0 ? carry : (uint32_t)__builtin_amdgcn_readlane((int)w[u - 1][3], 63);
-              if (lane == 0) p = from_prev;
-              uint32_t e0 = utf8_err_word(w[u][0], p);
-              uint32_t e1 = utf8_err_word(w[u][1], w[u][0]);
-              uint32_t e2 = utf8_err_word(w[u][2], w[u][1]);
-              uint32_t e3 = utf8_err_word(w[u][3], w[u][2]);
-              if (c == 0) e0 &= 0x80000000u;  // bytes 0..2 are checked against the fragment carry
-              if (c + 1 == nch && rem) {
-                const uint32_t keep[4] = {rem >= 4 ? 0x80808080u : (0x80808080u >> (8 * (4 - rem))),
-                                          rem >= 8 ? 0x80808080u : (rem <= 4 ? 0u : (0x80808080u >> (8 * (8 - rem)))),
-                                          rem >= 12 ? 0x80808080u : (rem <= 8 ? 0u : (0x80808080u >> (8 * (12 - rem)))),
-                                          rem <= 12 ? 0u : (0x80808080u >> (8 * (16 - rem)))};
-                e0 &= keep[0]; e1 &= keep[1]; e2 &= keep[2]; e3 &= keep[3];
-              }
-              if (c < nch) errf |= e0 | e1 | e2 | e3;
-            }
-            carry = (uint32_t)__builtin_amdgcn_readlane((int)w[U - 1][3], 63);
-          }
-        }
-      }
-      bool bad = __any(errf != 0);
-      if (validate && !bad) bad = edge_utf8_error(a, k, r);
-      if (bad) status = WSG_E_TEXT_UTF8;
-    }
-    if (lane == 0) {
-      a.desc[k].status = (uint16_t)status;
-      if (status) atomicMin((unsigned long long*)&a.sess_err[r.sess], (unsigned long long)k);
-    }
-  }
 }
 
 // ------------------------------------------------------------------ k_pieces
@@ -463,6 +355,22 @@ __device__ __forceinline__ uint32_t keep_bytes(uint32_t w, int keep) {
 }
 __device__ __forceinline__ uint32_t keep_flags(int keep) {  // UTF-8 flag mask of the first `keep` bytes
   return keep >= 4 ? 0x80808080u : (keep <= 0 ? 0u : (0x80808080u >> (8 * (4 - keep))));
+}
+
+// The 3 payload bytes before position `keep` (1..16) of a lane's chunk w[0..3],
+// pw = the 4 bytes before the chunk, in the edge layout (oldest byte in bits 0-7).
+// The lane holding a frame's last byte tests them: the SWAR pair rule flags a lone
+// invalid lead one byte late, so the frame's last byte is tested alone, and a FIN
+// frame of >= 3 bytes must not end inside a sequence (FrameUtf8Validator.java:83-96).
+__device__ __forceinline__ bool tail_error(uint32_t l3, bool fin) {
+  return utf8_bad_last((l3 >> 16) & 0xffu) || (fin && utf8_incomplete(l3 & 0xffu, (l3 >> 8) & 0xffu, (l3 >> 16) & 0xffu));
+}
+__device__ __forceinline__ uint32_t last3(uint32_t pw, uint32_t w0, uint32_t w1, uint32_t w2, uint32_t w3, int keep) {
+  const int t = keep + 1;  // window (pw ++ w) index of the first of the 3 bytes
+  const int q = t >> 2;
+  const uint32_t lo = q == 0 ? pw : (q == 1 ? w0 : (q == 2 ? w1 : (q == 3 ? w2 : w3)));
+  const uint32_t hi = q == 0 ? w0 : (q == 1 ? w1 : (q == 2 ? w2 : w3));
+  return alignbyte(hi, lo, (uint32_t)t & 3u) & 0xffffffu;
 }
 
 // 4 source bytes ending right before wire offset `pos`, unmasked (payload phase 0)
@@ -542,7 +450,12 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
   if (!full) {
     f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
   }
-  return f0 | f1 | f2 | f3;
+  uint32_t te = 0;
+  if ((d.info & PD_LAST) && keep >= 1 && keep <= 16) {
+    const bool ge3 = !((d.info & PD_FIRST) && lane == 0 && keep < 3);  // frame length >= 3
+    te = tail_error(last3(pw, w[0], w[1], w[2], w[3], keep), ge3 && (d.info & PD_FIN)) ? 1u : 0u;
+  }
+  return f0 | f1 | f2 | f3 | te;
 }
 
 
@@ -624,7 +537,9 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
       uint32_t e2 = utf8_err_word_fast(w[2], w[1]), e3 = utf8_err_word_fast(w[3], w[2]);
       if (j == 0) e0 &= 0x80000000u;
       e0 &= keep_flags(keep); e1 &= keep_flags(keep - 4); e2 &= keep_flags(keep - 8); e3 &= keep_flags(keep - 12);
-      if (e0 | e1 | e2 | e3) atomicOr(&a.utf8_err[lk], 1u);
+      const bool te = keep >= 1 && keep <= 16 &&
+                      tail_error(last3(pw, w[0], w[1], w[2], w[3], keep), j + keep >= 3 && (lr.code & CODE_FIN));
+      if (e0 | e1 | e2 | e3 | (te ? 1u : 0u)) atomicOr(&a.utf8_err[lk], 1u);
     }
   }
 }
@@ -667,8 +582,9 @@ __device__ __forceinline__ void funnel16(uint32_t sh, uint32_t W0, uint32_t W1, 
 // is lane 0's block of piece i+1 (readlane), the last piece's block 64 is one
 // extra load, and the UTF-8 carry of piece i+1 is lane 63's last word of piece i.
 template <int NT, int N>
-__device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const PieceDesc d, const uint32_t nb_last,
+__device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const PieceDesc d, const uint64_t info_last,
                                                 uint64_t pstart, int lane) {
+  const uint32_t nb_last = (uint32_t)(info_last >> PD_NB_SHIFT) & 2047u;
   const uint32_t aux = NT ? 2 : 0;
   const uint64_t s = d.info & PD_SRC_MASK;
   const uint64_t a16 = s & ~15ull;
@@ -743,6 +659,11 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
     if (i + 1 == N && !full) {
       f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
     }
+    if (i + 1 == N && (info_last & PD_LAST) && keep >= 1 && keep <= 16) {
+      // (a frame of N > 1 pieces has >= 3 bytes; with N == 1 the piece may start it)
+      const bool ge3 = N > 1 || !((d.info & PD_FIRST) && lane == 0 && keep < 3);
+      if (tail_error(last3(pw, w[i][0], w[i][1], w[i][2], w[i][3], keep), ge3 && (info_last & PD_FIN))) err |= 1u;
+    }
     err |= f0 | f1 | f2 | f3;
     if (i + 1 < N) carry = (uint32_t)__builtin_amdgcn_readlane((int)w[i][3], 63);
   }
@@ -767,8 +688,7 @@ __global__ __launch_bounds__(64) void k_piecesN(DecodeArgs a) {
 #pragma unroll
   for (int i = 0; i < N; ++i) fast = fast && !(d[i].info & PD_MULTI);
   if (fast) {
-    const uint32_t nb_last = (uint32_t)(d[N - 1].info >> PD_NB_SHIFT) & 2047u;
-    const uint32_t err = piece_fastN<NT, N>(a, d[0], nb_last, pstart, lane);
+    const uint32_t err = piece_fastN<NT, N>(a, d[0], d[N - 1].info, pstart, lane);
     if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d[0].frame], 1u);
     return;
   }
@@ -798,7 +718,14 @@ __global__ __launch_bounds__(256) void k_merge(DecodeArgs a) {
   const uint32_t ue = a.utf8_err[k];
   if (ue) a.utf8_err[k] = 0u;  // back to the idle state for the next batch
   if (!status && (r.code & CODE_VALIDATE) && (ue || edge_utf8_error(a, k, r))) status = WSG_E_TEXT_UTF8;
-  a.desc[k].status = (uint16_t)status;
+  wsg_frame_desc d;
+  d.payload_off = r.out_off;
+  d.payload_len = r.len;
+  d.opcode = (uint8_t)code_op(r.code);
+  d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
+                      ((r.code & CODE_MASKED) ? 1u : 0u));
+  d.status = (uint16_t)status;
+  a.desc[k] = d;
   if (status) atomicMin((unsigned long long*)&a.sess_err[r.sess], (unsigned long long)k);
 }
 
@@ -891,9 +818,6 @@ void launch_scan(const DecodeArgs& a, hipStream_t s) {
 }
 void launch_link(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(BLOCK), 0, s, a);
-}
-void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid) {
-  hipLaunchKernelGGL(k_unmask<4>, dim3(grid), dim3(256), 0, s, a);
 }
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
   // one 64-lane workgroup per two pieces, nontemporal loads/stores, XCD-aware

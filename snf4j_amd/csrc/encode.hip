@@ -1,12 +1,15 @@
 // encode.hip — the frame encode pipeline on gfx950 (FrameEncoder, FrameEncoder.java:69-135).
 //
-//   k_enc_len   thread per frame: wire length (FrameEncoder.length, :122-135),
-//               the close latch (:71-76: frames after a CLOSE of the same session,
-//               or of an already closed encoder, are dropped); block aggregates.
+//   k_enc_len   thread per frame: session, CLOSE positions (block max).
 //   k_enc_scan  one workgroup: exclusive scan of the block aggregates.
-//   k_enc_link  thread per frame: wire offset of each frame (prefix sum).
-//   k_enc_fix   final wire offsets + one descriptor per 1 KiB piece of wire_out.
-//   k_enc_piecesN one wave per 1 KiB of wire_out: header bytes (:80-106) and the
+//   k_enc_kept  thread per frame: the close latch (:71-76: frames after a CLOSE of
+//               the same session, or of an already closed encoder, are dropped),
+//               kept wire lengths (FrameEncoder.length, :122-135), block sums.
+//   k_enc_scan_sum / k_enc_fix   wire offsets; coarse piece -> frame index.
+//   k_enc_kept2 / k_enc_fix2   small batches: each block reduces the aggregates of
+//               the blocks before it itself (no separate scan launches).
+//   k_enc_desc  thread per 1 KiB piece of wire_out: its frame and descriptor.
+//   k_enc_piecesN one wave per 2 KiB of wire_out: header bytes (:80-106) and the
 //               payload XOR the injected mask key (:107-117), aligned 16-B stores.
 //   k_enc_final thread per session: FrameEncoder.closed carry-out.
 #include "wsgpu_internal.h"
@@ -55,39 +58,31 @@ __global__ __launch_bounds__(1024) void k_enc_scan(EncodeArgs a) {
   }
 }
 
-// Frame lengths are recomputed here with the latch applied: a dropped frame has
-// length 0, so the prefix sum is taken over "kept" lengths.  The first scan
-// (k_enc_len) only located CLOSE frames; kept lengths need the latch first.
-__global__ __launch_bounds__(BLOCK) void k_enc_link(EncodeArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const bool live = k < a.n_frames;
-  Agg v = AGG_ID;
-  int32_t lc = -1;
-  if (live) {
-    v.m0 = (a.frames[k].opcode & 15u) == WSG_OP_CLOSE ? (int32_t)k : -1;
-  }
-  Agg tot;
-  Agg ex = block_excl_scan(v, &tot);
-  if (live) {
-    const int32_t bp = a.blk_max[blockIdx.x];
-    lc = ex.m0 > bp ? ex.m0 : bp;
-    a.last_close[k] = lc;
-  }
-}
-
-// Second length pass: kept lengths with the latch, block sums (reuses blk_sum).
+// Kept lengths with the latch applied (a dropped frame has length 0, so the
+// prefix sum is taken over kept lengths): the last CLOSE before k from the block
+// scan + the scanned block prefix, then a block-local sum (reuses blk_sum).
 __global__ __launch_bounds__(BLOCK) void k_enc_kept(EncodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = k < a.n_frames;
+  wsg_encode_frame f;
   Agg v = AGG_ID;
-  if (k < a.n_frames) {
-    const uint32_t s = a.sess[k];
-    const bool dropped = a.closed[s] || a.last_close[k] >= (int32_t)a.session_first[s];
-    const uint32_t len = a.frames[k].payload_len;
-    v.sum = dropped ? 0ull : (uint64_t)enc_header_len(len, a.client_mode) + len;
+  if (live) {
+    f = a.frames[k];
+    v.m0 = (f.opcode & 15u) == WSG_OP_CLOSE ? (int32_t)k : -1;
   }
   Agg tot;
-  Agg ex = block_excl_scan(v, &tot);
-  if (k < a.n_frames) a.wire_off[k] = ex.sum;  // block-local, fixed up below
+  const Agg ex = block_excl_scan(v, &tot);
+  Agg w = AGG_ID;
+  if (live) {
+    const int32_t bp = a.blk_max[blockIdx.x];
+    const int32_t lc = ex.m0 > bp ? ex.m0 : bp;
+    a.last_close[k] = lc;
+    const uint32_t s = a.sess[k];
+    const bool dropped = a.closed[s] || lc >= (int32_t)a.session_first[s];
+    w.sum = dropped ? 0ull : (uint64_t)enc_header_len(f.payload_len, a.client_mode) + f.payload_len;
+  }
+  const Agg ew = block_excl_scan(w, &tot);
+  if (live) a.wire_off[k] = ew.sum;  // block-local, fixed up by k_enc_fix
   if (threadIdx.x == 0) a.blk_sum[blockIdx.x] = tot.sum;
 }
 
@@ -105,41 +100,126 @@ __global__ __launch_bounds__(1024) void k_enc_scan_sum(EncodeArgs a) {
   if (threadIdx.x == 0) a.wire_off[a.n_frames] = carry.sum;
 }
 
-// Final wire offsets, and the descriptors of the 1 KiB pieces of wire_out whose
-// first byte falls in this frame (k_enc_pieces).  A piece entirely inside the
-// frame's payload (or ending the output there) takes the fast path.
+// Coarse piece index for k_enc_desc: pidx[q] = the frame holding wire byte q * IDX_SPAN
+// (the frame whose extent [wire_off[k], wire_off[k+1]) contains it; dropped frames
+// have an empty extent and hold nothing).
+constexpr uint64_t IDX_SPAN = 64ull * PIECE;
+
+__device__ __forceinline__ void enc_index_frame(const EncodeArgs& a, uint64_t k, uint64_t wo, uint64_t end) {
+  for (uint64_t q = (wo + IDX_SPAN - 1) / IDX_SPAN; q * IDX_SPAN < end && q < a.n_idx; ++q) a.pidx[q] = (uint32_t)k;
+}
+
+// Final wire offsets (block-local prefix + block base) and the coarse index.
 __global__ __launch_bounds__(BLOCK) void k_enc_fix(EncodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   if (k >= a.n_frames) return;
   const uint64_t wo = a.wire_off[k] + a.blk_sum[blockIdx.x];
   a.wire_off[k] = wo;
-  if (!a.pieces) return;
   const uint32_t s = a.sess[k];
   if (a.closed[s] || a.last_close[k] >= (int32_t)a.session_first[s]) return;  // dropped
+  const uint32_t len = a.frames[k].payload_len;
+  enc_index_frame(a, k, wo, wo + enc_header_len(len, a.client_mode) + len);
+}
+
+// Small batches (<= ENC_SMALL_BLOCKS blocks of frames): the scans of the block
+// aggregates are not separate launches — every block reduces the aggregates of
+// the blocks before it itself (<= 256 loads, one per thread) — so the plan is
+// three launches (k_enc_len, k_enc_kept2, k_enc_fix2) instead of six.
+constexpr uint32_t ENC_SMALL_BLOCKS = 256;
+constexpr uint32_t SESS_DROPPED = 0x80000000u;  // sess[k] bit 31: frame dropped by the latch (small path)
+
+__device__ __forceinline__ Agg prefix_of_blocks(const EncodeArgs& a, bool want_sum) {
+  Agg p = AGG_ID, tot;
+  if (threadIdx.x < blockIdx.x) {
+    if (want_sum) p.sum = a.blk_sum[threadIdx.x];
+    else p.m0 = a.blk_max[threadIdx.x];
+  }
+  block_excl_scan(p, &tot);
+  return tot;
+}
+
+__global__ __launch_bounds__(BLOCK) void k_enc_kept2(EncodeArgs a) {
+  const int32_t bp = prefix_of_blocks(a, false).m0;  // last CLOSE before this block
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = k < a.n_frames;
+  wsg_encode_frame f;
+  Agg v = AGG_ID;
+  if (live) {
+    f = a.frames[k];
+    v.m0 = (f.opcode & 15u) == WSG_OP_CLOSE ? (int32_t)k : -1;
+  }
+  Agg tot;
+  const Agg ex = block_excl_scan(v, &tot);
+  Agg w = AGG_ID;
+  if (live) {
+    const int32_t lc = ex.m0 > bp ? ex.m0 : bp;
+    a.last_close[k] = lc;
+    const uint32_t s = a.sess[k];
+    const bool dropped = a.closed[s] || lc >= (int32_t)a.session_first[s];  // FrameEncoder.java:71-76
+    if (dropped) a.sess[k] = s | SESS_DROPPED;
+    w.sum = dropped ? 0ull : (uint64_t)enc_header_len(f.payload_len, a.client_mode) + f.payload_len;
+  }
+  const Agg ew = block_excl_scan(w, &tot);
+  if (live) a.wire_off[k] = ew.sum;  // block-local
+  if (threadIdx.x == 0) a.blk_sum[blockIdx.x] = tot.sum;
+}
+
+// Final offsets, coarse index, and the closed carry-out (by the last frame of
+// each session: it sent or follows a CLOSE); closed[] is not read here.
+__global__ __launch_bounds__(BLOCK) void k_enc_fix2(EncodeArgs a) {
+  const uint64_t base = prefix_of_blocks(a, true).sum;
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  if (blockIdx.x + 1 == gridDim.x && threadIdx.x == 0) a.wire_off[a.n_frames] = base + a.blk_sum[blockIdx.x];
+  if (k >= a.n_frames) return;
+  const uint64_t wo = a.wire_off[k] + base;
+  a.wire_off[k] = wo;
+  const uint32_t sk = a.sess[k], s = sk & ~SESS_DROPPED;
+  const wsg_encode_frame f = a.frames[k];
+  if (!(sk & SESS_DROPPED)) enc_index_frame(a, k, wo, wo + enc_header_len(f.payload_len, a.client_mode) + f.payload_len);
+  const bool last = k + 1 == a.n_frames || (a.sess[k + 1] & ~SESS_DROPPED) != s;
+  if (last && ((f.opcode & 15u) == WSG_OP_CLOSE || a.last_close[k] >= (int32_t)a.session_first[s])) a.closed[s] = 1;
+}
+
+// One thread per 1 KiB piece of wire_out: the frame holding the piece's first
+// byte is the last k with wire_off[k] <= ps, searched between the coarse index
+// entries around ps (usually one or two frames apart; the offsets stay in L2).
+// A piece entirely inside that frame's payload (or ending the output there)
+// takes the fast path of k_enc_piecesN.
+__global__ __launch_bounds__(256) void k_enc_desc(EncodeArgs a) {
+  const uint64_t pc = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (pc >= a.n_pieces) return;
+  const uint64_t total = a.wire_off[a.n_frames];
+  const uint64_t ps = pc * PIECE;
+  if (ps >= total) return;
+  const uint64_t q = ps / IDX_SPAN;
+  uint64_t lo = a.pidx[q];                                                   // wire_off[lo] <= q * SPAN <= ps
+  uint64_t hi = (q + 1) * IDX_SPAN < total ? (uint64_t)a.pidx[q + 1] + 1 : a.n_frames;  // ps < wire_off[hi]
+  while (hi - lo > 1) {
+    const uint64_t mid = (lo + hi) >> 1;
+    if (a.wire_off[mid] <= ps) lo = mid;
+    else hi = mid;
+  }
+  const uint64_t k = lo;
   const wsg_encode_frame f = a.frames[k];
   const uint32_t hl = enc_header_len(f.payload_len, a.client_mode);
-  const uint64_t total = a.wire_off[a.n_frames];
-  const uint64_t end = wo + hl + f.payload_len, pay0 = wo + hl;
-  const uint32_t m = (uint32_t)f.mask[0] | ((uint32_t)f.mask[1] << 8) | ((uint32_t)f.mask[2] << 16) |
-                     ((uint32_t)f.mask[3] << 24);
-  for (uint64_t pc = (wo + PIECE - 1) / PIECE; pc * PIECE < end && pc < a.n_pieces; ++pc) {
-    const uint64_t ps = pc * PIECE;
-    const bool single = ps >= pay0 && (ps + PIECE <= end || end == total);
-    PieceDesc d;
-    d.frame = (uint32_t)k;
-    if (single) {
-      const uint64_t j0 = ps - pay0;  // payload index of the piece's first byte
-      const uint32_t ph = (uint32_t)(j0 & 3);
-      const uint32_t mr = a.client_mode ? (ph ? (m >> (8 * ph)) | (m << (32 - 8 * ph)) : m) : 0u;
-      const uint64_t nb = end - ps < PIECE ? end - ps : PIECE;
-      d.info = ((f.payload_off + j0) & PD_SRC_MASK) | (nb << PD_NB_SHIFT);
-      d.mask = mr;
-    } else {
-      d.info = PD_MULTI;
-      d.mask = 0;
-    }
-    a.pieces[pc] = d;
+  const uint64_t wo = a.wire_off[k], pay0 = wo + hl, end = wo + hl + f.payload_len;
+  const bool single = ps >= pay0 && (ps + PIECE <= end || end == total);
+  PieceDesc d;
+  d.frame = (uint32_t)k;
+  if (single) {
+    const uint32_t m = (uint32_t)f.mask[0] | ((uint32_t)f.mask[1] << 8) | ((uint32_t)f.mask[2] << 16) |
+                       ((uint32_t)f.mask[3] << 24);
+    const uint64_t j0 = ps - pay0;  // payload index of the piece's first byte
+    const uint32_t ph = (uint32_t)(j0 & 3);
+    const uint32_t mr = a.client_mode ? (ph ? (m >> (8 * ph)) | (m << (32 - 8 * ph)) : m) : 0u;
+    const uint64_t nb = end - ps < PIECE ? end - ps : PIECE;
+    d.info = ((f.payload_off + j0) & PD_SRC_MASK) | (nb << PD_NB_SHIFT);
+    d.mask = mr;
+  } else {
+    d.info = PD_MULTI;
+    d.mask = 0;
   }
+  a.pieces[pc] = d;
 }
 
 // ------------------------------------------------------------------ k_enc_pieces
@@ -391,17 +471,27 @@ __global__ __launch_bounds__(256) void k_enc_final(EncodeArgs a) {
   }
 }
 
+bool enc_plan_small(const EncodeArgs& a) { return a.nblk <= ENC_SMALL_BLOCKS; }
+
 void launch_enc_len(const EncodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_enc_len, dim3(a.nblk), dim3(BLOCK), 0, s, a);
 }
 void launch_enc_scan(const EncodeArgs& a, hipStream_t s) {
+  if (enc_plan_small(a)) {
+    hipLaunchKernelGGL(k_enc_kept2, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL(k_enc_fix2, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+    return;
+  }
   hipLaunchKernelGGL(k_enc_scan, dim3(1), dim3(1024), 0, s, a);
-  hipLaunchKernelGGL(k_enc_link, dim3(a.nblk), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_enc_kept, dim3(a.nblk), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_enc_scan_sum, dim3(1), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(k_enc_fix, dim3(a.nblk), dim3(BLOCK), 0, s, a);
 }
+void launch_enc_desc(const EncodeArgs& a, hipStream_t s) {
+  if (a.n_pieces) hipLaunchKernelGGL(k_enc_desc, dim3((uint32_t)((a.n_pieces + 255) / 256)), dim3(256), 0, s, a);
+}
 void launch_enc_final(const EncodeArgs& a, hipStream_t s) {
+  if (enc_plan_small(a)) return;  // k_enc_fix2 wrote the carry-out
   hipLaunchKernelGGL(k_enc_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);
 }
 

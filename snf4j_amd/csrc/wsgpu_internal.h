@@ -52,7 +52,8 @@ __host__ __device__ inline uint64_t piece_bound(uint64_t wire_len, uint64_t n_fr
 // One 1 KiB piece of the payload output (16 B, one scalar load per wave).
 struct PieceDesc {
   uint64_t info;  // bits 0-47: wire offset of the piece's first payload byte; 48-58: payload bytes in
-                  // the piece (1..1024); 59: validate; 60: piece starts its frame; 61: spans several slots
+                  // the piece (1..1024); 59: validate; 60: piece starts its frame; 61: spans several slots;
+                  // 62: piece holds its frame's last payload byte; 63: the frame is FIN
   uint32_t mask;  // frame mask key (payload phase 0 at the piece start)
   uint32_t frame; // frame index
 };
@@ -61,6 +62,8 @@ constexpr uint32_t PD_NB_SHIFT = 48;
 constexpr uint64_t PD_VALIDATE = 1ull << 59;
 constexpr uint64_t PD_FIRST = 1ull << 60;
 constexpr uint64_t PD_MULTI = 1ull << 61;
+constexpr uint64_t PD_LAST = 1ull << 62;
+constexpr uint64_t PD_FIN = 1ull << 63;
 
 struct DecodeArgs {
   // inputs
@@ -81,7 +84,8 @@ struct DecodeArgs {
   // workspace
   FrameRec* rec;
   int32_t* prev;       // [3][n_frames]: last data / last TEXT|BINARY / last nonempty data frame before k
-  uint32_t* edge;      // [2][n_frames]: first 3 / last 3 payload bytes (unmasked)
+  uint32_t* edge;      // [2][n_frames]: first 3 / last 3 payload bytes (unmasked); the last 3 only
+                       // for non-FIN data frames (the carry into the next fragment or batch)
   uint64_t* blk_sum;   // [nblk] slot-bytes per block -> exclusive prefix
   int32_t* blk_max;    // [3][nblk] per-block max indices -> exclusive prefix max
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
@@ -108,28 +112,30 @@ struct EncodeArgs {
   uint64_t* blk_sum;   // [nblk]
   int32_t* blk_max;    // [nblk] last CLOSE frame index
   int32_t* last_close; // [n_frames] last CLOSE frame before k
-  struct PieceDesc* pieces;  // [n_pieces]: 1 KiB pieces of wire_out (k_enc_fix -> k_enc_pieces)
+  struct PieceDesc* pieces;  // [n_pieces]: 1 KiB pieces of wire_out (k_enc_desc -> k_enc_pieces)
   uint64_t n_pieces;
+  uint32_t* pidx;      // [n_idx]: frame holding wire byte q * 64 KiB (k_enc_fix / k_enc_plan1)
+  uint64_t n_idx;
   uint32_t nblk;
 };
 
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
 void launch_parse(const DecodeArgs& a, hipStream_t s);
 void launch_scan(const DecodeArgs& a, hipStream_t s);
 void launch_link(const DecodeArgs& a, hipStream_t s);
-void launch_unmask(const DecodeArgs& a, hipStream_t s, uint32_t grid);  // wave per frame (reference kernel)
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
 void launch_merge(const DecodeArgs& a, hipStream_t s);
 void launch_final(const DecodeArgs& a, hipStream_t s);
 
 void launch_enc_len(const EncodeArgs& a, hipStream_t s);
 void launch_enc_scan(const EncodeArgs& a, hipStream_t s);
+void launch_enc_desc(const EncodeArgs& a, hipStream_t s);
 void launch_enc_pieces(const EncodeArgs& a, hipStream_t s);
 void launch_enc_final(const EncodeArgs& a, hipStream_t s);
 

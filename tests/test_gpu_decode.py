@@ -336,3 +336,33 @@ def test_dense_small_frames(ctx, oracle, empties):
             fr.insert(len(fr) // 2, wsgen.bad_frame(rng, "utf8", True, 65536))
         sessions.append(fr)
     run_parity(ctx, oracle, sessions, rng=rng, n_batches=2, tag=f"dense {empties}")
+
+
+@pytest.mark.parametrize("masked", [True, False])
+def test_tail_utf8_large_frames(ctx, oracle, masked):
+    """A frame's last byte and the end of a FIN message are tested by the piece
+    kernel on the bytes it holds (decode.hip tail_error): invalid leads, stray
+    continuation bytes and truncated sequences at the end of frames whose last
+    piece is full, partial, 1-3 bytes long, or the frame's only piece, with the
+    frame FIN, followed by a continuation, or ending a fragmented message."""
+    rng = np.random.default_rng(21)
+    tails = [b"", b"\xff", b"\xc3", b"\xe2\x82", b"\xf0\x9f\x98", b"\xc3\xa9", b"\x80", b"\xed\xa0", b"\xf4\x90",
+             b"\xe2\x82\xac", b"\xf0\x9f\x98\x80", b"\xc0"]
+    lens = [1, 2, 3, 4, 15, 16, 17, 18, 31, 1020, 1021, 1022, 1023, 1024, 1025, 1026, 1027, 2047, 2048, 2049,
+            3071, 3072, 3073, 4096, 4097, 4098, 6000]
+    sessions = []
+    cm = not masked
+    for n in lens:
+        for t in tails:
+            if len(t) > n:
+                continue
+            body = b"a" * (n - len(t)) + t
+            m = tuple(int(x) for x in rng.integers(0, 256, 4))
+            sessions.append([wsgen.build_frame(1, True, 0, body, masked, m)])
+            sessions.append([wsgen.build_frame(1, False, 0, body, masked, m),
+                             wsgen.build_frame(0, True, 0, b"\x80\x80z", masked, m)])
+            sessions.append([wsgen.build_frame(1, False, 0, b"x\xe2", masked, m),
+                             wsgen.build_frame(0, True, 0, body, masked, m)])
+            sessions.append([wsgen.build_frame(1, False, 0, b"\xf0\x9f", masked, m),
+                             wsgen.build_frame(0, True, 0, t[:2], masked, m)])
+    run_parity(ctx, oracle, sessions, cm=cm, n_batches=2, rng=rng, tag="tails")

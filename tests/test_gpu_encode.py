@@ -90,3 +90,37 @@ def test_encode_decode_round_trip(ctx, oracle):
     got = b"".join(payload[int(d["payload_off"]):int(d["payload_off"]) + int(d["payload_len"])].tobytes()
                    for d in desc)
     assert got == msg
+
+
+@pytest.mark.parametrize("cm", [True, False])
+def test_large_encode_batch_multipass(ctx, oracle, cm):
+    """More frames than the one-workgroup plan takes (encode.hip ENC_PLAN1_MAX):
+    the multi-pass latch / offset scans and the coarse piece index, with CLOSE
+    frames mid-session and sessions already closed on entry (FrameEncoder.java:71-76)."""
+    rng = np.random.default_rng(77 + cm)
+    n_s = 3000
+    counts = rng.integers(0, 50, n_s)
+    pre_closed = rng.random(n_s) < 0.05
+    specs, first, exp = [], [0], []
+    for s in range(n_s):
+        enc = oracle.Encoder(cm)
+        for _ in range(int(counts[s])):
+            r = rng.random()
+            op = 8 if r < 0.01 else 9 if r < 0.03 else int(rng.choice([0, 1, 2]))
+            n = int(rng.integers(0, 125 if op >= 8 else (3000 if rng.random() < 0.05 else 200)))
+            p = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            fin, rsv = bool(rng.integers(0, 2)) or op >= 8, int(rng.integers(0, 8))
+            mask = tuple(int(x) for x in rng.integers(0, 256, 4))
+            specs.append((op, fin, rsv, p, mask))
+            e = enc.encode(op, fin, rsv, p, mask)
+            exp.append(b"" if pre_closed[s] else e)
+        first.append(len(specs))
+    assert len(specs) > 65536
+    pl, fr = _frames(specs)
+    closed = pre_closed.astype(np.uint8)
+    wire, off = ctx.encode_host(cm, pl, fr, np.array(first, np.uint32), closed)
+    assert int(off[-1]) == sum(len(e) for e in exp)
+    for k in range(len(specs)):
+        assert wire[int(off[k]):int(off[k + 1])].tobytes() == exp[k], k
+    for s in range(n_s):
+        assert closed[s] == (pre_closed[s] or any(specs[k][0] == 8 for k in range(first[s], first[s + 1])))

@@ -1,6 +1,6 @@
 // ubench_unmask.hip — kernel-level microbenchmark for the decode hot kernel.
 // Builds the full decode pipeline once on a synthetic batch in HBM, then times
-// k_unmask variants (grid size, unroll) and a plain 16-B copy of the same byte
+// k_pieces / k_piecesN variants and a plain 16-B copy of the same byte
 // count (the streaming ceiling of this chip), interleaved in one process.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I.. tools/ubench_unmask.hip \
 //         snf4j_amd/csrc/synth.hip -o /tmp/ubench
@@ -84,12 +84,6 @@ int main(int argc, char** argv) {
       if (vs[i].kind == 0) {
         const uint64_t n16 = (uint64_t)(wire_len / 16);
         hipLaunchKernelGGL(k_copy16, dim3(vs[i].grid), dim3(256), 0, st, (const uint4*)wire, (uint4*)payload, n16);
-      } else if (vs[i].kind == 4) {
-        hipLaunchKernelGGL(ws::k_unmask<4>, dim3(vs[i].grid), dim3(256), 0, st, a);
-      } else if (vs[i].kind == 2) {
-        hipLaunchKernelGGL(ws::k_unmask<2>, dim3(vs[i].grid), dim3(256), 0, st, a);
-      } else if (vs[i].kind == 1) {
-        hipLaunchKernelGGL(ws::k_unmask<1>, dim3(vs[i].grid), dim3(256), 0, st, a);
       } else if (vs[i].kind == 10) {
         hipLaunchKernelGGL((ws::k_pieces<1, 4, 0>), dim3((uint32_t)((npb + 3) / 4)), dim3(256), 0, st, a);
       } else if (vs[i].kind == 13) {
