@@ -245,7 +245,42 @@ def _timed(ctx, step, steps, warmup, dev, kernel):
     return el, kms / max(1, kn), pipeline_breakdown(ctx, step, dev)
 
 
-def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps, warmup, expect_errors=None):
+def _aggregate_line(ctx, dev, payload, desc, res, sf, n, n_s, steps, warmup, max_len=1 << 20):
+    """FrameAggregator (wsg_aggregate_batch_device) over the decoded batch: every
+    fragmented message's bytes gathered into one contiguous range.  k_agg_gather's
+    algorithmic bytes = member bytes read + written."""
+    import torch
+    from snf4j_amd._lib import RESULT_DTYPE
+    cap = payload.numel()
+    agg_out = torch.empty(cap, dtype=torch.uint8, device=dev)
+    out_desc = torch.empty((n + n_s) * 16, dtype=torch.uint8, device=dev)
+    out_res = torch.empty(n_s * 16, dtype=torch.uint8, device=dev)
+    astate = torch.zeros(n_s * 8, dtype=torch.uint8, device=dev)
+    total = torch.zeros(1, dtype=torch.int64, device=dev)
+
+    def step():
+        astate.zero_()
+        ctx.aggregate_device(max_len, desc, sf, res, payload, astate, agg_out, out_desc, out_res, total, n_frames=n)
+
+    step()
+    torch.cuda.synchronize(dev)
+    member = int(total.item())
+    r = out_res.cpu().numpy().view(RESULT_DTYPE)
+    assert int((r["error"] != 0).sum()) == 0
+    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_agg_gather")
+    ach = 2 * member / (kms / 1e3) / 1e9
+    return {"config": "FrameAggregator over the decoded configs[2] batch (maxAggregatedLength 1 MiB)",
+            "value": round(member * steps / el / 2**30, 3), "unit": "GiB/s (aggregated message bytes)",
+            "ms_per_step": round(el / steps * 1e3, 4), "member_bytes": member,
+            "output_frames": int(r["n_delivered"].sum()),
+            "roofline": {"kernel": "k_agg_gather", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": 2 * member,
+                         "avg_launch_ms": round(kms, 4)},
+            "pipeline_ms": {k: v for k, v in pipe.items() if k.startswith("k_agg")}}
+
+
+def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps, warmup, expect_errors=None,
+                 aggregate=False):
     """Decode GiB/s (wire) + k_piecesN roofline of one device-resident batch."""
     import numpy as np
     import torch
@@ -272,13 +307,15 @@ def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps
     el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_piecesN")
     alg = wl + payload_bytes
     ach = alg / (kms / 1e3) / 1e9
+    agg = _aggregate_line(ctx, dev, payload, desc, res, sf, n, n_s, steps, warmup) if aggregate else None
+    pipe = {k: v for k, v in pipe.items() if not k.startswith("k_agg")}
     return {"config": name, "value": round(wl * steps / el / 2**30, 3), "unit": "GiB/s (wire)",
             "ms_per_step": round(el / steps * 1e3, 4), "frames": n, "sessions": n_s, "wire_bytes": wl,
             "sessions_with_error": n_err,
             "roofline": {"kernel": "k_piecesN", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
                          "avg_launch_ms": round(kms, 4)},
-            "pipeline_ms": pipe}
+            "pipeline_ms": pipe, **({"aggregate": agg} if agg else {})}
 
 
 def measure_extras(ctx, dev, args):
@@ -310,7 +347,8 @@ def measure_extras(ctx, dev, args):
     line = _decode_line(ctx, dev, "configs[2]: mixed TEXT+BINARY 64 B-64 KiB log-uniform, 10% fragmented, "
                         "1% of text messages with invalid UTF-8, 1024 sessions", wire, wl,
                         torch.from_numpy(offh.astype(np.int64)).to(dev), torch.from_numpy(sfh.astype(np.int32)).to(dev),
-                        len(t), 1024, info["payload_bytes"], K, W, expect_errors=len(info["bad_sessions"]))
+                        len(t), 1024, info["payload_bytes"], K, W, expect_errors=len(info["bad_sessions"]),
+                        aggregate=True)
     line["mix"] = {k: v for k, v in info.items() if k != "bad_sessions"}
     out.append(line)
     del wire

@@ -56,8 +56,9 @@ typedef enum wsg_status {
     WSG_E_NEG_LEN = 15,        /* "Negative payload length (%d)"        FrameDecoder.available :390 */
     WSG_E_EXT_LEN = 16,        /* "Extended payload length (%d) > %d"   FrameDecoder.available :393
                                   (detail = plen, detail2 = Integer.MAX_VALUE - need) */
-    WSG_E_BATCH = 17           /* frame extent in the batch does not match its header
+    WSG_E_BATCH = 17,          /* frame extent in the batch does not match its header
                                   (a caller bug: never produced by the reference) */
+    WSG_E_AGG_TOO_BIG = 18     /* "Too big payload for aggregated frame"  FrameAggregator.java:93 (1009) */
 } wsg_status;
 
 /* API return codes (<0). */
@@ -70,6 +71,7 @@ typedef enum wsg_status {
 /* Close codes the reference writes with writenf(new CloseFrame(code)). */
 #define WSG_CLOSE_PROTOCOL_ERROR 1002  /* CloseFrame.PROTOCOL_ERROR */
 #define WSG_CLOSE_NON_UTF8 1007        /* CloseFrame.NON_UTF8 */
+#define WSG_CLOSE_TOO_BIG 1009         /* CloseFrame.TOO_BIG */
 
 /* RFC 6455 opcodes (Opcode.java:33-98). */
 #define WSG_OP_CONTINUATION 0
@@ -158,7 +160,7 @@ int wsg_sync(wsg_ctx* ctx);
 
 /* Kernel timing (hipEvents recorded around each kernel on the ctx stream).
  * enable: 0 off, 1 every kernel, 2 only the streaming kernels (k_piecesN,
- * k_enc_piecesN) — each event pair adds queue time, so a timed step uses 2. */
+ * k_enc_piecesN, k_agg_gather) — each event pair adds queue time, so a timed step uses 2. */
 int wsg_set_timing(wsg_ctx* ctx, int enable);
 /* out_ms[i] = accumulated milliseconds of kernel i since the last reset, out_count[i] = launches.
  * Kernel ids: see wsg_kernel_name(). Syncs the stream. */
@@ -263,6 +265,65 @@ int wsg_encode_batch_host(wsg_ctx* ctx, int client_mode,
                           const uint32_t* session_first, uint32_t n_sessions,
                           uint8_t* closed,
                           uint8_t* wire_out, uint64_t wire_cap, uint64_t* wire_off);
+
+/* ---------------- aggregate (FrameAggregator) ---------------- */
+/* Per-session carry of FrameAggregator.frame (FrameAggregator.java:44): the
+ * aggregated frame in progress.  Its bytes from earlier batches stay with the
+ * caller, as PayloadAggregator keeps its fragment list (PayloadAggregator.java:34). */
+typedef struct wsg_agg_state {
+    uint8_t open;      /* an aggregated frame is in progress (frame != null) */
+    uint8_t opcode;    /* its opcode: TEXT or BINARY */
+    uint8_t rsv;       /* its RSV bits (Frame.getRsvBits) */
+    uint8_t reserved;
+    uint32_t length;   /* IAggregatedFrame.getPayloadLength(): its bytes so far */
+} wsg_agg_state; /* 8 bytes */
+
+/* wsg_frame_desc.flags bits of aggregator output (besides FIN / RSV) */
+#define WSG_AGG_IN_AGG 0x02    /* payload in agg_out (else the frame's own slot in the decoder's payload) */
+#define WSG_AGG_PREFIXED 0x04  /* the message began in an earlier batch: its bytes from earlier
+                                  batches (held by the caller) come first */
+#define WSG_AGG_PENDING 0x08   /* not a frame: this batch's bytes of a message still open at the
+                                  end of the batch, for the caller to hold (replacing what it held
+                                  unless also PREFIXED) */
+
+/* Device-resident FrameAggregator over a decoded batch (FrameAggregator.decode,
+ * FrameAggregator.java:72-104, applied to each delivered frame of each session in
+ * order).  Inputs are the decoder's outputs for the batch:
+ *   desc[n_frames], payload       wsg_decode_batch_* desc_out / payload_out (payload_len = its
+ *                                 size in bytes, e.g. the decoder's payload_cap)
+ *   session_first[0..n_sessions]  as for the decode
+ *   dec_result[n_sessions]        only the first n_delivered frames of a session are aggregated
+ *   state[n_sessions]             carry in / out
+ * Outputs:
+ *   agg_out[agg_cap]              the bytes of every fragmented message, back to back in frame
+ *                                 order (agg_cap >= the batch's total payload bytes)
+ *   out_desc[n_frames+n_sessions] session s's output frames at out_desc[session_first[s] + s + i],
+ *                                 i < out_result[s].n_delivered: pass-through frames reference
+ *                                 `payload`, aggregated ones agg_out (WSG_AGG_IN_AGG); then, if the
+ *                                 session ends the batch inside a message, one WSG_AGG_PENDING entry
+ *   out_result[n_sessions]        error WSG_E_AGG_TOO_BIG (close 1009) with detail = the index of the
+ *                                 failing input frame within the session; nothing after it is output
+ *   agg_total (device, 1 x u64)   bytes written to agg_out */
+int wsg_aggregate_batch_device(wsg_ctx* ctx, int64_t max_aggregated_len,
+                               const wsg_frame_desc* desc, uint64_t n_frames,
+                               const uint32_t* session_first, uint32_t n_sessions,
+                               const wsg_session_result* dec_result,
+                               const uint8_t* payload, uint64_t payload_len,
+                               wsg_agg_state* state, uint8_t* agg_out, uint64_t agg_cap,
+                               wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                               uint64_t* agg_total);
+
+/* Same contract with host pointers: H2D, aggregate, D2H of the used agg_out
+ * bytes, descriptors, results and state; synchronises.  *agg_total is a host
+ * pointer here. */
+int wsg_aggregate_batch_host(wsg_ctx* ctx, int64_t max_aggregated_len,
+                             const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions,
+                             const wsg_session_result* dec_result,
+                             const uint8_t* payload, uint64_t payload_len,
+                             wsg_agg_state* state, uint8_t* agg_out, uint64_t agg_cap,
+                             wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                             uint64_t* agg_total);
 
 /* ---------------- synthetic workloads (bench / tests only) ---------------- */
 /* Fill a device batch of uniform frames: n_frames frames of payload_len bytes,

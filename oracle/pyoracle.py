@@ -75,6 +75,9 @@ def lib():
         L.or_encoded_length.restype = i64
         L.or_encode.argtypes = [p, i32, i32, i32, p, i64, p, p]
         L.or_encode.restype = i64
+        L.or_aggregator_init.argtypes = [p, i64]
+        L.or_aggregator_free.argtypes = [p]
+        L.or_aggregate.argtypes = [p, i32, i32, i32, p, i64, p]
         L.or_splitmix64.argtypes = [u64]
         L.or_splitmix64.restype = u64
         L.or_synth_uniform.argtypes = [u64, u64, u32, u32, i32, i32, i32, p, p, p]
@@ -267,6 +270,45 @@ def stream_decode(stream: bytes, chunks=(), client_mode=False, allow_extensions=
                                   (int(d["flags"]) >> 4) & 7, payload[off:off + ln].tobytes()))
     error = InvalidFrame(err.value, d1.value, d2.value, cc.value) if err.value else None
     return frames, error
+
+
+# ---------------------------------------------------------------- FrameAggregator
+class _CAgg(C.Structure):
+    _fields_ = [("max_len", C.c_int64), ("open", C.c_int), ("opcode", C.c_int), ("rsv", C.c_int),
+                ("length", C.c_int64), ("data", C.c_void_p), ("cap", C.c_int64)]
+
+
+E_AGG_TOO_BIG = 18
+
+
+class Aggregator:
+    """FrameAggregator(maxAggregatedLength) restated in C (FrameAggregator.java:72-104).
+    decode() returns the emitted OracleFrame, None, or raises InvalidFrame(18, close 1009)."""
+
+    def __init__(self, max_aggregated_len):
+        self._a = _CAgg()
+        lib().or_aggregator_init(C.byref(self._a), int(max_aggregated_len))
+
+    def __del__(self):
+        if getattr(self, "_a", None) is not None:
+            lib().or_aggregator_free(C.byref(self._a))
+            self._a = None
+
+    @property
+    def state(self):
+        return bool(self._a.open), int(self._a.opcode), int(self._a.rsv), int(self._a.length)
+
+    def decode(self, opcode, fin, rsv, payload: bytes):
+        b = bytes(payload)
+        a = np.frombuffer(b, dtype=np.uint8) if b else np.zeros(1, np.uint8)
+        f = _CFrame()
+        rc = lib().or_aggregate(C.byref(self._a), int(opcode), int(bool(fin)), int(rsv), a.ctypes.data, len(b),
+                                C.byref(f))
+        if rc == -1:
+            raise InvalidFrame(E_AGG_TOO_BIG, 0, 0, 1009)
+        if rc == 0:
+            return None
+        return OracleFrame(f.opcode, bool(f.fin), f.rsv, C.string_at(f.payload, f.len) if f.len else b"")
 
 
 # ---------------------------------------------------------------- FrameEncoder

@@ -329,6 +329,7 @@ int or_format_error(int err, int64_t detail, int64_t detail2, char* buf, int cap
     case WSG_E_NEG_LEN: return snprintf(buf, cap, "Negative payload length (%lld)", (long long)detail);
     case WSG_E_EXT_LEN: return snprintf(buf, cap, "Extended payload length (%lld) > %lld", (long long)detail, (long long)detail2);
     case WSG_E_BATCH: return snprintf(buf, cap, "Malformed batch");
+    case WSG_E_AGG_TOO_BIG: return snprintf(buf, cap, "Too big payload for aggregated frame");  /* FrameAggregator.java:93 */
     default: if (cap > 0) buf[0] = 0; return 0;
     }
 }
@@ -495,6 +496,69 @@ int64_t or_encode(or_encoder* e, int opcode, int fin, int rsv, const uint8_t* pa
 /* ------------------------------------------------------------------------ */
 /* Synthetic workload generator (must match the device generator bit for bit) */
 /* ------------------------------------------------------------------------ */
+/* ------------------------------------------------------------------------ */
+/* FrameAggregator.decode, FrameAggregator.java:72-104.                      */
+/* ------------------------------------------------------------------------ */
+void or_aggregator_init(or_aggregator* a, int64_t max_aggregated_len) {
+    memset(a, 0, sizeof(*a));
+    a->max_len = max_aggregated_len;
+}
+
+void or_aggregator_free(or_aggregator* a) {
+    free(a->data);
+    a->data = NULL;
+    a->cap = 0;
+}
+
+static void agg_append(or_aggregator* a, const uint8_t* p, int64_t len) {
+    if (a->length + len > a->cap) {
+        int64_t c = a->cap ? a->cap : 64;
+        while (c < a->length + len) c *= 2;
+        a->data = (uint8_t*)realloc(a->data, (size_t)c);
+        a->cap = c;
+    }
+    if (len) memcpy(a->data + a->length, p, (size_t)len);
+    a->length += len;
+}
+
+int or_aggregate(or_aggregator* a, int opcode, int fin, int rsv, const uint8_t* payload, int64_t len,
+                 or_frame* out) {
+    switch (opcode) {
+    case WSG_OP_BINARY:
+    case WSG_OP_TEXT:
+        if (fin) break;  /* a final data frame passes through (:77-79, :84-86) */
+        /* new AggregatedBinaryFrame/AggregatedTextFrame(true, rsv, payload) (:80, :87) */
+        a->open = 1;
+        a->opcode = opcode;
+        a->rsv = rsv;
+        a->length = 0;
+        agg_append(a, payload, len);
+        return 0;
+    case WSG_OP_CONTINUATION:
+        if (a->open) {
+            if (a->length + len > a->max_len) return -1;  /* tooBig (:92-94) */
+            agg_append(a, payload, len);                  /* addFragment (:95) */
+            if (!fin) return 0;
+            a->open = 0;                                  /* data = frame; frame = null (:99-100) */
+            out->opcode = a->opcode;
+            out->fin = 1;
+            out->rsv = a->rsv;
+            out->len = a->length;
+            out->payload = a->data;
+            return 1;
+        }
+        break;  /* falls through to out.add(data) (:103) */
+    default:
+        break;
+    }
+    out->opcode = opcode;
+    out->fin = fin;
+    out->rsv = rsv;
+    out->len = len;
+    out->payload = payload;
+    return 1;
+}
+
 uint64_t or_splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
     x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;

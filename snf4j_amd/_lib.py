@@ -60,6 +60,8 @@ try:
     ENCODE_DTYPE = np.dtype([("payload_off", "<u8"), ("payload_len", "<u4"), ("opcode", "u1"),
                              ("flags", "u1"), ("reserved", "u1", (2,)), ("mask", "u1", (4,)),
                              ("reserved2", "<u4")])
+    AGG_STATE_DTYPE = np.dtype([("open", "u1"), ("opcode", "u1"), ("rsv", "u1"), ("reserved", "u1"),
+                                ("length", "<u4")])
     SYNTH_DTYPE = np.dtype([("wire_off", "<u8"), ("msg_seed", "<u8"), ("payload_len", "<u4"), ("msg_pos", "<u4"),
                             ("msg_len", "<u4"), ("mask", "<u4"), ("inject_pos", "<i4"), ("opcode", "u1"),
                             ("flags", "u1"), ("text", "u1"), ("inject_kind", "u1")])
@@ -108,6 +110,8 @@ def _load():
         "wsg_synth_uniform": ([p, u64, u64, u32, u32, i32, i32, i32, p, p, p], i32),
         "wsg_copy_ceiling": ([p, p, p, u64, i32, P(C.c_double)], i32),
         "wsg_synth_frames": ([p, p, u64, p], i32),
+        "wsg_aggregate_batch_device": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, p], i32),
+        "wsg_aggregate_batch_host": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, P(u64)], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

@@ -18,11 +18,14 @@ import struct
 
 import numpy as np
 
-from ._lib import ENCODE_DTYPE, STATE_DTYPE
+from ._lib import AGG_STATE_DTYPE, DESC_DTYPE, ENCODE_DTYPE, RESULT_DTYPE, STATE_DTYPE
 from .context import Context, check_header, decoder_cfg, error_message, frame_available
-from .frame import CloseFrame, Frame, InvalidFrameException, Opcode, make_frame
+from .frame import (AggregatedBinaryFrame, AggregatedTextFrame, CloseFrame, Frame, InvalidFrameException, Opcode,
+                    make_frame)
 
-_CLOSE_FOR = {13: CloseFrame.NON_UTF8, 14: CloseFrame.NON_UTF8}
+AGG_IN_AGG, AGG_PREFIXED, AGG_PENDING = 0x02, 0x04, 0x08  # wsg_frame_desc.flags of aggregator output
+
+_CLOSE_FOR = {13: CloseFrame.NON_UTF8, 14: CloseFrame.NON_UTF8, 18: 1009}
 
 
 def _close_code(err: int) -> int:
@@ -275,3 +278,88 @@ class SessionBatcher:
             out.append((frames, exc))
             self.queue[s] = []
         return out
+
+
+class BatchAggregator:
+    """FrameAggregator (FrameAggregator.java:72-104) for every session of a batch
+    flow, run on the GPU over each decoded batch (wsg_aggregate_batch_*).  The
+    device lays every fragmented message's bytes back to back; the bytes of a
+    message still open at the end of a batch are held here per session, as the
+    reference's PayloadAggregator holds its fragment list (PayloadAggregator.java:34),
+    and put in front of the message's remaining bytes when it completes."""
+
+    def __init__(self, n_sessions: int, maxAggregatedLength: int, ctx: Context | None = None):
+        self.max_len = int(maxAggregatedLength)
+        self.ctx = ctx
+        self.state = np.zeros(n_sessions, dtype=AGG_STATE_DTYPE)
+        self.held = [[] for _ in range(n_sessions)]
+
+    def run(self, desc, session_first, dec_result, payload):
+        """Aggregate one decoded batch (host arrays as wsg_decode_batch_host returns
+        them).  Returns [(frames, InvalidFrameException | None)] per session."""
+        ctx = self.ctx or default_context()
+        sf = np.ascontiguousarray(session_first, dtype=np.uint32)
+        agg, od, ores = ctx.aggregate_host(self.max_len, desc, sf, dec_result, payload, self.state)
+        out = []
+        for s in range(len(sf) - 1):
+            base = int(sf[s]) + s
+            r = ores[s]
+            frames = []
+            for i in range(int(r["n_delivered"])):
+                d = od[base + i]
+                fl, o, ln = int(d["flags"]), int(d["payload_off"]), int(d["payload_len"])
+                rsv = (fl >> 4) & 7
+                if fl & AGG_IN_AGG:
+                    part = agg[o:o + ln].tobytes()
+                    parts = (self.held[s] if fl & AGG_PREFIXED else []) + [part]
+                    self.held[s] = []
+                    cls = AggregatedTextFrame if int(d["opcode"]) == 1 else AggregatedBinaryFrame
+                    frames.append(cls(rsv, b"".join(parts), parts))
+                else:
+                    frames.append(make_frame(int(d["opcode"]), bool(fl & 0x80), rsv, payload[o:o + ln].tobytes()))
+            exc = None
+            if r["error"]:
+                exc = InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
+                exc.close_code = int(r["close_code"])
+                exc.frame_index = int(r["detail"])
+            elif self.state[s]["open"]:
+                d = od[base + int(r["n_delivered"])]
+                assert int(d["flags"]) & AGG_PENDING
+                o, ln = int(d["payload_off"]), int(d["payload_len"])
+                kept = self.held[s] if int(d["flags"]) & AGG_PREFIXED else []
+                self.held[s] = kept + ([agg[o:o + ln].tobytes()] if ln else [])
+            else:
+                self.held[s] = []
+            out.append((frames, exc))
+        return out
+
+
+class FrameAggregator:
+    """GPU-backed FrameAggregator(maxAggregatedLength): IDecoder<Frame,Frame>
+    (FrameAggregator.java:40-104).  decode() of one frame runs a one-frame batch;
+    for throughput, BatchAggregator aggregates whole decoded batches."""
+
+    def __init__(self, maxAggregatedLength: int, ctx: Context | None = None):
+        self._b = BatchAggregator(1, maxAggregatedLength, ctx)
+
+    def getInboundType(self):
+        return Frame
+
+    def getOutboundType(self):
+        return Frame
+
+    def decode(self, session, data: Frame, out: list):
+        payload = bytes(data.getPayload())
+        desc = np.zeros(1, dtype=DESC_DTYPE)
+        desc[0]["payload_len"] = len(payload)
+        desc[0]["opcode"] = int(data.getOpcode())
+        desc[0]["flags"] = (0x80 if data.isFinalFragment() else 0) | ((data.getRsvBits() & 7) << 4)
+        res = np.zeros(1, dtype=RESULT_DTYPE)
+        res[0]["n_delivered"] = 1
+        pl = np.frombuffer(payload + bytes(16), dtype=np.uint8)
+        frames, exc = self._b.run(desc, np.array([0, 1], np.uint32), res, pl)[0]
+        if exc is not None:
+            _writenf(session, CloseFrame.of_status(exc.close_code))  # tooBig: CloseFrame.TOO_BIG (:66-69)
+            raise exc
+        for f in frames:
+            out.append(data if not isinstance(f, (AggregatedTextFrame, AggregatedBinaryFrame)) else f)

@@ -10,7 +10,7 @@ import ctypes as C
 import numpy as np
 
 from . import _lib
-from ._lib import DESC_DTYPE, ENCODE_DTYPE, RESULT_DTYPE, STATE_DTYPE, DecoderCfg, check, lib
+from ._lib import AGG_STATE_DTYPE, DESC_DTYPE, ENCODE_DTYPE, RESULT_DTYPE, STATE_DTYPE, DecoderCfg, check, lib
 
 MESSAGES = {
     1: "Unexpected opcode value ({d})",
@@ -30,6 +30,7 @@ MESSAGES = {
     15: "Negative payload length ({d})",
     16: "Extended payload length ({d}) > {d2}",
     17: "Malformed batch (frame extent does not match its header)",
+    18: "Too big payload for aggregated frame",
 }
 
 
@@ -162,6 +163,41 @@ class Context:
         check(lib.wsg_decode_batch_host_async(self._h, C.byref(cfg), _p(wire), wl, _p(frame_off), n_frames,
                                               _p(session_first), n_sessions, _p(state), _p(payload),
                                               int(np.prod(payload.shape)), _p(desc), _p(result)), self._h)
+
+    # -------------------------------------------------------------- aggregate
+    def aggregate_device(self, max_aggregated_len: int, desc, session_first, dec_result, payload, state, agg_out,
+                         out_desc, out_result, agg_total, n_frames: int | None = None):
+        """Enqueue FrameAggregator over a decoded device batch (wsg_aggregate_batch_device);
+        all arguments cuda tensors (desc / results / state as uint8 byte views)."""
+        n = desc.numel() // DESC_DTYPE.itemsize if n_frames is None else int(n_frames)
+        n_s = session_first.numel() - 1
+        check(lib.wsg_aggregate_batch_device(self._h, int(max_aggregated_len), _p(desc), n, _p(session_first), n_s,
+                                             _p(dec_result), _p(payload), payload.numel(), _p(state), _p(agg_out),
+                                             agg_out.numel(), _p(out_desc), _p(out_result), _p(agg_total)), self._h)
+
+    def aggregate_host(self, max_aggregated_len: int, desc: np.ndarray, session_first: np.ndarray,
+                       dec_result: np.ndarray, payload: np.ndarray, state: np.ndarray):
+        """FrameAggregator over a decoded host batch (wsg_aggregate_batch_host).  `state`
+        (AGG_STATE_DTYPE) is updated in place.  Returns (agg_out, out_desc, out_result):
+        session s's outputs are out_desc[session_first[s] + s + i]."""
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        session_first = np.ascontiguousarray(session_first, dtype=np.uint32)
+        dec_result = np.ascontiguousarray(dec_result, dtype=RESULT_DTYPE)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        assert state.dtype == AGG_STATE_DTYPE and state.flags.c_contiguous
+        n, n_s = len(desc), len(session_first) - 1
+        cap = int(desc["payload_len"].astype(np.uint64).sum()) + 16
+        agg = np.zeros(cap, dtype=np.uint8)
+        out_desc = np.zeros(n + n_s + 1, dtype=DESC_DTYPE)
+        out_res = np.zeros(max(1, n_s), dtype=RESULT_DTYPE)
+        total = C.c_uint64(0)
+        d = desc if n else np.zeros(1, DESC_DTYPE)
+        pl = payload if payload.size else np.zeros(16, np.uint8)
+        check(lib.wsg_aggregate_batch_host(self._h, int(max_aggregated_len), d.ctypes.data, n,
+                                           session_first.ctypes.data, n_s, dec_result.ctypes.data, pl.ctypes.data,
+                                           payload.size, state.ctypes.data, agg.ctypes.data, cap,
+                                           out_desc.ctypes.data, out_res.ctypes.data, C.byref(total)), self._h)
+        return agg[:total.value], out_desc[:n + n_s], out_res[:n_s]
 
     # -------------------------------------------------------------- encode
     def encode_device(self, client_mode: bool, payload, frames, session_first, closed, wire_out, wire_off):

@@ -1,0 +1,513 @@
+// aggregate.hip — FrameAggregator on gfx950 (FrameAggregator.java:72-104,
+// PayloadAggregator.java:32-73), run over a decoded batch.
+//
+// The reference keeps one aggregated frame per session and appends each
+// continuation's payload to it.  Here the per-session sequence becomes scans:
+//   an aggregated frame is open before frame k  <=>  the last TEXT/BINARY non-FIN
+//   frame ("start") before k comes after the last FIN continuation ("end") before
+//   k (a FIN continuation closes an open frame and leaves a closed one closed;
+//   a start opens or replaces) — two max-scans, session-segmented by comparing
+//   with session_first, the carried-in state standing for "before the batch";
+// member frames (starts, and continuations while open) have their payload bytes
+// laid back to back in agg_out by a sum-scan, so every aggregated message is one
+// contiguous range; the "too big" test of continuation k (:92-94) is the bytes of
+// its message before k (+ the bytes carried in) + its own length > max.
+//
+//   k_agg_a      thread per frame: class bits, block maxima of start / end indices
+//   k_agg_scan   one workgroup: exclusive scans of the block aggregates
+//   k_agg_b      thread per frame: open-before-k, membership, emit flag; block sums
+//                of member bytes and emitted frames
+//   k_agg_c      thread per frame: "too big" test, output descriptors, gather
+//                records, and the 1 KiB agg_out pieces starting in each member
+//   k_agg_gather one wave per 1 KiB piece of agg_out (grid-stride: the piece count
+//                is known only on the device): 16-B aligned stores, sources
+//                funnelled from aligned loads
+//   k_agg_final  thread per session: result, carry-out state, PENDING entry
+#include "wsgpu_internal.h"
+#include "wsgpu_scan.h"
+
+namespace ws {
+
+constexpr uint32_t AG_VALID = 1u;    // delivered by the decoder (the aggregator sees it)
+constexpr uint32_t AG_START = 2u;    // TEXT/BINARY, not FIN: opens (or replaces) the aggregated frame
+constexpr uint32_t AG_END = 4u;      // CONTINUATION, FIN
+constexpr uint32_t AG_CONT = 8u;     // CONTINUATION
+constexpr uint32_t AG_MEMBER = 16u;  // its payload belongs to the aggregated frame
+constexpr uint32_t AG_EMIT = 32u;    // emits an output frame (itself, or the aggregated frame)
+constexpr uint32_t AG_CARRY = 64u;   // member of the frame carried in from an earlier batch
+
+__device__ __forceinline__ uint64_t agg_pos(const AggArgs& a, uint64_t j) { return a.pl[j] + a.blk_sum[j / BLOCK]; }
+// cl / blk_cnt pack two counts: emitted frames (bits 0-31) and non-empty members (32-63)
+__device__ __forceinline__ uint64_t agg_cnt(const AggArgs& a, uint64_t j) {
+  return (a.cl[j] + a.blk_cnt[j / BLOCK]) & 0xffffffffull;
+}
+__device__ __forceinline__ uint64_t agg_mi(const AggArgs& a, uint64_t j) { return (a.cl[j] + a.blk_cnt[j / BLOCK]) >> 32; }
+
+// ------------------------------------------------------------------ k_agg_a
+__global__ __launch_bounds__(BLOCK) void k_agg_a(AggArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  Agg v = AGG_ID;
+  if (k < a.n_frames) {
+    const uint32_t s = find_session(a.session_first, a.n_sessions, k);
+    const bool valid = k - a.session_first[s] < a.dec_result[s].n_delivered;
+    uint32_t c = 0;
+    if (valid) {
+      const wsg_frame_desc d = a.desc[k];
+      const bool fin = (d.flags & 0x80u) != 0;
+      c = AG_VALID;
+      if ((d.opcode == WSG_OP_TEXT || d.opcode == WSG_OP_BINARY) && !fin) c |= AG_START;
+      if (d.opcode == WSG_OP_CONTINUATION) c |= AG_CONT | (fin ? AG_END : 0u);
+    }
+    a.code[k] = c;
+    a.sess[k] = s;
+    v.m0 = (c & AG_START) ? (int32_t)k : -1;
+    v.m1 = (c & AG_END) ? (int32_t)k : -1;
+  }
+  Agg tot;
+  block_excl_scan(v, &tot);
+  if (threadIdx.x == 0) {
+    a.blk_max[blockIdx.x] = tot.m0;
+    a.blk_max[a.nblk + blockIdx.x] = tot.m1;
+  }
+}
+
+// ------------------------------------------------------------------ k_agg_scan
+// One workgroup: exclusive scans of the block aggregates in place.  sums = 0:
+// the start / end maxima; sums = 1: member bytes and emitted frames (+ the total).
+__global__ __launch_bounds__(1024) void k_agg_scan(AggArgs a, int sums) {
+  Agg carry = AGG_ID;    // maxima (sums == 0) or member bytes (sums == 1)
+  uint64_t carry_n = 0;  // emitted frames (sums == 1)
+  for (uint32_t base = 0; base < a.nblk; base += 1024) {
+    const uint32_t b = base + threadIdx.x;
+    Agg v = AGG_ID, tot;
+    if (sums) {
+      Agg n = AGG_ID, tn;
+      if (b < a.nblk) {
+        v.sum = a.blk_sum[b];
+        n.sum = a.blk_cnt[b];
+      }
+      const Agg ev = block_excl_scan(v, &tot);
+      const Agg en = block_excl_scan(n, &tn);
+      if (b < a.nblk) {
+        a.blk_sum[b] = carry.sum + ev.sum;
+        a.blk_cnt[b] = carry_n + en.sum;
+      }
+      carry.sum += tot.sum;
+      carry_n += tn.sum;
+    } else {
+      if (b < a.nblk) {
+        v.m0 = a.blk_max[b];
+        v.m1 = a.blk_max[a.nblk + b];
+      }
+      const Agg ex = agg_op(carry, block_excl_scan(v, &tot));
+      if (b < a.nblk) {
+        a.blk_max[b] = ex.m0;
+        a.blk_max[a.nblk + b] = ex.m1;
+      }
+      carry = agg_op(carry, tot);
+    }
+  }
+  if (sums && threadIdx.x == 0) {
+    *a.agg_total = carry.sum;
+    *a.n_mem = carry_n >> 32;
+  }
+}
+
+// ------------------------------------------------------------------ k_agg_b
+__global__ __launch_bounds__(BLOCK) void k_agg_b(AggArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const bool live = k < a.n_frames;
+  uint32_t c = live ? a.code[k] : 0u;
+  Agg v = AGG_ID;
+  v.m0 = (c & AG_START) ? (int32_t)k : -1;
+  v.m1 = (c & AG_END) ? (int32_t)k : -1;
+  Agg tot;
+  Agg ex = block_excl_scan(v, &tot);
+  Agg w = AGG_ID;
+  uint64_t emit = 0;  // emitted frame (bit 0) | non-empty member (bit 32)
+  if (live) {
+    const int32_t bs = a.blk_max[blockIdx.x], be = a.blk_max[a.nblk + blockIdx.x];
+    const int32_t ls = ex.m0 > bs ? ex.m0 : bs, le = ex.m1 > be ? ex.m1 : be;
+    a.last[k] = ls;
+    a.last[a.n_frames + k] = le;
+    if (c & AG_VALID) {
+      const uint32_t s = a.sess[k];
+      const int32_t sf = (int32_t)a.session_first[s];
+      const bool in_batch = (ls > le ? ls : le) >= sf;
+      const bool open = in_batch ? ls > le : a.state[s].open != 0;  // FrameAggregator.frame != null
+      const bool member = (c & AG_START) || ((c & AG_CONT) && open);
+      const bool em = !member || ((c & AG_END) && open);  // out.add(data) (:103)
+      if (member) {
+        c |= AG_MEMBER;
+        if (!(c & AG_START) && ls < sf) c |= AG_CARRY;
+        w.sum = a.desc[k].payload_len;
+        if (w.sum) emit |= 1ull << 32;
+      }
+      if (em) { c |= AG_EMIT; emit |= 1u; }
+      a.code[k] = c;
+    }
+  }
+  Agg tw;
+  const Agg ew = block_excl_scan(w, &tw);
+  Agg e = AGG_ID;
+  e.sum = emit;
+  Agg te;
+  const Agg ee = block_excl_scan(e, &te);
+  if (live) {
+    a.pl[k] = ew.sum;
+    a.cl[k] = ee.sum;
+  }
+  if (threadIdx.x == 0) {
+    a.blk_sum[blockIdx.x] = tw.sum;
+    a.blk_cnt[blockIdx.x] = te.sum;
+  }
+}
+
+// ------------------------------------------------------------------ k_agg_c
+__global__ __launch_bounds__(BLOCK) void k_agg_c(AggArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool live = k < a.n_frames;
+  const uint32_t c = live ? a.code[k] : 0u;
+  // every record carries its position (non-members too: the gather's owner search
+  // needs positions non-decreasing over all frames)
+  uint64_t pos = live ? agg_pos(a, k) : 0ull, src = 0;
+  uint32_t mlen = 0;
+  if (c & AG_VALID) {
+    const uint32_t s = a.sess[k];
+    const uint32_t sf = a.session_first[s];
+    const wsg_frame_desc d = a.desc[k];
+    if (c & AG_MEMBER) {
+      mlen = d.payload_len;
+      src = d.payload_off;
+    }
+    uint64_t first = 0;
+    wsg_agg_state st = {0, 0, 0, 0, 0u};
+    if ((c & AG_MEMBER) || (c & AG_END)) {
+      st = a.state[s];
+      first = (c & AG_START) ? k : ((c & AG_CARRY) ? (uint64_t)sf : (uint64_t)a.last[k]);
+    }
+    if ((c & AG_MEMBER) && !(c & AG_START)) {  // a continuation of an open aggregated frame
+      const uint64_t held = ((c & AG_CARRY) ? (uint64_t)st.length : 0ull) + (pos - agg_pos(a, first));
+      if ((int64_t)(held + d.payload_len) > a.max_len)  // tooBig, FrameAggregator.java:92-94
+        atomicMin((unsigned long long*)&a.sess_err[s], (unsigned long long)k);
+    }
+    if (c & AG_EMIT) {
+      wsg_frame_desc o;
+      if (c & AG_MEMBER) {  // the FIN continuation: the aggregated frame (:97-100)
+        const uint64_t p0 = agg_pos(a, first);
+        uint32_t op, rsv;
+        if (c & AG_CARRY) {
+          op = st.opcode;
+          rsv = st.rsv;
+        } else {
+          const wsg_frame_desc ds = a.desc[first];
+          op = ds.opcode;
+          rsv = (ds.flags >> 4) & 7u;
+        }
+        o.payload_off = p0;
+        o.payload_len = (uint32_t)(pos + d.payload_len - p0);
+        o.opcode = (uint8_t)op;
+        o.flags = (uint8_t)(0x80u | (rsv << 4) | WSG_AGG_IN_AGG | ((c & AG_CARRY) ? WSG_AGG_PREFIXED : 0u));
+      } else {  // passed through unchanged (:103)
+        o = d;
+        o.flags = (uint8_t)(d.flags & 0xF1u);
+      }
+      o.status = 0;
+      a.out_desc[(uint64_t)sf + s + (agg_cnt(a, k) - agg_cnt(a, sf))] = o;
+    }
+  }
+  uint32_t mi = 0;
+  if (mlen) {  // the gather records are compacted to the non-empty members
+    mi = (uint32_t)agg_mi(a, k);
+    AggRec r;
+    r.pos = pos;
+    r.src = src;
+    r.mlen = mlen;
+    r.pad = 0;
+    a.rec[mi] = r;
+  }
+  // descriptors of the agg_out pieces whose first byte falls in this member's range,
+  // written cooperatively (as decode.hip k_link): a wave scan of the counts, then
+  // lane i writes the wave's pieces i, i+64, ... after a shuffle search for the owner
+  const uint64_t end = pos + mlen;
+  const uint32_t pc0 = (uint32_t)((pos + PIECE - 1) / PIECE);
+  uint32_t cnt = 0;
+  if (mlen) {
+    uint64_t p1 = (end + PIECE - 1) / PIECE;
+    if (p1 > a.n_pieces) p1 = a.n_pieces;
+    cnt = p1 > pc0 ? (uint32_t)(p1 - pc0) : 0u;
+  }
+  uint32_t cum = cnt;
+#pragma unroll
+  for (int sd = 1; sd < 64; sd <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)cum, sd, 64);
+    if (lane >= sd) cum += t;
+  }
+  const uint32_t T = (uint32_t)__shfl((int)cum, 63, 64);
+  cum -= cnt;
+  if (!T) return;
+  const uint64_t total = *a.agg_total;
+  for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
+    int o = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+      if ((uint32_t)__shfl((int)cum, o + step, 64) <= t) o += step;
+    const uint32_t o_cum = (uint32_t)__shfl((int)cum, o, 64);
+    const uint32_t o_pc0 = (uint32_t)__shfl((int)pc0, o, 64);
+    const uint64_t o_pos = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pos >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)pos, o, 64);
+    const uint64_t o_src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(src >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)src, o, 64);
+    const uint32_t o_len = (uint32_t)__shfl((int)mlen, o, 64);
+    const uint32_t o_k = (uint32_t)__shfl((int)mi, o, 64);
+    if (t >= T) continue;
+    const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
+    const uint64_t ps = pc * PIECE;
+    const uint64_t o_end = o_pos + o_len;
+    const uint32_t j0 = (uint32_t)(ps - o_pos);
+    const bool single = o_end >= ps + PIECE || o_end == total;
+    PieceDesc pd;
+    pd.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(o_end - ps < PIECE ? o_end - ps : PIECE) << PD_NB_SHIFT) |
+              (single ? 0ull : PD_MULTI);
+    pd.mask = 0;
+    pd.frame = o_k;
+    a.pieces[pc] = pd;
+  }
+}
+
+// ------------------------------------------------------------------ k_agg_gather
+__device__ __forceinline__ uint32_t ag_dpp_from_next(uint32_t v, uint32_t old) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
+}
+
+__device__ __forceinline__ void ag_store16(const AggArgs& a, uint64_t o, uint64_t lim, const uint32_t w[4]) {
+  if (o + 16 <= lim) {
+    __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (u32x4*)(a.agg_out + o));
+  } else {  // agg_out is not padded
+#pragma unroll
+    for (uint32_t i = 0; i < 16u; ++i)
+      if (o + i < lim) a.agg_out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
+  }
+}
+
+// 16 payload bytes at an arbitrary offset, from 4-B aligned loads (the payload
+// buffer is the decoder's, padded to 16-B slots: reading 4 bytes past a slot's
+// end stays inside the buffer except at its very end, where byte loads take over)
+__device__ __forceinline__ void ag_load16(const AggArgs& a, uint64_t s, uint64_t src_lim, uint32_t w[4]) {
+  const uint64_t a4 = s & ~3ull;
+  const uint32_t sh = (uint32_t)(s & 3u);
+  uint32_t dd[5];
+  if (a4 + 20u <= src_lim) {
+    const uint32_t* q = (const uint32_t*)(a.payload + a4);
+    dd[0] = q[0]; dd[1] = q[1]; dd[2] = q[2]; dd[3] = q[3]; dd[4] = q[4];
+  } else {
+#pragma unroll
+    for (int i = 0; i < 5; ++i) dd[i] = 0u;
+#pragma unroll
+    for (uint32_t i = 0; i < 20u; ++i)
+      if (a4 + i < src_lim) dd[i >> 2] |= (uint32_t)a.payload[a4 + i] << (8 * (i & 3));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) w[i] = alignbyte(dd[i + 1], dd[i], sh);
+}
+
+__global__ __launch_bounds__(64) void k_agg_gather(AggArgs a, uint64_t src_lim) {
+  const int lane = threadIdx.x;
+  const uint64_t total = *a.agg_total;
+  const uint64_t lim = total < a.agg_cap ? total : a.agg_cap;
+  const uint64_t np = (lim + PIECE - 1) / PIECE;
+  const uint64_t n_mem = *a.n_mem;
+  for (uint64_t p = blockIdx.x; p < np; p += gridDim.x) {
+    const PieceDesc d = a.pieces[p];
+    const uint64_t ps = p * PIECE;
+    const uint64_t o = ps + (uint64_t)lane * 16u;
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    if (!(d.info & PD_MULTI)) {  // the piece lies in one member's bytes
+      const uint64_t s = d.info & PD_SRC_MASK;
+      const uint32_t nb = (uint32_t)(d.info >> PD_NB_SHIFT) & 2047u;
+      const uint64_t a16 = s & ~15ull;
+      const uint32_t sh = (uint32_t)(s & 15u), b = sh & 3u;
+      u32x4 A, nx;
+      if (a16 + PIECE + 16u <= src_lim) {
+        A = *(const u32x4*)(a.payload + a16 + (uint64_t)lane * 16u);
+        nx = *(const u32x4*)(a.payload + a16 + PIECE);
+      } else {
+        uint32_t dd[4] = {0u, 0u, 0u, 0u}, ee[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t i = 0; i < 16u; ++i) {
+          if (a16 + lane * 16u + i < src_lim) dd[i >> 2] |= (uint32_t)a.payload[a16 + lane * 16u + i] << (8 * (i & 3));
+          if (a16 + PIECE + i < src_lim) ee[i >> 2] |= (uint32_t)a.payload[a16 + PIECE + i] << (8 * (i & 3));
+        }
+        A = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+        nx = (u32x4){ee[0], ee[1], ee[2], ee[3]};
+      }
+      const uint32_t W0 = A.x, W1 = A.y, W2 = A.z, W3 = A.w;
+      const uint32_t W4 = ag_dpp_from_next(A.x, nx.x), W5 = ag_dpp_from_next(A.y, nx.y);
+      const uint32_t W6 = ag_dpp_from_next(A.z, nx.z), W7 = ag_dpp_from_next(A.w, nx.w);
+      switch (sh >> 2) {  // wave-uniform
+        case 0: w[0] = alignbyte(W1, W0, b); w[1] = alignbyte(W2, W1, b); w[2] = alignbyte(W3, W2, b); w[3] = alignbyte(W4, W3, b); break;
+        case 1: w[0] = alignbyte(W2, W1, b); w[1] = alignbyte(W3, W2, b); w[2] = alignbyte(W4, W3, b); w[3] = alignbyte(W5, W4, b); break;
+        case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
+        default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
+      }
+      if ((uint32_t)lane * 16u < nb) ag_store16(a, o, lim, w);
+      continue;
+    }
+    // several members in the piece: lane l takes member record d.frame + l (records
+    // are the non-empty members, dense and in order), and the owner of byte o is the
+    // last record starting at or before o, found by a shuffle search
+    const uint64_t pend = ps + PIECE < lim ? ps + PIECE : lim;
+    const bool live = o < pend;
+    const uint64_t fl = (uint64_t)d.frame + (uint64_t)lane;
+    const bool have = fl < n_mem;
+    AggRec rl;
+    if (have) rl = a.rec[fl];
+    else { rl.pos = ~0ull; rl.mlen = 0; rl.src = 0; }
+    uint32_t lk = d.frame;
+    AggRec lr;
+    if (__any(have && rl.mlen && rl.pos + rl.mlen >= pend)) {
+      const int key = rl.pos >= pend ? 4096 : (rl.pos <= ps ? 0 : (int)(rl.pos - ps));
+      int posn = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1)
+        if (__shfl(key, posn + step, 64) <= lane * 16) posn += step;
+      lk = d.frame + (uint32_t)posn;
+      lr = a.rec[lk];
+    } else {  // more than 64 records (empty ones) reach into the piece: walk them
+      uint32_t kk = d.frame;
+      AggRec rr = a.rec[kk];
+      lr = rr;
+      for (;;) {
+        const bool beyond = live && o >= rr.pos + rr.mlen;
+        if (!__any(beyond) || kk + 1 >= n_mem) break;
+        ++kk;
+        rr = a.rec[kk];
+        if (beyond && rr.mlen) { lk = kk; lr = rr; }
+      }
+    }
+    if (!live) continue;
+    // the lane's 16 bytes may span members: byte-wise over consecutive records
+    if (o >= lr.pos && o + 16 <= lr.pos + lr.mlen) {
+      ag_load16(a, lr.src + (o - lr.pos), src_lim, w);
+    } else {
+      uint64_t blo = 0, bhi = 0;
+      uint32_t kk = lk;
+      AggRec rr = lr;
+      for (uint32_t i = 0; i < 16u; ++i) {
+        const uint64_t x = o + i;
+        if (x >= pend) break;
+        while (x >= rr.pos + rr.mlen && kk + 1 < n_mem) rr = a.rec[++kk];
+        const uint64_t byte = a.payload[rr.src + (x - rr.pos)];
+        if (i < 8) blo |= byte << (8 * i);
+        else bhi |= byte << (8 * (i - 8));
+      }
+      w[0] = (uint32_t)blo; w[1] = (uint32_t)(blo >> 32); w[2] = (uint32_t)bhi; w[3] = (uint32_t)(bhi >> 32);
+    }
+    ag_store16(a, o, pend, w);
+  }
+}
+
+// ------------------------------------------------------------------ k_agg_final
+__global__ __launch_bounds__(256) void k_agg_final(AggArgs a) {
+  const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s >= a.n_sessions) return;
+  const uint32_t sf = a.session_first[s];
+  const uint32_t nd = a.dec_result[s].n_delivered;
+  wsg_agg_state st = a.state[s];
+  wsg_session_result res = {0u, 0u, 0u, 0};
+  const uint64_t fe = a.sess_err[s];
+  if (fe != ~0ull) a.sess_err[s] = ~0ull;  // back to the idle state for the next batch
+  const uint64_t base = (uint64_t)sf + s;
+  if (nd == 0) {
+    if (st.open) {  // the carried frame stays open: an empty PENDING entry
+      wsg_frame_desc o = {0ull, 0u, st.opcode, (uint8_t)((st.rsv << 4) | WSG_AGG_IN_AGG | WSG_AGG_PREFIXED |
+                                                        WSG_AGG_PENDING), 0};
+      a.out_desc[base] = o;
+    }
+    a.out_result[s] = res;
+    return;
+  }
+  const uint64_t cs = agg_cnt(a, sf);
+  if (fe != ~0ull) {  // "Too big payload for aggregated frame" + CloseFrame(1009), :66-69
+    res.n_delivered = (uint32_t)(agg_cnt(a, fe) - cs);
+    res.error = WSG_E_AGG_TOO_BIG;
+    res.close_code = WSG_CLOSE_TOO_BIG;
+    res.detail = (int64_t)(fe - sf);
+    // the aggregator keeps the open frame (without the failing fragment)
+    const uint32_t c = a.code[fe];
+    const uint64_t first = (c & AG_CARRY) ? (uint64_t)sf : (uint64_t)a.last[fe];
+    const uint64_t inb = agg_pos(a, fe) - agg_pos(a, first);
+    if (!(c & AG_CARRY)) {
+      const wsg_frame_desc ds = a.desc[first];
+      st.opcode = ds.opcode;
+      st.rsv = (ds.flags >> 4) & 7u;
+      st.length = (uint32_t)inb;
+    } else {
+      st.length += (uint32_t)inb;
+    }
+    st.open = 1;
+    a.state[s] = st;
+    a.out_result[s] = res;
+    return;
+  }
+  const uint64_t L = (uint64_t)sf + nd - 1;
+  const uint32_t c = a.code[L];
+  res.n_delivered = (uint32_t)(agg_cnt(a, L) + ((c & AG_EMIT) ? 1u : 0u) - cs);
+  bool open;
+  if (c & AG_START) open = true;
+  else if (c & AG_END) open = false;
+  else {
+    const int32_t ls = a.last[L], le = a.last[a.n_frames + L];
+    open = (ls > le ? ls : le) >= (int32_t)sf ? ls > le : st.open != 0;
+  }
+  if (open) {
+    const int32_t ls = (c & AG_START) ? (int32_t)L : a.last[L];
+    const bool carry = ls < (int32_t)sf;
+    const uint64_t first = carry ? (uint64_t)sf : (uint64_t)ls;
+    const uint64_t p0 = agg_pos(a, first);
+    const uint64_t inb = agg_pos(a, L) + ((c & AG_MEMBER) ? a.desc[L].payload_len : 0u) - p0;
+    if (!carry) {
+      const wsg_frame_desc ds = a.desc[first];
+      st.opcode = ds.opcode;
+      st.rsv = (ds.flags >> 4) & 7u;
+      st.length = (uint32_t)inb;
+    } else {
+      st.length += (uint32_t)inb;
+    }
+    st.open = 1;
+    wsg_frame_desc o;
+    o.payload_off = p0;
+    o.payload_len = (uint32_t)inb;
+    o.opcode = st.opcode;
+    o.flags = (uint8_t)((st.rsv << 4) | WSG_AGG_IN_AGG | WSG_AGG_PENDING | (carry ? WSG_AGG_PREFIXED : 0u));
+    o.status = 0;
+    a.out_desc[base + res.n_delivered] = o;
+  } else {
+    st.open = 0;
+    st.opcode = 0;
+    st.rsv = 0;
+    st.length = 0;
+  }
+  a.state[s] = st;
+  a.out_result[s] = res;
+}
+
+// ------------------------------------------------------------------ launchers
+void launch_agg_plan(const AggArgs& a, hipStream_t s) {
+  if (!a.n_frames) return;
+  hipLaunchKernelGGL(k_agg_a, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 0);
+  hipLaunchKernelGGL(k_agg_b, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 1);
+  hipLaunchKernelGGL(k_agg_c, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+}
+void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim) {
+  // grid-stride over the pieces (their number is known only on the device)
+  const uint64_t g = a.n_pieces < 65536 ? a.n_pieces : 65536;
+  if (a.n_frames && g) hipLaunchKernelGGL(k_agg_gather, dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
+}
+void launch_agg_final(const AggArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_agg_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);
+}
+
+}  // namespace ws

@@ -15,7 +15,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc"};
+                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -62,6 +62,8 @@ struct wsg_ctx {
   DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total, pieces, utf8_err;
   // encode workspace
   DevBuf esess, elast_close, epieces, epidx;
+  // aggregate workspace
+  DevBuf a_code, a_last, a_pl, a_cl, a_rec, a_blk, a_sess_err, a_pieces;
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -124,7 +126,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT)) {
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER)) {
     f();
     return;
   }
@@ -179,6 +181,8 @@ int wsg_close(wsg_ctx* c) {
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
+  DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl, &c->a_rec, &c->a_blk, &c->a_sess_err, &c->a_pieces};
+  for (DevBuf* b : abufs) b->release();
   for (HostSlot& hs : c->slot) {
     DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
     for (DevBuf* b : sb) b->release();
@@ -608,6 +612,115 @@ int wsg_encode_batch_host(wsg_ctx* c, int client_mode, const uint8_t* payload, u
   if (total) HIP_TRY(c, hipMemcpyAsync(wire_out, c->h_wire.p, total, hipMemcpyDeviceToHost, s));
   if (n_sessions) HIP_TRY(c, hipMemcpyAsync(closed, c->h_closed.p, n_sessions, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
+
+int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg_frame_desc* desc,
+                               uint64_t n_frames, const uint32_t* session_first, uint32_t n_sessions,
+                               const wsg_session_result* dec_result, const uint8_t* payload, uint64_t payload_len,
+                               wsg_agg_state* state, uint8_t* agg_out, uint64_t agg_cap, wsg_frame_desc* out_desc,
+                               wsg_session_result* out_result, uint64_t* agg_total) {
+  if (!c) return WSG_API_EINVAL;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  if (n_frames >= (1ull << 30)) return set_err(c, WSG_API_ERANGE, "too many frames in one batch (max 2^30 - 1)");
+  if (((uintptr_t)payload & 15) || ((uintptr_t)agg_out & 15))
+    return set_err(c, WSG_API_EINVAL, "payload and agg_out must be 16-B aligned");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t F = n_frames ? n_frames : 1;
+  const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
+  AggArgs a;
+  a.max_len = max_aggregated_len;
+  a.desc = desc;
+  a.n_frames = n_frames;
+  a.session_first = session_first;
+  a.n_sessions = n_sessions;
+  a.dec_result = dec_result;
+  a.payload = payload;
+  a.state = state;
+  a.agg_out = agg_out;
+  a.agg_cap = agg_cap;
+  a.out_desc = out_desc;
+  a.out_result = out_result;
+  a.agg_total = agg_total;
+  a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  a.n_pieces = agg_cap / PIECE + 1;
+  HIP_TRY(c, c->a_code.ensure(F * 2 * sizeof(uint32_t)));
+  HIP_TRY(c, c->a_last.ensure(F * 2 * sizeof(int32_t)));
+  HIP_TRY(c, c->a_pl.ensure(F * sizeof(uint64_t)));
+  HIP_TRY(c, c->a_cl.ensure(F * sizeof(uint64_t) + sizeof(uint64_t)));
+  HIP_TRY(c, c->a_rec.ensure(F * sizeof(AggRec)));
+  HIP_TRY(c, c->a_blk.ensure(nblk * (2 * sizeof(uint64_t) + 2 * sizeof(int32_t))));
+  HIP_TRY(c, c->a_sess_err.ensure((uint64_t)n_sessions * sizeof(uint64_t), 0xff, c->stream));
+  HIP_TRY(c, c->a_pieces.ensure((a.n_pieces + 1) * sizeof(PieceDesc)));
+  a.code = (uint32_t*)c->a_code.p;
+  a.sess = a.code + F;
+  a.last = (int32_t*)c->a_last.p;
+  a.pl = (uint64_t*)c->a_pl.p;
+  a.cl = (uint64_t*)c->a_cl.p;
+  a.n_mem = a.cl + F;
+  a.rec = (AggRec*)c->a_rec.p;
+  a.blk_sum = (uint64_t*)c->a_blk.p;
+  a.blk_cnt = a.blk_sum + nblk;
+  a.blk_max = (int32_t*)(a.blk_cnt + nblk);
+  a.sess_err = (uint64_t*)c->a_sess_err.p;
+  a.pieces = (PieceDesc*)c->a_pieces.p;
+  if (!n_frames) HIP_TRY(c, hipMemsetAsync(agg_total, 0, sizeof(uint64_t), c->stream));
+  timed(c, K_AGG, [&] { launch_agg_plan(a, c->stream); });
+  timed(c, K_AGG_GATHER, [&] { launch_agg_gather(a, c->stream, payload_len); });
+  timed(c, K_AGG_FINAL, [&] { launch_agg_final(a, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_aggregate_batch_host(wsg_ctx* c, int64_t max_aggregated_len, const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions, const wsg_session_result* dec_result,
+                             const uint8_t* payload, uint64_t payload_len, wsg_agg_state* state, uint8_t* agg_out,
+                             uint64_t agg_cap, wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                             uint64_t* agg_total) {
+  if (!c || !agg_total) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t S = n_sessions;
+  DevBuf d_desc, d_sf, d_res, d_pay, d_state, d_agg, d_odesc, d_ores, d_tot;
+  struct Guard {
+    DevBuf* b[9];
+    ~Guard() { for (DevBuf* x : b) x->release(); }
+  } g{{&d_desc, &d_sf, &d_res, &d_pay, &d_state, &d_agg, &d_odesc, &d_ores, &d_tot}};
+  HIP_TRY(c, d_desc.ensure((n_frames + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, d_sf.ensure((S + 1) * sizeof(uint32_t)));
+  HIP_TRY(c, d_res.ensure((S + 1) * sizeof(wsg_session_result)));
+  HIP_TRY(c, d_pay.ensure(payload_len + 32));
+  HIP_TRY(c, d_state.ensure((S + 1) * sizeof(wsg_agg_state)));
+  HIP_TRY(c, d_agg.ensure(agg_cap + 32));
+  HIP_TRY(c, d_odesc.ensure((n_frames + S + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  HIP_TRY(c, d_tot.ensure(sizeof(uint64_t)));
+  hipStream_t s = c->stream;
+  if (n_frames) HIP_TRY(c, hipMemcpyAsync(d_desc.p, desc, n_frames * sizeof(wsg_frame_desc), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(d_sf.p, session_first, (S + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  if (S) {
+    HIP_TRY(c, hipMemcpyAsync(d_res.p, dec_result, S * sizeof(wsg_session_result), hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(d_state.p, state, S * sizeof(wsg_agg_state), hipMemcpyHostToDevice, s));
+  }
+  if (payload_len) HIP_TRY(c, hipMemcpyAsync(d_pay.p, payload, payload_len, hipMemcpyHostToDevice, s));
+  int rc = wsg_aggregate_batch_device(c, max_aggregated_len, (const wsg_frame_desc*)d_desc.p, n_frames,
+                                      (const uint32_t*)d_sf.p, n_sessions, (const wsg_session_result*)d_res.p,
+                                      (const uint8_t*)d_pay.p, payload_len, (wsg_agg_state*)d_state.p,
+                                      (uint8_t*)d_agg.p, agg_cap, (wsg_frame_desc*)d_odesc.p,
+                                      (wsg_session_result*)d_ores.p, (uint64_t*)d_tot.p);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(agg_total, d_tot.p, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  const uint64_t used = *agg_total < agg_cap ? *agg_total : agg_cap;
+  if (used) HIP_TRY(c, hipMemcpyAsync(agg_out, d_agg.p, used, hipMemcpyDeviceToHost, s));
+  if (n_frames + S)
+    HIP_TRY(c, hipMemcpyAsync(out_desc, d_odesc.p, (n_frames + S) * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, s));
+  if (S) {
+    HIP_TRY(c, hipMemcpyAsync(out_result, d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(state, d_state.p, S * sizeof(wsg_agg_state), hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(c, hipStreamSynchronize(s));
+  if (*agg_total > agg_cap) return set_err(c, WSG_API_ERANGE, "agg_cap %llu < %llu", (unsigned long long)agg_cap,
+                                           (unsigned long long)*agg_total);
   return WSG_API_OK;
 }
 

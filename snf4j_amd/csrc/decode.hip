@@ -212,9 +212,14 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
     bp.m2 = a.blk_max[2 * a.nblk + blockIdx.x];
     ex = agg_op(bp, ex);
     const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
-    a.prev[k] = jd;
-    a.prev[a.n_frames + k] = jm;
-    a.prev[2 * a.n_frames + k] = ex.m2 >> 1;
+    // read only for continuation frames, the frames of a message still open, and a
+    // session's last frame when it is not a FIN message start (k_merge, k_final):
+    // a complete one-frame message (the common case) needs none
+    if (!(code_is_start(r.code) && (r.code & CODE_FIN))) {
+      a.prev[k] = jd;
+      a.prev[a.n_frames + k] = jm;
+      a.prev[2 * a.n_frames + k] = ex.m2 >> 1;
+    }
     const uint32_t s = r.sess;
     const int32_t sf = (int32_t)a.session_first[s];
     const wsg_session_state st = a.state[s];

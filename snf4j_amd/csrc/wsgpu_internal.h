@@ -84,6 +84,7 @@ struct DecodeArgs {
   // workspace
   FrameRec* rec;
   int32_t* prev;       // [3][n_frames]: last data / last TEXT|BINARY / last nonempty data frame before k
+                       // (not written for a FIN TEXT/BINARY frame: no reader needs it)
   uint32_t* edge;      // [2][n_frames]: first 3 / last 3 payload bytes (unmasked); the last 3 only
                        // for non-FIN data frames (the carry into the next fragment or batch)
   uint64_t* blk_sum;   // [nblk] slot-bytes per block -> exclusive prefix
@@ -119,10 +120,48 @@ struct EncodeArgs {
   uint32_t nblk;
 };
 
+struct AggRec {     // gather record of a non-empty member (aggregate.hip k_agg_c -> k_agg_gather)
+  uint64_t pos;     // agg_out offset of its member bytes
+  uint64_t src;     // payload offset of its bytes
+  uint32_t mlen;    // member bytes (0 for non-members)
+  uint32_t pad;
+};
+
+struct AggArgs {
+  int64_t max_len;
+  const wsg_frame_desc* desc;
+  uint64_t n_frames;
+  const uint32_t* session_first;
+  uint32_t n_sessions;
+  const wsg_session_result* dec_result;
+  const uint8_t* payload;
+  wsg_agg_state* state;
+  uint8_t* agg_out;
+  uint64_t agg_cap;
+  wsg_frame_desc* out_desc;
+  wsg_session_result* out_result;
+  uint64_t* agg_total;
+  // workspace
+  uint32_t* code;      // [n] AG_* bits
+  uint32_t* sess;      // [n]
+  int32_t* last;       // [2][n] last start / last end before k (batch index, -1 = none)
+  uint64_t* pl;        // [n] block-local exclusive member bytes
+  uint64_t* cl;        // [n] block-local exclusive (emitted frames | non-empty members << 32)
+  uint64_t* blk_sum;   // [nblk] member bytes -> exclusive prefix
+  uint64_t* blk_cnt;   // [nblk] (emitted frames | non-empty members << 32) -> exclusive prefix
+  int32_t* blk_max;    // [2][nblk] block maxima of start / end -> exclusive prefix
+  uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none), idle between batches
+  AggRec* rec;         // [n] gather records of the non-empty members, in order
+  uint64_t* n_mem;     // [1] number of non-empty members
+  struct PieceDesc* pieces;  // [n_pieces]: agg_out pieces (frame holding the first byte)
+  uint64_t n_pieces;
+  uint32_t nblk;
+};
+
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -138,6 +177,10 @@ void launch_enc_scan(const EncodeArgs& a, hipStream_t s);
 void launch_enc_desc(const EncodeArgs& a, hipStream_t s);
 void launch_enc_pieces(const EncodeArgs& a, hipStream_t s);
 void launch_enc_final(const EncodeArgs& a, hipStream_t s);
+
+void launch_agg_plan(const AggArgs& a, hipStream_t s);
+void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim);
+void launch_agg_final(const AggArgs& a, hipStream_t s);
 
 void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 void launch_synth_frames(const wsg_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s);

@@ -143,6 +143,30 @@ class PongFrame(ControlFrame):
         super().__init__(Opcode.PONG, rsvBits, payload)
 
 
+class AggregatedTextFrame(TextFrame):
+    """AggregatedTextFrame (AggregatedTextFrame.java:35-90): a final TEXT frame built by
+    FrameAggregator from a fragmented message; `fragments` lists the parts it was
+    assembled from on the host (one per batch the message spanned)."""
+
+    def __init__(self, rsvBits: int, payload, fragments=None):
+        super().__init__(True, rsvBits, payload)
+        self.fragments = fragments if fragments is not None else [bytes(payload)]
+
+    def getFragments(self):
+        return self.fragments
+
+
+class AggregatedBinaryFrame(BinaryFrame):
+    """AggregatedBinaryFrame (AggregatedBinaryFrame.java:35-72)."""
+
+    def __init__(self, rsvBits: int, payload, fragments=None):
+        super().__init__(True, rsvBits, payload)
+        self.fragments = fragments if fragments is not None else [bytes(payload)]
+
+    def getFragments(self):
+        return self.fragments
+
+
 def make_frame(opcode: int, fin: bool, rsv: int, payload: bytes) -> Frame:
     """FrameDecoder.createFrame's opcode -> class dispatch (FrameDecoder.java:104-145)."""
     op = Opcode(opcode)

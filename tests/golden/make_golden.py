@@ -425,8 +425,67 @@ def session_kats():
     return out
 
 
+def aggregator_kats():
+    """FrameAggregatorTest.testMaxLength :48-89 and testDecode :91-139, and
+    WebSocketSessionTest.testFrameAggregation :1334-1365, all FrameAggregator(100).
+    Each input frame lists what the reference asserts comes out of decode():
+    nothing, the input itself ("passthrough", the tests' `f == out.get(0)`), the
+    aggregated frame, or the 1009 exception."""
+    E = "Too big payload for aggregated frame"
+
+    def f(op, fin, rsv, payload, out=None, passthrough=False, err=False):
+        d = {"opcode": OPS[op], "fin": fin, "rsv": rsv, "payload": hx(payload)}
+        if err:
+            d["expect"] = {"error": E, "close_code": 1009}
+        elif passthrough:
+            d["expect"] = {"out": [{"opcode": OPS[op], "fin": fin, "rsv": rsv, "payload": hx(payload),
+                                    "passthrough": True}]}
+        elif out is not None:
+            o_op, o_rsv, o_payload = out
+            d["expect"] = {"out": [{"opcode": OPS[o_op], "fin": True, "rsv": o_rsv, "payload": hx(o_payload),
+                                    "passthrough": False}]}
+        else:
+            d["expect"] = {"out": []}
+        return d
+
+    src = "frame/FrameAggregatorTest.java"
+    max_length = [
+        f("BINARY", True, 0, bytes(101), passthrough=True),                  # :55-58
+        f("BINARY", False, 4, bytes(50)),                                     # :60-64
+        f("CONTINUATION", True, 0, bytes(50), out=("BINARY", 4, bytes(100))),  # :65-73
+        f("TEXT", False, 0, bytes(50)),                                       # :75-78
+        f("CONTINUATION", True, 0, bytes(51), err=True),                      # :79-88
+    ]
+    decode = [
+        f("TEXT", True, 0, b"ABC", passthrough=True),                         # :97-100
+        f("PING", True, 0, b"", passthrough=True),                            # :102-106
+        f("TEXT", False, 0, b"ABC"),                                          # :108-110
+        f("CONTINUATION", False, 0, b"DEF"),                                  # :111-112
+        f("PING", True, 0, b"", passthrough=True),                            # :113-115
+        f("CONTINUATION", True, 0, b"GH", out=("TEXT", 0, b"ABCDEFGH")),      # :117-119
+        f("BINARY", False, 0, b"ABC"),                                        # :121-123
+        f("CONTINUATION", False, 0, b"DEF"),                                  # :124-125
+        f("PING", True, 0, b"", passthrough=True),                            # :126-128
+        f("CONTINUATION", True, 0, b"GH", out=("BINARY", 0, b"ABCDEFGH")),    # :130-132
+        f("CONTINUATION", True, 0, b"GH", passthrough=True),                  # :134-138
+    ]
+    session = [
+        f("TEXT", True, 0, b"ABC", passthrough=True),                         # :1340-1343
+        f("TEXT", False, 0, b"BCD"),                                          # :1345-1347
+        f("PING", True, 0, b"", passthrough=True),                            # :1348-1350
+        f("CONTINUATION", False, 0, b"EFG"),                                  # :1351-1353
+        f("CONTINUATION", True, 0, b"HIJ", out=("TEXT", 0, b"BCDEFGHIJ")),    # :1354-1357
+        f("BINARY", False, 0, bytes(99)),                                     # :1359-1361
+        f("CONTINUATION", False, 0, bytes(2), err=True),                      # :1362-1365 (CLOSE=1009)
+    ]
+    return [{"src": src + ":48-89", "max": 100, "frames": max_length},
+            {"src": src + ":91-139", "max": 100, "frames": decode},
+            {"src": "WebSocketSessionTest.java:1334-1365", "max": 100, "frames": session}]
+
+
 def main():
     data = {
+        "aggregator": aggregator_kats(),
         "builder": builder_kats(),
         "decode": decode_kats(),
         "available": available_kats(),

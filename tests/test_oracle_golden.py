@@ -199,3 +199,25 @@ def test_stream_chunking_independence(oracle):
         got, err = oracle.stream_decode(stream, chunks)
         assert err is None
         assert [(f.opcode, f.payload) for f in got] == [(f.opcode, f.payload) for f in ref]
+
+
+def test_aggregator_kat(oracle):
+    """FrameAggregatorTest / WebSocketSessionTest.testFrameAggregation vectors through the
+    oracle's FrameAggregator restatement."""
+    for seq in fixtures.load("aggregator"):
+        agg = oracle.Aggregator(seq["max"])
+        for i, f in enumerate(seq["frames"]):
+            exp = f["expect"]
+            payload = fixtures.unhex(f["payload"])
+            if "error" in exp:
+                with pytest.raises(oracle.InvalidFrame) as ei:
+                    agg.decode(f["opcode"], f["fin"], f["rsv"], payload)
+                assert str(ei.value) == exp["error"] and ei.value.close_code == exp["close_code"], (seq["src"], i)
+                break
+            got = agg.decode(f["opcode"], f["fin"], f["rsv"], payload)
+            if not exp["out"]:
+                assert got is None, (seq["src"], i)
+                continue
+            o = exp["out"][0]
+            assert (got.opcode, got.fin, got.rsv, got.payload) == \
+                   (o["opcode"], o["fin"], o["rsv"], fixtures.unhex(o["payload"])), (seq["src"], i)
