@@ -131,6 +131,9 @@ def main():
     ctx.set_timing(False)
     timing = ctx.timing()
     pipe = pipeline_breakdown(ctx, step, dev)
+    validator = None  # (before copy_ceiling, which overwrites the payload buffer)
+    if world == 1 and not args.no_extras and not args.binary:
+        validator = validator_line(ctx, dev, desc, sf, payload, n_s, F, P, args.extra_steps)
 
     # dominant kernel: k_piecesN reads each frame's payload bytes off the wire and writes them unmasked
     unmask_ms, unmask_n = timing["k_piecesN"]
@@ -206,12 +209,43 @@ def main():
         }
         if e2e:
             out["e2e_pinned"] = e2e
+        if validator:
+            out["validator_stage"] = validator
         if extras:
             out["configs_measured"] = extras
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:
         dist.destroy_process_group()
+
+
+def validator_line(ctx, dev, desc, sf, payload, n_s, F, P, steps):
+    """The standalone "ws-utf8-validator" stage (wsg_validate_batch_device: the split-off
+    validation a permessage-deflate session needs after inflate) over the decoded
+    headline batch's plain payloads: read-only streaming, roofline = payload bytes read."""
+    import torch
+    from snf4j_amd._lib import RESULT_DTYPE
+    vstate = torch.zeros(n_s * 8, dtype=torch.uint8, device=dev)
+    vres = torch.empty(n_s * 16, dtype=torch.uint8, device=dev)
+
+    def step():
+        vstate.zero_()
+        ctx.validate_device(desc, sf, payload, vstate, vres, n_frames=F)
+
+    step()
+    torch.cuda.synchronize(dev)
+    r = vres.cpu().numpy().view(RESULT_DTYPE)
+    assert int(r["error"].max()) == 0 and int(r["n_delivered"].sum()) == F
+    el, kms, pipe = _timed(ctx, step, steps, 2, dev, "k_piecesN")
+    alg = F * P
+    ach = alg / (kms / 1e3) / 1e9
+    return {"config": f"FrameUtf8Validator stage alone over {F} x {P} B plain TEXT payloads (decoded headline batch)",
+            "value": round(alg * steps / el / 2**30, 3), "unit": "GiB/s (payload)",
+            "ms_per_step": round(el / steps * 1e3, 4),
+            "roofline": {"kernel": "k_piecesN (validate only, no stores)", "achieved": round(ach, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                         "alg_bytes_per_launch": alg, "avg_launch_ms": round(kms, 4)},
+            "pipeline_ms": pipe}
 
 
 def pipeline_breakdown(ctx, step, dev, steps=5):

@@ -222,6 +222,26 @@ int wsg_decode_batch_host_async(wsg_ctx* ctx, const wsg_decoder_cfg* cfg,
                                 uint8_t* payload_out, uint64_t payload_cap,
                                 wsg_frame_desc* desc_out, wsg_session_result* result_out);
 
+/* FrameUtf8Validator alone — the "ws-utf8-validator" stage (FrameUtf8Validator.java:59-98)
+ * over frames whose payloads are already plain, for sessions where the fused
+ * validation cannot run (permessage-deflate: validation follows inflate,
+ * PerMessageDeflateExtension.java:316-326).  Every pointer is a device pointer.
+ *   desc[n_frames]                frame k: opcode, flags (FIN/RSV), payload at
+ *                                 payload[payload_off, +payload_len); ranges disjoint
+ *   session_first[0..n_sessions]  session s owns frames [session_first[s], session_first[s+1])
+ *   state[n_sessions]             carry in / out (text_open, tail; closed latches on failure)
+ *   result_out[n_sessions]        n_delivered = frames that passed; error WSG_E_TEXT_UTF8 (1007)
+ * A decode batch for such sessions runs with validate_utf8 = 0. */
+int wsg_validate_batch_device(wsg_ctx* ctx, const wsg_frame_desc* desc, uint64_t n_frames,
+                              const uint32_t* session_first, uint32_t n_sessions,
+                              const uint8_t* payload, uint64_t payload_len,
+                              wsg_session_state* state, wsg_session_result* result_out);
+/* Same contract with host pointers: H2D, validate, D2H, synchronise. */
+int wsg_validate_batch_host(wsg_ctx* ctx, const wsg_frame_desc* desc, uint64_t n_frames,
+                            const uint32_t* session_first, uint32_t n_sessions,
+                            const uint8_t* payload, uint64_t payload_len,
+                            wsg_session_state* state, wsg_session_result* result_out);
+
 /* FrameDecoder.available(ISession, byte[], off, len) for a decoder with no
  * pending partial payload (FrameDecoder.java:357-401): returns 0 if the header
  * is incomplete, the full frame length if available, otherwise len.  On the

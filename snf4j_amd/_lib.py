@@ -110,6 +110,8 @@ def _load():
         "wsg_synth_uniform": ([p, u64, u64, u32, u32, i32, i32, i32, p, p, p], i32),
         "wsg_copy_ceiling": ([p, p, p, u64, i32, P(C.c_double)], i32),
         "wsg_synth_frames": ([p, p, u64, p], i32),
+        "wsg_validate_batch_device": ([p, p, u64, p, u32, p, u64, p, p], i32),
+        "wsg_validate_batch_host": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_aggregate_batch_device": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, p], i32),
         "wsg_aggregate_batch_host": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, P(u64)], i32),
     }

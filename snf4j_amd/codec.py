@@ -363,3 +363,38 @@ class FrameAggregator:
             raise exc
         for f in frames:
             out.append(data if not isinstance(f, (AggregatedTextFrame, AggregatedBinaryFrame)) else f)
+
+
+class FrameUtf8Validator:
+    """GPU-backed FrameUtf8Validator: the "ws-utf8-validator" stage alone
+    (FrameUtf8Validator.java:40-100), for pipelines where validation cannot be fused
+    into the decode pass (permessage-deflate inflates between the two,
+    PerMessageDeflateExtension.java:316-326).  decode() of one frame runs a
+    one-frame batch (wsg_validate_batch_host); frames pass through unchanged."""
+
+    def __init__(self, ctx: Context | None = None):
+        self.ctx = ctx
+        self.state = np.zeros(1, dtype=STATE_DTYPE)
+
+    def getInboundType(self):
+        return Frame
+
+    def getOutboundType(self):
+        return Frame
+
+    def decode(self, session, frame: Frame, out: list):
+        ctx = self.ctx or default_context()
+        payload = bytes(frame.getPayload())
+        desc = np.zeros(1, dtype=DESC_DTYPE)
+        desc[0]["payload_len"] = len(payload)
+        desc[0]["opcode"] = int(frame.getOpcode())
+        desc[0]["flags"] = (0x80 if frame.isFinalFragment() else 0) | ((frame.getRsvBits() & 7) << 4)
+        self.state[0]["closed"] = 0  # the stage itself does not latch; the session closes on the exception
+        r = ctx.validate_host(desc, np.array([0, 1], np.uint32), np.frombuffer(payload + bytes(16), np.uint8),
+                              self.state)[0]
+        if r["error"]:
+            # the reference clears its context on FIN before validating (:83-88): a failed
+            # non-final frame leaves the context as it stands; the session closes anyway
+            _writenf(session, CloseFrame.of_status(int(r["close_code"])))
+            raise InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
+        out.append(frame)

@@ -164,6 +164,30 @@ class Context:
                                               _p(session_first), n_sessions, _p(state), _p(payload),
                                               int(np.prod(payload.shape)), _p(desc), _p(result)), self._h)
 
+    # -------------------------------------------------------------- validate (FrameUtf8Validator alone)
+    def validate_device(self, desc, session_first, payload, state, result_out, n_frames: int | None = None,
+                        payload_len: int | None = None):
+        """Enqueue the standalone UTF-8 validator stage over plain payloads (wsg_validate_batch_device)."""
+        n = desc.numel() // DESC_DTYPE.itemsize if n_frames is None else int(n_frames)
+        pl = payload.numel() if payload_len is None else int(payload_len)
+        check(lib.wsg_validate_batch_device(self._h, _p(desc), n, _p(session_first), session_first.numel() - 1,
+                                            _p(payload), pl, _p(state), _p(result_out)), self._h)
+
+    def validate_host(self, desc: np.ndarray, session_first: np.ndarray, payload: np.ndarray, state: np.ndarray):
+        """FrameUtf8Validator over a host batch of plain payloads; `state` updated in place.
+        Returns the per-session results."""
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        session_first = np.ascontiguousarray(session_first, dtype=np.uint32)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        assert state.dtype == STATE_DTYPE and state.flags.c_contiguous
+        n, n_s = len(desc), len(session_first) - 1
+        res = np.zeros(max(1, n_s), dtype=RESULT_DTYPE)
+        d = desc if n else np.zeros(1, DESC_DTYPE)
+        pl = payload if payload.size else np.zeros(16, np.uint8)
+        check(lib.wsg_validate_batch_host(self._h, d.ctypes.data, n, session_first.ctypes.data, n_s, pl.ctypes.data,
+                                          payload.size, state.ctypes.data, res.ctypes.data), self._h)
+        return res[:n_s]
+
     # -------------------------------------------------------------- aggregate
     def aggregate_device(self, max_aggregated_len: int, desc, session_first, dec_result, payload, state, agg_out,
                          out_desc, out_result, agg_total, n_frames: int | None = None):

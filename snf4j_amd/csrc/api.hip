@@ -64,6 +64,7 @@ struct wsg_ctx {
   DevBuf esess, elast_close, epieces, epidx;
   // aggregate workspace
   DevBuf a_code, a_last, a_pl, a_cl, a_rec, a_blk, a_sess_err, a_pieces;
+  DevBuf v_desc;  // validator-only mode: per-frame status scratch
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -181,7 +182,8 @@ int wsg_close(wsg_ctx* c) {
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
-  DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl, &c->a_rec, &c->a_blk, &c->a_sess_err, &c->a_pieces};
+  DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,     &c->a_rec,
+                     &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc};
   for (DevBuf* b : abufs) b->release();
   for (HostSlot& hs : c->slot) {
     DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
@@ -246,7 +248,7 @@ static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, 
   const uint64_t F = n_frames ? n_frames : 1;
   const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
   // + PIECES_PER_WAVE: k_piecesN reads its descriptors in groups
-  HIP_TRY(c, c->pieces.ensure((piece_bound(wire_len, F) + PIECES_PER_WAVE) * sizeof(PieceDesc)));
+  HIP_TRY(c, c->pieces.ensure((piece_bound(wire_len, F) + 8) * sizeof(PieceDesc)));
   // utf8_err / sess_err are kept in their idle state between batches (k_merge and
   // k_final reset what they read), so no per-batch memset is needed
   HIP_TRY(c, c->utf8_err.ensure(F * sizeof(uint32_t), 0, c->stream));
@@ -320,6 +322,9 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.pieces = (PieceDesc*)c->pieces.p;
   a.utf8_err = (uint32_t*)c->utf8_err.p;
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  a.n_pieces = piece_bound(wire_len, n_frames);
+  a.validator_only = 0;
+  a.in_desc = nullptr;
   if (n_frames) {
     timed(c, K_PARSE, [&] { launch_parse(a, c->stream); });
     timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
@@ -329,6 +334,85 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   }
   timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_validate_batch_device(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n_frames,
+                              const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                              uint64_t payload_len, wsg_session_state* state, wsg_session_result* result_out) {
+  if (!c) return WSG_API_EINVAL;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  if (n_frames >= (1ull << 30)) return set_err(c, WSG_API_ERANGE, "too many frames in one batch (max 2^30 - 1)");
+  if ((uintptr_t)payload & 3) return set_err(c, WSG_API_EINVAL, "payload must be 4-B aligned");
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = ensure_decode_ws(c, n_frames, n_sessions, payload_len);
+  if (rc) return rc;
+  HIP_TRY(c, c->v_desc.ensure((n_frames + 1) * sizeof(wsg_frame_desc)));
+  DecodeArgs a;
+  a.wire = payload;
+  a.wire_len = payload_len;
+  a.frame_off = nullptr;
+  a.n_frames = n_frames;
+  a.session_first = session_first;
+  a.n_sessions = n_sessions;
+  a.client_mode = 0;
+  a.allow_ext = 1;
+  a.validate = 1;
+  a.max_payload = INT64_MAX;
+  a.state = state;
+  a.payload_out = nullptr;  // validate only: the piece kernel stores nothing
+  a.desc = (wsg_frame_desc*)c->v_desc.p;
+  a.result = result_out;
+  a.rec = (FrameRec*)c->rec.p;
+  a.prev = (int32_t*)c->prev.p;
+  a.edge = (uint32_t*)c->edge.p;
+  a.blk_sum = (uint64_t*)c->blk_sum.p;
+  a.blk_max = (int32_t*)c->blk_max.p;
+  a.sess_err = (uint64_t*)c->sess_err.p;
+  a.total = (uint64_t*)c->total.p;
+  a.pieces = (PieceDesc*)c->pieces.p;
+  a.utf8_err = (uint32_t*)c->utf8_err.p;
+  a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  a.n_pieces = piece_bound(payload_len, n_frames);
+  a.validator_only = 1;
+  a.in_desc = desc;
+  if (n_frames) {
+    timed(c, K_PARSE, [&] { launch_vparse(a, c->stream); });
+    timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
+    timed(c, K_LINK, [&] { launch_link(a, c->stream); });
+    timed(c, K_UNMASK, [&] { launch_vpieces(a, c->stream, a.n_pieces); });
+    timed(c, K_MERGE, [&] { launch_merge(a, c->stream); });
+  }
+  timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_validate_batch_host(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n_frames, const uint32_t* session_first,
+                            uint32_t n_sessions, const uint8_t* payload, uint64_t payload_len, wsg_session_state* state,
+                            wsg_session_result* result_out) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t S = n_sessions;
+  HIP_TRY(c, c->h_desc.ensure((n_frames + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, c->h_sf.ensure((S + 1) * sizeof(uint32_t)));
+  HIP_TRY(c, c->h_payload.ensure(payload_len + 32));
+  HIP_TRY(c, c->h_state.ensure((S + 1) * sizeof(wsg_session_state)));
+  HIP_TRY(c, c->h_result.ensure((S + 1) * sizeof(wsg_session_result)));
+  hipStream_t s = c->stream;
+  if (n_frames) HIP_TRY(c, hipMemcpyAsync(c->h_desc.p, desc, n_frames * sizeof(wsg_frame_desc), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(c->h_sf.p, session_first, (S + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  if (payload_len) HIP_TRY(c, hipMemcpyAsync(c->h_payload.p, payload, payload_len, hipMemcpyHostToDevice, s));
+  if (S) HIP_TRY(c, hipMemcpyAsync(c->h_state.p, state, S * sizeof(wsg_session_state), hipMemcpyHostToDevice, s));
+  int rc = wsg_validate_batch_device(c, (const wsg_frame_desc*)c->h_desc.p, n_frames, (const uint32_t*)c->h_sf.p,
+                                     n_sessions, (const uint8_t*)c->h_payload.p, payload_len,
+                                     (wsg_session_state*)c->h_state.p, (wsg_session_result*)c->h_result.p);
+  if (rc) return rc;
+  if (S) {
+    HIP_TRY(c, hipMemcpyAsync(result_out, c->h_result.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(state, c->h_state.p, S * sizeof(wsg_session_state), hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(c, hipStreamSynchronize(s));
   return WSG_API_OK;
 }
 

@@ -152,6 +152,51 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ k_vparse
+// Validator-only mode (the "ws-utf8-validator" stage alone, FrameUtf8Validator.java:
+// 59-98, e.g. after permessage-deflate inflated the payloads): frame k is
+// in_desc[k], its plain payload at wire[payload_off, +len).  Builds the same
+// FrameRec / edges / block aggregates as k_parse, with no header rules.
+__device__ __forceinline__ uint32_t plain_byte(const DecodeArgs& a, uint64_t i) { return i < a.wire_len ? a.wire[i] : 0u; }
+
+__global__ __launch_bounds__(BLOCK) void k_vparse(DecodeArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  Agg v = AGG_ID;
+  if (k < a.n_frames) {
+    const wsg_frame_desc d = a.in_desc[k];
+    const uint32_t s = find_session(a.session_first, a.n_sessions, k);
+    const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
+    const uint32_t len = d.payload_len;
+    const uint64_t src = d.payload_off;
+    if (op <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry (as k_parse)
+      const uint32_t nf = len < 3 ? len : 3;
+      uint32_t f3 = 0, l3 = 0;
+      for (uint32_t i = 0; i < nf; ++i) f3 |= plain_byte(a, src + i) << (8 * i);
+      if (!fin)
+        for (uint32_t i = 0; i < nf; ++i) l3 |= plain_byte(a, src + len - 1 - i) << (8 * (2 - i));
+      a.edge[k] = f3;
+      a.edge[a.n_frames + k] = l3;
+    }
+    FrameRec r;
+    r.src = src;
+    r.out_off = 0;
+    r.len = len;
+    r.mask = 0;
+    r.code = (fin ? CODE_FIN : 0u) | (rsv << CODE_RSV_SHIFT) | (op << CODE_OP_SHIFT);
+    r.sess = s;
+    a.rec[k] = r;
+    v = frame_agg(k, r);
+  }
+  Agg tot;
+  block_excl_scan(v, &tot);
+  if (threadIdx.x == 0) {
+    a.blk_sum[blockIdx.x] = tot.sum;
+    a.blk_max[blockIdx.x] = tot.m0;
+    a.blk_max[a.nblk + blockIdx.x] = tot.m1;
+    a.blk_max[2 * a.nblk + blockIdx.x] = tot.m2;
+  }
+}
+
 // ------------------------------------------------------------------ k_scan
 // One workgroup: exclusive scan of the block aggregates in place, 4 entries per
 // thread per pass (one block scan per 4096 blocks).
@@ -227,7 +272,7 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
     if (!code_pre(r.code)) {
       // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
       const bool frag = jd >= sf ? !(ex.m0 & 1) : (st.fragmentation != 0);
-      extra |= rules_frag(op, frag) << CODE_FRAG_SHIFT;
+      if (!a.validator_only) extra |= rules_frag(op, frag) << CODE_FRAG_SHIFT;
       if (a.validate) {
         bool text = op == WSG_OP_TEXT;
         if (op == WSG_OP_CONTINUATION) text = jm >= sf ? (ex.m1 & 1) != 0 : (st.text_open != 0);
@@ -274,6 +319,7 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
     const uint32_t o_fk = (uint32_t)__shfl((int)fk, o, 64);
     if (t >= T) continue;
     const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
+    if (pc >= a.n_pieces) continue;  // beyond the grid: k_merge fails the frame (WSG_E_BATCH)
     const uint64_t ps = pc * PIECE;
     const uint64_t o_end = o_out + ((o_len + 15u) & ~15u);
     const uint32_t j0 = (uint32_t)(ps - o_out);
@@ -391,7 +437,8 @@ __device__ __forceinline__ uint32_t prev_word(const DecodeArgs& a, uint64_t pos,
 // (block 64 by a scalar load).  Returns the lane's UTF-8 error flags.
 template <int NT>
 __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceDesc d, uint64_t pstart, int lane) {
-  const uint32_t aux = NT ? 2 : 0;
+  const uint32_t aux = (NT & 1) ? 2 : 0;  // NT bit 0: nontemporal; bit 2: validate only, no stores
+  constexpr bool ST = !(NT & 4);
   const uint64_t s = d.info & PD_SRC_MASK;
   const uint32_t nb = (uint32_t)(d.info >> PD_NB_SHIFT) & 2047u;
   const uint64_t a16 = s & ~15ull;
@@ -440,11 +487,11 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
 #pragma unroll
   for (int i = 0; i < 4; ++i) w[i] ^= d.mask;
   if (full) {
-    __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
+    if (ST) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
   } else {  // the frame's last piece: zero the slot padding past the payload
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = keep_bytes(w[i], keep - 4 * i);
-    if (keep > 0) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
+    if (ST && keep > 0) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, boff, 0, aux);
   }
   if (!(d.info & PD_VALIDATE)) return 0u;
   const uint32_t first_prev = (d.info & PD_FIRST) ? 0u : (alignbyte(pv_hi, pv_lo, b) ^ d.mask);
@@ -470,7 +517,8 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
 template <int NT>
 __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDesc d, uint64_t pstart, uint64_t total,
                                               int lane) {
-  const uint32_t aux = NT ? 2 : 0;
+  const uint32_t aux = (NT & 1) ? 2 : 0;  // NT bit 0: nontemporal; bit 2: validate only, no stores
+  constexpr bool ST = !(NT & 4);
   const __amdgpu_buffer_rsrc_t rout =
       __builtin_amdgcn_make_buffer_rsrc((void*)(a.payload_out + pstart), 0, (int)PIECE, 0x00020000);
   const uint64_t pend = pstart + PIECE < total ? pstart + PIECE : total;
@@ -529,7 +577,7 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) w[i] = keep_bytes(alignbyte(dd[i + 1], dd[i], sh) ^ lr.mask, keep - 4 * i);
-    __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, (uint32_t)lane * 16u, 0, aux);
+    if (ST) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, (uint32_t)lane * 16u, 0, aux);
   }
   const bool lval = live && (lr.code & CODE_VALIDATE);
   if (__any(lval)) {
@@ -590,7 +638,8 @@ template <int NT, int N>
 __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const PieceDesc d, const uint64_t info_last,
                                                 uint64_t pstart, int lane) {
   const uint32_t nb_last = (uint32_t)(info_last >> PD_NB_SHIFT) & 2047u;
-  const uint32_t aux = NT ? 2 : 0;
+  const uint32_t aux = (NT & 1) ? 2 : 0;  // NT bit 0: nontemporal; bit 2: validate only, no stores
+  constexpr bool ST = !(NT & 4);
   const uint64_t s = d.info & PD_SRC_MASK;
   const uint64_t a16 = s & ~15ull;
   const uint32_t sh = (uint32_t)(s & 15u);
@@ -642,6 +691,7 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
   const int keep = (int)nb_last - lane * 16;
 #pragma unroll
   for (int i = 0; i < N; ++i) {
+    if (!ST) continue;
     if (i + 1 < N || full) {
       __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[i][0], w[i][1], w[i][2], w[i][3]}, rout, boff + i * PIECE, 0,
                                              aux);
@@ -720,6 +770,7 @@ __global__ __launch_bounds__(256) void k_merge(DecodeArgs a) {
   const FrameRec r = a.rec[k];
   const uint32_t pre = code_pre(r.code), post = code_post(r.code), frag = code_frag(r.code);
   uint32_t status = pre ? pre : (frag ? frag : post);
+  if (!status && r.out_off + r.len > a.n_pieces * PIECE) status = WSG_E_BATCH;  // slots beyond the piece grid
   const uint32_t ue = a.utf8_err[k];
   if (ue) a.utf8_err[k] = 0u;  // back to the idle state for the next batch
   if (!status && (r.code & CODE_VALIDATE) && (ue || edge_utf8_error(a, k, r))) status = WSG_E_TEXT_UTF8;
@@ -736,6 +787,7 @@ __global__ __launch_bounds__(256) void k_merge(DecodeArgs a) {
 
 // ------------------------------------------------------------------ k_final
 __device__ int64_t error_detail(const DecodeArgs& a, uint64_t k, uint32_t err) {
+  if (a.validator_only) return 0;  // (no wire headers: only the validator's 1007, which has no argument)
   const uint64_t o = a.frame_off[k];
   const uint32_t b0 = a.wire[o], b1 = a.wire[o + 1];
   switch (err) {
@@ -829,6 +881,16 @@ void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) 
   // (fastest in tools/ubench_unmask: 2 KiB in flight per wave)
   hipLaunchKernelGGL((k_piecesN<1, 1, PIECES_PER_WAVE>),
                      dim3((uint32_t)((n_pieces_bound + PIECES_PER_WAVE - 1) / PIECES_PER_WAVE)), dim3(64), 0, s, a);
+}
+void launch_vparse(const DecodeArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_vparse, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+}
+void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
+  // validate only: the piece kernel with its stores compiled out (NT bit 2)
+  // (read-only streaming wants more bytes in flight per wave than the copy does:
+  // VPIECES_PER_WAVE KiB)
+  hipLaunchKernelGGL((k_piecesN<5, 1, VPIECES_PER_WAVE>),
+                     dim3((uint32_t)((n_pieces_bound + VPIECES_PER_WAVE - 1) / VPIECES_PER_WAVE)), dim3(64), 0, s, a);
 }
 void launch_merge(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_merge, dim3((uint32_t)((a.n_frames + 255) / 256)), dim3(256), 0, s, a);

@@ -41,6 +41,7 @@ __host__ __device__ inline bool code_is_start(uint32_t c) {
 constexpr int BLOCK = 256;  // frames per block in the parse / link passes
 constexpr uint32_t PIECE = 1024;  // payload-output bytes per wave in k_pieces (64 lanes x 16 B)
 constexpr int PIECES_PER_WAVE = 2; // pieces one k_piecesN wave takes (tools/ubench_unmask)
+constexpr int VPIECES_PER_WAVE = 4;  // validate-only mode (read-only stream)
 constexpr int ENC_PIECES_PER_WAVE = 2;  // k_enc_piecesN (1 and 2 within 1% once no array is promoted to LDS)
 
 // Pieces needed for a batch, bounded from host-known sizes: the 16-B aligned
@@ -75,6 +76,10 @@ struct DecodeArgs {
   uint32_t n_sessions;
   int32_t client_mode, allow_ext, validate;
   int64_t max_payload;
+  // validator-only mode (wsg_validate_batch_*): frames come as descriptors of plain
+  // payloads in `wire` (k_vparse instead of k_parse), no fragmentation rules, no stores
+  int32_t validator_only;
+  const wsg_frame_desc* in_desc;
   // in/out
   wsg_session_state* state;
   // outputs
@@ -93,6 +98,7 @@ struct DecodeArgs {
   uint64_t* total;     // [1] total payload slot bytes
   struct PieceDesc* pieces;  // [piece_bound]: per-piece work descriptor (k_link)
   uint32_t* utf8_err;  // [n_frames]: a piece found a UTF-8 error inside the frame (k_pieces)
+  uint64_t n_pieces;   // pieces the grid covers (piece_bound): slots beyond are a malformed batch
   uint32_t nblk;
 };
 
@@ -169,6 +175,8 @@ void launch_parse(const DecodeArgs& a, hipStream_t s);
 void launch_scan(const DecodeArgs& a, hipStream_t s);
 void launch_link(const DecodeArgs& a, hipStream_t s);
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
+void launch_vparse(const DecodeArgs& a, hipStream_t s);
+void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
 void launch_merge(const DecodeArgs& a, hipStream_t s);
 void launch_final(const DecodeArgs& a, hipStream_t s);
 
