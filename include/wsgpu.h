@@ -286,6 +286,47 @@ int wsg_encode_batch_host(wsg_ctx* ctx, int client_mode,
                           uint8_t* closed,
                           uint8_t* wire_out, uint64_t wire_cap, uint64_t* wire_off);
 
+/* ---------------- host boundary: cross-session batcher + pinned pool ---------------- */
+/* The native core of the JNI shim: every session's socket bytes
+ * go in (wsg_batcher_feed, on the loop threads' behalf), frames are delimited on
+ * the host exactly as the session read loop does (FrameDecoder.available,
+ * FrameDecoder.java:357-401; StreamSession.java:798-854) with the header rules
+ * applied as soon as a header is complete (FrameDecoder.java:197-256), and
+ * wsg_batcher_flush decodes every complete frame of every session in one device
+ * batch.  Partial frames stay in the batcher.  Not thread-safe: one batcher per
+ * selector loop (or external locking). */
+typedef struct wsg_batcher wsg_batcher;
+
+typedef struct wsg_batch_view {  /* valid until the next flush / close */
+    uint64_t n_frames;
+    uint64_t wire_bytes;
+    uint32_t n_sessions;
+    uint32_t reserved;
+    const uint32_t* session_first;      /* [n_sessions + 1] */
+    const wsg_frame_desc* desc;         /* [n_frames] */
+    const uint8_t* payload;             /* unmasked payloads (desc.payload_off) */
+    const wsg_session_result* result;   /* [n_sessions]: frames delivered + the first error,
+                                           device-found or a header error found on the host */
+} wsg_batch_view;
+
+int wsg_batcher_open(wsg_ctx* ctx, const wsg_decoder_cfg* cfg, uint32_t n_sessions, wsg_batcher** out);
+int wsg_batcher_close(wsg_batcher* b);
+const char* wsg_batcher_last_error(wsg_batcher* b);
+/* Append bytes read from session `sid`'s socket (copied; the caller may reuse
+ * `data`, as the reference releases its buffer after decode, FrameDecoder.java:285-287). */
+int wsg_batcher_feed(wsg_batcher* b, uint32_t sid, const uint8_t* data, uint64_t len);
+/* Decode all complete frames fed since the last flush; synchronises. */
+int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out);
+int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* st);
+
+/* Pinned host buffers for socket reads (the role of IByteBufferAllocator,
+ * IByteBufferAllocator.java:38-149): power-of-two size classes, recycled on
+ * release, thread-safe.  wsg_host_alloc returns NULL on failure. */
+void* wsg_host_alloc(uint64_t capacity);
+int wsg_host_release(void* p);
+uint64_t wsg_host_capacity(const void* p);  /* 0 if p is not from the pool */
+int wsg_host_trim(void);                    /* frees the pool's idle buffers */
+
 /* ---------------- aggregate (FrameAggregator) ---------------- */
 /* Per-session carry of FrameAggregator.frame (FrameAggregator.java:44): the
  * aggregated frame in progress.  Its bytes from earlier batches stay with the

@@ -38,6 +38,12 @@ class SessionResult(C.Structure):
                 ("detail", C.c_int64)]
 
 
+class BatchView(C.Structure):
+    _fields_ = [("n_frames", C.c_uint64), ("wire_bytes", C.c_uint64), ("n_sessions", C.c_uint32),
+                ("reserved", C.c_uint32), ("session_first", C.c_void_p), ("desc", C.c_void_p),
+                ("payload", C.c_void_p), ("result", C.c_void_p)]
+
+
 class EncodeFrame(C.Structure):
     _fields_ = [("payload_off", C.c_uint64), ("payload_len", C.c_uint32), ("opcode", C.c_uint8),
                 ("flags", C.c_uint8), ("reserved", C.c_uint8 * 2), ("mask", C.c_uint8 * 4),
@@ -110,6 +116,16 @@ def _load():
         "wsg_synth_uniform": ([p, u64, u64, u32, u32, i32, i32, i32, p, p, p], i32),
         "wsg_copy_ceiling": ([p, p, p, u64, i32, P(C.c_double)], i32),
         "wsg_synth_frames": ([p, p, u64, p], i32),
+        "wsg_batcher_open": ([p, P(DecoderCfg), u32, P(p)], i32),
+        "wsg_batcher_close": ([p], i32),
+        "wsg_batcher_last_error": ([p], C.c_char_p),
+        "wsg_batcher_feed": ([p, u32, p, u64], i32),
+        "wsg_batcher_flush": ([p, P(BatchView)], i32),
+        "wsg_batcher_session_state": ([p, u32, P(SessionState)], i32),
+        "wsg_host_alloc": ([u64], p),
+        "wsg_host_release": ([p], i32),
+        "wsg_host_capacity": ([p], u64),
+        "wsg_host_trim": ([], i32),
         "wsg_validate_batch_device": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_validate_batch_host": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_aggregate_batch_device": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, p], i32),

@@ -398,3 +398,106 @@ class FrameUtf8Validator:
             _writenf(session, CloseFrame.of_status(int(r["close_code"])))
             raise InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
         out.append(frame)
+
+
+class NativeBatcher:
+    """The native cross-session batcher (wsg_batcher_*, batcher.hip): the C++ core a
+    JNI shim drives.  feed() takes a session's socket bytes, delimits frames on the
+    host as the session read loop does (FrameDecoder.available,
+    StreamSession.java:798-854) and applies the header rules as soon as a header is
+    complete; flush() decodes every complete frame of every session in one device
+    batch.  Same results as SessionBatcher, without Python in the per-frame loop."""
+
+    def __init__(self, n_sessions: int, clientMode: bool = False, allowExtensions: bool = False,
+                 maxPayloadLen: int = 65536, validate_utf8: bool = True, ctx: Context | None = None):
+        from ._lib import check, lib
+        import ctypes as C
+        self.ctx = ctx or default_context()
+        self.cfg = decoder_cfg(clientMode, allowExtensions, maxPayloadLen, validate_utf8)
+        self.n = n_sessions
+        h = C.c_void_p()
+        check(lib.wsg_batcher_open(self.ctx._h, C.byref(self.cfg), n_sessions, C.byref(h)), self.ctx._h)
+        self._h = h
+
+    def close(self):
+        from ._lib import lib
+        if getattr(self, "_h", None):
+            lib.wsg_batcher_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        from ._lib import WsgError, lib
+        if rc != 0:
+            raise WsgError(f"libwsgpu batcher error {rc}: {lib.wsg_batcher_last_error(self._h).decode()}")
+
+    def feed(self, sid: int, data):
+        from ._lib import lib
+        a = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+        if a.size:
+            self._check(lib.wsg_batcher_feed(self._h, int(sid), a.ctypes.data, a.size))
+
+    def flush_raw(self):
+        """Decode everything complete; returns numpy views (valid until the next flush):
+        (session_first, desc, payload, result, wire_bytes)."""
+        import ctypes as C
+        from ._lib import BatchView, lib
+        v = BatchView()
+        self._check(lib.wsg_batcher_flush(self._h, C.byref(v)))
+        n, s = int(v.n_frames), int(v.n_sessions)
+
+        def view(ptr, count, dtype):
+            if not count:
+                return np.zeros(0, dtype=dtype)
+            buf = (C.c_uint8 * (count * np.dtype(dtype).itemsize)).from_address(ptr)
+            return np.frombuffer(buf, dtype=dtype)
+
+        sf = view(v.session_first, s + 1, np.uint32)
+        desc = view(v.desc, n, DESC_DTYPE)
+        res = view(v.result, s, RESULT_DTYPE)
+        end = int((desc["payload_off"] + desc["payload_len"]).max()) if n else 0
+        payload = view(v.payload, end, np.uint8)
+        return sf, desc, payload, res, int(v.wire_bytes)
+
+    def flush(self):
+        """[(frames, InvalidFrameException | None)] per session, like SessionBatcher.flush."""
+        sf, desc, payload, res, _ = self.flush_raw()
+        out = []
+        for s in range(self.n):
+            r = res[s]
+            frames = []
+            for k in range(int(sf[s]), int(sf[s]) + int(r["n_delivered"])):
+                d = desc[k]
+                o, ln = int(d["payload_off"]), int(d["payload_len"])
+                frames.append(make_frame(int(d["opcode"]), bool(d["flags"] & 0x80), (int(d["flags"]) >> 4) & 7,
+                                         payload[o:o + ln].tobytes()))
+            exc = None
+            if r["error"]:
+                exc = InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
+                exc.close_code = int(r["close_code"])
+            out.append((frames, exc))
+        return out
+
+
+def pinned_alloc(capacity: int):
+    """A pinned host buffer from the library's pool (wsg_host_alloc), as a numpy
+    uint8 array of its class capacity; return it with pinned_release()."""
+    import ctypes as C
+    from ._lib import lib
+    p = lib.wsg_host_alloc(int(capacity))
+    if not p:
+        raise MemoryError("wsg_host_alloc failed")
+    n = int(lib.wsg_host_capacity(p))
+    return np.frombuffer((C.c_uint8 * n).from_address(p), dtype=np.uint8)
+
+
+def pinned_release(arr) -> None:
+    from ._lib import lib
+    rc = lib.wsg_host_release(arr.ctypes.data)
+    if rc != 0:
+        raise ValueError("buffer not from the pinned pool")

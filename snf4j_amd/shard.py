@@ -101,10 +101,11 @@ def time_steps(step, steps: int, sync=None, dist=None) -> float:
         step()
     if sync:
         sync()
-    if dist is not None:
-        dist.barrier()
+    # this rank's time ends at its own device sync; the barrier after it only lines
+    # the ranks up (its latency is not work), and the max over ranks is the job time
     elapsed = time.perf_counter() - t0
     if dist is not None:
+        dist.barrier()
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -169,15 +169,21 @@ def test_decoder_kat_through_gpu_frame_decoder(ctx):
                     assert f.getPayload() == fixtures.unhex(e["payload"]), v["src"]
 
 
-def test_session_kat_through_batcher(ctx):
-    """WebSocketSessionTest stream cases through the cross-session batcher."""
-    from snf4j_amd import SessionBatcher
+def _batcher(kind):
+    from snf4j_amd import NativeBatcher, SessionBatcher
+    return SessionBatcher if kind == "python" else NativeBatcher
+
+
+@pytest.mark.parametrize("kind", ["python", "native"])
+def test_session_kat_through_batcher(ctx, kind):
+    """WebSocketSessionTest stream cases through the cross-session batcher (the
+    Python SessionBatcher and the native wsg_batcher)."""
     cases = fixtures.load("session")
     by_max = {}
     for i, v in enumerate(cases):
         by_max.setdefault(v["max_payload"], []).append(i)
     for maxp, idx in by_max.items():
-        b = SessionBatcher(len(idx), clientMode=True, maxPayloadLen=maxp, ctx=ctx)
+        b = _batcher(kind)(len(idx), clientMode=True, maxPayloadLen=maxp, ctx=ctx)
         for sid, i in enumerate(idx):
             for ch in cases[i]["chunks"]:
                 b.feed(sid, fixtures.unhex(ch))
@@ -193,17 +199,17 @@ def test_session_kat_through_batcher(ctx):
                 assert exc is None
 
 
-def test_batcher_matches_stream_oracle(ctx, oracle):
-    """Random streams fed in random socket-read chunks through SessionBatcher, several
+@pytest.mark.parametrize("kind", ["python", "native"])
+def test_batcher_matches_stream_oracle(ctx, oracle, kind):
+    """Random streams fed in random socket-read chunks through the batcher, several
     flushes, against the oracle's session read loop."""
-    from snf4j_amd import SessionBatcher
     rng = np.random.default_rng(21)
     n = 40
     streams = [b"".join(wsgen.session_frames(rng, int(rng.integers(1, 10)),
                                              inject=(wsgen.INJECT_KINDS[int(rng.integers(0, 15))]
                                                      if rng.random() < 0.3 else None)))
                for _ in range(n)]
-    b = SessionBatcher(n, clientMode=False, maxPayloadLen=65536, ctx=ctx)
+    b = _batcher(kind)(n, clientMode=False, maxPayloadLen=65536, ctx=ctx)
     got = [[] for _ in range(n)]
     err = [None] * n
     pos = [0] * n
@@ -366,3 +372,45 @@ def test_tail_utf8_large_frames(ctx, oracle, masked):
             sessions.append([wsgen.build_frame(1, False, 0, b"\xf0\x9f", masked, m),
                              wsgen.build_frame(0, True, 0, t[:2], masked, m)])
     run_parity(ctx, oracle, sessions, cm=cm, n_batches=2, rng=rng, tag="tails")
+
+
+def test_native_batcher_large_random_chunks(ctx, oracle):
+    """The native batcher's threaded gather (> 8 MiB per flush) with frames split
+    across many feeds, against the oracle's read loop."""
+    from snf4j_amd import NativeBatcher
+    rng = np.random.default_rng(33)
+    n = 64
+    streams = [b"".join(wsgen.session_frames(rng, int(rng.integers(5, 40)), big=True)) for _ in range(n)]
+    b = NativeBatcher(n, ctx=ctx)
+    got = [[] for _ in range(n)]
+    err = [None] * n
+    pos = [0] * n
+    while any(pos[s] < len(streams[s]) for s in range(n)):
+        for s in range(n):
+            c = int(rng.integers(1, 200000))
+            if pos[s] < len(streams[s]):
+                b.feed(s, streams[s][pos[s]:pos[s] + c])
+                pos[s] += c
+        for s, (fr, e) in enumerate(b.flush()):
+            got[s] += fr
+            if e is not None and err[s] is None:
+                err[s] = e
+    for s in range(n):
+        frames, e = oracle.stream_decode(streams[s], [len(streams[s])])
+        assert [(f.opcode, f.fin, f.payload) for f in frames] == \
+               [(int(f.getOpcode()), f.isFinalFragment(), f.getPayload()) for f in got[s]], s
+        assert (str(e) if e else None) == (str(err[s]) if err[s] else None), s
+
+
+def test_pinned_pool(ctx):
+    from snf4j_amd.codec import pinned_alloc, pinned_release
+    a = pinned_alloc(5000)
+    assert a.size == 8192
+    a[:] = 7
+    addr = a.ctypes.data
+    pinned_release(a)
+    b2 = pinned_alloc(6000)  # recycled from the same size class
+    assert b2.ctypes.data == addr
+    pinned_release(b2)
+    with pytest.raises(ValueError):
+        pinned_release(np.zeros(16, np.uint8))
