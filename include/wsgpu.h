@@ -58,7 +58,13 @@ typedef enum wsg_status {
                                   (detail = plen, detail2 = Integer.MAX_VALUE - need) */
     WSG_E_BATCH = 17,          /* frame extent in the batch does not match its header
                                   (a caller bug: never produced by the reference) */
-    WSG_E_AGG_TOO_BIG = 18     /* "Too big payload for aggregated frame"  FrameAggregator.java:93 (1009) */
+    WSG_E_AGG_TOO_BIG = 18,    /* "Too big payload for aggregated frame"  FrameAggregator.java:93 (1009) */
+    WSG_E_INFLATE = 19,        /* InvalidFrameException(DecompressionException("decompression failure: invalid
+                                  compressed data format")): its message is the cause's toString()
+                                  (ZlibDecoder.java:256, DeflateDecoder.java:73-76,104-106) (1002) */
+    WSG_E_INFLATE_NO_DATA = 20,/* "Inflating of input data produced no data"  DeflateDecoder.java:129 (1002) */
+    WSG_E_INFLATE_CAPACITY = 21/* the session's output region is too small (a caller contract, never
+                                  produced by the reference): nothing of the session is committed */
 } wsg_status;
 
 /* API return codes (<0). */
@@ -385,6 +391,60 @@ int wsg_aggregate_batch_host(wsg_ctx* ctx, int64_t max_aggregated_len,
                              wsg_agg_state* state, uint8_t* agg_out, uint64_t agg_cap,
                              wsg_frame_desc* out_desc, wsg_session_result* out_result,
                              uint64_t* agg_total);
+
+/* ---------------- permessage-deflate decode (PerMessageDeflateDecoder) ---------------- */
+/* Per-session carry of PerMessageDeflateDecoder / DeflateDecoder / its raw ZlibDecoder
+ * (PerMessageDeflateDecoder.java:41, DeflateDecoder.java:47-58, ZlibDecoder.java:54-58). */
+typedef struct wsg_inflate_state {
+    uint8_t compressing;   /* PerMessageDeflateDecoder.compressing */
+    uint8_t has_decoder;   /* DeflateDecoder.decoder != null (an inflater exists) */
+    uint8_t finished;      /* its ZlibDecoder.finished: a final block ended the stream, later data
+                              passes through unchanged */
+    uint8_t reserved;
+    uint32_t window_len;   /* bytes of inflate history in window[s] (<= 32768) */
+} wsg_inflate_state; /* 8 bytes */
+
+#define WSG_INFLATE_WINDOW 32768
+#define WSG_DESC_REPLAY 0x02   /* input desc.flags: a frame of a message left open by the previous
+                                  batch, decoded again (from the message start) but not delivered */
+#define WSG_DESC_INFLATED 0x02 /* output desc.flags: payload in `out` (else the input payload) */
+
+/* Device-resident PerMessageDeflateDecoder over decoded frames (its decode() once per
+ * frame per session in order, PerMessageDeflateDecoder.java:68-105 + DeflateDecoder.java:
+ * 78-141): frames of TEXT/BINARY with RSV1, and continuations of such a message, are
+ * inflated (raw DEFLATE, RFC 1951; the 4-byte tail 00 00 FF FF appended after a final
+ * fragment), RSV1 is cleared; other frames pass through.  One workgroup per session.
+ *   desc[n_frames], payload[payload_len]   the decoder's frames (desc.flags WSG_DESC_REPLAY
+ *                                 marks frames re-sent for a message the previous batch left open)
+ *   session_first[0..n_sessions]  session s owns frames [session_first[s], session_first[s+1])
+ *   state[n_sessions], window[n_sessions * 32768]   carry in / out
+ *   out, out_off[n_sessions + 1]  session s writes its inflated bytes to out[out_off[s], out_off[s+1])
+ *   out_desc[n_frames]            per non-replay frame: inflated (WSG_DESC_INFLATED, offset in out)
+ *                                 or passed through (offset in payload)
+ *   out_result[n_sessions]        n_delivered = non-replay frames before the first error
+ *   replay_from[n_sessions]       if the batch ends inside a compressed message: the index (within
+ *                                 the session's frames of this batch) of its first frame, to be
+ *                                 re-sent with WSG_DESC_REPLAY; the state stays at that message's
+ *                                 start.  0xFFFFFFFF otherwise.
+ * no_context: PerMessageDeflateDecoder(noContext) — a new inflater (empty window) per message. */
+int wsg_inflate_batch_device(wsg_ctx* ctx, int no_context,
+                             const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions,
+                             const uint8_t* payload, uint64_t payload_len,
+                             wsg_inflate_state* state, uint8_t* window,
+                             uint8_t* out, const uint64_t* out_off,
+                             wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                             uint32_t* replay_from);
+/* Same contract with host pointers: H2D, inflate, D2H of out, descriptors, results,
+ * state and window; synchronises. */
+int wsg_inflate_batch_host(wsg_ctx* ctx, int no_context,
+                           const wsg_frame_desc* desc, uint64_t n_frames,
+                           const uint32_t* session_first, uint32_t n_sessions,
+                           const uint8_t* payload, uint64_t payload_len,
+                           wsg_inflate_state* state, uint8_t* window,
+                           uint8_t* out, const uint64_t* out_off,
+                           wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                           uint32_t* replay_from);
 
 /* ---------------- synthetic workloads (bench / tests only) ---------------- */
 /* Fill a device batch of uniform frames: n_frames frames of payload_len bytes,

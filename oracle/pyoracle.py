@@ -311,6 +311,90 @@ class Aggregator:
         return OracleFrame(f.opcode, bool(f.fin), f.rsv, C.string_at(f.payload, f.len) if f.len else b"")
 
 
+# ---------------------------------------------------------------- permessage-deflate decode
+E_INFLATE, E_INFLATE_NO_DATA = 19, 20
+INFLATE_MESSAGE = ("org.snf4j.core.codec.zip.DecompressionException: "
+                   "decompression failure: invalid compressed data format")
+
+
+class _ZlibRawDecoder:
+    """ZlibDecoder(Mode.RAW) (snf4j-core ZlibDecoder.java:180-280) over java.util.zip.Inflater,
+    i.e. zlib's raw inflate.  The inflate itself is zlib's: Python's zlib module binds the same
+    library (third-party dependency of the reference's JDK, version zlib.ZLIB_RUNTIME_VERSION);
+    the wrapper logic (finished stream, leftover bytes) is restated from ZlibDecoder."""
+
+    def __init__(self):
+        import zlib
+        self._zlib = zlib
+        self.d = zlib.decompressobj(-15)
+        self.finished = False
+
+    def decode(self, data: bytes) -> list:
+        if self.finished:              # :186-191: later data passes through
+            return [data] if data else []
+        if not data:                   # :193-195
+            return []
+        try:
+            out = self.d.decompress(data)
+        except self._zlib.error as e:  # DataFormatException -> DecompressionException (:255-257)
+            raise InvalidFrame(E_INFLATE, 0, 0, 1002) from e
+        bufs = [out] if out else []
+        if self.d.eof:                 # inflater.finished(): postFinish, leftover input added (:262-270)
+            self.finished = True
+            if self.d.unused_data:
+                bufs.append(self.d.unused_data)
+        return bufs
+
+
+class PerMessageDeflateDecoder:
+    """PerMessageDeflateDecoder(noContext) + DeflateDecoder restated (PerMessageDeflateDecoder.java:
+    68-105, DeflateDecoder.java:78-141).  decode() returns (opcode, fin, rsv, payload) or raises
+    InvalidFrame (19: the DecompressionException, 20: "Inflating of input data produced no data")."""
+    TAIL = b"\x00\x00\xff\xff"  # DeflateCodec.java:43
+
+    def __init__(self, no_context: bool):
+        self.no_context = bool(no_context)
+        self.compressing = False
+        self.decoder = None
+
+    def decode(self, opcode, fin, rsv, payload: bytes):
+        payload = bytes(payload)
+        allow = (opcode in (1, 2) and (rsv & 4)) or (opcode == 0 and self.compressing)
+        out = (opcode, bool(fin), rsv, payload)
+        if allow:
+            if self.decoder is None:
+                self.decoder = _ZlibRawDecoder()
+            bufs = self.decoder.decode(payload)
+            if fin:                                   # appendTail (:78-80)
+                bufs += self.decoder.decode(self.TAIL)
+            if fin and self.no_context:
+                self.decoder = None
+            if not bufs:
+                if len(payload) == 1 and payload[0] == 0:
+                    data = b""
+                else:
+                    raise InvalidFrame(E_INFLATE_NO_DATA, 0, 0, 1002)
+            else:
+                data = b"".join(bufs)
+            out = (opcode, bool(fin), rsv ^ 4 if rsv & 4 else rsv, data)   # rsvBits (:83-85)
+        if opcode < 8:
+            if fin:
+                self.compressing = False
+            elif (rsv & 4) and opcode in (1, 2):
+                self.compressing = True
+        return out
+
+
+def deflate_message(comp, data: bytes, fin: bool) -> bytes:
+    """PerMessageDeflateEncoder's payload for one fragment: zlib raw deflate with a sync
+    flush; the trailing 00 00 FF FF is removed from a final fragment (DeflateEncoder)."""
+    import zlib
+    b = comp.compress(data) + comp.flush(zlib.Z_SYNC_FLUSH)
+    if fin and b.endswith(b"\x00\x00\xff\xff"):
+        b = b[:-4]
+    return b
+
+
 # ---------------------------------------------------------------- FrameEncoder
 class _CEnc(C.Structure):
     _fields_ = [("client_mode", C.c_int), ("closed", C.c_int)]

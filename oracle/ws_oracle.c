@@ -330,6 +330,9 @@ int or_format_error(int err, int64_t detail, int64_t detail2, char* buf, int cap
     case WSG_E_EXT_LEN: return snprintf(buf, cap, "Extended payload length (%lld) > %lld", (long long)detail, (long long)detail2);
     case WSG_E_BATCH: return snprintf(buf, cap, "Malformed batch");
     case WSG_E_AGG_TOO_BIG: return snprintf(buf, cap, "Too big payload for aggregated frame");  /* FrameAggregator.java:93 */
+    /* InvalidFrameException(cause): the message is cause.toString() (DeflateDecoder.java:73-76, ZlibDecoder.java:256) */
+    case WSG_E_INFLATE: return snprintf(buf, cap, "org.snf4j.core.codec.zip.DecompressionException: decompression failure: invalid compressed data format");
+    case WSG_E_INFLATE_NO_DATA: return snprintf(buf, cap, "Inflating of input data produced no data");  /* DeflateDecoder.java:129 */
     default: if (cap > 0) buf[0] = 0; return 0;
     }
 }

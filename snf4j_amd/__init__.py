@@ -7,14 +7,14 @@ C ABI declared in include/wsgpu.h.  This package is the host-side mirror of the
 reference's codec interface over that ABI.
 """
 from . import _lib  # noqa: F401  (fails loudly if libwsgpu.so is missing)
-from .codec import (BatchAggregator, FrameAggregator, FrameDecoder, FrameEncoder, FrameUtf8Validator, NativeBatcher,
-                    SessionBatcher)
+from .codec import (BatchAggregator, BatchInflater, FrameAggregator, FrameDecoder, FrameEncoder, FrameUtf8Validator,
+                    NativeBatcher, PerMessageDeflateDecoder, SessionBatcher)
 from .context import Context, decoder_cfg, encoded_length, error_message, frame_available
 from .frame import (AggregatedBinaryFrame, AggregatedTextFrame, BinaryFrame, CloseFrame, ContinuationFrame, Frame,
                     InvalidFrameException, Opcode, PingFrame, PongFrame, TextFrame)
 
 __all__ = ["Context", "FrameDecoder", "FrameEncoder", "SessionBatcher", "FrameAggregator", "BatchAggregator",
-           "FrameUtf8Validator", "NativeBatcher",
+           "FrameUtf8Validator", "NativeBatcher", "BatchInflater", "PerMessageDeflateDecoder",
            "AggregatedTextFrame", "AggregatedBinaryFrame", "decoder_cfg", "encoded_length",
            "error_message", "frame_available", "Frame", "Opcode", "TextFrame", "BinaryFrame", "ContinuationFrame",
            "CloseFrame", "PingFrame", "PongFrame", "InvalidFrameException"]

@@ -68,6 +68,8 @@ try:
                              ("reserved2", "<u4")])
     AGG_STATE_DTYPE = np.dtype([("open", "u1"), ("opcode", "u1"), ("rsv", "u1"), ("reserved", "u1"),
                                 ("length", "<u4")])
+    INFLATE_STATE_DTYPE = np.dtype([("compressing", "u1"), ("has_decoder", "u1"), ("finished", "u1"),
+                                    ("reserved", "u1"), ("window_len", "<u4")])
     SYNTH_DTYPE = np.dtype([("wire_off", "<u8"), ("msg_seed", "<u8"), ("payload_len", "<u4"), ("msg_pos", "<u4"),
                             ("msg_len", "<u4"), ("mask", "<u4"), ("inject_pos", "<i4"), ("opcode", "u1"),
                             ("flags", "u1"), ("text", "u1"), ("inject_kind", "u1")])
@@ -126,6 +128,8 @@ def _load():
         "wsg_host_release": ([p], i32),
         "wsg_host_capacity": ([p], u64),
         "wsg_host_trim": ([], i32),
+        "wsg_inflate_batch_device": ([p, i32, p, u64, p, u32, p, u64, p, p, p, p, p, p, p], i32),
+        "wsg_inflate_batch_host": ([p, i32, p, u64, p, u32, p, u64, p, p, p, p, p, p, p], i32),
         "wsg_validate_batch_device": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_validate_batch_host": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_aggregate_batch_device": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, p], i32),

@@ -501,3 +501,131 @@ def pinned_release(arr) -> None:
     rc = lib.wsg_host_release(arr.ctypes.data)
     if rc != 0:
         raise ValueError("buffer not from the pinned pool")
+
+
+class BatchInflater:
+    """PerMessageDeflateDecoder (PerMessageDeflateDecoder.java:68-105) for every session of a
+    batch flow, run on the GPU over each decoded batch (wsg_inflate_batch_host).  The
+    per-session inflater state and its 32 KiB window stay in `state` / `window`; the
+    frames of a message a batch leaves open are re-sent with the next batch (replay),
+    so the device always restarts a message from its first frame.  Output regions are
+    sized from the compressed bytes and grown for a session that overflows."""
+
+    def __init__(self, n_sessions: int, noContext: bool = False, ctx: Context | None = None, ratio: int = 16):
+        from ._lib import INFLATE_STATE_DTYPE
+        self.no_context = bool(noContext)
+        self.ctx = ctx
+        self.n = n_sessions
+        self.state = np.zeros(n_sessions, dtype=INFLATE_STATE_DTYPE)
+        self.window = np.zeros(n_sessions * 32768, dtype=np.uint8)
+        self.held = [[] for _ in range(n_sessions)]   # (desc, payload bytes) of an open message
+        self.ratio = ratio
+
+    def _run(self, sids, per_session, caps):
+        """One device batch over sessions `sids` (frames: lists of (desc row, payload bytes, replay))."""
+        from ._lib import INFLATE_STATE_DTYPE
+        ctx = self.ctx or default_context()
+        rows, chunks, sf, pos = [], [], [0], 0
+        for s in sids:
+            for (d, p, rep) in per_session[s]:
+                r = np.array(d, dtype=DESC_DTYPE).reshape(())
+                r = r.copy()
+                r["payload_off"] = pos
+                r["payload_len"] = len(p)
+                r["flags"] = (int(d["flags"]) & ~0x02) | (0x02 if rep else 0)
+                rows.append(r)
+                chunks.append(p)
+                pos += len(p)
+            sf.append(len(rows))
+        desc = np.array(rows, dtype=DESC_DTYPE) if rows else np.zeros(0, DESC_DTYPE)
+        payload = np.frombuffer(b"".join(chunks) + bytes(16), dtype=np.uint8)
+        st = np.ascontiguousarray(self.state[sids]).astype(INFLATE_STATE_DTYPE)
+        win = np.ascontiguousarray(self.window.reshape(self.n, 32768)[sids]).reshape(-1)
+        out_off = np.zeros(len(sids) + 1, dtype=np.uint64)
+        out_off[1:] = np.cumsum([caps[s] for s in sids])
+        out, odesc, res, rf = ctx.inflate_host(self.no_context, desc, np.array(sf, np.uint32), payload, st, win,
+                                               out_off)
+        return sf, out, odesc, res, rf, st, win, payload
+
+    def run(self, desc, session_first, payload):
+        """Inflate one decoded batch (host arrays; the frames each session's decoder delivered).
+        Returns [(frames, InvalidFrameException | None)] per session."""
+        sf = np.asarray(session_first, dtype=np.int64)
+        payload = np.asarray(payload, dtype=np.uint8)
+        per = []
+        for s in range(self.n):
+            fr = [(d, b, True) for (d, b) in self.held[s]]
+            for k in range(int(sf[s]), int(sf[s + 1])):
+                d = desc[k]
+                o, ln = int(d["payload_off"]), int(d["payload_len"])
+                fr.append((d, payload[o:o + ln].tobytes(), False))
+            per.append(fr)
+        caps = {s: 65536 + self.ratio * sum(len(p) + 4 for (_, p, _) in per[s]) for s in range(self.n)}
+        results = [None] * self.n
+        todo = list(range(self.n))
+        while todo:
+            bsf, out, odesc, res, rf, st, win, _ = self._run(todo, per, caps)
+            retry = []
+            for i, s in enumerate(todo):
+                r = res[i]
+                if int(r["error"]) == 21:  # the output region overflowed: nothing committed, grow it
+                    caps[s] *= 8
+                    retry.append(s)
+                    continue
+                self.state[s] = st[i]
+                self.window.reshape(self.n, 32768)[s] = win.reshape(len(todo), 32768)[i]
+                frames = []
+                nd = int(r["n_delivered"])
+                ks = [k for k in range(int(bsf[i]), int(bsf[i + 1])) if not per[s][k - int(bsf[i])][2]]
+                for k in ks[:nd]:
+                    d = odesc[k]
+                    o, ln = int(d["payload_off"]), int(d["payload_len"])
+                    if int(d["flags"]) & 0x02:
+                        data = out[o:o + ln].tobytes()
+                    else:
+                        data = per[s][k - int(bsf[i])][1]
+                    f = make_frame(int(d["opcode"]), bool(d["flags"] & 0x80), (int(d["flags"]) >> 4) & 7, data)
+                    f.inflated = bool(int(d["flags"]) & 0x02)
+                    frames.append(f)
+                exc = None
+                if int(r["error"]):
+                    exc = InvalidFrameException(error_message(int(r["error"])))
+                    exc.close_code = int(r["close_code"])
+                    exc.frame_index = int(r["detail"])
+                    self.held[s] = []
+                elif int(rf[i]) != 0xFFFFFFFF:  # a message left open: re-send its frames next time
+                    self.held[s] = [(d, b) for (d, b, _) in per[s][int(rf[i]):]]
+                else:
+                    self.held[s] = []
+                results[s] = (frames, exc)
+            todo = retry
+        return results
+
+
+class PerMessageDeflateDecoder:
+    """GPU-backed PerMessageDeflateDecoder(noContext): IDecoder<Frame,Frame>
+    (PerMessageDeflateDecoder.java:33-107).  decode() of one frame runs a one-frame
+    batch (so every fragment crosses a batch boundary); BatchInflater inflates whole
+    decoded batches."""
+
+    def __init__(self, noContext: bool = False, ctx: Context | None = None):
+        self._b = BatchInflater(1, noContext, ctx)
+
+    def getInboundType(self):
+        return Frame
+
+    def getOutboundType(self):
+        return Frame
+
+    def decode(self, session, frame: Frame, out: list):
+        payload = bytes(frame.getPayload())
+        desc = np.zeros(1, dtype=DESC_DTYPE)
+        desc[0]["payload_len"] = len(payload)
+        desc[0]["opcode"] = int(frame.getOpcode())
+        desc[0]["flags"] = (0x80 if frame.isFinalFragment() else 0) | ((frame.getRsvBits() & 7) << 4)
+        frames, exc = self._b.run(desc, np.array([0, 1], np.uint32), np.frombuffer(payload, np.uint8))[0]
+        if exc is not None:
+            _writenf(session, CloseFrame.of_status(exc.close_code))  # protocolError (DeflateDecoder.java:64-72)
+            raise exc
+        for f in frames:
+            out.append(f if f.inflated else frame)  # a frame not inflated is the same object (:140)

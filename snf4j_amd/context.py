@@ -31,6 +31,9 @@ MESSAGES = {
     16: "Extended payload length ({d}) > {d2}",
     17: "Malformed batch (frame extent does not match its header)",
     18: "Too big payload for aggregated frame",
+    19: "org.snf4j.core.codec.zip.DecompressionException: decompression failure: invalid compressed data format",
+    20: "Inflating of input data produced no data",
+    21: "Inflate output region too small (batch contract)",
 }
 
 
@@ -187,6 +190,33 @@ class Context:
         check(lib.wsg_validate_batch_host(self._h, d.ctypes.data, n, session_first.ctypes.data, n_s, pl.ctypes.data,
                                           payload.size, state.ctypes.data, res.ctypes.data), self._h)
         return res[:n_s]
+
+    # -------------------------------------------------------------- inflate (permessage-deflate decode)
+    def inflate_host(self, no_context: bool, desc: np.ndarray, session_first: np.ndarray, payload: np.ndarray,
+                     state: np.ndarray, window: np.ndarray, out_off: np.ndarray):
+        """PerMessageDeflateDecoder over a host batch of decoded frames (wsg_inflate_batch_host).
+        `state` (INFLATE_STATE_DTYPE) and `window` (uint8, n_sessions x 32768) are updated in
+        place.  Returns (out, out_desc, results, replay_from)."""
+        from ._lib import INFLATE_STATE_DTYPE
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        session_first = np.ascontiguousarray(session_first, dtype=np.uint32)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        out_off = np.ascontiguousarray(out_off, dtype=np.uint64)
+        assert state.dtype == INFLATE_STATE_DTYPE and state.flags.c_contiguous
+        assert window.dtype == np.uint8 and window.flags.c_contiguous
+        n, n_s = len(desc), len(session_first) - 1
+        assert window.size >= n_s * 32768 and len(out_off) == n_s + 1
+        out = np.zeros(max(1, int(out_off[-1])), dtype=np.uint8)
+        odesc = np.zeros(max(1, n), dtype=DESC_DTYPE)
+        res = np.zeros(max(1, n_s), dtype=RESULT_DTYPE)
+        rf = np.zeros(max(1, n_s), dtype=np.uint32)
+        d = desc if n else np.zeros(1, DESC_DTYPE)
+        pl = payload if payload.size else np.zeros(16, np.uint8)
+        check(lib.wsg_inflate_batch_host(self._h, int(bool(no_context)), d.ctypes.data, n, session_first.ctypes.data,
+                                         n_s, pl.ctypes.data, payload.size, state.ctypes.data, window.ctypes.data,
+                                         out.ctypes.data, out_off.ctypes.data, odesc.ctypes.data, res.ctypes.data,
+                                         rf.ctypes.data), self._h)
+        return out, odesc[:n], res[:n_s], rf[:n_s]
 
     # -------------------------------------------------------------- aggregate
     def aggregate_device(self, max_aggregated_len: int, desc, session_first, dec_result, payload, state, agg_out,

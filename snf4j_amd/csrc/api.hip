@@ -15,7 +15,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final"};
+                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -805,6 +805,84 @@ int wsg_aggregate_batch_host(wsg_ctx* c, int64_t max_aggregated_len, const wsg_f
   HIP_TRY(c, hipStreamSynchronize(s));
   if (*agg_total > agg_cap) return set_err(c, WSG_API_ERANGE, "agg_cap %llu < %llu", (unsigned long long)agg_cap,
                                            (unsigned long long)*agg_total);
+  return WSG_API_OK;
+}
+
+int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                             uint64_t payload_len, wsg_inflate_state* state, uint8_t* window, uint8_t* out,
+                             const uint64_t* out_off, wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                             uint32_t* replay_from) {
+  if (!c) return WSG_API_EINVAL;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  InflArgs a;
+  a.no_context = no_context != 0;
+  a.desc = desc;
+  a.n_frames = n_frames;
+  a.session_first = session_first;
+  a.n_sessions = n_sessions;
+  a.payload = payload;
+  a.payload_len = payload_len;
+  a.state = state;
+  a.window = window;
+  a.out = out;
+  a.out_off = out_off;
+  a.out_desc = out_desc;
+  a.result = out_result;
+  a.replay_from = replay_from;
+  timed(c, K_INFLATE, [&] { launch_inflate(a, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_inflate_batch_host(wsg_ctx* c, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                           const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                           uint64_t payload_len, wsg_inflate_state* state, uint8_t* window, uint8_t* out,
+                           const uint64_t* out_off, wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                           uint32_t* replay_from) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t S = n_sessions, F = n_frames;
+  const uint64_t out_len = S ? out_off[S] : 0;
+  DevBuf d_desc, d_sf, d_pay, d_state, d_win, d_out, d_off, d_odesc, d_res, d_rf;
+  struct Guard {
+    DevBuf* b[10];
+    ~Guard() { for (DevBuf* x : b) x->release(); }
+  } g{{&d_desc, &d_sf, &d_pay, &d_state, &d_win, &d_out, &d_off, &d_odesc, &d_res, &d_rf}};
+  HIP_TRY(c, d_desc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, d_sf.ensure((S + 1) * sizeof(uint32_t)));
+  HIP_TRY(c, d_pay.ensure(payload_len + 32));
+  HIP_TRY(c, d_state.ensure((S + 1) * sizeof(wsg_inflate_state)));
+  HIP_TRY(c, d_win.ensure((S + 1) * WSG_INFLATE_WINDOW));
+  HIP_TRY(c, d_out.ensure(out_len + 32));
+  HIP_TRY(c, d_off.ensure((S + 1) * sizeof(uint64_t)));
+  HIP_TRY(c, d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, d_res.ensure((S + 1) * sizeof(wsg_session_result)));
+  HIP_TRY(c, d_rf.ensure((S + 1) * sizeof(uint32_t)));
+  hipStream_t s = c->stream;
+  if (F) HIP_TRY(c, hipMemcpyAsync(d_desc.p, desc, F * sizeof(wsg_frame_desc), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(d_sf.p, session_first, (S + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  if (payload_len) HIP_TRY(c, hipMemcpyAsync(d_pay.p, payload, payload_len, hipMemcpyHostToDevice, s));
+  if (S) {
+    HIP_TRY(c, hipMemcpyAsync(d_state.p, state, S * sizeof(wsg_inflate_state), hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(d_win.p, window, S * WSG_INFLATE_WINDOW, hipMemcpyHostToDevice, s));
+  }
+  HIP_TRY(c, hipMemcpyAsync(d_off.p, out_off, (S + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  int rc = wsg_inflate_batch_device(c, no_context, (const wsg_frame_desc*)d_desc.p, F, (const uint32_t*)d_sf.p,
+                                    n_sessions, (const uint8_t*)d_pay.p, payload_len, (wsg_inflate_state*)d_state.p,
+                                    (uint8_t*)d_win.p, (uint8_t*)d_out.p, (const uint64_t*)d_off.p,
+                                    (wsg_frame_desc*)d_odesc.p, (wsg_session_result*)d_res.p, (uint32_t*)d_rf.p);
+  if (rc) return rc;
+  if (out_len) HIP_TRY(c, hipMemcpyAsync(out, d_out.p, out_len, hipMemcpyDeviceToHost, s));
+  if (F) HIP_TRY(c, hipMemcpyAsync(out_desc, d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, s));
+  if (S) {
+    HIP_TRY(c, hipMemcpyAsync(out_result, d_res.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(state, d_state.p, S * sizeof(wsg_inflate_state), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(window, d_win.p, S * WSG_INFLATE_WINDOW, hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(replay_from, d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(c, hipStreamSynchronize(s));
   return WSG_API_OK;
 }
 

@@ -164,10 +164,27 @@ struct AggArgs {
   uint32_t nblk;
 };
 
+struct InflArgs {
+  int32_t no_context;
+  const wsg_frame_desc* desc;
+  uint64_t n_frames;
+  const uint32_t* session_first;
+  uint32_t n_sessions;
+  const uint8_t* payload;
+  uint64_t payload_len;
+  wsg_inflate_state* state;
+  uint8_t* window;
+  uint8_t* out;
+  const uint64_t* out_off;
+  wsg_frame_desc* out_desc;
+  wsg_session_result* result;
+  uint32_t* replay_from;
+};
+
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -189,6 +206,8 @@ void launch_enc_final(const EncodeArgs& a, hipStream_t s);
 void launch_agg_plan(const AggArgs& a, hipStream_t s);
 void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim);
 void launch_agg_final(const AggArgs& a, hipStream_t s);
+
+void launch_inflate(const InflArgs& a, hipStream_t s);
 
 void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 void launch_synth_frames(const wsg_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s);

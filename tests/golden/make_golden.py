@@ -483,8 +483,42 @@ def aggregator_kats():
             {"src": "WebSocketSessionTest.java:1334-1365", "max": 100, "frames": session}]
 
 
+def deflate_kats():
+    """PerMessageDeflateCodecTest (extensions/compress/PerMessageDeflateCodecTest.java):
+    testEncodeDecode :96-131 (frames that must come back unchanged after
+    PerMessageDeflateEncoder(8, noContext) -> PerMessageDeflateDecoder(noContext); the
+    rsv mask is 4 for compressed TEXT/BINARY, 0 otherwise), testDecodeUncompressed :235-260
+    (frames without RSV1 pass through as the same object) and testDecompressionFailure
+    :312-324 (a context-takeover stream decoded by a fresh decoder fails)."""
+    src = "extensions/compress/PerMessageDeflateCodecTest.java"
+
+    def seq_bytes(n):  # PerMessageDeflateCodecTest.bytes(len), :88-94
+        return bytes(i & 0xFF for i in range(n))
+
+    def f(op, fin, rsv, payload, mask):
+        return {"opcode": OPS[op], "fin": fin, "rsv": rsv, "payload": hx(payload), "rsv_mask": mask}
+
+    round_trip = [f("TEXT", True, 0, b"ABCDEFG", 4), f("TEXT", True, 3, b"1", 4), f("TEXT", True, 1, b"", 4),
+                  f("BINARY", True, 1, seq_bytes(1024), 4), f("PING", True, 0, seq_bytes(10), 0),
+                  f("PONG", True, 0, seq_bytes(10), 0),
+                  f("CLOSE", True, 0, bytes([0x03, 0xE8]) + b"XXX", 0),
+                  f("CONTINUATION", True, 1, seq_bytes(10), 0),
+                  f("TEXT", False, 0, b"ABCDEFG", 4), f("CONTINUATION", False, 0, b"IJKLMNOP", 0),
+                  f("CONTINUATION", True, 0, b"XYZ", 0)]
+    uncompressed = [f("TEXT", True, 0, b"TEXT", 0), f("TEXT", False, 0, b"TEXT", 0),
+                    f("CONTINUATION", False, 3, b"TEXT", 0), f("CONTINUATION", True, 0, b"TEXT", 0)]
+    return [{"src": src + ":96-131", "kind": "round_trip", "level": 8, "no_context": False, "frames": round_trip},
+            {"src": src + ":96-131", "kind": "round_trip", "level": 8, "no_context": True, "frames": round_trip},
+            {"src": src + ":235-260", "kind": "pass_through", "no_context": False, "frames": uncompressed},
+            {"src": src + ":312-324", "kind": "failure", "level": 8, "no_context": False,
+             "frames": [f("BINARY", True, 0, seq_bytes(2024), 4), f("BINARY", True, 0, seq_bytes(2024), 4)],
+             "error": "org.snf4j.core.codec.zip.DecompressionException: decompression failure: "
+                      "invalid compressed data format"}]
+
+
 def main():
     data = {
+        "deflate": deflate_kats(),
         "aggregator": aggregator_kats(),
         "builder": builder_kats(),
         "decode": decode_kats(),

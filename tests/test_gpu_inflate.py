@@ -1,0 +1,174 @@
+"""GPU parity of permessage-deflate decode (inflate.hip, wsg_inflate_batch_*) against the
+oracle (PerMessageDeflateDecoder / DeflateDecoder / ZlibDecoder restated over zlib) and the
+reference's PerMessageDeflateCodecTest vectors."""
+import zlib
+
+import numpy as np
+import pytest
+
+from tests import wsgen
+from tests.golden import fixtures
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a HIP device"
+    from snf4j_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def test_deflate_kat_through_gpu(ctx, oracle):
+    """PerMessageDeflateCodecTest through the GPU PerMessageDeflateDecoder, one frame per
+    batch: round trips (context takeover and not), pass-through identity, failure."""
+    from snf4j_amd import InvalidFrameException, PerMessageDeflateDecoder
+    from snf4j_amd.frame import make_frame
+    for seq in fixtures.load("deflate"):
+        frames = [(f["opcode"], f["fin"], f["rsv"], fixtures.unhex(f["payload"])) for f in seq["frames"]]
+        d = PerMessageDeflateDecoder(seq["no_context"], ctx=ctx)
+        if seq["kind"] == "pass_through":
+            for fr in frames:
+                x = make_frame(*fr)
+                out = []
+                d.decode(None, x, out)
+                assert out == [x] and out[0] is x, seq["src"]
+            continue
+        enc = wsgen.pm_deflate_encode(frames, seq["level"], seq["no_context"])
+        if seq["kind"] == "round_trip":
+            for e, f in zip(enc, frames):
+                out = []
+                d.decode(None, make_frame(*e), out)
+                assert len(out) == 1, seq["src"]
+                g = out[0]
+                assert (int(g.getOpcode()), g.isFinalFragment(), g.getRsvBits(), g.getPayload()) == f, seq["src"]
+        else:
+            with pytest.raises(InvalidFrameException) as ei:
+                d.decode(None, make_frame(*enc[1]), [])
+            assert ei.value.getMessage() == seq["error"]
+
+
+def _message(rng, big):
+    r = rng.random()
+    if r < 0.5:
+        body = wsgen.rand_text(rng, int(rng.integers(0, 6000 if big else 400)))
+    elif r < 0.75:
+        body = rng.integers(0, 256, int(rng.integers(0, 70000 if big else 500)), dtype=np.uint8).tobytes()
+    else:  # compressible binary: runs and repeats (long matches, short distances)
+        unit = rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes()
+        body = unit * int(rng.integers(1, 3000 if big else 50))
+    return body
+
+
+def _session(rng, n_msgs, level, no_context, big, corrupt):
+    """A compressed frame stream: messages deflated as PerMessageDeflateEncoder does, the
+    compressed bytes of a message cut into fragments at arbitrary byte positions, pings
+    between fragments, uncompressed messages, and (optionally) damaged bytes or a stream
+    that ends with a final block."""
+    comp = zlib.compressobj(level, zlib.DEFLATED, -15)
+    out = []
+    for _ in range(n_msgs):
+        r = rng.random()
+        if r < 0.15:  # an uncompressed message (no RSV1): passes through
+            out.append((int(rng.choice([1, 2])), True, 0, _message(rng, False)))
+            continue
+        if r < 0.22:
+            out.append((9, True, 0, b"ping"))
+            continue
+        body = _message(rng, big)
+        if no_context:
+            comp = zlib.compressobj(level, zlib.DEFLATED, -15)
+        if rng.random() < 0.03:  # a final block: the stream ends, later data passes raw
+            data = comp.compress(body) + comp.flush(zlib.Z_FINISH)
+            comp = zlib.compressobj(level, zlib.DEFLATED, -15)
+        else:
+            data = comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH)
+            data = data[:-4] if body else b"\x00"
+        if corrupt and rng.random() < 0.1 and data:
+            b = bytearray(data)
+            b[int(rng.integers(0, len(b)))] ^= 1 << int(rng.integers(0, 8))
+            data = bytes(b)
+        cuts = sorted(set(int(x) for x in rng.integers(0, len(data) + 1, int(rng.integers(0, 4)))))
+        parts = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
+        op = int(rng.choice([1, 2]))
+        for i, p in enumerate(parts):
+            out.append((op if i == 0 else 0, i == len(parts) - 1, (4 if i == 0 else 0) | int(rng.integers(0, 2)) * 2,
+                        p))
+            if i + 1 < len(parts) and rng.random() < 0.2:
+                out.append((10, True, 0, b""))
+    return out
+
+
+def _run(ctx, oracle, sessions, no_context, n_batches, rng):
+    from snf4j_amd import BatchInflater
+    from snf4j_amd._lib import DESC_DTYPE
+    n_s = len(sessions)
+    cuts = [[0] + sorted(int(x) for x in rng.integers(0, len(f) + 1, n_batches - 1)) + [len(f)] for f in sessions]
+    bi = BatchInflater(n_s, no_context, ctx=ctx)
+    got = [[] for _ in range(n_s)]
+    err = [None] * n_s
+    base = [0] * n_s
+    for b in range(n_batches):
+        rows, chunks, sf, pos = [], [], [0], 0
+        for s in range(n_s):
+            part = sessions[s][cuts[s][b]:cuts[s][b + 1]] if err[s] is None else []
+            for (op, fin, rsv, p) in part:
+                r = np.zeros((), dtype=DESC_DTYPE)
+                r["payload_off"], r["payload_len"], r["opcode"] = pos, len(p), op
+                r["flags"] = (0x80 if fin else 0) | (rsv << 4)
+                rows.append(r)
+                chunks.append(p)
+                pos += len(p)
+            sf.append(len(rows))
+        desc = np.array(rows, dtype=DESC_DTYPE) if rows else np.zeros(0, DESC_DTYPE)
+        payload = np.frombuffer(b"".join(chunks) + bytes(16), dtype=np.uint8)
+        for s, (frames, exc) in enumerate(bi.run(desc, np.array(sf, np.uint32), payload)):
+            got[s] += frames
+            if exc is not None and err[s] is None:
+                err[s] = (base[s] + exc.frame_index, exc.getMessage())
+            base[s] += sf[s + 1] - sf[s]
+    for s in range(n_s):
+        d = oracle.PerMessageDeflateDecoder(no_context)
+        exp, e = [], None
+        for i, fr in enumerate(sessions[s]):
+            try:
+                exp.append(d.decode(*fr))
+            except oracle.InvalidFrame as ex:
+                e = (i, str(ex))
+                break
+        assert err[s] == e, (s, err[s], e)
+        assert len(got[s]) == len(exp), s
+        for i, (g, o) in enumerate(zip(got[s], exp)):
+            assert (int(g.getOpcode()), g.isFinalFragment(), g.getRsvBits()) == o[:3], (s, i)
+            assert g.getPayload() == o[3], (s, i, len(g.getPayload()), len(o[3]))
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_inflate_random_batches(ctx, oracle, seed):
+    rng = np.random.default_rng(1300 + seed)
+    no_context = bool(seed & 1)
+    level = [1, 6, 9][seed % 3]
+    n_s = int(rng.integers(1, 48))
+    sessions = [_session(rng, int(rng.integers(0, 10)), level, no_context, big=seed >= 4, corrupt=seed in (2, 5))
+                for _ in range(n_s)]
+    _run(ctx, oracle, sessions, no_context, 1 + seed % 3, rng)
+
+
+def test_inflate_long_context_window(ctx, oracle):
+    """Context takeover over many messages: back-references reach 32 KiB into earlier
+    messages and earlier batches (the window carried in state/window)."""
+    rng = np.random.default_rng(77)
+    sessions = []
+    for _ in range(6):
+        comp = zlib.compressobj(9, zlib.DEFLATED, -15)
+        seed_text = wsgen.rand_text(rng, 3000)
+        frames = []
+        for m in range(30):
+            body = seed_text[int(rng.integers(0, 1000)):][:int(rng.integers(100, 3000))] + bytes([m])
+            data = comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH)
+            frames.append((1, True, 4, data[:-4]))
+        sessions.append(frames)
+    _run(ctx, oracle, sessions, False, 4, rng)

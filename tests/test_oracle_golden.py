@@ -221,3 +221,28 @@ def test_aggregator_kat(oracle):
             o = exp["out"][0]
             assert (got.opcode, got.fin, got.rsv, got.payload) == \
                    (o["opcode"], o["fin"], o["rsv"], fixtures.unhex(o["payload"])), (seq["src"], i)
+
+
+def test_deflate_kat(oracle):
+    """PerMessageDeflateCodecTest vectors through the oracle's PerMessageDeflateDecoder
+    restatement (inputs deflated as PerMessageDeflateEncoder does, tests/wsgen.py)."""
+    from tests.wsgen import pm_deflate_encode
+    for seq in fixtures.load("deflate"):
+        frames = [(f["opcode"], f["fin"], f["rsv"], fixtures.unhex(f["payload"])) for f in seq["frames"]]
+        if seq["kind"] == "pass_through":
+            d = oracle.PerMessageDeflateDecoder(seq["no_context"])
+            for fr in frames:
+                assert d.decode(*fr) == (fr[0], fr[1], fr[2], fr[3]), seq["src"]
+            continue
+        enc = pm_deflate_encode(frames, seq["level"], seq["no_context"])
+        for e, f, src in zip(enc, frames, seq["frames"]):
+            assert e[2] == f[2] | src["rsv_mask"], seq["src"]
+        if seq["kind"] == "round_trip":
+            d = oracle.PerMessageDeflateDecoder(seq["no_context"])
+            for e, f in zip(enc, frames):
+                assert d.decode(*e) == f, seq["src"]
+        else:  # the second message of a context-takeover stream, to a fresh decoder
+            d = oracle.PerMessageDeflateDecoder(seq["no_context"])
+            with pytest.raises(oracle.InvalidFrame) as ei:
+                d.decode(*enc[1])
+            assert oracle.format_error(ei.value.err) == seq["error"], seq["src"]

@@ -149,3 +149,36 @@ def make_batch(sessions_frames):
         first.append(len(off) - 1)
     wire = np.frombuffer(b"".join(chunks), dtype=np.uint8).copy() if chunks else np.zeros(0, np.uint8)
     return wire, np.array(off, dtype=np.uint64), np.array(first, dtype=np.uint32)
+
+
+def pm_deflate_encode(frames, level=8, no_context=False):
+    """PerMessageDeflateEncoder(level, noContext) restated for test inputs
+    (PerMessageDeflateEncoder.java:55-98, DeflateEncoder.java:60-106): TEXT/BINARY frames
+    without RSV1 and the continuations of such a message are deflated (raw, sync flush;
+    the tail 00 00 FF FF removed from a final fragment; an empty payload becomes 00) and
+    TEXT/BINARY get RSV1.  Input/output: (opcode, fin, rsv, payload) tuples."""
+    import zlib
+    out = []
+    comp = None
+    compressing = False
+    for op, fin, rsv, p in frames:
+        allow = (op in (1, 2) and not (rsv & 4)) or (op == 0 and compressing)
+        if allow:
+            if comp is None:
+                comp = zlib.compressobj(level, zlib.DEFLATED, -15)
+            b = (comp.compress(p) + comp.flush(zlib.Z_SYNC_FLUSH)) if p else b""
+            if fin and no_context:
+                comp = None
+            if not b:
+                b = b"\x00"
+            elif fin:
+                b = b[:-4]
+            out.append((op, fin, rsv | 4 if op in (1, 2) else rsv, b))
+        else:
+            out.append((op, fin, rsv, p))
+        if op < 8:
+            if fin:
+                compressing = False
+            elif not (rsv & 4) and op in (1, 2):
+                compressing = True
+    return out
