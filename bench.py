@@ -40,6 +40,7 @@ def parse():
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the secondary BASELINE configs (measured at N=1 only)")
     ap.add_argument("--extra-steps", type=int, default=10)
+    ap.add_argument("--inflate-only", action="store_true", help="only the permessage-deflate inflate line")
     return ap.parse_args()
 
 
@@ -95,6 +96,10 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     ctx = snf4j_amd.Context(local, stream=stream)
+    if args.inflate_only:
+        print(json.dumps(inflate_line(ctx, dev, args.extra_steps, 2)), flush=True)
+        ctx.close()
+        return
     F, P = args.frames, args.payload
     flen = snf4j_amd.encoded_length(P, True)
     fps = max(1, F // args.sessions)
@@ -313,6 +318,86 @@ def _aggregate_line(ctx, dev, payload, desc, res, sf, n, n_s, steps, warmup, max
             "pipeline_ms": {k: v for k, v in pipe.items() if k.startswith("k_agg")}}
 
 
+def inflate_line(ctx, dev, steps, warmup, n_s=8192, msgs=16, msg_bytes=4096, cpu_seconds=3.0):
+    """PerMessageDeflateDecoder (wsg_inflate_batch_device) over a device-resident batch of
+    compressed TEXT messages, context takeover.  Serial Huffman/LZ77
+    per session: the bound is per-workgroup decode latency, not HBM; the roofline figure
+    is reported against HBM for scale only.  cpu_baseline: zlib (the engine of
+    java.util.zip.Inflater that DeflateDecoder drives) on one host core."""
+    import zlib
+    import numpy as np
+    import torch
+    from snf4j_amd._lib import DESC_DTYPE, RESULT_DTYPE
+    from snf4j_amd.synth import deflate_batch
+    desc_h, sf_h, pl_h, plain = deflate_batch(0x1F1A, n_s, msgs, msg_bytes)
+    n = len(desc_h)
+    cap = msgs * msg_bytes
+    desc = torch.from_numpy(desc_h.view(np.uint8).copy()).to(dev)
+    sf = torch.from_numpy(sf_h.view(np.int32).copy()).to(dev)
+    payload = torch.from_numpy(pl_h.copy()).to(dev)
+    state = torch.zeros(n_s * 8, dtype=torch.uint8, device=dev)
+    window = torch.empty(n_s * 32768, dtype=torch.uint8, device=dev)
+    out = torch.empty(n_s * cap, dtype=torch.uint8, device=dev)
+    out_off = torch.arange(n_s + 1, dtype=torch.int64, device=dev) * cap
+    odesc = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    ores = torch.empty(n_s * 16, dtype=torch.uint8, device=dev)
+    rf = torch.empty(n_s, dtype=torch.int32, device=dev)
+
+    def step():
+        state.zero_()  # every step inflates the same streams from fresh decoders
+        ctx.inflate_device(False, desc, sf, payload, state, window, out, out_off, odesc, ores, rf, n_frames=n)
+
+    step()
+    torch.cuda.synchronize(dev)
+    r = ores.cpu().numpy().view(RESULT_DTYPE)
+    assert int(r["error"].max()) == 0 and int(r["n_delivered"].sum()) == n
+    od = odesc.cpu().numpy().view(DESC_DTYPE)
+    assert int(od["payload_len"].astype(np.int64).sum()) == plain
+    # spot check: sessions 0 and n_s-1 against zlib
+    oh = None
+    for s in (0, n_s - 1):
+        d = zlib.decompressobj(-15)
+        k0 = int(sf_h[s])
+        for k in range(k0, k0 + msgs):
+            o, ln = int(desc_h[k]["payload_off"]), int(desc_h[k]["payload_len"])
+            exp = d.decompress(pl_h[o:o + ln].tobytes() + b"\x00\x00\xff\xff")
+            go, gl = int(od[k]["payload_off"]), int(od[k]["payload_len"])
+            if oh is None:
+                oh = out.cpu().numpy()
+            assert oh[go:go + gl].tobytes() == exp, ("inflate mismatch", s, k)
+    del oh
+    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_inflate")
+    comp = int(pl_h.size) - 16
+    alg = comp + plain
+    ach = alg / (kms / 1e3) / 1e9
+    # CPU: zlib over the first sessions' streams, one thread
+    done, t = 0, 0.0
+    while t < cpu_seconds:
+        s = done % 64
+        k0 = int(sf_h[s])
+        t0 = time.perf_counter()
+        d = zlib.decompressobj(-15)
+        for k in range(k0, k0 + msgs):
+            o, ln = int(desc_h[k]["payload_off"]), int(desc_h[k]["payload_len"])
+            d.decompress(pl_h[o:o + ln].tobytes() + b"\x00\x00\xff\xff")
+        t += time.perf_counter() - t0
+        done += 1
+    cpu = done * msgs * msg_bytes / t / 2**30
+    return {"config": f"permessage-deflate inflate: {n_s} sessions x {msgs} TEXT messages x {msg_bytes} B, "
+                      f"context takeover, level 6 (compressed {comp / 1e6:.0f} MB -> {plain / 1e6:.0f} MB)",
+            "value": round(plain * steps / el / 2**30, 3), "unit": "GiB/s (inflated bytes)",
+            "ms_per_step": round(el / steps * 1e3, 4),
+            "roofline": {"kernel": "k_inflate", "bound": "serial decode latency per session (not hbm)",
+                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": round(kms, 4)},
+            "cpu_baseline": {"value": round(cpu, 4), "unit": "GiB/s (inflated bytes)", "cores": 1,
+                             "kind": "zlib",
+                             "sample": f"{done} session streams ({msgs} x {msg_bytes} B) inflated by zlib "
+                                       f"(java.util.zip.Inflater's engine) in {t:.1f} s, 1 thread"},
+            "pipeline_ms": pipe}
+
+
 def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps, warmup, expect_errors=None,
                  aggregate=False):
     """Decode GiB/s (wire) + k_piecesN roofline of one device-resident batch."""
@@ -421,6 +506,9 @@ def measure_extras(ctx, dev, args):
                              "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
                              "avg_launch_ms": round(kms, 4)},
                 "pipeline_ms": pipe})
+    del payload, wire_out
+    torch.cuda.empty_cache()
+    out.append(inflate_line(ctx, dev, K, W))
     return out
 
 

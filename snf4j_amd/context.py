@@ -192,6 +192,17 @@ class Context:
         return res[:n_s]
 
     # -------------------------------------------------------------- inflate (permessage-deflate decode)
+    def inflate_device(self, no_context: bool, desc, session_first, payload, state, window, out, out_off, out_desc,
+                       out_result, replay_from, n_frames: int | None = None):
+        """Enqueue PerMessageDeflateDecoder over a decoded device batch (wsg_inflate_batch_device);
+        all arguments cuda tensors (desc / state / results as uint8 byte views, out_off int64)."""
+        n = desc.numel() // DESC_DTYPE.itemsize if n_frames is None else int(n_frames)
+        n_s = session_first.numel() - 1
+        assert window.numel() >= n_s * 32768 and out_off.numel() == n_s + 1
+        check(lib.wsg_inflate_batch_device(self._h, int(bool(no_context)), _p(desc), n, _p(session_first), n_s,
+                                           _p(payload), payload.numel(), _p(state), _p(window), _p(out), _p(out_off),
+                                           _p(out_desc), _p(out_result), _p(replay_from)), self._h)
+
     def inflate_host(self, no_context: bool, desc: np.ndarray, session_first: np.ndarray, payload: np.ndarray,
                      state: np.ndarray, window: np.ndarray, out_off: np.ndarray):
         """PerMessageDeflateDecoder over a host batch of decoded frames (wsg_inflate_batch_host).

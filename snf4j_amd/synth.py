@@ -88,3 +88,50 @@ def mixed_plan(seed: int, n_sessions: int, target_wire_bytes: int, min_len: int 
             "fragmented_messages": int((nfrag > 1).sum()), "bad_messages": int(bad.sum()),
             "payload_bytes": int(plen.sum()), "bad_sessions": sorted(set(sess[bad].tolist()))}
     return t, off, sf, int(off[-1]), info
+
+
+def deflate_batch(seed: int, n_sessions: int, msgs_per_session: int, msg_bytes: int, level: int = 6,
+                  unique: int = 64):
+    """A decoded batch of permessage-deflate TEXT messages (one FIN frame each, RSV1) as
+    PerMessageDeflateEncoder sends them with context takeover: per session one raw
+    DEFLATE stream, Z_SYNC_FLUSH after every message, the 00 00 FF FF tail stripped
+    (DeflateEncoder.java / PerMessageDeflateEncoder.java).  Message text is word-salad
+    ASCII (chat/JSON-like, ~3x compressible).  `unique` distinct session streams are
+    compressed on the host and tiled over n_sessions (each copy at its own offset).
+    Returns (desc[n], session_first[n_s+1], payload, plain_bytes_per_batch)."""
+    import zlib
+    from ._lib import DESC_DTYPE
+    rng = np.random.default_rng(seed)
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+    vocab = [bytes(letters[rng.integers(0, 26, int(rng.integers(2, 10)))]) for _ in range(3000)]
+    vocab += [b'{"id":', b'"name":', b'"value":', b'},', b'"ts":', b'true', b'false', b'null']
+    u = min(unique, n_sessions)
+    streams, plain = [], []
+    for _ in range(u):
+        comp = zlib.compressobj(level, zlib.DEFLATED, -15)
+        msgs, tot = [], 0
+        for _ in range(msgs_per_session):
+            words, n = [], 0
+            while n < msg_bytes:
+                w = vocab[int(rng.integers(0, len(vocab)))] if rng.random() < 0.9 else str(
+                    int(rng.integers(0, 100000))).encode()
+                words.append(w)
+                n += len(w) + 1
+            body = b" ".join(words)[:msg_bytes]
+            tot += len(body)
+            msgs.append((comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH))[:-4])
+        streams.append(msgs)
+        plain.append(tot)
+    n = n_sessions * msgs_per_session
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    sizes = np.array([[len(m) for m in streams[s % u]] for s in range(n_sessions)], dtype=np.uint64).reshape(-1)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum(sizes, out=off[1:])
+    desc["payload_off"] = off[:-1]
+    desc["payload_len"] = sizes
+    desc["opcode"] = 1
+    desc["flags"] = 0x80 | (4 << 4)
+    blob = [b"".join(streams[s]) for s in range(u)]
+    payload = np.frombuffer(b"".join(blob[s % u] for s in range(n_sessions)) + bytes(16), dtype=np.uint8)
+    sf = (np.arange(n_sessions + 1) * msgs_per_session).astype(np.uint32)
+    return desc, sf, payload, int(sum(plain[s % u] for s in range(n_sessions)))
