@@ -401,7 +401,10 @@ typedef struct wsg_inflate_state {
     uint8_t finished;      /* its ZlibDecoder.finished: a final block ended the stream, later data
                               passes through unchanged */
     uint8_t reserved;
-    uint32_t window_len;   /* bytes of inflate history in window[s] (<= 32768) */
+    uint16_t window_len;   /* bytes of inflate history in window[s] (<= 32768) */
+    uint16_t window_phase; /* window[s] is a ring image: the history byte at stream position q
+                              sits at window[s][(q + window_phase) & 32767], the next position
+                              being q = 0 (opaque to the caller; zero for a new session) */
 } wsg_inflate_state; /* 8 bytes */
 
 #define WSG_INFLATE_WINDOW 32768

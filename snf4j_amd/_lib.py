@@ -69,7 +69,7 @@ try:
     AGG_STATE_DTYPE = np.dtype([("open", "u1"), ("opcode", "u1"), ("rsv", "u1"), ("reserved", "u1"),
                                 ("length", "<u4")])
     INFLATE_STATE_DTYPE = np.dtype([("compressing", "u1"), ("has_decoder", "u1"), ("finished", "u1"),
-                                    ("reserved", "u1"), ("window_len", "<u4")])
+                                    ("reserved", "u1"), ("window_len", "<u2"), ("window_phase", "<u2")])
     SYNTH_DTYPE = np.dtype([("wire_off", "<u8"), ("msg_seed", "<u8"), ("payload_len", "<u4"), ("msg_pos", "<u4"),
                             ("msg_len", "<u4"), ("mask", "<u4"), ("inject_pos", "<i4"), ("opcode", "u1"),
                             ("flags", "u1"), ("text", "u1"), ("inject_kind", "u1")])

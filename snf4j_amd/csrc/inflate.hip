@@ -6,17 +6,25 @@
 // DEFLATE is a serial bit stream per session (Huffman codes, back-references into
 // a 32 KiB window that persists across messages unless no_context), so the unit
 // of parallelism is the session: one 64-lane workgroup per session, the sessions
-// of a batch in parallel.  Inside a workgroup the decoder is uniform code (every
-// lane runs the same state machine on the same LDS data); the lanes split the
-// work that is wide: refilling the input stage from HBM, long back-reference
-// copies, flushing output from the LDS window ring to HBM, and the window carry.
+// of a batch in parallel.  The decoder itself is wave-uniform code (its registers
+// live in SGPRs, every LDS value it reads is made uniform with readfirstlane); the
+// lanes split the work that is wide: staging the input from HBM in aligned 16-byte
+// loads, building the Huffman lookup tables (one symbol per lane, ranks by ballot),
+// back-reference and stored-block copies, flushing output from the LDS window ring
+// to HBM in dwords, and the window carry.
+//
+// Decoding is table driven: a 9-bit root table for literal/length codes and an 8-bit
+// one for distances (longer codes, rare, fall back to a canonical walk), a 64-bit
+// bit buffer refilled 8 bytes at a time while at least 8 input bytes of the frame
+// remain, and the lazy byte-at-a-time path of zlib's inflate() for a frame's last
+// bytes, so that symbol completion at frame ends is zlib's exactly.
 //
 // zlib semantics the reference depends on, reproduced exactly:
-//   * bytes are pulled lazily: a symbol completes (and its output belongs to the
-//     frame) when its last bit's byte is read; a frame's inflate call decodes as
-//     far as its bytes allow (Java's Inflater loop until needsInput, ZlibDecoder
-//     .java:223-241), the tail 00 00 FF FF of a final fragment is fed in the same
-//     call (DeflateDecoder.java:96-99);
+//   * a symbol completes (and its output belongs to the frame) when its last bit's
+//     byte has been supplied; a frame's inflate call decodes as far as its bytes
+//     allow (Java's Inflater loop until needsInput, ZlibDecoder.java:223-241), the
+//     tail 00 00 FF FF of a final fragment is fed in the same call
+//     (DeflateDecoder.java:96-99);
 //   * the error checks of zlib's inflate/inflate_table at the same bits: invalid
 //     block type, stored lengths, too many length/distance symbols, over-subscribed
 //     or incomplete code sets (an incomplete set is allowed only for a single
@@ -35,7 +43,9 @@ namespace ws {
 namespace {
 
 constexpr uint32_t WMASK = WSG_INFLATE_WINDOW - 1;
-constexpr int IB = 2048;  // input stage bytes
+constexpr uint32_t IB = 2048;        // input stage bytes
+constexpr int LROOT = 9, DROOT = 8, CROOT = 7;
+constexpr int64_t FLUSH_AT = 8192;   // ring bytes held back before a flush to HBM
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -50,60 +60,146 @@ enum Mode : int { M_HEAD = 0, M_STORED, M_COPY, M_TABLE, M_LENLENS, M_CODELENS, 
 
 enum Err : int { E_NONE = 0, E_DATA = 1, E_NODATA = 2, E_CAP = 3 };
 
-// Canonical Huffman table in LDS (count per length, symbols by code order).
+// Table entry: [0,4) code length, [4,8) extra bits, [8,11) op, [16,32) value.
+enum Op : uint32_t { OP_LIT = 0, OP_BASE = 1, OP_EOB = 2, OP_BAD = 3, OP_LONG = 4 };
+enum Kind : int { T_LIT = 0, T_DIST = 1, T_CODES = 2 };
+
+__device__ __forceinline__ uint32_t ent(uint32_t len, uint32_t extra, uint32_t op, uint32_t val) {
+  return len | (extra << 4) | (op << 8) | (val << 16);
+}
+__device__ __forceinline__ uint32_t e_len(uint32_t e) { return e & 15u; }
+__device__ __forceinline__ uint32_t e_extra(uint32_t e) { return (e >> 4) & 15u; }
+__device__ __forceinline__ uint32_t e_op(uint32_t e) { return (e >> 8) & 7u; }
+__device__ __forceinline__ uint32_t e_val(uint32_t e) { return e >> 16; }
+
+// What symbol s of a table decodes to (zlib's inflate_table base/extra arrays: 286/287
+// and 30/31 are codes that decode as invalid).
+__device__ __forceinline__ uint32_t sym_entry(int kind, uint32_t s, uint32_t len) {
+  if (kind == T_CODES) return ent(len, 0, OP_LIT, s);
+  if (kind == T_DIST) return s < 30 ? ent(len, kDistExt[s], OP_BASE, kDistBase[s]) : ent(len, 0, OP_BAD, 0);
+  if (s < 256) return ent(len, 0, OP_LIT, s);
+  if (s == 256) return ent(len, 0, OP_EOB, 0);
+  if (s < 286) return ent(len, kLenExt[s - 257], OP_BASE, kLenBase[s - 257]);
+  return ent(len, 0, OP_BAD, 0);
+}
+
+__device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+
+// Canonical code arrays (count per length, symbols in code order) for codes longer
+// than the root table.
+template <int N>
 struct Huff {
   uint16_t cnt[16];
-  uint16_t sym[320];
+  uint16_t sym[N];
 };
 
-struct Lds {
-  uint8_t ring[WSG_INFLATE_WINDOW];  // the inflate window / output stage
-  uint8_t ibuf[IB];                  // input stage
-  Huff lit, dist, clen;
+struct alignas(16) Lds {
+  uint8_t ring[WSG_INFLATE_WINDOW];  // the inflate window / output stage (a ring image)
+  uint8_t ibuf[IB + 16];             // input stage
+  uint32_t lroot[1 << LROOT];        // literal/length root table (the code-length table in a header)
+  uint32_t droot[1 << DROOT];        // distance root table
+  Huff<288> lit;
+  Huff<32> dist;
   uint8_t lens[320];
-  uint16_t offs[16];
 };
 
-// Build a table over n lengths; returns the longest code length (0: no codes),
-// or -1 for an over-subscribed or (except a single 1-bit code of a LENS/DISTS
-// table) incomplete set, as zlib's inflate_table decides.
-__device__ int build(Huff& h, const uint8_t* length, int n, bool codes_type, uint16_t* offs) {
-  for (int l = 0; l < 16; ++l) h.cnt[l] = 0;
-  for (int s = 0; s < n; ++s) h.cnt[length[s]]++;
-  int maxl = 15;
-  while (maxl >= 1 && h.cnt[maxl] == 0) --maxl;
-  if (maxl == 0) return 0;
+// Build the root table (and the canonical arrays) of the n code lengths lens[0..n):
+// every lane takes symbols, ranks among equal lengths come from ballots.  Returns
+// the longest length (0: no codes — every entry is an invalid 1-bit code) or -1 for
+// a set zlib's inflate_table rejects: over-subscribed, or incomplete unless a single
+// 1-bit code of a literal/length or distance table.
+template <int N>
+__device__ int build_tab(uint32_t* root, int rbits, Huff<N>* h, const uint8_t* lens, int n, int kind, int lane) {
+  int cnt[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) cnt[l] = 0;
+  for (int b = 0; b < n; b += 64) {
+    const int s = b + lane;
+    const int l = s < n ? lens[s] : 0;
+#pragma unroll
+    for (int L = 1; L < 16; ++L) cnt[L] += __popcll(__ballot(l == L));
+  }
+  int maxl = 0;
+#pragma unroll
+  for (int L = 1; L < 16; ++L)
+    if (cnt[L]) maxl = L;
+  const uint32_t rsize = 1u << rbits;
+  if (maxl == 0) {  // zlib: a table of invalid 1-bit entries (only a distance table gets here)
+    for (uint32_t i = lane; i < rsize; i += 64) root[i] = ent(1, 0, OP_BAD, 0);
+    return 0;
+  }
   int left = 1;
-  for (int l = 1; l <= 15; ++l) {
-    left <<= 1;
-    left -= h.cnt[l];
+#pragma unroll
+  for (int L = 1; L < 16; ++L) {
+    left = (left << 1) - cnt[L];
     if (left < 0) return -1;  // over-subscribed
   }
-  if (left > 0 && (codes_type || maxl != 1)) return -1;  // incomplete
-  offs[1] = 0;
-  for (int l = 1; l < 15; ++l) offs[l + 1] = offs[l] + h.cnt[l];
-  for (int s = 0; s < n; ++s)
-    if (length[s]) h.sym[offs[length[s]]++] = (uint16_t)s;
+  if (left > 0 && (kind == T_CODES || maxl != 1)) return -1;  // incomplete
+  int first[16], offs[16];
+  {
+    int code = 0, off = 0;
+#pragma unroll
+    for (int L = 1; L < 16; ++L) {
+      code = (code + cnt[L - 1]) << 1;
+      first[L] = code;
+      offs[L] = off;
+      off += cnt[L];
+    }
+  }
+  if (h) {
+    int v = 0;
+#pragma unroll
+    for (int L = 0; L < 16; ++L)
+      if (lane == L) v = cnt[L];
+    if (lane < 16) h->cnt[lane] = (uint16_t)v;
+  }
+  if (left > 0)  // the single-code case: the other half of the table is invalid (1 bit)
+    for (uint32_t i = lane; i < rsize; i += 64) root[i] = ent(1, 0, OP_BAD, 0);
+  const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+  int seen[16];
+#pragma unroll
+  for (int L = 0; L < 16; ++L) seen[L] = 0;
+  for (int b = 0; b < n; b += 64) {
+    const int s = b + lane;
+    const int l = s < n ? lens[s] : 0;
+    int rank = 0, fc = 0, of = 0;
+#pragma unroll
+    for (int L = 1; L < 16; ++L) {
+      const uint64_t m = __ballot(l == L);
+      if (l == L) {
+        rank = seen[L] + __popcll(m & below);
+        fc = first[L];
+        of = offs[L];
+      }
+      seen[L] += __popcll(m);
+    }
+    if (l) {
+      if (h) h->sym[of + rank] = (uint16_t)s;
+      const uint32_t code = (uint32_t)(fc + rank);
+      const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);
+      if (l <= rbits) {
+        const uint32_t e = sym_entry(kind, (uint32_t)s, (uint32_t)l);
+        for (uint32_t j = rev; j < rsize; j += (1u << l)) root[j] = e;
+      } else {
+        root[rev & (rsize - 1)] = ent(0, 0, OP_LONG, 0);
+      }
+    }
+  }
   return maxl;
 }
 
-// Decode one symbol from the low `bits` bits of hold (first stream bit = code
-// MSB).  >= 0: the symbol, *nb its length; -1: more bits needed; -2: no code of
-// the table starts with these bits (zlib's invalid entry), *nb bits decide it.
-__device__ __forceinline__ int decode(const Huff& h, int maxl, uint64_t hold, int bits, int* nb) {
-  if (maxl == 0) {  // no codes at all: zlib's table of two invalid 1-bit entries
-    if (bits < 1) return -1;
-    *nb = 1;
-    return -2;
-  }
+// Canonical walk for a code longer than the root table: >= 0 the symbol (*nb its
+// length), -1 more bits needed.  Only complete codes reach here.
+template <int N>
+__device__ int canon(const Huff<N>& h, int maxl, uint64_t hold, int bits, int* nb) {
   int code = 0, first = 0, index = 0;
   for (int len = 1; len <= maxl; ++len) {
     if (len > bits) return -1;
     code |= (int)((hold >> (len - 1)) & 1u);
-    const int count = h.cnt[len];
+    const int count = (int)uni(h.cnt[len]);
     if (code - count < first) {
       *nb = len;
-      return h.sym[index + (code - first)];
+      return (int)uni(h.sym[index + (code - first)]);
     }
     index += count;
     first += count;
@@ -111,7 +207,25 @@ __device__ __forceinline__ int decode(const Huff& h, int maxl, uint64_t hold, in
     code <<= 1;
   }
   *nb = maxl;
-  return -2;
+  return -1;
+}
+
+// Table decode from the low `bits` bits of hold (bits above them zero or the stream's
+// own next bits): true with the entry when its code is complete.
+template <int N>
+__device__ __forceinline__ bool tdec(const uint32_t* root, int rbits, const Huff<N>* h, int maxl, int kind,
+                                     uint64_t hold, int bits, uint32_t* e) {
+  uint32_t x = uni(root[(uint32_t)hold & ((1u << rbits) - 1u)]);
+  if (e_op(x) == OP_LONG) {
+    int nb = 0;
+    const int s = canon(*h, maxl, hold, bits, &nb);
+    if (s < 0) return false;
+    x = sym_entry(kind, (uint32_t)s, (uint32_t)nb);
+  } else if ((int)e_len(x) > bits) {
+    return false;
+  }
+  *e = x;
+  return true;
 }
 
 }  // namespace
@@ -126,12 +240,24 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   const uint64_t obase = a.out_off[s], ocap = a.out_off[s + 1] - a.out_off[s];
   const wsg_inflate_state st0 = a.state[s];
   uint8_t* const win = a.window + (uint64_t)s * WSG_INFLATE_WINDOW;
+  uint8_t* const out = a.out + obase;
+  const bool pl_aligned = (((uintptr_t)a.payload) & 15u) == 0;
+  const bool win_aligned = (((uintptr_t)win) & 15u) == 0;
 
-  // carry-in: the inflater's history sits at ring positions [-wl, 0)
+  // carry-in: the window image goes to the ring as is; position 0 of this batch sits
+  // at ring slot ph, the history at positions [-wl0, 0)
   int compressing = st0.compressing, has_dec = st0.has_decoder, finished = st0.finished;
   const int wl0 = (has_dec && !finished) ? (int)(st0.window_len < WSG_INFLATE_WINDOW ? st0.window_len : WSG_INFLATE_WINDOW) : 0;
-  for (int i = lane; i < wl0; i += 64) L.ring[(uint32_t)(i - wl0) & WMASK] = win[i];
+  const uint32_t ph = wl0 ? (uint32_t)st0.window_phase & WMASK : 0u;
+  if (wl0) {
+    if (win_aligned)
+      for (uint32_t c = lane; c < WSG_INFLATE_WINDOW / 16; c += 64)
+        reinterpret_cast<uint4*>(L.ring)[c] = reinterpret_cast<const uint4*>(win)[c];
+    else
+      for (uint32_t i = lane; i < WSG_INFLATE_WINDOW; i += 64) L.ring[i] = win[i];
+  }
   __syncthreads();
+  auto ri = [&](int64_t p) -> uint32_t { return ((uint32_t)p + ph) & WMASK; };
 
   int64_t pos = 0;            // output bytes of this batch (session region offset)
   int64_t flushed = 0;        // ring bytes [flushed, pos) not yet in HBM
@@ -150,14 +276,53 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   uint32_t err_idx = 0, delivered = 0;
   int64_t err_end = 0;        // on a data error: output of the frames delivered before it
 
-  // flush ring bytes to HBM (all lanes); returns false past the region's end
+  // flush ring bytes [flushed, end) to HBM in dwords (all lanes); false past the region's end
   auto flush_to = [&](int64_t end) -> bool {
     if (end > (int64_t)ocap) return false;
-    for (int64_t i = flushed + lane; i < end; i += 64) a.out[obase + (uint64_t)i] = L.ring[(uint32_t)i & WMASK];
+    int64_t i0 = flushed;
+    int64_t head = (int64_t)((4u - (uint32_t)(((uintptr_t)(out + i0)) & 3u)) & 3u);
+    if (head > end - i0) head = end - i0;
+    if (lane < head) out[i0 + lane] = L.ring[ri(i0 + lane)];
+    i0 += head;
+    const int64_t nw = (end - i0) >> 2;
+    uint32_t* const ow = reinterpret_cast<uint32_t*>(out + i0);
+    if ((ri(i0) & 3u) == 0) {
+      for (int64_t w = lane; w < nw; w += 64) ow[w] = *reinterpret_cast<const uint32_t*>(L.ring + ri(i0 + 4 * w));
+    } else {
+      for (int64_t w = lane; w < nw; w += 64) {
+        const int64_t q = i0 + 4 * w;
+        ow[w] = (uint32_t)L.ring[ri(q)] | ((uint32_t)L.ring[ri(q + 1)] << 8) | ((uint32_t)L.ring[ri(q + 2)] << 16) |
+                ((uint32_t)L.ring[ri(q + 3)] << 24);
+      }
+    }
+    i0 += nw * 4;
+    if (lane < end - i0) out[i0 + lane] = L.ring[ri(i0 + lane)];
     flushed = end;
     return true;
   };
   auto flush = [&]() -> bool { return flush_to(pos); };
+  // a back-reference: every byte comes from [pos - dist, pos), so a chunk of 64 lanes
+  // never reads a byte of its own chunk
+  auto copy_match = [&](uint32_t len, uint32_t d) {
+    if (d >= len) {
+      for (uint32_t b = 0; b < len; b += 64) {
+        const uint32_t i = b + (uint32_t)lane;
+        if (i < len) {
+          const uint8_t v = L.ring[ri(pos - d + i)];
+          L.ring[ri(pos + i)] = v;
+        }
+      }
+    } else {
+      for (uint32_t b = 0; b < len; b += 64) {
+        const uint32_t i = b + (uint32_t)lane;
+        if (i < len) {
+          const uint8_t v = L.ring[ri(pos - d + i % d)];
+          L.ring[ri(pos + i)] = v;
+        }
+      }
+    }
+    pos += len;
+  };
 
   for (uint32_t k = f0; k < f1 && err == E_NONE; ++k) {
     const wsg_frame_desc d = a.desc[k];
@@ -186,26 +351,45 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
       const uint64_t src0 = d.payload_off;
       const uint32_t plen = d.payload_len;
       const uint32_t total_in = plen + (fin ? 4u : 0u);
-      uint32_t ip = 0;                 // bytes of this frame's input pulled
-      uint32_t ib_lo = 0, ib_hi = 0;   // ibuf holds payload bytes [ib_lo, ib_hi)
-      auto in_byte = [&](uint32_t i) -> uint32_t {  // i < total_in
-        if (i >= plen) {
-          const uint32_t t = i - plen;
-          return t < 2 ? 0x00u : 0xffu;
+      uint32_t ip = 0;                              // bytes of this frame's input pulled
+      uint32_t ib_lo = 0, ib_hi = 0, ib_off = 0;    // ibuf[ib_off..] holds input bytes [ib_lo, ib_hi)
+      // stage input from byte i: aligned 16-byte loads by all lanes
+      auto restage = [&](uint32_t i) {
+        const uint64_t g = src0 + i;
+        const uint64_t A = g & ~(uint64_t)15;
+        ib_off = (uint32_t)(g - A);
+        ib_lo = i;
+        ib_hi = (i + IB - ib_off) < total_in ? (i + IB - ib_off) : total_in;
+        for (uint32_t c = lane; c < IB / 16; c += 64) {
+          const uint64_t o = A + 16u * c;
+          uint4 v;
+          if (pl_aligned && o + 16 <= a.payload_len) {
+            v = *reinterpret_cast<const uint4*>(a.payload + o);
+          } else {
+            uint32_t w[4] = {0u, 0u, 0u, 0u};
+            for (int t = 0; t < 16; ++t)
+              if (o + t < a.payload_len) w[t >> 2] |= (uint32_t)a.payload[o + t] << (8 * (t & 3));
+            v = make_uint4(w[0], w[1], w[2], w[3]);
+          }
+          reinterpret_cast<uint4*>(L.ibuf)[c] = v;
         }
-        if (i >= ib_hi || i < ib_lo) {  // refill the input stage (all lanes, coalesced)
-          __syncthreads();
-          ib_lo = i;
-          ib_hi = i + IB < plen ? i + IB : plen;
-          for (uint32_t j = ib_lo + lane; j < ib_hi; j += 64)
-            L.ibuf[j - ib_lo] = (src0 + j < a.payload_len) ? a.payload[src0 + j] : 0u;
-          __syncthreads();
+        if (fin && lane < 4) {
+          const uint32_t t = plen + (uint32_t)lane;
+          if (t >= ib_lo && t < ib_hi) L.ibuf[ib_off + (t - ib_lo)] = lane < 2 ? 0x00u : 0xffu;
         }
-        return L.ibuf[i - ib_lo];
       };
-      auto out_byte = [&](uint32_t b) {
-        L.ring[(uint32_t)pos & WMASK] = (uint8_t)b;
-        ++pos;
+      auto in_byte = [&](uint32_t i) -> uint32_t {  // i < total_in
+        if (i < ib_lo || i >= ib_hi) restage(i);
+        return uni(L.ibuf[ib_off + (i - ib_lo)]);
+      };
+      // the 8 input bytes [i, i+8) (i + 8 <= ib_hi), little endian
+      auto load8 = [&](uint32_t i) -> uint64_t {
+        const uint32_t x = ib_off + (i - ib_lo);
+        const uint64_t* w = reinterpret_cast<const uint64_t*>(L.ibuf + (x & ~7u));
+        const uint64_t w0 = w[0], w1 = w[1];
+        const uint32_t sh = (x & 7u) * 8u;
+        const uint64_t v = sh ? ((w0 >> sh) | (w1 << (64u - sh))) : w0;
+        return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
       };
       // pull bytes until `n` bits are held; false when the frame's input is exhausted
       auto need = [&](int n) -> bool {
@@ -220,13 +404,22 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
         hold >>= n;
         bits -= n;
       };
-      // raw pass-through of the rest of the frame's input (a finished stream)
-      auto raw_rest = [&]() {
-        while (ip < total_in) {
-          if (pos - flushed >= 8192 && !flush()) { err = E_CAP; return; }
-          out_byte(in_byte(ip++));
+      // n input bytes from ip straight to the output (stored blocks, a finished stream)
+      auto copy_in = [&](uint32_t n) {
+        while (n) {
+          if (pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; return; }
+          if (ip < ib_lo || ip >= ib_hi) restage(ip);
+          uint32_t m = ib_hi - ip;
+          if (m > n) m = n;
+          if (m > 4096u) m = 4096u;
+          const uint32_t base = ib_off + (ip - ib_lo);
+          for (uint32_t t = lane; t < m; t += 64) L.ring[ri(pos + t)] = L.ibuf[base + t];
+          pos += m;
+          ip += m;
+          n -= m;
         }
       };
+      auto raw_rest = [&]() { copy_in(total_in - ip); };
 
       if (finished) {
         raw_rest();
@@ -234,7 +427,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
         // the inflate state machine: runs until the frame's input is exhausted
         bool more = true;
         while (more && err == E_NONE) {
-          if (pos - flushed >= 8192 && !flush()) { err = E_CAP; break; }
+          if (pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; break; }
           switch (mode) {
             case M_HEAD: {
               if (last) {  // after a final block: the stream is done
@@ -247,13 +440,10 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
               drop(3);
               if (type == 0) mode = M_STORED;
               else if (type == 1) {  // fixed tables
-                for (int i = 0; i < 144; ++i) L.lens[i] = 8;
-                for (int i = 144; i < 256; ++i) L.lens[i] = 9;
-                for (int i = 256; i < 280; ++i) L.lens[i] = 7;
-                for (int i = 280; i < 288; ++i) L.lens[i] = 8;
-                lmax = build(L.lit, L.lens, 288, false, L.offs);
-                for (int i = 0; i < 32; ++i) L.lens[i] = 5;
-                dmax = build(L.dist, L.lens, 32, false, L.offs);
+                for (int i = lane; i < 288; i += 64) L.lens[i] = i < 144 ? 8 : (i < 256 ? 9 : (i < 280 ? 7 : 8));
+                lmax = build_tab(L.lroot, LROOT, &L.lit, L.lens, 288, T_LIT, lane);
+                for (int i = lane; i < 32; i += 64) L.lens[i] = 5;
+                dmax = build_tab(L.droot, DROOT, &L.dist, L.lens, 32, T_DIST, lane);
                 mode = M_LEN;
               } else if (type == 2) mode = M_TABLE;
               else err = E_DATA;  // "invalid block type"
@@ -272,11 +462,10 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
             case M_COPY: {
               if (length == 0) { mode = M_HEAD; break; }
               // bits is 0 here: the stored bytes come straight from the input
-              uint32_t take = length;
               if (ip >= total_in) { more = false; break; }
+              uint32_t take = length;
               if (take > total_in - ip) take = total_in - ip;
-              if (take > 4096) take = 4096;
-              for (uint32_t i = 0; i < take; ++i) out_byte(in_byte(ip++));
+              copy_in(take);
               length -= take;
               break;
             }
@@ -299,7 +488,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
               }
               if (have < ncode) { more = false; break; }
               while (have < 19) L.lens[kClenOrder[have++]] = 0;
-              cmax = build(L.clen, L.lens, 19, true, L.offs);
+              cmax = build_tab<1>(L.lroot, CROOT, nullptr, L.lens, 19, T_CODES, lane);
               if (cmax < 0) { err = E_DATA; break; }  // "invalid code lengths set"
               have = 0;
               mode = M_CODELENS;
@@ -307,24 +496,28 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
             }
             case M_CODELENS: {
               while (have < nlen + ndist) {
-                int nb = 0, sym;
+                uint32_t e = 0;
+                bool ok;
                 if (cmax == 0) {  // zlib's empty code table: 1 bit, value 0, no check
-                  if (!need(1)) { sym = -1; } else { sym = 0; nb = 1; }
+                  ok = need(1);
+                  e = ent(1, 0, OP_LIT, 0);
                 } else {
-                  sym = decode(L.clen, cmax, hold, bits, &nb);
-                  while (sym == -1) {
+                  ok = tdec<1>(L.lroot, CROOT, nullptr, cmax, T_CODES, hold, bits, &e);
+                  while (!ok) {
                     if (!need(bits + 1)) break;
-                    sym = decode(L.clen, cmax, hold, bits, &nb);
+                    ok = tdec<1>(L.lroot, CROOT, nullptr, cmax, T_CODES, hold, bits, &e);
                   }
                 }
-                if (sym < 0) break;  // more input needed (an incomplete CODES set cannot be built)
+                if (!ok) break;  // more input needed
+                const int nb = (int)e_len(e);
+                const int sym = (int)e_val(e);
                 if (sym < 16) {
                   drop(nb);
                   L.lens[have++] = (uint8_t)sym;
                   continue;
                 }
                 const int xb = sym == 16 ? 2 : (sym == 17 ? 3 : 7);
-                if (!need(nb + xb)) { sym = -1; break; }
+                if (!need(nb + xb)) break;
                 drop(nb);
                 int len = 0, copy;
                 if (sym == 16) {
@@ -338,40 +531,92 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
                 }
                 drop(xb);
                 if (have + copy > nlen + ndist) { err = E_DATA; break; }  // "invalid bit length repeat"
-                while (copy--) L.lens[have++] = (uint8_t)len;
+                for (int i = lane; i < copy; i += 64) L.lens[have + i] = (uint8_t)len;
+                have += copy;
               }
               if (err) break;
               if (have < nlen + ndist) { more = false; break; }
               if (L.lens[256] == 0) { err = E_DATA; break; }  // "invalid code -- missing end-of-block"
-              lmax = build(L.lit, L.lens, nlen, false, L.offs);
+              lmax = build_tab(L.lroot, LROOT, &L.lit, L.lens, nlen, T_LIT, lane);
               if (lmax < 0) { err = E_DATA; break; }  // "invalid literal/lengths set"
-              dmax = build(L.dist, L.lens + nlen, ndist, false, L.offs);
+              dmax = build_tab(L.droot, DROOT, &L.dist, L.lens + nlen, ndist, T_DIST, lane);
               if (dmax < 0) { err = E_DATA; break; }  // "invalid distances set"
               mode = M_LEN;
               break;
             }
             case M_LEN: {
-              // literals in a run, flushing as the stage fills
-              for (int guard = 0; guard < 4096; ++guard) {
-                int nb = 0;
-                int sym = decode(L.lit, lmax, hold, bits, &nb);
-                while (sym == -1) {
-                  if (!need(bits + 1)) break;
-                  sym = decode(L.lit, lmax, hold, bits, &nb);
+              // fast path: whole symbols from a 64-bit buffer while >= 8 input bytes of
+              // the frame remain; on the way out the unused whole bytes go back, so the
+              // byte-at-a-time path below sees zlib's lazy state
+              if (bits < 8 && ip + 8 <= total_in) {
+                hold &= (1ull << bits) - 1ull;
+                for (;;) {
+                  if (pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; break; }
+                  if (bits < 48) {
+                    if (ip + 8 > total_in) break;
+                    if (ip + 8 > ib_hi || ip < ib_lo) restage(ip);
+                    hold |= load8(ip) << bits;
+                    const int nb = (63 - bits) >> 3;
+                    ip += (uint32_t)nb;
+                    bits += nb << 3;
+                  }
+                  uint32_t e = uni(L.lroot[(uint32_t)hold & ((1u << LROOT) - 1u)]);
+                  if (e_op(e) == OP_LONG) {
+                    int nb = 0;
+                    const int sy = canon(L.lit, lmax, hold, bits, &nb);
+                    e = sym_entry(T_LIT, (uint32_t)sy, (uint32_t)nb);
+                  }
+                  const uint32_t eo = e_op(e);
+                  if (eo == OP_BAD) { err = E_DATA; break; }  // "invalid literal/length code"
+                  drop((int)e_len(e));
+                  if (eo == OP_LIT) {
+                    L.ring[ri(pos)] = (uint8_t)e_val(e);
+                    ++pos;
+                    continue;
+                  }
+                  if (eo == OP_EOB) { mode = M_HEAD; break; }
+                  const uint32_t lx = e_extra(e);
+                  const uint32_t mlen = e_val(e) + (uint32_t)(hold & ((1ull << lx) - 1ull));
+                  drop((int)lx);
+                  uint32_t g = uni(L.droot[(uint32_t)hold & ((1u << DROOT) - 1u)]);
+                  if (e_op(g) == OP_LONG) {
+                    int nb = 0;
+                    const int sy = canon(L.dist, dmax, hold, bits, &nb);
+                    g = sym_entry(T_DIST, (uint32_t)sy, (uint32_t)nb);
+                  }
+                  if (e_op(g) == OP_BAD) { err = E_DATA; break; }  // "invalid distance code"
+                  drop((int)e_len(g));
+                  const uint32_t dx = e_extra(g);
+                  const uint32_t md = e_val(g) + (uint32_t)(hold & ((1ull << dx) - 1ull));
+                  drop((int)dx);
+                  if ((int64_t)md > pos - wstart) { err = E_DATA; break; }  // "invalid distance too far back"
+                  copy_match(mlen, md);
                 }
-                if (sym == -1) { more = false; break; }
-                if (sym == -2 || sym >= 286) { err = E_DATA; break; }  // "invalid literal/length code"
-                drop(nb);
-                if (sym < 256) {
-                  out_byte((uint32_t)sym);
-                  continue;
-                }
-                if (sym == 256) { mode = M_HEAD; break; }  // end of block
-                length = kLenBase[sym - 257];
-                extra = kLenExt[sym - 257];
-                mode = M_LENEXT;
+                ip -= (uint32_t)(bits >> 3);
+                bits &= 7;
+                hold &= (1ull << bits) - 1ull;
+                if (err || mode != M_LEN) break;
+              }
+              // one symbol, pulling bytes lazily
+              uint32_t e = 0;
+              bool ok = tdec(L.lroot, LROOT, &L.lit, lmax, T_LIT, hold, bits, &e);
+              while (!ok) {
+                if (!need(bits + 1)) break;
+                ok = tdec(L.lroot, LROOT, &L.lit, lmax, T_LIT, hold, bits, &e);
+              }
+              if (!ok) { more = false; break; }
+              const uint32_t eo = e_op(e);
+              if (eo == OP_BAD) { err = E_DATA; break; }  // "invalid literal/length code"
+              drop((int)e_len(e));
+              if (eo == OP_LIT) {
+                L.ring[ri(pos)] = (uint8_t)e_val(e);
+                ++pos;
                 break;
               }
+              if (eo == OP_EOB) { mode = M_HEAD; break; }  // end of block
+              length = e_val(e);
+              extra = e_extra(e);
+              mode = M_LENEXT;
               break;
             }
             case M_LENEXT: {
@@ -384,17 +629,17 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
               break;
             }
             case M_DIST: {
-              int nb = 0;
-              int sym = decode(L.dist, dmax, hold, bits, &nb);
-              while (sym == -1) {
+              uint32_t e = 0;
+              bool ok = tdec(L.droot, DROOT, &L.dist, dmax, T_DIST, hold, bits, &e);
+              while (!ok) {
                 if (!need(bits + 1)) break;
-                sym = decode(L.dist, dmax, hold, bits, &nb);
+                ok = tdec(L.droot, DROOT, &L.dist, dmax, T_DIST, hold, bits, &e);
               }
-              if (sym == -1) { more = false; break; }
-              if (sym == -2 || sym >= 30) { err = E_DATA; break; }  // "invalid distance code"
-              drop(nb);
-              dist = kDistBase[sym];
-              extra = kDistExt[sym];
+              if (!ok) { more = false; break; }
+              if (e_op(e) == OP_BAD) { err = E_DATA; break; }  // "invalid distance code"
+              drop((int)e_len(e));
+              dist = e_val(e);
+              extra = e_extra(e);
               mode = M_DISTEXT;
               break;
             }
@@ -405,15 +650,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
                 drop((int)extra);
               }
               if ((int64_t)dist > pos - wstart) { err = E_DATA; break; }  // "invalid distance too far back"
-              // the copy: lanes in chunks that never read a byte of their own chunk
-              const uint32_t step = dist < 64u ? dist : 64u;
-              for (uint32_t b = 0; b < length; b += step) {
-                const uint32_t i = b + (uint32_t)lane;
-                if ((uint32_t)lane < step && i < length)
-                  L.ring[(uint32_t)(pos + i) & WMASK] = L.ring[(uint32_t)(pos + i - dist) & WMASK];
-                __syncthreads();
-              }
-              pos += length;
+              copy_match(length, dist);
               mode = M_LEN;
               break;
             }
@@ -501,27 +738,35 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
     st.compressing = open ? 0 : (uint8_t)compressing;
     st.has_decoder = (uint8_t)chas;
     st.finished = (uint8_t)cfin;
+    st.window_len = 0;
+    st.window_phase = 0;
     if (chas && !cfin) {
       const int64_t n = (P - W) < WSG_INFLATE_WINDOW ? (P - W) : WSG_INFLATE_WINDOW;
-      // bytes [P-n, P): the ring holds [pos-32768, pos), earlier ones are in HBM (this
-      // batch's output) or in the old window; the old window moves only downwards
+      // the new image: slot j holds position q(j) in [P - 32768, P).  q < 0: the old
+      // image already has it (same phase); q >= pos - 32768: the ring; else this
+      // batch's output in HBM (flushed).  Slots below the history are don't-care.
+      const uint32_t nph = ri(P);
+      const int64_t ring_lo = pos - (int64_t)WSG_INFLATE_WINDOW;
+      const int64_t lo = (P - n) > 0 ? (P - n) : 0;
       __threadfence_block();
-      for (int64_t b = 0; b < n; b += 64) {
-        const int64_t j = b + lane;
-        uint32_t v = 0;
-        if (j < n) {
-          const int64_t q = P - n + j;
-          if (q >= pos - (int64_t)WSG_INFLATE_WINDOW) v = L.ring[(uint32_t)q & WMASK];
-          else if (q >= 0) v = a.out[obase + (uint64_t)q];
-          else v = win[wl0 + q];
+      for (uint32_t c = lane; c < WSG_INFLATE_WINDOW / 16; c += 64) {
+        const uint32_t j0 = 16u * c;
+        const int64_t q0 = P - (int64_t)WSG_INFLATE_WINDOW + (int64_t)((j0 - nph) & WMASK);
+        const bool wraps = nph > j0 && nph < j0 + 16u;
+        if (!wraps && q0 + 16 <= lo) continue;  // nothing to write
+        if (!wraps && win_aligned && q0 >= 0 && q0 >= ring_lo) {
+          reinterpret_cast<uint4*>(win)[c] = reinterpret_cast<const uint4*>(L.ring)[c];
+          continue;
         }
-        __syncthreads();
-        if (j < n) win[j] = (uint8_t)v;
-        __syncthreads();
+        for (uint32_t t = 0; t < 16u; ++t) {
+          const uint32_t j = j0 + t;
+          const int64_t q = P - (int64_t)WSG_INFLATE_WINDOW + (int64_t)((j - nph) & WMASK);
+          if (q < lo) continue;
+          win[j] = q >= ring_lo ? L.ring[j] : out[q];
+        }
       }
-      st.window_len = (uint32_t)n;
-    } else {
-      st.window_len = 0;
+      st.window_len = (uint16_t)n;
+      st.window_phase = (uint16_t)nph;
     }
     if (open) rf = (uint32_t)snap_k;
     if (lane == 0) a.state[s] = st;
