@@ -41,6 +41,7 @@ def parse():
                     help="skip the secondary BASELINE configs (measured at N=1 only)")
     ap.add_argument("--extra-steps", type=int, default=10)
     ap.add_argument("--inflate-only", action="store_true", help="only the permessage-deflate inflate line")
+    ap.add_argument("--inflate-sessions", type=int, nargs="+", default=[8192])
     return ap.parse_args()
 
 
@@ -97,7 +98,8 @@ def main():
     stream = torch.cuda.current_stream(dev)
     ctx = snf4j_amd.Context(local, stream=stream)
     if args.inflate_only:
-        print(json.dumps(inflate_line(ctx, dev, args.extra_steps, 2)), flush=True)
+        for n_s in args.inflate_sessions:
+            print(json.dumps(inflate_line(ctx, dev, args.extra_steps, 2, n_s=n_s, cpu_seconds=0.2)), flush=True)
         ctx.close()
         return
     F, P = args.frames, args.payload

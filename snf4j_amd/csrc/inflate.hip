@@ -45,7 +45,9 @@ namespace {
 constexpr uint32_t WMASK = WSG_INFLATE_WINDOW - 1;
 constexpr uint32_t IB = 2048;        // input stage bytes
 constexpr int LROOT = 9, DROOT = 8, CROOT = 7;
-constexpr int64_t FLUSH_AT = 8192;   // ring bytes held back before a flush to HBM
+constexpr int32_t FLUSH_AT = 8192;   // ring bytes held back before a flush to HBM
+// positions are 32-bit: a session's output per batch is capped below 2 GiB (else CAP)
+constexpr int32_t POS_LIMIT = 0x7fff0000;
 
 __constant__ uint16_t kLenBase[29] = {3,  4,  5,  6,  7,  8,  9,  10, 11,  13,  15,  17,  19,  23, 27,
                                       31, 35, 43, 51, 59, 67, 83, 99, 115, 131, 163, 195, 227, 258};
@@ -84,6 +86,7 @@ __device__ __forceinline__ uint32_t sym_entry(int kind, uint32_t s, uint32_t len
 }
 
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
+__device__ __forceinline__ uint64_t uni64(uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); }
 
 // Canonical code arrays (count per length, symbols in code order) for codes longer
 // than the root table.
@@ -191,7 +194,7 @@ __device__ int build_tab(uint32_t* root, int rbits, Huff<N>* h, const uint8_t* l
 // Canonical walk for a code longer than the root table: >= 0 the symbol (*nb its
 // length), -1 more bits needed.  Only complete codes reach here.
 template <int N>
-__device__ int canon(const Huff<N>& h, int maxl, uint64_t hold, int bits, int* nb) {
+__device__ __forceinline__ int canon(const Huff<N>& h, int maxl, uint64_t hold, int bits, int* nb) {
   int code = 0, first = 0, index = 0;
   for (int len = 1; len <= maxl; ++len) {
     if (len > bits) return -1;
@@ -230,14 +233,31 @@ __device__ __forceinline__ bool tdec(const uint32_t* root, int rbits, const Huff
 
 }  // namespace
 
+// Phase clocks for tools/prof_inflate.hip (compiled out of the library).
+#ifdef WSG_INFLATE_PROF
+__device__ unsigned long long g_infl_prof[24];
+#define PROF_T(v) const uint64_t v = clock64()
+#define PROF_ACC(i, v) pf_[i] += clock64() - (v)
+#define PROF_CNT(i, n) pf_[i] += (uint64_t)(n)
+#else
+#define PROF_T(v)
+#define PROF_ACC(i, v)
+#define PROF_CNT(i, n)
+#endif
+
 // One workgroup (one wave) per session.
 __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   __shared__ Lds L;
   const int lane = threadIdx.x;
   const uint32_t s = blockIdx.x;
   if (s >= a.n_sessions) return;
+#ifdef WSG_INFLATE_PROF
+  uint64_t pf_[24] = {};
+#endif
+  PROF_T(t_all);
   const uint32_t f0 = a.session_first[s], f1 = a.session_first[s + 1];
-  const uint64_t obase = a.out_off[s], ocap = a.out_off[s + 1] - a.out_off[s];
+  const uint64_t obase = a.out_off[s], ocap64 = a.out_off[s + 1] - a.out_off[s];
+  const int32_t ocap = ocap64 < (uint64_t)POS_LIMIT ? (int32_t)ocap64 : POS_LIMIT;
   const wsg_inflate_state st0 = a.state[s];
   uint8_t* const win = a.window + (uint64_t)s * WSG_INFLATE_WINDOW;
   uint8_t* const out = a.out + obase;
@@ -249,6 +269,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   int compressing = st0.compressing, has_dec = st0.has_decoder, finished = st0.finished;
   const int wl0 = (has_dec && !finished) ? (int)(st0.window_len < WSG_INFLATE_WINDOW ? st0.window_len : WSG_INFLATE_WINDOW) : 0;
   const uint32_t ph = wl0 ? (uint32_t)st0.window_phase & WMASK : 0u;
+  PROF_T(t_cin);
   if (wl0) {
     if (win_aligned)
       for (uint32_t c = lane; c < WSG_INFLATE_WINDOW / 16; c += 64)
@@ -257,11 +278,12 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
       for (uint32_t i = lane; i < WSG_INFLATE_WINDOW; i += 64) L.ring[i] = win[i];
   }
   __syncthreads();
-  auto ri = [&](int64_t p) -> uint32_t { return ((uint32_t)p + ph) & WMASK; };
+  PROF_ACC(1, t_cin);
+  auto ri = [&](int32_t p) -> uint32_t { return ((uint32_t)p + ph) & WMASK; };
 
-  int64_t pos = 0;            // output bytes of this batch (session region offset)
-  int64_t flushed = 0;        // ring bytes [flushed, pos) not yet in HBM
-  int64_t wstart = -wl0;      // position where the current inflater's history starts
+  int32_t pos = 0;            // output bytes of this batch (session region offset)
+  int32_t flushed = 0;        // ring bytes [flushed, pos) not yet in HBM
+  int32_t wstart = -wl0;      // position where the current inflater's history starts
   // inflater registers (persist across frames: one continuous stream)
   int mode = M_HEAD, last = 0;
   uint64_t hold = 0;
@@ -271,26 +293,27 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   uint32_t length = 0, dist = 0, extra = 0;
   // the message-start snapshot (a batch ending inside a message commits it)
   int snap_k = -1, snap_has = 0, snap_fin = 0;
-  int64_t snap_pos = 0, snap_wstart = 0;
+  int32_t snap_pos = 0, snap_wstart = 0;
   int err = E_NONE;
   uint32_t err_idx = 0, delivered = 0;
-  int64_t err_end = 0;        // on a data error: output of the frames delivered before it
+  int32_t err_end = 0;        // on a data error: output of the frames delivered before it
 
   // flush ring bytes [flushed, end) to HBM in dwords (all lanes); false past the region's end
-  auto flush_to = [&](int64_t end) -> bool {
-    if (end > (int64_t)ocap) return false;
-    int64_t i0 = flushed;
-    int64_t head = (int64_t)((4u - (uint32_t)(((uintptr_t)(out + i0)) & 3u)) & 3u);
+  auto flush_to = [&](int32_t end) -> bool {
+    if (end > ocap) return false;
+    PROF_T(t_fl);
+    int32_t i0 = flushed;
+    int32_t head = (int32_t)((4u - (uint32_t)(((uintptr_t)(out + i0)) & 3u)) & 3u);
     if (head > end - i0) head = end - i0;
     if (lane < head) out[i0 + lane] = L.ring[ri(i0 + lane)];
     i0 += head;
-    const int64_t nw = (end - i0) >> 2;
+    const int32_t nw = (end - i0) >> 2;
     uint32_t* const ow = reinterpret_cast<uint32_t*>(out + i0);
     if ((ri(i0) & 3u) == 0) {
-      for (int64_t w = lane; w < nw; w += 64) ow[w] = *reinterpret_cast<const uint32_t*>(L.ring + ri(i0 + 4 * w));
+      for (int32_t w = lane; w < nw; w += 64) ow[w] = *reinterpret_cast<const uint32_t*>(L.ring + ri(i0 + 4 * w));
     } else {
-      for (int64_t w = lane; w < nw; w += 64) {
-        const int64_t q = i0 + 4 * w;
+      for (int32_t w = lane; w < nw; w += 64) {
+        const int32_t q = i0 + 4 * w;
         ow[w] = (uint32_t)L.ring[ri(q)] | ((uint32_t)L.ring[ri(q + 1)] << 8) | ((uint32_t)L.ring[ri(q + 2)] << 16) |
                 ((uint32_t)L.ring[ri(q + 3)] << 24);
       }
@@ -298,6 +321,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
     i0 += nw * 4;
     if (lane < end - i0) out[i0 + lane] = L.ring[ri(i0 + lane)];
     flushed = end;
+    PROF_ACC(6, t_fl);
     return true;
   };
   auto flush = [&]() -> bool { return flush_to(pos); };
@@ -325,7 +349,9 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   };
 
   for (uint32_t k = f0; k < f1 && err == E_NONE; ++k) {
+    PROF_T(t_fr);
     const wsg_frame_desc d = a.desc[k];
+    PROF_CNT(15, 1);
     const bool replay = (d.flags & WSG_DESC_REPLAY) != 0;
     const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
     const bool allow = ((op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u)) || (op == WSG_OP_CONTINUATION && compressing);
@@ -346,7 +372,8 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
         bits = 0;
         wstart = pos;
       }
-      const int64_t fstart = pos;
+      const int32_t fstart = pos;
+      PROF_ACC(8, t_fr);
       // the frame's input: its payload, then the tail 00 00 FF FF if final
       const uint64_t src0 = d.payload_off;
       const uint32_t plen = d.payload_len;
@@ -358,6 +385,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
         const uint64_t g = src0 + i;
         const uint64_t A = g & ~(uint64_t)15;
         ib_off = (uint32_t)(g - A);
+        PROF_CNT(12, 1);
         ib_lo = i;
         ib_hi = (i + IB - ib_off) < total_in ? (i + IB - ib_off) : total_in;
         for (uint32_t c = lane; c < IB / 16; c += 64) {
@@ -381,15 +409,6 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
       auto in_byte = [&](uint32_t i) -> uint32_t {  // i < total_in
         if (i < ib_lo || i >= ib_hi) restage(i);
         return uni(L.ibuf[ib_off + (i - ib_lo)]);
-      };
-      // the 8 input bytes [i, i+8) (i + 8 <= ib_hi), little endian
-      auto load8 = [&](uint32_t i) -> uint64_t {
-        const uint32_t x = ib_off + (i - ib_lo);
-        const uint64_t* w = reinterpret_cast<const uint64_t*>(L.ibuf + (x & ~7u));
-        const uint64_t w0 = w[0], w1 = w[1];
-        const uint32_t sh = (x & 7u) * 8u;
-        const uint64_t v = sh ? ((w0 >> sh) | (w1 << (64u - sh))) : w0;
-        return ((uint64_t)uni((uint32_t)(v >> 32)) << 32) | (uint64_t)uni((uint32_t)v);
       };
       // pull bytes until `n` bits are held; false when the frame's input is exhausted
       auto need = [&](int n) -> bool {
@@ -428,6 +447,11 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
         bool more = true;
         while (more && err == E_NONE) {
           if (pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; break; }
+          PROF_T(t_it);
+#ifdef WSG_INFLATE_PROF
+          const int mode0 = mode;
+          if (mode0 == M_HEAD) PROF_CNT(14, 1);
+#endif
           switch (mode) {
             case M_HEAD: {
               if (last) {  // after a final block: the stream is done
@@ -550,21 +574,57 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
               // byte-at-a-time path below sees zlib's lazy state
               if (bits < 8 && ip + 8 <= total_in) {
                 hold &= (1ull << bits) - 1ull;
-                for (;;) {
-                  if (pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; break; }
-                  if (bits < 48) {
-                    if (ip + 8 > total_in) break;
-                    if (ip + 8 > ib_hi || ip < ib_lo) restage(ip);
-                    hold |= load8(ip) << bits;
-                    const int nb = (63 - bits) >> 3;
-                    ip += (uint32_t)nb;
-                    bits += nb << 3;
+                PROF_T(t_fast);
+                // whole dwords of the stage from here on: align to its 4-byte grid (the
+                // stage grid is the absolute address's, so this holds across restages)
+                while (((uint32_t)(src0 + ip)) & 3u) {
+                  hold |= (uint64_t)in_byte(ip++) << bits;
+                  bits += 8;
+                }
+                if (ip + 4 > ib_hi || ip < ib_lo) restage(ip);
+                const uint32_t* const ib32 = reinterpret_cast<const uint32_t*>(L.ibuf);
+                uint32_t nxt = ib32[(ib_off + (ip - ib_lo)) >> 2];  // prefetched: made uniform at use
+                // + 32 bits (bits < 32); false when fewer than 4 input bytes of the frame remain
+                auto refill = [&]() -> bool {
+                  if (ip + 4 > total_in) return false;
+                  hold |= (uint64_t)uni(nxt) << bits;
+                  bits += 32;
+                  ip += 4;
+                  if (ip + 4 <= total_in) {
+                    if (ip + 4 > ib_hi) restage(ip);
+                    nxt = ib32[(ib_off + (ip - ib_lo)) >> 2];
                   }
+                  return true;
+                };
+                for (;;) {
+                  // the decoder registers are wave-uniform: keep them in SGPRs
+                  hold = uni64(hold);
+                  bits = (int)uni((uint32_t)bits);
+                  pos = (int32_t)uni((uint32_t)pos);
+                  ip = uni(ip);
+                  // >= 32 bits at every lookup: a literal/length code and its extra bits fit
+                  if (bits < 32) {
+                    if (pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; break; }
+                    if (!refill()) break;
+                  }
+                  PROF_T(t_sym);
                   uint32_t e = uni(L.lroot[(uint32_t)hold & ((1u << LROOT) - 1u)]);
+                  if ((e & 0x700u) == 0u) {  // a literal (the common case first)
+                    PROF_ACC(16, t_sym);
+                    L.ring[ri(pos)] = (uint8_t)(e >> 16);
+                    ++pos;
+                    hold >>= (e & 15u);
+                    bits -= (int)(e & 15u);
+                    PROF_CNT(9, 1);
+                    continue;
+                  }
                   if (e_op(e) == OP_LONG) {
+                    PROF_T(t_long);
                     int nb = 0;
                     const int sy = canon(L.lit, lmax, hold, bits, &nb);
                     e = sym_entry(T_LIT, (uint32_t)sy, (uint32_t)nb);
+                    PROF_ACC(17, t_long);
+                    PROF_CNT(18, 1);
                   }
                   const uint32_t eo = e_op(e);
                   if (eo == OP_BAD) { err = E_DATA; break; }  // "invalid literal/length code"
@@ -574,29 +634,53 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
                     ++pos;
                     continue;
                   }
+                  PROF_T(t_m);
                   if (eo == OP_EOB) { mode = M_HEAD; break; }
                   const uint32_t lx = e_extra(e);
                   const uint32_t mlen = e_val(e) + (uint32_t)(hold & ((1ull << lx) - 1ull));
                   drop((int)lx);
+                  // a distance code and its extra bits need up to 28 bits
+                  if (bits < 28 && !refill()) {
+                    length = mlen;  // the lazy path goes on at the distance
+                    mode = M_DIST;
+                    break;
+                  }
                   uint32_t g = uni(L.droot[(uint32_t)hold & ((1u << DROOT) - 1u)]);
                   if (e_op(g) == OP_LONG) {
                     int nb = 0;
                     const int sy = canon(L.dist, dmax, hold, bits, &nb);
                     g = sym_entry(T_DIST, (uint32_t)sy, (uint32_t)nb);
+                    PROF_CNT(19, 1);
                   }
                   if (e_op(g) == OP_BAD) { err = E_DATA; break; }  // "invalid distance code"
                   drop((int)e_len(g));
+                  PROF_ACC(20, t_m);
+                  PROF_T(t_c);
                   const uint32_t dx = e_extra(g);
                   const uint32_t md = e_val(g) + (uint32_t)(hold & ((1ull << dx) - 1ull));
                   drop((int)dx);
-                  if ((int64_t)md > pos - wstart) { err = E_DATA; break; }  // "invalid distance too far back"
-                  copy_match(mlen, md);
+                  if ((int32_t)md > pos - wstart) { err = E_DATA; break; }  // "invalid distance too far back"
+                  PROF_CNT(10, 1);
+                  PROF_CNT(11, mlen);
+                  if (md >= mlen && mlen <= 64u) {  // one chunk, no overlap
+                    if ((uint32_t)lane < mlen) {
+                      const uint8_t v = L.ring[ri(pos - (int32_t)md + lane)];
+                      L.ring[ri(pos + lane)] = v;
+                    }
+                    pos += (int32_t)mlen;
+                  } else {
+                    copy_match(mlen, md);
+                  }
+                  PROF_ACC(21, t_c);
+                  PROF_ACC(22, t_sym);
                 }
                 ip -= (uint32_t)(bits >> 3);
                 bits &= 7;
                 hold &= (1ull << bits) - 1ull;
+                PROF_ACC(2, t_fast);
                 if (err || mode != M_LEN) break;
               }
+              PROF_CNT(13, 1);
               // one symbol, pulling bytes lazily
               uint32_t e = 0;
               bool ok = tdec(L.lroot, LROOT, &L.lit, lmax, T_LIT, hold, bits, &e);
@@ -649,7 +733,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
                 dist += (uint32_t)(hold & ((1u << extra) - 1u));
                 drop((int)extra);
               }
-              if ((int64_t)dist > pos - wstart) { err = E_DATA; break; }  // "invalid distance too far back"
+              if ((int32_t)dist > pos - wstart) { err = E_DATA; break; }  // "invalid distance too far back"
               copy_match(length, dist);
               mode = M_LEN;
               break;
@@ -667,6 +751,11 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
               break;
             }
           }
+#ifdef WSG_INFLATE_PROF
+          if (mode0 <= M_CODELENS) PROF_ACC(3, t_it);
+          else if (mode0 <= M_DISTEXT) PROF_ACC(4, t_it);
+          else PROF_ACC(5, t_it);
+#endif
         }
         if (err == E_NONE && mode == M_DONE && !finished) {
           finished = 1;
@@ -679,7 +768,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
         break;
       }
       if (fin && a.no_context) has_dec = 0;  // decoder.event(ENDING); decoder = null (DeflateDecoder.java:107-110)
-      const int64_t produced = pos - fstart;
+      const int32_t produced = pos - fstart;
       if (produced == 0) {  // no buffer came out (DeflateDecoder.java:122-131)
         const bool single_zero = plen == 1 && a.payload[src0] == 0;
         if (!single_zero) {
@@ -718,6 +807,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   if ((err == E_DATA || err == E_NODATA) && err_end > flushed && !flush_to(err_end)) err = E_CAP;
   __syncthreads();
 
+  PROF_T(t_cm);
   wsg_session_result res = {delivered, 0u, 0u, 0};
   uint32_t rf = 0xffffffffu;
   if (err == E_CAP) {  // nothing committed: the caller retries with a larger region
@@ -731,8 +821,8 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   } else {
     // commit: at the start of a message left open, else at the end
     const bool open = compressing && snap_k >= 0;
-    const int64_t P = open ? snap_pos : pos;
-    const int64_t W = open ? snap_wstart : wstart;
+    const int32_t P = open ? snap_pos : pos;
+    const int32_t W = open ? snap_wstart : wstart;
     const int chas = open ? snap_has : has_dec, cfin = open ? snap_fin : finished;
     wsg_inflate_state st = st0;
     st.compressing = open ? 0 : (uint8_t)compressing;
@@ -741,17 +831,17 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
     st.window_len = 0;
     st.window_phase = 0;
     if (chas && !cfin) {
-      const int64_t n = (P - W) < WSG_INFLATE_WINDOW ? (P - W) : WSG_INFLATE_WINDOW;
+      const int32_t n = (P - W) < (int32_t)WSG_INFLATE_WINDOW ? (P - W) : (int32_t)WSG_INFLATE_WINDOW;
       // the new image: slot j holds position q(j) in [P - 32768, P).  q < 0: the old
       // image already has it (same phase); q >= pos - 32768: the ring; else this
       // batch's output in HBM (flushed).  Slots below the history are don't-care.
       const uint32_t nph = ri(P);
-      const int64_t ring_lo = pos - (int64_t)WSG_INFLATE_WINDOW;
-      const int64_t lo = (P - n) > 0 ? (P - n) : 0;
+      const int32_t ring_lo = pos - (int32_t)WSG_INFLATE_WINDOW;
+      const int32_t lo = (P - n) > 0 ? (P - n) : 0;
       __threadfence_block();
       for (uint32_t c = lane; c < WSG_INFLATE_WINDOW / 16; c += 64) {
         const uint32_t j0 = 16u * c;
-        const int64_t q0 = P - (int64_t)WSG_INFLATE_WINDOW + (int64_t)((j0 - nph) & WMASK);
+        const int32_t q0 = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)((j0 - nph) & WMASK);
         const bool wraps = nph > j0 && nph < j0 + 16u;
         if (!wraps && q0 + 16 <= lo) continue;  // nothing to write
         if (!wraps && win_aligned && q0 >= 0 && q0 >= ring_lo) {
@@ -760,7 +850,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
         }
         for (uint32_t t = 0; t < 16u; ++t) {
           const uint32_t j = j0 + t;
-          const int64_t q = P - (int64_t)WSG_INFLATE_WINDOW + (int64_t)((j - nph) & WMASK);
+          const int32_t q = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)((j - nph) & WMASK);
           if (q < lo) continue;
           win[j] = q >= ring_lo ? L.ring[j] : out[q];
         }
@@ -775,6 +865,12 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
     a.result[s] = res;
     a.replay_from[s] = rf;
   }
+  PROF_ACC(7, t_cm);
+  PROF_ACC(0, t_all);
+#ifdef WSG_INFLATE_PROF
+  if (lane == 0)
+    for (int i = 0; i < 24; ++i) atomicAdd(&g_infl_prof[i], (unsigned long long)pf_[i]);
+#endif
 }
 
 void launch_inflate(const InflArgs& a, hipStream_t s) {

@@ -1,0 +1,7 @@
+#!/bin/bash
+# Diagnostic binaries for k_inflate (phase clocks and a plain runner for counters).
+set -e
+cd "$(dirname "$0")/.."
+H="/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -Iinclude -Isnf4j_amd/csrc"
+$H tools/prof_inflate.hip -o tools/prof_inflate
+$H -DNO_PROF tools/prof_inflate.hip -o tools/run_inflate
