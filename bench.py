@@ -41,6 +41,7 @@ def parse():
                     help="skip the secondary BASELINE configs (measured at N=1 only)")
     ap.add_argument("--extra-steps", type=int, default=10)
     ap.add_argument("--inflate-only", action="store_true", help="only the permessage-deflate inflate line")
+    ap.add_argument("--handshake-only", action="store_true", help="only the server handshake line")
     ap.add_argument("--inflate-sessions", type=int, nargs="+", default=[8192])
     return ap.parse_args()
 
@@ -97,6 +98,9 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     ctx = snf4j_amd.Context(local, stream=stream)
+    if args.handshake_only:
+        print(json.dumps(handshake_line(ctx, dev, args.extra_steps, 2)), flush=True)
+        return
     if args.inflate_only:
         for n_s in args.inflate_sessions:
             print(json.dumps(inflate_line(ctx, dev, args.extra_steps, 2, n_s=n_s, cpu_seconds=0.2)), flush=True)
@@ -439,6 +443,70 @@ def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps
             "pipeline_ms": pipe, **({"aggregate": agg} if agg else {})}
 
 
+def handshake_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
+    """Server opening handshakes (wsg_handshake_accept_batch_device)
+    over a device-resident connection storm: n browser-like upgrade requests, random keys.
+    One lane per request: the bound is per-lane serial parsing + SHA-1, reported against
+    HBM for scale.  cpu_baseline: the Python restatement (oracle/handshake_oracle.py) on
+    one host core (no JDK on the box)."""
+    import base64
+    import numpy as np
+    import torch
+    from oracle import handshake_oracle as H
+    from snf4j_amd._lib import HS_RESP_STRIDE, HS_RESULT_DTYPE, HsConfig
+    tmpl = H.request("/chat?room=lobby", [
+        ("Host", "ws.example.com:8080"), ("Connection", "Upgrade"), ("Pragma", "no-cache"),
+        ("Cache-Control", "no-cache"), ("User-Agent", "Mozilla/5.0 (X11; Linux x86_64) AppleWebKit/537.36"),
+        ("Upgrade", "websocket"), ("Origin", "https://example.com"), ("Sec-WebSocket-Version", "13"),
+        ("Accept-Encoding", "gzip, deflate, br"), ("Accept-Language", "en-US,en;q=0.9"),
+        ("Sec-WebSocket-Key", "A" * 24)])
+    L = len(tmpl)
+    kpos = tmpl.index(b"A" * 24)
+    rng = np.random.default_rng(0x4A5)
+    raw = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    k24 = np.frombuffer(b"".join(base64.b64encode(r.tobytes()) for r in raw), dtype=np.uint8).reshape(n, 24)
+    buf = np.tile(np.frombuffer(tmpl, dtype=np.uint8), (n, 1))
+    buf[:, kpos:kpos + 24] = k24
+    req = torch.from_numpy(buf.reshape(-1)).to(dev)
+    off = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
+    resp = torch.empty(n * HS_RESP_STRIDE, dtype=torch.uint8, device=dev)
+    res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    cfg = HsConfig(65536, 0, 0, 0, 0)
+
+    def step():
+        ctx.handshake_accept_device(cfg, req, off, resp, res, n=n)
+
+    step()
+    torch.cuda.synchronize(dev)
+    r = res.cpu().numpy().view(HS_RESULT_DTYPE)
+    assert (r["kind"] == H.ACCEPT).all() and (r["http_status"] == 101).all()
+    rh = resp.view(n, HS_RESP_STRIDE)
+    for i in (0, 1, n // 2, n - 1):  # spot check against the restatement
+        exp = H.accept(buf[i].tobytes())["response"]
+        assert rh[i, :int(r["resp_len"][i])].cpu().numpy().tobytes() == exp, i
+    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_hs_accept")
+    rl = int(r["resp_len"][0])
+    alg = n * (L + 8 + rl + 16)
+    ach = alg / (kms / 1e3) / 1e9
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < cpu_seconds:
+        H.accept(buf[done % n].tobytes())
+        done += 1
+    t = time.perf_counter() - t0
+    return {"config": f"server handshake: {n} upgrade requests of {L} B (browser-like, random keys), "
+                      "HandshakeDecoder + Handshaker.accept + 101 response with Sec-WebSocket-Accept",
+            "value": round(n * steps / el / 1e6, 3), "unit": "M handshakes/s",
+            "ms_per_step": round(el / steps * 1e3, 4),
+            "roofline": {"kernel": "k_hs_accept", "bound": "per-lane serial parse + SHA-1 (not hbm)",
+                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": round(kms, 4)},
+            "cpu_baseline": {"value": round(done / t / 1e6, 5), "unit": "M handshakes/s", "cores": 1, "kind": "port",
+                             "sample": f"{done} requests through the Python restatement "
+                                       f"(oracle/handshake_oracle.py) in {t:.1f} s, 1 thread; no JDK on the box"},
+            "pipeline_ms": pipe}
+
+
 def measure_extras(ctx, dev, args):
     """The other 1-GPU configurations of BASELINE.json, each a device-resident batch."""
     import numpy as np
@@ -511,6 +579,7 @@ def measure_extras(ctx, dev, args):
     del payload, wire_out
     torch.cuda.empty_cache()
     out.append(inflate_line(ctx, dev, K, W))
+    out.append(handshake_line(ctx, dev, K, W))
     return out
 
 

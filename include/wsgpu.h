@@ -449,6 +449,90 @@ int wsg_inflate_batch_host(wsg_ctx* ctx, int no_context,
                            wsg_frame_desc* out_desc, wsg_session_result* out_result,
                            uint32_t* replay_from);
 
+/* ---------------- opening handshake, server side ------- */
+/* Replaces, for a batch of server sessions whose handshake request arrives
+ * together (a connection storm), the read-loop pair
+ *   HandshakeDecoder.available/decode   handshake/HandshakeDecoder.java:141-235
+ *     (HttpUtils.available/splitRequestLine/splitHeaderField HttpUtils.java:77-220,
+ *      HandshakeFactory.parse/parseFields HandshakeFactory.java:47-127,
+ *      HandshakeFrame.addValue HandshakeFrame.java:74-91)
+ *   Handshaker.handshake(request) -> accept   handshake/Handshaker.java:208-405,555-578
+ *     (HandshakeUtils.parseKey/generateAnswerKey HandshakeUtils.java:93-115, Base64Util)
+ * and formats the response the way HandshakeEncoder/HandshakeFactory.format do
+ * (HandshakeFactory.java:129-158).  One GPU lane per request.
+ *
+ * The lane resolves every request whose form it can decide exactly; the rest come
+ * back as WSG_HS_DEFER for the Java Handshaker (the policy layer that stays on the
+ * host): folded or name-continued header lines, a repeated Upgrade/Connection/
+ * Host/Sec-WebSocket-* field, non-ASCII bytes in the request line or those fields,
+ * request URIs outside [A-Za-z0-9-._~!*'()/?=&+,;$] and %XX (java.net.URI decides
+ * the rest), Host values outside [A-Za-z0-9.-:], subprotocol / extension offers
+ * when the config supports any, a config with its own acceptRequestUri or
+ * customizeHeaders, and frames of more lines than one HandshakeDecoder chunk (50). */
+#define WSG_HS_RESP_STRIDE 160   /* response bytes reserved per request */
+
+typedef struct wsg_hs_config {
+    uint32_t max_length;      /* getMaxHandshakeFrameLength() (65536) */
+    uint8_t ignore_host;      /* ignoreHostHeaderField() */
+    uint8_t subprotocols;     /* getSupportedSubProtocols() != null: offers are deferred */
+    uint8_t extensions;       /* getSupportedExtensions() != null: offers are deferred */
+    uint8_t host_policy;      /* acceptRequestUri/customizeHeaders overridden: accepts are deferred */
+} wsg_hs_config;
+
+typedef enum wsg_hs_kind {
+    WSG_HS_NEED_MORE = 0,     /* no complete frame yet (available() == 0) */
+    WSG_HS_DEFER = 1,         /* the Java HandshakeDecoder/Handshaker takes this request */
+    WSG_HS_PARSE_ERROR = 2,   /* HandshakeDecoder: writenf(HandshakeResponse(status)) + exception (:194-203) */
+    WSG_HS_ACCEPT = 3         /* Handshaker.accept returned a response (101 or a refusal) */
+} wsg_hs_kind;
+
+typedef enum wsg_hs_cause {
+    WSG_HSC_NONE = 0,
+    WSG_HSC_BAD_REQUEST_LINE = 1,    /* "Invalid http request"              HandshakeFactory.java:100 */
+    WSG_HSC_BAD_VERSION = 2,         /* "Invalid http request version"      :103 */
+    WSG_HSC_FORBIDDEN = 3,           /* "Forbidden http request command"    :106 (403) */
+    WSG_HSC_TOO_LARGE = 4,           /* "Handshake frame too large"         HandshakeDecoder.java:169 (413) */
+    WSG_HSC_MISSING_VERSION = 5,     /* "Missing websocket version"         Handshaker.java:232 */
+    WSG_HSC_INCORRECT_VERSION = 6,   /* "Incorrect websocket version: %s"   :219 (detail = the token) */
+    WSG_HSC_UNSUPPORTED_VERSION = 7, /* "Unsupported websocket version: %s" :229 (426; detail = the value) */
+    WSG_HSC_MISSING_UPGRADE = 8,     /* "Missing websocket upgrade"         :425 */
+    WSG_HSC_MISSING_CONNECTION = 9,  /* "Missing websocket connection"      :429 */
+    WSG_HSC_INVALID_UPGRADE = 10,    /* "Invalid websocket upgrade: %s"     :441 */
+    WSG_HSC_INVALID_CONNECTION = 11, /* "Invalid websocket connection: %s"  :437 */
+    WSG_HSC_MISSING_HOST = 12,       /* "Missing websocket request host"    :336 */
+    WSG_HSC_MISSING_KEY = 13,        /* "Missing websocket key"             :254 */
+    WSG_HSC_INVALID_KEY = 14,        /* "Invalid websocket key: %s"         :251 */
+    /* why a request was deferred (WSG_HS_DEFER) */
+    WSG_HSC_D_LINE_FORM = 32, WSG_HSC_D_REPEATED = 33, WSG_HSC_D_NON_ASCII = 34, WSG_HSC_D_URI = 35,
+    WSG_HSC_D_HOST = 36, WSG_HSC_D_SUBPROTOCOL = 37, WSG_HSC_D_EXTENSION = 38, WSG_HSC_D_POLICY = 39,
+    WSG_HSC_D_LINES = 40
+} wsg_hs_cause;
+
+typedef struct wsg_hs_result {
+    uint32_t frame_len;    /* handshake frame bytes (HandshakeDecoder.available); the rest of the
+                              request buffer is the first WebSocket bytes of the session */
+    uint16_t http_status;  /* 101, 400, 403, 413, 426 (0 for NEED_MORE / DEFER) */
+    uint8_t kind;          /* wsg_hs_kind */
+    uint8_t cause;         /* wsg_hs_cause: the exception message or Handshaker closing reason */
+    uint16_t resp_len;     /* bytes of the formatted response at resp + i * WSG_HS_RESP_STRIDE */
+    uint16_t detail_len;   /* the %s of the cause: request bytes [detail_off, +detail_len) */
+    uint32_t detail_off;
+} wsg_hs_result; /* 16 bytes */
+
+/* HttpUtils.available over one request buffer with HandshakeDecoder's default chunk
+ * (50 lines): the frame length, or 0 (no complete frame / the chunk is full). */
+int wsg_handshake_available(const uint8_t* data, uint64_t len);
+
+/* Requests i in [0, n): req[req_off[i], req_off[i+1]) (device pointers, req and resp
+ * 16-B aligned).  Writes
+ * result[i] and, for PARSE_ERROR / ACCEPT, the response bytes to
+ * resp[i * WSG_HS_RESP_STRIDE, + resp_len). */
+int wsg_handshake_accept_batch_device(wsg_ctx* ctx, const wsg_hs_config* cfg, const uint8_t* req,
+                                      const uint64_t* req_off, uint32_t n, uint8_t* resp, wsg_hs_result* result);
+/* Same with host pointers (H2D, kernel, D2H). */
+int wsg_handshake_accept_batch_host(wsg_ctx* ctx, const wsg_hs_config* cfg, const uint8_t* req,
+                                    const uint64_t* req_off, uint32_t n, uint8_t* resp, wsg_hs_result* result);
+
 /* ---------------- synthetic workloads (bench / tests only) ---------------- */
 /* Fill a device batch of uniform frames: n_frames frames of payload_len bytes,
  * frame k at k*frame_len in wire (frame_len = wsg_encoded_length(payload_len, masked)),

@@ -10,11 +10,13 @@ from . import _lib  # noqa: F401  (fails loudly if libwsgpu.so is missing)
 from .codec import (BatchAggregator, BatchInflater, FrameAggregator, FrameDecoder, FrameEncoder, FrameUtf8Validator,
                     NativeBatcher, PerMessageDeflateDecoder, SessionBatcher)
 from .context import Context, decoder_cfg, encoded_length, error_message, frame_available
+from .handshake import BatchHandshaker, HandshakeConfig, HandshakeOutcome
 from .frame import (AggregatedBinaryFrame, AggregatedTextFrame, BinaryFrame, CloseFrame, ContinuationFrame, Frame,
                     InvalidFrameException, Opcode, PingFrame, PongFrame, TextFrame)
 
 __all__ = ["Context", "FrameDecoder", "FrameEncoder", "SessionBatcher", "FrameAggregator", "BatchAggregator",
            "FrameUtf8Validator", "NativeBatcher", "BatchInflater", "PerMessageDeflateDecoder",
            "AggregatedTextFrame", "AggregatedBinaryFrame", "decoder_cfg", "encoded_length",
-           "error_message", "frame_available", "Frame", "Opcode", "TextFrame", "BinaryFrame", "ContinuationFrame",
+           "error_message", "frame_available",
+           "BatchHandshaker", "HandshakeConfig", "HandshakeOutcome", "Frame", "Opcode", "TextFrame", "BinaryFrame", "ContinuationFrame",
            "CloseFrame", "PingFrame", "PongFrame", "InvalidFrameException"]

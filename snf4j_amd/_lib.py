@@ -50,6 +50,14 @@ class EncodeFrame(C.Structure):
                 ("reserved2", C.c_uint32)]
 
 
+class HsConfig(C.Structure):
+    _fields_ = [("max_length", C.c_uint32), ("ignore_host", C.c_uint8), ("subprotocols", C.c_uint8),
+                ("extensions", C.c_uint8), ("host_policy", C.c_uint8)]
+
+
+HS_RESP_STRIDE = 160
+
+
 assert C.sizeof(SessionState) == 8 and C.sizeof(FrameDesc) == 16
 assert C.sizeof(SessionResult) == 16 and C.sizeof(EncodeFrame) == 24
 
@@ -74,6 +82,9 @@ try:
                             ("msg_len", "<u4"), ("mask", "<u4"), ("inject_pos", "<i4"), ("opcode", "u1"),
                             ("flags", "u1"), ("text", "u1"), ("inject_kind", "u1")])
     assert SYNTH_DTYPE.itemsize == 40
+    HS_RESULT_DTYPE = np.dtype([("frame_len", "<u4"), ("http_status", "<u2"), ("kind", "u1"), ("cause", "u1"),
+                                ("resp_len", "<u2"), ("detail_len", "<u2"), ("detail_off", "<u4")])
+    assert HS_RESULT_DTYPE.itemsize == 16
 except ImportError:  # pragma: no cover
     np = None
 
@@ -134,6 +145,9 @@ def _load():
         "wsg_validate_batch_host": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_aggregate_batch_device": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, p], i32),
         "wsg_aggregate_batch_host": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, P(u64)], i32),
+        "wsg_handshake_available": ([p, u64], i32),
+        "wsg_handshake_accept_batch_device": ([p, P(HsConfig), p, p, u32, p, p], i32),
+        "wsg_handshake_accept_batch_host": ([p, P(HsConfig), p, p, u32, p, p], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

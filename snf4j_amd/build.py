@@ -9,7 +9,7 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libwsgpu.so")
-SOURCES = ["decode.hip", "encode.hip", "aggregate.hip", "synth.hip", "api.hip", "batcher.hip", "inflate.hip"]
+SOURCES = ["decode.hip", "encode.hip", "aggregate.hip", "synth.hip", "api.hip", "batcher.hip", "inflate.hip", "handshake.hip"]
 HEADERS = ["ws_rules.h", "wsgpu_internal.h", "wsgpu_scan.h", "../../include/wsgpu.h"]
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -disable-promote-alloca-to-lds: a dynamically indexed local array must not turn

@@ -229,6 +229,30 @@ class Context:
                                          rf.ctypes.data), self._h)
         return out, odesc[:n], res[:n_s], rf[:n_s]
 
+    # -------------------------------------------------------------- handshake
+    def handshake_accept_device(self, cfg, req, req_off, resp, result, n: int | None = None):
+        """Enqueue the server handshake over a device batch (wsg_handshake_accept_batch_device):
+        req uint8, req_off int64 (n + 1), resp uint8 (n * HS_RESP_STRIDE), result uint8 byte view
+        (n * 16), all cuda tensors."""
+        n = req_off.numel() - 1 if n is None else int(n)
+        assert resp.numel() >= n * _lib.HS_RESP_STRIDE and result.numel() >= n * 16
+        check(lib.wsg_handshake_accept_batch_device(self._h, C.byref(cfg), _p(req), _p(req_off), n, _p(resp),
+                                                    _p(result)), self._h)
+
+    def handshake_accept_host(self, cfg, req: np.ndarray, req_off: np.ndarray):
+        """The server handshake over a host batch (wsg_handshake_accept_batch_host).
+        Returns (resp [n, HS_RESP_STRIDE] uint8, result HS_RESULT_DTYPE[n])."""
+        from ._lib import HS_RESULT_DTYPE
+        req = np.ascontiguousarray(req, dtype=np.uint8)
+        req_off = np.ascontiguousarray(req_off, dtype=np.uint64)
+        n = len(req_off) - 1
+        resp = np.zeros((max(1, n), _lib.HS_RESP_STRIDE), dtype=np.uint8)
+        res = np.zeros(max(1, n), dtype=HS_RESULT_DTYPE)
+        r = req if req.size else np.zeros(16, np.uint8)
+        check(lib.wsg_handshake_accept_batch_host(self._h, C.byref(cfg), r.ctypes.data, req_off.ctypes.data, n,
+                                                  resp.ctypes.data, res.ctypes.data), self._h)
+        return resp[:n], res[:n]
+
     # -------------------------------------------------------------- aggregate
     def aggregate_device(self, max_aggregated_len: int, desc, session_first, dec_result, payload, state, agg_out,
                          out_desc, out_result, agg_total, n_frames: int | None = None):

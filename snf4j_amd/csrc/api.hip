@@ -15,7 +15,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate"};
+                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -127,7 +127,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE)) {
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT)) {
     f();
     return;
   }
@@ -882,6 +882,59 @@ int wsg_inflate_batch_host(wsg_ctx* c, int no_context, const wsg_frame_desc* des
     HIP_TRY(c, hipMemcpyAsync(window, d_win.p, S * WSG_INFLATE_WINDOW, hipMemcpyDeviceToHost, s));
     HIP_TRY(c, hipMemcpyAsync(replay_from, d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
   }
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
+
+// ---- opening handshake (server side), SURVEY §8f rank 4 ----
+
+int wsg_handshake_available(const uint8_t* data, uint64_t len) {
+  if (!data && len) return WSG_API_EINVAL;
+  int capped = 0;
+  int64_t lines_end = 0;
+  return ws::hs_frame_len(data, (int64_t)len, &capped, &lines_end);
+}
+
+int wsg_handshake_accept_batch_device(wsg_ctx* c, const wsg_hs_config* cfg, const uint8_t* req,
+                                      const uint64_t* req_off, uint32_t n, uint8_t* resp, wsg_hs_result* result) {
+  if (!c || !cfg) return WSG_API_EINVAL;
+  if (!n) return WSG_API_OK;
+  if (!req || !req_off || !resp || !result) return set_err(c, WSG_API_EINVAL, "null batch pointer");
+  if (((uintptr_t)req & 15) || ((uintptr_t)resp & 15))
+    return set_err(c, WSG_API_EINVAL, "req and resp must be 16-B aligned");
+  HIP_TRY(c, hipSetDevice(c->device));
+  timed(c, K_HS_ACCEPT, [&] { ws::launch_hs_accept(*cfg, req, req_off, n, resp, result, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_handshake_accept_batch_host(wsg_ctx* c, const wsg_hs_config* cfg, const uint8_t* req,
+                                    const uint64_t* req_off, uint32_t n, uint8_t* resp, wsg_hs_result* result) {
+  if (!c || !cfg) return WSG_API_EINVAL;
+  if (!n) return WSG_API_OK;
+  if (!req_off || !resp || !result) return set_err(c, WSG_API_EINVAL, "null batch pointer");
+  for (uint32_t i = 0; i < n; ++i)
+    if (req_off[i + 1] < req_off[i]) return set_err(c, WSG_API_EINVAL, "req_off not ascending at %u", i);
+  if (req_off[0] != 0) return set_err(c, WSG_API_EINVAL, "req_off[0] must be 0");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t len = req_off[n];
+  DevBuf d_req, d_off, d_resp, d_res;
+  struct Guard {
+    DevBuf* b[4];
+    ~Guard() { for (DevBuf* x : b) x->release(); }
+  } g{{&d_req, &d_off, &d_resp, &d_res}};
+  HIP_TRY(c, d_req.ensure(len + 16));
+  HIP_TRY(c, d_off.ensure(((uint64_t)n + 1) * sizeof(uint64_t)));
+  HIP_TRY(c, d_resp.ensure((uint64_t)n * WSG_HS_RESP_STRIDE));
+  HIP_TRY(c, d_res.ensure((uint64_t)n * sizeof(wsg_hs_result)));
+  hipStream_t s = c->stream;
+  if (len) HIP_TRY(c, hipMemcpyAsync(d_req.p, req, len, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(d_off.p, req_off, ((uint64_t)n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  int rc = wsg_handshake_accept_batch_device(c, cfg, (const uint8_t*)d_req.p, (const uint64_t*)d_off.p, n,
+                                             (uint8_t*)d_resp.p, (wsg_hs_result*)d_res.p);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(resp, d_resp.p, (uint64_t)n * WSG_HS_RESP_STRIDE, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(result, d_res.p, (uint64_t)n * sizeof(wsg_hs_result), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   return WSG_API_OK;
 }

@@ -1,0 +1,601 @@
+// handshake.hip — the server side of the WebSocket opening handshake on gfx950:
+// HandshakeDecoder (HandshakeDecoder.java:141-235) + Handshaker.accept
+// (Handshaker.java:208-405) + the response format of HandshakeFactory.format
+// (HandshakeFactory.java:129-158), for a batch of requests, one lane per request.
+//
+// A request is a few hundred bytes of serial HTTP parsing, so the lane is the unit:
+// 64 requests per wave, each lane walking its own bytes (they stay in the L1/L2
+// lines the first pass brought in).  No LDS, no cross-lane traffic.  The lane
+// decides every request whose form it can reproduce exactly and defers the rest to
+// the Java Handshaker (wsgpu.h lists the deferred forms).
+#include "wsgpu_internal.h"
+
+namespace ws {
+
+namespace {
+
+constexpr uint8_t CR = 13, LF = 10, SP = ' ', HT = '\t';
+constexpr int MAX_LINES = 50;  // HandshakeDecoder.DEFAULT_MAX_LINES_IN_CHUNK (HandshakeDecoder.java:50)
+
+struct Span {
+  int32_t b, e;  // [b, e) in the request; b < 0: absent
+};
+
+// A lane's view of its request: bytes come from 16-B aligned blocks held in
+// registers, so a forward scan costs one load per 16 bytes instead of one per byte
+// (the batch buffer is 16-B aligned: a block never leaves the allocation's granule).
+struct Req {
+  const uint4* base;  // the aligned block holding byte 0
+  uint32_t lead;      // byte 0's offset in that block
+  int32_t cq = -1;    // cached block index
+  uint4 blk;
+  __device__ uint8_t operator[](int32_t i) {
+    const uint32_t a = lead + (uint32_t)i;
+    const int32_t q = (int32_t)(a >> 4);
+    if (q != cq) {
+      cq = q;
+      blk = base[q];
+    }
+    const uint32_t o = a & 15u;
+    const uint32_t w = o < 8u ? (o < 4u ? blk.x : blk.y) : (o < 12u ? blk.z : blk.w);
+    return (uint8_t)(w >> (8u * (o & 3u)));
+  }
+};
+
+// Target fields (upper-cased names, HandshakeFrame.key: HandshakeFrame.java:128-130).
+enum Field : int { F_HOST = 0, F_UPGRADE, F_CONNECTION, F_KEY, F_VERSION, F_PROTOCOL, F_EXTENSIONS, F_COUNT };
+
+__device__ __constant__ char kFieldNames[F_COUNT][25] = {"HOST", "UPGRADE", "CONNECTION", "SEC-WEBSOCKET-KEY",
+                                                         "SEC-WEBSOCKET-VERSION", "SEC-WEBSOCKET-PROTOCOL",
+                                                         "SEC-WEBSOCKET-EXTENSIONS"};
+__device__ __constant__ uint8_t kFieldLen[F_COUNT] = {4, 7, 10, 17, 21, 22, 24};
+
+__device__ __constant__ char kGuid[37] = "258EAFA5-E914-47DA-95CA-C5AB0DC85B11";  // HandshakeUtils.KEY_GUID
+__device__ __constant__ char kB64[65] = "ABCDEFGHIJKLMNOPQRSTUVWXYZabcdefghijklmnopqrstuvwxyz0123456789+/";
+
+__device__ __forceinline__ uint8_t up(uint8_t c) { return (c >= 'a' && c <= 'z') ? (uint8_t)(c - 32) : c; }
+
+// Base64Util.DECODING (Base64Util.java:48-68): -1 for bytes outside the alphabet ('=' included).
+__device__ __forceinline__ int b64v(uint8_t c) {
+  if (c >= 'A' && c <= 'Z') return c - 'A';
+  if (c >= 'a' && c <= 'z') return c - 'a' + 26;
+  if (c >= '0' && c <= '9') return c - '0' + 52;
+  if (c == '+') return 62;
+  if (c == '/') return 63;
+  return -1;
+}
+
+// String.trim(): chars <= ' ' off both ends.
+__device__ __forceinline__ Span trim(Req& d, Span s) {
+  while (s.b < s.e && d[s.b] <= SP) ++s.b;
+  while (s.e > s.b && d[s.e - 1] <= SP) --s.e;
+  return s;
+}
+
+// Iterate HttpUtils.values(s) (HttpUtils.java:311-333): split at ',', trim, skip empty.
+// f(token) returns true to stop; returns that token (b < 0 when none stopped).
+template <typename F>
+__device__ Span each_value(Req& d, Span s, F&& f) {
+  int32_t t0 = s.b;
+  for (int32_t i = s.b; i <= s.e; ++i) {
+    if (i == s.e || d[i] == ',') {
+      const Span t = trim(d, Span{t0, i});
+      if (t.e > t.b && f(t)) return t;
+      t0 = i + 1;
+    }
+  }
+  return Span{-1, -1};
+}
+
+// Integer.parseInt over ASCII: optional sign, decimal digits, int range.
+__device__ bool parse_int(Req& d, Span t, int64_t* v) {
+  int32_t i = t.b;
+  bool neg = false;
+  if (d[i] == '-' || d[i] == '+') {
+    neg = d[i] == '-';
+    if (t.e - t.b == 1) return false;
+    ++i;
+  }
+  int64_t x = 0;
+  for (; i < t.e; ++i) {
+    const uint8_t c = d[i];
+    if (c < '0' || c > '9') return false;
+    x = x * 10 + (c - '0');
+    if (x > 2147483648ll) return false;
+  }
+  if (!neg && x > 2147483647ll) return false;
+  *v = neg ? -x : x;
+  return true;
+}
+
+// equalsIgnoreCase against an upper-case ASCII literal.
+__device__ bool eq_icase(Req& d, Span t, const char* lit, int n) {
+  if (t.e - t.b != n) return false;
+  for (int i = 0; i < n; ++i)
+    if (up(d[t.b + i]) != (uint8_t)lit[i]) return false;
+  return true;
+}
+
+__device__ bool eq_exact(Req& d, Span t, const char* lit, int n) {
+  if (t.e - t.b != n) return false;
+  for (int i = 0; i < n; ++i)
+    if (d[t.b + i] != (uint8_t)lit[i]) return false;
+  return true;
+}
+
+// Handshaker.contains (Handshaker.java:407-418)
+__device__ bool contains(Req& d, Span s, const char* lit, int n) {
+  return each_value(d, s, [&](Span t) { return eq_icase(d, t, lit, n); }).b >= 0;
+}
+
+// --- SHA-1 (MessageDigest "SHA1") over key bytes + KEY_GUID: at most 24 + 36 bytes.
+__device__ __forceinline__ uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
+
+__device__ void sha1_block(uint32_t h[5], const uint32_t w0[16]) {
+  uint32_t w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = w0[i];
+  uint32_t a = h[0], b = h[1], c = h[2], dd = h[3], e = h[4];
+#pragma unroll
+  for (int t = 0; t < 80; ++t) {
+    if (t >= 16) w[t & 15] = rol(w[(t + 13) & 15] ^ w[(t + 8) & 15] ^ w[(t + 2) & 15] ^ w[t & 15], 1);
+    uint32_t f, k;
+    if (t < 20) { f = (b & c) | (~b & dd); k = 0x5A827999u; }
+    else if (t < 40) { f = b ^ c ^ dd; k = 0x6ED9EBA1u; }
+    else if (t < 60) { f = (b & c) | (b & dd) | (c & dd); k = 0x8F1BBCDCu; }
+    else { f = b ^ c ^ dd; k = 0xCA62C1D6u; }
+    const uint32_t tmp = rol(a, 5) + f + e + k + w[t & 15];
+    e = dd;
+    dd = c;
+    c = rol(b, 30);
+    b = a;
+    a = tmp;
+  }
+  h[0] += a; h[1] += b; h[2] += c; h[3] += dd; h[4] += e;
+}
+
+// Sec-WebSocket-Accept = Base64(SHA1(key + GUID)) (HandshakeUtils.generateAnswerKey,
+// HandshakeUtils.java:98-111): 28 characters to out.
+__device__ void accept_key(Req& d, Span key, uint8_t* out) {
+  const int kl = key.e - key.b;  // 22..24 (a parseable key)
+  const int total = kl + 36;     // <= 60: two blocks after padding
+  uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+  for (int blk = 0; blk < 2; ++blk) {
+    uint32_t w[16];
+    for (int j = 0; j < 16; ++j) {
+      uint32_t v = 0;
+      for (int q = 0; q < 4; ++q) {
+        const int i = blk * 64 + j * 4 + q;
+        uint32_t byte;
+        if (i < kl) byte = d[key.b + i];
+        else if (i < total) byte = (uint8_t)kGuid[i - kl];
+        else if (i == total) byte = 0x80u;
+        else byte = 0u;
+        v = (v << 8) | byte;
+      }
+      w[j] = v;
+    }
+    if (blk == 1) w[15] = (uint32_t)total * 8u;  // 60 bytes > 55: the length lands in block 2
+    sha1_block(h, w);
+  }
+  uint8_t dig[21];
+  for (int i = 0; i < 20; ++i) dig[i] = (uint8_t)(h[i >> 2] >> (24 - 8 * (i & 3)));
+  dig[20] = 0;
+  // Base64Util.encode (padding '='): 20 bytes -> 6 full groups + 2 bytes
+  int o = 0;
+  for (int i = 0; i < 18; i += 3) {
+    const uint32_t v = ((uint32_t)dig[i] << 16) | ((uint32_t)dig[i + 1] << 8) | dig[i + 2];
+    out[o++] = (uint8_t)kB64[(v >> 18) & 63];
+    out[o++] = (uint8_t)kB64[(v >> 12) & 63];
+    out[o++] = (uint8_t)kB64[(v >> 6) & 63];
+    out[o++] = (uint8_t)kB64[v & 63];
+  }
+  const uint32_t v = ((uint32_t)dig[18] << 16) | ((uint32_t)dig[19] << 8);
+  out[o++] = (uint8_t)kB64[(v >> 18) & 63];
+  out[o++] = (uint8_t)kB64[(v >> 12) & 63];
+  out[o++] = (uint8_t)kB64[(v >> 6) & 63];
+  out[o++] = '=';
+}
+
+// HandshakeUtils.parseKey (HandshakeUtils.java:113-120) over Base64Util.decode
+// (Base64Util.java:253-350, not MIME): true when the key decodes to 16 bytes.
+__device__ bool key_ok(Req& d, Span k) {
+  int32_t len = k.e - k.b, end = k.e;
+  if (len < 2) return false;  // EMPTY (0 bytes) or null
+  if (d[end - 1] == '=') {
+    --end;
+    --len;
+    if (d[end - 1] == '=') {
+      --end;
+      --len;
+    }
+  }
+  if (len == 0) return false;
+  int calc = (len / 4) * 3;
+  switch (len & 3) {
+    case 1: return false;
+    case 2: calc += 1; break;
+    case 3: calc += 2; break;
+    default: break;
+  }
+  for (int32_t i = k.b; i < end; ++i)
+    if (b64v(d[i]) < 0) return false;
+  return calc == 16;
+}
+
+// The request URI forms the lane accepts as java.net.URI would (a relative
+// reference without scheme, authority-safe characters, well-formed escapes).
+__device__ bool uri_fast(Req& d, Span u) {
+  for (int32_t i = u.b; i < u.e; ++i) {
+    const uint8_t c = d[i];
+    if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9')) continue;
+    switch (c) {
+      case '-': case '.': case '_': case '~': case '!': case '*': case '\'': case '(': case ')':
+      case '/': case '?': case '=': case '&': case '+': case ',': case ';': case '$':
+        continue;
+      case '%': {
+        auto hx = [](uint8_t x) { return (x >= '0' && x <= '9') || (x >= 'a' && x <= 'f') || (x >= 'A' && x <= 'F'); };
+        if (i + 2 < u.e && hx(d[i + 1]) && hx(d[i + 2])) {
+          i += 2;
+          continue;
+        }
+        return false;
+      }
+      default:
+        return false;
+    }
+  }
+  return true;
+}
+
+__device__ bool host_fast(Req& d, Span h) {
+  for (int32_t i = h.b; i < h.e; ++i) {
+    const uint8_t c = d[i];
+    if (!((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '.' || c == '-' ||
+          c == ':'))
+      return false;
+  }
+  return true;
+}
+
+__device__ bool ascii(Req& d, Span s) {
+  for (int32_t i = s.b; i < s.e; ++i)
+    if (d[i] >= 0x80) return false;
+  return true;
+}
+
+// Response bytes gathered into dwords: one 4-B store per 4 bytes (resp is 16-B aligned
+// and the stride a multiple of 4).  done() stores the last partial dword.
+struct Out {
+  uint8_t* p;
+  int n = 0;
+  uint32_t w = 0;
+  __device__ void byte(uint32_t c) {
+    w |= c << (8 * (n & 3));
+    if ((++n & 3) == 0) {
+      reinterpret_cast<uint32_t*>(p)[(n >> 2) - 1] = w;
+      w = 0;
+    }
+  }
+  __device__ void put(const char* s) {
+    while (*s) byte((uint8_t)*s++);
+  }
+  __device__ void put(const uint8_t* s, int len) {
+    for (int i = 0; i < len; ++i) byte(s[i]);
+  }
+  __device__ int done() {
+    if (n & 3) reinterpret_cast<uint32_t*>(p)[n >> 2] = w;
+    return n;
+  }
+};
+
+// HandshakeFactory.format of a HandshakeResponse(status) (HandshakeFactory.java:141-157)
+__device__ int status_response(uint8_t* resp, int status) {
+  Out o{resp};
+  switch (status) {
+    case 400: o.put("HTTP/1.1 400 Bad Request\r\n\r\n"); break;
+    case 403: o.put("HTTP/1.1 403 Forbidden\r\n\r\n"); break;
+    case 413: o.put("HTTP/1.1 413 Request Entity Too Large\r\n\r\n"); break;
+    case 426: o.put("HTTP/1.1 426 Upgrade Required\r\nSec-WebSocket-Version: 13\r\n\r\n"); break;
+    default: break;
+  }
+  return o.done();
+}
+
+}  // namespace
+
+// HttpUtils.available (HttpUtils.java:77-110) with HandshakeDecoder's lines array of
+// MAX_LINES*2+1 entries: frame length, or 0 (incomplete, or *capped: the chunk is
+// full).  *lines_end: the end of the last complete line recorded, the chunk
+// HandshakeDecoder.available0 (:221-233) hands to decode when no frame is complete.
+template <typename D>
+__host__ __device__ int frame_len_t(D& d, int64_t len, int* capped, int64_t* lines_end) {
+  const int max_count = MAX_LINES * 2 + 1 - 3;
+  int line_count = 0;
+  uint8_t prev, curr = 0;
+  bool end = false;
+  *capped = 0;
+  *lines_end = 0;
+  for (int64_t i = 0; i < len; ++i) {
+    prev = curr;
+    curr = d[i];
+    if (curr == LF) {
+      if (prev == CR) {
+        if (end) return (int)(i + 1);
+        if (line_count > max_count) {
+          *capped = 1;
+          return 0;
+        }
+        end = true;
+        line_count += 2;
+        *lines_end = i + 1;
+      }
+    } else if (curr != CR) {
+      end = false;
+    }
+  }
+  return 0;
+}
+
+__host__ __device__ int hs_frame_len(const uint8_t* d, int64_t len, int* capped, int64_t* lines_end) {
+  return frame_len_t(d, len, capped, lines_end);
+}
+
+namespace {
+
+__device__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t* resp, wsg_hs_result* res) {
+  wsg_hs_result r = {0u, 0, WSG_HS_NEED_MORE, WSG_HSC_NONE, 0, 0, 0u};
+  auto finish = [&](int kind, int status, int cause, Span detail) {
+    r.kind = (uint8_t)kind;
+    r.http_status = (uint16_t)status;
+    r.cause = (uint8_t)cause;
+    if (detail.b >= 0) {
+      r.detail_off = (uint32_t)detail.b;
+      r.detail_len = (uint16_t)(detail.e - detail.b);
+    }
+    if (kind == WSG_HS_PARSE_ERROR || (kind == WSG_HS_ACCEPT && status != 101))
+      r.resp_len = (uint16_t)status_response(resp, status);
+    *res = r;
+  };
+  const Span none{-1, -1};
+  int capped = 0;
+  int64_t lines_end = 0;
+  const int flen = frame_len_t(d, n, &capped, &lines_end);
+  if (capped) {
+    finish(WSG_HS_DEFER, 0, WSG_HSC_D_LINES, none);
+    return;
+  }
+  // No complete frame: HandshakeDecoder still decodes the complete lines as a chunk
+  // (available0, :221-233), so the length cap and the request line are judged now.
+  const bool partial = flen == 0;
+  const int32_t limit = partial ? (int32_t)lines_end : flen;
+  if (partial && limit == 0) {
+    finish(WSG_HS_NEED_MORE, 0, WSG_HSC_NONE, none);
+    return;
+  }
+  r.frame_len = (uint32_t)flen;
+  // HandshakeDecoder.decode (:166-171): frameLength > maxLength -> 413
+  if ((uint32_t)limit > cfg.max_length) {
+    finish(WSG_HS_PARSE_ERROR, 413, WSG_HSC_TOO_LARGE, none);
+    return;
+  }
+  // second pass over the lines of the frame: the request line, then header fields
+  Span fld[F_COUNT];
+  for (int f = 0; f < F_COUNT; ++f) fld[f] = none;
+  Span uri = none;
+  {
+    // the lines HttpUtils.available recorded: CRLF-ended, up to the CRLF met with
+    // `end` still set (the scan of hs_frame_len, replayed)
+    int32_t line0 = 0;
+    uint8_t prev, curr = 0;
+    bool end = false;
+    int line_no = 0;
+    for (int32_t i = 0; i < limit; ++i) {
+      prev = curr;
+      curr = d[i];
+      if (curr != LF) {
+        if (curr != CR) end = false;
+        continue;
+      }
+      if (prev != CR) continue;
+      if (end) break;
+      end = true;
+      const int32_t lb = line0, le = i - 1;
+      line0 = i + 1;
+      if (line_no++ == 0) {
+        // HandshakeFactory.parse (:96-107) with HttpUtils.splitRequestLine (:125-157), out[10]
+        Span tok[3];
+        int count = 0;
+        int32_t t0 = lb;
+        uint8_t p2, c2 = 0;
+        bool over = false;
+        for (int32_t j = lb; j < le && !over; ++j) {
+          p2 = c2;
+          c2 = d[j];
+          if (c2 == SP) {
+            if (p2 != SP) {
+              if (count < 3) tok[count] = Span{t0, j};
+              ++count;
+              if (count * 2 > 8) over = true;
+            }
+          } else if (p2 == SP) {
+            t0 = j;
+          }
+        }
+        if (!over) {
+          if (count < 3) tok[count] = (c2 == SP) ? Span{le, le} : Span{t0, le};
+          ++count;
+        }
+        if (count != 3) {
+          finish(WSG_HS_PARSE_ERROR, 400, WSG_HSC_BAD_REQUEST_LINE, none);
+          return;
+        }
+        if (!eq_exact(d, tok[2], "HTTP/1.1", 8)) {  // HttpUtils.equals (:198-215)
+          finish(WSG_HS_PARSE_ERROR, 400, WSG_HSC_BAD_VERSION, none);
+          return;
+        }
+        if (!eq_exact(d, tok[0], "GET", 3)) {
+          finish(WSG_HS_PARSE_ERROR, 403, WSG_HSC_FORBIDDEN, none);
+          return;
+        }
+        uri = tok[1];
+        if (partial) {  // the fields are judged once the frame is complete
+          finish(WSG_HS_NEED_MORE, 0, WSG_HSC_NONE, none);
+          return;
+        }
+        continue;
+      }
+      // HttpUtils.splitHeaderField (:159-196): only the plain "name: value" form (4)
+      // is taken here; folded lines (-4/-2) and bare names (2) go to the host
+      if (lb < le && (d[lb] == SP || d[lb] == HT)) {
+        finish(WSG_HS_DEFER, 0, WSG_HSC_D_LINE_FORM, none);
+        return;
+      }
+      int32_t fs = -1;
+      for (int32_t j = lb; j < le; ++j)
+        if (d[j] == ':') {
+          fs = j;
+          break;
+        }
+      if (fs < 0) {
+        finish(WSG_HS_DEFER, 0, WSG_HSC_D_LINE_FORM, none);
+        return;
+      }
+      int32_t vb = fs + 1;
+      while (vb < le && (d[vb] == SP || d[vb] == HT)) ++vb;
+      int32_t ve = le;  // rtrimAscii (:230-239)
+      while (ve > vb && (d[ve - 1] == SP || d[ve - 1] == HT)) --ve;
+      const int nl = fs - lb;
+      for (int f = 0; f < F_COUNT; ++f) {
+        if (nl != kFieldLen[f]) continue;
+        bool m = true;
+        for (int q = 0; q < nl && m; ++q) m = up(d[lb + q]) == (uint8_t)kFieldNames[f][q];
+        if (!m) continue;
+        if (fld[f].b >= 0) {  // a repeated field joins its values with ", " (HandshakeFrame.java:80-85)
+          finish(WSG_HS_DEFER, 0, WSG_HSC_D_REPEATED, none);
+          return;
+        }
+        fld[f] = Span{vb, ve};
+        if (!ascii(d, fld[f])) {
+          finish(WSG_HS_DEFER, 0, WSG_HSC_D_NON_ASCII, none);
+          return;
+        }
+        break;
+      }
+    }
+  }
+  if (!ascii(d, uri)) {
+    finish(WSG_HS_DEFER, 0, WSG_HSC_D_NON_ASCII, none);
+    return;
+  }
+  // Handshaker.accept (:375-405): version, basic fields, uri, key, subprotocol, extensions
+  if (fld[F_VERSION].b < 0) {
+    finish(WSG_HS_ACCEPT, 400, WSG_HSC_MISSING_VERSION, none);
+    return;
+  }
+  {
+    bool bad = false, found = false;
+    const Span t = each_value(d, fld[F_VERSION], [&](Span v) {
+      int64_t x = 0;
+      if (!parse_int(d, v, &x)) {
+        bad = true;
+        return true;
+      }
+      if (x == 13) {
+        found = true;
+        return true;
+      }
+      return false;
+    });
+    if (bad) {
+      finish(WSG_HS_ACCEPT, 400, WSG_HSC_INCORRECT_VERSION, t);
+      return;
+    }
+    if (!found) {
+      finish(WSG_HS_ACCEPT, 426, WSG_HSC_UNSUPPORTED_VERSION, fld[F_VERSION]);
+      return;
+    }
+  }
+  if (fld[F_UPGRADE].b < 0) {
+    finish(WSG_HS_ACCEPT, 400, WSG_HSC_MISSING_UPGRADE, none);
+    return;
+  }
+  if (fld[F_CONNECTION].b < 0) {
+    finish(WSG_HS_ACCEPT, 400, WSG_HSC_MISSING_CONNECTION, none);
+    return;
+  }
+  if (!contains(d, fld[F_UPGRADE], "WEBSOCKET", 9)) {
+    finish(WSG_HS_ACCEPT, 400, WSG_HSC_INVALID_UPGRADE, fld[F_UPGRADE]);
+    return;
+  }
+  if (!contains(d, fld[F_CONNECTION], "UPGRADE", 7)) {
+    finish(WSG_HS_ACCEPT, 400, WSG_HSC_INVALID_CONNECTION, fld[F_CONNECTION]);
+    return;
+  }
+  // acceptUri (:327-373)
+  if (!uri_fast(d, uri)) {
+    finish(WSG_HS_DEFER, 0, WSG_HSC_D_URI, none);
+    return;
+  }
+  if (fld[F_HOST].b < 0) {
+    if (!cfg.ignore_host) {
+      finish(WSG_HS_ACCEPT, 400, WSG_HSC_MISSING_HOST, none);
+      return;
+    }
+  } else if (!host_fast(d, fld[F_HOST])) {
+    finish(WSG_HS_DEFER, 0, WSG_HSC_D_HOST, none);
+    return;
+  }
+  if (cfg.host_policy) {  // acceptRequestUri / customizeHeaders are Java callbacks
+    finish(WSG_HS_DEFER, 0, WSG_HSC_D_POLICY, none);
+    return;
+  }
+  // acceptKey (:242-257)
+  if (fld[F_KEY].b < 0) {
+    finish(WSG_HS_ACCEPT, 400, WSG_HSC_MISSING_KEY, none);
+    return;
+  }
+  if (!key_ok(d, fld[F_KEY])) {
+    finish(WSG_HS_ACCEPT, 400, WSG_HSC_INVALID_KEY, fld[F_KEY]);
+    return;
+  }
+  // acceptSubProtocol / acceptExtensions (:259-325): only with supported ones configured
+  if (cfg.subprotocols && fld[F_PROTOCOL].b >= 0 && fld[F_PROTOCOL].e > fld[F_PROTOCOL].b) {
+    finish(WSG_HS_DEFER, 0, WSG_HSC_D_SUBPROTOCOL, none);
+    return;
+  }
+  if (cfg.extensions && fld[F_EXTENSIONS].b >= 0 && fld[F_EXTENSIONS].e > fld[F_EXTENSIONS].b) {
+    finish(WSG_HS_DEFER, 0, WSG_HSC_D_EXTENSION, none);
+    return;
+  }
+  // 101 with Upgrade, Connection, Sec-WebSocket-Accept (:386-391)
+  Out o{resp};
+  o.put("HTTP/1.1 101 Switching Protocols\r\nUpgrade: websocket\r\nConnection: Upgrade\r\nSec-WebSocket-Accept: ");
+  uint8_t acc[28];
+  accept_key(d, fld[F_KEY], acc);
+  o.put(acc, 28);
+  o.put("\r\n\r\n");
+  const int rl = o.done();
+  finish(WSG_HS_ACCEPT, 101, WSG_HSC_NONE, none);
+  res->resp_len = (uint16_t)rl;
+}
+
+__global__ __launch_bounds__(256) void k_hs_accept(wsg_hs_config cfg, const uint8_t* req, const uint64_t* req_off,
+                                                   uint32_t n, uint8_t* resp, wsg_hs_result* result) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t b = req_off[i], e = req_off[i + 1];
+  Req d;
+  d.base = reinterpret_cast<const uint4*>(req + (b & ~(uint64_t)15));
+  d.lead = (uint32_t)(b & 15u);
+  accept_one(d, (int64_t)(e - b), cfg, resp + (uint64_t)i * WSG_HS_RESP_STRIDE, result + i);
+}
+
+}  // namespace
+
+void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64_t* req_off, uint32_t n,
+                      uint8_t* resp, wsg_hs_result* result, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(k_hs_accept, dim3((n + 255) / 256), dim3(256), 0, s, cfg, req, req_off, n, resp, result);
+}
+
+}  // namespace ws

@@ -184,7 +184,7 @@ struct InflArgs {
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -208,6 +208,10 @@ void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim);
 void launch_agg_final(const AggArgs& a, hipStream_t s);
 
 void launch_inflate(const InflArgs& a, hipStream_t s);
+
+void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64_t* req_off, uint32_t n,
+                      uint8_t* resp, wsg_hs_result* result, hipStream_t s);
+__host__ __device__ int hs_frame_len(const uint8_t* d, int64_t len, int* capped, int64_t* lines_end);
 
 void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s);
 void launch_synth_frames(const wsg_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s);

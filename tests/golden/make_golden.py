@@ -516,8 +516,115 @@ def deflate_kats():
                       "invalid compressed data format"}]
 
 
+def handshake_kats():
+    """Opening-handshake vectors (server side), transcribed from the reference's tests
+    under snf4j-websocket/src/test/java/org/snf4j/websocket/handshake/:
+    HttpUtilsTest.testAvailable :113-129 and testSplitRequestLine :211-230 ('|' = CRLF,
+    HandshakeTest.bytes :36-63), HandshakeUtilsTest.testGenerateAnswerKey :153-159 and
+    testParseKey :162-175, HandshakeDecoderTest.testDecode :76-107 / testDecodeTooBigFrame
+    :120-138 / testDecodeFailures :141-160, and the server cases of HanshakerTest
+    (request() :111-133 builds Host, Upgrade, Connection, Sec-WebSocket-Key,
+    Sec-WebSocket-Version in that order; testServerHandshake :206-236, testAcceptVersion
+    :245-270, testAcceptBasicFields :274-299, testAssertUri :311-356, testAcceptKey :359-382).
+    A Handshaker case is the request bytes HandshakeFactory.format writes for the test's
+    HandshakeRequest, with the status and closing reason the test asserts."""
+    src = "snf4j-websocket/src/test/java/org/snf4j/websocket/handshake/"
+
+    def pipe(s):
+        return s.replace("|", "\r\n").encode()
+
+    avail = [("", 0, []), ("x", 0, []), ("xx", 0, []), ("\n", 0, []), ("\r", 0, []), ("\r\n", 0, [""]),
+             ("1|22|333|", 0, ["1", "22", "333"]), ("1|22|333|4444", 0, ["1", "22", "333"]),
+             ("||", 4, [""]), ("||ccc", 4, [""]), ("xxx|yy||", 11, ["xxx", "yy"]),
+             ("xxx|yy||6", 11, ["xxx", "yy"]), ("xxx|yy||86", 11, ["xxx", "yy"]),
+             ("xxx|yy||86|", 11, ["xxx", "yy"]), ("xxx|yy|||", 11, ["xxx", "yy"])]
+    split = [("", [""]), (" ", ["", ""]), ("  ", ["", ""]), ("a", ["a"]), ("ab", ["ab"]), ("a ", ["a", ""]),
+             ("ab ", ["ab", ""]), (" a", ["", "a"]), (" ab", ["", "ab"]), (" a ", ["", "a", ""]),
+             (" ab ", ["", "ab", ""]), ("   ab     ", ["", "ab", ""]), ("a b", ["a", "b"]), ("a  b", ["a", "b"]),
+             ("ac bd", ["ac", "bd"]), ("ac  bd", ["ac", "bd"]), (" ac  bd ", ["", "ac", "bd", ""])]
+    out = []
+    for s, n, lines in avail:
+        out.append({"src": src + "HttpUtilsTest.java:113-129", "kind": "available", "data": hx(pipe(s)),
+                    "lines_len": 100, "expect": n, "lines": lines})
+    for s, items in split:
+        out.append({"src": src + "HttpUtilsTest.java:211-230", "kind": "split_request_line", "data": hx(s.encode()),
+                    "items": items})
+    out.append({"src": src + "HandshakeUtilsTest.java:153-159", "kind": "answer_key",
+                "key": "dGhlIHNhbXBsZSBub25jZQ==", "accept": "s3pPLMBiTxaQ9kYGzzhZRbK+xOo="})
+    b16 = bytes(range(1, 17))
+    for key, ok in [(base64.b64encode(b16).decode(), True), (base64.b64encode(b16[:15]).decode(), False),
+                    (base64.b64encode(b16 + b"\x11").decode(), False), ("A???", False)]:
+        out.append({"src": src + "HandshakeUtilsTest.java:162-175", "kind": "parse_key", "key": key, "valid": ok})
+
+    def case(where, req, status, kind, cause, detail=None, response=None, **cfg):
+        c = {"src": src + where, "kind": "accept", "request": hx(req), "cfg": cfg,
+             "expect": {"kind": kind, "status": status, "cause": cause, "detail": detail}}
+        if response is not None:
+            c["expect"]["response"] = hx(response)
+        return c
+
+    dec = pipe("GET /uri HTTP/1.1|Host: snf4j.org||")
+    # the decoder passes these frames on: the combined outcome is Handshaker.accept's (no version field)
+    out.append(case("HandshakeDecoderTest.java:76-107", dec, 400, "accept", "MISSING_VERSION"))
+    out.append(case("HandshakeDecoderTest.java:120-128", dec, 400, "accept", "MISSING_VERSION", max_length=len(dec)))
+    out.append(case("HandshakeDecoderTest.java:130-138", dec, 413, "parse_error", "TOO_LARGE",
+                    response=b"HTTP/1.1 413 Request Entity Too Large\r\n\r\n", max_length=len(dec) - 1))
+    out.append(case("HandshakeDecoderTest.java:141-151", pipe("POST /uri HTTP/1.1|Host: snf4j.org||"), 403,
+                    "parse_error", "FORBIDDEN", response=b"HTTP/1.1 403 Forbidden\r\n\r\n"))
+    out.append(case("HandshakeDecoderTest.java:152-160", pipe("GET /uri HTTP/1.2|Host: snf4j.org||"), 400,
+                    "parse_error", "BAD_VERSION", response=b"HTTP/1.1 400 Bad Request\r\n\r\n"))
+    out.append(case("HandshakeDecoderTest.java:94-97", dec[:4], 0, "need_more", "NONE"))
+
+    def req(uri="/uri", upper=None, host="snf4j.org", upgrade=None, connection=None, key=None, version=None):
+        def v(s):
+            return s if upper is None else (s.upper() if upper else s.lower())
+        f = []
+        if host is not None:
+            f.append((v("Host"), host))
+        if upgrade != "no":
+            f.append((v("Upgrade"), v(upgrade or "websocket")))
+        if connection != "no":
+            f.append((v("Connection"), v(connection or "Upgrade")))
+        if key != "no":
+            f.append((v("Sec-WebSocket-Key"), key or "dGhlIHNhbXBsZSBub25jZQ=="))
+        if version != "no":
+            f.append((v("Sec-WebSocket-Version"), version or "13"))
+        b = b"GET " + uri.encode() + b" HTTP/1.1\r\n"
+        for n, val in f:
+            b += n.encode() + b": " + val.encode() + b"\r\n"
+        return b + b"\r\n"
+
+    ok101 = (b"HTTP/1.1 101 Switching Protocols\r\nUpgrade: websocket\r\nConnection: Upgrade\r\n"
+             b"Sec-WebSocket-Accept: s3pPLMBiTxaQ9kYGzzhZRbK+xOo=\r\n\r\n")
+    bad = b"HTTP/1.1 400 Bad Request\r\n\r\n"
+    h = "HanshakerTest.java:"
+    for up in (None, True, False):
+        out.append(case(h + "206-221", req(upper=up), 101, "accept", "NONE", response=ok101))
+    out.append(case(h + "249-252", req(version="no"), 400, "accept", "MISSING_VERSION", response=bad))
+    out.append(case(h + "253-256", req(version="ab"), 400, "accept", "INCORRECT_VERSION", "ab", response=bad))
+    v426 = b"HTTP/1.1 426 Upgrade Required\r\nSec-WebSocket-Version: 13\r\n\r\n"
+    out.append(case(h + "257-260", req(version="14"), 426, "accept", "UNSUPPORTED_VERSION", "14", response=v426))
+    out.append(case(h + "261-263", req(version="13, 14"), 101, "accept", "NONE", response=ok101))
+    out.append(case(h + "264-266", req(version="12, 13, 14"), 101, "accept", "NONE", response=ok101))
+    out.append(case(h + "267-270", req(version="12, 14"), 426, "accept", "UNSUPPORTED_VERSION", "12, 14",
+                    response=v426))
+    out.append(case(h + "278-282", req(upgrade="no"), 400, "accept", "MISSING_UPGRADE", response=bad))
+    out.append(case(h + "283-287", req(upgrade="xxx"), 400, "accept", "INVALID_UPGRADE", "xxx", response=bad))
+    out.append(case(h + "289-293", req(connection="no"), 400, "accept", "MISSING_CONNECTION", response=bad))
+    out.append(case(h + "294-298", req(connection="xxx"), 400, "accept", "INVALID_CONNECTION", "xxx", response=bad))
+    for uri in ("/uri?find%20c", "//host/uri", "host/uri"):
+        out.append(case(h + "327-329", req(uri=uri), 101, "accept", "NONE", response=ok101))
+    out.append(case(h + "348-353", req(host=None), 400, "accept", "MISSING_HOST", response=bad))
+    out.append(case(h + "354-355", req(uri="/find", host=None), 101, "accept", "NONE", response=ok101,
+                    ignore_host=1))
+    out.append(case(h + "363-367", req(key="no"), 400, "accept", "MISSING_KEY", response=bad))
+    out.append(case(h + "368-372", req(key="AAAA"), 400, "accept", "INVALID_KEY", "AAAA", response=bad))
+    return out
+
+
 def main():
     data = {
+        "handshake": handshake_kats(),
         "deflate": deflate_kats(),
         "aggregator": aggregator_kats(),
         "builder": builder_kats(),

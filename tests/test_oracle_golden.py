@@ -246,3 +246,44 @@ def test_deflate_kat(oracle):
             with pytest.raises(oracle.InvalidFrame) as ei:
                 d.decode(*enc[1])
             assert oracle.format_error(ei.value.err) == seq["error"], seq["src"]
+
+
+HS_KIND = {"need_more": 0, "defer": 1, "parse_error": 2, "accept": 3}
+
+
+def _hs_cause(name):
+    from snf4j_amd.handshake import CAUSE_NAMES
+    return {v: k for k, v in CAUSE_NAMES.items()}[name]
+
+
+def hs_cfg(c):
+    return dict(max_length=c.get("max_length", 65536), ignore_host=bool(c.get("ignore_host", 0)))
+
+
+@pytest.mark.parametrize("idx", range(len(fixtures.load("handshake"))))
+def test_handshake_kat(idx):
+    """The handshake restatement against HttpUtilsTest / HandshakeUtilsTest /
+    HandshakeDecoderTest / HanshakerTest vectors."""
+    from oracle import handshake_oracle as H
+    v = fixtures.load("handshake")[idx]
+    if v["kind"] == "available":
+        data = fixtures.unhex(v["data"])
+        n, lines, _ = H.available(data, v["lines_len"])
+        assert n == v["expect"], v
+        assert [data[b:e].decode() for b, e in lines] == v["lines"], v
+    elif v["kind"] == "split_request_line":
+        data = fixtures.unhex(v["data"])
+        assert [data[b:e].decode() for b, e in H.split_request_line(data, 0, len(data), 50)] == v["items"], v
+    elif v["kind"] == "answer_key":
+        assert H.answer_key(v["key"]) == v["accept"]
+    elif v["kind"] == "parse_key":
+        k = H.base64_decode(v["key"])
+        assert (k is not None and len(k) == 16) == v["valid"], v
+    else:
+        r = H.accept(fixtures.unhex(v["request"]), **hs_cfg(v["cfg"]))
+        e = v["expect"]
+        assert r["kind"] == HS_KIND[e["kind"]], (v, r)
+        assert r["status"] == e["status"] and r["cause"] == _hs_cause(e["cause"]), (v, r)
+        assert r["detail"] == e["detail"], (v, r)
+        if "response" in e:
+            assert r["response"] == fixtures.unhex(e["response"]), (v, r)
