@@ -2,6 +2,7 @@
 // kernel timing, device/host batch entry points, host-side framing helpers.
 #include <stdarg.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <string>
@@ -15,7 +16,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept"};
+                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -65,6 +66,8 @@ struct wsg_ctx {
   // aggregate workspace
   DevBuf a_code, a_last, a_pl, a_cl, a_rec, a_blk, a_sess_err, a_pieces;
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
+  DevBuf i_tok, i_lit, i_stat, i_tab;  // inflate pre-decode workspace
+  int infl_tokens = 1;               // WSG_INFLATE_TOKENS=0 turns the pre-decode off
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -127,7 +130,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT)) {
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_INFL_TOK)) {
     f();
     return;
   }
@@ -156,6 +159,7 @@ int wsg_open(int device, void* stream, wsg_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return WSG_API_EHIP;
   wsg_ctx* c = new wsg_ctx();
   c->device = device;
+  if (const char* e = getenv("WSG_INFLATE_TOKENS")) c->infl_tokens = atoi(e) != 0;
   if (stream) {
     c->stream = (hipStream_t)stream;
   } else {
@@ -183,7 +187,8 @@ int wsg_close(wsg_ctx* c) {
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
   DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,     &c->a_rec,
-                     &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc};
+                     &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc, &c->i_tok, &c->i_lit,
+                     &c->i_stat, &c->i_tab};
   for (DevBuf* b : abufs) b->release();
   for (HostSlot& hs : c->slot) {
     DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
@@ -831,6 +836,27 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   a.out_desc = out_desc;
   a.result = out_result;
   a.replay_from = replay_from;
+  a.tok = nullptr;
+  a.lit = nullptr;
+  a.lit_len = 0;
+  a.tstat = nullptr;
+  a.tab = nullptr;
+  a.n_lanes = 0;
+  if (c->infl_tokens && n_frames) {
+    const uint32_t lanes = (uint32_t)(n_frames < 65536 ? ((n_frames + 63) / 64) * 64 : 65536);
+    const uint64_t lit_len = infl_lit_bytes(payload_len, n_frames);
+    HIP_TRY(c, c->i_tok.ensure(infl_tok_words(payload_len, n_frames) * 4));
+    HIP_TRY(c, c->i_lit.ensure(lit_len));
+    HIP_TRY(c, c->i_stat.ensure(n_frames * sizeof(InflTokStat)));
+    HIP_TRY(c, c->i_tab.ensure((uint64_t)lanes * infl_tab_bytes()));
+    a.tok = (uint32_t*)c->i_tok.p;
+    a.lit = (uint8_t*)c->i_lit.p;
+    a.lit_len = lit_len;
+    a.tstat = (InflTokStat*)c->i_stat.p;
+    a.tab = (uint8_t*)c->i_tab.p;
+    a.n_lanes = lanes;
+    timed(c, K_INFL_TOK, [&] { launch_infl_tok(a, c->stream); });
+  }
   timed(c, K_INFLATE, [&] { launch_inflate(a, c->stream); });
   HIP_TRY(c, hipGetLastError());
   return WSG_API_OK;

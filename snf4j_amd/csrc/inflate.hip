@@ -233,6 +233,353 @@ __device__ __forceinline__ bool tdec(const uint32_t* root, int rbits, const Huff
 
 }  // namespace
 
+namespace {
+
+constexpr uint32_t TOK_SLACK = 80;  // per-frame slack of the token / literal regions
+
+// ---------------------------------------------------------------------------------
+// Message-parallel pre-decode (k_infl_tok).  permessage-deflate ends every message
+// with a sync flush (the stripped 00 00 FF FF), so a message that is one FIN frame
+// starts a new block on a byte boundary with an empty bit buffer: its Huffman decode
+// does not depend on anything before it.  One LANE per such frame decodes the frame
+// (payload + tail) into a token stream: literal runs (bytes in a side stream) and
+// (length, distance) pairs.  k_inflate then replays the tokens into its window ring
+// instead of decoding, when its own state at that frame is the clean one the lane
+// assumed; back-reference bounds are checked there, against the real history.  A
+// frame the lane cannot finish cleanly (a final block, data errors, input ending
+// inside a block, an incomplete code set, token space exhausted) is marked not ok
+// and k_inflate decodes it itself: the serial decoder stays the authority.
+// ---------------------------------------------------------------------------------
+
+// per-lane tables in HBM scratch
+struct LaneTab {
+  uint32_t lroot[1 << LROOT];
+  uint32_t droot[1 << DROOT];
+  uint32_t croot[1 << CROOT];
+  uint16_t lcnt[16], lsym[288];
+  uint16_t dcnt[16], dsym[32];
+  uint16_t offs[16];
+  uint8_t lens[320];
+};
+
+// A lane's input: the frame's payload through a 16-B block held in registers, then the tail.
+struct Src {
+  const uint8_t* pay;    // batch payload
+  uint64_t pay_len;
+  uint64_t off;          // the frame's payload offset
+  uint32_t plen;
+  int64_t cq;
+  uint4 blk;
+  __device__ uint32_t at(uint32_t i) {
+    if (i >= plen) return (i - plen) < 2u ? 0x00u : 0xffu;  // DeflateCodec TAIL 00 00 FF FF
+    const uint64_t g = off + i;
+    const int64_t q = (int64_t)(g >> 4);
+    if (q != cq) {
+      cq = q;
+      if ((uint64_t)q * 16 + 16 <= pay_len) {
+        blk = reinterpret_cast<const uint4*>(pay)[q];
+      } else {
+        uint32_t w[4] = {0u, 0u, 0u, 0u};
+        for (int t = 0; t < 16; ++t)
+          if ((uint64_t)q * 16 + t < pay_len) w[t >> 2] |= (uint32_t)pay[(uint64_t)q * 16 + t] << (8 * (t & 3));
+        blk = make_uint4(w[0], w[1], w[2], w[3]);
+      }
+    }
+    const uint32_t o = (uint32_t)(g & 15u);
+    const uint32_t w = o < 8u ? (o < 4u ? blk.x : blk.y) : (o < 12u ? blk.z : blk.w);
+    return (w >> (8u * (o & 3u))) & 0xffu;
+  }
+};
+
+// Canonical tables of lens[0..n) into root (rbits) + cnt/sym: the longest length, or
+// -1 for any set that is not complete (over-subscribed, incomplete, empty): the
+// serial decoder then takes the frame and applies zlib's exact rules.
+__device__ int lane_build(LaneTab* T, uint32_t* root, int rbits, uint16_t* cnt, uint16_t* sym, const uint8_t* lens,
+                          int n, int kind) {
+  // counts and running offsets live in registers (a select chain per symbol): a
+  // read-modify-write of counters in HBM scratch would chain every symbol on its latency
+  int c[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) c[l] = 0;
+  for (int s = 0; s < n; ++s) {
+    const int l = lens[s];
+#pragma unroll
+    for (int L = 1; L < 16; ++L) c[L] += (l == L) ? 1 : 0;
+  }
+  int left = 1, maxl = 0;
+#pragma unroll
+  for (int l = 1; l < 16; ++l) {
+    left = (left << 1) - c[l];
+    if (c[l]) maxl = l;
+  }
+  bool bad = false;
+  {
+    int lf = 1;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) {
+      lf = (lf << 1) - c[l];
+      bad |= lf < 0;
+    }
+  }
+  if (bad || left != 0 || maxl == 0) return -1;
+  int o[16];
+  {
+    int off = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) {
+      o[l] = off;
+      off += c[l];
+    }
+  }
+#pragma unroll
+  for (int l = 1; l < 16; ++l) cnt[l] = (uint16_t)c[l];
+  for (int s = 0; s < n; ++s) {
+    const int l = lens[s];
+    if (!l) continue;
+    int at = 0;
+#pragma unroll
+    for (int L = 1; L < 16; ++L)
+      if (l == L) at = o[L]++;
+    sym[at] = (uint16_t)s;
+  }
+  const uint32_t rsize = 1u << rbits;
+  int code = 0, idx = 0;
+  for (int l = 1; l <= maxl; ++l) {
+    int cl = 0;
+#pragma unroll
+    for (int L = 1; L < 16; ++L)
+      if (l == L) cl = c[L];
+    for (int i = 0; i < cl; ++i, ++idx, ++code) {
+      const uint32_t sy = sym[idx];
+      const uint32_t rev = __builtin_bitreverse32((uint32_t)code) >> (32 - l);
+      if (l <= rbits) {
+        const uint32_t e = sym_entry(kind, sy, (uint32_t)l);
+        for (uint32_t j = rev; j < rsize; j += (1u << l)) root[j] = e;
+      } else {
+        root[rev & (rsize - 1)] = ent(0, 0, OP_LONG, 0);
+      }
+    }
+    code <<= 1;
+  }
+  return maxl;
+}
+
+// The symbol at the bit buffer (>= maxl bits held, or the whole rest of the input):
+// the table entry, or OP_BAD with len 0 when the code runs past the bits held.
+__device__ __forceinline__ uint32_t lane_sym(const uint32_t* root, int rbits, const uint16_t* cnt, const uint16_t* sym,
+                                             int maxl, int kind, uint64_t hold, int bits) {
+  uint32_t e = root[(uint32_t)hold & ((1u << rbits) - 1u)];
+  if (e_op(e) == OP_LONG) {
+    int code = 0, first = 0, index = 0;
+    e = ent(0, 0, OP_BAD, 0);
+    for (int len = 1; len <= maxl && len <= bits; ++len) {
+      code |= (int)((hold >> (len - 1)) & 1u);
+      const int count = cnt[len];
+      if (code - count < first) {
+        e = sym_entry(kind, sym[index + (code - first)], (uint32_t)len);
+        break;
+      }
+      index += count;
+      first += count;
+      first <<= 1;
+      code <<= 1;
+    }
+  }
+  if ((int)e_len(e) > bits || e_len(e) == 0) return ent(0, 0, OP_BAD, 0);
+  return e;
+}
+
+__device__ __forceinline__ uint64_t tok_base(uint64_t po, uint64_t k) { return po + (uint64_t)TOK_SLACK * k; }
+__device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
+  return (3 * po + (uint64_t)TOK_SLACK * k + 3) & ~(uint64_t)3;
+}
+
+__global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
+  const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane_id >= a.n_lanes) return;
+  LaneTab* const T = reinterpret_cast<LaneTab*>(a.tab) + lane_id;
+  for (uint64_t k = lane_id; k < a.n_frames; k += a.n_lanes) {
+    const wsg_frame_desc d = a.desc[k];
+    InflTokStat st = {0u, 0u, 0u, 0u};
+    const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
+    const bool cand = fin && (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u) &&
+                      !(d.flags & WSG_DESC_REPLAY) && d.payload_off + d.payload_len <= a.payload_len;
+    if (!cand) {
+      a.tstat[k] = st;
+      continue;
+    }
+    const uint32_t plen = d.payload_len, total = plen + 4u;
+    const uint32_t tok_cap = plen + 68u, lit_cap = 3u * total + 60u;
+    uint32_t* const tok = a.tok + tok_base(d.payload_off, k);
+    uint8_t* const lit = a.lit + lit_base(d.payload_off, k);
+    Src src{a.payload, a.payload_len, d.payload_off, plen, -1, make_uint4(0, 0, 0, 0)};
+    uint64_t hold = 0;
+    int bits = 0;
+    uint32_t ip = 0, ntok = 0, nlit = 0, run = 0, outlen = 0, litw = 0;
+    bool ok = true;
+    auto refill = [&]() {
+      while (bits <= 56 && ip < total) {
+        hold |= (uint64_t)src.at(ip++) << bits;
+        bits += 8;
+      }
+    };
+    auto drop = [&](int n) {
+      hold >>= n;
+      bits -= n;
+    };
+    auto put_lit = [&](uint32_t b) -> bool {
+      if (nlit >= lit_cap) return false;
+      litw |= b << (8 * (nlit & 3u));
+      if ((++nlit & 3u) == 0) {
+        reinterpret_cast<uint32_t*>(lit)[(nlit >> 2) - 1] = litw;
+        litw = 0;
+      }
+      ++run;
+      ++outlen;
+      return true;
+    };
+    auto put_tok = [&](uint32_t t) -> bool {
+      if (ntok >= tok_cap) return false;
+      tok[ntok++] = t;
+      return true;
+    };
+    auto end_run = [&]() -> bool {
+      if (!run) return true;
+      const bool r = put_tok(run);
+      run = 0;
+      return r;
+    };
+    for (;;) {
+      refill();
+      if (bits == 0 && ip >= total) break;  // clean: all input used, on a block boundary
+      if (bits < 3) { ok = false; break; }
+      const uint32_t last = (uint32_t)(hold & 1u), type = (uint32_t)((hold >> 1) & 3u);
+      drop(3);
+      if (last) { ok = false; break; }      // a final block: the stream ends (k_inflate handles it)
+      if (type == 0) {                      // stored
+        drop(bits & 7);
+        refill();
+        if (bits < 32) { ok = false; break; }
+        const uint32_t ln = (uint32_t)(hold & 0xffffu), nl = (uint32_t)((hold >> 16) & 0xffffu);
+        if (ln != (nl ^ 0xffffu)) { ok = false; break; }
+        drop(32);
+        for (uint32_t i = 0; i < ln && ok; ++i) {
+          refill();
+          if (bits < 8) { ok = false; break; }
+          ok = put_lit((uint32_t)(hold & 0xffu));
+          drop(8);
+        }
+        if (!ok) break;
+        continue;
+      }
+      int lmax, dmax;
+      if (type == 1) {  // fixed codes
+        for (int i = 0; i < 288; ++i) T->lens[i] = i < 144 ? 8 : (i < 256 ? 9 : (i < 280 ? 7 : 8));
+        lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, 288, T_LIT);
+        for (int i = 0; i < 30; ++i) T->lens[i] = 5;
+        // zlib's fixed distance set has 30 codes of 5 bits + the 2 invalid ones: complete with 32
+        T->lens[30] = 5;
+        T->lens[31] = 5;
+        dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, 32, T_DIST);
+      } else if (type == 2) {  // dynamic codes
+        refill();
+        if (bits < 14) { ok = false; break; }
+        const int nlen = (int)(hold & 31u) + 257, ndist = (int)((hold >> 5) & 31u) + 1,
+                  ncode = (int)((hold >> 10) & 15u) + 4;
+        drop(14);
+        if (nlen > 286 || ndist > 30) { ok = false; break; }
+        for (int i = 0; i < 19; ++i) T->lens[kClenOrder[i]] = 0;
+        for (int i = 0; i < ncode; ++i) {
+          refill();
+          if (bits < 3) { ok = false; break; }
+          T->lens[kClenOrder[i]] = (uint8_t)(hold & 7u);
+          drop(3);
+        }
+        if (!ok) break;
+        const int cmax = lane_build(T, T->croot, CROOT, T->lcnt, T->lsym, T->lens, 19, T_CODES);
+        if (cmax < 0) { ok = false; break; }
+        int have = 0;
+        while (have < nlen + ndist) {
+          refill();
+          const uint32_t e = T->croot[(uint32_t)hold & ((1u << CROOT) - 1u)];
+          const int nb = (int)e_len(e);
+          if (nb == 0 || nb > bits) { ok = false; break; }
+          const int sy = (int)e_val(e);
+          if (sy < 16) {
+            drop(nb);
+            T->lens[have++] = (uint8_t)sy;
+            continue;
+          }
+          const int xb = sy == 16 ? 2 : (sy == 17 ? 3 : 7);
+          if (nb + xb > bits) { ok = false; break; }
+          drop(nb);
+          int len = 0, copy;
+          if (sy == 16) {
+            if (have == 0) { ok = false; break; }
+            len = T->lens[have - 1];
+            copy = 3 + (int)(hold & 3u);
+          } else if (sy == 17) {
+            copy = 3 + (int)(hold & 7u);
+          } else {
+            copy = 11 + (int)(hold & 127u);
+          }
+          drop(xb);
+          if (have + copy > nlen + ndist) { ok = false; break; }
+          for (int i = 0; i < copy; ++i) T->lens[have + i] = (uint8_t)len;
+          have += copy;
+        }
+        if (!ok) break;
+        if (T->lens[256] == 0) { ok = false; break; }
+        lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, nlen, T_LIT);
+        // the distance lengths follow the literal/length ones in lens[]: move them first
+        for (int i = 0; i < ndist; ++i) T->lens[i] = T->lens[nlen + i];
+        dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, ndist, T_DIST);
+      } else {
+        ok = false;
+        break;
+      }
+      if (lmax < 0 || dmax < 0) { ok = false; break; }
+      // the block's symbols
+      for (;;) {
+        refill();
+        const uint32_t e = lane_sym(T->lroot, LROOT, T->lcnt, T->lsym, lmax, T_LIT, hold, bits);
+        const uint32_t eo = e_op(e);
+        if (eo == OP_BAD) { ok = false; break; }
+        drop((int)e_len(e));
+        if (eo == OP_LIT) {
+          if (!put_lit(e_val(e))) { ok = false; break; }
+          continue;
+        }
+        if (eo == OP_EOB) break;
+        const int lx = (int)e_extra(e);
+        if (lx > bits) { ok = false; break; }
+        const uint32_t mlen = e_val(e) + (uint32_t)(hold & ((1ull << lx) - 1ull));
+        drop(lx);
+        refill();
+        const uint32_t g = lane_sym(T->droot, DROOT, T->dcnt, T->dsym, dmax, T_DIST, hold, bits);
+        if (e_op(g) == OP_BAD) { ok = false; break; }
+        drop((int)e_len(g));
+        const int dx = (int)e_extra(g);
+        if (dx > bits) { ok = false; break; }
+        const uint32_t md = e_val(g) + (uint32_t)(hold & ((1ull << dx) - 1ull));
+        drop(dx);
+        if (!end_run() || !put_tok(0x80000000u | ((mlen - 3u) << 16) | (md - 1u))) { ok = false; break; }
+        outlen += mlen;
+      }
+      if (!ok) break;
+    }
+    if (ok) ok = end_run();
+    if (nlit & 3u) reinterpret_cast<uint32_t*>(lit)[nlit >> 2] = litw;
+    st.ok = ok ? 1u : 0u;
+    st.n_tok = ntok;
+    st.n_lit = nlit;
+    st.out_len = outlen;
+    a.tstat[k] = st;
+  }
+}
+
+}  // namespace
+
 // Phase clocks for tools/prof_inflate.hip (compiled out of the library).
 #ifdef WSG_INFLATE_PROF
 __device__ unsigned long long g_infl_prof[24];
@@ -440,8 +787,68 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
       };
       auto raw_rest = [&]() { copy_in(total_in - ip); };
 
+      // A single-frame message met in the clean state k_infl_tok assumed: replay its
+      // tokens instead of decoding.
+      bool tok_use = false;
+      if (a.tstat && !finished && !compressing && fin && !replay && (op == WSG_OP_TEXT || op == WSG_OP_BINARY) &&
+          mode == M_HEAD && bits == 0 && !last)
+        tok_use = uni(a.tstat[k].ok) != 0u;
       if (finished) {
         raw_rest();
+      } else if (tok_use) {
+        const uint32_t n_tok = uni(a.tstat[k].n_tok), n_lit = uni(a.tstat[k].n_lit);
+        const uint32_t* const T = a.tok + tok_base(d.payload_off, k);
+        const uint64_t lb = lit_base(d.payload_off, k);
+        uint32_t li = 0, lw_lo = 0, lw_hi = 0, lw_off = 0;  // ibuf holds literal bytes [lw_lo, lw_hi) from lw_off
+        auto lit_stage = [&](uint32_t i) {
+          const uint64_t g = lb + i;
+          const uint64_t A = g & ~(uint64_t)15;
+          lw_off = (uint32_t)(g - A);
+          lw_lo = i;
+          lw_hi = (i + IB - lw_off) < n_lit ? (i + IB - lw_off) : n_lit;
+          for (uint32_t c = lane; c < IB / 16; c += 64) {
+            const uint64_t o = A + 16u * c;
+            if (o + 16 <= a.lit_len) reinterpret_cast<uint4*>(L.ibuf)[c] = reinterpret_cast<const uint4*>(a.lit)[o >> 4];
+          }
+        };
+        uint32_t nxt = (uint32_t)lane < n_tok ? T[lane] : 0u;
+        for (uint32_t t0 = 0; t0 < n_tok && err == E_NONE; t0 += 64) {
+          const uint32_t cur = nxt;
+          if (t0 + 64 < n_tok) nxt = (t0 + 64 + (uint32_t)lane < n_tok) ? T[t0 + 64 + lane] : 0u;
+          const uint32_t cnt = (n_tok - t0) < 64u ? (n_tok - t0) : 64u;
+          for (uint32_t j = 0; j < cnt; ++j) {
+            const uint32_t tk = (uint32_t)__builtin_amdgcn_readlane((int)cur, (int)j);
+            pos = (int32_t)uni((uint32_t)pos);
+            if (pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; break; }
+            if (tk & 0x80000000u) {
+              const uint32_t mlen = ((tk >> 16) & 255u) + 3u, md = (tk & 0x7fffu) + 1u;
+              if ((int32_t)md > pos - wstart) { err = E_DATA; break; }  // "invalid distance too far back"
+              if (md >= mlen && mlen <= 64u) {
+                if ((uint32_t)lane < mlen) {
+                  const uint8_t v = L.ring[ri(pos - (int32_t)md + lane)];
+                  L.ring[ri(pos + lane)] = v;
+                }
+                pos += (int32_t)mlen;
+              } else {
+                copy_match(mlen, md);
+              }
+            } else {
+              uint32_t run = tk;
+              while (run) {
+                if (li < lw_lo || li >= lw_hi) lit_stage(li);
+                uint32_t m = lw_hi - li;
+                if (m > run) m = run;
+                const uint32_t base = lw_off + (li - lw_lo);
+                for (uint32_t t = lane; t < m; t += 64) L.ring[ri(pos + (int32_t)t)] = L.ibuf[base + t];
+                pos += (int32_t)m;
+                li += m;
+                run -= m;
+                if (run && pos - flushed >= FLUSH_AT && !flush()) { err = E_CAP; break; }
+              }
+              if (err) break;
+            }
+          }
+        }
       } else {
         // the inflate state machine: runs until the frame's input is exhausted
         bool more = true;
@@ -872,6 +1279,16 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
     for (int i = 0; i < 24; ++i) atomicAdd(&g_infl_prof[i], (unsigned long long)pf_[i]);
 #endif
 }
+
+void launch_infl_tok(const InflArgs& a, hipStream_t s) {
+  if (a.n_lanes && a.n_frames) hipLaunchKernelGGL(k_infl_tok, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+}
+
+uint64_t infl_tok_words(uint64_t payload_len, uint64_t n_frames) { return payload_len + (uint64_t)TOK_SLACK * n_frames + 64; }
+uint64_t infl_lit_bytes(uint64_t payload_len, uint64_t n_frames) {
+  return 3 * payload_len + (uint64_t)TOK_SLACK * n_frames + 256;
+}
+uint64_t infl_tab_bytes() { return sizeof(LaneTab); }
 
 void launch_inflate(const InflArgs& a, hipStream_t s) {
   if (a.n_sessions) hipLaunchKernelGGL(k_inflate, dim3(a.n_sessions), dim3(64), 0, s, a);

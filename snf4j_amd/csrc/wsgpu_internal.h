@@ -179,12 +179,23 @@ struct InflArgs {
   wsg_frame_desc* out_desc;
   wsg_session_result* result;
   uint32_t* replay_from;
+  // message-parallel pre-decode (k_infl_tok); tstat == nullptr: k_inflate decodes every frame
+  uint32_t* tok;              // token regions (per frame: payload_off + 80 k words)
+  uint8_t* lit;               // literal regions (per frame: 3 payload_off + 80 k bytes, 4-B aligned)
+  uint64_t lit_len;           // bytes allocated at lit
+  struct InflTokStat* tstat;  // [n_frames]
+  uint8_t* tab;               // n_lanes per-lane table blocks
+  uint32_t n_lanes;
+};
+
+struct InflTokStat {
+  uint32_t ok, n_tok, n_lit, out_len;
 };
 
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -208,6 +219,10 @@ void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim);
 void launch_agg_final(const AggArgs& a, hipStream_t s);
 
 void launch_inflate(const InflArgs& a, hipStream_t s);
+void launch_infl_tok(const InflArgs& a, hipStream_t s);
+uint64_t infl_tok_words(uint64_t payload_len, uint64_t n_frames);
+uint64_t infl_lit_bytes(uint64_t payload_len, uint64_t n_frames);
+uint64_t infl_tab_bytes();
 
 void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64_t* req_off, uint32_t n,
                       uint8_t* resp, wsg_hs_result* result, hipStream_t s);
