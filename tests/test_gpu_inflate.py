@@ -172,3 +172,48 @@ def test_inflate_long_context_window(ctx, oracle):
             frames.append((1, True, 4, data[:-4]))
         sessions.append(frames)
     _run(ctx, oracle, sessions, False, 4, rng)
+
+
+def test_inflate_predecode_matches_serial_and_zlib(oracle):
+    """k_infl_tok + token replay against the serial decoder alone (WSG_INFLATE_TOKENS=0) and
+    zlib, on a bench-shaped batch (single-frame messages, context takeover), split over
+    two batches so the second replays tokens against a carried-in window."""
+    import os
+    import zlib
+    from snf4j_amd import Context
+    from snf4j_amd._lib import DESC_DTYPE, INFLATE_STATE_DTYPE
+    from snf4j_amd.synth import deflate_batch
+    n_s, msgs, mb = 96, 8, 2048
+    desc, sf, payload, plain = deflate_batch(0xD1F, n_s, msgs, mb, unique=12)
+    outs = []
+    for flag in ("1", "0"):
+        os.environ["WSG_INFLATE_TOKENS"] = flag
+        try:
+            c = Context(0)
+        finally:
+            os.environ.pop("WSG_INFLATE_TOKENS", None)
+        state = np.zeros(n_s, dtype=INFLATE_STATE_DTYPE)
+        window = np.zeros(n_s * 32768, dtype=np.uint8)
+        got = [[] for _ in range(n_s)]
+        for half in (0, 1):  # messages [0, msgs/2) then [msgs/2, msgs) of every session
+            idx = np.concatenate([np.arange(s * msgs, (s + 1) * msgs)[half * msgs // 2:(half + 1) * msgs // 2]
+                                  for s in range(n_s)])
+            d = desc[idx].copy()
+            sfh = (np.arange(n_s + 1) * (msgs // 2)).astype(np.uint32)
+            out_off = (np.arange(n_s + 1) * (msgs // 2) * mb).astype(np.uint64)
+            out, od, res, rf = c.inflate_host(False, d, sfh, payload, state, window, out_off)
+            assert (res["error"] == 0).all() and (rf == 0xFFFFFFFF).all()
+            for s in range(n_s):
+                for j in range(msgs // 2):
+                    o = od[s * (msgs // 2) + j]
+                    got[s].append(out[int(o["payload_off"]):int(o["payload_off"]) + int(o["payload_len"])].tobytes())
+        c.close()
+        outs.append(got)
+    assert outs[0] == outs[1]
+    for s in range(n_s):
+        z = zlib.decompressobj(-15)
+        for j in range(msgs):
+            o = desc[s * msgs + j]
+            exp = z.decompress(payload[int(o["payload_off"]):int(o["payload_off"]) + int(o["payload_len"])].tobytes()
+                               + b"\x00\x00\xff\xff")
+            assert outs[0][s][j] == exp, (s, j)
