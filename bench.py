@@ -72,6 +72,41 @@ def cpu_baseline(args, seconds):
                       f"no JDK on the box, the Java reference is not runnable)"}
 
 
+def cpu_baseline_mt(args, seconds, threads=16):
+    """The same C restatement on `threads` host threads, one Batch (own sessions) per
+    thread: the N-thread figure SURVEY.md §8(d) asks for beside the 1-thread one.
+    ctypes releases the GIL around each oracle call, so the threads decode in parallel.
+    The GPU box's CPU share is 16 threads (os.cpu_count() shows the whole machine)."""
+    import threading
+    from oracle import pyoracle
+    pyoracle.build()
+    n = min(args.frames, 16384)
+    fps = max(1, args.frames // args.sessions)
+    wire, off, sf = pyoracle.synth_uniform(1234, n, args.payload, min(fps, n), opcode=2 if args.binary else 1,
+                                           masked=True, text=not args.binary)
+    n_s = len(sf) - 1
+    counts = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(i):
+        b = pyoracle.Batch(False, False, 65536, not args.no_validate, n_s)
+        while time.perf_counter() < stop:
+            b.decode(wire, off, sf)
+            counts[i] += 1
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    el = time.perf_counter() - t0
+    gib = sum(counts) * int(off[-1]) / el / 2**30
+    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+            "sample": f"{threads} threads, each decoding {n} frames x {args.payload} B repeatedly for {el:.1f} s "
+                      f"({sum(counts)} batches) with the C restatement (oracle/)"}
+
+
 def main():
     args = parse()
     import numpy as np
@@ -172,9 +207,10 @@ def main():
         torch.cuda.empty_cache()
         extras = measure_extras(ctx, dev, args)
 
-    cpu = None
+    cpu = cpu_mt = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_seconds)
+        cpu_mt = cpu_baseline_mt(args, 5.0)
 
     if rank == 0:
         total_wire = wire_bytes * world
@@ -217,6 +253,7 @@ def main():
             },
             "pipeline_ms": pipe,
             "cpu_baseline": cpu,
+            "cpu_baseline_threads": cpu_mt,
         }
         if e2e:
             out["e2e_pinned"] = e2e
