@@ -299,8 +299,10 @@ int wsg_encode_batch_host(wsg_ctx* ctx, int client_mode,
  * FrameDecoder.java:357-401; StreamSession.java:798-854) with the header rules
  * applied as soon as a header is complete (FrameDecoder.java:197-256), and
  * wsg_batcher_flush decodes every complete frame of every session in one device
- * batch.  Partial frames stay in the batcher.  Not thread-safe: one batcher per
- * selector loop (or external locking). */
+ * batch.  Partial frames stay in the batcher.  wsg_batcher_feed may run
+ * concurrently for distinct sessions (each touches only its session's slot: one
+ * feeder per selector loop, sessions owned by one loop); flush, session_state and
+ * close must not overlap a feed. */
 typedef struct wsg_batcher wsg_batcher;
 
 typedef struct wsg_batch_view {  /* valid until the next flush / close */
