@@ -402,6 +402,39 @@ def test_native_batcher_large_random_chunks(ctx, oracle):
         assert (str(e) if e else None) == (str(err[s]) if err[s] else None), s
 
 
+def test_native_batcher_concurrent_feeders(ctx, oracle):
+    """wsg_batcher_feed from 4 threads at once, each owning a slice of the sessions (one
+    feeder per selector loop), then one flush: the same frames and verdicts as the
+    oracle's read loop."""
+    import threading
+    from snf4j_amd import NativeBatcher
+    rng = np.random.default_rng(34)
+    n = 48
+    streams = [b"".join(wsgen.session_frames(rng, int(rng.integers(5, 30)), big=bool(s % 3 == 0))) for s in range(n)]
+    cuts = [sorted(int(x) for x in rng.integers(0, len(st) + 1, int(rng.integers(1, 12)))) for st in streams]
+    b = NativeBatcher(n, ctx=ctx)
+
+    def feeder(i):
+        for s in range(i, n, 4):
+            edges = [0] + cuts[s] + [len(streams[s])]
+            for a0, a1 in zip(edges, edges[1:]):
+                if a1 > a0:
+                    b.feed(s, streams[s][a0:a1])
+
+    ts = [threading.Thread(target=feeder, args=(i,)) for i in range(4)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    res = b.flush()
+    for s in range(n):
+        fr, e = res[s]
+        frames, oe = oracle.stream_decode(streams[s], [len(streams[s])])
+        assert [(f.opcode, f.fin, f.payload) for f in frames] == \
+               [(int(f.getOpcode()), f.isFinalFragment(), f.getPayload()) for f in fr], s
+        assert (str(oe) if oe else None) == (str(e) if e else None), s
+
+
 def test_pinned_pool(ctx):
     from snf4j_amd.codec import pinned_alloc, pinned_release
     a = pinned_alloc(5000)
