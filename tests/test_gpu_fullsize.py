@@ -83,3 +83,55 @@ def test_full_size_planted_utf8_errors(batch):
             assert int(r["n_delivered"][s]) == plant[s][0], s
         else:
             assert int(r["error"][s]) == 0 and int(r["n_delivered"][s]) == fps, s
+
+
+def test_full_size_encode_decode_round_trip():
+    """configs[4] at full size: 64 x 16 MiB messages in 64 KiB frames, client-masked on the
+    GPU, then decoded by the server path on the GPU: every payload byte comes back, every
+    header is the reference's (BINARY then CONTINUATION, FIN on the last, u64 length form)."""
+    import numpy as np
+    import torch
+    from snf4j_amd import Context, decoder_cfg, encoded_length
+    from snf4j_amd._lib import DESC_DTYPE, ENCODE_DTYPE, RESULT_DTYPE
+    M, FR, FP = 64, 256, 65536
+    n = M * FR
+    dev = torch.device("cuda", 0)
+    ctx = Context(0)
+    try:
+        g = torch.Generator(device=dev).manual_seed(9)
+        payload = torch.randint(0, 256, (n * FP,), dtype=torch.uint8, device=dev, generator=g)
+        fr = np.zeros(n, dtype=ENCODE_DTYPE)
+        fr["payload_off"] = np.arange(n, dtype=np.uint64) * FP
+        fr["payload_len"] = FP
+        j = np.arange(n) % FR
+        fr["opcode"] = np.where(j == 0, 2, 0)
+        fr["flags"] = np.where(j == FR - 1, 0x80, 0)
+        fr["mask"] = np.random.default_rng(5).integers(0, 256, (n, 4), dtype=np.uint8)
+        frames = torch.from_numpy(fr.view(np.uint8).copy()).to(dev)
+        sfe = torch.from_numpy((np.arange(M + 1) * FR).astype(np.int32)).to(dev)
+        closed = torch.zeros(M, dtype=torch.uint8, device=dev)
+        elen = encoded_length(FP, True)
+        wire = torch.empty(n * elen + 64, dtype=torch.uint8, device=dev)
+        wire_off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        ctx.encode_device(True, payload, frames, sfe, closed, wire, wire_off)
+        torch.cuda.synchronize(dev)
+        assert int(wire_off[-1].item()) == n * elen
+        w = wire[:n * elen].view(n, elen)
+        hdr = w[:, :10].cpu().numpy()
+        assert (hdr[:, 1] == 0xFF).all() and (hdr[:, 2:10] == np.array([0, 0, 0, 0, 0, 1, 0, 0], np.uint8)).all()
+        assert (hdr[:, 0] == np.where(j == 0, 0x02, 0x00) | np.where(j == FR - 1, 0x80, 0)).all()
+        assert np.array_equal(w[:, 10:14].cpu().numpy(), fr["mask"])
+        out = torch.empty(n * elen + 16 * n + 16, dtype=torch.uint8, device=dev)
+        desc = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+        res = torch.empty(M * 16, dtype=torch.uint8, device=dev)
+        state = torch.zeros(M * 8, dtype=torch.uint8, device=dev)
+        ctx.decode_device(decoder_cfg(False, False, 65536, True), wire, wire_off, sfe, state, out, desc, res,
+                          wire_len=n * elen)
+        torch.cuda.synchronize(dev)
+        r = res.cpu().numpy().view(RESULT_DTYPE)
+        assert int(r["error"].max()) == 0 and int(r["n_delivered"].sum()) == n
+        d = desc.cpu().numpy().view(DESC_DTYPE)
+        assert np.array_equal(d["payload_off"], np.arange(n, dtype=np.uint64) * FP)
+        assert torch.equal(out[:n * FP], payload)
+    finally:
+        ctx.close()
