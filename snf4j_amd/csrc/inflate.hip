@@ -270,6 +270,13 @@ struct Src {
   uint32_t plen;
   int64_t cq;
   uint4 blk;
+  __device__ uint4 ld(int64_t q) const {
+    if ((uint64_t)q * 16 + 16 <= pay_len) return reinterpret_cast<const uint4*>(pay)[q];
+    uint32_t w[4] = {0u, 0u, 0u, 0u};
+    for (int t = 0; t < 16; ++t)
+      if ((uint64_t)q * 16 + t < pay_len) w[t >> 2] |= (uint32_t)pay[(uint64_t)q * 16 + t] << (8 * (t & 3));
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
   __device__ uint32_t at(uint32_t i) {
     if (i >= plen) return (i - plen) < 2u ? 0x00u : 0xffu;  // DeflateCodec TAIL 00 00 FF FF
     const uint64_t g = off + i;
@@ -417,10 +424,38 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
     int bits = 0;
     uint32_t ip = 0, ntok = 0, nlit = 0, run = 0, outlen = 0, litw = 0;
     bool ok = true;
+    // The bit buffer is refilled with up to 8 bytes at once from a 32-byte window of
+    // two 16-B blocks held in registers (one funnel shift, no per-byte branches); the
+    // window moves on by one block when the lane leaves the first one.
+    int64_t wq = (int64_t)(d.payload_off >> 4);
+    uint4 wc = src.ld(wq), wn = src.ld(wq + 1);
     auto refill = [&]() {
-      while (bits <= 56 && ip < total) {
-        hold |= (uint64_t)src.at(ip++) << bits;
-        bits += 8;
+      if (bits > 56 || ip >= total) return;
+      const uint32_t o = (uint32_t)((d.payload_off + ip) & 15u);
+      const uint32_t q = o >> 2, sh = o & 3u;
+      const uint32_t D0 = wc.x, D1 = wc.y, D2 = wc.z, D3 = wc.w, D4 = wn.x, D5 = wn.y;
+      const uint32_t A = q == 0 ? D0 : q == 1 ? D1 : q == 2 ? D2 : D3;
+      const uint32_t B = q == 0 ? D1 : q == 1 ? D2 : q == 2 ? D3 : D4;
+      const uint32_t C = q == 0 ? D2 : q == 1 ? D3 : q == 2 ? D4 : D5;
+      const uint32_t lo = __builtin_amdgcn_alignbyte(B, A, sh);
+      const uint32_t hi = __builtin_amdgcn_alignbyte(C, B, sh);
+      uint64_t v = ((uint64_t)hi << 32) | lo;
+      // the tail 00 00 FF FF from byte plen on (DeflateCodec TAIL)
+      const int32_t k0 = (int32_t)plen - (int32_t)ip;
+      if (k0 < 8) {
+        const uint64_t tail = 0xFFFF0000ull;
+        v = k0 > 0 ? ((v & ((1ull << (8 * k0)) - 1ull)) | (tail << (8 * k0))) : (tail >> (8 * (-k0 < 8 ? -k0 : 7)));
+      }
+      uint32_t nb = (uint32_t)(64 - bits) >> 3;
+      if (nb > total - ip) nb = total - ip;
+      if (nb < 8) v &= (1ull << (8 * nb)) - 1ull;
+      hold |= v << bits;
+      bits += 8 * (int)nb;
+      ip += nb;
+      if ((int64_t)((d.payload_off + ip) >> 4) > wq) {
+        ++wq;
+        wc = wn;
+        wn = src.ld(wq + 1);
       }
     };
     auto drop = [&](int n) {
