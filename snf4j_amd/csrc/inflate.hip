@@ -252,10 +252,10 @@ constexpr uint32_t TOK_SLACK = 80;  // per-frame slack of the token / literal re
 // ---------------------------------------------------------------------------------
 
 // per-lane tables in HBM scratch
-struct LaneTab {
-  uint32_t lroot[1 << LROOT];
-  uint32_t droot[1 << DROOT];
-  uint32_t croot[1 << CROOT];
+struct LaneTab {  // root entries: len | symbol << 4, len 0 = a longer code
+  uint16_t lroot[1 << LROOT];
+  uint16_t droot[1 << DROOT];
+  uint16_t croot[1 << CROOT];
   uint16_t lcnt[16], lsym[288];
   uint16_t dcnt[16], dsym[32];
   uint16_t offs[16];
@@ -301,7 +301,7 @@ struct Src {
 // Canonical tables of lens[0..n) into root (rbits) + cnt/sym: the longest length, or
 // -1 for any set that is not complete (over-subscribed, incomplete, empty): the
 // serial decoder then takes the frame and applies zlib's exact rules.
-__device__ int lane_build(LaneTab* T, uint32_t* root, int rbits, uint16_t* cnt, uint16_t* sym, const uint8_t* lens,
+__device__ int lane_build(LaneTab* T, uint16_t* root, int rbits, uint16_t* cnt, uint16_t* sym, const uint8_t* lens,
                           int n, int kind) {
   // counts and running offsets live in registers (a select chain per symbol): a
   // read-modify-write of counters in HBM scratch would chain every symbol on its latency
@@ -360,30 +360,32 @@ __device__ int lane_build(LaneTab* T, uint32_t* root, int rbits, uint16_t* cnt, 
       const uint32_t sy = sym[idx];
       const uint32_t rev = __builtin_bitreverse32((uint32_t)code) >> (32 - l);
       if (l <= rbits) {
-        const uint32_t e = sym_entry(kind, sy, (uint32_t)l);
+        const uint16_t e = (uint16_t)((uint32_t)l | (sy << 4));
         for (uint32_t j = rev; j < rsize; j += (1u << l)) root[j] = e;
       } else {
-        root[rev & (rsize - 1)] = ent(0, 0, OP_LONG, 0);
+        root[rev & (rsize - 1)] = 0;
       }
     }
     code <<= 1;
   }
+  (void)kind;
   return maxl;
 }
 
 // The symbol at the bit buffer (>= maxl bits held, or the whole rest of the input):
 // the table entry, or OP_BAD with len 0 when the code runs past the bits held.
-__device__ __forceinline__ uint32_t lane_sym(const uint32_t* root, int rbits, const uint16_t* cnt, const uint16_t* sym,
-                                             int maxl, int kind, uint64_t hold, int bits) {
-  uint32_t e = root[(uint32_t)hold & ((1u << rbits) - 1u)];
-  if (e_op(e) == OP_LONG) {
+__device__ __forceinline__ uint32_t lane_sym(const uint16_t* root, int rbits, const uint16_t* cnt, const uint16_t* sym,
+                                             int maxl, const uint32_t* ents, uint64_t hold, int bits) {
+  const uint32_t r = root[(uint32_t)hold & ((1u << rbits) - 1u)];
+  uint32_t len = r & 15u, sy = r >> 4;
+  if (len == 0) {
     int code = 0, first = 0, index = 0;
-    e = ent(0, 0, OP_BAD, 0);
-    for (int len = 1; len <= maxl && len <= bits; ++len) {
-      code |= (int)((hold >> (len - 1)) & 1u);
-      const int count = cnt[len];
+    for (int l = 1; l <= maxl && l <= bits; ++l) {
+      code |= (int)((hold >> (l - 1)) & 1u);
+      const int count = cnt[l];
       if (code - count < first) {
-        e = sym_entry(kind, sym[index + (code - first)], (uint32_t)len);
+        len = (uint32_t)l;
+        sy = sym[index + (code - first)];
         break;
       }
       index += count;
@@ -391,10 +393,12 @@ __device__ __forceinline__ uint32_t lane_sym(const uint32_t* root, int rbits, co
       first <<= 1;
       code <<= 1;
     }
+    if (len == 0) return ent(0, 0, OP_BAD, 0);
   }
-  if ((int)e_len(e) > bits || e_len(e) == 0) return ent(0, 0, OP_BAD, 0);
-  return e;
+  if ((int)len > bits) return ent(0, 0, OP_BAD, 0);
+  return ents ? (ents[sy] | len) : ent(len, 0, OP_LIT, sy);
 }
+
 
 __device__ __forceinline__ uint64_t tok_base(uint64_t po, uint64_t k) { return po + (uint64_t)TOK_SLACK * k; }
 __device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
@@ -402,6 +406,11 @@ __device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
 }
 
 __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
+  // symbol -> entry (base, extra bits, op) for the 16-bit root entries
+  __shared__ uint32_t lit_ent[288], dist_ent[32];
+  for (int i = threadIdx.x; i < 288; i += 64) lit_ent[i] = sym_entry(T_LIT, (uint32_t)i, 0);
+  if (threadIdx.x < 32) dist_ent[threadIdx.x] = sym_entry(T_DIST, threadIdx.x, 0);
+  __syncthreads();
   const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane_id >= a.n_lanes) return;
   LaneTab* const T = reinterpret_cast<LaneTab*>(a.tab) + lane_id;
@@ -536,7 +545,7 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
         int have = 0;
         while (have < nlen + ndist) {
           refill();
-          const uint32_t e = T->croot[(uint32_t)hold & ((1u << CROOT) - 1u)];
+          const uint32_t e = lane_sym(T->croot, CROOT, nullptr, nullptr, cmax, nullptr, hold, bits);
           const int nb = (int)e_len(e);
           if (nb == 0 || nb > bits) { ok = false; break; }
           const int sy = (int)e_val(e);
@@ -577,7 +586,7 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
       // the block's symbols
       for (;;) {
         refill();
-        const uint32_t e = lane_sym(T->lroot, LROOT, T->lcnt, T->lsym, lmax, T_LIT, hold, bits);
+        const uint32_t e = lane_sym(T->lroot, LROOT, T->lcnt, T->lsym, lmax, lit_ent, hold, bits);
         const uint32_t eo = e_op(e);
         if (eo == OP_BAD) { ok = false; break; }
         drop((int)e_len(e));
@@ -591,7 +600,7 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
         const uint32_t mlen = e_val(e) + (uint32_t)(hold & ((1ull << lx) - 1ull));
         drop(lx);
         refill();
-        const uint32_t g = lane_sym(T->droot, DROOT, T->dcnt, T->dsym, dmax, T_DIST, hold, bits);
+        const uint32_t g = lane_sym(T->droot, DROOT, T->dcnt, T->dsym, dmax, dist_ent, hold, bits);
         if (e_op(g) == OP_BAD) { ok = false; break; }
         drop((int)e_len(g));
         const int dx = (int)e_extra(g);
