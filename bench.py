@@ -1,36 +1,59 @@
 """Benchmark: device-resident WebSocket frame decode (unmask + UTF-8 validation)
 on MI355X, one process per GPU, sessions sharded across GPUs with no collective.
 
-  python bench.py [--gpus N] [--steps K] [--warmup W] [--frames F] [--payload P]
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config north|1|3] [--frames F] [--payload P]
 
 A step = one pass of the decode pipeline (libwsgpu's HIP kernels) over one batch
 of F synthetic masked frames per GPU resident in HBM.  Default workload: the
 north-star 1-GPU case, 1 M x 4 KiB masked TEXT frames (valid UTF-8, ~70 % ASCII
 bytes) in 1024 sessions, validation on.  Prints ONE JSON line (rank 0).
+
+--gpus N > 1 without a torch.distributed environment starts N rank processes
+itself (torch.distributed.run, 127.0.0.1) before anything touches a GPU and
+exits with their status; under a launcher, --gpus must equal WORLD_SIZE.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+import benchsupport  # noqa: E402  (synthetic batches + copy ceiling; loads libwsbench.so on first use)
+
 METRIC = "WebSocket frame decode GiB/s device-resident at 1/2/4/8 MI355X; % HBM peak"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+# per-GPU workloads of BASELINE.json (configs[2] and configs[4] are measured as extra
+# lines of the N=1 run; configs[0] needs a JDK)
+CONFIGS = {
+    # north star: unmask + UTF-8 of 1 M x 4 KiB masked TEXT frames at 1 GPU
+    "north": dict(frames=1 << 20, payload=4096, sessions=1024, binary=False),
+    # configs[1]: 1 M masked BINARY frames, 1 KiB payload, 256 sessions (unmask only)
+    "1": dict(frames=1 << 20, payload=1024, sessions=256, binary=True),
+    # configs[3]: 64 M x 4 KiB sharded by session over 8 GPUs = 8 M frames per GPU
+    # (weak scaling: the per-GPU shard is fixed at every N; 64 M frames do not fit one GPU)
+    "3": dict(frames=8 << 20, payload=4096, sessions=1024, binary=False),
+}
 
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None, help="GPUs (rank processes); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--frames", type=int, default=1 << 20, help="frames per GPU")
-    ap.add_argument("--payload", type=int, default=4096)
-    ap.add_argument("--sessions", type=int, default=1024, help="sessions per GPU")
+    ap.add_argument("--config", choices=sorted(CONFIGS), default="north",
+                    help="per-GPU workload: north (1M x 4 KiB TEXT), 1 (configs[1]), 3 (configs[3] shard, 8M x 4 KiB)")
+    ap.add_argument("--frames", type=int, default=None, help="frames per GPU (overrides --config)")
+    ap.add_argument("--payload", type=int, default=None)
+    ap.add_argument("--sessions", type=int, default=None, help="sessions per GPU")
     ap.add_argument("--binary", action="store_true", help="BINARY frames (unmask only, no UTF-8 work)")
     ap.add_argument("--no-validate", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -43,7 +66,61 @@ def parse():
     ap.add_argument("--inflate-only", action="store_true", help="only the permessage-deflate inflate line")
     ap.add_argument("--handshake-only", action="store_true", help="only the server handshake line")
     ap.add_argument("--inflate-sessions", type=int, nargs="+", default=[8192])
-    return ap.parse_args()
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    for k in ("frames", "payload", "sessions"):
+        if getattr(args, k) is None:
+            setattr(args, k, cfg[k])
+    args.binary = args.binary or cfg["binary"]
+    return args
+
+
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_or_check_world(args) -> int:
+    """The N of --gpus N.  Without a torch.distributed environment and N > 1, start
+    the N rank processes (one per GPU) as children of this process and exit with
+    their status: nothing here has touched a GPU yet.  Under a launcher, --gpus must
+    match WORLD_SIZE, so a line never reports fewer GPUs than were asked for."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None:
+        n = 1 if args.gpus is None else args.gpus
+        if n > 1:
+            cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                   "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__),
+                   *sys.argv[1:]]
+            sys.exit(subprocess.call(cmd))
+        return 1
+    world = int(env_world)
+    if args.gpus is not None and args.gpus != world:
+        sys.exit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (one rank process per GPU)")
+    return world
+
+
+def cpu_threads() -> tuple[int, str]:
+    """Host threads for the N-thread CPU baseline: this process's CPU affinity,
+    capped by OMP_NUM_THREADS when set (the GPU box's CPU share is 16, while the
+    affinity mask may list the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit() and 0 < int(omp) < aff:
+        return int(omp), f"min(sched_getaffinity={aff}, OMP_NUM_THREADS={omp})"
+    return aff, f"sched_getaffinity={aff}"
+
+
+def config0_line():
+    """configs[0]: the reference's loopback echo (snf4j SelectorLoop, Java) on the CPU.
+    Needs a JDK and the snf4j jars on the box; reported, never substituted."""
+    java = shutil.which("java")
+    return {"config": "configs[0]: snf4j-websocket loopback echo over 127.0.0.1, 1 session, 4 KiB masked binary "
+                      "frames (CPU reference codec, no GPU)",
+            "status": ("not runnable (java found at %s, but the snf4j jars do not travel to the box)" % java
+                       if java else "not runnable (no JDK on the box: `java` not on PATH)"),
+            "value": None}
 
 
 def cpu_baseline(args, seconds):
@@ -72,14 +149,15 @@ def cpu_baseline(args, seconds):
                       f"no JDK on the box, the Java reference is not runnable)"}
 
 
-def cpu_baseline_mt(args, seconds, threads=16):
-    """The same C restatement on `threads` host threads, one Batch (own sessions) per
-    thread: the N-thread figure SURVEY.md §8(d) asks for beside the 1-thread one.
-    ctypes releases the GIL around each oracle call, so the threads decode in parallel.
-    The GPU box's CPU share is 16 threads (os.cpu_count() shows the whole machine)."""
+def cpu_baseline_mt(args, seconds):
+    """The same C restatement on N host threads (cpu_threads()), one Batch (own
+    sessions) per thread: the N-thread figure SURVEY.md §8(d) asks for beside the
+    1-thread one.  ctypes releases the GIL around each oracle call, so the threads
+    decode in parallel."""
     import threading
     from oracle import pyoracle
     pyoracle.build()
+    threads, how = cpu_threads()
     n = min(args.frames, 16384)
     fps = max(1, args.frames // args.sessions)
     wire, off, sf = pyoracle.synth_uniform(1234, n, args.payload, min(fps, n), opcode=2 if args.binary else 1,
@@ -102,17 +180,17 @@ def cpu_baseline_mt(args, seconds, threads=16):
         t.join()
     el = time.perf_counter() - t0
     gib = sum(counts) * int(off[-1]) / el / 2**30
-    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port",
+    return {"value": round(gib, 4), "unit": "GiB/s", "cores": threads, "kind": "port", "cores_from": how,
             "sample": f"{threads} threads, each decoding {n} frames x {args.payload} B repeatedly for {el:.1f} s "
                       f"({sum(counts)} batches) with the C restatement (oracle/)"}
 
 
 def main():
     args = parse()
+    world = launch_or_check_world(args)  # (may start the rank processes and exit)
     import numpy as np
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
@@ -122,8 +200,11 @@ def main():
         dist.init_process_group("gloo")
     # WSG_BENCH_ONE_DEVICE=1 puts every rank on device 0: a rehearsal of the N>1
     # code path (barrier, max over ranks) on a 1-GPU box, never a reported number
-    if os.environ.get("WSG_BENCH_ONE_DEVICE") == "1":
+    one_device = os.environ.get("WSG_BENCH_ONE_DEVICE") == "1"
+    if one_device:
         local = 0
+    elif local >= torch.cuda.device_count():
+        sys.exit(f"bench.py: rank {rank} needs GPU {local}, but {torch.cuda.device_count()} are visible")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
@@ -151,7 +232,7 @@ def main():
     off = torch.empty(F + 1, dtype=torch.int64, device=dev)
     sf = torch.empty(n_s + 1, dtype=torch.int32, device=dev)
     # sessions of rank r are global sessions [r*n_s, (r+1)*n_s): shard by session, own seed
-    ctx.synth_uniform(rank_seed(0x5EED, rank), F, P, fps, opcode, True, text, wire, off, sf)
+    benchsupport.synth_uniform(ctx, rank_seed(0x5EED, rank), F, P, fps, opcode, True, text, wire, off, sf)
     payload_cap = F * flen + 16 * F + 16
     payload = torch.empty(payload_cap, dtype=torch.uint8, device=dev)
     desc = torch.empty(F * 16, dtype=torch.uint8, device=dev)
@@ -185,7 +266,7 @@ def main():
     unmask_ms, unmask_n = timing["k_piecesN"]
     avg_unmask_s = unmask_ms / 1e3 / max(1, unmask_n)
     alg_bytes = wire_bytes + F * P  # per launch: wire read + payload written
-    copy = ctx.copy_ceiling(wire, payload, wire_bytes)
+    copy = benchsupport.copy_ceiling(ctx, wire, payload, wire_bytes)
     achieved = alg_bytes / avg_unmask_s / 1e9
     traffic = None
     if os.path.exists(args.pmc_json):
@@ -205,16 +286,19 @@ def main():
     if world == 1 and not args.no_extras:
         del wire, payload, desc, res, state, off, sf
         torch.cuda.empty_cache()
-        extras = measure_extras(ctx, dev, args)
+        extras = [config0_line()] + measure_extras(ctx, dev, args)
 
+    # the CPU baseline runs after every timed region, on rank 0 only (at N > 1 the
+    # other ranks wait for it at the closing barrier)
     cpu = cpu_mt = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args, args.cpu_seconds)
         cpu_mt = cpu_baseline_mt(args, 5.0)
 
     if rank == 0:
         total_wire = wire_bytes * world
         value = total_wire * args.steps / elapsed / 2**30
+        ms_step = elapsed / args.steps * 1e3
         out = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -222,13 +306,15 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "ms_per_step": round(ms_step, 4),
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic",
             "config": {
+                "baseline_config": {"north": "north star (1 GPU)", "1": "configs[1]",
+                                    "3": "configs[3] (per-GPU shard of 64M x 4 KiB over 8 GPUs)"}[args.config],
                 "workload": (f"{F} x {P} B masked {'BINARY' if args.binary else 'TEXT'} frames per GPU, "
                              f"{n_s} sessions per GPU, unmask{'' if args.binary or args.no_validate else ' + UTF-8 validation'}"
                              f", server-side decode (FrameDecoder+FrameUtf8Validator)"),
@@ -250,6 +336,10 @@ def main():
                 "avg_launch_ms": round(avg_unmask_s * 1e3, 4),
                 "copy_ceiling_GBs": round(copy, 1),
                 "frac_of_copy_ceiling": round(achieved / copy, 4),
+                # the north star's "HBM read-bandwidth fraction": wire bytes read / time / 8 TB/s,
+                # over the streaming kernel and over the whole step
+                "read_frac": round(wire_bytes / avg_unmask_s / 1e9 / HBM_PEAK_GBS, 4),
+                "read_frac_step": round(wire_bytes / (ms_step / 1e3) / 1e9 / HBM_PEAK_GBS, 4),
             },
             "pipeline_ms": pipe,
             "cpu_baseline": cpu,
@@ -264,6 +354,7 @@ def main():
         print(json.dumps(out), flush=True)
     ctx.close()
     if dist:
+        dist.barrier()  # (the other ranks wait here for rank 0's CPU baseline)
         dist.destroy_process_group()
 
 
@@ -371,7 +462,7 @@ def inflate_line(ctx, dev, steps, warmup, n_s=8192, msgs=16, msg_bytes=4096, cpu
     import numpy as np
     import torch
     from snf4j_amd._lib import DESC_DTYPE, RESULT_DTYPE
-    from snf4j_amd.synth import deflate_batch
+    from benchsupport.synth import deflate_batch
     desc_h, sf_h, pl_h, plain = deflate_batch(0x1F1A, n_s, msgs, msg_bytes)
     n = len(desc_h)
     cap = msgs * msg_bytes
@@ -550,7 +641,7 @@ def measure_extras(ctx, dev, args):
     import torch
     from snf4j_amd import encoded_length
     from snf4j_amd._lib import ENCODE_DTYPE
-    from snf4j_amd.synth import mixed_plan
+    from benchsupport.synth import mixed_plan
     out = []
     K, W = args.extra_steps, 2
     # configs[1]: 1 M masked BINARY frames, 1 KiB payload, 256 sessions (unmask only)
@@ -559,16 +650,30 @@ def measure_extras(ctx, dev, args):
     wire = torch.empty(F * flen + 64, dtype=torch.uint8, device=dev)
     off = torch.empty(F + 1, dtype=torch.int64, device=dev)
     sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
-    ctx.synth_uniform(0xC0F2, F, P, F // S, 2, True, 0, wire, off, sf)
+    benchsupport.synth_uniform(ctx, 0xC0F2, F, P, F // S, 2, True, 0, wire, off, sf)
     out.append(_decode_line(ctx, dev, "configs[1]: 1M x 1 KiB masked BINARY, 256 sessions", wire, F * flen, off, sf,
                             F, S, F * P, K, W, expect_errors=0))
+    del wire, off, sf
+    torch.cuda.empty_cache()
+    # configs[3]'s per-GPU shard on this GPU: 8 M x 4 KiB masked TEXT, 1024 sessions
+    # (34.4 GB in + 34.4 GB out in one batch; `bench.py --gpus N --config 3` is the scaling run)
+    c3 = CONFIGS["3"]
+    F, P, S = c3["frames"], c3["payload"], c3["sessions"]
+    flen = encoded_length(P, True)
+    wire = torch.empty(F * flen + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(F + 1, dtype=torch.int64, device=dev)
+    sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    benchsupport.synth_uniform(ctx, 0xC0F4, F, P, F // S, 1, True, 1, wire, off, sf)
+    out.append(_decode_line(ctx, dev, "configs[3] per-GPU shard: 8M x 4 KiB masked TEXT, 1024 sessions, "
+                            "unmask + UTF-8 (1/8 of 64M x 4 KiB)", wire, F * flen, off, sf,
+                            F, S, F * P, max(3, K // 2), W, expect_errors=0))
     del wire, off, sf
     torch.cuda.empty_cache()
     # configs[2]: mixed text+binary 64 B-64 KiB, UTF-8 on, 1 K sessions, >= 4 GiB wire
     t, offh, sfh, wl, info = mixed_plan(0xC0F3, 1024, 4 << 30)
     tab = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
     wire = torch.zeros(wl + 64, dtype=torch.uint8, device=dev)
-    ctx.synth_frames(tab, wire)
+    benchsupport.synth_frames(ctx, tab, wire)
     del tab
     line = _decode_line(ctx, dev, "configs[2]: mixed TEXT+BINARY 64 B-64 KiB log-uniform, 10% fragmented, "
                         "1% of text messages with invalid UTF-8, 1024 sessions", wire, wl,

@@ -1,9 +1,14 @@
-// synth.hip — synthetic frame batches generated in HBM (bench / tests only).
-// Byte-identical to the oracle's or_synth_uniform (oracle/ws_oracle.c), so a
-// sample copied back can be checked on the host.
-#include "wsgpu_internal.h"
+// synth.hip — libwsbench.so: synthetic frame batches generated in HBM and the
+// streaming-copy ceiling (bench.py / GPU tests only; include/wsbench.h).  Not part
+// of the codec library.  Byte-identical to the oracle's or_synth_uniform
+// (oracle/ws_oracle.c), so a sample copied back can be checked on the host.
+#include <stdint.h>
 
-namespace ws {
+#include <hip/hip_runtime.h>
+
+#include "../../include/wsbench.h"
+
+namespace wsb {
 
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
@@ -111,10 +116,10 @@ __global__ __launch_bounds__(256) void k_synth_header(uint64_t seed, uint64_t n_
   }
 }
 
-// Table-driven batches (wsg_synth_frames): one workgroup per frame; thread 0
+// Table-driven batches (wsb_synth_frames): one workgroup per frame; thread 0
 // writes the header, the threads generate the message's 16-B chunks that
 // overlap this fragment and store the fragment's bytes (masked).
-__device__ __forceinline__ void msg_chunk(const wsg_synth_frame& f, uint64_t c, uint8_t tmp[16]) {
+__device__ __forceinline__ void msg_chunk(const wsb_synth_frame& f, uint64_t c, uint8_t tmp[16]) {
   const uint64_t h = splitmix64(f.msg_seed + c);
   if (f.text) {
     synth_text16(h, tmp);
@@ -140,10 +145,10 @@ __device__ __forceinline__ void msg_chunk(const wsg_synth_frame& f, uint64_t c, 
   }
 }
 
-__global__ __launch_bounds__(256) void k_synth_frames(const wsg_synth_frame* __restrict__ t, uint64_t n,
+__global__ __launch_bounds__(256) void k_synth_frames(const wsb_synth_frame* __restrict__ t, uint64_t n,
                                                       uint8_t* wire) {
   for (uint64_t k = blockIdx.x; k < n; k += gridDim.x) {
-    const wsg_synth_frame f = t[k];
+    const wsb_synth_frame f = t[k];
     const int masked = f.flags & 1;
     uint8_t* w = wire + f.wire_off;
     const uint32_t hl = hdr_len(f.payload_len, masked);
@@ -180,7 +185,7 @@ __global__ __launch_bounds__(256) void k_synth_frames(const wsg_synth_frame* __r
   }
 }
 
-void launch_synth_frames(const wsg_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s) {
+void launch_synth_frames(const wsb_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s) {
   if (n) hipLaunchKernelGGL(k_synth_frames, dim3((uint32_t)(n < 65536 ? n : 65536)), dim3(256), 0, s, t, n, wire);
 }
 
@@ -209,4 +214,51 @@ void launch_synth(uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32
                        wire);
 }
 
-}  // namespace ws
+}  // namespace wsb
+
+// ------------------------------------------------------------------ C ABI (wsbench.h)
+extern "C" {
+
+static int ready(int device) { return hipSetDevice(device) == hipSuccess ? 0 : -1; }
+
+int wsb_synth_uniform(int device, void* stream, uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps,
+                      int opcode, int masked, int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first) {
+  if (fps == 0 || !wire || !frame_off || !session_first) return -1;
+  if (ready(device)) return -2;
+  wsb::launch_synth(seed, n_frames, payload_len, fps, opcode, masked, text, wire, frame_off, session_first,
+                    (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int wsb_synth_frames(int device, void* stream, const wsb_synth_frame* table, uint64_t n_frames, uint8_t* wire) {
+  if (n_frames && (!table || !wire)) return -1;
+  if (ready(device)) return -2;
+  wsb::launch_synth_frames(table, n_frames, wire, (hipStream_t)stream);
+  return hipGetLastError() == hipSuccess ? 0 : -2;
+}
+
+int wsb_copy_ceiling(int device, void* stream, const void* src, void* dst, uint64_t bytes, int reps, double* gbs) {
+  if (!gbs || reps <= 0 || !src || !dst) return -1;
+  if (ready(device)) return -2;
+  hipStream_t s = (hipStream_t)stream;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -2;
+  float best = 1e30f;
+  int rc = 0;
+  for (int r = 0; r <= reps && !rc; ++r) {
+    float ms = 0.f;
+    if (hipEventRecord(e0, s) != hipSuccess) rc = -2;
+    wsb::launch_copy_ceiling(src, dst, bytes, s);
+    if (!rc && (hipEventRecord(e1, s) != hipSuccess || hipEventSynchronize(e1) != hipSuccess ||
+                hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+      rc = -2;
+    if (!rc && r > 0 && ms < best) best = ms;  // the first run warms up
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  if (rc) return rc;
+  *gbs = 2.0 * (double)(bytes / 16 * 16) / (best * 1e-3) / 1e9;
+  return 0;
+}
+
+}  // extern "C"

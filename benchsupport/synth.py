@@ -1,13 +1,18 @@
 """Host planner of synthetic mixed batches (BASELINE.json configs[2]; SURVEY.md §8d
 "Config 3"): the host decides message sizes, text/binary, fragmentation, session
-placement and injected invalid UTF-8; wsg_synth_frames writes the bytes on the
-device.  Bench and test infrastructure only — the decode path never calls it.
+placement and injected invalid UTF-8; wsb_synth_frames (libwsbench.so) writes the
+bytes on the device.  Bench and test infrastructure only — the decode path never
+calls it.
 """
 from __future__ import annotations
 
 import numpy as np
 
-from ._lib import SYNTH_DTYPE
+# wsb_synth_frame (include/wsbench.h)
+SYNTH_DTYPE = np.dtype([("wire_off", "<u8"), ("msg_seed", "<u8"), ("payload_len", "<u4"), ("msg_pos", "<u4"),
+                        ("msg_len", "<u4"), ("mask", "<u4"), ("inject_pos", "<i4"), ("opcode", "u1"),
+                        ("flags", "u1"), ("text", "u1"), ("inject_kind", "u1")])
+assert SYNTH_DTYPE.itemsize == 40
 
 
 def header_len(payload_len, masked: bool):
@@ -23,15 +28,18 @@ def mixed_plan(seed: int, n_sessions: int, target_wire_bytes: int, min_len: int 
     UTF-8, ~70 % ASCII bytes) else BINARY; `frag_frac` of them fragmented into 2..max_frags
     frames cut at arbitrary bytes (code points split across fragments); `bad_frac` of the
     text messages carry one injected invalid sequence.  Sessions own contiguous frames.
+    The wire holds at least target_wire_bytes.
 
     Returns (table[SYNTH_DTYPE], frame_off u64[n+1], session_first u32[n_sessions+1], wire_len,
     info dict)."""
     rng = np.random.default_rng(seed)
     lo, hi = np.log(min_len), np.log(max_len + 1)
     mean = (max_len - min_len) / (hi - lo)
-    n_msgs = max(n_sessions, int(target_wire_bytes / (mean + 10)) + 1)
+    n_msgs = max(n_sessions, int(1.25 * target_wire_bytes / (mean + 10)) + 16)
     L = np.exp(rng.uniform(lo, hi, n_msgs)).astype(np.int64).clip(min_len, max_len)
-    approx = np.cumsum(L + 10)
+    # a message's wire bytes are >= its payload + the smallest header (2 B, + 4 B mask),
+    # so cutting where these lower bounds reach the target gives wire_len >= target
+    approx = np.cumsum(L + (6 if masked else 2))
     n_msgs = max(min(n_msgs, int(np.searchsorted(approx, target_wire_bytes)) + 1), 1)
     L = L[:n_msgs]
     is_text = rng.random(n_msgs) < text_frac
@@ -100,7 +108,7 @@ def deflate_batch(seed: int, n_sessions: int, msgs_per_session: int, msg_bytes: 
     compressed on the host and tiled over n_sessions (each copy at its own offset).
     Returns (desc[n], session_first[n_s+1], payload, plain_bytes_per_batch)."""
     import zlib
-    from ._lib import DESC_DTYPE
+    from snf4j_amd._lib import DESC_DTYPE
     rng = np.random.default_rng(seed)
     letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
     vocab = [bytes(letters[rng.integers(0, 26, int(rng.integers(2, 10)))]) for _ in range(3000)]

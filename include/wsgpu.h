@@ -159,6 +159,9 @@ int wsg_open(int device, void* stream, wsg_ctx** out);
 int wsg_close(wsg_ctx* ctx);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */
 int wsg_set_stream(wsg_ctx* ctx, void* stream);
+/* The hipStream_t the context enqueues its kernels on (for a caller that orders its
+ * own copies or kernels with the codec's). */
+int wsg_get_stream(wsg_ctx* ctx, void** stream);
 const char* wsg_last_error(wsg_ctx* ctx);
 /* Pre-size device workspace so later batch calls do no allocation (graph-capture safe). */
 int wsg_reserve(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len);
@@ -534,41 +537,6 @@ int wsg_handshake_accept_batch_device(wsg_ctx* ctx, const wsg_hs_config* cfg, co
 /* Same with host pointers (H2D, kernel, D2H). */
 int wsg_handshake_accept_batch_host(wsg_ctx* ctx, const wsg_hs_config* cfg, const uint8_t* req,
                                     const uint64_t* req_off, uint32_t n, uint8_t* resp, wsg_hs_result* result);
-
-/* ---------------- synthetic workloads (bench / tests only) ---------------- */
-/* Fill a device batch of uniform frames: n_frames frames of payload_len bytes,
- * frame k at k*frame_len in wire (frame_len = wsg_encoded_length(payload_len, masked)),
- * opcode/fin/masked as given, payload bytes from splitmix64(seed ^ session) where
- * session = k / frames_per_session; text = 1 generates valid UTF-8 (mixed 1-4 byte
- * code points, ~70% ASCII bytes).  Also fills frame_off and session_first. */
-int wsg_synth_uniform(wsg_ctx* ctx, uint64_t seed, uint64_t n_frames, uint32_t payload_len,
-                      uint32_t frames_per_session, int opcode, int masked, int text,
-                      uint8_t* wire, uint64_t* frame_off, uint32_t* session_first);
-
-/* One frame of a table-driven synthetic batch (wsg_synth_frames): the host
- * plans messages, fragmentation and sessions (snf4j_amd/synth.py); the device
- * writes headers and payloads.  Message bytes are a pure function of
- * (msg_seed, byte position), so a message cut into fragments at any byte splits
- * its code points across frame boundaries. */
-typedef struct wsg_synth_frame {
-    uint64_t wire_off;     /* frame start in wire */
-    uint64_t msg_seed;     /* message content seed */
-    uint32_t payload_len;  /* this fragment's payload length */
-    uint32_t msg_pos;      /* offset of this fragment's payload within its message */
-    uint32_t msg_len;      /* whole message length */
-    uint32_t mask;         /* mask key (little-endian bytes), used when masked */
-    int32_t inject_pos;    /* message offset of an injected invalid UTF-8 sequence, -1 = none */
-    uint8_t opcode;
-    uint8_t flags;         /* bit7 = FIN, bit0 = masked */
-    uint8_t text;          /* 1 = valid UTF-8 content (~70% ASCII), 0 = random bytes */
-    uint8_t inject_kind;   /* 0: C0 80, 1: ED A0 80, 2: F4 90 80 80, 3: E2 82 'a', 4: FF */
-} wsg_synth_frame; /* 40 bytes */
-
-int wsg_synth_frames(wsg_ctx* ctx, const wsg_synth_frame* table, uint64_t n_frames, uint8_t* wire);
-
-/* Measured streaming ceiling of this device: best-of-`reps` nontemporal 16-B
- * copy of `bytes` from src to dst (device pointers), in GB/s of read+write. */
-int wsg_copy_ceiling(wsg_ctx* ctx, const void* src, void* dst, uint64_t bytes, int reps, double* gbs);
 
 #ifdef __cplusplus
 }

@@ -6,7 +6,8 @@ import time
 import torch
 
 sys.path.insert(0, ".")
-import snf4j_amd
+import benchsupport  # noqa: E402
+import snf4j_amd  # noqa: E402
 
 F, P, S = 1 << 18, 4096, 256
 dev = torch.device("cuda", 0)
@@ -16,7 +17,7 @@ ctx0 = snf4j_amd.Context(0)
 wire = torch.empty(WB + 64, dtype=torch.uint8, device=dev)
 off = torch.empty(F + 1, dtype=torch.int64, device=dev)
 sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
-ctx0.synth_uniform(7, F, P, F // S, 1, True, 1, wire, off, sf)
+benchsupport.synth_uniform(ctx0, 7, F, P, F // S, 1, True, 1, wire, off, sf)
 torch.cuda.synchronize(dev)
 cfg = snf4j_amd.decoder_cfg(False, False, 65536, True)
 h_wire = wire[:WB].cpu().pin_memory()

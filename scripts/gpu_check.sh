@@ -1,10 +1,10 @@
 #!/bin/bash
-# GPU validation pass: parity tests, smoke, bench.  Every GPU step has its own
-# time limit; the script stops at the first fault/abort/timeout (exit >= 2 or signal).
+# GPU validation pass: parity tests, smoke, the N=2 launcher rehearsal, bench.
+# Every GPU step has its own time limit; the script stops at the first failure.
+#   scripts/gpu_check.sh [quick]   (quick: no full bench)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 step() {  # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   echo "=== $name ($(date +%T))"
@@ -13,8 +13,11 @@ step() {  # step <name> <seconds> <cmd...>
   echo "--- $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
   return $rc
 }
-step pytest_gpu 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider; rc=$?; ok $rc || exit $rc
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"; rc=$?; ok $rc || exit $rc
-step bench_small 300 python bench.py --frames 262144 --steps 5 --warmup 2 --no-cpu-baseline; rc=$?; ok $rc || exit $rc
-step bench 600 python bench.py --e2e; rc=$?; ok $rc || exit $rc
+step pytest_gpu 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 300 --timeout-method thread || exit $?
+step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
+# N=2 through bench.py's own launcher, both ranks on device 0 (a rehearsal, not a number)
+WSG_BENCH_ONE_DEVICE=1 step bench_n2_rehearsal 300 python bench.py --gpus 2 --frames 262144 --steps 5 --warmup 2 --cpu-seconds 2 || exit $?
+step bench_config3 300 python bench.py --config 3 --steps 5 --warmup 2 --no-extras --no-cpu-baseline || exit $?
+[ "$1" = quick ] && { echo ALL_DONE; exit 0; }
+step bench 600 python bench.py --e2e || exit $?
 echo ALL_DONE

@@ -78,10 +78,6 @@ try:
                                 ("length", "<u4")])
     INFLATE_STATE_DTYPE = np.dtype([("compressing", "u1"), ("has_decoder", "u1"), ("finished", "u1"),
                                     ("reserved", "u1"), ("window_len", "<u2"), ("window_phase", "<u2")])
-    SYNTH_DTYPE = np.dtype([("wire_off", "<u8"), ("msg_seed", "<u8"), ("payload_len", "<u4"), ("msg_pos", "<u4"),
-                            ("msg_len", "<u4"), ("mask", "<u4"), ("inject_pos", "<i4"), ("opcode", "u1"),
-                            ("flags", "u1"), ("text", "u1"), ("inject_kind", "u1")])
-    assert SYNTH_DTYPE.itemsize == 40
     HS_RESULT_DTYPE = np.dtype([("frame_len", "<u4"), ("http_status", "<u2"), ("kind", "u1"), ("cause", "u1"),
                                 ("resp_len", "<u2"), ("detail_len", "<u2"), ("detail_off", "<u4")])
     assert HS_RESULT_DTYPE.itemsize == 16
@@ -109,6 +105,7 @@ def _load():
         "wsg_open": ([i32, p, P(p)], i32),
         "wsg_close": ([p], i32),
         "wsg_set_stream": ([p, p], i32),
+        "wsg_get_stream": ([p, P(p)], i32),
         "wsg_last_error": ([p], C.c_char_p),
         "wsg_reserve": ([p, u64, u32, u64], i32),
         "wsg_sync": ([p], i32),
@@ -126,9 +123,6 @@ def _load():
         "wsg_encoded_length": ([u32, i32], u64),
         "wsg_encode_batch_device": ([p, i32, p, u64, p, u64, p, u32, p, p, u64, p], i32),
         "wsg_encode_batch_host": ([p, i32, p, u64, p, u64, p, u32, p, p, u64, p], i32),
-        "wsg_synth_uniform": ([p, u64, u64, u32, u32, i32, i32, i32, p, p, p], i32),
-        "wsg_copy_ceiling": ([p, p, p, u64, i32, P(C.c_double)], i32),
-        "wsg_synth_frames": ([p, p, u64, p], i32),
         "wsg_batcher_open": ([p, P(DecoderCfg), u32, P(p)], i32),
         "wsg_batcher_close": ([p], i32),
         "wsg_batcher_last_error": ([p], C.c_char_p),

@@ -1,4 +1,6 @@
-"""Build libwsgpu.so (HIP for gfx950) in-tree: snf4j_amd/libwsgpu.so."""
+"""Build the HIP libraries (gfx950) in-tree:
+  snf4j_amd/libwsgpu.so      the codec (include/wsgpu.h)
+  benchsupport/libwsbench.so synthetic batches + copy ceiling for bench/tests (include/wsbench.h)"""
 from __future__ import annotations
 
 import os
@@ -9,8 +11,12 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libwsgpu.so")
-SOURCES = ["decode.hip", "encode.hip", "aggregate.hip", "synth.hip", "api.hip", "batcher.hip", "inflate.hip", "handshake.hip"]
+SOURCES = ["decode.hip", "encode.hip", "aggregate.hip", "api.hip", "batcher.hip", "inflate.hip", "handshake.hip"]
 HEADERS = ["ws_rules.h", "wsgpu_internal.h", "wsgpu_scan.h", "../../include/wsgpu.h"]
+BENCH_DIR = os.path.join(os.path.dirname(HERE), "benchsupport")
+BENCH_SRC = os.path.join(BENCH_DIR, "csrc", "synth.hip")
+BENCH_OUT = os.path.join(BENCH_DIR, "libwsbench.so")
+BENCH_HDR = os.path.join(os.path.dirname(HERE), "include", "wsbench.h")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 # -disable-promote-alloca-to-lds: a dynamically indexed local array must not turn
 # into an LDS allocation, which slows the dispatch of the piece kernels' millions
@@ -27,7 +33,20 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
+def build_bench(force: bool = False) -> str:
+    if not force and os.path.exists(BENCH_OUT) and all(
+            os.path.getmtime(d) <= os.path.getmtime(BENCH_OUT) for d in (BENCH_SRC, BENCH_HDR)):
+        return BENCH_OUT
+    tmp = BENCH_OUT + ".tmp"
+    r = subprocess.run([HIPCC, *FLAGS, "-shared", BENCH_SRC, "-o", tmp], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {BENCH_SRC}:\n{r.stderr}")
+    os.replace(tmp, BENCH_OUT)
+    return BENCH_OUT
+
+
 def build(force: bool = False, verbose: bool = False) -> str:
+    build_bench(force)
     if not force and not _stale():
         return OUT
     objdir = os.path.join(HERE, "_build")

@@ -103,6 +103,13 @@ class Context:
     def set_stream(self, stream):
         check(lib.wsg_set_stream(self._h, C.c_void_p(_stream_handle(stream))), self._h)
 
+    @property
+    def stream_handle(self) -> int:
+        """The hipStream_t the context enqueues on (wsg_get_stream)."""
+        h = C.c_void_p()
+        check(lib.wsg_get_stream(self._h, C.byref(h)), self._h)
+        return int(h.value or 0)
+
     def sync(self):
         check(lib.wsg_sync(self._h), self._h)
 
@@ -313,26 +320,6 @@ class Context:
                                         n_frames, session_first.ctypes.data, n_sessions, closed.ctypes.data,
                                         wire.ctypes.data, cap, wire_off.ctypes.data), self._h)
         return wire[:int(wire_off[-1])], wire_off
-
-    def copy_ceiling(self, src, dst, nbytes: int, reps: int = 5) -> float:
-        """GB/s (read+write) of the device's best streaming copy over nbytes (tensors)."""
-        g = C.c_double(0)
-        check(lib.wsg_copy_ceiling(self._h, _p(src), _p(dst), int(nbytes), int(reps), C.byref(g)), self._h)
-        return float(g.value)
-
-    # -------------------------------------------------------------- synthetic data
-    def synth_uniform(self, seed, n_frames, payload_len, frames_per_session, opcode, masked, text, wire,
-                      frame_off, session_first):
-        check(lib.wsg_synth_uniform(self._h, int(seed), int(n_frames), int(payload_len), int(frames_per_session),
-                                    int(opcode), int(masked), int(text), _p(wire), _p(frame_off),
-                                    _p(session_first)), self._h)
-
-
-    def synth_frames(self, table, wire):
-        """Table-driven synthetic batch (wsg_synth_frames); `table` is a device
-        uint8 tensor holding SYNTH_DTYPE records (snf4j_amd/synth.py)."""
-        n = table.numel() // 40
-        check(lib.wsg_synth_frames(self._h, _p(table), int(n), _p(wire)), self._h)
 
 
 def frame_available(buf: bytes, length: int | None = None):

@@ -16,7 +16,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_synth",    "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok"};
+                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -212,6 +212,12 @@ int wsg_set_stream(wsg_ctx* c, void* stream) {
     c->own_stream = false;
   }
   c->stream = (hipStream_t)stream;
+  return WSG_API_OK;
+}
+
+int wsg_get_stream(wsg_ctx* c, void** stream) {
+  if (!c || !stream) return WSG_API_EINVAL;
+  *stream = (void*)c->stream;
   return WSG_API_OK;
 }
 
@@ -962,47 +968,6 @@ int wsg_handshake_accept_batch_host(wsg_ctx* c, const wsg_hs_config* cfg, const 
   HIP_TRY(c, hipMemcpyAsync(resp, d_resp.p, (uint64_t)n * WSG_HS_RESP_STRIDE, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(result, d_res.p, (uint64_t)n * sizeof(wsg_hs_result), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
-  return WSG_API_OK;
-}
-
-int wsg_copy_ceiling(wsg_ctx* c, const void* src, void* dst, uint64_t bytes, int reps, double* gbs) {
-  if (!c || !gbs || reps <= 0) return WSG_API_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
-  hipEvent_t e0, e1;
-  HIP_TRY(c, hipEventCreate(&e0));
-  HIP_TRY(c, hipEventCreate(&e1));
-  float best = 1e30f;
-  for (int r = 0; r <= reps; ++r) {
-    HIP_TRY(c, hipEventRecord(e0, c->stream));
-    launch_copy_ceiling(src, dst, bytes, c->stream);
-    HIP_TRY(c, hipEventRecord(e1, c->stream));
-    HIP_TRY(c, hipEventSynchronize(e1));
-    float ms = 0.f;
-    HIP_TRY(c, hipEventElapsedTime(&ms, e0, e1));
-    if (r > 0 && ms < best) best = ms;  // first run warms up
-  }
-  (void)hipEventDestroy(e0);
-  (void)hipEventDestroy(e1);
-  *gbs = 2.0 * (double)(bytes / 16 * 16) / (best * 1e-3) / 1e9;
-  return WSG_API_OK;
-}
-
-int wsg_synth_uniform(wsg_ctx* c, uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode,
-                      int masked, int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first) {
-  if (!c || fps == 0) return WSG_API_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
-  timed(c, K_SYNTH, [&] {
-    launch_synth(seed, n_frames, payload_len, fps, opcode, masked, text, wire, frame_off, session_first, c->stream);
-  });
-  HIP_TRY(c, hipGetLastError());
-  return WSG_API_OK;
-}
-
-int wsg_synth_frames(wsg_ctx* c, const wsg_synth_frame* table, uint64_t n_frames, uint8_t* wire) {
-  if (!c || (n_frames && (!table || !wire))) return WSG_API_EINVAL;
-  HIP_TRY(c, hipSetDevice(c->device));
-  timed(c, K_SYNTH, [&] { launch_synth_frames(table, n_frames, wire, c->stream); });
-  HIP_TRY(c, hipGetLastError());
   return WSG_API_OK;
 }
 

@@ -1,5 +1,5 @@
 // wsgpu_internal.h — device workspace layout and launch interface shared by the
-// kernels (decode.hip, encode.hip, synth.hip) and the C ABI (api.hip).
+// kernels (decode.hip, encode.hip, ...) and the C ABI (api.hip).
 #pragma once
 #include <stdint.h>
 
@@ -195,7 +195,7 @@ struct InflTokStat {
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_SYNTH, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -228,10 +228,5 @@ void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64
                       uint8_t* resp, wsg_hs_result* result, hipStream_t s);
 __host__ __device__ int hs_frame_len(const uint8_t* d, int64_t len, int* capped, int64_t* lines_end);
 
-void launch_copy_ceiling(const void* src, void* dst, uint64_t bytes, hipStream_t s);
-void launch_synth_frames(const wsg_synth_frame* t, uint64_t n, uint8_t* wire, hipStream_t s);
-void launch_synth(uint64_t seed, uint64_t n_frames, uint32_t payload_len, uint32_t fps, int opcode,
-                  int masked, int text, uint8_t* wire, uint64_t* frame_off, uint32_t* session_first,
-                  hipStream_t s);
 
 }  // namespace ws

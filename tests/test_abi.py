@@ -28,6 +28,22 @@ def test_exports_every_header_symbol(L):
     assert L.lib.wsg_num_kernels() >= 5
 
 
+def test_bench_library_exports_wsbench_header():
+    """libwsbench.so (bench/test support) exports what include/wsbench.h declares,
+    and the codec library does not carry the bench-only entry points."""
+    import re
+    from snf4j_amd import _lib
+    import benchsupport
+    with open(os.path.join(ROOT, "include", "wsbench.h")) as fh:
+        syms = sorted(set(re.findall(r"\b(wsb_[a-z_]+)\(", fh.read())))
+    assert syms == ["wsb_copy_ceiling", "wsb_synth_frames", "wsb_synth_uniform"]
+    raw = C.CDLL(benchsupport.LIB_PATH)
+    assert all(hasattr(raw, s) for s in syms)
+    codec = C.CDLL(_lib.LIB_PATH)
+    for s in ("wsg_synth_uniform", "wsg_synth_frames", "wsg_copy_ceiling"):
+        assert not hasattr(codec, s), s
+
+
 def test_library_is_gfx950_code_object(L):
     with open(L.LIB_PATH, "rb") as fh:
         blob = fh.read()

@@ -4,6 +4,8 @@ identical first-error frame / message / close code per session."""
 import numpy as np
 import pytest
 
+import benchsupport
+
 from tests import wsgen
 from tests.golden import fixtures
 
@@ -244,7 +246,7 @@ def test_device_resident_synth_parity(ctx, oracle):
         wire = torch.empty(nf * flen + 64, dtype=torch.uint8, device=dev)
         off = torch.empty(nf + 1, dtype=torch.int64, device=dev)
         sf = torch.empty(n_s + 1, dtype=torch.int32, device=dev)
-        ctx.synth_uniform(77, nf, plen, fps, op, True, text, wire, off, sf)
+        benchsupport.synth_uniform(ctx, 77, nf, plen, fps, op, True, text, wire, off, sf)
         state = torch.zeros(n_s * 8, dtype=torch.uint8, device=dev)
         payload = torch.empty(nf * flen + 16 * nf + 16, dtype=torch.uint8, device=dev)
         desc = torch.empty(nf * 16, dtype=torch.uint8, device=dev)

@@ -1,5 +1,7 @@
-"""Parity at the north-star size (BASELINE.json: 1 M x 4 KiB masked TEXT frames, 1 GPU),
-through size-independent properties the oracle does not need to replay:
+"""Parity at full size, through size-independent properties the oracle does not need
+to replay, on the north-star batch (BASELINE.json: 1 M x 4 KiB masked TEXT frames,
+1 GPU) and on configs[3]'s per-GPU shard (64 M x 4 KiB over 8 GPUs = 8 M x 4 KiB,
+34.4 GB in + 34.4 GB out in one batch on one GPU):
   * unmasking is an involution: every decoded payload XOR its frame's mask is the wire
     payload, checked over all 4.3 GB on the device;
   * UTF-8 verdicts: invalid bytes planted in chosen frames fail exactly those sessions at
@@ -7,27 +9,32 @@ through size-independent properties the oracle does not need to replay:
     all its frames."""
 import pytest
 
+import benchsupport
+
 pytestmark = pytest.mark.gpu
 
-F, P, S = 1 << 20, 4096, 1024
+P, S = 4096, 1024
 FLEN = P + 8  # 2 + 2 (u16 length) + 4 (mask)
 
 
-@pytest.fixture(scope="module")
-def batch():
+@pytest.fixture(scope="module", params=[1 << 20, 8 << 20], ids=["north_1Mx4K", "configs3_shard_8Mx4K"])
+def batch(request):
     import torch
     from snf4j_amd import Context
+    F = request.param
     dev = torch.device("cuda", 0)
     ctx = Context(0)
     wire = torch.empty(F * FLEN + 64, dtype=torch.uint8, device=dev)
     off = torch.empty(F + 1, dtype=torch.int64, device=dev)
     sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
-    ctx.synth_uniform(0x5EED, F, P, F // S, 1, True, 1, wire, off, sf)
-    yield ctx, dev, wire, off, sf
+    benchsupport.synth_uniform(ctx, 0x5EED ^ F, F, P, F // S, 1, True, 1, wire, off, sf)
+    yield F, ctx, dev, wire, off, sf
     ctx.close()
+    del wire, off, sf
+    torch.cuda.empty_cache()
 
 
-def _decode(ctx, dev, wire, off, sf):
+def _decode(F, ctx, dev, wire, off, sf):
     import torch
     from snf4j_amd import decoder_cfg
     payload = torch.empty(F * FLEN + 16 * F + 16, dtype=torch.uint8, device=dev)
@@ -44,8 +51,8 @@ def test_full_size_unmask_involution(batch):
     import numpy as np
     import torch
     from snf4j_amd._lib import DESC_DTYPE, RESULT_DTYPE
-    ctx, dev, wire, off, sf = batch
-    payload, desc, res = _decode(ctx, dev, wire, off, sf)
+    F, ctx, dev, wire, off, sf = batch
+    payload, desc, res = _decode(F, ctx, dev, wire, off, sf)
     r = res.cpu().numpy().view(RESULT_DTYPE)
     assert int(r["error"].max()) == 0 and int(r["n_delivered"].sum()) == F
     d = desc.cpu().numpy().view(DESC_DTYPE)
@@ -62,9 +69,9 @@ def test_full_size_unmask_involution(batch):
 def test_full_size_planted_utf8_errors(batch):
     import torch
     from snf4j_amd._lib import RESULT_DTYPE
-    ctx, dev, wire, off, sf = batch
+    F, ctx, dev, wire, off, sf = batch
     fps = F // S
-    plant = {3: (17, 0), 500: (1023, 4095), 1023: (0, 2048)}  # session -> (frame in session, payload byte)
+    plant = {3: (17, 0), 500: (fps - 1, 4095), 1023: (0, 2048)}  # session -> (frame in session, payload byte)
     w = wire[:F * FLEN].view(F, FLEN)
     saved = []
     for s, (j, b) in plant.items():
@@ -72,7 +79,7 @@ def test_full_size_planted_utf8_errors(batch):
         saved.append((k, b, int(w[k, 8 + b].item())))
         w[k, 8 + b] = w[k, 4 + (b & 3)] ^ 0xFF  # unmasks to 0xFF: never valid UTF-8
     try:
-        _, _, res = _decode(ctx, dev, wire, off, sf)
+        _, _, res = _decode(F, ctx, dev, wire, off, sf)
     finally:
         for k, b, v in saved:
             w[k, 8 + b] = v

@@ -182,7 +182,7 @@ def test_inflate_predecode_matches_serial_and_zlib(oracle):
     import zlib
     from snf4j_amd import Context
     from snf4j_amd._lib import DESC_DTYPE, INFLATE_STATE_DTYPE
-    from snf4j_amd.synth import deflate_batch
+    from benchsupport.synth import deflate_batch
     n_s, msgs, mb = 96, 8, 2048
     desc, sf, payload, plain = deflate_batch(0xD1F, n_s, msgs, mb, unique=12)
     outs = []

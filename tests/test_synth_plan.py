@@ -1,7 +1,7 @@
 """The mixed-batch planner (snf4j_amd/synth.py, BASELINE configs[2]): structure only, CPU."""
 import numpy as np
 
-from snf4j_amd.synth import header_len, mixed_plan
+from benchsupport.synth import header_len, mixed_plan
 
 
 def test_plan_structure():
@@ -31,3 +31,18 @@ def test_plan_structure():
     assert msgs == info["messages"]
     assert (t["text"][t["inject_pos"] >= 0] == 1).all()
     assert 64 <= t["msg_len"].min() and t["msg_len"].max() <= 65536
+
+
+def test_deflate_batch_plan_inflates_with_zlib():
+    """The permessage-deflate bench batch (benchsupport.synth.deflate_batch): every
+    session's messages inflate with zlib, context takeover, tail appended."""
+    import zlib
+    from benchsupport.synth import deflate_batch
+    desc, sf, pl, plain = deflate_batch(7, 4, 3, 512, unique=2)
+    total = 0
+    for s in range(len(sf) - 1):
+        d = zlib.decompressobj(-15)
+        for k in range(int(sf[s]), int(sf[s + 1])):
+            o, n = int(desc[k]["payload_off"]), int(desc[k]["payload_len"])
+            total += len(d.decompress(pl[o:o + n].tobytes() + b"\x00\x00\xff\xff"))
+    assert total == plain

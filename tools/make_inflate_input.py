@@ -5,7 +5,7 @@ import sys
 import numpy as np
 
 sys.path.insert(0, ".")
-from snf4j_amd.synth import deflate_batch  # noqa: E402
+from benchsupport.synth import deflate_batch  # noqa: E402
 
 n_s = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
 desc, sf, payload, plain = deflate_batch(0x1F1A, n_s, 16, 4096)

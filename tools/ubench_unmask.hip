@@ -3,12 +3,14 @@
 // k_pieces / k_piecesN variants and a plain 16-B copy of the same byte
 // count (the streaming ceiling of this chip), interleaved in one process.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I.. tools/ubench_unmask.hip \
-//         snf4j_amd/csrc/synth.hip -o /tmp/ubench
+//         benchsupport/csrc/synth.hip -o /tmp/ubench
 //   /tmp/ubench [frames] [payload] [text]
 #include <stdio.h>
 #include <stdlib.h>
 
 #include <vector>
+
+#include "../include/wsbench.h"
 
 #include "../snf4j_amd/csrc/decode.hip"
 
@@ -42,7 +44,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&sf, (S + 1) * 4));
   hipStream_t st;
   CK(hipStreamCreate(&st));
-  ws::launch_synth(0x5EED, F, P, fps, text ? 1 : 2, 1, text, wire, off, sf, st);
+  wsb_synth_uniform(0, st, 0x5EED, F, P, fps, text ? 1 : 2, 1, text, wire, off, sf);
   ws::DecodeArgs a{};
   a.wire = wire; a.wire_len = wire_len; a.frame_off = off; a.n_frames = F; a.session_first = sf; a.n_sessions = S;
   a.client_mode = 0; a.allow_ext = 0; a.validate = text; a.max_payload = 65536;
