@@ -66,6 +66,8 @@ def parse():
     ap.add_argument("--inflate-only", action="store_true", help="only the permessage-deflate inflate line")
     ap.add_argument("--handshake-only", action="store_true", help="only the server handshake line")
     ap.add_argument("--inflate-sessions", type=int, nargs="+", default=[8192])
+    ap.add_argument("--only", default=None,
+                    help="print only one secondary line: configs1|configs2|configs3|encode|validator|inflate|handshake")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     for k in ("frames", "payload", "sessions"):
@@ -214,6 +216,10 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     ctx = snf4j_amd.Context(local, stream=stream)
+    if args.only:
+        print(json.dumps(EXTRA_LINES[args.only](ctx, dev, args.extra_steps, 2)), flush=True)
+        ctx.close()
+        return
     if args.handshake_only:
         print(json.dumps(handshake_line(ctx, dev, args.extra_steps, 2)), flush=True)
         return
@@ -635,28 +641,25 @@ def handshake_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
             "pipeline_ms": pipe}
 
 
-def measure_extras(ctx, dev, args):
-    """The other 1-GPU configurations of BASELINE.json, each a device-resident batch."""
-    import numpy as np
+def line_configs1(ctx, dev, K, W):
+    """configs[1]: 1 M masked BINARY frames, 1 KiB payload, 256 sessions (unmask only)."""
     import torch
     from snf4j_amd import encoded_length
-    from snf4j_amd._lib import ENCODE_DTYPE
-    from benchsupport.synth import mixed_plan
-    out = []
-    K, W = args.extra_steps, 2
-    # configs[1]: 1 M masked BINARY frames, 1 KiB payload, 256 sessions (unmask only)
     F, P, S = 1 << 20, 1024, 256
     flen = encoded_length(P, True)
     wire = torch.empty(F * flen + 64, dtype=torch.uint8, device=dev)
     off = torch.empty(F + 1, dtype=torch.int64, device=dev)
     sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
     benchsupport.synth_uniform(ctx, 0xC0F2, F, P, F // S, 2, True, 0, wire, off, sf)
-    out.append(_decode_line(ctx, dev, "configs[1]: 1M x 1 KiB masked BINARY, 256 sessions", wire, F * flen, off, sf,
-                            F, S, F * P, K, W, expect_errors=0))
-    del wire, off, sf
-    torch.cuda.empty_cache()
-    # configs[3]'s per-GPU shard on this GPU: 8 M x 4 KiB masked TEXT, 1024 sessions
-    # (34.4 GB in + 34.4 GB out in one batch; `bench.py --gpus N --config 3` is the scaling run)
+    return _decode_line(ctx, dev, "configs[1]: 1M x 1 KiB masked BINARY, 256 sessions", wire, F * flen, off, sf,
+                        F, S, F * P, K, W, expect_errors=0)
+
+
+def line_configs3(ctx, dev, K, W):
+    """configs[3]'s per-GPU shard on this GPU: 8 M x 4 KiB masked TEXT, 1024 sessions (34.4 GB in +
+    34.4 GB out in one batch; `bench.py --gpus N --config 3` is the scaling run)."""
+    import torch
+    from snf4j_amd import encoded_length
     c3 = CONFIGS["3"]
     F, P, S = c3["frames"], c3["payload"], c3["sessions"]
     flen = encoded_length(P, True)
@@ -664,12 +667,17 @@ def measure_extras(ctx, dev, args):
     off = torch.empty(F + 1, dtype=torch.int64, device=dev)
     sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
     benchsupport.synth_uniform(ctx, 0xC0F4, F, P, F // S, 1, True, 1, wire, off, sf)
-    out.append(_decode_line(ctx, dev, "configs[3] per-GPU shard: 8M x 4 KiB masked TEXT, 1024 sessions, "
-                            "unmask + UTF-8 (1/8 of 64M x 4 KiB)", wire, F * flen, off, sf,
-                            F, S, F * P, max(3, K // 2), W, expect_errors=0))
-    del wire, off, sf
-    torch.cuda.empty_cache()
-    # configs[2]: mixed text+binary 64 B-64 KiB, UTF-8 on, 1 K sessions, >= 4 GiB wire
+    return _decode_line(ctx, dev, "configs[3] per-GPU shard: 8M x 4 KiB masked TEXT, 1024 sessions, "
+                        "unmask + UTF-8 (1/8 of 64M x 4 KiB)", wire, F * flen, off, sf,
+                        F, S, F * P, max(3, K // 2), W, expect_errors=0)
+
+
+def line_configs2(ctx, dev, K, W, aggregate=True):
+    """configs[2]: mixed text+binary 64 B-64 KiB, UTF-8 on, 1 K sessions, >= 4 GiB wire (+ the
+    FrameAggregator line over the decoded batch)."""
+    import numpy as np
+    import torch
+    from benchsupport.synth import mixed_plan
     t, offh, sfh, wl, info = mixed_plan(0xC0F3, 1024, 4 << 30)
     tab = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
     wire = torch.zeros(wl + 64, dtype=torch.uint8, device=dev)
@@ -679,12 +687,17 @@ def measure_extras(ctx, dev, args):
                         "1% of text messages with invalid UTF-8, 1024 sessions", wire, wl,
                         torch.from_numpy(offh.astype(np.int64)).to(dev), torch.from_numpy(sfh.astype(np.int32)).to(dev),
                         len(t), 1024, info["payload_bytes"], K, W, expect_errors=len(info["bad_sessions"]),
-                        aggregate=True)
+                        aggregate=aggregate)
     line["mix"] = {k: v for k, v in info.items() if k != "bad_sessions"}
-    out.append(line)
-    del wire
-    torch.cuda.empty_cache()
-    # configs[4]: client-side encode, 64 messages x 16 MiB in 64 KiB frames (header emit + mask)
+    return line
+
+
+def line_encode(ctx, dev, K, W):
+    """configs[4]: client-side encode, 64 messages x 16 MiB in 64 KiB frames (header emit + mask)."""
+    import numpy as np
+    import torch
+    from snf4j_amd import encoded_length
+    from snf4j_amd._lib import ENCODE_DTYPE
     M, FR, FP = 64, 256, 65536
     n = M * FR
     payload = torch.randint(0, 256, (M * FR * FP,), dtype=torch.uint8, device=dev)
@@ -711,17 +724,51 @@ def measure_extras(ctx, dev, args):
     el, kms, pipe = _timed(ctx, enc, K, W, dev, "k_enc_piecesN")
     alg = M * FR * FP + n * elen
     ach = alg / (kms / 1e3) / 1e9
-    out.append({"config": "configs[4]: client encode, 64 x 16 MiB messages in 64 KiB frames (header + mask)",
-                "value": round(n * elen * K / el / 2**30, 3), "unit": "GiB/s (wire out)",
-                "ms_per_step": round(el / K * 1e3, 4), "frames": n,
-                "roofline": {"kernel": "k_enc_piecesN", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                             "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
-                             "avg_launch_ms": round(kms, 4)},
-                "pipeline_ms": pipe})
-    del payload, wire_out
-    torch.cuda.empty_cache()
-    out.append(inflate_line(ctx, dev, K, W))
-    out.append(handshake_line(ctx, dev, K, W))
+    return {"config": "configs[4]: client encode, 64 x 16 MiB messages in 64 KiB frames (header + mask)",
+            "value": round(n * elen * K / el / 2**30, 3), "unit": "GiB/s (wire out)",
+            "ms_per_step": round(el / K * 1e3, 4), "frames": n,
+            "roofline": {"kernel": "k_enc_piecesN", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": round(kms, 4)},
+            "pipeline_ms": pipe}
+
+
+def line_validator(ctx, dev, K, W):
+    """The FrameUtf8Validator stage alone over the decoded headline batch (bench --only validator)."""
+    import torch
+    import snf4j_amd
+    c = CONFIGS["north"]
+    F, P, S = c["frames"], c["payload"], c["sessions"]
+    flen = snf4j_amd.encoded_length(P, True)
+    wire = torch.empty(F * flen + 64, dtype=torch.uint8, device=dev)
+    off = torch.empty(F + 1, dtype=torch.int64, device=dev)
+    sf = torch.empty(S + 1, dtype=torch.int32, device=dev)
+    benchsupport.synth_uniform(ctx, 0x5EED, F, P, F // S, 1, True, 1, wire, off, sf)
+    payload = torch.empty(F * flen + 16 * F + 16, dtype=torch.uint8, device=dev)
+    desc = torch.empty(F * 16, dtype=torch.uint8, device=dev)
+    res = torch.empty(S * 16, dtype=torch.uint8, device=dev)
+    state = torch.zeros(S * 8, dtype=torch.uint8, device=dev)
+    ctx.reserve(F, S, F * flen)
+    ctx.decode_device(snf4j_amd.decoder_cfg(False, False, 65536, True), wire, off, sf, state, payload, desc, res,
+                      wire_len=F * flen)
+    torch.cuda.synchronize(dev)
+    del wire
+    return validator_line(ctx, dev, desc, sf, payload, S, F, P, K)
+
+
+EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2": line_configs2,
+               "encode": line_encode, "validator": line_validator,
+               "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
+               "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W)}
+
+
+def measure_extras(ctx, dev, args):
+    """The other 1-GPU configurations of BASELINE.json, each a device-resident batch."""
+    import torch
+    out = []
+    for name in ("configs1", "configs3", "configs2", "encode", "inflate", "handshake"):
+        out.append(EXTRA_LINES[name](ctx, dev, args.extra_steps, 2))
+        torch.cuda.empty_cache()
     return out
 
 

@@ -10,7 +10,8 @@ import os
 import re
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libwsgpu.so")
+# WSG_LIB: another build of the same library (A/B runs of kernel variants, scripts/ab_lib.sh)
+LIB_PATH = os.environ.get("WSG_LIB") or os.path.join(HERE, "libwsgpu.so")
 HEADER = os.path.join(os.path.dirname(HERE), "include", "wsgpu.h")
 
 

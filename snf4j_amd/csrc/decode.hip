@@ -496,8 +496,8 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
   if (!(d.info & PD_VALIDATE)) return 0u;
   const uint32_t first_prev = (d.info & PD_FIRST) ? 0u : (alignbyte(pv_hi, pv_lo, b) ^ d.mask);
   const uint32_t pw = dpp_from_prev(w[3], first_prev);
-  uint32_t f0 = utf8_err_word_fast(w[0], pw), f1 = utf8_err_word_fast(w[1], w[0]);
-  uint32_t f2 = utf8_err_word_fast(w[2], w[1]), f3 = utf8_err_word_fast(w[3], w[2]);
+  uint32_t f0 = utf8_err_word_raw(w[0], pw), f1 = utf8_err_word_raw(w[1], w[0]);
+  uint32_t f2 = utf8_err_word_raw(w[2], w[1]), f3 = utf8_err_word_raw(w[3], w[2]);
   if (lane == 0 && (d.info & PD_FIRST)) f0 &= 0x80000000u;  // bytes 0..2: checked against the fragment carry
   if (!full) {
     f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
@@ -507,7 +507,7 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
     const bool ge3 = !((d.info & PD_FIRST) && lane == 0 && keep < 3);  // frame length >= 3
     te = tail_error(last3(pw, w[0], w[1], w[2], w[3], keep), ge3 && (d.info & PD_FIN)) ? 1u : 0u;
   }
-  return f0 | f1 | f2 | f3 | te;
+  return ((f0 | f1 | f2 | f3) & H80) | te;
 }
 
 
@@ -586,8 +586,8 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
     if (j == 0) pw = 0u;
     else if (prev_k != lk) pw = prev_word(a, lr.src + j, lr.mask);  // lane 0 inside a frame
     if (lval) {
-      uint32_t e0 = utf8_err_word_fast(w[0], pw), e1 = utf8_err_word_fast(w[1], w[0]);
-      uint32_t e2 = utf8_err_word_fast(w[2], w[1]), e3 = utf8_err_word_fast(w[3], w[2]);
+      uint32_t e0 = utf8_err_word_raw(w[0], pw), e1 = utf8_err_word_raw(w[1], w[0]);
+      uint32_t e2 = utf8_err_word_raw(w[2], w[1]), e3 = utf8_err_word_raw(w[3], w[2]);
       if (j == 0) e0 &= 0x80000000u;
       e0 &= keep_flags(keep); e1 &= keep_flags(keep - 4); e2 &= keep_flags(keep - 8); e3 &= keep_flags(keep - 12);
       const bool te = keep >= 1 && keep <= 16 &&
@@ -671,21 +671,32 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
     }
   }
   uint32_t w[N][4];
+  if (sh == 0) {  // wave-uniform: a 16-B aligned source (plain payload slots) needs no funnel
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    u32x4 n;
-    if (i + 1 < N) {
-      n.x = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].x, 0);
-      n.y = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].y, 0);
-      n.z = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].z, 0);
-      n.w = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].w, 0);
-    } else {
-      n = nx;
+    for (int i = 0; i < N; ++i) {
+      w[i][0] = A[i].x; w[i][1] = A[i].y; w[i][2] = A[i].z; w[i][3] = A[i].w;
     }
-    funnel16(sh, A[i].x, A[i].y, A[i].z, A[i].w, dpp_from_next(A[i].x, n.x), dpp_from_next(A[i].y, n.y),
-             dpp_from_next(A[i].z, n.z), dpp_from_next(A[i].w, n.w), w[i]);
+  } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) w[i][k] ^= d.mask;
+    for (int i = 0; i < N; ++i) {
+      u32x4 n;
+      if (i + 1 < N) {
+        n.x = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].x, 0);
+        n.y = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].y, 0);
+        n.z = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].z, 0);
+        n.w = (uint32_t)__builtin_amdgcn_readlane((int)A[i + 1].w, 0);
+      } else {
+        n = nx;
+      }
+      funnel16(sh, A[i].x, A[i].y, A[i].z, A[i].w, dpp_from_next(A[i].x, n.x), dpp_from_next(A[i].y, n.y),
+               dpp_from_next(A[i].z, n.z), dpp_from_next(A[i].w, n.w), w[i]);
+    }
+  }
+  if (ST) {  // (validate only: plain payloads, no mask)
+#pragma unroll
+    for (int i = 0; i < N; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) w[i][k] ^= d.mask;
   }
   const bool full = nb_last >= PIECE;
   const int keep = (int)nb_last - lane * 16;
@@ -708,8 +719,8 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const uint32_t pw = dpp_from_prev(w[i][3], carry);
-    uint32_t f0 = utf8_err_word_fast(w[i][0], pw), f1 = utf8_err_word_fast(w[i][1], w[i][0]);
-    uint32_t f2 = utf8_err_word_fast(w[i][2], w[i][1]), f3 = utf8_err_word_fast(w[i][3], w[i][2]);
+    uint32_t f0 = utf8_err_word_raw(w[i][0], pw), f1 = utf8_err_word_raw(w[i][1], w[i][0]);
+    uint32_t f2 = utf8_err_word_raw(w[i][2], w[i][1]), f3 = utf8_err_word_raw(w[i][3], w[i][2]);
     if (i == 0 && lane == 0 && (d.info & PD_FIRST)) f0 &= 0x80000000u;  // bytes 0..2: the fragment carry's
     if (i + 1 == N && !full) {
       f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
@@ -719,7 +730,7 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
       const bool ge3 = N > 1 || !((d.info & PD_FIRST) && lane == 0 && keep < 3);
       if (tail_error(last3(pw, w[i][0], w[i][1], w[i][2], w[i][3], keep), ge3 && (info_last & PD_FIN))) err |= 1u;
     }
-    err |= f0 | f1 | f2 | f3;
+    err |= (f0 | f1 | f2 | f3) & H80;
     if (i + 1 < N) carry = (uint32_t)__builtin_amdgcn_readlane((int)w[i][3], 63);
   }
   return err;

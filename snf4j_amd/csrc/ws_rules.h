@@ -194,28 +194,34 @@ WS_HD uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
 // is flagged one byte late; the frame-level verdict stays exact because the
 // last byte of every validated frame is also tested with utf8_bad_last
 // (k_merge).  Exhaustively checked against the DFA in tests/cpp/utf8_rule_check.cpp.
-WS_HD uint32_t utf8_err_word_fast(uint32_t w, uint32_t p) {
-  const uint32_t w2 = w << 2, w3 = w << 3;
-  const uint32_t hw = w & H80;
-  const uint32_t cw = hw & (w << 1);
-  const uint32_t gw = cw & w2;
-  const uint32_t fw = gw & w3;
-  const uint32_t hp = p & H80;
-  const uint32_t cp = hp & (p << 1);
+// Unmasked form: bit 7 of each byte is the flag, the other bits are don't-care
+// (the kernels OR the words of a lane and mask once).  24 VALU operations a word:
+//   continuation count: w<<1, w<<2, w<<3 and three ANDs give ">= C0/E0/F0" in bit 7,
+//   three byte-aligns move them 1/2/3 bytes on, one OR3 and one XOR with "10xxxxxx";
+//   pair tables: th on previous-byte bits 5..3, tl on its bits 2..0, tb on the
+//   byte's bits 5..4 (80/90/A0/B0 class); a common class bit is an error.
+WS_HD uint32_t utf8_err_word_raw(uint32_t w, uint32_t p) {
+  const uint32_t t1 = w << 1;
+  const uint32_t cw = w & t1;          // bit 7: byte >= C0
+  const uint32_t gw = cw & (w << 2);   // >= E0
+  const uint32_t fw = gw & (w << 3);   // >= F0
+  const uint32_t cont = w & ~t1;       // bit 7: 10xxxxxx
+  const uint32_t tp = p << 1;
+  const uint32_t cp = p & tp;
   const uint32_t gp = cp & (p << 2);
   const uint32_t fp = gp & (p << 3);
   const uint32_t c1 = alignbyte(cw, cp, 3);  // previous byte >= C0
   const uint32_t expect = c1 | alignbyte(gw, gp, 2) | alignbyte(fw, fp, 1);
-  uint32_t err = expect ^ (hw ^ cw);
+  const uint32_t err = expect ^ cont;
   // pair tables: bits A=1 C0/C1, B=2 F5..F7, C=4 E0, D=8 ED, E=16 F0, F=32 F4, G=64 F8..FF
   const uint32_t p1 = alignbyte(w, p, 3);
-  const uint32_t ih = ((p1 >> 4) & 0x03030303u) | ((p1 >> 1) & 0x04040404u);  // C/D/E/F x low-nibble bit 3
-  const uint32_t th = perm_bytes(0x40080000u, 0x32040001u, ih);
+  const uint32_t th = perm_bytes(0x40320804u, 0x00000001u, (p1 >> 3) & 0x07070707u);  // C0-7,C8-F,...,F8-F
   const uint32_t tl = perm_bytes(0x42424A60u, 0x40404155u, p1 & 0x07070707u);
   const uint32_t tb = perm_bytes(0u, 0x6B6B6757u, (w >> 4) & 0x03030303u);  // second byte 80/90/A0/B0 class
-  err |= ((th & tl & tb) + 0x7F7F7F7Fu) & c1;
-  return err & H80;
+  return err | (((th & tl & tb) + 0x7F7F7F7Fu) & c1);
 }
+
+WS_HD uint32_t utf8_err_word_fast(uint32_t w, uint32_t p) { return utf8_err_word_raw(w, p) & H80; }
 
 // Last byte of a frame is a lead the DFA rejects on its own (C0, C1, F5..FF):
 // the pair rule above would flag it only at the next byte.
