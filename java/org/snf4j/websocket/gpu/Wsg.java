@@ -1,0 +1,124 @@
+/*
+ * JNI binding of libwsgpu (include/wsgpu.h) through libwsgpu_jni (jni/wsgpu_jni.c).
+ *
+ * The C ABI carries plain pointers and sizes; here every array argument is a
+ * direct ByteBuffer (pinned host memory from PinnedByteBufferAllocator when it
+ * must cross PCIe at full rate).  Struct layouts (little-endian, see wsgpu.h):
+ *   wsg_frame_desc      16 B: u64 payload_off, u32 payload_len, u8 opcode, u8 flags, u16 status
+ *   wsg_session_result  16 B: u32 n_delivered, u16 error, u16 close_code, i64 detail
+ *   wsg_session_state    8 B
+ *   wsg_encode_frame    24 B: u64 payload_off, u32 payload_len, u8 opcode, u8 flags, u8[2], u8[4] mask, u32
+ *
+ * This repository's image has no JDK: this file is the integration source a
+ * maintainer builds (jni/Makefile); the same ABI is exercised from Python
+ * (snf4j_amd/_lib.py) by the tests and the bench.
+ */
+package org.snf4j.websocket.gpu;
+
+import java.nio.ByteBuffer;
+
+final class Wsg {
+
+	static {
+		System.loadLibrary("wsgpu_jni");
+	}
+
+	private Wsg() {
+	}
+
+	/* wsg_status (wsgpu.h), the reference's exception classes */
+	static final int OK = 0, E_OPCODE = 1, E_RSV = 2, E_MASKING = 3, E_FRAG_CONTROL = 4, E_CONTROL_LEN = 5,
+			E_CLOSE_LEN = 6, E_CONT_OUTSIDE = 7, E_NONCONT_INSIDE = 8, E_MIN_LEN = 9, E_MAX_PAYLOAD = 10,
+			E_TOO_LONG = 11, E_CLOSE_STATUS = 12, E_CLOSE_REASON = 13, E_TEXT_UTF8 = 14, E_NEG_LEN = 15,
+			E_EXT_LEN = 16, E_BATCH = 17;
+
+	static final int DESC_BYTES = 16, RESULT_BYTES = 16, STATE_BYTES = 8, ENCODE_FRAME_BYTES = 24;
+
+	/**
+	 * The InvalidFrameException message the reference builds for a status
+	 * (FrameDecoder.java:200-255, :390-393; FrameUtf8Validator.java:31).
+	 */
+	static String message(int status, long detail, long detail2) {
+		switch (status) {
+		case E_OPCODE: return "Unexpected opcode value (" + detail + ")";
+		case E_RSV: return "Unexpected non-zero RSV bits (" + detail + ")";
+		case E_MASKING: return "Unexpected payload masking";
+		case E_FRAG_CONTROL: return "Fragmented control frame";
+		case E_CONTROL_LEN: return "Invalid payload length (" + detail + ") in control frame";
+		case E_CLOSE_LEN: return "Invalid payload length (" + detail + ") in close frame";
+		case E_CONT_OUTSIDE: return "Continuation frame outside fragmented message";
+		case E_NONCONT_INSIDE: return "Non-continuation frame while inside fragmented massage";
+		case E_MIN_LEN: return "Invalid minimal payload length";
+		case E_MAX_PAYLOAD: return "Invalid maximum payload length";
+		case E_TOO_LONG: return "Maximum frame length (" + detail + ") has been exceeded";
+		case E_CLOSE_STATUS: return "Invalid close frame status code (" + detail + ")";
+		case E_CLOSE_REASON: return "Invalid close frame reason value: bytes are not UTF-8";
+		case E_TEXT_UTF8: return "Invalid text frame payload: bytes are not UTF-8";
+		case E_NEG_LEN: return "Negative payload length (" + detail + ")";
+		case E_EXT_LEN: return "Extended payload length (" + detail + ") > " + detail2;
+		default: return "Malformed batch (status " + status + ")";
+		}
+	}
+
+	/** The CloseFrame status the reference writes for a status (FrameDecoder.java:92-102). */
+	static int closeCode(int status) {
+		return status == E_CLOSE_REASON || status == E_TEXT_UTF8 ? 1007 : 1002;
+	}
+
+	/* ---- context: wsg_open / wsg_reserve / wsg_close / wsg_last_error ---- */
+	static native long open(int device);
+
+	static native int reserve(long ctx, long maxFrames, int maxSessions, long maxWireLen);
+
+	static native void close(long ctx);
+
+	static native String lastError(long ctx);
+
+	/* ---- host framing: FrameDecoder.available (FrameDecoder.java:357-401) ---- */
+	/** wsg_frame_available over b[off, off+len); on -1, err = {status, detail, detail2}. */
+	static native long frameAvailable(byte[] b, int off, int len, long[] err);
+
+	/** The same over a direct buffer (the IBaseDecoder ByteBuffer overload, :290-332). */
+	static native long frameAvailableDirect(ByteBuffer b, int off, int len, long[] err);
+
+	/** wsg_check_header: the header rules of FrameDecoder.decode (:197-256); detail[0] = argument. */
+	static native int checkHeader(boolean clientMode, boolean allowExtensions, long maxPayloadLen,
+			boolean fragmentation, ByteBuffer data, int off, int len, long[] detail);
+
+	/* ---- cross-session batcher: wsg_batcher_* ---- */
+	static native long batcherOpen(long ctx, boolean clientMode, boolean allowExtensions, long maxPayloadLen,
+			boolean validateUtf8, int nSessions);
+
+	static native int batcherClose(long batcher);
+
+	/** wsg_batcher_feed: bytes of session sid (copied). */
+	static native int batcherFeed(long batcher, int sid, ByteBuffer data, int off, int len);
+
+	static native int batcherFeedArray(long batcher, int sid, byte[] data, int off, int len);
+
+	/**
+	 * wsg_batcher_flush: decodes every complete frame fed since the last flush.
+	 * views[0..3] receive session_first, desc, payload and result wrapped as direct
+	 * buffers (valid until the next flush); counts = {n_frames, wire_bytes}.
+	 */
+	static native int batcherFlush(long batcher, ByteBuffer[] views, long[] counts);
+
+	/** wsg_batcher_session_state into st (8 bytes). */
+	static native int batcherSessionState(long batcher, int sid, byte[] st);
+
+	/* ---- encode: wsg_encoded_length / wsg_encode_batch_host ---- */
+	static native long encodedLength(int payloadLen, boolean clientMode);
+
+	static native int encodeBatchHost(long ctx, boolean clientMode, ByteBuffer payload, long payloadLen,
+			ByteBuffer frames, long nFrames, ByteBuffer sessionFirst, int nSessions, ByteBuffer closed,
+			ByteBuffer wireOut, long wireCap, ByteBuffer wireOff);
+
+	/* ---- validator stage alone: wsg_validate_batch_host ---- */
+	static native int validateBatchHost(long ctx, ByteBuffer desc, long nFrames, ByteBuffer sessionFirst,
+			int nSessions, ByteBuffer payload, long payloadLen, ByteBuffer state, ByteBuffer result);
+
+	/* ---- pinned host pool: wsg_host_alloc / wsg_host_release ---- */
+	static native ByteBuffer allocPinned(int capacity);
+
+	static native int releasePinned(ByteBuffer buffer);
+}

@@ -1,0 +1,190 @@
+/* libwsgpu_jni.so: the JNI glue between org.snf4j.websocket.gpu.Wsg (java/) and
+ * the C ABI of libwsgpu.so (include/wsgpu.h).  Every array crosses as a direct
+ * ByteBuffer (GetDirectBufferAddress, no copy); byte[] only for the <= 14 header
+ * bytes available() looks at and for batcher feeds from heap buffers.
+ * Build: jni/Makefile (needs a JDK for jni.h; this repository's image has none). */
+#include <jni.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "../include/wsgpu.h"
+
+#define CTX(x) ((wsg_ctx*)(intptr_t)(x))
+#define BATCHER(x) ((wsg_batcher*)(intptr_t)(x))
+
+static uint8_t* addr(JNIEnv* env, jobject bb) {
+    return bb ? (uint8_t*)(*env)->GetDirectBufferAddress(env, bb) : NULL;
+}
+
+static wsg_decoder_cfg decoder_cfg(jboolean client, jboolean ext, jlong max_payload, jboolean validate) {
+    wsg_decoder_cfg c;
+    memset(&c, 0, sizeof c);
+    c.client_mode = client ? 1 : 0;
+    c.allow_extensions = ext ? 1 : 0;
+    c.max_payload_len = max_payload;
+    c.validate_utf8 = validate ? 1 : 0;
+    return c;
+}
+
+/* ---- context ---- */
+JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_open(JNIEnv* env, jclass c, jint device) {
+    wsg_ctx* ctx = NULL;
+    return wsg_open(device, NULL, &ctx) == WSG_API_OK ? (jlong)(intptr_t)ctx : 0;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_reserve(JNIEnv* env, jclass c, jlong ctx, jlong frames,
+                                                                jint sessions, jlong wire) {
+    return wsg_reserve(CTX(ctx), (uint64_t)frames, (uint32_t)sessions, (uint64_t)wire);
+}
+
+JNIEXPORT void JNICALL Java_org_snf4j_websocket_gpu_Wsg_close(JNIEnv* env, jclass c, jlong ctx) {
+    wsg_close(CTX(ctx));
+}
+
+JNIEXPORT jstring JNICALL Java_org_snf4j_websocket_gpu_Wsg_lastError(JNIEnv* env, jclass c, jlong ctx) {
+    return (*env)->NewStringUTF(env, wsg_last_error(CTX(ctx)));
+}
+
+/* ---- FrameDecoder.available (FrameDecoder.java:357-401) ----
+ * err[0..2] = {status, detail, detail2} when the result is -1; err[3] = the whole
+ * frame's length once its header is complete (the decoder tracks the rest of a
+ * partial frame with it, as FrameDecoder.availablePayload does, :348-355). */
+static jlong available(JNIEnv* env, const uint8_t* hdr, jint len, jlongArray err) {
+    int32_t e = 0;
+    int64_t d1 = 0, d2 = 0;
+    int64_t r = wsg_frame_available(hdr, (uint64_t)len, &e, &d1, &d2);
+    jlong v[4] = {e, d1, d2, 0};
+    if (r > 0) {
+        int32_t e2 = 0;
+        int64_t t1 = 0, t2 = 0;
+        int64_t whole = wsg_frame_available(hdr, (uint64_t)INT32_MAX, &e2, &t1, &t2);
+        v[3] = whole > 0 ? whole : r;
+    }
+    (*env)->SetLongArrayRegion(env, err, 0, 4, v);
+    return (jlong)r;
+}
+
+JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_frameAvailable(JNIEnv* env, jclass c, jbyteArray b, jint off,
+                                                                        jint len, jlongArray err) {
+    uint8_t hdr[16] = {0}; /* only the header is ever read: <= 14 bytes */
+    jint n = len < 14 ? len : 14;
+    (*env)->GetByteArrayRegion(env, b, off, n, (jbyte*)hdr);
+    return available(env, hdr, len, err);
+}
+
+JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_frameAvailableDirect(JNIEnv* env, jclass c, jobject b,
+                                                                              jint off, jint len, jlongArray err) {
+    uint8_t hdr[16] = {0};
+    memcpy(hdr, addr(env, b) + off, len < 14 ? (size_t)len : 14);
+    return available(env, hdr, len, err);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_checkHeader(JNIEnv* env, jclass c, jboolean client,
+                                                                    jboolean ext, jlong max_payload, jboolean frag,
+                                                                    jobject data, jint off, jint len,
+                                                                    jlongArray detail) {
+    wsg_decoder_cfg cfg = decoder_cfg(client, ext, max_payload, 0);
+    int64_t d = 0;
+    int32_t s = wsg_check_header(&cfg, frag ? 1 : 0, addr(env, data) + off, (uint64_t)len, &d);
+    jlong v = d;
+    (*env)->SetLongArrayRegion(env, detail, 0, 1, &v);
+    return s;
+}
+
+/* ---- cross-session batcher ---- */
+JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherOpen(JNIEnv* env, jclass c, jlong ctx, jboolean client,
+                                                                     jboolean ext, jlong max_payload,
+                                                                     jboolean validate, jint sessions) {
+    wsg_decoder_cfg cfg = decoder_cfg(client, ext, max_payload, validate);
+    wsg_batcher* b = NULL;
+    return wsg_batcher_open(CTX(ctx), &cfg, (uint32_t)sessions, &b) == WSG_API_OK ? (jlong)(intptr_t)b : 0;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherClose(JNIEnv* env, jclass c, jlong b) {
+    return wsg_batcher_close(BATCHER(b));
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFeed(JNIEnv* env, jclass c, jlong b, jint sid,
+                                                                    jobject data, jint off, jint len) {
+    return wsg_batcher_feed(BATCHER(b), (uint32_t)sid, addr(env, data) + off, (uint64_t)len);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFeedArray(JNIEnv* env, jclass c, jlong b, jint sid,
+                                                                         jbyteArray data, jint off, jint len) {
+    /* the batcher copies the bytes, so a critical section is enough */
+    jbyte* p = (jbyte*)(*env)->GetPrimitiveArrayCritical(env, data, NULL);
+    if (!p) return WSG_API_ENOMEM;
+    int rc = wsg_batcher_feed(BATCHER(b), (uint32_t)sid, (const uint8_t*)p + off, (uint64_t)len);
+    (*env)->ReleasePrimitiveArrayCritical(env, data, p, JNI_ABORT);
+    return rc;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFlush(JNIEnv* env, jclass c, jlong b,
+                                                                     jobjectArray views, jlongArray counts) {
+    wsg_batch_view v;
+    int rc = wsg_batcher_flush(BATCHER(b), &v);
+    if (rc != WSG_API_OK) return rc;
+    /* payload offsets run to the last descriptor's end; the region is < 2 GiB by contract */
+    uint64_t pay = 0;
+    for (uint64_t k = 0; k < v.n_frames; ++k) {
+        uint64_t e = v.desc[k].payload_off + v.desc[k].payload_len;
+        if (e > pay) pay = e;
+    }
+    (*env)->SetObjectArrayElement(env, views, 0,
+                                  (*env)->NewDirectByteBuffer(env, (void*)v.session_first,
+                                                              (jlong)(v.n_sessions + 1) * sizeof(uint32_t)));
+    (*env)->SetObjectArrayElement(env, views, 1,
+                                  (*env)->NewDirectByteBuffer(env, (void*)v.desc,
+                                                              (jlong)v.n_frames * sizeof(wsg_frame_desc)));
+    (*env)->SetObjectArrayElement(env, views, 2, (*env)->NewDirectByteBuffer(env, (void*)v.payload, (jlong)pay));
+    (*env)->SetObjectArrayElement(env, views, 3,
+                                  (*env)->NewDirectByteBuffer(env, (void*)v.result,
+                                                              (jlong)v.n_sessions * sizeof(wsg_session_result)));
+    jlong n[2] = {(jlong)v.n_frames, (jlong)v.wire_bytes};
+    (*env)->SetLongArrayRegion(env, counts, 0, 2, n);
+    return WSG_API_OK;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherSessionState(JNIEnv* env, jclass c, jlong b, jint sid,
+                                                                            jbyteArray st) {
+    wsg_session_state s;
+    int rc = wsg_batcher_session_state(BATCHER(b), (uint32_t)sid, &s);
+    if (rc == WSG_API_OK) (*env)->SetByteArrayRegion(env, st, 0, sizeof s, (const jbyte*)&s);
+    return rc;
+}
+
+/* ---- encode ---- */
+JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_encodedLength(JNIEnv* env, jclass c, jint len,
+                                                                       jboolean client) {
+    return (jlong)wsg_encoded_length((uint32_t)len, client ? 1 : 0);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encodeBatchHost(
+        JNIEnv* env, jclass c, jlong ctx, jboolean client, jobject payload, jlong payload_len, jobject frames,
+        jlong n_frames, jobject session_first, jint n_sessions, jobject closed, jobject wire_out, jlong wire_cap,
+        jobject wire_off) {
+    return wsg_encode_batch_host(CTX(ctx), client ? 1 : 0, addr(env, payload), (uint64_t)payload_len,
+                                 (const wsg_encode_frame*)addr(env, frames), (uint64_t)n_frames,
+                                 (const uint32_t*)addr(env, session_first), (uint32_t)n_sessions, addr(env, closed),
+                                 addr(env, wire_out), (uint64_t)wire_cap, (uint64_t*)addr(env, wire_off));
+}
+
+/* ---- the validator stage alone ---- */
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_validateBatchHost(
+        JNIEnv* env, jclass c, jlong ctx, jobject desc, jlong n_frames, jobject session_first, jint n_sessions,
+        jobject payload, jlong payload_len, jobject state, jobject result) {
+    return wsg_validate_batch_host(CTX(ctx), (const wsg_frame_desc*)addr(env, desc), (uint64_t)n_frames,
+                                   (const uint32_t*)addr(env, session_first), (uint32_t)n_sessions,
+                                   addr(env, payload), (uint64_t)payload_len, (wsg_session_state*)addr(env, state),
+                                   (wsg_session_result*)addr(env, result));
+}
+
+/* ---- pinned host pool (IByteBufferAllocator.allocate / release) ---- */
+JNIEXPORT jobject JNICALL Java_org_snf4j_websocket_gpu_Wsg_allocPinned(JNIEnv* env, jclass c, jint capacity) {
+    void* p = wsg_host_alloc((uint64_t)capacity);
+    return p ? (*env)->NewDirectByteBuffer(env, p, (jlong)wsg_host_capacity(p)) : NULL;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_releasePinned(JNIEnv* env, jclass c, jobject b) {
+    return wsg_host_release(addr(env, b));
+}
