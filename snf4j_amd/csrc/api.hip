@@ -15,7 +15,7 @@ using namespace ws;
 namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
-                                           "k_merge",   "k_final",    "k_enc_len",  "k_enc_scan",
+                                           "k_seams",   "k_final",    "k_enc_len",  "k_enc_scan",
                                            "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok"};
 
 struct DevBuf {
@@ -60,7 +60,7 @@ struct wsg_ctx {
   bool own_stream = false;
   std::string err;
   // decode workspace
-  DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total, pieces, utf8_err;
+  DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total, pieces, seams, n_seams;
   // encode workspace
   DevBuf esess, elast_close, epieces, epidx;
   // aggregate workspace
@@ -68,6 +68,7 @@ struct wsg_ctx {
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
   DevBuf i_tok, i_lit, i_stat, i_tab;  // inflate pre-decode workspace
   int infl_tokens = 1;               // WSG_INFLATE_TOKENS=0 turns the pre-decode off
+  int fused_scan = 1;                // WSG_FUSED_SCAN=0: always launch k_scan (A/B)
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -160,6 +161,7 @@ int wsg_open(int device, void* stream, wsg_ctx** out) {
   wsg_ctx* c = new wsg_ctx();
   c->device = device;
   if (const char* e = getenv("WSG_INFLATE_TOKENS")) c->infl_tokens = atoi(e) != 0;
+  if (const char* e = getenv("WSG_FUSED_SCAN")) c->fused_scan = atoi(e) != 0;
   if (stream) {
     c->stream = (hipStream_t)stream;
   } else {
@@ -182,7 +184,7 @@ int wsg_close(wsg_ctx* c) {
   drain_timing(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
   DevBuf* bufs[] = {&c->rec,     &c->prev,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
-                    &c->total,   &c->pieces, &c->utf8_err, &c->esess,   &c->elast_close, &c->epieces, &c->epidx, &c->h_wire, &c->h_off,    &c->h_sf,
+                    &c->total,   &c->pieces, &c->seams, &c->n_seams, &c->esess,   &c->elast_close, &c->epieces, &c->epidx, &c->h_wire, &c->h_off,    &c->h_sf,
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
@@ -260,9 +262,10 @@ static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, 
   const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
   // + PIECES_PER_WAVE: k_piecesN reads its descriptors in groups
   HIP_TRY(c, c->pieces.ensure((piece_bound(wire_len, F) + 8) * sizeof(PieceDesc)));
-  // utf8_err / sess_err are kept in their idle state between batches (k_merge and
-  // k_final reset what they read), so no per-batch memset is needed
-  HIP_TRY(c, c->utf8_err.ensure(F * sizeof(uint32_t), 0, c->stream));
+  // n_seams / sess_err are kept in their idle state between batches (k_final resets
+  // what it reads), so no per-batch memset is needed
+  HIP_TRY(c, c->seams.ensure(F * sizeof(uint32_t)));
+  HIP_TRY(c, c->n_seams.ensure(sizeof(uint32_t), 0, c->stream));
   HIP_TRY(c, c->rec.ensure(F * sizeof(FrameRec)));
   HIP_TRY(c, c->prev.ensure(3 * F * sizeof(int32_t)));
   HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));
@@ -331,17 +334,19 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
   a.pieces = (PieceDesc*)c->pieces.p;
-  a.utf8_err = (uint32_t*)c->utf8_err.p;
+  a.seams = (uint32_t*)c->seams.p;
+  a.n_seams = (uint32_t*)c->n_seams.p;
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
   a.n_pieces = piece_bound(wire_len, n_frames);
   a.validator_only = 0;
   a.in_desc = nullptr;
+  a.fused_scan = a.nblk <= FUSED_SCAN_MAX_BLOCKS && c->fused_scan;
   if (n_frames) {
     timed(c, K_PARSE, [&] { launch_parse(a, c->stream); });
-    timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
+    if (!a.fused_scan) timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
     timed(c, K_LINK, [&] { launch_link(a, c->stream); });
     timed(c, K_UNMASK, [&] { launch_pieces(a, c->stream, piece_bound(wire_len, n_frames)); });
-    timed(c, K_MERGE, [&] { launch_merge(a, c->stream); });
+    timed(c, K_SEAMS, [&] { launch_seams(a, c->stream); });
   }
   timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());
@@ -382,17 +387,19 @@ int wsg_validate_batch_device(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
   a.pieces = (PieceDesc*)c->pieces.p;
-  a.utf8_err = (uint32_t*)c->utf8_err.p;
+  a.seams = (uint32_t*)c->seams.p;
+  a.n_seams = (uint32_t*)c->n_seams.p;
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
   a.n_pieces = piece_bound(payload_len, n_frames);
   a.validator_only = 1;
   a.in_desc = desc;
+  a.fused_scan = a.nblk <= FUSED_SCAN_MAX_BLOCKS && c->fused_scan;
   if (n_frames) {
     timed(c, K_PARSE, [&] { launch_vparse(a, c->stream); });
-    timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
+    if (!a.fused_scan) timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
     timed(c, K_LINK, [&] { launch_link(a, c->stream); });
     timed(c, K_UNMASK, [&] { launch_vpieces(a, c->stream, a.n_pieces); });
-    timed(c, K_MERGE, [&] { launch_merge(a, c->stream); });
+    timed(c, K_SEAMS, [&] { launch_seams(a, c->stream); });
   }
   timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());

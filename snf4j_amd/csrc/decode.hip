@@ -8,14 +8,18 @@
 //             start / nonempty frame indices = max-scans).
 //   k_link    thread per frame: payload slot offset, the fragmentation rule
 //             (:229-236) from the previous data frame's FIN, text-message
-//             membership for the validator (FrameUtf8Validator.java:59-70).
+//             membership for the validator (FrameUtf8Validator.java:59-70), the
+//             frame's wsg_frame_desc with its status in the reference's check order,
+//             the piece descriptors.  (Small grids reduce the block aggregates
+//             themselves: no k_scan launch.)
 //   k_piecesN one wave per 2 KiB of payload output: coalesced 16-B loads, 4-byte
 //             XOR unmask (:268-273), aligned 16-B stores into the frame slots,
 //             per-lane SWAR UTF-8 rule with the 3-byte carry taken from the
 //             neighbour lane (DPP) and the verdict folded by wavefront ballot.
-//   k_merge   thread per frame: status in the reference's check order, the
-//             fragment-seam UTF-8 bytes against the message carry, wsg_frame_desc,
-//             the first failing frame per session (atomicMin).
+//             A UTF-8 error sets its frame's status and the session's first
+//             failing frame (atomicMin) directly.
+//   k_seams   the validated continuation frames k_link listed: their first bytes
+//             against the message carry (none in a batch of unfragmented messages).
 //   k_final   thread per session: wsg_session_result + carry-out state.
 #include "wsgpu_internal.h"
 #include "wsgpu_scan.h"
@@ -248,17 +252,33 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   }
   Agg tot;
   Agg ex = block_excl_scan(v, &tot);
-  uint32_t extra = 0;
-  if (live) {
-    Agg bp;
+  // the aggregate of every frame before this block: k_scan's exclusive scan, or (small
+  // grids, no k_scan launch) this block's own reduction of k_parse's block aggregates
+  Agg bp;
+  if (a.fused_scan) {
+    Agg t = AGG_ID;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += BLOCK) {
+      Agg e;
+      e.sum = a.blk_sum[b];
+      e.m0 = a.blk_max[b];
+      e.m1 = a.blk_max[a.nblk + b];
+      e.m2 = a.blk_max[2 * a.nblk + b];
+      t = agg_op(t, e);
+    }
+    block_excl_scan(t, &bp);
+    if (blockIdx.x + 1 == a.nblk && threadIdx.x == 0) *a.total = bp.sum + tot.sum;
+  } else {
     bp.sum = a.blk_sum[blockIdx.x];
     bp.m0 = a.blk_max[blockIdx.x];
     bp.m1 = a.blk_max[a.nblk + blockIdx.x];
     bp.m2 = a.blk_max[2 * a.nblk + blockIdx.x];
+  }
+  uint32_t extra = 0;
+  if (live) {
     ex = agg_op(bp, ex);
     const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
     // read only for continuation frames, the frames of a message still open, and a
-    // session's last frame when it is not a FIN message start (k_merge, k_final):
+    // session's last frame when it is not a FIN message start (k_seams, k_final):
     // a complete one-frame message (the common case) needs none
     if (!(code_is_start(r.code) && (r.code & CODE_FIN))) {
       a.prev[k] = jd;
@@ -269,18 +289,37 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
     const int32_t sf = (int32_t)a.session_first[s];
     const wsg_session_state st = a.state[s];
     const uint32_t op = code_op(r.code);
+    uint32_t frag_err = 0;
+    bool text = false;
     if (!code_pre(r.code)) {
       // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
       const bool frag = jd >= sf ? !(ex.m0 & 1) : (st.fragmentation != 0);
-      if (!a.validator_only) extra |= rules_frag(op, frag) << CODE_FRAG_SHIFT;
+      if (!a.validator_only) frag_err = rules_frag(op, frag);
       if (a.validate) {
-        bool text = op == WSG_OP_TEXT;
+        text = op == WSG_OP_TEXT;
         if (op == WSG_OP_CONTINUATION) text = jm >= sf ? (ex.m1 & 1) != 0 : (st.text_open != 0);
-        if (text) extra |= CODE_VALIDATE;
       }
     }
+    // the frame's status in the reference's check order (header rules, fragmentation,
+    // lengths / close); the validator's verdict (k_pieces, k_seams) only on frames
+    // that pass all of them, so a failed frame is never validated
+    uint32_t status = code_pre(r.code) ? code_pre(r.code) : (frag_err ? frag_err : code_post(r.code));
+    if (!status && ex.sum + r.len > a.n_pieces * PIECE) status = WSG_E_BATCH;  // slots beyond the piece grid
+    extra = (frag_err << CODE_FRAG_SHIFT) | ((text && !status) ? CODE_VALIDATE : 0u);
     a.rec[k].out_off = ex.sum;
-    a.rec[k].code = r.code | extra;  // (wsg_frame_desc is written whole by k_merge)
+    a.rec[k].code = r.code | extra;
+    wsg_frame_desc d;
+    d.payload_off = ex.sum;
+    d.payload_len = r.len;
+    d.opcode = (uint8_t)op;
+    d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
+                        ((r.code & CODE_MASKED) ? 1u : 0u));
+    d.status = (uint16_t)status;
+    a.desc[k] = d;
+    if (status) atomicMin((unsigned long long*)&a.sess_err[s], (unsigned long long)k);
+    // a validated continuation: its first bytes are checked against the message carry
+    // by k_seams (every other validated frame is checked whole by k_pieces)
+    if ((extra & CODE_VALIDATE) && op == WSG_OP_CONTINUATION) a.seams[atomicAdd(a.n_seams, 1u)] = (uint32_t)k;
   }
   // Descriptors of the pieces whose first output byte falls in a frame's slot,
   // written cooperatively: the wave's pieces are contiguous, lane i writes the
@@ -299,10 +338,10 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
   const uint32_t T = (uint32_t)__shfl((int)cum, 63, 64);
   cum -= cnt;  // exclusive
   if (!T) return;
-  const uint64_t total = *a.total;
   // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31
   const uint32_t fk = (uint32_t)k | ((extra & CODE_VALIDATE) ? 0x80000000u : 0u) |
                      ((live && (r.code & CODE_FIN)) ? 0x40000000u : 0u);
+  const bool cont = live && code_op(r.code) == WSG_OP_CONTINUATION;
   for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
     int o = 0;
 #pragma unroll
@@ -317,20 +356,23 @@ __global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
     const uint32_t o_len = (uint32_t)__shfl((int)(live ? r.len : 0u), o, 64);
     const uint32_t o_mask = (uint32_t)__shfl((int)(live ? r.mask : 0u), o, 64);
     const uint32_t o_fk = (uint32_t)__shfl((int)fk, o, 64);
+    const bool o_cont = __shfl((int)cont, o, 64) != 0;
     if (t >= T) continue;
     const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
-    if (pc >= a.n_pieces) continue;  // beyond the grid: k_merge fails the frame (WSG_E_BATCH)
+    if (pc >= a.n_pieces) continue;  // beyond the grid: the frame failed with WSG_E_BATCH above
     const uint64_t ps = pc * PIECE;
     const uint64_t o_end = o_out + ((o_len + 15u) & ~15u);
     const uint32_t j0 = (uint32_t)(ps - o_out);
     const uint32_t left = o_len - j0;
-    const bool single = o_end >= ps + PIECE || o_end == total;
+    // runs past its frame's slot: other frames' bytes follow, unless it is the batch's
+    // last frame (a slot ending the payload region)
+    const bool single = o_end >= ps + PIECE || (uint64_t)(o_fk & 0x3fffffffu) + 1 == a.n_frames;
     PieceDesc d;
     d.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) |
              ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI) |
              (left <= PIECE ? PD_LAST : 0ull) | ((o_fk & 0x40000000u) ? PD_FIN : 0ull);
     d.mask = o_mask;
-    d.frame = o_fk & 0x3fffffffu;
+    d.frame = (o_fk & PDF_INDEX) | (o_cont ? PDF_CONT : 0u);
     a.pieces[pc] = d;
   }
 }
@@ -424,6 +466,14 @@ __device__ __forceinline__ uint32_t last3(uint32_t pw, uint32_t w0, uint32_t w1,
   return alignbyte(hi, lo, (uint32_t)t & 3u) & 0xffffffu;
 }
 
+// A piece found invalid UTF-8 in frame k (which passed every other rule: k_link
+// validates no failed frame): FrameUtf8Validator's 1007 (FrameUtf8Validator.java:
+// 54-57, 78-96) as the frame's status, and the session's first failing frame.
+__device__ __forceinline__ void report_utf8(const DecodeArgs& a, uint32_t k) {
+  a.desc[k].status = (uint16_t)WSG_E_TEXT_UTF8;
+  atomicMin((unsigned long long*)&a.sess_err[a.rec[k].sess], (unsigned long long)k);
+}
+
 // 4 source bytes ending right before wire offset `pos`, unmasked (payload phase 0)
 __device__ __forceinline__ uint32_t prev_word(const DecodeArgs& a, uint64_t pos, uint32_t mask) {
   uint32_t w = 0;
@@ -498,14 +548,17 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
   const uint32_t pw = dpp_from_prev(w[3], first_prev);
   uint32_t f0 = utf8_err_word_raw(w[0], pw), f1 = utf8_err_word_raw(w[1], w[0]);
   uint32_t f2 = utf8_err_word_raw(w[2], w[1]), f3 = utf8_err_word_raw(w[3], w[2]);
-  if (lane == 0 && (d.info & PD_FIRST)) f0 &= 0x80000000u;  // bytes 0..2: checked against the fragment carry
+  // a continuation's bytes 0..2 are checked against the message carry (k_seams); a
+  // message start has no carry, and the zero word before it is exact
+  const bool cont_head = lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT);
+  if (cont_head) f0 &= 0x80000000u;
   if (!full) {
     f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
   }
   uint32_t te = 0;
   if ((d.info & PD_LAST) && keep >= 1 && keep <= 16) {
-    const bool ge3 = !((d.info & PD_FIRST) && lane == 0 && keep < 3);  // frame length >= 3
-    te = tail_error(last3(pw, w[0], w[1], w[2], w[3], keep), ge3 && (d.info & PD_FIN)) ? 1u : 0u;
+    const bool whole = !(cont_head && keep < 3);  // (a short continuation ends on the carry: k_seams)
+    te = tail_error(last3(pw, w[0], w[1], w[2], w[3], keep), whole && (d.info & PD_FIN)) ? 1u : 0u;
   }
   return ((f0 | f1 | f2 | f3) & H80) | te;
 }
@@ -524,14 +577,15 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
   const uint64_t pend = pstart + PIECE < total ? pstart + PIECE : total;
   const uint64_t my = pstart + (uint64_t)lane * 16u;
   const bool live = my < pend;
-  uint32_t lk = d.frame;  // frame owning this lane's 16 output bytes
+  const uint32_t fr0 = d.frame & PDF_INDEX;
+  uint32_t lk = fr0;  // frame owning this lane's 16 output bytes
   FrameRec lr;
   {
     // lane-parallel lookup: lane l takes record d.frame + l and the 16-B chunk of the
     // piece where that frame's slot starts (0 for the piece's first frame, 64 past
     // the piece end); the chunks are non-decreasing over the lanes, so the owner of
     // chunk i is the last lane whose chunk is <= i: a 6-step search over shuffles
-    const uint64_t fl = (uint64_t)d.frame + (uint64_t)lane;
+    const uint64_t fl = (uint64_t)fr0 + (uint64_t)lane;
     const bool have = fl < a.n_frames;
     const uint64_t fs = have ? a.rec[fl].out_off : ~0ull;
     const uint64_t fslot = have ? (uint64_t)((a.rec[fl].len + 15u) & ~15u) : 0ull;
@@ -541,10 +595,10 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
 #pragma unroll
       for (int step = 32; step >= 1; step >>= 1)
         if (__shfl(c, pos + step, 64) <= lane) pos += step;
-      lk = d.frame + (uint32_t)pos;
+      lk = fr0 + (uint32_t)pos;
       lr = a.rec[lk];  // just loaded by lane pos: a cache hit
     } else {  // more than 64 frames (empty ones) in the piece: walk the records
-      uint32_t kk = d.frame;
+      uint32_t kk = fr0;
       FrameRec rr = a.rec[kk];
       lr = rr;
       uint64_t send = rr.out_off + ((rr.len + 15u) & ~15u);
@@ -586,13 +640,15 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
     if (j == 0) pw = 0u;
     else if (prev_k != lk) pw = prev_word(a, lr.src + j, lr.mask);  // lane 0 inside a frame
     if (lval) {
+      const bool cont = code_op(lr.code) == WSG_OP_CONTINUATION;
       uint32_t e0 = utf8_err_word_raw(w[0], pw), e1 = utf8_err_word_raw(w[1], w[0]);
       uint32_t e2 = utf8_err_word_raw(w[2], w[1]), e3 = utf8_err_word_raw(w[3], w[2]);
-      if (j == 0) e0 &= 0x80000000u;
+      if (j == 0 && cont) e0 &= 0x80000000u;  // a continuation's head: k_seams
       e0 &= keep_flags(keep); e1 &= keep_flags(keep - 4); e2 &= keep_flags(keep - 8); e3 &= keep_flags(keep - 12);
       const bool te = keep >= 1 && keep <= 16 &&
-                      tail_error(last3(pw, w[0], w[1], w[2], w[3], keep), j + keep >= 3 && (lr.code & CODE_FIN));
-      if (e0 | e1 | e2 | e3 | (te ? 1u : 0u)) atomicOr(&a.utf8_err[lk], 1u);
+                      tail_error(last3(pw, w[0], w[1], w[2], w[3], keep),
+                                 (j + keep >= 3 || !cont) && (lr.code & CODE_FIN));
+      if (e0 | e1 | e2 | e3 | (te ? 1u : 0u)) report_utf8(a, lk);
     }
   }
 }
@@ -611,7 +667,7 @@ __global__ __launch_bounds__(64 * WPB) void k_pieces(DecodeArgs a) {
   if (pstart >= total) return;
   if (!(d.info & PD_MULTI)) {
     const uint32_t err = piece_fast<NT>(a, d, pstart, lane);
-    if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d.frame], 1u);
+    if (__any(err != 0) && lane == 0) report_utf8(a, d.frame & PDF_INDEX);
     return;
   }
   piece_general<NT>(a, d, pstart, total, lane);
@@ -721,13 +777,14 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
     const uint32_t pw = dpp_from_prev(w[i][3], carry);
     uint32_t f0 = utf8_err_word_raw(w[i][0], pw), f1 = utf8_err_word_raw(w[i][1], w[i][0]);
     uint32_t f2 = utf8_err_word_raw(w[i][2], w[i][1]), f3 = utf8_err_word_raw(w[i][3], w[i][2]);
-    if (i == 0 && lane == 0 && (d.info & PD_FIRST)) f0 &= 0x80000000u;  // bytes 0..2: the fragment carry's
+    const bool cont_head = i == 0 && lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT);
+    if (cont_head) f0 &= 0x80000000u;  // a continuation's bytes 0..2: k_seams
     if (i + 1 == N && !full) {
       f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
     }
     if (i + 1 == N && (info_last & PD_LAST) && keep >= 1 && keep <= 16) {
       // (a frame of N > 1 pieces has >= 3 bytes; with N == 1 the piece may start it)
-      const bool ge3 = N > 1 || !((d.info & PD_FIRST) && lane == 0 && keep < 3);
+      const bool ge3 = N > 1 || !(lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT) && keep < 3);
       if (tail_error(last3(pw, w[i][0], w[i][1], w[i][2], w[i][3], keep), ge3 && (info_last & PD_FIN))) err |= 1u;
     }
     err |= (f0 | f1 | f2 | f3) & H80;
@@ -755,7 +812,7 @@ __global__ __launch_bounds__(64) void k_piecesN(DecodeArgs a) {
   for (int i = 0; i < N; ++i) fast = fast && !(d[i].info & PD_MULTI);
   if (fast) {
     const uint32_t err = piece_fastN<NT, N>(a, d[0], d[N - 1].info, pstart, lane);
-    if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d[0].frame], 1u);
+    if (__any(err != 0) && lane == 0) report_utf8(a, d[0].frame & PDF_INDEX);
     return;
   }
 #pragma unroll
@@ -764,36 +821,25 @@ __global__ __launch_bounds__(64) void k_piecesN(DecodeArgs a) {
     if (ps >= total) return;
     if (!(d[i].info & PD_MULTI)) {
       const uint32_t err = piece_fast<NT>(a, d[i], ps, lane);
-      if (__any(err != 0) && lane == 0) atomicOr(&a.utf8_err[d[i].frame], 1u);
+      if (__any(err != 0) && lane == 0) report_utf8(a, d[i].frame & PDF_INDEX);
     } else {
       piece_general<NT>(a, d[i], ps, total, lane);
     }
   }
 }
 
-// ------------------------------------------------------------------ k_merge
-// Per frame: the first error in the reference's check order (header rules,
-// fragmentation, lengths/close, then the validator), and the first failing
-// frame per session.
-__global__ __launch_bounds__(256) void k_merge(DecodeArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
-  if (k >= a.n_frames) return;
-  const FrameRec r = a.rec[k];
-  const uint32_t pre = code_pre(r.code), post = code_post(r.code), frag = code_frag(r.code);
-  uint32_t status = pre ? pre : (frag ? frag : post);
-  if (!status && r.out_off + r.len > a.n_pieces * PIECE) status = WSG_E_BATCH;  // slots beyond the piece grid
-  const uint32_t ue = a.utf8_err[k];
-  if (ue) a.utf8_err[k] = 0u;  // back to the idle state for the next batch
-  if (!status && (r.code & CODE_VALIDATE) && (ue || edge_utf8_error(a, k, r))) status = WSG_E_TEXT_UTF8;
-  wsg_frame_desc d;
-  d.payload_off = r.out_off;
-  d.payload_len = r.len;
-  d.opcode = (uint8_t)code_op(r.code);
-  d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
-                      ((r.code & CODE_MASKED) ? 1u : 0u));
-  d.status = (uint16_t)status;
-  a.desc[k] = d;
-  if (status) atomicMin((unsigned long long*)&a.sess_err[r.sess], (unsigned long long)k);
+// ------------------------------------------------------------------ k_seams
+// The validated continuation frames k_link listed: their first (<= 3) bytes against
+// the message carry, and the end of a FIN message shorter than 3 bytes in this
+// frame (FrameUtf8Validator.java:78-96 at the fragment seams).  Every other
+// verdict is already in desc (k_link: header / fragmentation / length rules;
+// k_pieces: UTF-8 inside frames).  A batch of unfragmented messages lists none.
+__global__ __launch_bounds__(256) void k_seams(DecodeArgs a) {
+  const uint32_t n = *a.n_seams;
+  for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u) {
+    const uint32_t k = a.seams[i];
+    if (a.desc[k].status == 0 && edge_utf8_error(a, k, a.rec[k])) report_utf8(a, k);
+  }
 }
 
 // ------------------------------------------------------------------ k_final
@@ -818,6 +864,7 @@ __device__ int64_t error_detail(const DecodeArgs& a, uint64_t k, uint32_t err) {
 
 __global__ __launch_bounds__(256) void k_final(DecodeArgs a) {
   const uint32_t s = blockIdx.x * 256u + threadIdx.x;
+  if (s == 0) *a.n_seams = 0u;  // (k_seams has read it) back to the idle state for the next batch
   if (s >= a.n_sessions) return;
   wsg_session_state st = a.state[s];
   wsg_session_result res = {0u, 0u, 0u, 0};
@@ -903,8 +950,9 @@ void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound)
   hipLaunchKernelGGL((k_piecesN<5, 1, VPIECES_PER_WAVE>),
                      dim3((uint32_t)((n_pieces_bound + VPIECES_PER_WAVE - 1) / VPIECES_PER_WAVE)), dim3(64), 0, s, a);
 }
-void launch_merge(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_merge, dim3((uint32_t)((a.n_frames + 255) / 256)), dim3(256), 0, s, a);
+void launch_seams(const DecodeArgs& a, hipStream_t s) {
+  const uint64_t nb = (a.n_frames + 255) / 256;
+  hipLaunchKernelGGL(k_seams, dim3((uint32_t)(nb < 512 ? nb : 512)), dim3(256), 0, s, a);
 }
 void launch_final(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);

@@ -193,7 +193,7 @@ WS_HD uint32_t perm_bytes(uint32_t hi, uint32_t lo, uint32_t sel) {
 // flagged on the SECOND byte of the pair.  So an invalid lead (C0, C1, F5..FF)
 // is flagged one byte late; the frame-level verdict stays exact because the
 // last byte of every validated frame is also tested with utf8_bad_last
-// (k_merge).  Exhaustively checked against the DFA in tests/cpp/utf8_rule_check.cpp.
+// (k_pieces).  Exhaustively checked against the DFA in tests/cpp/utf8_rule_check.cpp.
 // Unmasked form: bit 7 of each byte is the flag, the other bits are don't-care
 // (the kernels OR the words of a lane and mask once).  24 VALU operations a word:
 //   continuation count: w<<1, w<<2, w<<3 and three ANDs give ">= C0/E0/F0" in bit 7,

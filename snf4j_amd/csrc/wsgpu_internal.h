@@ -56,8 +56,10 @@ struct PieceDesc {
                   // the piece (1..1024); 59: validate; 60: piece starts its frame; 61: spans several slots;
                   // 62: piece holds its frame's last payload byte; 63: the frame is FIN
   uint32_t mask;  // frame mask key (payload phase 0 at the piece start)
-  uint32_t frame; // frame index
+  uint32_t frame; // frame index | PDF_CONT
 };
+constexpr uint32_t PDF_INDEX = 0x3fffffffu;  // PieceDesc.frame: the frame index
+constexpr uint32_t PDF_CONT = 0x80000000u;   // the frame is a continuation (its head is k_seams')
 constexpr uint64_t PD_SRC_MASK = (1ull << 48) - 1;
 constexpr uint32_t PD_NB_SHIFT = 48;
 constexpr uint64_t PD_VALIDATE = 1ull << 59;
@@ -97,10 +99,15 @@ struct DecodeArgs {
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
   uint64_t* total;     // [1] total payload slot bytes
   struct PieceDesc* pieces;  // [piece_bound]: per-piece work descriptor (k_link)
-  uint32_t* utf8_err;  // [n_frames]: a piece found a UTF-8 error inside the frame (k_pieces)
+  uint32_t* seams;     // [n_frames]: validated continuation frames (k_link) for k_seams
+  uint32_t* n_seams;   // [1] entries in seams (k_final returns it to 0)
   uint64_t n_pieces;   // pieces the grid covers (piece_bound): slots beyond are a malformed batch
   uint32_t nblk;
+  int32_t fused_scan;  // k_link reduces the block aggregates itself (nblk <= FUSED_SCAN_MAX_BLOCKS)
 };
+
+// grids up to this many parse/link blocks skip the k_scan launch
+constexpr uint32_t FUSED_SCAN_MAX_BLOCKS = 4096;
 
 struct EncodeArgs {
   int32_t client_mode;
@@ -194,7 +201,7 @@ struct InflTokStat {
 
 // kernel ids for timing
 enum KernelId {
-  K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_MERGE, K_FINAL,
+  K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_SEAMS, K_FINAL,
   K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_COUNT
 };
 
@@ -205,7 +212,7 @@ void launch_link(const DecodeArgs& a, hipStream_t s);
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
 void launch_vparse(const DecodeArgs& a, hipStream_t s);
 void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
-void launch_merge(const DecodeArgs& a, hipStream_t s);
+void launch_seams(const DecodeArgs& a, hipStream_t s);
 void launch_final(const DecodeArgs& a, hipStream_t s);
 
 void launch_enc_len(const EncodeArgs& a, hipStream_t s);

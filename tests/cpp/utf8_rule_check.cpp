@@ -36,8 +36,9 @@ static int64_t rule_first_words(const uint8_t* s, int n) {
   return -1;
 }
 
-// the kernels' fast rule: word form over the string, head (first 3 bytes) by the
-// exact rule as k_merge does, plus the last-byte test; returns the first flag.
+// the kernels' fast rule on a continuation frame: word form over the string, head
+// (first 3 bytes) by the exact rule as k_seams does, plus the last-byte test;
+// returns the first flag.
 static int64_t fast_first(const uint8_t* s, int n) {
   std::vector<uint8_t> b(8 + ((n + 3) & ~3) + 4, 0);
   for (int i = 0; i < n; ++i) b[8 + i] = s[i];
@@ -59,16 +60,36 @@ done:
   return first;
 }
 
+// the fast rule on a message start (a TEXT frame, k_pieces alone): word form over
+// the whole string with a zero word before it, plus the last-byte test.
+static int64_t fast_first_start(const uint8_t* s, int n) {
+  std::vector<uint8_t> b(8 + ((n + 3) & ~3) + 4, 0);
+  for (int i = 0; i < n; ++i) b[8 + i] = s[i];
+  int64_t first = -1;
+  for (int wi = 0; wi * 4 < n && first < 0; ++wi) {
+    uint32_t w, p;
+    memcpy(&w, &b[8 + 4 * wi], 4);
+    memcpy(&p, &b[4 + 4 * wi], 4);
+    uint32_t e = ws::utf8_err_word_fast(w, p);
+    for (int j = 0; j < 4 && 4 * wi + j < n; ++j)
+      if (e & (0x80u << (8 * j))) { first = 4 * wi + j; break; }
+  }
+  if (n > 0 && ws::utf8_bad_last(s[n - 1]) && (first < 0 || first > n - 1)) first = n - 1;
+  return first;
+}
+
 static long fails = 0;
 static void check(const uint8_t* s, int n) {
   int64_t dfa = or_utf8_reject_pos(0, s, n);
-  int64_t r1 = rule_first(s, n), r2 = rule_first_words(s, n), r3 = fast_first(s, n);
+  int64_t r1 = rule_first(s, n), r2 = rule_first_words(s, n), r3 = fast_first(s, n),
+          r4 = fast_first_start(s, n);
   bool bad = dfa != r1 || dfa != r2;
   // fast rule: same verdict; first flag at the reject byte, or one byte later when
   // the reject byte is a lead rejected on its own (C0, C1, F5..FF)
-  if (dfa < 0) bad |= r3 >= 0;
-  else bad |= !(r3 == dfa || (r3 == dfa + 1 && ws::utf8_bad_last(s[dfa])) ||
-                (r3 == n - 1 && dfa == n - 1));
+  for (int64_t r : {r3, r4}) {
+    if (dfa < 0) bad |= r >= 0;
+    else bad |= !(r == dfa || (r == dfa + 1 && ws::utf8_bad_last(s[dfa])) || (r == n - 1 && dfa == n - 1));
+  }
   if (!bad && dfa < 0) {
     or_utf8_ctx c = {0, 0};
     or_utf8_validate(&c, s, n);
@@ -76,8 +97,8 @@ static void check(const uint8_t* s, int n) {
     bad = (c.state != 0) != ws::utf8_incomplete(l3, l2, l1);
   }
   if (bad && fails++ < 10) {
-    printf("MISMATCH dfa=%lld rule=%lld words=%lld fast=%lld :", (long long)dfa, (long long)r1, (long long)r2,
-           (long long)r3);
+    printf("MISMATCH dfa=%lld rule=%lld words=%lld fast=%lld start=%lld :", (long long)dfa, (long long)r1,
+           (long long)r2, (long long)r3, (long long)r4);
     for (int i = 0; i < n; ++i) printf(" %02x", s[i]);
     printf("\n");
   }

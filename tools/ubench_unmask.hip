@@ -56,11 +56,11 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&a.blk_sum, a.nblk * 8)); CK(hipMalloc(&a.blk_max, 3 * a.nblk * 4));
   CK(hipMalloc(&a.sess_err, S * 8)); CK(hipMalloc(&a.total, 8));
   const uint64_t npb = ws::piece_bound(wire_len, F);
-  CK(hipMalloc(&a.pieces, (npb + 8) * sizeof(ws::PieceDesc))); CK(hipMalloc(&a.utf8_err, F * 4));
+  CK(hipMalloc(&a.pieces, (npb + 8) * sizeof(ws::PieceDesc))); CK(hipMalloc(&a.seams, F * 4)); CK(hipMalloc(&a.n_seams, 4));
   CK(hipMemsetAsync(a.sess_err, 0xff, S * 8, st));
-  CK(hipMemsetAsync(a.utf8_err, 0, F * 4, st));
+  CK(hipMemsetAsync(a.n_seams, 0, 4, st));
   ws::launch_parse(a, st); ws::launch_scan(a, st); ws::launch_link(a, st);
-  ws::launch_pieces(a, st, npb); ws::launch_merge(a, st); ws::launch_final(a, st);
+  ws::launch_pieces(a, st, npb); ws::launch_seams(a, st); ws::launch_final(a, st);
   CK(hipStreamSynchronize(st));
   std::vector<uint8_t> res(S * 16);
   CK(hipMemcpy(res.data(), a.result, S * 16, hipMemcpyDeviceToHost));
@@ -76,7 +76,7 @@ int main(int argc, char** argv) {
   std::vector<V> vs = {
       {"copy16 g=8192", 0, 8192}, {"pieces nt W1", 13, 0}, {"pieces nt W1 xcd", 14, 0},
       {"piecesN2 xcd", 18, 0}, {"piecesN4 xcd", 19, 0}, {"piecesN3 xcd", 24, 0}, {"piecesN4", 25, 0},
-      {"parse", 20, 0}, {"scan", 23, 0}, {"link", 21, 0}, {"merge", 22, 0},  // pipeline order
+      {"parse", 20, 0}, {"scan", 23, 0}, {"link", 21, 0}, {"seams", 22, 0},  // pipeline order
   };
   std::vector<double> best(vs.size(), 1e30), sum(vs.size(), 0);
   const int rounds = 8;
@@ -109,7 +109,7 @@ int main(int argc, char** argv) {
       } else if (vs[i].kind == 21) {
         ws::launch_link(a, st);
       } else if (vs[i].kind == 22) {
-        ws::launch_merge(a, st);
+        ws::launch_seams(a, st);
       } else if (vs[i].kind == 23) {
         ws::launch_scan(a, st);
       }
