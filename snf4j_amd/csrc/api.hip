@@ -262,10 +262,10 @@ static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, 
   const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
   // + PIECES_PER_WAVE: k_piecesN reads its descriptors in groups
   HIP_TRY(c, c->pieces.ensure((piece_bound(wire_len, F) + 8) * sizeof(PieceDesc)));
-  // n_seams / sess_err are kept in their idle state between batches (k_final resets
-  // what it reads), so no per-batch memset is needed
-  HIP_TRY(c, c->seams.ensure(F * sizeof(uint32_t)));
-  HIP_TRY(c, c->n_seams.ensure(sizeof(uint32_t), 0, c->stream));
+  // sess_err is kept in its idle state between batches (k_final resets what it
+  // reads), so no per-batch memset is needed
+  HIP_TRY(c, c->seams.ensure(nblk * BLOCK * sizeof(uint32_t)));
+  HIP_TRY(c, c->n_seams.ensure(nblk * sizeof(uint32_t)));
   HIP_TRY(c, c->rec.ensure(F * sizeof(FrameRec)));
   HIP_TRY(c, c->prev.ensure(3 * F * sizeof(int32_t)));
   HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));

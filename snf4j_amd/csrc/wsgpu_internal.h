@@ -99,8 +99,8 @@ struct DecodeArgs {
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
   uint64_t* total;     // [1] total payload slot bytes
   struct PieceDesc* pieces;  // [piece_bound]: per-piece work descriptor (k_link)
-  uint32_t* seams;     // [n_frames]: validated continuation frames (k_link) for k_seams
-  uint32_t* n_seams;   // [1] entries in seams (k_final returns it to 0)
+  uint32_t* seams;     // [nblk * BLOCK]: validated continuation frames, k_link block b's at b * BLOCK
+  uint32_t* n_seams;   // [nblk]: entries of k_link block b
   uint64_t n_pieces;   // pieces the grid covers (piece_bound): slots beyond are a malformed batch
   uint32_t nblk;
   int32_t fused_scan;  // k_link reduces the block aggregates itself (nblk <= FUSED_SCAN_MAX_BLOCKS)

@@ -56,9 +56,8 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&a.blk_sum, a.nblk * 8)); CK(hipMalloc(&a.blk_max, 3 * a.nblk * 4));
   CK(hipMalloc(&a.sess_err, S * 8)); CK(hipMalloc(&a.total, 8));
   const uint64_t npb = ws::piece_bound(wire_len, F);
-  CK(hipMalloc(&a.pieces, (npb + 8) * sizeof(ws::PieceDesc))); CK(hipMalloc(&a.seams, F * 4)); CK(hipMalloc(&a.n_seams, 4));
+  CK(hipMalloc(&a.pieces, (npb + 8) * sizeof(ws::PieceDesc))); CK(hipMalloc(&a.seams, (uint64_t)a.nblk * 256 * 4)); CK(hipMalloc(&a.n_seams, a.nblk * 4));
   CK(hipMemsetAsync(a.sess_err, 0xff, S * 8, st));
-  CK(hipMemsetAsync(a.n_seams, 0, 4, st));
   ws::launch_parse(a, st); ws::launch_scan(a, st); ws::launch_link(a, st);
   ws::launch_pieces(a, st, npb); ws::launch_seams(a, st); ws::launch_final(a, st);
   CK(hipStreamSynchronize(st));
