@@ -15,7 +15,7 @@ using namespace ws;
 namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
-                                           "k_seams",   "k_final",    "k_enc_len",  "k_enc_scan",
+                                           "k_final",    "k_enc_len",  "k_enc_scan",
                                            "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok"};
 
 struct DevBuf {
@@ -60,7 +60,7 @@ struct wsg_ctx {
   bool own_stream = false;
   std::string err;
   // decode workspace
-  DevBuf rec, prev, edge, blk_sum, blk_max, sess_err, total, pieces, seams, n_seams;
+  DevBuf rec, vflag, slink, edge, blk_sum, blk_max, sess_err, total, pieces;
   // encode workspace
   DevBuf esess, elast_close, epieces, epidx;
   // aggregate workspace
@@ -183,8 +183,8 @@ int wsg_close(wsg_ctx* c) {
   if (c->s_out) (void)hipStreamSynchronize(c->s_out);
   drain_timing(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
-  DevBuf* bufs[] = {&c->rec,     &c->prev,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
-                    &c->total,   &c->pieces, &c->seams, &c->n_seams, &c->esess,   &c->elast_close, &c->epieces, &c->epidx, &c->h_wire, &c->h_off,    &c->h_sf,
+  DevBuf* bufs[] = {&c->rec,     &c->vflag,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
+                    &c->total,   &c->pieces, &c->slink, &c->esess,   &c->elast_close, &c->epieces, &c->epidx, &c->h_wire, &c->h_off,    &c->h_sf,
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
@@ -259,18 +259,17 @@ int wsg_reset_timing(wsg_ctx* c) {
 
 static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, uint64_t wire_len) {
   const uint64_t F = n_frames ? n_frames : 1;
-  const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
+  const uint64_t nblk = (F + DBLOCK - 1) / DBLOCK;
   // + PIECES_PER_WAVE: k_piecesN reads its descriptors in groups
   HIP_TRY(c, c->pieces.ensure((piece_bound(wire_len, F) + 8) * sizeof(PieceDesc)));
   // sess_err is kept in its idle state between batches (k_final resets what it
   // reads), so no per-batch memset is needed
-  HIP_TRY(c, c->seams.ensure(nblk * BLOCK * sizeof(uint32_t)));
-  HIP_TRY(c, c->n_seams.ensure(nblk * sizeof(uint32_t)));
   HIP_TRY(c, c->rec.ensure(F * sizeof(FrameRec)));
-  HIP_TRY(c, c->prev.ensure(3 * F * sizeof(int32_t)));
+  HIP_TRY(c, c->vflag.ensure(F));
+  HIP_TRY(c, c->slink.ensure(3 * (uint64_t)(n_sessions ? n_sessions : 1) * sizeof(int32_t)));
   HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));
   HIP_TRY(c, c->blk_sum.ensure(nblk * sizeof(uint64_t)));
-  HIP_TRY(c, c->blk_max.ensure(3 * nblk * sizeof(int32_t)));
+  HIP_TRY(c, c->blk_max.ensure(4 * nblk * sizeof(int32_t)));
   HIP_TRY(c, c->sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t), 0xff, c->stream));
   HIP_TRY(c, c->total.ensure(sizeof(uint64_t)));
   return WSG_API_OK;
@@ -327,16 +326,15 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.desc = desc_out;
   a.result = result_out;
   a.rec = (FrameRec*)c->rec.p;
-  a.prev = (int32_t*)c->prev.p;
+  a.vflag = (uint8_t*)c->vflag.p;
+  a.slink = (int32_t*)c->slink.p;
   a.edge = (uint32_t*)c->edge.p;
   a.blk_sum = (uint64_t*)c->blk_sum.p;
   a.blk_max = (int32_t*)c->blk_max.p;
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
   a.pieces = (PieceDesc*)c->pieces.p;
-  a.seams = (uint32_t*)c->seams.p;
-  a.n_seams = (uint32_t*)c->n_seams.p;
-  a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  a.nblk = (uint32_t)((n_frames + DBLOCK - 1) / DBLOCK);
   a.n_pieces = piece_bound(wire_len, n_frames);
   a.validator_only = 0;
   a.in_desc = nullptr;
@@ -346,7 +344,6 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
     if (!a.fused_scan) timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
     timed(c, K_LINK, [&] { launch_link(a, c->stream); });
     timed(c, K_UNMASK, [&] { launch_pieces(a, c->stream, piece_bound(wire_len, n_frames)); });
-    timed(c, K_SEAMS, [&] { launch_seams(a, c->stream); });
   }
   timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());
@@ -380,16 +377,15 @@ int wsg_validate_batch_device(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n
   a.desc = (wsg_frame_desc*)c->v_desc.p;
   a.result = result_out;
   a.rec = (FrameRec*)c->rec.p;
-  a.prev = (int32_t*)c->prev.p;
+  a.vflag = (uint8_t*)c->vflag.p;
+  a.slink = (int32_t*)c->slink.p;
   a.edge = (uint32_t*)c->edge.p;
   a.blk_sum = (uint64_t*)c->blk_sum.p;
   a.blk_max = (int32_t*)c->blk_max.p;
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
   a.pieces = (PieceDesc*)c->pieces.p;
-  a.seams = (uint32_t*)c->seams.p;
-  a.n_seams = (uint32_t*)c->n_seams.p;
-  a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  a.nblk = (uint32_t)((n_frames + DBLOCK - 1) / DBLOCK);
   a.n_pieces = piece_bound(payload_len, n_frames);
   a.validator_only = 1;
   a.in_desc = desc;
@@ -399,7 +395,6 @@ int wsg_validate_batch_device(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n
     if (!a.fused_scan) timed(c, K_SCAN, [&] { launch_scan(a, c->stream); });
     timed(c, K_LINK, [&] { launch_link(a, c->stream); });
     timed(c, K_UNMASK, [&] { launch_vpieces(a, c->stream, a.n_pieces); });
-    timed(c, K_SEAMS, [&] { launch_seams(a, c->stream); });
   }
   timed(c, K_FINAL, [&] { launch_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());

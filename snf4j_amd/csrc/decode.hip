@@ -3,23 +3,22 @@
 //   k_parse   thread per frame: header parse + the per-frame rules of
 //             FrameDecoder.decode (:197-256), close status/reason (:121-136),
 //             first/last payload bytes; block aggregates for the scans.
-//   k_scan    one workgroup: exclusive scan of the block aggregates
-//             (payload slot bytes = the length prefix-scan; last data / message
-//             start / nonempty frame indices = max-scans).
+//   k_scan    one workgroup: exclusive scan of the block aggregates (payload slot
+//             bytes = the length prefix-scan; last data / message start / nonempty
+//             frame indices = max-scans; the UTF-8 carry).  Grids up to
+//             FUSED_SCAN_MAX_BLOCKS skip it: k_link reduces the aggregates itself.
 //   k_link    thread per frame: payload slot offset, the fragmentation rule
 //             (:229-236) from the previous data frame's FIN, text-message
 //             membership for the validator (FrameUtf8Validator.java:59-70), the
-//             frame's wsg_frame_desc with its status in the reference's check order,
-//             the piece descriptors.  (Small grids reduce the block aggregates
-//             themselves: no k_scan launch.)
+//             UTF-8 seam of a continuation frame against the scanned carry, the
+//             frame's wsg_frame_desc with its status in the reference's check
+//             order, the piece descriptors.
 //   k_piecesN one wave per 2 KiB of payload output: coalesced 16-B loads, 4-byte
 //             XOR unmask (:268-273), aligned 16-B stores into the frame slots,
 //             per-lane SWAR UTF-8 rule with the 3-byte carry taken from the
 //             neighbour lane (DPP) and the verdict folded by wavefront ballot.
 //             A UTF-8 error sets its frame's status and the session's first
 //             failing frame (atomicMin) directly.
-//   k_seams   the validated continuation frames k_link listed: their first bytes
-//             against the message carry (none in a batch of unfragmented messages).
 //   k_final   thread per session: wsg_session_result + carry-out state.
 #include "wsgpu_internal.h"
 #include "wsgpu_scan.h"
@@ -37,123 +36,202 @@ __device__ bool utf8_valid_run(const uint8_t* wire, uint64_t off, uint32_t n, ui
   return !utf8_incomplete(p3, p2, p1);
 }
 
-// Per-frame scan input: payload slot bytes, and the "last frame of a kind" max
-// fields as (k << 1) | bit carrying what k_link needs about that frame (FIN of
-// the last data frame, TEXT-ness of the last message start), so k_link never
-// reads another frame's record.  Frame indices < 2^30 (wsg_decode_batch_device).
-__device__ __forceinline__ Agg frame_agg(uint64_t k, const FrameRec& r) {
-  Agg v;
+// ------------------------------------------------------------------ scan element
+// Per-frame scan input: payload slot bytes, the "last frame of a kind" max fields as
+// (k << 1) | bit carrying what k_link needs about that frame (FIN of the last data
+// frame, TEXT-ness of the last message start), and the UTF-8 carry c3, so k_link
+// never reads another frame's record.  Frame indices < 2^30 (wsg_decode_batch_device).
+//
+// c3 is the FrameUtf8Validator state a frame inherits (FrameUtf8Validator.java:59-98):
+// the last <= 3 payload bytes of the data frames since the last reset, newest in bits
+// 16-23 (the edge layout), their count in bits 24-25, bit 26 = reset.  A message start
+// resets it (FrameUtf8Validator.java:64-67), and so does a session's first frame, whose
+// element carries the session's tail from the previous batch; a FIN frame contributes
+// zero bytes (its message ended complete, or the frame failed).  carry_op is the
+// associative "last 3 bytes of the concatenation, restarted at a reset".
+struct DAgg {
+  uint64_t sum;
+  int32_t m0, m1, m2;
+  uint32_t c3;
+};
+constexpr DAgg DAGG_ID = {0ull, -1, -1, -1, 0u};
+constexpr uint32_t C3_RESET = 1u << 26;
+
+__device__ __forceinline__ uint32_t carry_op(uint32_t x, uint32_t y) {
+  if (y & C3_RESET) return y;
+  const uint32_t nx = (x >> 24) & 3u, ny = (y >> 24) & 3u;
+  const uint32_t n = nx + ny < 3u ? nx + ny : 3u;
+  return ((x & 0xffffffu) >> (8 * ny)) | (y & 0xffffffu) | (n << 24) | (x & C3_RESET);
+}
+__device__ __forceinline__ DAgg agg_op(const DAgg& x, const DAgg& y) {
+  DAgg r;
+  r.sum = x.sum + y.sum;
+  r.m0 = x.m0 > y.m0 ? x.m0 : y.m0;
+  r.m1 = x.m1 > y.m1 ? x.m1 : y.m1;
+  r.m2 = x.m2 > y.m2 ? x.m2 : y.m2;
+  r.c3 = carry_op(x.c3, y.c3);
+  return r;
+}
+__device__ __forceinline__ DAgg agg_shfl_up(const DAgg& v, int d) {
+  DAgg t;
+  t.sum = shfl_up_u64(v.sum, d);
+  t.m0 = __shfl_up(v.m0, d, 64);
+  t.m1 = __shfl_up(v.m1, d, 64);
+  t.m2 = __shfl_up(v.m2, d, 64);
+  t.c3 = (uint32_t)__shfl_up((int)v.c3, d, 64);
+  return t;
+}
+
+// the session's carry from the previous batch, as a reset element
+__device__ __forceinline__ uint32_t tail_c3(const wsg_session_state& st) {
+  const uint32_t n = st.tail_len < 3 ? st.tail_len : 3u;  // tail[0] the oldest
+  const uint32_t t = (uint32_t)st.tail[0] | ((uint32_t)st.tail[1] << 8) | ((uint32_t)st.tail[2] << 16);
+  return C3_RESET | (n << 24) | ((t << (24 - 8 * n)) & 0xffffffu);
+}
+
+// l3: the frame's last 3 payload bytes (edge layout; 0 for a FIN frame)
+__device__ __forceinline__ DAgg frame_agg(uint64_t k, const FrameRec& r, uint32_t l3, bool sess_first,
+                                          const wsg_session_state* state) {
+  DAgg v;
   v.sum = (uint64_t)((r.len + 15u) & ~15u);
   const bool data = code_is_data(r.code);
   v.m0 = data ? (int32_t)((k << 1) | ((r.code & CODE_FIN) ? 1u : 0u)) : -1;
   v.m1 = code_is_start(r.code) ? (int32_t)((k << 1) | (code_op(r.code) == WSG_OP_TEXT ? 1u : 0u)) : -1;
   v.m2 = (data && r.len) ? (int32_t)(k << 1) : -1;
+  uint32_t c = (data && r.len) ? (l3 & 0xffffffu) | ((r.len < 3 ? r.len : 3u) << 24) : 0u;
+  if (code_is_start(r.code)) c |= C3_RESET;
+  else if (sess_first) c = carry_op(tail_c3(state[r.sess]), c);
+  v.c3 = c;
   return v;
 }
 
+__device__ __forceinline__ DAgg load_blk(const DecodeArgs& a, uint32_t b) {
+  DAgg e;
+  e.sum = a.blk_sum[b];
+  e.m0 = a.blk_max[b];
+  e.m1 = a.blk_max[a.nblk + b];
+  e.m2 = a.blk_max[2 * a.nblk + b];
+  e.c3 = (uint32_t)a.blk_max[3 * a.nblk + b];
+  return e;
+}
+__device__ __forceinline__ void store_blk(const DecodeArgs& a, uint32_t b, const DAgg& e) {
+  a.blk_sum[b] = e.sum;
+  a.blk_max[b] = e.m0;
+  a.blk_max[a.nblk + b] = e.m1;
+  a.blk_max[2 * a.nblk + b] = e.m2;
+  a.blk_max[3 * a.nblk + b] = (int32_t)e.c3;
+}
+
+// Session of frame k: two wave-uniform searches (scalar loads) bound the sessions
+// of the wave's 64 frames, and a lane searches only inside those bounds — not at
+// all when the wave's frames belong to one session.
+__device__ __forceinline__ uint32_t wave_session(const DecodeArgs& a, uint64_t k) {
+  const uint32_t kw = __builtin_amdgcn_readfirstlane((uint32_t)(k & ~63ull));  // (frame indices < 2^30)
+  const uint64_t kl = kw + 63u < a.n_frames ? kw + 63u : a.n_frames - 1;
+  const uint32_t s_lo = find_session(a.session_first, a.n_sessions, kw);
+  const uint32_t s_hi = find_session_in(a.session_first, s_lo, a.n_sessions - 1, kl);
+  return find_session_in(a.session_first, s_lo, s_hi, k);
+}
+
 // ------------------------------------------------------------------ k_parse
-__global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  Agg v = AGG_ID;
+// Frame k's header rules and record; returns its scan element.  d[0..5]: the wire
+// words from o & ~3 (zero past the wire end).
+__device__ __forceinline__ DAgg parse_one(const DecodeArgs& a, uint64_t k, uint64_t o, uint64_t e, const uint32_t d[6],
+                                          uint32_t s) {
+  const uint64_t ext = e > o ? e - o : 0;
+  const uint32_t sh = (uint32_t)(o & 3);
+  const uint32_t w0 = alignbyte(d[1], d[0], sh), w1 = alignbyte(d[2], d[1], sh), w2 = alignbyte(d[3], d[2], sh);
+  const uint32_t w3 = alignbyte(d[4], d[3], sh), w4 = alignbyte(d[5], d[4], sh);
+  Header hd;
+  uint32_t pre = 0, post = 0, len = 0, f3 = 0, l3 = 0;
+  uint64_t src = o;
+  if (!parse_header_words(w0, w1, w2, w3, w4, ext, hd)) {
+    pre = WSG_E_BATCH;
+    hd.opcode = w0 & 15u; hd.fin = (w0 >> 7) & 1u; hd.rsv = (w0 >> 4) & 7u; hd.masked = 0; hd.mask = 0;
+  } else {
+    pre = rules_pre(hd, a.client_mode, a.allow_ext);
+    post = rules_post(hd, a.max_payload);
+    if (!pre && !post && (uint64_t)hd.hdr_len + hd.plen != ext) pre = WSG_E_BATCH;
+    if (!pre && !post) {
+      len = (uint32_t)hd.plen;
+      src = o + hd.hdr_len;
+      if (hd.opcode == WSG_OP_CLOSE && len >= 2) {  // createFrame, FrameDecoder.java:121-136
+        uint32_t b0 = a.wire[src] ^ (hd.mask & 0xffu);
+        uint32_t b1 = a.wire[src + 1] ^ ((hd.mask >> 8) & 0xffu);
+        if (!close_status_ok((b0 << 8) | b1)) post = WSG_E_CLOSE_STATUS;
+        else if (len > 2 && !utf8_valid_run(a.wire, src + 2, len - 2, hd.mask, 2)) post = WSG_E_CLOSE_REASON;
+      }
+      if (hd.opcode <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry
+        // first 3 payload bytes: within the header's 20 loaded bytes (hdr_len <= 14)
+        const uint32_t nf = len < 3 ? len : 3;
+        const uint32_t keep3 = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : (nf == 1 ? 0xffu : 0u));
+        f3 = (bytes_at(w0, w1, w2, w3, w4, hd.hdr_len) ^ hd.mask) & keep3;
+        // last 3 payload bytes: only a non-FIN fragment's are needed (the carry into the
+        // next fragment or batch); a frame's own last-byte and end-of-message tests
+        // run in k_pieces on bytes it holds, so a FIN frame costs no second line here
+        if (nf && !hd.fin) {
+          const uint64_t e3 = src + len - nf;  // first of the last nf bytes
+          const uint64_t q = e3 & ~3ull;
+          uint32_t lo, hi;
+          if (q + 8 <= a.wire_len) {
+            lo = *(const uint32_t*)(a.wire + q);
+            hi = *(const uint32_t*)(a.wire + q + 4);
+          } else {
+            lo = hi = 0;
+#pragma unroll
+            for (uint32_t i = 0; i < 8; ++i)
+              if (q + i < a.wire_len) (i < 4 ? lo : hi) |= (uint32_t)a.wire[q + i] << (8 * (i & 3));
+          }
+          const uint32_t t = alignbyte(hi, lo, (uint32_t)(e3 & 3));  // bytes e3.. e3+3
+          const uint32_t ph = (uint32_t)(len - nf) & 3u;            // mask phase of byte e3
+          const uint32_t m = (hd.mask >> (8 * ph)) | (ph ? hd.mask << (32 - 8 * ph) : 0u);
+          const uint32_t u = t ^ m;                                  // unmasked bytes e3..e3+3
+          for (uint32_t i = 0; i < nf; ++i) {  // byte len-1-i (newest first) -> bits 16-8i
+            const uint32_t j = nf - 1 - i;     // its index in u
+            l3 |= ((u >> (8 * j)) & 0xffu) << (8 * (2 - i));
+          }
+        }
+      }
+    }
+  }
+  a.edge[k] = f3;
+  a.edge[a.n_frames + k] = l3;
+  if (pre || post) len = 0;
+  FrameRec r;
+  r.src = src;
+  r.len = len;
+  r.mask = hd.mask;
+  r.code = (pre << CODE_PRE_SHIFT) | (post << CODE_POST_SHIFT) | (hd.fin ? CODE_FIN : 0u) |
+           (hd.rsv << CODE_RSV_SHIFT) | (hd.masked ? CODE_MASKED : 0u) | (hd.opcode << CODE_OP_SHIFT);
+  r.sess = s;
+  a.rec[k] = r;
+  return frame_agg(k, r, l3, k == a.session_first[s], a.state);
+}
+
+__global__ __launch_bounds__(DBLOCK) void k_parse(DecodeArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
+  DAgg v = DAGG_ID;
   if (k < a.n_frames) {
-    const uint32_t s = find_session(a.session_first, a.n_sessions, k);
     const uint64_t o = a.frame_off[k], e = a.frame_off[k + 1];
-    const uint64_t ext = e > o ? e - o : 0;
-    // wire bytes o .. o+19 as five words, zero past the wire end
-    uint32_t w0, w1, w2, w3, w4;
+    // wire words from o & ~3 (zero past the wire end)
+    uint32_t d[6];
     const uint64_t a4 = o & ~3ull;
     if (a4 + 24 <= a.wire_len) {
       const uint32_t* p = (const uint32_t*)(a.wire + a4);
-      const uint32_t d0 = p[0], d1 = p[1], d2 = p[2], d3 = p[3], d4 = p[4], d5 = p[5];
-      const uint32_t sh = (uint32_t)(o & 3);
-      w0 = alignbyte(d1, d0, sh); w1 = alignbyte(d2, d1, sh); w2 = alignbyte(d3, d2, sh);
-      w3 = alignbyte(d4, d3, sh); w4 = alignbyte(d5, d4, sh);
-    } else {
-      uint64_t lo = 0, mid = 0, hi = 0;
 #pragma unroll
-      for (int i = 0; i < 20; ++i) {
-        const uint64_t b = (o + i < a.wire_len) ? a.wire[o + i] : 0u;
-        if (i < 8) lo |= b << (8 * i);
-        else if (i < 16) mid |= b << (8 * (i - 8));
-        else hi |= b << (8 * (i - 16));
-      }
-      w0 = (uint32_t)lo; w1 = (uint32_t)(lo >> 32); w2 = (uint32_t)mid; w3 = (uint32_t)(mid >> 32); w4 = (uint32_t)hi;
-    }
-    Header hd;
-    uint32_t pre = 0, post = 0, len = 0;
-    uint64_t src = o;
-    if (!parse_header_words(w0, w1, w2, w3, w4, ext, hd)) {
-      pre = WSG_E_BATCH;
-      hd.opcode = w0 & 15u; hd.fin = (w0 >> 7) & 1u; hd.rsv = (w0 >> 4) & 7u; hd.masked = 0; hd.mask = 0;
+      for (int j = 0; j < 6; ++j) d[j] = p[j];
     } else {
-      pre = rules_pre(hd, a.client_mode, a.allow_ext);
-      post = rules_post(hd, a.max_payload);
-      if (!pre && !post && (uint64_t)hd.hdr_len + hd.plen != ext) pre = WSG_E_BATCH;
-      if (!pre && !post) {
-        len = (uint32_t)hd.plen;
-        src = o + hd.hdr_len;
-        if (hd.opcode == WSG_OP_CLOSE && len >= 2) {  // createFrame, FrameDecoder.java:121-136
-          uint32_t b0 = a.wire[src] ^ (hd.mask & 0xffu);
-          uint32_t b1 = a.wire[src + 1] ^ ((hd.mask >> 8) & 0xffu);
-          if (!close_status_ok((b0 << 8) | b1)) post = WSG_E_CLOSE_STATUS;
-          else if (len > 2 && !utf8_valid_run(a.wire, src + 2, len - 2, hd.mask, 2)) post = WSG_E_CLOSE_REASON;
-        }
-        if (hd.opcode <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry
-          // first 3 payload bytes: within the header's 20 loaded bytes (hdr_len <= 14)
-          uint32_t l3 = 0;
-          const uint32_t nf = len < 3 ? len : 3;
-          const uint32_t keep3 = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : (nf == 1 ? 0xffu : 0u));
-          const uint32_t f3 = (bytes_at(w0, w1, w2, w3, w4, hd.hdr_len) ^ hd.mask) & keep3;
-          // last 3 payload bytes: only a non-FIN fragment's are needed (the carry into the
-          // next fragment or batch); a frame's own last-byte and end-of-message tests
-          // run in k_pieces on bytes it holds, so a FIN frame costs no second line here
-          if (nf && !hd.fin) {
-            const uint64_t e3 = src + len - nf;  // first of the last nf bytes
-            const uint64_t q = e3 & ~3ull;
-            uint32_t lo, hi;
-            if (q + 8 <= a.wire_len) {
-              lo = *(const uint32_t*)(a.wire + q);
-              hi = *(const uint32_t*)(a.wire + q + 4);
-            } else {
-              lo = hi = 0;
 #pragma unroll
-              for (uint32_t i = 0; i < 8; ++i)
-                if (q + i < a.wire_len) (i < 4 ? lo : hi) |= (uint32_t)a.wire[q + i] << (8 * (i & 3));
-            }
-            const uint32_t t = alignbyte(hi, lo, (uint32_t)(e3 & 3));  // bytes e3.. e3+3
-            const uint32_t ph = (uint32_t)(len - nf) & 3u;            // mask phase of byte e3
-            const uint32_t m = (hd.mask >> (8 * ph)) | (ph ? hd.mask << (32 - 8 * ph) : 0u);
-            const uint32_t u = t ^ m;                                  // unmasked bytes e3..e3+3
-            for (uint32_t i = 0; i < nf; ++i) {  // byte len-1-i (newest first) -> bits 16-8i
-              const uint32_t j = nf - 1 - i;     // its index in u
-              l3 |= ((u >> (8 * j)) & 0xffu) << (8 * (2 - i));
-            }
-          }
-          a.edge[k] = f3;
-          a.edge[a.n_frames + k] = l3;
-        }
-      }
+      for (int j = 0; j < 6; ++j) d[j] = 0u;
+#pragma unroll
+      for (uint32_t b = 0; b < 24u; ++b)
+        if (a4 + b < a.wire_len) d[b >> 2] |= (uint32_t)a.wire[a4 + b] << (8 * (b & 3));
     }
-    if (pre || post) len = 0;
-    FrameRec r;
-    r.src = src;
-    r.out_off = 0;
-    r.len = len;
-    r.mask = hd.mask;
-    r.code = (pre << CODE_PRE_SHIFT) | (post << CODE_POST_SHIFT) | (hd.fin ? CODE_FIN : 0u) |
-             (hd.rsv << CODE_RSV_SHIFT) | (hd.masked ? CODE_MASKED : 0u) | (hd.opcode << CODE_OP_SHIFT);
-    r.sess = s;
-    a.rec[k] = r;
-    v = frame_agg(k, r);
+    v = parse_one(a, k, o, e, d, wave_session(a, k));
   }
-  Agg tot;
-  block_excl_scan(v, &tot);
-  if (threadIdx.x == 0) {
-    a.blk_sum[blockIdx.x] = tot.sum;
-    a.blk_max[blockIdx.x] = tot.m0;
-    a.blk_max[a.nblk + blockIdx.x] = tot.m1;
-    a.blk_max[2 * a.nblk + blockIdx.x] = tot.m2;
-  }
+  DAgg tot;
+  block_excl_scan_t(v, &tot, DAGG_ID);
+  if (threadIdx.x == 0) store_blk(a, blockIdx.x, tot);
 }
 
 // ------------------------------------------------------------------ k_vparse
@@ -163,75 +241,58 @@ __global__ __launch_bounds__(BLOCK) void k_parse(DecodeArgs a) {
 // FrameRec / edges / block aggregates as k_parse, with no header rules.
 __device__ __forceinline__ uint32_t plain_byte(const DecodeArgs& a, uint64_t i) { return i < a.wire_len ? a.wire[i] : 0u; }
 
-__global__ __launch_bounds__(BLOCK) void k_vparse(DecodeArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  Agg v = AGG_ID;
+__global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
+  DAgg v = DAGG_ID;
   if (k < a.n_frames) {
-    const wsg_frame_desc d = a.in_desc[k];
-    const uint32_t s = find_session(a.session_first, a.n_sessions, k);
-    const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
-    const uint32_t len = d.payload_len;
-    const uint64_t src = d.payload_off;
-    if (op <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry (as k_parse)
-      const uint32_t nf = len < 3 ? len : 3;
+    {
+      const uint32_t s = wave_session(a, k);
+      const wsg_frame_desc d = a.in_desc[k];
+      const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
+      const uint32_t len = d.payload_len;
+      const uint64_t src = d.payload_off;
       uint32_t f3 = 0, l3 = 0;
-      for (uint32_t i = 0; i < nf; ++i) f3 |= plain_byte(a, src + i) << (8 * i);
-      if (!fin)
-        for (uint32_t i = 0; i < nf; ++i) l3 |= plain_byte(a, src + len - 1 - i) << (8 * (2 - i));
+      if (op <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry (as k_parse)
+        const uint32_t nf = len < 3 ? len : 3;
+        for (uint32_t j = 0; j < nf; ++j) f3 |= plain_byte(a, src + j) << (8 * j);
+        if (!fin)
+          for (uint32_t j = 0; j < nf; ++j) l3 |= plain_byte(a, src + len - 1 - j) << (8 * (2 - j));
+      }
       a.edge[k] = f3;
       a.edge[a.n_frames + k] = l3;
+      FrameRec r;
+      r.src = src;
+      r.len = len;
+      r.mask = 0;
+      r.code = (fin ? CODE_FIN : 0u) | (rsv << CODE_RSV_SHIFT) | (op << CODE_OP_SHIFT);
+      r.sess = s;
+      a.rec[k] = r;
+      v = agg_op(v, frame_agg(k, r, l3, k == a.session_first[s], a.state));
     }
-    FrameRec r;
-    r.src = src;
-    r.out_off = 0;
-    r.len = len;
-    r.mask = 0;
-    r.code = (fin ? CODE_FIN : 0u) | (rsv << CODE_RSV_SHIFT) | (op << CODE_OP_SHIFT);
-    r.sess = s;
-    a.rec[k] = r;
-    v = frame_agg(k, r);
   }
-  Agg tot;
-  block_excl_scan(v, &tot);
-  if (threadIdx.x == 0) {
-    a.blk_sum[blockIdx.x] = tot.sum;
-    a.blk_max[blockIdx.x] = tot.m0;
-    a.blk_max[a.nblk + blockIdx.x] = tot.m1;
-    a.blk_max[2 * a.nblk + blockIdx.x] = tot.m2;
-  }
+  DAgg tot;
+  block_excl_scan_t(v, &tot, DAGG_ID);
+  if (threadIdx.x == 0) store_blk(a, blockIdx.x, tot);
 }
 
 // ------------------------------------------------------------------ k_scan
 // One workgroup: exclusive scan of the block aggregates in place, 4 entries per
 // thread per pass (one block scan per 4096 blocks).
 __global__ __launch_bounds__(1024) void k_scan(DecodeArgs a) {
-  Agg carry = AGG_ID;
+  DAgg carry = DAGG_ID;
   for (uint32_t base = 0; base < a.nblk; base += 4096) {
     const uint32_t b0 = base + threadIdx.x * 4;
-    Agg e[4], t = AGG_ID;
+    DAgg e[4], t = DAGG_ID;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t b = b0 + i;
-      e[i] = AGG_ID;
-      if (b < a.nblk) {
-        e[i].sum = a.blk_sum[b];
-        e[i].m0 = a.blk_max[b];
-        e[i].m1 = a.blk_max[a.nblk + b];
-        e[i].m2 = a.blk_max[2 * a.nblk + b];
-      }
+      e[i] = b0 + i < a.nblk ? load_blk(a, b0 + i) : DAGG_ID;
       t = agg_op(t, e[i]);
     }
-    Agg tot;
-    Agg ex = agg_op(carry, block_excl_scan(t, &tot));
+    DAgg tot;
+    DAgg ex = agg_op(carry, block_excl_scan_t(t, &tot, DAGG_ID));
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const uint32_t b = b0 + i;
-      if (b < a.nblk) {
-        a.blk_sum[b] = ex.sum;
-        a.blk_max[b] = ex.m0;
-        a.blk_max[a.nblk + b] = ex.m1;
-        a.blk_max[2 * a.nblk + b] = ex.m2;
-      }
+      if (b0 + i < a.nblk) store_blk(a, b0 + i, ex);
       ex = agg_op(ex, e[i]);
     }
     carry = agg_op(carry, tot);
@@ -239,211 +300,176 @@ __global__ __launch_bounds__(1024) void k_scan(DecodeArgs a) {
   if (threadIdx.x == 0) *a.total = carry.sum;
 }
 
-// ------------------------------------------------------------------ k_link
-__global__ __launch_bounds__(BLOCK) void k_link(DecodeArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
-  const int lane = threadIdx.x & 63;
-  const bool live = k < a.n_frames;
-  FrameRec r;
-  Agg v = AGG_ID;
-  if (live) {
-    r = a.rec[k];
-    v = frame_agg(k, r);
-  }
-  Agg tot;
-  Agg ex = block_excl_scan(v, &tot);
-  // the aggregate of every frame before this block: k_scan's exclusive scan, or (small
-  // grids, no k_scan launch) this block's own reduction of k_parse's block aggregates
-  Agg bp;
-  if (a.fused_scan) {
-    Agg t = AGG_ID;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += BLOCK) {
-      Agg e;
-      e.sum = a.blk_sum[b];
-      e.m0 = a.blk_max[b];
-      e.m1 = a.blk_max[a.nblk + b];
-      e.m2 = a.blk_max[2 * a.nblk + b];
-      t = agg_op(t, e);
-    }
-    block_excl_scan(t, &bp);
-    if (blockIdx.x + 1 == a.nblk && threadIdx.x == 0) *a.total = bp.sum + tot.sum;
-  } else {
-    bp.sum = a.blk_sum[blockIdx.x];
-    bp.m0 = a.blk_max[blockIdx.x];
-    bp.m1 = a.blk_max[a.nblk + blockIdx.x];
-    bp.m2 = a.blk_max[2 * a.nblk + blockIdx.x];
-  }
-  uint32_t extra = 0;
-  if (live) {
-    ex = agg_op(bp, ex);
-    const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
-    // read only for continuation frames, the frames of a message still open, and a
-    // session's last frame when it is not a FIN message start (k_seams, k_final):
-    // a complete one-frame message (the common case) needs none
-    if (!(code_is_start(r.code) && (r.code & CODE_FIN))) {
-      a.prev[k] = jd;
-      a.prev[a.n_frames + k] = jm;
-      a.prev[2 * a.n_frames + k] = ex.m2 >> 1;
-    }
-    const uint32_t s = r.sess;
-    const int32_t sf = (int32_t)a.session_first[s];
-    const wsg_session_state st = a.state[s];
-    const uint32_t op = code_op(r.code);
-    uint32_t frag_err = 0;
-    bool text = false;
-    if (!code_pre(r.code)) {
-      // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
-      const bool frag = jd >= sf ? !(ex.m0 & 1) : (st.fragmentation != 0);
-      if (!a.validator_only) frag_err = rules_frag(op, frag);
-      if (a.validate) {
-        text = op == WSG_OP_TEXT;
-        if (op == WSG_OP_CONTINUATION) text = jm >= sf ? (ex.m1 & 1) != 0 : (st.text_open != 0);
-      }
-    }
-    // the frame's status in the reference's check order (header rules, fragmentation,
-    // lengths / close); the validator's verdict (k_pieces, k_seams) only on frames
-    // that pass all of them, so a failed frame is never validated
-    uint32_t status = code_pre(r.code) ? code_pre(r.code) : (frag_err ? frag_err : code_post(r.code));
-    if (!status && ex.sum + r.len > a.n_pieces * PIECE) status = WSG_E_BATCH;  // slots beyond the piece grid
-    extra = (frag_err << CODE_FRAG_SHIFT) | ((text && !status) ? CODE_VALIDATE : 0u);
-    a.rec[k].out_off = ex.sum;
-    a.rec[k].code = r.code | extra;
-    wsg_frame_desc d;
-    d.payload_off = ex.sum;
-    d.payload_len = r.len;
-    d.opcode = (uint8_t)op;
-    d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
-                        ((r.code & CODE_MASKED) ? 1u : 0u));
-    d.status = (uint16_t)status;
-    a.desc[k] = d;
-    if (status) atomicMin((unsigned long long*)&a.sess_err[s], (unsigned long long)k);
-  }
-  // a validated continuation: its first bytes are checked against the message carry
-  // by k_seams (every other validated frame is checked whole by k_pieces).  The
-  // block's entries are compacted into its own region of `seams` (no global atomic:
-  // one counter shared by every block cost 75 us on a 10%-fragmented batch)
-  {
-    __shared__ uint32_t wcnt[BLOCK / 64];
-    const bool seam = live && (extra & CODE_VALIDATE) && code_op(r.code) == WSG_OP_CONTINUATION;
-    const uint64_t m = __ballot(seam);
-    const int wid = threadIdx.x >> 6;
-    if (lane == 0) wcnt[wid] = (uint32_t)__builtin_popcountll(m);
-    __syncthreads();
-    uint32_t base = 0, n = 0;
-#pragma unroll
-    for (int i = 0; i < BLOCK / 64; ++i) {
-      base += i < wid ? wcnt[i] : 0u;
-      n += wcnt[i];
-    }
-    if (seam)
-      a.seams[(uint64_t)blockIdx.x * BLOCK + base +
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] =
-          (uint32_t)k;
-    if (threadIdx.x == 0) a.n_seams[blockIdx.x] = n;
-  }
-  // Descriptors of the pieces whose first output byte falls in a frame's slot,
-  // written cooperatively: the wave's pieces are contiguous, lane i writes the
-  // wave's pieces i, i+64, ... (coalesced 16-B stores) after finding the owning
-  // frame with a shuffle search over the exclusive piece counts.
-  const uint64_t slot = live ? (uint64_t)((r.len + 15u) & ~15u) : 0ull;
-  const uint64_t slot_end = ex.sum + slot;
-  const uint32_t pc0 = (uint32_t)((ex.sum + PIECE - 1) / PIECE);
-  const uint32_t cnt = slot ? (uint32_t)((slot_end + PIECE - 1) / PIECE) - pc0 : 0u;
-  uint32_t cum = cnt;  // inclusive wave scan of the counts
-#pragma unroll
-  for (int sd = 1; sd < 64; sd <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)cum, sd, 64);
-    if (lane >= sd) cum += t;
-  }
-  const uint32_t T = (uint32_t)__shfl((int)cum, 63, 64);
-  cum -= cnt;  // exclusive
-  if (!T) return;
-  // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31
-  const uint32_t fk = (uint32_t)k | ((extra & CODE_VALIDATE) ? 0x80000000u : 0u) |
-                     ((live && (r.code & CODE_FIN)) ? 0x40000000u : 0u);
-  const bool cont = live && code_op(r.code) == WSG_OP_CONTINUATION;
-  for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
-    int o = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1)
-      if ((uint32_t)__shfl((int)cum, o + step, 64) <= t) o += step;
-    const uint32_t o_cum = (uint32_t)__shfl((int)cum, o, 64);
-    const uint32_t o_pc0 = (uint32_t)__shfl((int)pc0, o, 64);
-    const uint64_t o_out = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex.sum >> 32), o, 64) << 32) |
-                           (uint32_t)__shfl((int)(uint32_t)ex.sum, o, 64);
-    const uint64_t o_src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(r.src >> 32), o, 64) << 32) |
-                           (uint32_t)__shfl((int)(uint32_t)r.src, o, 64);
-    const uint32_t o_len = (uint32_t)__shfl((int)(live ? r.len : 0u), o, 64);
-    const uint32_t o_mask = (uint32_t)__shfl((int)(live ? r.mask : 0u), o, 64);
-    const uint32_t o_fk = (uint32_t)__shfl((int)fk, o, 64);
-    const bool o_cont = __shfl((int)cont, o, 64) != 0;
-    if (t >= T) continue;
-    const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
-    if (pc >= a.n_pieces) continue;  // beyond the grid: the frame failed with WSG_E_BATCH above
-    const uint64_t ps = pc * PIECE;
-    const uint64_t o_end = o_out + ((o_len + 15u) & ~15u);
-    const uint32_t j0 = (uint32_t)(ps - o_out);
-    const uint32_t left = o_len - j0;
-    // runs past its frame's slot: other frames' bytes follow, unless it is the batch's
-    // last frame (a slot ending the payload region)
-    const bool single = o_end >= ps + PIECE || (uint64_t)(o_fk & 0x3fffffffu) + 1 == a.n_frames;
-    PieceDesc d;
-    d.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) |
-             ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI) |
-             (left <= PIECE ? PD_LAST : 0ull) | ((o_fk & 0x40000000u) ? PD_FIN : 0ull);
-    d.mask = o_mask;
-    d.frame = (o_fk & PDF_INDEX) | (o_cont ? PDF_CONT : 0u);
-    a.pieces[pc] = d;
-  }
-}
-
 // ------------------------------------------------------------------ UTF-8 seams
-// Carry bytes of the text message before frame k (<= 3, oldest first).
-__device__ uint32_t message_carry(const DecodeArgs& a, uint64_t k, uint32_t op, uint32_t sess, uint8_t c[3]) {
-  if (op != WSG_OP_CONTINUATION) return 0;  // a TEXT frame starts its message
-  const int32_t sf = (int32_t)a.session_first[sess];
-  const int32_t ms = a.prev[a.n_frames + k];
-  const bool in_batch = ms >= sf;
-  const int32_t lo = in_batch ? ms : sf;
-  uint8_t rev[3];  // newest first
-  uint32_t n = 0;
-  int32_t j = a.prev[2 * a.n_frames + k];
-  while (n < 3 && j >= lo) {
-    const uint32_t lj = a.rec[j].len;
-    const uint32_t l3 = a.edge[a.n_frames + j];
-    const uint32_t have = lj < 3 ? lj : 3;
-    for (uint32_t i = 0; i < have && n < 3; ++i) rev[n++] = (uint8_t)(l3 >> (8 * (2 - i)));
-    j = a.prev[2 * a.n_frames + j];
-  }
-  if (n < 3 && !in_batch) {
-    const wsg_session_state st = a.state[sess];
-    for (uint32_t i = 0; i < st.tail_len && n < 3; ++i) rev[n++] = st.tail[st.tail_len - 1 - i];
-  }
-  for (uint32_t i = 0; i < n; ++i) c[i] = rev[n - 1 - i];
-  return n;
-}
-
-// UTF-8 verdict of the first (<=3) bytes of the frame after the carry, and of
-// the message end (FIN): FrameUtf8Validator.java:78-96 at the fragment seams.
-__device__ bool edge_utf8_error(const DecodeArgs& a, uint64_t k, const FrameRec& r) {
-  uint8_t s[6];
-  const uint32_t op = code_op(r.code);
-  uint32_t n = message_carry(a, k, op, r.sess, s);
-  const uint32_t nc = n;
-  const uint32_t f3 = a.edge[k];
-  const uint32_t nh = r.len < 3 ? r.len : 3;
-  for (uint32_t i = 0; i < nh; ++i) s[n++] = (uint8_t)(f3 >> (8 * i));
+// UTF-8 verdict of a validated continuation frame's first (<= 3) bytes after the
+// message carry c3, and of the message end when a FIN frame shorter than 3 bytes
+// ends on the carry: FrameUtf8Validator.java:78-96 at the fragment seams (every
+// other byte of the frame is checked by k_pieces).
+__device__ bool seam_utf8_error(uint32_t c3, uint32_t f3, uint32_t len, bool fin) {
+  // the carry then the frame's head bytes, oldest in bits 0-7 (registers, no array)
+  const uint32_t nc = (c3 >> 24) & 3u, nh = len < 3 ? len : 3u, n = nc + nh;
+  const uint64_t win = (uint64_t)((c3 & 0xffffffu) >> (24 - 8 * nc)) | ((uint64_t)f3 << (8 * nc));
   for (uint32_t i = nc; i < n; ++i) {
-    const uint32_t p1 = i >= 1 ? s[i - 1] : 0, p2 = i >= 2 ? s[i - 2] : 0, p3 = i >= 3 ? s[i - 3] : 0;
-    if (utf8_err_byte(p3, p2, p1, s[i])) return true;
+    const uint32_t p1 = i >= 1 ? (uint32_t)(win >> (8 * (i - 1))) & 0xffu : 0u;
+    const uint32_t p2 = i >= 2 ? (uint32_t)(win >> (8 * (i - 2))) & 0xffu : 0u;
+    const uint32_t p3 = i >= 3 ? (uint32_t)(win >> (8 * (i - 3))) & 0xffu : 0u;
+    if (utf8_err_byte(p3, p2, p1, (uint32_t)(win >> (8 * i)) & 0xffu)) return true;
   }
   // the frame's last byte, and the end of a FIN message of >= 3 bytes in this frame,
   // are tested by k_pieces (tail_error); a shorter FIN frame ends on the carry
-  if ((r.code & CODE_FIN) && r.len < 3) {
-    const uint32_t t1 = n >= 1 ? s[n - 1] : 0, t2 = n >= 2 ? s[n - 2] : 0, t3 = n >= 3 ? s[n - 3] : 0;
+  if (fin && len < 3) {
+    const uint32_t t1 = n >= 1 ? (uint32_t)(win >> (8 * (n - 1))) & 0xffu : 0u;
+    const uint32_t t2 = n >= 2 ? (uint32_t)(win >> (8 * (n - 2))) & 0xffu : 0u;
+    const uint32_t t3 = n >= 3 ? (uint32_t)(win >> (8 * (n - 3))) & 0xffu : 0u;
     if (utf8_incomplete(t3, t2, t1)) return true;
   }
   return false;
+}
+
+// ------------------------------------------------------------------ k_link
+__global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
+  const int lane = threadIdx.x & 63;
+  // the aggregate of every frame before this block: k_scan's exclusive scan, or (small
+  // grids, no k_scan launch) this block's own reduction of k_parse's block aggregates.
+  // Coalesced loads (entry i * DBLOCK + t); the sums and maxima commute and fold as
+  // loaded, the order-sensitive carries go through LDS so that each thread folds a
+  // contiguous run of them, in order.
+  DAgg bp;
+  if (a.fused_scan) {
+    __shared__ uint32_t c3s[FUSED_SCAN_MAX_BLOCKS];
+    DAgg t = DAGG_ID;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += DBLOCK) {
+      const DAgg e = load_blk(a, b);
+      t.sum += e.sum;
+      t.m0 = t.m0 > e.m0 ? t.m0 : e.m0;
+      t.m1 = t.m1 > e.m1 ? t.m1 : e.m1;
+      t.m2 = t.m2 > e.m2 ? t.m2 : e.m2;
+      c3s[b] = e.c3;
+    }
+    __syncthreads();
+    const uint32_t per = (blockIdx.x + DBLOCK - 1) / DBLOCK;
+    const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < blockIdx.x ? b0 + per : blockIdx.x;
+    for (uint32_t b = b0; b < b1; ++b) t.c3 = carry_op(t.c3, c3s[b]);
+    block_excl_scan_t(t, &bp, DAGG_ID);
+  } else {
+    bp = load_blk(a, blockIdx.x);
+  }
+  {
+    const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
+    const bool live = k < a.n_frames;
+    FrameRec r = {0ull, 0u, 0u, 0u, 0u};
+    DAgg v = DAGG_ID;
+    wsg_session_state st = {};
+    bool first = false;
+    if (live) {
+      r = a.rec[k];
+      const uint32_t l3 = (code_is_data(r.code) && r.len && !(r.code & CODE_FIN)) ? a.edge[a.n_frames + k] : 0u;
+      first = k == a.session_first[r.sess];
+      st = a.state[r.sess];
+      v = frame_agg(k, r, l3, first, a.state);
+    }
+    DAgg tot;
+    DAgg ex = agg_op(bp, block_excl_scan_t(v, &tot, DAGG_ID));
+    if (a.fused_scan && blockIdx.x + 1 == a.nblk && threadIdx.x == 0) *a.total = bp.sum + tot.sum;
+    uint32_t validate = 0;
+    if (live) {
+      const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
+      const uint32_t s = r.sess;
+      const int32_t sf = (int32_t)a.session_first[s];
+      const uint32_t op = code_op(r.code);
+      uint32_t frag_err = 0;
+      bool text = false;
+      if (!code_pre(r.code)) {
+        // FrameDecoder.fragmentation before this frame: FIN of the previous data frame
+        const bool frag = jd >= sf ? !(ex.m0 & 1) : (st.fragmentation != 0);
+        if (!a.validator_only) frag_err = rules_frag(op, frag);
+        if (a.validate) {
+          text = op == WSG_OP_TEXT;
+          if (op == WSG_OP_CONTINUATION) text = jm >= sf ? (ex.m1 & 1) != 0 : (st.text_open != 0);
+        }
+      }
+      // the frame's status in the reference's check order (header rules, fragmentation,
+      // lengths / close, then the validator); a failed frame is never validated
+      uint32_t status = code_pre(r.code) ? code_pre(r.code) : (frag_err ? frag_err : code_post(r.code));
+      if (!status && ex.sum + r.len > a.n_pieces * PIECE) status = WSG_E_BATCH;  // slots beyond the piece grid
+      // a validated continuation's head against the message carry (the inherited
+      // validator state: the session tail for its first frame)
+      if (!status && text && op == WSG_OP_CONTINUATION &&
+          seam_utf8_error(first ? tail_c3(st) : ex.c3, a.edge[k], r.len, (r.code & CODE_FIN) != 0))
+        status = WSG_E_TEXT_UTF8;
+      validate = (text && !status) ? 1u : 0u;
+      a.vflag[k] = (uint8_t)validate;
+      wsg_frame_desc d;
+      d.payload_off = ex.sum;
+      d.payload_len = r.len;
+      d.opcode = (uint8_t)op;
+      d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4) |
+                          ((r.code & CODE_MASKED) ? 1u : 0u));
+      d.status = (uint16_t)status;
+      a.desc[k] = d;
+      if (status) atomicMin((unsigned long long*)&a.sess_err[s], (unsigned long long)k);
+      // the session's last frame: what k_final needs for the carry-out state (the last
+      // data frame, the last message start, the validator carry through this frame)
+      if (k + 1 == a.session_first[s + 1]) {
+        a.slink[s] = code_is_data(r.code) ? (int32_t)k : jd;
+        a.slink[a.n_sessions + s] = code_is_start(r.code) ? (int32_t)k : jm;
+        a.slink[2 * a.n_sessions + s] = (int32_t)(first ? v.c3 : carry_op(ex.c3, v.c3));
+      }
+    }
+    // Descriptors of the pieces whose first output byte falls in a frame's slot,
+    // written cooperatively: the wave's pieces are contiguous, lane i writes the
+    // wave's pieces i, i+64, ... (coalesced 16-B stores) after finding the owning
+    // frame with a shuffle search over the exclusive piece counts.
+    const uint64_t slot = live ? (uint64_t)((r.len + 15u) & ~15u) : 0ull;
+    const uint64_t slot_end = ex.sum + slot;
+    const uint32_t pc0 = (uint32_t)((ex.sum + PIECE - 1) / PIECE);
+    const uint32_t cnt = slot ? (uint32_t)((slot_end + PIECE - 1) / PIECE) - pc0 : 0u;
+    uint32_t cum = cnt;  // inclusive wave scan of the counts
+#pragma unroll
+    for (int sd = 1; sd < 64; sd <<= 1) {
+      const uint32_t t = (uint32_t)__shfl_up((int)cum, sd, 64);
+      if (lane >= sd) cum += t;
+    }
+    const uint32_t T = (uint32_t)__shfl((int)cum, 63, 64);
+    cum -= cnt;  // exclusive
+    if (!T) return;
+    // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31
+    const uint32_t fk = (uint32_t)k | (validate ? 0x80000000u : 0u) | ((live && (r.code & CODE_FIN)) ? 0x40000000u : 0u);
+    const bool cont = live && code_op(r.code) == WSG_OP_CONTINUATION;
+    for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
+      int o = 0;
+#pragma unroll
+      for (int step = 32; step >= 1; step >>= 1)
+        if ((uint32_t)__shfl((int)cum, o + step, 64) <= t) o += step;
+      const uint32_t o_cum = (uint32_t)__shfl((int)cum, o, 64);
+      const uint32_t o_pc0 = (uint32_t)__shfl((int)pc0, o, 64);
+      const uint64_t o_out = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex.sum >> 32), o, 64) << 32) |
+                             (uint32_t)__shfl((int)(uint32_t)ex.sum, o, 64);
+      const uint64_t o_src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(r.src >> 32), o, 64) << 32) |
+                             (uint32_t)__shfl((int)(uint32_t)r.src, o, 64);
+      const uint32_t o_len = (uint32_t)__shfl((int)r.len, o, 64);
+      const uint32_t o_mask = (uint32_t)__shfl((int)r.mask, o, 64);
+      const uint32_t o_fk = (uint32_t)__shfl((int)fk, o, 64);
+      const bool o_cont = __shfl((int)cont, o, 64) != 0;
+      if (t >= T) continue;
+      const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
+      if (pc >= a.n_pieces) continue;  // beyond the grid: the frame failed with WSG_E_BATCH above
+      const uint64_t ps = pc * PIECE;
+      const uint64_t o_end = o_out + ((o_len + 15u) & ~15u);
+      const uint32_t j0 = (uint32_t)(ps - o_out);
+      const uint32_t left = o_len - j0;
+      // runs past its frame's slot: other frames' bytes follow, unless it is the batch's
+      // last frame (a slot ending the payload region)
+      const bool single = o_end >= ps + PIECE || (uint64_t)(o_fk & 0x3fffffffu) + 1 == a.n_frames;
+      PieceDesc d;
+      d.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) |
+               ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI) |
+               (left <= PIECE ? PD_LAST : 0ull) | ((o_fk & 0x40000000u) ? PD_FIN : 0ull);
+      d.mask = o_mask;
+      d.frame = (o_fk & PDF_INDEX) | (o_cont ? PDF_CONT : 0u);
+      a.pieces[pc] = d;
+    }
+  }
 }
 
 // ------------------------------------------------------------------ k_pieces
@@ -568,7 +594,7 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
   const uint32_t pw = dpp_from_prev(w[3], first_prev);
   uint32_t f0 = utf8_err_word_raw(w[0], pw), f1 = utf8_err_word_raw(w[1], w[0]);
   uint32_t f2 = utf8_err_word_raw(w[2], w[1]), f3 = utf8_err_word_raw(w[3], w[2]);
-  // a continuation's bytes 0..2 are checked against the message carry (k_seams); a
+  // a continuation's bytes 0..2 are checked against the message carry (k_link); a
   // message start has no carry, and the zero word before it is exact
   const bool cont_head = lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT);
   if (cont_head) f0 &= 0x80000000u;
@@ -577,7 +603,7 @@ __device__ __forceinline__ uint32_t piece_fast(const DecodeArgs& a, const PieceD
   }
   uint32_t te = 0;
   if ((d.info & PD_LAST) && keep >= 1 && keep <= 16) {
-    const bool whole = !(cont_head && keep < 3);  // (a short continuation ends on the carry: k_seams)
+    const bool whole = !(cont_head && keep < 3);  // (a short continuation ends on the carry: k_link)
     te = tail_error(last3(pw, w[0], w[1], w[2], w[3], keep), whole && (d.info & PD_FIN)) ? 1u : 0u;
   }
   return ((f0 | f1 | f2 | f3) & H80) | te;
@@ -599,7 +625,8 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
   const bool live = my < pend;
   const uint32_t fr0 = d.frame & PDF_INDEX;
   uint32_t lk = fr0;  // frame owning this lane's 16 output bytes
-  FrameRec lr;
+  uint64_t lout;       // its slot (desc: k_link's payload_off / payload_len)
+  uint32_t llen;
   {
     // lane-parallel lookup: lane l takes record d.frame + l and the 16-B chunk of the
     // piece where that frame's slot starts (0 for the piece's first frame, 64 past
@@ -607,8 +634,10 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
     // chunk i is the last lane whose chunk is <= i: a 6-step search over shuffles
     const uint64_t fl = (uint64_t)fr0 + (uint64_t)lane;
     const bool have = fl < a.n_frames;
-    const uint64_t fs = have ? a.rec[fl].out_off : ~0ull;
-    const uint64_t fslot = have ? (uint64_t)((a.rec[fl].len + 15u) & ~15u) : 0ull;
+    wsg_frame_desc fd = {};
+    if (have) fd = a.desc[fl];
+    const uint64_t fs = have ? fd.payload_off : ~0ull;
+    const uint64_t fslot = have ? (uint64_t)((fd.payload_len + 15u) & ~15u) : 0ull;
     if (__any(have && fslot && fs + fslot >= pend)) {  // the 64 records reach the piece end
       const int c = fs >= pend ? 64 : (fs <= pstart ? 0 : (int)((fs - pstart) >> 4));
       int pos = 0;
@@ -616,24 +645,27 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
       for (int step = 32; step >= 1; step >>= 1)
         if (__shfl(c, pos + step, 64) <= lane) pos += step;
       lk = fr0 + (uint32_t)pos;
-      lr = a.rec[lk];  // just loaded by lane pos: a cache hit
+      lout = (uint64_t)__shfl((int)(uint32_t)fs, pos, 64) | ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(fs >> 32), pos, 64) << 32);
+      llen = (uint32_t)__shfl((int)fd.payload_len, pos, 64);
     } else {  // more than 64 frames (empty ones) in the piece: walk the records
       uint32_t kk = fr0;
-      FrameRec rr = a.rec[kk];
-      lr = rr;
-      uint64_t send = rr.out_off + ((rr.len + 15u) & ~15u);
+      wsg_frame_desc rd = a.desc[kk];
+      lout = rd.payload_off;
+      llen = rd.payload_len;
+      uint64_t send = rd.payload_off + ((rd.payload_len + 15u) & ~15u);
       for (;;) {
         const bool beyond = live && my >= send;
         if (!__any(beyond)) break;
         ++kk;
-        rr = a.rec[kk];
-        if (beyond) { lk = kk; lr = rr; }
-        send = rr.out_off + ((rr.len + 15u) & ~15u);
+        rd = a.desc[kk];
+        if (beyond) { lk = kk; lout = rd.payload_off; llen = rd.payload_len; }
+        send = rd.payload_off + ((rd.payload_len + 15u) & ~15u);
       }
     }
   }
-  const uint32_t j = (uint32_t)(my - lr.out_off);
-  const int keep = live ? (int)lr.len - (int)j : 0;
+  const FrameRec lr = a.rec[lk];  // (src, mask, code: k_parse's record)
+  const uint32_t j = (uint32_t)(my - lout);
+  const int keep = live ? (int)llen - (int)j : 0;
   uint32_t w[4] = {0u, 0u, 0u, 0u};
   if (live) {
     const uint64_t s = lr.src + j;
@@ -653,7 +685,7 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
     for (int i = 0; i < 4; ++i) w[i] = keep_bytes(alignbyte(dd[i + 1], dd[i], sh) ^ lr.mask, keep - 4 * i);
     if (ST) __builtin_amdgcn_raw_buffer_store_b128((u32x4){w[0], w[1], w[2], w[3]}, rout, (uint32_t)lane * 16u, 0, aux);
   }
-  const bool lval = live && (lr.code & CODE_VALIDATE);
+  const bool lval = live && a.vflag[lk];
   if (__any(lval)) {
     uint32_t pw = dpp_from_prev(w[3], 0u);
     const uint32_t prev_k = (uint32_t)__builtin_amdgcn_update_dpp((int)0xffffffffu, (int)lk, 0x138, 0xf, 0xf, false);
@@ -663,7 +695,7 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
       const bool cont = code_op(lr.code) == WSG_OP_CONTINUATION;
       uint32_t e0 = utf8_err_word_raw(w[0], pw), e1 = utf8_err_word_raw(w[1], w[0]);
       uint32_t e2 = utf8_err_word_raw(w[2], w[1]), e3 = utf8_err_word_raw(w[3], w[2]);
-      if (j == 0 && cont) e0 &= 0x80000000u;  // a continuation's head: k_seams
+      if (j == 0 && cont) e0 &= 0x80000000u;  // a continuation's head: k_link
       e0 &= keep_flags(keep); e1 &= keep_flags(keep - 4); e2 &= keep_flags(keep - 8); e3 &= keep_flags(keep - 12);
       const bool te = keep >= 1 && keep <= 16 &&
                       tail_error(last3(pw, w[0], w[1], w[2], w[3], keep),
@@ -798,7 +830,7 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
     uint32_t f0 = utf8_err_word_raw(w[i][0], pw), f1 = utf8_err_word_raw(w[i][1], w[i][0]);
     uint32_t f2 = utf8_err_word_raw(w[i][2], w[i][1]), f3 = utf8_err_word_raw(w[i][3], w[i][2]);
     const bool cont_head = i == 0 && lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT);
-    if (cont_head) f0 &= 0x80000000u;  // a continuation's bytes 0..2: k_seams
+    if (cont_head) f0 &= 0x80000000u;  // a continuation's bytes 0..2: k_link
     if (i + 1 == N && !full) {
       f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
     }
@@ -848,18 +880,6 @@ __global__ __launch_bounds__(64) void k_piecesN(DecodeArgs a) {
   }
 }
 
-// ------------------------------------------------------------------ k_seams
-// The validated continuation frames k_link listed: their first (<= 3) bytes against
-// the message carry, and the end of a FIN message shorter than 3 bytes in this
-// frame (FrameUtf8Validator.java:78-96 at the fragment seams).  Every other
-// verdict is already in desc (k_link: header / fragmentation / length rules;
-// k_pieces: UTF-8 inside frames).  A batch of unfragmented messages lists none.
-__global__ __launch_bounds__(BLOCK) void k_seams(DecodeArgs a) {
-  if (threadIdx.x >= a.n_seams[blockIdx.x]) return;  // (k_link block b's entries)
-  const uint32_t k = a.seams[(uint64_t)blockIdx.x * BLOCK + threadIdx.x];
-  if (a.desc[k].status == 0 && edge_utf8_error(a, k, a.rec[k])) report_utf8(a, k);
-}
-
 // ------------------------------------------------------------------ k_final
 __device__ int64_t error_detail(const DecodeArgs& a, uint64_t k, uint32_t err) {
   if (a.validator_only) return 0;  // (no wire headers: only the validator's 1007, which has no argument)
@@ -901,35 +921,21 @@ __global__ __launch_bounds__(256) void k_final(DecodeArgs a) {
     st.closed = 1;
   } else {
     res.n_delivered = se - sf;
-    if (se > sf) {
-      const uint64_t last = se - 1;
-      const uint32_t cl = a.rec[last].code;
-      const int32_t ld = code_is_data(cl) ? (int32_t)last : a.prev[last];
+    if (se > sf) {  // k_link's record of the session's last frame
+      const int32_t ld = a.slink[s];                          // last data frame
       if (ld >= (int32_t)sf) {
         const bool frag = !(a.rec[ld].code & CODE_FIN);
         st.fragmentation = frag;
         bool text = false;
-        int32_t ls = -1;
         if (a.validate && frag) {
-          ls = code_is_start(cl) ? (int32_t)last : a.prev[a.n_frames + last];
+          const int32_t ls = a.slink[a.n_sessions + s];         // last message start
           text = ls >= (int32_t)sf ? code_op(a.rec[ls].code) == WSG_OP_TEXT : (st.text_open != 0);
         }
-        if (text) {  // tail = last <= 3 bytes of the open text message
-          uint8_t rev[3];
-          uint32_t n = 0;
-          const bool in_batch = ls >= (int32_t)sf;
-          const int32_t lo = in_batch ? ls : (int32_t)sf;
-          int32_t j = (code_is_data(cl) && a.rec[last].len) ? (int32_t)last : a.prev[2 * a.n_frames + last];
-          while (n < 3 && j >= lo) {
-            const uint32_t lj = a.rec[j].len, l3 = a.edge[a.n_frames + j];
-            const uint32_t have = lj < 3 ? lj : 3;
-            for (uint32_t i = 0; i < have && n < 3; ++i) rev[n++] = (uint8_t)(l3 >> (8 * (2 - i)));
-            j = a.prev[2 * a.n_frames + j];
-          }
-          if (n < 3 && !in_batch)
-            for (uint32_t i = 0; i < st.tail_len && n < 3; ++i) rev[n++] = st.tail[st.tail_len - 1 - i];
+        if (text) {  // tail = last <= 3 bytes of the open text message: the validator carry
+          const uint32_t c3 = (uint32_t)a.slink[2 * a.n_sessions + s];
+          const uint32_t n = (c3 >> 24) & 3u;
+          for (uint32_t i = 0; i < n; ++i) st.tail[i] = (uint8_t)(c3 >> (24 - 8 * (n - i)));
           st.tail_len = (uint8_t)n;
-          for (uint32_t i = 0; i < n; ++i) st.tail[i] = rev[n - 1 - i];
         } else {
           st.tail_len = 0;
         }
@@ -943,13 +949,13 @@ __global__ __launch_bounds__(256) void k_final(DecodeArgs a) {
 
 // ------------------------------------------------------------------ launchers
 void launch_parse(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_parse, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_parse, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
 void launch_scan(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, a);
 }
 void launch_link(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
   // one 64-lane workgroup per two pieces, nontemporal loads/stores, XCD-aware
@@ -958,7 +964,7 @@ void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) 
                      dim3((uint32_t)((n_pieces_bound + PIECES_PER_WAVE - 1) / PIECES_PER_WAVE)), dim3(64), 0, s, a);
 }
 void launch_vparse(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_vparse, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_vparse, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
 void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
   // validate only: the piece kernel with its stores compiled out (NT bit 2)
@@ -966,9 +972,6 @@ void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound)
   // VPIECES_PER_WAVE KiB)
   hipLaunchKernelGGL((k_piecesN<5, 1, VPIECES_PER_WAVE>),
                      dim3((uint32_t)((n_pieces_bound + VPIECES_PER_WAVE - 1) / VPIECES_PER_WAVE)), dim3(64), 0, s, a);
-}
-void launch_seams(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_seams, dim3(a.nblk), dim3(BLOCK), 0, s, a);
 }
 void launch_final(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);

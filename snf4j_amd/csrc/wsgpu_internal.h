@@ -9,10 +9,10 @@
 
 namespace ws {
 
-// Per-frame record of the decode pipeline (32 B, one scalar load per frame).
+// Per-frame record of the decode pipeline (24 B, written once by k_parse; k_link's
+// per-frame outputs are the frame's wsg_frame_desc and vflag).
 struct FrameRec {
   uint64_t src;      // absolute wire offset of the payload
-  uint64_t out_off;  // payload slot offset in payload_out (16-B aligned), set by k_link
   uint32_t len;      // payload length (0 when the header failed a rule)
   uint32_t mask;     // mask key, little-endian u32 of the 4 wire bytes
   uint32_t code;     // packed: see CODE_*
@@ -23,7 +23,6 @@ struct FrameRec {
 constexpr uint32_t CODE_PRE_SHIFT = 0;      // 5 bits: rule error before the fragmentation test
 constexpr uint32_t CODE_POST_SHIFT = 5;     // 5 bits: length / close rules after it
 constexpr uint32_t CODE_FRAG_SHIFT = 10;    // 5 bits: fragmentation error (k_link)
-constexpr uint32_t CODE_VALIDATE = 1u << 15;  // frame belongs to a text message (k_link)
 constexpr uint32_t CODE_FIN = 1u << 16;
 constexpr uint32_t CODE_RSV_SHIFT = 17;     // 3 bits
 constexpr uint32_t CODE_MASKED = 1u << 20;
@@ -38,7 +37,8 @@ __host__ __device__ inline bool code_is_start(uint32_t c) {
   return (code_op(c) == 1u || code_op(c) == 2u) && !code_pre(c);
 }
 
-constexpr int BLOCK = 256;  // frames per block in the parse / link passes
+constexpr int BLOCK = 256;    // frames per block in the encode / aggregate passes
+constexpr int DBLOCK = 256;   // frames (threads) per block in the decode parse / link passes
 constexpr uint32_t PIECE = 1024;  // payload-output bytes per wave in k_pieces (64 lanes x 16 B)
 constexpr int PIECES_PER_WAVE = 2; // pieces one k_piecesN wave takes (tools/ubench_unmask)
 constexpr int VPIECES_PER_WAVE = 4;  // validate-only mode (read-only stream)
@@ -59,7 +59,7 @@ struct PieceDesc {
   uint32_t frame; // frame index | PDF_CONT
 };
 constexpr uint32_t PDF_INDEX = 0x3fffffffu;  // PieceDesc.frame: the frame index
-constexpr uint32_t PDF_CONT = 0x80000000u;   // the frame is a continuation (its head is k_seams')
+constexpr uint32_t PDF_CONT = 0x80000000u;   // the frame is a continuation (its head is k_link's)
 constexpr uint64_t PD_SRC_MASK = (1ull << 48) - 1;
 constexpr uint32_t PD_NB_SHIFT = 48;
 constexpr uint64_t PD_VALIDATE = 1ull << 59;
@@ -90,23 +90,22 @@ struct DecodeArgs {
   wsg_session_result* result;
   // workspace
   FrameRec* rec;
-  int32_t* prev;       // [3][n_frames]: last data / last TEXT|BINARY / last nonempty data frame before k
-                       // (not written for a FIN TEXT/BINARY frame: no reader needs it)
+  uint8_t* vflag;      // [n_frames]: the frame is validated (a text-message frame that passed every rule)
+  int32_t* slink;      // [3][n_sessions]: of the session's last frame, the last data frame, the last
+                       // message start (<= it) and the validator carry through it (k_link -> k_final)
   uint32_t* edge;      // [2][n_frames]: first 3 / last 3 payload bytes (unmasked); the last 3 only
                        // for non-FIN data frames (the carry into the next fragment or batch)
   uint64_t* blk_sum;   // [nblk] slot-bytes per block -> exclusive prefix
-  int32_t* blk_max;    // [3][nblk] per-block max indices -> exclusive prefix max
+  int32_t* blk_max;    // [4][nblk] per-block max indices and UTF-8 carry -> exclusive prefix
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
   uint64_t* total;     // [1] total payload slot bytes
   struct PieceDesc* pieces;  // [piece_bound]: per-piece work descriptor (k_link)
-  uint32_t* seams;     // [nblk * BLOCK]: validated continuation frames, k_link block b's at b * BLOCK
-  uint32_t* n_seams;   // [nblk]: entries of k_link block b
   uint64_t n_pieces;   // pieces the grid covers (piece_bound): slots beyond are a malformed batch
   uint32_t nblk;
   int32_t fused_scan;  // k_link reduces the block aggregates itself (nblk <= FUSED_SCAN_MAX_BLOCKS)
 };
 
-// grids up to this many parse/link blocks skip the k_scan launch
+// grids up to this many parse/link blocks (DBLOCK frames each) skip the k_scan launch
 constexpr uint32_t FUSED_SCAN_MAX_BLOCKS = 4096;
 
 struct EncodeArgs {
@@ -201,7 +200,7 @@ struct InflTokStat {
 
 // kernel ids for timing
 enum KernelId {
-  K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_SEAMS, K_FINAL,
+  K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
   K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_COUNT
 };
 
@@ -212,7 +211,6 @@ void launch_link(const DecodeArgs& a, hipStream_t s);
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
 void launch_vparse(const DecodeArgs& a, hipStream_t s);
 void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound);
-void launch_seams(const DecodeArgs& a, hipStream_t s);
 void launch_final(const DecodeArgs& a, hipStream_t s);
 
 void launch_enc_len(const EncodeArgs& a, hipStream_t s);

@@ -30,47 +30,62 @@ __device__ __forceinline__ Agg agg_op(const Agg& x, const Agg& y) {
   return r;
 }
 
-__device__ __forceinline__ Agg wave_incl_scan(Agg v) {
+__device__ __forceinline__ Agg agg_shfl_up(const Agg& v, int d) {
+  Agg t;
+  t.sum = shfl_up_u64(v.sum, d);
+  t.m0 = __shfl_up(v.m0, d, 64);
+  t.m1 = __shfl_up(v.m1, d, 64);
+  t.m2 = __shfl_up(v.m2, d, 64);
+  return t;
+}
+
+constexpr Agg AGG_ID = {0ull, -1, -1, -1};
+
+// Scans over any element type T with agg_op(T, T) (associative, applied in frame
+// order: it need not commute) and agg_shfl_up(T, d).
+template <class T>
+__device__ __forceinline__ T wave_incl_scan(T v) {
   const int lane = threadIdx.x & 63;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    Agg t;
-    t.sum = shfl_up_u64(v.sum, d);
-    t.m0 = __shfl_up(v.m0, d, 64);
-    t.m1 = __shfl_up(v.m1, d, 64);
-    t.m2 = __shfl_up(v.m2, d, 64);
+    const T t = agg_shfl_up(v, d);
     if (lane >= d) v = agg_op(t, v);
   }
   return v;
 }
 
-constexpr Agg AGG_ID = {0ull, -1, -1, -1};
-
 // Block-wide exclusive scan; nthreads = blockDim.x (multiple of 64, <= 1024).
-__device__ inline Agg block_excl_scan(Agg v, Agg* total) {
-  __shared__ Agg wsum[16];
+template <class T>
+__device__ inline T block_excl_scan_t(T v, T* total, const T id) {
+  __shared__ T wsum[16];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  Agg inc = wave_incl_scan(v);
+  T inc = wave_incl_scan(v);
   if (lane == 63) wsum[wid] = inc;
   __syncthreads();
-  Agg pre = AGG_ID, tot = AGG_ID;
+  T pre = id, tot = id;
   for (int i = 0; i < nw; ++i) {
     if (i < wid) pre = agg_op(pre, wsum[i]);
     tot = agg_op(tot, wsum[i]);
   }
   __syncthreads();
   // exclusive within the wave: inclusive of lane-1
-  Agg ex;
-  ex.sum = shfl_up_u64(inc.sum, 1);
-  ex.m0 = __shfl_up(inc.m0, 1, 64);
-  ex.m1 = __shfl_up(inc.m1, 1, 64);
-  ex.m2 = __shfl_up(inc.m2, 1, 64);
-  if (lane == 0) ex = AGG_ID;
+  T ex = agg_shfl_up(inc, 1);
+  if (lane == 0) ex = id;
   *total = tot;
   return agg_op(pre, ex);
 }
 
-// session owning frame k: largest s with session_first[s] <= k
+__device__ inline Agg block_excl_scan(Agg v, Agg* total) { return block_excl_scan_t(v, total, AGG_ID); }
+
+// session owning frame k: largest s in [lo, hi] with session_first[s] <= k
+__device__ __forceinline__ uint32_t find_session_in(const uint32_t* sf, uint32_t lo, uint32_t hi, uint64_t k) {
+  while (lo < hi) {
+    uint32_t mid = (lo + hi + 1) >> 1;
+    if ((uint64_t)sf[mid] <= k) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
 __device__ __forceinline__ uint32_t find_session(const uint32_t* sf, uint32_t n_sessions, uint64_t k) {
   uint32_t lo = 0, hi = n_sessions ? n_sessions - 1 : 0;
   while (lo < hi) {

@@ -51,15 +51,17 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&a.state, S * 8)); CK(hipMemset(a.state, 0, S * 8));
   a.payload_out = payload;
   CK(hipMalloc(&a.desc, F * 16)); CK(hipMalloc(&a.result, S * 16));
-  a.nblk = (uint32_t)((F + 255) / 256);
-  CK(hipMalloc(&a.rec, F * sizeof(ws::FrameRec))); CK(hipMalloc(&a.prev, 3 * F * 4)); CK(hipMalloc(&a.edge, 2 * F * 4));
-  CK(hipMalloc(&a.blk_sum, a.nblk * 8)); CK(hipMalloc(&a.blk_max, 3 * a.nblk * 4));
+  a.nblk = (uint32_t)((F + ws::DBLOCK - 1) / ws::DBLOCK);
+  CK(hipMalloc(&a.rec, F * sizeof(ws::FrameRec))); CK(hipMalloc(&a.vflag, F)); CK(hipMalloc(&a.slink, 3 * S * 4));
+  CK(hipMalloc(&a.edge, 2 * F * 4));
+  CK(hipMalloc(&a.blk_sum, a.nblk * 8)); CK(hipMalloc(&a.blk_max, 4 * a.nblk * 4));
   CK(hipMalloc(&a.sess_err, S * 8)); CK(hipMalloc(&a.total, 8));
   const uint64_t npb = ws::piece_bound(wire_len, F);
-  CK(hipMalloc(&a.pieces, (npb + 8) * sizeof(ws::PieceDesc))); CK(hipMalloc(&a.seams, (uint64_t)a.nblk * 256 * 4)); CK(hipMalloc(&a.n_seams, a.nblk * 4));
+  a.n_pieces = npb;
+  CK(hipMalloc(&a.pieces, (npb + 8) * sizeof(ws::PieceDesc)));
   CK(hipMemsetAsync(a.sess_err, 0xff, S * 8, st));
   ws::launch_parse(a, st); ws::launch_scan(a, st); ws::launch_link(a, st);
-  ws::launch_pieces(a, st, npb); ws::launch_seams(a, st); ws::launch_final(a, st);
+  ws::launch_pieces(a, st, npb); ws::launch_final(a, st);
   CK(hipStreamSynchronize(st));
   std::vector<uint8_t> res(S * 16);
   CK(hipMemcpy(res.data(), a.result, S * 16, hipMemcpyDeviceToHost));
@@ -75,7 +77,7 @@ int main(int argc, char** argv) {
   std::vector<V> vs = {
       {"copy16 g=8192", 0, 8192}, {"pieces nt W1", 13, 0}, {"pieces nt W1 xcd", 14, 0},
       {"piecesN2 xcd", 18, 0}, {"piecesN4 xcd", 19, 0}, {"piecesN3 xcd", 24, 0}, {"piecesN4", 25, 0},
-      {"parse", 20, 0}, {"scan", 23, 0}, {"link", 21, 0}, {"seams", 22, 0},  // pipeline order
+      {"parse", 20, 0}, {"scan", 23, 0}, {"link", 21, 0},  // pipeline order
   };
   std::vector<double> best(vs.size(), 1e30), sum(vs.size(), 0);
   const int rounds = 8;
@@ -107,8 +109,6 @@ int main(int argc, char** argv) {
         ws::launch_parse(a, st);
       } else if (vs[i].kind == 21) {
         ws::launch_link(a, st);
-      } else if (vs[i].kind == 22) {
-        ws::launch_seams(a, st);
       } else if (vs[i].kind == 23) {
         ws::launch_scan(a, st);
       }
