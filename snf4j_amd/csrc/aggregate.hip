@@ -19,14 +19,16 @@
 //                of member bytes and emitted frames
 //   k_agg_c      thread per frame: "too big" test, output descriptors, gather
 //                records, and the 1 KiB agg_out pieces starting in each member
-//   k_agg_gather one wave per 1 KiB piece of agg_out (grid-stride: the piece count
-//                is known only on the device): 16-B aligned stores, sources
-//                funnelled from aligned loads
+//   k_agg_gather one wave per AGG_PIECES_PER_WAVE 1 KiB pieces of agg_out (grid-stride:
+//                the piece count is known only on the device): 16-B aligned
+//                stores, sources funnelled from aligned loads
 //   k_agg_final  thread per session: result, carry-out state, PENDING entry
 #include "wsgpu_internal.h"
 #include "wsgpu_scan.h"
 
 namespace ws {
+
+constexpr int AGG_PIECES_PER_WAVE = 2;
 
 constexpr uint32_t AG_VALID = 1u;    // delivered by the decoder (the aggregator sees it)
 constexpr uint32_t AG_START = 2u;    // TEXT/BINARY, not FIN: opens (or replaces) the aggregated frame
@@ -312,98 +314,155 @@ __device__ __forceinline__ void ag_load16(const AggArgs& a, uint64_t s, uint64_t
   for (int i = 0; i < 4; ++i) w[i] = alignbyte(dd[i + 1], dd[i], sh);
 }
 
+// A piece spanning several members: lane l takes member record d.frame + l (records
+// are the non-empty members, dense and in order), and the owner of byte o is the
+// last record starting at or before o, found by a shuffle search.
+// (the record load is issued with the other pieces' loads: ag_multi_rec)
+__device__ __forceinline__ AggRec ag_multi_rec(const AggArgs& a, const PieceDesc d, uint64_t n_mem, int lane) {
+  const uint64_t fl = (uint64_t)d.frame + (uint64_t)lane;
+  AggRec rl;
+  if (fl < n_mem) rl = a.rec[fl];
+  else { rl.pos = ~0ull; rl.mlen = 0; rl.src = 0; }
+  return rl;
+}
+__device__ void ag_piece_multi(const AggArgs& a, const PieceDesc d, const AggRec rl, uint64_t ps, uint64_t lim,
+                               uint64_t n_mem, uint64_t src_lim, int lane) {
+  const uint64_t o = ps + (uint64_t)lane * 16u;
+  uint32_t w[4] = {0u, 0u, 0u, 0u};
+  const uint64_t pend = ps + PIECE < lim ? ps + PIECE : lim;
+  const bool live = o < pend;
+  const bool have = (uint64_t)d.frame + (uint64_t)lane < n_mem;
+  uint32_t lk = d.frame;
+  AggRec lr;
+  if (__any(have && rl.mlen && rl.pos + rl.mlen >= pend)) {
+    const int key = rl.pos >= pend ? 4096 : (rl.pos <= ps ? 0 : (int)(rl.pos - ps));
+    int posn = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+      if (__shfl(key, posn + step, 64) <= lane * 16) posn += step;
+    lk = d.frame + (uint32_t)posn;
+    // the owner's record: lane posn holds it
+    lr.pos = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rl.pos >> 32), posn, 64) << 32) |
+             (uint32_t)__shfl((int)(uint32_t)rl.pos, posn, 64);
+    lr.src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rl.src >> 32), posn, 64) << 32) |
+             (uint32_t)__shfl((int)(uint32_t)rl.src, posn, 64);
+    lr.mlen = (uint32_t)__shfl((int)rl.mlen, posn, 64);
+  } else {  // more than 64 records (empty ones) reach into the piece: walk them
+    uint32_t kk = d.frame;
+    AggRec rr = a.rec[kk];
+    lr = rr;
+    for (;;) {
+      const bool beyond = live && o >= rr.pos + rr.mlen;
+      if (!__any(beyond) || kk + 1 >= n_mem) break;
+      ++kk;
+      rr = a.rec[kk];
+      if (beyond && rr.mlen) { lk = kk; lr = rr; }
+    }
+  }
+  if (!live) return;
+  // the lane's 16 bytes may span members: byte-wise over consecutive records
+  if (o >= lr.pos && o + 16 <= lr.pos + lr.mlen) {
+    // two aligned 16-B blocks and a per-lane funnel (the shift differs per member)
+    const uint64_t sa = lr.src + (o - lr.pos);
+    const uint64_t a16 = sa & ~15ull;
+    if (a16 + 32u <= src_lim) {
+      const u32x4 A = *(const u32x4*)(a.payload + a16), B = *(const u32x4*)(a.payload + a16 + 16u);
+      const uint32_t q = (uint32_t)(sa >> 2) & 3u, b = (uint32_t)sa & 3u;
+      const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
+      uint32_t x[5];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) x[i] = q == 0 ? W[i] : (q == 1 ? W[i + 1] : (q == 2 ? W[i + 2] : W[i + 3]));
+#pragma unroll
+      for (int i = 0; i < 4; ++i) w[i] = alignbyte(x[i + 1], x[i], b);
+    } else {
+      ag_load16(a, sa, src_lim, w);
+    }
+  } else {
+    uint64_t blo = 0, bhi = 0;
+    uint32_t kk = lk;
+    AggRec rr = lr;
+    for (uint32_t i = 0; i < 16u; ++i) {
+      const uint64_t x = o + i;
+      if (x >= pend) break;
+      while (x >= rr.pos + rr.mlen && kk + 1 < n_mem) rr = a.rec[++kk];
+      const uint64_t byte = a.payload[rr.src + (x - rr.pos)];
+      if (i < 8) blo |= byte << (8 * i);
+      else bhi |= byte << (8 * (i - 8));
+    }
+    w[0] = (uint32_t)blo; w[1] = (uint32_t)(blo >> 32); w[2] = (uint32_t)bhi; w[3] = (uint32_t)(bhi >> 32);
+  }
+  ag_store16(a, o, pend, w);
+}
+
+// One wave per N consecutive 1 KiB pieces of agg_out, grid-stride over the piece
+// groups: the next group's descriptors are loaded a group ahead, and every piece's
+// first loads (its source blocks, or a multi-member piece's records) are issued
+// before any piece is finished — the kernel is latency-bound.
+template <int N>
 __global__ __launch_bounds__(64) void k_agg_gather(AggArgs a, uint64_t src_lim) {
   const int lane = threadIdx.x;
   const uint64_t total = *a.agg_total;
   const uint64_t lim = total < a.agg_cap ? total : a.agg_cap;
   const uint64_t np = (lim + PIECE - 1) / PIECE;
+  const uint64_t nq = (np + N - 1) / N;
   const uint64_t n_mem = *a.n_mem;
-  for (uint64_t p = blockIdx.x; p < np; p += gridDim.x) {
-    const PieceDesc d = a.pieces[p];
-    const uint64_t ps = p * PIECE;
-    const uint64_t o = ps + (uint64_t)lane * 16u;
-    uint32_t w[4] = {0u, 0u, 0u, 0u};
-    if (!(d.info & PD_MULTI)) {  // the piece lies in one member's bytes
-      const uint64_t s = d.info & PD_SRC_MASK;
-      const uint32_t nb = (uint32_t)(d.info >> PD_NB_SHIFT) & 2047u;
-      const uint64_t a16 = s & ~15ull;
-      const uint32_t sh = (uint32_t)(s & 15u), b = sh & 3u;
-      u32x4 A, nx;
-      if (a16 + PIECE + 16u <= src_lim) {
-        A = *(const u32x4*)(a.payload + a16 + (uint64_t)lane * 16u);
-        nx = *(const u32x4*)(a.payload + a16 + PIECE);
-      } else {
-        uint32_t dd[4] = {0u, 0u, 0u, 0u}, ee[4] = {0u, 0u, 0u, 0u};
-        for (uint32_t i = 0; i < 16u; ++i) {
-          if (a16 + lane * 16u + i < src_lim) dd[i >> 2] |= (uint32_t)a.payload[a16 + lane * 16u + i] << (8 * (i & 3));
-          if (a16 + PIECE + i < src_lim) ee[i >> 2] |= (uint32_t)a.payload[a16 + PIECE + i] << (8 * (i & 3));
+  uint64_t q = blockIdx.x;
+  PieceDesc dn[N];  // the next group's descriptors, loaded a group ahead
+#pragma unroll
+  for (int i = 0; i < N; ++i) dn[i] = q * N + i < np ? a.pieces[q * N + i] : PieceDesc{PD_MULTI, 0u, 0u};
+  for (; q < nq; q += gridDim.x) {
+    PieceDesc d[N];
+    u32x4 A[N], nx[N];
+    AggRec rl[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) d[i] = dn[i];
+    const uint64_t qn = q + gridDim.x;
+#pragma unroll
+    for (int i = 0; i < N; ++i) dn[i] = qn * N + i < np ? a.pieces[qn * N + i] : PieceDesc{PD_MULTI, 0u, 0u};
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint64_t p = q * N + i;
+      if (p < np && (d[i].info & PD_MULTI)) rl[i] = ag_multi_rec(a, d[i], n_mem, lane);
+      if (p < np && !(d[i].info & PD_MULTI)) {  // the piece lies in one member's bytes
+        const uint64_t a16 = (d[i].info & PD_SRC_MASK) & ~15ull;
+        if (a16 + PIECE + 16u <= src_lim) {
+          A[i] = *(const u32x4*)(a.payload + a16 + (uint64_t)lane * 16u);
+          nx[i] = *(const u32x4*)(a.payload + a16 + PIECE);
+        } else {
+          uint32_t dd[4] = {0u, 0u, 0u, 0u}, ee[4] = {0u, 0u, 0u, 0u};
+          for (uint32_t b = 0; b < 16u; ++b) {
+            if (a16 + lane * 16u + b < src_lim) dd[b >> 2] |= (uint32_t)a.payload[a16 + lane * 16u + b] << (8 * (b & 3));
+            if (a16 + PIECE + b < src_lim) ee[b >> 2] |= (uint32_t)a.payload[a16 + PIECE + b] << (8 * (b & 3));
+          }
+          A[i] = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+          nx[i] = (u32x4){ee[0], ee[1], ee[2], ee[3]};
         }
-        A = (u32x4){dd[0], dd[1], dd[2], dd[3]};
-        nx = (u32x4){ee[0], ee[1], ee[2], ee[3]};
       }
-      const uint32_t W0 = A.x, W1 = A.y, W2 = A.z, W3 = A.w;
-      const uint32_t W4 = ag_dpp_from_next(A.x, nx.x), W5 = ag_dpp_from_next(A.y, nx.y);
-      const uint32_t W6 = ag_dpp_from_next(A.z, nx.z), W7 = ag_dpp_from_next(A.w, nx.w);
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) {
+      const uint64_t p = q * N + i;
+      if (p >= np) break;
+      const uint64_t ps = p * PIECE;
+      if (d[i].info & PD_MULTI) {
+        ag_piece_multi(a, d[i], rl[i], ps, lim, n_mem, src_lim, lane);
+        continue;
+      }
+      const uint64_t s = d[i].info & PD_SRC_MASK;
+      const uint32_t nb = (uint32_t)(d[i].info >> PD_NB_SHIFT) & 2047u;
+      const uint32_t sh = (uint32_t)(s & 15u), b = sh & 3u;
+      const uint32_t W0 = A[i].x, W1 = A[i].y, W2 = A[i].z, W3 = A[i].w;
+      const uint32_t W4 = ag_dpp_from_next(A[i].x, nx[i].x), W5 = ag_dpp_from_next(A[i].y, nx[i].y);
+      const uint32_t W6 = ag_dpp_from_next(A[i].z, nx[i].z), W7 = ag_dpp_from_next(A[i].w, nx[i].w);
+      uint32_t w[4];
       switch (sh >> 2) {  // wave-uniform
         case 0: w[0] = alignbyte(W1, W0, b); w[1] = alignbyte(W2, W1, b); w[2] = alignbyte(W3, W2, b); w[3] = alignbyte(W4, W3, b); break;
         case 1: w[0] = alignbyte(W2, W1, b); w[1] = alignbyte(W3, W2, b); w[2] = alignbyte(W4, W3, b); w[3] = alignbyte(W5, W4, b); break;
         case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
         default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
       }
-      if ((uint32_t)lane * 16u < nb) ag_store16(a, o, lim, w);
-      continue;
+      if ((uint32_t)lane * 16u < nb) ag_store16(a, ps + (uint64_t)lane * 16u, lim, w);
     }
-    // several members in the piece: lane l takes member record d.frame + l (records
-    // are the non-empty members, dense and in order), and the owner of byte o is the
-    // last record starting at or before o, found by a shuffle search
-    const uint64_t pend = ps + PIECE < lim ? ps + PIECE : lim;
-    const bool live = o < pend;
-    const uint64_t fl = (uint64_t)d.frame + (uint64_t)lane;
-    const bool have = fl < n_mem;
-    AggRec rl;
-    if (have) rl = a.rec[fl];
-    else { rl.pos = ~0ull; rl.mlen = 0; rl.src = 0; }
-    uint32_t lk = d.frame;
-    AggRec lr;
-    if (__any(have && rl.mlen && rl.pos + rl.mlen >= pend)) {
-      const int key = rl.pos >= pend ? 4096 : (rl.pos <= ps ? 0 : (int)(rl.pos - ps));
-      int posn = 0;
-#pragma unroll
-      for (int step = 32; step >= 1; step >>= 1)
-        if (__shfl(key, posn + step, 64) <= lane * 16) posn += step;
-      lk = d.frame + (uint32_t)posn;
-      lr = a.rec[lk];
-    } else {  // more than 64 records (empty ones) reach into the piece: walk them
-      uint32_t kk = d.frame;
-      AggRec rr = a.rec[kk];
-      lr = rr;
-      for (;;) {
-        const bool beyond = live && o >= rr.pos + rr.mlen;
-        if (!__any(beyond) || kk + 1 >= n_mem) break;
-        ++kk;
-        rr = a.rec[kk];
-        if (beyond && rr.mlen) { lk = kk; lr = rr; }
-      }
-    }
-    if (!live) continue;
-    // the lane's 16 bytes may span members: byte-wise over consecutive records
-    if (o >= lr.pos && o + 16 <= lr.pos + lr.mlen) {
-      ag_load16(a, lr.src + (o - lr.pos), src_lim, w);
-    } else {
-      uint64_t blo = 0, bhi = 0;
-      uint32_t kk = lk;
-      AggRec rr = lr;
-      for (uint32_t i = 0; i < 16u; ++i) {
-        const uint64_t x = o + i;
-        if (x >= pend) break;
-        while (x >= rr.pos + rr.mlen && kk + 1 < n_mem) rr = a.rec[++kk];
-        const uint64_t byte = a.payload[rr.src + (x - rr.pos)];
-        if (i < 8) blo |= byte << (8 * i);
-        else bhi |= byte << (8 * (i - 8));
-      }
-      w[0] = (uint32_t)blo; w[1] = (uint32_t)(blo >> 32); w[2] = (uint32_t)bhi; w[3] = (uint32_t)(bhi >> 32);
-    }
-    ag_store16(a, o, pend, w);
   }
 }
 
@@ -503,8 +562,12 @@ void launch_agg_plan(const AggArgs& a, hipStream_t s) {
 }
 void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim) {
   // grid-stride over the pieces (their number is known only on the device)
-  const uint64_t g = a.n_pieces < 65536 ? a.n_pieces : 65536;
-  if (a.n_frames && g) hipLaunchKernelGGL(k_agg_gather, dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
+  // (2 pieces per wave beat 1 and 4, and the XCD-aware order lost 12-40 % here:
+  // same-box A/B on the configs[2] batch)
+  const uint64_t nq = (a.n_pieces + AGG_PIECES_PER_WAVE - 1) / AGG_PIECES_PER_WAVE;
+  const uint64_t g = nq < 65536 ? nq : 65536;
+  if (a.n_frames && g)
+    hipLaunchKernelGGL((k_agg_gather<AGG_PIECES_PER_WAVE>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
 }
 void launch_agg_final(const AggArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_agg_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);

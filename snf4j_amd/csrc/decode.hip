@@ -129,7 +129,8 @@ __device__ __forceinline__ uint32_t wave_session(const DecodeArgs& a, uint64_t k
   const uint32_t kw = __builtin_amdgcn_readfirstlane((uint32_t)(k & ~63ull));  // (frame indices < 2^30)
   const uint64_t kl = kw + 63u < a.n_frames ? kw + 63u : a.n_frames - 1;
   const uint32_t s_lo = find_session(a.session_first, a.n_sessions, kw);
-  const uint32_t s_hi = find_session_in(a.session_first, s_lo, a.n_sessions - 1, kl);
+  if (s_lo + 1 >= a.n_sessions || a.session_first[s_lo + 1] > kl) return s_lo;  // one session
+  const uint32_t s_hi = find_session_in(a.session_first, s_lo + 1, a.n_sessions - 1, kl);
   return find_session_in(a.session_first, s_lo, s_hi, k);
 }
 
