@@ -60,7 +60,7 @@ struct wsg_ctx {
   bool own_stream = false;
   std::string err;
   // decode workspace
-  DevBuf rec, vflag, slink, edge, blk_sum, blk_max, sess_err, total, pieces;
+  DevBuf rec, vflag, slink, edge, blk_sum, blk_max, chunk, sess_err, total, pieces;
   // encode workspace
   DevBuf esess, elast_close, epieces, epidx;
   // aggregate workspace
@@ -183,7 +183,7 @@ int wsg_close(wsg_ctx* c) {
   if (c->s_out) (void)hipStreamSynchronize(c->s_out);
   drain_timing(c);
   for (auto e : c->free_events) (void)hipEventDestroy(e);
-  DevBuf* bufs[] = {&c->rec,     &c->vflag,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
+  DevBuf* bufs[] = {&c->rec,     &c->vflag, &c->chunk,    &c->edge,     &c->blk_sum,  &c->blk_max,   &c->sess_err,
                     &c->total,   &c->pieces, &c->slink, &c->esess,   &c->elast_close, &c->epieces, &c->epidx, &c->h_wire, &c->h_off,    &c->h_sf,
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
@@ -270,6 +270,7 @@ static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, 
   HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));
   HIP_TRY(c, c->blk_sum.ensure(nblk * sizeof(uint64_t)));
   HIP_TRY(c, c->blk_max.ensure(4 * nblk * sizeof(int32_t)));
+  HIP_TRY(c, c->chunk.ensure((nblk / SCAN_CHUNK + 1) * (sizeof(uint64_t) + 4 * sizeof(int32_t))));
   HIP_TRY(c, c->sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t), 0xff, c->stream));
   HIP_TRY(c, c->total.ensure(sizeof(uint64_t)));
   return WSG_API_OK;
@@ -331,6 +332,8 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.edge = (uint32_t*)c->edge.p;
   a.blk_sum = (uint64_t*)c->blk_sum.p;
   a.blk_max = (int32_t*)c->blk_max.p;
+  a.chunk_sum = (uint64_t*)c->chunk.p;
+  a.chunk_max = (int32_t*)(a.chunk_sum + (n_frames + DBLOCK - 1) / DBLOCK / SCAN_CHUNK + 1);
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
   a.pieces = (PieceDesc*)c->pieces.p;
@@ -382,6 +385,8 @@ int wsg_validate_batch_device(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n
   a.edge = (uint32_t*)c->edge.p;
   a.blk_sum = (uint64_t*)c->blk_sum.p;
   a.blk_max = (int32_t*)c->blk_max.p;
+  a.chunk_sum = (uint64_t*)c->chunk.p;
+  a.chunk_max = (int32_t*)(a.chunk_sum + (n_frames + DBLOCK - 1) / DBLOCK / SCAN_CHUNK + 1);
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
   a.pieces = (PieceDesc*)c->pieces.p;

@@ -3,10 +3,11 @@
 //   k_parse   thread per frame: header parse + the per-frame rules of
 //             FrameDecoder.decode (:197-256), close status/reason (:121-136),
 //             first/last payload bytes; block aggregates for the scans.
-//   k_scan    one workgroup: exclusive scan of the block aggregates (payload slot
-//             bytes = the length prefix-scan; last data / message start / nonempty
-//             frame indices = max-scans; the UTF-8 carry).  Grids up to
-//             FUSED_SCAN_MAX_BLOCKS skip it: k_link reduces the aggregates itself.
+//   k_scan    a workgroup per 4096 block aggregates: exclusive scan within the
+//             chunk (payload slot bytes = the length prefix-scan; last data /
+//             message start / nonempty frame indices = max-scans; the UTF-8
+//             carry).  Grids up to FUSED_SCAN_MAX_BLOCKS skip it: k_link reduces
+//             the aggregates itself.
 //   k_link    thread per frame: payload slot offset, the fragmentation rule
 //             (:229-236) from the previous data frame's FIN, text-message
 //             membership for the validator (FrameUtf8Validator.java:59-70), the
@@ -277,28 +278,32 @@ __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
 }
 
 // ------------------------------------------------------------------ k_scan
-// One workgroup: exclusive scan of the block aggregates in place, 4 entries per
-// thread per pass (one block scan per 4096 blocks).
+// Grids beyond FUSED_SCAN_MAX_BLOCKS: one workgroup per chunk of SCAN_CHUNK block
+// aggregates scans its chunk in place (exclusive within the chunk, 4 entries per
+// thread) and leaves the chunk's total; k_link folds the totals of the chunks
+// before its own (a handful) in order.
 __global__ __launch_bounds__(1024) void k_scan(DecodeArgs a) {
-  DAgg carry = DAGG_ID;
-  for (uint32_t base = 0; base < a.nblk; base += 4096) {
-    const uint32_t b0 = base + threadIdx.x * 4;
-    DAgg e[4], t = DAGG_ID;
+  const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
+  DAgg e[4], t = DAGG_ID;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      e[i] = b0 + i < a.nblk ? load_blk(a, b0 + i) : DAGG_ID;
-      t = agg_op(t, e[i]);
-    }
-    DAgg tot;
-    DAgg ex = agg_op(carry, block_excl_scan_t(t, &tot, DAGG_ID));
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if (b0 + i < a.nblk) store_blk(a, b0 + i, ex);
-      ex = agg_op(ex, e[i]);
-    }
-    carry = agg_op(carry, tot);
+  for (int i = 0; i < 4; ++i) {
+    e[i] = b0 + i < a.nblk ? load_blk(a, b0 + i) : DAGG_ID;
+    t = agg_op(t, e[i]);
   }
-  if (threadIdx.x == 0) *a.total = carry.sum;
+  DAgg tot;
+  DAgg ex = block_excl_scan_t(t, &tot, DAGG_ID);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    if (b0 + i < a.nblk) store_blk(a, b0 + i, ex);
+    ex = agg_op(ex, e[i]);
+  }
+  if (threadIdx.x == 0) {
+    a.chunk_sum[blockIdx.x] = tot.sum;
+    a.chunk_max[4 * blockIdx.x + 0] = tot.m0;
+    a.chunk_max[4 * blockIdx.x + 1] = tot.m1;
+    a.chunk_max[4 * blockIdx.x + 2] = tot.m2;
+    a.chunk_max[4 * blockIdx.x + 3] = (int32_t)tot.c3;
+  }
 }
 
 // ------------------------------------------------------------------ UTF-8 seams
@@ -352,8 +357,18 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
     const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < blockIdx.x ? b0 + per : blockIdx.x;
     for (uint32_t b = b0; b < b1; ++b) t.c3 = carry_op(t.c3, c3s[b]);
     block_excl_scan_t(t, &bp, DAGG_ID);
-  } else {
-    bp = load_blk(a, blockIdx.x);
+  } else {  // k_scan's chunks: the totals of the chunks before this block's, then its own prefix
+    bp = DAGG_ID;
+    for (uint32_t c = 0; c < blockIdx.x / SCAN_CHUNK; ++c) {
+      DAgg e;
+      e.sum = a.chunk_sum[c];
+      e.m0 = a.chunk_max[4 * c + 0];
+      e.m1 = a.chunk_max[4 * c + 1];
+      e.m2 = a.chunk_max[4 * c + 2];
+      e.c3 = (uint32_t)a.chunk_max[4 * c + 3];
+      bp = agg_op(bp, e);
+    }
+    bp = agg_op(bp, load_blk(a, blockIdx.x));
   }
   {
     const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
@@ -371,7 +386,7 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
     }
     DAgg tot;
     DAgg ex = agg_op(bp, block_excl_scan_t(v, &tot, DAGG_ID));
-    if (a.fused_scan && blockIdx.x + 1 == a.nblk && threadIdx.x == 0) *a.total = bp.sum + tot.sum;
+    if (blockIdx.x + 1 == a.nblk && threadIdx.x == 0) *a.total = bp.sum + tot.sum;
     uint32_t validate = 0;
     if (live) {
       const int32_t jd = ex.m0 >> 1, jm = ex.m1 >> 1;  // (-1 >> 1 == -1)
@@ -953,7 +968,7 @@ void launch_parse(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_parse, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
 void launch_scan(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, s, a);
+  hipLaunchKernelGGL(k_scan, dim3((a.nblk + SCAN_CHUNK - 1) / SCAN_CHUNK), dim3(1024), 0, s, a);
 }
 void launch_link(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(DBLOCK), 0, s, a);

@@ -97,6 +97,8 @@ struct DecodeArgs {
                        // for non-FIN data frames (the carry into the next fragment or batch)
   uint64_t* blk_sum;   // [nblk] slot-bytes per block -> exclusive prefix
   int32_t* blk_max;    // [4][nblk] per-block max indices and UTF-8 carry -> exclusive prefix
+  uint64_t* chunk_sum; // [nblk / SCAN_CHUNK + 1] k_scan chunk totals (grids beyond FUSED_SCAN_MAX_BLOCKS)
+  int32_t* chunk_max;  // [nblk / SCAN_CHUNK + 1][4]
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
   uint64_t* total;     // [1] total payload slot bytes
   struct PieceDesc* pieces;  // [piece_bound]: per-piece work descriptor (k_link)
@@ -107,6 +109,7 @@ struct DecodeArgs {
 
 // grids up to this many parse/link blocks (DBLOCK frames each) skip the k_scan launch
 constexpr uint32_t FUSED_SCAN_MAX_BLOCKS = 4096;
+constexpr uint32_t SCAN_CHUNK = 4096;  // block aggregates per k_scan workgroup
 
 struct EncodeArgs {
   int32_t client_mode;

@@ -54,7 +54,7 @@ int main(int argc, char** argv) {
   a.nblk = (uint32_t)((F + ws::DBLOCK - 1) / ws::DBLOCK);
   CK(hipMalloc(&a.rec, F * sizeof(ws::FrameRec))); CK(hipMalloc(&a.vflag, F)); CK(hipMalloc(&a.slink, 3 * S * 4));
   CK(hipMalloc(&a.edge, 2 * F * 4));
-  CK(hipMalloc(&a.blk_sum, a.nblk * 8)); CK(hipMalloc(&a.blk_max, 4 * a.nblk * 4));
+  CK(hipMalloc(&a.blk_sum, a.nblk * 8)); CK(hipMalloc(&a.blk_max, 4 * a.nblk * 4)); CK(hipMalloc(&a.chunk_sum, (a.nblk / ws::SCAN_CHUNK + 1) * 8)); CK(hipMalloc(&a.chunk_max, (a.nblk / ws::SCAN_CHUNK + 1) * 16));
   CK(hipMalloc(&a.sess_err, S * 8)); CK(hipMalloc(&a.total, 8));
   const uint64_t npb = ws::piece_bound(wire_len, F);
   a.n_pieces = npb;
