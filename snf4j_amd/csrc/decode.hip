@@ -242,6 +242,15 @@ __global__ __launch_bounds__(DBLOCK) void k_parse(DecodeArgs a) {
 // in_desc[k], its plain payload at wire[payload_off, +len).  Builds the same
 // FrameRec / edges / block aggregates as k_parse, with no header rules.
 __device__ __forceinline__ uint32_t plain_byte(const DecodeArgs& a, uint64_t i) { return i < a.wire_len ? a.wire[i] : 0u; }
+// the 4 plain bytes at i (zero past the end), from two aligned dword loads
+__device__ __forceinline__ uint32_t plain_word(const DecodeArgs& a, uint64_t i) {
+  const uint64_t q = i & ~3ull;
+  if (q + 8 <= a.wire_len) {
+    const uint32_t lo = *(const uint32_t*)(a.wire + q), hi = *(const uint32_t*)(a.wire + q + 4);
+    return alignbyte(hi, lo, (uint32_t)(i & 3u));
+  }
+  return plain_byte(a, i) | (plain_byte(a, i + 1) << 8) | (plain_byte(a, i + 2) << 16) | (plain_byte(a, i + 3) << 24);
+}
 
 __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
@@ -254,11 +263,11 @@ __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
       const uint32_t len = d.payload_len;
       const uint64_t src = d.payload_off;
       uint32_t f3 = 0, l3 = 0;
-      if (op <= WSG_OP_TEXT) {  // fragment-boundary bytes for the UTF-8 carry (as k_parse)
+      if (op <= WSG_OP_TEXT && len) {  // fragment-boundary bytes for the UTF-8 carry (as k_parse)
         const uint32_t nf = len < 3 ? len : 3;
-        for (uint32_t j = 0; j < nf; ++j) f3 |= plain_byte(a, src + j) << (8 * j);
-        if (!fin)
-          for (uint32_t j = 0; j < nf; ++j) l3 |= plain_byte(a, src + len - 1 - j) << (8 * (2 - j));
+        const uint32_t keep = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : 0xffu);
+        f3 = plain_word(a, src) & keep;
+        if (!fin) l3 = (plain_word(a, src + len - nf) & keep) << (8 * (3 - nf));  // newest in bits 16-23
       }
       a.edge[k] = f3;
       a.edge[a.n_frames + k] = l3;
