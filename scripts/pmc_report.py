@@ -22,7 +22,7 @@ CLOCK_GHZ, CUS, SIMDS = 2.4, 256, 4
 
 
 def short(name: str) -> str:
-    n = name.split("(")[0]
+    n = name.replace("(anonymous namespace)::", "").split("(")[0]
     for p in ("void ", "ws::", "wsb::"):
         n = n.replace(p, "")
     return n.strip()

@@ -21,6 +21,8 @@ struct Span {
   int32_t b, e;  // [b, e) in the request; b < 0: absent
 };
 
+// Every function taking a Req is force-inlined: a Req passed by reference to an
+// outlined call lives in scratch, and then every byte access went through memory.
 // A lane's view of its request: bytes come from 16-B aligned blocks held in
 // registers, so a forward scan costs one load per 16 bytes instead of one per byte
 // (the batch buffer is 16-B aligned: a block never leaves the allocation's granule).
@@ -36,9 +38,11 @@ struct Req {
       cq = q;
       blk = base[q];
     }
+    // (shifts of computed halves: a select among blk's fields became a dynamically
+    // indexed load, which kept the whole Req in scratch)
     const uint32_t o = a & 15u;
-    const uint32_t w = o < 8u ? (o < 4u ? blk.x : blk.y) : (o < 12u ? blk.z : blk.w);
-    return (uint8_t)(w >> (8u * (o & 3u)));
+    const uint64_t lo = (uint64_t)blk.x | ((uint64_t)blk.y << 32), hi = (uint64_t)blk.z | ((uint64_t)blk.w << 32);
+    return (uint8_t)(((o & 8u) ? hi : lo) >> (8u * (o & 7u)));
   }
 };
 
@@ -75,7 +79,7 @@ __device__ __forceinline__ Span trim(Req& d, Span s) {
 // Iterate HttpUtils.values(s) (HttpUtils.java:311-333): split at ',', trim, skip empty.
 // f(token) returns true to stop; returns that token (b < 0 when none stopped).
 template <typename F>
-__device__ Span each_value(Req& d, Span s, F&& f) {
+__device__ __forceinline__ Span each_value(Req& d, Span s, F&& f) {
   int32_t t0 = s.b;
   for (int32_t i = s.b; i <= s.e; ++i) {
     if (i == s.e || d[i] == ',') {
@@ -88,7 +92,7 @@ __device__ Span each_value(Req& d, Span s, F&& f) {
 }
 
 // Integer.parseInt over ASCII: optional sign, decimal digits, int range.
-__device__ bool parse_int(Req& d, Span t, int64_t* v) {
+__device__ __forceinline__ bool parse_int(Req& d, Span t, int64_t* v) {
   int32_t i = t.b;
   bool neg = false;
   if (d[i] == '-' || d[i] == '+') {
@@ -109,14 +113,14 @@ __device__ bool parse_int(Req& d, Span t, int64_t* v) {
 }
 
 // equalsIgnoreCase against an upper-case ASCII literal.
-__device__ bool eq_icase(Req& d, Span t, const char* lit, int n) {
+__device__ __forceinline__ bool eq_icase(Req& d, Span t, const char* lit, int n) {
   if (t.e - t.b != n) return false;
   for (int i = 0; i < n; ++i)
     if (up(d[t.b + i]) != (uint8_t)lit[i]) return false;
   return true;
 }
 
-__device__ bool eq_exact(Req& d, Span t, const char* lit, int n) {
+__device__ __forceinline__ bool eq_exact(Req& d, Span t, const char* lit, int n) {
   if (t.e - t.b != n) return false;
   for (int i = 0; i < n; ++i)
     if (d[t.b + i] != (uint8_t)lit[i]) return false;
@@ -124,14 +128,14 @@ __device__ bool eq_exact(Req& d, Span t, const char* lit, int n) {
 }
 
 // Handshaker.contains (Handshaker.java:407-418)
-__device__ bool contains(Req& d, Span s, const char* lit, int n) {
+__device__ __forceinline__ bool contains(Req& d, Span s, const char* lit, int n) {
   return each_value(d, s, [&](Span t) { return eq_icase(d, t, lit, n); }).b >= 0;
 }
 
 // --- SHA-1 (MessageDigest "SHA1") over key bytes + KEY_GUID: at most 24 + 36 bytes.
 __device__ __forceinline__ uint32_t rol(uint32_t x, int n) { return (x << n) | (x >> (32 - n)); }
 
-__device__ void sha1_block(uint32_t h[5], const uint32_t w0[16]) {
+__device__ __forceinline__ void sha1_block(uint32_t h[5], const uint32_t w0[16]) {
   uint32_t w[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = w0[i];
@@ -155,20 +159,33 @@ __device__ void sha1_block(uint32_t h[5], const uint32_t w0[16]) {
 }
 
 // Sec-WebSocket-Accept = Base64(SHA1(key + GUID)) (HandshakeUtils.generateAnswerKey,
-// HandshakeUtils.java:98-111): 28 characters to out.
-__device__ void accept_key(Req& d, Span key, uint8_t* out) {
-  const int kl = key.e - key.b;  // 22..24 (a parseable key)
-  const int total = kl + 36;     // <= 60: two blocks after padding
+// HandshakeUtils.java:98-111): 28 characters to the response.  Specialised on the key length,
+// so that every message byte's source (key byte, GUID constant, padding) is known at
+// compile time and the message words stay in registers.
+template <int KL, class O>
+__device__ __forceinline__ void accept_key_n(Req& d, int32_t kb, O& out) {
+  constexpr int total = KL + 36;  // <= 60: two blocks after padding
+  uint32_t kw[(KL + 3) / 4];      // the key bytes, big-endian words
+#pragma unroll
+  for (int j = 0; j < (KL + 3) / 4; ++j) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v = (v << 8) | (j * 4 + q < KL ? (uint32_t)d[kb + j * 4 + q] : 0u);
+    kw[j] = v;
+  }
   uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
+#pragma unroll
   for (int blk = 0; blk < 2; ++blk) {
     uint32_t w[16];
+#pragma unroll
     for (int j = 0; j < 16; ++j) {
       uint32_t v = 0;
+#pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int i = blk * 64 + j * 4 + q;
         uint32_t byte;
-        if (i < kl) byte = d[key.b + i];
-        else if (i < total) byte = (uint8_t)kGuid[i - kl];
+        if (i < KL) byte = (kw[i >> 2] >> (24 - 8 * (i & 3))) & 0xffu;
+        else if (i < total) byte = (uint8_t)"258EAFA5-E914-47DA-95CA-C5AB0DC85B11"[i - KL];  // KEY_GUID
         else if (i == total) byte = 0x80u;
         else byte = 0u;
         v = (v << 8) | byte;
@@ -178,28 +195,38 @@ __device__ void accept_key(Req& d, Span key, uint8_t* out) {
     if (blk == 1) w[15] = (uint32_t)total * 8u;  // 60 bytes > 55: the length lands in block 2
     sha1_block(h, w);
   }
-  uint8_t dig[21];
-  for (int i = 0; i < 20; ++i) dig[i] = (uint8_t)(h[i >> 2] >> (24 - 8 * (i & 3)));
-  dig[20] = 0;
   // Base64Util.encode (padding '='): 20 bytes -> 6 full groups + 2 bytes
-  int o = 0;
-  for (int i = 0; i < 18; i += 3) {
-    const uint32_t v = ((uint32_t)dig[i] << 16) | ((uint32_t)dig[i + 1] << 8) | dig[i + 2];
-    out[o++] = (uint8_t)kB64[(v >> 18) & 63];
-    out[o++] = (uint8_t)kB64[(v >> 12) & 63];
-    out[o++] = (uint8_t)kB64[(v >> 6) & 63];
-    out[o++] = (uint8_t)kB64[v & 63];
+  uint32_t dg[7];  // digest bytes in 3-byte groups
+#pragma unroll
+  for (int g = 0; g < 7; ++g) {
+    uint32_t v = 0;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+      const int i = g * 3 + q;
+      v = (v << 8) | (i < 20 ? (h[i >> 2] >> (24 - 8 * (i & 3))) & 0xffu : 0u);
+    }
+    dg[g] = v;
   }
-  const uint32_t v = ((uint32_t)dig[18] << 16) | ((uint32_t)dig[19] << 8);
-  out[o++] = (uint8_t)kB64[(v >> 18) & 63];
-  out[o++] = (uint8_t)kB64[(v >> 12) & 63];
-  out[o++] = (uint8_t)kB64[(v >> 6) & 63];
-  out[o++] = '=';
+#pragma unroll
+  for (int g = 0; g < 7; ++g) {
+    out.byte((uint8_t)kB64[(dg[g] >> 18) & 63]);
+    out.byte((uint8_t)kB64[(dg[g] >> 12) & 63]);
+    out.byte((uint8_t)kB64[(dg[g] >> 6) & 63]);
+    out.byte(g < 6 ? (uint8_t)kB64[dg[g] & 63] : (uint8_t)'=');
+  }
+}
+template <class O>
+__device__ __forceinline__ void accept_key(Req& d, Span key, O& out) {
+  switch (key.e - key.b) {  // 22..24 (a parseable key)
+    case 22: accept_key_n<22>(d, key.b, out); break;
+    case 23: accept_key_n<23>(d, key.b, out); break;
+    default: accept_key_n<24>(d, key.b, out); break;
+  }
 }
 
 // HandshakeUtils.parseKey (HandshakeUtils.java:113-120) over Base64Util.decode
 // (Base64Util.java:253-350, not MIME): true when the key decodes to 16 bytes.
-__device__ bool key_ok(Req& d, Span k) {
+__device__ __forceinline__ bool key_ok(Req& d, Span k) {
   int32_t len = k.e - k.b, end = k.e;
   if (len < 2) return false;  // EMPTY (0 bytes) or null
   if (d[end - 1] == '=') {
@@ -225,7 +252,7 @@ __device__ bool key_ok(Req& d, Span k) {
 
 // The request URI forms the lane accepts as java.net.URI would (a relative
 // reference without scheme, authority-safe characters, well-formed escapes).
-__device__ bool uri_fast(Req& d, Span u) {
+__device__ __forceinline__ bool uri_fast(Req& d, Span u) {
   for (int32_t i = u.b; i < u.e; ++i) {
     const uint8_t c = d[i];
     if ((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9')) continue;
@@ -248,7 +275,7 @@ __device__ bool uri_fast(Req& d, Span u) {
   return true;
 }
 
-__device__ bool host_fast(Req& d, Span h) {
+__device__ __forceinline__ bool host_fast(Req& d, Span h) {
   for (int32_t i = h.b; i < h.e; ++i) {
     const uint8_t c = d[i];
     if (!((c >= 'a' && c <= 'z') || (c >= 'A' && c <= 'Z') || (c >= '0' && c <= '9') || c == '.' || c == '-' ||
@@ -258,24 +285,28 @@ __device__ bool host_fast(Req& d, Span h) {
   return true;
 }
 
-__device__ bool ascii(Req& d, Span s) {
+__device__ __forceinline__ bool ascii(Req& d, Span s) {
   for (int32_t i = s.b; i < s.e; ++i)
     if (d[i] >= 0x80) return false;
   return true;
 }
 
-// Response bytes gathered into dwords: one 4-B store per 4 bytes (resp is 16-B aligned
-// and the stride a multiple of 4).  done() stores the last partial dword.
+// Response bytes gathered into 16-B blocks: one aligned 16-B store per 16 bytes (resp
+// is 16-B aligned and the stride a multiple of 16; dword stores to 64 strided lanes
+// cost a partial line each).  done() stores the last partial block.
 struct Out {
   uint8_t* p;
   int n = 0;
-  uint32_t w = 0;
+  uint64_t lo = 0, hi = 0;
   __device__ void byte(uint32_t c) {
-    w |= c << (8 * (n & 3));
-    if ((++n & 3) == 0) {
-      reinterpret_cast<uint32_t*>(p)[(n >> 2) - 1] = w;
-      w = 0;
+    const int k = n & 15;
+    if (k < 8) lo |= (uint64_t)c << (8 * k);
+    else hi |= (uint64_t)c << (8 * (k - 8));
+    if (k == 15) {
+      reinterpret_cast<uint4*>(p)[n >> 4] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
+      lo = hi = 0;
     }
+    ++n;
   }
   __device__ void put(const char* s) {
     while (*s) byte((uint8_t)*s++);
@@ -284,7 +315,8 @@ struct Out {
     for (int i = 0; i < len; ++i) byte(s[i]);
   }
   __device__ int done() {
-    if (n & 3) reinterpret_cast<uint32_t*>(p)[n >> 2] = w;
+    if (n & 15)
+      reinterpret_cast<uint4*>(p)[n >> 4] = make_uint4((uint32_t)lo, (uint32_t)(lo >> 32), (uint32_t)hi, (uint32_t)(hi >> 32));
     return n;
   }
 };
@@ -309,7 +341,7 @@ __device__ int status_response(uint8_t* resp, int status) {
 // full).  *lines_end: the end of the last complete line recorded, the chunk
 // HandshakeDecoder.available0 (:221-233) hands to decode when no frame is complete.
 template <typename D>
-__host__ __device__ int frame_len_t(D& d, int64_t len, int* capped, int64_t* lines_end) {
+__host__ __device__ __forceinline__ int frame_len_t(D& d, int64_t len, int* capped, int64_t* lines_end) {
   const int max_count = MAX_LINES * 2 + 1 - 3;
   int line_count = 0;
   uint8_t prev, curr = 0;
@@ -343,7 +375,7 @@ __host__ __device__ int hs_frame_len(const uint8_t* d, int64_t len, int* capped,
 
 namespace {
 
-__device__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t* resp, wsg_hs_result* res) {
+__device__ __forceinline__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t* resp, wsg_hs_result* res) {
   wsg_hs_result r = {0u, 0, WSG_HS_NEED_MORE, WSG_HSC_NONE, 0, 0, 0u};
   auto finish = [&](int kind, int status, int cause, Span detail) {
     r.kind = (uint8_t)kind;
@@ -404,7 +436,12 @@ __device__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t*
       line0 = i + 1;
       if (line_no++ == 0) {
         // HandshakeFactory.parse (:96-107) with HttpUtils.splitRequestLine (:125-157), out[10]
-        Span tok[3];
+        Span tok0 = none, tok1 = none, tok2 = none;  // (named: a dynamically indexed array goes to scratch)
+        auto set_tok = [&](int c, Span t) {  // (selects, not stores through a chosen pointer)
+          tok0 = c == 0 ? t : tok0;
+          tok1 = c == 1 ? t : tok1;
+          tok2 = c == 2 ? t : tok2;
+        };
         int count = 0;
         int32_t t0 = lb;
         uint8_t p2, c2 = 0;
@@ -414,7 +451,7 @@ __device__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t*
           c2 = d[j];
           if (c2 == SP) {
             if (p2 != SP) {
-              if (count < 3) tok[count] = Span{t0, j};
+              set_tok(count, Span{t0, j});
               ++count;
               if (count * 2 > 8) over = true;
             }
@@ -423,22 +460,22 @@ __device__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t*
           }
         }
         if (!over) {
-          if (count < 3) tok[count] = (c2 == SP) ? Span{le, le} : Span{t0, le};
+          set_tok(count, (c2 == SP) ? Span{le, le} : Span{t0, le});
           ++count;
         }
         if (count != 3) {
           finish(WSG_HS_PARSE_ERROR, 400, WSG_HSC_BAD_REQUEST_LINE, none);
           return;
         }
-        if (!eq_exact(d, tok[2], "HTTP/1.1", 8)) {  // HttpUtils.equals (:198-215)
+        if (!eq_exact(d, tok2, "HTTP/1.1", 8)) {  // HttpUtils.equals (:198-215)
           finish(WSG_HS_PARSE_ERROR, 400, WSG_HSC_BAD_VERSION, none);
           return;
         }
-        if (!eq_exact(d, tok[0], "GET", 3)) {
+        if (!eq_exact(d, tok0, "GET", 3)) {
           finish(WSG_HS_PARSE_ERROR, 403, WSG_HSC_FORBIDDEN, none);
           return;
         }
-        uri = tok[1];
+        uri = tok1;
         if (partial) {  // the fields are judged once the frame is complete
           finish(WSG_HS_NEED_MORE, 0, WSG_HSC_NONE, none);
           return;
@@ -466,21 +503,30 @@ __device__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t*
       int32_t ve = le;  // rtrimAscii (:230-239)
       while (ve > vb && (d[ve - 1] == SP || d[ve - 1] == HT)) --ve;
       const int nl = fs - lb;
-      for (int f = 0; f < F_COUNT; ++f) {
+      int fi = -1;
+      for (int f = 0; f < F_COUNT && fi < 0; ++f) {
         if (nl != kFieldLen[f]) continue;
         bool m = true;
         for (int q = 0; q < nl && m; ++q) m = up(d[lb + q]) == (uint8_t)kFieldNames[f][q];
-        if (!m) continue;
-        if (fld[f].b >= 0) {  // a repeated field joins its values with ", " (HandshakeFrame.java:80-85)
+        if (m) fi = f;
+      }
+      if (fi >= 0) {
+        // fld is touched with constant indices only (a switch), so it stays in registers
+        bool seen = false;
+#pragma unroll
+        for (int f = 0; f < F_COUNT; ++f)
+          if (f == fi) {
+            seen = fld[f].b >= 0;
+            if (!seen) fld[f] = Span{vb, ve};
+          }
+        if (seen) {  // a repeated field joins its values with ", " (HandshakeFrame.java:80-85)
           finish(WSG_HS_DEFER, 0, WSG_HSC_D_REPEATED, none);
           return;
         }
-        fld[f] = Span{vb, ve};
-        if (!ascii(d, fld[f])) {
+        if (!ascii(d, Span{vb, ve})) {
           finish(WSG_HS_DEFER, 0, WSG_HSC_D_NON_ASCII, none);
           return;
         }
-        break;
       }
     }
   }
@@ -571,16 +617,14 @@ __device__ void accept_one(Req& d, int64_t n, const wsg_hs_config& cfg, uint8_t*
   // 101 with Upgrade, Connection, Sec-WebSocket-Accept (:386-391)
   Out o{resp};
   o.put("HTTP/1.1 101 Switching Protocols\r\nUpgrade: websocket\r\nConnection: Upgrade\r\nSec-WebSocket-Accept: ");
-  uint8_t acc[28];
-  accept_key(d, fld[F_KEY], acc);
-  o.put(acc, 28);
+  accept_key(d, fld[F_KEY], o);  // 28 characters
   o.put("\r\n\r\n");
   const int rl = o.done();
   finish(WSG_HS_ACCEPT, 101, WSG_HSC_NONE, none);
   res->resp_len = (uint16_t)rl;
 }
 
-__global__ __launch_bounds__(256) void k_hs_accept(wsg_hs_config cfg, const uint8_t* req, const uint64_t* req_off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_hs_accept(wsg_hs_config cfg, const uint8_t* req, const uint64_t* req_off,
                                                    uint32_t n, uint8_t* resp, wsg_hs_result* result) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
