@@ -16,7 +16,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok"};
+                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -66,8 +66,9 @@ struct wsg_ctx {
   // aggregate workspace
   DevBuf a_code, a_last, a_pl, a_cl, a_rec, a_blk, a_sess_err, a_pieces;
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
-  DevBuf i_tok, i_lit, i_stat, i_tab;  // inflate pre-decode workspace
+  DevBuf i_tok, i_lit, i_stat, i_tab, i_fast;  // inflate pre-decode workspace
   int infl_tokens = 1;               // WSG_INFLATE_TOKENS=0 turns the pre-decode off
+  int infl_fast = 1;                 // WSG_INFLATE_FAST=0 turns the parallel token replay off (A/B)
   int fused_scan = 1;                // WSG_FUSED_SCAN=0: always launch k_scan (A/B)
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
@@ -161,6 +162,7 @@ int wsg_open(int device, void* stream, wsg_ctx** out) {
   wsg_ctx* c = new wsg_ctx();
   c->device = device;
   if (const char* e = getenv("WSG_INFLATE_TOKENS")) c->infl_tokens = atoi(e) != 0;
+  if (const char* e = getenv("WSG_INFLATE_FAST")) c->infl_fast = atoi(e) != 0;
   if (const char* e = getenv("WSG_FUSED_SCAN")) c->fused_scan = atoi(e) != 0;
   if (stream) {
     c->stream = (hipStream_t)stream;
@@ -190,7 +192,7 @@ int wsg_close(wsg_ctx* c) {
   for (DevBuf* b : bufs) b->release();
   DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,     &c->a_rec,
                      &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc, &c->i_tok, &c->i_lit,
-                     &c->i_stat, &c->i_tab};
+                     &c->i_stat, &c->i_tab, &c->i_fast};
   for (DevBuf* b : abufs) b->release();
   for (HostSlot& hs : c->slot) {
     DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
@@ -855,6 +857,7 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   a.tstat = nullptr;
   a.tab = nullptr;
   a.n_lanes = 0;
+  a.fast_done = nullptr;
   if (c->infl_tokens && n_frames) {
     const uint32_t lanes = (uint32_t)(n_frames < 65536 ? ((n_frames + 63) / 64) * 64 : 65536);
     const uint64_t lit_len = infl_lit_bytes(payload_len, n_frames);
@@ -869,6 +872,11 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
     a.tab = (uint8_t*)c->i_tab.p;
     a.n_lanes = lanes;
     timed(c, K_INFL_TOK, [&] { launch_infl_tok(a, c->stream); });
+    if (c->infl_fast) {
+      HIP_TRY(c, c->i_fast.ensure(n_sessions));
+      a.fast_done = (uint8_t*)c->i_fast.p;
+      timed(c, K_INFL_FAST, [&] { launch_infl_fast(a, c->stream); });
+    }
   }
   timed(c, K_INFLATE, [&] { launch_inflate(a, c->stream); });
   HIP_TRY(c, hipGetLastError());

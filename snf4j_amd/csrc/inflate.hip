@@ -642,6 +642,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   const int lane = threadIdx.x;
   const uint32_t s = blockIdx.x;
   if (s >= a.n_sessions) return;
+  if (a.fast_done && a.fast_done[s]) return;  // replayed in parallel by k_infl_fast
 #ifdef WSG_INFLATE_PROF
   uint64_t pf_[24] = {};
 #endif
@@ -1322,6 +1323,241 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
   if (lane == 0)
     for (int i = 0; i < 24; ++i) atomicAdd(&g_infl_prof[i], (unsigned long long)pf_[i]);
 #endif
+}
+
+// ---------------------------------------------------------------------------------
+// Parallel token replay (k_infl_fast).  A session whose frames in this batch are all
+// single-frame compressed messages that k_infl_tok decoded cleanly, met in the clean
+// state (no message open, no final block seen), needs no serial decoder and no LDS
+// window: per message, the 64 lanes expand the tokens into one descriptor per output
+// byte (a literal, or the absolute session position it copies: a back-reference byte
+// i of (length, distance) at p copies p - distance + i mod distance), chase the
+// copies that land inside the chunk through LDS, gather the ones that land before it
+// from the session's output in HBM (or the carried window image), and store the
+// chunk.  Every output byte is resolved independently, so nothing serialises on a
+// window round trip, and 16 KiB of LDS per wave lets 10 sessions share a CU.  A
+// session it cannot finish (a distance too far back, capacity, any frame that does
+// not qualify) is left to k_inflate, which runs the serial decoder for exactly the
+// sessions without fast_done and overwrites whatever this kernel wrote.
+// ---------------------------------------------------------------------------------
+namespace {
+
+constexpr uint32_t FC = 4096;             // output bytes resolved per chunk
+constexpr uint32_t FD_LIT = 0x80000000u;  // descriptor: a resolved byte (bits 0-7)
+constexpr int32_t FD_BIAS = 32768;        // descriptor: position + FD_BIAS (history positions are >= -32768)
+
+__device__ __forceinline__ uint32_t wave_excl_add(uint32_t v, uint32_t* total) {
+  const int lane = threadIdx.x & 63;
+  uint32_t inc = v;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+    if (lane >= d) inc += t;
+  }
+  *total = (uint32_t)__shfl((int)inc, 63, 64);
+  return inc - v;
+}
+
+__global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
+  __shared__ uint32_t fd[FC];
+  const int lane = threadIdx.x;
+  const uint32_t s = blockIdx.x;
+  if (s >= a.n_sessions) return;
+  const uint32_t f0 = a.session_first[s], f1 = a.session_first[s + 1];
+  const uint64_t obase = a.out_off[s], ocap64 = a.out_off[s + 1] - a.out_off[s];
+  const int64_t ocap = ocap64 < (uint64_t)POS_LIMIT ? (int64_t)ocap64 : (int64_t)POS_LIMIT;
+  const wsg_inflate_state st0 = a.state[s];
+  // does the session qualify?  (every frame: a FIN TEXT/BINARY frame with RSV1, not a
+  // replay, tokens ok, some output; the state clean; the outputs fit)
+  bool ok = !st0.compressing && !(st0.has_decoder && st0.finished);
+  uint64_t need = 0;
+  for (uint32_t k = f0 + (uint32_t)lane; k < f1; k += 64) {
+    const wsg_frame_desc d = a.desc[k];
+    const InflTokStat t = a.tstat[k];
+    const uint32_t op = d.opcode & 15u, rsv = (d.flags >> 4) & 7u;
+    ok = ok && (d.flags & 0x80u) && (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u) &&
+         !(d.flags & WSG_DESC_REPLAY) && t.ok && t.out_len;
+    need += t.out_len;
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)need, d, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(need >> 32), d, 64);
+    need += ((uint64_t)hi << 32) | lo;
+  }
+  if (__any(!ok) || (int64_t)need > ocap) {
+    if (lane == 0) a.fast_done[s] = 0;
+    return;
+  }
+  const uint8_t* const win = a.window + (uint64_t)s * WSG_INFLATE_WINDOW;
+  uint8_t* const out = a.out + obase;
+  const int wl0 = (st0.has_decoder && !st0.finished) ? (int)(st0.window_len < WSG_INFLATE_WINDOW ? st0.window_len : WSG_INFLATE_WINDOW) : 0;
+  const uint32_t ph = wl0 ? (uint32_t)st0.window_phase & WMASK : 0u;
+  // the session's output so far, read around L1 (bytes this wave stored a chunk ago)
+  const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)ocap, 0x00020000);
+  int has_dec = st0.has_decoder;
+  int32_t pos = 0, wstart = -wl0;
+  bool bad = false;
+  for (uint32_t k = f0; k < f1 && !bad; ++k) {
+    const wsg_frame_desc d = a.desc[k];
+    const InflTokStat ts = a.tstat[k];
+    if (!has_dec) {  // new ZlibDecoder(RAW): a fresh history (DeflateDecoder.java:80-93)
+      has_dec = 1;
+      wstart = pos;
+    }
+    const int32_t P0 = pos;
+    const uint32_t L = ts.out_len, n_tok = ts.n_tok;
+    const uint32_t* const T = a.tok + tok_base(d.payload_off, k);
+    const uint8_t* const lit = a.lit + lit_base(d.payload_off, k);
+    uint32_t tt = 0, t_off = 0, t_li = 0;  // the first token not fully emitted: index, output offset, literal index
+    for (uint32_t c0 = 0; c0 < L && !bad; c0 += FC) {
+      const uint32_t c1 = c0 + FC < L ? c0 + FC : L, n = c1 - c0;
+      const int32_t C0 = P0 + (int32_t)c0;  // absolute position of the chunk's first byte
+      // 1. expand the tokens that overlap [c0, c1) into fd
+      uint32_t t = tt, o = t_off, li = t_li;
+      bool crossed = false;
+      while (t < n_tok && o < c1) {
+        const bool valid = t + (uint32_t)lane < n_tok;
+        const uint32_t tk = valid ? T[t + lane] : 0u;
+        const bool ism = (tk & 0x80000000u) != 0;
+        const uint32_t len = !valid ? 0u : (ism ? ((tk >> 16) & 255u) + 3u : tk);
+        uint32_t tot_len, tot_lit;
+        const uint32_t to = o + wave_excl_add(len, &tot_len);
+        const uint32_t tli = li + wave_excl_add(ism ? 0u : len, &tot_lit);
+        if (valid && to < c1 && to + len > c0) {
+          const uint32_t b0 = to > c0 ? to : c0, b1 = to + len < c1 ? to + len : c1;
+          if (ism) {
+            const uint32_t md = (tk & 0x7fffu) + 1u;
+            if ((int32_t)md > P0 + (int32_t)to - wstart) bad = true;  // "invalid distance too far back"
+            const int32_t src0 = P0 + (int32_t)to - (int32_t)md + FD_BIAS;
+            uint32_t r = (b0 - to) % md;
+            for (uint32_t j = b0; j < b1; ++j) {
+              fd[j - c0] = (uint32_t)(src0 + (int32_t)r);
+              if (++r == md) r = 0;
+            }
+          } else {
+            for (uint32_t j = b0; j < b1; ++j) fd[j - c0] = FD_LIT | lit[tli + (j - to)];
+          }
+        }
+        const uint64_t cross = __ballot(valid && to + len > c1);
+        if (cross) {  // the chunk ends inside this token: the next chunk starts from it
+          const int f = __builtin_ctzll(cross);
+          tt = t + (uint32_t)f;
+          t_off = (uint32_t)__shfl((int)to, f, 64);
+          t_li = (uint32_t)__shfl((int)tli, f, 64);
+          crossed = true;
+          break;
+        }
+        t += 64u;
+        o += tot_len;
+        li += tot_lit;
+      }
+      if (!crossed) {
+        tt = t < n_tok ? t : n_tok;
+        t_off = o;
+        t_li = li;
+      }
+      if (__any(bad)) {
+        bad = true;
+        break;
+      }
+      __syncthreads();
+      // 2. chase copies inside the chunk: a byte's source precedes it, so a chain
+      //    ends at a literal or at a byte before the chunk (kept as a position)
+      for (uint32_t j = (uint32_t)lane; j < n; j += 64) {
+        uint32_t v = fd[j];
+        while (!(v & FD_LIT) && (int32_t)v - FD_BIAS >= C0) v = fd[(int32_t)v - FD_BIAS - C0];
+        fd[j] = v;
+      }
+      __syncthreads();
+      // 3. gather the bytes that come from before the chunk: this batch's output (HBM),
+      //    or the window carried in
+      for (uint32_t j0 = 0; j0 < n; j0 += 256) {
+        uint32_t v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t j = j0 + 64u * u + (uint32_t)lane;
+          v[u] = j < n ? fd[j] : FD_LIT;
+          if (!(v[u] & FD_LIT)) {
+            const int32_t q = (int32_t)v[u] - FD_BIAS;
+            v[u] = FD_LIT | (q >= 0 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rout, (uint32_t)q, 0, 1)
+                                    : (uint32_t)win[((uint32_t)q + ph) & WMASK]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t j = j0 + 64u * u + (uint32_t)lane;
+          if (j < n) fd[j] = v[u];
+        }
+      }
+      __syncthreads();
+      // 4. store the chunk: head bytes to a 4-B boundary, dwords, tail bytes
+      uint8_t* const dst = out + C0;
+      uint32_t head = (uint32_t)((4u - (uint32_t)((uintptr_t)dst & 3u)) & 3u);
+      if (head > n) head = n;
+      if ((uint32_t)lane < head) dst[lane] = (uint8_t)fd[lane];
+      const uint32_t nw = (n - head) >> 2;
+      for (uint32_t w = (uint32_t)lane; w < nw; w += 64) {
+        const uint32_t b = head + 4u * w;
+        reinterpret_cast<uint32_t*>(dst + head)[w] =
+            (fd[b] & 0xffu) | ((fd[b + 1] & 0xffu) << 8) | ((fd[b + 2] & 0xffu) << 16) | ((fd[b + 3] & 0xffu) << 24);
+      }
+      const uint32_t tb = head + 4u * nw;
+      if ((uint32_t)lane < n - tb) dst[tb + lane] = (uint8_t)fd[tb + lane];
+      // the stores complete before the next chunk gathers from them
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+      __syncthreads();
+    }
+    if (bad) break;
+    pos += (int32_t)L;
+    if (lane == 0) {
+      wsg_frame_desc o;
+      o.payload_off = obase + (uint64_t)P0;
+      o.payload_len = L;
+      o.opcode = (uint8_t)(d.opcode & 15u);
+      const uint32_t rsv = (d.flags >> 4) & 7u;
+      o.flags = (uint8_t)((1u << 7) | ((rsv ^ 4u) << 4) | WSG_DESC_INFLATED);  // rsvBits(): RSV1 cleared (:83-85)
+      o.status = 0;
+      a.out_desc[k] = o;
+    }
+    if (a.no_context) has_dec = 0;  // decoder.event(ENDING); decoder = null (DeflateDecoder.java:107-110)
+  }
+  if (bad) {
+    if (lane == 0) a.fast_done[s] = 0;
+    return;
+  }
+  // commit (k_inflate's, with no message left open): the state and the window image
+  wsg_inflate_state st = st0;
+  st.compressing = 0;
+  st.has_decoder = (uint8_t)has_dec;
+  st.finished = 0;
+  st.window_len = 0;
+  st.window_phase = 0;
+  if (has_dec) {
+    const int32_t P = pos, nh = (P - wstart) < (int32_t)WSG_INFLATE_WINDOW ? (P - wstart) : (int32_t)WSG_INFLATE_WINDOW;
+    const uint32_t nph = ((uint32_t)P + ph) & WMASK;
+    const int32_t lo = (P - nh) > 0 ? (P - nh) : 0;
+    // slot j holds position q(j) in [P - 32768, P); q < 0: the old image has it already
+    uint8_t* const wout = a.window + (uint64_t)s * WSG_INFLATE_WINDOW;
+    for (uint32_t j = (uint32_t)lane; j < WSG_INFLATE_WINDOW; j += 64) {
+      const int32_t q = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)((j - nph) & WMASK);
+      if (q >= lo) wout[j] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rout, (uint32_t)q, 0, 1);
+    }
+    st.window_len = (uint16_t)nh;
+    st.window_phase = (uint16_t)nph;
+  }
+  if (lane == 0) {
+    a.state[s] = st;
+    wsg_session_result res = {f1 - f0, 0u, 0u, 0};
+    a.result[s] = res;
+    a.replay_from[s] = 0xffffffffu;
+    a.fast_done[s] = 1;
+  }
+}
+
+}  // namespace
+
+void launch_infl_fast(const InflArgs& a, hipStream_t s) {
+  if (a.n_sessions && a.tstat && a.fast_done) hipLaunchKernelGGL(k_infl_fast, dim3(a.n_sessions), dim3(64), 0, s, a);
 }
 
 void launch_infl_tok(const InflArgs& a, hipStream_t s) {

@@ -195,6 +195,7 @@ struct InflArgs {
   struct InflTokStat* tstat;  // [n_frames]
   uint8_t* tab;               // n_lanes per-lane table blocks
   uint32_t n_lanes;
+  uint8_t* fast_done;         // [n_sessions]: k_infl_fast finished the session (k_inflate skips it)
 };
 
 struct InflTokStat {
@@ -204,7 +205,7 @@ struct InflTokStat {
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -228,6 +229,7 @@ void launch_agg_final(const AggArgs& a, hipStream_t s);
 
 void launch_inflate(const InflArgs& a, hipStream_t s);
 void launch_infl_tok(const InflArgs& a, hipStream_t s);
+void launch_infl_fast(const InflArgs& a, hipStream_t s);
 uint64_t infl_tok_words(uint64_t payload_len, uint64_t n_frames);
 uint64_t infl_lit_bytes(uint64_t payload_len, uint64_t n_frames);
 uint64_t infl_tab_bytes();

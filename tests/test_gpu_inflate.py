@@ -217,3 +217,38 @@ def test_inflate_predecode_matches_serial_and_zlib(oracle):
             exp = z.decompress(payload[int(o["payload_off"]):int(o["payload_off"]) + int(o["payload_len"])].tobytes()
                                + b"\x00\x00\xff\xff")
             assert outs[0][s][j] == exp, (s, j)
+
+
+def test_inflate_parallel_replay_fallbacks(ctx, oracle):
+    """k_infl_fast (the parallel token replay) next to sessions it must leave to the
+    serial decoder, in the same batches: a message whose back-reference reaches before
+    the decoder's history ("invalid distance too far back"), fragmented messages, an
+    uncompressed message, a final block; and sessions it takes, with context carried
+    across batches and with no_context.  Every session against the oracle."""
+    rng = np.random.default_rng(2024)
+    for no_context in (False, True):
+        sessions = []
+        for i in range(40):
+            comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+            text = wsgen.rand_text(rng, 4000)
+            msgs = []
+            for m in range(int(rng.integers(2, 12))):
+                if no_context:
+                    comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+                body = text[int(rng.integers(0, 2000)):][:int(rng.integers(50, 2000))] + bytes([m])
+                data = comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH)
+                msgs.append((1, True, 4, data[:-4]))
+            kind = i % 6
+            if kind == 1 and len(msgs) > 2 and not no_context:
+                msgs = msgs[1:]  # its first message now refers to history it never had
+            elif kind == 2:  # a fragmented message in the middle
+                op, fin, rsv, p = msgs[1]
+                cut = len(p) // 2
+                msgs[1:2] = [(op, False, 4, p[:cut]), (0, True, 0, p[cut:])]
+            elif kind == 3:
+                msgs.insert(1, (2, True, 0, b"plain"))
+            elif kind == 4:
+                comp2 = zlib.compressobj(6, zlib.DEFLATED, -15)
+                msgs.append((1, True, 4, comp2.compress(b"the end") + comp2.flush(zlib.Z_FINISH)))
+            sessions.append(msgs)
+        _run(ctx, oracle, sessions, no_context, 3, rng)
