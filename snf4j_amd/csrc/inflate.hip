@@ -37,6 +37,7 @@
 //   * a frame that produces no bytes fails unless its payload is the single byte
 //     00 (DeflateDecoder.java:122-131).
 #include "wsgpu_internal.h"
+#include "wsgpu_scan.h"
 
 namespace ws {
 
@@ -405,6 +406,265 @@ __device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
   return (3 * po + (uint64_t)TOK_SLACK * k + 3) & ~(uint64_t)3;
 }
 
+// One message's pre-decode into per-frame token regions (MULTI: several frames; the
+// single-frame instantiation keeps the segment and attribution steps out of its loop).
+template <bool MULTI>
+__device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const uint32_t* lit_ent,
+                                            const uint32_t* dist_ent, uint64_t k, uint64_t kend, uint32_t in_len) {
+  const wsg_frame_desc d = a.desc[k];
+  // the next data frame of the message after j (j < kend)
+  auto next_frame = [&](uint64_t j) -> uint64_t {
+    for (++j; j < kend; ++j)
+      if ((a.desc[j].opcode & 15u) < 8u) break;
+    return j;
+  };
+  const uint32_t total = in_len + 4u;
+  constexpr bool multi = MULTI;
+  // input reader: segment = a frame's payload, message offsets [seg_lo, seg_lo + seg_len)
+  uint64_t seg_k = k, seg_off = d.payload_off;
+  uint32_t seg_lo = 0, seg_len = d.payload_len;
+  Src src{a.payload, a.payload_len, d.payload_off, d.payload_len, -1, make_uint4(0, 0, 0, 0)};
+  // output attribution: the frame whose bytes complete a symbol (zlib: a symbol belongs
+  // to the inflate call that supplies its last bit's byte), per-frame token regions
+  uint64_t fa = k;
+  uint32_t fa_hi = k == kend ? total : d.payload_len;  // message offset where frame fa's bytes end
+  uint32_t tok_cap = d.payload_len + 68u, lit_cap = 3u * (d.payload_len + 4u) + 60u;
+  uint32_t* tok = a.tok + tok_base(d.payload_off, k);
+  uint8_t* lit = a.lit + lit_base(d.payload_off, k);
+  uint64_t hold = 0;
+  int bits = 0;
+  uint32_t ip = 0, ntok = 0, nlit = 0, run = 0, outlen = 0, litw = 0;
+  bool ok = true;
+  // The bit buffer is refilled with up to 8 bytes at once from a 32-byte window of
+  // two 16-B blocks held in registers (one funnel shift, no per-byte branches); the
+  // window moves on by one block when the lane leaves the first one.
+  int64_t wq = (int64_t)(seg_off >> 4);
+  uint4 wc = src.ld(wq), wn = src.ld(wq + 1);
+  auto refill = [&]() {
+    if (bits > 56 || ip >= total) return;
+    while (multi && seg_k != kend && ip == seg_lo + seg_len) {  // on to the next frame's payload
+      seg_lo += seg_len;
+      seg_k = next_frame(seg_k);
+      const wsg_frame_desc dn = a.desc[seg_k];
+      seg_off = dn.payload_off;
+      seg_len = dn.payload_len;
+      wq = (int64_t)(seg_off >> 4);
+      wc = src.ld(wq);
+      wn = src.ld(wq + 1);
+    }
+    const uint64_t g = seg_off + (ip - seg_lo);  // payload address of input byte ip
+    const uint32_t o = (uint32_t)(g & 15u);
+    const uint32_t q = o >> 2, sh = o & 3u;
+    const uint32_t D0 = wc.x, D1 = wc.y, D2 = wc.z, D3 = wc.w, D4 = wn.x, D5 = wn.y;
+    const uint32_t A = q == 0 ? D0 : q == 1 ? D1 : q == 2 ? D2 : D3;
+    const uint32_t B = q == 0 ? D1 : q == 1 ? D2 : q == 2 ? D3 : D4;
+    const uint32_t C = q == 0 ? D2 : q == 1 ? D3 : q == 2 ? D4 : D5;
+    const uint32_t lo = __builtin_amdgcn_alignbyte(B, A, sh);
+    const uint32_t hi = __builtin_amdgcn_alignbyte(C, B, sh);
+    uint64_t v = ((uint64_t)hi << 32) | lo;
+    const int32_t k0 = (int32_t)(seg_lo + seg_len) - (int32_t)ip;  // bytes left in this segment
+    uint32_t nb = (uint32_t)(64 - bits) >> 3;
+    if (seg_k == kend) {
+      // the last segment: the tail 00 00 FF FF from its end on (DeflateCodec TAIL)
+      if (k0 < 8) {
+        const uint64_t tail = 0xFFFF0000ull;
+        v = k0 > 0 ? ((v & ((1ull << (8 * k0)) - 1ull)) | (tail << (8 * k0))) : (tail >> (8 * (-k0 < 8 ? -k0 : 7)));
+      }
+      if (nb > total - ip) nb = total - ip;
+    } else if (nb > (uint32_t)k0) {
+      nb = (uint32_t)k0;  // a segment's bytes only: the next one is elsewhere
+    }
+    if (nb < 8) v &= (1ull << (8 * nb)) - 1ull;
+    hold |= v << bits;
+    bits += 8 * (int)nb;
+    ip += nb;
+    if ((int64_t)((seg_off + (ip - seg_lo)) >> 4) > wq) {
+      ++wq;
+      wc = wn;
+      wn = src.ld(wq + 1);
+    }
+  };
+  auto drop = [&](int n) {
+    hold >>= n;
+    bits -= n;
+  };
+  auto put_lit = [&](uint32_t b) -> bool {
+    if (nlit >= lit_cap) return false;
+    litw |= b << (8 * (nlit & 3u));
+    if ((++nlit & 3u) == 0) {
+      reinterpret_cast<uint32_t*>(lit)[(nlit >> 2) - 1] = litw;
+      litw = 0;
+    }
+    ++run;
+    ++outlen;
+    return true;
+  };
+  auto put_tok = [&](uint32_t t) -> bool {
+    if (ntok >= tok_cap) return false;
+    tok[ntok++] = t;
+    return true;
+  };
+  auto end_run = [&]() -> bool {
+    if (!run) return true;
+    const bool r = put_tok(run);
+    run = 0;
+    return r;
+  };
+  // close frame fa (its stats), open the next data frame's regions
+  auto close_frame = [&]() -> bool {
+    if (!end_run()) return false;
+    if (nlit & 3u) reinterpret_cast<uint32_t*>(lit)[nlit >> 2] = litw;
+    a.tstat[fa] = InflTokStat{1u, ntok, nlit, outlen};
+    if (fa == kend) return true;
+    const uint32_t lo = fa_hi;
+    fa = next_frame(fa);
+    const wsg_frame_desc df = a.desc[fa];
+    fa_hi = fa == kend ? total : lo + df.payload_len;
+    tok_cap = df.payload_len + 68u;
+    lit_cap = 3u * (df.payload_len + 4u) + 60u;
+    tok = a.tok + tok_base(df.payload_off, fa);
+    lit = a.lit + lit_base(df.payload_off, fa);
+    ntok = nlit = run = outlen = litw = 0;
+    return true;
+  };
+  // a symbol just completed: its last bit's byte decides its frame
+  auto attrib = [&]() -> bool {
+    if (!multi) return true;
+    const uint32_t lb = (8u * ip - (uint32_t)bits - 1u) >> 3;
+    while (lb >= fa_hi && fa != kend)
+      if (!close_frame()) return false;
+    return true;
+  };
+  for (;;) {
+    refill();
+    if (bits == 0 && ip >= total) break;  // clean: all input used, on a block boundary
+    if (bits < 3) { ok = false; break; }
+    const uint32_t last = (uint32_t)(hold & 1u), type = (uint32_t)((hold >> 1) & 3u);
+    drop(3);
+    if (last) { ok = false; break; }      // a final block: the stream ends (k_inflate handles it)
+    if (type == 0) {                      // stored
+      drop(bits & 7);
+      refill();
+      if (bits < 32) { ok = false; break; }
+      const uint32_t ln = (uint32_t)(hold & 0xffffu), nl = (uint32_t)((hold >> 16) & 0xffffu);
+      if (ln != (nl ^ 0xffffu)) { ok = false; break; }
+      drop(32);
+      for (uint32_t i = 0; i < ln && ok; ++i) {
+        refill();
+        if (bits < 8) { ok = false; break; }
+        const uint32_t b = (uint32_t)(hold & 0xffu);
+        drop(8);
+        ok = attrib() && put_lit(b);
+      }
+      if (!ok) break;
+      continue;
+    }
+    int lmax, dmax;
+    if (type == 1) {  // fixed codes
+      for (int i = 0; i < 288; ++i) T->lens[i] = i < 144 ? 8 : (i < 256 ? 9 : (i < 280 ? 7 : 8));
+      lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, 288, T_LIT);
+      for (int i = 0; i < 30; ++i) T->lens[i] = 5;
+      // zlib's fixed distance set has 30 codes of 5 bits + the 2 invalid ones: complete with 32
+      T->lens[30] = 5;
+      T->lens[31] = 5;
+      dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, 32, T_DIST);
+    } else if (type == 2) {  // dynamic codes
+      refill();
+      if (bits < 14) { ok = false; break; }
+      const int nlen = (int)(hold & 31u) + 257, ndist = (int)((hold >> 5) & 31u) + 1,
+                ncode = (int)((hold >> 10) & 15u) + 4;
+      drop(14);
+      if (nlen > 286 || ndist > 30) { ok = false; break; }
+      for (int i = 0; i < 19; ++i) T->lens[kClenOrder[i]] = 0;
+      for (int i = 0; i < ncode; ++i) {
+        refill();
+        if (bits < 3) { ok = false; break; }
+        T->lens[kClenOrder[i]] = (uint8_t)(hold & 7u);
+        drop(3);
+      }
+      if (!ok) break;
+      const int cmax = lane_build(T, T->croot, CROOT, T->lcnt, T->lsym, T->lens, 19, T_CODES);
+      if (cmax < 0) { ok = false; break; }
+      int have = 0;
+      while (have < nlen + ndist) {
+        refill();
+        const uint32_t e = lane_sym(T->croot, CROOT, nullptr, nullptr, cmax, nullptr, hold, bits);
+        const int nb = (int)e_len(e);
+        if (nb == 0 || nb > bits) { ok = false; break; }
+        const int sy = (int)e_val(e);
+        if (sy < 16) {
+          drop(nb);
+          T->lens[have++] = (uint8_t)sy;
+          continue;
+        }
+        const int xb = sy == 16 ? 2 : (sy == 17 ? 3 : 7);
+        if (nb + xb > bits) { ok = false; break; }
+        drop(nb);
+        int len = 0, copy;
+        if (sy == 16) {
+          if (have == 0) { ok = false; break; }
+          len = T->lens[have - 1];
+          copy = 3 + (int)(hold & 3u);
+        } else if (sy == 17) {
+          copy = 3 + (int)(hold & 7u);
+        } else {
+          copy = 11 + (int)(hold & 127u);
+        }
+        drop(xb);
+        if (have + copy > nlen + ndist) { ok = false; break; }
+        for (int i = 0; i < copy; ++i) T->lens[have + i] = (uint8_t)len;
+        have += copy;
+      }
+      if (!ok) break;
+      if (T->lens[256] == 0) { ok = false; break; }
+      lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, nlen, T_LIT);
+      // the distance lengths follow the literal/length ones in lens[]: move them first
+      for (int i = 0; i < ndist; ++i) T->lens[i] = T->lens[nlen + i];
+      dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, ndist, T_DIST);
+    } else {
+      ok = false;
+      break;
+    }
+    if (lmax < 0 || dmax < 0) { ok = false; break; }
+    // the block's symbols
+    for (;;) {
+      refill();
+      const uint32_t e = lane_sym(T->lroot, LROOT, T->lcnt, T->lsym, lmax, lit_ent, hold, bits);
+      const uint32_t eo = e_op(e);
+      if (eo == OP_BAD) { ok = false; break; }
+      drop((int)e_len(e));
+      if (eo == OP_LIT) {
+        if (!attrib() || !put_lit(e_val(e))) { ok = false; break; }
+        continue;
+      }
+      if (eo == OP_EOB) break;
+      const int lx = (int)e_extra(e);
+      if (lx > bits) { ok = false; break; }
+      const uint32_t mlen = e_val(e) + (uint32_t)(hold & ((1ull << lx) - 1ull));
+      drop(lx);
+      refill();
+      const uint32_t g = lane_sym(T->droot, DROOT, T->dcnt, T->dsym, dmax, dist_ent, hold, bits);
+      if (e_op(g) == OP_BAD) { ok = false; break; }
+      drop((int)e_len(g));
+      const int dx = (int)e_extra(g);
+      if (dx > bits) { ok = false; break; }
+      const uint32_t md = e_val(g) + (uint32_t)(hold & ((1ull << dx) - 1ull));
+      drop(dx);
+      if (!attrib() || !end_run() || !put_tok(0x80000000u | ((mlen - 3u) << 16) | (md - 1u))) { ok = false; break; }
+      outlen += mlen;
+    }
+    if (!ok) break;
+  }
+  // the frames left: the last symbol's frame and any after it (no output: the
+  // serial decoder then decides, DeflateDecoder.java:122-131)
+  while (ok) {
+    const bool last = fa == kend;
+    if (!close_frame()) ok = false;
+    if (last) break;
+  }
+  if (!ok) a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};  // the message goes to the serial decoder
+}
+
 __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
   // symbol -> entry (base, extra bits, op) for the 16-bit root entries
   __shared__ uint32_t lit_ent[288], dist_ent[32];
@@ -416,209 +676,42 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
   LaneTab* const T = reinterpret_cast<LaneTab*>(a.tab) + lane_id;
   for (uint64_t k = lane_id; k < a.n_frames; k += a.n_lanes) {
     const wsg_frame_desc d = a.desc[k];
-    InflTokStat st = {0u, 0u, 0u, 0u};
     const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
-    const bool cand = fin && (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u) &&
-                      !(d.flags & WSG_DESC_REPLAY) && d.payload_off + d.payload_len <= a.payload_len;
-    if (!cand) {
-      a.tstat[k] = st;
+    const bool start = (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u) && !(d.flags & WSG_DESC_REPLAY) &&
+                       d.payload_off + d.payload_len <= a.payload_len;
+    if (!start) {
+      // a continuation's stats are its message's (the start frame's lane writes them)
+      if (op != WSG_OP_CONTINUATION) a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
       continue;
     }
-    const uint32_t plen = d.payload_len, total = plen + 4u;
-    const uint32_t tok_cap = plen + 68u, lit_cap = 3u * total + 60u;
-    uint32_t* const tok = a.tok + tok_base(d.payload_off, k);
-    uint8_t* const lit = a.lit + lit_base(d.payload_off, k);
-    Src src{a.payload, a.payload_len, d.payload_off, plen, -1, make_uint4(0, 0, 0, 0)};
-    uint64_t hold = 0;
-    int bits = 0;
-    uint32_t ip = 0, ntok = 0, nlit = 0, run = 0, outlen = 0, litw = 0;
-    bool ok = true;
-    // The bit buffer is refilled with up to 8 bytes at once from a 32-byte window of
-    // two 16-B blocks held in registers (one funnel shift, no per-byte branches); the
-    // window moves on by one block when the lane leaves the first one.
-    int64_t wq = (int64_t)(d.payload_off >> 4);
-    uint4 wc = src.ld(wq), wn = src.ld(wq + 1);
-    auto refill = [&]() {
-      if (bits > 56 || ip >= total) return;
-      const uint32_t o = (uint32_t)((d.payload_off + ip) & 15u);
-      const uint32_t q = o >> 2, sh = o & 3u;
-      const uint32_t D0 = wc.x, D1 = wc.y, D2 = wc.z, D3 = wc.w, D4 = wn.x, D5 = wn.y;
-      const uint32_t A = q == 0 ? D0 : q == 1 ? D1 : q == 2 ? D2 : D3;
-      const uint32_t B = q == 0 ? D1 : q == 1 ? D2 : q == 2 ? D3 : D4;
-      const uint32_t C = q == 0 ? D2 : q == 1 ? D3 : q == 2 ? D4 : D5;
-      const uint32_t lo = __builtin_amdgcn_alignbyte(B, A, sh);
-      const uint32_t hi = __builtin_amdgcn_alignbyte(C, B, sh);
-      uint64_t v = ((uint64_t)hi << 32) | lo;
-      // the tail 00 00 FF FF from byte plen on (DeflateCodec TAIL)
-      const int32_t k0 = (int32_t)plen - (int32_t)ip;
-      if (k0 < 8) {
-        const uint64_t tail = 0xFFFF0000ull;
-        v = k0 > 0 ? ((v & ((1ull << (8 * k0)) - 1ull)) | (tail << (8 * k0))) : (tail >> (8 * (-k0 < 8 ? -k0 : 7)));
-      }
-      uint32_t nb = (uint32_t)(64 - bits) >> 3;
-      if (nb > total - ip) nb = total - ip;
-      if (nb < 8) v &= (1ull << (8 * nb)) - 1ull;
-      hold |= v << bits;
-      bits += 8 * (int)nb;
-      ip += nb;
-      if ((int64_t)((d.payload_off + ip) >> 4) > wq) {
-        ++wq;
-        wc = wn;
-        wn = src.ld(wq + 1);
-      }
-    };
-    auto drop = [&](int n) {
-      hold >>= n;
-      bits -= n;
-    };
-    auto put_lit = [&](uint32_t b) -> bool {
-      if (nlit >= lit_cap) return false;
-      litw |= b << (8 * (nlit & 3u));
-      if ((++nlit & 3u) == 0) {
-        reinterpret_cast<uint32_t*>(lit)[(nlit >> 2) - 1] = litw;
-        litw = 0;
-      }
-      ++run;
-      ++outlen;
-      return true;
-    };
-    auto put_tok = [&](uint32_t t) -> bool {
-      if (ntok >= tok_cap) return false;
-      tok[ntok++] = t;
-      return true;
-    };
-    auto end_run = [&]() -> bool {
-      if (!run) return true;
-      const bool r = put_tok(run);
-      run = 0;
-      return r;
-    };
-    for (;;) {
-      refill();
-      if (bits == 0 && ip >= total) break;  // clean: all input used, on a block boundary
-      if (bits < 3) { ok = false; break; }
-      const uint32_t last = (uint32_t)(hold & 1u), type = (uint32_t)((hold >> 1) & 3u);
-      drop(3);
-      if (last) { ok = false; break; }      // a final block: the stream ends (k_inflate handles it)
-      if (type == 0) {                      // stored
-        drop(bits & 7);
-        refill();
-        if (bits < 32) { ok = false; break; }
-        const uint32_t ln = (uint32_t)(hold & 0xffffu), nl = (uint32_t)((hold >> 16) & 0xffffu);
-        if (ln != (nl ^ 0xffffu)) { ok = false; break; }
-        drop(32);
-        for (uint32_t i = 0; i < ln && ok; ++i) {
-          refill();
-          if (bits < 8) { ok = false; break; }
-          ok = put_lit((uint32_t)(hold & 0xffu));
-          drop(8);
+    // The message: frame k and, if it is not FIN, the session's continuation frames up
+    // to the FIN one (control frames between them are not part of the stream).  A
+    // message the batch does not hold whole goes to the serial decoder.
+    uint64_t kend = k, se = k + 1;
+    uint32_t in_len = d.payload_len;  // compressed bytes of the whole message
+    bool whole = fin != 0;
+    if (!fin) {
+      se = a.session_first[find_session(a.session_first, a.n_sessions, k) + 1];
+      for (uint64_t j = k + 1; j < se; ++j) {
+        const wsg_frame_desc dj = a.desc[j];
+        const uint32_t oj = dj.opcode & 15u;
+        if (oj >= 8u) continue;
+        if (oj != WSG_OP_CONTINUATION || (dj.flags & WSG_DESC_REPLAY) || dj.payload_off + dj.payload_len > a.payload_len)
+          break;
+        in_len += dj.payload_len;
+        if (dj.flags & 0x80u) {
+          kend = j;
+          whole = true;
+          break;
         }
-        if (!ok) break;
-        continue;
       }
-      int lmax, dmax;
-      if (type == 1) {  // fixed codes
-        for (int i = 0; i < 288; ++i) T->lens[i] = i < 144 ? 8 : (i < 256 ? 9 : (i < 280 ? 7 : 8));
-        lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, 288, T_LIT);
-        for (int i = 0; i < 30; ++i) T->lens[i] = 5;
-        // zlib's fixed distance set has 30 codes of 5 bits + the 2 invalid ones: complete with 32
-        T->lens[30] = 5;
-        T->lens[31] = 5;
-        dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, 32, T_DIST);
-      } else if (type == 2) {  // dynamic codes
-        refill();
-        if (bits < 14) { ok = false; break; }
-        const int nlen = (int)(hold & 31u) + 257, ndist = (int)((hold >> 5) & 31u) + 1,
-                  ncode = (int)((hold >> 10) & 15u) + 4;
-        drop(14);
-        if (nlen > 286 || ndist > 30) { ok = false; break; }
-        for (int i = 0; i < 19; ++i) T->lens[kClenOrder[i]] = 0;
-        for (int i = 0; i < ncode; ++i) {
-          refill();
-          if (bits < 3) { ok = false; break; }
-          T->lens[kClenOrder[i]] = (uint8_t)(hold & 7u);
-          drop(3);
-        }
-        if (!ok) break;
-        const int cmax = lane_build(T, T->croot, CROOT, T->lcnt, T->lsym, T->lens, 19, T_CODES);
-        if (cmax < 0) { ok = false; break; }
-        int have = 0;
-        while (have < nlen + ndist) {
-          refill();
-          const uint32_t e = lane_sym(T->croot, CROOT, nullptr, nullptr, cmax, nullptr, hold, bits);
-          const int nb = (int)e_len(e);
-          if (nb == 0 || nb > bits) { ok = false; break; }
-          const int sy = (int)e_val(e);
-          if (sy < 16) {
-            drop(nb);
-            T->lens[have++] = (uint8_t)sy;
-            continue;
-          }
-          const int xb = sy == 16 ? 2 : (sy == 17 ? 3 : 7);
-          if (nb + xb > bits) { ok = false; break; }
-          drop(nb);
-          int len = 0, copy;
-          if (sy == 16) {
-            if (have == 0) { ok = false; break; }
-            len = T->lens[have - 1];
-            copy = 3 + (int)(hold & 3u);
-          } else if (sy == 17) {
-            copy = 3 + (int)(hold & 7u);
-          } else {
-            copy = 11 + (int)(hold & 127u);
-          }
-          drop(xb);
-          if (have + copy > nlen + ndist) { ok = false; break; }
-          for (int i = 0; i < copy; ++i) T->lens[have + i] = (uint8_t)len;
-          have += copy;
-        }
-        if (!ok) break;
-        if (T->lens[256] == 0) { ok = false; break; }
-        lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, nlen, T_LIT);
-        // the distance lengths follow the literal/length ones in lens[]: move them first
-        for (int i = 0; i < ndist; ++i) T->lens[i] = T->lens[nlen + i];
-        dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, ndist, T_DIST);
-      } else {
-        ok = false;
-        break;
-      }
-      if (lmax < 0 || dmax < 0) { ok = false; break; }
-      // the block's symbols
-      for (;;) {
-        refill();
-        const uint32_t e = lane_sym(T->lroot, LROOT, T->lcnt, T->lsym, lmax, lit_ent, hold, bits);
-        const uint32_t eo = e_op(e);
-        if (eo == OP_BAD) { ok = false; break; }
-        drop((int)e_len(e));
-        if (eo == OP_LIT) {
-          if (!put_lit(e_val(e))) { ok = false; break; }
-          continue;
-        }
-        if (eo == OP_EOB) break;
-        const int lx = (int)e_extra(e);
-        if (lx > bits) { ok = false; break; }
-        const uint32_t mlen = e_val(e) + (uint32_t)(hold & ((1ull << lx) - 1ull));
-        drop(lx);
-        refill();
-        const uint32_t g = lane_sym(T->droot, DROOT, T->dcnt, T->dsym, dmax, dist_ent, hold, bits);
-        if (e_op(g) == OP_BAD) { ok = false; break; }
-        drop((int)e_len(g));
-        const int dx = (int)e_extra(g);
-        if (dx > bits) { ok = false; break; }
-        const uint32_t md = e_val(g) + (uint32_t)(hold & ((1ull << dx) - 1ull));
-        drop(dx);
-        if (!end_run() || !put_tok(0x80000000u | ((mlen - 3u) << 16) | (md - 1u))) { ok = false; break; }
-        outlen += mlen;
-      }
-      if (!ok) break;
     }
-    if (ok) ok = end_run();
-    if (nlit & 3u) reinterpret_cast<uint32_t*>(lit)[nlit >> 2] = litw;
-    st.ok = ok ? 1u : 0u;
-    st.n_tok = ntok;
-    st.n_lit = nlit;
-    st.out_len = outlen;
-    a.tstat[k] = st;
+    if (!whole) {
+      a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
+      continue;
+    }
+    if (kend == k) tok_message<false>(a, T, lit_ent, dist_ent, k, kend, in_len);
+    else tok_message<true>(a, T, lit_ent, dist_ent, k, kend, in_len);
   }
 }
 
@@ -1326,10 +1419,10 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
 }
 
 // ---------------------------------------------------------------------------------
-// Parallel token replay (k_infl_fast).  A session whose frames in this batch are all
-// single-frame compressed messages that k_infl_tok decoded cleanly, met in the clean
-// state (no message open, no final block seen), needs no serial decoder and no LDS
-// window: per message, the 64 lanes expand the tokens into one descriptor per output
+// Parallel token replay (k_infl_fast).  A session whose compressed messages in this
+// batch k_infl_tok all decoded cleanly (whole messages, one frame or several), met in
+// the clean state (no message open, no final block seen), needs no serial decoder and
+// no LDS window (its other frames pass through): per message, the 64 lanes expand the tokens into one descriptor per output
 // byte (a literal, or the absolute session position it copies: a back-reference byte
 // i of (length, distance) at p copies p - distance + i mod distance), chase the
 // copies that land inside the chunk through LDS, gather the ones that land before it
@@ -1367,24 +1460,9 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
   const uint64_t obase = a.out_off[s], ocap64 = a.out_off[s + 1] - a.out_off[s];
   const int64_t ocap = ocap64 < (uint64_t)POS_LIMIT ? (int64_t)ocap64 : (int64_t)POS_LIMIT;
   const wsg_inflate_state st0 = a.state[s];
-  // does the session qualify?  (every frame: a FIN TEXT/BINARY frame with RSV1, not a
-  // replay, tokens ok, some output; the state clean; the outputs fit)
-  bool ok = !st0.compressing && !(st0.has_decoder && st0.finished);
-  uint64_t need = 0;
-  for (uint32_t k = f0 + (uint32_t)lane; k < f1; k += 64) {
-    const wsg_frame_desc d = a.desc[k];
-    const InflTokStat t = a.tstat[k];
-    const uint32_t op = d.opcode & 15u, rsv = (d.flags >> 4) & 7u;
-    ok = ok && (d.flags & 0x80u) && (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u) &&
-         !(d.flags & WSG_DESC_REPLAY) && t.ok && t.out_len;
-    need += t.out_len;
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)need, d, 64), hi = (uint32_t)__shfl_xor((int)(uint32_t)(need >> 32), d, 64);
-    need += ((uint64_t)hi << 32) | lo;
-  }
-  if (__any(!ok) || (int64_t)need > ocap) {
+  // the state must be clean (no message open, no final block seen); every frame is
+  // checked as it comes (a session that fails a check is left to k_inflate)
+  if (st0.compressing || (st0.has_decoder && st0.finished)) {
     if (lane == 0) a.fast_done[s] = 0;
     return;
   }
@@ -1397,9 +1475,28 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
   int has_dec = st0.has_decoder;
   int32_t pos = 0, wstart = -wl0;
   bool bad = false;
+  int compressing = 0;
   for (uint32_t k = f0; k < f1 && !bad; ++k) {
     const wsg_frame_desc d = a.desc[k];
+    const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
+    if (d.flags & WSG_DESC_REPLAY) { bad = true; break; }
+    // PerMessageDeflateDecoder (:69-105): a TEXT/BINARY frame with RSV1 starts a compressed
+    // message, its continuations belong to it; anything else passes through unchanged
+    const bool start = (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u);
+    if (!start && !(op == WSG_OP_CONTINUATION && compressing)) {
+      if (lane == 0) {
+        wsg_frame_desc o = d;
+        o.flags = (uint8_t)(d.flags & 0xF1u);
+        o.status = 0;
+        a.out_desc[k] = o;
+      }
+      if (op < 8u && fin) compressing = 0;
+      continue;
+    }
+    if (start && compressing) { bad = true; break; }
+    // the message's pre-decode (its start frame's lane wrote every frame's stats)
     const InflTokStat ts = a.tstat[k];
+    if (!ts.ok || !ts.out_len || (int64_t)pos + ts.out_len > ocap) { bad = true; break; }
     if (!has_dec) {  // new ZlibDecoder(RAW): a fresh history (DeflateDecoder.java:80-93)
       has_dec = 1;
       wstart = pos;
@@ -1513,14 +1610,16 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
       wsg_frame_desc o;
       o.payload_off = obase + (uint64_t)P0;
       o.payload_len = L;
-      o.opcode = (uint8_t)(d.opcode & 15u);
-      const uint32_t rsv = (d.flags >> 4) & 7u;
-      o.flags = (uint8_t)((1u << 7) | ((rsv ^ 4u) << 4) | WSG_DESC_INFLATED);  // rsvBits(): RSV1 cleared (:83-85)
+      o.opcode = (uint8_t)op;
+      const uint32_t orsv = (rsv & 4u) ? (rsv ^ 4u) : rsv;  // rsvBits(): RSV1 cleared (:83-85)
+      o.flags = (uint8_t)((fin << 7) | (orsv << 4) | WSG_DESC_INFLATED);
       o.status = 0;
       a.out_desc[k] = o;
     }
-    if (a.no_context) has_dec = 0;  // decoder.event(ENDING); decoder = null (DeflateDecoder.java:107-110)
+    if (fin && a.no_context) has_dec = 0;  // decoder.event(ENDING); decoder = null (DeflateDecoder.java:107-110)
+    compressing = fin ? 0 : 1;
   }
+  if (compressing) bad = true;  // a message left open: k_inflate's snapshot and replay_from
   if (bad) {
     if (lane == 0) a.fast_done[s] = 0;
     return;

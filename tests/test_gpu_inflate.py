@@ -252,3 +252,35 @@ def test_inflate_parallel_replay_fallbacks(ctx, oracle):
                 msgs.append((1, True, 4, comp2.compress(b"the end") + comp2.flush(zlib.Z_FINISH)))
             sessions.append(msgs)
         _run(ctx, oracle, sessions, no_context, 3, rng)
+
+
+@pytest.mark.parametrize("no_context", [False, True])
+def test_inflate_fragmented_messages_predecoded(ctx, oracle, no_context):
+    """Compressed messages cut into 2-6 fragments at arbitrary bytes (tiny fragments
+    that complete no symbol included), pings and uncompressed frames between them:
+    k_infl_tok decodes whole multi-frame messages and attributes each symbol to the
+    fragment that supplies its last bit's byte (zlib's rule), so k_infl_fast can take
+    these sessions; every frame against the oracle."""
+    rng = np.random.default_rng(4242 + no_context)
+    sessions = []
+    for i in range(48):
+        comp = zlib.compressobj(int(rng.choice([1, 6, 9])), zlib.DEFLATED, -15)
+        text = wsgen.rand_text(rng, 3000)
+        frames = []
+        for m in range(int(rng.integers(1, 8))):
+            if no_context:
+                comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+            body = text[int(rng.integers(0, 1500)):][:int(rng.integers(20, 3000))] + bytes([m])
+            data = (comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH))[:-4]
+            n_cuts = int(rng.integers(1, 6))
+            cuts = sorted(set(int(x) for x in rng.integers(1, len(data), n_cuts))) if len(data) > 1 else []
+            parts = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
+            op = int(rng.choice([1, 2]))
+            for j, p in enumerate(parts):
+                frames.append((op if j == 0 else 0, j == len(parts) - 1, 4 if j == 0 else 0, p))
+                if j + 1 < len(parts) and rng.random() < 0.3:
+                    frames.append((9, True, 0, b"ping"))
+            if rng.random() < 0.2:
+                frames.append((1, True, 0, b"plain text"))
+        sessions.append(frames)
+    _run(ctx, oracle, sessions, no_context, 2, rng)
