@@ -284,3 +284,87 @@ def test_inflate_fragmented_messages_predecoded(ctx, oracle, no_context):
                 frames.append((1, True, 0, b"plain text"))
         sessions.append(frames)
     _run(ctx, oracle, sessions, no_context, 2, rng)
+
+
+def test_inflate_fast_replay_takes_fragmented_sessions(oracle):
+    """With WSG_INFLATE_FAST=2 the serial pass does not run at all, so every session must
+    be finished by the pre-decode + parallel replay: fragmented compressed messages
+    (fragments of >= 200 bytes, so each completes a symbol), pings, uncompressed frames,
+    context carried over three batches."""
+    import os
+    from snf4j_amd import Context
+    rng = np.random.default_rng(777)
+    sessions = []
+    for i in range(32):
+        comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+        text = wsgen.rand_text(rng, 4000)
+        frames = []
+        for m in range(int(rng.integers(1, 6))):
+            body = text[int(rng.integers(0, 1000)):][:int(rng.integers(1500, 3500))] + bytes([m])
+            data = (comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH))[:-4]
+            cuts, c = [], 0
+            while len(data) - c >= 400 and rng.random() < 0.7:
+                c += int(rng.integers(200, len(data) - c - 199))
+                cuts.append(c)
+            parts = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
+            op = int(rng.choice([1, 2]))
+            for j, p in enumerate(parts):
+                frames.append((op if j == 0 else 0, j == len(parts) - 1, 4 if j == 0 else 0, p))
+                if j + 1 < len(parts) and rng.random() < 0.3:
+                    frames.append((9, True, 0, b"ping"))
+            if rng.random() < 0.3:
+                frames.append((2, True, 0, b"raw"))
+        sessions.append(frames)
+    os.environ["WSG_INFLATE_FAST"] = "2"
+    try:
+        c = Context(0)
+    finally:
+        os.environ.pop("WSG_INFLATE_FAST", None)
+    try:
+        # cut each session only after a FIN data frame (a message boundary)
+        n_b = 3
+        cut_sessions = []
+        for fr in sessions:
+            e = [j + 1 for j, f in enumerate(fr) if f[1] and f[0] < 8]
+            pts = sorted(rng.choice(e, size=min(n_b - 1, len(e)), replace=False).tolist()) if e else []
+            cut_sessions.append((fr, pts))
+        _run_cuts(c, oracle, cut_sessions, False, n_b)
+    finally:
+        c.close()
+
+
+def _run_cuts(ctx, oracle, cut_sessions, no_context, n_batches):
+    """_run with given cut points per session (frame indices where batches split)."""
+    from snf4j_amd import BatchInflater
+    from snf4j_amd._lib import DESC_DTYPE
+    sessions = [fr for fr, _ in cut_sessions]
+    n_s = len(sessions)
+    cuts = []
+    for fr, pts in cut_sessions:
+        pts = (pts + [len(fr)] * n_batches)[:n_batches - 1]
+        cuts.append([0] + sorted(pts) + [len(fr)])
+    bi = BatchInflater(n_s, no_context, ctx=ctx)
+    got = [[] for _ in range(n_s)]
+    for b in range(n_batches):
+        rows, chunks, sf, pos = [], [], [0], 0
+        for s in range(n_s):
+            for (op, fin, rsv, p) in sessions[s][cuts[s][b]:cuts[s][b + 1]]:
+                r = np.zeros((), dtype=DESC_DTYPE)
+                r["payload_off"], r["payload_len"], r["opcode"] = pos, len(p), op
+                r["flags"] = (0x80 if fin else 0) | (rsv << 4)
+                rows.append(r)
+                chunks.append(p)
+                pos += len(p)
+            sf.append(len(rows))
+        desc = np.array(rows, dtype=DESC_DTYPE) if rows else np.zeros(0, DESC_DTYPE)
+        payload = np.frombuffer(b"".join(chunks) + bytes(16), dtype=np.uint8)
+        for s, (frames, exc) in enumerate(bi.run(desc, np.array(sf, np.uint32), payload)):
+            assert exc is None, (s, b, exc)
+            got[s] += frames
+    for s in range(n_s):
+        d = oracle.PerMessageDeflateDecoder(no_context)
+        exp = [d.decode(*fr) for fr in sessions[s]]
+        assert len(got[s]) == len(exp), s
+        for i, (g, o) in enumerate(zip(got[s], exp)):
+            assert (int(g.getOpcode()), g.isFinalFragment(), g.getRsvBits()) == o[:3], (s, i)
+            assert g.getPayload() == o[3], (s, i)
