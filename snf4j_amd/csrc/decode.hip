@@ -45,11 +45,14 @@ __device__ bool utf8_valid_run(const uint8_t* wire, uint64_t off, uint32_t n, ui
 //
 // c3 is the FrameUtf8Validator state a frame inherits (FrameUtf8Validator.java:59-98):
 // the last <= 3 payload bytes of the data frames since the last reset, newest in bits
-// 16-23 (the edge layout), their count in bits 24-25, bit 26 = reset.  A message start
-// resets it (FrameUtf8Validator.java:64-67), and so does a session's first frame, whose
-// element carries the session's tail from the previous batch; a FIN frame contributes
-// zero bytes (its message ended complete, or the frame failed).  carry_op is the
-// associative "last 3 bytes of the concatenation, restarted at a reset".
+// 16-23 (the edge layout), their count in bits 24-25, bit 26 = reset, bit 27 = the
+// session's tail from the previous batch still goes in front.  A message start resets
+// it (FrameUtf8Validator.java:64-67), and so does a session's first frame, marked
+// pending: k_parse reads no session state (so it can run while the previous batch
+// still streams), and k_link puts the tail in front where a carry is used
+// (resolve_c3).  A FIN frame contributes zero bytes (its message ended complete, or
+// the frame failed).  carry_op is the associative "last 3 bytes of the concatenation,
+// restarted at a reset".
 struct DAgg {
   uint64_t sum;
   int32_t m0, m1, m2;
@@ -57,12 +60,13 @@ struct DAgg {
 };
 constexpr DAgg DAGG_ID = {0ull, -1, -1, -1, 0u};
 constexpr uint32_t C3_RESET = 1u << 26;
+constexpr uint32_t C3_PENDING = 1u << 27;
 
 __device__ __forceinline__ uint32_t carry_op(uint32_t x, uint32_t y) {
   if (y & C3_RESET) return y;
   const uint32_t nx = (x >> 24) & 3u, ny = (y >> 24) & 3u;
   const uint32_t n = nx + ny < 3u ? nx + ny : 3u;
-  return ((x & 0xffffffu) >> (8 * ny)) | (y & 0xffffffu) | (n << 24) | (x & C3_RESET);
+  return ((x & 0xffffffu) >> (8 * ny)) | (y & 0xffffffu) | (n << 24) | (x & (C3_RESET | C3_PENDING));
 }
 __device__ __forceinline__ DAgg agg_op(const DAgg& x, const DAgg& y) {
   DAgg r;
@@ -90,9 +94,13 @@ __device__ __forceinline__ uint32_t tail_c3(const wsg_session_state& st) {
   return C3_RESET | (n << 24) | ((t << (24 - 8 * n)) & 0xffffffu);
 }
 
+// a carry of frame k's session with its pending tail put in front
+__device__ __forceinline__ uint32_t resolve_c3(uint32_t c, const wsg_session_state& st) {
+  return (c & C3_PENDING) ? carry_op(tail_c3(st), c & ~(C3_RESET | C3_PENDING)) : c;
+}
+
 // l3: the frame's last 3 payload bytes (edge layout; 0 for a FIN frame)
-__device__ __forceinline__ DAgg frame_agg(uint64_t k, const FrameRec& r, uint32_t l3, bool sess_first,
-                                          const wsg_session_state* state) {
+__device__ __forceinline__ DAgg frame_agg(uint64_t k, const FrameRec& r, uint32_t l3, bool sess_first) {
   DAgg v;
   v.sum = (uint64_t)((r.len + 15u) & ~15u);
   const bool data = code_is_data(r.code);
@@ -101,7 +109,7 @@ __device__ __forceinline__ DAgg frame_agg(uint64_t k, const FrameRec& r, uint32_
   v.m2 = (data && r.len) ? (int32_t)(k << 1) : -1;
   uint32_t c = (data && r.len) ? (l3 & 0xffffffu) | ((r.len < 3 ? r.len : 3u) << 24) : 0u;
   if (code_is_start(r.code)) c |= C3_RESET;
-  else if (sess_first) c = carry_op(tail_c3(state[r.sess]), c);
+  else if (sess_first) c |= C3_RESET | C3_PENDING;
   v.c3 = c;
   return v;
 }
@@ -207,7 +215,7 @@ __device__ __forceinline__ DAgg parse_one(const DecodeArgs& a, uint64_t k, uint6
            (hd.rsv << CODE_RSV_SHIFT) | (hd.masked ? CODE_MASKED : 0u) | (hd.opcode << CODE_OP_SHIFT);
   r.sess = s;
   a.rec[k] = r;
-  return frame_agg(k, r, l3, k == a.session_first[s], a.state);
+  return frame_agg(k, r, l3, k == a.session_first[s]);
 }
 
 __global__ __launch_bounds__(DBLOCK) void k_parse(DecodeArgs a) {
@@ -278,7 +286,7 @@ __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
       r.code = (fin ? CODE_FIN : 0u) | (rsv << CODE_RSV_SHIFT) | (op << CODE_OP_SHIFT);
       r.sess = s;
       a.rec[k] = r;
-      v = agg_op(v, frame_agg(k, r, l3, k == a.session_first[s], a.state));
+      v = agg_op(v, frame_agg(k, r, l3, k == a.session_first[s]));
     }
   }
   DAgg tot;
@@ -391,7 +399,7 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
       const uint32_t l3 = (code_is_data(r.code) && r.len && !(r.code & CODE_FIN)) ? a.edge[a.n_frames + k] : 0u;
       first = k == a.session_first[r.sess];
       st = a.state[r.sess];
-      v = frame_agg(k, r, l3, first, a.state);
+      v = frame_agg(k, r, l3, first);
     }
     DAgg tot;
     DAgg ex = agg_op(bp, block_excl_scan_t(v, &tot, DAGG_ID));
@@ -420,7 +428,7 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
       // a validated continuation's head against the message carry (the inherited
       // validator state: the session tail for its first frame)
       if (!status && text && op == WSG_OP_CONTINUATION &&
-          seam_utf8_error(first ? tail_c3(st) : ex.c3, a.edge[k], r.len, (r.code & CODE_FIN) != 0))
+          seam_utf8_error(first ? tail_c3(st) : resolve_c3(ex.c3, st), a.edge[k], r.len, (r.code & CODE_FIN) != 0))
         status = WSG_E_TEXT_UTF8;
       validate = (text && !status) ? 1u : 0u;
       a.vflag[k] = (uint8_t)validate;
@@ -438,7 +446,7 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
       if (k + 1 == a.session_first[s + 1]) {
         a.slink[s] = code_is_data(r.code) ? (int32_t)k : jd;
         a.slink[a.n_sessions + s] = code_is_start(r.code) ? (int32_t)k : jm;
-        a.slink[2 * a.n_sessions + s] = (int32_t)(first ? v.c3 : carry_op(ex.c3, v.c3));
+        a.slink[2 * a.n_sessions + s] = (int32_t)resolve_c3(first ? v.c3 : carry_op(ex.c3, v.c3), st);
       }
     }
     // Descriptors of the pieces whose first output byte falls in a frame's slot,
