@@ -1428,7 +1428,7 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
 // copies that land inside the chunk through LDS, gather the ones that land before it
 // from the session's output in HBM (or the carried window image), and store the
 // chunk.  Every output byte is resolved independently, so nothing serialises on a
-// window round trip, and 16 KiB of LDS per wave lets 10 sessions share a CU.  A
+// window round trip; a session is one 256-thread workgroup (4 waves, 16 KiB of LDS).  A
 // session it cannot finish (a distance too far back, capacity, any frame that does
 // not qualify) is left to k_inflate, which runs the serial decoder for exactly the
 // sessions without fast_done and overwrites whatever this kernel wrote.
@@ -1439,21 +1439,35 @@ constexpr uint32_t FC = 4096;             // output bytes resolved per chunk
 constexpr uint32_t FD_LIT = 0x80000000u;  // descriptor: a resolved byte (bits 0-7)
 constexpr int32_t FD_BIAS = 32768;        // descriptor: position + FD_BIAS (history positions are >= -32768)
 
-__device__ __forceinline__ uint32_t wave_excl_add(uint32_t v, uint32_t* total) {
-  const int lane = threadIdx.x & 63;
-  uint32_t inc = v;
+constexpr int FNT = 256;  // threads per session (4 waves)
+
+// block-wide exclusive sum of a packed (hi, lo) pair of 32-bit counts; the totals
+__device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, uint64_t* wsum) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t inc = v;
 #pragma unroll
   for (int d = 1; d < 64; d <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)inc, d, 64);
+    const uint64_t t = shfl_up_u64(inc, d);
     if (lane >= d) inc += t;
   }
-  *total = (uint32_t)__shfl((int)inc, 63, 64);
-  return inc - v;
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint64_t pre = 0, tot = 0;
+#pragma unroll
+  for (int w = 0; w < FNT / 64; ++w) {
+    pre += w < wid ? wsum[w] : 0ull;
+    tot += wsum[w];
+  }
+  __syncthreads();
+  *total = tot;
+  return pre + inc - v;
 }
 
-__global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
+__global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
   __shared__ uint32_t fd[FC];
-  const int lane = threadIdx.x;
+  __shared__ uint64_t wsum[FNT / 64];
+  __shared__ uint32_t x_first, x_off, x_li;
+  const int lane = threadIdx.x;  // (the block's thread: FNT per session)
   const uint32_t s = blockIdx.x;
   if (s >= a.n_sessions) return;
   const uint32_t f0 = a.session_first[s], f1 = a.session_first[s + 1];
@@ -1517,9 +1531,11 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
         const uint32_t tk = valid ? T[t + lane] : 0u;
         const bool ism = (tk & 0x80000000u) != 0;
         const uint32_t len = !valid ? 0u : (ism ? ((tk >> 16) & 255u) + 3u : tk);
-        uint32_t tot_len, tot_lit;
-        const uint32_t to = o + wave_excl_add(len, &tot_len);
-        const uint32_t tli = li + wave_excl_add(ism ? 0u : len, &tot_lit);
+        uint64_t tot;
+        const uint64_t ex = blk_excl_add2(((uint64_t)len << 32) | (ism ? 0u : len), &tot, wsum);
+        const uint32_t tot_len = (uint32_t)(tot >> 32), tot_lit = (uint32_t)tot;
+        const uint32_t to = o + (uint32_t)(ex >> 32);
+        const uint32_t tli = li + (uint32_t)ex;
         if (valid && to < c1 && to + len > c0) {
           const uint32_t b0 = to > c0 ? to : c0, b1 = to + len < c1 ? to + len : c1;
           if (ism) {
@@ -1535,16 +1551,25 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
             for (uint32_t j = b0; j < b1; ++j) fd[j - c0] = FD_LIT | lit[tli + (j - to)];
           }
         }
-        const uint64_t cross = __ballot(valid && to + len > c1);
-        if (cross) {  // the chunk ends inside this token: the next chunk starts from it
-          const int f = __builtin_ctzll(cross);
-          tt = t + (uint32_t)f;
-          t_off = (uint32_t)__shfl((int)to, f, 64);
-          t_li = (uint32_t)__shfl((int)tli, f, 64);
+        // the chunk ends inside a token: the next chunk starts from the first such one
+        if (threadIdx.x == 0) x_first = 0xffffffffu;
+        __syncthreads();
+        if (valid && to + len > c1) atomicMin(&x_first, (uint32_t)lane);
+        __syncthreads();
+        const uint32_t f = x_first;
+        if ((uint32_t)lane == f) {
+          x_off = to;
+          x_li = tli;
+        }
+        __syncthreads();
+        if (f != 0xffffffffu) {
+          tt = t + f;
+          t_off = x_off;
+          t_li = x_li;
           crossed = true;
           break;
         }
-        t += 64u;
+        t += (uint32_t)FNT;
         o += tot_len;
         li += tot_lit;
       }
@@ -1553,14 +1578,13 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
         t_off = o;
         t_li = li;
       }
-      if (__any(bad)) {
+      if (__syncthreads_or(bad)) {
         bad = true;
         break;
       }
-      __syncthreads();
       // 2. chase copies inside the chunk: a byte's source precedes it, so a chain
       //    ends at a literal or at a byte before the chunk (kept as a position)
-      for (uint32_t j = (uint32_t)lane; j < n; j += 64) {
+      for (uint32_t j = (uint32_t)lane; j < n; j += FNT) {
         uint32_t v = fd[j];
         while (!(v & FD_LIT) && (int32_t)v - FD_BIAS >= C0) v = fd[(int32_t)v - FD_BIAS - C0];
         fd[j] = v;
@@ -1568,11 +1592,11 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
       __syncthreads();
       // 3. gather the bytes that come from before the chunk: this batch's output (HBM),
       //    or the window carried in
-      for (uint32_t j0 = 0; j0 < n; j0 += 256) {
+      for (uint32_t j0 = 0; j0 < n; j0 += 4 * FNT) {
         uint32_t v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const uint32_t j = j0 + 64u * u + (uint32_t)lane;
+          const uint32_t j = j0 + (uint32_t)FNT * u + (uint32_t)lane;
           v[u] = j < n ? fd[j] : FD_LIT;
           if (!(v[u] & FD_LIT)) {
             const int32_t q = (int32_t)v[u] - FD_BIAS;
@@ -1582,7 +1606,7 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          const uint32_t j = j0 + 64u * u + (uint32_t)lane;
+          const uint32_t j = j0 + (uint32_t)FNT * u + (uint32_t)lane;
           if (j < n) fd[j] = v[u];
         }
       }
@@ -1593,7 +1617,7 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
       if (head > n) head = n;
       if ((uint32_t)lane < head) dst[lane] = (uint8_t)fd[lane];
       const uint32_t nw = (n - head) >> 2;
-      for (uint32_t w = (uint32_t)lane; w < nw; w += 64) {
+      for (uint32_t w = (uint32_t)lane; w < nw; w += FNT) {
         const uint32_t b = head + 4u * w;
         reinterpret_cast<uint32_t*>(dst + head)[w] =
             (fd[b] & 0xffu) | ((fd[b + 1] & 0xffu) << 8) | ((fd[b + 2] & 0xffu) << 16) | ((fd[b + 3] & 0xffu) << 24);
@@ -1637,7 +1661,7 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
     const int32_t lo = (P - nh) > 0 ? (P - nh) : 0;
     // slot j holds position q(j) in [P - 32768, P); q < 0: the old image has it already
     uint8_t* const wout = a.window + (uint64_t)s * WSG_INFLATE_WINDOW;
-    for (uint32_t j = (uint32_t)lane; j < WSG_INFLATE_WINDOW; j += 64) {
+    for (uint32_t j = (uint32_t)lane; j < WSG_INFLATE_WINDOW; j += FNT) {
       const int32_t q = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)((j - nph) & WMASK);
       if (q >= lo) wout[j] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rout, (uint32_t)q, 0, 1);
     }
@@ -1656,7 +1680,7 @@ __global__ __launch_bounds__(64) void k_infl_fast(InflArgs a) {
 }  // namespace
 
 void launch_infl_fast(const InflArgs& a, hipStream_t s) {
-  if (a.n_sessions && a.tstat && a.fast_done) hipLaunchKernelGGL(k_infl_fast, dim3(a.n_sessions), dim3(64), 0, s, a);
+  if (a.n_sessions && a.tstat && a.fast_done) hipLaunchKernelGGL(k_infl_fast, dim3(a.n_sessions), dim3(FNT), 0, s, a);
 }
 
 void launch_infl_tok(const InflArgs& a, hipStream_t s) {
