@@ -132,7 +132,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_INFL_TOK)) {
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_INFL_TOK && kid != K_INFL_FAST)) {
     f();
     return;
   }
