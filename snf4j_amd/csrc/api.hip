@@ -68,6 +68,7 @@ struct wsg_ctx {
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
   DevBuf i_tok, i_lit, i_stat, i_tab, i_fast;  // inflate pre-decode workspace
   int infl_tokens = 1;               // WSG_INFLATE_TOKENS=0 turns the pre-decode off
+  uint32_t infl_lanes = 262144;      // k_infl_tok lanes at most (WSG_INFLATE_LANES, A/B): 4 waves a SIMD, 1 GB of lane tables
   int infl_fast = 1;                 // WSG_INFLATE_FAST=0 turns the parallel token replay off (A/B); 2: it alone (tests)
   int fused_scan = 1;                // WSG_FUSED_SCAN=0: always launch k_scan (A/B)
   // host-path device buffers
@@ -163,6 +164,7 @@ int wsg_open(int device, void* stream, wsg_ctx** out) {
   c->device = device;
   if (const char* e = getenv("WSG_INFLATE_TOKENS")) c->infl_tokens = atoi(e) != 0;
   if (const char* e = getenv("WSG_INFLATE_FAST")) c->infl_fast = atoi(e);
+  if (const char* e = getenv("WSG_INFLATE_LANES")) c->infl_lanes = (uint32_t)atoi(e) < 64u ? 64u : (uint32_t)atoi(e) & ~63u;
   if (const char* e = getenv("WSG_FUSED_SCAN")) c->fused_scan = atoi(e) != 0;
   if (stream) {
     c->stream = (hipStream_t)stream;
@@ -859,7 +861,7 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   a.n_lanes = 0;
   a.fast_done = nullptr;
   if (c->infl_tokens && n_frames) {
-    const uint32_t lanes = (uint32_t)(n_frames < 65536 ? ((n_frames + 63) / 64) * 64 : 65536);
+    const uint32_t lanes = (uint32_t)(n_frames < c->infl_lanes ? ((n_frames + 63) / 64) * 64 : c->infl_lanes);
     const uint64_t lit_len = infl_lit_bytes(payload_len, n_frames);
     HIP_TRY(c, c->i_tok.ensure(infl_tok_words(payload_len, n_frames) * 4));
     HIP_TRY(c, c->i_lit.ensure(lit_len));

@@ -252,14 +252,19 @@ constexpr uint32_t TOK_SLACK = 80;  // per-frame slack of the token / literal re
 // and k_inflate decodes it itself: the serial decoder stays the authority.
 // ---------------------------------------------------------------------------------
 
-// per-lane tables in HBM scratch
-struct LaneTab {  // root entries: len | symbol << 4, len 0 = a longer code
-  uint16_t lroot[1 << LROOT];
-  uint16_t droot[1 << DROOT];
+// per-lane tables in HBM scratch.  Two levels: a root entry is len | symbol << 4 for a
+// code of at most rbits bits; for a longer code it points at a sub-table after the
+// root (len 0 | sub-table bits << 4 | offset << 7), indexed by the code's next bits, whose
+// entries carry the full length.  Any symbol is two dependent loads at most (a walk
+// of the canonical counts costs one load per code bit, and the wave waits for its
+// slowest lane).
+constexpr int LSUB = 340;  // zlib's bound for 286 codes of <= 15 bits over a 9-bit root (852 - 512)
+constexpr int DSUB = 256;  // a distance set needing more goes to the serial decoder
+struct LaneTab {
+  uint16_t lroot[(1 << LROOT) + LSUB];
+  uint16_t droot[(1 << DROOT) + DSUB];
   uint16_t croot[1 << CROOT];
-  uint16_t lcnt[16], lsym[288];
-  uint16_t dcnt[16], dsym[32];
-  uint16_t offs[16];
+  uint16_t sym[288];  // symbols in canonical order (table build)
   uint8_t lens[320];
 };
 
@@ -278,32 +283,14 @@ struct Src {
       if ((uint64_t)q * 16 + t < pay_len) w[t >> 2] |= (uint32_t)pay[(uint64_t)q * 16 + t] << (8 * (t & 3));
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
-  __device__ uint32_t at(uint32_t i) {
-    if (i >= plen) return (i - plen) < 2u ? 0x00u : 0xffu;  // DeflateCodec TAIL 00 00 FF FF
-    const uint64_t g = off + i;
-    const int64_t q = (int64_t)(g >> 4);
-    if (q != cq) {
-      cq = q;
-      if ((uint64_t)q * 16 + 16 <= pay_len) {
-        blk = reinterpret_cast<const uint4*>(pay)[q];
-      } else {
-        uint32_t w[4] = {0u, 0u, 0u, 0u};
-        for (int t = 0; t < 16; ++t)
-          if ((uint64_t)q * 16 + t < pay_len) w[t >> 2] |= (uint32_t)pay[(uint64_t)q * 16 + t] << (8 * (t & 3));
-        blk = make_uint4(w[0], w[1], w[2], w[3]);
-      }
-    }
-    const uint32_t o = (uint32_t)(g & 15u);
-    const uint32_t w = o < 8u ? (o < 4u ? blk.x : blk.y) : (o < 12u ? blk.z : blk.w);
-    return (w >> (8u * (o & 3u))) & 0xffu;
-  }
 };
 
-// Canonical tables of lens[0..n) into root (rbits) + cnt/sym: the longest length, or
-// -1 for any set that is not complete (over-subscribed, incomplete, empty): the
-// serial decoder then takes the frame and applies zlib's exact rules.
-__device__ int lane_build(LaneTab* T, uint16_t* root, int rbits, uint16_t* cnt, uint16_t* sym, const uint8_t* lens,
-                          int n, int kind) {
+// Canonical two-level table of lens[0..n) (rbits root bits, at most sub entries after
+// the root): the longest length, or -1 for any set that is not complete (over-subscribed,
+// incomplete, empty) or that needs more sub-table room: the serial decoder then takes
+// the frame and applies zlib's exact rules.  Sub-tables are sized as zlib's
+// inflate_table sizes them: grown while the codes left at the next length do not fill it.
+__device__ int lane_build(uint16_t* root, int rbits, int sub, uint16_t* sym, const uint8_t* lens, int n) {
   // counts and running offsets live in registers (a select chain per symbol): a
   // read-modify-write of counters in HBM scratch would chain every symbol on its latency
   int c[16];
@@ -315,19 +302,12 @@ __device__ int lane_build(LaneTab* T, uint16_t* root, int rbits, uint16_t* cnt, 
     for (int L = 1; L < 16; ++L) c[L] += (l == L) ? 1 : 0;
   }
   int left = 1, maxl = 0;
+  bool bad = false;
 #pragma unroll
   for (int l = 1; l < 16; ++l) {
     left = (left << 1) - c[l];
+    bad |= left < 0;
     if (c[l]) maxl = l;
-  }
-  bool bad = false;
-  {
-    int lf = 1;
-#pragma unroll
-    for (int l = 1; l < 16; ++l) {
-      lf = (lf << 1) - c[l];
-      bad |= lf < 0;
-    }
   }
   if (bad || left != 0 || maxl == 0) return -1;
   int o[16];
@@ -339,8 +319,6 @@ __device__ int lane_build(LaneTab* T, uint16_t* root, int rbits, uint16_t* cnt, 
       off += c[l];
     }
   }
-#pragma unroll
-  for (int l = 1; l < 16; ++l) cnt[l] = (uint16_t)c[l];
   for (int s = 0; s < n; ++s) {
     const int l = lens[s];
     if (!l) continue;
@@ -351,7 +329,8 @@ __device__ int lane_build(LaneTab* T, uint16_t* root, int rbits, uint16_t* cnt, 
     sym[at] = (uint16_t)s;
   }
   const uint32_t rsize = 1u << rbits;
-  int code = 0, idx = 0;
+  uint32_t code = 0, pfx = 0xffffffffu, next = rsize, sbase = 0, sbits = 0;
+  int idx = 0;
   for (int l = 1; l <= maxl; ++l) {
     int cl = 0;
 #pragma unroll
@@ -359,43 +338,50 @@ __device__ int lane_build(LaneTab* T, uint16_t* root, int rbits, uint16_t* cnt, 
       if (l == L) cl = c[L];
     for (int i = 0; i < cl; ++i, ++idx, ++code) {
       const uint32_t sy = sym[idx];
-      const uint32_t rev = __builtin_bitreverse32((uint32_t)code) >> (32 - l);
+      const uint32_t rev = __builtin_bitreverse32(code) >> (32 - l);
+      const uint16_t e = (uint16_t)((uint32_t)l | (sy << 4));
       if (l <= rbits) {
-        const uint16_t e = (uint16_t)((uint32_t)l | (sy << 4));
         for (uint32_t j = rev; j < rsize; j += (1u << l)) root[j] = e;
       } else {
-        root[rev & (rsize - 1)] = 0;
+        if ((rev & (rsize - 1u)) != pfx) {  // a new root prefix: its sub-table
+          pfx = rev & (rsize - 1u);
+          // c[] holds the codes not yet placed at each length (this one included)
+          int curr = l - rbits, room = 1 << curr;
+          while (curr + rbits < maxl) {
+            int cn = 0;
+#pragma unroll
+            for (int L = 1; L < 16; ++L)
+              if (curr + rbits == L) cn = c[L];
+            room -= cn;
+            if (room <= 0) break;
+            ++curr;
+            room <<= 1;
+          }
+          if (next + (1u << curr) > rsize + (uint32_t)sub) return -1;
+          sbase = next;
+          sbits = (uint32_t)curr;
+          next += 1u << curr;
+          root[pfx] = (uint16_t)((sbits << 4) | ((sbase - rsize) << 7));
+        }
+        for (uint32_t j = rev >> rbits; j < (1u << sbits); j += 1u << (l - rbits)) root[sbase + j] = e;
       }
+#pragma unroll
+      for (int L = 1; L < 16; ++L)
+        if (l == L) --c[L];
     }
     code <<= 1;
   }
-  (void)kind;
   return maxl;
 }
 
-// The symbol at the bit buffer (>= maxl bits held, or the whole rest of the input):
-// the table entry, or OP_BAD with len 0 when the code runs past the bits held.
-__device__ __forceinline__ uint32_t lane_sym(const uint16_t* root, int rbits, const uint16_t* cnt, const uint16_t* sym,
-                                             int maxl, const uint32_t* ents, uint64_t hold, int bits) {
-  const uint32_t r = root[(uint32_t)hold & ((1u << rbits) - 1u)];
-  uint32_t len = r & 15u, sy = r >> 4;
-  if (len == 0) {
-    int code = 0, first = 0, index = 0;
-    for (int l = 1; l <= maxl && l <= bits; ++l) {
-      code |= (int)((hold >> (l - 1)) & 1u);
-      const int count = cnt[l];
-      if (code - count < first) {
-        len = (uint32_t)l;
-        sy = sym[index + (code - first)];
-        break;
-      }
-      index += count;
-      first += count;
-      first <<= 1;
-      code <<= 1;
-    }
-    if (len == 0) return ent(0, 0, OP_BAD, 0);
-  }
+// The symbol at the bit buffer: the table entry, or OP_BAD with len 0 when the code
+// runs past the bits held (the rest of the input: a complete set fills every slot).
+__device__ __forceinline__ uint32_t lane_sym(const uint16_t* root, int rbits, const uint32_t* ents, uint64_t hold,
+                                             int bits) {
+  uint32_t r = root[(uint32_t)hold & ((1u << rbits) - 1u)];
+  if ((r & 15u) == 0)
+    r = root[(1u << rbits) + (r >> 7) + ((uint32_t)(hold >> rbits) & ((1u << ((r >> 4) & 7u)) - 1u))];
+  const uint32_t len = r & 15u, sy = r >> 4;
   if ((int)len > bits) return ent(0, 0, OP_BAD, 0);
   return ents ? (ents[sy] | len) : ent(len, 0, OP_LIT, sy);
 }
@@ -410,7 +396,7 @@ __device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
 // single-frame instantiation keeps the segment and attribution steps out of its loop).
 template <bool MULTI>
 __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const uint32_t* lit_ent,
-                                            const uint32_t* dist_ent, uint64_t k, uint64_t kend, uint32_t in_len) {
+                                            uint64_t k, uint64_t kend, uint32_t in_len) {
   const wsg_frame_desc d = a.desc[k];
   // the next data frame of the message after j (j < kend)
   auto next_frame = [&](uint64_t j) -> uint64_t {
@@ -562,12 +548,12 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
     int lmax, dmax;
     if (type == 1) {  // fixed codes
       for (int i = 0; i < 288; ++i) T->lens[i] = i < 144 ? 8 : (i < 256 ? 9 : (i < 280 ? 7 : 8));
-      lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, 288, T_LIT);
+      lmax = lane_build(T->lroot, LROOT, LSUB, T->sym, T->lens, 288);
       for (int i = 0; i < 30; ++i) T->lens[i] = 5;
       // zlib's fixed distance set has 30 codes of 5 bits + the 2 invalid ones: complete with 32
       T->lens[30] = 5;
       T->lens[31] = 5;
-      dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, 32, T_DIST);
+      dmax = lane_build(T->droot, DROOT, DSUB, T->sym, T->lens, 32);
     } else if (type == 2) {  // dynamic codes
       refill();
       if (bits < 14) { ok = false; break; }
@@ -583,12 +569,12 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
         drop(3);
       }
       if (!ok) break;
-      const int cmax = lane_build(T, T->croot, CROOT, T->lcnt, T->lsym, T->lens, 19, T_CODES);
+      const int cmax = lane_build(T->croot, CROOT, 0, T->sym, T->lens, 19);
       if (cmax < 0) { ok = false; break; }
       int have = 0;
       while (have < nlen + ndist) {
         refill();
-        const uint32_t e = lane_sym(T->croot, CROOT, nullptr, nullptr, cmax, nullptr, hold, bits);
+        const uint32_t e = lane_sym(T->croot, CROOT, nullptr, hold, bits);
         const int nb = (int)e_len(e);
         if (nb == 0 || nb > bits) { ok = false; break; }
         const int sy = (int)e_val(e);
@@ -617,41 +603,45 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
       }
       if (!ok) break;
       if (T->lens[256] == 0) { ok = false; break; }
-      lmax = lane_build(T, T->lroot, LROOT, T->lcnt, T->lsym, T->lens, nlen, T_LIT);
+      lmax = lane_build(T->lroot, LROOT, LSUB, T->sym, T->lens, nlen);
       // the distance lengths follow the literal/length ones in lens[]: move them first
       for (int i = 0; i < ndist; ++i) T->lens[i] = T->lens[nlen + i];
-      dmax = lane_build(T, T->droot, DROOT, T->dcnt, T->dsym, T->lens, ndist, T_DIST);
+      dmax = lane_build(T->droot, DROOT, DSUB, T->sym, T->lens, ndist);
     } else {
       ok = false;
       break;
     }
     if (lmax < 0 || dmax < 0) { ok = false; break; }
-    // the block's symbols
+    // the block's symbols, one code a step: a literal/length code, or the distance code
+    // of the length before it.  One lookup path for both keeps the 64 lanes in step (a
+    // length and its distance as one step runs both paths on every step, as some lane
+    // of 64 almost always has a match).
+    uint32_t mlen = 0;  // a length waiting for its distance
     for (;;) {
-      refill();
-      const uint32_t e = lane_sym(T->lroot, LROOT, T->lcnt, T->lsym, lmax, lit_ent, hold, bits);
-      const uint32_t eo = e_op(e);
-      if (eo == OP_BAD) { ok = false; break; }
-      drop((int)e_len(e));
-      if (eo == OP_LIT) {
-        if (!attrib() || !put_lit(e_val(e))) { ok = false; break; }
-        continue;
+      if (bits < 32) refill();  // a step takes at most 15 + 13 bits
+      const bool dist = mlen != 0;
+      const uint16_t* const root = dist ? T->droot : T->lroot;
+      const int rb = dist ? DROOT : LROOT;
+      uint32_t r = root[(uint32_t)hold & ((1u << rb) - 1u)];
+      if ((r & 15u) == 0)
+        r = root[(1u << rb) + (r >> 7) + ((uint32_t)(hold >> rb) & ((1u << ((r >> 4) & 7u)) - 1u))];
+      const uint32_t len = r & 15u;
+      const uint32_t e = lit_ent[(r >> 4) + (dist ? 288u : 0u)];  // dist_ent follows lit_ent
+      const uint32_t x = e_extra(e), eo = e_op(e);
+      if ((int)(len + x) > bits || eo == OP_BAD) { ok = false; break; }
+      const uint32_t v = e_val(e) + ((uint32_t)(hold >> len) & ((1u << x) - 1u));
+      drop((int)(len + x));
+      if (dist) {
+        if (!attrib() || !end_run() || !put_tok(0x80000000u | ((mlen - 3u) << 16) | (v - 1u))) { ok = false; break; }
+        outlen += mlen;
+        mlen = 0;
+      } else if (eo == OP_LIT) {
+        if (!attrib() || !put_lit(v)) { ok = false; break; }
+      } else if (eo == OP_EOB) {
+        break;
+      } else {
+        mlen = v;
       }
-      if (eo == OP_EOB) break;
-      const int lx = (int)e_extra(e);
-      if (lx > bits) { ok = false; break; }
-      const uint32_t mlen = e_val(e) + (uint32_t)(hold & ((1ull << lx) - 1ull));
-      drop(lx);
-      refill();
-      const uint32_t g = lane_sym(T->droot, DROOT, T->dcnt, T->dsym, dmax, dist_ent, hold, bits);
-      if (e_op(g) == OP_BAD) { ok = false; break; }
-      drop((int)e_len(g));
-      const int dx = (int)e_extra(g);
-      if (dx > bits) { ok = false; break; }
-      const uint32_t md = e_val(g) + (uint32_t)(hold & ((1ull << dx) - 1ull));
-      drop(dx);
-      if (!attrib() || !end_run() || !put_tok(0x80000000u | ((mlen - 3u) << 16) | (md - 1u))) { ok = false; break; }
-      outlen += mlen;
     }
     if (!ok) break;
   }
@@ -667,9 +657,9 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
 
 __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
   // symbol -> entry (base, extra bits, op) for the 16-bit root entries
-  __shared__ uint32_t lit_ent[288], dist_ent[32];
-  for (int i = threadIdx.x; i < 288; i += 64) lit_ent[i] = sym_entry(T_LIT, (uint32_t)i, 0);
-  if (threadIdx.x < 32) dist_ent[threadIdx.x] = sym_entry(T_DIST, threadIdx.x, 0);
+  __shared__ uint32_t ents[288 + 32];  // literal/length entries, then distance entries
+  for (int i = threadIdx.x; i < 288; i += 64) ents[i] = sym_entry(T_LIT, (uint32_t)i, 0);
+  if (threadIdx.x < 32) ents[288 + threadIdx.x] = sym_entry(T_DIST, threadIdx.x, 0);
   __syncthreads();
   const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane_id >= a.n_lanes) return;
@@ -710,8 +700,8 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
       a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
       continue;
     }
-    if (kend == k) tok_message<false>(a, T, lit_ent, dist_ent, k, kend, in_len);
-    else tok_message<true>(a, T, lit_ent, dist_ent, k, kend, in_len);
+    if (kend == k) tok_message<false>(a, T, ents, k, kend, in_len);
+    else tok_message<true>(a, T, ents, k, kend, in_len);
   }
 }
 
