@@ -66,10 +66,12 @@ struct wsg_ctx {
   // aggregate workspace
   DevBuf a_code, a_last, a_pl, a_cl, a_rec, a_blk, a_sess_err, a_pieces;
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
-  DevBuf i_tok, i_lit, i_stat, i_tab, i_fast;  // inflate pre-decode workspace
+  DevBuf i_tok, i_lit, i_stat, i_tab, i_fast, i_ord;  // inflate pre-decode workspace
   int infl_tokens = 1;               // WSG_INFLATE_TOKENS=0 turns the pre-decode off
   uint32_t infl_lanes = 262144;      // k_infl_tok lanes at most (WSG_INFLATE_LANES, A/B): 4 waves a SIMD, 1 GB of lane tables
-  int infl_fast = 1;                 // WSG_INFLATE_FAST=0 turns the parallel token replay off (A/B); 2: it alone (tests)
+  int infl_fast = 1;
+  int infl_lds = 1;                  // WSG_INFLATE_LDS=0: the pre-decode keeps its tables in HBM (A/B)
+  int infl_order = 1;                // WSG_INFLATE_ORDER=0: lanes take frames in batch order (A/B)                 // WSG_INFLATE_FAST=0 turns the parallel token replay off (A/B); 2: it alone (tests)
   int fused_scan = 1;                // WSG_FUSED_SCAN=0: always launch k_scan (A/B)
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
@@ -164,6 +166,8 @@ int wsg_open(int device, void* stream, wsg_ctx** out) {
   c->device = device;
   if (const char* e = getenv("WSG_INFLATE_TOKENS")) c->infl_tokens = atoi(e) != 0;
   if (const char* e = getenv("WSG_INFLATE_FAST")) c->infl_fast = atoi(e);
+  if (const char* e = getenv("WSG_INFLATE_LDS")) c->infl_lds = atoi(e) != 0;
+  if (const char* e = getenv("WSG_INFLATE_ORDER")) c->infl_order = atoi(e) != 0;
   if (const char* e = getenv("WSG_INFLATE_LANES")) c->infl_lanes = (uint32_t)atoi(e) < 64u ? 64u : (uint32_t)atoi(e) & ~63u;
   if (const char* e = getenv("WSG_FUSED_SCAN")) c->fused_scan = atoi(e) != 0;
   if (stream) {
@@ -194,7 +198,7 @@ int wsg_close(wsg_ctx* c) {
   for (DevBuf* b : bufs) b->release();
   DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,     &c->a_rec,
                      &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc, &c->i_tok, &c->i_lit,
-                     &c->i_stat, &c->i_tab, &c->i_fast};
+                     &c->i_stat, &c->i_tab, &c->i_fast, &c->i_ord};
   for (DevBuf* b : abufs) b->release();
   for (HostSlot& hs : c->slot) {
     DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
@@ -860,6 +864,9 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   a.tab = nullptr;
   a.n_lanes = 0;
   a.fast_done = nullptr;
+  a.order = nullptr;
+  a.ord_cnt = nullptr;
+  a.tok_lds = c->infl_lds;
   if (c->infl_tokens && n_frames) {
     const uint32_t lanes = (uint32_t)(n_frames < c->infl_lanes ? ((n_frames + 63) / 64) * 64 : c->infl_lanes);
     const uint64_t lit_len = infl_lit_bytes(payload_len, n_frames);
@@ -873,6 +880,13 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
     a.tstat = (InflTokStat*)c->i_stat.p;
     a.tab = (uint8_t*)c->i_tab.p;
     a.n_lanes = lanes;
+    a.order = nullptr;
+    a.ord_cnt = nullptr;
+    if (c->infl_order) {
+      HIP_TRY(c, c->i_ord.ensure(infl_ord_words(n_frames) * 4));
+      a.order = (uint32_t*)c->i_ord.p;
+      a.ord_cnt = a.order + n_frames;
+    }
     timed(c, K_INFL_TOK, [&] { launch_infl_tok(a, c->stream); });
     if (c->infl_fast) {
       HIP_TRY(c, c->i_fast.ensure(n_sessions));

@@ -252,6 +252,28 @@ constexpr uint32_t TOK_SLACK = 80;  // per-frame slack of the token / literal re
 // and k_inflate decodes it itself: the serial decoder stays the authority.
 // ---------------------------------------------------------------------------------
 
+// Phase clocks for tools/prof_inflate.hip and tools/prof_infl_tok.hip (compiled out of the library).
+#ifdef WSG_INFLATE_PROF
+__device__ unsigned long long g_infl_prof[24];
+#define PROF_T(v) const uint64_t v = clock64()
+#define PROF_ACC(i, v) pf_[i] += clock64() - (v)
+#define PROF_CNT(i, n) pf_[i] += (uint64_t)(n)
+#else
+#define PROF_T(v)
+#define PROF_ACC(i, v)
+#define PROF_CNT(i, n)
+#endif
+#ifdef WSG_INFLATE_TOK_PROF
+__device__ unsigned long long g_tok_prof[8];
+#define TPROF_T(v) const uint64_t v = clock64()
+#define TPROF_ACC(i, v) pf_[i] += clock64() - (v)
+#define TPROF_CNT(i, n) pf_[i] += (uint64_t)(n)
+#else
+#define TPROF_T(v)
+#define TPROF_ACC(i, v)
+#define TPROF_CNT(i, n)
+#endif
+
 // per-lane tables in HBM scratch.  Two levels: a root entry is len | symbol << 4 for a
 // code of at most rbits bits; for a longer code it points at a sub-table after the
 // root (len 0 | sub-table bits << 4 | offset << 7), indexed by the code's next bits, whose
@@ -396,7 +418,9 @@ __device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
 // single-frame instantiation keeps the segment and attribution steps out of its loop).
 template <bool MULTI>
 __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const uint32_t* lit_ent,
-                                            uint64_t k, uint64_t kend, uint32_t in_len) {
+                                            uint64_t k, uint64_t kend, uint32_t in_len, uint64_t* pf_) {
+  (void)pf_;
+  TPROF_T(t_msg);
   const wsg_frame_desc d = a.desc[k];
   // the next data frame of the message after j (j < kend)
   auto next_frame = [&](uint64_t j) -> uint64_t {
@@ -478,7 +502,9 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
     if (nlit >= lit_cap) return false;
     litw |= b << (8 * (nlit & 3u));
     if ((++nlit & 3u) == 0) {
+#ifndef TOK_EXP_NOSTORE
       reinterpret_cast<uint32_t*>(lit)[(nlit >> 2) - 1] = litw;
+#endif
       litw = 0;
     }
     ++run;
@@ -487,7 +513,11 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
   };
   auto put_tok = [&](uint32_t t) -> bool {
     if (ntok >= tok_cap) return false;
+#ifdef TOK_EXP_NOSTORE
+    ntok++;
+#else
     tok[ntok++] = t;
+#endif
     return true;
   };
   auto end_run = [&]() -> bool {
@@ -546,6 +576,8 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
       continue;
     }
     int lmax, dmax;
+    TPROF_CNT(5, 1);
+    TPROF_T(t_hdr);
     if (type == 1) {  // fixed codes
       for (int i = 0; i < 288; ++i) T->lens[i] = i < 144 ? 8 : (i < 256 ? 9 : (i < 280 ? 7 : 8));
       lmax = lane_build(T->lroot, LROOT, LSUB, T->sym, T->lens, 288);
@@ -603,21 +635,26 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
       }
       if (!ok) break;
       if (T->lens[256] == 0) { ok = false; break; }
+      TPROF_T(t_bld);
       lmax = lane_build(T->lroot, LROOT, LSUB, T->sym, T->lens, nlen);
       // the distance lengths follow the literal/length ones in lens[]: move them first
       for (int i = 0; i < ndist; ++i) T->lens[i] = T->lens[nlen + i];
       dmax = lane_build(T->droot, DROOT, DSUB, T->sym, T->lens, ndist);
+      TPROF_ACC(2, t_bld);
     } else {
       ok = false;
       break;
     }
+    TPROF_ACC(1, t_hdr);
     if (lmax < 0 || dmax < 0) { ok = false; break; }
+    TPROF_T(t_sym);
     // the block's symbols, one code a step: a literal/length code, or the distance code
     // of the length before it.  One lookup path for both keeps the 64 lanes in step (a
     // length and its distance as one step runs both paths on every step, as some lane
     // of 64 almost always has a match).
     uint32_t mlen = 0;  // a length waiting for its distance
     for (;;) {
+      TPROF_CNT(4, 1);
       if (bits < 32) refill();  // a step takes at most 15 + 13 bits
       const bool dist = mlen != 0;
       const uint16_t* const root = dist ? T->droot : T->lroot;
@@ -643,6 +680,7 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
         mlen = v;
       }
     }
+    TPROF_ACC(3, t_sym);
     if (!ok) break;
   }
   // the frames left: the last symbol's frame and any after it (no output: the
@@ -653,18 +691,459 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
     if (last) break;
   }
   if (!ok) a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};  // the message goes to the serial decoder
+  TPROF_ACC(0, t_msg);
+  TPROF_CNT(6, 1);
+}
+
+// ---------------------------------------------------------------------------------
+// Single-frame messages from LDS (the common case).  A lane's tables in HBM scratch
+// made every step wait on a global load (and, through the in-order vector memory
+// counter, on the window loads and the output stores issued before it), and 128K
+// lanes' tables do not fit L2.  Here a lane's tables and its input live in LDS:
+//   * literal/length table: 8-bit root + up to QL_SUB sub-table entries; distance:
+//     7-bit root + QD_SUB (a set needing more runs on the HBM tables instead);
+//     fixed-code blocks use shared 9/5-bit tables built once per workgroup;
+//   * the input: a 64-B ring of the payload's 32-B aligned chunks, topped up at
+//     wave-uniform points (when some lane is about to run dry) from a chunk already
+//     loaded into registers, so the only wait on global memory is there;
+//   * the code lengths of a header in the distance table's space (byte q of a lane
+//     in dword q / 4), the code-length code table in the literal table's.
+// The output (literal bytes, tokens) goes to HBM as in tok_message; nothing waits on
+// those stores until the next ring top-up.
+// ---------------------------------------------------------------------------------
+constexpr int QL_ROOT = 8, QD_ROOT = 7, QC_ROOT = 7;  // per-lane root bits
+constexpr int QL_SUB = 96, QD_SUB = 32;              // sub-table entries a lane may use
+constexpr int QL_N = (1 << QL_ROOT) + QL_SUB;        // u16 entries per lane
+constexpr int QD_N = (1 << QD_ROOT) + QD_SUB;
+constexpr int QF_LROOT = 9, QF_DROOT = 5;            // fixed codes (shared tables)
+constexpr uint32_t QF_L = 0, QF_D = 1u << QF_LROOT;  // their u16 offsets
+constexpr uint32_t Q_LT = QF_D + (1u << QF_DROOT);   // lane tables: entry j of lane i at Q_LT + j * 64 + i
+constexpr uint32_t Q_DT = Q_LT + QL_N * 64;
+constexpr uint32_t Q_TAB = Q_DT + QD_N * 64;
+constexpr int Q_RING = 17;                           // ring dwords per lane: 16 + slot 0 mirrored
+static_assert(QD_N * 2 >= 320, "the code lengths of a header fit a lane's distance table");
+static_assert((Q_DT * 2) % 4 == 0, "code-length dwords are aligned");
+
+struct TokLds {
+  uint32_t ents[320];        // symbol -> entry: literal/length, then distance
+  uint16_t tab[Q_TAB];       // fixed tables, then the lanes' tables
+  uint32_t ring[Q_RING * 64];  // input ring: dword slot s of lane i at s * 64 + i
+};
+
+enum : int { Q_OK = 0, Q_BAD = 1, Q_BAIL = 2 };
+
+// Canonical two-level table of n code lengths into tab (entry j at base + (j << 6)):
+// root entries len | symbol << 4; a prefix of longer codes points at its sub-table
+// (len 0 | sub bits << 4 | offset << 8), sized by the longest code under the prefix.
+// Codes are canonical, so the long codes take the top root prefixes and, code order
+// and length order agreeing, the longest code under a prefix is the one that ends
+// it.  Returns the longest length, -1 for a set that is not complete (the serial
+// decoder applies zlib's rules), -2 when the sub-tables need more than sub entries.
+template <class LensF>
+__device__ int q_build(uint16_t* tab, uint32_t base, int rb, int sub, LensF lens, int n) {
+  int c[16];
+#pragma unroll
+  for (int l = 0; l < 16; ++l) c[l] = 0;
+  for (int s = 0; s < n; ++s) {
+    const int l = lens(s);
+#pragma unroll
+    for (int L = 1; L < 16; ++L) c[L] += (l == L) ? 1 : 0;
+  }
+  int left = 1, maxl = 0;
+  bool bad = false;
+#pragma unroll
+  for (int l = 1; l < 16; ++l) {
+    left = (left << 1) - c[l];
+    bad |= left < 0;
+    if (c[l]) maxl = l;
+  }
+  if (bad || left != 0 || maxl == 0) return -1;
+  int nx[16];  // first code of each length (MSB-first)
+  {
+    int code = 0;
+    nx[0] = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) {
+      code = (code + c[l - 1]) << 1;
+      nx[l] = code;
+    }
+  }
+  const uint32_t rsize = 1u << rb;
+  if (maxl > rb) {
+    // the long prefixes: from the first rb-bit code no shorter code takes
+    int P = 0, L = rb + 1;
+#pragma unroll
+    for (int l = 1; l < 16; ++l)
+      if (l == rb) P = nx[l] + c[l];
+    uint32_t used = 0;
+    for (; P < (int)rsize; ++P) {
+      const int pend = (P + 1) << (15 - rb);
+      for (;;) {  // the end (left-justified to 15 bits) of the codes of length <= L
+        int e = 0;
+#pragma unroll
+        for (int l = 1; l < 16; ++l)
+          if (l == L) e = (nx[l] + c[l]) << (15 - l);
+        if (e >= pend) break;
+        ++L;
+      }
+      const uint32_t sb = (uint32_t)(L - rb);
+      if (used + (1u << sb) > (uint32_t)sub) return -2;
+      const uint32_t slot = __builtin_bitreverse32((uint32_t)P) >> (32 - rb);
+      tab[base + (slot << 6)] = (uint16_t)((sb << 4) | (used << 8));
+      used += 1u << sb;
+    }
+  }
+  for (int s = 0; s < n; ++s) {
+    const int l = lens(s);
+    if (!l) continue;
+    int code = 0;
+#pragma unroll
+    for (int L = 1; L < 16; ++L)
+      if (l == L) code = nx[L]++;
+    const uint32_t rev = __builtin_bitreverse32((uint32_t)code) >> (32 - l);
+    const uint16_t e = (uint16_t)((uint32_t)l | ((uint32_t)s << 4));
+    if (l <= rb) {
+      for (uint32_t j = rev; j < rsize; j += 1u << l) tab[base + (j << 6)] = e;
+    } else {
+      const uint32_t r = tab[base + ((rev & (rsize - 1u)) << 6)];
+      const uint32_t sb = (r >> 4) & 15u, off = r >> 8;
+      for (uint32_t j = rev >> rb; j < (1u << sb); j += 1u << (l - rb)) tab[base + ((rsize + off + j) << 6)] = e;
+    }
+  }
+  return maxl;
+}
+
+// The fixed-code tables (RFC 1951 3.2.6), shared by the workgroup.
+__device__ void q_fixed_tables(uint16_t* tab, int t) {
+  for (int s = t; s < 288; s += 64) {
+    int l, code;
+    if (s < 144) { l = 8; code = 0x30 + s; }
+    else if (s < 256) { l = 9; code = 0x190 + (s - 144); }
+    else if (s < 280) { l = 7; code = s - 256; }
+    else { l = 8; code = 0xC0 + (s - 280); }
+    const uint32_t rev = __builtin_bitreverse32((uint32_t)code) >> (32 - l);
+    for (uint32_t j = rev; j < (1u << QF_LROOT); j += 1u << l) tab[QF_L + j] = (uint16_t)(l | (s << 4));
+  }
+  if (t < 32) tab[QF_D + (__builtin_bitreverse32((uint32_t)t) >> 27)] = (uint16_t)(5 | (t << 4));
+}
+
+// One single-frame message from LDS.  Q_BAIL: a table needs more sub-table room than
+// the LDS gives a lane; the caller decodes the message with the HBM tables instead.
+__device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, const wsg_frame_desc& d, uint64_t k,
+                                              uint64_t* pf_) {
+  (void)pf_;
+  const uint32_t lane = threadIdx.x;
+  const uint32_t plen = d.payload_len, total = plen + 4u;
+  const uint64_t off = d.payload_off;
+  const uint32_t tok_cap = plen + 68u, lit_cap = 3u * (plen + 4u) + 60u;
+  uint32_t* const tok = a.tok + tok_base(off, k);
+  uint8_t* const lit = a.lit + lit_base(off, k);
+  uint16_t* const tab = Q.tab;
+  uint8_t* const lensb = reinterpret_cast<uint8_t*>(Q.tab + Q_DT);  // code length s: byte s & 3 of dword (s >> 2) * 64 + lane
+  const uint32_t lt = Q_LT + lane, dt = Q_DT + lane;
+  // --- the input ring ---
+  const uint8_t* const pay = a.payload;
+  const uint64_t pay_len = a.payload_len;
+  auto chunk = [&](uint64_t g, uint32_t* w) {  // the 32 bytes at g (32-B aligned), zeros past the payload
+    if (g + 32 <= pay_len) {
+      const uint4 x = reinterpret_cast<const uint4*>(pay + g)[0], y = reinterpret_cast<const uint4*>(pay + g)[1];
+      w[0] = x.x; w[1] = x.y; w[2] = x.z; w[3] = x.w; w[4] = y.x; w[5] = y.y; w[6] = y.z; w[7] = y.w;
+    } else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        uint32_t v = 0;
+        for (int b = 0; b < 4; ++b)
+          if (g + 4 * i + b < pay_len) v |= (uint32_t)pay[g + 4 * i + b] << (8 * b);
+        w[i] = v;
+      }
+    }
+  };
+  auto put_chunk = [&](uint64_t g, const uint32_t* w) {
+    const uint32_t s0 = (uint32_t)(g >> 2) & 15u;  // 0 or 8
+#pragma unroll
+    for (int i = 0; i < 8; ++i) Q.ring[(s0 + i) * 64 + lane] = w[i];
+    if (s0 == 0) Q.ring[16 * 64 + lane] = w[0];
+  };
+  uint64_t fill = off & ~(uint64_t)31;  // the next chunk to enter the ring
+  const uint64_t pe = off + plen;        // where the payload ends: the tail 00 00 FF FF goes there
+  auto top_up = [&]() {
+    uint32_t w[8];
+    chunk(fill, w);
+    if (fill + 32 > pe) {  // DeflateCodec TAIL after the payload, in the ring itself
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const uint64_t g = fill + 4 * i + b;
+          if (g >= pe) {
+            const uint64_t q = g - pe;
+            const uint32_t by = q < 2 ? 0x00u : (q < 4 ? 0xffu : 0x00u);
+            w[i] = (w[i] & ~(0xffu << (8 * b))) | (by << (8 * b));
+          }
+        }
+    }
+    put_chunk(fill, w);
+    fill += 32;
+  };
+  top_up();
+  top_up();
+  uint64_t hold = 0;
+  int bits = 0;
+  uint32_t ip = 0;                                   // message offset of the next input byte
+  uint32_t avail = (uint32_t)(fill - off);           // ring bytes from ip on
+  const uint32_t off32 = (uint32_t)off;
+  // top-up: at a point every active lane reaches, when some lane has under 4 bytes in
+  // the ring, every lane with room loads a chunk into it.  The load is waited on right
+  // there: a chunk loaded ahead into registers kept a load pending across the step
+  // loop, and the compiler then waited on the vector memory counter at every step.
+  auto service = [&]() {
+    if (__any(ip < total && avail < 4u)) {
+      if (avail <= 32u) {
+        top_up();
+        avail += 32u;
+      }
+    }
+  };
+  // at least 32 bits held (or the rest of the input): up to 4 bytes from the ring,
+  // branch-free (the tail is in the ring)
+  auto refill = [&]() {
+    const uint32_t ipg = off32 + ip;
+    const uint32_t sl = (ipg >> 2) & 15u;
+    const uint32_t d0 = Q.ring[sl * 64 + lane], d1 = Q.ring[(sl + 1) * 64 + lane];
+    uint32_t v = __builtin_amdgcn_alignbyte(d1, d0, ipg & 3u);
+    const uint32_t rem = total - ip;
+    const uint32_t nb = bits < 32 ? (rem < 4u ? rem : 4u) : 0u;
+    v &= nb == 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u);
+    hold |= (uint64_t)v << bits;
+    bits += 8 * (int)nb;
+    ip += nb;
+    avail -= nb;
+  };
+  auto drop = [&](int n) {
+    hold >>= n;
+    bits -= n;
+  };
+  // --- the output ---
+  uint32_t ntok = 0, nlit = 0, run = 0, outlen = 0, litw = 0;
+  auto put_lit = [&](uint32_t b) -> bool {
+    if (nlit >= lit_cap) return false;
+    litw |= b << (8 * (nlit & 3u));
+    if ((++nlit & 3u) == 0) {
+      reinterpret_cast<uint32_t*>(lit)[(nlit >> 2) - 1] = litw;
+      litw = 0;
+    }
+    ++run;
+    ++outlen;
+    return true;
+  };
+  auto put_tok = [&](uint32_t t) -> bool {
+    if (ntok >= tok_cap) return false;
+    tok[ntok++] = t;
+    return true;
+  };
+  auto end_run = [&]() -> bool {
+    if (!run) return true;
+    const bool r = put_tok(run);
+    run = 0;
+    return r;
+  };
+  int st = Q_OK;
+  for (;;) {
+    service();
+    refill();
+    if (bits == 0 && ip >= total) break;  // clean: all input used, on a block boundary
+    if (bits < 3) { st = Q_BAD; break; }
+    const uint32_t last = (uint32_t)(hold & 1u), type = (uint32_t)((hold >> 1) & 3u);
+    drop(3);
+    if (last) { st = Q_BAD; break; }  // a final block: the stream ends (k_inflate handles it)
+    if (type == 0) {                  // stored
+      drop(bits & 7);
+      service();
+      refill();
+      if (bits < 32) { st = Q_BAD; break; }
+      const uint32_t ln = (uint32_t)(hold & 0xffffu), nl = (uint32_t)((hold >> 16) & 0xffffu);
+      if (ln != (nl ^ 0xffffu)) { st = Q_BAD; break; }
+      drop(32);
+      for (uint32_t i = 0; i < ln; ++i) {
+        service();
+        refill();
+        if (bits < 8 || !put_lit((uint32_t)(hold & 0xffu))) { st = Q_BAD; break; }
+        drop(8);
+      }
+      if (st != Q_OK) break;
+      continue;
+    }
+    if (type == 3) { st = Q_BAD; break; }
+    const bool fixed = type == 1;
+    TPROF_CNT(5, 1);
+    TPROF_T(t_hdr);
+    if (!fixed) {  // dynamic codes
+      service();
+      refill();
+      if (bits < 14) { st = Q_BAD; break; }
+      const int nlen = (int)(hold & 31u) + 257, ndist = (int)((hold >> 5) & 31u) + 1,
+                ncode = (int)((hold >> 10) & 15u) + 4;
+      drop(14);
+      if (nlen > 286 || ndist > 30) { st = Q_BAD; break; }
+      // code-length code lengths: 19 nibbles in registers, by symbol
+      uint32_t cl0 = 0, cl1 = 0, cl2 = 0;
+      for (int i = 0; i < ncode; ++i) {
+        service();
+        refill();
+        if (bits < 3) { st = Q_BAD; break; }
+        const uint32_t v = (uint32_t)(hold & 7u), s = kClenOrder[i], sh = 4u * (s & 7u);
+        if (s < 8) cl0 |= v << sh;
+        else if (s < 16) cl1 |= v << sh;
+        else cl2 |= v << sh;
+        drop(3);
+      }
+      if (st != Q_OK) break;
+      auto clen = [&](int s) -> int {
+        const uint32_t w = s < 8 ? cl0 : (s < 16 ? cl1 : cl2);
+        return (int)((w >> (4 * (s & 7))) & 15u);
+      };
+      const int cmax = q_build(tab, lt, QC_ROOT, 0, clen, 19);
+      if (cmax < 0) { st = Q_BAD; break; }
+      // the code lengths, into the distance table's space
+      int have = 0, prev = 0, len256 = 0;
+      while (have < nlen + ndist) {
+        service();
+        refill();
+        const uint32_t r = tab[lt + (((uint32_t)hold & ((1u << QC_ROOT) - 1u)) << 6)];
+        const int nb = (int)(r & 15u), sy = (int)(r >> 4);
+        if (nb == 0 || nb > bits) { st = Q_BAD; break; }
+        int copy = 1, len = sy, xb = 0;
+        if (sy >= 16) {
+          xb = sy == 16 ? 2 : (sy == 17 ? 3 : 7);
+          if (nb + xb > bits) { st = Q_BAD; break; }
+          const int x = (int)((hold >> nb) & ((1u << xb) - 1u));
+          if (sy == 16) {
+            if (have == 0) { st = Q_BAD; break; }
+            len = prev;
+            copy = 3 + x;
+          } else {
+            len = 0;
+            copy = (sy == 17 ? 3 : 11) + x;
+          }
+        }
+        drop(nb + xb);
+        if (have + copy > nlen + ndist) { st = Q_BAD; break; }
+        for (int i = 0; i < copy; ++i) {
+          const int q = have + i;
+          lensb[4u * (((uint32_t)q >> 2) * 64u + lane) + ((uint32_t)q & 3u)] = (uint8_t)len;
+        }
+        if (have <= 256 && 256 < have + copy) len256 = len;
+        have += copy;
+        prev = len;
+      }
+      if (st != Q_OK) break;
+      if (len256 == 0) { st = Q_BAD; break; }
+      // the distance lengths into registers (their space becomes the distance table)
+      uint32_t dl[4] = {0u, 0u, 0u, 0u};
+      for (int i = 0; i < ndist; ++i) {
+        const uint32_t q = (uint32_t)(nlen + i);
+        const uint32_t v = lensb[4u * ((q >> 2) * 64u + lane) + (q & 3u)];
+        const uint32_t w = (uint32_t)i >> 3, sh = 4u * ((uint32_t)i & 7u);
+        if (w == 0) dl[0] |= v << sh;
+        else if (w == 1) dl[1] |= v << sh;
+        else if (w == 2) dl[2] |= v << sh;
+        else dl[3] |= v << sh;
+      }
+      auto llen = [&](int s) -> int {
+        return lensb[4u * (((uint32_t)s >> 2) * 64u + lane) + ((uint32_t)s & 3u)];
+      };
+      auto dlen = [&](int s) -> int {
+        const uint32_t w = (uint32_t)s >> 3;
+        const uint32_t x = w == 0 ? dl[0] : (w == 1 ? dl[1] : (w == 2 ? dl[2] : dl[3]));
+        return (int)((x >> (4 * (s & 7))) & 15u);
+      };
+      TPROF_T(t_bld);
+      const int lmax = q_build(tab, lt, QL_ROOT, QL_SUB, llen, nlen);
+      if (lmax == -2) { st = Q_BAIL; break; }
+      if (lmax < 0) { st = Q_BAD; break; }
+      const int dmax = q_build(tab, dt, QD_ROOT, QD_SUB, dlen, ndist);
+      if (dmax == -2) { st = Q_BAIL; break; }
+      if (dmax < 0) { st = Q_BAD; break; }
+      TPROF_ACC(2, t_bld);
+    }
+    TPROF_ACC(1, t_hdr);
+    TPROF_T(t_sym);
+    // the block's symbols, one code a step (literal/length, or the distance of the
+    // length before it) through one lookup path
+    const uint32_t lbase = fixed ? QF_L : lt, dbase = fixed ? QF_D : dt;
+    const uint32_t lrb = fixed ? QF_LROOT : QL_ROOT, drb = fixed ? QF_DROOT : QD_ROOT;
+    const uint32_t tsh = fixed ? 0u : 6u;  // entry j at base + (j << tsh)
+    uint32_t mlen = 0;                     // a length waiting for its distance
+    uint32_t* const lit32 = reinterpret_cast<uint32_t*>(lit);
+    // Branch-light: the stores are unconditional (a token slot a step does not keep is
+    // rewritten by a later step or lies past the frame's count; the partial literal
+    // word is rewritten until it is full), so the 64 lanes run one instruction stream.
+    for (;;) {
+      TPROF_CNT(4, 1);
+      service();
+      refill();  // a step takes at most 15 + 13 bits
+      const bool dist = mlen != 0;
+      const uint32_t base = dist ? dbase : lbase, rb = dist ? drb : lrb;
+      uint32_t r = tab[base + (((uint32_t)hold & ((1u << rb) - 1u)) << tsh)];
+      if ((r & 15u) == 0)
+        r = tab[base + (((1u << rb) + (r >> 8) + ((uint32_t)(hold >> rb) & ((1u << ((r >> 4) & 15u)) - 1u))) << tsh)];
+      const uint32_t len = r & 15u;
+      const uint32_t e = Q.ents[(r >> 4) + (dist ? 288u : 0u)];
+      const uint32_t x = e_extra(e), eo = e_op(e);
+      const uint32_t v = e_val(e) + ((uint32_t)(hold >> len) & ((1u << x) - 1u));
+      const bool is_lit = !dist && eo == OP_LIT, is_len = !dist && eo == OP_BASE;
+      const uint32_t has_run = (dist && run) ? 1u : 0u;
+      const bool bad = (int)(len + x) > bits || eo == OP_BAD || (is_lit && nlit >= lit_cap) ||
+                       (dist && ntok + 1u + has_run > tok_cap);
+      if (bad) { st = Q_BAD; break; }
+      drop((int)(len + x));
+      if (!dist && eo == OP_EOB) break;
+      const uint32_t nlit2 = nlit + (is_lit ? 1u : 0u);
+      const uint32_t litw2 = is_lit ? (litw | (v << (8u * (nlit & 3u)))) : litw;
+      const bool word_done = is_lit && (nlit2 & 3u) == 0u;
+      lit32[(nlit2 >> 2) - (word_done ? 1u : 0u)] = litw2;  // the word just filled, else the partial one
+      tok[ntok] = run;
+      tok[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
+      ntok += dist ? 1u + has_run : 0u;
+      litw = word_done ? 0u : litw2;
+      nlit = nlit2;
+      outlen += is_lit ? 1u : (dist ? mlen : 0u);
+      run = dist ? 0u : run + (is_lit ? 1u : 0u);
+      mlen = is_len ? v : (dist ? 0u : mlen);
+    }
+    TPROF_ACC(3, t_sym);
+    if (st != Q_OK) break;
+  }
+  if (st == Q_OK) {
+    if (!end_run()) st = Q_BAD;
+    else {
+      if (nlit & 3u) reinterpret_cast<uint32_t*>(lit)[nlit >> 2] = litw;
+      a.tstat[k] = InflTokStat{1u, ntok, nlit, outlen};
+    }
+  }
+  if (st == Q_BAD) a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};  // the message goes to the serial decoder
+  return st;
 }
 
 __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
   // symbol -> entry (base, extra bits, op) for the 16-bit root entries
-  __shared__ uint32_t ents[288 + 32];  // literal/length entries, then distance entries
+  __shared__ TokLds Q;
+  uint32_t* const ents = Q.ents;  // literal/length entries, then distance entries
   for (int i = threadIdx.x; i < 288; i += 64) ents[i] = sym_entry(T_LIT, (uint32_t)i, 0);
   if (threadIdx.x < 32) ents[288 + threadIdx.x] = sym_entry(T_DIST, threadIdx.x, 0);
+  q_fixed_tables(Q.tab, threadIdx.x);
   __syncthreads();
   const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
   if (lane_id >= a.n_lanes) return;
+#ifdef WSG_INFLATE_TOK_PROF
+  uint64_t pf_[8] = {};
+#define PF_PTR pf_
+#else
+#define PF_PTR nullptr
+#endif
   LaneTab* const T = reinterpret_cast<LaneTab*>(a.tab) + lane_id;
-  for (uint64_t k = lane_id; k < a.n_frames; k += a.n_lanes) {
+  for (uint64_t i = lane_id; i < a.n_frames; i += a.n_lanes) {
+    const uint64_t k = a.order ? a.order[i] : i;
     const wsg_frame_desc d = a.desc[k];
     const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
     const bool start = (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && (rsv & 4u) && !(d.flags & WSG_DESC_REPLAY) &&
@@ -700,24 +1179,24 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
       a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
       continue;
     }
-    if (kend == k) tok_message<false>(a, T, ents, k, kend, in_len);
-    else tok_message<true>(a, T, ents, k, kend, in_len);
+    if (kend == k) {
+      TPROF_T(t_msg);
+      const int st = a.tok_lds ? tok_single_lds(a, Q, d, k, PF_PTR) : Q_BAIL;
+      TPROF_ACC(0, t_msg);
+      TPROF_CNT(6, 1);
+      TPROF_CNT(7, st == Q_BAIL);
+      if (st == Q_BAIL) tok_message<false>(a, T, ents, k, kend, in_len, PF_PTR);
+    } else {
+      tok_message<true>(a, T, ents, k, kend, in_len, PF_PTR);
+    }
   }
+#ifdef WSG_INFLATE_TOK_PROF
+  for (int i = 0; i < 8; ++i) atomicAdd(&g_tok_prof[i], (unsigned long long)pf_[i]);
+#endif
 }
 
 }  // namespace
 
-// Phase clocks for tools/prof_inflate.hip (compiled out of the library).
-#ifdef WSG_INFLATE_PROF
-__device__ unsigned long long g_infl_prof[24];
-#define PROF_T(v) const uint64_t v = clock64()
-#define PROF_ACC(i, v) pf_[i] += clock64() - (v)
-#define PROF_CNT(i, n) pf_[i] += (uint64_t)(n)
-#else
-#define PROF_T(v)
-#define PROF_ACC(i, v)
-#define PROF_CNT(i, n)
-#endif
 
 // One workgroup (one wave) per session.
 __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
@@ -1667,6 +2146,58 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
   }
 }
 
+// Message order for the pre-decode: a wave's 64 lanes step in lock-step until its
+// longest message ends, so lanes are given messages of similar size (a counting sort
+// of the frames by payload length, longest first; the order within a size bucket
+// does not matter: every frame writes only its own regions).
+constexpr uint32_t ORD_BUCKETS = 4096;
+__device__ __forceinline__ uint32_t ord_bucket(uint32_t len) {
+  const uint32_t b = len >> 4;
+  return ORD_BUCKETS - 1u - (b < ORD_BUCKETS - 1u ? b : ORD_BUCKETS - 1u);
+}
+
+__global__ __launch_bounds__(256) void k_ord_hist(InflArgs a) {
+  __shared__ uint32_t h[ORD_BUCKETS];
+  for (uint32_t i = threadIdx.x; i < ORD_BUCKETS; i += 256) h[i] = 0;
+  __syncthreads();
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < a.n_frames; k += (uint64_t)gridDim.x * 256)
+    atomicAdd(&h[ord_bucket(a.desc[k].payload_len)], 1u);
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < ORD_BUCKETS; i += 256)
+    if (h[i]) atomicAdd(&a.ord_cnt[i], h[i]);
+}
+
+__global__ __launch_bounds__(1024) void k_ord_scan(InflArgs a) {
+  // exclusive scan of the bucket counts, 4 per thread
+  __shared__ uint32_t part[1024];
+  const uint32_t t = threadIdx.x;
+  uint32_t v[4], sum = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    v[i] = a.ord_cnt[4 * t + i];
+    sum += v[i];
+  }
+  part[t] = sum;
+  __syncthreads();
+  for (uint32_t d = 1; d < 1024; d <<= 1) {
+    const uint32_t x = t >= d ? part[t - d] : 0u;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  uint32_t run = part[t] - sum;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    a.ord_cnt[4 * t + i] = run;
+    run += v[i];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_ord_scatter(InflArgs a) {
+  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < a.n_frames; k += (uint64_t)gridDim.x * 256)
+    a.order[atomicAdd(&a.ord_cnt[ord_bucket(a.desc[k].payload_len)], 1u)] = (uint32_t)k;
+}
+
 }  // namespace
 
 void launch_infl_fast(const InflArgs& a, hipStream_t s) {
@@ -1674,8 +2205,17 @@ void launch_infl_fast(const InflArgs& a, hipStream_t s) {
 }
 
 void launch_infl_tok(const InflArgs& a, hipStream_t s) {
-  if (a.n_lanes && a.n_frames) hipLaunchKernelGGL(k_infl_tok, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+  if (!a.n_lanes || !a.n_frames) return;
+  if (a.order) {
+    const uint32_t g = (uint32_t)((a.n_frames + 255) / 256 < 1024 ? (a.n_frames + 255) / 256 : 1024);
+    (void)hipMemsetAsync(a.ord_cnt, 0, ORD_BUCKETS * sizeof(uint32_t), s);  // errors show at the launch check
+    hipLaunchKernelGGL(k_ord_hist, dim3(g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_ord_scan, dim3(1), dim3(1024), 0, s, a);
+    hipLaunchKernelGGL(k_ord_scatter, dim3(g), dim3(256), 0, s, a);
+  }
+  hipLaunchKernelGGL(k_infl_tok, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
 }
+uint64_t infl_ord_words(uint64_t n_frames) { return n_frames + ORD_BUCKETS; }
 
 uint64_t infl_tok_words(uint64_t payload_len, uint64_t n_frames) { return payload_len + (uint64_t)TOK_SLACK * n_frames + 64; }
 uint64_t infl_lit_bytes(uint64_t payload_len, uint64_t n_frames) {

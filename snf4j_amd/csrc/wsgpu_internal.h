@@ -196,6 +196,9 @@ struct InflArgs {
   uint8_t* tab;               // n_lanes per-lane table blocks
   uint32_t n_lanes;
   uint8_t* fast_done;         // [n_sessions]: k_infl_fast finished the session (k_inflate skips it)
+  int tok_lds;                // k_infl_tok decodes single-frame messages from LDS tables (else HBM tables)
+  uint32_t* order;            // [n_frames] frame order for k_infl_tok's lanes (longest first), or null
+  uint32_t* ord_cnt;          // [ORD_BUCKETS] its counting-sort buckets
 };
 
 struct InflTokStat {
@@ -232,6 +235,7 @@ void launch_infl_tok(const InflArgs& a, hipStream_t s);
 void launch_infl_fast(const InflArgs& a, hipStream_t s);
 uint64_t infl_tok_words(uint64_t payload_len, uint64_t n_frames);
 uint64_t infl_lit_bytes(uint64_t payload_len, uint64_t n_frames);
+uint64_t infl_ord_words(uint64_t n_frames);  // order + bucket counts
 uint64_t infl_tab_bytes();
 
 void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64_t* req_off, uint32_t n,

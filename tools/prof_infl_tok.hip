@@ -1,0 +1,77 @@
+// Phase profile of k_infl_tok (the message-parallel pre-decode): the kernel compiled
+// with WSG_INFLATE_TOK_PROF (clock64 per phase, summed over lanes) over a batch
+// written by tools/make_inflate_input.py.  Diagnostic only; not part of the library.
+#define WSG_INFLATE_TOK_PROF 1
+#include "../snf4j_amd/csrc/inflate.hip"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e_), __LINE__); exit(1); } } while (0)
+
+int main(int argc, char** argv) {
+  FILE* f = fopen(argc > 1 ? argv[1] : "gpurun_out/infl_in.bin", "rb");
+  if (!f) { printf("no input\n"); return 1; }
+  const uint32_t max_lanes = argc > 2 ? (uint32_t)atoi(argv[2]) : 262144u;
+  const int use_lds = argc > 3 ? atoi(argv[3]) : 1;
+  const int use_order = argc > 4 ? atoi(argv[4]) : 1;
+  uint64_t hdr[4];  // n_frames, n_sessions, payload_len, cap per session
+  if (fread(hdr, 8, 4, f) != 4) return 1;
+  const uint64_t n = hdr[0], ns = hdr[1], pl = hdr[2];
+  std::vector<wsg_frame_desc> desc(n);
+  std::vector<uint32_t> sf(ns + 1);
+  std::vector<uint8_t> payload(pl);
+  if (fread(desc.data(), sizeof(wsg_frame_desc), n, f) != n) return 1;
+  if (fread(sf.data(), 4, ns + 1, f) != ns + 1) return 1;
+  if (fread(payload.data(), 1, pl, f) != pl) return 1;
+  fclose(f);
+  const uint32_t lanes = (uint32_t)(n < max_lanes ? ((n + 63) / 64) * 64 : max_lanes);
+  ws::InflArgs a{};
+  wsg_frame_desc* d_desc;
+  uint32_t *d_sf, *d_tok;
+  uint8_t *d_pl, *d_lit, *d_tab;
+  ws::InflTokStat* d_stat;
+  CK(hipMalloc(&d_desc, n * sizeof(wsg_frame_desc)));
+  CK(hipMalloc(&d_sf, (ns + 1) * 4));
+  CK(hipMalloc(&d_pl, pl));
+  CK(hipMalloc(&d_tok, ws::infl_tok_words(pl, n) * 4));
+  CK(hipMalloc(&d_lit, ws::infl_lit_bytes(pl, n)));
+  CK(hipMalloc(&d_stat, n * sizeof(ws::InflTokStat)));
+  CK(hipMalloc(&d_tab, (uint64_t)lanes * ws::infl_tab_bytes()));
+  CK(hipMemcpy(d_desc, desc.data(), n * sizeof(wsg_frame_desc), hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_sf, sf.data(), (ns + 1) * 4, hipMemcpyHostToDevice));
+  CK(hipMemcpy(d_pl, payload.data(), pl, hipMemcpyHostToDevice));
+  a.desc = d_desc; a.n_frames = n; a.session_first = d_sf; a.n_sessions = (uint32_t)ns;
+  a.payload = d_pl; a.payload_len = pl;
+  a.tok = d_tok; a.lit = d_lit; a.lit_len = ws::infl_lit_bytes(pl, n); a.tstat = d_stat; a.tab = d_tab; a.n_lanes = lanes;
+  a.tok_lds = use_lds;
+  if (use_order) {
+    CK(hipMalloc(&a.order, ws::infl_ord_words(n) * 4));
+    a.ord_cnt = a.order + n;
+  }
+  unsigned long long z[8] = {};
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int rep = 0; rep < 3; ++rep) {
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(ws::g_tok_prof), z, sizeof(z)));
+    CK(hipEventRecord(e0));
+    ws::launch_infl_tok(a, 0);
+    CK(hipEventRecord(e1));
+    CK(hipDeviceSynchronize());
+    float ms = 0;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    unsigned long long p[8] = {};
+    CK(hipMemcpyFromSymbol(p, HIP_SYMBOL(ws::g_tok_prof), sizeof(p)));
+    std::vector<ws::InflTokStat> st(n);
+    CK(hipMemcpy(st.data(), d_stat, n * sizeof(ws::InflTokStat), hipMemcpyDeviceToHost));
+    uint64_t ok = 0;
+    for (auto& x : st) ok += x.ok != 0;
+    const double m = p[6] ? (double)p[6] : 1.0;
+    printf("rep %d: %.3f ms, %u lanes, %llu messages, %llu ok\n", rep, ms, lanes, (unsigned long long)p[6],
+           (unsigned long long)ok);
+    const char* names[8] = {"message total", "header+tables", "tables (dynamic)", "symbol loop", "steps", "blocks", "messages", "lds bail-outs"};
+    for (int i = 0; i < 8; ++i) printf("  %-18s %12.1f per message%s\n", names[i], (double)p[i] / m, i < 4 ? " cycles" : "");
+  }
+  return 0;
+}
