@@ -368,3 +368,86 @@ def _run_cuts(ctx, oracle, cut_sessions, no_context, n_batches):
         for i, (g, o) in enumerate(zip(got[s], exp)):
             assert (int(g.getOpcode()), g.isFinalFragment(), g.getRsvBits()) == o[:3], (s, i)
             assert g.getPayload() == o[3], (s, i)
+
+
+def _lds_path_messages(rng):
+    """Single-frame compressed messages aimed at the pre-decode's LDS table paths:
+    fixed-code blocks (Z_FIXED), stored blocks (level 0), near-uniform bytes over all
+    256 values (most literal codes 8-9 bits: more 9-bit prefixes than the LDS sub-table
+    room of a lane, so the lane falls back to its HBM tables), skewed far back-references
+    (distance codes longer than the 7-bit LDS root), tiny and multi-block messages."""
+    kinds = []
+    for i in range(48):
+        k = i % 6
+        if k == 0:
+            body = bytes(rng.integers(97, 123, int(rng.integers(1, 600)), dtype=np.uint8))
+            kinds.append(("fixed", body, zlib.compressobj(6, zlib.DEFLATED, -15, 8, zlib.Z_FIXED)))
+        elif k == 1:
+            body = bytes(rng.integers(0, 256, int(rng.integers(1, 3000)), dtype=np.uint8))
+            kinds.append(("stored", body, zlib.compressobj(0, zlib.DEFLATED, -15)))
+        elif k == 2:
+            p = np.where(np.arange(256) < 128, 3.0, 1.0)
+            body = bytes(rng.choice(256, int(rng.integers(4000, 9000)), p=p / p.sum()).astype(np.uint8))
+            kinds.append(("wide", body, zlib.compressobj(6, zlib.DEFLATED, -15)))
+        elif k == 3:
+            # repeats of chunks at geometric distances: a long tail of distance codes
+            base = bytes(rng.integers(97, 123, 30000, dtype=np.uint8))
+            parts = []
+            for _ in range(400):
+                d = int(min(29999, rng.geometric(0.002)))
+                s = int(rng.integers(0, 30000 - 8))
+                parts.append(base[s:s + 6] + base[max(0, s - d):max(0, s - d) + 5])
+            kinds.append(("far", b"".join(parts), zlib.compressobj(9, zlib.DEFLATED, -15)))
+        elif k == 4:
+            body = bytes(rng.integers(97, 100, int(rng.integers(1, 8)), dtype=np.uint8))
+            kinds.append(("tiny", body, zlib.compressobj(6, zlib.DEFLATED, -15)))
+        else:
+            # several blocks in one message: a small memLevel forces block splits
+            words = [bytes(rng.integers(97, 123, int(rng.integers(2, 9)), dtype=np.uint8)) for _ in range(300)]
+            body = b" ".join(words[int(j)] for j in rng.integers(0, 300, 6000))
+            kinds.append(("blocks", body, zlib.compressobj(6, zlib.DEFLATED, -15, 1)))
+    return kinds
+
+
+def test_inflate_lds_table_paths(oracle):
+    """The pre-decode's LDS path (default) against its HBM tables (WSG_INFLATE_LDS=0), the
+    serial decoder alone (WSG_INFLATE_TOKENS=0) and zlib, one session per message (no
+    context), every message a single FIN frame."""
+    import os
+    from snf4j_amd import Context
+    from snf4j_amd._lib import DESC_DTYPE, INFLATE_STATE_DTYPE
+    rng = np.random.default_rng(0x1D5)
+    kinds = _lds_path_messages(rng)
+    comp = []
+    for _, body, c in kinds:
+        comp.append((c.compress(body) + c.flush(zlib.Z_SYNC_FLUSH))[:-4])
+    n = len(kinds)
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum([len(x) for x in comp], out=off[1:])
+    desc["payload_off"] = off[:-1]
+    desc["payload_len"] = [len(x) for x in comp]
+    desc["opcode"] = 1
+    desc["flags"] = 0x80 | (4 << 4)
+    payload = np.frombuffer(b"".join(comp) + bytes(16), dtype=np.uint8)
+    sf = np.arange(n + 1, dtype=np.uint32)
+    cap = max(len(b) for _, b, _ in kinds) + 64
+    out_off = (np.arange(n + 1) * cap).astype(np.uint64)
+    results = []
+    for env in ({}, {"WSG_INFLATE_LDS": "0"}, {"WSG_INFLATE_TOKENS": "0"}):
+        os.environ.update(env)
+        try:
+            c = Context(0)
+        finally:
+            for k in env:
+                os.environ.pop(k, None)
+        state = np.zeros(n, dtype=INFLATE_STATE_DTYPE)
+        window = np.zeros(n * 32768, dtype=np.uint8)
+        out, od, res, rf = c.inflate_host(True, desc, sf, payload, state, window, out_off)
+        c.close()
+        assert (res["error"] == 0).all(), (env, res["error"])
+        results.append([out[int(o["payload_off"]):int(o["payload_off"]) + int(o["payload_len"])].tobytes() for o in od])
+    for i, (kind, body, _) in enumerate(kinds):
+        assert zlib.decompressobj(-15).decompress(comp[i] + b"\x00\x00\xff\xff") == body
+        for r in results:
+            assert r[i] == body, (i, kind)
