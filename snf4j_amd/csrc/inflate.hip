@@ -728,6 +728,7 @@ struct TokLds {
   uint32_t ents[320];        // symbol -> entry: literal/length, then distance
   uint16_t tab[Q_TAB];       // fixed tables, then the lanes' tables
   uint32_t ring[Q_RING * 64];  // input ring: dword slot s of lane i at s * 64 + i
+  uint32_t cnt[16 * 64];       // literal/length table build: count, then next code, of length L at L * 64 + i
 };
 
 enum : int { Q_OK = 0, Q_BAD = 1, Q_BAIL = 2 };
@@ -808,6 +809,97 @@ __device__ int q_build(uint16_t* tab, uint32_t base, int rb, int sub, LensF lens
       const uint32_t r = tab[base + ((rev & (rsize - 1u)) << 6)];
       const uint32_t sb = (r >> 4) & 15u, off = r >> 8;
       for (uint32_t j = rev >> rb; j < (1u << sb); j += 1u << (l - rb)) tab[base + ((rsize + off + j) << 6)] = e;
+    }
+  }
+  return maxl;
+}
+
+// q_build for the literal/length set (up to 286 codes): the counts and each symbol's
+// code come from per-lane LDS counters (an atomic add a symbol, four lengths a read)
+// instead of a 15-way select chain a symbol in registers.
+__device__ int q_build_lit(TokLds& Q, uint32_t lane, const uint8_t* lensb, int n) {
+  uint16_t* const tab = Q.tab;
+  const uint32_t base = Q_LT + lane;
+  constexpr int rb = QL_ROOT;
+  uint32_t* const cnt = Q.cnt;
+#pragma unroll
+  for (int L = 0; L < 16; ++L) cnt[L * 64 + lane] = 0;
+  const uint32_t* const lw = reinterpret_cast<const uint32_t*>(lensb);
+  const int nw = (n + 3) >> 2;
+  for (int q = 0; q < nw; ++q) {
+    const uint32_t w = lw[q * 64 + lane];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t l = 4 * q + b < n ? (w >> (8 * b)) & 15u : 0u;
+      atomicAdd(&cnt[l * 64 + lane], 1u);  // length 0 counts into slot 0, unused
+    }
+  }
+  int c[16];
+  c[0] = 0;
+#pragma unroll
+  for (int l = 1; l < 16; ++l) c[l] = (int)cnt[l * 64 + lane];
+  int left = 1, maxl = 0;
+  bool bad = false;
+#pragma unroll
+  for (int l = 1; l < 16; ++l) {
+    left = (left << 1) - c[l];
+    bad |= left < 0;
+    if (c[l]) maxl = l;
+  }
+  if (bad || left != 0 || maxl == 0) return -1;
+  int nx[16];
+  {
+    int code = 0;
+    nx[0] = 0;
+#pragma unroll
+    for (int l = 1; l < 16; ++l) {
+      code = (code + c[l - 1]) << 1;
+      nx[l] = code;
+      cnt[l * 64 + lane] = (uint32_t)code;  // the next code of each length
+    }
+  }
+  const uint32_t rsize = 1u << rb;
+  if (maxl > rb) {
+    int P = nx[rb] + c[rb], L = rb + 1;
+    uint32_t used = 0;
+    for (; P < (int)rsize; ++P) {
+      const int pend = (P + 1) << (15 - rb);
+      for (;;) {
+        int e = 0;
+#pragma unroll
+        for (int l = 1; l < 16; ++l)
+          if (l == L) e = (nx[l] + c[l]) << (15 - l);
+        if (e >= pend) break;
+        ++L;
+      }
+      const uint32_t sb = (uint32_t)(L - rb);
+      if (used + (1u << sb) > (uint32_t)QL_SUB) return -2;
+      const uint32_t slot = __builtin_bitreverse32((uint32_t)P) >> (32 - rb);
+      tab[base + (slot << 6)] = (uint16_t)((sb << 4) | (used << 8));
+      used += 1u << sb;
+    }
+  }
+  for (int q = 0; q < nw; ++q) {
+    const uint32_t w = lw[q * 64 + lane];
+    uint32_t l4[4], code4[4];
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      l4[b] = 4 * q + b < n ? (w >> (8 * b)) & 15u : 0u;
+      code4[b] = atomicAdd(&cnt[l4[b] * 64 + lane], 1u);
+    }
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t l = l4[b];
+      if (!l) continue;
+      const uint32_t rev = __builtin_bitreverse32(code4[b]) >> (32 - l);
+      const uint16_t e = (uint16_t)(l | ((uint32_t)(4 * q + b) << 4));
+      if (l <= (uint32_t)rb) {
+        for (uint32_t j = rev; j < rsize; j += 1u << l) tab[base + (j << 6)] = e;
+      } else {
+        const uint32_t r = tab[base + ((rev & (rsize - 1u)) << 6)];
+        const uint32_t sb = (r >> 4) & 15u, off = r >> 8;
+        for (uint32_t j = rev >> rb; j < (1u << sb); j += 1u << (l - rb)) tab[base + ((rsize + off + j) << 6)] = e;
+      }
     }
   }
   return maxl;
@@ -918,6 +1010,11 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     bits += 8 * (int)nb;
     ip += nb;
     avail -= nb;
+  };
+  auto ring_word = [&](uint32_t q) -> uint32_t {  // the 4 bytes at message offset q
+    const uint32_t ipg = off32 + q;
+    const uint32_t sl = (ipg >> 2) & 15u;
+    return __builtin_amdgcn_alignbyte(Q.ring[(sl + 1) * 64 + lane], Q.ring[sl * 64 + lane], ipg & 3u);
   };
   auto drop = [&](int n) {
     hold >>= n;
@@ -1049,16 +1146,13 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         else if (w == 2) dl[2] |= v << sh;
         else dl[3] |= v << sh;
       }
-      auto llen = [&](int s) -> int {
-        return lensb[4u * (((uint32_t)s >> 2) * 64u + lane) + ((uint32_t)s & 3u)];
-      };
       auto dlen = [&](int s) -> int {
         const uint32_t w = (uint32_t)s >> 3;
         const uint32_t x = w == 0 ? dl[0] : (w == 1 ? dl[1] : (w == 2 ? dl[2] : dl[3]));
         return (int)((x >> (4 * (s & 7))) & 15u);
       };
       TPROF_T(t_bld);
-      const int lmax = q_build(tab, lt, QL_ROOT, QL_SUB, llen, nlen);
+      const int lmax = q_build_lit(Q, lane, lensb, nlen);
       if (lmax == -2) { st = Q_BAIL; break; }
       if (lmax < 0) { st = Q_BAD; break; }
       const int dmax = q_build(tab, dt, QD_ROOT, QD_SUB, dlen, ndist);
@@ -1078,10 +1172,25 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     // Branch-light: the stores are unconditional (a token slot a step does not keep is
     // rewritten by a later step or lies past the frame's count; the partial literal
     // word is rewritten until it is full), so the 64 lanes run one instruction stream.
+    uint32_t rw = ring_word(ip);  // the ring word at ip, read a step ahead
     for (;;) {
       TPROF_CNT(4, 1);
-      service();
-      refill();  // a step takes at most 15 + 13 bits
+      if (__any(ip < total && avail < 4u)) {  // service(), then the word again
+        if (avail <= 32u) {
+          top_up();
+          avail += 32u;
+        }
+        rw = ring_word(ip);
+      }
+      {  // refill() from rw; the next word's read overlaps this step's lookups
+        const uint32_t rem = total - ip;
+        const uint32_t nb = bits < 32 ? (rem < 4u ? rem : 4u) : 0u;
+        hold |= (uint64_t)(rw & (nb == 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u))) << bits;
+        bits += 8 * (int)nb;
+        ip += nb;
+        avail -= nb;
+        rw = ring_word(ip);
+      }
       const bool dist = mlen != 0;
       const uint32_t base = dist ? dbase : lbase, rb = dist ? drb : lrb;
       uint32_t r = tab[base + (((uint32_t)hold & ((1u << rb) - 1u)) << tsh)];
@@ -1093,11 +1202,16 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       const uint32_t v = e_val(e) + ((uint32_t)(hold >> len) & ((1u << x) - 1u));
       const bool is_lit = !dist && eo == OP_LIT, is_len = !dist && eo == OP_BASE;
       const uint32_t has_run = (dist && run) ? 1u : 0u;
-      const bool bad = (int)(len + x) > bits || eo == OP_BAD || (is_lit && nlit >= lit_cap) ||
-                       (dist && ntok + 1u + has_run > tok_cap);
-      if (bad) { st = Q_BAD; break; }
+      // (bitwise: one exit test, no short-circuit branches)
+      const bool bad = ((int)(len + x) > bits) | (eo == OP_BAD) | (is_lit & (nlit >= lit_cap)) |
+                       (dist & (ntok + 1u + has_run > tok_cap));
+      const bool eob = !dist & (eo == OP_EOB);
+      if (bad | eob) {
+        if (bad) st = Q_BAD;
+        else drop((int)len);
+        break;
+      }
       drop((int)(len + x));
-      if (!dist && eo == OP_EOB) break;
       const uint32_t nlit2 = nlit + (is_lit ? 1u : 0u);
       const uint32_t litw2 = is_lit ? (litw | (v << (8u * (nlit & 3u)))) : litw;
       const bool word_done = is_lit && (nlit2 & 3u) == 0u;
