@@ -984,37 +984,33 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   uint32_t ip = 0;                                   // message offset of the next input byte
   uint32_t avail = (uint32_t)(fill - off);           // ring bytes from ip on
   const uint32_t off32 = (uint32_t)off;
-  // top-up: at a point every active lane reaches, when some lane has under 4 bytes in
+  auto ring_word = [&](uint32_t q) -> uint32_t {  // the 4 bytes at message offset q
+    const uint32_t ipg = off32 + q;
+    const uint32_t sl = (ipg >> 2) & 15u;
+    return __builtin_amdgcn_alignbyte(Q.ring[(sl + 1) * 64 + lane], Q.ring[sl * 64 + lane], ipg & 3u);
+  };
+  // Input, a step: at least 32 bits held (or the rest of the input), up to 4 bytes
+  // from the ring word at ip, read a step ahead so its latency overlaps the step.
+  // Top-up: at a point every active lane reaches, when some lane has under 4 bytes in
   // the ring, every lane with room loads a chunk into it.  The load is waited on right
   // there: a chunk loaded ahead into registers kept a load pending across the step
   // loop, and the compiler then waited on the vector memory counter at every step.
-  auto service = [&]() {
+  uint32_t rw = ring_word(0);
+  auto in_step = [&]() {
     if (__any(ip < total && avail < 4u)) {
       if (avail <= 32u) {
         top_up();
         avail += 32u;
       }
+      rw = ring_word(ip);
     }
-  };
-  // at least 32 bits held (or the rest of the input): up to 4 bytes from the ring,
-  // branch-free (the tail is in the ring)
-  auto refill = [&]() {
-    const uint32_t ipg = off32 + ip;
-    const uint32_t sl = (ipg >> 2) & 15u;
-    const uint32_t d0 = Q.ring[sl * 64 + lane], d1 = Q.ring[(sl + 1) * 64 + lane];
-    uint32_t v = __builtin_amdgcn_alignbyte(d1, d0, ipg & 3u);
     const uint32_t rem = total - ip;
     const uint32_t nb = bits < 32 ? (rem < 4u ? rem : 4u) : 0u;
-    v &= nb == 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u);
-    hold |= (uint64_t)v << bits;
+    hold |= (uint64_t)(rw & (nb == 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u))) << bits;
     bits += 8 * (int)nb;
     ip += nb;
     avail -= nb;
-  };
-  auto ring_word = [&](uint32_t q) -> uint32_t {  // the 4 bytes at message offset q
-    const uint32_t ipg = off32 + q;
-    const uint32_t sl = (ipg >> 2) & 15u;
-    return __builtin_amdgcn_alignbyte(Q.ring[(sl + 1) * 64 + lane], Q.ring[sl * 64 + lane], ipg & 3u);
+    rw = ring_word(ip);
   };
   auto drop = [&](int n) {
     hold >>= n;
@@ -1046,8 +1042,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   };
   int st = Q_OK;
   for (;;) {
-    service();
-    refill();
+    in_step();
     if (bits == 0 && ip >= total) break;  // clean: all input used, on a block boundary
     if (bits < 3) { st = Q_BAD; break; }
     const uint32_t last = (uint32_t)(hold & 1u), type = (uint32_t)((hold >> 1) & 3u);
@@ -1055,15 +1050,13 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     if (last) { st = Q_BAD; break; }  // a final block: the stream ends (k_inflate handles it)
     if (type == 0) {                  // stored
       drop(bits & 7);
-      service();
-      refill();
+      in_step();
       if (bits < 32) { st = Q_BAD; break; }
       const uint32_t ln = (uint32_t)(hold & 0xffffu), nl = (uint32_t)((hold >> 16) & 0xffffu);
       if (ln != (nl ^ 0xffffu)) { st = Q_BAD; break; }
       drop(32);
       for (uint32_t i = 0; i < ln; ++i) {
-        service();
-        refill();
+        in_step();
         if (bits < 8 || !put_lit((uint32_t)(hold & 0xffu))) { st = Q_BAD; break; }
         drop(8);
       }
@@ -1075,8 +1068,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     TPROF_CNT(5, 1);
     TPROF_T(t_hdr);
     if (!fixed) {  // dynamic codes
-      service();
-      refill();
+      in_step();
       if (bits < 14) { st = Q_BAD; break; }
       const int nlen = (int)(hold & 31u) + 257, ndist = (int)((hold >> 5) & 31u) + 1,
                 ncode = (int)((hold >> 10) & 15u) + 4;
@@ -1085,8 +1077,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       // code-length code lengths: 19 nibbles in registers, by symbol
       uint32_t cl0 = 0, cl1 = 0, cl2 = 0;
       for (int i = 0; i < ncode; ++i) {
-        service();
-        refill();
+        in_step();
         if (bits < 3) { st = Q_BAD; break; }
         const uint32_t v = (uint32_t)(hold & 7u), s = kClenOrder[i], sh = 4u * (s & 7u);
         if (s < 8) cl0 |= v << sh;
@@ -1101,11 +1092,13 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       };
       const int cmax = q_build(tab, lt, QC_ROOT, 0, clen, 19);
       if (cmax < 0) { st = Q_BAD; break; }
-      // the code lengths, into the distance table's space
+      // the code lengths, into the distance table's space (zeroed first: runs of zeros
+      // then write nothing)
+      uint32_t* const lw32 = reinterpret_cast<uint32_t*>(lensb);
+      for (int q = 0; q < 80; ++q) lw32[q * 64 + lane] = 0;
       int have = 0, prev = 0, len256 = 0;
       while (have < nlen + ndist) {
-        service();
-        refill();
+        in_step();
         const uint32_t r = tab[lt + (((uint32_t)hold & ((1u << QC_ROOT) - 1u)) << 6)];
         const int nb = (int)(r & 15u), sy = (int)(r >> 4);
         if (nb == 0 || nb > bits) { st = Q_BAD; break; }
@@ -1125,7 +1118,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         }
         drop(nb + xb);
         if (have + copy > nlen + ndist) { st = Q_BAD; break; }
-        for (int i = 0; i < copy; ++i) {
+        for (int i = 0; len && i < copy; ++i) {
           const int q = have + i;
           lensb[4u * (((uint32_t)q >> 2) * 64u + lane) + ((uint32_t)q & 3u)] = (uint8_t)len;
         }
@@ -1172,25 +1165,9 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     // Branch-light: the stores are unconditional (a token slot a step does not keep is
     // rewritten by a later step or lies past the frame's count; the partial literal
     // word is rewritten until it is full), so the 64 lanes run one instruction stream.
-    uint32_t rw = ring_word(ip);  // the ring word at ip, read a step ahead
     for (;;) {
       TPROF_CNT(4, 1);
-      if (__any(ip < total && avail < 4u)) {  // service(), then the word again
-        if (avail <= 32u) {
-          top_up();
-          avail += 32u;
-        }
-        rw = ring_word(ip);
-      }
-      {  // refill() from rw; the next word's read overlaps this step's lookups
-        const uint32_t rem = total - ip;
-        const uint32_t nb = bits < 32 ? (rem < 4u ? rem : 4u) : 0u;
-        hold |= (uint64_t)(rw & (nb == 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u))) << bits;
-        bits += 8 * (int)nb;
-        ip += nb;
-        avail -= nb;
-        rw = ring_word(ip);
-      }
+      in_step();  // a step takes at most 15 + 13 bits
       const bool dist = mlen != 0;
       const uint32_t base = dist ? dbase : lbase, rb = dist ? drb : lrb;
       uint32_t r = tab[base + (((uint32_t)hold & ((1u << rb) - 1u)) << tsh)];
