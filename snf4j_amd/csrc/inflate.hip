@@ -264,6 +264,14 @@ __device__ unsigned long long g_infl_prof[24];
 #define PROF_CNT(i, n)
 #endif
 #ifdef WSG_INFLATE_TOK_PROF
+__device__ unsigned long long g_fast_prof[8];
+#define FPROF_T(v) const uint64_t v = clock64()
+#define FPROF_ACC(i, v) if (threadIdx.x == 0) atomicAdd(&g_fast_prof[i], (unsigned long long)(clock64() - (v)))
+#else
+#define FPROF_T(v)
+#define FPROF_ACC(i, v)
+#endif
+#ifdef WSG_INFLATE_TOK_PROF
 __device__ unsigned long long g_tok_prof[8];
 #define TPROF_T(v) const uint64_t v = clock64()
 #define TPROF_ACC(i, v) pf_[i] += clock64() - (v)
@@ -2000,6 +2008,9 @@ constexpr uint32_t FD_LIT = 0x80000000u;  // descriptor: a resolved byte (bits 0
 constexpr int32_t FD_BIAS = 32768;        // descriptor: position + FD_BIAS (history positions are >= -32768)
 
 constexpr int FNT = 256;  // threads per session (4 waves)
+#ifndef WSG_FAST_WAVES
+#define WSG_FAST_WAVES 6  // waves a SIMD: the register budget (80 VGPRs) that keeps 6 sessions a CU
+#endif
 
 // block-wide exclusive sum of a packed (hi, lo) pair of 32-bit counts; the totals
 __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, uint64_t* wsum) {
@@ -2023,10 +2034,11 @@ __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, u
   return pre + inc - v;
 }
 
-__global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
+__global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WAVES))) void k_infl_fast(InflArgs a) {
   __shared__ uint32_t fd[FC];
+  __shared__ uint32_t lbuf[FC / 4 + 2];  // the chunk's literal bytes (at most FC), from a dword boundary
   __shared__ uint64_t wsum[FNT / 64];
-  __shared__ uint32_t x_first, x_off, x_li;
+  __shared__ uint32_t x_first, x_off, x_li, x_lf;
   const int lane = threadIdx.x;  // (the block's thread: FNT per session)
   const uint32_t s = blockIdx.x;
   if (s >= a.n_sessions) return;
@@ -2040,6 +2052,7 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
     if (lane == 0) a.fast_done[s] = 0;
     return;
   }
+  FPROF_T(f_all);
   const uint8_t* const win = a.window + (uint64_t)s * WSG_INFLATE_WINDOW;
   uint8_t* const out = a.out + obase;
   const int wl0 = (st0.has_decoder && !st0.finished) ? (int)(st0.window_len < WSG_INFLATE_WINDOW ? st0.window_len : WSG_INFLATE_WINDOW) : 0;
@@ -2080,15 +2093,28 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
     const uint32_t* const T = a.tok + tok_base(d.payload_off, k);
     const uint8_t* const lit = a.lit + lit_base(d.payload_off, k);
     uint32_t tt = 0, t_off = 0, t_li = 0;  // the first token not fully emitted: index, output offset, literal index
+    uint32_t l_first = 0;                  // the index of the chunk's first literal
     for (uint32_t c0 = 0; c0 < L && !bad; c0 += FC) {
       const uint32_t c1 = c0 + FC < L ? c0 + FC : L, n = c1 - c0;
       const int32_t C0 = P0 + (int32_t)c0;  // absolute position of the chunk's first byte
+      FPROF_T(f_ex);
+      // 0. the chunk's literal bytes into LDS (one coalesced read; the expansion below
+      //    reads a literal run's bytes one by one)
+      const uint64_t lg = (uint64_t)(lit - a.lit) + l_first;  // the chunk's first literal, in a.lit
+      const uint64_t lw0 = lg >> 2;
+      for (uint32_t w = (uint32_t)lane; w < FC / 4 + 2; w += FNT)
+        lbuf[w] = (lw0 + w) * 4 + 4 <= a.lit_len ? reinterpret_cast<const uint32_t*>(a.lit)[lw0 + w] : 0u;
+      const uint32_t lsh = (uint32_t)(lg & 3u) - l_first;  // literal index i is byte i + lsh of lbuf
+      __syncthreads();
+      const uint8_t* const lb = reinterpret_cast<const uint8_t*>(lbuf);
       // 1. expand the tokens that overlap [c0, c1) into fd
       uint32_t t = tt, o = t_off, li = t_li;
       bool crossed = false;
+      uint32_t tk_next = t + (uint32_t)lane < n_tok ? T[t + lane] : 0u;  // a round of tokens read ahead
       while (t < n_tok && o < c1) {
         const bool valid = t + (uint32_t)lane < n_tok;
-        const uint32_t tk = valid ? T[t + lane] : 0u;
+        const uint32_t tk = valid ? tk_next : 0u;
+        tk_next = t + (uint32_t)FNT + (uint32_t)lane < n_tok ? T[t + FNT + lane] : 0u;
         const bool ism = (tk & 0x80000000u) != 0;
         const uint32_t len = !valid ? 0u : (ism ? ((tk >> 16) & 255u) + 3u : tk);
         uint64_t tot;
@@ -2108,24 +2134,26 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
               if (++r == md) r = 0;
             }
           } else {
-            for (uint32_t j = b0; j < b1; ++j) fd[j - c0] = FD_LIT | lit[tli + (j - to)];
+            for (uint32_t j = b0; j < b1; ++j) fd[j - c0] = FD_LIT | lb[tli + (j - to) + lsh];
           }
         }
         // the chunk ends inside a token: the next chunk starts from the first such one
-        if (threadIdx.x == 0) x_first = 0xffffffffu;
-        __syncthreads();
-        if (valid && to + len > c1) atomicMin(&x_first, (uint32_t)lane);
-        __syncthreads();
-        const uint32_t f = x_first;
-        if ((uint32_t)lane == f) {
-          x_off = to;
-          x_li = tli;
-        }
-        __syncthreads();
-        if (f != 0xffffffffu) {
+        if (__syncthreads_or(valid && to + len > c1)) {
+          if (threadIdx.x == 0) x_first = 0xffffffffu;
+          __syncthreads();
+          if (valid && to + len > c1) atomicMin(&x_first, (uint32_t)lane);
+          __syncthreads();
+          const uint32_t f = x_first;
+          if ((uint32_t)lane == f) {
+            x_off = to;
+            x_li = tli;
+            x_lf = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
+          }
+          __syncthreads();
           tt = t + f;
           t_off = x_off;
           t_li = x_li;
+          l_first = x_lf;
           crossed = true;
           break;
         }
@@ -2137,11 +2165,14 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
         tt = t < n_tok ? t : n_tok;
         t_off = o;
         t_li = li;
+        l_first = li;
       }
       if (__syncthreads_or(bad)) {
         bad = true;
         break;
       }
+      FPROF_ACC(0, f_ex);
+      FPROF_T(f_ch);
       // 2. chase copies inside the chunk: a byte's source precedes it, so a chain
       //    ends at a literal or at a byte before the chunk (kept as a position)
       for (uint32_t j = (uint32_t)lane; j < n; j += FNT) {
@@ -2150,13 +2181,16 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
         fd[j] = v;
       }
       __syncthreads();
+      FPROF_ACC(1, f_ch);
+      FPROF_T(f_ga);
       // 3. gather the bytes that come from before the chunk: this batch's output (HBM),
       //    or the window carried in
-      for (uint32_t j0 = 0; j0 < n; j0 += 4 * FNT) {
-        uint32_t v[4];
+      {  // a thread's FC / FNT bytes: every load in flight at once
+        constexpr int GU = FC / FNT;
+        uint32_t v[GU];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t j = j0 + (uint32_t)FNT * u + (uint32_t)lane;
+        for (int u = 0; u < GU; ++u) {
+          const uint32_t j = (uint32_t)FNT * u + (uint32_t)lane;
           v[u] = j < n ? fd[j] : FD_LIT;
           if (!(v[u] & FD_LIT)) {
             const int32_t q = (int32_t)v[u] - FD_BIAS;
@@ -2165,12 +2199,14 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
           }
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const uint32_t j = j0 + (uint32_t)FNT * u + (uint32_t)lane;
+        for (int u = 0; u < GU; ++u) {
+          const uint32_t j = (uint32_t)FNT * u + (uint32_t)lane;
           if (j < n) fd[j] = v[u];
         }
       }
       __syncthreads();
+      FPROF_ACC(2, f_ga);
+      FPROF_T(f_st);
       // 4. store the chunk: head bytes to a 4-B boundary, dwords, tail bytes
       uint8_t* const dst = out + C0;
       uint32_t head = (uint32_t)((4u - (uint32_t)((uintptr_t)dst & 3u)) & 3u);
@@ -2187,6 +2223,7 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
       // the stores complete before the next chunk gathers from them
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __syncthreads();
+      FPROF_ACC(3, f_st);
     }
     if (bad) break;
     pos += (int32_t)L;
@@ -2221,9 +2258,34 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
     const int32_t lo = (P - nh) > 0 ? (P - nh) : 0;
     // slot j holds position q(j) in [P - 32768, P); q < 0: the old image has it already
     uint8_t* const wout = a.window + (uint64_t)s * WSG_INFLATE_WINDOW;
-    for (uint32_t j = (uint32_t)lane; j < WSG_INFLATE_WINDOW; j += FNT) {
-      const int32_t q = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)((j - nph) & WMASK);
-      if (q >= lo) wout[j] = (uint8_t)__builtin_amdgcn_raw_buffer_load_b8(rout, (uint32_t)q, 0, 1);
+    // a dword of slots a thread, 8 dwords (32 byte loads) in flight; slots whose position
+    // is before lo keep the old image's byte
+    uint32_t* const wout32 = reinterpret_cast<uint32_t*>(wout);
+    for (uint32_t w0 = 0; w0 < WSG_INFLATE_WINDOW / 4; w0 += 8 * FNT) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const uint32_t w = w0 + (uint32_t)FNT * u + (uint32_t)lane;
+        uint32_t x = 0;
+        bool all = true;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+          const int32_t q = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)((4 * w + b - nph) & WMASK);
+          if (q >= lo) x |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rout, (uint32_t)q, 0, 1) << (8 * b);
+          else all = false;
+        }
+        if (!all) {  // merge with the old image
+          const uint32_t old = wout32[w];
+#pragma unroll
+          for (int b = 0; b < 4; ++b) {
+            const int32_t q = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)((4 * w + b - nph) & WMASK);
+            if (q < lo) x |= old & (0xffu << (8 * b));
+          }
+        }
+        v[u] = x;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) wout32[w0 + (uint32_t)FNT * u + (uint32_t)lane] = v[u];
     }
     st.window_len = (uint16_t)nh;
     st.window_phase = (uint16_t)nph;
@@ -2235,6 +2297,7 @@ __global__ __launch_bounds__(FNT) void k_infl_fast(InflArgs a) {
     a.replay_from[s] = 0xffffffffu;
     a.fast_done[s] = 1;
   }
+  FPROF_ACC(4, f_all);
 }
 
 // Message order for the pre-decode: a wave's 64 lanes step in lock-step until its

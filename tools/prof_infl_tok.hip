@@ -41,6 +41,26 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(d_desc, desc.data(), n * sizeof(wsg_frame_desc), hipMemcpyHostToDevice));
   CK(hipMemcpy(d_sf, sf.data(), (ns + 1) * 4, hipMemcpyHostToDevice));
   CK(hipMemcpy(d_pl, payload.data(), pl, hipMemcpyHostToDevice));
+  const uint64_t cap = hdr[3];
+  wsg_inflate_state* d_state;
+  uint8_t *d_win, *d_out, *d_fast;
+  wsg_frame_desc* d_odesc;
+  wsg_session_result* d_res;
+  uint32_t* d_rf;
+  uint64_t* d_off;
+  std::vector<uint64_t> ooff(ns + 1);
+  for (uint64_t i = 0; i <= ns; ++i) ooff[i] = i * cap;
+  CK(hipMalloc(&d_state, ns * sizeof(wsg_inflate_state)));
+  CK(hipMalloc(&d_win, ns * 32768));
+  CK(hipMalloc(&d_out, ns * cap));
+  CK(hipMalloc(&d_fast, ns));
+  CK(hipMalloc(&d_odesc, n * sizeof(wsg_frame_desc)));
+  CK(hipMalloc(&d_res, ns * sizeof(wsg_session_result)));
+  CK(hipMalloc(&d_rf, ns * 4));
+  CK(hipMalloc(&d_off, (ns + 1) * 8));
+  CK(hipMemcpy(d_off, ooff.data(), (ns + 1) * 8, hipMemcpyHostToDevice));
+  a.state = d_state; a.window = d_win; a.out = d_out; a.out_off = d_off; a.out_desc = d_odesc; a.result = d_res;
+  a.replay_from = d_rf; a.fast_done = d_fast;
   a.desc = d_desc; a.n_frames = n; a.session_first = d_sf; a.n_sessions = (uint32_t)ns;
   a.payload = d_pl; a.payload_len = pl;
   a.tok = d_tok; a.lit = d_lit; a.lit_len = ws::infl_lit_bytes(pl, n); a.tstat = d_stat; a.tab = d_tab; a.n_lanes = lanes;
@@ -68,6 +88,19 @@ int main(int argc, char** argv) {
     uint64_t ok = 0;
     for (auto& x : st) ok += x.ok != 0;
     const double m = p[6] ? (double)p[6] : 1.0;
+    // then the parallel replay of the sessions, its phase clocks
+    CK(hipMemset(d_state, 0, ns * sizeof(wsg_inflate_state)));
+    CK(hipMemcpyToSymbol(HIP_SYMBOL(ws::g_fast_prof), z, sizeof(z)));
+    CK(hipEventRecord(e0));
+    ws::launch_infl_fast(a, 0);
+    CK(hipEventRecord(e1));
+    CK(hipDeviceSynchronize());
+    float fms = 0;
+    CK(hipEventElapsedTime(&fms, e0, e1));
+    unsigned long long fp[8] = {};
+    CK(hipMemcpyFromSymbol(fp, HIP_SYMBOL(ws::g_fast_prof), sizeof(fp)));
+    printf("fast replay %.3f ms: per session cycles: expand %.0f chase %.0f gather %.0f store %.0f total %.0f\n", fms,
+           (double)fp[0] / ns, (double)fp[1] / ns, (double)fp[2] / ns, (double)fp[3] / ns, (double)fp[4] / ns);
     printf("rep %d: %.3f ms, %u lanes, %llu messages, %llu ok\n", rep, ms, lanes, (unsigned long long)p[6],
            (unsigned long long)ok);
     const char* names[8] = {"message total", "header+tables", "tables (dynamic)", "symbol loop", "steps", "blocks", "messages", "lds bail-outs"};
