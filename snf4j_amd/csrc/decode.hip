@@ -860,8 +860,11 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
 #pragma unroll
   for (int i = 0; i < N; ++i) {
     const uint32_t pw = dpp_from_prev(w[i][3], carry);
-    uint32_t f0 = utf8_err_word_raw(w[i][0], pw), f1 = utf8_err_word_raw(w[i][1], w[i][0]);
-    uint32_t f2 = utf8_err_word_raw(w[i][2], w[i][1]), f3 = utf8_err_word_raw(w[i][3], w[i][2]);
+    U8W up, u0, u1, u2, u3;
+    u8w_one(pw, up);
+    u8w_pair(w[i][0], w[i][1], u0, u1);
+    u8w_pair(w[i][2], w[i][3], u2, u3);
+    uint32_t f0 = u8w_err(u0, up), f1 = u8w_err(u1, u0), f2 = u8w_err(u2, u1), f3 = u8w_err(u3, u2);
     const bool cont_head = i == 0 && lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT);
     if (cont_head) f0 &= 0x80000000u;  // a continuation's bytes 0..2: k_link
     if (i + 1 == N && !full) {

@@ -223,6 +223,58 @@ WS_HD uint32_t utf8_err_word_raw(uint32_t w, uint32_t p) {
 
 WS_HD uint32_t utf8_err_word_fast(uint32_t w, uint32_t p) { return utf8_err_word_raw(w, p) & H80; }
 
+// The same rule split into per-word values, so that a word's shifts and masks are
+// computed once and serve it both as the current word and as the next word's
+// predecessor: the kernels run utf8_err_word_raw over runs of consecutive words.
+//   t1 = w << 1; c/g/f = ">= C0/E0/F0" in bit 7; z = bits 5..3 of each byte (the
+//   previous-byte table index, and the byte's own 80/88/.../B8 class: tb is the
+//   bits 5..4 table with each entry doubled); l = bits 2..0.
+// Two consecutive words share 64-bit shifts (v_lshlrev_b64: the bits that cross
+// from the low word into the high one land in bits 0..2 of its byte 0, which the
+// rule never reads).  u8w_err(x, p) == utf8_err_word_raw(x.w, p.w) in bit 7 of
+// each byte (tests/cpp/utf8_rule_check.cpp).
+struct U8W {
+  uint32_t w, t1, c, g, f, z, l;
+};
+
+WS_HD void u8w_finish(U8W& x, uint32_t w, uint32_t s1, uint32_t s2, uint32_t s3, uint32_t r3) {
+  x.w = w;
+  x.t1 = s1;
+  x.c = w & s1;
+  x.g = x.c & s2;
+  x.f = x.g & s3;
+  x.z = r3 & 0x07070707u;
+  x.l = w & 0x07070707u;
+}
+
+WS_HD void u8w_one(uint32_t w, U8W& x) { u8w_finish(x, w, w << 1, w << 2, w << 3, w >> 3); }
+
+WS_HD void u8w_pair(uint32_t wa, uint32_t wb, U8W& a, U8W& b) {
+  const uint64_t P = ((uint64_t)wb << 32) | wa;
+  uint64_t S1, S2, S3, R3;
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(WSG_U8W_SHIFT32)
+  // (written out: the compiler splits a 64-bit shift by a constant into two 32-bit ops)
+  asm("v_lshlrev_b64 %0, 1, %1" : "=v"(S1) : "v"(P));
+  asm("v_lshlrev_b64 %0, 2, %1" : "=v"(S2) : "v"(P));
+  asm("v_lshlrev_b64 %0, 3, %1" : "=v"(S3) : "v"(P));
+  asm("v_lshrrev_b64 %0, 3, %1" : "=v"(R3) : "v"(P));
+#else
+  S1 = P << 1; S2 = P << 2; S3 = P << 3; R3 = P >> 3;
+#endif
+  u8w_finish(a, wa, (uint32_t)S1, (uint32_t)S2, (uint32_t)S3, (uint32_t)R3);
+  u8w_finish(b, wb, (uint32_t)(S1 >> 32), (uint32_t)(S2 >> 32), (uint32_t)(S3 >> 32), (uint32_t)(R3 >> 32));
+}
+
+WS_HD uint32_t u8w_err(const U8W& x, const U8W& p) {
+  const uint32_t c1 = alignbyte(x.c, p.c, 3);  // previous byte >= C0
+  const uint32_t expect = c1 | alignbyte(x.g, p.g, 2) | alignbyte(x.f, p.f, 1);
+  const uint32_t err = expect ^ (x.w & ~x.t1);
+  const uint32_t th = perm_bytes(0x40320804u, 0x00000001u, alignbyte(x.z, p.z, 3));
+  const uint32_t tl = perm_bytes(0x42424A60u, 0x40404155u, alignbyte(x.l, p.l, 3));
+  const uint32_t tb = perm_bytes(0x6B6B6B6Bu, 0x67675757u, x.z);
+  return err | (((th & tl & tb) + 0x7F7F7F7Fu) & c1);
+}
+
 // Last byte of a frame is a lead the DFA rejects on its own (C0, C1, F5..FF):
 // the pair rule above would flag it only at the next byte.
 WS_HD bool utf8_bad_last(uint32_t b) { return b == 0xC0u || b == 0xC1u || b >= 0xF5u; }

@@ -60,6 +60,18 @@ done:
   return first;
 }
 
+// the kernels' per-word form (U8W: shared shifts, 64-bit pair shifts) must equal
+// utf8_err_word_fast in bit 7 of every byte, single words and pairs alike
+static long u8w_fails = 0;
+static void u8w_check(uint32_t w, uint32_t p) {
+  ws::U8W x, q, a, b;
+  ws::u8w_one(w, x);
+  ws::u8w_one(p, q);
+  ws::u8w_pair(p, w, a, b);
+  const uint32_t want = ws::utf8_err_word_fast(w, p);
+  if ((ws::u8w_err(x, q) & ws::H80) != want || (ws::u8w_err(b, a) & ws::H80) != want) ++u8w_fails;
+}
+
 // the fast rule on a message start (a TEXT frame, k_pieces alone): word form over
 // the whole string with a zero word before it, plus the last-byte test.
 static int64_t fast_first_start(const uint8_t* s, int n) {
@@ -71,6 +83,7 @@ static int64_t fast_first_start(const uint8_t* s, int n) {
     memcpy(&w, &b[8 + 4 * wi], 4);
     memcpy(&p, &b[4 + 4 * wi], 4);
     uint32_t e = ws::utf8_err_word_fast(w, p);
+    u8w_check(w, p);
     for (int j = 0; j < 4 && 4 * wi + j < n; ++j)
       if (e & (0x80u << (8 * j))) { first = 4 * wi + j; break; }
   }
@@ -138,6 +151,13 @@ int main(int argc, char** argv) {
     check(s, n);
     ++count;
   }
-  printf("checked %ld strings, %ld mismatches\n", count, fails);
-  return fails ? 1 : 0;
+  // every (previous byte, byte) pair at every byte position of the word
+  for (int a = 0; a < 256; ++a)
+    for (int b = 0; b < 256; ++b)
+      for (int j = 0; j < 4; ++j) {
+        const uint64_t v = ((uint64_t)b << 32 | (uint64_t)a << 24) << (8 * j);
+        u8w_check((uint32_t)(v >> 32), (uint32_t)v);
+      }
+  printf("checked %ld strings, %ld mismatches, %ld per-word form mismatches\n", count, fails, u8w_fails);
+  return fails || u8w_fails ? 1 : 0;
 }

@@ -40,15 +40,16 @@ def test_validator_kat_through_gpu(ctx):
                 assert out == [fr] and out[0] is fr
 
 
-def _plain_batch(parts, rng):
-    """desc / session_first / payload of plain frames, payload offsets unaligned."""
+def _plain_batch(parts, rng, aligned=False):
+    """desc / session_first / payload of plain frames, payload offsets unaligned
+    (or each payload at a 16-B boundary)."""
     from snf4j_amd._lib import DESC_DTYPE
     n = sum(len(p) for p in parts)
     desc = np.zeros(n, dtype=DESC_DTYPE)
     chunks, pos, k, sf = [], 0, 0, [0]
     for fr in parts:
         for (op, fin, p) in fr:
-            gap = int(rng.integers(0, 7))
+            gap = (-pos) % 16 if aligned else int(rng.integers(0, 7))
             chunks.append(bytes(gap))
             pos += gap
             desc[k]["payload_off"] = pos
@@ -121,3 +122,63 @@ def test_validate_random_batches(ctx, oracle, seed):
         assert failed[s] == exp_fail, (seed, s)
         if exp_fail is None:
             assert passed[s] == len(sessions[s]), (seed, s)
+
+
+def _check_sessions(ctx, oracle, rng, sessions, n_batches, aligned=False):
+    from snf4j_amd._lib import STATE_DTYPE
+    n_s = len(sessions)
+    cuts = [[0] + sorted(int(x) for x in rng.integers(0, len(f) + 1, n_batches - 1)) + [len(f)] for f in sessions]
+    state = np.zeros(n_s, dtype=STATE_DTYPE)
+    passed = [0] * n_s
+    failed = [None] * n_s
+    for b in range(n_batches):
+        parts = [sessions[s][cuts[s][b]:cuts[s][b + 1]] for s in range(n_s)]
+        desc, sf, payload = _plain_batch(parts, rng, aligned)
+        res = ctx.validate_host(desc, sf, payload, state)
+        for s in range(n_s):
+            if failed[s] is not None:
+                continue
+            passed[s] += int(res[s]["n_delivered"])
+            if res[s]["error"]:
+                assert int(res[s]["error"]) == 14 and int(res[s]["close_code"]) == 1007
+                failed[s] = passed[s]
+    for s in range(n_s):
+        v = oracle.Validator()
+        exp_fail = None
+        for i, (op, fin, p) in enumerate(sessions[s]):
+            if not v.decode(op, fin, p):
+                exp_fail = i
+                break
+        assert failed[s] == exp_fail, s
+        if exp_fail is None:
+            assert passed[s] == len(sessions[s]), s
+
+
+@pytest.mark.parametrize("seed,aligned", [(0, False), (1, True), (2, False), (3, True)])
+def test_validate_large_frames(ctx, oracle, seed, aligned):
+    """Frames of 1-40 KiB, so that whole 4 KiB groups of pieces take the
+    lane-contiguous validate path: invalid sequences planted anywhere (piece and
+    lane boundaries, the last bytes, the first bytes of a continuation), code
+    points cut by fragment ends, 16-B aligned and unaligned payload offsets."""
+    rng = np.random.default_rng(4200 + seed)
+    sessions = []
+    for _ in range(int(rng.integers(20, 60))):
+        frames = []
+        for _ in range(int(rng.integers(1, 5))):
+            body = wsgen.rand_text(rng, int(rng.integers(400, 16000)))
+            if rng.random() < 0.3:
+                bad = wsgen.BAD_UTF8[int(rng.integers(0, len(wsgen.BAD_UTF8)))]
+                r = rng.random()
+                at = (len(body) if r < 0.2 else int(rng.integers(0, 3)) if r < 0.3
+                      else (int(rng.integers(1, max(2, len(body) // 1024))) * 1024 + int(rng.integers(-3, 4))) if r < 0.6
+                      else int(rng.integers(0, len(body) + 1)))
+                at = max(0, min(len(body), at))
+                body = body[:at] + bad + body[at:]
+            if rng.random() < 0.15 and len(body) > 1:  # truncated last code point: fails at FIN
+                body = body[:-1]
+            cuts = sorted(int(x) for x in rng.integers(0, len(body) + 1, int(rng.integers(0, 3))))
+            pieces = [body[a:b] for a, b in zip([0] + cuts, cuts + [len(body)])]
+            for i, pc in enumerate(pieces):
+                frames.append((1 if i == 0 else 0, i == len(pieces) - 1, pc))
+        sessions.append(frames)
+    _check_sessions(ctx, oracle, rng, sessions, 1 + seed % 2, aligned)

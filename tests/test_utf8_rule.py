@@ -15,3 +15,4 @@ def test_rule_equals_dfa(tmp_path):
     r = subprocess.run([exe, "5", "300000"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "0 mismatches" in r.stdout
+    assert "0 per-word form mismatches" in r.stdout
