@@ -41,7 +41,10 @@ constexpr int BLOCK = 256;    // frames per block in the encode / aggregate pass
 constexpr int DBLOCK = 256;   // frames (threads) per block in the decode parse / link passes
 constexpr uint32_t PIECE = 1024;  // payload-output bytes per wave in k_pieces (64 lanes x 16 B)
 constexpr int PIECES_PER_WAVE = 2; // pieces one k_piecesN wave takes (tools/ubench_unmask)
-constexpr int VPIECES_PER_WAVE = 4;  // validate-only mode (read-only stream)
+#ifndef WSG_VPIECES
+#define WSG_VPIECES 4
+#endif
+constexpr int VPIECES_PER_WAVE = WSG_VPIECES;  // validate-only mode (read-only stream)
 constexpr int ENC_PIECES_PER_WAVE = 2;  // k_enc_piecesN (1 and 2 within 1% once no array is promoted to LDS)
 
 // Pieces needed for a batch, bounded from host-known sizes: the 16-B aligned
