@@ -48,6 +48,9 @@ def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (rank processes); default WORLD_SIZE or 1")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--event-every", type=int, default=4,
+                    help="timed steps bracket the streaming kernel with a HIP event pair in one step of "
+                         "this many (an event pair costs ~12 us of queue time: tools/ubench_graph.hip)")
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", choices=sorted(CONFIGS), default="north",
                     help="per-GPU workload: north (1M x 4 KiB TEXT), 1 (configs[1]), 3 (configs[3] shard, 8M x 4 KiB)")
@@ -189,6 +192,7 @@ def cpu_baseline_mt(args, seconds):
 
 def main():
     args = parse()
+    EVENT_EVERY[0] = max(1, args.event_every)
     world = launch_or_check_world(args)  # (may start the rank processes and exit)
     import numpy as np
     import torch
@@ -260,8 +264,10 @@ def main():
     # timed region: events around the streaming kernel only (its roofline figure)
     ctx.reset_timing()
     ctx.set_timing("hot")
+    ctx.set_timing_every(EVENT_EVERY[0])
     elapsed = time_steps(step, args.steps, sync=lambda: torch.cuda.synchronize(dev), dist=dist)
     ctx.set_timing(False)
+    ctx.set_timing_every(1)
     timing = ctx.timing()
     pipe = pipeline_breakdown(ctx, step, dev)
     validator = None  # (before copy_ceiling, which overwrites the payload buffer)
@@ -340,6 +346,7 @@ def main():
                 "traffic": traffic,
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(avg_unmask_s * 1e3, 4),
+                "launches_timed": int(unmask_n), "event_every": EVENT_EVERY[0],
                 "copy_ceiling_GBs": round(copy, 1),
                 "frac_of_copy_ceiling": round(achieved / copy, 4),
                 # the north star's "HBM read-bandwidth fraction": wire bytes read / time / 8 TB/s,
@@ -393,6 +400,9 @@ def validator_line(ctx, dev, desc, sf, payload, n_s, F, P, steps):
             "pipeline_ms": pipe}
 
 
+EVENT_EVERY = [4]  # set from --event-every in main()
+
+
 def pipeline_breakdown(ctx, step, dev, steps=5):
     """Per-kernel averages (ms) from a separate, untimed pass with an event pair
     around every kernel (diagnostic: the pairs themselves add queue time)."""
@@ -416,9 +426,11 @@ def _timed(ctx, step, steps, warmup, dev, kernel):
     torch.cuda.synchronize(dev)
     ctx.reset_timing()
     ctx.set_timing("hot")
+    ctx.set_timing_every(EVENT_EVERY[0])
     from snf4j_amd.shard import time_steps
     el = time_steps(step, steps, sync=lambda: torch.cuda.synchronize(dev))
     ctx.set_timing(False)
+    ctx.set_timing_every(1)
     tm = ctx.timing()
     # a list of kernels: the sum of their average durations (a pipeline of launches per step)
     kms = sum(tm[k][0] / max(1, tm[k][1]) for k in (kernel if isinstance(kernel, (list, tuple)) else [kernel]))

@@ -171,6 +171,10 @@ int wsg_sync(wsg_ctx* ctx);
  * enable: 0 off, 1 every kernel, 2 only the streaming kernels (k_piecesN,
  * k_enc_piecesN, k_agg_gather) — each event pair adds queue time, so a timed step uses 2. */
 int wsg_set_timing(wsg_ctx* ctx, int enable);
+/* Mode 2 brackets one launch in `every` of each streaming kernel (default 1): an
+ * event pair costs ~12 us of queue time (tools/ubench_graph.hip), so a timed region
+ * samples the kernel's duration instead of paying that on every step. */
+int wsg_set_timing_every(wsg_ctx* ctx, uint32_t every);
 /* out_ms[i] = accumulated milliseconds of kernel i since the last reset, out_count[i] = launches.
  * Kernel ids: see wsg_kernel_name(). Syncs the stream. */
 int wsg_get_timing(wsg_ctx* ctx, double* out_ms, uint64_t* out_count, int max_kernels);

@@ -111,6 +111,7 @@ def _load():
         "wsg_reserve": ([p, u64, u32, u64], i32),
         "wsg_sync": ([p], i32),
         "wsg_set_timing": ([p, i32], i32),
+        "wsg_set_timing_every": ([p, u32], i32),
         "wsg_get_timing": ([p, P(C.c_double), P(u64), i32], i32),
         "wsg_reset_timing": ([p], i32),
         "wsg_kernel_name": ([i32], C.c_char_p),

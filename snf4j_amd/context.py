@@ -121,6 +121,10 @@ class Context:
         costs queue time, so timed steps bracket only the kernel the roofline needs)."""
         check(lib.wsg_set_timing(self._h, 2 if on == "hot" else int(bool(on))), self._h)
 
+    def set_timing_every(self, every: int):
+        """'hot' timing brackets one launch in `every` of each streaming kernel."""
+        check(lib.wsg_set_timing_every(self._h, int(every)), self._h)
+
     def reset_timing(self):
         check(lib.wsg_reset_timing(self._h), self._h)
 

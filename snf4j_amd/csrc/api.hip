@@ -82,6 +82,8 @@ struct wsg_ctx {
   hipEvent_t ev_prev_state = nullptr;  // state download of the previous async batch
   // timing
   int timing = 0;  // 0 off, 1 every kernel, 2 the streaming kernels only (WSG_TIMING_*)
+  uint32_t timing_every = 1;  // mode 2: bracket one launch in timing_every of a streaming kernel
+  uint64_t timing_seen[K_COUNT] = {};
   std::vector<EventPair> pending;
   std::vector<hipEvent_t> free_events;
   double ms[K_COUNT] = {};
@@ -136,6 +138,10 @@ static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
   if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_INFL_TOK && kid != K_INFL_FAST)) {
+    f();
+    return;
+  }
+  if (c->timing == 2 && (c->timing_seen[kid]++ % c->timing_every) != 0) {
     f();
     return;
   }
@@ -238,6 +244,13 @@ int wsg_sync(wsg_ctx* c) {
   if (c->s_in) HIP_TRY(c, hipStreamSynchronize(c->s_in));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   if (c->s_out) HIP_TRY(c, hipStreamSynchronize(c->s_out));
+  return WSG_API_OK;
+}
+
+int wsg_set_timing_every(wsg_ctx* c, uint32_t every) {
+  if (!c || every == 0) return WSG_API_EINVAL;
+  c->timing_every = every;
+  for (auto& n : c->timing_seen) n = 0;
   return WSG_API_OK;
 }
 
