@@ -70,7 +70,7 @@ def parse():
     ap.add_argument("--handshake-only", action="store_true", help="only the server handshake line")
     ap.add_argument("--inflate-sessions", type=int, nargs="+", default=[8192])
     ap.add_argument("--only", default=None,
-                    help="print only one secondary line: configs1|configs2|configs3|encode|validator|inflate|handshake")
+                    help="print only one secondary line: configs1|configs2|configs3|encode|validator|inflate|handshake|hs_client")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     for k in ("frames", "payload", "sessions"):
@@ -770,17 +770,78 @@ def line_validator(ctx, dev, K, W):
     return validator_line(ctx, dev, desc, sf, payload, S, F, P, K)
 
 
+def handshake_client_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
+    """Client opening handshakes (wsg_handshake_validate_batch_device): n servers'
+    101 responses, each validated against the key its session sent (HandshakeDecoder
+    in client mode + Handshaker.validate).  One lane per response.  cpu_baseline: the
+    Python restatement on one host core (no JDK on the box)."""
+    import base64
+    import numpy as np
+    import torch
+    from oracle import handshake_oracle as H
+    from snf4j_amd._lib import HS_EXPECTED_STRIDE, HS_RESULT_DTYPE, HsConfig
+    tmpl = H.response(101, "Switching Protocols", [
+        ("Server", "nginx/1.25.3"), ("Date", "Sat, 17 Oct 2026 00:00:00 GMT"), ("Connection", "upgrade"),
+        ("Upgrade", "websocket"), ("Sec-WebSocket-Accept", "A" * 28)])
+    L = len(tmpl)
+    apos = tmpl.index(b"A" * 28)
+    rng = np.random.default_rng(0xC11E)
+    raw = rng.integers(0, 256, (n, 16), dtype=np.uint8)
+    keys = [base64.b64encode(r.tobytes()) for r in raw]
+    k24 = np.frombuffer(b"".join(keys), dtype=np.uint8).reshape(n, 24)
+    acc = np.frombuffer(b"".join(H.answer_key(k.decode()).encode() for k in keys), dtype=np.uint8).reshape(n, 28)
+    buf = np.tile(np.frombuffer(tmpl, dtype=np.uint8), (n, 1))
+    buf[:, apos:apos + 28] = acc
+    resp = torch.from_numpy(buf.reshape(-1)).to(dev)
+    off = torch.arange(n + 1, dtype=torch.int64, device=dev) * L
+    kd = torch.from_numpy(k24.reshape(-1).copy()).to(dev)
+    exp = torch.empty(n * HS_EXPECTED_STRIDE, dtype=torch.uint8, device=dev)
+    res = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+    cfg = HsConfig(65536, 0, 0, 0, 0)
+
+    def step():
+        ctx.handshake_validate_device(cfg, resp, off, kd, exp, res, n=n)
+
+    step()
+    torch.cuda.synchronize(dev)
+    r = res.cpu().numpy().view(HS_RESULT_DTYPE)
+    assert (r["kind"] == H.FINISHED).all(), "client handshake of the synthetic batch failed"
+    for i in (0, 1, n // 2, n - 1):  # spot check against the restatement
+        assert H.validate(buf[i].tobytes(), keys[i].decode())["kind"] == H.FINISHED, i
+    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, "k_hs_validate")
+    alg = n * (L + 8 + 24 + 28 + 16)
+    ach = alg / (kms / 1e3) / 1e9
+    done, t0 = 0, time.perf_counter()
+    while time.perf_counter() - t0 < cpu_seconds:
+        H.validate(buf[done % n].tobytes(), keys[done % n].decode())
+        done += 1
+    t = time.perf_counter() - t0
+    return {"config": f"client handshake: {n} server responses of {L} B (101, random keys), "
+                      "HandshakeDecoder(clientMode) + Handshaker.validate (key challenge, basic fields)",
+            "value": round(n * steps / el / 1e6, 3), "unit": "M handshakes/s",
+            "ms_per_step": round(el / steps * 1e3, 4),
+            "roofline": {"kernel": "k_hs_validate", "bound": "per-lane serial parse + SHA-1 (not hbm)",
+                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": round(kms, 4)},
+            "cpu_baseline": {"value": round(done / t / 1e6, 5), "unit": "M handshakes/s", "cores": 1, "kind": "port",
+                             "sample": f"{done} responses through the Python restatement "
+                                       f"(oracle/handshake_oracle.py) in {t:.1f} s, 1 thread; no JDK on the box"},
+            "pipeline_ms": pipe}
+
+
 EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2": line_configs2,
                "encode": line_encode, "validator": line_validator,
                "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
-               "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W)}
+               "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W),
+               "hs_client": lambda ctx, dev, K, W: handshake_client_line(ctx, dev, K, W)}
 
 
 def measure_extras(ctx, dev, args):
     """The other 1-GPU configurations of BASELINE.json, each a device-resident batch."""
     import torch
     out = []
-    for name in ("configs1", "configs3", "configs2", "encode", "inflate", "handshake"):
+    for name in ("configs1", "configs3", "configs2", "encode", "inflate", "handshake", "hs_client"):
         out.append(EXTRA_LINES[name](ctx, dev, args.extra_steps, 2))
         torch.cuda.empty_cache()
     return out

@@ -492,7 +492,10 @@ typedef enum wsg_hs_kind {
     WSG_HS_NEED_MORE = 0,     /* no complete frame yet (available() == 0) */
     WSG_HS_DEFER = 1,         /* the Java HandshakeDecoder/Handshaker takes this request */
     WSG_HS_PARSE_ERROR = 2,   /* HandshakeDecoder: writenf(HandshakeResponse(status)) + exception (:194-203) */
-    WSG_HS_ACCEPT = 3         /* Handshaker.accept returned a response (101 or a refusal) */
+    WSG_HS_ACCEPT = 3,        /* Handshaker.accept returned a response (101 or a refusal) */
+    /* client side (wsg_handshake_validate_batch_*) */
+    WSG_HS_FINISHED = 4,      /* Handshaker.validate(response) true: the session switches (:557-560) */
+    WSG_HS_CLOSING = 5        /* validate false: the session closes with getClosingReason() (:561-563) */
 } wsg_hs_kind;
 
 typedef enum wsg_hs_cause {
@@ -511,6 +514,17 @@ typedef enum wsg_hs_cause {
     WSG_HSC_MISSING_HOST = 12,       /* "Missing websocket request host"    :336 */
     WSG_HSC_MISSING_KEY = 13,        /* "Missing websocket key"             :254 */
     WSG_HSC_INVALID_KEY = 14,        /* "Invalid websocket key: %s"         :251 */
+    /* client side: HandshakeDecoder(clientMode) exceptions and Handshaker.validate reasons */
+    WSG_HSC_BAD_RESPONSE_LINE = 15,     /* "Invalid http response"          HandshakeFactory.java:110 */
+    WSG_HSC_BAD_RESPONSE_VERSION = 16,  /* "Invalid http response version"  :113 */
+    WSG_HSC_BAD_RESPONSE_STATUS = 17,   /* "Invalid http response status"   :119 */
+    WSG_HSC_INVALID_STATUS = 18,        /* "Invalid websocket response status: %d" Handshaker.java:542 (http_status) */
+    WSG_HSC_MISSING_ACCEPT = 19,        /* "Missing websocket key challenge" :458 */
+    WSG_HSC_INVALID_ACCEPT = 20,        /* "Invalid websocket key challenge. Actual: %s. Expected: %s" :455
+                                           (detail = actual; expected = the 28 bytes at expected_out) */
+    WSG_HSC_MISSING_SUBPROTOCOL = 21,   /* "Missing websocket sub protocol" :476 */
+    WSG_HSC_INVALID_SUBPROTOCOL = 22,   /* "Invalid websocket sub protocol: %s" :483 */
+    WSG_HSC_INVALID_EXTENSIONS = 23,    /* validateExtensions false with no reason set (:529-532): null */
     /* why a request was deferred (WSG_HS_DEFER) */
     WSG_HSC_D_LINE_FORM = 32, WSG_HSC_D_REPEATED = 33, WSG_HSC_D_NON_ASCII = 34, WSG_HSC_D_URI = 35,
     WSG_HSC_D_HOST = 36, WSG_HSC_D_SUBPROTOCOL = 37, WSG_HSC_D_EXTENSION = 38, WSG_HSC_D_POLICY = 39,
@@ -541,6 +555,32 @@ int wsg_handshake_accept_batch_device(wsg_ctx* ctx, const wsg_hs_config* cfg, co
 /* Same with host pointers (H2D, kernel, D2H). */
 int wsg_handshake_accept_batch_host(wsg_ctx* ctx, const wsg_hs_config* cfg, const uint8_t* req,
                                     const uint64_t* req_off, uint32_t n, uint8_t* resp, wsg_hs_result* result);
+
+/* Client side of the opening handshake (a client opening many connections at once):
+ *   HandshakeDecoder(clientMode = true).available/decode   HandshakeDecoder.java:141-235
+ *     (HandshakeFactory.parse, response branch            HandshakeFactory.java:108-123)
+ *   Handshaker.handshake(response) -> validate            Handshaker.java:420-544, 555-566
+ *     (validateBasicFields / validateKeyChallenge / validateSubProtocol / validateExtensions)
+ * Response i is resp[resp_off[i], resp_off[i+1]) (the bytes the session has received);
+ * keys[24 i, +24) is the Sec-WebSocket-Key the session sent (HandshakeUtils.generateKey:
+ * Base64 of 16 bytes).  result[i].kind is NEED_MORE, DEFER, PARSE_ERROR (the exception
+ * HandshakeDecoder throws in client mode: no response is written), FINISHED or CLOSING
+ * (cause = the closing reason, http_status = the response status).  expected_out[32 i,
+ * +28) receives Base64(SHA-1(key + GUID)) once the frame is complete (resp_len = 28).
+ * cfg: max_length; subprotocols / extensions = the config lists are non-empty.
+ * Deferred to the Java Handshaker: the header forms the server side defers (folded or
+ * name-only lines, repeats of Upgrade/Connection/Sec-WebSocket-Accept/-Protocol/
+ * -Extensions, non-ASCII bytes in those), a Sec-WebSocket-Protocol answer when the
+ * config lists subprotocols (a string match against the list), and an extensions
+ * answer when it lists extensions (IExtension.validateResponse). */
+#define WSG_HS_EXPECTED_STRIDE 32
+int wsg_handshake_validate_batch_device(wsg_ctx* ctx, const wsg_hs_config* cfg, const uint8_t* resp,
+                                        const uint64_t* resp_off, const uint8_t* keys, uint32_t n,
+                                        uint8_t* expected_out, wsg_hs_result* result);
+/* Same with host pointers (H2D, kernel, D2H). */
+int wsg_handshake_validate_batch_host(wsg_ctx* ctx, const wsg_hs_config* cfg, const uint8_t* resp,
+                                      const uint64_t* resp_off, const uint8_t* keys, uint32_t n,
+                                      uint8_t* expected_out, wsg_hs_result* result);
 
 #ifdef __cplusplus
 }

@@ -1,4 +1,5 @@
-"""CPU restatement of the server side of snf4j's WebSocket opening handshake.
+"""CPU restatement of snf4j's WebSocket opening handshake (server side, and the
+client side's response validation).
 
 TEST INFRASTRUCTURE ONLY: tests/, __graft_entry__.smoke() and bench.py's
 cpu_baseline leg use this as the checker; the product path is k_hs_accept
@@ -18,6 +19,11 @@ Restated from (paths under snf4j-websocket/src/main/java/org/snf4j/websocket/):
                                        acceptKey / acceptSubProtocol / acceptExtensions / accept
   handshake/HandshakeUtils.java:93-120 generateAnswerKey / parseKey
   snf4j-core/.../util/Base64Util.java:253-350 decode (not MIME)
+  client side:
+  handshake/HandshakeFactory.java:108-123  parse, response branch (HttpUtils.digits :271-284)
+  handshake/HandshakeDecoder.java:141-210  decode in client mode (exceptions are thrown)
+  handshake/Handshaker.java:420-544    validateBasicFields / validateKeyChallenge /
+                                       validateSubProtocol / validateExtensions / validate
 
 java.net.URI is not restated: `accept` answers only for the forms whose
 validity follows from RFC 2396's grammar as java.net.URI implements it (relative
@@ -42,6 +48,9 @@ C_NONE, C_BAD_REQUEST_LINE, C_BAD_VERSION, C_FORBIDDEN, C_TOO_LARGE = 0, 1, 2, 3
 C_MISSING_VERSION, C_INCORRECT_VERSION, C_UNSUPPORTED_VERSION = 5, 6, 7
 C_MISSING_UPGRADE, C_MISSING_CONNECTION, C_INVALID_UPGRADE, C_INVALID_CONNECTION = 8, 9, 10, 11
 C_MISSING_HOST, C_MISSING_KEY, C_INVALID_KEY = 12, 13, 14
+FINISHED, CLOSING = 4, 5
+C_BAD_RESPONSE_LINE, C_BAD_RESPONSE_VERSION, C_BAD_RESPONSE_STATUS, C_INVALID_STATUS = 15, 16, 17, 18
+C_MISSING_ACCEPT, C_INVALID_ACCEPT, C_MISSING_SUBPROTOCOL, C_INVALID_SUBPROTOCOL, C_INVALID_EXTENSIONS = 19, 20, 21, 22, 23
 D_LINE_FORM, D_REPEATED, D_NON_ASCII, D_URI, D_HOST, D_SUBPROTOCOL, D_EXTENSION, D_POLICY, D_LINES = range(32, 41)
 
 MESSAGES = {C_BAD_REQUEST_LINE: "Invalid http request", C_BAD_VERSION: "Invalid http request version",
@@ -52,7 +61,14 @@ MESSAGES = {C_BAD_REQUEST_LINE: "Invalid http request", C_BAD_VERSION: "Invalid 
             C_INVALID_UPGRADE: "Invalid websocket upgrade: %s",
             C_INVALID_CONNECTION: "Invalid websocket connection: %s",
             C_MISSING_HOST: "Missing websocket request host", C_MISSING_KEY: "Missing websocket key",
-            C_INVALID_KEY: "Invalid websocket key: %s"}
+            C_INVALID_KEY: "Invalid websocket key: %s",
+            C_BAD_RESPONSE_LINE: "Invalid http response", C_BAD_RESPONSE_VERSION: "Invalid http response version",
+            C_BAD_RESPONSE_STATUS: "Invalid http response status",
+            C_INVALID_STATUS: "Invalid websocket response status: %s",
+            C_MISSING_ACCEPT: "Missing websocket key challenge",
+            C_INVALID_ACCEPT: "Invalid websocket key challenge. Actual: %s. Expected: %s",
+            C_MISSING_SUBPROTOCOL: "Missing websocket sub protocol",
+            C_INVALID_SUBPROTOCOL: "Invalid websocket sub protocol: %s"}
 
 
 class InvalidHandshake(Exception):
@@ -454,6 +470,161 @@ def gpu_defers(data: bytes, max_length=65536, ignore_host=False, subprotocols=Fa
 def request(uri="/uri", fields=None) -> bytes:
     """A request the way HandshakeFactory.format writes one (:133-140, :150-156)."""
     out = b"GET " + uri.encode() + b" HTTP/1.1\r\n"
+    for n, v in (fields or []):
+        out += n.encode() + b": " + v.encode() + b"\r\n"
+    return out + b"\r\n"
+
+
+# ----------------------------------------------------------------- client side
+def parse_response(data: bytes, lines) -> tuple:
+    """HandshakeFactory.parse (:108-123) for a response: (status, Frame)."""
+    b, e = lines[0]
+    tok = split_request_line(data, b, e)           # splitResponseLine = splitRequestLine
+    if len(tok) < 3:
+        raise InvalidHandshake(C_BAD_RESPONSE_LINE)
+    if data[tok[0][0]:tok[0][1]] != b"HTTP/1.1":
+        raise InvalidHandshake(C_BAD_RESPONSE_VERSION)
+    st = data[tok[1][0]:tok[1][1]]
+    if not all(0x30 <= c <= 0x39 for c in st) or len(st) != 3:   # HttpUtils.digits, STATUS_CODE_LENGTH
+        raise InvalidHandshake(C_BAD_RESPONSE_STATUS)
+    status = int(st)
+    f = Frame()
+    for (b, e) in lines[1:]:
+        code, t = split_header_field(data, b, e)
+        if code == 4:
+            if f.pending is not None:
+                raise InvalidHandshake(-2)
+            f.add(ascii_str(data[t[0]:t[1]]), rtrim(data, t[2], t[3]))
+        elif code == 2:
+            if f.pending is not None:
+                raise InvalidHandshake(-2)
+            f.pending = ascii_str(data[t[0]:t[1]])
+        elif code == -4:
+            if f.pending is not None:
+                f.add(ascii_str(data[t[0]:t[1]]), rtrim(data, t[2], t[3]))
+            else:
+                f.append(" ")
+                f.append(rtrim(data, t[0], t[3]))
+        elif code == -2:
+            if f.pending is not None:
+                f.pending += ascii_str(data[t[0]:t[1]])
+            else:
+                f.append(" ")
+                f.append(rtrim(data, t[0], t[1]))
+    return status, f
+
+
+def validate(data: bytes, key: str, max_length=65536, subprotocols=None, extensions=False):
+    """HandshakeDecoder(clientMode).decode + Handshaker.handshake(response) for one
+    response buffer and the key the session sent.  subprotocols: the configured list
+    (None or empty: none); extensions: the configured list is non-empty.  Returns
+    dict(kind, status, cause, detail, frame_len, expected, subprotocol); kind is None
+    when IExtension.validateResponse decides (not restated)."""
+    flen, lines, capped = available(data)
+    r = dict(kind=NEED_MORE, status=0, cause=C_NONE, detail=None, frame_len=flen, expected=None, subprotocol=None)
+    if capped:
+        return dict(r, kind=DEFER, cause=D_LINES)
+    if flen == 0:
+        if not lines:
+            return r
+        end = lines[-1][1] + 2
+        if end > max_length:
+            return dict(r, kind=PARSE_ERROR, cause=C_TOO_LARGE)
+        try:
+            status, _ = parse_response(data[:end], lines[:1])
+        except InvalidHandshake as e:
+            return dict(r, kind=PARSE_ERROR, cause=e.cause)
+        return dict(r, status=status)
+    if flen > max_length:
+        return dict(r, kind=PARSE_ERROR, cause=C_TOO_LARGE)
+    try:
+        status, f = parse_response(data[:flen], lines)
+    except InvalidHandshake as e:
+        return dict(r, kind=PARSE_ERROR, cause=e.cause)
+    r["status"] = status
+
+    def closing(cause, detail=None):
+        return dict(r, kind=CLOSING, cause=cause, detail=detail)
+    if status != 101:                                          # validate (:535-544)
+        return closing(C_INVALID_STATUS, str(status))
+    u, c = f.get("Upgrade"), f.get("Connection")                 # validateBasicFields (:420-444)
+    if u is None:
+        return closing(C_MISSING_UPGRADE)
+    if c is None:
+        return closing(C_MISSING_CONNECTION)
+    if not any(t.lower() == "websocket" for t in values(u)):
+        return closing(C_INVALID_UPGRADE, u)
+    if not any(t.lower() == "upgrade" for t in values(c)):
+        return closing(C_INVALID_CONNECTION, c)
+    expected = answer_key(key)                                   # validateKeyChallenge (:446-460)
+    r["expected"] = expected
+    actual = f.get("Sec-WebSocket-Accept")
+    if actual is None:
+        return closing(C_MISSING_ACCEPT)
+    if actual != expected:
+        return closing(C_INVALID_ACCEPT, actual)
+    received = f.get("Sec-WebSocket-Protocol")                   # validateSubProtocol (:462-485)
+    if subprotocols:
+        if received is None:
+            return closing(C_MISSING_SUBPROTOCOL)
+        if received not in subprotocols:
+            return closing(C_INVALID_SUBPROTOCOL, received)
+        r["subprotocol"] = received
+    elif received is not None:
+        return closing(C_INVALID_SUBPROTOCOL, received)
+    ext = f.get("Sec-WebSocket-Extensions")                      # validateExtensions (:487-533)
+    if ext is not None:
+        if extensions:
+            return dict(r, kind=None)
+        return closing(C_INVALID_EXTENSIONS)
+    return dict(r, kind=FINISHED)
+
+
+CLIENT_TARGETS = ("UPGRADE", "CONNECTION", "SEC-WEBSOCKET-ACCEPT", "SEC-WEBSOCKET-PROTOCOL", "SEC-WEBSOCKET-EXTENSIONS")
+
+
+def gpu_defers_client(data: bytes, key: str, max_length=65536, subprotocols=None, extensions=False):
+    """The forms k_hs_validate hands to the Java Handshaker, in its walk order (the
+    status line, then the header lines, then validate), or None."""
+    flen, lines, capped = available(data)
+    if capped:
+        return D_LINES
+    if flen == 0 or flen > max_length:
+        return None
+    try:
+        parse_response(data[:flen], lines[:1])
+    except InvalidHandshake:
+        return None
+    seen = set()
+    for (b, e) in lines[1:]:
+        code, t = split_header_field(data, b, e)
+        if code != 4:
+            return D_LINE_FORM
+        name = ascii_str(data[t[0]:t[1]]).upper()
+        if name in CLIENT_TARGETS:
+            if name in seen:
+                return D_REPEATED
+            seen.add(name)
+            if any(x >= 0x80 for x in data[t[2]:t[3]]):
+                return D_NON_ASCII
+    r = validate(data, key, max_length, None, False)
+    if r["kind"] == CLOSING and r["cause"] in (C_INVALID_STATUS, C_MISSING_UPGRADE, C_MISSING_CONNECTION,
+                                                 C_INVALID_UPGRADE, C_INVALID_CONNECTION, C_MISSING_ACCEPT,
+                                                 C_INVALID_ACCEPT):
+        return None
+    _, f = parse_response(data[:flen], lines)
+    if subprotocols and f.get("Sec-WebSocket-Protocol") is not None:
+        return D_SUBPROTOCOL
+    if not subprotocols and f.get("Sec-WebSocket-Protocol") is not None:
+        return None
+    if extensions and f.get("Sec-WebSocket-Extensions") is not None:
+        return D_EXTENSION
+    return None
+
+
+def response(status=101, reason="Switching Protocols", fields=None) -> bytes:
+    """A response the way HandshakeFactory.format writes one (:141-157)."""
+    out = b"HTTP/1.1 %03d %s\r\n" % (status, reason.encode())
     for n, v in (fields or []):
         out += n.encode() + b": " + v.encode() + b"\r\n"
     return out + b"\r\n"

@@ -5,7 +5,7 @@
 # and the kernel-trace stats copied to gpurun_out/prof/ROUND_<line>_*.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 round=$1; shift
-lines=${*:-north configs1 configs2 configs3 encode validator inflate handshake}
+lines=${*:-north configs1 configs2 configs3 encode validator inflate handshake hs_client}
 for l in $lines; do
   echo "[$(date +%T)] profiling $l"
   if [ "$l" = north ]; then args="--no-extras"; else args="--only $l"; fi

@@ -10,7 +10,8 @@ from . import _lib  # noqa: F401  (fails loudly if libwsgpu.so is missing)
 from .codec import (BatchAggregator, BatchInflater, FrameAggregator, FrameDecoder, FrameEncoder, FrameUtf8Validator,
                     NativeBatcher, PerMessageDeflateDecoder, SessionBatcher)
 from .context import Context, decoder_cfg, encoded_length, error_message, frame_available
-from .handshake import BatchHandshaker, HandshakeConfig, HandshakeOutcome
+from .handshake import (BatchClientHandshaker, BatchHandshaker, ClientConfig, ClientHandshakeOutcome, HandshakeConfig,
+                        HandshakeOutcome)
 from .frame import (AggregatedBinaryFrame, AggregatedTextFrame, BinaryFrame, CloseFrame, ContinuationFrame, Frame,
                     InvalidFrameException, Opcode, PingFrame, PongFrame, TextFrame)
 

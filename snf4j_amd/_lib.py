@@ -57,6 +57,7 @@ class HsConfig(C.Structure):
 
 
 HS_RESP_STRIDE = 160
+HS_EXPECTED_STRIDE = 32   # wsg_handshake_validate_batch_*: expected Sec-WebSocket-Accept per session
 
 
 assert C.sizeof(SessionState) == 8 and C.sizeof(FrameDesc) == 16
@@ -144,6 +145,8 @@ def _load():
         "wsg_handshake_available": ([p, u64], i32),
         "wsg_handshake_accept_batch_device": ([p, P(HsConfig), p, p, u32, p, p], i32),
         "wsg_handshake_accept_batch_host": ([p, P(HsConfig), p, p, u32, p, p], i32),
+        "wsg_handshake_validate_batch_device": ([p, P(HsConfig), p, p, p, u32, p, p], i32),
+        "wsg_handshake_validate_batch_host": ([p, P(HsConfig), p, p, p, u32, p, p], i32),
     }
     for name, (args, res) in sig.items():
         f = getattr(L, name)

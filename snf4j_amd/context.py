@@ -264,6 +264,32 @@ class Context:
                                                   resp.ctypes.data, res.ctypes.data), self._h)
         return resp[:n], res[:n]
 
+    def handshake_validate_device(self, cfg, resp, resp_off, keys, expected, result, n: int | None = None):
+        """Enqueue the client handshake over a device batch (wsg_handshake_validate_batch_device):
+        resp uint8, resp_off int64 (n + 1), keys uint8 (n * 24), expected uint8
+        (n * HS_EXPECTED_STRIDE), result uint8 byte view (n * 16), all cuda tensors."""
+        n = resp_off.numel() - 1 if n is None else int(n)
+        assert keys.numel() >= n * 24 and expected.numel() >= n * _lib.HS_EXPECTED_STRIDE and result.numel() >= n * 16
+        check(lib.wsg_handshake_validate_batch_device(self._h, C.byref(cfg), _p(resp), _p(resp_off), _p(keys), n,
+                                                      _p(expected), _p(result)), self._h)
+
+    def handshake_validate_host(self, cfg, resp: np.ndarray, resp_off: np.ndarray, keys: np.ndarray):
+        """The client handshake over a host batch (wsg_handshake_validate_batch_host).
+        Returns (expected [n, HS_EXPECTED_STRIDE] uint8, result HS_RESULT_DTYPE[n])."""
+        from ._lib import HS_RESULT_DTYPE
+        resp = np.ascontiguousarray(resp, dtype=np.uint8)
+        resp_off = np.ascontiguousarray(resp_off, dtype=np.uint64)
+        keys = np.ascontiguousarray(keys, dtype=np.uint8).reshape(-1)
+        n = len(resp_off) - 1
+        assert keys.size >= n * 24
+        exp = np.zeros((max(1, n), _lib.HS_EXPECTED_STRIDE), dtype=np.uint8)
+        res = np.zeros(max(1, n), dtype=HS_RESULT_DTYPE)
+        r = resp if resp.size else np.zeros(16, np.uint8)
+        k = keys if keys.size else np.zeros(24, np.uint8)
+        check(lib.wsg_handshake_validate_batch_host(self._h, C.byref(cfg), r.ctypes.data, resp_off.ctypes.data,
+                                                    k.ctypes.data, n, exp.ctypes.data, res.ctypes.data), self._h)
+        return exp[:n], res[:n]
+
     # -------------------------------------------------------------- aggregate
     def aggregate_device(self, max_aggregated_len: int, desc, session_first, dec_result, payload, state, agg_out,
                          out_desc, out_result, agg_total, n_frames: int | None = None):

@@ -16,7 +16,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast"};
+                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -137,7 +137,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_INFL_TOK && kid != K_INFL_FAST)) {
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST)) {
     f();
     return;
   }
@@ -1012,6 +1012,58 @@ int wsg_handshake_accept_batch_host(wsg_ctx* c, const wsg_hs_config* cfg, const 
                                              (uint8_t*)d_resp.p, (wsg_hs_result*)d_res.p);
   if (rc) return rc;
   HIP_TRY(c, hipMemcpyAsync(resp, d_resp.p, (uint64_t)n * WSG_HS_RESP_STRIDE, hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipMemcpyAsync(result, d_res.p, (uint64_t)n * sizeof(wsg_hs_result), hipMemcpyDeviceToHost, s));
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
+
+// ---- opening handshake (client side): validate the servers' responses ----
+
+int wsg_handshake_validate_batch_device(wsg_ctx* c, const wsg_hs_config* cfg, const uint8_t* resp,
+                                        const uint64_t* resp_off, const uint8_t* keys, uint32_t n,
+                                        uint8_t* expected_out, wsg_hs_result* result) {
+  if (!c || !cfg) return WSG_API_EINVAL;
+  if (!n) return WSG_API_OK;
+  if (!resp || !resp_off || !keys || !expected_out || !result) return set_err(c, WSG_API_EINVAL, "null batch pointer");
+  if (((uintptr_t)resp & 15) || ((uintptr_t)expected_out & 15))
+    return set_err(c, WSG_API_EINVAL, "resp and expected_out must be 16-B aligned");
+  HIP_TRY(c, hipSetDevice(c->device));
+  timed(c, K_HS_VALIDATE,
+        [&] { ws::launch_hs_validate(*cfg, resp, resp_off, keys, n, expected_out, result, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int wsg_handshake_validate_batch_host(wsg_ctx* c, const wsg_hs_config* cfg, const uint8_t* resp,
+                                      const uint64_t* resp_off, const uint8_t* keys, uint32_t n,
+                                      uint8_t* expected_out, wsg_hs_result* result) {
+  if (!c || !cfg) return WSG_API_EINVAL;
+  if (!n) return WSG_API_OK;
+  if (!resp_off || !keys || !expected_out || !result) return set_err(c, WSG_API_EINVAL, "null batch pointer");
+  for (uint32_t i = 0; i < n; ++i)
+    if (resp_off[i + 1] < resp_off[i]) return set_err(c, WSG_API_EINVAL, "resp_off not ascending at %u", i);
+  if (resp_off[0] != 0) return set_err(c, WSG_API_EINVAL, "resp_off[0] must be 0");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t len = resp_off[n];
+  DevBuf d_resp, d_off, d_keys, d_exp, d_res;
+  struct Guard {
+    DevBuf* b[5];
+    ~Guard() { for (DevBuf* x : b) x->release(); }
+  } g{{&d_resp, &d_off, &d_keys, &d_exp, &d_res}};
+  HIP_TRY(c, d_resp.ensure(len + 16));
+  HIP_TRY(c, d_off.ensure(((uint64_t)n + 1) * sizeof(uint64_t)));
+  HIP_TRY(c, d_keys.ensure((uint64_t)n * 24));
+  HIP_TRY(c, d_exp.ensure((uint64_t)n * WSG_HS_EXPECTED_STRIDE));
+  HIP_TRY(c, d_res.ensure((uint64_t)n * sizeof(wsg_hs_result)));
+  hipStream_t s = c->stream;
+  if (len) HIP_TRY(c, hipMemcpyAsync(d_resp.p, resp, len, hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(d_off.p, resp_off, ((uint64_t)n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(d_keys.p, keys, (uint64_t)n * 24, hipMemcpyHostToDevice, s));
+  int rc = wsg_handshake_validate_batch_device(c, cfg, (const uint8_t*)d_resp.p, (const uint64_t*)d_off.p,
+                                               (const uint8_t*)d_keys.p, n, (uint8_t*)d_exp.p,
+                                               (wsg_hs_result*)d_res.p);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemcpyAsync(expected_out, d_exp.p, (uint64_t)n * WSG_HS_EXPECTED_STRIDE, hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipMemcpyAsync(result, d_res.p, (uint64_t)n * sizeof(wsg_hs_result), hipMemcpyDeviceToHost, s));
   HIP_TRY(c, hipStreamSynchronize(s));
   return WSG_API_OK;

@@ -1,7 +1,10 @@
-// handshake.hip — the server side of the WebSocket opening handshake on gfx950:
-// HandshakeDecoder (HandshakeDecoder.java:141-235) + Handshaker.accept
-// (Handshaker.java:208-405) + the response format of HandshakeFactory.format
-// (HandshakeFactory.java:129-158), for a batch of requests, one lane per request.
+// handshake.hip — the WebSocket opening handshake on gfx950, one lane per session:
+//   server side (k_hs_accept): HandshakeDecoder (HandshakeDecoder.java:141-235) +
+//     Handshaker.accept (Handshaker.java:208-405) + the response format of
+//     HandshakeFactory.format (HandshakeFactory.java:129-158), for a batch of requests;
+//   client side (k_hs_validate): HandshakeDecoder in client mode (the response branch
+//     of HandshakeFactory.parse, HandshakeFactory.java:108-123) + Handshaker.validate
+//     (Handshaker.java:420-544), for a batch of responses and the keys the sessions sent.
 //
 // A request is a few hundred bytes of serial HTTP parsing, so the lane is the unit:
 // 64 requests per wave, each lane walking its own bytes (they stay in the L1/L2
@@ -162,8 +165,8 @@ __device__ __forceinline__ void sha1_block(uint32_t h[5], const uint32_t w0[16])
 // HandshakeUtils.java:98-111): 28 characters to the response.  Specialised on the key length,
 // so that every message byte's source (key byte, GUID constant, padding) is known at
 // compile time and the message words stay in registers.
-template <int KL, class O>
-__device__ __forceinline__ void accept_key_n(Req& d, int32_t kb, O& out) {
+template <int KL, class S, class O>
+__device__ __forceinline__ void accept_key_n(S& d, int32_t kb, O& out) {
   constexpr int total = KL + 36;  // <= 60: two blocks after padding
   uint32_t kw[(KL + 3) / 4];      // the key bytes, big-endian words
 #pragma unroll
@@ -635,7 +638,290 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k
   accept_one(d, (int64_t)(e - b), cfg, resp + (uint64_t)i * WSG_HS_RESP_STRIDE, result + i);
 }
 
+// ------------------------------------------------------------------ client side
+// Target fields of a response (upper-cased names, HandshakeFrame.key).
+enum CField : int { C_UPGRADE = 0, C_CONNECTION, C_ACCEPT, C_PROTOCOL, C_EXTENSIONS, C_COUNT };
+__device__ __constant__ char kCliNames[C_COUNT][25] = {"UPGRADE", "CONNECTION", "SEC-WEBSOCKET-ACCEPT",
+                                                       "SEC-WEBSOCKET-PROTOCOL", "SEC-WEBSOCKET-EXTENSIONS"};
+__device__ __constant__ uint8_t kCliLen[C_COUNT] = {7, 10, 20, 22, 24};
+
+// The 24 characters of the key a session sent, as six dwords in registers.
+struct KeyWords {
+  uint32_t w0, w1, w2, w3, w4, w5;
+  __device__ uint8_t operator[](int32_t i) const {
+    const int q = i >> 2;
+    const uint32_t w = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : q == 3 ? w3 : q == 4 ? w4 : w5;
+    return (uint8_t)(w >> (8 * (i & 3)));
+  }
+};
+
+// The expected Sec-WebSocket-Accept, gathered in registers (named words and selects:
+// an indexed member array went to scratch).
+struct KeySink {
+  uint32_t w0 = 0u, w1 = 0u, w2 = 0u, w3 = 0u, w4 = 0u, w5 = 0u, w6 = 0u;
+  int n = 0;
+  __device__ void byte(uint32_t c) {
+    const uint32_t v = c << (8 * (n & 3));
+    switch (n >> 2) {
+      case 0: w0 |= v; break;
+      case 1: w1 |= v; break;
+      case 2: w2 |= v; break;
+      case 3: w3 |= v; break;
+      case 4: w4 |= v; break;
+      case 5: w5 |= v; break;
+      default: w6 |= v; break;
+    }
+    ++n;
+  }
+  __device__ uint8_t at(int i) const {
+    const int q = i >> 2;
+    const uint32_t w = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : q == 3 ? w3 : q == 4 ? w4 : q == 5 ? w5 : w6;
+    return (uint8_t)(w >> (8 * (i & 3)));
+  }
+};
+
+__device__ __forceinline__ void validate_one(Req& d, int64_t n, const wsg_hs_config& cfg, const KeyWords& key,
+                                             uint8_t* expected, wsg_hs_result* res) {
+  wsg_hs_result r = {0u, 0, WSG_HS_NEED_MORE, WSG_HSC_NONE, 0, 0, 0u};
+  auto finish = [&](int kind, int cause, Span detail) {
+    r.kind = (uint8_t)kind;
+    r.cause = (uint8_t)cause;
+    if (detail.b >= 0) {
+      r.detail_off = (uint32_t)detail.b;
+      r.detail_len = (uint16_t)(detail.e - detail.b);
+    }
+    *res = r;
+  };
+  const Span none{-1, -1};
+  int capped = 0;
+  int64_t lines_end = 0;
+  const int flen = frame_len_t(d, n, &capped, &lines_end);
+  if (capped) {
+    finish(WSG_HS_DEFER, WSG_HSC_D_LINES, none);
+    return;
+  }
+  // no complete frame: the complete lines are decoded as a chunk (available0,
+  // HandshakeDecoder.java:212-224), so the length cap and the status line are judged now
+  const bool partial = flen == 0;
+  const int32_t limit = partial ? (int32_t)lines_end : flen;
+  if (partial && limit == 0) {
+    finish(WSG_HS_NEED_MORE, WSG_HSC_NONE, none);
+    return;
+  }
+  r.frame_len = (uint32_t)flen;
+  if ((uint32_t)limit > cfg.max_length) {  // :168-170; client mode throws (:192-193)
+    finish(WSG_HS_PARSE_ERROR, WSG_HSC_TOO_LARGE, none);
+    return;
+  }
+  Span fld[C_COUNT];
+  for (int f = 0; f < C_COUNT; ++f) fld[f] = none;
+  int status = 0;
+  {
+    int32_t line0 = 0;
+    uint8_t prev, curr = 0;
+    bool end = false;
+    int line_no = 0;
+    for (int32_t i = 0; i < limit; ++i) {
+      prev = curr;
+      curr = d[i];
+      if (curr != LF) {
+        if (curr != CR) end = false;
+        continue;
+      }
+      if (prev != CR) continue;
+      if (end) break;
+      end = true;
+      const int32_t lb = line0, le = i - 1;
+      line0 = i + 1;
+      if (line_no++ == 0) {
+        // HandshakeFactory.parse, response branch (:108-123): HttpUtils.splitResponseLine
+        // (= splitRequestLine, HttpUtils.java:138-176, out[10]) gives >= 3 tokens
+        Span tok0 = none, tok1 = none;
+        int count = 0;
+        int32_t t0 = lb;
+        uint8_t p2, c2 = 0;
+        bool over = false;
+        for (int32_t j = lb; j < le && !over; ++j) {
+          p2 = c2;
+          c2 = d[j];
+          if (c2 == SP) {
+            if (p2 != SP) {
+              const Span t{t0, j};
+              tok0 = count == 0 ? t : tok0;
+              tok1 = count == 1 ? t : tok1;
+              ++count;
+              if (count * 2 > 8) over = true;
+            }
+          } else if (p2 == SP) {
+            t0 = j;
+          }
+        }
+        if (!over) {
+          const Span t = (c2 == SP) ? Span{le, le} : Span{t0, le};
+          tok0 = count == 0 ? t : tok0;
+          tok1 = count == 1 ? t : tok1;
+          ++count;
+        }
+        if (count < 3) {
+          finish(WSG_HS_PARSE_ERROR, WSG_HSC_BAD_RESPONSE_LINE, none);
+          return;
+        }
+        if (!eq_exact(d, tok0, "HTTP/1.1", 8)) {
+          finish(WSG_HS_PARSE_ERROR, WSG_HSC_BAD_RESPONSE_VERSION, none);
+          return;
+        }
+        // HttpUtils.digits (:271-284) and STATUS_CODE_LENGTH (3)
+        bool digits = tok1.e - tok1.b == 3;
+        for (int32_t j = tok1.b; j < tok1.e && digits; ++j) {
+          const uint8_t c = d[j];
+          if (c < '0' || c > '9') digits = false;
+          else status = status * 10 + (c - '0');
+        }
+        if (!digits) {
+          finish(WSG_HS_PARSE_ERROR, WSG_HSC_BAD_RESPONSE_STATUS, none);
+          return;
+        }
+        r.http_status = (uint16_t)status;
+        if (partial) {
+          finish(WSG_HS_NEED_MORE, WSG_HSC_NONE, none);
+          return;
+        }
+        continue;
+      }
+      // header fields: the plain "name: value" form only, as on the server side
+      if (lb < le && (d[lb] == SP || d[lb] == HT)) {
+        finish(WSG_HS_DEFER, WSG_HSC_D_LINE_FORM, none);
+        return;
+      }
+      int32_t fs = -1;
+      for (int32_t j = lb; j < le; ++j)
+        if (d[j] == ':') {
+          fs = j;
+          break;
+        }
+      if (fs < 0) {
+        finish(WSG_HS_DEFER, WSG_HSC_D_LINE_FORM, none);
+        return;
+      }
+      int32_t vb = fs + 1;
+      while (vb < le && (d[vb] == SP || d[vb] == HT)) ++vb;
+      int32_t ve = le;
+      while (ve > vb && (d[ve - 1] == SP || d[ve - 1] == HT)) --ve;
+      const int nl = fs - lb;
+      int fi = -1;
+      for (int f = 0; f < C_COUNT && fi < 0; ++f) {
+        if (nl != kCliLen[f]) continue;
+        bool m = true;
+        for (int q = 0; q < nl && m; ++q) m = up(d[lb + q]) == (uint8_t)kCliNames[f][q];
+        if (m) fi = f;
+      }
+      if (fi >= 0) {
+        bool seen = false;
+#pragma unroll
+        for (int f = 0; f < C_COUNT; ++f)
+          if (f == fi) {
+            seen = fld[f].b >= 0;
+            if (!seen) fld[f] = Span{vb, ve};
+          }
+        if (seen) {
+          finish(WSG_HS_DEFER, WSG_HSC_D_REPEATED, none);
+          return;
+        }
+        if (!ascii(d, Span{vb, ve})) {
+          finish(WSG_HS_DEFER, WSG_HSC_D_NON_ASCII, none);
+          return;
+        }
+      }
+    }
+  }
+  // Handshaker.validate (:535-544)
+  if (status != 101) {
+    finish(WSG_HS_CLOSING, WSG_HSC_INVALID_STATUS, none);
+    return;
+  }
+  // validateBasicFields (:420-444)
+  if (fld[C_UPGRADE].b < 0) {
+    finish(WSG_HS_CLOSING, WSG_HSC_MISSING_UPGRADE, none);
+    return;
+  }
+  if (fld[C_CONNECTION].b < 0) {
+    finish(WSG_HS_CLOSING, WSG_HSC_MISSING_CONNECTION, none);
+    return;
+  }
+  if (!contains(d, fld[C_UPGRADE], "WEBSOCKET", 9)) {
+    finish(WSG_HS_CLOSING, WSG_HSC_INVALID_UPGRADE, fld[C_UPGRADE]);
+    return;
+  }
+  if (!contains(d, fld[C_CONNECTION], "UPGRADE", 7)) {
+    finish(WSG_HS_CLOSING, WSG_HSC_INVALID_CONNECTION, fld[C_CONNECTION]);
+    return;
+  }
+  // validateKeyChallenge (:446-460): HandshakeUtils.generateAnswerKey(key)
+  KeySink ex;
+  accept_key_n<24>(key, 0, ex);
+  reinterpret_cast<uint4*>(expected)[0] = make_uint4(ex.w0, ex.w1, ex.w2, ex.w3);
+  reinterpret_cast<uint4*>(expected)[1] = make_uint4(ex.w4, ex.w5, ex.w6, 0u);
+  r.resp_len = 28;
+  const Span act = fld[C_ACCEPT];
+  if (act.b < 0) {
+    finish(WSG_HS_CLOSING, WSG_HSC_MISSING_ACCEPT, none);
+    return;
+  }
+  bool same = act.e - act.b == 28;
+#pragma unroll
+  for (int i = 0; i < 28; ++i) same = same && d[act.b + (same ? i : 0)] == ex.at(i);
+  if (!same) {
+    finish(WSG_HS_CLOSING, WSG_HSC_INVALID_ACCEPT, act);
+    return;
+  }
+  // validateSubProtocol (:462-485): a match against the configured list is Java's
+  const Span pr = fld[C_PROTOCOL];
+  if (cfg.subprotocols) {
+    if (pr.b < 0) {
+      finish(WSG_HS_CLOSING, WSG_HSC_MISSING_SUBPROTOCOL, none);
+      return;
+    }
+    finish(WSG_HS_DEFER, WSG_HSC_D_SUBPROTOCOL, none);
+    return;
+  }
+  if (pr.b >= 0) {
+    finish(WSG_HS_CLOSING, WSG_HSC_INVALID_SUBPROTOCOL, pr);
+    return;
+  }
+  // validateExtensions (:487-533): IExtension.validateResponse is Java's
+  if (fld[C_EXTENSIONS].b >= 0) {
+    if (cfg.extensions) {
+      finish(WSG_HS_DEFER, WSG_HSC_D_EXTENSION, none);
+      return;
+    }
+    finish(WSG_HS_CLOSING, WSG_HSC_INVALID_EXTENSIONS, none);
+    return;
+  }
+  finish(WSG_HS_FINISHED, WSG_HSC_NONE, none);
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_hs_validate(
+    wsg_hs_config cfg, const uint8_t* resp, const uint64_t* resp_off, const uint8_t* keys, uint32_t n,
+    uint8_t* expected, wsg_hs_result* result) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t b = resp_off[i], e = resp_off[i + 1];
+  Req d;
+  d.base = reinterpret_cast<const uint4*>(resp + (b & ~(uint64_t)15));
+  d.lead = (uint32_t)(b & 15u);
+  const uint32_t* kp = reinterpret_cast<const uint32_t*>(keys + (uint64_t)i * 24u);
+  const KeyWords k{kp[0], kp[1], kp[2], kp[3], kp[4], kp[5]};
+  validate_one(d, (int64_t)(e - b), cfg, k, expected + (uint64_t)i * WSG_HS_EXPECTED_STRIDE, result + i);
+}
+
 }  // namespace
+
+void launch_hs_validate(const wsg_hs_config& cfg, const uint8_t* resp, const uint64_t* resp_off, const uint8_t* keys,
+                        uint32_t n, uint8_t* expected, wsg_hs_result* result, hipStream_t s) {
+  if (n)
+    hipLaunchKernelGGL(k_hs_validate, dim3((n + 255) / 256), dim3(256), 0, s, cfg, resp, resp_off, keys, n, expected,
+                       result);
+}
 
 void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64_t* req_off, uint32_t n,
                       uint8_t* resp, wsg_hs_result* result, hipStream_t s) {

@@ -211,7 +211,7 @@ struct InflTokStat {
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -243,6 +243,8 @@ uint64_t infl_tab_bytes();
 
 void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64_t* req_off, uint32_t n,
                       uint8_t* resp, wsg_hs_result* result, hipStream_t s);
+void launch_hs_validate(const wsg_hs_config& cfg, const uint8_t* resp, const uint64_t* resp_off, const uint8_t* keys,
+                        uint32_t n, uint8_t* expected, wsg_hs_result* result, hipStream_t s);
 __host__ __device__ int hs_frame_len(const uint8_t* d, int64_t len, int* capped, int64_t* lines_end);
 
 

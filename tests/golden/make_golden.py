@@ -622,8 +622,111 @@ def handshake_kats():
     return out
 
 
+def handshake_client_kats():
+    """Client-side handshake vectors: a response buffer, the key the session sent and
+    the combined outcome of HandshakeDecoder(clientMode) + Handshaker.handshake(response).
+    Transcribed from the reference's tests under snf4j-websocket/src/test/java/org/snf4j/
+    websocket/handshake/: HandshakeFactoryTest.testParse :80-99 (the response rows, and
+    the request rows parsed as responses), HandshakeDecoderTest.testDecode :113-120 and
+    testDecodeFailures :173-183, and HanshakerTest's client cases (response() :135-154
+    adds Upgrade, Connection, Sec-WebSocket-Accept, -Protocol, -Extensions in that order;
+    testValidateStatus :482-493, testValidateBasicFields :496-536, testValidateAnswerKey
+    :539-547, testValidateSubProtocol :550-589, testValidateExtensions :612-622 for the
+    configs without IExtension objects).  Key: the RFC 6455 sample the tests'
+    assertValidate answers with generateAnswerKey."""
+    src = "snf4j-websocket/src/test/java/org/snf4j/websocket/handshake/"
+    key, acc = "dGhlIHNhbXBsZSBub25jZQ==", "s3pPLMBiTxaQ9kYGzzhZRbK+xOo="
+
+    def pipe(s):
+        return s.replace("|", "\r\n").encode()
+
+    def case(where, resp, kind, cause, status=0, detail=None, subprotocol=None, **cfg):
+        return {"src": src + where, "kind": "validate", "response": hx(resp), "key": key, "cfg": cfg,
+                "expect": {"kind": kind, "status": status, "cause": cause, "detail": detail,
+                           "subprotocol": subprotocol}}
+    out = []
+    f = "HandshakeFactoryTest.java:"
+    # parsed responses; the Handshaker then judges them (no Upgrade field / not 101)
+    out.append(case(f + "91", pipe("HTTP/1.1 101 Switching Protocols|x: y||"), "closing", "MISSING_UPGRADE", 101))
+    out.append(case(f + "92", pipe("HTTP/1.1   102   Switching Protocols |x: y||"), "closing", "INVALID_STATUS", 102,
+                    "102"))
+    for row, s, cause in [("80", "GET /chat HTTP/1.1|xxx: yyy||", "BAD_RESPONSE_VERSION"),
+                          ("82", "GET /chat HTTP/1.1 |xxx: yyy||", "BAD_RESPONSE_VERSION"),
+                          ("85", "GET /chat|xxx: yyy||", "BAD_RESPONSE_LINE"),
+                          ("86", "GET /chat |xxx: yyy||", "BAD_RESPONSE_VERSION"),
+                          ("87", "GET|xxx: yyy||", "BAD_RESPONSE_LINE"),
+                          ("88", "GET |xxx: yyy||", "BAD_RESPONSE_LINE"),
+                          ("89", "|xxx: yyy||", "BAD_RESPONSE_LINE"),
+                          ("94", " HTTP/1.1 A01 Switching Protocols|x: y||", "BAD_RESPONSE_VERSION"),
+                          ("95", "HTTP/1.1 A01 Switching Protocols|x: y||", "BAD_RESPONSE_STATUS"),
+                          ("96", "HTTP/1.1 0A1 Switching Protocols|x: y||", "BAD_RESPONSE_STATUS"),
+                          ("97", "HTTP/1.1 10A Switching Protocols|x: y||", "BAD_RESPONSE_STATUS"),
+                          ("98", "HTTP/1.1 1010 Switching Protocols|x: y||", "BAD_RESPONSE_STATUS"),
+                          ("99", "HTTP/1.0 10A Switching Protocols|x: y||", "BAD_RESPONSE_VERSION")]:
+        out.append(case(f + row, pipe(s), "parse_error", cause))
+    d = "HandshakeDecoderTest.java:"
+    out.append(case(d + "113-120", pipe("HTTP/1.1 400 Bad Request||"), "closing", "INVALID_STATUS", 400, "400"))
+    out.append(case(d + "173-182", pipe("HTTP/1.3 400 Bad Request||"), "parse_error", "BAD_RESPONSE_VERSION"))
+
+    def resp(status=101, upper=None, upgrade=None, connection=None, accept=None, protocols=None, extensions=None):
+        def v(x):
+            return x if upper is None else (x.upper() if upper else x.lower())
+        fl = []
+        if upgrade != "no":
+            fl.append((v("Upgrade"), v(upgrade or "websocket")))
+        if connection != "no":
+            fl.append((v("Connection"), v(connection or "Upgrade")))
+        if accept != "no":
+            fl.append((v("Sec-WebSocket-Accept"), accept or acc))
+        if protocols is not None:
+            fl.append((v("Sec-WebSocket-Protocol"), protocols))
+        if extensions is not None:
+            fl.append((v("Sec-WebSocket-Extensions"), extensions))
+        b = b"HTTP/1.1 %03d X\r\n" % status       # HandshakeFactory.format (:141-157), reason "X"
+        for n, val in fl:
+            b += n.encode() + b": " + val.encode() + b"\r\n"
+        return b + b"\r\n"
+    h = "HanshakerTest.java:"
+    out.append(case(h + "482-493", resp(100), "closing", "INVALID_STATUS", 100, "100"))
+    for up in (None, True):
+        out.append(case(h + "497-500", resp(upper=up), "finished", "NONE", 101))
+    for u in ("websocket", "Websocket", "Websocket,xxx", "yyy, Websocket ", "yyy, websocket , xxx"):
+        out.append(case(h + "501-516", resp(upgrade=u), "finished", "NONE", 101))
+    out.append(case(h + "518-520", resp(upgrade="no"), "closing", "MISSING_UPGRADE", 101))
+    out.append(case(h + "521-523", resp(upgrade="xxx"), "closing", "INVALID_UPGRADE", 101, "xxx"))
+    out.append(case(h + "527-529", resp(connection="no"), "closing", "MISSING_CONNECTION", 101))
+    out.append(case(h + "530-532", resp(connection="xxx"), "closing", "INVALID_CONNECTION", 101, "xxx"))
+    out.append(case(h + "533-535", resp(connection="xxx,yyy, zzz"), "closing", "INVALID_CONNECTION", 101,
+                    "xxx,yyy, zzz"))
+    out.append(case(h + "540", resp(), "finished", "NONE", 101))
+    out.append(case(h + "541-542", resp(accept="no"), "closing", "MISSING_ACCEPT", 101))
+    out.append(case(h + "543-546", resp(accept="AAAA"), "closing", "INVALID_ACCEPT", 101, "AAAA"))
+    out.append(case(h + "553", resp(), "finished", "NONE", 101))
+    out.append(case(h + "554-556", resp(), "finished", "NONE", 101, subprotocols=[]))
+    out.append(case(h + "557-559", resp(protocols="proto1"), "closing", "INVALID_SUBPROTOCOL", 101, "proto1",
+                    subprotocols=[]))
+    p1, p12 = ["proto1"], ["proto1", "proto2"]
+    out.append(case(h + "563-564", resp(), "closing", "MISSING_SUBPROTOCOL", 101, subprotocols=p1))
+    out.append(case(h + "565-567", resp(protocols="proto1"), "finished", "NONE", 101, None, "proto1", subprotocols=p1))
+    out.append(case(h + "568-570", resp(protocols="proto2"), "closing", "INVALID_SUBPROTOCOL", 101, "proto2",
+                    subprotocols=p1))
+    out.append(case(h + "574-575", resp(), "closing", "MISSING_SUBPROTOCOL", 101, subprotocols=p12))
+    out.append(case(h + "576-578", resp(protocols="proto3"), "closing", "INVALID_SUBPROTOCOL", 101, "proto3",
+                    subprotocols=p12))
+    out.append(case(h + "579-581", resp(protocols="proto1, proto2"), "closing", "INVALID_SUBPROTOCOL", 101,
+                    "proto1, proto2", subprotocols=p12))
+    out.append(case(h + "582-584", resp(protocols="proto2"), "finished", "NONE", 101, None, "proto2",
+                    subprotocols=p12))
+    out.append(case(h + "585-587", resp(protocols=""), "closing", "INVALID_SUBPROTOCOL", 101, "", subprotocols=p12))
+    out.append(case(h + "616", resp(), "finished", "NONE", 101))
+    out.append(case(h + "617-619", resp(), "finished", "NONE", 101, extensions=False))
+    out.append(case(h + "620-622", resp(extensions="ext1; param1"), "closing", "INVALID_EXTENSIONS", 101))
+    return out
+
+
 def main():
     data = {
+        "handshake_client": handshake_client_kats(),
         "handshake": handshake_kats(),
         "deflate": deflate_kats(),
         "aggregator": aggregator_kats(),

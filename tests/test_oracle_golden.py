@@ -248,7 +248,7 @@ def test_deflate_kat(oracle):
             assert oracle.format_error(ei.value.err) == seq["error"], seq["src"]
 
 
-HS_KIND = {"need_more": 0, "defer": 1, "parse_error": 2, "accept": 3}
+HS_KIND = {"need_more": 0, "defer": 1, "parse_error": 2, "accept": 3, "finished": 4, "closing": 5}
 
 
 def _hs_cause(name):
@@ -287,3 +287,20 @@ def test_handshake_kat(idx):
         assert r["detail"] == e["detail"], (v, r)
         if "response" in e:
             assert r["response"] == fixtures.unhex(e["response"]), (v, r)
+
+
+@pytest.mark.parametrize("idx", range(len(fixtures.load("handshake_client"))))
+def test_handshake_client_kat(idx):
+    """The client-side restatement (response parse + Handshaker.validate) against the
+    HandshakeFactoryTest / HandshakeDecoderTest / HanshakerTest client vectors."""
+    from oracle import handshake_oracle as H
+    v = fixtures.load("handshake_client")[idx]
+    c = v["cfg"]
+    r = H.validate(fixtures.unhex(v["response"]), v["key"], c.get("max_length", 65536), c.get("subprotocols"),
+                   bool(c.get("extensions", False)))
+    e = v["expect"]
+    assert r["kind"] == HS_KIND[e["kind"]], (v, r)
+    assert r["status"] == e["status"] and r["cause"] == _hs_cause(e["cause"]), (v, r)
+    assert r["detail"] == e["detail"] and r["subprotocol"] == e["subprotocol"], (v, r)
+    if e["cause"] == "INVALID_ACCEPT":  # "... Expected: " + generateAnswerKey(key), ending in "="
+        assert r["expected"] == H.answer_key(v["key"]) and r["expected"].endswith("=")
