@@ -613,9 +613,9 @@ def gpu_defers_client(data: bytes, key: str, max_length=65536, subprotocols=None
                                                  C_INVALID_ACCEPT):
         return None
     _, f = parse_response(data[:flen], lines)
-    if subprotocols and f.get("Sec-WebSocket-Protocol") is not None:
-        return D_SUBPROTOCOL
-    if not subprotocols and f.get("Sec-WebSocket-Protocol") is not None:
+    if subprotocols:  # a missing answer closes; a present one is Java's list match
+        return D_SUBPROTOCOL if f.get("Sec-WebSocket-Protocol") is not None else None
+    if f.get("Sec-WebSocket-Protocol") is not None:
         return None
     if extensions and f.get("Sec-WebSocket-Extensions") is not None:
         return D_EXTENSION
