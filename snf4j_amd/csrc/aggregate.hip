@@ -74,40 +74,58 @@ __global__ __launch_bounds__(BLOCK) void k_agg_a(AggArgs a) {
 }
 
 // ------------------------------------------------------------------ k_agg_scan
-// One workgroup: exclusive scans of the block aggregates in place.  sums = 0:
-// the start / end maxima; sums = 1: member bytes and emitted frames (+ the total).
+// One workgroup: exclusive scans of the block aggregates in place, 4 consecutive
+// entries per thread (one pass up to 4096 blocks: a pass is a dependent load ->
+// block scan -> store round trip).  sums = 0: the start / end maxima; sums = 1:
+// member bytes and emitted frames (+ the totals).
 __global__ __launch_bounds__(1024) void k_agg_scan(AggArgs a, int sums) {
   Agg carry = AGG_ID;    // maxima (sums == 0) or member bytes (sums == 1)
   uint64_t carry_n = 0;  // emitted frames (sums == 1)
-  for (uint32_t base = 0; base < a.nblk; base += 1024) {
-    const uint32_t b = base + threadIdx.x;
-    Agg v = AGG_ID, tot;
-    if (sums) {
-      Agg n = AGG_ID, tn;
-      if (b < a.nblk) {
-        v.sum = a.blk_sum[b];
-        n.sum = a.blk_cnt[b];
+  for (uint32_t base = 0; base < a.nblk; base += 4096) {
+    const uint32_t b0 = base + threadIdx.x * 4;
+    Agg e[4], t = AGG_ID, tot;
+    uint64_t en[4], tn = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const bool in = b0 + i < a.nblk;
+      e[i] = AGG_ID;
+      en[i] = 0;
+      if (sums) {
+        if (in) {
+          e[i].sum = a.blk_sum[b0 + i];
+          en[i] = a.blk_cnt[b0 + i];
+        }
+        tn += en[i];
+      } else if (in) {
+        e[i].m0 = a.blk_max[b0 + i];
+        e[i].m1 = a.blk_max[a.nblk + b0 + i];
       }
-      const Agg ev = block_excl_scan(v, &tot);
-      const Agg en = block_excl_scan(n, &tn);
-      if (b < a.nblk) {
-        a.blk_sum[b] = carry.sum + ev.sum;
-        a.blk_cnt[b] = carry_n + en.sum;
-      }
-      carry.sum += tot.sum;
-      carry_n += tn.sum;
-    } else {
-      if (b < a.nblk) {
-        v.m0 = a.blk_max[b];
-        v.m1 = a.blk_max[a.nblk + b];
-      }
-      const Agg ex = agg_op(carry, block_excl_scan(v, &tot));
-      if (b < a.nblk) {
-        a.blk_max[b] = ex.m0;
-        a.blk_max[a.nblk + b] = ex.m1;
-      }
-      carry = agg_op(carry, tot);
+      t = agg_op(t, e[i]);
     }
+    // the emitted-frame counts ride in the m-fields' place: a second scan of sums
+    Agg ex = block_excl_scan(t, &tot);
+    Agg nv = AGG_ID, ntot;
+    nv.sum = tn;
+    Agg nex = AGG_ID;
+    if (sums) nex = block_excl_scan(nv, &ntot);
+    ex = agg_op(carry, ex);
+    uint64_t xn = carry_n + nex.sum;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      if (b0 + i < a.nblk) {
+        if (sums) {
+          a.blk_sum[b0 + i] = ex.sum;
+          a.blk_cnt[b0 + i] = xn;
+        } else {
+          a.blk_max[b0 + i] = ex.m0;
+          a.blk_max[a.nblk + b0 + i] = ex.m1;
+        }
+      }
+      ex = agg_op(ex, e[i]);
+      xn += en[i];
+    }
+    carry = agg_op(carry, tot);
+    if (sums) carry_n += ntot.sum;
   }
   if (sums && threadIdx.x == 0) {
     *a.agg_total = carry.sum;

@@ -152,3 +152,30 @@ def test_aggregate_truncated_sessions(ctx, oracle):
         assert exc is None and len(frames) == len(exp), s
         for g, o in zip(frames, exp):
             assert g.getPayload() == o.payload and int(g.getOpcode()) == o.opcode, s
+
+
+def test_aggregate_multi_pass_block_scan(ctx, oracle):
+    """More than 4096 blocks of 256 frames (1.1 M tiny frames), so k_agg_scan carries
+    its scans across passes: every session's output against the oracle."""
+    from snf4j_amd import BatchAggregator
+    rng = np.random.default_rng(4097)
+    n_s, per = 128, 8600
+    ops = rng.choice([0, 0, 1, 2, 9], size=(n_s, per))
+    fins = rng.random((n_s, per)) < 0.35
+    lens = rng.integers(0, 4, size=(n_s, per))
+    sessions = []
+    for s in range(n_s):
+        fr = []
+        for i in range(per):
+            op = int(ops[s, i])
+            fr.append((op, True if op >= 8 else bool(fins[s, i]), 0, bytes([i & 255]) * int(lens[s, i])))
+        sessions.append(fr)
+    desc, sf, res, payload = _batch(sessions)
+    assert len(desc) > 4096 * 256
+    out = BatchAggregator(n_s, 1 << 20, ctx=ctx).run(desc, sf, res, payload)
+    for s, (frames, exc) in enumerate(out):
+        agg = oracle.Aggregator(1 << 20)
+        exp = [f for f in (agg.decode(*fr) for fr in sessions[s]) if f is not None]
+        assert exc is None and len(frames) == len(exp), s
+        for g, o in zip(frames, exp):
+            assert g.getPayload() == o.payload and int(g.getOpcode()) == o.opcode, s
