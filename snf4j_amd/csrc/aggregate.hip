@@ -14,7 +14,8 @@
 // its message before k (+ the bytes carried in) + its own length > max.
 //
 //   k_agg_a      thread per frame: class bits, block maxima of start / end indices
-//   k_agg_scan   one workgroup: exclusive scans of the block aggregates
+//   k_agg_scan   one workgroup: exclusive scans of the block aggregates (the maxima
+//                only above 4096 blocks: below, k_agg_b folds them itself)
 //   k_agg_b      thread per frame: open-before-k, membership, emit flag; block sums
 //                of member bytes and emitted frames
 //   k_agg_c      thread per frame: "too big" test, output descriptors, gather
@@ -145,8 +146,25 @@ __global__ __launch_bounds__(BLOCK) void k_agg_b(AggArgs a) {
   Agg ex = block_excl_scan(v, &tot);
   Agg w = AGG_ID;
   uint64_t emit = 0;  // emitted frame (bit 0) | non-empty member (bit 32)
+  // the start / end maxima of every frame before this block: up to 4096 blocks the
+  // block folds k_agg_a's block maxima itself (coalesced; max commutes), so the
+  // first k_agg_scan launch is skipped; beyond, k_agg_scan left the exclusive maxima
+  int32_t bs, be;
+  if (a.nblk <= FUSED_SCAN_MAX_BLOCKS) {
+    Agg f = AGG_ID, ft;
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += BLOCK) {
+      const int32_t x0 = a.blk_max[b], x1 = a.blk_max[a.nblk + b];
+      f.m0 = x0 > f.m0 ? x0 : f.m0;
+      f.m1 = x1 > f.m1 ? x1 : f.m1;
+    }
+    block_excl_scan(f, &ft);
+    bs = ft.m0;
+    be = ft.m1;
+  } else {
+    bs = a.blk_max[blockIdx.x];
+    be = a.blk_max[a.nblk + blockIdx.x];
+  }
   if (live) {
-    const int32_t bs = a.blk_max[blockIdx.x], be = a.blk_max[a.nblk + blockIdx.x];
     const int32_t ls = ex.m0 > bs ? ex.m0 : bs, le = ex.m1 > be ? ex.m1 : be;
     a.last[k] = ls;
     a.last[a.n_frames + k] = le;
@@ -573,7 +591,7 @@ __global__ __launch_bounds__(256) void k_agg_final(AggArgs a) {
 void launch_agg_plan(const AggArgs& a, hipStream_t s) {
   if (!a.n_frames) return;
   hipLaunchKernelGGL(k_agg_a, dim3(a.nblk), dim3(BLOCK), 0, s, a);
-  hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 0);
+  if (a.nblk > FUSED_SCAN_MAX_BLOCKS) hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 0);
   hipLaunchKernelGGL(k_agg_b, dim3(a.nblk), dim3(BLOCK), 0, s, a);
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 1);
   hipLaunchKernelGGL(k_agg_c, dim3(a.nblk), dim3(BLOCK), 0, s, a);
