@@ -51,7 +51,7 @@ __global__ __launch_bounds__(BLOCK) void k_agg_a(AggArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
   Agg v = AGG_ID;
   if (k < a.n_frames) {
-    const uint32_t s = find_session(a.session_first, a.n_sessions, k);
+    const uint32_t s = wave_find_session(a.session_first, a.n_sessions, a.n_frames, k);
     const bool valid = k - a.session_first[s] < a.dec_result[s].n_delivered;
     uint32_t c = 0;
     if (valid) {

@@ -131,16 +131,8 @@ __device__ __forceinline__ void store_blk(const DecodeArgs& a, uint32_t b, const
   a.blk_max[3 * a.nblk + b] = (int32_t)e.c3;
 }
 
-// Session of frame k: two wave-uniform searches (scalar loads) bound the sessions
-// of the wave's 64 frames, and a lane searches only inside those bounds — not at
-// all when the wave's frames belong to one session.
 __device__ __forceinline__ uint32_t wave_session(const DecodeArgs& a, uint64_t k) {
-  const uint32_t kw = __builtin_amdgcn_readfirstlane((uint32_t)(k & ~63ull));  // (frame indices < 2^30)
-  const uint64_t kl = kw + 63u < a.n_frames ? kw + 63u : a.n_frames - 1;
-  const uint32_t s_lo = find_session(a.session_first, a.n_sessions, kw);
-  if (s_lo + 1 >= a.n_sessions || a.session_first[s_lo + 1] > kl) return s_lo;  // one session
-  const uint32_t s_hi = find_session_in(a.session_first, s_lo + 1, a.n_sessions - 1, kl);
-  return find_session_in(a.session_first, s_lo, s_hi, k);
+  return wave_find_session(a.session_first, a.n_sessions, a.n_frames, k);
 }
 
 // ------------------------------------------------------------------ k_parse

@@ -26,7 +26,7 @@ __global__ __launch_bounds__(BLOCK) void k_enc_len(EncodeArgs a) {
   Agg v = AGG_ID;
   if (k < a.n_frames) {
     const wsg_encode_frame f = a.frames[k];
-    const uint32_t s = find_session(a.session_first, a.n_sessions, k);
+    const uint32_t s = wave_find_session(a.session_first, a.n_sessions, a.n_frames, k);
     a.sess[k] = s;
     v.sum = (uint64_t)enc_header_len(f.payload_len, a.client_mode) + f.payload_len;
     v.m0 = (f.opcode & 15u) == WSG_OP_CLOSE ? (int32_t)k : -1;

@@ -96,6 +96,19 @@ __device__ __forceinline__ uint32_t find_session(const uint32_t* sf, uint32_t n_
   return lo;
 }
 
+// Session of frame k when a wave's 64 lanes take frames k & ~63 .. +63: two
+// wave-uniform searches (scalar loads) bound the sessions of the wave's frames, and
+// a lane searches only inside those bounds — not at all when they share a session.
+__device__ __forceinline__ uint32_t wave_find_session(const uint32_t* sf, uint32_t n_sessions, uint64_t n_frames,
+                                                      uint64_t k) {
+  const uint32_t kw = __builtin_amdgcn_readfirstlane((uint32_t)(k & ~63ull));  // (frame indices < 2^30)
+  const uint64_t kl = kw + 63u < n_frames ? kw + 63u : n_frames - 1;
+  const uint32_t s_lo = find_session(sf, n_sessions, kw);
+  if (s_lo + 1 >= n_sessions || sf[s_lo + 1] > kl) return s_lo;  // one session
+  const uint32_t s_hi = find_session_in(sf, s_lo + 1, n_sessions - 1, kl);
+  return find_session_in(sf, s_lo, s_hi, k);
+}
+
 // Workgroups are dealt round-robin to the 8 XCDs (blocks b and b+8 share one);
 // give each XCD a contiguous run of pieces so the source lines two neighbouring
 // pieces share (funnel block, UTF-8 carry word) meet in the same L2.  Bijective
