@@ -117,6 +117,18 @@ final class Wsg {
 	static native int validateBatchHost(long ctx, ByteBuffer desc, long nFrames, ByteBuffer sessionFirst,
 			int nSessions, ByteBuffer payload, long payloadLen, ByteBuffer state, ByteBuffer result);
 
+	/* ---- opening handshake: wsg_handshake_available / wsg_handshake_accept_batch_host /
+	 * wsg_handshake_validate_batch_host (the GpuHandshakeDecoder stages of INTEGRATION.md
+	 * 1.3d-e).  config = {maxLength, ignoreHost, subprotocols, extensions, hostPolicy}
+	 * as wsg_hs_config; results are 16-byte wsg_hs_result records. ---- */
+	static native int handshakeAvailable(byte[] b, int off, int len);
+
+	static native int handshakeAcceptBatchHost(long ctx, int[] config, ByteBuffer req, ByteBuffer reqOff, int n,
+			ByteBuffer resp, ByteBuffer result);
+
+	static native int handshakeValidateBatchHost(long ctx, int[] config, ByteBuffer resp, ByteBuffer respOff,
+			ByteBuffer keys, int n, ByteBuffer expected, ByteBuffer result);
+
 	/* ---- pinned host pool: wsg_host_alloc / wsg_host_release ---- */
 	static native ByteBuffer allocPinned(int capacity);
 

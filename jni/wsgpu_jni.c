@@ -179,6 +179,49 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_validateBatchHost(
                                    (wsg_session_result*)addr(env, result));
 }
 
+/* ---- opening handshake (HandshakeDecoder + Handshaker, server and client side) ---- */
+static int hs_config(JNIEnv* env, jintArray a, wsg_hs_config* c) {
+    jint v[5] = {65536, 0, 0, 0, 0};
+    if (a) {
+        jsize n = (*env)->GetArrayLength(env, a);
+        (*env)->GetIntArrayRegion(env, a, 0, n < 5 ? n : 5, v);
+    }
+    memset(c, 0, sizeof *c);
+    c->max_length = (uint32_t)v[0];
+    c->ignore_host = v[1] ? 1 : 0;
+    c->subprotocols = v[2] ? 1 : 0;
+    c->extensions = v[3] ? 1 : 0;
+    c->host_policy = v[4] ? 1 : 0;
+    return 0;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_handshakeAvailable(JNIEnv* env, jclass c, jbyteArray b,
+                                                                           jint off, jint len) {
+    uint8_t buf[8192];
+    if (len < 0 || len > (jint)sizeof buf) return -1;  /* larger frames go to the Java HandshakeDecoder */
+    (*env)->GetByteArrayRegion(env, b, off, len, (jbyte*)buf);
+    return wsg_handshake_available(buf, (uint64_t)len);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_handshakeAcceptBatchHost(
+        JNIEnv* env, jclass c, jlong ctx, jintArray config, jobject req, jobject req_off, jint n, jobject resp,
+        jobject result) {
+    wsg_hs_config cfg;
+    hs_config(env, config, &cfg);
+    return wsg_handshake_accept_batch_host(CTX(ctx), &cfg, addr(env, req), (const uint64_t*)addr(env, req_off),
+                                           (uint32_t)n, addr(env, resp), (wsg_hs_result*)addr(env, result));
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_handshakeValidateBatchHost(
+        JNIEnv* env, jclass c, jlong ctx, jintArray config, jobject resp, jobject resp_off, jobject keys, jint n,
+        jobject expected, jobject result) {
+    wsg_hs_config cfg;
+    hs_config(env, config, &cfg);
+    return wsg_handshake_validate_batch_host(CTX(ctx), &cfg, addr(env, resp), (const uint64_t*)addr(env, resp_off),
+                                             addr(env, keys), (uint32_t)n, addr(env, expected),
+                                             (wsg_hs_result*)addr(env, result));
+}
+
 /* ---- pinned host pool (IByteBufferAllocator.allocate / release) ---- */
 JNIEXPORT jobject JNICALL Java_org_snf4j_websocket_gpu_Wsg_allocPinned(JNIEnv* env, jclass c, jint capacity) {
     void* p = wsg_host_alloc((uint64_t)capacity);
