@@ -262,14 +262,15 @@ __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
       const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
       const uint32_t len = d.payload_len;
       const uint64_t src = d.payload_off;
-      uint32_t f3 = 0, l3 = 0;
+      uint32_t l3 = 0;
       if (op <= WSG_OP_TEXT && len) {  // fragment-boundary bytes for the UTF-8 carry (as k_parse)
         const uint32_t nf = len < 3 ? len : 3;
         const uint32_t keep = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : 0xffu);
-        f3 = plain_word(a, src) & keep;
+        // a frame's first bytes matter only at a continuation's seam (k_link); a message
+        // start is validated whole by the piece kernel: no scattered line per TEXT frame
+        if (op == WSG_OP_CONTINUATION) a.edge[k] = plain_word(a, src) & keep;
         if (!fin) l3 = (plain_word(a, src + len - nf) & keep) << (8 * (3 - nf));  // newest in bits 16-23
       }
-      a.edge[k] = f3;
       a.edge[a.n_frames + k] = l3;
       FrameRec r;
       r.src = src;
