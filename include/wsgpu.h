@@ -561,7 +561,8 @@ int wsg_handshake_accept_batch_host(wsg_ctx* ctx, const wsg_hs_config* cfg, cons
  *     (HandshakeFactory.parse, response branch            HandshakeFactory.java:108-123)
  *   Handshaker.handshake(response) -> validate            Handshaker.java:420-544, 555-566
  *     (validateBasicFields / validateKeyChallenge / validateSubProtocol / validateExtensions)
- * Response i is resp[resp_off[i], resp_off[i+1]) (the bytes the session has received);
+ * Response i is resp[resp_off[i], resp_off[i+1]) (the bytes the session has received;
+ * resp and expected_out 16-B aligned, keys 4-B aligned);
  * keys[24 i, +24) is the Sec-WebSocket-Key the session sent (HandshakeUtils.generateKey:
  * Base64 of 16 bytes).  result[i].kind is NEED_MORE, DEFER, PARSE_ERROR (the exception
  * HandshakeDecoder throws in client mode: no response is written), FINISHED or CLOSING

@@ -1025,8 +1025,8 @@ int wsg_handshake_validate_batch_device(wsg_ctx* c, const wsg_hs_config* cfg, co
   if (!c || !cfg) return WSG_API_EINVAL;
   if (!n) return WSG_API_OK;
   if (!resp || !resp_off || !keys || !expected_out || !result) return set_err(c, WSG_API_EINVAL, "null batch pointer");
-  if (((uintptr_t)resp & 15) || ((uintptr_t)expected_out & 15))
-    return set_err(c, WSG_API_EINVAL, "resp and expected_out must be 16-B aligned");
+  if (((uintptr_t)resp & 15) || ((uintptr_t)expected_out & 15) || ((uintptr_t)keys & 3))
+    return set_err(c, WSG_API_EINVAL, "resp and expected_out must be 16-B aligned, keys 4-B aligned");
   HIP_TRY(c, hipSetDevice(c->device));
   timed(c, K_HS_VALIDATE,
         [&] { ws::launch_hs_validate(*cfg, resp, resp_off, keys, n, expected_out, result, c->stream); });
