@@ -2347,9 +2347,23 @@ __global__ __launch_bounds__(1024) void k_ord_scan(InflArgs a) {
   }
 }
 
+// One frame a thread: ranks within the block's bucket from LDS counters, then one
+// global atomic per (block, bucket) reserves the block's run of each bucket.  (A
+// global atomic per frame serialised on the few buckets similar messages share:
+// 342 us for 131 K frames.)
 __global__ __launch_bounds__(256) void k_ord_scatter(InflArgs a) {
-  for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k < a.n_frames; k += (uint64_t)gridDim.x * 256)
-    a.order[atomicAdd(&a.ord_cnt[ord_bucket(a.desc[k].payload_len)], 1u)] = (uint32_t)k;
+  __shared__ uint32_t cnt[ORD_BUCKETS];
+  for (uint32_t i = threadIdx.x; i < ORD_BUCKETS; i += 256) cnt[i] = 0;
+  __syncthreads();
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  const bool live = k < a.n_frames;
+  const uint32_t b = live ? ord_bucket(a.desc[k].payload_len) : 0u;
+  const uint32_t r = live ? atomicAdd(&cnt[b], 1u) : 0u;
+  __syncthreads();
+  // the first frame of each bucket in the block reserves the bucket's run
+  if (live && r == 0) cnt[b] = atomicAdd(&a.ord_cnt[b], cnt[b]);
+  __syncthreads();
+  if (live) a.order[cnt[b] + r] = (uint32_t)k;
 }
 
 }  // namespace
@@ -2365,7 +2379,7 @@ void launch_infl_tok(const InflArgs& a, hipStream_t s) {
     (void)hipMemsetAsync(a.ord_cnt, 0, ORD_BUCKETS * sizeof(uint32_t), s);  // errors show at the launch check
     hipLaunchKernelGGL(k_ord_hist, dim3(g), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_ord_scan, dim3(1), dim3(1024), 0, s, a);
-    hipLaunchKernelGGL(k_ord_scatter, dim3(g), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_ord_scatter, dim3((uint32_t)((a.n_frames + 255) / 256)), dim3(256), 0, s, a);
   }
   hipLaunchKernelGGL(k_infl_tok, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
 }
