@@ -2261,11 +2261,24 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
     // a dword of slots a thread, 8 dwords (32 byte loads) in flight; slots whose position
     // is before lo keep the old image's byte
     uint32_t* const wout32 = reinterpret_cast<uint32_t*>(wout);
+    const uint32_t mis = (uint32_t)((uintptr_t)out & 3u);  // the output's offset from a dword boundary
     for (uint32_t w0 = 0; w0 < WSG_INFLATE_WINDOW / 4; w0 += 8 * FNT) {
       uint32_t v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const uint32_t w = w0 + (uint32_t)FNT * u + (uint32_t)lane;
+        // a slot dword whose 4 positions are consecutive output bytes (not across the
+        // ring's end, none before lo): two aligned dword loads and a funnel, not 4 byte loads
+        const uint32_t i0 = (4u * w - nph) & WMASK;
+        const int32_t q0 = P - (int32_t)WSG_INFLATE_WINDOW + (int32_t)i0;
+        const uint32_t sh = (uint32_t)(q0 + (int32_t)mis) & 3u;
+        if (i0 <= WMASK - 3u && q0 >= lo && q0 >= (int32_t)sh) {
+          const int32_t qa = q0 - (int32_t)sh;  // out + qa is dword-aligned
+          const uint32_t l = (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rout, (uint32_t)qa, 0, 1);
+          const uint32_t h = sh ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b32(rout, (uint32_t)qa + 4u, 0, 1) : 0u;
+          v[u] = __builtin_amdgcn_alignbyte(h, l, sh);
+          continue;
+        }
         uint32_t x = 0;
         bool all = true;
 #pragma unroll
