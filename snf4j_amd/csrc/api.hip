@@ -290,7 +290,7 @@ static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, 
   HIP_TRY(c, c->slink.ensure(3 * (uint64_t)(n_sessions ? n_sessions : 1) * sizeof(int32_t)));
   HIP_TRY(c, c->edge.ensure(2 * F * sizeof(uint32_t)));
   HIP_TRY(c, c->blk_sum.ensure(nblk * sizeof(uint64_t)));
-  HIP_TRY(c, c->blk_max.ensure(4 * nblk * sizeof(int32_t)));
+  HIP_TRY(c, c->blk_max.ensure(4 * ((nblk + 3) & ~3ull) * sizeof(int32_t)));  // rows 16-B aligned (decode.hip blk_stride)
   HIP_TRY(c, c->chunk.ensure((nblk / SCAN_CHUNK + 1) * (sizeof(uint64_t) + 4 * sizeof(int32_t))));
   HIP_TRY(c, c->sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t), 0xff, c->stream));
   HIP_TRY(c, c->total.ensure(sizeof(uint64_t)));

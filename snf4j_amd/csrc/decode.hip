@@ -114,21 +114,27 @@ __device__ __forceinline__ DAgg frame_agg(uint64_t k, const FrameRec& r, uint32_
   return v;
 }
 
+// Block aggregates: blk_sum[b], and the maxima / carry in four rows of blk_max
+// whose stride is nblk rounded up to 4, so that every row is 16-B aligned (k_link
+// folds them with 16-B loads).
+__device__ __forceinline__ uint32_t blk_stride(const DecodeArgs& a) { return (a.nblk + 3u) & ~3u; }
 __device__ __forceinline__ DAgg load_blk(const DecodeArgs& a, uint32_t b) {
+  const uint32_t st = blk_stride(a);
   DAgg e;
   e.sum = a.blk_sum[b];
   e.m0 = a.blk_max[b];
-  e.m1 = a.blk_max[a.nblk + b];
-  e.m2 = a.blk_max[2 * a.nblk + b];
-  e.c3 = (uint32_t)a.blk_max[3 * a.nblk + b];
+  e.m1 = a.blk_max[st + b];
+  e.m2 = a.blk_max[2 * st + b];
+  e.c3 = (uint32_t)a.blk_max[3 * st + b];
   return e;
 }
 __device__ __forceinline__ void store_blk(const DecodeArgs& a, uint32_t b, const DAgg& e) {
+  const uint32_t st = blk_stride(a);
   a.blk_sum[b] = e.sum;
   a.blk_max[b] = e.m0;
-  a.blk_max[a.nblk + b] = e.m1;
-  a.blk_max[2 * a.nblk + b] = e.m2;
-  a.blk_max[3 * a.nblk + b] = (int32_t)e.c3;
+  a.blk_max[st + b] = e.m1;
+  a.blk_max[2 * st + b] = e.m2;
+  a.blk_max[3 * st + b] = (int32_t)e.c3;
 }
 
 __device__ __forceinline__ uint32_t wave_session(const DecodeArgs& a, uint64_t k) {
@@ -354,13 +360,34 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
   if (a.fused_scan) {
     __shared__ uint32_t c3s[FUSED_SCAN_MAX_BLOCKS];
     DAgg t = DAGG_ID;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += DBLOCK) {
-      const DAgg e = load_blk(a, b);
-      t.sum += e.sum;
-      t.m0 = t.m0 > e.m0 ? t.m0 : e.m0;
-      t.m1 = t.m1 > e.m1 ? t.m1 : e.m1;
-      t.m2 = t.m2 > e.m2 ? t.m2 : e.m2;
-      c3s[b] = e.c3;
+    // four consecutive blocks a thread: 16-B loads of each row (6 loads per 4 blocks)
+    const uint32_t nb = blockIdx.x, st = blk_stride(a);
+    for (uint32_t b = threadIdx.x * 4u; b < nb; b += DBLOCK * 4u) {
+      if (b + 4u <= nb) {
+        const int4 x0 = *reinterpret_cast<const int4*>(a.blk_max + b);
+        const int4 x1 = *reinterpret_cast<const int4*>(a.blk_max + st + b);
+        const int4 x2 = *reinterpret_cast<const int4*>(a.blk_max + 2 * st + b);
+        const int4 x3 = *reinterpret_cast<const int4*>(a.blk_max + 3 * st + b);
+        const ulonglong2 s0 = *reinterpret_cast<const ulonglong2*>(a.blk_sum + b);
+        const ulonglong2 s1 = *reinterpret_cast<const ulonglong2*>(a.blk_sum + b + 2);
+        t.sum += s0.x + s0.y + s1.x + s1.y;
+        t.m0 = max(max(t.m0, max(x0.x, x0.y)), max(x0.z, x0.w));
+        t.m1 = max(max(t.m1, max(x1.x, x1.y)), max(x1.z, x1.w));
+        t.m2 = max(max(t.m2, max(x2.x, x2.y)), max(x2.z, x2.w));
+        c3s[b] = (uint32_t)x3.x;
+        c3s[b + 1] = (uint32_t)x3.y;
+        c3s[b + 2] = (uint32_t)x3.z;
+        c3s[b + 3] = (uint32_t)x3.w;
+      } else {
+        for (uint32_t i = b; i < nb; ++i) {
+          const DAgg e = load_blk(a, i);
+          t.sum += e.sum;
+          t.m0 = t.m0 > e.m0 ? t.m0 : e.m0;
+          t.m1 = t.m1 > e.m1 ? t.m1 : e.m1;
+          t.m2 = t.m2 > e.m2 ? t.m2 : e.m2;
+          c3s[i] = e.c3;
+        }
+      }
     }
     __syncthreads();
     const uint32_t per = (blockIdx.x + DBLOCK - 1) / DBLOCK;
