@@ -77,13 +77,14 @@ __device__ __forceinline__ DAgg agg_op(const DAgg& x, const DAgg& y) {
   r.c3 = carry_op(x.c3, y.c3);
   return r;
 }
-__device__ __forceinline__ DAgg agg_shfl_up(const DAgg& v, int d) {
+template <int CTRL, int RM>
+__device__ __forceinline__ DAgg agg_dpp(const DAgg& v) {
   DAgg t;
-  t.sum = shfl_up_u64(v.sum, d);
-  t.m0 = __shfl_up(v.m0, d, 64);
-  t.m1 = __shfl_up(v.m1, d, 64);
-  t.m2 = __shfl_up(v.m2, d, 64);
-  t.c3 = (uint32_t)__shfl_up((int)v.c3, d, 64);
+  t.sum = dpp_u64<CTRL, RM>(v.sum, 0ull);
+  t.m0 = (int32_t)dpp_u32<CTRL, RM>((uint32_t)v.m0, 0xffffffffu);
+  t.m1 = (int32_t)dpp_u32<CTRL, RM>((uint32_t)v.m1, 0xffffffffu);
+  t.m2 = (int32_t)dpp_u32<CTRL, RM>((uint32_t)v.m2, 0xffffffffu);
+  t.c3 = dpp_u32<CTRL, RM>(v.c3, 0u);  // (carry_op(0, y) == y: DAGG_ID.c3)
   return t;
 }
 

@@ -30,27 +30,46 @@ __device__ __forceinline__ Agg agg_op(const Agg& x, const Agg& y) {
   return r;
 }
 
-__device__ __forceinline__ Agg agg_shfl_up(const Agg& v, int d) {
+// DPP move of a dword across the wave: lanes without a source (row_shr past the
+// start of their row of 16, rows outside RM, lane 0 of wave_shr) keep `id`.
+template <int CTRL, int RM>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t v, uint32_t id) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)id, (int)v, CTRL, RM, 0xf, false);
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ uint64_t dpp_u64(uint64_t v, uint64_t id) {
+  return ((uint64_t)dpp_u32<CTRL, RM>((uint32_t)(v >> 32), (uint32_t)(id >> 32)) << 32) |
+         dpp_u32<CTRL, RM>((uint32_t)v, (uint32_t)id);
+}
+constexpr int DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118;
+constexpr int DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143, DPP_WAVE_SHR1 = 0x138;
+
+// the element of the lane the DPP control names, the identity where there is none
+template <int CTRL, int RM>
+__device__ __forceinline__ Agg agg_dpp(const Agg& v) {
   Agg t;
-  t.sum = shfl_up_u64(v.sum, d);
-  t.m0 = __shfl_up(v.m0, d, 64);
-  t.m1 = __shfl_up(v.m1, d, 64);
-  t.m2 = __shfl_up(v.m2, d, 64);
+  t.sum = dpp_u64<CTRL, RM>(v.sum, 0ull);
+  t.m0 = (int32_t)dpp_u32<CTRL, RM>((uint32_t)v.m0, 0xffffffffu);
+  t.m1 = (int32_t)dpp_u32<CTRL, RM>((uint32_t)v.m1, 0xffffffffu);
+  t.m2 = (int32_t)dpp_u32<CTRL, RM>((uint32_t)v.m2, 0xffffffffu);
   return t;
 }
 
 constexpr Agg AGG_ID = {0ull, -1, -1, -1};
 
 // Scans over any element type T with agg_op(T, T) (associative, applied in frame
-// order: it need not commute) and agg_shfl_up(T, d).
+// order: it need not commute) and agg_dpp<CTRL, RM>(T) (identity where no source).
+// The wave scan is DPP moves (VALU, no LDS round trip a step): Hillis-Steele inside
+// each row of 16 lanes (row_shr 1, 2, 4, 8), then row 0's total into row 1 and row
+// 2's into row 3 (row_bcast:15), then rows 0-1's total into rows 2-3 (row_bcast:31).
 template <class T>
 __device__ __forceinline__ T wave_incl_scan(T v) {
-  const int lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const T t = agg_shfl_up(v, d);
-    if (lane >= d) v = agg_op(t, v);
-  }
+  v = agg_op(agg_dpp<DPP_ROW_SHR1, 0xf>(v), v);
+  v = agg_op(agg_dpp<DPP_ROW_SHR2, 0xf>(v), v);
+  v = agg_op(agg_dpp<DPP_ROW_SHR4, 0xf>(v), v);
+  v = agg_op(agg_dpp<DPP_ROW_SHR8, 0xf>(v), v);
+  v = agg_op(agg_dpp<DPP_ROW_BCAST15, 0xa>(v), v);
+  v = agg_op(agg_dpp<DPP_ROW_BCAST31, 0xc>(v), v);
   return v;
 }
 
@@ -68,8 +87,8 @@ __device__ inline T block_excl_scan_t(T v, T* total, const T id) {
     tot = agg_op(tot, wsum[i]);
   }
   __syncthreads();
-  // exclusive within the wave: inclusive of lane-1
-  T ex = agg_shfl_up(inc, 1);
+  // exclusive within the wave: inclusive of lane-1 (lane 0: the identity)
+  T ex = agg_dpp<DPP_WAVE_SHR1, 0xf>(inc);
   if (lane == 0) ex = id;
   *total = tot;
   return agg_op(pre, ex);
