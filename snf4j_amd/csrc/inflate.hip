@@ -2015,12 +2015,13 @@ constexpr int FNT = 256;  // threads per session (4 waves)
 // block-wide exclusive sum of a packed (hi, lo) pair of 32-bit counts; the totals
 __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, uint64_t* wsum) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint64_t inc = v;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t t = shfl_up_u64(inc, d);
-    if (lane >= d) inc += t;
-  }
+  uint64_t inc = v;  // wave scan by DPP row operations (wsgpu_scan.h wave_incl_scan)
+  inc += dpp_u64<DPP_ROW_SHR1, 0xf>(inc, 0ull);
+  inc += dpp_u64<DPP_ROW_SHR2, 0xf>(inc, 0ull);
+  inc += dpp_u64<DPP_ROW_SHR4, 0xf>(inc, 0ull);
+  inc += dpp_u64<DPP_ROW_SHR8, 0xf>(inc, 0ull);
+  inc += dpp_u64<DPP_ROW_BCAST15, 0xa>(inc, 0ull);
+  inc += dpp_u64<DPP_ROW_BCAST31, 0xc>(inc, 0ull);
   if (lane == 63) wsum[wid] = inc;
   __syncthreads();
   uint64_t pre = 0, tot = 0;
