@@ -277,12 +277,8 @@ __global__ __launch_bounds__(BLOCK) void k_agg_c(AggArgs a) {
     cnt = p1 > pc0 ? (uint32_t)(p1 - pc0) : 0u;
   }
   uint32_t cum = cnt;
-#pragma unroll
-  for (int sd = 1; sd < 64; sd <<= 1) {
-    const uint32_t t = (uint32_t)__shfl_up((int)cum, sd, 64);
-    if (lane >= sd) cum += t;
-  }
-  const uint32_t T = (uint32_t)__shfl((int)cum, 63, 64);
+  cum = wave_incl_sum_u32(cum);
+  const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cum, 63);
   cum -= cnt;
   if (!T) return;
   const uint64_t total = *a.agg_total;

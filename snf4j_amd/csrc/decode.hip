@@ -479,12 +479,8 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
     const uint32_t pc0 = (uint32_t)((ex.sum + PIECE - 1) / PIECE);
     const uint32_t cnt = slot ? (uint32_t)((slot_end + PIECE - 1) / PIECE) - pc0 : 0u;
     uint32_t cum = cnt;  // inclusive wave scan of the counts
-#pragma unroll
-    for (int sd = 1; sd < 64; sd <<= 1) {
-      const uint32_t t = (uint32_t)__shfl_up((int)cum, sd, 64);
-      if (lane >= sd) cum += t;
-    }
-    const uint32_t T = (uint32_t)__shfl((int)cum, 63, 64);
+    cum = wave_incl_sum_u32(cum);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cum, 63);
     cum -= cnt;  // exclusive
     if (!T) return;
     // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31

@@ -57,6 +57,17 @@ __device__ __forceinline__ Agg agg_dpp(const Agg& v) {
 
 constexpr Agg AGG_ID = {0ull, -1, -1, -1};
 
+// inclusive wave scan of a 32-bit sum by DPP
+__device__ __forceinline__ uint32_t wave_incl_sum_u32(uint32_t v) {
+  v += dpp_u32<DPP_ROW_SHR1, 0xf>(v, 0u);
+  v += dpp_u32<DPP_ROW_SHR2, 0xf>(v, 0u);
+  v += dpp_u32<DPP_ROW_SHR4, 0xf>(v, 0u);
+  v += dpp_u32<DPP_ROW_SHR8, 0xf>(v, 0u);
+  v += dpp_u32<DPP_ROW_BCAST15, 0xa>(v, 0u);
+  v += dpp_u32<DPP_ROW_BCAST31, 0xc>(v, 0u);
+  return v;
+}
+
 // Scans over any element type T with agg_op(T, T) (associative, applied in frame
 // order: it need not commute) and agg_dpp<CTRL, RM>(T) (identity where no source).
 // The wave scan is DPP moves (VALU, no LDS round trip a step): Hillis-Steele inside
