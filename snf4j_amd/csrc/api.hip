@@ -684,7 +684,7 @@ int wsg_encode_batch_device(wsg_ctx* c, int client_mode, const uint8_t* payload,
   a.n_pieces = wire_cap / PIECE + 1;
   a.n_idx = a.n_pieces / 64 + 2;
   if (n_frames) {
-    HIP_TRY(c, c->epieces.ensure((a.n_pieces + PIECES_PER_WAVE) * sizeof(PieceDesc)));
+    HIP_TRY(c, c->epieces.ensure((a.n_pieces + ENC_PIECES_PER_WAVE) * sizeof(PieceDesc)));
     HIP_TRY(c, c->epidx.ensure(a.n_idx * sizeof(uint32_t)));
   }
   a.pieces = (PieceDesc*)c->epieces.p;

@@ -45,7 +45,10 @@ constexpr int PIECES_PER_WAVE = 2; // pieces one k_piecesN wave takes (tools/ube
 #define WSG_VPIECES 4
 #endif
 constexpr int VPIECES_PER_WAVE = WSG_VPIECES;  // validate-only mode (read-only stream)
-constexpr int ENC_PIECES_PER_WAVE = 2;  // k_enc_piecesN (1 and 2 within 1% once no array is promoted to LDS)
+#ifndef WSG_ENC_PIECES
+#define WSG_ENC_PIECES 2
+#endif
+constexpr int ENC_PIECES_PER_WAVE = WSG_ENC_PIECES;  // k_enc_piecesN (1 and 2 within 1% once no array is promoted to LDS)
 
 // Pieces needed for a batch, bounded from host-known sizes: the 16-B aligned
 // payload slots total sum(align16(len)) <= wire_len - 2F + 15F.
