@@ -592,12 +592,16 @@ void launch_agg_plan(const AggArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 1);
   hipLaunchKernelGGL(k_agg_c, dim3(a.nblk), dim3(BLOCK), 0, s, a);
 }
+#ifndef WSG_AGG_GRID_CAP
+#define WSG_AGG_GRID_CAP 65536
+#endif
+constexpr uint64_t AGG_GRID_CAP = WSG_AGG_GRID_CAP;  // waves of the grid-stride gather (build override for A/B)
 void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim) {
   // grid-stride over the pieces (their number is known only on the device)
   // (2 pieces per wave beat 1 and 4, and the XCD-aware order lost 12-40 % here:
   // same-box A/B on the configs[2] batch)
   const uint64_t nq = (a.n_pieces + AGG_PIECES_PER_WAVE - 1) / AGG_PIECES_PER_WAVE;
-  const uint64_t g = nq < 65536 ? nq : 65536;
+  const uint64_t g = nq < AGG_GRID_CAP ? nq : AGG_GRID_CAP;
   if (a.n_frames && g)
     hipLaunchKernelGGL((k_agg_gather<AGG_PIECES_PER_WAVE>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
 }
