@@ -708,19 +708,35 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
 // made every step wait on a global load (and, through the in-order vector memory
 // counter, on the window loads and the output stores issued before it), and 128K
 // lanes' tables do not fit L2.  Here a lane's tables and its input live in LDS:
-//   * literal/length table: 8-bit root + up to QL_SUB sub-table entries; distance:
-//     7-bit root + QD_SUB (a set needing more runs on the HBM tables instead);
+//   * literal/length table: 7-bit root + up to QL_SUB sub-table entries; distance:
+//     6-bit root + QD_SUB (a set needing more runs on the HBM tables instead).  With
+//     the code lengths kept as nibbles that is 47 KB a workgroup, 3 per CU (8/96 and
+//     7/32 with byte lengths took 76 KB, 2 per CU: k_infl_tok 4.39 -> 4.11 ms);
 //     fixed-code blocks use shared 9/5-bit tables built once per workgroup;
 //   * the input: a 64-B ring of the payload's 32-B aligned chunks, topped up at
 //     wave-uniform points (when some lane is about to run dry) from a chunk already
 //     loaded into registers, so the only wait on global memory is there;
-//   * the code lengths of a header in the distance table's space (byte q of a lane
-//     in dword q / 4), the code-length code table in the literal table's.
+//   * the code lengths of a header in the distance table's space (nibble q of a lane
+//     in dword q / 8), the code-length code table in the literal table's.
 // The output (literal bytes, tokens) goes to HBM as in tok_message; nothing waits on
 // those stores until the next ring top-up.
 // ---------------------------------------------------------------------------------
-constexpr int QL_ROOT = 8, QD_ROOT = 7, QC_ROOT = 7;  // per-lane root bits
-constexpr int QL_SUB = 96, QD_SUB = 32;              // sub-table entries a lane may use
+// Root widths and sub-table room (build overrides for A/B): what the bench's headers
+// need per width is in DESIGN.md §9 (tools/infl_table_sizes.py).
+#ifndef WSG_QL_ROOT
+#define WSG_QL_ROOT 7
+#endif
+#ifndef WSG_QL_SUB
+#define WSG_QL_SUB 72
+#endif
+#ifndef WSG_QD_ROOT
+#define WSG_QD_ROOT 6
+#endif
+#ifndef WSG_QD_SUB
+#define WSG_QD_SUB 20
+#endif
+constexpr int QL_ROOT = WSG_QL_ROOT, QD_ROOT = WSG_QD_ROOT, QC_ROOT = 7;  // per-lane root bits
+constexpr int QL_SUB = WSG_QL_SUB, QD_SUB = WSG_QD_SUB;                  // sub-table entries a lane may use
 constexpr int QL_N = (1 << QL_ROOT) + QL_SUB;        // u16 entries per lane
 constexpr int QD_N = (1 << QD_ROOT) + QD_SUB;
 constexpr int QF_LROOT = 9, QF_DROOT = 5;            // fixed codes (shared tables)
@@ -729,7 +745,10 @@ constexpr uint32_t Q_LT = QF_D + (1u << QF_DROOT);   // lane tables: entry j of 
 constexpr uint32_t Q_DT = Q_LT + QL_N * 64;
 constexpr uint32_t Q_TAB = Q_DT + QD_N * 64;
 constexpr int Q_RING = 17;                           // ring dwords per lane: 16 + slot 0 mirrored
-static_assert(QD_N * 2 >= 320, "the code lengths of a header fit a lane's distance table");
+constexpr int Q_LENW = 40;                           // code-length dwords per lane (320 nibbles)
+static_assert(QD_N * 2 >= Q_LENW * 4, "the code lengths of a header fit a lane's distance table");
+static_assert(QL_N >= (1 << QC_ROOT), "the code-length code table fits a lane's literal table");
+static_assert(QL_SUB < 256 && QD_SUB < 256, "sub-table offsets fit a root entry's 8 bits");
 static_assert((Q_DT * 2) % 4 == 0, "code-length dwords are aligned");
 
 struct TokLds {
@@ -738,6 +757,8 @@ struct TokLds {
   uint32_t ring[Q_RING * 64];  // input ring: dword slot s of lane i at s * 64 + i
   uint32_t cnt[16 * 64];       // literal/length table build: count, then next code, of length L at L * 64 + i
 };
+static_assert(sizeof(TokLds) <= 160 * 1024 / 3 || WSG_QL_ROOT != 7 || WSG_QD_ROOT != 6,
+              "the default tables fit 3 workgroups per CU (160 KiB of LDS)");
 
 enum : int { Q_OK = 0, Q_BAD = 1, Q_BAIL = 2 };
 
@@ -825,20 +846,19 @@ __device__ int q_build(uint16_t* tab, uint32_t base, int rb, int sub, LensF lens
 // q_build for the literal/length set (up to 286 codes): the counts and each symbol's
 // code come from per-lane LDS counters (an atomic add a symbol, four lengths a read)
 // instead of a 15-way select chain a symbol in registers.
-__device__ int q_build_lit(TokLds& Q, uint32_t lane, const uint8_t* lensb, int n) {
+__device__ int q_build_lit(TokLds& Q, uint32_t lane, const uint32_t* lw, int n) {
   uint16_t* const tab = Q.tab;
   const uint32_t base = Q_LT + lane;
   constexpr int rb = QL_ROOT;
   uint32_t* const cnt = Q.cnt;
 #pragma unroll
   for (int L = 0; L < 16; ++L) cnt[L * 64 + lane] = 0;
-  const uint32_t* const lw = reinterpret_cast<const uint32_t*>(lensb);
-  const int nw = (n + 3) >> 2;
+  const int nw = (n + 7) >> 3;  // code length s: nibble s & 7 of dword (s >> 3) * 64 + lane (zero past n)
   for (int q = 0; q < nw; ++q) {
     const uint32_t w = lw[q * 64 + lane];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      const uint32_t l = 4 * q + b < n ? (w >> (8 * b)) & 15u : 0u;
+    for (int b = 0; b < 8; ++b) {
+      const uint32_t l = (w >> (4 * b)) & 15u;
       atomicAdd(&cnt[l * 64 + lane], 1u);  // length 0 counts into slot 0, unused
     }
   }
@@ -889,18 +909,18 @@ __device__ int q_build_lit(TokLds& Q, uint32_t lane, const uint8_t* lensb, int n
   }
   for (int q = 0; q < nw; ++q) {
     const uint32_t w = lw[q * 64 + lane];
-    uint32_t l4[4], code4[4];
+    uint32_t l4[8], code4[8];
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
-      l4[b] = 4 * q + b < n ? (w >> (8 * b)) & 15u : 0u;
+    for (int b = 0; b < 8; ++b) {
+      l4[b] = (w >> (4 * b)) & 15u;
       code4[b] = atomicAdd(&cnt[l4[b] * 64 + lane], 1u);
     }
 #pragma unroll
-    for (int b = 0; b < 4; ++b) {
+    for (int b = 0; b < 8; ++b) {
       const uint32_t l = l4[b];
       if (!l) continue;
       const uint32_t rev = __builtin_bitreverse32(code4[b]) >> (32 - l);
-      const uint16_t e = (uint16_t)(l | ((uint32_t)(4 * q + b) << 4));
+      const uint16_t e = (uint16_t)(l | ((uint32_t)(8 * q + b) << 4));
       if (l <= (uint32_t)rb) {
         for (uint32_t j = rev; j < rsize; j += 1u << l) tab[base + (j << 6)] = e;
       } else {
@@ -939,7 +959,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   uint32_t* const tok = a.tok + tok_base(off, k);
   uint8_t* const lit = a.lit + lit_base(off, k);
   uint16_t* const tab = Q.tab;
-  uint8_t* const lensb = reinterpret_cast<uint8_t*>(Q.tab + Q_DT);  // code length s: byte s & 3 of dword (s >> 2) * 64 + lane
+  uint32_t* const lw32 = reinterpret_cast<uint32_t*>(Q.tab + Q_DT);  // code length s: nibble s & 7 of dword (s >> 3) * 64 + lane
   const uint32_t lt = Q_LT + lane, dt = Q_DT + lane;
   // --- the input ring ---
   const uint8_t* const pay = a.payload;
@@ -1102,8 +1122,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       if (cmax < 0) { st = Q_BAD; break; }
       // the code lengths, into the distance table's space (zeroed first: runs of zeros
       // then write nothing)
-      uint32_t* const lw32 = reinterpret_cast<uint32_t*>(lensb);
-      for (int q = 0; q < 80; ++q) lw32[q * 64 + lane] = 0;
+      for (int q = 0; q < Q_LENW; ++q) lw32[q * 64 + lane] = 0;
       int have = 0, prev = 0, len256 = 0;
       while (have < nlen + ndist) {
         in_step();
@@ -1127,8 +1146,8 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         drop(nb + xb);
         if (have + copy > nlen + ndist) { st = Q_BAD; break; }
         for (int i = 0; len && i < copy; ++i) {
-          const int q = have + i;
-          lensb[4u * (((uint32_t)q >> 2) * 64u + lane) + ((uint32_t)q & 3u)] = (uint8_t)len;
+          const uint32_t q = (uint32_t)(have + i);
+          lw32[(q >> 3) * 64u + lane] |= (uint32_t)len << (4u * (q & 7u));
         }
         if (have <= 256 && 256 < have + copy) len256 = len;
         have += copy;
@@ -1140,7 +1159,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       uint32_t dl[4] = {0u, 0u, 0u, 0u};
       for (int i = 0; i < ndist; ++i) {
         const uint32_t q = (uint32_t)(nlen + i);
-        const uint32_t v = lensb[4u * ((q >> 2) * 64u + lane) + (q & 3u)];
+        const uint32_t v = (lw32[(q >> 3) * 64u + lane] >> (4u * (q & 7u))) & 15u;
         const uint32_t w = (uint32_t)i >> 3, sh = 4u * ((uint32_t)i & 7u);
         if (w == 0) dl[0] |= v << sh;
         else if (w == 1) dl[1] |= v << sh;
@@ -1153,7 +1172,13 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         return (int)((x >> (4 * (s & 7))) & 15u);
       };
       TPROF_T(t_bld);
-      const int lmax = q_build_lit(Q, lane, lensb, nlen);
+      // (the distance lengths after the literal ones are in the same dwords: cleared
+      // first, so the literal build counts only its own)
+      for (int i = 0; i < ndist; ++i) {
+        const uint32_t q = (uint32_t)(nlen + i);
+        lw32[(q >> 3) * 64u + lane] &= ~(15u << (4u * (q & 7u)));
+      }
+      const int lmax = q_build_lit(Q, lane, lw32, nlen);
       if (lmax == -2) { st = Q_BAIL; break; }
       if (lmax < 0) { st = Q_BAD; break; }
       const int dmax = q_build(tab, dt, QD_ROOT, QD_SUB, dlen, ndist);
