@@ -373,9 +373,10 @@ def _run_cuts(ctx, oracle, cut_sessions, no_context, n_batches):
 def _lds_path_messages(rng):
     """Single-frame compressed messages aimed at the pre-decode's LDS table paths:
     fixed-code blocks (Z_FIXED), stored blocks (level 0), near-uniform bytes over all
-    256 values (most literal codes 8-9 bits: more 9-bit prefixes than the LDS sub-table
-    room of a lane, so the lane falls back to its HBM tables), skewed far back-references
-    (distance codes longer than the 7-bit LDS root), tiny and multi-block messages."""
+    256 values (most literal codes 8-9 bits: every 7-bit root prefix needs a sub-table,
+    far more than the LDS sub-table room of a lane, so the lane falls back to its HBM
+    tables), skewed far back-references (distance codes longer than the 6-bit LDS root),
+    tiny and multi-block messages."""
     kinds = []
     for i in range(48):
         k = i % 6
