@@ -333,6 +333,13 @@ int wsg_batcher_feed(wsg_batcher* b, uint32_t sid, const uint8_t* data, uint64_t
 /* Decode all complete frames fed since the last flush; synchronises. */
 int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out);
 int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* st);
+/* Give slot `sid` to a new session: drops the pending partial frame and any bytes
+ * fed since the last flush, and zeroes the carry (fragmentation, UTF-8 context,
+ * closed latch), as a freshly constructed FrameDecoder + FrameUtf8Validator
+ * (FrameDecoder.java:43-63, FrameUtf8Validator.java:42).  The JNI shim calls it
+ * from the decoder's session-end hook (IEventDrivenCodec.event ENDING /
+ * removed, IEventDrivenCodec.java:36-62). */
+int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid);
 
 /* Pinned host buffers for socket reads (the role of IByteBufferAllocator,
  * IByteBufferAllocator.java:38-149): power-of-two size classes, recycled on

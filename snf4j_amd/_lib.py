@@ -132,6 +132,7 @@ def _load():
         "wsg_batcher_feed": ([p, u32, p, u64], i32),
         "wsg_batcher_flush": ([p, P(BatchView)], i32),
         "wsg_batcher_session_state": ([p, u32, P(SessionState)], i32),
+        "wsg_batcher_session_reset": ([p, u32], i32),
         "wsg_host_alloc": ([u64], p),
         "wsg_host_release": ([p], i32),
         "wsg_host_capacity": ([p], u64),

@@ -442,6 +442,12 @@ class NativeBatcher:
         if a.size:
             self._check(lib.wsg_batcher_feed(self._h, int(sid), a.ctypes.data, a.size))
 
+    def reset_session(self, sid: int):
+        """Hand slot `sid` to a new session (wsg_batcher_session_reset): the partial
+        frame and the carry are dropped, as a fresh FrameDecoder would start."""
+        from ._lib import lib
+        self._check(lib.wsg_batcher_session_reset(self._h, int(sid)))
+
     def flush_raw(self):
         """Decode everything complete; returns numpy views (valid until the next flush):
         (session_first, desc, payload, result, wire_bytes)."""

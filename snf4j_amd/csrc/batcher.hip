@@ -262,6 +262,155 @@ int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* s
   return WSG_API_OK;
 }
 
+// A session slot handed to a new session: a fresh FrameDecoder (FrameDecoder.java:
+// 43-63: no partial frame, fragmentation and closed cleared) and a fresh
+// FrameUtf8Validator (no context, FrameUtf8Validator.java:42).  Bytes fed but not
+// flushed are dropped with the old session.
+int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
+  if (!b || sid >= b->n) return WSG_API_EINVAL;
+  SessIn& x = b->s[sid];
+  std::vector<uint8_t>().swap(x.buf);
+  std::vector<uint32_t>().swap(x.lens);
+  x.complete = 0;
+  x.frag = false;
+  x.host_err = 0;
+  x.d1 = 0;
+  b->state[sid] = wsg_session_state{};
+  return WSG_API_OK;
+}
+
+// ------------------------------------------------------------------ encode batcher
+// FrameEncoder.encode (FrameEncoder.java:69-120) for every session of a selector
+// loop in one device batch per loop iteration.  add() copies a frame's payload
+// into a pinned arena in arrival order and keeps a 24-B record; flush() orders the
+// records by session (a stable counting sort: a session's frames keep their order,
+// their payloads stay where they landed, wsg_encode_frame.payload_off points at
+// them) and encodes them in one wsg_encode_batch_host call.  The close latch
+// (:71-76) is per session and persists across flushes.
+struct wsg_enc_batcher {
+  wsg_ctx* ctx = nullptr;
+  int client = 0;
+  uint32_t n = 0;
+  std::vector<uint8_t> closed;           // FrameEncoder.closed per session
+  std::vector<uint32_t> rec_sid;         // session of each queued frame, arrival order
+  std::vector<wsg_encode_frame> rec;     // queued frames, arrival order
+  std::vector<uint32_t> count;           // queued frames per session
+  PinnedBuf arena, frames, sf, cl, wire, off;
+  uint64_t arena_len = 0;
+  std::string err;
+};
+
+static int eset(wsg_enc_batcher* b, int code, const char* msg) {
+  if (b) b->err = msg ? msg : "";
+  return code;
+}
+
+int wsg_enc_batcher_open(wsg_ctx* ctx, int client_mode, uint32_t n_sessions, wsg_enc_batcher** out) {
+  if (!ctx || !out) return WSG_API_EINVAL;
+  wsg_enc_batcher* b = new wsg_enc_batcher();
+  b->ctx = ctx;
+  b->client = client_mode ? 1 : 0;
+  b->n = n_sessions;
+  b->closed.assign(n_sessions, 0);
+  b->count.assign(n_sessions, 0);
+  *out = b;
+  return WSG_API_OK;
+}
+
+int wsg_enc_batcher_close(wsg_enc_batcher* b) {
+  if (!b) return WSG_API_EINVAL;
+  (void)wsg_sync(b->ctx);
+  PinnedBuf* bufs[] = {&b->arena, &b->frames, &b->sf, &b->cl, &b->wire, &b->off};
+  for (PinnedBuf* p : bufs) p->release();
+  delete b;
+  return WSG_API_OK;
+}
+
+const char* wsg_enc_batcher_last_error(wsg_enc_batcher* b) { return b ? b->err.c_str() : "null batcher"; }
+
+int wsg_enc_batcher_add(wsg_enc_batcher* b, uint32_t sid, uint8_t opcode, uint8_t flags, const uint8_t* mask,
+                        const uint8_t* payload, uint32_t len) {
+  if (!b || sid >= b->n || (len && !payload)) return WSG_API_EINVAL;
+  if (b->closed[sid]) return WSG_API_OK;  // FrameEncoder.java:71-76: nothing after a CLOSE (latched earlier)
+  const uint64_t at = (b->arena_len + 15) & ~15ull;
+  if (at + len + 16 > b->arena.n) {  // grow, keeping what is queued (pinned: the H2D source)
+    PinnedBuf g;
+    if (g.ensure(std::max<uint64_t>(at + len + 16, 2 * b->arena.n)) != hipSuccess)
+      return eset(b, WSG_API_ENOMEM, "pinned arena");
+    if (b->arena_len) memcpy(g.p, b->arena.p, b->arena_len);
+    b->arena.release();
+    b->arena = g;
+  }
+  if (len) memcpy(b->arena.p + at, payload, len);
+  b->arena_len = at + len;
+  wsg_encode_frame f{};
+  f.payload_off = at;
+  f.payload_len = len;
+  f.opcode = opcode;
+  f.flags = flags;
+  if (mask) memcpy(f.mask, mask, 4);
+  b->rec.push_back(f);
+  b->rec_sid.push_back(sid);
+  ++b->count[sid];
+  return WSG_API_OK;
+}
+
+int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out) {
+  if (!b || !out) return WSG_API_EINVAL;
+  const uint32_t S = b->n;
+  const uint64_t F = b->rec.size();
+  B_TRY(b, b->frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
+  B_TRY(b, b->sf.ensure((S + 1) * sizeof(uint32_t)));
+  B_TRY(b, b->cl.ensure(S + 1));
+  B_TRY(b, b->off.ensure((F + 1) * sizeof(uint64_t)));
+  uint32_t* sf = (uint32_t*)b->sf.p;
+  sf[0] = 0;
+  for (uint32_t i = 0; i < S; ++i) sf[i + 1] = sf[i] + b->count[i];
+  {  // stable counting sort of the records by session
+    std::vector<uint32_t> pos(sf, sf + S);
+    wsg_encode_frame* fr = (wsg_encode_frame*)b->frames.p;
+    for (uint64_t k = 0; k < F; ++k) fr[pos[b->rec_sid[k]]++] = b->rec[k];
+  }
+  uint64_t need = 0;
+  for (uint64_t k = 0; k < F; ++k) need += wsg_encoded_length(b->rec[k].payload_len, b->client);
+  B_TRY(b, b->wire.ensure(need + 32));
+  if (S) memcpy(b->cl.p, b->closed.data(), S);
+  int rc = wsg_encode_batch_host(b->ctx, b->client, b->arena.p, b->arena_len, (const wsg_encode_frame*)b->frames.p, F,
+                                 sf, S, b->cl.p, b->wire.p, b->wire.n, (uint64_t*)b->off.p);
+  if (rc) return eset(b, rc, wsg_last_error(b->ctx));
+  if (S) memcpy(b->closed.data(), b->cl.p, S);
+  if (!F) ((uint64_t*)b->off.p)[0] = 0;
+  b->rec.clear();
+  b->rec_sid.clear();
+  std::fill(b->count.begin(), b->count.end(), 0u);
+  b->arena_len = 0;
+  out->n_frames = F;
+  out->wire_bytes = ((const uint64_t*)b->off.p)[F];
+  out->n_sessions = S;
+  out->reserved = 0;
+  out->session_first = sf;
+  out->wire_off = (const uint64_t*)b->off.p;
+  out->wire = b->wire.p;
+  return WSG_API_OK;
+}
+
+int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid) {
+  if (!b || sid >= b->n) return WSG_API_EINVAL;
+  if (b->count[sid]) {  // drop the slot's queued frames (their arena bytes stay until the flush)
+    uint64_t j = 0;
+    for (uint64_t k = 0; k < b->rec.size(); ++k)
+      if (b->rec_sid[k] != sid) {
+        b->rec[j] = b->rec[k];
+        b->rec_sid[j++] = b->rec_sid[k];
+      }
+    b->rec.resize(j);
+    b->rec_sid.resize(j);
+    b->count[sid] = 0;
+  }
+  b->closed[sid] = 0;
+  return WSG_API_OK;
+}
+
 // ------------------------------------------------------------------ pinned pool
 // IByteBufferAllocator in the native layer: pinned (page-locked) host buffers in
 // power-of-two size classes, recycled on release, so socket reads land where the

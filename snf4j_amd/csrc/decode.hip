@@ -115,6 +115,83 @@ __device__ __forceinline__ DAgg frame_agg(uint64_t k, const FrameRec& r, uint32_
   return v;
 }
 
+// ------------------------------------------------------------------ validator-only scan element
+// The ws-utf8-validator stage alone (wsg_validate_batch_*) sees frame orders the
+// decoder would reject, so it follows FrameUtf8Validator.java:59-98 literally: one
+// context per session, opened by a TEXT frame when none is open, CONTINUED by a TEXT
+// frame when one is, carried by a CONTINUATION only while open, closed by any
+// validated FIN frame; BINARY and control frames leave it alone.  Per frame that is
+// a function of the state (open, last <= 3 bytes of the context's payload):
+//   TEXT !FIN, bytes t : (o, b) -> (1, o ? b.t : t)        OPENS  A = B = t
+//   CONT !FIN, bytes t : (o, b) -> (o, b.t)  (garbage if !o) PASS   A = t
+//   TEXT / CONT FIN    : -> (0, -)                          CONST  o = 0
+//   BINARY, control    : identity                           PASS   A = empty
+// and the composition of any run of them is one of
+//   PASS  (o, b) -> (o, b.A)     OPENS (o, b) -> (1, o ? b.A : B)     CONST -> (o_out, B)
+// fa = A (c3 layout, bits 0-25) | kind << 28 | o_out << 30; fb = B (0 unless a state
+// with an open context can come out of it).  A session's first frame is composed
+// with CONST(its carried-in state), so every exclusive prefix inside a session is a
+// CONST: the context open before the frame and its last bytes.
+struct VAgg {
+  uint64_t sum;
+  uint32_t fa, fb;
+};
+constexpr VAgg VAGG_ID = {0ull, 0u, 0u};
+constexpr uint32_t VK_PASS = 0u, VK_OPENS = 1u, VK_CONST = 2u;
+constexpr uint32_t VC_MASK = 0x3ffffffu;  // bytes + count
+__device__ __forceinline__ uint32_t vkind(uint32_t fa) { return (fa >> 28) & 3u; }
+__device__ __forceinline__ uint32_t vopen(uint32_t fa) { return (fa >> 30) & 1u; }
+__device__ __forceinline__ uint32_t vcat(uint32_t x, uint32_t y) { return carry_op(x & VC_MASK, y & VC_MASK); }
+
+__device__ __forceinline__ VAgg agg_op(const VAgg& x, const VAgg& y) {
+  VAgg r;
+  r.sum = x.sum + y.sum;
+  const uint32_t kx = vkind(x.fa), ky = vkind(y.fa);
+  if (ky == VK_CONST) {
+    r.fa = y.fa; r.fb = y.fb;
+    return r;
+  }
+  // bytes of an open context after x, then y appends to them; else y's own opening
+  const bool xb = kx == VK_OPENS || (kx == VK_CONST && vopen(x.fa));
+  r.fb = xb ? vcat(x.fb, y.fa) : (ky == VK_OPENS ? y.fb : 0u);
+  if (kx == VK_CONST) {
+    r.fa = (VK_CONST << 28) | ((vopen(x.fa) || ky == VK_OPENS) ? (1u << 30) : 0u);
+    if (!(r.fa >> 30)) r.fb = 0u;
+  } else {
+    r.fa = vcat(x.fa, y.fa) | ((kx == VK_OPENS || ky == VK_OPENS ? VK_OPENS : VK_PASS) << 28);
+  }
+  return r;
+}
+template <int CTRL, int RM>
+__device__ __forceinline__ VAgg agg_dpp(const VAgg& v) {
+  VAgg t;
+  t.sum = dpp_u64<CTRL, RM>(v.sum, 0ull);
+  t.fa = dpp_u32<CTRL, RM>(v.fa, 0u);
+  t.fb = dpp_u32<CTRL, RM>(v.fb, 0u);
+  return t;
+}
+
+// frame k's element (l3: its last 3 payload bytes, 0 for a FIN frame)
+__device__ __forceinline__ VAgg vframe_agg(const FrameRec& r, uint32_t l3, bool sess_first, const wsg_session_state* st) {
+  VAgg v;
+  v.sum = (uint64_t)((r.len + 15u) & ~15u);
+  const uint32_t op = code_op(r.code);
+  const uint32_t t = r.len ? (l3 & 0xffffffu) | ((r.len < 3 ? r.len : 3u) << 24) : 0u;
+  v.fb = 0u;
+  if (op != WSG_OP_TEXT && op != WSG_OP_CONTINUATION) v.fa = 0u;
+  else if (r.code & CODE_FIN) v.fa = VK_CONST << 28;
+  else if (op == WSG_OP_TEXT) { v.fa = t | (VK_OPENS << 28); v.fb = t; }
+  else v.fa = t;
+  if (sess_first) {  // the state carried in from the previous batch
+    VAgg c;
+    c.sum = 0;
+    c.fa = (VK_CONST << 28) | (st->text_open ? (1u << 30) : 0u);
+    c.fb = st->text_open ? (tail_c3(*st) & VC_MASK) : 0u;
+    v = agg_op(c, v);
+  }
+  return v;
+}
+
 // Block aggregates: blk_sum[b], and the maxima / carry in four rows of blk_max
 // whose stride is nblk rounded up to 4, so that every row is 16-B aligned (k_link
 // folds them with 16-B loads).
@@ -137,6 +214,18 @@ __device__ __forceinline__ void store_blk(const DecodeArgs& a, uint32_t b, const
   a.blk_max[2 * st + b] = e.m2;
   a.blk_max[3 * st + b] = (int32_t)e.c3;
 }
+// (validator-only mode: fa, fb in rows 0 and 1)
+__device__ __forceinline__ void load_blk(const DecodeArgs& a, uint32_t b, VAgg& e) {
+  e.sum = a.blk_sum[b];
+  e.fa = (uint32_t)a.blk_max[b];
+  e.fb = (uint32_t)a.blk_max[blk_stride(a) + b];
+}
+__device__ __forceinline__ void store_blk(const DecodeArgs& a, uint32_t b, const VAgg& e) {
+  a.blk_sum[b] = e.sum;
+  a.blk_max[b] = (int32_t)e.fa;
+  a.blk_max[blk_stride(a) + b] = (int32_t)e.fb;
+}
+__device__ __forceinline__ void load_blk(const DecodeArgs& a, uint32_t b, DAgg& e) { e = load_blk(a, b); }
 
 __device__ __forceinline__ uint32_t wave_session(const DecodeArgs& a, uint64_t k) {
   return wave_find_session(a.session_first, a.n_sessions, a.n_frames, k);
@@ -261,36 +350,34 @@ __device__ __forceinline__ uint32_t plain_word(const DecodeArgs& a, uint64_t i) 
 
 __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
-  DAgg v = DAGG_ID;
+  VAgg v = VAGG_ID;
   if (k < a.n_frames) {
-    {
-      const uint32_t s = wave_session(a, k);
-      const wsg_frame_desc d = a.in_desc[k];
-      const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
-      const uint32_t len = d.payload_len;
-      const uint64_t src = d.payload_off;
-      uint32_t l3 = 0;
-      if (op <= WSG_OP_TEXT && len) {  // fragment-boundary bytes for the UTF-8 carry (as k_parse)
-        const uint32_t nf = len < 3 ? len : 3;
-        const uint32_t keep = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : 0xffu);
-        // a frame's first bytes matter only at a continuation's seam (k_link); a message
-        // start is validated whole by the piece kernel: no scattered line per TEXT frame
-        if (op == WSG_OP_CONTINUATION) a.edge[k] = plain_word(a, src) & keep;
-        if (!fin) l3 = (plain_word(a, src + len - nf) & keep) << (8 * (3 - nf));  // newest in bits 16-23
-      }
-      a.edge[a.n_frames + k] = l3;
-      FrameRec r;
-      r.src = src;
-      r.len = len;
-      r.mask = 0;
-      r.code = (fin ? CODE_FIN : 0u) | (rsv << CODE_RSV_SHIFT) | (op << CODE_OP_SHIFT);
-      r.sess = s;
-      a.rec[k] = r;
-      v = agg_op(v, frame_agg(k, r, l3, k == a.session_first[s]));
+    const uint32_t s = wave_session(a, k);
+    const wsg_frame_desc d = a.in_desc[k];
+    const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
+    const uint32_t len = d.payload_len;
+    const uint64_t src = d.payload_off;
+    uint32_t l3 = 0;
+    // the last bytes of a non-FIN text/continuation frame: the carry into what follows.
+    // (a frame's first bytes matter only at a seam, which k_link knows: it loads them)
+    if (op <= WSG_OP_TEXT && len && !fin) {
+      const uint32_t nf = len < 3 ? len : 3;
+      const uint32_t keep = nf >= 3 ? 0xffffffu : (nf == 2 ? 0xffffu : 0xffu);
+      l3 = (plain_word(a, src + len - nf) & keep) << (8 * (3 - nf));  // newest in bits 16-23
     }
+    a.edge[a.n_frames + k] = l3;
+    FrameRec r;
+    r.src = src;
+    r.len = len;
+    r.mask = 0;
+    r.code = (fin ? CODE_FIN : 0u) | (rsv << CODE_RSV_SHIFT) | (op << CODE_OP_SHIFT);
+    r.sess = s;
+    a.rec[k] = r;
+    const bool first = k == a.session_first[s];
+    v = vframe_agg(r, l3, first, first ? &a.state[s] : nullptr);
   }
-  DAgg tot;
-  block_excl_scan_t(v, &tot, DAGG_ID);
+  VAgg tot;
+  block_excl_scan_t(v, &tot, VAGG_ID);
   if (threadIdx.x == 0) store_blk(a, blockIdx.x, tot);
 }
 
@@ -299,28 +386,53 @@ __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
 // aggregates scans its chunk in place (exclusive within the chunk, 4 entries per
 // thread) and leaves the chunk's total; k_link folds the totals of the chunks
 // before its own (a handful) in order.
+__device__ __forceinline__ void store_chunk(const DecodeArgs& a, uint32_t c, const DAgg& t) {
+  a.chunk_sum[c] = t.sum;
+  a.chunk_max[4 * c + 0] = t.m0;
+  a.chunk_max[4 * c + 1] = t.m1;
+  a.chunk_max[4 * c + 2] = t.m2;
+  a.chunk_max[4 * c + 3] = (int32_t)t.c3;
+}
+__device__ __forceinline__ void store_chunk(const DecodeArgs& a, uint32_t c, const VAgg& t) {
+  a.chunk_sum[c] = t.sum;
+  a.chunk_max[4 * c + 0] = (int32_t)t.fa;
+  a.chunk_max[4 * c + 1] = (int32_t)t.fb;
+}
+__device__ __forceinline__ void load_chunk(const DecodeArgs& a, uint32_t c, DAgg& e) {
+  e.sum = a.chunk_sum[c];
+  e.m0 = a.chunk_max[4 * c + 0];
+  e.m1 = a.chunk_max[4 * c + 1];
+  e.m2 = a.chunk_max[4 * c + 2];
+  e.c3 = (uint32_t)a.chunk_max[4 * c + 3];
+}
+__device__ __forceinline__ void load_chunk(const DecodeArgs& a, uint32_t c, VAgg& e) {
+  e.sum = a.chunk_sum[c];
+  e.fa = (uint32_t)a.chunk_max[4 * c + 0];
+  e.fb = (uint32_t)a.chunk_max[4 * c + 1];
+}
+
+__device__ __forceinline__ DAgg agg_ident(const DAgg*) { return DAGG_ID; }
+__device__ __forceinline__ VAgg agg_ident(const VAgg*) { return VAGG_ID; }
+
+template <class T>
 __global__ __launch_bounds__(1024) void k_scan(DecodeArgs a) {
+  const T ident = agg_ident((const T*)nullptr);
   const uint32_t b0 = blockIdx.x * SCAN_CHUNK + threadIdx.x * 4;
-  DAgg e[4], t = DAGG_ID;
+  T e[4], t = ident;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    e[i] = b0 + i < a.nblk ? load_blk(a, b0 + i) : DAGG_ID;
+    e[i] = ident;
+    if (b0 + i < a.nblk) load_blk(a, b0 + i, e[i]);
     t = agg_op(t, e[i]);
   }
-  DAgg tot;
-  DAgg ex = block_excl_scan_t(t, &tot, DAGG_ID);
+  T tot;
+  T ex = block_excl_scan_t(t, &tot, ident);
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     if (b0 + i < a.nblk) store_blk(a, b0 + i, ex);
     ex = agg_op(ex, e[i]);
   }
-  if (threadIdx.x == 0) {
-    a.chunk_sum[blockIdx.x] = tot.sum;
-    a.chunk_max[4 * blockIdx.x + 0] = tot.m0;
-    a.chunk_max[4 * blockIdx.x + 1] = tot.m1;
-    a.chunk_max[4 * blockIdx.x + 2] = tot.m2;
-    a.chunk_max[4 * blockIdx.x + 3] = (int32_t)tot.c3;
-  }
+  if (threadIdx.x == 0) store_chunk(a, blockIdx.x, tot);
 }
 
 // ------------------------------------------------------------------ UTF-8 seams
@@ -347,6 +459,59 @@ __device__ bool seam_utf8_error(uint32_t c3, uint32_t f3, uint32_t len, bool fin
     if (utf8_incomplete(t3, t2, t1)) return true;
   }
   return false;
+}
+
+// Descriptors of the pieces whose first output byte falls in a frame's slot,
+// written cooperatively: the wave's pieces are contiguous, lane i writes the
+// wave's pieces i, i+64, ... (coalesced 16-B stores) after finding the owning
+// frame with a shuffle search over the exclusive piece counts.  cont: the frame's
+// head bytes are checked against a carry by k_link (PDF_CONT).
+__device__ __forceinline__ void write_pieces(const DecodeArgs& a, bool live, uint64_t k, const FrameRec& r,
+                                             uint64_t ex_sum, bool validate, bool cont, int lane) {
+  const uint64_t slot = live ? (uint64_t)((r.len + 15u) & ~15u) : 0ull;
+  const uint64_t slot_end = ex_sum + slot;
+  const uint32_t pc0 = (uint32_t)((ex_sum + PIECE - 1) / PIECE);
+  const uint32_t cnt = slot ? (uint32_t)((slot_end + PIECE - 1) / PIECE) - pc0 : 0u;
+  uint32_t cum = cnt;  // inclusive wave scan of the counts
+  cum = wave_incl_sum_u32(cum);
+  const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cum, 63);
+  cum -= cnt;  // exclusive
+  if (!T) return;
+  // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31
+  const uint32_t fk = (uint32_t)k | (validate ? 0x80000000u : 0u) | ((live && (r.code & CODE_FIN)) ? 0x40000000u : 0u);
+  for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
+    int o = 0;
+#pragma unroll
+    for (int step = 32; step >= 1; step >>= 1)
+      if ((uint32_t)__shfl((int)cum, o + step, 64) <= t) o += step;
+    const uint32_t o_cum = (uint32_t)__shfl((int)cum, o, 64);
+    const uint32_t o_pc0 = (uint32_t)__shfl((int)pc0, o, 64);
+    const uint64_t o_out = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex_sum >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)ex_sum, o, 64);
+    const uint64_t o_src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(r.src >> 32), o, 64) << 32) |
+                           (uint32_t)__shfl((int)(uint32_t)r.src, o, 64);
+    const uint32_t o_len = (uint32_t)__shfl((int)r.len, o, 64);
+    const uint32_t o_mask = (uint32_t)__shfl((int)r.mask, o, 64);
+    const uint32_t o_fk = (uint32_t)__shfl((int)fk, o, 64);
+    const bool o_cont = __shfl((int)cont, o, 64) != 0;
+    if (t >= T) continue;
+    const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
+    if (pc >= a.n_pieces) continue;  // beyond the grid: the frame failed with WSG_E_BATCH above
+    const uint64_t ps = pc * PIECE;
+    const uint64_t o_end = o_out + ((o_len + 15u) & ~15u);
+    const uint32_t j0 = (uint32_t)(ps - o_out);
+    const uint32_t left = o_len - j0;
+    // runs past its frame's slot: other frames' bytes follow, unless it is the batch's
+    // last frame (a slot ending the payload region)
+    const bool single = o_end >= ps + PIECE || (uint64_t)(o_fk & 0x3fffffffu) + 1 == a.n_frames;
+    PieceDesc d;
+    d.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) |
+             ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI) |
+             (left <= PIECE ? PD_LAST : 0ull) | ((o_fk & 0x40000000u) ? PD_FIN : 0ull);
+    d.mask = o_mask;
+    d.frame = (o_fk & PDF_INDEX) | (o_cont ? PDF_CONT : 0u);
+    a.pieces[pc] = d;
+  }
 }
 
 // ------------------------------------------------------------------ k_link
@@ -452,7 +617,8 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
           seam_utf8_error(first ? tail_c3(st) : resolve_c3(ex.c3, st), a.edge[k], r.len, (r.code & CODE_FIN) != 0))
         status = WSG_E_TEXT_UTF8;
       validate = (text && !status) ? 1u : 0u;
-      a.vflag[k] = (uint8_t)validate;
+      // bit 1: the head is checked against a carry here (piece_general masks it)
+      a.vflag[k] = (uint8_t)(validate | ((validate && op == WSG_OP_CONTINUATION) ? 2u : 0u));
       wsg_frame_desc d;
       d.payload_off = ex.sum;
       d.payload_len = r.len;
@@ -470,56 +636,97 @@ __global__ __launch_bounds__(DBLOCK) void k_link(DecodeArgs a) {
         a.slink[2 * a.n_sessions + s] = (int32_t)resolve_c3(first ? v.c3 : carry_op(ex.c3, v.c3), st);
       }
     }
-    // Descriptors of the pieces whose first output byte falls in a frame's slot,
-    // written cooperatively: the wave's pieces are contiguous, lane i writes the
-    // wave's pieces i, i+64, ... (coalesced 16-B stores) after finding the owning
-    // frame with a shuffle search over the exclusive piece counts.
-    const uint64_t slot = live ? (uint64_t)((r.len + 15u) & ~15u) : 0ull;
-    const uint64_t slot_end = ex.sum + slot;
-    const uint32_t pc0 = (uint32_t)((ex.sum + PIECE - 1) / PIECE);
-    const uint32_t cnt = slot ? (uint32_t)((slot_end + PIECE - 1) / PIECE) - pc0 : 0u;
-    uint32_t cum = cnt;  // inclusive wave scan of the counts
-    cum = wave_incl_sum_u32(cum);
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cum, 63);
-    cum -= cnt;  // exclusive
-    if (!T) return;
-    // per-frame fields a piece needs: src, slot start, len, mask, frame | validate << 31
-    const uint32_t fk = (uint32_t)k | (validate ? 0x80000000u : 0u) | ((live && (r.code & CODE_FIN)) ? 0x40000000u : 0u);
-    const bool cont = live && code_op(r.code) == WSG_OP_CONTINUATION;
-    for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
-      int o = 0;
-#pragma unroll
-      for (int step = 32; step >= 1; step >>= 1)
-        if ((uint32_t)__shfl((int)cum, o + step, 64) <= t) o += step;
-      const uint32_t o_cum = (uint32_t)__shfl((int)cum, o, 64);
-      const uint32_t o_pc0 = (uint32_t)__shfl((int)pc0, o, 64);
-      const uint64_t o_out = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(ex.sum >> 32), o, 64) << 32) |
-                             (uint32_t)__shfl((int)(uint32_t)ex.sum, o, 64);
-      const uint64_t o_src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(r.src >> 32), o, 64) << 32) |
-                             (uint32_t)__shfl((int)(uint32_t)r.src, o, 64);
-      const uint32_t o_len = (uint32_t)__shfl((int)r.len, o, 64);
-      const uint32_t o_mask = (uint32_t)__shfl((int)r.mask, o, 64);
-      const uint32_t o_fk = (uint32_t)__shfl((int)fk, o, 64);
-      const bool o_cont = __shfl((int)cont, o, 64) != 0;
-      if (t >= T) continue;
-      const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
-      if (pc >= a.n_pieces) continue;  // beyond the grid: the frame failed with WSG_E_BATCH above
-      const uint64_t ps = pc * PIECE;
-      const uint64_t o_end = o_out + ((o_len + 15u) & ~15u);
-      const uint32_t j0 = (uint32_t)(ps - o_out);
-      const uint32_t left = o_len - j0;
-      // runs past its frame's slot: other frames' bytes follow, unless it is the batch's
-      // last frame (a slot ending the payload region)
-      const bool single = o_end >= ps + PIECE || (uint64_t)(o_fk & 0x3fffffffu) + 1 == a.n_frames;
-      PieceDesc d;
-      d.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(left < PIECE ? left : PIECE) << PD_NB_SHIFT) |
-               ((o_fk & 0x80000000u) ? PD_VALIDATE : 0ull) | (j0 == 0 ? PD_FIRST : 0ull) | (single ? 0ull : PD_MULTI) |
-               (left <= PIECE ? PD_LAST : 0ull) | ((o_fk & 0x40000000u) ? PD_FIN : 0ull);
-      d.mask = o_mask;
-      d.frame = (o_fk & PDF_INDEX) | (o_cont ? PDF_CONT : 0u);
-      a.pieces[pc] = d;
+    write_pieces(a, live, k, r, ex.sum, validate != 0, live && code_op(r.code) == WSG_OP_CONTINUATION, lane);
+  }
+}
+
+// ------------------------------------------------------------------ k_vlink
+// k_link of the validator-only stage: the exclusive scan of the VAgg elements
+// gives every frame the FrameUtf8Validator context it meets (open or not, its last
+// <= 3 bytes).  A frame is validated when it is TEXT, or a CONTINUATION while a
+// context is open (FrameUtf8Validator.java:63-75); a validated frame that meets an
+// open context (a CONTINUATION, or a TEXT frame continuing it) has its head bytes
+// checked against that carry here, the rest by the piece kernel.
+__global__ __launch_bounds__(DBLOCK) void k_vlink(DecodeArgs a) {
+  const int lane = threadIdx.x & 63;
+  VAgg bp;
+  if (a.fused_scan) {  // fold the block aggregates before this block (in order: staged in LDS)
+    __shared__ uint32_t fas[FUSED_SCAN_MAX_BLOCKS], fbs[FUSED_SCAN_MAX_BLOCKS];
+    const uint32_t nb = blockIdx.x, st = blk_stride(a);
+    uint64_t sum = 0;
+    for (uint32_t b = threadIdx.x; b < nb; b += DBLOCK) {
+      sum += a.blk_sum[b];
+      fas[b] = (uint32_t)a.blk_max[b];
+      fbs[b] = (uint32_t)a.blk_max[st + b];
+    }
+    __syncthreads();
+    const uint32_t per = (nb + DBLOCK - 1) / DBLOCK;
+    const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < nb ? b0 + per : nb;
+    VAgg t = VAGG_ID;
+    for (uint32_t b = b0; b < b1; ++b) t = agg_op(t, VAgg{0ull, fas[b], fbs[b]});
+    t.sum = sum;  // (the sums commute: folded as loaded)
+    block_excl_scan_t(t, &bp, VAGG_ID);
+  } else {
+    bp = VAGG_ID;
+    for (uint32_t c = 0; c < blockIdx.x / SCAN_CHUNK; ++c) {
+      VAgg e;
+      load_chunk(a, c, e);
+      bp = agg_op(bp, e);
+    }
+    VAgg e;
+    load_blk(a, blockIdx.x, e);
+    bp = agg_op(bp, e);
+  }
+  const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
+  const bool live = k < a.n_frames;
+  FrameRec r = {0ull, 0u, 0u, 0u, 0u};
+  VAgg v = VAGG_ID;
+  wsg_session_state st = {};
+  bool first = false;
+  if (live) {
+    r = a.rec[k];
+    const uint32_t l3 = (r.len && !(r.code & CODE_FIN)) ? a.edge[a.n_frames + k] : 0u;
+    first = k == a.session_first[r.sess];
+    if (first) st = a.state[r.sess];
+    v = vframe_agg(r, l3, first, &st);
+  }
+  VAgg tot;
+  const VAgg ex = agg_op(bp, block_excl_scan_t(v, &tot, VAGG_ID));
+  if (blockIdx.x + 1 == a.nblk && threadIdx.x == 0) *a.total = bp.sum + tot.sum;
+  bool validate = false, seam = false;
+  if (live) {
+    const uint32_t s = r.sess;
+    const uint32_t op = code_op(r.code);
+    // the context this frame meets: the session's carried-in state, or the (CONST) prefix
+    const bool open = first ? st.text_open != 0 : vopen(ex.fa) != 0;
+    const uint32_t carry = first ? (st.text_open ? tail_c3(st) & VC_MASK : 0u) : ex.fb;
+    validate = op == WSG_OP_TEXT || (op == WSG_OP_CONTINUATION && open);
+    seam = validate && open;
+    uint32_t status = 0;
+    if (ex.sum + r.len > a.n_pieces * PIECE) status = WSG_E_BATCH;  // slots beyond the piece grid
+    if (!status && seam) {
+      const uint32_t nh = r.len < 3 ? r.len : 3u;
+      const uint32_t f3 = nh ? plain_word(a, r.src) & (0xffffffu >> (8 * (3 - nh))) : 0u;
+      if (seam_utf8_error(carry, f3, r.len, (r.code & CODE_FIN) != 0)) status = WSG_E_TEXT_UTF8;
+    }
+    validate = validate && !status;
+    seam = seam && validate;
+    a.vflag[k] = (uint8_t)((validate ? 1u : 0u) | (seam ? 2u : 0u));
+    wsg_frame_desc d;
+    d.payload_off = ex.sum;
+    d.payload_len = r.len;
+    d.opcode = (uint8_t)op;
+    d.flags = (uint8_t)(((r.code & CODE_FIN) ? 0x80u : 0u) | (((r.code >> CODE_RSV_SHIFT) & 7u) << 4));
+    d.status = (uint16_t)status;
+    a.desc[k] = d;
+    if (status) atomicMin((unsigned long long*)&a.sess_err[s], (unsigned long long)k);
+    if (k + 1 == a.session_first[s + 1]) {  // the context after the session's last frame (k_final)
+      const VAgg inc = agg_op(ex, v);      // (a CONST: v of a session's first frame is one)
+      a.slink[a.n_sessions + s] = (int32_t)vopen(inc.fa);
+      a.slink[2 * a.n_sessions + s] = (int32_t)inc.fb;
     }
   }
+  write_pieces(a, live, k, r, ex.sum, validate, seam, lane);
 }
 
 // ------------------------------------------------------------------ k_pieces
@@ -742,7 +949,7 @@ __device__ __forceinline__ void piece_general(const DecodeArgs& a, const PieceDe
     if (j == 0) pw = 0u;
     else if (prev_k != lk) pw = prev_word(a, lr.src + j, lr.mask);  // lane 0 inside a frame
     if (lval) {
-      const bool cont = code_op(lr.code) == WSG_OP_CONTINUATION;
+      const bool cont = (a.vflag[lk] & 2u) != 0;  // a seam frame: its head is k_link's
       uint32_t e0 = utf8_err_word_raw(w[0], pw), e1 = utf8_err_word_raw(w[1], w[0]);
       uint32_t e2 = utf8_err_word_raw(w[2], w[1]), e3 = utf8_err_word_raw(w[3], w[2]);
       if (j == 0 && cont) e0 &= 0x80000000u;  // a continuation's head: k_link
@@ -974,7 +1181,14 @@ __global__ __launch_bounds__(256) void k_final(DecodeArgs a) {
     st.closed = 1;
   } else {
     res.n_delivered = se - sf;
-    if (se > sf) {  // k_link's record of the session's last frame
+    if (se > sf && a.validator_only) {  // k_vlink: the validator context after the last frame
+      const bool open = a.slink[a.n_sessions + s] != 0;
+      const uint32_t c3 = (uint32_t)a.slink[2 * a.n_sessions + s];
+      const uint32_t n = open ? (c3 >> 24) & 3u : 0u;
+      for (uint32_t i = 0; i < n; ++i) st.tail[i] = (uint8_t)(c3 >> (24 - 8 * (n - i)));
+      st.tail_len = (uint8_t)n;
+      st.text_open = open;
+    } else if (se > sf) {  // k_link's record of the session's last frame
       const int32_t ld = a.slink[s];                          // last data frame
       if (ld >= (int32_t)sf) {
         const bool frag = !(a.rec[ld].code & CODE_FIN);
@@ -1005,10 +1219,13 @@ void launch_parse(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_parse, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
 void launch_scan(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan, dim3((a.nblk + SCAN_CHUNK - 1) / SCAN_CHUNK), dim3(1024), 0, s, a);
+  const dim3 g((a.nblk + SCAN_CHUNK - 1) / SCAN_CHUNK);
+  if (a.validator_only) hipLaunchKernelGGL(k_scan<VAgg>, g, dim3(1024), 0, s, a);
+  else hipLaunchKernelGGL(k_scan<DAgg>, g, dim3(1024), 0, s, a);
 }
 void launch_link(const DecodeArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
+  if (a.validator_only) hipLaunchKernelGGL(k_vlink, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
+  else hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
   // one 64-lane workgroup per two pieces, nontemporal loads/stores, XCD-aware

@@ -449,3 +449,59 @@ def test_pinned_pool(ctx):
     pinned_release(b2)
     with pytest.raises(ValueError):
         pinned_release(np.zeros(16, np.uint8))
+
+
+def test_native_batcher_session_reset_reuses_slot(ctx, oracle):
+    """A slot handed to a new session (wsg_batcher_session_reset) decodes exactly as
+    a fresh FrameDecoder + FrameUtf8Validator: the old session's closed latch (it
+    failed), its open fragmented text message with a split code point, its partial
+    frame and bytes fed but never flushed are all gone."""
+    from snf4j_amd import NativeBatcher
+    rng = np.random.default_rng(404)
+    m = (1, 2, 3, 4)
+    old = [
+        # failed: a bad opcode closes the session
+        wsgen.build_frame(1, True, 0, b"hi", True, m) + bytes([0x83, 0x80]) + bytes(m),
+        # an open text message ending inside a code point, and half of the next frame
+        wsgen.build_frame(1, False, 0, b"ab\xe2\x82", True, m) + wsgen.build_frame(0, True, 0, b"\xac!", True, m)[:5],
+        # a fragmented binary message left open (FrameDecoder.fragmentation)
+        wsgen.build_frame(2, False, 0, b"\x00" * 300, True, m),
+        b"",
+    ]
+    unflushed = [b"", b"", wsgen.build_frame(0, True, 0, b"zz", True, m)[:3], wsgen.build_frame(1, True, 0, b"x", True, m)]
+    n = len(old)
+    b = NativeBatcher(n, ctx=ctx)
+    for s in range(n):
+        if old[s]:
+            b.feed(s, old[s])
+    first = b.flush()
+    assert first[0][1] is not None and first[1][1] is None and first[2][1] is None
+    for s in range(n):
+        if unflushed[s]:
+            b.feed(s, unflushed[s])
+        b.reset_session(s)
+    # the new sessions start with a continuation (an error for a fresh decoder: it must
+    # not continue the old session's message) or with ordinary traffic
+    new = [b"".join(wsgen.session_frames(rng, int(rng.integers(1, 8)))) for _ in range(n)]
+    new[1] = wsgen.build_frame(0, True, 0, b"\xac", True, m) + new[1]
+    new[2] = wsgen.build_frame(0, True, 0, b"more", True, m) + new[2]
+    got = [[] for _ in range(n)]
+    err = [None] * n
+    pos = [0] * n
+    while any(pos[s] < len(new[s]) for s in range(n)):
+        for s in range(n):
+            if pos[s] < len(new[s]):
+                c = int(rng.integers(1, 700))
+                b.feed(s, new[s][pos[s]:pos[s] + c])
+                pos[s] += c
+        for s, (fr, e) in enumerate(b.flush()):
+            got[s] += fr
+            if e is not None and err[s] is None:
+                err[s] = e
+    for s in range(n):
+        frames, e = oracle.stream_decode(new[s], [len(new[s])])
+        assert [(f.opcode, f.fin, f.payload) for f in frames] == \
+               [(int(f.getOpcode()), f.isFinalFragment(), f.getPayload()) for f in got[s]], s
+        assert (str(e) if e else None) == (str(err[s]) if err[s] else None), s
+    assert err[1] is not None and err[2] is not None  # a fresh decoder rejects the leading continuation
+    b.close()

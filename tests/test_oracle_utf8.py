@@ -94,3 +94,14 @@ def test_dfa_matches_python_strict_decoder_on_random_strings(oracle):
             except UnicodeDecodeError:
                 exp.append(False)
         np.testing.assert_array_equal(got, np.array(exp))
+
+
+def test_oracle_validator_context_rule(oracle):
+    """FrameUtf8Validator.java:63-95 in any frame order: BINARY leaves an open
+    context alone, TEXT continues it, an orphan CONTINUATION is not validated."""
+    v = oracle.Validator()
+    assert [v.decode(*f) for f in [(1, False, b"\xdf"), (2, True, b"\xff"), (0, True, b"\xdf\xdf")]] == [True, True, False]
+    v = oracle.Validator()
+    assert [v.decode(*f) for f in [(1, False, b"\xe2\x82"), (1, True, b"\xac")]] == [True, True]
+    v = oracle.Validator()
+    assert [v.decode(*f) for f in [(0, False, b"\xff"), (0, True, b"\xff"), (1, True, b"ok")]] == [True, True, True]
