@@ -333,6 +333,35 @@ int wsg_batcher_feed(wsg_batcher* b, uint32_t sid, const uint8_t* data, uint64_t
 /* Decode all complete frames fed since the last flush; synchronises. */
 int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out);
 int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* st);
+/* The decoders after "ws-decoder" that a flush runs in the same device batch, in the
+ * pipeline order the reference builds (DefaultWebSocketSessionConfig.java:276-281,
+ * PerMessageDeflateExtension.java:316-326; a FrameAggregator the application puts
+ * after them):
+ *   ws-decoder -> [inflate: PerMessageDeflateDecoder(noContext)] ->
+ *   [validate: FrameUtf8Validator] -> [aggregate: FrameAggregator(max)]
+ * With inflate on, the decode runs with the fused UTF-8 check off and `validate`
+ * is the ws-utf8-validator stage after inflate (wsg_validate_batch_*); without
+ * inflate, `validate` is the fused check (cfg.validate_utf8).  Every stage sees
+ * the frames the stage before it delivered, per session in order, and keeps its
+ * own carry between flushes: the inflater state and 32 KiB window, the frames of
+ * a compressed message a batch leaves open (re-sent with the next batch), the
+ * validator context, the aggregated message in progress and its bytes.  A
+ * session's result is that of the LAST stage that failed it (its failure is the
+ * earliest in the stream), n_delivered counts the flush's output frames, and any
+ * failure latches the session closed.  Output frames: desc.flags bit 0x02
+ * (WSG_OUT_AGGREGATED) marks an aggregated message (AggregatedTextFrame /
+ * AggregatedBinaryFrame, FrameAggregator.java:76-99); payloads are in the view's
+ * payload region.  Call before the first feed. */
+typedef struct wsg_stage_cfg {
+    uint8_t inflate;             /* PerMessageDeflateDecoder after the decoder */
+    uint8_t inflate_no_context;  /* its noContext (PerMessageDeflateDecoder.java:52-56) */
+    uint8_t validate;            /* FrameUtf8Validator (ws-utf8-validator) */
+    uint8_t aggregate;           /* FrameAggregator */
+    uint32_t reserved;
+    int64_t max_aggregated_len;  /* FrameAggregator(maxAggregatedLength) */
+} wsg_stage_cfg;
+#define WSG_OUT_AGGREGATED 0x02
+int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages);
 /* Give slot `sid` to a new session: drops the pending partial frame and any bytes
  * fed since the last flush, and zeroes the carry (fragmentation, UTF-8 context,
  * closed latch), as a freshly constructed FrameDecoder + FrameUtf8Validator
@@ -340,6 +369,51 @@ int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* s
  * from the decoder's session-end hook (IEventDrivenCodec.event ENDING /
  * removed, IEventDrivenCodec.java:36-62). */
 int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid);
+
+/* ---------------- host boundary: cross-session encode batcher ---------------- */
+/* FrameEncoder.encode (FrameEncoder.java:69-120) for all sessions of a selector
+ * loop, one device batch per flush (the encode side of the loop batching, as
+ * EncodeTask.java:333-407 hands each write to the session's encoder chain).
+ * add() copies a frame's payload into a pinned arena and queues it; flush() orders
+ * the queued frames by session (each session's in arrival order) and encodes them
+ * in one wsg_encode_batch_host call; the close latch (:71-76) persists per session.
+ * Not thread-safe: one loop thread drives it. */
+typedef struct wsg_enc_batcher wsg_enc_batcher;
+
+typedef struct wsg_enc_view {  /* valid until the next add / flush / close */
+    uint64_t n_frames;
+    uint64_t wire_bytes;
+    uint32_t n_sessions;
+    uint32_t reserved;
+    const uint32_t* session_first;  /* [n_sessions + 1]: session s's frames [sf[s], sf[s+1]) */
+    const uint64_t* wire_off;       /* [n_frames + 1]: frame k's wire bytes [off[k], off[k+1]),
+                                       empty for a frame dropped after the session's CLOSE */
+    const uint8_t* wire;            /* session s's frames are contiguous: [off[sf[s]], off[sf[s+1]]) */
+} wsg_enc_view;
+
+int wsg_enc_batcher_open(wsg_ctx* ctx, int client_mode, uint32_t n_sessions, wsg_enc_batcher** out);
+int wsg_enc_batcher_close(wsg_enc_batcher* b);
+const char* wsg_enc_batcher_last_error(wsg_enc_batcher* b);
+/* Queue Frame(opcode, flags = FIN << 7 | RSV << 4, payload) of session `sid`;
+ * `mask` (client mode) is the 4-byte key, FrameEncoder.java:109-118. */
+int wsg_enc_batcher_add(wsg_enc_batcher* b, uint32_t sid, uint8_t opcode, uint8_t flags, const uint8_t* mask,
+                        const uint8_t* payload, uint32_t len);
+int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out);
+/* slot `sid` for a new session: its queued frames are dropped, the close latch cleared */
+int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid);
+
+/* ---------------- device per selector loop (multi-GPU policy) ---------------- */
+/* Sessions shard over the node's GPUs by selector loop, with no cross-device
+ * exchange (a session belongs to one loop, DefaultWebSocketSessionConfig.java:
+ * 276-281, one decoder per session): the JNI shim opens each loop's batcher on
+ * wsg_device_for_loop(loop id).  A new loop goes to the device with the fewest
+ * loops, ties to the one with the fewest wire bytes accounted (wsg_device_account
+ * after each flush); a loop keeps its device until released.  Process-wide,
+ * thread-safe.  wsg_device_policy_init fixes the device count (else the HIP count). */
+int wsg_device_policy_init(int n_devices);
+int wsg_device_for_loop(uint64_t loop_id);                 /* device index, or < 0 */
+int wsg_device_account(int device, uint64_t wire_bytes);
+int wsg_device_release_loop(uint64_t loop_id);
 
 /* Pinned host buffers for socket reads (the role of IByteBufferAllocator,
  * IByteBufferAllocator.java:38-149): power-of-two size classes, recycled on

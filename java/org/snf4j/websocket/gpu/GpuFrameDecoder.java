@@ -1,16 +1,24 @@
 /*
  * The "ws-decoder" stage on the MI355X: FrameDecoder (FrameDecoder.java:41-403)
- * with FrameUtf8Validator (FrameUtf8Validator.java:59-98) fused, decoded in
- * cross-session device batches (WsgBatcher).
+ * decoded in cross-session device batches (WsgBatcher), with the GPU stages that
+ * directly follow it in the pipeline run in the same batch: the UTF-8 check
+ * (FrameUtf8Validator.java:59-98, fused into the decode kernels), or, when
+ * permessage-deflate was negotiated, inflate then the validator
+ * (PerMessageDeflateExtension.java:316-326), and an aggregator behind them.
  *
  * available() is the reference's frame delimiting, on the loop thread
  * (FrameDecoder.java:290-401, through wsg_frame_available).  decode() hands the
  * bytes to the batcher and releases `data` exactly once (FrameDecoder.java:285-287);
- * it returns with `out` empty.  The frames come back in deliver(), on the
- * session's loop thread, and go through the decoders after "ws-decoder" and the
- * handler, in order.  The first error does what FrameDecoder.java:92-102 does:
+ * it returns with `out` empty.  The frames come back in deliver(), on the loop
+ * thread, and go through the decoders after the batched stages and the handler, in
+ * order.  The first error does what FrameDecoder.java:92-102 does:
  * writenf(CloseFrame(code)), the closed latch, and an InvalidFrameException with
  * the reference's message (GENTLE close, InvalidFrameException.java:75-77).
+ *
+ * The session slot is taken at the first decode (the pipeline is then complete:
+ * the handshake has switched the decoders and the extensions have added theirs)
+ * and given back at the session's end (IEventDrivenCodec, as ZlibDecoder does,
+ * ZlibDecoder.java:281-301), which resets it for the next session.
  */
 package org.snf4j.websocket.gpu;
 
@@ -22,6 +30,8 @@ import org.snf4j.core.codec.IBaseDecoder;
 import org.snf4j.core.codec.ICodec;
 import org.snf4j.core.codec.ICodecPipeline;
 import org.snf4j.core.codec.IDecoder;
+import org.snf4j.core.codec.IEventDrivenCodec;
+import org.snf4j.core.handler.SessionEvent;
 import org.snf4j.core.session.ISession;
 import org.snf4j.core.session.IStreamSession;
 import org.snf4j.websocket.IWebSocketSessionConfig;
@@ -29,27 +39,27 @@ import org.snf4j.websocket.frame.CloseFrame;
 import org.snf4j.websocket.frame.Frame;
 import org.snf4j.websocket.frame.InvalidFrameException;
 
-public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame> {
+public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventDrivenCodec {
 
 	private final WsgBatcher batcher;
 	private final boolean clientMode, allowExtensions;
 	private final int maxPayloadLen;
-	final int sid;
+	int sid = -1;
 	long nativeBatcher;
 	private ISession session;
 	/** FrameDecoder.closed (:63): after the first error all input is swallowed. */
 	private boolean closed;
+	/** the session ended: the slot went back to the batcher */
+	private boolean released;
 	/** bytes of the current frame still to come (FrameDecoder.availablePayload, :348-355) */
 	private long remaining;
 	private final long[] err = new long[4];
 
-	public GpuFrameDecoder(boolean clientMode, boolean allowExtensions, int maxPayloadLen, boolean validateUtf8,
-			WsgBatcher batcher) {
+	public GpuFrameDecoder(boolean clientMode, boolean allowExtensions, int maxPayloadLen, WsgBatcher batcher) {
 		this.batcher = batcher;
 		this.clientMode = clientMode;
 		this.allowExtensions = allowExtensions;
 		this.maxPayloadLen = maxPayloadLen;
-		this.sid = batcher.register(this, clientMode, allowExtensions, maxPayloadLen, validateUtf8);
 	}
 
 	@Override
@@ -60,10 +70,6 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame> {
 	@Override
 	public Class<Frame> getOutboundType() {
 		return Frame.class;
-	}
-
-	ISession session() {
-		return session;
 	}
 
 	/** FrameDecoder.available(ISession, byte[], int, int) (FrameDecoder.java:357-401). */
@@ -114,32 +120,68 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame> {
 	public void decode(ISession session, ByteBuffer data, List<Frame> out) throws Exception {
 		try {
 			this.session = session;
-			if (closed)
+			if (closed || released)
 				return;
+			if (sid < 0)
+				sid = batcher.register(this, stages(session.getCodecPipeline()));
 			if (remaining > 0)
 				remaining -= data.remaining();
-			batcher.enqueue(this, session, data);
+			batcher.enqueue(this, data);
 		} finally {
 			session.release(data);
 		}
 	}
 
+	/**
+	 * The batch configuration: this decoder's arguments and the GPU stages that
+	 * directly follow it, in the order the reference pipeline has them
+	 * (permessage-deflate decoder, ws-utf8-validator, an aggregator); those are
+	 * marked batched.
+	 */
+	private WsgBatcher.Cfg stages(ICodecPipeline pipeline) {
+		List<ICodec<?, ?>> after = new ArrayList<ICodec<?, ?>>();
+		boolean seen = false;
+		for (Object key : pipeline.decoderKeys()) {
+			if (seen)
+				after.add(pipeline.get(key));
+			else
+				seen = IWebSocketSessionConfig.WEBSOCKET_DECODER.equals(key);
+		}
+		int i = 0;
+		GpuPerMessageDeflateDecoder inflate = null;
+		GpuFrameUtf8Validator validator = null;
+		GpuFrameAggregator aggregator = null;
+		if (i < after.size() && after.get(i) instanceof GpuPerMessageDeflateDecoder)
+			inflate = (GpuPerMessageDeflateDecoder) after.get(i++);
+		if (i < after.size() && after.get(i) instanceof GpuFrameUtf8Validator)
+			validator = (GpuFrameUtf8Validator) after.get(i++);
+		// the aggregator batches only behind the validator, or directly behind the decoder
+		if ((validator != null || i == 0) && i < after.size() && after.get(i) instanceof GpuFrameAggregator)
+			aggregator = (GpuFrameAggregator) after.get(i++);
+		for (int k = 0; k < i; ++k)
+			((GpuStage) after.get(k)).setBatched();
+		return new WsgBatcher.Cfg(clientMode, allowExtensions, maxPayloadLen, validator != null, inflate != null,
+				inflate != null && inflate.noContext, aggregator != null,
+				aggregator != null ? aggregator.maxAggregatedLength : 0);
+	}
+
 	/** The session's frames of one device batch, on its loop thread. */
 	void deliver(List<Frame> frames, int error, long detail) {
-		if (closed)
+		if (closed || released)
 			return;
+		List<IDecoder<Object, Object>> chain = chain();
 		for (Frame f : frames)
-			downstream(f);
+			if (!downstream(f, chain))
+				return;
 		if (error != Wsg.OK)
 			fail(session, error, detail, 0, false);
 	}
 
-	/** The decoders after "ws-decoder", then the handler (DefaultCodecExecutor.java:557-584). */
-	@SuppressWarnings({ "unchecked", "rawtypes" })
-	private void downstream(Frame frame) {
+	/** The decoders after "ws-decoder" the batch did not run (once per delivery). */
+	@SuppressWarnings("unchecked")
+	private List<IDecoder<Object, Object>> chain() {
 		ICodecPipeline pipeline = session.getCodecPipeline();
-		List<Object> in = new ArrayList<Object>(1);
-		in.add(frame);
+		List<IDecoder<Object, Object>> chain = new ArrayList<IDecoder<Object, Object>>();
 		boolean after = false;
 		for (Object key : pipeline.decoderKeys()) {
 			if (!after) {
@@ -147,20 +189,34 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame> {
 				continue;
 			}
 			ICodec<?, ?> c = pipeline.get(key);
+			if (c instanceof GpuStage && ((GpuStage) c).isBatched())
+				continue;
+			chain.add((IDecoder<Object, Object>) c);
+		}
+		return chain;
+	}
+
+	/** One frame through the rest of the pipeline, then the handler (DefaultCodecExecutor.java:557-584). */
+	private boolean downstream(Frame frame, List<IDecoder<Object, Object>> chain) {
+		List<Object> in = new ArrayList<Object>(1);
+		in.add(frame);
+		for (IDecoder<Object, Object> c : chain) {
 			List<Object> next = new ArrayList<Object>();
 			for (Object o : in) {
 				try {
-					((IDecoder) c).decode(session, o, next);
+					c.decode(session, o, next);
 				} catch (Exception e) {
 					session.getHandler().exception(e);
 					session.close();
-					return;
+					closed = true;
+					return false;
 				}
 			}
 			in = next;
 		}
 		for (Object o : in)
 			session.getHandler().read(o);
+		return true;
 	}
 
 	private void fail(ISession session, int status, long detail, long detail2, boolean inAvailable) {
@@ -174,5 +230,32 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame> {
 		// (InternalSelectorLoop.java:589-601), then the GENTLE close (InternalSession.java:804-829)
 		session.getHandler().exception(e);
 		session.close();
+	}
+
+	/* ---- IEventDrivenCodec (IEventDrivenCodec.java:36-62) ---- */
+
+	@Override
+	public void added(ISession session, ICodecPipeline pipeline) {
+		this.session = session;
+	}
+
+	/** The session is ending: its slot goes back to the batcher, reset for the next session. */
+	@Override
+	public void event(ISession session, SessionEvent event) {
+		if (event == SessionEvent.ENDING)
+			release();
+	}
+
+	@Override
+	public void removed(ISession session, ICodecPipeline pipeline) {
+		release();
+	}
+
+	private void release() {
+		if (!released) {
+			released = true;
+			if (sid >= 0)
+				batcher.unregister(this);
+		}
 	}
 }

@@ -1,45 +1,62 @@
 /*
  * The "ws-encoder" stage: FrameEncoder (FrameEncoder.java:41-136) with the header
- * emit and the client-side masking of large frames on the MI355X
- * (wsg_encode_batch_host, k_enc_* kernels).  Small frames are header bytes plus a
- * short copy, cheaper on the loop thread than a PCIe round trip: they go through
- * the reference's own FrameEncoder.  The mask comes from the same
- * java.util.Random stream as FrameEncoder.RANDOM (:43,111); the close latch
- * (:71-76) is the `closed` byte passed to the device.  Output buffers come from
- * session.allocate (:78) and belong to the session writer.
+ * emit and the client-side masking done on the MI355X for every session of the
+ * selector loop in one device batch per loop iteration (WsgBatcher,
+ * wsg_enc_batcher_*: k_enc_* kernels).
+ *
+ * encode() runs on the loop thread (EncodeTask.java:216-245).  A frame from the
+ * device threshold up (4 KiB by default, so configs' 64 KiB fragments all go to
+ * the device) is queued and encode() returns with `out` empty; the batch is
+ * written to the session after the loop iteration's reads (session.writenf of the
+ * encoded bytes, which no Frame encoder takes).  Smaller frames are header bytes
+ * plus a short copy: they go through the reference FrameEncoder on the spot,
+ * unless frames of the session are already queued, in which case they queue
+ * behind them so the session's frames keep their order.  A CLOSE frame first
+ * writes everything queued (the closing handshake, WebSocketSession.CloseTask,
+ * writes it right before session.close()), then latches (:71-76).  Masks come
+ * from a java.util.Random as FrameEncoder.RANDOM draws them (:43,111).
  */
 package org.snf4j.websocket.gpu;
 
 import java.nio.ByteBuffer;
-import java.nio.ByteOrder;
 import java.util.List;
 import java.util.Random;
 
+import org.snf4j.core.codec.ICodecPipeline;
 import org.snf4j.core.codec.IEncoder;
+import org.snf4j.core.codec.IEventDrivenCodec;
+import org.snf4j.core.handler.SessionEvent;
 import org.snf4j.core.session.ISession;
+import org.snf4j.core.session.IStreamSession;
 import org.snf4j.websocket.frame.Frame;
 import org.snf4j.websocket.frame.FrameEncoder;
 import org.snf4j.websocket.frame.Opcode;
 
-public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer> {
+public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer>, IEventDrivenCodec {
 
 	private static final Random RANDOM = new Random();
+	public static final int DEFAULT_DEVICE_THRESHOLD = 4096;
 	/** frames with at least this many payload bytes are encoded on the device */
 	private final int deviceThreshold;
 	private final boolean clientMode;
 	private final FrameEncoder small;
 	private final WsgBatcher batcher;
-	private final ByteBuffer closed = ByteBuffer.allocateDirect(1);
-	private final ByteBuffer sessionFirst = ByteBuffer.allocateDirect(8).order(ByteOrder.LITTLE_ENDIAN);
-	private final ByteBuffer frameRec = ByteBuffer.allocateDirect(Wsg.ENCODE_FRAME_BYTES).order(ByteOrder.LITTLE_ENDIAN);
-	private final ByteBuffer wireOff = ByteBuffer.allocateDirect(16).order(ByteOrder.LITTLE_ENDIAN);
+	int sid = -1;
+	long nativeBatcher;
+	private IStreamSession session;
+	/** FrameEncoder.closed (:71-76) */
+	private boolean closed;
+	private boolean released;
 
 	public GpuFrameEncoder(boolean clientMode, WsgBatcher batcher, int deviceThreshold) {
 		this.clientMode = clientMode;
 		this.batcher = batcher;
 		this.deviceThreshold = deviceThreshold;
 		this.small = new FrameEncoder(clientMode);
-		sessionFirst.putInt(0, 0).putInt(4, 1);
+	}
+
+	public GpuFrameEncoder(boolean clientMode, WsgBatcher batcher) {
+		this(clientMode, batcher, DEFAULT_DEVICE_THRESHOLD);
 	}
 
 	@Override
@@ -52,43 +69,55 @@ public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer> {
 		return ByteBuffer.class;
 	}
 
-	@Override
-	public void encode(ISession session, Frame frame, List<ByteBuffer> out) throws Exception {
-		if (closed.get(0) != 0)
-			return;  // FrameEncoder.java:71-76
-		if (frame.getPayloadLength() < deviceThreshold) {
-			small.encode(session, frame, out);
-			if (frame.getOpcode() == Opcode.CLOSE)
-				closed.put(0, (byte) 1);
-			return;
-		}
-		byte[] p = frame.getPayload();
-		ByteBuffer payload = session.allocate(p.length);
-		payload.put(p).flip();
-		int len = (int) Wsg.encodedLength(p.length, clientMode);
-		ByteBuffer wire = session.allocate(len);
-		frameRec.clear();
-		frameRec.putLong(0, 0).putInt(8, p.length).put(12, (byte) frame.getOpcode().value())
-				.put(13, (byte) ((frame.isFinalFragment() ? 0x80 : 0) | (frame.getRsvBits() << 4)));
-		if (clientMode) {
-			byte[] mask = new byte[4];
-			RANDOM.nextBytes(mask);
-			for (int i = 0; i < 4; ++i)
-				frameRec.put(16 + i, mask[i]);
-		}
-		int rc = Wsg.encodeBatchHost(batcher.ctx, clientMode, direct(payload), p.length, frameRec, 1, sessionFirst, 1,
-				closed, direct(wire), len, wireOff);
-		session.release(payload);
-		if (rc != 0)
-			throw new IllegalStateException("wsg_encode_batch_host: " + Wsg.lastError(batcher.ctx));
-		wire.position(0).limit(len);
-		out.add(wire);
+	IStreamSession session() {
+		return session;
 	}
 
-	/** Session buffers must be direct to cross JNI (PinnedByteBufferAllocator gives pinned ones). */
-	private static ByteBuffer direct(ByteBuffer b) {
-		if (!b.isDirect())
-			throw new IllegalStateException("GpuFrameEncoder needs a direct-buffer allocator");
-		return b;
+	@Override
+	public void encode(ISession session, Frame frame, List<ByteBuffer> out) throws Exception {
+		this.session = (IStreamSession) session;
+		if (closed || released)
+			return;  // FrameEncoder.java:71-76
+		if (frame.getOpcode() == Opcode.CLOSE) {
+			if (sid >= 0 && batcher.hasQueued(this))
+				batcher.flushEncodes();  // what was written before the CLOSE goes out first
+			small.encode(session, frame, out);
+			closed = true;
+			return;
+		}
+		boolean queued = sid >= 0 && batcher.hasQueued(this);
+		if (frame.getPayloadLength() < deviceThreshold && !queued) {
+			small.encode(session, frame, out);
+			return;
+		}
+		if (sid < 0)
+			sid = batcher.registerEncoder(this, clientMode);
+		batcher.enqueueEncode(this, frame, clientMode ? RANDOM.nextInt() : 0);
+	}
+
+	/* ---- IEventDrivenCodec: the slot goes back at the session's end ---- */
+
+	@Override
+	public void added(ISession session, ICodecPipeline pipeline) {
+		this.session = (IStreamSession) session;
+	}
+
+	@Override
+	public void event(ISession session, SessionEvent event) {
+		if (event == SessionEvent.ENDING)
+			release();
+	}
+
+	@Override
+	public void removed(ISession session, ICodecPipeline pipeline) {
+		release();
+	}
+
+	private void release() {
+		if (!released) {
+			released = true;
+			if (sid >= 0)
+				batcher.unregisterEncoder(this);
+		}
 	}
 }

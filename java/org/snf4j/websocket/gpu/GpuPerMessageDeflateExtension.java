@@ -1,0 +1,94 @@
+/*
+ * permessage-deflate with the MI355X inflate: PerMessageDeflateExtension
+ * (PerMessageDeflateExtension.java:45-328) negotiates exactly as the reference
+ * (this class delegates offer / acceptOffer / validateResponse / response to it),
+ * and the negotiated extension's updateDecoders puts the reference
+ * PerMessageDeflateDecoder after "ws-decoder" (:316-326), which is then wrapped
+ * in a GpuPerMessageDeflateDecoder under the same key.  The decoder's noContext is
+ * the negotiated one: the client's no_context_takeover for a server, the server's
+ * for a client (:321-325), read back from the response parameters.  Compression
+ * (updateEncoders) is the reference's.
+ */
+package org.snf4j.websocket.gpu;
+
+import java.util.List;
+
+import org.snf4j.core.codec.ICodec;
+import org.snf4j.core.codec.ICodecPipeline;
+import org.snf4j.websocket.extensions.IExtension;
+import org.snf4j.websocket.extensions.InvalidExtensionException;
+import org.snf4j.websocket.extensions.compress.PerMessageDeflateDecoder;
+import org.snf4j.websocket.extensions.compress.PerMessageDeflateExtension;
+
+public class GpuPerMessageDeflateExtension implements IExtension {
+
+	private static final String CLIENT_NO_CONTEXT = "client_no_context_takeover";
+	private static final String SERVER_NO_CONTEXT = "server_no_context_takeover";
+
+	private final PerMessageDeflateExtension delegate;
+	/** null: not negotiated yet; true: the server side (acceptOffer); false: the client side */
+	private final Boolean server;
+
+	public GpuPerMessageDeflateExtension(PerMessageDeflateExtension delegate) {
+		this(delegate, null);
+	}
+
+	public GpuPerMessageDeflateExtension() {
+		this(new PerMessageDeflateExtension(), null);
+	}
+
+	private GpuPerMessageDeflateExtension(PerMessageDeflateExtension delegate, Boolean server) {
+		this.delegate = delegate;
+		this.server = server;
+	}
+
+	@Override
+	public String getName() {
+		return delegate.getName();
+	}
+
+	@Override
+	public Object getGroupId() {
+		return delegate.getGroupId();
+	}
+
+	@Override
+	public IExtension acceptOffer(List<String> offer) throws InvalidExtensionException {
+		IExtension e = delegate.acceptOffer(offer);
+		return e == null ? null : new GpuPerMessageDeflateExtension((PerMessageDeflateExtension) e, Boolean.TRUE);
+	}
+
+	@Override
+	public IExtension validateResponse(List<String> response) throws InvalidExtensionException {
+		IExtension e = delegate.validateResponse(response);
+		return e == null ? null : new GpuPerMessageDeflateExtension((PerMessageDeflateExtension) e, Boolean.FALSE);
+	}
+
+	@Override
+	public List<String> offer() {
+		return delegate.offer();
+	}
+
+	@Override
+	public List<String> response() {
+		return delegate.response();
+	}
+
+	@Override
+	public void updateEncoders(ICodecPipeline pipeline) {
+		delegate.updateEncoders(pipeline);
+	}
+
+	@Override
+	public void updateDecoders(ICodecPipeline pipeline) {
+		delegate.updateDecoders(pipeline);
+		ICodec<?, ?> c = pipeline.get(PerMessageDeflateExtension.PERMESSAGE_DEFLATE_DECODER);
+		if (c instanceof PerMessageDeflateDecoder) {
+			List<String> r = delegate.response();
+			boolean noContext = r.contains(Boolean.TRUE.equals(server) ? CLIENT_NO_CONTEXT : SERVER_NO_CONTEXT);
+			pipeline.replace(PerMessageDeflateExtension.PERMESSAGE_DEFLATE_DECODER,
+					PerMessageDeflateExtension.PERMESSAGE_DEFLATE_DECODER,
+					new GpuPerMessageDeflateDecoder(noContext, (PerMessageDeflateDecoder) c));
+		}
+	}
+}

@@ -37,8 +37,11 @@ public class PinnedByteBufferAllocator extends DefaultAllocator {
 		ByteBuffer b = Wsg.allocPinned(capacity);
 		if (b == null)
 			throw new OutOfMemoryError("wsg_host_alloc(" + capacity + ")");
+		// exactly the requested capacity: DefaultAllocator decides everything from capacity()
+		// (a power-of-two class capacity would make reduce() reallocate on every call).  A slice
+		// from position 0 keeps the pool buffer's address, which release() looks up.
 		b.limit(capacity);
-		return b;
+		return b.slice();
 	}
 
 	/** The replaced buffer goes back to the pool once its bytes are copied. */

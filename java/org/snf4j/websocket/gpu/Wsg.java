@@ -30,7 +30,10 @@ final class Wsg {
 	static final int OK = 0, E_OPCODE = 1, E_RSV = 2, E_MASKING = 3, E_FRAG_CONTROL = 4, E_CONTROL_LEN = 5,
 			E_CLOSE_LEN = 6, E_CONT_OUTSIDE = 7, E_NONCONT_INSIDE = 8, E_MIN_LEN = 9, E_MAX_PAYLOAD = 10,
 			E_TOO_LONG = 11, E_CLOSE_STATUS = 12, E_CLOSE_REASON = 13, E_TEXT_UTF8 = 14, E_NEG_LEN = 15,
-			E_EXT_LEN = 16, E_BATCH = 17;
+			E_EXT_LEN = 16, E_BATCH = 17, E_AGG_TOO_BIG = 18, E_INFLATE = 19, E_INFLATE_NO_DATA = 20;
+
+	/** wsg_frame_desc.flags of a batch with stages: an aggregated message (WSG_OUT_AGGREGATED). */
+	static final int OUT_AGGREGATED = 0x02;
 
 	static final int DESC_BYTES = 16, RESULT_BYTES = 16, STATE_BYTES = 8, ENCODE_FRAME_BYTES = 24;
 
@@ -56,13 +59,16 @@ final class Wsg {
 		case E_TEXT_UTF8: return "Invalid text frame payload: bytes are not UTF-8";
 		case E_NEG_LEN: return "Negative payload length (" + detail + ")";
 		case E_EXT_LEN: return "Extended payload length (" + detail + ") > " + detail2;
+		case E_AGG_TOO_BIG: return "Too big payload for aggregated frame";
+		case E_INFLATE: return "org.snf4j.core.codec.zip.DecompressionException: decompression failure: invalid compressed data format";
+		case E_INFLATE_NO_DATA: return "Inflating of input data produced no data";
 		default: return "Malformed batch (status " + status + ")";
 		}
 	}
 
 	/** The CloseFrame status the reference writes for a status (FrameDecoder.java:92-102). */
 	static int closeCode(int status) {
-		return status == E_CLOSE_REASON || status == E_TEXT_UTF8 ? 1007 : 1002;
+		return status == E_CLOSE_REASON || status == E_TEXT_UTF8 ? 1007 : status == E_AGG_TOO_BIG ? 1009 : 1002;
 	}
 
 	/* ---- context: wsg_open / wsg_reserve / wsg_close / wsg_last_error ---- */
@@ -105,6 +111,36 @@ final class Wsg {
 
 	/** wsg_batcher_session_state into st (8 bytes). */
 	static native int batcherSessionState(long batcher, int sid, byte[] st);
+
+	/** wsg_batcher_session_reset: slot sid for a new session (a fresh decoder and stages). */
+	static native int batcherSessionReset(long batcher, int sid);
+
+	/**
+	 * wsg_batcher_set_stages: the decoders after "ws-decoder" each flush runs in the
+	 * same device batch (PerMessageDeflateDecoder, FrameUtf8Validator, FrameAggregator).
+	 */
+	static native int batcherSetStages(long batcher, boolean inflate, boolean noContext, boolean validate,
+			boolean aggregate, long maxAggregatedLength);
+
+	/* ---- device per selector loop: wsg_device_for_loop / _account / _release_loop ---- */
+	static native int deviceForLoop(long loopId);
+
+	static native int deviceAccount(int device, long wireBytes);
+
+	static native int deviceReleaseLoop(long loopId);
+
+	/* ---- cross-session encode batcher: wsg_enc_batcher_* ---- */
+	static native long encBatcherOpen(long ctx, boolean clientMode, int nSessions);
+
+	static native int encBatcherClose(long batcher);
+
+	/** wsg_enc_batcher_add: Frame(opcode, flags = FIN << 7 | RSV << 4, payload) of session sid; mask big-endian. */
+	static native int encBatcherAdd(long batcher, int sid, int opcode, int flags, int mask, byte[] payload);
+
+	/** wsg_enc_batcher_flush: views = {session_first, wire_off, wire} (valid until the next add / flush). */
+	static native int encBatcherFlush(long batcher, ByteBuffer[] views);
+
+	static native int encBatcherSessionReset(long batcher, int sid);
 
 	/* ---- encode: wsg_encoded_length / wsg_encode_batch_host ---- */
 	static native long encodedLength(int payloadLen, boolean clientMode);

@@ -1,16 +1,28 @@
 /*
- * Cross-session batching of the frame decoder (the host side of the MI355X codec).
+ * Cross-session batching of the frame codec (the host side of the MI355X codec).
  *
- * One WsgBatcher serves the sessions of one selector loop.  GpuFrameDecoder.decode()
- * feeds each session's bytes (wsg_batcher_feed copies them and does the host
- * framing); the first feed of a loop iteration schedules flush() with
- * ISession.executenf (ISession.java:368), so it runs on the loop thread after the
- * iteration's reads: one device batch (wsg_batcher_flush: gather to pinned
- * staging, H2D, decode + UTF-8 kernels, D2H) for every session that read.  The
- * frames then go back to each session on its own loop thread (executenf again)
- * and through the rest of its codec pipeline, as DefaultCodecExecutor.decode
- * (DefaultCodecExecutor.java:557-584) and CodecExecutorAdapter.read
- * (CodecExecutorAdapter.java:228-254) would have passed them.
+ * One WsgBatcher serves the sessions of one selector loop, on that loop's thread.
+ * GpuFrameDecoder.decode() feeds each session's bytes (wsg_batcher_feed copies them
+ * and does the host framing); GpuFrameEncoder.encode() queues each frame
+ * (wsg_enc_batcher_add copies its payload).  The first of either in a loop
+ * iteration schedules flush() with SelectorLoop.executenf, which QUEUES the task
+ * (InternalSelectorLoop.java:1002-1011, 1038-1046) — ISession.executenf would run it
+ * inline on the loop thread (InternalSession.java:720-733) — so the flush runs in the
+ * loop's task phase (InternalSelectorLoop.java:641, 751-758), after every read of
+ * the iteration: one device batch per native batcher for every session that read
+ * (gather to pinned staging, H2D, decode + UTF-8 kernels and the batched stages
+ * after them, D2H), then one encode batch for every session that wrote.  Frames
+ * go back to each session in order, through the rest of its codec pipeline, as
+ * DefaultCodecExecutor.decode (DefaultCodecExecutor.java:557-584) and
+ * CodecExecutorAdapter.read (CodecExecutorAdapter.java:228-254) would have passed
+ * them; encoded bytes are written with session.writenf, which no Frame encoder
+ * accepts, so they go to the socket as they are (DefaultCodecExecutor.java:390-410).
+ *
+ * Session slots are reused: a decoder or encoder registers when its session first
+ * sends or receives data and unregisters at the session's end (IEventDrivenCodec
+ * ENDING / removed), which resets the native slot (wsg_batcher_session_reset,
+ * wsg_enc_batcher_session_reset).  One device per loop: WsgDevices hands the loops
+ * of a process out over the node's GPUs.
  */
 package org.snf4j.websocket.gpu;
 
@@ -18,10 +30,15 @@ import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
 import java.util.ArrayList;
 import java.util.HashMap;
+import java.util.LinkedHashSet;
 import java.util.List;
 import java.util.Map;
+import java.util.Set;
 
-import org.snf4j.core.session.ISession;
+import org.snf4j.core.SelectorLoop;
+import org.snf4j.core.session.IStreamSession;
+import org.snf4j.websocket.frame.AggregatedBinaryFrame;
+import org.snf4j.websocket.frame.AggregatedTextFrame;
 import org.snf4j.websocket.frame.BinaryFrame;
 import org.snf4j.websocket.frame.CloseFrame;
 import org.snf4j.websocket.frame.ContinuationFrame;
@@ -32,16 +49,31 @@ import org.snf4j.websocket.frame.TextFrame;
 
 public final class WsgBatcher {
 
-	/** A decoder configuration (FrameDecoder constructor arguments + fused validation). */
-	private static final class Cfg {
+	/**
+	 * A decoder configuration: FrameDecoder constructor arguments, fused validation and
+	 * the batched stages after the decoder (wsg_batcher_open and wsg_batcher_set_stages
+	 * take one each).
+	 */
+	static final class Cfg {
 		final boolean clientMode, allowExtensions, validate;
 		final int maxPayloadLen;
+		final boolean inflate, noContext, aggregate;
+		final int maxAggregatedLength;
 
-		Cfg(boolean clientMode, boolean allowExtensions, int maxPayloadLen, boolean validate) {
+		Cfg(boolean clientMode, boolean allowExtensions, int maxPayloadLen, boolean validate, boolean inflate,
+				boolean noContext, boolean aggregate, int maxAggregatedLength) {
 			this.clientMode = clientMode;
 			this.allowExtensions = allowExtensions;
 			this.maxPayloadLen = maxPayloadLen;
 			this.validate = validate;
+			this.inflate = inflate;
+			this.noContext = noContext;
+			this.aggregate = aggregate;
+			this.maxAggregatedLength = maxAggregatedLength;
+		}
+
+		boolean hasStages() {
+			return inflate || aggregate;
 		}
 
 		@Override
@@ -50,33 +82,56 @@ public final class WsgBatcher {
 				return false;
 			Cfg c = (Cfg) o;
 			return c.clientMode == clientMode && c.allowExtensions == allowExtensions && c.validate == validate
-					&& c.maxPayloadLen == maxPayloadLen;
+					&& c.maxPayloadLen == maxPayloadLen && c.inflate == inflate && c.noContext == noContext
+					&& c.aggregate == aggregate && c.maxAggregatedLength == maxAggregatedLength;
 		}
 
 		@Override
 		public int hashCode() {
-			return (clientMode ? 1 : 0) | (allowExtensions ? 2 : 0) | (validate ? 4 : 0) | (maxPayloadLen << 3);
+			return (clientMode ? 1 : 0) | (allowExtensions ? 2 : 0) | (validate ? 4 : 0) | (inflate ? 8 : 0)
+					| (noContext ? 16 : 0) | (aggregate ? 32 : 0) | (maxPayloadLen << 6) ^ maxAggregatedLength;
 		}
 	}
 
-	/** One native batcher (wsg_batcher_open takes one configuration) and its sessions. */
+	/** One native decode batcher and the decoders holding its slots. */
 	private final class Native {
 		final long handle;
 		final GpuFrameDecoder[] slots;
-		int used;
-		final List<GpuFrameDecoder> dirty = new ArrayList<GpuFrameDecoder>();
+		int next;
+		final Set<GpuFrameDecoder> dirty = new LinkedHashSet<GpuFrameDecoder>();
 
 		Native(Cfg c) {
 			handle = Wsg.batcherOpen(ctx, c.clientMode, c.allowExtensions, c.maxPayloadLen, c.validate, maxSessions);
 			if (handle == 0)
 				throw new IllegalStateException("wsg_batcher_open: " + Wsg.lastError(ctx));
+			if (c.hasStages() && Wsg.batcherSetStages(handle, c.inflate, c.noContext, c.validate, c.aggregate,
+					c.maxAggregatedLength) != 0)
+				throw new IllegalStateException("wsg_batcher_set_stages: " + Wsg.lastError(ctx));
 			slots = new GpuFrameDecoder[maxSessions];
 		}
 	}
 
+	/** One native encode batcher (wsg_enc_batcher_open takes the client mode). */
+	private final class EncNative {
+		final long handle;
+		final GpuFrameEncoder[] slots;
+		int next;
+		final Set<GpuFrameEncoder> dirty = new LinkedHashSet<GpuFrameEncoder>();
+
+		EncNative(boolean clientMode) {
+			handle = Wsg.encBatcherOpen(ctx, clientMode, maxSessions);
+			if (handle == 0)
+				throw new IllegalStateException("wsg_enc_batcher_open: " + Wsg.lastError(ctx));
+			slots = new GpuFrameEncoder[maxSessions];
+		}
+	}
+
 	final long ctx;
+	final int device;
+	private final SelectorLoop loop;
 	private final int maxSessions;
 	private final Map<Cfg, Native> natives = new HashMap<Cfg, Native>();
+	private final EncNative[] encNatives = new EncNative[2];
 	private boolean flushScheduled;
 	private final Runnable flushTask = new Runnable() {
 		@Override
@@ -86,37 +141,49 @@ public final class WsgBatcher {
 	};
 
 	/**
-	 * @param device      HIP device index
+	 * @param loop        the selector loop whose sessions this batcher serves
+	 * @param device      HIP device index (WsgDevices.deviceFor(loop) spreads loops over the GPUs)
 	 * @param maxSessions sessions of the selector loop
 	 * @param maxFrames   frames a flush may hold (workspace reserved once, wsg_reserve)
 	 * @param maxWireLen  wire bytes a flush may hold
 	 */
-	public WsgBatcher(int device, int maxSessions, long maxFrames, long maxWireLen) {
+	public WsgBatcher(SelectorLoop loop, int device, int maxSessions, long maxFrames, long maxWireLen) {
 		// a flush's payload region is handed to Java as one direct buffer (< 2 GiB)
 		if (maxWireLen + 16 * maxFrames + 16 > Integer.MAX_VALUE)
 			throw new IllegalArgumentException("maxWireLen + 16 * maxFrames must stay below 2 GiB");
+		if (loop == null)
+			throw new IllegalArgumentException("loop is null");
 		ctx = Wsg.open(device);
 		if (ctx == 0)
 			throw new IllegalStateException("wsg_open(" + device + ") failed");
+		this.device = device;
+		this.loop = loop;
 		this.maxSessions = maxSessions;
 		if (Wsg.reserve(ctx, maxFrames, maxSessions, maxWireLen) != 0)
 			throw new IllegalStateException("wsg_reserve: " + Wsg.lastError(ctx));
 	}
 
-	/** A session slot for a new decoder (called from GpuFrameDecoder's constructor). */
-	synchronized int register(GpuFrameDecoder d, boolean clientMode, boolean allowExtensions, int maxPayloadLen,
-			boolean validate) {
-		Cfg c = new Cfg(clientMode, allowExtensions, maxPayloadLen, validate);
+	/** A batcher on the device WsgDevices assigns to the loop. */
+	public WsgBatcher(SelectorLoop loop, int maxSessions, long maxFrames, long maxWireLen) {
+		this(loop, WsgDevices.deviceFor(loop), maxSessions, maxFrames, maxWireLen);
+	}
+
+	/* ------------------------------------------------------------------ decode side */
+
+	/** A session slot for a decoder (at its first decode), in a fresh state. */
+	synchronized int register(GpuFrameDecoder d, Cfg c) {
 		Native n = natives.get(c);
 		if (n == null) {
 			n = new Native(c);
 			natives.put(c, n);
 		}
 		for (int i = 0; i < maxSessions; ++i) {
-			int sid = (n.used + i) % maxSessions;
+			int sid = (n.next + i) % maxSessions;
 			if (n.slots[sid] == null) {
+				if (Wsg.batcherSessionReset(n.handle, sid) != 0)
+					throw new IllegalStateException("wsg_batcher_session_reset: " + sid);
 				n.slots[sid] = d;
-				n.used = sid + 1;
+				n.next = sid + 1;
 				d.nativeBatcher = n.handle;
 				return sid;
 			}
@@ -124,35 +191,104 @@ public final class WsgBatcher {
 		throw new IllegalStateException("no free session slot (maxSessions " + maxSessions + ")");
 	}
 
-	/** The session ended: its slot is free again (its carry state is reset on reuse by the caller). */
+	/** The session ended: its slot is free again, with its bytes and carry dropped. */
 	synchronized void unregister(GpuFrameDecoder d) {
 		for (Native n : natives.values())
-			if (n.handle == d.nativeBatcher && n.slots[d.sid] == d)
+			if (n.handle == d.nativeBatcher && d.sid >= 0 && n.slots[d.sid] == d) {
 				n.slots[d.sid] = null;
+				n.dirty.remove(d);
+				Wsg.batcherSessionReset(n.handle, d.sid);
+			}
 	}
 
 	/** Feed a session's bytes and make sure a flush runs after this loop iteration. */
-	synchronized void enqueue(GpuFrameDecoder d, ISession session, ByteBuffer data) {
+	synchronized void enqueue(GpuFrameDecoder d, ByteBuffer data) {
 		int rc;
 		if (data.hasArray())
 			rc = Wsg.batcherFeedArray(d.nativeBatcher, d.sid, data.array(), data.arrayOffset() + data.position(),
 					data.remaining());
-		else
+		else if (data.isDirect())
 			rc = Wsg.batcherFeed(d.nativeBatcher, d.sid, data, data.position(), data.remaining());
+		else {  // a read-only heap buffer: no array, no address
+			byte[] b = new byte[data.remaining()];
+			data.duplicate().get(b);
+			rc = Wsg.batcherFeedArray(d.nativeBatcher, d.sid, b, 0, b.length);
+		}
 		if (rc != 0)
 			throw new IllegalStateException("wsg_batcher_feed: " + rc);
 		for (Native n : natives.values())
-			if (n.handle == d.nativeBatcher && !n.dirty.contains(d))
+			if (n.handle == d.nativeBatcher)
 				n.dirty.add(d);
+		schedule();
+	}
+
+	/* ------------------------------------------------------------------ encode side */
+
+	synchronized int registerEncoder(GpuFrameEncoder e, boolean clientMode) {
+		int m = clientMode ? 1 : 0;
+		if (encNatives[m] == null)
+			encNatives[m] = new EncNative(clientMode);
+		EncNative n = encNatives[m];
+		for (int i = 0; i < maxSessions; ++i) {
+			int sid = (n.next + i) % maxSessions;
+			if (n.slots[sid] == null) {
+				if (Wsg.encBatcherSessionReset(n.handle, sid) != 0)
+					throw new IllegalStateException("wsg_enc_batcher_session_reset: " + sid);
+				n.slots[sid] = e;
+				n.next = sid + 1;
+				e.nativeBatcher = n.handle;
+				return sid;
+			}
+		}
+		throw new IllegalStateException("no free encoder slot (maxSessions " + maxSessions + ")");
+	}
+
+	synchronized void unregisterEncoder(GpuFrameEncoder e) {
+		for (EncNative n : encNatives)
+			if (n != null && n.handle == e.nativeBatcher && e.sid >= 0 && n.slots[e.sid] == e) {
+				n.slots[e.sid] = null;
+				n.dirty.remove(e);
+				Wsg.encBatcherSessionReset(n.handle, e.sid);
+			}
+	}
+
+	/** Queue a frame of the encoder's session; it is written by the next flush. */
+	synchronized void enqueueEncode(GpuFrameEncoder e, Frame frame, int mask) {
+		int flags = (frame.isFinalFragment() ? 0x80 : 0) | ((frame.getRsvBits() & 7) << 4);
+		int rc = Wsg.encBatcherAdd(e.nativeBatcher, e.sid, frame.getOpcode().value(), flags, mask, frame.getPayload());
+		if (rc != 0)
+			throw new IllegalStateException("wsg_enc_batcher_add: " + rc);
+		for (EncNative n : encNatives)
+			if (n != null && n.handle == e.nativeBatcher)
+				n.dirty.add(e);
+		schedule();
+	}
+
+	/** True if the encoder's session has frames queued (later frames must queue behind them). */
+	synchronized boolean hasQueued(GpuFrameEncoder e) {
+		for (EncNative n : encNatives)
+			if (n != null && n.dirty.contains(e))
+				return true;
+		return false;
+	}
+
+	/* ------------------------------------------------------------------ flush */
+
+	private void schedule() {
 		if (!flushScheduled) {
 			flushScheduled = true;
-			session.executenf(flushTask);
+			loop.executenf(flushTask);  // queued: runs after this iteration's reads
 		}
 	}
 
-	/** One device batch per native batcher; frames go back to their sessions. */
+	/** One device batch per native batcher; frames go back to their sessions, bytes to the sockets. */
 	synchronized void flush() {
 		flushScheduled = false;
+		flushDecodes();
+		flushEncodes();
+	}
+
+	private void flushDecodes() {
 		ByteBuffer[] views = new ByteBuffer[4];
 		long[] counts = new long[2];
 		for (Native n : natives.values()) {
@@ -161,11 +297,14 @@ public final class WsgBatcher {
 			int rc = Wsg.batcherFlush(n.handle, views, counts);
 			if (rc != 0)
 				throw new IllegalStateException("wsg_batcher_flush: " + rc);
+			WsgDevices.account(device, counts[1]);
 			ByteBuffer sf = views[0].order(ByteOrder.LITTLE_ENDIAN);
 			ByteBuffer desc = views[1].order(ByteOrder.LITTLE_ENDIAN);
 			ByteBuffer payload = views[2];
 			ByteBuffer result = views[3].order(ByteOrder.LITTLE_ENDIAN);
-			for (GpuFrameDecoder d : n.dirty) {
+			List<GpuFrameDecoder> ds = new ArrayList<GpuFrameDecoder>(n.dirty);
+			n.dirty.clear();
+			for (GpuFrameDecoder d : ds) {
 				final int first = sf.getInt(4 * d.sid);
 				final int delivered = result.getInt(Wsg.RESULT_BYTES * d.sid);
 				final int error = result.getShort(Wsg.RESULT_BYTES * d.sid + 4) & 0xffff;
@@ -173,16 +312,39 @@ public final class WsgBatcher {
 				final List<Frame> frames = new ArrayList<Frame>(delivered);
 				for (int i = 0; i < delivered; ++i)
 					frames.add(frame(desc, payload, first + i));
-				final GpuFrameDecoder dec = d;
-				// the views are reused by the next flush: frames own byte[] copies (Frame.java:53)
-				d.session().executenf(new Runnable() {
-					@Override
-					public void run() {
-						dec.deliver(frames, error, detail);
-					}
-				});
+				// on the loop thread that owns the session (this batcher's loop); the views are
+				// reused by the next flush, so frames own byte[] copies (Frame.java:53)
+				d.deliver(frames, error, detail);
 			}
+		}
+	}
+
+	/** Encode every queued frame (also called by an encoder before it writes a CLOSE frame). */
+	synchronized void flushEncodes() {
+		ByteBuffer[] views = new ByteBuffer[3];
+		for (EncNative n : encNatives) {
+			if (n == null || n.dirty.isEmpty())
+				continue;
+			int rc = Wsg.encBatcherFlush(n.handle, views);
+			if (rc != 0)
+				throw new IllegalStateException("wsg_enc_batcher_flush: " + rc);
+			ByteBuffer sf = views[0].order(ByteOrder.LITTLE_ENDIAN);
+			ByteBuffer off = views[1].order(ByteOrder.LITTLE_ENDIAN);
+			ByteBuffer wire = views[2];
+			List<GpuFrameEncoder> es = new ArrayList<GpuFrameEncoder>(n.dirty);
 			n.dirty.clear();
+			for (GpuFrameEncoder e : es) {
+				long from = off.getLong(8 * sf.getInt(4 * e.sid)), to = off.getLong(8 * sf.getInt(4 * (e.sid + 1)));
+				int len = (int) (to - from);
+				IStreamSession session = e.session();
+				if (len == 0 || session == null)
+					continue;
+				ByteBuffer out = session.allocate(len);  // FrameEncoder.java:78: the session's allocator
+				ByteBuffer src = wire.duplicate();
+				src.position((int) from).limit((int) to);
+				out.put(src).flip();
+				session.writenf(out);  // no Frame encoder takes a ByteBuffer: straight to the socket
+			}
 		}
 	}
 
@@ -199,6 +361,8 @@ public final class WsgBatcher {
 		ByteBuffer p = payload.duplicate();
 		p.position((int) off);
 		p.get(data);
+		if ((flags & Wsg.OUT_AGGREGATED) != 0)  // FrameAggregator's message (FrameAggregator.java:76-99)
+			return opcode == 1 ? new AggregatedTextFrame(true, rsv, data) : new AggregatedBinaryFrame(true, rsv, data);
 		switch (opcode) {
 		case 0: return new ContinuationFrame(fin, rsv, data);
 		case 1: return new TextFrame(fin, rsv, data);
@@ -214,6 +378,11 @@ public final class WsgBatcher {
 		for (Native n : natives.values())
 			Wsg.batcherClose(n.handle);
 		natives.clear();
+		for (int i = 0; i < encNatives.length; ++i)
+			if (encNatives[i] != null) {
+				Wsg.encBatcherClose(encNatives[i].handle);
+				encNatives[i] = null;
+			}
 		Wsg.close(ctx);
 	}
 }

@@ -106,7 +106,30 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherClose(JNIEnv* env
 
 JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFeed(JNIEnv* env, jclass c, jlong b, jint sid,
                                                                     jobject data, jint off, jint len) {
-    return wsg_batcher_feed(BATCHER(b), (uint32_t)sid, addr(env, data) + off, (uint64_t)len);
+    /* a direct buffer only: a heap buffer has no address (the Java side copies those) */
+    uint8_t* p = addr(env, data);
+    jlong cap = data ? (*env)->GetDirectBufferCapacity(env, data) : -1;
+    if (!p || cap < 0 || off < 0 || len < 0 || (jlong)off + (jlong)len > cap) return WSG_API_EINVAL;
+    return wsg_batcher_feed(BATCHER(b), (uint32_t)sid, p + off, (uint64_t)len);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherSessionReset(JNIEnv* env, jclass c, jlong b,
+                                                                            jint sid) {
+    return wsg_batcher_session_reset(BATCHER(b), (uint32_t)sid);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherSetStages(JNIEnv* env, jclass c, jlong b,
+                                                                         jboolean inflate, jboolean no_context,
+                                                                         jboolean validate, jboolean aggregate,
+                                                                         jlong max_aggregated) {
+    wsg_stage_cfg st;
+    memset(&st, 0, sizeof st);
+    st.inflate = inflate ? 1 : 0;
+    st.inflate_no_context = no_context ? 1 : 0;
+    st.validate = validate ? 1 : 0;
+    st.aggregate = aggregate ? 1 : 0;
+    st.max_aggregated_len = (int64_t)max_aggregated;
+    return wsg_batcher_set_stages(BATCHER(b), &st);
 }
 
 JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFeedArray(JNIEnv* env, jclass c, jlong b, jint sid,
@@ -151,6 +174,70 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherSessionState(JNIE
     int rc = wsg_batcher_session_state(BATCHER(b), (uint32_t)sid, &s);
     if (rc == WSG_API_OK) (*env)->SetByteArrayRegion(env, st, 0, sizeof s, (const jbyte*)&s);
     return rc;
+}
+
+/* ---- device per selector loop ---- */
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_deviceForLoop(JNIEnv* env, jclass c, jlong loop) {
+    return wsg_device_for_loop((uint64_t)loop);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_deviceAccount(JNIEnv* env, jclass c, jint device,
+                                                                      jlong bytes) {
+    return wsg_device_account(device, (uint64_t)bytes);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_deviceReleaseLoop(JNIEnv* env, jclass c, jlong loop) {
+    return wsg_device_release_loop((uint64_t)loop);
+}
+
+/* ---- cross-session encode batcher ---- */
+#define ENC_BATCHER(x) ((wsg_enc_batcher*)(intptr_t)(x))
+
+JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherOpen(JNIEnv* env, jclass c, jlong ctx,
+                                                                        jboolean client, jint sessions) {
+    wsg_enc_batcher* b = NULL;
+    return wsg_enc_batcher_open(CTX(ctx), client ? 1 : 0, (uint32_t)sessions, &b) == WSG_API_OK ? (jlong)(intptr_t)b
+                                                                                                  : 0;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherClose(JNIEnv* env, jclass c, jlong b) {
+    return wsg_enc_batcher_close(ENC_BATCHER(b));
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherAdd(JNIEnv* env, jclass c, jlong b, jint sid,
+                                                                      jint opcode, jint flags, jint mask,
+                                                                      jbyteArray payload) {
+    uint8_t m[4] = {(uint8_t)(mask >> 24), (uint8_t)(mask >> 16), (uint8_t)(mask >> 8), (uint8_t)mask};
+    jsize n = payload ? (*env)->GetArrayLength(env, payload) : 0;
+    /* the batcher copies the payload into its pinned arena */
+    jbyte* p = n ? (jbyte*)(*env)->GetPrimitiveArrayCritical(env, payload, NULL) : NULL;
+    if (n && !p) return WSG_API_ENOMEM;
+    int rc = wsg_enc_batcher_add(ENC_BATCHER(b), (uint32_t)sid, (uint8_t)opcode, (uint8_t)flags, m,
+                                 (const uint8_t*)p, (uint32_t)n);
+    if (p) (*env)->ReleasePrimitiveArrayCritical(env, payload, p, JNI_ABORT);
+    return rc;
+}
+
+/* views[0] = session_first, views[1] = wire_off, views[2] = wire (valid until the next add/flush) */
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherFlush(JNIEnv* env, jclass c, jlong b,
+                                                                        jobjectArray views) {
+    wsg_enc_view v;
+    int rc = wsg_enc_batcher_flush(ENC_BATCHER(b), &v);
+    if (rc != WSG_API_OK) return rc;
+    (*env)->SetObjectArrayElement(env, views, 0,
+                                  (*env)->NewDirectByteBuffer(env, (void*)v.session_first,
+                                                              (jlong)(v.n_sessions + 1) * sizeof(uint32_t)));
+    (*env)->SetObjectArrayElement(env, views, 1,
+                                  (*env)->NewDirectByteBuffer(env, (void*)v.wire_off,
+                                                              (jlong)(v.n_frames + 1) * sizeof(uint64_t)));
+    (*env)->SetObjectArrayElement(env, views, 2,
+                                  (*env)->NewDirectByteBuffer(env, (void*)v.wire, (jlong)v.wire_bytes));
+    return WSG_API_OK;
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherSessionReset(JNIEnv* env, jclass c, jlong b,
+                                                                               jint sid) {
+    return wsg_enc_batcher_session_reset(ENC_BATCHER(b), (uint32_t)sid);
 }
 
 /* ---- encode ---- */

@@ -7,15 +7,15 @@ C ABI declared in include/wsgpu.h.  This package is the host-side mirror of the
 reference's codec interface over that ABI.
 """
 from . import _lib  # noqa: F401  (fails loudly if libwsgpu.so is missing)
-from .codec import (BatchAggregator, BatchInflater, FrameAggregator, FrameDecoder, FrameEncoder, FrameUtf8Validator,
-                    NativeBatcher, PerMessageDeflateDecoder, SessionBatcher)
+from .codec import (BatchAggregator, BatchInflater, EncodeBatcher, FrameAggregator, FrameDecoder, FrameEncoder,
+                    FrameUtf8Validator, NativeBatcher, PerMessageDeflateDecoder, SessionBatcher)
 from .context import Context, decoder_cfg, encoded_length, error_message, frame_available
 from .handshake import (BatchClientHandshaker, BatchHandshaker, ClientConfig, ClientHandshakeOutcome, HandshakeConfig,
                         HandshakeOutcome)
 from .frame import (AggregatedBinaryFrame, AggregatedTextFrame, BinaryFrame, CloseFrame, ContinuationFrame, Frame,
                     InvalidFrameException, Opcode, PingFrame, PongFrame, TextFrame)
 
-__all__ = ["Context", "FrameDecoder", "FrameEncoder", "SessionBatcher", "FrameAggregator", "BatchAggregator",
+__all__ = ["Context", "FrameDecoder", "FrameEncoder", "EncodeBatcher", "SessionBatcher", "FrameAggregator", "BatchAggregator",
            "FrameUtf8Validator", "NativeBatcher", "BatchInflater", "PerMessageDeflateDecoder",
            "AggregatedTextFrame", "AggregatedBinaryFrame", "decoder_cfg", "encoded_length",
            "error_message", "frame_available",

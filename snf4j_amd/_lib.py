@@ -45,6 +45,17 @@ class BatchView(C.Structure):
                 ("payload", C.c_void_p), ("result", C.c_void_p)]
 
 
+class StageCfg(C.Structure):
+    _fields_ = [("inflate", C.c_uint8), ("inflate_no_context", C.c_uint8), ("validate", C.c_uint8),
+                ("aggregate", C.c_uint8), ("reserved", C.c_uint32), ("max_aggregated_len", C.c_int64)]
+
+
+class EncView(C.Structure):
+    _fields_ = [("n_frames", C.c_uint64), ("wire_bytes", C.c_uint64), ("n_sessions", C.c_uint32),
+                ("reserved", C.c_uint32), ("session_first", C.c_void_p), ("wire_off", C.c_void_p),
+                ("wire", C.c_void_p)]
+
+
 class EncodeFrame(C.Structure):
     _fields_ = [("payload_off", C.c_uint64), ("payload_len", C.c_uint32), ("opcode", C.c_uint8),
                 ("flags", C.c_uint8), ("reserved", C.c_uint8 * 2), ("mask", C.c_uint8 * 4),
@@ -133,6 +144,17 @@ def _load():
         "wsg_batcher_flush": ([p, P(BatchView)], i32),
         "wsg_batcher_session_state": ([p, u32, P(SessionState)], i32),
         "wsg_batcher_session_reset": ([p, u32], i32),
+        "wsg_batcher_set_stages": ([p, P(StageCfg)], i32),
+        "wsg_device_policy_init": ([i32], i32),
+        "wsg_device_for_loop": ([u64], i32),
+        "wsg_device_account": ([i32, u64], i32),
+        "wsg_device_release_loop": ([u64], i32),
+        "wsg_enc_batcher_open": ([p, i32, u32, P(p)], i32),
+        "wsg_enc_batcher_close": ([p], i32),
+        "wsg_enc_batcher_last_error": ([p], C.c_char_p),
+        "wsg_enc_batcher_add": ([p, u32, C.c_uint8, C.c_uint8, p, p, u32], i32),
+        "wsg_enc_batcher_flush": ([p, P(EncView)], i32),
+        "wsg_enc_batcher_session_reset": ([p, u32], i32),
         "wsg_host_alloc": ([u64], p),
         "wsg_host_release": ([p], i32),
         "wsg_host_capacity": ([p], u64),

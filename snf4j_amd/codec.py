@@ -442,6 +442,16 @@ class NativeBatcher:
         if a.size:
             self._check(lib.wsg_batcher_feed(self._h, int(sid), a.ctypes.data, a.size))
 
+    def set_stages(self, inflate: bool = False, noContext: bool = False, validate: bool = True,
+                   aggregate: bool = False, maxAggregatedLength: int = 0):
+        """The decoders after "ws-decoder" that each flush runs in the same device batch
+        (wsg_batcher_set_stages): PerMessageDeflateDecoder(noContext) -> FrameUtf8Validator
+        -> FrameAggregator(maxAggregatedLength), as the pipeline orders them."""
+        import ctypes as C
+        from ._lib import StageCfg, lib
+        c = StageCfg(int(inflate), int(noContext), int(validate), int(aggregate), 0, int(maxAggregatedLength))
+        self._check(lib.wsg_batcher_set_stages(self._h, C.byref(c)))
+
     def reset_session(self, sid: int):
         """Hand slot `sid` to a new session (wsg_batcher_session_reset): the partial
         frame and the carry are dropped, as a fresh FrameDecoder would start."""
@@ -480,14 +490,77 @@ class NativeBatcher:
             for k in range(int(sf[s]), int(sf[s]) + int(r["n_delivered"])):
                 d = desc[k]
                 o, ln = int(d["payload_off"]), int(d["payload_len"])
-                frames.append(make_frame(int(d["opcode"]), bool(d["flags"] & 0x80), (int(d["flags"]) >> 4) & 7,
-                                         payload[o:o + ln].tobytes()))
+                data, rsv = payload[o:o + ln].tobytes(), (int(d["flags"]) >> 4) & 7
+                if int(d["flags"]) & AGG_IN_AGG:  # WSG_OUT_AGGREGATED: a FrameAggregator message
+                    cls = AggregatedTextFrame if int(d["opcode"]) == 1 else AggregatedBinaryFrame
+                    frames.append(cls(rsv, data, [data]))
+                else:
+                    frames.append(make_frame(int(d["opcode"]), bool(d["flags"] & 0x80), rsv, data))
             exc = None
             if r["error"]:
                 exc = InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
                 exc.close_code = int(r["close_code"])
             out.append((frames, exc))
         return out
+
+
+class EncodeBatcher:
+    """The native cross-session encode batcher (wsg_enc_batcher_*, batcher.hip):
+    FrameEncoder.encode (FrameEncoder.java:69-120) for every session of a loop in
+    one device batch per flush.  add() queues a frame (the payload is copied to a
+    pinned arena); flush() returns each session's wire bytes, its frames in the
+    order they were added, with the close latch (:71-76) kept across flushes."""
+
+    def __init__(self, n_sessions: int, clientMode: bool, ctx: Context | None = None):
+        from ._lib import check, lib
+        import ctypes as C
+        self.ctx = ctx or default_context()
+        self.n = n_sessions
+        h = C.c_void_p()
+        check(lib.wsg_enc_batcher_open(self.ctx._h, int(bool(clientMode)), n_sessions, C.byref(h)), self.ctx._h)
+        self._h = h
+
+    def close(self):
+        from ._lib import lib
+        if getattr(self, "_h", None):
+            lib.wsg_enc_batcher_close(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        from ._lib import WsgError, lib
+        if rc != 0:
+            raise WsgError(f"libwsgpu encode batcher error {rc}: {lib.wsg_enc_batcher_last_error(self._h).decode()}")
+
+    def add(self, sid: int, frame: Frame, mask=(0, 0, 0, 0)):
+        from ._lib import lib
+        p = np.frombuffer(bytes(frame.getPayload()), dtype=np.uint8)
+        m = np.asarray(mask, dtype=np.uint8)
+        flags = (0x80 if frame.isFinalFragment() else 0) | ((frame.getRsvBits() & 7) << 4)
+        self._check(lib.wsg_enc_batcher_add(self._h, int(sid), int(frame.getOpcode()), flags, m.ctypes.data,
+                                            p.ctypes.data if p.size else None, int(p.size)))
+
+    def reset_session(self, sid: int):
+        from ._lib import lib
+        self._check(lib.wsg_enc_batcher_session_reset(self._h, int(sid)))
+
+    def flush(self):
+        """[wire bytes of session s] (its frames back to back)."""
+        import ctypes as C
+        from ._lib import EncView, lib
+        v = EncView()
+        self._check(lib.wsg_enc_batcher_flush(self._h, C.byref(v)))
+        n, s = int(v.n_frames), int(v.n_sessions)
+        sf = np.ctypeslib.as_array((C.c_uint32 * (s + 1)).from_address(v.session_first))
+        off = np.ctypeslib.as_array((C.c_uint64 * (n + 1)).from_address(v.wire_off))
+        wire = (C.c_uint8 * int(v.wire_bytes)).from_address(v.wire) if v.wire_bytes else b""
+        wb = bytes(wire)
+        return [wb[int(off[sf[i]]):int(off[sf[i + 1]])] for i in range(s)]
 
 
 def pinned_alloc(capacity: int):

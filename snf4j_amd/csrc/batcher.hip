@@ -75,6 +75,23 @@ uint64_t frame_total(const uint8_t* p) {
 
 }  // namespace
 
+// The decoders after "ws-decoder" that run in the same flush (wsg_batcher_set_stages):
+// per session, what each stage keeps between batches.
+struct StageSess {
+  std::vector<wsg_frame_desc> held_desc;  // inflate: frames of a compressed message a batch left open
+  std::vector<uint8_t> held_bytes;        //   (their payloads; re-sent with WSG_DESC_REPLAY)
+  std::vector<uint8_t> agg_held;          // aggregator: bytes of a message still open (PayloadAggregator)
+  bool agg_held_valid = false;
+};
+
+// One stage's input or output: per-session frames with their payloads.
+struct StageBatch {
+  std::vector<uint32_t> sf;             // [S + 1]
+  std::vector<wsg_frame_desc> desc;     // payload_off into pay (16-B aligned slots)
+  std::vector<uint8_t> pay;
+  std::vector<uint32_t> n_ok;           // [S] frames of the session that go on (<= its count)
+};
+
 struct wsg_batcher {
   wsg_ctx* ctx = nullptr;
   wsg_decoder_cfg cfg{};
@@ -84,6 +101,16 @@ struct wsg_batcher {
   PinnedBuf wire, off, sf, st, payload, desc, result;
   uint32_t threads = 8;
   std::string err;
+  // stages after the decoder (wsg_batcher_set_stages)
+  wsg_stage_cfg stages{};
+  bool has_stages = false;
+  std::vector<StageSess> ss;
+  std::vector<wsg_inflate_state> istate;
+  std::vector<uint8_t> iwin;
+  std::vector<wsg_session_state> vstate;
+  std::vector<wsg_agg_state> astate;
+  StageBatch fin;                       // the flush's output when stages run
+  std::vector<wsg_session_result> fres;
 };
 
 static int bset(wsg_batcher* b, int code, const char* msg) {
@@ -96,6 +123,274 @@ static int bset(wsg_batcher* b, int code, const char* msg) {
     hipError_t _e = (expr);                                                      \
     if (_e != hipSuccess) return bset((b), WSG_API_EHIP, hipGetErrorString(_e)); \
   } while (0)
+
+// ------------------------------------------------------------------ stages after the decoder
+static inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
+
+// append one frame (descriptor + payload bytes) to a stage batch
+static void push_frame(StageBatch& o, wsg_frame_desc d, const uint8_t* bytes) {
+  const uint64_t pos = o.pay.size();
+  d.payload_off = pos;
+  o.pay.resize(pos + al16(d.payload_len));
+  if (d.payload_len) memcpy(o.pay.data() + pos, bytes, d.payload_len);
+  o.desc.push_back(d);
+}
+
+// the decoder's delivered frames, per session
+static void stage_input(StageBatch& o, uint32_t S, const uint32_t* sf, const wsg_frame_desc* desc, const uint8_t* pay,
+                        const wsg_session_result* res) {
+  o.sf.assign(S + 1, 0);
+  o.n_ok.assign(S, 0);
+  o.desc.clear();
+  o.pay.clear();
+  uint64_t bytes = 0;
+  for (uint32_t s = 0; s < S; ++s)
+    for (uint32_t k = sf[s]; k < sf[s] + res[s].n_delivered; ++k) bytes += al16(desc[k].payload_len);
+  o.pay.reserve(bytes + 16);
+  for (uint32_t s = 0; s < S; ++s) {
+    o.sf[s] = (uint32_t)o.desc.size();
+    for (uint32_t k = sf[s]; k < sf[s] + res[s].n_delivered; ++k) {
+      wsg_frame_desc d = desc[k];
+      d.flags &= 0xf0u | 0x80u;  // FIN, RSV (the "was masked" bit is the decoder's)
+      push_frame(o, d, pay + desc[k].payload_off);
+    }
+    o.n_ok[s] = res[s].n_delivered;
+  }
+  o.sf[S] = (uint32_t)o.desc.size();
+}
+
+// a later stage failed session s: its result, and the session is closed
+static void stage_fail(wsg_batcher* b, uint32_t s, const wsg_session_result& r) {
+  b->fres[s].error = r.error;
+  b->fres[s].close_code = r.close_code;
+  b->fres[s].detail = r.detail;
+  b->state[s].closed = 1;
+}
+
+// PerMessageDeflateDecoder over `in` (PerMessageDeflateDecoder.java:68-105): sessions
+// with new frames, each after the frames of a message it left open; a session whose
+// output region overflows is run again with a larger one (nothing of it is committed).
+static int stage_inflate(wsg_batcher* b, const StageBatch& in, StageBatch& out) {
+  const uint32_t S = b->n;
+  std::vector<std::vector<wsg_frame_desc>> od(S);
+  std::vector<std::vector<uint8_t>> op(S);
+  std::vector<uint32_t> todo;
+  std::vector<uint64_t> cap(S, 0);
+  for (uint32_t s = 0; s < S; ++s) {
+    if (in.sf[s + 1] == in.sf[s]) continue;
+    todo.push_back(s);
+    uint64_t c = b->ss[s].held_bytes.size();
+    for (uint32_t k = in.sf[s]; k < in.sf[s + 1]; ++k) c += in.desc[k].payload_len + 4;
+    cap[s] = 65536 + 16 * c;
+  }
+  while (!todo.empty()) {
+    const uint32_t T = (uint32_t)todo.size();
+    StageBatch x;
+    x.sf.push_back(0);
+    std::vector<wsg_inflate_state> st(T);
+    std::vector<uint8_t> win((uint64_t)T * WSG_INFLATE_WINDOW);
+    std::vector<uint64_t> oo(T + 1, 0);
+    for (uint32_t i = 0; i < T; ++i) {
+      const uint32_t s = todo[i];
+      const StageSess& h = b->ss[s];
+      for (const wsg_frame_desc& hd : h.held_desc) {
+        wsg_frame_desc d = hd;
+        d.flags |= WSG_DESC_REPLAY;
+        push_frame(x, d, h.held_bytes.data() + hd.payload_off);
+      }
+      for (uint32_t k = in.sf[s]; k < in.sf[s + 1]; ++k) {
+        wsg_frame_desc d = in.desc[k];
+        d.flags &= (uint8_t)~WSG_DESC_REPLAY;
+        push_frame(x, d, in.pay.data() + in.desc[k].payload_off);
+      }
+      x.sf.push_back((uint32_t)x.desc.size());
+      st[i] = b->istate[s];
+      memcpy(win.data() + (uint64_t)i * WSG_INFLATE_WINDOW, b->iwin.data() + (uint64_t)s * WSG_INFLATE_WINDOW,
+             WSG_INFLATE_WINDOW);
+      oo[i + 1] = oo[i] + cap[s];
+    }
+    x.pay.resize(x.pay.size() + 16);
+    const uint64_t F = x.desc.size();
+    std::vector<uint8_t> ob(oo[T] + 32);
+    std::vector<wsg_frame_desc> odesc(F + 1);
+    std::vector<wsg_session_result> r(T);
+    std::vector<uint32_t> rf(T);
+    int rc = wsg_inflate_batch_host(b->ctx, b->stages.inflate_no_context, x.desc.data(), F, x.sf.data(), T,
+                                    x.pay.data(), x.pay.size(), st.data(), win.data(), ob.data(), oo.data(),
+                                    odesc.data(), r.data(), rf.data());
+    if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+    std::vector<uint32_t> retry;
+    for (uint32_t i = 0; i < T; ++i) {
+      const uint32_t s = todo[i];
+      if (r[i].error == WSG_E_INFLATE_CAPACITY) {
+        cap[s] *= 8;
+        retry.push_back(s);
+        continue;
+      }
+      b->istate[s] = st[i];
+      memcpy(b->iwin.data() + (uint64_t)s * WSG_INFLATE_WINDOW, win.data() + (uint64_t)i * WSG_INFLATE_WINDOW,
+             WSG_INFLATE_WINDOW);
+      StageSess& h = b->ss[s];
+      const uint32_t nheld = (uint32_t)h.held_desc.size();
+      uint32_t j = 0;
+      for (uint32_t k = x.sf[i] + nheld; k < x.sf[i + 1] && j < r[i].n_delivered; ++k, ++j) {
+        wsg_frame_desc d = odesc[k];
+        const bool infl = (d.flags & WSG_DESC_INFLATED) != 0;
+        const uint8_t* src = infl ? ob.data() + d.payload_off : x.pay.data() + x.desc[k].payload_off;
+        d.flags &= 0xf0u | 0x80u;
+        const uint64_t pos = op[s].size();
+        op[s].resize(pos + al16(d.payload_len));
+        if (d.payload_len) memcpy(op[s].data() + pos, src, d.payload_len);
+        d.payload_off = pos;
+        od[s].push_back(d);
+      }
+      std::vector<wsg_frame_desc> nhd;
+      std::vector<uint8_t> nhb;
+      if (r[i].error) {
+        stage_fail(b, s, r[i]);
+      } else if (rf[i] != 0xFFFFFFFFu) {  // a message left open: its frames go again with the next batch
+        for (uint32_t k = x.sf[i] + rf[i]; k < x.sf[i + 1]; ++k) {
+          wsg_frame_desc d = x.desc[k];
+          d.flags &= (uint8_t)~WSG_DESC_REPLAY;
+          const uint64_t pos = nhb.size();
+          nhb.resize(pos + d.payload_len);
+          if (d.payload_len) memcpy(nhb.data() + pos, x.pay.data() + x.desc[k].payload_off, d.payload_len);
+          d.payload_off = pos;
+          nhd.push_back(d);
+        }
+      }
+      h.held_desc.swap(nhd);
+      h.held_bytes.swap(nhb);
+    }
+    todo.swap(retry);
+  }
+  out.sf.assign(S + 1, 0);
+  out.n_ok.assign(S, 0);
+  out.desc.clear();
+  out.pay.clear();
+  for (uint32_t s = 0; s < S; ++s) {
+    out.sf[s] = (uint32_t)out.desc.size();
+    const uint64_t base = out.pay.size();
+    out.pay.insert(out.pay.end(), op[s].begin(), op[s].end());
+    for (wsg_frame_desc d : od[s]) {
+      d.payload_off += base;
+      out.desc.push_back(d);
+    }
+    out.n_ok[s] = (uint32_t)od[s].size();
+  }
+  out.sf[S] = (uint32_t)out.desc.size();
+  return WSG_API_OK;
+}
+
+// FrameUtf8Validator over `io` (FrameUtf8Validator.java:59-98): the frames a
+// session passes before its first failure go on.
+static int stage_validate(wsg_batcher* b, StageBatch& io) {
+  const uint32_t S = b->n;
+  if (io.pay.size() < 16) io.pay.resize(16);
+  std::vector<wsg_session_result> r(S);
+  int rc = wsg_validate_batch_host(b->ctx, io.desc.data(), io.desc.size(), io.sf.data(), S, io.pay.data(),
+                                   io.pay.size(), b->vstate.data(), r.data());
+  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  for (uint32_t s = 0; s < S; ++s) {
+    io.n_ok[s] = std::min(io.n_ok[s], r[s].n_delivered);
+    if (r[s].error) stage_fail(b, s, r[s]);
+  }
+  return WSG_API_OK;
+}
+
+// FrameAggregator over `in` (FrameAggregator.java:72-104) into `out`: pass-through
+// frames keep their bytes, an aggregated message is its held bytes (earlier
+// batches, PayloadAggregator.java:34) + this batch's.
+static int stage_aggregate(wsg_batcher* b, const StageBatch& in, StageBatch& out) {
+  const uint32_t S = b->n;
+  const uint64_t F = in.desc.size();
+  std::vector<wsg_session_result> dres(S);
+  for (uint32_t s = 0; s < S; ++s) dres[s].n_delivered = in.n_ok[s];
+  std::vector<uint8_t> pay(in.pay);
+  pay.resize(pay.size() + 16);
+  const uint64_t cap = pay.size();
+  std::vector<uint8_t> ab(cap + 32);
+  std::vector<wsg_frame_desc> odesc(F + S + 1);
+  std::vector<wsg_session_result> r(S);
+  uint64_t tot = 0;
+  int rc = wsg_aggregate_batch_host(b->ctx, b->stages.max_aggregated_len, in.desc.data(), F, in.sf.data(), S,
+                                    dres.data(), pay.data(), pay.size(), b->astate.data(), ab.data(), cap,
+                                    odesc.data(), r.data(), &tot);
+  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  out.sf.assign(S + 1, 0);
+  out.n_ok.assign(S, 0);
+  out.desc.clear();
+  out.pay.clear();
+  for (uint32_t s = 0; s < S; ++s) {
+    out.sf[s] = (uint32_t)out.desc.size();
+    StageSess& h = b->ss[s];
+    const uint64_t base = (uint64_t)in.sf[s] + s;
+    for (uint32_t i = 0; i < r[s].n_delivered; ++i) {
+      wsg_frame_desc d = odesc[base + i];
+      if (d.flags & WSG_AGG_IN_AGG) {
+        std::vector<uint8_t> m;
+        if ((d.flags & WSG_AGG_PREFIXED) && h.agg_held_valid) m = h.agg_held;
+        m.insert(m.end(), ab.data() + d.payload_off, ab.data() + d.payload_off + d.payload_len);
+        h.agg_held.clear();
+        h.agg_held_valid = false;
+        d.flags = (uint8_t)((d.flags & 0xf0u) | 0x80u | WSG_OUT_AGGREGATED);
+        d.payload_len = (uint32_t)m.size();
+        push_frame(out, d, m.data());
+      } else {
+        d.flags &= 0xf0u | 0x80u;
+        push_frame(out, d, pay.data() + d.payload_off);
+      }
+    }
+    out.n_ok[s] = r[s].n_delivered;
+    if (r[s].error) {
+      stage_fail(b, s, r[s]);
+      h.agg_held.clear();
+      h.agg_held_valid = false;
+    } else if (b->astate[s].open) {  // this batch's bytes of the message still open
+      const wsg_frame_desc& d = odesc[base + r[s].n_delivered];
+      if (!((d.flags & WSG_AGG_PREFIXED) && h.agg_held_valid)) h.agg_held.clear();
+      h.agg_held.insert(h.agg_held.end(), ab.data() + d.payload_off, ab.data() + d.payload_off + d.payload_len);
+      h.agg_held_valid = true;
+    } else {
+      h.agg_held.clear();
+      h.agg_held_valid = false;
+    }
+  }
+  out.sf[S] = (uint32_t)out.desc.size();
+  return WSG_API_OK;
+}
+
+static int run_stages(wsg_batcher* b, const uint32_t* sf, const wsg_frame_desc* desc, const uint8_t* pay,
+                      const wsg_session_result* res) {
+  const uint32_t S = b->n;
+  b->fres.assign(res, res + S);
+  StageBatch a, t;
+  stage_input(a, S, sf, desc, pay, res);
+  int rc;
+  if (b->stages.inflate) {
+    if ((rc = stage_inflate(b, a, t))) return rc;
+    a.sf.swap(t.sf); a.desc.swap(t.desc); a.pay.swap(t.pay); a.n_ok.swap(t.n_ok);
+    if (b->stages.validate && (rc = stage_validate(b, a))) return rc;
+  }
+  if (b->stages.aggregate) {
+    if ((rc = stage_aggregate(b, a, t))) return rc;
+    a.sf.swap(t.sf); a.desc.swap(t.desc); a.pay.swap(t.pay); a.n_ok.swap(t.n_ok);
+  }
+  // the output: each session's frames that went through every stage
+  StageBatch& f = b->fin;
+  f.sf.assign(S + 1, 0);
+  f.desc.clear();
+  f.pay.clear();
+  f.pay.reserve(a.pay.size() + 16);
+  for (uint32_t s = 0; s < S; ++s) {
+    f.sf[s] = (uint32_t)f.desc.size();
+    for (uint32_t k = a.sf[s]; k < a.sf[s] + a.n_ok[s]; ++k) push_frame(f, a.desc[k], a.pay.data() + a.desc[k].payload_off);
+    b->fres[s].n_delivered = (uint32_t)f.desc.size() - f.sf[s];
+  }
+  f.sf[S] = (uint32_t)f.desc.size();
+  f.pay.resize(f.pay.size() + 16);
+  return WSG_API_OK;
+}
 
 extern "C" {
 
@@ -253,6 +548,38 @@ int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out) {
   out->desc = (const wsg_frame_desc*)b->desc.p;
   out->payload = b->payload.p;
   out->result = res;
+  if (!b->has_stages) return WSG_API_OK;
+  const int rc2 = run_stages(b, sf, (const wsg_frame_desc*)b->desc.p, b->payload.p, res);
+  if (rc2) return rc2;
+  for (uint32_t i = 0; i < S; ++i)
+    if (b->state[i].closed) {  // a stage failed it: the session swallows further input
+      std::vector<uint8_t>().swap(b->s[i].buf);
+      b->s[i].host_err = 0;
+      b->s[i].complete = 0;
+      b->s[i].lens.clear();
+    }
+  out->n_frames = b->fin.desc.size();
+  out->session_first = b->fin.sf.data();
+  out->desc = b->fin.desc.data();
+  out->payload = b->fin.pay.data();
+  out->result = b->fres.data();
+  return WSG_API_OK;
+}
+
+int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
+  if (!b || !stages) return WSG_API_EINVAL;
+  if (stages->aggregate && stages->max_aggregated_len < 0) return bset(b, WSG_API_EINVAL, "max_aggregated_len < 0");
+  b->stages = *stages;
+  b->has_stages = stages->inflate || stages->aggregate;
+  // with inflate the text is validated after it (PerMessageDeflateExtension.java:316-326);
+  // without, the validator is the fused check
+  b->cfg.validate_utf8 = stages->inflate ? 0 : (stages->validate ? 1 : 0);
+  const uint32_t S = b->n;
+  b->ss.assign(S, StageSess{});
+  b->istate.assign(S, wsg_inflate_state{});
+  b->iwin.assign((uint64_t)S * WSG_INFLATE_WINDOW, 0);
+  b->vstate.assign(S, wsg_session_state{});
+  b->astate.assign(S, wsg_agg_state{});
   return WSG_API_OK;
 }
 
@@ -276,6 +603,13 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
   x.host_err = 0;
   x.d1 = 0;
   b->state[sid] = wsg_session_state{};
+  if (b->has_stages) {  // fresh stage decoders too
+    b->ss[sid] = StageSess{};
+    b->istate[sid] = wsg_inflate_state{};
+    memset(b->iwin.data() + (uint64_t)sid * WSG_INFLATE_WINDOW, 0, WSG_INFLATE_WINDOW);
+    b->vstate[sid] = wsg_session_state{};
+    b->astate[sid] = wsg_agg_state{};
+  }
   return WSG_API_OK;
 }
 
@@ -304,6 +638,11 @@ static int eset(wsg_enc_batcher* b, int code, const char* msg) {
   if (b) b->err = msg ? msg : "";
   return code;
 }
+#define E_TRY(b, expr)                                                           \
+  do {                                                                           \
+    hipError_t _e = (expr);                                                      \
+    if (_e != hipSuccess) return eset((b), WSG_API_EHIP, hipGetErrorString(_e)); \
+  } while (0)
 
 int wsg_enc_batcher_open(wsg_ctx* ctx, int client_mode, uint32_t n_sessions, wsg_enc_batcher** out) {
   if (!ctx || !out) return WSG_API_EINVAL;
@@ -359,10 +698,10 @@ int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out) {
   if (!b || !out) return WSG_API_EINVAL;
   const uint32_t S = b->n;
   const uint64_t F = b->rec.size();
-  B_TRY(b, b->frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
-  B_TRY(b, b->sf.ensure((S + 1) * sizeof(uint32_t)));
-  B_TRY(b, b->cl.ensure(S + 1));
-  B_TRY(b, b->off.ensure((F + 1) * sizeof(uint64_t)));
+  E_TRY(b, b->frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
+  E_TRY(b, b->sf.ensure((S + 1) * sizeof(uint32_t)));
+  E_TRY(b, b->cl.ensure(S + 1));
+  E_TRY(b, b->off.ensure((F + 1) * sizeof(uint64_t)));
   uint32_t* sf = (uint32_t*)b->sf.p;
   sf[0] = 0;
   for (uint32_t i = 0; i < S; ++i) sf[i + 1] = sf[i] + b->count[i];
@@ -373,7 +712,7 @@ int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out) {
   }
   uint64_t need = 0;
   for (uint64_t k = 0; k < F; ++k) need += wsg_encoded_length(b->rec[k].payload_len, b->client);
-  B_TRY(b, b->wire.ensure(need + 32));
+  E_TRY(b, b->wire.ensure(need + 32));
   if (S) memcpy(b->cl.p, b->closed.data(), S);
   int rc = wsg_encode_batch_host(b->ctx, b->client, b->arena.p, b->arena_len, (const wsg_encode_frame*)b->frames.p, F,
                                  sf, S, b->cl.p, b->wire.p, b->wire.n, (uint64_t*)b->off.p);
@@ -408,6 +747,64 @@ int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid) {
     b->count[sid] = 0;
   }
   b->closed[sid] = 0;
+  return WSG_API_OK;
+}
+
+// ------------------------------------------------------------------ device per selector loop
+// One device per loop: the sessions of a loop share its batcher, and
+// nothing is shared between devices.  A new loop goes to the device with the fewest
+// loops, ties to the one with the fewest wire bytes accounted so far.
+static std::mutex g_dev_mu;
+static std::vector<uint32_t> g_dev_loops;
+static std::vector<uint64_t> g_dev_bytes;
+static std::map<uint64_t, int> g_dev_of;
+
+static int dev_init_locked() {
+  if (!g_dev_loops.empty()) return (int)g_dev_loops.size();
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return 0;
+  g_dev_loops.assign((size_t)n, 0);
+  g_dev_bytes.assign((size_t)n, 0);
+  return n;
+}
+
+int wsg_device_policy_init(int n_devices) {
+  if (n_devices <= 0) return WSG_API_EINVAL;
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  g_dev_loops.assign((size_t)n_devices, 0);
+  g_dev_bytes.assign((size_t)n_devices, 0);
+  g_dev_of.clear();
+  return WSG_API_OK;
+}
+
+int wsg_device_for_loop(uint64_t loop_id) {
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  auto it = g_dev_of.find(loop_id);
+  if (it != g_dev_of.end()) return it->second;
+  const int n = dev_init_locked();
+  if (n <= 0) return WSG_API_EHIP;
+  int best = 0;
+  for (int i = 1; i < n; ++i)
+    if (g_dev_loops[i] < g_dev_loops[best] || (g_dev_loops[i] == g_dev_loops[best] && g_dev_bytes[i] < g_dev_bytes[best]))
+      best = i;
+  ++g_dev_loops[best];
+  g_dev_of[loop_id] = best;
+  return best;
+}
+
+int wsg_device_account(int device, uint64_t wire_bytes) {
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  if (device < 0 || (size_t)device >= g_dev_bytes.size()) return WSG_API_EINVAL;
+  g_dev_bytes[(size_t)device] += wire_bytes;
+  return WSG_API_OK;
+}
+
+int wsg_device_release_loop(uint64_t loop_id) {
+  std::lock_guard<std::mutex> g(g_dev_mu);
+  auto it = g_dev_of.find(loop_id);
+  if (it == g_dev_of.end()) return WSG_API_EINVAL;
+  --g_dev_loops[(size_t)it->second];
+  g_dev_of.erase(it);
   return WSG_API_OK;
 }
 

@@ -124,3 +124,39 @@ def test_large_encode_batch_multipass(ctx, oracle, cm):
         assert wire[int(off[k]):int(off[k + 1])].tobytes() == exp[k], k
     for s in range(n_s):
         assert closed[s] == (pre_closed[s] or any(specs[k][0] == 8 for k in range(first[s], first[s + 1])))
+
+
+def test_encode_batcher_matches_oracle(ctx, oracle):
+    """The native cross-session encode batcher (wsg_enc_batcher_*): frames of many
+    sessions added interleaved over several flushes, 64 KiB frames and small ones,
+    CLOSE latches (frames after it dropped, also in later flushes), a slot reset
+    for a new session; every session's wire bytes == the oracle FrameEncoder's."""
+    from snf4j_amd import EncodeBatcher
+    from snf4j_amd.frame import make_frame
+    for cm in (True, False):
+        rng = np.random.default_rng(808 + cm)
+        n = 37
+        b = EncodeBatcher(n, cm, ctx=ctx)
+        enc = [oracle.Encoder(cm) for _ in range(n)]
+        for flush in range(4):
+            want = [b""] * n
+            for _ in range(int(rng.integers(50, 300))):
+                s = int(rng.integers(0, n))
+                r = rng.random()
+                op = 8 if r < 0.01 else 9 if r < 0.05 else int(rng.choice([0, 1, 2]))
+                ln = int(rng.integers(0, 126)) if op >= 8 else 65536 if rng.random() < 0.1 else \
+                    int(rng.integers(0, 3000))
+                if op == 8 and ln == 1:
+                    ln = 2
+                p = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                fin, rsv = bool(rng.integers(0, 2)) or op >= 8, int(rng.integers(0, 8))
+                mask = tuple(int(x) for x in rng.integers(0, 256, 4))
+                b.add(s, make_frame(op, fin, rsv, p), mask)
+                want[s] += enc[s].encode(op, fin, rsv, p, mask if cm else (0, 0, 0, 0))
+            if flush == 2:  # slot 3 goes to a new session: queued frames dropped, latch cleared
+                b.reset_session(3)
+                enc[3] = oracle.Encoder(cm)
+                want[3] = b""
+            got = b.flush()
+            assert got == want, (cm, flush)
+        b.close()

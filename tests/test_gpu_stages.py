@@ -1,0 +1,137 @@
+"""GPU parity of the native batcher with the decoders after "ws-decoder" in the same
+flush (wsg_batcher_set_stages): FrameDecoder -> PerMessageDeflateDecoder ->
+FrameUtf8Validator -> FrameAggregator, the pipeline snf4j builds when
+permessage-deflate is negotiated (DefaultWebSocketSessionConfig.java:276-281,
+PerMessageDeflateExtension.java:316-326) with an application FrameAggregator after
+it.  The oracle runs the same chain frame by frame per session: the C restatement's
+session read loop, then the restated PerMessageDeflateDecoder (over zlib), the
+restated FrameUtf8Validator and FrameAggregator, stopping at the first exception."""
+import zlib
+
+import numpy as np
+import pytest
+
+from tests import wsgen
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from snf4j_amd import Context
+    c = Context(0)
+    yield c
+    c.close()
+
+
+def _messages(rng, n_msgs, no_context, bad_utf8):
+    """(opcode, fin, rsv, payload) of one session: compressed text/binary messages cut
+    into fragments with pings between them, uncompressed messages, invalid UTF-8 in a
+    few compressed text messages, corrupt compressed bytes now and then."""
+    comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+    out = []
+    for _ in range(n_msgs):
+        r = rng.random()
+        if r < 0.15:
+            op = int(rng.choice([1, 2]))
+            body = wsgen.rand_text(rng, int(rng.integers(0, 300))) if op == 1 else \
+                rng.integers(0, 256, int(rng.integers(0, 300)), dtype=np.uint8).tobytes()
+            out.append((op, True, 0, body))
+            continue
+        if r < 0.2:
+            out.append((9, True, 0, b"ping"))
+            continue
+        op = 1 if rng.random() < 0.7 else 2
+        body = wsgen.rand_text(rng, int(rng.integers(0, 3000))) if op == 1 else \
+            rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        if op == 1 and rng.random() < bad_utf8:
+            bad = wsgen.BAD_UTF8[int(rng.integers(0, len(wsgen.BAD_UTF8)))]
+            at = int(rng.integers(0, len(body) + 1))
+            body = body[:at] + bad + body[at:]
+        if no_context:
+            comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+        data = comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH)
+        data = data[:-4] if body else b"\x00"
+        if rng.random() < 0.02 and data:
+            b = bytearray(data)
+            b[int(rng.integers(0, len(b)))] ^= 0x10
+            data = bytes(b)
+        cuts = sorted(set(int(x) for x in rng.integers(0, len(data) + 1, int(rng.integers(0, 4)))))
+        parts = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
+        for i, p in enumerate(parts):
+            out.append((op if i == 0 else 0, i == len(parts) - 1, 4 if i == 0 else 0, p))
+            if i + 1 < len(parts) and rng.random() < 0.2:
+                out.append((10, True, 0, b""))
+    return out
+
+
+def _oracle_chain(oracle, stream, no_context, validate, aggregate, max_agg):
+    """[(opcode, fin, rsv, payload)] the handler receives, and the first error
+    (message, close code) or None."""
+    frames, derr = oracle.stream_decode(stream, [len(stream)], client_mode=False, allow_extensions=True, max_payload_len=1 << 20,
+                                        validate_utf8=False)
+    inf = oracle.PerMessageDeflateDecoder(no_context)
+    val = oracle.Validator()
+    agg = oracle.Aggregator(max_agg) if aggregate else None
+    out = []
+    for f in frames:
+        try:
+            op, fin, rsv, p = inf.decode(f.opcode, f.fin, f.rsv, f.payload)
+        except oracle.InvalidFrame as e:
+            return out, (str(e), e.close_code)
+        if validate and not val.decode(op, fin, p):
+            return out, (oracle.format_error(14), 1007)
+        if agg is not None:
+            try:
+                g = agg.decode(op, fin, rsv, p)
+            except oracle.InvalidFrame as e:
+                return out, (oracle.format_error(18), 1009)
+            if g is None:
+                continue
+            op, fin, rsv, p = g.opcode, g.fin, g.rsv, g.payload
+        out.append((op, fin, rsv, p))
+    if derr is not None:
+        return out, (str(derr), derr.close_code)
+    return out, None
+
+
+@pytest.mark.parametrize("seed,no_context,aggregate", [(0, False, True), (1, True, True), (2, False, False),
+                                                       (3, False, True)])
+def test_batcher_stage_chain_matches_oracle(ctx, oracle, seed, no_context, aggregate):
+    from snf4j_amd import NativeBatcher
+    rng = np.random.default_rng(6100 + seed)
+    n = 48
+    max_agg = 4000 if seed == 3 else 1 << 20
+    streams = []
+    for s in range(n):
+        msgs = _messages(rng, int(rng.integers(1, 14)), no_context, bad_utf8=0.05)
+        wire = b"".join(wsgen.build_frame(op, fin, rsv, p, True, tuple(int(x) for x in rng.integers(0, 256, 4)))
+                        for (op, fin, rsv, p) in msgs)
+        if s % 11 == 5:  # a protocol error after some frames (opcode 3)
+            wire += bytes([0x83, 0x80, 1, 2, 3, 4])
+        streams.append(wire)
+    b = NativeBatcher(n, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=ctx)
+    b.set_stages(inflate=True, noContext=no_context, validate=True, aggregate=aggregate,
+                 maxAggregatedLength=max_agg)
+    got = [[] for _ in range(n)]
+    err = [None] * n
+    pos = [0] * n
+    while any(pos[s] < len(streams[s]) for s in range(n)):
+        for s in range(n):
+            if pos[s] < len(streams[s]):
+                c = int(rng.integers(1, 4000))
+                b.feed(s, streams[s][pos[s]:pos[s] + c])
+                pos[s] += c
+        for s, (fr, e) in enumerate(b.flush()):
+            got[s] += fr
+            if e is not None:
+                assert err[s] is None, s  # one error per session, then it is closed
+                err[s] = (e.getMessage(), e.close_code)
+    n_err = 0
+    for s in range(n):
+        exp, eerr = _oracle_chain(oracle, streams[s], no_context, True, aggregate, max_agg)
+        assert err[s] == eerr, (s, err[s], eerr)
+        assert [(int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload()) for f in got[s]] == exp, s
+        n_err += eerr is not None
+    assert n_err  # the generator produced failures of some kind
+    b.close()

@@ -1,7 +1,8 @@
 """The Java integration sources (java/, jni/) against the C ABI, without a JDK:
 every native method of Wsg.java has its JNI function in jni/wsgpu_jni.c (and no
-JNI function lacks its declaration), and every libwsgpu entry point the glue calls
-is declared in include/wsgpu.h and exported by libwsgpu.so."""
+JNI function lacks its declaration), every libwsgpu entry point the glue calls
+is declared in include/wsgpu.h and exported by libwsgpu.so, and the stage
+classes keep the reference's keys, types and lifecycle hooks."""
 import ctypes as C
 import os
 import re
@@ -15,10 +16,24 @@ def _read(*p):
         return fh.read()
 
 
+def _java(name):
+    return _read("java/org/snf4j/websocket/gpu", name)
+
+
 def test_every_native_method_has_its_jni_function():
-    natives = set(re.findall(r"static native \S+ (\w+)\(", _read("java/org/snf4j/websocket/gpu/Wsg.java")))
+    natives = set(re.findall(r"static native \S+ (\w+)\(", _java("Wsg.java")))
     jni = set(re.findall(r"Java_org_snf4j_websocket_gpu_Wsg_(\w+)\(", _read("jni/wsgpu_jni.c")))
     assert natives and natives == jni, (natives - jni, jni - natives)
+
+
+def test_every_native_method_is_used():
+    natives = set(re.findall(r"static native \S+ (\w+)\(", _java("Wsg.java")))
+    body = "".join(_java(f) for f in os.listdir(JAVA) if f != "Wsg.java")
+    unused = {n for n in natives if f"Wsg.{n}(" not in body}
+    # the handshake natives are bound for the handshake stages INTEGRATION.md §1.3d-e describes
+    assert unused <= {"handshakeAvailable", "handshakeAcceptBatchHost", "handshakeValidateBatchHost",
+                      "batcherSessionState", "checkHeader", "encodedLength", "encodeBatchHost",
+                      "validateBatchHost"}, unused
 
 
 def test_glue_calls_only_declared_exported_entry_points():
@@ -31,24 +46,61 @@ def test_glue_calls_only_declared_exported_entry_points():
 
 
 def test_stage_classes_keep_the_reference_keys_and_types():
-    cfg = _read("java/org/snf4j/websocket/gpu/GpuWebSocketSessionConfig.java")
+    cfg = _java("GpuWebSocketSessionConfig.java")
     assert "pipeline.replace(HANDSHAKE_DECODER, WEBSOCKET_DECODER" in cfg
     assert "pipeline.replace(HANDSHAKE_ENCODER, WEBSOCKET_ENCODER" in cfg
-    assert "WEBSOCKET_UTF8_VALIDATOR" in cfg
-    dec = _read("java/org/snf4j/websocket/gpu/GpuFrameDecoder.java")
-    assert "implements IBaseDecoder<ByteBuffer, Frame>" in dec
-    assert "session.release(data)" in dec  # exactly once, FrameDecoder.java:285-287
-    assert "executenf" in _read("java/org/snf4j/websocket/gpu/WsgBatcher.java")
+    # the validator stage is the GPU one now (fused or after GPU inflate), not the CPU FrameUtf8Validator
+    assert "addAfter(WEBSOCKET_DECODER, WEBSOCKET_UTF8_VALIDATOR, new GpuFrameUtf8Validator())" in cfg
+    assert "new FrameUtf8Validator()" not in cfg
+    dec = _java("GpuFrameDecoder.java")
+    assert "implements IBaseDecoder<ByteBuffer, Frame>, IEventDrivenCodec" in dec
+    assert dec.count("session.release(data)") == 1  # exactly once, FrameDecoder.java:285-287
+    assert "implements IEncoder<Frame, ByteBuffer>, IEventDrivenCodec" in _java("GpuFrameEncoder.java")
+    for f in ("GpuPerMessageDeflateDecoder.java", "GpuFrameAggregator.java", "GpuFrameUtf8Validator.java"):
+        assert "implements IDecoder<Frame, Frame>" in _java(f) and "GpuStage" in _java(f), f
+    ext = _java("GpuPerMessageDeflateExtension.java")
+    assert "implements IExtension" in ext and "PERMESSAGE_DEFLATE_DECODER" in ext
     files = sorted(os.listdir(JAVA))
-    assert files == ["GpuFrameDecoder.java", "GpuFrameEncoder.java", "GpuWebSocketSessionConfig.java",
-                     "PinnedByteBufferAllocator.java", "Wsg.java", "WsgBatcher.java"]
+    assert files == ["GpuFrameAggregator.java", "GpuFrameDecoder.java", "GpuFrameEncoder.java",
+                     "GpuFrameUtf8Validator.java", "GpuPerMessageDeflateDecoder.java",
+                     "GpuPerMessageDeflateExtension.java", "GpuStage.java", "GpuWebSocketSessionConfig.java",
+                     "PinnedByteBufferAllocator.java", "Wsg.java", "WsgBatcher.java", "WsgDevices.java"]
+
+
+def test_session_lifecycle_reaches_the_native_reset():
+    """ENDING / removed -> unregister -> wsg_batcher_session_reset (and the encoder's)."""
+    dec = _java("GpuFrameDecoder.java")
+    assert "event == SessionEvent.ENDING" in dec and "batcher.unregister(this)" in dec
+    assert "public void removed(ISession session, ICodecPipeline pipeline)" in dec
+    enc = _java("GpuFrameEncoder.java")
+    assert "event == SessionEvent.ENDING" in enc and "batcher.unregisterEncoder(this)" in enc
+    b = _java("WsgBatcher.java")
+    assert "Wsg.batcherSessionReset(n.handle, d.sid)" in b and "Wsg.encBatcherSessionReset(n.handle, e.sid)" in b
+    assert "wsg_batcher_session_reset" in _read("jni/wsgpu_jni.c")
+
+
+def test_flush_is_deferred_not_inline():
+    """The flush is queued on the loop (SelectorLoop.executenf always queues), never
+    ISession.executenf, which runs the task inline on the loop thread."""
+    b = _java("WsgBatcher.java")
+    assert "loop.executenf(flushTask)" in b
+    assert "session.executenf" not in b and ".executenf(new Runnable" not in b
+
+
+def test_feed_handles_every_buffer_kind():
+    b = _java("WsgBatcher.java")
+    assert "data.hasArray()" in b and "data.isDirect()" in b and "data.duplicate().get(b)" in b
+    jni = _read("jni/wsgpu_jni.c")
+    assert "GetDirectBufferCapacity" in jni and "if (!p || cap < 0" in jni
 
 
 def test_java_messages_match_the_python_mirror():
     """Wsg.message() builds the reference's exception texts: the same table as
     snf4j_amd/context.py MESSAGES (checked against the oracle in test_abi)."""
     from snf4j_amd.context import MESSAGES
-    java = _read("java/org/snf4j/websocket/gpu/Wsg.java")
-    for code in range(1, 17):
+    java = _java("Wsg.java")
+    for code in range(1, 21):
+        if code == 17:
+            continue
         text = MESSAGES[code].split("{")[0].rstrip(" (")
         assert text in java, (code, text)

@@ -122,3 +122,24 @@ def test_gloo_world2_sharded_decode():
     ok, elapsed = q.get(timeout=5)
     assert ok, "sharded decode differs from the single-process decode"
     assert elapsed >= 0.2 - 1e-3  # rank 1's 2 x 0.1 s dominates: max over ranks
+
+
+def test_native_loop_device_policy():
+    """wsg_device_for_loop (the JNI shim's WsgDevices): a new selector loop goes to
+    the device with the fewest loops, ties to the fewest wire bytes accounted; a
+    loop keeps its device; a released loop frees its share."""
+    from snf4j_amd._lib import lib
+    assert lib.wsg_device_policy_init(8) == 0
+    devs = [lib.wsg_device_for_loop(100 + i) for i in range(8)]
+    assert sorted(devs) == list(range(8))
+    assert [lib.wsg_device_for_loop(100 + i) for i in range(8)] == devs  # stable
+    # bytes break the ties of the second round: the least loaded devices first
+    for d in range(8):
+        assert lib.wsg_device_account(d, (8 - d) * 1000) == 0
+    second = [lib.wsg_device_for_loop(200 + i) for i in range(8)]
+    assert second == list(range(7, -1, -1))
+    # a released loop's device takes the next loop
+    assert lib.wsg_device_release_loop(100 + devs.index(3)) == 0
+    assert lib.wsg_device_for_loop(999) == 3
+    assert lib.wsg_device_release_loop(12345) != 0
+    assert lib.wsg_device_account(8, 1) != 0
