@@ -44,6 +44,15 @@ CONFIGS = {
 }
 
 
+
+def apply_tuning(ctx):
+    """A/B runs (scripts/ab_env.sh): WSG_TUNE_<NAME>=<value> in the bench's environment
+    sets the context switch wsg_set_tuning(<NAME>) — the harness reads it, not the library."""
+    for name in ctx.TUNING:
+        v = os.environ.get("WSG_TUNE_" + name.upper())
+        if v is not None:
+            ctx.set_tuning(name, int(v))
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=None, help="GPUs (rank processes); default WORLD_SIZE or 1")
@@ -220,6 +229,7 @@ def main():
 
     stream = torch.cuda.current_stream(dev)
     ctx = snf4j_amd.Context(local, stream=stream)
+    apply_tuning(ctx)
     if args.only:
         print(json.dumps(EXTRA_LINES[args.only](ctx, dev, args.extra_steps, 2)), flush=True)
         ctx.close()
@@ -280,15 +290,22 @@ def main():
     alg_bytes = wire_bytes + F * P  # per launch: wire read + payload written
     copy = benchsupport.copy_ceiling(ctx, wire, payload, wire_bytes)
     achieved = alg_bytes / avg_unmask_s / 1e9
-    traffic = None
+    # HBM bytes per launch from the PMC counters: PMC cannot run in the same process as
+    # the timed region (separate rocprofv3 --pmc passes, MI355X_MICROARCH.md), so this is
+    # the committed measurement of the same kernel on the same workload, labelled with
+    # its file (traffic_source); null when none exists for this workload
+    traffic = traffic_source = None
     if os.path.exists(args.pmc_json):
         try:
             with open(args.pmc_json) as fh:
                 pmc = json.load(fh)
             key = f"{'binary' if args.binary else 'text'}_{F}x{P}"
             traffic = pmc.get(key, {}).get("hbm_bytes_per_launch")
+            if traffic is not None:
+                traffic_source = (os.path.relpath(args.pmc_json, ROOT) + f" [{key}] <- " +
+                                  pmc[key].get("source", "") + " (a separate PMC run, not this process)")
         except Exception:
-            traffic = None
+            traffic = traffic_source = None
 
     e2e = None
     if args.e2e:
@@ -344,6 +361,7 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": traffic,
+                "traffic_source": traffic_source,
                 "alg_bytes_per_launch": alg_bytes,
                 "avg_launch_ms": round(avg_unmask_s * 1e3, 4),
                 "launches_timed": int(unmask_n), "event_every": EVENT_EVERY[0],
@@ -881,6 +899,7 @@ def e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev, reps=6):
     torch.cuda.empty_cache()
     # pipelined library host path (copy-in / kernel / copy-out streams, two staging slots)
     pctx = snf4j_amd.Context(dev.index, stream=torch.cuda.Stream(dev))
+    apply_tuning(pctx)
     bufs = []
     for _ in range(2):
         bufs.append({"pay": torch.empty(wire_bytes + 16 * F, dtype=torch.uint8).pin_memory() if not bufs else None,

@@ -157,6 +157,24 @@ int wsg_version(void);
  * null stream: to run on the null stream, call wsg_set_stream(ctx, NULL)). */
 int wsg_open(int device, void* stream, wsg_ctx** out);
 int wsg_close(wsg_ctx* ctx);
+/* Measurement and test switches of a context (the defaults are the product; each
+ * alternative is kept to A/B the choice it documents in DESIGN.md):
+ *   WSG_TUNE_INFLATE_TOKENS  0: no lane pre-decode, the serial inflate decodes every frame
+ *   WSG_TUNE_INFLATE_FAST    0: no parallel token replay; 2 (tests only): the replay alone,
+ *                            sessions it does not take are left unprocessed
+ *   WSG_TUNE_INFLATE_LDS     0: the lane pre-decode keeps its tables in HBM
+ *   WSG_TUNE_INFLATE_ORDER   0: lanes take frames in batch order (not longest first)
+ *   WSG_TUNE_INFLATE_LANES   k_infl_tok lanes at most (multiple of 64)
+ *   WSG_TUNE_FUSED_SCAN      0: always launch k_scan (k_link does not fold block aggregates) */
+enum {
+    WSG_TUNE_INFLATE_TOKENS = 1,
+    WSG_TUNE_INFLATE_FAST = 2,
+    WSG_TUNE_INFLATE_LDS = 3,
+    WSG_TUNE_INFLATE_ORDER = 4,
+    WSG_TUNE_INFLATE_LANES = 5,
+    WSG_TUNE_FUSED_SCAN = 6
+};
+int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */
 int wsg_set_stream(wsg_ctx* ctx, void* stream);
 /* The hipStream_t the context enqueues its kernels on (for a caller that orders its

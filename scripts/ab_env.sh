@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B of an environment switch on one build, interleaved:
-#   scripts/ab_env.sh VAR "v1 v2 ..." <python expr over d (the JSON line)> [bench args]
+#   scripts/ab_env.sh WSG_TUNE_<NAME> "v1 v2 ..." (bench.py apply_tuning) <python expr over d (the JSON line)> [bench args]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 VAR=$1; VALS=$2; EXPR=$3; shift 3

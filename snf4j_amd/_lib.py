@@ -145,6 +145,7 @@ def _load():
         "wsg_batcher_session_state": ([p, u32, P(SessionState)], i32),
         "wsg_batcher_session_reset": ([p, u32], i32),
         "wsg_batcher_set_stages": ([p, P(StageCfg)], i32),
+        "wsg_set_tuning": ([p, i32, C.c_int64], i32),
         "wsg_device_policy_init": ([i32], i32),
         "wsg_device_for_loop": ([u64], i32),
         "wsg_device_account": ([i32, u64], i32),

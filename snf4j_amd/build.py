@@ -25,29 +25,49 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-u
          "-mllvm", "-disable-promote-alloca-to-lds"]
 
 
-def _stale() -> bool:
-    if not os.path.exists(OUT):
-        return True
-    t = os.path.getmtime(OUT)
-    deps = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
-    return any(os.path.getmtime(d) > t for d in deps)
+def _digest(paths, flags) -> str:
+    """sha256 of the sources, headers and compile flags a library is built from."""
+    import hashlib
+    h = hashlib.sha256(" ".join(flags).encode())
+    for p in paths:
+        h.update(os.path.basename(p).encode())
+        with open(p, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()
+
+
+def _fresh(out: str, digest: str) -> bool:
+    """The library exists and was built from exactly these sources (its .srchash
+    sidecar): a binary pushed with other sources is rebuilt, whatever the mtimes."""
+    try:
+        with open(out + ".srchash") as fh:
+            return os.path.exists(out) and fh.read().strip() == digest
+    except OSError:
+        return False
+
+
+def _record(out: str, digest: str) -> None:
+    with open(out + ".srchash", "w") as fh:
+        fh.write(digest + "\n")
 
 
 def build_bench(force: bool = False) -> str:
-    if not force and os.path.exists(BENCH_OUT) and all(
-            os.path.getmtime(d) <= os.path.getmtime(BENCH_OUT) for d in (BENCH_SRC, BENCH_HDR)):
+    digest = _digest([BENCH_SRC, BENCH_HDR], FLAGS)
+    if not force and _fresh(BENCH_OUT, digest):
         return BENCH_OUT
     tmp = BENCH_OUT + ".tmp"
     r = subprocess.run([HIPCC, *FLAGS, "-shared", BENCH_SRC, "-o", tmp], capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"hipcc failed for {BENCH_SRC}:\n{r.stderr}")
     os.replace(tmp, BENCH_OUT)
+    _record(BENCH_OUT, digest)
     return BENCH_OUT
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
     build_bench(force)
-    if not force and not _stale():
+    digest = _digest([os.path.join(CSRC, s) for s in SOURCES + HEADERS], FLAGS)
+    if not force and _fresh(OUT, digest):
         return OUT
     objdir = os.path.join(HERE, "_build")
     os.makedirs(objdir, exist_ok=True)
@@ -70,6 +90,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     os.replace(tmp, OUT)
+    _record(OUT, digest)
     return OUT
 
 

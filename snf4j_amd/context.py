@@ -69,6 +69,13 @@ class Context:
     torch.cuda.Stream.  Torch's default stream has handle 0, which is passed on
     with wsg_set_stream (wsg_open(NULL) would create a private stream instead)."""
 
+    TUNING = {"inflate_tokens": 1, "inflate_fast": 2, "inflate_lds": 3, "inflate_order": 4, "inflate_lanes": 5,
+              "fused_scan": 6}
+
+    def set_tuning(self, name: str, value: int):
+        """A measurement / test switch of this context (wsg_set_tuning; wsgpu.h lists them)."""
+        check(lib.wsg_set_tuning(self._h, self.TUNING[name], int(value)), self._h)
+
     def __init__(self, device: int = 0, stream="torch"):
         h = C.c_void_p()
         rc = lib.wsg_open(int(device), None, C.byref(h))

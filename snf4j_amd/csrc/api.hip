@@ -67,12 +67,13 @@ struct wsg_ctx {
   DevBuf a_code, a_last, a_pl, a_cl, a_rec, a_blk, a_sess_err, a_pieces;
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
   DevBuf i_tok, i_lit, i_stat, i_tab, i_fast, i_ord;  // inflate pre-decode workspace
-  int infl_tokens = 1;               // WSG_INFLATE_TOKENS=0 turns the pre-decode off
-  uint32_t infl_lanes = 262144;      // k_infl_tok lanes at most (WSG_INFLATE_LANES, A/B): 4 waves a SIMD, 1 GB of lane tables
-  int infl_fast = 1;
-  int infl_lds = 1;                  // WSG_INFLATE_LDS=0: the pre-decode keeps its tables in HBM (A/B)
-  int infl_order = 1;                // WSG_INFLATE_ORDER=0: lanes take frames in batch order (A/B)                 // WSG_INFLATE_FAST=0 turns the parallel token replay off (A/B); 2: it alone (tests)
-  int fused_scan = 1;                // WSG_FUSED_SCAN=0: always launch k_scan (A/B)
+  // measurement / test switches (wsg_set_tuning; the defaults are the product)
+  int infl_tokens = 1;               // WSG_TUNE_INFLATE_TOKENS 0: no lane pre-decode (serial decoder only)
+  uint32_t infl_lanes = 262144;      // WSG_TUNE_INFLATE_LANES: k_infl_tok lanes at most
+  int infl_fast = 1;                 // WSG_TUNE_INFLATE_FAST 0: no parallel token replay; 2: it alone (tests)
+  int infl_lds = 1;                  // WSG_TUNE_INFLATE_LDS 0: the pre-decode keeps its tables in HBM
+  int infl_order = 1;                // WSG_TUNE_INFLATE_ORDER 0: lanes take frames in batch order
+  int fused_scan = 1;                // WSG_TUNE_FUSED_SCAN 0: always launch k_scan
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -170,12 +171,6 @@ int wsg_open(int device, void* stream, wsg_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return WSG_API_EHIP;
   wsg_ctx* c = new wsg_ctx();
   c->device = device;
-  if (const char* e = getenv("WSG_INFLATE_TOKENS")) c->infl_tokens = atoi(e) != 0;
-  if (const char* e = getenv("WSG_INFLATE_FAST")) c->infl_fast = atoi(e);
-  if (const char* e = getenv("WSG_INFLATE_LDS")) c->infl_lds = atoi(e) != 0;
-  if (const char* e = getenv("WSG_INFLATE_ORDER")) c->infl_order = atoi(e) != 0;
-  if (const char* e = getenv("WSG_INFLATE_LANES")) c->infl_lanes = (uint32_t)atoi(e) < 64u ? 64u : (uint32_t)atoi(e) & ~63u;
-  if (const char* e = getenv("WSG_FUSED_SCAN")) c->fused_scan = atoi(e) != 0;
   if (stream) {
     c->stream = (hipStream_t)stream;
   } else {
@@ -217,6 +212,20 @@ int wsg_close(wsg_ctx* c) {
   if (c->s_out) (void)hipStreamDestroy(c->s_out);
   if (c->own_stream) (void)hipStreamDestroy(c->stream);
   delete c;
+  return WSG_API_OK;
+}
+
+int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
+  if (!c) return WSG_API_EINVAL;
+  switch (key) {
+    case WSG_TUNE_INFLATE_TOKENS: c->infl_tokens = value != 0; break;
+    case WSG_TUNE_INFLATE_FAST: c->infl_fast = (int)value; break;
+    case WSG_TUNE_INFLATE_LDS: c->infl_lds = value != 0; break;
+    case WSG_TUNE_INFLATE_ORDER: c->infl_order = value != 0; break;
+    case WSG_TUNE_INFLATE_LANES: c->infl_lanes = value < 64 ? 64u : (uint32_t)value & ~63u; break;
+    case WSG_TUNE_FUSED_SCAN: c->fused_scan = value != 0; break;
+    default: return set_err(c, WSG_API_EINVAL, "unknown tuning key");
+  }
   return WSG_API_OK;
 }
 

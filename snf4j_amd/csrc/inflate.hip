@@ -421,6 +421,7 @@ __device__ __forceinline__ uint64_t tok_base(uint64_t po, uint64_t k) { return p
 __device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
   return (3 * po + (uint64_t)TOK_SLACK * k + 3) & ~(uint64_t)3;
 }
+__device__ __forceinline__ uint32_t lit_cap_of(uint32_t plen) { return 3u * (plen + 4u) + 60u; }
 
 // One message's pre-decode into per-frame token regions (MULTI: several frames; the
 // single-frame instantiation keeps the segment and attribution steps out of its loop).
@@ -446,7 +447,7 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
   // to the inflate call that supplies its last bit's byte), per-frame token regions
   uint64_t fa = k;
   uint32_t fa_hi = k == kend ? total : d.payload_len;  // message offset where frame fa's bytes end
-  uint32_t tok_cap = d.payload_len + 68u, lit_cap = 3u * (d.payload_len + 4u) + 60u;
+  uint32_t tok_cap = d.payload_len + 68u, lit_cap = lit_cap_of(d.payload_len);
   uint32_t* tok = a.tok + tok_base(d.payload_off, k);
   uint8_t* lit = a.lit + lit_base(d.payload_off, k);
   uint64_t hold = 0;
@@ -545,7 +546,7 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
     const wsg_frame_desc df = a.desc[fa];
     fa_hi = fa == kend ? total : lo + df.payload_len;
     tok_cap = df.payload_len + 68u;
-    lit_cap = 3u * (df.payload_len + 4u) + 60u;
+    lit_cap = lit_cap_of(df.payload_len);
     tok = a.tok + tok_base(df.payload_off, fa);
     lit = a.lit + lit_base(df.payload_off, fa);
     ntok = nlit = run = outlen = litw = 0;
@@ -955,7 +956,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   const uint32_t lane = threadIdx.x;
   const uint32_t plen = d.payload_len, total = plen + 4u;
   const uint64_t off = d.payload_off;
-  const uint32_t tok_cap = plen + 68u, lit_cap = 3u * (plen + 4u) + 60u;
+  const uint32_t tok_cap = plen + 68u, lit_cap = lit_cap_of(plen);
   uint32_t* const tok = a.tok + tok_base(off, k);
   uint8_t* const lit = a.lit + lit_base(off, k);
   uint16_t* const tab = Q.tab;
@@ -1195,9 +1196,11 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     const uint32_t tsh = fixed ? 0u : 6u;  // entry j at base + (j << tsh)
     uint32_t mlen = 0;                     // a length waiting for its distance
     uint32_t* const lit32 = reinterpret_cast<uint32_t*>(lit);
-    // Branch-light: the stores are unconditional (a token slot a step does not keep is
-    // rewritten by a later step or lies past the frame's count; the partial literal
-    // word is rewritten until it is full), so the 64 lanes run one instruction stream.
+    // Branch-light: one instruction stream for the 64 lanes; the stores are masked to
+    // the lanes that complete something (a literal word, a match and the literal run
+    // before it), so every output byte is written once.  (Unconditional stores of the
+    // partial word and of a token slot every step wrote ~6x the token + literal bytes
+    // per launch, and each ring top-up waited for all of them.)
     for (;;) {
       TPROF_CNT(4, 1);
       in_step();  // a step takes at most 15 + 13 bits
@@ -1225,9 +1228,11 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       const uint32_t nlit2 = nlit + (is_lit ? 1u : 0u);
       const uint32_t litw2 = is_lit ? (litw | (v << (8u * (nlit & 3u)))) : litw;
       const bool word_done = is_lit && (nlit2 & 3u) == 0u;
-      lit32[(nlit2 >> 2) - (word_done ? 1u : 0u)] = litw2;  // the word just filled, else the partial one
-      tok[ntok] = run;
-      tok[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
+      if (word_done) lit32[(nlit2 >> 2) - 1u] = litw2;  // the word just filled
+      if (dist) {
+        if (has_run) tok[ntok] = run;
+        tok[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
+      }
       ntok += dist ? 1u + has_run : 0u;
       litw = word_done ? 0u : litw2;
       nlit = nlit2;

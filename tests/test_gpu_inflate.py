@@ -175,7 +175,7 @@ def test_inflate_long_context_window(ctx, oracle):
 
 
 def test_inflate_predecode_matches_serial_and_zlib(oracle):
-    """k_infl_tok + token replay against the serial decoder alone (WSG_INFLATE_TOKENS=0) and
+    """k_infl_tok + token replay against the serial decoder alone (set_tuning inflate_tokens 0) and
     zlib, on a bench-shaped batch (single-frame messages, context takeover), split over
     two batches so the second replays tokens against a carried-in window."""
     import os
@@ -186,12 +186,9 @@ def test_inflate_predecode_matches_serial_and_zlib(oracle):
     n_s, msgs, mb = 96, 8, 2048
     desc, sf, payload, plain = deflate_batch(0xD1F, n_s, msgs, mb, unique=12)
     outs = []
-    for flag in ("1", "0"):
-        os.environ["WSG_INFLATE_TOKENS"] = flag
-        try:
-            c = Context(0)
-        finally:
-            os.environ.pop("WSG_INFLATE_TOKENS", None)
+    for flag in (1, 0):
+        c = Context(0)
+        c.set_tuning("inflate_tokens", flag)
         state = np.zeros(n_s, dtype=INFLATE_STATE_DTYPE)
         window = np.zeros(n_s * 32768, dtype=np.uint8)
         got = [[] for _ in range(n_s)]
@@ -287,7 +284,7 @@ def test_inflate_fragmented_messages_predecoded(ctx, oracle, no_context):
 
 
 def test_inflate_fast_replay_takes_fragmented_sessions(oracle):
-    """With WSG_INFLATE_FAST=2 the serial pass does not run at all, so every session must
+    """With set_tuning inflate_fast 2 the serial pass does not run at all, so every session must
     be finished by the pre-decode + parallel replay: fragmented compressed messages
     (fragments of >= 200 bytes, so each completes a symbol), pings, uncompressed frames,
     context carried over three batches."""
@@ -315,11 +312,8 @@ def test_inflate_fast_replay_takes_fragmented_sessions(oracle):
             if rng.random() < 0.3:
                 frames.append((2, True, 0, b"raw"))
         sessions.append(frames)
-    os.environ["WSG_INFLATE_FAST"] = "2"
-    try:
-        c = Context(0)
-    finally:
-        os.environ.pop("WSG_INFLATE_FAST", None)
+    c = Context(0)
+    c.set_tuning("inflate_fast", 2)
     try:
         # cut each session only after a FIN data frame (a message boundary)
         n_b = 3
@@ -411,8 +405,8 @@ def _lds_path_messages(rng):
 
 
 def test_inflate_lds_table_paths(oracle):
-    """The pre-decode's LDS path (default) against its HBM tables (WSG_INFLATE_LDS=0), the
-    serial decoder alone (WSG_INFLATE_TOKENS=0) and zlib, one session per message (no
+    """The pre-decode's LDS path (default) against its HBM tables (set_tuning inflate_lds 0), the
+    serial decoder alone (set_tuning inflate_tokens 0) and zlib, one session per message (no
     context), every message a single FIN frame."""
     import os
     from snf4j_amd import Context
@@ -435,13 +429,10 @@ def test_inflate_lds_table_paths(oracle):
     cap = max(len(b) for _, b, _ in kinds) + 64
     out_off = (np.arange(n + 1) * cap).astype(np.uint64)
     results = []
-    for env in ({}, {"WSG_INFLATE_LDS": "0"}, {"WSG_INFLATE_TOKENS": "0"}):
-        os.environ.update(env)
-        try:
-            c = Context(0)
-        finally:
-            for k in env:
-                os.environ.pop(k, None)
+    for env in ({}, {"inflate_lds": 0}, {"inflate_tokens": 0}):
+        c = Context(0)
+        for k, v in env.items():
+            c.set_tuning(k, v)
         state = np.zeros(n, dtype=INFLATE_STATE_DTYPE)
         window = np.zeros(n * 32768, dtype=np.uint8)
         out, od, res, rf = c.inflate_host(True, desc, sf, payload, state, window, out_off)
