@@ -95,8 +95,12 @@ typedef struct wsg_decoder_cfg {
     int32_t allow_extensions;  /* FrameDecoder.allowExtensions: RSV bits allowed */
     int64_t max_payload_len;   /* FrameDecoder.maxPayloadLen */
     int32_t validate_utf8;     /* 1 = FrameUtf8Validator runs after the decoder */
-    int32_t reserved;
+    int32_t flags;             /* WSG_CFG_* */
 } wsg_decoder_cfg;
+/* wsg_decoder_cfg.flags: frames need not be adjacent in `wire` (frame k's extent is its
+ * header's, frame_off[k + 1] is not its end; frames must not overlap and must lie in
+ * wire[0, wire_len)): the native batcher lands each session's reads where they fall. */
+#define WSG_CFG_SPARSE 1
 
 /* Per-session carry state, passed explicitly in and out of every batch.
  * It is the part of FrameDecoder / FrameUtf8Validator state that survives a
@@ -324,10 +328,9 @@ int wsg_encode_batch_host(wsg_ctx* ctx, int client_mode,
  * FrameDecoder.java:357-401; StreamSession.java:798-854) with the header rules
  * applied as soon as a header is complete (FrameDecoder.java:197-256), and
  * wsg_batcher_flush decodes every complete frame of every session in one device
- * batch.  Partial frames stay in the batcher.  wsg_batcher_feed may run
- * concurrently for distinct sessions (each touches only its session's slot: one
- * feeder per selector loop, sessions owned by one loop); flush, session_state and
- * close must not overlap a feed. */
+ * batch.  Partial frames stay in the batcher.  One thread drives a batcher (a
+ * selector loop's: the sessions of one loop share it); wsg_batcher_feed_many spreads
+ * the sessions of its reads over worker threads itself. */
 typedef struct wsg_batcher wsg_batcher;
 
 typedef struct wsg_batch_view {  /* valid until the next flush / close */
@@ -340,16 +343,34 @@ typedef struct wsg_batch_view {  /* valid until the next flush / close */
     const uint8_t* payload;             /* unmasked payloads (desc.payload_off) */
     const wsg_session_result* result;   /* [n_sessions]: frames delivered + the first error,
                                            device-found or a header error found on the host */
+    const int64_t* detail2;             /* [n_sessions]: the message's second argument, for
+                                           WSG_E_EXT_LEN (Integer.MAX_VALUE - the header's length,
+                                           FrameDecoder.java:393); 0 otherwise */
 } wsg_batch_view;
 
 int wsg_batcher_open(wsg_ctx* ctx, const wsg_decoder_cfg* cfg, uint32_t n_sessions, wsg_batcher** out);
 int wsg_batcher_close(wsg_batcher* b);
 const char* wsg_batcher_last_error(wsg_batcher* b);
-/* Append bytes read from session `sid`'s socket (copied; the caller may reuse
- * `data`, as the reference releases its buffer after decode, FrameDecoder.java:285-287). */
+/* Append bytes read from session `sid`'s socket (copied into the open batch's pinned
+ * arena, after the session's carried partial frame; the caller may reuse `data`, as
+ * the reference releases its buffer after decode, FrameDecoder.java:285-287). */
 int wsg_batcher_feed(wsg_batcher* b, uint32_t sid, const uint8_t* data, uint64_t len);
 /* Decode all complete frames fed since the last flush; synchronises. */
 int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out);
+/* Many socket reads at once (e.g. one selector-loop iteration's): reads of one
+ * session in order; the sessions are fed by up to 16 threads (sid mod T). */
+int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, const uint8_t* const* data,
+                          const uint64_t* lens);
+/* The pipelined flush: flush_async gathers every complete frame into pinned
+ * staging and queues H2D, decode and D2H (wsg_decode_batch_host_async) without
+ * waiting, so the next feeds and the next gather overlap the device and PCIe
+ * work; wsg_batcher_wait returns the oldest queued flush's results (a view valid
+ * until the flush after next).  At most two flushes in flight; the carry state
+ * chains through them on the device side, and host changes (a slot reset, a
+ * header error found on the host) apply to the next batch queued.
+ * wsg_batcher_flush = wait for the queued ones (results dropped) + flush_async + wait. */
+int wsg_batcher_flush_async(wsg_batcher* b);
+int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out);
 int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* st);
 /* The decoders after "ws-decoder" that a flush runs in the same device batch, in the
  * pipeline order the reference builds (DefaultWebSocketSessionConfig.java:276-281,

@@ -166,7 +166,7 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 	}
 
 	/** The session's frames of one device batch, on its loop thread. */
-	void deliver(List<Frame> frames, int error, long detail) {
+	void deliver(List<Frame> frames, int error, long detail, long detail2) {
 		if (closed || released)
 			return;
 		List<IDecoder<Object, Object>> chain = chain();
@@ -174,7 +174,7 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 			if (!downstream(f, chain))
 				return;
 		if (error != Wsg.OK)
-			fail(session, error, detail, 0, false);
+			fail(session, error, detail, detail2, false);
 	}
 
 	/** The decoders after "ws-decoder" the batch did not run (once per delivery). */

@@ -104,10 +104,16 @@ final class Wsg {
 
 	/**
 	 * wsg_batcher_flush: decodes every complete frame fed since the last flush.
-	 * views[0..3] receive session_first, desc, payload and result wrapped as direct
+	 * views[0..4] receive session_first, desc, payload, result and detail2 wrapped as direct
 	 * buffers (valid until the next flush); counts = {n_frames, wire_bytes}.
 	 */
 	static native int batcherFlush(long batcher, ByteBuffer[] views, long[] counts);
+
+	/** wsg_batcher_flush_async: gather and queue the decode of every complete frame (no wait). */
+	static native int batcherFlushAsync(long batcher);
+
+	/** wsg_batcher_wait: the oldest queued flush's results, as batcherFlush gives them. */
+	static native int batcherWait(long batcher, ByteBuffer[] views, long[] counts);
 
 	/** wsg_batcher_session_state into st (8 bytes). */
 	static native int batcherSessionState(long batcher, int sid, byte[] st);

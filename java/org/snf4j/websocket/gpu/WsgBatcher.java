@@ -281,27 +281,39 @@ public final class WsgBatcher {
 		}
 	}
 
-	/** One device batch per native batcher; frames go back to their sessions, bytes to the sockets. */
+	/**
+	 * One device batch per native batcher; frames go back to their sessions, bytes to
+	 * the sockets.  The decode batches are queued first (wsg_batcher_flush_async), the
+	 * encode batch runs while they are on the device, then each decode is collected.
+	 */
 	synchronized void flush() {
 		flushScheduled = false;
-		flushDecodes();
-		flushEncodes();
-	}
-
-	private void flushDecodes() {
-		ByteBuffer[] views = new ByteBuffer[4];
-		long[] counts = new long[2];
+		List<Native> queued = new ArrayList<Native>();
 		for (Native n : natives.values()) {
 			if (n.dirty.isEmpty())
 				continue;
-			int rc = Wsg.batcherFlush(n.handle, views, counts);
+			int rc = Wsg.batcherFlushAsync(n.handle);
 			if (rc != 0)
-				throw new IllegalStateException("wsg_batcher_flush: " + rc);
+				throw new IllegalStateException("wsg_batcher_flush_async: " + rc);
+			queued.add(n);
+		}
+		flushEncodes();
+		collectDecodes(queued);
+	}
+
+	private void collectDecodes(List<Native> queued) {
+		ByteBuffer[] views = new ByteBuffer[5];
+		long[] counts = new long[2];
+		for (Native n : queued) {
+			int rc = Wsg.batcherWait(n.handle, views, counts);
+			if (rc != 0)
+				throw new IllegalStateException("wsg_batcher_wait: " + rc);
 			WsgDevices.account(device, counts[1]);
 			ByteBuffer sf = views[0].order(ByteOrder.LITTLE_ENDIAN);
 			ByteBuffer desc = views[1].order(ByteOrder.LITTLE_ENDIAN);
 			ByteBuffer payload = views[2];
 			ByteBuffer result = views[3].order(ByteOrder.LITTLE_ENDIAN);
+			ByteBuffer detail2 = views[4].order(ByteOrder.LITTLE_ENDIAN);
 			List<GpuFrameDecoder> ds = new ArrayList<GpuFrameDecoder>(n.dirty);
 			n.dirty.clear();
 			for (GpuFrameDecoder d : ds) {
@@ -309,12 +321,13 @@ public final class WsgBatcher {
 				final int delivered = result.getInt(Wsg.RESULT_BYTES * d.sid);
 				final int error = result.getShort(Wsg.RESULT_BYTES * d.sid + 4) & 0xffff;
 				final long detail = result.getLong(Wsg.RESULT_BYTES * d.sid + 8);
+				final long d2 = detail2.getLong(8 * d.sid);  // Extended payload length's bound (:393)
 				final List<Frame> frames = new ArrayList<Frame>(delivered);
 				for (int i = 0; i < delivered; ++i)
 					frames.add(frame(desc, payload, first + i));
 				// on the loop thread that owns the session (this batcher's loop); the views are
 				// reused by the next flush, so frames own byte[] copies (Frame.java:53)
-				d.deliver(frames, error, detail);
+				d.deliver(frames, error, detail, d2);
 			}
 		}
 	}

@@ -142,11 +142,31 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFeedArray(JNIEnv*
     return rc;
 }
 
+static int batch_views(JNIEnv* env, const wsg_batch_view* pv, jobjectArray views, jlongArray counts);
+
 JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFlush(JNIEnv* env, jclass c, jlong b,
                                                                      jobjectArray views, jlongArray counts) {
     wsg_batch_view v;
     int rc = wsg_batcher_flush(BATCHER(b), &v);
     if (rc != WSG_API_OK) return rc;
+    return batch_views(env, &v, views, counts);
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFlushAsync(JNIEnv* env, jclass c, jlong b) {
+    return wsg_batcher_flush_async(BATCHER(b));
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherWait(JNIEnv* env, jclass c, jlong b,
+                                                                    jobjectArray views, jlongArray counts) {
+    wsg_batch_view v;
+    int rc = wsg_batcher_wait(BATCHER(b), &v);
+    if (rc != WSG_API_OK) return rc;
+    return batch_views(env, &v, views, counts);
+}
+
+/* the flush view as four direct buffers: session_first, desc, payload, result */
+static int batch_views(JNIEnv* env, const wsg_batch_view* pv, jobjectArray views, jlongArray counts) {
+    wsg_batch_view v = *pv;
     /* payload offsets run to the last descriptor's end; the region is < 2 GiB by contract */
     uint64_t pay = 0;
     for (uint64_t k = 0; k < v.n_frames; ++k) {
@@ -163,6 +183,10 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFlush(JNIEnv* env
     (*env)->SetObjectArrayElement(env, views, 3,
                                   (*env)->NewDirectByteBuffer(env, (void*)v.result,
                                                               (jlong)v.n_sessions * sizeof(wsg_session_result)));
+    if ((*env)->GetArrayLength(env, views) > 4)
+        (*env)->SetObjectArrayElement(env, views, 4,
+                                      (*env)->NewDirectByteBuffer(env, (void*)v.detail2,
+                                                                  (jlong)v.n_sessions * sizeof(int64_t)));
     jlong n[2] = {(jlong)v.n_frames, (jlong)v.wire_bytes};
     (*env)->SetLongArrayRegion(env, counts, 0, 2, n);
     return WSG_API_OK;

@@ -21,7 +21,7 @@ class WsgError(RuntimeError):
 
 class DecoderCfg(C.Structure):
     _fields_ = [("client_mode", C.c_int32), ("allow_extensions", C.c_int32),
-                ("max_payload_len", C.c_int64), ("validate_utf8", C.c_int32), ("reserved", C.c_int32)]
+                ("max_payload_len", C.c_int64), ("validate_utf8", C.c_int32), ("flags", C.c_int32)]
 
 
 class SessionState(C.Structure):
@@ -42,7 +42,7 @@ class SessionResult(C.Structure):
 class BatchView(C.Structure):
     _fields_ = [("n_frames", C.c_uint64), ("wire_bytes", C.c_uint64), ("n_sessions", C.c_uint32),
                 ("reserved", C.c_uint32), ("session_first", C.c_void_p), ("desc", C.c_void_p),
-                ("payload", C.c_void_p), ("result", C.c_void_p)]
+                ("payload", C.c_void_p), ("result", C.c_void_p), ("detail2", C.c_void_p)]
 
 
 class StageCfg(C.Structure):
@@ -144,6 +144,9 @@ def _load():
         "wsg_batcher_flush": ([p, P(BatchView)], i32),
         "wsg_batcher_session_state": ([p, u32, P(SessionState)], i32),
         "wsg_batcher_session_reset": ([p, u32], i32),
+        "wsg_batcher_feed_many": ([p, u32, p, p, p], i32),
+        "wsg_batcher_flush_async": ([p], i32),
+        "wsg_batcher_wait": ([p, P(BatchView)], i32),
         "wsg_batcher_set_stages": ([p, P(StageCfg)], i32),
         "wsg_set_tuning": ([p, i32, C.c_int64], i32),
         "wsg_device_policy_init": ([i32], i32),

@@ -458,6 +458,45 @@ class NativeBatcher:
         from ._lib import lib
         self._check(lib.wsg_batcher_session_reset(self._h, int(sid)))
 
+    def feed_many(self, sids, chunks):
+        """Many socket reads in one call (wsg_batcher_feed_many): chunks[i] of session
+        sids[i]; each session's reads in order, the sessions fed by several threads."""
+        import ctypes as C
+        from ._lib import lib
+        n = len(sids)
+        arrs = [c if isinstance(c, np.ndarray) else np.frombuffer(bytes(c), dtype=np.uint8) for c in chunks]
+        sid_a = np.ascontiguousarray(sids, dtype=np.uint32)
+        ptrs = (C.c_void_p * max(1, n))(*[a.ctypes.data if a.size else None for a in arrs])
+        lens = np.array([a.size for a in arrs], dtype=np.uint64)
+        self._check(lib.wsg_batcher_feed_many(self._h, n, sid_a.ctypes.data, C.addressof(ptrs), lens.ctypes.data))
+
+    def feed_many_ptrs(self, sids, ptrs, lens):
+        """feed_many over numpy arrays: session ids (u32), host addresses (u64) and
+        lengths (u64) of the reads — no per-read Python objects."""
+        from ._lib import lib
+        sids = np.ascontiguousarray(sids, dtype=np.uint32)
+        ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint64)
+        self._check(lib.wsg_batcher_feed_many(self._h, len(sids), sids.ctypes.data, ptrs.ctypes.data,
+                                              lens.ctypes.data))
+
+    def flush_async(self):
+        """Queue the decode of everything complete (wsg_batcher_flush_async); collect it
+        with wait().  At most two in flight."""
+        from ._lib import lib
+        self._check(lib.wsg_batcher_flush_async(self._h))
+
+    def wait_raw(self):
+        """The oldest queued flush's results (wsg_batcher_wait), as flush_raw returns them."""
+        import ctypes as C
+        from ._lib import BatchView, lib
+        v = BatchView()
+        self._check(lib.wsg_batcher_wait(self._h, C.byref(v)))
+        return self._views(v)
+
+    def wait(self):
+        return self._frames(*self.wait_raw()[:4])
+
     def flush_raw(self):
         """Decode everything complete; returns numpy views (valid until the next flush):
         (session_first, desc, payload, result, wire_bytes)."""
@@ -465,6 +504,10 @@ class NativeBatcher:
         from ._lib import BatchView, lib
         v = BatchView()
         self._check(lib.wsg_batcher_flush(self._h, C.byref(v)))
+        return self._views(v)
+
+    def _views(self, v):
+        import ctypes as C
         n, s = int(v.n_frames), int(v.n_sessions)
 
         def view(ptr, count, dtype):
@@ -478,11 +521,15 @@ class NativeBatcher:
         res = view(v.result, s, RESULT_DTYPE)
         end = int((desc["payload_off"] + desc["payload_len"]).max()) if n else 0
         payload = view(v.payload, end, np.uint8)
+        self._detail2 = view(v.detail2, s, np.int64) if v.detail2 else np.zeros(s, np.int64)
         return sf, desc, payload, res, int(v.wire_bytes)
 
     def flush(self):
         """[(frames, InvalidFrameException | None)] per session, like SessionBatcher.flush."""
-        sf, desc, payload, res, _ = self.flush_raw()
+        return self._frames(*self.flush_raw()[:4])
+
+    def _frames(self, sf, desc, payload, res):
+        d2 = self._detail2
         out = []
         for s in range(self.n):
             r = res[s]
@@ -498,7 +545,7 @@ class NativeBatcher:
                     frames.append(make_frame(int(d["opcode"]), bool(d["flags"] & 0x80), rsv, data))
             exc = None
             if r["error"]:
-                exc = InvalidFrameException(error_message(int(r["error"]), int(r["detail"])))
+                exc = InvalidFrameException(error_message(int(r["error"]), int(r["detail"]), int(d2[s])))
                 exc.close_code = int(r["close_code"])
             out.append((frames, exc))
         return out

@@ -154,6 +154,11 @@ static void timed(wsg_ctx* c, int kid, F&& f) {
   c->pending.push_back(p);
 }
 
+namespace ws {
+hipError_t ctx_wait_prev_state(wsg_ctx* c) { return c->ev_prev_state ? hipEventSynchronize(c->ev_prev_state) : hipSuccess; }
+hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e) { return hipEventRecord(e, c->s_out ? c->s_out : c->stream); }
+}  // namespace ws
+
 extern "C" {
 
 int wsg_version(void) { return WSG_ABI_VERSION; }
@@ -371,6 +376,7 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.n_pieces = piece_bound(wire_len, n_frames);
   a.validator_only = 0;
   a.in_desc = nullptr;
+  a.sparse = (cfg->flags & WSG_CFG_SPARSE) != 0;
   a.fused_scan = a.nblk <= FUSED_SCAN_MAX_BLOCKS && c->fused_scan;
   if (n_frames) {
     timed(c, K_PARSE, [&] { launch_parse(a, c->stream); });
@@ -424,6 +430,7 @@ int wsg_validate_batch_device(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n
   a.n_pieces = piece_bound(payload_len, n_frames);
   a.validator_only = 1;
   a.in_desc = desc;
+  a.sparse = 0;
   a.fused_scan = a.nblk <= FUSED_SCAN_MAX_BLOCKS && c->fused_scan;
   if (n_frames) {
     timed(c, K_PARSE, [&] { launch_vparse(a, c->stream); });

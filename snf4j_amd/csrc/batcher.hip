@@ -1,22 +1,30 @@
 // batcher.hip — the host side of the drop-in boundary:
-// the cross-session batcher a JNI shim drives, and a pinned-host buffer pool in
+// the cross-session batchers a JNI shim drives, and a pinned-host buffer pool in
 // the role of snf4j's IByteBufferAllocator (IByteBufferAllocator.java:38-149).
 //
 // The reference decodes inside each session's read loop: StreamSession
 // .consumeBuffer (StreamSession.java:798-854) asks FrameDecoder.available()
 // (FrameDecoder.java:357-401) how many bytes form the next frame and hands that
-// many to decode().  Here every session's socket bytes are fed to one batcher;
-// it runs the same delimiting per session on the host (available(), then the
-// header-only rules as soon as a header is complete, as FrameDecoder.decode does
-// before the payload arrives, :197-256), keeps complete frames in the session's
-// input buffer with the partial one after them, and flush() gathers all
-// sessions' complete frames into pinned staging (threads over byte-balanced
-// slices of the sessions) and decodes them in ONE device batch
-// (wsg_decode_batch_host_async).  Per-session decoder state (fragmentation,
-// UTF-8 carry, closed) persists across flushes.
+// many to decode().  Here every session's socket bytes are fed to one batcher:
+// a feed copies each session's reads (after its carried partial frame) into a
+// region of the open batch's pinned arena and delimits the frames there
+// (available(), then the header-only rules as soon as a header is complete, as
+// FrameDecoder.decode does before the payload arrives, :197-256); complete
+// frames stay where they landed (WSG_CFG_SPARSE), the partial tail is carried.
+// flush_async submits the arena as one device batch (wsg_decode_batch_host_async:
+// H2D, decode, D2H) without gathering anything; up to two batches are in flight
+// while the next one is fed.  Per-session decoder state (fragmentation, UTF-8
+// carry, closed) chains through the batches on the device.  The stages after the
+// decoder (inflate, validator, aggregator) and the cross-session encode batcher
+// are here too.
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <memory>
 #include <map>
 #include <mutex>
 #include <string>
@@ -48,12 +56,11 @@ struct PinnedBuf {
 };
 
 struct SessIn {
-  std::vector<uint8_t> buf;    // complete frames [0, complete), then the partial frame's bytes
-  size_t complete = 0;         // bytes of complete frames
-  std::vector<uint32_t> lens;  // lengths of the complete frames
-  bool frag = false;           // FrameDecoder.fragmentation as of the complete frames
+  std::vector<uint8_t> buf;    // the partial frame's bytes, carried to the session's next read
+  bool frag = false;           // FrameDecoder.fragmentation as of the frames fed so far
   int32_t host_err = 0;        // header error seen on the host (its frame may never complete)
-  int64_t d1 = 0;
+  int64_t d1 = 0, d2 = 0;
+  bool host_closed = false;    // the session failed: further input is swallowed
 };
 
 uint32_t hdr_len(const uint8_t* p) {
@@ -72,6 +79,75 @@ uint64_t frame_total(const uint8_t* p) {
   }
   return hdr_len(p) + len;
 }
+
+// A persistent pool for the batcher's host work (feeds, the flush gather): creating
+// threads per call cost ~30 us each, per round.  run(T, fn) runs fn(0..T-1) on the
+// pool and the calling thread and returns when all are done.
+class Pool {
+ public:
+  explicit Pool(uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) w_.emplace_back([this] { loop(); });
+  }
+  ~Pool() {
+    {
+      std::lock_guard<std::mutex> g(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : w_) t.join();
+  }
+  uint32_t size() const { return (uint32_t)w_.size() + 1; }
+  void run(uint32_t T, const std::function<void(uint32_t)>& fn) {
+    if (T <= 1 || w_.empty()) {
+      for (uint32_t t = 0; t < T; ++t) fn(t);
+      return;
+    }
+    {
+      std::lock_guard<std::mutex> g(m_);
+      job_ = &fn;
+      njobs_ = T;
+      next_.store(0);
+      left_ = T;
+      ++gen_;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> l(m_);
+    done_.wait(l, [this] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  void work() {
+    for (;;) {
+      const uint32_t t = next_.fetch_add(1);
+      if (t >= njobs_) return;
+      (*job_)(t);
+      std::lock_guard<std::mutex> g(m_);
+      if (--left_ == 0) done_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> l(m_);
+        cv_.wait(l, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> w_;
+  std::mutex m_;
+  std::condition_variable cv_, done_;
+  const std::function<void(uint32_t)>* job_ = nullptr;
+  uint32_t njobs_ = 0, left_ = 0;
+  std::atomic<uint32_t> next_{0};
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
 
 }  // namespace
 
@@ -92,14 +168,42 @@ struct StageBatch {
   std::vector<uint32_t> n_ok;           // [S] frames of the session that go on (<= its count)
 };
 
+// One flush's pinned staging and results (two alternate: a flush can be in flight
+// while the next one gathers).
+struct HostErr {
+  uint32_t sid;
+  int32_t err;
+  int64_t d1, d2;
+};
+struct FlushSlot {
+  // the batch's wire: each feed's bytes of a session land in a region of the arena
+  // (its carried partial frame first), so the flush gathers nothing; the complete
+  // frames are where they landed (WSG_CFG_SPARSE), a partial tail is a gap
+  PinnedBuf arena;
+  uint64_t arena_len = 0;
+  std::vector<std::vector<uint64_t>> fo;  // [n]: the session's complete frames (arena offsets), in order
+  std::vector<uint64_t> fb;               // [n]: their bytes
+  PinnedBuf off, sf, payload, desc, result;
+  uint64_t F = 0, W = 0;
+  std::vector<HostErr> host_err;  // header errors found on the host after this batch's frames
+  std::vector<uint32_t> resets;   // slots given to a new session while this batch was in flight
+  std::vector<int64_t> detail2;   // [n]: the view's detail2
+  hipEvent_t done = nullptr;      // after its downloads
+};
+
 struct wsg_batcher {
   wsg_ctx* ctx = nullptr;
   wsg_decoder_cfg cfg{};
   uint32_t n = 0;
   std::vector<SessIn> s;
-  std::vector<wsg_session_state> state;
-  PinnedBuf wire, off, sf, st, payload, desc, result;
+  std::vector<wsg_session_state> state;  // the carry as of the last waited flush (+ host changes)
+  PinnedBuf st;                          // the carry the device batches chain through
+  FlushSlot fs[3];                       // one being fed, up to two in flight
+  int open = 0;                          // the slot feeds land in
+  std::deque<int> q;                     // flushes in flight, oldest first
+  std::vector<std::pair<uint32_t, int>> patch;  // host changes for the next batch's state: 0 reset, 1 closed
   uint32_t threads = 8;
+  std::unique_ptr<Pool> pool;           // threads - 1 workers (the caller is the last one)
   std::string err;
   // stages after the decoder (wsg_batcher_set_stages)
   wsg_stage_cfg stages{};
@@ -404,6 +508,11 @@ int wsg_batcher_open(wsg_ctx* ctx, const wsg_decoder_cfg* cfg, uint32_t n_sessio
   b->state.assign(n_sessions, wsg_session_state{});
   const unsigned hw = std::thread::hardware_concurrency();
   b->threads = hw ? std::min(16u, hw) : 8u;
+  b->pool.reset(new Pool(b->threads - 1));
+  for (FlushSlot& f : b->fs) {
+    f.fo.resize(n_sessions);
+    f.fb.assign(n_sessions, 0);
+  }
   *out = b;
   return WSG_API_OK;
 }
@@ -411,32 +520,41 @@ int wsg_batcher_open(wsg_ctx* ctx, const wsg_decoder_cfg* cfg, uint32_t n_sessio
 int wsg_batcher_close(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
   (void)wsg_sync(b->ctx);
-  PinnedBuf* bufs[] = {&b->wire, &b->off, &b->sf, &b->st, &b->payload, &b->desc, &b->result};
-  for (PinnedBuf* p : bufs) p->release();
+  for (FlushSlot& f : b->fs) {
+    PinnedBuf* bufs[] = {&f.arena, &f.off, &f.sf, &f.payload, &f.desc, &f.result};
+    for (PinnedBuf* p : bufs) p->release();
+    if (f.done) (void)hipEventDestroy(f.done);
+  }
+  b->st.release();
   delete b;
   return WSG_API_OK;
 }
 
 const char* wsg_batcher_last_error(wsg_batcher* b) { return b ? b->err.c_str() : "null batcher"; }
 
-int wsg_batcher_feed(wsg_batcher* b, uint32_t sid, const uint8_t* data, uint64_t len) {
-  if (!b || sid >= b->n || (len && !data)) return WSG_API_EINVAL;
+// The session read loop over one session's region (StreamSession.java:798-854 over
+// FrameDecoder.available, FrameDecoder.java:357-401): the region holds its carried
+// partial frame and this feed's reads; every complete frame stays where it is (its
+// offset is recorded), the header rules apply as soon as a header is complete
+// (:197-256), and a partial tail is copied out to be carried.  Touches only session
+// sid's state and region.
+static void frame_region(wsg_batcher* b, FlushSlot& f, uint32_t sid, uint64_t start, uint64_t end) {
   SessIn& x = b->s[sid];
-  if (b->state[sid].closed || x.host_err) return WSG_API_OK;  // FrameDecoder.closed: input is swallowed
-  if (x.buf.capacity() < x.buf.size() + len) x.buf.reserve(std::max(x.buf.size() + len, 2 * x.buf.capacity()));
-  x.buf.insert(x.buf.end(), data, data + len);
-  size_t pos = x.complete;
+  const uint8_t* const ar = f.arena.p;
+  uint64_t pos = start;
   for (;;) {
-    const uint64_t rem = x.buf.size() - pos;
+    const uint64_t rem = end - pos;
     uint8_t hdr[16] = {0};  // available() and the header rules read <= 14 bytes
-    memcpy(hdr, x.buf.data() + pos, rem < 14 ? rem : 14);
+    memcpy(hdr, ar + pos, rem < 14 ? rem : 14);
     int32_t e = 0;
     int64_t d1 = 0, d2 = 0;
     const int64_t r = wsg_frame_available(hdr, rem, &e, &d1, &d2);  // FrameDecoder.available
     if (r < 0) {  // the u64 length errors (:388-394)
       x.host_err = e;
       x.d1 = d1;
-      break;
+      x.d2 = d2;
+      x.buf.clear();
+      return;
     }
     if (r == 0) break;  // header incomplete
     const uint32_t hl = hdr_len(hdr);
@@ -444,119 +562,276 @@ int wsg_batcher_feed(wsg_batcher* b, uint32_t sid, const uint8_t* data, uint64_t
     if (he && he != WSG_E_BATCH) {  // a header rule fails now (:197-256)
       x.host_err = he;
       x.d1 = d1;
-      break;
+      x.d2 = 0;
+      x.buf.clear();
+      return;
     }
     const uint64_t total = frame_total(hdr);
-    if (rem < total) break;  // partial frame: stays on the host (FrameDecoder.java:276-283)
+    if (rem < total) break;  // partial frame: carried (FrameDecoder.java:276-283)
     const uint32_t op = hdr[0] & 15u;
     if (op <= WSG_OP_BINARY) x.frag = !(hdr[0] & 0x80u);
-    x.lens.push_back((uint32_t)total);
+    f.fo[sid].push_back(pos);
+    f.fb[sid] += total;
     pos += total;
   }
-  x.complete = pos;
+  x.buf.assign(ar + pos, ar + end);
+}
+
+// Arena bytes on demand, keeping what is there (pinned: the H2D source)
+static hipError_t arena_grow(FlushSlot& f, uint64_t need) {
+  if (need <= f.arena.n && f.arena.p) return hipSuccess;
+  PinnedBuf g;
+  const hipError_t e = g.ensure(std::max<uint64_t>(need, 2 * (uint64_t)f.arena.n));
+  if (e != hipSuccess) return e;
+  if (f.arena_len) memcpy(g.p, f.arena.p, f.arena_len);
+  f.arena.release();
+  f.arena = g;
+  return hipSuccess;
+}
+
+// Many socket reads at once (a selector loop's reads of one iteration, in order):
+// each session with reads gets one region of the open batch's pinned arena, its
+// carried partial frame then its reads, copied there and framed in place by up to
+// 16 threads (the sessions are independent): the bytes are copied once, into
+// memory the DMA engines read.
+int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, const uint8_t* const* data,
+                          const uint64_t* lens) {
+  if (!b || (n && (!sids || !data || !lens))) return WSG_API_EINVAL;
+  const uint32_t S = b->n;
+  for (uint32_t i = 0; i < n; ++i)
+    if (sids[i] >= S || (lens[i] && !data[i])) return WSG_API_EINVAL;
+  // the reads of each session, in order (a stable counting sort by session)
+  std::vector<uint32_t> first(S + 1, 0), order(n);
+  for (uint32_t i = 0; i < n; ++i) ++first[sids[i] + 1];
+  for (uint32_t s = 0; s < S; ++s) first[s + 1] += first[s];
+  {
+    std::vector<uint32_t> at(first.begin(), first.end() - 1);
+    for (uint32_t i = 0; i < n; ++i) order[at[sids[i]]++] = i;
+  }
+  FlushSlot& f = b->fs[b->open];
+  // regions: the sessions that read, each its carried bytes + its reads.  A session
+  // still inside one large frame after these reads only appends them to its carried
+  // bytes (copying a growing partial frame into a region at every read would be
+  // quadratic); the frame gets its region once complete.
+  std::vector<uint32_t> ts, acc;
+  std::vector<uint64_t> rs;  // region starts (then the end)
+  uint64_t pos = f.arena_len;
+  for (uint32_t s = 0; s < S; ++s) {
+    if (first[s + 1] == first[s]) continue;
+    const SessIn& x = b->s[s];
+    if (b->state[s].closed || x.host_err || x.host_closed) continue;  // FrameDecoder.closed: input swallowed
+    uint64_t add = 0;
+    for (uint32_t j = first[s]; j < first[s + 1]; ++j) add += lens[order[j]];
+    if (!add) continue;
+    if (x.buf.size() >= 14 && x.buf.size() + add < frame_total(x.buf.data())) {
+      acc.push_back(s);
+      continue;
+    }
+    ts.push_back(s);
+    rs.push_back(pos);
+    pos += x.buf.size() + add;
+  }
+  for (uint32_t s : acc) {
+    SessIn& x = b->s[s];
+    for (uint32_t j = first[s]; j < first[s + 1]; ++j) {
+      const uint32_t r = order[j];
+      x.buf.insert(x.buf.end(), data[r], data[r] + lens[r]);
+    }
+  }
+  if (ts.empty()) return WSG_API_OK;
+  rs.push_back(pos);
+  B_TRY(b, arena_grow(f, pos + 64));
+  auto region = [&](uint32_t i) {
+    const uint32_t s = ts[i];
+    SessIn& x = b->s[s];
+    uint8_t* d = f.arena.p + rs[i];
+    if (!x.buf.empty()) memcpy(d, x.buf.data(), x.buf.size());
+    d += x.buf.size();
+    for (uint32_t j = first[s]; j < first[s + 1]; ++j) {
+      const uint32_t r = order[j];
+      if (lens[r]) memcpy(d, data[r], lens[r]);
+      d += lens[r];
+    }
+    frame_region(b, f, s, rs[i], rs[i + 1]);
+  };
+  const uint64_t bytes = pos - f.arena_len;
+  const uint32_t R = (uint32_t)ts.size();
+  const uint32_t T = bytes < (4u << 20) ? 1u : std::min<uint32_t>(b->pool->size(), R);
+  if (T <= 1) {
+    for (uint32_t i = 0; i < R; ++i) region(i);
+  } else {  // byte-balanced runs of regions, one a thread
+    std::vector<uint32_t> cut(T + 1, R);
+    cut[0] = 0;
+    for (uint32_t t = 1; t < T; ++t) {
+      const uint64_t target = f.arena_len + bytes * t / T;
+      uint32_t i = cut[t - 1];
+      while (i < R && rs[i + 1] <= target) ++i;
+      cut[t] = i;
+    }
+    b->pool->run(T, [&](uint32_t t) {
+      for (uint32_t i = cut[t]; i < cut[t + 1]; ++i) region(i);
+    });
+  }
+  f.arena_len = pos;
   return WSG_API_OK;
 }
 
-int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out) {
-  if (!b || !out) return WSG_API_EINVAL;
+int wsg_batcher_feed(wsg_batcher* b, uint32_t sid, const uint8_t* data, uint64_t len) {
+  if (!b || sid >= b->n || (len && !data)) return WSG_API_EINVAL;
+  return wsg_batcher_feed_many(b, 1, &sid, &data, &len);
+}
+
+// The carry state the next batch starts from: the previous batch's downloaded state
+// (or the host copy when none is in flight) with the host's changes since applied.
+static int stage_state(wsg_batcher* b) {
   const uint32_t S = b->n;
-  std::vector<uint64_t> sbytes(S + 1, 0);
-  std::vector<uint32_t> sfr(S + 1, 0);
-  for (uint32_t i = 0; i < S; ++i) {
-    sbytes[i + 1] = sbytes[i] + b->s[i].complete;
-    sfr[i + 1] = sfr[i] + (uint32_t)b->s[i].lens.size();
-  }
-  const uint64_t W = sbytes[S], F = sfr[S];
-  B_TRY(b, b->wire.ensure(W + 64));
-  B_TRY(b, b->off.ensure((F + 1) * sizeof(uint64_t)));
-  B_TRY(b, b->sf.ensure((S + 1) * sizeof(uint32_t)));
   B_TRY(b, b->st.ensure((S + 1) * sizeof(wsg_session_state)));
-  const uint64_t pcap = W + 16 * F + 16;
-  B_TRY(b, b->payload.ensure(pcap));
-  B_TRY(b, b->desc.ensure((F + 1) * sizeof(wsg_frame_desc)));
-  B_TRY(b, b->result.ensure((S + 1) * sizeof(wsg_session_result)));
-  uint64_t* off = (uint64_t*)b->off.p;
-  uint32_t* sf = (uint32_t*)b->sf.p;
-  memcpy(sf, sfr.data(), (S + 1) * sizeof(uint32_t));
-  if (S) memcpy(b->st.p, b->state.data(), S * sizeof(wsg_session_state));
-  // gather the complete frames into pinned staging: byte-balanced slices of the
-  // sessions, one thread each (a single thread below 8 MiB)
-  auto work = [&](uint32_t lo, uint32_t hi) {
-    for (uint32_t i = lo; i < hi; ++i) {
-      SessIn& x = b->s[i];
-      if (x.complete) memcpy(b->wire.p + sbytes[i], x.buf.data(), x.complete);
-      uint64_t o = sbytes[i];
-      uint32_t k = sfr[i];
-      for (uint32_t l : x.lens) {
-        off[k++] = o;
-        o += l;
-      }
-    }
-  };
-  const uint32_t T = (W < (8u << 20) || S < 2) ? 1u : std::min<uint32_t>(b->threads, S);
-  if (T <= 1) {
-    work(0, S);
-  } else {
-    std::vector<std::thread> pool;
-    uint32_t lo = 0;
-    for (uint32_t t = 0; t < T && lo < S; ++t) {
-      uint32_t hi = lo + 1;
-      if (t + 1 == T) {
-        hi = S;
-      } else {
-        const uint64_t target = W * (t + 1) / T;
-        while (hi < S && sbytes[hi + 1] <= target) ++hi;
-      }
-      pool.emplace_back(work, lo, hi);
-      lo = hi;
-    }
-    for (auto& th : pool) th.join();
+  wsg_session_state* st = (wsg_session_state*)b->st.p;
+  if (b->q.empty()) {
+    if (S) memcpy(st, b->state.data(), S * sizeof(wsg_session_state));
+  } else {  // the state download of the batch in flight (it completes before its payload)
+    B_TRY(b, ws::ctx_wait_prev_state(b->ctx));
   }
-  off[F] = W;
-  int rc = wsg_decode_batch_host_async(b->ctx, &b->cfg, b->wire.p, W, off, F, sf, S, (wsg_session_state*)b->st.p,
-                                       b->payload.p, pcap, (wsg_frame_desc*)b->desc.p,
-                                       (wsg_session_result*)b->result.p);
-  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
-  rc = wsg_sync(b->ctx);
-  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
-  if (S) memcpy(b->state.data(), b->st.p, S * sizeof(wsg_session_state));
-  // consume the decoded frames; merge the host-detected header errors of the
-  // sessions the device did not fail first (their frame may never complete)
-  wsg_session_result* res = (wsg_session_result*)b->result.p;
+  for (const auto& pt : b->patch) {
+    if (pt.second == 0) st[pt.first] = wsg_session_state{};  // a reset slot
+    else st[pt.first].closed = 1;                            // failed on the host / by a stage
+  }
+  b->patch.clear();
+  return WSG_API_OK;
+}
+
+int wsg_batcher_flush_async(wsg_batcher* b) {
+  if (!b) return WSG_API_EINVAL;
+  if (b->q.size() >= 2) return bset(b, WSG_API_ERANGE, "two flushes in flight: wsg_batcher_wait first");
+  const uint32_t S = b->n;
+  int rc;
+  const int slot = b->open;
+  FlushSlot& f = b->fs[slot];
+  // the batch's frames, session by session, where they landed
+  uint64_t F = 0, W = 0;
+  for (uint32_t i = 0; i < S; ++i) {
+    F += f.fo[i].size();
+    W += f.fb[i];
+  }
+  const uint64_t wl = f.arena_len;
+  B_TRY(b, arena_grow(f, wl + 64));
+  B_TRY(b, f.off.ensure((F + 1) * sizeof(uint64_t)));
+  B_TRY(b, f.sf.ensure((S + 1) * sizeof(uint32_t)));
+  const uint64_t pcap = wl + 16 * F + 16;
+  B_TRY(b, f.payload.ensure(pcap));
+  B_TRY(b, f.desc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, f.result.ensure((S + 1) * sizeof(wsg_session_result)));
+  if (!f.done) B_TRY(b, hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
+  uint64_t* off = (uint64_t*)f.off.p;
+  uint32_t* sf = (uint32_t*)f.sf.p;
+  uint64_t k = 0;
+  for (uint32_t i = 0; i < S; ++i) {
+    sf[i] = (uint32_t)k;
+    for (uint64_t o : f.fo[i]) off[k++] = o;
+  }
+  sf[S] = (uint32_t)k;
+  off[F] = wl;
+  // a header error found on the host follows the frames fed so far: it is this batch's
+  f.host_err.clear();
   for (uint32_t i = 0; i < S; ++i) {
     SessIn& x = b->s[i];
-    if (x.complete) {
-      x.buf.erase(x.buf.begin(), x.buf.begin() + (ptrdiff_t)x.complete);
-      x.complete = 0;
-      x.lens.clear();
-    }
-    if (!res[i].error && x.host_err && !b->state[i].closed) {
-      res[i].error = (uint16_t)x.host_err;
-      res[i].close_code = WSG_CLOSE_PROTOCOL_ERROR;  // every header / length rule closes with 1002
-      res[i].detail = x.d1;
-      b->state[i].closed = 1;
-    }
-    if (b->state[i].closed) {
-      std::vector<uint8_t>().swap(x.buf);  // a closed session swallows further input
+    if (x.host_err) {
+      f.host_err.push_back({i, x.host_err, x.d1, x.d2});
       x.host_err = 0;
+      x.host_closed = true;
+      std::vector<uint8_t>().swap(x.buf);
     }
   }
-  out->n_frames = F;
+  f.resets.clear();
+  f.F = F;
+  f.W = W;
+  // the carry this batch starts from (waits for the previous batch's state download)
+  rc = stage_state(b);
+  if (rc) return rc;
+  wsg_decoder_cfg cfg = b->cfg;
+  cfg.flags |= WSG_CFG_SPARSE;
+  rc = wsg_decode_batch_host_async(b->ctx, &cfg, f.arena.p, wl, off, F, sf, S, (wsg_session_state*)b->st.p,
+                                   f.payload.p, pcap, (wsg_frame_desc*)f.desc.p, (wsg_session_result*)f.result.p);
+  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  B_TRY(b, ws::ctx_record_out(b->ctx, f.done));
+  b->q.push_back(slot);
+  // feeds go to the next slot (waited: at most two in flight)
+  b->open = (b->open + 1) % 3;
+  FlushSlot& g = b->fs[b->open];
+  g.arena_len = 0;
+  for (uint32_t i = 0; i < S; ++i) {
+    g.fo[i].clear();
+    g.fb[i] = 0;
+  }
+  return WSG_API_OK;
+}
+
+int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
+  if (!b || !out) return WSG_API_EINVAL;
+  if (b->q.empty()) return bset(b, WSG_API_ERANGE, "no flush in flight");
+  const int slot = b->q.front();
+  b->q.pop_front();
+  FlushSlot& f = b->fs[slot];
+  B_TRY(b, hipEventSynchronize(f.done));
+  const uint32_t S = b->n;
+  const wsg_session_state* st = (const wsg_session_state*)b->st.p;
+  if (b->q.empty()) {  // the state after the last batch (else the newer batch owns the pinned copy)
+    for (uint32_t i = 0; i < S; ++i) {
+      const bool keep_closed = b->state[i].closed && !st[i].closed;  // latched on the host meanwhile
+      b->state[i] = st[i];
+      if (keep_closed) b->state[i].closed = 1;
+    }
+    for (const auto& pt : b->patch) {
+      if (pt.second == 0) b->state[pt.first] = wsg_session_state{};
+      else b->state[pt.first].closed = 1;
+    }
+  }
+  wsg_session_result* res = (wsg_session_result*)f.result.p;
+  for (uint32_t sid : f.resets) res[sid] = wsg_session_result{};  // a new session has the slot now
+  f.detail2.assign(S, 0);
+  // the host-detected header errors of the sessions the device did not fail first
+  for (const auto& he : f.host_err) {
+    const uint32_t i = he.sid;
+    if (std::find(f.resets.begin(), f.resets.end(), i) != f.resets.end()) continue;
+    if (!res[i].error) {
+      res[i].error = (uint16_t)he.err;
+      res[i].close_code = WSG_CLOSE_PROTOCOL_ERROR;  // every header / length rule closes with 1002
+      res[i].detail = he.d1;
+      f.detail2[i] = he.d2;
+    }
+    b->state[i].closed = 1;
+    b->patch.push_back({i, 1});
+  }
+  out->n_frames = f.F;
   out->n_sessions = S;
-  out->wire_bytes = W;
-  out->session_first = sf;
-  out->desc = (const wsg_frame_desc*)b->desc.p;
-  out->payload = b->payload.p;
+  out->wire_bytes = f.W;
+  out->session_first = (const uint32_t*)f.sf.p;
+  out->desc = (const wsg_frame_desc*)f.desc.p;
+  out->payload = f.payload.p;
   out->result = res;
-  if (!b->has_stages) return WSG_API_OK;
-  const int rc2 = run_stages(b, sf, (const wsg_frame_desc*)b->desc.p, b->payload.p, res);
-  if (rc2) return rc2;
+  out->detail2 = f.detail2.data();
+  out->reserved = 0;
+  // a session failed by the device swallows further input
   for (uint32_t i = 0; i < S; ++i)
-    if (b->state[i].closed) {  // a stage failed it: the session swallows further input
-      std::vector<uint8_t>().swap(b->s[i].buf);
-      b->s[i].host_err = 0;
-      b->s[i].complete = 0;
-      b->s[i].lens.clear();
+    if (res[i].error) {
+      b->state[i].closed = 1;
+      SessIn& x = b->s[i];
+      std::vector<uint8_t>().swap(x.buf);
+      x.host_closed = true;
+    }
+  if (!b->has_stages) return WSG_API_OK;
+  const int rc2 = run_stages(b, out->session_first, out->desc, out->payload, res);
+  if (rc2) return rc2;
+  for (uint32_t i = 0; i < S; ++i) {
+    if (b->fres[i].error != res[i].error) f.detail2[i] = 0;  // (a stage's error has no second argument)
+  }
+  for (uint32_t i = 0; i < S; ++i)
+    if (b->fres[i].error && !res[i].error) {  // a stage failed it: the session swallows further input
+      b->patch.push_back({i, 1});
+      SessIn& x = b->s[i];
+      std::vector<uint8_t>().swap(x.buf);
+      x.host_err = 0;
+      x.host_closed = true;
     }
   out->n_frames = b->fin.desc.size();
   out->session_first = b->fin.sf.data();
@@ -564,6 +839,18 @@ int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out) {
   out->payload = b->fin.pay.data();
   out->result = b->fres.data();
   return WSG_API_OK;
+}
+
+int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out) {
+  if (!b || !out) return WSG_API_EINVAL;
+  while (!b->q.empty()) {  // (results of unwaited async flushes are dropped)
+    wsg_batch_view v;
+    int rc = wsg_batcher_wait(b, &v);
+    if (rc) return rc;
+  }
+  int rc = wsg_batcher_flush_async(b);
+  if (rc) return rc;
+  return wsg_batcher_wait(b, out);
 }
 
 int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
@@ -597,12 +884,16 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
   if (!b || sid >= b->n) return WSG_API_EINVAL;
   SessIn& x = b->s[sid];
   std::vector<uint8_t>().swap(x.buf);
-  std::vector<uint32_t>().swap(x.lens);
-  x.complete = 0;
+  FlushSlot& f = b->fs[b->open];  // its frames fed since the last flush are dropped (gaps now)
+  f.fo[sid].clear();
+  f.fb[sid] = 0;
   x.frag = false;
   x.host_err = 0;
-  x.d1 = 0;
+  x.d1 = x.d2 = 0;
+  x.host_closed = false;
   b->state[sid] = wsg_session_state{};
+  for (int slot : b->q) b->fs[slot].resets.push_back(sid);  // the old session's results in flight are dropped
+  b->patch.push_back({sid, 0});
   if (b->has_stages) {  // fresh stage decoders too
     b->ss[sid] = StageSess{};
     b->istate[sid] = wsg_inflate_state{};

@@ -249,7 +249,9 @@ __device__ __forceinline__ DAgg parse_one(const DecodeArgs& a, uint64_t k, uint6
   } else {
     pre = rules_pre(hd, a.client_mode, a.allow_ext);
     post = rules_post(hd, a.max_payload);
-    if (!pre && !post && (uint64_t)hd.hdr_len + hd.plen != ext) pre = WSG_E_BATCH;
+    // the batch's frame extent must be the header's (sparse: the frame must fit before the wire end)
+    if (!pre && !post && (a.sparse ? (uint64_t)hd.hdr_len + hd.plen > ext : (uint64_t)hd.hdr_len + hd.plen != ext))
+      pre = WSG_E_BATCH;
     if (!pre && !post) {
       len = (uint32_t)hd.plen;
       src = o + hd.hdr_len;
@@ -310,7 +312,7 @@ __global__ __launch_bounds__(DBLOCK) void k_parse(DecodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
   DAgg v = DAGG_ID;
   if (k < a.n_frames) {
-    const uint64_t o = a.frame_off[k], e = a.frame_off[k + 1];
+    const uint64_t o = a.frame_off[k], e = a.sparse ? a.wire_len : a.frame_off[k + 1];
     // wire words from o & ~3 (zero past the wire end)
     uint32_t d[6];
     const uint64_t a4 = o & ~3ull;

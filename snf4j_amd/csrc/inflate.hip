@@ -2038,8 +2038,20 @@ constexpr uint32_t FD_LIT = 0x80000000u;  // descriptor: a resolved byte (bits 0
 constexpr int32_t FD_BIAS = 32768;        // descriptor: position + FD_BIAS (history positions are >= -32768)
 
 constexpr int FNT = 256;  // threads per session (4 waves)
+// WSG_FAST_RING=1 (A/B build, not the default): the session's last 32 KiB of output in
+// an LDS ring, so a copy's source bytes come from LDS instead of HBM, and the ring is
+// the window image the batch commits.  52 KB of LDS a session allows 3 sessions a CU
+// instead of 6: k_infl_fast 2.27 -> 3.07 ms (same-box), the VALU-bound expansion
+// loses more from the halved occupancy than the gather gains.
+#ifndef WSG_FAST_RING
+#define WSG_FAST_RING 0
+#endif
 #ifndef WSG_FAST_WAVES
+#if WSG_FAST_RING
+#define WSG_FAST_WAVES 3  // waves a SIMD: what the LDS allows (3 sessions of 4 waves a CU)
+#else
 #define WSG_FAST_WAVES 6  // waves a SIMD: the register budget (80 VGPRs) that keeps 6 sessions a CU
+#endif
 #endif
 
 // block-wide exclusive sum of a packed (hi, lo) pair of 32-bit counts; the totals
@@ -2068,6 +2080,10 @@ __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, u
 __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WAVES))) void k_infl_fast(InflArgs a) {
   __shared__ uint32_t fd[FC];
   __shared__ uint32_t lbuf[FC / 4 + 2];  // the chunk's literal bytes (at most FC), from a dword boundary
+#if WSG_FAST_RING
+  __shared__ uint4 ring16[WSG_INFLATE_WINDOW / 16];  // history: position p at byte (p + ph) & WMASK
+  uint8_t* const ring = reinterpret_cast<uint8_t*>(ring16);
+#endif
   __shared__ uint64_t wsum[FNT / 64];
   __shared__ uint32_t x_first, x_off, x_li, x_lf;
   const int lane = threadIdx.x;  // (the block's thread: FNT per session)
@@ -2094,6 +2110,12 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
   int32_t pos = 0, wstart = -wl0;
   bool bad = false;
   int compressing = 0;
+#if WSG_FAST_RING
+  if (wl0) {  // the carried-in history (a ring image with the same phase)
+    for (uint32_t i = (uint32_t)lane; i < WSG_INFLATE_WINDOW / 16; i += FNT) ring16[i] = reinterpret_cast<const uint4*>(win)[i];
+    __syncthreads();
+  }
+#endif
   for (uint32_t k = f0; k < f1 && !bad; ++k) {
     const wsg_frame_desc d = a.desc[k];
     const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
@@ -2225,8 +2247,12 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           v[u] = j < n ? fd[j] : FD_LIT;
           if (!(v[u] & FD_LIT)) {
             const int32_t q = (int32_t)v[u] - FD_BIAS;
+#if WSG_FAST_RING
+            v[u] = FD_LIT | (uint32_t)ring[((uint32_t)q + ph) & WMASK];  // (q >= C0 - 32768: still in the ring)
+#else
             v[u] = FD_LIT | (q >= 0 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rout, (uint32_t)q, 0, 1)
                                     : (uint32_t)win[((uint32_t)q + ph) & WMASK]);
+#endif
           }
         }
 #pragma unroll
@@ -2251,6 +2277,11 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       }
       const uint32_t tb = head + 4u * nw;
       if ((uint32_t)lane < n - tb) dst[tb + lane] = (uint8_t)fd[tb + lane];
+#if WSG_FAST_RING
+      // into the history ring (the chunk's gathers are done: the slots it overwrites, 32 KiB
+      // back, are no longer read)
+      for (uint32_t j = (uint32_t)lane; j < n; j += FNT) ring[((uint32_t)C0 + j + ph) & WMASK] = (uint8_t)fd[j];
+#endif
       // the stores complete before the next chunk gathers from them
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __syncthreads();
@@ -2283,6 +2314,16 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
   st.finished = 0;
   st.window_len = 0;
   st.window_phase = 0;
+#if WSG_FAST_RING
+  if (has_dec) {  // the ring is the new window image (its phase moves with the output)
+    const int32_t P = pos, nh = (P - wstart) < (int32_t)WSG_INFLATE_WINDOW ? (P - wstart) : (int32_t)WSG_INFLATE_WINDOW;
+    __syncthreads();
+    uint4* const wout16 = reinterpret_cast<uint4*>(a.window + (uint64_t)s * WSG_INFLATE_WINDOW);
+    for (uint32_t i = (uint32_t)lane; i < WSG_INFLATE_WINDOW / 16; i += FNT) wout16[i] = ring16[i];
+    st.window_len = (uint16_t)nh;
+    st.window_phase = (uint16_t)(((uint32_t)P + ph) & WMASK);
+  }
+#else
   if (has_dec) {
     const int32_t P = pos, nh = (P - wstart) < (int32_t)WSG_INFLATE_WINDOW ? (P - wstart) : (int32_t)WSG_INFLATE_WINDOW;
     const uint32_t nph = ((uint32_t)P + ph) & WMASK;
@@ -2334,6 +2375,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
     st.window_len = (uint16_t)nh;
     st.window_phase = (uint16_t)nph;
   }
+#endif
   if (lane == 0) {
     a.state[s] = st;
     wsg_session_result res = {f1 - f0, 0u, 0u, 0};

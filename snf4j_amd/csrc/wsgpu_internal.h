@@ -88,6 +88,7 @@ struct DecodeArgs {
   // payloads in `wire` (k_vparse instead of k_parse), no fragmentation rules, no stores
   int32_t validator_only;
   const wsg_frame_desc* in_desc;
+  int32_t sparse;  // WSG_CFG_SPARSE: a frame's extent is its header's (frames need not be adjacent)
   // in/out
   wsg_session_state* state;
   // outputs
@@ -218,6 +219,12 @@ enum KernelId {
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
+// the context's pipelined host path (api.hip), for the native batcher: wait until the
+// previous async batch's state download is done; record `e` after everything queued
+// on the copy-out stream
+hipError_t ctx_wait_prev_state(wsg_ctx* c);
+hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e);
+
 void launch_parse(const DecodeArgs& a, hipStream_t s);
 void launch_scan(const DecodeArgs& a, hipStream_t s);
 void launch_link(const DecodeArgs& a, hipStream_t s);

@@ -404,30 +404,30 @@ def test_native_batcher_large_random_chunks(ctx, oracle):
         assert (str(e) if e else None) == (str(err[s]) if err[s] else None), s
 
 
-def test_native_batcher_concurrent_feeders(ctx, oracle):
-    """wsg_batcher_feed from 4 threads at once, each owning a slice of the sessions (one
-    feeder per selector loop), then one flush: the same frames and verdicts as the
-    oracle's read loop."""
-    import threading
+def test_native_batcher_feed_many_threaded(ctx, oracle):
+    """wsg_batcher_feed_many with every session's reads of a round in one call (the
+    sessions framed in place by several threads, > 4 MiB a call), big frames that stay
+    partial over several rounds (carried, then landed once complete), then one flush:
+    the same frames and verdicts as the oracle's read loop."""
     from snf4j_amd import NativeBatcher
     rng = np.random.default_rng(34)
     n = 48
     streams = [b"".join(wsgen.session_frames(rng, int(rng.integers(5, 30)), big=bool(s % 3 == 0))) for s in range(n)]
-    cuts = [sorted(int(x) for x in rng.integers(0, len(st) + 1, int(rng.integers(1, 12)))) for st in streams]
+    cuts = [[0] + sorted(int(x) for x in rng.integers(0, len(st) + 1, int(rng.integers(1, 12)))) + [len(st)]
+            for st in streams]
     b = NativeBatcher(n, ctx=ctx)
-
-    def feeder(i):
-        for s in range(i, n, 4):
-            edges = [0] + cuts[s] + [len(streams[s])]
-            for a0, a1 in zip(edges, edges[1:]):
-                if a1 > a0:
-                    b.feed(s, streams[s][a0:a1])
-
-    ts = [threading.Thread(target=feeder, args=(i,)) for i in range(4)]
-    for t in ts:
-        t.start()
-    for t in ts:
-        t.join()
+    for r in range(max(len(c) for c in cuts) - 1):
+        sids, chunks = [], []
+        for s in range(n):
+            if r + 1 < len(cuts[s]) and cuts[s][r + 1] > cuts[s][r]:
+                # a round's read of a session, sometimes split in two reads of the same call
+                a0, a1 = cuts[s][r], cuts[s][r + 1]
+                m = int(rng.integers(a0, a1 + 1))
+                for x0, x1 in ((a0, m), (m, a1)):
+                    if x1 > x0:
+                        sids.append(s)
+                        chunks.append(streams[s][x0:x1])
+        b.feed_many(sids, chunks)
     res = b.flush()
     for s in range(n):
         fr, e = res[s]
@@ -504,4 +504,68 @@ def test_native_batcher_session_reset_reuses_slot(ctx, oracle):
                [(int(f.getOpcode()), f.isFinalFragment(), f.getPayload()) for f in got[s]], s
         assert (str(e) if e else None) == (str(err[s]) if err[s] else None), s
     assert err[1] is not None and err[2] is not None  # a fresh decoder rejects the leading continuation
+    b.close()
+
+
+def test_native_batcher_pipelined_flushes(ctx, oracle):
+    """wsg_batcher_feed_many + flush_async/wait with two flushes in flight: the next
+    reads and gather overlap the device work, the carry chains through the batches on
+    the device.  Random socket chunks (threaded feeds above 4 MiB), header errors the
+    host finds (opcode 3), sessions reset while a flush is in flight; every session's
+    frames and first error == the oracle's read loop (a reset session: its new stream)."""
+    from snf4j_amd import NativeBatcher
+    rng = np.random.default_rng(515)
+    n = 96
+    streams = [b"".join(wsgen.session_frames(rng, int(rng.integers(1, 12)), big=(s % 3 == 0),
+                                            inject=(wsgen.INJECT_KINDS[int(rng.integers(0, 15))]
+                                                    if rng.random() < 0.2 else None)))
+               for s in range(n)]
+    for s in range(0, n, 13):  # a header error the host sees first: a bad opcode after some frames
+        streams[s] += bytes([0x83, 0x85, 1, 2, 3, 4]) + b"\x00" * 5
+    b = NativeBatcher(n, ctx=ctx)
+    got = [[] for _ in range(n)]
+    err = [None] * n
+    pos = [0] * n
+    reset_at = {7: 1, 31: 2, 50: 3}  # session -> round at which its slot gets a new session
+    new = {}
+    pending = 0
+
+    def collect():
+        for s, (fr, e) in enumerate(b.wait()):
+            got[s] += fr
+            if e is not None and err[s] is None:
+                err[s] = e
+
+    rnd = 0
+    while any(pos[s] < len(streams[s]) for s in range(n)) or pending:
+        sids, chunks = [], []
+        for s in range(n):
+            if reset_at.get(s) == rnd:
+                b.reset_session(s)  # (a flush may be in flight: its results for s are dropped)
+                streams[s] = new[s] = b"".join(wsgen.session_frames(rng, int(rng.integers(1, 8))))
+                pos[s], got[s], err[s] = 0, [], None
+            for _ in range(int(rng.integers(0, 3))):
+                if pos[s] < len(streams[s]):
+                    c = int(rng.integers(1, 150000))
+                    sids.append(s)
+                    chunks.append(streams[s][pos[s]:pos[s] + c])
+                    pos[s] += c
+        if sids:
+            b.feed_many(sids, chunks)
+        if pending == 2:
+            collect()
+            pending -= 1
+        if any(pos[s] < len(streams[s]) for s in range(n)) or sids:
+            b.flush_async()
+            pending += 1
+        else:
+            collect()
+            pending -= 1
+        rnd += 1
+    for s in range(n):
+        frames, e = oracle.stream_decode(streams[s], [len(streams[s])])
+        assert [(f.opcode, f.fin, f.payload) for f in frames] == \
+               [(int(f.getOpcode()), f.isFinalFragment(), f.getPayload()) for f in got[s]], s
+        assert (str(e) if e else None) == (str(err[s]) if err[s] else None), s
+    assert set(new) == set(reset_at)
     b.close()

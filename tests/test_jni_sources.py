@@ -33,7 +33,7 @@ def test_every_native_method_is_used():
     # the handshake natives are bound for the handshake stages INTEGRATION.md §1.3d-e describes
     assert unused <= {"handshakeAvailable", "handshakeAcceptBatchHost", "handshakeValidateBatchHost",
                       "batcherSessionState", "checkHeader", "encodedLength", "encodeBatchHost",
-                      "validateBatchHost"}, unused
+                      "validateBatchHost", "batcherFlush"}, unused
 
 
 def test_glue_calls_only_declared_exported_entry_points():
