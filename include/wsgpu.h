@@ -169,14 +169,18 @@ int wsg_close(wsg_ctx* ctx);
  *   WSG_TUNE_INFLATE_LDS     0: the lane pre-decode keeps its tables in HBM
  *   WSG_TUNE_INFLATE_ORDER   0: lanes take frames in batch order (not longest first)
  *   WSG_TUNE_INFLATE_LANES   k_infl_tok lanes at most (multiple of 64)
- *   WSG_TUNE_FUSED_SCAN      0: always launch k_scan (k_link does not fold block aggregates) */
+ *   WSG_TUNE_FUSED_SCAN      0: always launch k_scan (k_link does not fold block aggregates)
+ *   WSG_TUNE_AGG_UNITS       aggregator gather units per wave: 1, 2 (default) or 4
+ *   WSG_TUNE_AGG_GRID        aggregator gather waves at most (default 65536) */
 enum {
     WSG_TUNE_INFLATE_TOKENS = 1,
     WSG_TUNE_INFLATE_FAST = 2,
     WSG_TUNE_INFLATE_LDS = 3,
     WSG_TUNE_INFLATE_ORDER = 4,
     WSG_TUNE_INFLATE_LANES = 5,
-    WSG_TUNE_FUSED_SCAN = 6
+    WSG_TUNE_FUSED_SCAN = 6,
+    WSG_TUNE_AGG_UNITS = 7,
+    WSG_TUNE_AGG_GRID = 8
 };
 int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */

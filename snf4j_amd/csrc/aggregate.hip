@@ -18,18 +18,16 @@
 //                only above 4096 blocks: below, k_agg_b folds them itself)
 //   k_agg_b      thread per frame: open-before-k, membership, emit flag; block sums
 //                of member bytes and emitted frames
-//   k_agg_c      thread per frame: "too big" test, output descriptors, gather
-//                records, and the 1 KiB agg_out pieces starting in each member
-//   k_agg_gather one wave per AGG_PIECES_PER_WAVE 1 KiB pieces of agg_out (grid-stride:
-//                the piece count is known only on the device): 16-B aligned
-//                stores, sources funnelled from aligned loads
+//   k_agg_c      thread per frame: "too big" test, output descriptors, and the
+//                gather units of each member (<= 1 KiB of agg_out, one source range)
+//   k_agg_gather one wave per 2 gather units (WSG_TUNE_AGG_UNITS) (grid-stride: the
+//                unit count is known only on the device): 16-B aligned stores,
+//                sources funnelled from aligned loads
 //   k_agg_final  thread per session: result, carry-out state, PENDING entry
 #include "wsgpu_internal.h"
 #include "wsgpu_scan.h"
 
 namespace ws {
-
-constexpr int AGG_PIECES_PER_WAVE = 2;
 
 constexpr uint32_t AG_VALID = 1u;    // delivered by the decoder (the aggregator sees it)
 constexpr uint32_t AG_START = 2u;    // TEXT/BINARY, not FIN: opens (or replaces) the aggregated frame
@@ -40,10 +38,14 @@ constexpr uint32_t AG_EMIT = 32u;    // emits an output frame (itself, or the ag
 constexpr uint32_t AG_CARRY = 64u;   // member of the frame carried in from an earlier batch
 
 __device__ __forceinline__ uint64_t agg_pos(const AggArgs& a, uint64_t j) { return a.pl[j] + a.blk_sum[j / BLOCK]; }
-// cl / blk_cnt pack two counts: emitted frames (bits 0-31) and non-empty members (32-63)
+// cl / blk_cnt pack two counts: emitted frames (bits 0-31) and gather units (32-63)
 __device__ __forceinline__ uint64_t agg_cnt(const AggArgs& a, uint64_t j) {
   return (a.cl[j] + a.blk_cnt[j / BLOCK]) & 0xffffffffull;
 }
+// A member's bytes go out as gather units: 64 16-B blocks of agg_out each (the first
+// and last block partial), ceil((m + 15) / 1 KiB) of them for m bytes at any
+// alignment (one may come out empty).  A unit copies one source range: no lookups.
+__device__ __forceinline__ uint32_t agg_units(uint64_t m) { return m ? (uint32_t)((m + 15u + PIECE - 1u) / PIECE) : 0u; }
 __device__ __forceinline__ uint64_t agg_mi(const AggArgs& a, uint64_t j) { return (a.cl[j] + a.blk_cnt[j / BLOCK]) >> 32; }
 
 // ------------------------------------------------------------------ k_agg_a
@@ -130,7 +132,7 @@ __global__ __launch_bounds__(1024) void k_agg_scan(AggArgs a, int sums) {
   }
   if (sums && threadIdx.x == 0) {
     *a.agg_total = carry.sum;
-    *a.n_mem = carry_n >> 32;
+    *a.n_units = carry_n >> 32;
   }
 }
 
@@ -145,7 +147,7 @@ __global__ __launch_bounds__(BLOCK) void k_agg_b(AggArgs a) {
   Agg tot;
   Agg ex = block_excl_scan(v, &tot);
   Agg w = AGG_ID;
-  uint64_t emit = 0;  // emitted frame (bit 0) | non-empty member (bit 32)
+  uint64_t emit = 0;  // emitted frame (bit 0) | gather units (bits 32-63)
   // the start / end maxima of every frame before this block: up to 4096 blocks the
   // block folds k_agg_a's block maxima itself (coalesced; max commutes), so the
   // first k_agg_scan launch is skipped; beyond, k_agg_scan left the exclusive maxima
@@ -179,7 +181,7 @@ __global__ __launch_bounds__(BLOCK) void k_agg_b(AggArgs a) {
         c |= AG_MEMBER;
         if (!(c & AG_START) && ls < sf) c |= AG_CARRY;
         w.sum = a.desc[k].payload_len;
-        if (w.sum) emit |= 1ull << 32;
+        emit |= (uint64_t)agg_units(w.sum) << 32;
       }
       if (em) { c |= AG_EMIT; emit |= 1u; }
       a.code[k] = c;
@@ -207,8 +209,6 @@ __global__ __launch_bounds__(BLOCK) void k_agg_c(AggArgs a) {
   const int lane = threadIdx.x & 63;
   const bool live = k < a.n_frames;
   const uint32_t c = live ? a.code[k] : 0u;
-  // every record carries its position (non-members too: the gather's owner search
-  // needs positions non-decreasing over all frames)
   uint64_t pos = live ? agg_pos(a, k) : 0ull, src = 0;
   uint32_t mlen = 0;
   if (c & AG_VALID) {
@@ -255,58 +255,43 @@ __global__ __launch_bounds__(BLOCK) void k_agg_c(AggArgs a) {
       a.out_desc[(uint64_t)sf + s + (agg_cnt(a, k) - agg_cnt(a, sf))] = o;
     }
   }
-  uint32_t mi = 0;
-  if (mlen) {  // the gather records are compacted to the non-empty members
-    mi = (uint32_t)agg_mi(a, k);
-    AggRec r;
-    r.pos = pos;
-    r.src = src;
-    r.mlen = mlen;
-    r.pad = 0;
-    a.rec[mi] = r;
-  }
-  // descriptors of the agg_out pieces whose first byte falls in this member's range,
-  // written cooperatively (as decode.hip k_link): a wave scan of the counts, then
-  // lane i writes the wave's pieces i, i+64, ... after a shuffle search for the owner
-  const uint64_t end = pos + mlen;
-  const uint32_t pc0 = (uint32_t)((pos + PIECE - 1) / PIECE);
-  uint32_t cnt = 0;
-  if (mlen) {
-    uint64_t p1 = (end + PIECE - 1) / PIECE;
-    if (p1 > a.n_pieces) p1 = a.n_pieces;
-    cnt = p1 > pc0 ? (uint32_t)(p1 - pc0) : 0u;
-  }
+  // the member's gather units, written cooperatively (as decode.hip k_link): a wave
+  // scan of the counts, then lane i writes the wave's units i, i+64, ... after a
+  // shuffle search for the owner.  Unit u covers agg_out blocks [pos/16 + 64u, +64)
+  // clipped to the member: info = its first output byte | its byte count << 48,
+  // mask:frame = the source offset of that byte.
+  const uint32_t cnt = agg_units(mlen);
+  const uint64_t u0 = cnt ? agg_mi(a, k) : 0ull;
   uint32_t cum = cnt;
   cum = wave_incl_sum_u32(cum);
   const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)cum, 63);
   cum -= cnt;
   if (!T) return;
-  const uint64_t total = *a.agg_total;
   for (uint32_t t = lane; t < ((T + 63u) & ~63u); t += 64) {
     int o = 0;
 #pragma unroll
     for (int step = 32; step >= 1; step >>= 1)
       if ((uint32_t)__shfl((int)cum, o + step, 64) <= t) o += step;
     const uint32_t o_cum = (uint32_t)__shfl((int)cum, o, 64);
-    const uint32_t o_pc0 = (uint32_t)__shfl((int)pc0, o, 64);
+    const uint64_t o_u0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(u0 >> 32), o, 64) << 32) |
+                          (uint32_t)__shfl((int)(uint32_t)u0, o, 64);
     const uint64_t o_pos = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(pos >> 32), o, 64) << 32) |
                            (uint32_t)__shfl((int)(uint32_t)pos, o, 64);
     const uint64_t o_src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(src >> 32), o, 64) << 32) |
                            (uint32_t)__shfl((int)(uint32_t)src, o, 64);
     const uint32_t o_len = (uint32_t)__shfl((int)mlen, o, 64);
-    const uint32_t o_k = (uint32_t)__shfl((int)mi, o, 64);
     if (t >= T) continue;
-    const uint64_t pc = (uint64_t)o_pc0 + (t - o_cum);
-    const uint64_t ps = pc * PIECE;
-    const uint64_t o_end = o_pos + o_len;
-    const uint32_t j0 = (uint32_t)(ps - o_pos);
-    const bool single = o_end >= ps + PIECE || o_end == total;
+    const uint64_t u = o_u0 + (t - o_cum);
+    if (u >= a.n_pieces) continue;  // holds bytes at or beyond agg_cap only
+    const uint64_t b0 = ((o_pos >> 4) + (uint64_t)(t - o_cum) * 64u) * 16u;
+    const uint64_t ubs = b0 > o_pos ? b0 : o_pos;
+    const uint64_t ube = b0 + PIECE < o_pos + o_len ? b0 + PIECE : o_pos + o_len;
+    const uint64_t s0 = o_src + (ubs - o_pos);
     PieceDesc pd;
-    pd.info = ((o_src + j0) & PD_SRC_MASK) | ((uint64_t)(o_end - ps < PIECE ? o_end - ps : PIECE) << PD_NB_SHIFT) |
-              (single ? 0ull : PD_MULTI);
-    pd.mask = 0;
-    pd.frame = o_k;
-    a.pieces[pc] = pd;
+    pd.info = (ubs & PD_SRC_MASK) | ((ube > ubs ? ube - ubs : 0ull) << PD_NB_SHIFT);
+    pd.mask = (uint32_t)s0;
+    pd.frame = (uint32_t)(s0 >> 32);
+    a.pieces[u] = pd;
   }
 }
 
@@ -315,174 +300,77 @@ __device__ __forceinline__ uint32_t ag_dpp_from_next(uint32_t v, uint32_t old) {
   return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x130, 0xf, 0xf, false);
 }
 
-__device__ __forceinline__ void ag_store16(const AggArgs& a, uint64_t o, uint64_t lim, const uint32_t w[4]) {
-  if (o + 16 <= lim) {
-    __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (u32x4*)(a.agg_out + o));
-  } else {  // agg_out is not padded
-#pragma unroll
-    for (uint32_t i = 0; i < 16u; ++i)
-      if (o + i < lim) a.agg_out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
-  }
+// bytes [lo, hi) of the 16-B block at agg_out + o (a unit's partial first or last
+// block: the rest of the block belongs to the neighbouring member)
+__device__ __forceinline__ void ag_store_part(const AggArgs& a, uint64_t o, uint32_t lo, uint32_t hi, uint64_t lim,
+                                              const uint32_t w[4]) {
+  if (o + hi > lim) hi = o < lim ? (uint32_t)(lim - o) : 0u;
+  for (uint32_t i = lo; i < hi; ++i) a.agg_out[o + i] = (uint8_t)(w[i >> 2] >> (8 * (i & 3)));
 }
 
-// 16 payload bytes at an arbitrary offset, from 4-B aligned loads (the payload
-// buffer is the decoder's, padded to 16-B slots: reading 4 bytes past a slot's
-// end stays inside the buffer except at its very end, where byte loads take over)
-__device__ __forceinline__ void ag_load16(const AggArgs& a, uint64_t s, uint64_t src_lim, uint32_t w[4]) {
-  const uint64_t a4 = s & ~3ull;
-  const uint32_t sh = (uint32_t)(s & 3u);
-  uint32_t dd[5];
-  if (a4 + 20u <= src_lim) {
-    const uint32_t* q = (const uint32_t*)(a.payload + a4);
-    dd[0] = q[0]; dd[1] = q[1]; dd[2] = q[2]; dd[3] = q[3]; dd[4] = q[4];
-  } else {
-#pragma unroll
-    for (int i = 0; i < 5; ++i) dd[i] = 0u;
-#pragma unroll
-    for (uint32_t i = 0; i < 20u; ++i)
-      if (a4 + i < src_lim) dd[i >> 2] |= (uint32_t)a.payload[a4 + i] << (8 * (i & 3));
-  }
-#pragma unroll
-  for (int i = 0; i < 4; ++i) w[i] = alignbyte(dd[i + 1], dd[i], sh);
-}
-
-// A piece spanning several members: lane l takes member record d.frame + l (records
-// are the non-empty members, dense and in order), and the owner of byte o is the
-// last record starting at or before o, found by a shuffle search.
-// (the record load is issued with the other pieces' loads: ag_multi_rec)
-__device__ __forceinline__ AggRec ag_multi_rec(const AggArgs& a, const PieceDesc d, uint64_t n_mem, int lane) {
-  const uint64_t fl = (uint64_t)d.frame + (uint64_t)lane;
-  AggRec rl;
-  if (fl < n_mem) rl = a.rec[fl];
-  else { rl.pos = ~0ull; rl.mlen = 0; rl.src = 0; }
-  return rl;
-}
-__device__ void ag_piece_multi(const AggArgs& a, const PieceDesc d, const AggRec rl, uint64_t ps, uint64_t lim,
-                               uint64_t n_mem, uint64_t src_lim, int lane) {
-  const uint64_t o = ps + (uint64_t)lane * 16u;
-  uint32_t w[4] = {0u, 0u, 0u, 0u};
-  const uint64_t pend = ps + PIECE < lim ? ps + PIECE : lim;
-  const bool live = o < pend;
-  const bool have = (uint64_t)d.frame + (uint64_t)lane < n_mem;
-  uint32_t lk = d.frame;
-  AggRec lr;
-  if (__any(have && rl.mlen && rl.pos + rl.mlen >= pend)) {
-    const int key = rl.pos >= pend ? 4096 : (rl.pos <= ps ? 0 : (int)(rl.pos - ps));
-    int posn = 0;
-#pragma unroll
-    for (int step = 32; step >= 1; step >>= 1)
-      if (__shfl(key, posn + step, 64) <= lane * 16) posn += step;
-    lk = d.frame + (uint32_t)posn;
-    // the owner's record: lane posn holds it
-    lr.pos = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rl.pos >> 32), posn, 64) << 32) |
-             (uint32_t)__shfl((int)(uint32_t)rl.pos, posn, 64);
-    lr.src = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(rl.src >> 32), posn, 64) << 32) |
-             (uint32_t)__shfl((int)(uint32_t)rl.src, posn, 64);
-    lr.mlen = (uint32_t)__shfl((int)rl.mlen, posn, 64);
-  } else {  // more than 64 records (empty ones) reach into the piece: walk them
-    uint32_t kk = d.frame;
-    AggRec rr = a.rec[kk];
-    lr = rr;
-    for (;;) {
-      const bool beyond = live && o >= rr.pos + rr.mlen;
-      if (!__any(beyond) || kk + 1 >= n_mem) break;
-      ++kk;
-      rr = a.rec[kk];
-      if (beyond && rr.mlen) { lk = kk; lr = rr; }
-    }
-  }
-  if (!live) return;
-  // the lane's 16 bytes may span members: byte-wise over consecutive records
-  if (o >= lr.pos && o + 16 <= lr.pos + lr.mlen) {
-    // two aligned 16-B blocks and a per-lane funnel (the shift differs per member)
-    const uint64_t sa = lr.src + (o - lr.pos);
-    const uint64_t a16 = sa & ~15ull;
-    if (a16 + 32u <= src_lim) {
-      const u32x4 A = *(const u32x4*)(a.payload + a16), B = *(const u32x4*)(a.payload + a16 + 16u);
-      const uint32_t q = (uint32_t)(sa >> 2) & 3u, b = (uint32_t)sa & 3u;
-      const uint32_t W[8] = {A.x, A.y, A.z, A.w, B.x, B.y, B.z, B.w};
-      uint32_t x[5];
-#pragma unroll
-      for (int i = 0; i < 5; ++i) x[i] = q == 0 ? W[i] : (q == 1 ? W[i + 1] : (q == 2 ? W[i + 2] : W[i + 3]));
-#pragma unroll
-      for (int i = 0; i < 4; ++i) w[i] = alignbyte(x[i + 1], x[i], b);
-    } else {
-      ag_load16(a, sa, src_lim, w);
-    }
-  } else {
-    uint64_t blo = 0, bhi = 0;
-    uint32_t kk = lk;
-    AggRec rr = lr;
-    for (uint32_t i = 0; i < 16u; ++i) {
-      const uint64_t x = o + i;
-      if (x >= pend) break;
-      while (x >= rr.pos + rr.mlen && kk + 1 < n_mem) rr = a.rec[++kk];
-      const uint64_t byte = a.payload[rr.src + (x - rr.pos)];
-      if (i < 8) blo |= byte << (8 * i);
-      else bhi |= byte << (8 * (i - 8));
-    }
-    w[0] = (uint32_t)blo; w[1] = (uint32_t)(blo >> 32); w[2] = (uint32_t)bhi; w[3] = (uint32_t)(bhi >> 32);
-  }
-  ag_store16(a, o, pend, w);
-}
-
-// One wave per N consecutive 1 KiB pieces of agg_out, grid-stride over the piece
-// groups: the next group's descriptors are loaded a group ahead, and every piece's
-// first loads (its source blocks, or a multi-member piece's records) are issued
-// before any piece is finished — the kernel is latency-bound.
+// One wave per N gather units, grid-stride over the unit groups: the next group's
+// descriptors are loaded a group ahead, every unit's source blocks are loaded before
+// any unit is stored (the kernel is latency-bound).  Lane l of a unit
+// stores agg_out block ubs/16 + l: 16 bytes funnelled by the unit's (wave-uniform)
+// source shift from its own aligned source block and its right neighbour's (DPP).
 template <int N>
 __global__ __launch_bounds__(64) void k_agg_gather(AggArgs a, uint64_t src_lim) {
   const int lane = threadIdx.x;
   const uint64_t total = *a.agg_total;
   const uint64_t lim = total < a.agg_cap ? total : a.agg_cap;
-  const uint64_t np = (lim + PIECE - 1) / PIECE;
-  const uint64_t nq = (np + N - 1) / N;
-  const uint64_t n_mem = *a.n_mem;
+  const uint64_t nu0 = *a.n_units;
+  const uint64_t nu = nu0 < a.n_pieces ? nu0 : a.n_pieces;
+  const uint64_t nq = (nu + N - 1) / N;
   uint64_t q = blockIdx.x;
   PieceDesc dn[N];  // the next group's descriptors, loaded a group ahead
 #pragma unroll
-  for (int i = 0; i < N; ++i) dn[i] = q * N + i < np ? a.pieces[q * N + i] : PieceDesc{PD_MULTI, 0u, 0u};
+  for (int i = 0; i < N; ++i) dn[i] = q * N + i < nu ? a.pieces[q * N + i] : PieceDesc{0ull, 0u, 0u};
   for (; q < nq; q += gridDim.x) {
     PieceDesc d[N];
     u32x4 A[N], nx[N];
-    AggRec rl[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) d[i] = dn[i];
     const uint64_t qn = q + gridDim.x;
 #pragma unroll
-    for (int i = 0; i < N; ++i) dn[i] = qn * N + i < np ? a.pieces[qn * N + i] : PieceDesc{PD_MULTI, 0u, 0u};
+    for (int i = 0; i < N; ++i) dn[i] = qn * N + i < nu ? a.pieces[qn * N + i] : PieceDesc{0ull, 0u, 0u};
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const uint64_t p = q * N + i;
-      if (p < np && (d[i].info & PD_MULTI)) rl[i] = ag_multi_rec(a, d[i], n_mem, lane);
-      if (p < np && !(d[i].info & PD_MULTI)) {  // the piece lies in one member's bytes
-        const uint64_t a16 = (d[i].info & PD_SRC_MASK) & ~15ull;
-        if (a16 + PIECE + 16u <= src_lim) {
-          A[i] = *(const u32x4*)(a.payload + a16 + (uint64_t)lane * 16u);
-          nx[i] = *(const u32x4*)(a.payload + a16 + PIECE);
-        } else {
-          uint32_t dd[4] = {0u, 0u, 0u, 0u}, ee[4] = {0u, 0u, 0u, 0u};
-          for (uint32_t b = 0; b < 16u; ++b) {
-            if (a16 + lane * 16u + b < src_lim) dd[b >> 2] |= (uint32_t)a.payload[a16 + lane * 16u + b] << (8 * (b & 3));
-            if (a16 + PIECE + b < src_lim) ee[b >> 2] |= (uint32_t)a.payload[a16 + PIECE + b] << (8 * (b & 3));
-          }
-          A[i] = (u32x4){dd[0], dd[1], dd[2], dd[3]};
-          nx[i] = (u32x4){ee[0], ee[1], ee[2], ee[3]};
+      const uint64_t ubs = d[i].info & PD_SRC_MASK;
+      const uint32_t nb = (uint32_t)(d[i].info >> PD_NB_SHIFT) & 2047u;
+      const uint32_t head = (uint32_t)ubs & 15u;
+      const uint64_t s0 = ((uint64_t)d[i].frame << 32) | d[i].mask;
+      const uint32_t span = head + nb;  // bytes of the unit's blocks from the first block's start
+      A[i] = (u32x4){0u, 0u, 0u, 0u};
+      nx[i] = A[i];
+      if (!nb) continue;
+      const uint64_t sb = s0 - head;  // source of the first block's byte 0 (wraps below 0: slow path)
+      const uint64_t a16 = sb & ~15ull;
+      if (s0 >= head && a16 + PIECE + 16u <= src_lim) {
+        // source blocks [a16, a16 + sh + span): lane l's, and the one after the wave's
+        const uint32_t need = ((uint32_t)sb & 15u) + span;
+        if ((uint32_t)lane * 16u < need) A[i] = *(const u32x4*)(a.payload + a16 + (uint64_t)lane * 16u);
+        if (need > PIECE) nx[i] = *(const u32x4*)(a.payload + a16 + PIECE);
+      } else {  // near either end of the payload buffer: byte loads
+        uint32_t dd[4] = {0u, 0u, 0u, 0u}, ee[4] = {0u, 0u, 0u, 0u};
+        for (uint32_t b = 0; b < 16u; ++b) {
+          const uint64_t x = sb + lane * 16u + b, y = sb + PIECE + b;  // (sb + .. wraps back above 0)
+          if (x < src_lim) dd[b >> 2] |= (uint32_t)a.payload[x] << (8 * (b & 3));
+          if (y < src_lim) ee[b >> 2] |= (uint32_t)a.payload[y] << (8 * (b & 3));
         }
+        // bytes already funnelled: shift 0 below
+        A[i] = (u32x4){dd[0], dd[1], dd[2], dd[3]};
+        nx[i] = (u32x4){ee[0], ee[1], ee[2], ee[3]};
+        d[i].info |= 1ull << 63;  // marks the unaligned-load path
       }
     }
 #pragma unroll
     for (int i = 0; i < N; ++i) {
-      const uint64_t p = q * N + i;
-      if (p >= np) break;
-      const uint64_t ps = p * PIECE;
-      if (d[i].info & PD_MULTI) {
-        ag_piece_multi(a, d[i], rl[i], ps, lim, n_mem, src_lim, lane);
-        continue;
-      }
-      const uint64_t s = d[i].info & PD_SRC_MASK;
+      const uint64_t ubs = d[i].info & PD_SRC_MASK;
       const uint32_t nb = (uint32_t)(d[i].info >> PD_NB_SHIFT) & 2047u;
-      const uint32_t sh = (uint32_t)(s & 15u), b = sh & 3u;
+      if (!nb) continue;
+      const uint32_t head = (uint32_t)ubs & 15u;
+      const uint64_t s0 = ((uint64_t)d[i].frame << 32) | d[i].mask;
+      const uint32_t sh = (d[i].info >> 63) ? 0u : (uint32_t)(s0 - head) & 15u, b = sh & 3u;
       const uint32_t W0 = A[i].x, W1 = A[i].y, W2 = A[i].z, W3 = A[i].w;
       const uint32_t W4 = ag_dpp_from_next(A[i].x, nx[i].x), W5 = ag_dpp_from_next(A[i].y, nx[i].y);
       const uint32_t W6 = ag_dpp_from_next(A[i].z, nx[i].z), W7 = ag_dpp_from_next(A[i].w, nx[i].w);
@@ -493,7 +381,14 @@ __global__ __launch_bounds__(64) void k_agg_gather(AggArgs a, uint64_t src_lim) 
         case 2: w[0] = alignbyte(W3, W2, b); w[1] = alignbyte(W4, W3, b); w[2] = alignbyte(W5, W4, b); w[3] = alignbyte(W6, W5, b); break;
         default: w[0] = alignbyte(W4, W3, b); w[1] = alignbyte(W5, W4, b); w[2] = alignbyte(W6, W5, b); w[3] = alignbyte(W7, W6, b); break;
       }
-      if ((uint32_t)lane * 16u < nb) ag_store16(a, ps + (uint64_t)lane * 16u, lim, w);
+      const uint32_t span = head + nb, l16 = (uint32_t)lane * 16u;
+      if (l16 >= span) continue;
+      const uint64_t o = (ubs & ~15ull) + l16;
+      const uint32_t lo = lane ? 0u : head, hi = span - l16 < 16u ? span - l16 : 16u;
+      if (lo == 0 && hi == 16u && o + 16u <= lim)
+        __builtin_nontemporal_store((u32x4){w[0], w[1], w[2], w[3]}, (u32x4*)(a.agg_out + o));
+      else
+        ag_store_part(a, o, lo, hi, lim, w);
     }
   }
 }
@@ -592,18 +487,14 @@ void launch_agg_plan(const AggArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 1);
   hipLaunchKernelGGL(k_agg_c, dim3(a.nblk), dim3(BLOCK), 0, s, a);
 }
-#ifndef WSG_AGG_GRID_CAP
-#define WSG_AGG_GRID_CAP 65536
-#endif
-constexpr uint64_t AGG_GRID_CAP = WSG_AGG_GRID_CAP;  // waves of the grid-stride gather (build override for A/B)
-void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim) {
-  // grid-stride over the pieces (their number is known only on the device)
-  // (2 pieces per wave beat 1 and 4, and the XCD-aware order lost 12-40 % here:
-  // same-box A/B on the configs[2] batch)
-  const uint64_t nq = (a.n_pieces + AGG_PIECES_PER_WAVE - 1) / AGG_PIECES_PER_WAVE;
-  const uint64_t g = nq < AGG_GRID_CAP ? nq : AGG_GRID_CAP;
-  if (a.n_frames && g)
-    hipLaunchKernelGGL((k_agg_gather<AGG_PIECES_PER_WAVE>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
+void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim, int per_wave, uint32_t grid_cap) {
+  // grid-stride over the units (their number is known only on the device; n_pieces bounds it)
+  const uint64_t nq = (a.n_pieces + per_wave - 1) / per_wave;
+  const uint64_t g = nq < grid_cap ? nq : grid_cap;
+  if (!a.n_frames || !g) return;
+  if (per_wave == 1) hipLaunchKernelGGL((k_agg_gather<1>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
+  else if (per_wave == 4) hipLaunchKernelGGL((k_agg_gather<4>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
+  else hipLaunchKernelGGL((k_agg_gather<2>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
 }
 void launch_agg_final(const AggArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_agg_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);

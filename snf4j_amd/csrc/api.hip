@@ -64,7 +64,7 @@ struct wsg_ctx {
   // encode workspace
   DevBuf esess, elast_close, epieces, epidx;
   // aggregate workspace
-  DevBuf a_code, a_last, a_pl, a_cl, a_rec, a_blk, a_sess_err, a_pieces;
+  DevBuf a_code, a_last, a_pl, a_cl, a_blk, a_sess_err, a_pieces;
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
   DevBuf i_tok, i_lit, i_stat, i_tab, i_fast, i_ord;  // inflate pre-decode workspace
   // measurement / test switches (wsg_set_tuning; the defaults are the product)
@@ -74,6 +74,8 @@ struct wsg_ctx {
   int infl_lds = 1;                  // WSG_TUNE_INFLATE_LDS 0: the pre-decode keeps its tables in HBM
   int infl_order = 1;                // WSG_TUNE_INFLATE_ORDER 0: lanes take frames in batch order
   int fused_scan = 1;                // WSG_TUNE_FUSED_SCAN 0: always launch k_scan
+  int agg_units = 2;                 // WSG_TUNE_AGG_UNITS: k_agg_gather units per wave (1, 2 or 4)
+  uint32_t agg_grid = 65536;         // WSG_TUNE_AGG_GRID: k_agg_gather waves at most
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -202,7 +204,7 @@ int wsg_close(wsg_ctx* c) {
                     &c->h_state, &c->h_payload, &c->h_desc, &c->h_result, &c->h_frames, &c->h_closed,
                     &c->h_wire_off};
   for (DevBuf* b : bufs) b->release();
-  DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,     &c->a_rec,
+  DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,
                      &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc, &c->i_tok, &c->i_lit,
                      &c->i_stat, &c->i_tab, &c->i_fast, &c->i_ord};
   for (DevBuf* b : abufs) b->release();
@@ -229,6 +231,11 @@ int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
     case WSG_TUNE_INFLATE_ORDER: c->infl_order = value != 0; break;
     case WSG_TUNE_INFLATE_LANES: c->infl_lanes = value < 64 ? 64u : (uint32_t)value & ~63u; break;
     case WSG_TUNE_FUSED_SCAN: c->fused_scan = value != 0; break;
+    case WSG_TUNE_AGG_UNITS:
+      if (value != 1 && value != 2 && value != 4) return set_err(c, WSG_API_EINVAL, "AGG_UNITS is 1, 2 or 4");
+      c->agg_units = (int)value;
+      break;
+    case WSG_TUNE_AGG_GRID: c->agg_grid = value < 1 ? 1u : (value > (1 << 24) ? (1u << 24) : (uint32_t)value); break;
     default: return set_err(c, WSG_API_EINVAL, "unknown tuning key");
   }
   return WSG_API_OK;
@@ -782,12 +789,13 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   a.out_result = out_result;
   a.agg_total = agg_total;
   a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
-  a.n_pieces = agg_cap / PIECE + 1;
+  // gather units: a member of m bytes has ceil((m + 15) / 1 KiB); those holding bytes below
+  // agg_cap number at most agg_cap / 1 KiB + 2 per member before them
+  a.n_pieces = agg_cap / PIECE + 2 * F + 2;
   HIP_TRY(c, c->a_code.ensure(F * 2 * sizeof(uint32_t)));
   HIP_TRY(c, c->a_last.ensure(F * 2 * sizeof(int32_t)));
   HIP_TRY(c, c->a_pl.ensure(F * sizeof(uint64_t)));
   HIP_TRY(c, c->a_cl.ensure(F * sizeof(uint64_t) + sizeof(uint64_t)));
-  HIP_TRY(c, c->a_rec.ensure(F * sizeof(AggRec)));
   HIP_TRY(c, c->a_blk.ensure(nblk * (2 * sizeof(uint64_t) + 2 * sizeof(int32_t))));
   HIP_TRY(c, c->a_sess_err.ensure((uint64_t)n_sessions * sizeof(uint64_t), 0xff, c->stream));
   HIP_TRY(c, c->a_pieces.ensure((a.n_pieces + 1) * sizeof(PieceDesc)));
@@ -796,8 +804,7 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   a.last = (int32_t*)c->a_last.p;
   a.pl = (uint64_t*)c->a_pl.p;
   a.cl = (uint64_t*)c->a_cl.p;
-  a.n_mem = a.cl + F;
-  a.rec = (AggRec*)c->a_rec.p;
+  a.n_units = a.cl + F;
   a.blk_sum = (uint64_t*)c->a_blk.p;
   a.blk_cnt = a.blk_sum + nblk;
   a.blk_max = (int32_t*)(a.blk_cnt + nblk);
@@ -805,7 +812,7 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   a.pieces = (PieceDesc*)c->a_pieces.p;
   if (!n_frames) HIP_TRY(c, hipMemsetAsync(agg_total, 0, sizeof(uint64_t), c->stream));
   timed(c, K_AGG, [&] { launch_agg_plan(a, c->stream); });
-  timed(c, K_AGG_GATHER, [&] { launch_agg_gather(a, c->stream, payload_len); });
+  timed(c, K_AGG_GATHER, [&] { launch_agg_gather(a, c->stream, payload_len, c->agg_units, c->agg_grid); });
   timed(c, K_AGG_FINAL, [&] { launch_agg_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());
   return WSG_API_OK;

@@ -2155,7 +2155,11 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       //    reads a literal run's bytes one by one)
       const uint64_t lg = (uint64_t)(lit - a.lit) + l_first;  // the chunk's first literal, in a.lit
       const uint64_t lw0 = lg >> 2;
-      for (uint32_t w = (uint32_t)lane; w < FC / 4 + 2; w += FNT)
+      // only the message's literals from l_first on (at most a chunk's worth): text is mostly
+      // matches, so this is a fraction of the FC bytes the buffer holds
+      const uint32_t lrem = ts.n_lit > l_first ? ts.n_lit - l_first : 0u;
+      const uint32_t lw_n = (lrem < FC ? lrem : FC) / 4u + 2u;
+      for (uint32_t w = (uint32_t)lane; w < lw_n; w += FNT)
         lbuf[w] = (lw0 + w) * 4 + 4 <= a.lit_len ? reinterpret_cast<const uint32_t*>(a.lit)[lw0 + w] : 0u;
       const uint32_t lsh = (uint32_t)(lg & 3u) - l_first;  // literal index i is byte i + lsh of lbuf
       __syncthreads();

@@ -142,13 +142,6 @@ struct EncodeArgs {
   uint32_t nblk;
 };
 
-struct AggRec {     // gather record of a non-empty member (aggregate.hip k_agg_c -> k_agg_gather)
-  uint64_t pos;     // agg_out offset of its member bytes
-  uint64_t src;     // payload offset of its bytes
-  uint32_t mlen;    // member bytes (0 for non-members)
-  uint32_t pad;
-};
-
 struct AggArgs {
   int64_t max_len;
   const wsg_frame_desc* desc;
@@ -168,15 +161,14 @@ struct AggArgs {
   uint32_t* sess;      // [n]
   int32_t* last;       // [2][n] last start / last end before k (batch index, -1 = none)
   uint64_t* pl;        // [n] block-local exclusive member bytes
-  uint64_t* cl;        // [n] block-local exclusive (emitted frames | non-empty members << 32)
+  uint64_t* cl;        // [n] block-local exclusive (emitted frames | gather units << 32)
   uint64_t* blk_sum;   // [nblk] member bytes -> exclusive prefix
-  uint64_t* blk_cnt;   // [nblk] (emitted frames | non-empty members << 32) -> exclusive prefix
+  uint64_t* blk_cnt;   // [nblk] (emitted frames | gather units << 32) -> exclusive prefix
   int32_t* blk_max;    // [2][nblk] block maxima of start / end -> exclusive prefix
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none), idle between batches
-  AggRec* rec;         // [n] gather records of the non-empty members, in order
-  uint64_t* n_mem;     // [1] number of non-empty members
-  struct PieceDesc* pieces;  // [n_pieces]: agg_out pieces (frame holding the first byte)
-  uint64_t n_pieces;
+  uint64_t* n_units;   // [1] gather units of the batch (k_agg_scan)
+  struct PieceDesc* pieces;  // [n_pieces]: gather units (k_agg_c -> k_agg_gather)
+  uint64_t n_pieces;         // bound on the units (agg_units_bound)
   uint32_t nblk;
 };
 
@@ -240,7 +232,7 @@ void launch_enc_pieces(const EncodeArgs& a, hipStream_t s);
 void launch_enc_final(const EncodeArgs& a, hipStream_t s);
 
 void launch_agg_plan(const AggArgs& a, hipStream_t s);
-void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim);
+void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim, int per_wave, uint32_t grid_cap);
 void launch_agg_final(const AggArgs& a, hipStream_t s);
 
 void launch_inflate(const InflArgs& a, hipStream_t s);
