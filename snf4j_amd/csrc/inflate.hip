@@ -2033,7 +2033,16 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
 // ---------------------------------------------------------------------------------
 namespace {
 
-constexpr uint32_t FC = 4096;             // output bytes resolved per chunk
+#ifndef WSG_FAST_GU
+#define WSG_FAST_GU 16  // gather loads in flight a thread (of the FC / FNT bytes it resolves)
+#endif
+#ifndef WSG_FAST_CU
+#define WSG_FAST_CU 8  // window-commit dwords in flight a thread
+#endif
+#ifndef WSG_FAST_CHUNK
+#define WSG_FAST_CHUNK 4096
+#endif
+constexpr uint32_t FC = WSG_FAST_CHUNK;   // output bytes resolved per chunk (a multiple of FNT)
 constexpr uint32_t FD_LIT = 0x80000000u;  // descriptor: a resolved byte (bits 0-7)
 constexpr int32_t FD_BIAS = 32768;        // descriptor: position + FD_BIAS (history positions are >= -32768)
 
@@ -2242,13 +2251,15 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       FPROF_T(f_ga);
       // 3. gather the bytes that come from before the chunk: this batch's output (HBM),
       //    or the window carried in
-      {  // a thread's FC / FNT bytes: every load in flight at once
-        constexpr int GU = FC / FNT;
+      // a thread's FC / FNT bytes, WSG_FAST_GU loads in flight at once
+#pragma unroll
+      for (int u0 = 0; u0 < (int)(FC / FNT); u0 += WSG_FAST_GU) {
+        constexpr int GU = WSG_FAST_GU;
         uint32_t v[GU];
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
-          const uint32_t j = (uint32_t)FNT * u + (uint32_t)lane;
-          v[u] = j < n ? fd[j] : FD_LIT;
+          const uint32_t j = (uint32_t)FNT * (u0 + u) + (uint32_t)lane;
+          v[u] = j < n && u0 + u < (int)(FC / FNT) ? fd[j] : FD_LIT;
           if (!(v[u] & FD_LIT)) {
             const int32_t q = (int32_t)v[u] - FD_BIAS;
 #if WSG_FAST_RING
@@ -2261,8 +2272,8 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         }
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
-          const uint32_t j = (uint32_t)FNT * u + (uint32_t)lane;
-          if (j < n) fd[j] = v[u];
+          const uint32_t j = (uint32_t)FNT * (u0 + u) + (uint32_t)lane;
+          if (j < n && u0 + u < (int)(FC / FNT)) fd[j] = v[u];
         }
       }
       __syncthreads();
@@ -2338,10 +2349,10 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
     // is before lo keep the old image's byte
     uint32_t* const wout32 = reinterpret_cast<uint32_t*>(wout);
     const uint32_t mis = (uint32_t)((uintptr_t)out & 3u);  // the output's offset from a dword boundary
-    for (uint32_t w0 = 0; w0 < WSG_INFLATE_WINDOW / 4; w0 += 8 * FNT) {
-      uint32_t v[8];
+    for (uint32_t w0 = 0; w0 < WSG_INFLATE_WINDOW / 4; w0 += WSG_FAST_CU * FNT) {
+      uint32_t v[WSG_FAST_CU];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < WSG_FAST_CU; ++u) {
         const uint32_t w = w0 + (uint32_t)FNT * u + (uint32_t)lane;
         // a slot dword whose 4 positions are consecutive output bytes (not across the
         // ring's end, none before lo): two aligned dword loads and a funnel, not 4 byte loads
@@ -2374,7 +2385,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         v[u] = x;
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) wout32[w0 + (uint32_t)FNT * u + (uint32_t)lane] = v[u];
+      for (int u = 0; u < WSG_FAST_CU; ++u) wout32[w0 + (uint32_t)FNT * u + (uint32_t)lane] = v[u];
     }
     st.window_len = (uint16_t)nh;
     st.window_phase = (uint16_t)nph;
