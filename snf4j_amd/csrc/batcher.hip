@@ -33,6 +33,10 @@
 
 #include "wsgpu_internal.h"
 
+#if !defined(__HIP_DEVICE_COMPILE__)
+#include <immintrin.h>
+#endif
+
 namespace {
 
 struct PinnedBuf {
@@ -589,6 +593,39 @@ static hipError_t arena_grow(FlushSlot& f, uint64_t need) {
   return hipSuccess;
 }
 
+// Socket bytes into the pinned arena.  The arena is written once and then only read
+// by the DMA engine, so the bulk goes out with streaming stores (no read-for-ownership
+// of the destination lines, nothing of it left in the cache); the caller's
+// synchronisation after the pool's run orders them (sfence here).
+#if !defined(__HIP_DEVICE_COMPILE__)
+__attribute__((target("avx2"))) static void copy_stream_avx2(uint8_t* d, const uint8_t* s, uint64_t n) {
+  uint64_t h = (32u - ((uintptr_t)d & 31u)) & 31u;
+  if (h > n) h = n;
+  memcpy(d, s, h);
+  d += h;
+  s += h;
+  n -= h;
+  uint64_t i = 0;
+  for (; i + 128 <= n; i += 128) {
+    const __m256i x0 = _mm256_loadu_si256((const __m256i*)(s + i)), x1 = _mm256_loadu_si256((const __m256i*)(s + i + 32));
+    const __m256i x2 = _mm256_loadu_si256((const __m256i*)(s + i + 64)), x3 = _mm256_loadu_si256((const __m256i*)(s + i + 96));
+    _mm256_stream_si256((__m256i*)(d + i), x0);
+    _mm256_stream_si256((__m256i*)(d + i + 32), x1);
+    _mm256_stream_si256((__m256i*)(d + i + 64), x2);
+    _mm256_stream_si256((__m256i*)(d + i + 96), x3);
+  }
+  memcpy(d + i, s + i, n - i);
+  _mm_sfence();
+}
+static const bool g_avx2 = __builtin_cpu_supports("avx2");
+static void copy_to_arena(uint8_t* d, const uint8_t* s, uint64_t n) {
+  if (n >= 4096 && g_avx2) copy_stream_avx2(d, s, n);
+  else memcpy(d, s, n);
+}
+#else  // (the device pass parses host code too)
+static void copy_to_arena(uint8_t* d, const uint8_t* s, uint64_t n) { memcpy(d, s, n); }
+#endif
+
 // Many socket reads at once (a selector loop's reads of one iteration, in order):
 // each session with reads gets one region of the open batch's pinned arena, its
 // carried partial frame then its reads, copied there and framed in place by up to
@@ -645,11 +682,11 @@ int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, cons
     const uint32_t s = ts[i];
     SessIn& x = b->s[s];
     uint8_t* d = f.arena.p + rs[i];
-    if (!x.buf.empty()) memcpy(d, x.buf.data(), x.buf.size());
+    if (!x.buf.empty()) copy_to_arena(d, x.buf.data(), x.buf.size());
     d += x.buf.size();
     for (uint32_t j = first[s]; j < first[s + 1]; ++j) {
       const uint32_t r = order[j];
-      if (lens[r]) memcpy(d, data[r], lens[r]);
+      if (lens[r]) copy_to_arena(d, data[r], lens[r]);
       d += lens[r];
     }
     frame_region(b, f, s, rs[i], rs[i + 1]);
