@@ -86,6 +86,17 @@ __device__ __forceinline__ uint32_t sym_entry(int kind, uint32_t s, uint32_t len
   return ent(len, 0, OP_BAD, 0);
 }
 
+// The lane decoders' entry tables hold the length and distance symbols only (a literal's
+// entry is its byte): ents[0, 32) length symbols 256..287, ents[32, 64) distance 0..31.
+constexpr int N_ENTS = 64;
+__device__ __forceinline__ uint32_t ents_init(uint32_t i) {
+  return i < 32u ? sym_entry(T_LIT, 256u + i, 0) : sym_entry(T_DIST, i - 32u, 0);
+}
+__device__ __forceinline__ uint32_t tok_ent(const uint32_t* ents, uint32_t sym, bool dist) {
+  const uint32_t e = ents[(sym + (dist ? 32u : 0u - 256u)) & 63u];
+  return (!dist && sym < 256u) ? ent(0, 0, OP_LIT, sym) : e;
+}
+
 __device__ __forceinline__ uint32_t uni(uint32_t x) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)x); }
 __device__ __forceinline__ uint64_t uni64(uint64_t x) { return ((uint64_t)uni((uint32_t)(x >> 32)) << 32) | uni((uint32_t)x); }
 
@@ -672,7 +683,7 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
       if ((r & 15u) == 0)
         r = root[(1u << rb) + (r >> 7) + ((uint32_t)(hold >> rb) & ((1u << ((r >> 4) & 7u)) - 1u))];
       const uint32_t len = r & 15u;
-      const uint32_t e = lit_ent[(r >> 4) + (dist ? 288u : 0u)];  // dist_ent follows lit_ent
+      const uint32_t e = tok_ent(lit_ent, r >> 4, dist);
       const uint32_t x = e_extra(e), eo = e_op(e);
       if ((int)(len + x) > bits || eo == OP_BAD) { ok = false; break; }
       const uint32_t v = e_val(e) + ((uint32_t)(hold >> len) & ((1u << x) - 1u));
@@ -728,7 +739,10 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
 #define WSG_QL_ROOT 7
 #endif
 #ifndef WSG_QL_SUB
-#define WSG_QL_SUB 72
+#define WSG_QL_SUB 44
+#endif
+#ifndef WSG_TOK_WG_PER_CU
+#define WSG_TOK_WG_PER_CU 4
 #endif
 #ifndef WSG_QD_ROOT
 #define WSG_QD_ROOT 6
@@ -745,7 +759,10 @@ constexpr uint32_t QF_L = 0, QF_D = 1u << QF_LROOT;  // their u16 offsets
 constexpr uint32_t Q_LT = QF_D + (1u << QF_DROOT);   // lane tables: entry j of lane i at Q_LT + j * 64 + i
 constexpr uint32_t Q_DT = Q_LT + QL_N * 64;
 constexpr uint32_t Q_TAB = Q_DT + QD_N * 64;
-constexpr int Q_RING = 17;                           // ring dwords per lane: 16 + slot 0 mirrored
+#ifndef WSG_TOK_MIRROR
+#define WSG_TOK_MIRROR 1
+#endif
+constexpr int Q_RING = 16 + WSG_TOK_MIRROR;          // ring dwords per lane (+ slot 0 mirrored: no wrap test)
 constexpr int Q_LENW = 40;                           // code-length dwords per lane (320 nibbles)
 static_assert(QD_N * 2 >= Q_LENW * 4, "the code lengths of a header fit a lane's distance table");
 static_assert(QL_N >= (1 << QC_ROOT), "the code-length code table fits a lane's literal table");
@@ -753,13 +770,14 @@ static_assert(QL_SUB < 256 && QD_SUB < 256, "sub-table offsets fit a root entry'
 static_assert((Q_DT * 2) % 4 == 0, "code-length dwords are aligned");
 
 struct TokLds {
-  uint32_t ents[320];        // symbol -> entry: literal/length, then distance
-  uint16_t tab[Q_TAB];       // fixed tables, then the lanes' tables
+  uint32_t ents[N_ENTS];       // length / distance symbol -> entry (tok_ent)
+  uint16_t tab[Q_TAB];         // fixed tables, then the lanes' tables
   uint32_t ring[Q_RING * 64];  // input ring: dword slot s of lane i at s * 64 + i
-  uint32_t cnt[16 * 64];       // literal/length table build: count, then next code, of length L at L * 64 + i
+  uint32_t cnt[8 * 64];        // literal/length table build: count, then next code, of length L in
+                               // half L & 1 of dword (L >> 1) * 64 + i (both < 2^16)
 };
-static_assert(sizeof(TokLds) <= 160 * 1024 / 3 || WSG_QL_ROOT != 7 || WSG_QD_ROOT != 6,
-              "the default tables fit 3 workgroups per CU (160 KiB of LDS)");
+static_assert(sizeof(TokLds) <= 160 * 1024 / WSG_TOK_WG_PER_CU || WSG_QL_ROOT != 7 || WSG_QD_ROOT != 6,
+              "the default tables fit WSG_TOK_WG_PER_CU workgroups per CU (160 KiB of LDS)");
 
 enum : int { Q_OK = 0, Q_BAD = 1, Q_BAIL = 2 };
 
@@ -851,22 +869,22 @@ __device__ int q_build_lit(TokLds& Q, uint32_t lane, const uint32_t* lw, int n) 
   uint16_t* const tab = Q.tab;
   const uint32_t base = Q_LT + lane;
   constexpr int rb = QL_ROOT;
-  uint32_t* const cnt = Q.cnt;
+  uint32_t* const cnt = Q.cnt;  // length L: half L & 1 of dword (L >> 1) * 64 + lane
 #pragma unroll
-  for (int L = 0; L < 16; ++L) cnt[L * 64 + lane] = 0;
+  for (int L = 0; L < 8; ++L) cnt[L * 64 + lane] = 0;
   const int nw = (n + 7) >> 3;  // code length s: nibble s & 7 of dword (s >> 3) * 64 + lane (zero past n)
   for (int q = 0; q < nw; ++q) {
     const uint32_t w = lw[q * 64 + lane];
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       const uint32_t l = (w >> (4 * b)) & 15u;
-      atomicAdd(&cnt[l * 64 + lane], 1u);  // length 0 counts into slot 0, unused
+      atomicAdd(&cnt[(l >> 1) * 64 + lane], 1u << (16u * (l & 1u)));  // length 0 counts into slot 0, unused
     }
   }
   int c[16];
   c[0] = 0;
 #pragma unroll
-  for (int l = 1; l < 16; ++l) c[l] = (int)cnt[l * 64 + lane];
+  for (int l = 1; l < 16; ++l) c[l] = (int)((cnt[(l >> 1) * 64 + lane] >> (16 * (l & 1))) & 0xffffu);
   int left = 1, maxl = 0;
   bool bad = false;
 #pragma unroll
@@ -884,8 +902,10 @@ __device__ int q_build_lit(TokLds& Q, uint32_t lane, const uint32_t* lw, int n) 
     for (int l = 1; l < 16; ++l) {
       code = (code + c[l - 1]) << 1;
       nx[l] = code;
-      cnt[l * 64 + lane] = (uint32_t)code;  // the next code of each length
     }
+#pragma unroll
+    for (int L = 0; L < 8; ++L)  // the next code of each length (length 0's slot unused)
+      cnt[L * 64 + lane] = (uint32_t)nx[2 * L] | ((uint32_t)nx[2 * L + 1] << 16);
   }
   const uint32_t rsize = 1u << rb;
   if (maxl > rb) {
@@ -914,7 +934,7 @@ __device__ int q_build_lit(TokLds& Q, uint32_t lane, const uint32_t* lw, int n) 
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
       l4[b] = (w >> (4 * b)) & 15u;
-      code4[b] = atomicAdd(&cnt[l4[b] * 64 + lane], 1u);
+      code4[b] = (atomicAdd(&cnt[(l4[b] >> 1) * 64 + lane], 1u << (16u * (l4[b] & 1u))) >> (16u * (l4[b] & 1u))) & 0xffffu;
     }
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -983,7 +1003,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     const uint32_t s0 = (uint32_t)(g >> 2) & 15u;  // 0 or 8
 #pragma unroll
     for (int i = 0; i < 8; ++i) Q.ring[(s0 + i) * 64 + lane] = w[i];
-    if (s0 == 0) Q.ring[16 * 64 + lane] = w[0];
+    if (WSG_TOK_MIRROR && s0 == 0) Q.ring[16 * 64 + lane] = w[0];
   };
   uint64_t fill = off & ~(uint64_t)31;  // the next chunk to enter the ring
   const uint64_t pe = off + plen;        // where the payload ends: the tail 00 00 FF FF goes there
@@ -1016,7 +1036,8 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   auto ring_word = [&](uint32_t q) -> uint32_t {  // the 4 bytes at message offset q
     const uint32_t ipg = off32 + q;
     const uint32_t sl = (ipg >> 2) & 15u;
-    return __builtin_amdgcn_alignbyte(Q.ring[(sl + 1) * 64 + lane], Q.ring[sl * 64 + lane], ipg & 3u);
+    const uint32_t sn = WSG_TOK_MIRROR ? sl + 1u : ((sl + 1u) & 15u);
+    return __builtin_amdgcn_alignbyte(Q.ring[sn * 64 + lane], Q.ring[sl * 64 + lane], ipg & 3u);
   };
   // Input, a step: at least 32 bits held (or the rest of the input), up to 4 bytes
   // from the ring word at ip, read a step ahead so its latency overlaps the step.
@@ -1210,7 +1231,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       if ((r & 15u) == 0)
         r = tab[base + (((1u << rb) + (r >> 8) + ((uint32_t)(hold >> rb) & ((1u << ((r >> 4) & 15u)) - 1u))) << tsh)];
       const uint32_t len = r & 15u;
-      const uint32_t e = Q.ents[(r >> 4) + (dist ? 288u : 0u)];
+      const uint32_t e = tok_ent(Q.ents, r >> 4, dist);
       const uint32_t x = e_extra(e), eo = e_op(e);
       const uint32_t v = e_val(e) + ((uint32_t)(hold >> len) & ((1u << x) - 1u));
       const bool is_lit = !dist && eo == OP_LIT, is_len = !dist && eo == OP_BASE;
@@ -1257,9 +1278,8 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
 __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
   // symbol -> entry (base, extra bits, op) for the 16-bit root entries
   __shared__ TokLds Q;
-  uint32_t* const ents = Q.ents;  // literal/length entries, then distance entries
-  for (int i = threadIdx.x; i < 288; i += 64) ents[i] = sym_entry(T_LIT, (uint32_t)i, 0);
-  if (threadIdx.x < 32) ents[288 + threadIdx.x] = sym_entry(T_DIST, threadIdx.x, 0);
+  uint32_t* const ents = Q.ents;  // length entries, then distance entries (tok_ent)
+  for (int i = threadIdx.x; i < N_ENTS; i += 64) ents[i] = ents_init((uint32_t)i);
   q_fixed_tables(Q.tab, threadIdx.x);
   __syncthreads();
   const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
