@@ -848,8 +848,72 @@ def handshake_client_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
             "pipeline_ms": pipe}
 
 
+def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=8192):
+    """The native batcher with the decoders snf4j puts after "ws-decoder" when
+    permessage-deflate is negotiated (FrameDecoder -> PerMessageDeflateDecoder ->
+    FrameUtf8Validator, PerMessageDeflateExtension.java:316-326), end to end from host
+    socket reads to host frames: per round one `chunk`-byte read of every session
+    (wsg_batcher_feed_many), then wsg_batcher_flush_async (H2D, decode, inflate,
+    validate, D2H), two flushes in flight.  Value: inflated bytes delivered per second."""
+    import numpy as np
+    import torch
+    import snf4j_amd
+    from benchsupport.synth import deflate_wire
+    wire_np, starts, plain = deflate_wire(0x1F1A, n_s, msgs, msg_bytes)
+    h_wire = torch.from_numpy(wire_np).pin_memory()
+    hw = h_wire.numpy()
+    base = hw.ctypes.data
+    rounds = []
+    pos, endv = starts[:-1].copy(), starts[1:].copy()
+    while (pos < endv).any():
+        live = np.nonzero(pos < endv)[0]
+        ln = np.minimum(endv[live] - pos[live], chunk)
+        rounds.append((live.astype(np.uint32), (base + pos[live]).astype(np.uint64), ln.astype(np.uint64)))
+        pos[live] += chunk
+    pctx = snf4j_amd.Context(dev.index, stream=torch.cuda.Stream(dev))
+    apply_tuning(pctx)
+    nb = snf4j_amd.NativeBatcher(n_s, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=pctx)
+    nb.set_stages(inflate=True, noContext=False, validate=True)
+    times = []
+    for rep in range(W + K):
+        for s in range(n_s):
+            nb.reset_session(s)  # the same streams again, from fresh sessions
+        t0 = time.perf_counter()
+        pending, out_bytes, n_fr = 0, 0, 0
+        for sids, ptrs, lens in rounds:
+            nb.feed_many_ptrs(sids, ptrs, lens)
+            if pending == 2:
+                sfb, descb, _, resb, _ = nb.wait_raw()
+                assert int(resb["error"].max()) == 0
+                out_bytes += int(descb["payload_len"].astype(np.int64).sum())
+                n_fr += len(descb)
+                pending -= 1
+            nb.flush_async()
+            pending += 1
+        while pending:
+            sfb, descb, _, resb, _ = nb.wait_raw()
+            assert int(resb["error"].max()) == 0
+            out_bytes += int(descb["payload_len"].astype(np.int64).sum())
+            n_fr += len(descb)
+            pending -= 1
+        t = time.perf_counter() - t0
+        assert out_bytes == plain and n_fr == n_s * msgs, (out_bytes, plain, n_fr)
+        if rep >= W:
+            times.append(t)
+    nb.close()
+    pctx.close()
+    t = float(np.median(times))
+    return {"config": f"native batcher + stages (inflate -> validator), {n_s} sessions x {msgs} compressed TEXT "
+                      f"messages x {msg_bytes} B, context takeover, {chunk} B reads ({wire_np.size / 1e6:.0f} MB wire "
+                      f"-> {plain / 1e6:.0f} MB)",
+            "value": round(plain / t / 2**30, 3), "unit": "GiB/s (inflated bytes, host to host)",
+            "wire_GiB_per_s": round(wire_np.size / t / 2**30, 3), "ms_per_batch": round(t * 1e3, 3),
+            "reps": K, "rounds": len(rounds),
+            "api": "wsg_batcher_feed_many + wsg_batcher_flush_async/wait with wsg_batcher_set_stages"}
+
+
 EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2": line_configs2,
-               "encode": line_encode, "validator": line_validator,
+               "encode": line_encode, "validator": line_validator, "e2e_stages": e2e_stages_line,
                "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
                "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W),
                "hs_client": lambda ctx, dev, K, W: handshake_client_line(ctx, dev, K, W)}

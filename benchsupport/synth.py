@@ -143,3 +143,39 @@ def deflate_batch(seed: int, n_sessions: int, msgs_per_session: int, msg_bytes: 
     payload = np.frombuffer(b"".join(blob[s % u] for s in range(n_sessions)) + bytes(16), dtype=np.uint8)
     sf = (np.arange(n_sessions + 1) * msgs_per_session).astype(np.uint32)
     return desc, sf, payload, int(sum(plain[s % u] for s in range(n_sessions)))
+
+
+def deflate_wire(seed: int, n_sessions: int, msgs_per_session: int, msg_bytes: int, unique: int = 64):
+    """deflate_batch's messages as a client sends them on the wire: one masked TEXT frame
+    per message with RSV1 set (FrameEncoder.java:81-118 over PerMessageDeflateEncoder's
+    output), each session's frames back to back.  Returns (wire u8, session start
+    offsets [n_s + 1], plain bytes per batch)."""
+    desc, sf, payload, plain = deflate_batch(seed, n_sessions, msgs_per_session, msg_bytes, unique=unique)
+    rng = np.random.default_rng(seed ^ 0x3A5C)
+    u = min(unique, n_sessions)
+    per = []
+    for s in range(u):
+        parts = []
+        for k in range(int(sf[s]), int(sf[s + 1])):
+            o, n = int(desc[k]["payload_off"]), int(desc[k]["payload_len"])
+            p = payload[o:o + n]
+            hl = int(header_len(n, True))
+            fr = np.empty(hl + n, dtype=np.uint8)
+            fr[0] = 0x80 | 0x40 | 1
+            if n <= 125:
+                fr[1] = 0x80 | n
+            elif n <= 0xFFFF:
+                fr[1], fr[2], fr[3] = 0x80 | 126, n >> 8, n & 0xFF
+            else:
+                fr[1] = 0x80 | 127
+                fr[2:10] = np.frombuffer(n.to_bytes(8, "big"), np.uint8)
+            m = rng.integers(0, 256, 4, dtype=np.uint8)
+            fr[hl - 4:hl] = m
+            fr[hl:] = p ^ np.resize(m, n)
+            parts.append(fr)
+        per.append(np.concatenate(parts))
+    sizes = np.array([per[s % u].size for s in range(n_sessions)], dtype=np.int64)
+    starts = np.zeros(n_sessions + 1, dtype=np.int64)
+    np.cumsum(sizes, out=starts[1:])
+    wire = np.concatenate([per[s % u] for s in range(n_sessions)])
+    return wire, starts, plain
