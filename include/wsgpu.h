@@ -252,7 +252,9 @@ int wsg_decode_batch_host(wsg_ctx* ctx, const wsg_decoder_cfg* cfg,
  * until wsg_sync(ctx).  The carry state of batch i+1 is uploaded only after
  * batch i's state came back, so successive batches may share sessions and one
  * host state array.  payload_cap >= wire_len + 16 * n_frames: the whole payload
- * region is copied back, its used size being known only on the device. */
+ * region is copied back, its used size being known only on the device.
+ * payload_out == NULL: the payloads stay on the device (descriptors, results and
+ * state are still downloaded); the native batcher's stages read them there. */
 int wsg_decode_batch_host_async(wsg_ctx* ctx, const wsg_decoder_cfg* cfg,
                                 const uint8_t* wire, uint64_t wire_len,
                                 const uint64_t* frame_off, uint64_t n_frames,

@@ -83,6 +83,7 @@ struct wsg_ctx {
   HostSlot slot[2];
   int next_slot = 0;
   hipEvent_t ev_prev_state = nullptr;  // state download of the previous async batch
+  uint8_t* last_async_payload = nullptr;  // device payload of the last async batch (batcher stages)
   // timing
   int timing = 0;  // 0 off, 1 every kernel, 2 the streaming kernels only (WSG_TIMING_*)
   uint32_t timing_every = 1;  // mode 2: bracket one launch in timing_every of a streaming kernel
@@ -159,6 +160,8 @@ static void timed(wsg_ctx* c, int kid, F&& f) {
 namespace ws {
 hipError_t ctx_wait_prev_state(wsg_ctx* c) { return c->ev_prev_state ? hipEventSynchronize(c->ev_prev_state) : hipSuccess; }
 hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e) { return hipEventRecord(e, c->s_out ? c->s_out : c->stream); }
+hipStream_t ctx_stream(wsg_ctx* c) { return c->stream; }
+uint8_t* ctx_async_payload(wsg_ctx* c) { return c->last_async_payload; }
 }  // namespace ws
 
 extern "C" {
@@ -598,8 +601,10 @@ int wsg_decode_batch_host_async(wsg_ctx* c, const wsg_decoder_cfg* cfg, const ui
                               hipMemcpyDeviceToHost, c->s_out));
   if (n_frames) {
     HIP_TRY(c, hipMemcpyAsync(desc_out, h.desc.p, n_frames * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, c->s_out));
-    HIP_TRY(c, hipMemcpyAsync(payload_out, h.payload.p, wire_len + 16 * n_frames, hipMemcpyDeviceToHost, c->s_out));
+    if (payload_out)
+      HIP_TRY(c, hipMemcpyAsync(payload_out, h.payload.p, wire_len + 16 * n_frames, hipMemcpyDeviceToHost, c->s_out));
   }
+  c->last_async_payload = (uint8_t*)h.payload.p;
   HIP_TRY(c, hipEventRecord(h.ev_out, c->s_out));
   h.used = true;
   return WSG_API_OK;

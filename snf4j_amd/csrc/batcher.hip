@@ -153,10 +153,92 @@ class Pool {
   bool stop_ = false;
 };
 
+// ------------------------------------------------------------------ stage chain: device buffers
+// A device buffer that only grows.  grow_keep() keeps the first `keep` bytes (a
+// stream-ordered copy) when it has to move.
+struct DBuf {
+  uint8_t* p = nullptr;
+  size_t n = 0;
+  hipError_t ensure(size_t bytes) {
+    if (bytes <= n && p) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+    const size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
+    hipError_t e = hipMalloc((void**)&p, want);
+    if (e == hipSuccess) n = want;
+    return e;
+  }
+  hipError_t grow_keep(size_t bytes, size_t keep, hipStream_t s) {
+    if (bytes <= n && p) return hipSuccess;
+    const size_t want = bytes + bytes / 4;
+    uint8_t* q = nullptr;
+    hipError_t e = hipMalloc((void**)&q, want);
+    if (e != hipSuccess) return e;
+    if (p && keep) {
+      e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
+      if (e == hipSuccess) e = hipStreamSynchronize(s);
+    }
+    if (p) (void)hipFree(p);
+    p = q;
+    n = want;
+    return e;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+};
+
+typedef unsigned int ws_u32x4 __attribute__((ext_vector_type(4)));
+
+// One copy of the stage chain's output gather: `len` bytes from the stage arena to
+// the flush's output region (split so that no copy exceeds COPY_MAX).
+struct StageCopy {
+  uint64_t src, dst;
+  uint32_t len, pad;
+};
+constexpr uint32_t COPY_MAX = 65536;
+
+// One workgroup per copy.  Output slots are 16-B aligned; a source is 16-B aligned when
+// it is a decoder payload slot, byte-aligned when it is inflated output (messages back
+// to back), so the widest access both sides allow is used.
+__global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
+                                                    const StageCopy* __restrict__ cp) {
+  const StageCopy c = cp[blockIdx.x];
+  const uint8_t* s = src + c.src;
+  uint8_t* d = dst + c.dst;
+  const uint32_t t = threadIdx.x;
+  const uint64_t al = c.src | c.dst;
+  uint32_t done = 0;
+  if ((al & 15) == 0) {
+    done = c.len & ~15u;
+    for (uint32_t i = 16 * t; i < done; i += 16 * 256)
+      __builtin_nontemporal_store(__builtin_nontemporal_load((const ws_u32x4*)(s + i)), (ws_u32x4*)(d + i));
+  } else if ((al & 3) == 0) {
+    done = c.len & ~3u;
+    for (uint32_t i = 4 * t; i < done; i += 4 * 256) *(uint32_t*)(d + i) = *(const uint32_t*)(s + i);
+  } else {
+    // dst aligned, src not: each thread assembles a dword from the source dwords around it
+    const uint32_t sh = (uint32_t)(c.src & 3) * 8;
+    const uint32_t* s4 = (const uint32_t*)(s - (c.src & 3));
+    if ((c.dst & 3) == 0 && c.len >= 8) {
+      done = (c.len - 4) & ~3u;  // the last source dword may lie past the source: bytes below
+      for (uint32_t i = 4 * t; i < done; i += 4 * 256) {
+        const uint32_t lo = s4[i / 4], hi = s4[i / 4 + 1];
+        *(uint32_t*)(d + i) = (uint32_t)((((uint64_t)hi << 32) | lo) >> sh);
+      }
+    }
+  }
+  for (uint32_t i = done + t; i < c.len; i += 256) d[i] = s[i];
+}
+
 }  // namespace
 
 // The decoders after "ws-decoder" that run in the same flush (wsg_batcher_set_stages):
-// per session, what each stage keeps between batches.
+// per session, what each stage keeps between batches on the host (the device keeps
+// the inflater state and window, the validator context and the aggregator state).
 struct StageSess {
   std::vector<wsg_frame_desc> held_desc;  // inflate: frames of a compressed message a batch left open
   std::vector<uint8_t> held_bytes;        //   (their payloads; re-sent with WSG_DESC_REPLAY)
@@ -164,12 +246,12 @@ struct StageSess {
   bool agg_held_valid = false;
 };
 
-// One stage's input or output: per-session frames with their payloads.
-struct StageBatch {
-  std::vector<uint32_t> sf;             // [S + 1]
-  std::vector<wsg_frame_desc> desc;     // payload_off into pay (16-B aligned slots)
-  std::vector<uint8_t> pay;
-  std::vector<uint32_t> n_ok;           // [S] frames of the session that go on (<= its count)
+// A stage's frames: per session, descriptors whose payload_off is an offset in the
+// stage arena (device).
+struct StageList {
+  std::vector<uint32_t> sf;           // [S + 1]
+  std::vector<wsg_frame_desc> desc;
+  std::vector<uint32_t> n_ok;         // [S] frames of the session that go on (<= its count)
 };
 
 // One flush's pinned staging and results (two alternate: a flush can be in flight
@@ -188,6 +270,8 @@ struct FlushSlot {
   std::vector<std::vector<uint64_t>> fo;  // [n]: the session's complete frames (arena offsets), in order
   std::vector<uint64_t> fb;               // [n]: their bytes
   PinnedBuf off, sf, payload, desc, result;
+  DBuf dpay;                              // with stages: the decoded payloads, kept on the device
+  uint64_t pcap = 0;                      //   (their region's size)
   uint64_t F = 0, W = 0;
   std::vector<HostErr> host_err;  // header errors found on the host after this batch's frames
   std::vector<uint32_t> resets;   // slots given to a new session while this batch was in flight
@@ -209,15 +293,17 @@ struct wsg_batcher {
   uint32_t threads = 8;
   std::unique_ptr<Pool> pool;           // threads - 1 workers (the caller is the last one)
   std::string err;
-  // stages after the decoder (wsg_batcher_set_stages)
+  // stages after the decoder (wsg_batcher_set_stages), run on the device at wait()
   wsg_stage_cfg stages{};
   bool has_stages = false;
   std::vector<StageSess> ss;
-  std::vector<wsg_inflate_state> istate;
-  std::vector<uint8_t> iwin;
-  std::vector<wsg_session_state> vstate;
-  std::vector<wsg_agg_state> astate;
-  StageBatch fin;                       // the flush's output when stages run
+  DBuf d_istate, d_iwin, d_vstate, d_astate;  // per-session stage carry (device-resident)
+  DBuf sarena;    // a flush's stage bytes: decoded payloads | held frames | inflated | aggregated
+  DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot, d_copy, d_fin;
+  PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot;  // stage results downloaded
+  PinnedBuf fin_pay;                    // the flush's output payloads when stages run
+  std::vector<uint32_t> fin_sf;
+  std::vector<wsg_frame_desc> fin_desc;
   std::vector<wsg_session_result> fres;
 };
 
@@ -235,38 +321,6 @@ static int bset(wsg_batcher* b, int code, const char* msg) {
 // ------------------------------------------------------------------ stages after the decoder
 static inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 
-// append one frame (descriptor + payload bytes) to a stage batch
-static void push_frame(StageBatch& o, wsg_frame_desc d, const uint8_t* bytes) {
-  const uint64_t pos = o.pay.size();
-  d.payload_off = pos;
-  o.pay.resize(pos + al16(d.payload_len));
-  if (d.payload_len) memcpy(o.pay.data() + pos, bytes, d.payload_len);
-  o.desc.push_back(d);
-}
-
-// the decoder's delivered frames, per session
-static void stage_input(StageBatch& o, uint32_t S, const uint32_t* sf, const wsg_frame_desc* desc, const uint8_t* pay,
-                        const wsg_session_result* res) {
-  o.sf.assign(S + 1, 0);
-  o.n_ok.assign(S, 0);
-  o.desc.clear();
-  o.pay.clear();
-  uint64_t bytes = 0;
-  for (uint32_t s = 0; s < S; ++s)
-    for (uint32_t k = sf[s]; k < sf[s] + res[s].n_delivered; ++k) bytes += al16(desc[k].payload_len);
-  o.pay.reserve(bytes + 16);
-  for (uint32_t s = 0; s < S; ++s) {
-    o.sf[s] = (uint32_t)o.desc.size();
-    for (uint32_t k = sf[s]; k < sf[s] + res[s].n_delivered; ++k) {
-      wsg_frame_desc d = desc[k];
-      d.flags &= 0xf0u | 0x80u;  // FIN, RSV (the "was masked" bit is the decoder's)
-      push_frame(o, d, pay + desc[k].payload_off);
-    }
-    o.n_ok[s] = res[s].n_delivered;
-  }
-  o.sf[S] = (uint32_t)o.desc.size();
-}
-
 // a later stage failed session s: its result, and the session is closed
 static void stage_fail(wsg_batcher* b, uint32_t s, const wsg_session_result& r) {
   b->fres[s].error = r.error;
@@ -275,228 +329,359 @@ static void stage_fail(wsg_batcher* b, uint32_t s, const wsg_session_result& r) 
   b->state[s].closed = 1;
 }
 
-// PerMessageDeflateDecoder over `in` (PerMessageDeflateDecoder.java:68-105): sessions
-// with new frames, each after the frames of a message it left open; a session whose
-// output region overflows is run again with a larger one (nothing of it is committed).
-static int stage_inflate(wsg_batcher* b, const StageBatch& in, StageBatch& out) {
+template <typename T>
+static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
+  hipError_t e = d.ensure((v.size() + 1) * sizeof(T));
+  if (e != hipSuccess || v.empty()) return e;
+  return hipMemcpyAsync(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+}
+
+// PerMessageDeflateDecoder over `cur` (PerMessageDeflateDecoder.java:68-105), on the
+// device: each session's frames after the frames of a message it left open; the
+// inflated bytes go to the arena after `used`.  A session whose output region
+// overflows is run again with a larger one (nothing of it was committed).
+static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t& used) {
   const uint32_t S = b->n;
+  hipStream_t st = ws::ctx_stream(b->ctx);
   std::vector<std::vector<wsg_frame_desc>> od(S);
-  std::vector<std::vector<uint8_t>> op(S);
   std::vector<uint32_t> todo;
-  std::vector<uint64_t> cap(S, 0);
+  std::vector<uint64_t> cap(S, 0), held_at(S, 0);
+  // the held frames' bytes go after the decoded payloads
+  uint64_t hpos = used;
   for (uint32_t s = 0; s < S; ++s) {
-    if (in.sf[s + 1] == in.sf[s]) continue;
+    const StageSess& h = b->ss[s];
+    uint64_t c = 0;
+    if (!h.held_desc.empty()) {
+      held_at[s] = hpos;
+      hpos = al16(hpos + h.held_bytes.size());
+      for (const wsg_frame_desc& hd : h.held_desc) c += hd.payload_len + 4;
+    }
+    for (uint32_t k = cur.sf[s]; k < cur.sf[s + 1]; ++k) c += cur.desc[k].payload_len + 4;
+    if (h.held_desc.empty() && cur.sf[s + 1] == cur.sf[s]) continue;
     todo.push_back(s);
-    uint64_t c = b->ss[s].held_bytes.size();
-    for (uint32_t k = in.sf[s]; k < in.sf[s + 1]; ++k) c += in.desc[k].payload_len + 4;
-    cap[s] = 65536 + 16 * c;
+    cap[s] = al16(4096 + 8 * c);
   }
+  B_TRY(b, b->sarena.ensure(hpos + 64));
+  if (f.pcap) B_TRY(b, hipMemcpyAsync(b->sarena.p, f.dpay.p, f.pcap, hipMemcpyDeviceToDevice, st));
+  for (uint32_t s = 0; s < S; ++s) {
+    const StageSess& h = b->ss[s];
+    if (!h.held_bytes.empty())
+      B_TRY(b, hipMemcpyAsync(b->sarena.p + held_at[s], h.held_bytes.data(), h.held_bytes.size(),
+                              hipMemcpyHostToDevice, st));
+  }
+  uint64_t ipos = al16(hpos);
+  std::vector<uint32_t> nheld(S, 0);
   while (!todo.empty()) {
-    const uint32_t T = (uint32_t)todo.size();
-    StageBatch x;
-    x.sf.push_back(0);
-    std::vector<wsg_inflate_state> st(T);
-    std::vector<uint8_t> win((uint64_t)T * WSG_INFLATE_WINDOW);
-    std::vector<uint64_t> oo(T + 1, 0);
-    for (uint32_t i = 0; i < T; ++i) {
-      const uint32_t s = todo[i];
+    // this attempt's input: the todo sessions' frames; every session takes part (the
+    // carry is indexed by session), the others with no frames
+    StageList x;
+    x.sf.assign(S + 1, 0);
+    std::vector<uint64_t> oo(S + 1, 0);
+    size_t ti = 0;
+    for (uint32_t s = 0; s < S; ++s) {
+      x.sf[s] = (uint32_t)x.desc.size();
+      const bool in = ti < todo.size() && todo[ti] == s;
+      oo[s + 1] = oo[s] + (in ? cap[s] : 0);
+      if (!in) continue;
+      ++ti;
       const StageSess& h = b->ss[s];
       for (const wsg_frame_desc& hd : h.held_desc) {
         wsg_frame_desc d = hd;
         d.flags |= WSG_DESC_REPLAY;
-        push_frame(x, d, h.held_bytes.data() + hd.payload_off);
+        d.payload_off += held_at[s];
+        x.desc.push_back(d);
       }
-      for (uint32_t k = in.sf[s]; k < in.sf[s + 1]; ++k) {
-        wsg_frame_desc d = in.desc[k];
+      nheld[s] = (uint32_t)h.held_desc.size();
+      for (uint32_t k = cur.sf[s]; k < cur.sf[s + 1]; ++k) {
+        wsg_frame_desc d = cur.desc[k];
         d.flags &= (uint8_t)~WSG_DESC_REPLAY;
-        push_frame(x, d, in.pay.data() + in.desc[k].payload_off);
+        x.desc.push_back(d);
       }
-      x.sf.push_back((uint32_t)x.desc.size());
-      st[i] = b->istate[s];
-      memcpy(win.data() + (uint64_t)i * WSG_INFLATE_WINDOW, b->iwin.data() + (uint64_t)s * WSG_INFLATE_WINDOW,
-             WSG_INFLATE_WINDOW);
-      oo[i + 1] = oo[i] + cap[s];
     }
-    x.pay.resize(x.pay.size() + 16);
+    x.sf[S] = (uint32_t)x.desc.size();
     const uint64_t F = x.desc.size();
-    std::vector<uint8_t> ob(oo[T] + 32);
-    std::vector<wsg_frame_desc> odesc(F + 1);
-    std::vector<wsg_session_result> r(T);
-    std::vector<uint32_t> rf(T);
-    int rc = wsg_inflate_batch_host(b->ctx, b->stages.inflate_no_context, x.desc.data(), F, x.sf.data(), T,
-                                    x.pay.data(), x.pay.size(), st.data(), win.data(), ob.data(), oo.data(),
-                                    odesc.data(), r.data(), rf.data());
+    B_TRY(b, b->sarena.grow_keep(ipos + oo[S] + 64, ipos, st));
+    B_TRY(b, upload(b->d_desc, x.desc, st));
+    B_TRY(b, upload(b->d_sf, x.sf, st));
+    B_TRY(b, upload(b->d_ooff, oo, st));
+    B_TRY(b, b->d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+    B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+    B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
+    int rc = wsg_inflate_batch_device(b->ctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
+                                      (const uint32_t*)b->d_sf.p, S, b->sarena.p, ipos, (wsg_inflate_state*)b->d_istate.p,
+                                      b->d_iwin.p, b->sarena.p + ipos, (const uint64_t*)b->d_ooff.p,
+                                      (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
+                                      (uint32_t*)b->d_rf.p);
     if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+    B_TRY(b, b->h_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+    B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+    B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
+    if (F) B_TRY(b, hipMemcpyAsync(b->h_odesc.p, b->d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, st));
+    B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
+    B_TRY(b, hipMemcpyAsync(b->h_rf.p, b->d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    B_TRY(b, hipStreamSynchronize(st));
+    const wsg_frame_desc* odesc = (const wsg_frame_desc*)b->h_odesc.p;
+    const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
+    const uint32_t* rf = (const uint32_t*)b->h_rf.p;
     std::vector<uint32_t> retry;
-    for (uint32_t i = 0; i < T; ++i) {
-      const uint32_t s = todo[i];
-      if (r[i].error == WSG_E_INFLATE_CAPACITY) {
+    struct Held {
+      uint32_t s;
+      uint64_t src, dst, len;
+    };
+    std::vector<Held> hd_copies;
+    for (uint32_t s : todo) {
+      if (r[s].error == WSG_E_INFLATE_CAPACITY) {
         cap[s] *= 8;
         retry.push_back(s);
         continue;
       }
-      b->istate[s] = st[i];
-      memcpy(b->iwin.data() + (uint64_t)s * WSG_INFLATE_WINDOW, win.data() + (uint64_t)i * WSG_INFLATE_WINDOW,
-             WSG_INFLATE_WINDOW);
       StageSess& h = b->ss[s];
-      const uint32_t nheld = (uint32_t)h.held_desc.size();
       uint32_t j = 0;
-      for (uint32_t k = x.sf[i] + nheld; k < x.sf[i + 1] && j < r[i].n_delivered; ++k, ++j) {
+      for (uint32_t k = x.sf[s] + nheld[s]; k < x.sf[s + 1] && j < r[s].n_delivered; ++k, ++j) {
         wsg_frame_desc d = odesc[k];
-        const bool infl = (d.flags & WSG_DESC_INFLATED) != 0;
-        const uint8_t* src = infl ? ob.data() + d.payload_off : x.pay.data() + x.desc[k].payload_off;
+        if (d.flags & WSG_DESC_INFLATED) d.payload_off += ipos;  // (else the input's arena offset)
         d.flags &= 0xf0u | 0x80u;
-        const uint64_t pos = op[s].size();
-        op[s].resize(pos + al16(d.payload_len));
-        if (d.payload_len) memcpy(op[s].data() + pos, src, d.payload_len);
-        d.payload_off = pos;
         od[s].push_back(d);
       }
       std::vector<wsg_frame_desc> nhd;
-      std::vector<uint8_t> nhb;
-      if (r[i].error) {
-        stage_fail(b, s, r[i]);
-      } else if (rf[i] != 0xFFFFFFFFu) {  // a message left open: its frames go again with the next batch
-        for (uint32_t k = x.sf[i] + rf[i]; k < x.sf[i + 1]; ++k) {
+      uint64_t nb = 0;
+      if (r[s].error) {
+        stage_fail(b, s, r[s]);
+      } else if (rf[s] != 0xFFFFFFFFu) {  // a message left open: its frames go again with the next batch
+        for (uint32_t k = x.sf[s] + rf[s]; k < x.sf[s + 1]; ++k) {
           wsg_frame_desc d = x.desc[k];
           d.flags &= (uint8_t)~WSG_DESC_REPLAY;
-          const uint64_t pos = nhb.size();
-          nhb.resize(pos + d.payload_len);
-          if (d.payload_len) memcpy(nhb.data() + pos, x.pay.data() + x.desc[k].payload_off, d.payload_len);
-          d.payload_off = pos;
+          hd_copies.push_back({s, d.payload_off, nb, d.payload_len});
+          d.payload_off = nb;
+          nb += d.payload_len;
           nhd.push_back(d);
         }
       }
       h.held_desc.swap(nhd);
-      h.held_bytes.swap(nhb);
+      h.held_bytes.assign(nb, 0);
     }
+    for (const Held& c : hd_copies)
+      if (c.len)
+        B_TRY(b, hipMemcpyAsync(b->ss[c.s].held_bytes.data() + c.dst, b->sarena.p + c.src, c.len,
+                                hipMemcpyDeviceToHost, st));
+    if (!hd_copies.empty()) B_TRY(b, hipStreamSynchronize(st));
+    ipos = al16(ipos + oo[S]);
     todo.swap(retry);
   }
-  out.sf.assign(S + 1, 0);
-  out.n_ok.assign(S, 0);
-  out.desc.clear();
-  out.pay.clear();
+  cur.sf.assign(S + 1, 0);
+  cur.n_ok.assign(S, 0);
+  cur.desc.clear();
   for (uint32_t s = 0; s < S; ++s) {
-    out.sf[s] = (uint32_t)out.desc.size();
-    const uint64_t base = out.pay.size();
-    out.pay.insert(out.pay.end(), op[s].begin(), op[s].end());
-    for (wsg_frame_desc d : od[s]) {
-      d.payload_off += base;
-      out.desc.push_back(d);
-    }
-    out.n_ok[s] = (uint32_t)od[s].size();
+    cur.sf[s] = (uint32_t)cur.desc.size();
+    cur.desc.insert(cur.desc.end(), od[s].begin(), od[s].end());
+    cur.n_ok[s] = (uint32_t)od[s].size();
   }
-  out.sf[S] = (uint32_t)out.desc.size();
+  cur.sf[S] = (uint32_t)cur.desc.size();
+  used = ipos;
   return WSG_API_OK;
 }
 
-// FrameUtf8Validator over `io` (FrameUtf8Validator.java:59-98): the frames a
-// session passes before its first failure go on.
-static int stage_validate(wsg_batcher* b, StageBatch& io) {
+// FrameUtf8Validator over `cur` (FrameUtf8Validator.java:59-98), on the device: the
+// frames a session passes before its first failure go on.
+static int stage_validate(wsg_batcher* b, StageList& cur, uint64_t used) {
   const uint32_t S = b->n;
-  if (io.pay.size() < 16) io.pay.resize(16);
-  std::vector<wsg_session_result> r(S);
-  int rc = wsg_validate_batch_host(b->ctx, io.desc.data(), io.desc.size(), io.sf.data(), S, io.pay.data(),
-                                   io.pay.size(), b->vstate.data(), r.data());
+  hipStream_t st = ws::ctx_stream(b->ctx);
+  B_TRY(b, upload(b->d_desc, cur.desc, st));
+  B_TRY(b, upload(b->d_sf, cur.sf, st));
+  B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  int rc = wsg_validate_batch_device(b->ctx, (const wsg_frame_desc*)b->d_desc.p, cur.desc.size(),
+                                     (const uint32_t*)b->d_sf.p, S, b->sarena.p, used,
+                                     (wsg_session_state*)b->d_vstate.p, (wsg_session_result*)b->d_ores.p);
   if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
+  B_TRY(b, hipStreamSynchronize(st));
+  const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
   for (uint32_t s = 0; s < S; ++s) {
-    io.n_ok[s] = std::min(io.n_ok[s], r[s].n_delivered);
+    cur.n_ok[s] = std::min(cur.n_ok[s], r[s].n_delivered);
     if (r[s].error) stage_fail(b, s, r[s]);
   }
   return WSG_API_OK;
 }
 
-// FrameAggregator over `in` (FrameAggregator.java:72-104) into `out`: pass-through
-// frames keep their bytes, an aggregated message is its held bytes (earlier
-// batches, PayloadAggregator.java:34) + this batch's.
-static int stage_aggregate(wsg_batcher* b, const StageBatch& in, StageBatch& out) {
+// The flush's output, gathered on the device into one region and downloaded once:
+// `copies` move arena bytes to 16-B slots of it; `host_parts` are bytes only the host
+// holds (an aggregated message's bytes from earlier batches), written after.
+struct FinParts {
+  std::vector<StageCopy> copies;
+  std::vector<std::pair<uint64_t, std::vector<uint8_t>>> host_parts;
+  uint64_t len = 0;
+};
+
+static void fin_push(wsg_batcher* b, FinParts& fp, wsg_frame_desc d, uint64_t src, uint32_t dev_len,
+                     std::vector<uint8_t>* prefix) {
+  const uint64_t pos = fp.len;
+  const uint64_t pre = prefix ? prefix->size() : 0;
+  d.payload_off = pos;
+  d.payload_len = (uint32_t)(pre + dev_len);
+  for (uint64_t o = 0; o < dev_len; o += COPY_MAX) {
+    const uint32_t n = (uint32_t)std::min<uint64_t>(COPY_MAX, dev_len - o);
+    fp.copies.push_back({src + o, pos + pre + o, n, 0});
+  }
+  if (pre) fp.host_parts.emplace_back(pos, std::move(*prefix));
+  fp.len = al16(pos + pre + dev_len);
+  b->fin_desc.push_back(d);
+}
+
+// FrameAggregator over `cur` (FrameAggregator.java:72-104), on the device, straight
+// into the output list: pass-through frames keep their bytes, an aggregated message is
+// its held bytes (earlier batches, PayloadAggregator.java:34) + this batch's.
+static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinParts& fp,
+                           std::vector<std::pair<uint32_t, StageCopy>>& pending) {
   const uint32_t S = b->n;
-  const uint64_t F = in.desc.size();
+  hipStream_t st = ws::ctx_stream(b->ctx);
+  const uint64_t F = cur.desc.size();
   std::vector<wsg_session_result> dres(S);
-  for (uint32_t s = 0; s < S; ++s) dres[s].n_delivered = in.n_ok[s];
-  std::vector<uint8_t> pay(in.pay);
-  pay.resize(pay.size() + 16);
-  const uint64_t cap = pay.size();
-  std::vector<uint8_t> ab(cap + 32);
-  std::vector<wsg_frame_desc> odesc(F + S + 1);
-  std::vector<wsg_session_result> r(S);
-  uint64_t tot = 0;
-  int rc = wsg_aggregate_batch_host(b->ctx, b->stages.max_aggregated_len, in.desc.data(), F, in.sf.data(), S,
-                                    dres.data(), pay.data(), pay.size(), b->astate.data(), ab.data(), cap,
-                                    odesc.data(), r.data(), &tot);
-  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
-  out.sf.assign(S + 1, 0);
-  out.n_ok.assign(S, 0);
-  out.desc.clear();
-  out.pay.clear();
+  uint64_t bytes = 16;
   for (uint32_t s = 0; s < S; ++s) {
-    out.sf[s] = (uint32_t)out.desc.size();
+    dres[s].n_delivered = cur.n_ok[s];
+    for (uint32_t k = cur.sf[s]; k < cur.sf[s] + cur.n_ok[s]; ++k) bytes += cur.desc[k].payload_len;
+  }
+  const uint64_t A0 = al16(used), cap = al16(bytes);
+  B_TRY(b, b->sarena.grow_keep(A0 + cap + 64, used, st));
+  B_TRY(b, upload(b->d_desc, cur.desc, st));
+  B_TRY(b, upload(b->d_sf, cur.sf, st));
+  B_TRY(b, upload(b->d_res, dres, st));
+  B_TRY(b, b->d_odesc.ensure((F + S + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->d_tot.ensure(sizeof(uint64_t)));
+  int rc = wsg_aggregate_batch_device(b->ctx, b->stages.max_aggregated_len, (const wsg_frame_desc*)b->d_desc.p, F,
+                                      (const uint32_t*)b->d_sf.p, S, (const wsg_session_result*)b->d_res.p,
+                                      b->sarena.p, used, (wsg_agg_state*)b->d_astate.p, b->sarena.p + A0, cap,
+                                      (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
+                                      (uint64_t*)b->d_tot.p);
+  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  B_TRY(b, b->h_odesc.ensure((F + S + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->h_astate.ensure((S + 1) * sizeof(wsg_agg_state)));
+  B_TRY(b, hipMemcpyAsync(b->h_odesc.p, b->d_odesc.p, (F + S) * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, st));
+  B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
+  B_TRY(b, hipMemcpyAsync(b->h_astate.p, b->d_astate.p, S * sizeof(wsg_agg_state), hipMemcpyDeviceToHost, st));
+  B_TRY(b, hipStreamSynchronize(st));
+  const wsg_frame_desc* odesc = (const wsg_frame_desc*)b->h_odesc.p;
+  const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
+  const wsg_agg_state* ast = (const wsg_agg_state*)b->h_astate.p;
+  for (uint32_t s = 0; s < S; ++s) {
+    b->fin_sf[s] = (uint32_t)b->fin_desc.size();
     StageSess& h = b->ss[s];
-    const uint64_t base = (uint64_t)in.sf[s] + s;
+    const uint64_t base = (uint64_t)cur.sf[s] + s;
     for (uint32_t i = 0; i < r[s].n_delivered; ++i) {
       wsg_frame_desc d = odesc[base + i];
       if (d.flags & WSG_AGG_IN_AGG) {
-        std::vector<uint8_t> m;
-        if ((d.flags & WSG_AGG_PREFIXED) && h.agg_held_valid) m = h.agg_held;
-        m.insert(m.end(), ab.data() + d.payload_off, ab.data() + d.payload_off + d.payload_len);
+        std::vector<uint8_t> pre;
+        if ((d.flags & WSG_AGG_PREFIXED) && h.agg_held_valid) pre.swap(h.agg_held);
         h.agg_held.clear();
         h.agg_held_valid = false;
         d.flags = (uint8_t)((d.flags & 0xf0u) | 0x80u | WSG_OUT_AGGREGATED);
-        d.payload_len = (uint32_t)m.size();
-        push_frame(out, d, m.data());
+        fin_push(b, fp, d, A0 + d.payload_off, d.payload_len, &pre);
       } else {
         d.flags &= 0xf0u | 0x80u;
-        push_frame(out, d, pay.data() + d.payload_off);
+        fin_push(b, fp, d, d.payload_off, d.payload_len, nullptr);
       }
     }
-    out.n_ok[s] = r[s].n_delivered;
+    b->fres[s].n_delivered = (uint32_t)b->fin_desc.size() - b->fin_sf[s];
     if (r[s].error) {
       stage_fail(b, s, r[s]);
       h.agg_held.clear();
       h.agg_held_valid = false;
-    } else if (b->astate[s].open) {  // this batch's bytes of the message still open
+    } else if (ast[s].open) {  // this batch's bytes of the message still open, held after the download
       const wsg_frame_desc& d = odesc[base + r[s].n_delivered];
       if (!((d.flags & WSG_AGG_PREFIXED) && h.agg_held_valid)) h.agg_held.clear();
-      h.agg_held.insert(h.agg_held.end(), ab.data() + d.payload_off, ab.data() + d.payload_off + d.payload_len);
       h.agg_held_valid = true;
+      if (d.payload_len) pending.push_back({s, StageCopy{A0 + d.payload_off, 0, d.payload_len, 0}});
     } else {
       h.agg_held.clear();
       h.agg_held_valid = false;
     }
   }
-  out.sf[S] = (uint32_t)out.desc.size();
   return WSG_API_OK;
 }
 
-static int run_stages(wsg_batcher* b, const uint32_t* sf, const wsg_frame_desc* desc, const uint8_t* pay,
-                      const wsg_session_result* res) {
+// The stage chain over a waited flush: the decoder's delivered frames (their payloads
+// still on the device, f.dpay) through inflate -> validator -> aggregator on the
+// device, then one gather and one download of what the handler receives.
+static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
   const uint32_t S = b->n;
+  hipStream_t st = ws::ctx_stream(b->ctx);
   b->fres.assign(res, res + S);
-  StageBatch a, t;
-  stage_input(a, S, sf, desc, pay, res);
+  const uint32_t* sf = (const uint32_t*)f.sf.p;
+  const wsg_frame_desc* desc = (const wsg_frame_desc*)f.desc.p;
+  StageList cur;
+  cur.sf.assign(S + 1, 0);
+  cur.n_ok.assign(S, 0);
+  for (uint32_t s = 0; s < S; ++s) {
+    cur.sf[s] = (uint32_t)cur.desc.size();
+    for (uint32_t k = sf[s]; k < sf[s] + res[s].n_delivered; ++k) {
+      wsg_frame_desc d = desc[k];
+      d.flags &= 0xf0u | 0x80u;  // FIN, RSV (the "was masked" bit is the decoder's)
+      cur.desc.push_back(d);
+    }
+    cur.n_ok[s] = res[s].n_delivered;
+  }
+  cur.sf[S] = (uint32_t)cur.desc.size();
+  uint64_t used = al16(f.pcap);
   int rc;
   if (b->stages.inflate) {
-    if ((rc = stage_inflate(b, a, t))) return rc;
-    a.sf.swap(t.sf); a.desc.swap(t.desc); a.pay.swap(t.pay); a.n_ok.swap(t.n_ok);
-    if (b->stages.validate && (rc = stage_validate(b, a))) return rc;
+    if ((rc = stage_inflate(b, f, cur, used))) return rc;
+    if (b->stages.validate && (rc = stage_validate(b, cur, used))) return rc;
+  } else {
+    B_TRY(b, b->sarena.ensure(used + 64));
+    if (f.pcap) B_TRY(b, hipMemcpyAsync(b->sarena.p, f.dpay.p, f.pcap, hipMemcpyDeviceToDevice, st));
   }
+  FinParts fp;
+  std::vector<std::pair<uint32_t, StageCopy>> pending;
+  b->fin_sf.assign(S + 1, 0);
+  b->fin_desc.clear();
   if (b->stages.aggregate) {
-    if ((rc = stage_aggregate(b, a, t))) return rc;
-    a.sf.swap(t.sf); a.desc.swap(t.desc); a.pay.swap(t.pay); a.n_ok.swap(t.n_ok);
+    if ((rc = stage_aggregate(b, cur, used, fp, pending))) return rc;
+  } else {
+    for (uint32_t s = 0; s < S; ++s) {
+      b->fin_sf[s] = (uint32_t)b->fin_desc.size();
+      for (uint32_t k = cur.sf[s]; k < cur.sf[s] + cur.n_ok[s]; ++k)
+        fin_push(b, fp, cur.desc[k], cur.desc[k].payload_off, cur.desc[k].payload_len, nullptr);
+      b->fres[s].n_delivered = cur.n_ok[s];
+    }
   }
-  // the output: each session's frames that went through every stage
-  StageBatch& f = b->fin;
-  f.sf.assign(S + 1, 0);
-  f.desc.clear();
-  f.pay.clear();
-  f.pay.reserve(a.pay.size() + 16);
-  for (uint32_t s = 0; s < S; ++s) {
-    f.sf[s] = (uint32_t)f.desc.size();
-    for (uint32_t k = a.sf[s]; k < a.sf[s] + a.n_ok[s]; ++k) push_frame(f, a.desc[k], a.pay.data() + a.desc[k].payload_off);
-    b->fres[s].n_delivered = (uint32_t)f.desc.size() - f.sf[s];
+  b->fin_sf[S] = (uint32_t)b->fin_desc.size();
+  // the output: gathered on the device, downloaded once
+  B_TRY(b, b->fin_pay.ensure(fp.len + 16));
+  if (!fp.copies.empty()) {
+    B_TRY(b, upload(b->d_copy, fp.copies, st));
+    B_TRY(b, b->d_fin.ensure(fp.len + 16));
+    hipLaunchKernelGGL(k_stage_copy, dim3((uint32_t)fp.copies.size()), dim3(256), 0, st, b->sarena.p, b->d_fin.p,
+                       (const StageCopy*)b->d_copy.p);
+    B_TRY(b, hipGetLastError());
+    B_TRY(b, hipMemcpyAsync(b->fin_pay.p, b->d_fin.p, fp.len, hipMemcpyDeviceToHost, st));
   }
-  f.sf[S] = (uint32_t)f.desc.size();
-  f.pay.resize(f.pay.size() + 16);
+  std::vector<std::vector<uint8_t>> pend_bytes(pending.size());
+  for (size_t i = 0; i < pending.size(); ++i) {
+    pend_bytes[i].resize(pending[i].second.len);
+    B_TRY(b, hipMemcpyAsync(pend_bytes[i].data(), b->sarena.p + pending[i].second.src, pending[i].second.len,
+                            hipMemcpyDeviceToHost, st));
+  }
+  B_TRY(b, hipStreamSynchronize(st));
+  for (auto& hp : fp.host_parts)
+    if (!hp.second.empty()) memcpy(b->fin_pay.p + hp.first, hp.second.data(), hp.second.size());
+  for (size_t i = 0; i < pending.size(); ++i) {
+    std::vector<uint8_t>& held = b->ss[pending[i].first].agg_held;
+    held.insert(held.end(), pend_bytes[i].begin(), pend_bytes[i].end());
+  }
+  return WSG_API_OK;
+}
+
+// zero session sid's device-resident stage carry (a fresh inflater, validator and
+// aggregator), in stream order
+static int stage_reset_dev(wsg_batcher* b, uint32_t sid) {
+  hipStream_t st = ws::ctx_stream(b->ctx);
+  B_TRY(b, hipMemsetAsync(b->d_istate.p + (uint64_t)sid * sizeof(wsg_inflate_state), 0, sizeof(wsg_inflate_state), st));
+  B_TRY(b, hipMemsetAsync(b->d_iwin.p + (uint64_t)sid * WSG_INFLATE_WINDOW, 0, WSG_INFLATE_WINDOW, st));
+  B_TRY(b, hipMemsetAsync(b->d_vstate.p + (uint64_t)sid * sizeof(wsg_session_state), 0, sizeof(wsg_session_state), st));
+  B_TRY(b, hipMemsetAsync(b->d_astate.p + (uint64_t)sid * sizeof(wsg_agg_state), 0, sizeof(wsg_agg_state), st));
   return WSG_API_OK;
 }
 
@@ -527,9 +712,15 @@ int wsg_batcher_close(wsg_batcher* b) {
   for (FlushSlot& f : b->fs) {
     PinnedBuf* bufs[] = {&f.arena, &f.off, &f.sf, &f.payload, &f.desc, &f.result};
     for (PinnedBuf* p : bufs) p->release();
+    f.dpay.release();
     if (f.done) (void)hipEventDestroy(f.done);
   }
   b->st.release();
+  DBuf* dbufs[] = {&b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->sarena, &b->d_sf, &b->d_desc,
+                   &b->d_odesc, &b->d_res, &b->d_ores, &b->d_rf, &b->d_ooff, &b->d_tot, &b->d_copy, &b->d_fin};
+  for (DBuf* d : dbufs) d->release();
+  PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot, &b->fin_pay};
+  for (PinnedBuf* p : hbufs) p->release();
   delete b;
   return WSG_API_OK;
 }
@@ -755,7 +946,7 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
   B_TRY(b, f.off.ensure((F + 1) * sizeof(uint64_t)));
   B_TRY(b, f.sf.ensure((S + 1) * sizeof(uint32_t)));
   const uint64_t pcap = wl + 16 * F + 16;
-  B_TRY(b, f.payload.ensure(pcap));
+  if (!b->has_stages) B_TRY(b, f.payload.ensure(pcap));
   B_TRY(b, f.desc.ensure((F + 1) * sizeof(wsg_frame_desc)));
   B_TRY(b, f.result.ensure((S + 1) * sizeof(wsg_session_result)));
   if (!f.done) B_TRY(b, hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
@@ -787,9 +978,19 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
   if (rc) return rc;
   wsg_decoder_cfg cfg = b->cfg;
   cfg.flags |= WSG_CFG_SPARSE;
+  // with stages the payloads stay on the device: copied (in stream order, before a later
+  // batch can reuse the context's staging slot) to this flush's device region
   rc = wsg_decode_batch_host_async(b->ctx, &cfg, f.arena.p, wl, off, F, sf, S, (wsg_session_state*)b->st.p,
-                                   f.payload.p, pcap, (wsg_frame_desc*)f.desc.p, (wsg_session_result*)f.result.p);
+                                   b->has_stages ? nullptr : f.payload.p, pcap, (wsg_frame_desc*)f.desc.p,
+                                   (wsg_session_result*)f.result.p);
   if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  f.pcap = 0;
+  if (b->has_stages && F) {
+    B_TRY(b, f.dpay.ensure(pcap));
+    B_TRY(b, hipMemcpyAsync(f.dpay.p, ws::ctx_async_payload(b->ctx), pcap, hipMemcpyDeviceToDevice,
+                            ws::ctx_stream(b->ctx)));
+    f.pcap = pcap;
+  }
   B_TRY(b, ws::ctx_record_out(b->ctx, f.done));
   b->q.push_back(slot);
   // feeds go to the next slot (waited: at most two in flight)
@@ -857,7 +1058,7 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
       x.host_closed = true;
     }
   if (!b->has_stages) return WSG_API_OK;
-  const int rc2 = run_stages(b, out->session_first, out->desc, out->payload, res);
+  const int rc2 = run_stages(b, f, res);
   if (rc2) return rc2;
   for (uint32_t i = 0; i < S; ++i) {
     if (b->fres[i].error != res[i].error) f.detail2[i] = 0;  // (a stage's error has no second argument)
@@ -870,10 +1071,10 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
       x.host_err = 0;
       x.host_closed = true;
     }
-  out->n_frames = b->fin.desc.size();
-  out->session_first = b->fin.sf.data();
-  out->desc = b->fin.desc.data();
-  out->payload = b->fin.pay.data();
+  out->n_frames = b->fin_desc.size();
+  out->session_first = b->fin_sf.data();
+  out->desc = b->fin_desc.data();
+  out->payload = b->fin_pay.p;
   out->result = b->fres.data();
   return WSG_API_OK;
 }
@@ -900,10 +1101,15 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
   b->cfg.validate_utf8 = stages->inflate ? 0 : (stages->validate ? 1 : 0);
   const uint32_t S = b->n;
   b->ss.assign(S, StageSess{});
-  b->istate.assign(S, wsg_inflate_state{});
-  b->iwin.assign((uint64_t)S * WSG_INFLATE_WINDOW, 0);
-  b->vstate.assign(S, wsg_session_state{});
-  b->astate.assign(S, wsg_agg_state{});
+  if (b->has_stages) {  // the device-resident stage carry, zeroed (fresh stage decoders)
+    hipStream_t st = ws::ctx_stream(b->ctx);
+    B_TRY(b, b->d_istate.ensure(((uint64_t)S + 1) * sizeof(wsg_inflate_state)));
+    B_TRY(b, b->d_iwin.ensure(((uint64_t)S + 1) * WSG_INFLATE_WINDOW));
+    B_TRY(b, b->d_vstate.ensure(((uint64_t)S + 1) * sizeof(wsg_session_state)));
+    B_TRY(b, b->d_astate.ensure(((uint64_t)S + 1) * sizeof(wsg_agg_state)));
+    DBuf* z[] = {&b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate};
+    for (DBuf* d : z) B_TRY(b, hipMemsetAsync(d->p, 0, d->n, st));
+  }
   return WSG_API_OK;
 }
 
@@ -933,10 +1139,8 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
   b->patch.push_back({sid, 0});
   if (b->has_stages) {  // fresh stage decoders too
     b->ss[sid] = StageSess{};
-    b->istate[sid] = wsg_inflate_state{};
-    memset(b->iwin.data() + (uint64_t)sid * WSG_INFLATE_WINDOW, 0, WSG_INFLATE_WINDOW);
-    b->vstate[sid] = wsg_session_state{};
-    b->astate[sid] = wsg_agg_state{};
+    const int rc = stage_reset_dev(b, sid);
+    if (rc) return rc;
   }
   return WSG_API_OK;
 }
