@@ -880,10 +880,15 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
             nb.reset_session(s)  # the same streams again, from fresh sessions
         t0 = time.perf_counter()
         pending, out_bytes, n_fr = 0, 0, 0
+        tw = tf = 0.0
         for sids, ptrs, lens in rounds:
+            ta = time.perf_counter()
             nb.feed_many_ptrs(sids, ptrs, lens)
+            tf += time.perf_counter() - ta
             if pending == 2:
+                ta = time.perf_counter()
                 sfb, descb, _, resb, _ = nb.wait_raw()
+                tw += time.perf_counter() - ta
                 assert int(resb["error"].max()) == 0
                 out_bytes += int(descb["payload_len"].astype(np.int64).sum())
                 n_fr += len(descb)
@@ -891,7 +896,9 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
             nb.flush_async()
             pending += 1
         while pending:
+            ta = time.perf_counter()
             sfb, descb, _, resb, _ = nb.wait_raw()
+            tw += time.perf_counter() - ta
             assert int(resb["error"].max()) == 0
             out_bytes += int(descb["payload_len"].astype(np.int64).sum())
             n_fr += len(descb)
@@ -899,16 +906,16 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
         t = time.perf_counter() - t0
         assert out_bytes == plain and n_fr == n_s * msgs, (out_bytes, plain, n_fr)
         if rep >= W:
-            times.append(t)
+            times.append((t, tf, tw))
     nb.close()
     pctx.close()
-    t = float(np.median(times))
+    t, tf, tw = sorted(times)[len(times) // 2]
     return {"config": f"native batcher + stages (inflate -> validator), {n_s} sessions x {msgs} compressed TEXT "
                       f"messages x {msg_bytes} B, context takeover, {chunk} B reads ({wire_np.size / 1e6:.0f} MB wire "
                       f"-> {plain / 1e6:.0f} MB)",
             "value": round(plain / t / 2**30, 3), "unit": "GiB/s (inflated bytes, host to host)",
             "wire_GiB_per_s": round(wire_np.size / t / 2**30, 3), "ms_per_batch": round(t * 1e3, 3),
-            "reps": K, "rounds": len(rounds),
+            "reps": K, "rounds": len(rounds), "feed_ms": round(tf * 1e3, 3), "wait_ms": round(tw * 1e3, 3),
             "api": "wsg_batcher_feed_many + wsg_batcher_flush_async/wait with wsg_batcher_set_stages"}
 
 

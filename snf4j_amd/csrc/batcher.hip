@@ -272,6 +272,7 @@ struct FlushSlot {
   PinnedBuf off, sf, payload, desc, result;
   DBuf dpay;                              // with stages: the decoded payloads, kept on the device
   uint64_t pcap = 0;                      //   (their region's size)
+  hipEvent_t dpay_done = nullptr;         //   after their copy (the stage stream waits for it)
   uint64_t F = 0, W = 0;
   std::vector<HostErr> host_err;  // header errors found on the host after this batch's frames
   std::vector<uint32_t> resets;   // slots given to a new session while this batch was in flight
@@ -296,6 +297,8 @@ struct wsg_batcher {
   // stages after the decoder (wsg_batcher_set_stages), run on the device at wait()
   wsg_stage_cfg stages{};
   bool has_stages = false;
+  wsg_ctx* sctx = nullptr;  // the stages' own context (stream + workspace): a flush's stages run
+                            // beside the next flush's upload and decode on the batcher's context
   std::vector<StageSess> ss;
   DBuf d_istate, d_iwin, d_vstate, d_astate;  // per-session stage carry (device-resident)
   DBuf sarena;    // a flush's stage bytes: decoded payloads | held frames | inflated | aggregated
@@ -342,7 +345,7 @@ static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
 // overflows is run again with a larger one (nothing of it was committed).
 static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t& used) {
   const uint32_t S = b->n;
-  hipStream_t st = ws::ctx_stream(b->ctx);
+  hipStream_t st = ws::ctx_stream(b->sctx);
   std::vector<std::vector<wsg_frame_desc>> od(S);
   std::vector<uint32_t> todo;
   std::vector<uint64_t> cap(S, 0), held_at(S, 0);
@@ -407,12 +410,12 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     B_TRY(b, b->d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
     B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
     B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
-    int rc = wsg_inflate_batch_device(b->ctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
+    int rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
                                       (const uint32_t*)b->d_sf.p, S, b->sarena.p, ipos, (wsg_inflate_state*)b->d_istate.p,
                                       b->d_iwin.p, b->sarena.p + ipos, (const uint64_t*)b->d_ooff.p,
                                       (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
                                       (uint32_t*)b->d_rf.p);
-    if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+    if (rc) return bset(b, rc, wsg_last_error(b->sctx));
     B_TRY(b, b->h_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
     B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
     B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
@@ -485,14 +488,14 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
 // frames a session passes before its first failure go on.
 static int stage_validate(wsg_batcher* b, StageList& cur, uint64_t used) {
   const uint32_t S = b->n;
-  hipStream_t st = ws::ctx_stream(b->ctx);
+  hipStream_t st = ws::ctx_stream(b->sctx);
   B_TRY(b, upload(b->d_desc, cur.desc, st));
   B_TRY(b, upload(b->d_sf, cur.sf, st));
   B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
-  int rc = wsg_validate_batch_device(b->ctx, (const wsg_frame_desc*)b->d_desc.p, cur.desc.size(),
+  int rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_desc.p, cur.desc.size(),
                                      (const uint32_t*)b->d_sf.p, S, b->sarena.p, used,
                                      (wsg_session_state*)b->d_vstate.p, (wsg_session_result*)b->d_ores.p);
-  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  if (rc) return bset(b, rc, wsg_last_error(b->sctx));
   B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
   B_TRY(b, hipStreamSynchronize(st));
@@ -534,7 +537,7 @@ static void fin_push(wsg_batcher* b, FinParts& fp, wsg_frame_desc d, uint64_t sr
 static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinParts& fp,
                            std::vector<std::pair<uint32_t, StageCopy>>& pending) {
   const uint32_t S = b->n;
-  hipStream_t st = ws::ctx_stream(b->ctx);
+  hipStream_t st = ws::ctx_stream(b->sctx);
   const uint64_t F = cur.desc.size();
   std::vector<wsg_session_result> dres(S);
   uint64_t bytes = 16;
@@ -550,12 +553,12 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinPar
   B_TRY(b, b->d_odesc.ensure((F + S + 1) * sizeof(wsg_frame_desc)));
   B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, b->d_tot.ensure(sizeof(uint64_t)));
-  int rc = wsg_aggregate_batch_device(b->ctx, b->stages.max_aggregated_len, (const wsg_frame_desc*)b->d_desc.p, F,
+  int rc = wsg_aggregate_batch_device(b->sctx, b->stages.max_aggregated_len, (const wsg_frame_desc*)b->d_desc.p, F,
                                       (const uint32_t*)b->d_sf.p, S, (const wsg_session_result*)b->d_res.p,
                                       b->sarena.p, used, (wsg_agg_state*)b->d_astate.p, b->sarena.p + A0, cap,
                                       (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
                                       (uint64_t*)b->d_tot.p);
-  if (rc) return bset(b, rc, wsg_last_error(b->ctx));
+  if (rc) return bset(b, rc, wsg_last_error(b->sctx));
   B_TRY(b, b->h_odesc.ensure((F + S + 1) * sizeof(wsg_frame_desc)));
   B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, b->h_astate.ensure((S + 1) * sizeof(wsg_agg_state)));
@@ -607,7 +610,7 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinPar
 // device, then one gather and one download of what the handler receives.
 static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
   const uint32_t S = b->n;
-  hipStream_t st = ws::ctx_stream(b->ctx);
+  hipStream_t st = ws::ctx_stream(b->sctx);
   b->fres.assign(res, res + S);
   const uint32_t* sf = (const uint32_t*)f.sf.p;
   const wsg_frame_desc* desc = (const wsg_frame_desc*)f.desc.p;
@@ -625,6 +628,7 @@ static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* re
   }
   cur.sf[S] = (uint32_t)cur.desc.size();
   uint64_t used = al16(f.pcap);
+  if (f.pcap) B_TRY(b, hipStreamWaitEvent(st, f.dpay_done, 0));
   int rc;
   if (b->stages.inflate) {
     if ((rc = stage_inflate(b, f, cur, used))) return rc;
@@ -677,7 +681,7 @@ static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* re
 // zero session sid's device-resident stage carry (a fresh inflater, validator and
 // aggregator), in stream order
 static int stage_reset_dev(wsg_batcher* b, uint32_t sid) {
-  hipStream_t st = ws::ctx_stream(b->ctx);
+  hipStream_t st = ws::ctx_stream(b->sctx);
   B_TRY(b, hipMemsetAsync(b->d_istate.p + (uint64_t)sid * sizeof(wsg_inflate_state), 0, sizeof(wsg_inflate_state), st));
   B_TRY(b, hipMemsetAsync(b->d_iwin.p + (uint64_t)sid * WSG_INFLATE_WINDOW, 0, WSG_INFLATE_WINDOW, st));
   B_TRY(b, hipMemsetAsync(b->d_vstate.p + (uint64_t)sid * sizeof(wsg_session_state), 0, sizeof(wsg_session_state), st));
@@ -714,6 +718,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     for (PinnedBuf* p : bufs) p->release();
     f.dpay.release();
     if (f.done) (void)hipEventDestroy(f.done);
+    if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
   }
   b->st.release();
   DBuf* dbufs[] = {&b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->sarena, &b->d_sf, &b->d_desc,
@@ -721,6 +726,7 @@ int wsg_batcher_close(wsg_batcher* b) {
   for (DBuf* d : dbufs) d->release();
   PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot, &b->fin_pay};
   for (PinnedBuf* p : hbufs) p->release();
+  if (b->sctx) (void)wsg_close(b->sctx);
   delete b;
   return WSG_API_OK;
 }
@@ -986,9 +992,11 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
   if (rc) return bset(b, rc, wsg_last_error(b->ctx));
   f.pcap = 0;
   if (b->has_stages && F) {
+    if (!f.dpay_done) B_TRY(b, hipEventCreateWithFlags(&f.dpay_done, hipEventDisableTiming));
     B_TRY(b, f.dpay.ensure(pcap));
     B_TRY(b, hipMemcpyAsync(f.dpay.p, ws::ctx_async_payload(b->ctx), pcap, hipMemcpyDeviceToDevice,
                             ws::ctx_stream(b->ctx)));
+    B_TRY(b, hipEventRecord(f.dpay_done, ws::ctx_stream(b->ctx)));
     f.pcap = pcap;
   }
   B_TRY(b, ws::ctx_record_out(b->ctx, f.done));
@@ -1102,7 +1110,11 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
   const uint32_t S = b->n;
   b->ss.assign(S, StageSess{});
   if (b->has_stages) {  // the device-resident stage carry, zeroed (fresh stage decoders)
-    hipStream_t st = ws::ctx_stream(b->ctx);
+    if (!b->sctx) {
+      const int rc = wsg_open(ws::ctx_device(b->ctx), nullptr, &b->sctx);
+      if (rc) return bset(b, rc, "wsg_open (stage context)");
+    }
+    hipStream_t st = ws::ctx_stream(b->sctx);
     B_TRY(b, b->d_istate.ensure(((uint64_t)S + 1) * sizeof(wsg_inflate_state)));
     B_TRY(b, b->d_iwin.ensure(((uint64_t)S + 1) * WSG_INFLATE_WINDOW));
     B_TRY(b, b->d_vstate.ensure(((uint64_t)S + 1) * sizeof(wsg_session_state)));

@@ -219,6 +219,7 @@ hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e);
 // the context's kernel stream, and the device payload of its last async batch (valid
 // in stream order until a later batch reuses that staging slot)
 hipStream_t ctx_stream(wsg_ctx* c);
+int ctx_device(wsg_ctx* c);
 uint8_t* ctx_async_payload(wsg_ctx* c);
 
 void launch_parse(const DecodeArgs& a, hipStream_t s);
