@@ -234,6 +234,20 @@ __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ 
   for (uint32_t i = done + t; i < c.len; i += 256) d[i] = s[i];
 }
 
+// Fresh stage decoders for the sessions in sids[0..n): one workgroup per session zeroes
+// its inflater state and window, validator context and aggregator state.
+__global__ __launch_bounds__(256) void k_stage_reset(const uint32_t* __restrict__ sids, wsg_inflate_state* istate,
+                                                     uint8_t* iwin, wsg_session_state* vstate, wsg_agg_state* astate) {
+  const uint32_t sid = sids[blockIdx.x];
+  ws_u32x4* w = (ws_u32x4*)(iwin + (uint64_t)sid * WSG_INFLATE_WINDOW);
+  for (uint32_t i = threadIdx.x; i < WSG_INFLATE_WINDOW / 16; i += 256) w[i] = (ws_u32x4){0u, 0u, 0u, 0u};
+  if (threadIdx.x == 0) {
+    istate[sid] = wsg_inflate_state{};
+    vstate[sid] = wsg_session_state{};
+    astate[sid] = wsg_agg_state{};
+  }
+}
+
 }  // namespace
 
 // The decoders after "ws-decoder" that run in the same flush (wsg_batcher_set_stages):
@@ -300,6 +314,9 @@ struct wsg_batcher {
   wsg_ctx* sctx = nullptr;  // the stages' own context (stream + workspace): a flush's stages run
                             // beside the next flush's upload and decode on the batcher's context
   std::vector<StageSess> ss;
+  std::vector<uint8_t> stage_closed;    // failed by a stage: its later decoded frames go nowhere
+  std::vector<uint32_t> stage_resets;   // sessions whose device stage carry is zeroed before the next run
+  DBuf d_resets;
   DBuf d_istate, d_iwin, d_vstate, d_astate;  // per-session stage carry (device-resident)
   DBuf sarena;    // a flush's stage bytes: decoded payloads | held frames | inflated | aggregated
   DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot, d_copy, d_fin;
@@ -326,6 +343,7 @@ static inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 
 // a later stage failed session s: its result, and the session is closed
 static void stage_fail(wsg_batcher* b, uint32_t s, const wsg_session_result& r) {
+  b->stage_closed[s] = 1;
   b->fres[s].error = r.error;
   b->fres[s].close_code = r.close_code;
   b->fres[s].detail = r.detail;
@@ -612,6 +630,18 @@ static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* re
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
   b->fres.assign(res, res + S);
+  if (!b->stage_resets.empty()) {  // sessions handed to new sessions since the last run
+    B_TRY(b, upload(b->d_resets, b->stage_resets, st));
+    hipLaunchKernelGGL(k_stage_reset, dim3((uint32_t)b->stage_resets.size()), dim3(256), 0, st,
+                       (const uint32_t*)b->d_resets.p, (wsg_inflate_state*)b->d_istate.p, b->d_iwin.p,
+                       (wsg_session_state*)b->d_vstate.p, (wsg_agg_state*)b->d_astate.p);
+    B_TRY(b, hipGetLastError());
+    b->stage_resets.clear();
+  }
+  // a session a stage failed in an earlier flush is closed (InternalSession.controlClose):
+  // the frames decoded for it in flushes already in flight reach no stage and no handler
+  for (uint32_t s = 0; s < S; ++s)
+    if (b->stage_closed[s]) b->fres[s] = wsg_session_result{};
   const uint32_t* sf = (const uint32_t*)f.sf.p;
   const wsg_frame_desc* desc = (const wsg_frame_desc*)f.desc.p;
   StageList cur;
@@ -619,12 +649,13 @@ static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* re
   cur.n_ok.assign(S, 0);
   for (uint32_t s = 0; s < S; ++s) {
     cur.sf[s] = (uint32_t)cur.desc.size();
-    for (uint32_t k = sf[s]; k < sf[s] + res[s].n_delivered; ++k) {
+    const uint32_t nd = b->stage_closed[s] ? 0u : res[s].n_delivered;
+    for (uint32_t k = sf[s]; k < sf[s] + nd; ++k) {
       wsg_frame_desc d = desc[k];
       d.flags &= 0xf0u | 0x80u;  // FIN, RSV (the "was masked" bit is the decoder's)
       cur.desc.push_back(d);
     }
-    cur.n_ok[s] = res[s].n_delivered;
+    cur.n_ok[s] = nd;
   }
   cur.sf[S] = (uint32_t)cur.desc.size();
   uint64_t used = al16(f.pcap);
@@ -678,16 +709,6 @@ static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* re
   return WSG_API_OK;
 }
 
-// zero session sid's device-resident stage carry (a fresh inflater, validator and
-// aggregator), in stream order
-static int stage_reset_dev(wsg_batcher* b, uint32_t sid) {
-  hipStream_t st = ws::ctx_stream(b->sctx);
-  B_TRY(b, hipMemsetAsync(b->d_istate.p + (uint64_t)sid * sizeof(wsg_inflate_state), 0, sizeof(wsg_inflate_state), st));
-  B_TRY(b, hipMemsetAsync(b->d_iwin.p + (uint64_t)sid * WSG_INFLATE_WINDOW, 0, WSG_INFLATE_WINDOW, st));
-  B_TRY(b, hipMemsetAsync(b->d_vstate.p + (uint64_t)sid * sizeof(wsg_session_state), 0, sizeof(wsg_session_state), st));
-  B_TRY(b, hipMemsetAsync(b->d_astate.p + (uint64_t)sid * sizeof(wsg_agg_state), 0, sizeof(wsg_agg_state), st));
-  return WSG_API_OK;
-}
 
 extern "C" {
 
@@ -721,7 +742,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
   }
   b->st.release();
-  DBuf* dbufs[] = {&b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->sarena, &b->d_sf, &b->d_desc,
+  DBuf* dbufs[] = {&b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->sarena, &b->d_sf, &b->d_desc,
                    &b->d_odesc, &b->d_res, &b->d_ores, &b->d_rf, &b->d_ooff, &b->d_tot, &b->d_copy, &b->d_fin};
   for (DBuf* d : dbufs) d->release();
   PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot, &b->fin_pay};
@@ -1109,6 +1130,8 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
   b->cfg.validate_utf8 = stages->inflate ? 0 : (stages->validate ? 1 : 0);
   const uint32_t S = b->n;
   b->ss.assign(S, StageSess{});
+  b->stage_closed.assign(S, 0);
+  b->stage_resets.clear();
   if (b->has_stages) {  // the device-resident stage carry, zeroed (fresh stage decoders)
     if (!b->sctx) {
       const int rc = wsg_open(ws::ctx_device(b->ctx), nullptr, &b->sctx);
@@ -1149,10 +1172,10 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
   b->state[sid] = wsg_session_state{};
   for (int slot : b->q) b->fs[slot].resets.push_back(sid);  // the old session's results in flight are dropped
   b->patch.push_back({sid, 0});
-  if (b->has_stages) {  // fresh stage decoders too
+  if (b->has_stages) {  // fresh stage decoders too (the device carry is zeroed before the next stage run)
     b->ss[sid] = StageSess{};
-    const int rc = stage_reset_dev(b, sid);
-    if (rc) return rc;
+    b->stage_closed[sid] = 0;
+    b->stage_resets.push_back(sid);
   }
   return WSG_API_OK;
 }

@@ -135,3 +135,58 @@ def test_batcher_stage_chain_matches_oracle(ctx, oracle, seed, no_context, aggre
         n_err += eerr is not None
     assert n_err  # the generator produced failures of some kind
     b.close()
+
+
+@pytest.mark.parametrize("seed,aggregate", [(10, True), (11, False)])
+def test_batcher_stage_chain_pipelined(ctx, oracle, seed, aggregate):
+    """The same chain with two flushes in flight (wsg_batcher_flush_async / wait): a
+    session a stage fails in one flush gets nothing from the flush already in flight
+    behind it (the session is closed), and a reset slot starts from fresh stage decoders."""
+    from snf4j_amd import NativeBatcher
+    rng = np.random.default_rng(6200 + seed)
+    n = 40
+    streams = []
+    for s in range(n):
+        msgs = _messages(rng, int(rng.integers(4, 16)), False, bad_utf8=0.15)
+        streams.append(b"".join(wsgen.build_frame(op, fin, rsv, p, True, tuple(int(x) for x in rng.integers(0, 256, 4)))
+                                for (op, fin, rsv, p) in msgs))
+    b = NativeBatcher(n, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=ctx)
+    b.set_stages(inflate=True, noContext=False, validate=True, aggregate=aggregate, maxAggregatedLength=1 << 20)
+    for rnd in range(2):  # round 1: every slot reset, the same streams again from fresh sessions
+        if rnd:
+            for s in range(n):
+                b.reset_session(s)
+        got = [[] for _ in range(n)]
+        err = [None] * n
+        pos = [0] * n
+        pending = 0
+
+        def collect():
+            for s, (fr, e) in enumerate(b.wait()):
+                got[s] += fr
+                if e is not None:
+                    assert err[s] is None, s
+                    err[s] = (e.getMessage(), e.close_code)
+
+        while any(pos[s] < len(streams[s]) for s in range(n)):
+            for s in range(n):
+                if pos[s] < len(streams[s]):
+                    c = int(rng.integers(1, 1500))
+                    b.feed(s, streams[s][pos[s]:pos[s] + c])
+                    pos[s] += c
+            if pending == 2:
+                collect()
+                pending -= 1
+            b.flush_async()
+            pending += 1
+        while pending:
+            collect()
+            pending -= 1
+        n_err = 0
+        for s in range(n):
+            exp, eerr = _oracle_chain(oracle, streams[s], False, True, aggregate, 1 << 20)
+            assert err[s] == eerr, (rnd, s, err[s], eerr)
+            assert [(int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload()) for f in got[s]] == exp, (rnd, s)
+            n_err += eerr is not None
+        assert n_err
+    b.close()
