@@ -169,6 +169,9 @@ int wsg_close(wsg_ctx* ctx);
  *   WSG_TUNE_INFLATE_LDS     0: the lane pre-decode keeps its tables in HBM
  *   WSG_TUNE_INFLATE_ORDER   0: lanes take frames in batch order (not longest first)
  *   WSG_TUNE_INFLATE_LANES   k_infl_tok lanes at most (multiple of 64)
+ *   WSG_TUNE_INFLATE_TABS    HBM table blocks (3,880 B each) for the lanes whose message needs the
+ *                            HBM-table decoder (default 32768; beyond, such messages take the
+ *                            serial decoder)
  *   WSG_TUNE_FUSED_SCAN      0: always launch k_scan (k_link does not fold block aggregates)
  *   WSG_TUNE_AGG_UNITS       aggregator gather units per wave: 1, 2 (default) or 4
  *   WSG_TUNE_AGG_GRID        aggregator gather waves at most (default 65536) */
@@ -180,7 +183,8 @@ enum {
     WSG_TUNE_INFLATE_LANES = 5,
     WSG_TUNE_FUSED_SCAN = 6,
     WSG_TUNE_AGG_UNITS = 7,
-    WSG_TUNE_AGG_GRID = 8
+    WSG_TUNE_AGG_GRID = 8,
+    WSG_TUNE_INFLATE_TABS = 9
 };
 int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */
@@ -191,6 +195,10 @@ int wsg_get_stream(wsg_ctx* ctx, void** stream);
 const char* wsg_last_error(wsg_ctx* ctx);
 /* Pre-size device workspace so later batch calls do no allocation (graph-capture safe). */
 int wsg_reserve(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len);
+/* The same for permessage-deflate batches (wsg_inflate_batch_*): frames, sessions and
+ * compressed payload bytes of the largest batch.  Kept apart from wsg_reserve because
+ * the inflate workspace is ~7 B per compressed byte (token and literal regions). */
+int wsg_reserve_inflate(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions, uint64_t max_payload_len);
 int wsg_sync(wsg_ctx* ctx);
 
 /* Kernel timing (hipEvents recorded around each kernel on the ctx stream).

@@ -121,6 +121,7 @@ def _load():
         "wsg_get_stream": ([p, P(p)], i32),
         "wsg_last_error": ([p], C.c_char_p),
         "wsg_reserve": ([p, u64, u32, u64], i32),
+        "wsg_reserve_inflate": ([p, u64, u32, u64], i32),
         "wsg_sync": ([p], i32),
         "wsg_set_timing": ([p, i32], i32),
         "wsg_set_timing_every": ([p, u32], i32),

@@ -66,10 +66,11 @@ struct wsg_ctx {
   // aggregate workspace
   DevBuf a_code, a_last, a_pl, a_cl, a_blk, a_sess_err, a_pieces;
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
-  DevBuf i_tok, i_lit, i_stat, i_tab, i_fast, i_ord;  // inflate pre-decode workspace
+  DevBuf i_tok, i_lit, i_stat, i_tab, i_tabcnt, i_fast, i_ord;  // inflate pre-decode workspace
   // measurement / test switches (wsg_set_tuning; the defaults are the product)
   int infl_tokens = 1;               // WSG_TUNE_INFLATE_TOKENS 0: no lane pre-decode (serial decoder only)
   uint32_t infl_lanes = 262144;      // WSG_TUNE_INFLATE_LANES: k_infl_tok lanes at most
+  uint32_t infl_tabs = 32768;        // HBM table blocks for the lanes that need them (WSG_TUNE_INFLATE_TABS)
   int infl_fast = 1;                 // WSG_TUNE_INFLATE_FAST 0: no parallel token replay; 2: it alone (tests)
   int infl_lds = 1;                  // WSG_TUNE_INFLATE_LDS 0: the pre-decode keeps its tables in HBM
   int infl_order = 1;                // WSG_TUNE_INFLATE_ORDER 0: lanes take frames in batch order
@@ -210,7 +211,7 @@ int wsg_close(wsg_ctx* c) {
   for (DevBuf* b : bufs) b->release();
   DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,
                      &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc, &c->i_tok, &c->i_lit,
-                     &c->i_stat, &c->i_tab, &c->i_fast, &c->i_ord};
+                     &c->i_stat, &c->i_tab, &c->i_tabcnt, &c->i_fast, &c->i_ord};
   for (DevBuf* b : abufs) b->release();
   for (HostSlot& hs : c->slot) {
     DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
@@ -234,6 +235,7 @@ int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
     case WSG_TUNE_INFLATE_LDS: c->infl_lds = value != 0; break;
     case WSG_TUNE_INFLATE_ORDER: c->infl_order = value != 0; break;
     case WSG_TUNE_INFLATE_LANES: c->infl_lanes = value < 64 ? 64u : (uint32_t)value & ~63u; break;
+    case WSG_TUNE_INFLATE_TABS: c->infl_tabs = value < 0 ? 0u : (value > (1 << 22) ? (1u << 22) : (uint32_t)value); break;
     case WSG_TUNE_FUSED_SCAN: c->fused_scan = value != 0; break;
     case WSG_TUNE_AGG_UNITS:
       if (value != 1 && value != 2 && value != 4) return set_err(c, WSG_API_EINVAL, "AGG_UNITS is 1, 2 or 4");
@@ -330,6 +332,27 @@ static int ensure_encode_ws(wsg_ctx* c, uint64_t n_frames) {
   HIP_TRY(c, c->blk_sum.ensure(nblk * sizeof(uint64_t)));
   HIP_TRY(c, c->blk_max.ensure(3 * nblk * sizeof(int32_t)));
   return WSG_API_OK;
+}
+
+// the lane pre-decode's workspace for a batch of n_frames frames and payload_len
+// compressed bytes (grow-only, so a batch within a reservation allocates nothing)
+static int ensure_inflate_ws(wsg_ctx* c, uint64_t n_frames, uint64_t payload_len) {
+  const uint64_t lanes = n_frames < c->infl_lanes ? ((n_frames + 63) / 64) * 64 : c->infl_lanes;
+  const uint64_t n_tab = lanes < c->infl_tabs ? lanes : c->infl_tabs;
+  HIP_TRY(c, c->i_tok.ensure(infl_tok_words(payload_len, n_frames) * 4));
+  HIP_TRY(c, c->i_lit.ensure(infl_lit_bytes(payload_len, n_frames)));
+  HIP_TRY(c, c->i_stat.ensure(n_frames * sizeof(InflTokStat)));
+  HIP_TRY(c, c->i_tab.ensure(n_tab * infl_tab_bytes()));
+  HIP_TRY(c, c->i_tabcnt.ensure(sizeof(uint32_t)));
+  if (c->infl_order) HIP_TRY(c, c->i_ord.ensure(infl_ord_words(n_frames) * 4));
+  return WSG_API_OK;
+}
+
+int wsg_reserve_inflate(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t max_payload_len) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, c->i_fast.ensure(max_sessions ? max_sessions : 1));
+  return ensure_inflate_ws(c, max_frames, max_payload_len);
 }
 
 int wsg_reserve(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len) {
@@ -904,6 +927,8 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   a.lit_len = 0;
   a.tstat = nullptr;
   a.tab = nullptr;
+  a.n_tab = 0;
+  a.tab_cnt = nullptr;
   a.n_lanes = 0;
   a.fast_done = nullptr;
   a.order = nullptr;
@@ -912,26 +937,27 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   if (c->infl_tokens && n_frames) {
     const uint32_t lanes = (uint32_t)(n_frames < c->infl_lanes ? ((n_frames + 63) / 64) * 64 : c->infl_lanes);
     const uint64_t lit_len = infl_lit_bytes(payload_len, n_frames);
-    HIP_TRY(c, c->i_tok.ensure(infl_tok_words(payload_len, n_frames) * 4));
-    HIP_TRY(c, c->i_lit.ensure(lit_len));
-    HIP_TRY(c, c->i_stat.ensure(n_frames * sizeof(InflTokStat)));
-    HIP_TRY(c, c->i_tab.ensure((uint64_t)lanes * infl_tab_bytes()));
+    const int rc = ensure_inflate_ws(c, n_frames, payload_len);
+    if (rc) return rc;
+    const uint32_t n_tab = lanes < c->infl_tabs ? lanes : c->infl_tabs;
+    HIP_TRY(c, hipMemsetAsync(c->i_tabcnt.p, 0, sizeof(uint32_t), c->stream));
     a.tok = (uint32_t*)c->i_tok.p;
     a.lit = (uint8_t*)c->i_lit.p;
     a.lit_len = lit_len;
     a.tstat = (InflTokStat*)c->i_stat.p;
     a.tab = (uint8_t*)c->i_tab.p;
+    a.n_tab = n_tab;
+    a.tab_cnt = (uint32_t*)c->i_tabcnt.p;
     a.n_lanes = lanes;
     a.order = nullptr;
     a.ord_cnt = nullptr;
     if (c->infl_order) {
-      HIP_TRY(c, c->i_ord.ensure(infl_ord_words(n_frames) * 4));
       a.order = (uint32_t*)c->i_ord.p;
       a.ord_cnt = a.order + n_frames;
     }
     timed(c, K_INFL_TOK, [&] { launch_infl_tok(a, c->stream); });
     if (c->infl_fast) {
-      HIP_TRY(c, c->i_fast.ensure(n_sessions));
+      HIP_TRY(c, c->i_fast.ensure(n_sessions));  // (sessions: not covered by wsg_reserve_inflate)
       a.fast_done = (uint8_t*)c->i_fast.p;
       timed(c, K_INFL_FAST, [&] { launch_infl_fast(a, c->stream); });
     }

@@ -1290,7 +1290,7 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
 #else
 #define PF_PTR nullptr
 #endif
-  LaneTab* const T = reinterpret_cast<LaneTab*>(a.tab) + lane_id;
+  LaneTab* T = nullptr;  // the lane's HBM tables, taken from the pool when first needed
   for (uint64_t i = lane_id; i < a.n_frames; i += a.n_lanes) {
     const uint64_t k = a.order ? a.order[i] : i;
     const wsg_frame_desc d = a.desc[k];
@@ -1334,10 +1334,20 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
       TPROF_ACC(0, t_msg);
       TPROF_CNT(6, 1);
       TPROF_CNT(7, st == Q_BAIL);
-      if (st == Q_BAIL) tok_message<false>(a, T, ents, k, kend, in_len, PF_PTR);
-    } else {
-      tok_message<true>(a, T, ents, k, kend, in_len, PF_PTR);
+      if (st != Q_BAIL) continue;
     }
+    if (!T) {
+      const uint32_t slot = atomicAdd(a.tab_cnt, 1u);
+      if (slot < a.n_tab) T = reinterpret_cast<LaneTab*>(a.tab) + slot;
+    }
+    if (!T) {  // no table block left: the serial decoder takes the message
+      a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
+      continue;
+    }
+    if (kend == k)
+      tok_message<false>(a, T, ents, k, kend, in_len, PF_PTR);
+    else
+      tok_message<true>(a, T, ents, k, kend, in_len, PF_PTR);
   }
 #ifdef WSG_INFLATE_TOK_PROF
   for (int i = 0; i < 8; ++i) atomicAdd(&g_tok_prof[i], (unsigned long long)pf_[i]);

@@ -192,7 +192,9 @@ struct InflArgs {
   uint8_t* lit;               // literal regions (per frame: 3 payload_off + 80 k bytes, 4-B aligned)
   uint64_t lit_len;           // bytes allocated at lit
   struct InflTokStat* tstat;  // [n_frames]
-  uint8_t* tab;               // n_lanes per-lane table blocks
+  uint8_t* tab;               // n_tab table blocks for the lanes that take the HBM-table decoder
+  uint32_t n_tab;             //   (a lane takes one when it first needs it, from *tab_cnt;
+  uint32_t* tab_cnt;          //   with none left its message goes to the serial decoder)
   uint32_t n_lanes;
   uint8_t* fast_done;         // [n_sessions]: k_infl_fast finished the session (k_inflate skips it)
   int tok_lds;                // k_infl_tok decodes single-frame messages from LDS tables (else HBM tables)

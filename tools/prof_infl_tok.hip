@@ -64,6 +64,9 @@ int main(int argc, char** argv) {
   a.desc = d_desc; a.n_frames = n; a.session_first = d_sf; a.n_sessions = (uint32_t)ns;
   a.payload = d_pl; a.payload_len = pl;
   a.tok = d_tok; a.lit = d_lit; a.lit_len = ws::infl_lit_bytes(pl, n); a.tstat = d_stat; a.tab = d_tab; a.n_lanes = lanes;
+  a.n_tab = lanes;  // (a block per lane: d_tab holds lanes tables)
+  CK(hipMalloc(&a.tab_cnt, 4));
+  CK(hipMemset(a.tab_cnt, 0, 4));
   a.tok_lds = use_lds;
   if (use_order) {
     CK(hipMalloc(&a.order, ws::infl_ord_words(n) * 4));
@@ -76,6 +79,7 @@ int main(int argc, char** argv) {
   for (int rep = 0; rep < 3; ++rep) {
     CK(hipMemcpyToSymbol(HIP_SYMBOL(ws::g_tok_prof), z, sizeof(z)));
     CK(hipEventRecord(e0));
+    CK(hipMemsetAsync(a.tab_cnt, 0, 4, 0));
     ws::launch_infl_tok(a, 0);
     CK(hipEventRecord(e1));
     CK(hipDeviceSynchronize());
