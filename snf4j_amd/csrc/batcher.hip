@@ -159,6 +159,7 @@ class Pool {
 struct DBuf {
   uint8_t* p = nullptr;
   size_t n = 0;
+  PinnedBuf up;  // staging of upload() (a DMA from pinned memory, no copy through a runtime bounce buffer)
   hipError_t ensure(size_t bytes) {
     if (bytes <= n && p) return hipSuccess;
     if (p) (void)hipFree(p);
@@ -188,6 +189,7 @@ struct DBuf {
     if (p) (void)hipFree(p);
     p = nullptr;
     n = 0;
+    up.release();
   }
 };
 
@@ -204,9 +206,12 @@ constexpr uint32_t COPY_MAX = 65536;
 // One workgroup per copy.  Output slots are 16-B aligned; a source is 16-B aligned when
 // it is a decoder payload slot, byte-aligned when it is inflated output (messages back
 // to back), so the widest access both sides allow is used.
+constexpr uint32_t GATHER_GROUPS = 128;  // workgroups of the output gather (enough to fill PCIe)
+
 __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                    const StageCopy* __restrict__ cp) {
-  const StageCopy c = cp[blockIdx.x];
+                                                    const StageCopy* __restrict__ cp, uint32_t n) {
+  for (uint32_t ci = blockIdx.x; ci < n; ci += gridDim.x) {
+  const StageCopy c = cp[ci];
   const uint8_t* s = src + c.src;
   uint8_t* d = dst + c.dst;
   const uint32_t t = threadIdx.x;
@@ -232,6 +237,7 @@ __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ 
     }
   }
   for (uint32_t i = done + t; i < c.len; i += 256) d[i] = s[i];
+  }
 }
 
 // Fresh stage decoders for the sessions in sids[0..n): one workgroup per session zeroes
@@ -268,6 +274,23 @@ struct StageList {
   std::vector<uint32_t> n_ok;         // [S] frames of the session that go on (<= its count)
 };
 
+// A flush's output when stages run: what the handler receives, gathered on the device
+// (`copies` move stage-arena bytes to 16-B slots of d_pay; `host_parts` are bytes only
+// the host holds, an aggregated message's bytes from earlier batches) and downloaded
+// on the batcher's download stream, so that the next flush's stages can run meanwhile.
+struct StageOut {
+  std::vector<uint32_t> sf;
+  std::vector<wsg_frame_desc> desc;
+  std::vector<wsg_session_result> res;
+  std::vector<StageCopy> copies;
+  std::vector<std::pair<uint64_t, std::vector<uint8_t>>> host_parts;
+  uint64_t len = 0;
+  PinnedBuf pay;
+  DBuf d_copy;
+  hipEvent_t gathered = nullptr, downloaded = nullptr;
+  bool staged = false;  // computed, download queued (wsg_batcher_wait collects it)
+};
+
 // One flush's pinned staging and results (two alternate: a flush can be in flight
 // while the next one gathers).
 struct HostErr {
@@ -287,6 +310,7 @@ struct FlushSlot {
   DBuf dpay;                              // with stages: the decoded payloads, kept on the device
   uint64_t pcap = 0;                      //   (their region's size)
   hipEvent_t dpay_done = nullptr;         //   after their copy (the stage stream waits for it)
+  StageOut so;                            // the stages' output
   uint64_t F = 0, W = 0;
   std::vector<HostErr> host_err;  // header errors found on the host after this batch's frames
   std::vector<uint32_t> resets;   // slots given to a new session while this batch was in flight
@@ -318,13 +342,12 @@ struct wsg_batcher {
   std::vector<uint32_t> stage_resets;   // sessions whose device stage carry is zeroed before the next run
   DBuf d_resets;
   DBuf d_istate, d_iwin, d_vstate, d_astate;  // per-session stage carry (device-resident)
-  DBuf sarena;    // a flush's stage bytes: decoded payloads | held frames | inflated | aggregated
-  DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot, d_copy, d_fin;
+  DBuf* ar = nullptr;  // the stage arena at hand: its flush's dpay (decoded payloads | held frames |
+                       // inflated | aggregated)
+  DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot;
   PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot;  // stage results downloaded
-  PinnedBuf fin_pay;                    // the flush's output payloads when stages run
-  std::vector<uint32_t> fin_sf;
-  std::vector<wsg_frame_desc> fin_desc;
-  std::vector<wsg_session_result> fres;
+  hipStream_t s_dl = nullptr;           // downloads of stage outputs
+  StageOut* out = nullptr;              // the output the stage run at hand writes
 };
 
 static int bset(wsg_batcher* b, int code, const char* msg) {
@@ -344,17 +367,20 @@ static inline uint64_t al16(uint64_t x) { return (x + 15) & ~15ull; }
 // a later stage failed session s: its result, and the session is closed
 static void stage_fail(wsg_batcher* b, uint32_t s, const wsg_session_result& r) {
   b->stage_closed[s] = 1;
-  b->fres[s].error = r.error;
-  b->fres[s].close_code = r.close_code;
-  b->fres[s].detail = r.detail;
+  b->out->res[s].error = r.error;
+  b->out->res[s].close_code = r.close_code;
+  b->out->res[s].detail = r.detail;
   b->state[s].closed = 1;
 }
 
 template <typename T>
 static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
-  hipError_t e = d.ensure((v.size() + 1) * sizeof(T));
+  const size_t bytes = v.size() * sizeof(T);
+  hipError_t e = d.ensure(bytes + sizeof(T));
+  if (e == hipSuccess) e = d.up.ensure(bytes + sizeof(T));
   if (e != hipSuccess || v.empty()) return e;
-  return hipMemcpyAsync(d.p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice, s);
+  memcpy(d.up.p, v.data(), bytes);
+  return hipMemcpyAsync(d.p, d.up.p, bytes, hipMemcpyHostToDevice, s);
 }
 
 // PerMessageDeflateDecoder over `cur` (PerMessageDeflateDecoder.java:68-105), on the
@@ -364,7 +390,10 @@ static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
 static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t& used) {
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
-  std::vector<std::vector<wsg_frame_desc>> od(S);
+  std::vector<wsg_frame_desc> od;  // the sessions' output frames, a session's contiguous at od_at[s]
+  std::vector<uint64_t> od_at(S, 0);
+  std::vector<uint32_t> od_n(S, 0);
+  bool in_order = true;            // (a session re-run for capacity comes after the others)
   std::vector<uint32_t> todo;
   std::vector<uint64_t> cap(S, 0), held_at(S, 0);
   // the held frames' bytes go after the decoded payloads
@@ -382,12 +411,11 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     todo.push_back(s);
     cap[s] = al16(4096 + 8 * c);
   }
-  B_TRY(b, b->sarena.ensure(hpos + 64));
-  if (f.pcap) B_TRY(b, hipMemcpyAsync(b->sarena.p, f.dpay.p, f.pcap, hipMemcpyDeviceToDevice, st));
+  B_TRY(b, b->ar->grow_keep(hpos + 64, f.pcap, st));
   for (uint32_t s = 0; s < S; ++s) {
     const StageSess& h = b->ss[s];
     if (!h.held_bytes.empty())
-      B_TRY(b, hipMemcpyAsync(b->sarena.p + held_at[s], h.held_bytes.data(), h.held_bytes.size(),
+      B_TRY(b, hipMemcpyAsync(b->ar->p + held_at[s], h.held_bytes.data(), h.held_bytes.size(),
                               hipMemcpyHostToDevice, st));
   }
   uint64_t ipos = al16(hpos);
@@ -421,7 +449,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     }
     x.sf[S] = (uint32_t)x.desc.size();
     const uint64_t F = x.desc.size();
-    B_TRY(b, b->sarena.grow_keep(ipos + oo[S] + 64, ipos, st));
+    B_TRY(b, b->ar->grow_keep(ipos + oo[S] + 64, ipos, st));
     B_TRY(b, upload(b->d_desc, x.desc, st));
     B_TRY(b, upload(b->d_sf, x.sf, st));
     B_TRY(b, upload(b->d_ooff, oo, st));
@@ -429,8 +457,8 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
     B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
     int rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
-                                      (const uint32_t*)b->d_sf.p, S, b->sarena.p, ipos, (wsg_inflate_state*)b->d_istate.p,
-                                      b->d_iwin.p, b->sarena.p + ipos, (const uint64_t*)b->d_ooff.p,
+                                      (const uint32_t*)b->d_sf.p, S, b->ar->p, ipos, (wsg_inflate_state*)b->d_istate.p,
+                                      b->d_iwin.p, b->ar->p + ipos, (const uint64_t*)b->d_ooff.p,
                                       (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
                                       (uint32_t*)b->d_rf.p);
     if (rc) return bset(b, rc, wsg_last_error(b->sctx));
@@ -458,12 +486,14 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
       }
       StageSess& h = b->ss[s];
       uint32_t j = 0;
+      od_at[s] = od.size();
       for (uint32_t k = x.sf[s] + nheld[s]; k < x.sf[s + 1] && j < r[s].n_delivered; ++k, ++j) {
         wsg_frame_desc d = odesc[k];
         if (d.flags & WSG_DESC_INFLATED) d.payload_off += ipos;  // (else the input's arena offset)
         d.flags &= 0xf0u | 0x80u;
-        od[s].push_back(d);
+        od.push_back(d);
       }
+      od_n[s] = j;
       std::vector<wsg_frame_desc> nhd;
       uint64_t nb = 0;
       if (r[s].error) {
@@ -483,21 +513,29 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     }
     for (const Held& c : hd_copies)
       if (c.len)
-        B_TRY(b, hipMemcpyAsync(b->ss[c.s].held_bytes.data() + c.dst, b->sarena.p + c.src, c.len,
+        B_TRY(b, hipMemcpyAsync(b->ss[c.s].held_bytes.data() + c.dst, b->ar->p + c.src, c.len,
                                 hipMemcpyDeviceToHost, st));
     if (!hd_copies.empty()) B_TRY(b, hipStreamSynchronize(st));
     ipos = al16(ipos + oo[S]);
+    if (!retry.empty()) in_order = false;
     todo.swap(retry);
   }
   cur.sf.assign(S + 1, 0);
   cur.n_ok.assign(S, 0);
-  cur.desc.clear();
+  uint64_t k = 0;
   for (uint32_t s = 0; s < S; ++s) {
-    cur.sf[s] = (uint32_t)cur.desc.size();
-    cur.desc.insert(cur.desc.end(), od[s].begin(), od[s].end());
-    cur.n_ok[s] = (uint32_t)od[s].size();
+    cur.sf[s] = (uint32_t)k;
+    cur.n_ok[s] = od_n[s];
+    k += od_n[s];
   }
-  cur.sf[S] = (uint32_t)cur.desc.size();
+  cur.sf[S] = (uint32_t)k;
+  if (in_order) {
+    cur.desc.swap(od);
+  } else {
+    cur.desc.resize(k);
+    for (uint32_t s = 0; s < S; ++s)
+      std::copy(od.begin() + od_at[s], od.begin() + od_at[s] + od_n[s], cur.desc.begin() + cur.sf[s]);
+  }
   used = ipos;
   return WSG_API_OK;
 }
@@ -511,7 +549,7 @@ static int stage_validate(wsg_batcher* b, StageList& cur, uint64_t used) {
   B_TRY(b, upload(b->d_sf, cur.sf, st));
   B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   int rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_desc.p, cur.desc.size(),
-                                     (const uint32_t*)b->d_sf.p, S, b->sarena.p, used,
+                                     (const uint32_t*)b->d_sf.p, S, b->ar->p, used,
                                      (wsg_session_state*)b->d_vstate.p, (wsg_session_result*)b->d_ores.p);
   if (rc) return bset(b, rc, wsg_last_error(b->sctx));
   B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
@@ -525,17 +563,9 @@ static int stage_validate(wsg_batcher* b, StageList& cur, uint64_t used) {
   return WSG_API_OK;
 }
 
-// The flush's output, gathered on the device into one region and downloaded once:
-// `copies` move arena bytes to 16-B slots of it; `host_parts` are bytes only the host
-// holds (an aggregated message's bytes from earlier batches), written after.
-struct FinParts {
-  std::vector<StageCopy> copies;
-  std::vector<std::pair<uint64_t, std::vector<uint8_t>>> host_parts;
-  uint64_t len = 0;
-};
-
-static void fin_push(wsg_batcher* b, FinParts& fp, wsg_frame_desc d, uint64_t src, uint32_t dev_len,
-                     std::vector<uint8_t>* prefix) {
+// append an output frame: dev_len bytes at arena offset src, after `prefix` (host bytes)
+static void fin_push(wsg_batcher* b, wsg_frame_desc d, uint64_t src, uint32_t dev_len, std::vector<uint8_t>* prefix) {
+  StageOut& fp = *b->out;
   const uint64_t pos = fp.len;
   const uint64_t pre = prefix ? prefix->size() : 0;
   d.payload_off = pos;
@@ -546,14 +576,13 @@ static void fin_push(wsg_batcher* b, FinParts& fp, wsg_frame_desc d, uint64_t sr
   }
   if (pre) fp.host_parts.emplace_back(pos, std::move(*prefix));
   fp.len = al16(pos + pre + dev_len);
-  b->fin_desc.push_back(d);
+  fp.desc.push_back(d);
 }
 
 // FrameAggregator over `cur` (FrameAggregator.java:72-104), on the device, straight
 // into the output list: pass-through frames keep their bytes, an aggregated message is
 // its held bytes (earlier batches, PayloadAggregator.java:34) + this batch's.
-static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinParts& fp,
-                           std::vector<std::pair<uint32_t, StageCopy>>& pending) {
+static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
   const uint64_t F = cur.desc.size();
@@ -564,7 +593,7 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinPar
     for (uint32_t k = cur.sf[s]; k < cur.sf[s] + cur.n_ok[s]; ++k) bytes += cur.desc[k].payload_len;
   }
   const uint64_t A0 = al16(used), cap = al16(bytes);
-  B_TRY(b, b->sarena.grow_keep(A0 + cap + 64, used, st));
+  B_TRY(b, b->ar->grow_keep(A0 + cap + 64, used, st));
   B_TRY(b, upload(b->d_desc, cur.desc, st));
   B_TRY(b, upload(b->d_sf, cur.sf, st));
   B_TRY(b, upload(b->d_res, dres, st));
@@ -573,7 +602,7 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinPar
   B_TRY(b, b->d_tot.ensure(sizeof(uint64_t)));
   int rc = wsg_aggregate_batch_device(b->sctx, b->stages.max_aggregated_len, (const wsg_frame_desc*)b->d_desc.p, F,
                                       (const uint32_t*)b->d_sf.p, S, (const wsg_session_result*)b->d_res.p,
-                                      b->sarena.p, used, (wsg_agg_state*)b->d_astate.p, b->sarena.p + A0, cap,
+                                      b->ar->p, used, (wsg_agg_state*)b->d_astate.p, b->ar->p + A0, cap,
                                       (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
                                       (uint64_t*)b->d_tot.p);
   if (rc) return bset(b, rc, wsg_last_error(b->sctx));
@@ -587,8 +616,9 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinPar
   const wsg_frame_desc* odesc = (const wsg_frame_desc*)b->h_odesc.p;
   const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
   const wsg_agg_state* ast = (const wsg_agg_state*)b->h_astate.p;
+  std::vector<std::pair<uint32_t, StageCopy>> pending;
   for (uint32_t s = 0; s < S; ++s) {
-    b->fin_sf[s] = (uint32_t)b->fin_desc.size();
+    b->out->sf[s] = (uint32_t)b->out->desc.size();
     StageSess& h = b->ss[s];
     const uint64_t base = (uint64_t)cur.sf[s] + s;
     for (uint32_t i = 0; i < r[s].n_delivered; ++i) {
@@ -599,13 +629,13 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinPar
         h.agg_held.clear();
         h.agg_held_valid = false;
         d.flags = (uint8_t)((d.flags & 0xf0u) | 0x80u | WSG_OUT_AGGREGATED);
-        fin_push(b, fp, d, A0 + d.payload_off, d.payload_len, &pre);
+        fin_push(b, d, A0 + d.payload_off, d.payload_len, &pre);
       } else {
         d.flags &= 0xf0u | 0x80u;
-        fin_push(b, fp, d, d.payload_off, d.payload_len, nullptr);
+        fin_push(b, d, d.payload_off, d.payload_len, nullptr);
       }
     }
-    b->fres[s].n_delivered = (uint32_t)b->fin_desc.size() - b->fin_sf[s];
+    b->out->res[s].n_delivered = (uint32_t)b->out->desc.size() - b->out->sf[s];
     if (r[s].error) {
       stage_fail(b, s, r[s]);
       h.agg_held.clear();
@@ -620,28 +650,52 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used, FinPar
       h.agg_held_valid = false;
     }
   }
+  // the held bytes are needed before the next flush's stages run: fetched now
+  if (!pending.empty()) {
+    std::vector<std::vector<uint8_t>> pend_bytes(pending.size());
+    for (size_t i = 0; i < pending.size(); ++i) {
+      pend_bytes[i].resize(pending[i].second.len);
+      B_TRY(b, hipMemcpyAsync(pend_bytes[i].data(), b->ar->p + pending[i].second.src, pending[i].second.len,
+                              hipMemcpyDeviceToHost, st));
+    }
+    B_TRY(b, hipStreamSynchronize(st));
+    for (size_t i = 0; i < pending.size(); ++i) {
+      std::vector<uint8_t>& held = b->ss[pending[i].first].agg_held;
+      held.insert(held.end(), pend_bytes[i].begin(), pend_bytes[i].end());
+    }
+  }
   return WSG_API_OK;
 }
 
-// The stage chain over a waited flush: the decoder's delivered frames (their payloads
-// still on the device, f.dpay) through inflate -> validator -> aggregator on the
-// device, then one gather and one download of what the handler receives.
-static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
+// The stage chain over a flush whose decode is done: the decoder's delivered frames
+// (their payloads still on the device, f.dpay) through inflate -> validator ->
+// aggregator on the device, then one gather, and the download of what the handler
+// receives queued on the download stream (collected by stage_finish).
+static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
-  b->fres.assign(res, res + S);
+  StageOut& o = f.so;
+  b->out = &o;
+  b->ar = &f.dpay;
+  o.res.assign(res, res + S);
+  o.sf.assign(S + 1, 0);
+  o.desc.clear();
+  o.copies.clear();
+  o.host_parts.clear();
+  o.len = 0;
   if (!b->stage_resets.empty()) {  // sessions handed to new sessions since the last run
     B_TRY(b, upload(b->d_resets, b->stage_resets, st));
     hipLaunchKernelGGL(k_stage_reset, dim3((uint32_t)b->stage_resets.size()), dim3(256), 0, st,
                        (const uint32_t*)b->d_resets.p, (wsg_inflate_state*)b->d_istate.p, b->d_iwin.p,
                        (wsg_session_state*)b->d_vstate.p, (wsg_agg_state*)b->d_astate.p);
     B_TRY(b, hipGetLastError());
+    B_TRY(b, hipStreamSynchronize(st));  // (d_resets is reused)
     b->stage_resets.clear();
   }
   // a session a stage failed in an earlier flush is closed (InternalSession.controlClose):
   // the frames decoded for it in flushes already in flight reach no stage and no handler
   for (uint32_t s = 0; s < S; ++s)
-    if (b->stage_closed[s]) b->fres[s] = wsg_session_result{};
+    if (b->stage_closed[s]) o.res[s] = wsg_session_result{};
   const uint32_t* sf = (const uint32_t*)f.sf.p;
   const wsg_frame_desc* desc = (const wsg_frame_desc*)f.desc.p;
   StageList cur;
@@ -665,50 +719,53 @@ static int run_stages(wsg_batcher* b, FlushSlot& f, const wsg_session_result* re
     if ((rc = stage_inflate(b, f, cur, used))) return rc;
     if (b->stages.validate && (rc = stage_validate(b, cur, used))) return rc;
   } else {
-    B_TRY(b, b->sarena.ensure(used + 64));
-    if (f.pcap) B_TRY(b, hipMemcpyAsync(b->sarena.p, f.dpay.p, f.pcap, hipMemcpyDeviceToDevice, st));
+    B_TRY(b, b->ar->grow_keep(used + 64, f.pcap, st));
   }
-  FinParts fp;
-  std::vector<std::pair<uint32_t, StageCopy>> pending;
-  b->fin_sf.assign(S + 1, 0);
-  b->fin_desc.clear();
   if (b->stages.aggregate) {
-    if ((rc = stage_aggregate(b, cur, used, fp, pending))) return rc;
+    if ((rc = stage_aggregate(b, cur, used))) return rc;
   } else {
     for (uint32_t s = 0; s < S; ++s) {
-      b->fin_sf[s] = (uint32_t)b->fin_desc.size();
+      o.sf[s] = (uint32_t)o.desc.size();
       for (uint32_t k = cur.sf[s]; k < cur.sf[s] + cur.n_ok[s]; ++k)
-        fin_push(b, fp, cur.desc[k], cur.desc[k].payload_off, cur.desc[k].payload_len, nullptr);
-      b->fres[s].n_delivered = cur.n_ok[s];
+        fin_push(b, cur.desc[k], cur.desc[k].payload_off, cur.desc[k].payload_len, nullptr);
+      o.res[s].n_delivered = cur.n_ok[s];
     }
   }
-  b->fin_sf[S] = (uint32_t)b->fin_desc.size();
-  // the output: gathered on the device, downloaded once
-  B_TRY(b, b->fin_pay.ensure(fp.len + 16));
-  if (!fp.copies.empty()) {
-    B_TRY(b, upload(b->d_copy, fp.copies, st));
-    B_TRY(b, b->d_fin.ensure(fp.len + 16));
-    hipLaunchKernelGGL(k_stage_copy, dim3((uint32_t)fp.copies.size()), dim3(256), 0, st, b->sarena.p, b->d_fin.p,
-                       (const StageCopy*)b->d_copy.p);
+  o.sf[S] = (uint32_t)o.desc.size();
+  // the output: gathered from this flush's arena straight into the pinned host buffer
+  // by a few workgroups on the download stream (PCIe writes), so the next flush's
+  // stages have the GPU meanwhile (a runtime D2H here is a blit kernel that takes
+  // every CU while it waits on PCIe)
+  if (!o.gathered) B_TRY(b, hipEventCreateWithFlags(&o.gathered, hipEventDisableTiming));
+  if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, hipEventDisableTiming));
+  if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
+  B_TRY(b, o.pay.ensure(o.len + 16));
+  if (!o.copies.empty()) {
+    B_TRY(b, upload(o.d_copy, o.copies, st));
+    B_TRY(b, hipEventRecord(o.gathered, st));
+    B_TRY(b, hipStreamWaitEvent(b->s_dl, o.gathered, 0));
+    uint8_t* dst = nullptr;
+    B_TRY(b, hipHostGetDevicePointer((void**)&dst, o.pay.p, 0));
+    const uint32_t n = (uint32_t)o.copies.size();
+    hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, GATHER_GROUPS)), dim3(256), 0, b->s_dl, b->ar->p,
+                       dst, (const StageCopy*)o.d_copy.p, n);
     B_TRY(b, hipGetLastError());
-    B_TRY(b, hipMemcpyAsync(b->fin_pay.p, b->d_fin.p, fp.len, hipMemcpyDeviceToHost, st));
   }
-  std::vector<std::vector<uint8_t>> pend_bytes(pending.size());
-  for (size_t i = 0; i < pending.size(); ++i) {
-    pend_bytes[i].resize(pending[i].second.len);
-    B_TRY(b, hipMemcpyAsync(pend_bytes[i].data(), b->sarena.p + pending[i].second.src, pending[i].second.len,
-                            hipMemcpyDeviceToHost, st));
-  }
-  B_TRY(b, hipStreamSynchronize(st));
-  for (auto& hp : fp.host_parts)
-    if (!hp.second.empty()) memcpy(b->fin_pay.p + hp.first, hp.second.data(), hp.second.size());
-  for (size_t i = 0; i < pending.size(); ++i) {
-    std::vector<uint8_t>& held = b->ss[pending[i].first].agg_held;
-    held.insert(held.end(), pend_bytes[i].begin(), pend_bytes[i].end());
-  }
+  B_TRY(b, hipEventRecord(o.downloaded, b->s_dl));
+  o.staged = true;
   return WSG_API_OK;
 }
 
+// Wait for a flush's stage output and put in the bytes only the host holds.
+static int stage_finish(wsg_batcher* b, FlushSlot& f) {
+  StageOut& o = f.so;
+  B_TRY(b, hipEventSynchronize(o.downloaded));
+  for (auto& hp : o.host_parts)
+    if (!hp.second.empty()) memcpy(o.pay.p + hp.first, hp.second.data(), hp.second.size());
+  o.host_parts.clear();
+  o.staged = false;
+  return WSG_API_OK;
+}
 
 extern "C" {
 
@@ -734,19 +791,29 @@ int wsg_batcher_open(wsg_ctx* ctx, const wsg_decoder_cfg* cfg, uint32_t n_sessio
 int wsg_batcher_close(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
   (void)wsg_sync(b->ctx);
+  if (b->sctx) (void)wsg_sync(b->sctx);
+  if (b->s_dl) (void)hipStreamSynchronize(b->s_dl);
   for (FlushSlot& f : b->fs) {
     PinnedBuf* bufs[] = {&f.arena, &f.off, &f.sf, &f.payload, &f.desc, &f.result};
     for (PinnedBuf* p : bufs) p->release();
     f.dpay.release();
+    f.so.pay.release();
+    f.so.d_copy.release();
+    if (f.so.gathered) (void)hipEventDestroy(f.so.gathered);
+    if (f.so.downloaded) (void)hipEventDestroy(f.so.downloaded);
     if (f.done) (void)hipEventDestroy(f.done);
     if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
   }
   b->st.release();
-  DBuf* dbufs[] = {&b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->sarena, &b->d_sf, &b->d_desc,
-                   &b->d_odesc, &b->d_res, &b->d_ores, &b->d_rf, &b->d_ooff, &b->d_tot, &b->d_copy, &b->d_fin};
+  DBuf* dbufs[] = {&b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->d_sf, &b->d_desc,
+                   &b->d_odesc, &b->d_res, &b->d_ores, &b->d_rf, &b->d_ooff, &b->d_tot};
   for (DBuf* d : dbufs) d->release();
-  PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot, &b->fin_pay};
+  PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot};
   for (PinnedBuf* p : hbufs) p->release();
+  if (b->s_dl) {
+    (void)hipStreamSynchronize(b->s_dl);
+    (void)hipStreamDestroy(b->s_dl);
+  }
   if (b->sctx) (void)wsg_close(b->sctx);
   delete b;
   return WSG_API_OK;
@@ -1033,6 +1100,22 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
   return WSG_API_OK;
 }
 
+// A flush's decode results as wsg_batcher_wait hands them on: slots reset since are
+// empty, host-detected header errors fill in for sessions the device did not fail.
+static void adjusted_results(wsg_batcher* b, const FlushSlot& g, std::vector<wsg_session_result>& r) {
+  const wsg_session_result* res = (const wsg_session_result*)g.result.p;
+  r.assign(res, res + b->n);
+  for (uint32_t sid : g.resets) r[sid] = wsg_session_result{};
+  for (const auto& he : g.host_err) {
+    if (std::find(g.resets.begin(), g.resets.end(), he.sid) != g.resets.end()) continue;
+    if (!r[he.sid].error) {
+      r[he.sid].error = (uint16_t)he.err;
+      r[he.sid].close_code = WSG_CLOSE_PROTOCOL_ERROR;
+      r[he.sid].detail = he.d1;
+    }
+  }
+}
+
 int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   if (!b || !out) return WSG_API_EINVAL;
   if (b->q.empty()) return bset(b, WSG_API_ERANGE, "no flush in flight");
@@ -1087,24 +1170,36 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
       x.host_closed = true;
     }
   if (!b->has_stages) return WSG_API_OK;
-  const int rc2 = run_stages(b, f, res);
+  int rc2 = f.so.staged ? WSG_API_OK : stage_compute(b, f, res);
   if (rc2) return rc2;
+  // the next flush's stages, while this one's output downloads (its decode done)
+  if (!b->q.empty()) {
+    FlushSlot& g = b->fs[b->q.front()];
+    if (!g.so.staged && hipEventQuery(g.done) == hipSuccess) {
+      std::vector<wsg_session_result> gres;
+      adjusted_results(b, g, gres);
+      if ((rc2 = stage_compute(b, g, gres.data()))) return rc2;
+    }
+  }
+  if ((rc2 = stage_finish(b, f))) return rc2;
+  StageOut& o = f.so;
+  for (uint32_t sid : f.resets) o.res[sid] = wsg_session_result{};  // (also those reset after its stages ran)
   for (uint32_t i = 0; i < S; ++i) {
-    if (b->fres[i].error != res[i].error) f.detail2[i] = 0;  // (a stage's error has no second argument)
+    if (o.res[i].error != res[i].error) f.detail2[i] = 0;  // (a stage's error has no second argument)
   }
   for (uint32_t i = 0; i < S; ++i)
-    if (b->fres[i].error && !res[i].error) {  // a stage failed it: the session swallows further input
+    if (o.res[i].error && !res[i].error) {  // a stage failed it: the session swallows further input
       b->patch.push_back({i, 1});
       SessIn& x = b->s[i];
       std::vector<uint8_t>().swap(x.buf);
       x.host_err = 0;
       x.host_closed = true;
     }
-  out->n_frames = b->fin_desc.size();
-  out->session_first = b->fin_sf.data();
-  out->desc = b->fin_desc.data();
-  out->payload = b->fin_pay.p;
-  out->result = b->fres.data();
+  out->n_frames = o.desc.size();
+  out->session_first = o.sf.data();
+  out->desc = o.desc.data();
+  out->payload = o.pay.p;
+  out->result = o.res.data();
   return WSG_API_OK;
 }
 

@@ -283,6 +283,35 @@ def test_inflate_fragmented_messages_predecoded(ctx, oracle, no_context):
     _run(ctx, oracle, sessions, no_context, 2, rng)
 
 
+@pytest.mark.parametrize("tabs", [0, 5])
+def test_inflate_table_pool_exhausted(oracle, tabs):
+    """Multi-frame compressed messages need the lane pre-decode's HBM tables, taken from a
+    pool (set_tuning inflate_tabs): with none or only a few, the lanes left without one
+    hand their messages to the serial decoder, and every frame still matches the oracle."""
+    from snf4j_amd import Context
+    rng = np.random.default_rng(9100 + tabs)
+    sessions = []
+    for i in range(40):
+        comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+        text = wsgen.rand_text(rng, 3000)
+        frames = []
+        for m in range(int(rng.integers(1, 6))):
+            body = text[int(rng.integers(0, 1500)):][:int(rng.integers(200, 3000))] + bytes([m])
+            data = (comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH))[:-4]
+            cuts = sorted(set(int(x) for x in rng.integers(1, len(data), int(rng.integers(1, 4))))) \
+                if len(data) > 1 else []
+            parts = [data[a:b] for a, b in zip([0] + cuts, cuts + [len(data)])]
+            for j, p in enumerate(parts):
+                frames.append((1 if j == 0 else 0, j == len(parts) - 1, 4 if j == 0 else 0, p))
+        sessions.append(frames)
+    c = Context(0)
+    c.set_tuning("inflate_tabs", tabs)
+    try:
+        _run(c, oracle, sessions, False, 2, rng)
+    finally:
+        c.close()
+
+
 def test_inflate_fast_replay_takes_fragmented_sessions(oracle):
     """With set_tuning inflate_fast 2 the serial pass does not run at all, so every session must
     be finished by the pre-decode + parallel replay: fragmented compressed messages

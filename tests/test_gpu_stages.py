@@ -190,3 +190,37 @@ def test_batcher_stage_chain_pipelined(ctx, oracle, seed, aggregate):
             n_err += eerr is not None
         assert n_err
     b.close()
+
+
+def test_batcher_stage_chain_capacity_rerun(ctx, oracle):
+    """Messages that inflate far more than the stage's first output region per session
+    (4 KiB + 8x the compressed bytes): those sessions are re-run with larger regions,
+    nothing of the first run having been committed, beside sessions that fit."""
+    from snf4j_amd import NativeBatcher
+    rng = np.random.default_rng(6300)
+    n = 24
+    streams = []
+    for s in range(n):
+        comp = zlib.compressobj(9, zlib.DEFLATED, -15)
+        wire = b""
+        for m in range(int(rng.integers(1, 5))):
+            if s % 3 == 0:
+                body = bytes([65 + m]) * int(rng.integers(20000, 120000))  # ~1000:1
+            else:
+                body = wsgen.rand_text(rng, int(rng.integers(10, 2000)))
+            data = (comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH))[:-4]
+            wire += wsgen.build_frame(1, True, 4, data, True, tuple(int(x) for x in rng.integers(0, 256, 4)))
+        streams.append(wire)
+    b = NativeBatcher(n, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=ctx)
+    b.set_stages(inflate=True, noContext=False, validate=True, aggregate=False)
+    got = [[] for _ in range(n)]
+    for s in range(n):
+        b.feed(s, streams[s])
+    for s, (fr, e) in enumerate(b.flush()):
+        assert e is None, (s, e)
+        got[s] += fr
+    for s in range(n):
+        exp, eerr = _oracle_chain(oracle, streams[s], False, True, False, 1 << 20)
+        assert eerr is None
+        assert [(int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload()) for f in got[s]] == exp, s
+    b.close()

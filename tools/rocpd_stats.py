@@ -13,7 +13,7 @@ c = sqlite3.connect(a.db)
 rows = c.execute("select name, start, end, duration, stream_id from kernels order by start").fetchall()
 agg = {}
 for name, s, e, d, sid in rows:
-    n = re.sub(r"\(.*", "", name)[:60]
+    n = re.sub(r"\(.*", "", name.replace("(anonymous namespace)::", ""))[:60]
     t = agg.setdefault(n, [0, 0])
     t[0] += 1
     t[1] += d
@@ -24,4 +24,4 @@ for n, (k, d) in sorted(agg.items(), key=lambda x: -x[1][1]):
 if a.timeline:
     t0 = rows[-a.timeline][1]
     for name, s, e, d, sid in rows[-a.timeline:]:
-        print(f"{(s - t0) / 1e3:10.1f} us +{d / 1e3:8.1f} stream {sid} {re.sub(r'[(<].*', '', name)[:50]}")
+        print(f"{(s - t0) / 1e3:10.1f} us +{d / 1e3:8.1f} stream {sid} {re.sub(r'[(<].*', '', name.replace('(anonymous namespace)::', ''))[:50]}")
