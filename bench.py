@@ -71,7 +71,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--pmc-json", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--e2e", action="store_true", help="also time the pinned host->device->host path")
+    ap.add_argument("--e2e", action="store_true",
+                    help="also time the pinned host->device->host paths (on by default at N=1 with the extra lines)")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the host->device->host lines")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the secondary BASELINE configs (measured at N=1 only)")
     ap.add_argument("--extra-steps", type=int, default=10)
@@ -308,7 +310,7 @@ def main():
             traffic = traffic_source = None
 
     e2e = None
-    if args.e2e:
+    if (args.e2e or (world == 1 and not args.no_extras)) and not args.no_e2e:
         e2e = e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev)
 
     extras = None
@@ -316,6 +318,8 @@ def main():
         del wire, payload, desc, res, state, off, sf
         torch.cuda.empty_cache()
         extras = [config0_line()] + measure_extras(ctx, dev, args)
+        if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
+            e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 1)
 
     # the CPU baseline runs after every timed region, on rank 0 only (at N > 1 the
     # other ranks wait for it at the closing barrier)
