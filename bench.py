@@ -320,6 +320,7 @@ def main():
         extras = [config0_line()] + measure_extras(ctx, dev, args)
         if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
             e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 1)
+            e2e["native_encode_batcher"] = e2e_encode_line(ctx, dev, 3, 1)
 
     # the CPU baseline runs after every timed region, on rank 0 only (at N > 1 the
     # other ranks wait for it at the closing barrier)
@@ -923,8 +924,66 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
             "api": "wsg_batcher_feed_many + wsg_batcher_flush_async/wait with wsg_batcher_set_stages"}
 
 
+def e2e_encode_line(ctx, dev, K, W, n_s=64, msg_bytes=16 << 20, frame=65536, per_round=16):
+    """The native encode batcher host to host on configs[4]'s shape (64 client sessions,
+    a 16 MiB message each in 64 KiB fragments, FrameEncoder.java:69-120): per round
+    (a loop iteration) every session queues `per_round` fragments
+    (wsg_enc_batcher_add copies them into the pinned arena), then
+    wsg_enc_batcher_flush_async; two flushes in flight, each waited view's wire bytes
+    counted.  Value: wire bytes out per second."""
+    import numpy as np
+    import snf4j_amd
+    from snf4j_amd.frame import make_frame
+    rng = np.random.default_rng(0xE4C)
+    src = rng.integers(0, 256, msg_bytes, dtype=np.uint8)  # the same message bytes for every session
+    nf = msg_bytes // frame
+    frames = [make_frame(2 if i == 0 else 0, i == nf - 1, 0, src[i * frame:(i + 1) * frame].tobytes())
+              for i in range(nf)]
+    from snf4j_amd._lib import lib
+    eb = snf4j_amd.EncodeBatcher(n_s, True, ctx=ctx)
+    masks = rng.integers(0, 256, (n_s, nf, 4), dtype=np.uint8)
+    pays = [np.frombuffer(f.getPayload(), np.uint8) for f in frames]
+    flags = [(0x80 if f.isFinalFragment() else 0) for f in frames]
+    ops = [int(f.getOpcode()) for f in frames]
+    times = []
+    wire_total = 0
+    for rep in range(W + K):
+        t0 = time.perf_counter()
+        pending, wb = 0, 0
+        for r in range(0, nf, per_round):
+            for s in range(n_s):
+                for i in range(r, min(nf, r + per_round)):
+                    rc = lib.wsg_enc_batcher_add(eb._h, s, ops[i], flags[i], masks[s, i].ctypes.data,
+                                                 pays[i].ctypes.data, frame)
+                    assert rc == 0
+            if pending == 2:
+                sf, off, wire = eb.wait_raw()
+                wb += int(off[-1])
+                pending -= 1
+            eb.flush_async()
+            pending += 1
+        while pending:
+            sf, off, wire = eb.wait_raw()
+            wb += int(off[-1])
+            pending -= 1
+        t = time.perf_counter() - t0
+        if rep >= W:
+            times.append(t)
+        wire_total = wb
+    eb.close()
+    exp = n_s * nf * (frame + 14)
+    assert wire_total == exp, (wire_total, exp)
+    t = float(np.median(times))
+    return {"config": f"native encode batcher, configs[4] shape: {n_s} client sessions x {msg_bytes >> 20} MiB in "
+                      f"{frame >> 10} KiB fragments, {per_round} fragments a session per flush, host to host",
+            "value": round(wire_total / t / 2**30, 3), "unit": "GiB/s (wire out, host to host)",
+            "ms_per_batch": round(t * 1e3, 3), "reps": K,
+            "api": "wsg_enc_batcher_add + wsg_enc_batcher_flush_async/wait, two flushes in flight"}
+
+
 EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2": line_configs2,
                "encode": line_encode, "validator": line_validator, "e2e_stages": e2e_stages_line,
+               "e2e_encode": e2e_encode_line,
                "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
                "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W),
                "hs_client": lambda ctx, dev, K, W: handshake_client_line(ctx, dev, K, W)}

@@ -429,7 +429,7 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid);
  * EncodeTask.java:333-407 hands each write to the session's encoder chain).
  * add() copies a frame's payload into a pinned arena and queues it; flush() orders
  * the queued frames by session (each session's in arrival order) and encodes them
- * in one wsg_encode_batch_host call; the close latch (:71-76) persists per session.
+ * in one device batch; the close latch (:71-76) persists per session.
  * Not thread-safe: one loop thread drives it. */
 typedef struct wsg_enc_batcher wsg_enc_batcher;
 
@@ -452,6 +452,13 @@ const char* wsg_enc_batcher_last_error(wsg_enc_batcher* b);
 int wsg_enc_batcher_add(wsg_enc_batcher* b, uint32_t sid, uint8_t opcode, uint8_t flags, const uint8_t* mask,
                         const uint8_t* payload, uint32_t len);
 int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out);
+/* Pipelined form: flush_async queues the encode of everything added so far (H2D on
+ * the batcher's upload stream, kernels on the context's stream, D2H on its download
+ * stream) and returns; add() then fills the next of three slots.  wait() returns the
+ * oldest flush's view (valid until that slot is flushed again).  At most two in
+ * flight.  A session reset while its frames are in flight drops them from the view. */
+int wsg_enc_batcher_flush_async(wsg_enc_batcher* b);
+int wsg_enc_batcher_wait(wsg_enc_batcher* b, wsg_enc_view* out);
 /* slot `sid` for a new session: its queued frames are dropped, the close latch cleared */
 int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid);
 

@@ -159,6 +159,8 @@ def _load():
         "wsg_enc_batcher_last_error": ([p], C.c_char_p),
         "wsg_enc_batcher_add": ([p, u32, C.c_uint8, C.c_uint8, p, p, u32], i32),
         "wsg_enc_batcher_flush": ([p, P(EncView)], i32),
+        "wsg_enc_batcher_flush_async": ([p], i32),
+        "wsg_enc_batcher_wait": ([p, P(EncView)], i32),
         "wsg_enc_batcher_session_reset": ([p, u32], i32),
         "wsg_host_alloc": ([u64], p),
         "wsg_host_release": ([p], i32),

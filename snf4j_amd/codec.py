@@ -602,6 +602,38 @@ class EncodeBatcher:
         from ._lib import EncView, lib
         v = EncView()
         self._check(lib.wsg_enc_batcher_flush(self._h, C.byref(v)))
+        return self._sessions(v)
+
+    def flush_async(self):
+        """Queue the encode of everything added so far (wsg_enc_batcher_flush_async);
+        collect it with wait().  At most two in flight."""
+        from ._lib import lib
+        self._check(lib.wsg_enc_batcher_flush_async(self._h))
+
+    def wait_raw(self):
+        """The oldest queued flush (wsg_enc_batcher_wait) as numpy views, valid until
+        that slot is flushed again: (session_first, wire_off, wire)."""
+        import ctypes as C
+        from ._lib import EncView, lib
+        v = EncView()
+        self._check(lib.wsg_enc_batcher_wait(self._h, C.byref(v)))
+        n, s = int(v.n_frames), int(v.n_sessions)
+        sf = np.ctypeslib.as_array((C.c_uint32 * (s + 1)).from_address(v.session_first))
+        off = np.ctypeslib.as_array((C.c_uint64 * (n + 1)).from_address(v.wire_off))
+        wire = np.ctypeslib.as_array((C.c_uint8 * int(v.wire_bytes)).from_address(v.wire)) if v.wire_bytes \
+            else np.zeros(0, np.uint8)
+        return sf, off, wire
+
+    def wait(self):
+        """[wire bytes of session s] of the oldest queued flush."""
+        import ctypes as C
+        from ._lib import EncView, lib
+        v = EncView()
+        self._check(lib.wsg_enc_batcher_wait(self._h, C.byref(v)))
+        return self._sessions(v)
+
+    def _sessions(self, v):
+        import ctypes as C
         n, s = int(v.n_frames), int(v.n_sessions)
         sf = np.ctypeslib.as_array((C.c_uint32 * (s + 1)).from_address(v.session_first))
         off = np.ctypeslib.as_array((C.c_uint64 * (n + 1)).from_address(v.wire_off))

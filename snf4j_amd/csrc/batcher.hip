@@ -1283,16 +1283,32 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
 // their payloads stay where they landed, wsg_encode_frame.payload_off points at
 // them) and encodes them in one wsg_encode_batch_host call.  The close latch
 // (:71-76) is per session and persists across flushes.
+// One encode flush's pinned staging and device buffers (three: one being filled by
+// add(), up to two in flight).
+struct EncSlot {
+  PinnedBuf arena, frames, sf, cl, wire, off;
+  uint64_t arena_len = 0, F = 0, need = 0;
+  DBuf d_pay, d_frames, d_sf, d_cl, d_wire, d_off;
+  hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_out = nullptr;
+  std::vector<uint32_t> resets;  // sessions reset while this flush was in flight: their bytes are dropped
+  // the view with those sessions' frames left out (built only when there are some)
+  std::vector<uint32_t> v_sf;
+  std::vector<uint64_t> v_off;
+  std::vector<uint8_t> v_wire;
+};
+
 struct wsg_enc_batcher {
   wsg_ctx* ctx = nullptr;
   int client = 0;
   uint32_t n = 0;
-  std::vector<uint8_t> closed;           // FrameEncoder.closed per session
+  std::vector<uint8_t> closed;           // FrameEncoder.closed per session, as of the frames flushed so far
   std::vector<uint32_t> rec_sid;         // session of each queued frame, arrival order
   std::vector<wsg_encode_frame> rec;     // queued frames, arrival order
   std::vector<uint32_t> count;           // queued frames per session
-  PinnedBuf arena, frames, sf, cl, wire, off;
-  uint64_t arena_len = 0;
+  EncSlot es[3];
+  int open = 0;                          // the slot add() fills
+  std::deque<int> q;                     // flushes in flight, oldest first
+  hipStream_t s_in = nullptr, s_out = nullptr;  // uploads / downloads (kernels on the context's stream)
   std::string err;
 };
 
@@ -1321,8 +1337,19 @@ int wsg_enc_batcher_open(wsg_ctx* ctx, int client_mode, uint32_t n_sessions, wsg
 int wsg_enc_batcher_close(wsg_enc_batcher* b) {
   if (!b) return WSG_API_EINVAL;
   (void)wsg_sync(b->ctx);
-  PinnedBuf* bufs[] = {&b->arena, &b->frames, &b->sf, &b->cl, &b->wire, &b->off};
-  for (PinnedBuf* p : bufs) p->release();
+  if (b->s_in) (void)hipStreamSynchronize(b->s_in);
+  if (b->s_out) (void)hipStreamSynchronize(b->s_out);
+  for (EncSlot& e : b->es) {
+    PinnedBuf* bufs[] = {&e.arena, &e.frames, &e.sf, &e.cl, &e.wire, &e.off};
+    for (PinnedBuf* p : bufs) p->release();
+    DBuf* dbufs[] = {&e.d_pay, &e.d_frames, &e.d_sf, &e.d_cl, &e.d_wire, &e.d_off};
+    for (DBuf* d : dbufs) d->release();
+    hipEvent_t evs[] = {e.ev_in, e.ev_k, e.ev_out};
+    for (hipEvent_t v : evs)
+      if (v) (void)hipEventDestroy(v);
+  }
+  if (b->s_in) (void)hipStreamDestroy(b->s_in);
+  if (b->s_out) (void)hipStreamDestroy(b->s_out);
   delete b;
   return WSG_API_OK;
 }
@@ -1333,17 +1360,18 @@ int wsg_enc_batcher_add(wsg_enc_batcher* b, uint32_t sid, uint8_t opcode, uint8_
                         const uint8_t* payload, uint32_t len) {
   if (!b || sid >= b->n || (len && !payload)) return WSG_API_EINVAL;
   if (b->closed[sid]) return WSG_API_OK;  // FrameEncoder.java:71-76: nothing after a CLOSE (latched earlier)
-  const uint64_t at = (b->arena_len + 15) & ~15ull;
-  if (at + len + 16 > b->arena.n) {  // grow, keeping what is queued (pinned: the H2D source)
+  EncSlot& e = b->es[b->open];
+  const uint64_t at = (e.arena_len + 15) & ~15ull;
+  if (at + len + 16 > e.arena.n) {  // grow, keeping what is queued (pinned: the H2D source)
     PinnedBuf g;
-    if (g.ensure(std::max<uint64_t>(at + len + 16, 2 * b->arena.n)) != hipSuccess)
+    if (g.ensure(std::max<uint64_t>(at + len + 16, 2 * e.arena.n)) != hipSuccess)
       return eset(b, WSG_API_ENOMEM, "pinned arena");
-    if (b->arena_len) memcpy(g.p, b->arena.p, b->arena_len);
-    b->arena.release();
-    b->arena = g;
+    if (e.arena_len) memcpy(g.p, e.arena.p, e.arena_len);
+    e.arena.release();
+    e.arena = g;
   }
-  if (len) memcpy(b->arena.p + at, payload, len);
-  b->arena_len = at + len;
+  if (len) memcpy(e.arena.p + at, payload, len);
+  e.arena_len = at + len;
   wsg_encode_frame f{};
   f.payload_off = at;
   f.payload_len = len;
@@ -1356,43 +1384,133 @@ int wsg_enc_batcher_add(wsg_enc_batcher* b, uint32_t sid, uint8_t opcode, uint8_
   return WSG_API_OK;
 }
 
-int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out) {
-  if (!b || !out) return WSG_API_EINVAL;
+// Queue the encode of everything added since the last flush: frames ordered by session
+// (stable), H2D on the batcher's upload stream, the kernels on the context's stream,
+// D2H on its download stream.  The close latch a batch starts from is known on the
+// host (a CLOSE frame latches its session for every later frame, FrameEncoder.java:
+// 71-76), so the next batch can be queued before this one comes back.
+int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
+  if (!b) return WSG_API_EINVAL;
+  if (b->q.size() >= 2) return eset(b, WSG_API_ERANGE, "two flushes in flight: wsg_enc_batcher_wait first");
   const uint32_t S = b->n;
   const uint64_t F = b->rec.size();
-  E_TRY(b, b->frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
-  E_TRY(b, b->sf.ensure((S + 1) * sizeof(uint32_t)));
-  E_TRY(b, b->cl.ensure(S + 1));
-  E_TRY(b, b->off.ensure((F + 1) * sizeof(uint64_t)));
-  uint32_t* sf = (uint32_t*)b->sf.p;
+  const int slot = b->open;
+  EncSlot& e = b->es[slot];
+  E_TRY(b, hipSetDevice(ws::ctx_device(b->ctx)));
+  if (!b->s_in) E_TRY(b, hipStreamCreateWithFlags(&b->s_in, hipStreamNonBlocking));
+  if (!b->s_out) E_TRY(b, hipStreamCreateWithFlags(&b->s_out, hipStreamNonBlocking));
+  hipEvent_t* evs[] = {&e.ev_in, &e.ev_k, &e.ev_out};
+  for (hipEvent_t* v : evs)
+    if (!*v) E_TRY(b, hipEventCreateWithFlags(v, hipEventDisableTiming));
+  E_TRY(b, e.frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
+  E_TRY(b, e.sf.ensure((S + 1) * sizeof(uint32_t)));
+  E_TRY(b, e.cl.ensure(S + 1));
+  E_TRY(b, e.off.ensure((F + 1) * sizeof(uint64_t)));
+  uint32_t* sf = (uint32_t*)e.sf.p;
   sf[0] = 0;
   for (uint32_t i = 0; i < S; ++i) sf[i + 1] = sf[i] + b->count[i];
   {  // stable counting sort of the records by session
     std::vector<uint32_t> pos(sf, sf + S);
-    wsg_encode_frame* fr = (wsg_encode_frame*)b->frames.p;
+    wsg_encode_frame* fr = (wsg_encode_frame*)e.frames.p;
     for (uint64_t k = 0; k < F; ++k) fr[pos[b->rec_sid[k]]++] = b->rec[k];
   }
   uint64_t need = 0;
   for (uint64_t k = 0; k < F; ++k) need += wsg_encoded_length(b->rec[k].payload_len, b->client);
-  E_TRY(b, b->wire.ensure(need + 32));
-  if (S) memcpy(b->cl.p, b->closed.data(), S);
-  int rc = wsg_encode_batch_host(b->ctx, b->client, b->arena.p, b->arena_len, (const wsg_encode_frame*)b->frames.p, F,
-                                 sf, S, b->cl.p, b->wire.p, b->wire.n, (uint64_t*)b->off.p);
+  E_TRY(b, e.wire.ensure(need + 32));
+  if (S) memcpy(e.cl.p, b->closed.data(), S);
+  for (uint64_t k = 0; k < F; ++k)  // the latch the next batch starts from
+    if (b->rec[k].opcode == WSG_OP_CLOSE) b->closed[b->rec_sid[k]] = 1;
+  E_TRY(b, e.d_pay.ensure(e.arena_len + 32));
+  E_TRY(b, e.d_frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
+  E_TRY(b, e.d_sf.ensure((S + 1) * sizeof(uint32_t)));
+  E_TRY(b, e.d_cl.ensure(S + 1));
+  E_TRY(b, e.d_wire.ensure(need + 32));
+  E_TRY(b, e.d_off.ensure((F + 1) * sizeof(uint64_t)));
+  if (e.arena_len) E_TRY(b, hipMemcpyAsync(e.d_pay.p, e.arena.p, e.arena_len, hipMemcpyHostToDevice, b->s_in));
+  if (F) E_TRY(b, hipMemcpyAsync(e.d_frames.p, e.frames.p, F * sizeof(wsg_encode_frame), hipMemcpyHostToDevice, b->s_in));
+  E_TRY(b, hipMemcpyAsync(e.d_sf.p, e.sf.p, (S + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, b->s_in));
+  if (S) E_TRY(b, hipMemcpyAsync(e.d_cl.p, e.cl.p, S, hipMemcpyHostToDevice, b->s_in));
+  E_TRY(b, hipEventRecord(e.ev_in, b->s_in));
+  hipStream_t ks = ws::ctx_stream(b->ctx);
+  E_TRY(b, hipStreamWaitEvent(ks, e.ev_in, 0));
+  int rc = wsg_encode_batch_device(b->ctx, b->client, e.d_pay.p, e.arena_len, (const wsg_encode_frame*)e.d_frames.p,
+                                   F, (const uint32_t*)e.d_sf.p, S, e.d_cl.p, e.d_wire.p, need + 32,
+                                   (uint64_t*)e.d_off.p);
   if (rc) return eset(b, rc, wsg_last_error(b->ctx));
-  if (S) memcpy(b->closed.data(), b->cl.p, S);
-  if (!F) ((uint64_t*)b->off.p)[0] = 0;
+  if (!F) E_TRY(b, hipMemsetAsync(e.d_off.p, 0, sizeof(uint64_t), ks));
+  E_TRY(b, hipEventRecord(e.ev_k, ks));
+  E_TRY(b, hipStreamWaitEvent(b->s_out, e.ev_k, 0));
+  E_TRY(b, hipMemcpyAsync(e.off.p, e.d_off.p, (F + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, b->s_out));
+  // (the kept frames' bytes are at most `need`: frames dropped after a CLOSE take none)
+  if (need) E_TRY(b, hipMemcpyAsync(e.wire.p, e.d_wire.p, need, hipMemcpyDeviceToHost, b->s_out));
+  E_TRY(b, hipEventRecord(e.ev_out, b->s_out));
+  e.F = F;
+  e.need = need;
+  e.resets.clear();
+  b->q.push_back(slot);
   b->rec.clear();
   b->rec_sid.clear();
   std::fill(b->count.begin(), b->count.end(), 0u);
-  b->arena_len = 0;
+  b->open = (b->open + 1) % 3;
+  b->es[b->open].arena_len = 0;
+  return WSG_API_OK;
+}
+
+// The oldest encode flush in flight: session s's wire bytes are
+// wire[off[sf[s]], off[sf[s+1]]).  Valid until that slot is reused (two flushes later).
+int wsg_enc_batcher_wait(wsg_enc_batcher* b, wsg_enc_view* out) {
+  if (!b || !out) return WSG_API_EINVAL;
+  if (b->q.empty()) return eset(b, WSG_API_ERANGE, "no encode flush in flight");
+  const int slot = b->q.front();
+  b->q.pop_front();
+  EncSlot& e = b->es[slot];
+  E_TRY(b, hipEventSynchronize(e.ev_out));
+  const uint32_t S = b->n;
+  const uint64_t F = e.F;
+  const uint32_t* sf = (const uint32_t*)e.sf.p;
+  const uint64_t* off = (const uint64_t*)e.off.p;
   out->n_frames = F;
-  out->wire_bytes = ((const uint64_t*)b->off.p)[F];
+  out->wire_bytes = off[F];
   out->n_sessions = S;
   out->reserved = 0;
   out->session_first = sf;
-  out->wire_off = (const uint64_t*)b->off.p;
-  out->wire = b->wire.p;
+  out->wire_off = off;
+  out->wire = e.wire.p;
+  if (e.resets.empty()) return WSG_API_OK;
+  // a slot handed to a new session while this flush was in flight: the old session's
+  // frames are left out (their bytes must not reach the new session)
+  std::vector<uint8_t> drop(S, 0);
+  for (uint32_t s : e.resets) drop[s] = 1;
+  e.v_sf.assign(S + 1, 0);
+  e.v_off.assign(1, 0);
+  e.v_wire.clear();
+  for (uint32_t s = 0; s < S; ++s) {
+    e.v_sf[s] = (uint32_t)(e.v_off.size() - 1);
+    if (drop[s]) continue;
+    for (uint32_t k = sf[s]; k < sf[s + 1]; ++k) {
+      e.v_wire.insert(e.v_wire.end(), e.wire.p + off[k], e.wire.p + off[k + 1]);
+      e.v_off.push_back(e.v_wire.size());
+    }
+  }
+  e.v_sf[S] = (uint32_t)(e.v_off.size() - 1);
+  out->n_frames = e.v_off.size() - 1;
+  out->wire_bytes = e.v_wire.size();
+  out->session_first = e.v_sf.data();
+  out->wire_off = e.v_off.data();
+  out->wire = e.v_wire.data();
   return WSG_API_OK;
+}
+
+int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out) {
+  if (!b || !out) return WSG_API_EINVAL;
+  while (!b->q.empty()) {  // (views of unwaited async flushes are dropped)
+    wsg_enc_view v;
+    const int rc = wsg_enc_batcher_wait(b, &v);
+    if (rc) return rc;
+  }
+  const int rc = wsg_enc_batcher_flush_async(b);
+  if (rc) return rc;
+  return wsg_enc_batcher_wait(b, out);
 }
 
 int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid) {
@@ -1409,6 +1527,7 @@ int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid) {
     b->count[sid] = 0;
   }
   b->closed[sid] = 0;
+  for (int slot : b->q) b->es[slot].resets.push_back(sid);
   return WSG_API_OK;
 }
 

@@ -160,3 +160,45 @@ def test_encode_batcher_matches_oracle(ctx, oracle):
             got = b.flush()
             assert got == want, (cm, flush)
         b.close()
+
+
+def test_encode_batcher_pipelined(ctx, oracle):
+    """wsg_enc_batcher_flush_async / wait with two flushes in flight: each flush's view
+    equals the oracle FrameEncoders' output for the frames added before it; a CLOSE in
+    a flush still in flight latches the frames added after it (the latch is known on
+    the host); a slot reset while its frames are in flight drops them from the view."""
+    from snf4j_amd import EncodeBatcher
+    from snf4j_amd.frame import make_frame
+    for cm in (True, False):
+        rng = np.random.default_rng(909 + cm)
+        n = 29
+        b = EncodeBatcher(n, cm, ctx=ctx)
+        enc = [oracle.Encoder(cm) for _ in range(n)]
+        pending = []  # expected views of the flushes in flight, oldest first
+        for flush in range(8):
+            want = [b""] * n
+            for _ in range(int(rng.integers(30, 200))):
+                s = int(rng.integers(0, n))
+                r = rng.random()
+                op = 8 if r < 0.01 else 9 if r < 0.05 else int(rng.choice([0, 1, 2]))
+                ln = int(rng.integers(0, 126)) if op >= 8 else 65536 if rng.random() < 0.1 else \
+                    int(rng.integers(0, 3000))
+                if op == 8 and ln == 1:
+                    ln = 2
+                p = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+                fin, rsv = bool(rng.integers(0, 2)) or op >= 8, int(rng.integers(0, 8))
+                mask = tuple(int(x) for x in rng.integers(0, 256, 4))
+                b.add(s, make_frame(op, fin, rsv, p), mask)
+                want[s] += enc[s].encode(op, fin, rsv, p, mask if cm else (0, 0, 0, 0))
+            b.flush_async()
+            pending.append(want)
+            if flush == 4:  # slot 5 to a new session while two flushes hold its frames
+                b.reset_session(5)
+                enc[5] = oracle.Encoder(cm)
+                for w in pending:
+                    w[5] = b""
+            if len(pending) == 2:
+                assert b.wait() == pending.pop(0), (cm, flush)
+        while pending:
+            assert b.wait() == pending.pop(0), cm
+        b.close()
