@@ -451,6 +451,11 @@ const char* wsg_enc_batcher_last_error(wsg_enc_batcher* b);
  * `mask` (client mode) is the 4-byte key, FrameEncoder.java:109-118. */
 int wsg_enc_batcher_add(wsg_enc_batcher* b, uint32_t sid, uint8_t opcode, uint8_t flags, const uint8_t* mask,
                         const uint8_t* payload, uint32_t len);
+/* Many frames in one call (a loop iteration's writes), as n add() calls in order;
+ * masks: 4 bytes a frame (client mode) or NULL. */
+int wsg_enc_batcher_add_many(wsg_enc_batcher* b, uint32_t n, const uint32_t* sids, const uint8_t* opcodes,
+                             const uint8_t* flags, const uint8_t* masks, const uint8_t* const* payloads,
+                             const uint32_t* lens);
 int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out);
 /* Pipelined form: flush_async queues the encode of everything added so far (H2D on
  * the batcher's upload stream, kernels on the context's stream, D2H on its download

@@ -160,6 +160,7 @@ def _load():
         "wsg_enc_batcher_add": ([p, u32, C.c_uint8, C.c_uint8, p, p, u32], i32),
         "wsg_enc_batcher_flush": ([p, P(EncView)], i32),
         "wsg_enc_batcher_flush_async": ([p], i32),
+        "wsg_enc_batcher_add_many": ([p, u32, p, p, p, p, p, p], i32),
         "wsg_enc_batcher_wait": ([p, P(EncView)], i32),
         "wsg_enc_batcher_session_reset": ([p, u32], i32),
         "wsg_host_alloc": ([u64], p),

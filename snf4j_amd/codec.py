@@ -592,6 +592,21 @@ class EncodeBatcher:
         self._check(lib.wsg_enc_batcher_add(self._h, int(sid), int(frame.getOpcode()), flags, m.ctypes.data,
                                             p.ctypes.data if p.size else None, int(p.size)))
 
+    def add_many_ptrs(self, sids, opcodes, flags, masks, ptrs, lens):
+        """wsg_enc_batcher_add_many over numpy arrays: per frame its session (u32),
+        opcode and FIN/RSV flags (u8), 4-byte mask (u8 [n, 4], or None), payload host
+        address (u64) and length (u32), in the order add() would take them."""
+        from ._lib import lib
+        sids = np.ascontiguousarray(sids, dtype=np.uint32)
+        opcodes = np.ascontiguousarray(opcodes, dtype=np.uint8)
+        flags = np.ascontiguousarray(flags, dtype=np.uint8)
+        ptrs = np.ascontiguousarray(ptrs, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        m = np.ascontiguousarray(masks, dtype=np.uint8) if masks is not None else None
+        self._check(lib.wsg_enc_batcher_add_many(self._h, len(sids), sids.ctypes.data, opcodes.ctypes.data,
+                                                 flags.ctypes.data, m.ctypes.data if m is not None else None,
+                                                 ptrs.ctypes.data, lens.ctypes.data))
+
     def reset_session(self, sid: int):
         from ._lib import lib
         self._check(lib.wsg_enc_batcher_session_reset(self._h, int(sid)))

@@ -1309,6 +1309,7 @@ struct wsg_enc_batcher {
   int open = 0;                          // the slot add() fills
   std::deque<int> q;                     // flushes in flight, oldest first
   hipStream_t s_in = nullptr, s_out = nullptr;  // uploads / downloads (kernels on the context's stream)
+  std::unique_ptr<Pool> pool;                   // add_many's copies
   std::string err;
 };
 
@@ -1330,6 +1331,8 @@ int wsg_enc_batcher_open(wsg_ctx* ctx, int client_mode, uint32_t n_sessions, wsg
   b->n = n_sessions;
   b->closed.assign(n_sessions, 0);
   b->count.assign(n_sessions, 0);
+  const unsigned hw = std::thread::hardware_concurrency();
+  b->pool.reset(new Pool((hw ? std::min(16u, hw) : 8u) - 1));
   *out = b;
   return WSG_API_OK;
 }
@@ -1355,6 +1358,59 @@ int wsg_enc_batcher_close(wsg_enc_batcher* b) {
 }
 
 const char* wsg_enc_batcher_last_error(wsg_enc_batcher* b) { return b ? b->err.c_str() : "null batcher"; }
+
+// Many frames at once (a loop iteration's writes): placed in arrival order as add()
+// places them, the payload copies spread over the pool (streaming stores, as the
+// decode feed's) when there are megabytes of them.
+int wsg_enc_batcher_add_many(wsg_enc_batcher* b, uint32_t n, const uint32_t* sids, const uint8_t* opcodes,
+                             const uint8_t* flags, const uint8_t* masks, const uint8_t* const* payloads,
+                             const uint32_t* lens) {
+  if (!b || (n && (!sids || !opcodes || !flags || !payloads || !lens))) return WSG_API_EINVAL;
+  for (uint32_t i = 0; i < n; ++i)
+    if (sids[i] >= b->n || (lens[i] && !payloads[i])) return WSG_API_EINVAL;
+  EncSlot& e = b->es[b->open];
+  std::vector<uint64_t> at(n, ~0ull);
+  uint64_t pos = e.arena_len, bytes = 0;
+  for (uint32_t i = 0; i < n; ++i) {
+    if (b->closed[sids[i]]) continue;  // FrameEncoder.java:71-76
+    at[i] = (pos + 15) & ~15ull;
+    pos = at[i] + lens[i];
+    bytes += lens[i];
+  }
+  if (pos + 16 > e.arena.n) {
+    PinnedBuf g;
+    if (g.ensure(std::max<uint64_t>(pos + 16, 2 * e.arena.n)) != hipSuccess)
+      return eset(b, WSG_API_ENOMEM, "pinned arena");
+    if (e.arena_len) memcpy(g.p, e.arena.p, e.arena_len);
+    e.arena.release();
+    e.arena = g;
+  }
+  const uint32_t T = bytes < (4u << 20) ? 1u : std::min<uint32_t>(b->pool->size(), n);
+  auto copy = [&](uint32_t i) {
+    if (at[i] != ~0ull && lens[i]) copy_to_arena(e.arena.p + at[i], payloads[i], lens[i]);
+  };
+  if (T <= 1) {
+    for (uint32_t i = 0; i < n; ++i) copy(i);
+  } else {
+    b->pool->run(T, [&](uint32_t t) {
+      for (uint32_t i = (uint32_t)((uint64_t)n * t / T); i < (uint32_t)((uint64_t)n * (t + 1) / T); ++i) copy(i);
+    });
+  }
+  for (uint32_t i = 0; i < n; ++i) {
+    if (at[i] == ~0ull) continue;
+    wsg_encode_frame f{};
+    f.payload_off = at[i];
+    f.payload_len = lens[i];
+    f.opcode = opcodes[i];
+    f.flags = flags[i];
+    if (masks) memcpy(f.mask, masks + 4 * (uint64_t)i, 4);
+    b->rec.push_back(f);
+    b->rec_sid.push_back(sids[i]);
+    ++b->count[sids[i]];
+  }
+  e.arena_len = pos;
+  return WSG_API_OK;
+}
 
 int wsg_enc_batcher_add(wsg_enc_batcher* b, uint32_t sid, uint8_t opcode, uint8_t flags, const uint8_t* mask,
                         const uint8_t* payload, uint32_t len) {

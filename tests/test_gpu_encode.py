@@ -177,6 +177,7 @@ def test_encode_batcher_pipelined(ctx, oracle):
         pending = []  # expected views of the flushes in flight, oldest first
         for flush in range(8):
             want = [b""] * n
+            many = []  # odd flushes: the frames go in with one wsg_enc_batcher_add_many
             for _ in range(int(rng.integers(30, 200))):
                 s = int(rng.integers(0, n))
                 r = rng.random()
@@ -188,8 +189,15 @@ def test_encode_batcher_pipelined(ctx, oracle):
                 p = rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
                 fin, rsv = bool(rng.integers(0, 2)) or op >= 8, int(rng.integers(0, 8))
                 mask = tuple(int(x) for x in rng.integers(0, 256, 4))
-                b.add(s, make_frame(op, fin, rsv, p), mask)
+                if flush & 1:
+                    many.append((s, op, (0x80 if fin else 0) | (rsv << 4), mask, np.frombuffer(p, np.uint8)))
+                else:
+                    b.add(s, make_frame(op, fin, rsv, p), mask)
                 want[s] += enc[s].encode(op, fin, rsv, p, mask if cm else (0, 0, 0, 0))
+            if many:
+                b.add_many_ptrs([m[0] for m in many], [m[1] for m in many], [m[2] for m in many],
+                                np.array([m[3] for m in many], dtype=np.uint8),
+                                [m[4].ctypes.data if m[4].size else 0 for m in many], [m[4].size for m in many])
             b.flush_async()
             pending.append(want)
             if flush == 4:  # slot 5 to a new session while two flushes hold its frames
