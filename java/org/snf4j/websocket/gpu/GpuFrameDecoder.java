@@ -99,7 +99,7 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 			r = Wsg.frameAvailableDirect(b, b.position(), len, err);
 		else {  // (read-only heap buffer) the header copy of :310-331
 			byte[] hdr = new byte[Math.min(len, 14)];
-			b.get(hdr);
+			b.duplicate().get(hdr);  // available() must not move the buffer (IBaseDecoder.java:58-70)
 			r = Wsg.frameAvailable(hdr, 0, len, err);
 		}
 		return checked(session, r);

@@ -75,7 +75,11 @@ JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_frameAvailable(JNIEnv* 
 JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_frameAvailableDirect(JNIEnv* env, jclass c, jobject b,
                                                                               jint off, jint len, jlongArray err) {
     uint8_t hdr[16] = {0};
-    memcpy(hdr, addr(env, b) + off, len < 14 ? (size_t)len : 14);
+    uint8_t* p = addr(env, b);
+    jlong cap = b ? (*env)->GetDirectBufferCapacity(env, b) : -1;
+    jint n = len < 14 ? len : 14;
+    if (!p || cap < 0 || off < 0 || len < 0 || (jlong)off + (jlong)n > cap) return -2; /* not a direct buffer */
+    memcpy(hdr, p + off, (size_t)n);
     return available(env, hdr, len, err);
 }
 
@@ -85,7 +89,10 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_checkHeader(JNIEnv* env,
                                                                     jlongArray detail) {
     wsg_decoder_cfg cfg = decoder_cfg(client, ext, max_payload, 0);
     int64_t d = 0;
-    int32_t s = wsg_check_header(&cfg, frag ? 1 : 0, addr(env, data) + off, (uint64_t)len, &d);
+    uint8_t* p = addr(env, data);
+    jlong cap = data ? (*env)->GetDirectBufferCapacity(env, data) : -1;
+    if (!p || cap < 0 || off < 0 || len < 0 || (jlong)off + (jlong)len > cap) return WSG_API_EINVAL;
+    int32_t s = wsg_check_header(&cfg, frag ? 1 : 0, p + off, (uint64_t)len, &d);
     jlong v = d;
     (*env)->SetLongArrayRegion(env, detail, 0, 1, &v);
     return s;
