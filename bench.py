@@ -321,6 +321,7 @@ def main():
         if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
             e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 1)
             e2e["native_encode_batcher"] = e2e_encode_line(ctx, dev, 3, 1)
+            e2e["native_batcher_aggregate"] = e2e_aggregate_line(ctx, dev, 3, 1)
 
     # the CPU baseline runs after every timed region, on rank 0 only (at N > 1 the
     # other ranks wait for it at the closing barrier)
@@ -981,9 +982,78 @@ def e2e_encode_line(ctx, dev, K, W, n_s=64, msg_bytes=16 << 20, frame=65536, per
             "api": "per round wsg_enc_batcher_add_many + wsg_enc_batcher_flush_async/wait, two flushes in flight"}
 
 
+def e2e_aggregate_line(ctx, dev, K, W, chunk=65536):
+    """The native batcher with FrameAggregator after the decoder (wsg_batcher_set_stages
+    aggregate; FrameAggregator.java:72-104) on configs[2]'s 4 GiB mixed batch, host to
+    host: per round one `chunk`-byte read of every session, two flushes in flight;
+    the decode's UTF-8 check stays fused.  Value: wire bytes fed per second."""
+    import numpy as np
+    import torch
+    import snf4j_amd
+    from benchsupport.synth import mixed_plan
+    t, offh, sfh, wl, info = mixed_plan(0xC0F3, 1024, 4 << 30)
+    n_s = 1024
+    tab = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
+    wire = torch.zeros(wl + 64, dtype=torch.uint8, device=dev)
+    benchsupport.synth_frames(ctx, tab, wire)
+    del tab
+    h_wire = torch.empty(wl, dtype=torch.uint8).pin_memory()
+    h_wire.copy_(wire[:wl])
+    del wire
+    torch.cuda.empty_cache()
+    hw = h_wire.numpy()
+    base = hw.ctypes.data
+    starts = offh[sfh[:-1].astype(np.int64)].astype(np.int64)
+    ends = offh[sfh[1:].astype(np.int64)].astype(np.int64)
+    rounds = []
+    pos = starts.copy()
+    while (pos < ends).any():
+        live = np.nonzero(pos < ends)[0]
+        ln = np.minimum(ends[live] - pos[live], chunk)
+        rounds.append((live.astype(np.uint32), (base + pos[live]).astype(np.uint64), ln.astype(np.uint64)))
+        pos[live] += chunk
+    pctx = snf4j_amd.Context(dev.index, stream=torch.cuda.Stream(dev))
+    apply_tuning(pctx)
+    nb = snf4j_amd.NativeBatcher(n_s, clientMode=False, allowExtensions=False, maxPayloadLen=65536, ctx=pctx)
+    nb.set_stages(inflate=False, validate=True, aggregate=True, maxAggregatedLength=16 << 20)
+    times = []
+    n_out = n_err = 0
+    for rep in range(W + K):
+        for s in range(n_s):
+            nb.reset_session(s)
+        t0 = time.perf_counter()
+        pending, n_out, n_err = 0, 0, 0
+        for sids, ptrs, lens in rounds:
+            nb.feed_many_ptrs(sids, ptrs, lens)
+            if pending == 2:
+                sfb, descb, _, resb, _ = nb.wait_raw()
+                n_out += int(resb["n_delivered"].astype(np.int64).sum())
+                n_err += int((resb["error"] != 0).sum())
+                pending -= 1
+            nb.flush_async()
+            pending += 1
+        while pending:
+            sfb, descb, _, resb, _ = nb.wait_raw()
+            n_out += int(resb["n_delivered"].astype(np.int64).sum())
+            n_err += int((resb["error"] != 0).sum())
+            pending -= 1
+        tt = time.perf_counter() - t0
+        if rep >= W:
+            times.append(tt)
+    nb.close()
+    pctx.close()
+    assert n_err == len(info["bad_sessions"]), (n_err, len(info["bad_sessions"]))
+    tm = float(np.median(times))
+    return {"config": f"native batcher + FrameAggregator stage, configs[2] batch ({wl / 2**30:.2f} GiB wire, 1024 sessions, "
+                      f"10% of messages fragmented, 1% with invalid UTF-8), {chunk} B reads, host to host",
+            "value": round(wl / tm / 2**30, 3), "unit": "GiB/s (wire, host to host)", "ms_per_batch": round(tm * 1e3, 2),
+            "frames_out": n_out, "sessions_failed": n_err, "reps": K, "rounds": len(rounds),
+            "api": "wsg_batcher_feed_many + wsg_batcher_flush_async/wait with wsg_batcher_set_stages(aggregate)"}
+
+
 EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2": line_configs2,
                "encode": line_encode, "validator": line_validator, "e2e_stages": e2e_stages_line,
-               "e2e_encode": e2e_encode_line,
+               "e2e_encode": e2e_encode_line, "e2e_aggregate": e2e_aggregate_line,
                "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
                "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W),
                "hs_client": lambda ctx, dev, K, W: handshake_client_line(ctx, dev, K, W)}
