@@ -991,7 +991,9 @@ def e2e_aggregate_line(ctx, dev, K, W, chunk=65536):
     import torch
     import snf4j_amd
     from benchsupport.synth import mixed_plan
-    t, offh, sfh, wl, info = mixed_plan(0xC0F3, 1024, 4 << 30)
+    # configs[2]'s mix without the invalid UTF-8 (a failed session swallows the rest of its
+    # input: with 1% bad messages most of the 4 GiB would never reach the aggregator)
+    t, offh, sfh, wl, info = mixed_plan(0xC0F3, 1024, 4 << 30, bad_frac=0.0)
     n_s = 1024
     tab = torch.from_numpy(t.view(np.uint8).copy()).to(dev)
     wire = torch.zeros(wl + 64, dtype=torch.uint8, device=dev)
@@ -1044,8 +1046,8 @@ def e2e_aggregate_line(ctx, dev, K, W, chunk=65536):
     pctx.close()
     assert n_err == len(info["bad_sessions"]), (n_err, len(info["bad_sessions"]))
     tm = float(np.median(times))
-    return {"config": f"native batcher + FrameAggregator stage, configs[2] batch ({wl / 2**30:.2f} GiB wire, 1024 sessions, "
-                      f"10% of messages fragmented, 1% with invalid UTF-8), {chunk} B reads, host to host",
+    return {"config": f"native batcher + FrameAggregator stage, configs[2]'s mix ({wl / 2**30:.2f} GiB wire, 1024 sessions, "
+                      f"10% of messages fragmented, no invalid UTF-8), {chunk} B reads, host to host",
             "value": round(wl / tm / 2**30, 3), "unit": "GiB/s (wire, host to host)", "ms_per_batch": round(tm * 1e3, 2),
             "frames_out": n_out, "sessions_failed": n_err, "reps": K, "rounds": len(rounds),
             "api": "wsg_batcher_feed_many + wsg_batcher_flush_async/wait with wsg_batcher_set_stages(aggregate)"}
