@@ -206,7 +206,8 @@ constexpr uint32_t COPY_MAX = 65536;
 // One workgroup per copy.  Output slots are 16-B aligned; a source is 16-B aligned when
 // it is a decoder payload slot, byte-aligned when it is inflated output (messages back
 // to back), so the widest access both sides allow is used.
-constexpr uint32_t GATHER_GROUPS = 128;  // workgroups of the output gather (enough to fill PCIe)
+constexpr uint32_t GATHER_GROUPS = 32;  // workgroups of the output gather: enough to fill PCIe, few enough
+                                         // that the next flush's small downloads still get a share of it
 
 __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                     const StageCopy* __restrict__ cp, uint32_t n) {
@@ -346,6 +347,8 @@ struct wsg_batcher {
                        // inflated | aggregated)
   DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot;
   PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot;  // stage results downloaded
+  PinnedBuf h_pend;                     // aggregator bytes held for the next flush, downloaded
+  DBuf d_pend;
   hipStream_t s_dl = nullptr;           // downloads of stage outputs
   StageOut* out = nullptr;              // the output the stage run at hand writes
 };
@@ -650,18 +653,29 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
       h.agg_held_valid = false;
     }
   }
-  // the held bytes are needed before the next flush's stages run: fetched now
+  // the held bytes are needed before the next flush's stages run: fetched now, all of
+  // them by one gather into pinned memory (a copy call per session cost ~25 us each)
   if (!pending.empty()) {
-    std::vector<std::vector<uint8_t>> pend_bytes(pending.size());
-    for (size_t i = 0; i < pending.size(); ++i) {
-      pend_bytes[i].resize(pending[i].second.len);
-      B_TRY(b, hipMemcpyAsync(pend_bytes[i].data(), b->ar->p + pending[i].second.src, pending[i].second.len,
-                              hipMemcpyDeviceToHost, st));
+    std::vector<StageCopy> pc;
+    uint64_t tot = 0;
+    for (auto& pe : pending) {
+      for (uint64_t o = 0; o < pe.second.len; o += COPY_MAX)
+        pc.push_back({pe.second.src + o, tot + o, (uint32_t)std::min<uint64_t>(COPY_MAX, pe.second.len - o), 0});
+      pe.second.dst = tot;
+      tot = al16(tot + pe.second.len);
     }
+    B_TRY(b, b->h_pend.ensure(tot + 16));
+    B_TRY(b, upload(b->d_pend, pc, st));
+    uint8_t* dst = nullptr;
+    B_TRY(b, hipHostGetDevicePointer((void**)&dst, b->h_pend.p, 0));
+    const uint32_t n = (uint32_t)pc.size();
+    hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, GATHER_GROUPS)), dim3(256), 0, st, b->ar->p, dst,
+                       (const StageCopy*)b->d_pend.p, n);
+    B_TRY(b, hipGetLastError());
     B_TRY(b, hipStreamSynchronize(st));
-    for (size_t i = 0; i < pending.size(); ++i) {
-      std::vector<uint8_t>& held = b->ss[pending[i].first].agg_held;
-      held.insert(held.end(), pend_bytes[i].begin(), pend_bytes[i].end());
+    for (const auto& pe : pending) {
+      std::vector<uint8_t>& held = b->ss[pe.first].agg_held;
+      held.insert(held.end(), b->h_pend.p + pe.second.dst, b->h_pend.p + pe.second.dst + pe.second.len);
     }
   }
   return WSG_API_OK;
@@ -805,10 +819,10 @@ int wsg_batcher_close(wsg_batcher* b) {
     if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
   }
   b->st.release();
-  DBuf* dbufs[] = {&b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->d_sf, &b->d_desc,
+  DBuf* dbufs[] = {&b->d_pend, &b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->d_sf, &b->d_desc,
                    &b->d_odesc, &b->d_res, &b->d_ores, &b->d_rf, &b->d_ooff, &b->d_tot};
   for (DBuf* d : dbufs) d->release();
-  PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot};
+  PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot, &b->h_pend};
   for (PinnedBuf* p : hbufs) p->release();
   if (b->s_dl) {
     (void)hipStreamSynchronize(b->s_dl);
