@@ -206,7 +206,7 @@ constexpr uint32_t COPY_MAX = 65536;
 // One workgroup per copy.  Output slots are 16-B aligned; a source is 16-B aligned when
 // it is a decoder payload slot, byte-aligned when it is inflated output (messages back
 // to back), so the widest access both sides allow is used.
-constexpr uint32_t GATHER_GROUPS = 32;  // workgroups of the output gather: enough to fill PCIe, few enough
+constexpr uint32_t GATHER_GROUPS = 12;  // workgroups of the output gather: enough to fill PCIe, few enough
                                          // that the next flush's small downloads still get a share of it
 
 __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
