@@ -37,6 +37,26 @@
 #include <immintrin.h>
 #endif
 
+// -DWSG_STAGE_PROF (a measurement build, scripts/build_variant.sh): host time of each
+// stage-chain phase, summed per batcher and printed at close.
+#ifdef WSG_STAGE_PROF
+#include <chrono>
+#include <cstdio>
+static double g_sp[16];
+static const char* g_sp_name[16] = {"compute", "inflate.input", "inflate.kernels+sync", "inflate.results",
+                                    "validate", "aggregate", "fin.list", "gather.launch", "finish.sync", "wait.total",
+                                    "precompute", "gather.pay_ensure", "gather.upload", "inflate.x", "", ""};
+struct SpT {
+  int i;
+  std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
+  explicit SpT(int k) : i(k) {}
+  ~SpT() { g_sp[i] += std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count(); }
+};
+#define SP(k) SpT sp_##k(k)
+#else
+#define SP(k) (void)0
+#endif
+
 namespace {
 
 struct PinnedBuf {
@@ -452,6 +472,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     }
     x.sf[S] = (uint32_t)x.desc.size();
     const uint64_t F = x.desc.size();
+    SP(13);
     B_TRY(b, b->ar->grow_keep(ipos + oo[S] + 64, ipos, st));
     B_TRY(b, upload(b->d_desc, x.desc, st));
     B_TRY(b, upload(b->d_sf, x.sf, st));
@@ -471,7 +492,10 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     if (F) B_TRY(b, hipMemcpyAsync(b->h_odesc.p, b->d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, st));
     B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
     B_TRY(b, hipMemcpyAsync(b->h_rf.p, b->d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    B_TRY(b, hipStreamSynchronize(st));
+    {
+      SP(2);
+      B_TRY(b, hipStreamSynchronize(st));
+    }
     const wsg_frame_desc* odesc = (const wsg_frame_desc*)b->h_odesc.p;
     const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
     const uint32_t* rf = (const uint32_t*)b->h_rf.p;
@@ -546,6 +570,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
 // FrameUtf8Validator over `cur` (FrameUtf8Validator.java:59-98), on the device: the
 // frames a session passes before its first failure go on.
 static int stage_validate(wsg_batcher* b, StageList& cur, uint64_t used) {
+  SP(4);
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
   B_TRY(b, upload(b->d_desc, cur.desc, st));
@@ -586,6 +611,7 @@ static void fin_push(wsg_batcher* b, wsg_frame_desc d, uint64_t src, uint32_t de
 // into the output list: pass-through frames keep their bytes, an aggregated message is
 // its held bytes (earlier batches, PayloadAggregator.java:34) + this batch's.
 static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
+  SP(5);
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
   const uint64_t F = cur.desc.size();
@@ -686,6 +712,7 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
 // aggregator on the device, then one gather, and the download of what the handler
 // receives queued on the download stream (collected by stage_finish).
 static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
+  SP(0);
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
   StageOut& o = f.so;
@@ -746,6 +773,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
     }
   }
   o.sf[S] = (uint32_t)o.desc.size();
+  SP(7);
   // the output: gathered from this flush's arena straight into the pinned host buffer
   // by a few workgroups on the download stream (PCIe writes), so the next flush's
   // stages have the GPU meanwhile (a runtime D2H here is a blit kernel that takes
@@ -753,9 +781,15 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   if (!o.gathered) B_TRY(b, hipEventCreateWithFlags(&o.gathered, hipEventDisableTiming));
   if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, hipEventDisableTiming));
   if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
-  B_TRY(b, o.pay.ensure(o.len + 16));
+  {
+    SP(11);
+    B_TRY(b, o.pay.ensure(o.len + 16));
+  }
   if (!o.copies.empty()) {
-    B_TRY(b, upload(o.d_copy, o.copies, st));
+    {
+      SP(12);
+      B_TRY(b, upload(o.d_copy, o.copies, st));
+    }
     B_TRY(b, hipEventRecord(o.gathered, st));
     B_TRY(b, hipStreamWaitEvent(b->s_dl, o.gathered, 0));
     uint8_t* dst = nullptr;
@@ -772,6 +806,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
 
 // Wait for a flush's stage output and put in the bytes only the host holds.
 static int stage_finish(wsg_batcher* b, FlushSlot& f) {
+  SP(8);
   StageOut& o = f.so;
   B_TRY(b, hipEventSynchronize(o.downloaded));
   for (auto& hp : o.host_parts)
@@ -829,6 +864,10 @@ int wsg_batcher_close(wsg_batcher* b) {
     (void)hipStreamDestroy(b->s_dl);
   }
   if (b->sctx) (void)wsg_close(b->sctx);
+#ifdef WSG_STAGE_PROF
+  for (int i = 0; i < 16; ++i)
+    if (g_sp[i] > 0) fprintf(stderr, "[stage prof] %-22s %9.3f ms\n", g_sp_name[i], g_sp[i]);
+#endif
   delete b;
   return WSG_API_OK;
 }
@@ -1131,6 +1170,7 @@ static void adjusted_results(wsg_batcher* b, const FlushSlot& g, std::vector<wsg
 }
 
 int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
+  SP(9);
   if (!b || !out) return WSG_API_EINVAL;
   if (b->q.empty()) return bset(b, WSG_API_ERANGE, "no flush in flight");
   const int slot = b->q.front();
@@ -1190,6 +1230,7 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   if (!b->q.empty()) {
     FlushSlot& g = b->fs[b->q.front()];
     if (!g.so.staged && hipEventQuery(g.done) == hipSuccess) {
+      SP(10);
       std::vector<wsg_session_result> gres;
       adjusted_results(b, g, gres);
       if ((rc2 = stage_compute(b, g, gres.data()))) return rc2;
