@@ -283,6 +283,27 @@ def test_inflate_fragmented_messages_predecoded(ctx, oracle, no_context):
     _run(ctx, oracle, sessions, no_context, 2, rng)
 
 
+def test_inflate_after_reserve(oracle):
+    """wsg_reserve_inflate pre-sizes the lane pre-decode's workspace (token and literal
+    regions, table pool, order): a batch within the reservation decodes as without it."""
+    from snf4j_amd import Context
+    rng = np.random.default_rng(9200)
+    sessions = []
+    for i in range(24):
+        comp = zlib.compressobj(6, zlib.DEFLATED, -15)
+        frames = []
+        for m in range(int(rng.integers(1, 6))):
+            body = wsgen.rand_text(rng, int(rng.integers(50, 2500)))
+            frames.append((1, True, 4, (comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH))[:-4]))
+        sessions.append(frames)
+    c = Context(0)
+    try:
+        c.reserve_inflate(4096, 64, 1 << 22)
+        _run(c, oracle, sessions, False, 2, rng)
+    finally:
+        c.close()
+
+
 @pytest.mark.parametrize("tabs", [0, 5])
 def test_inflate_table_pool_exhausted(oracle, tabs):
     """Multi-frame compressed messages need the lane pre-decode's HBM tables, taken from a
