@@ -1107,11 +1107,12 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
   return err;
 }
 
-template <int NT, int XCD, int N>
-__global__ __launch_bounds__(64) void k_piecesN(DecodeArgs a) {
-  const int lane = threadIdx.x;
+template <int NT, int XCD, int N, int WPB = 1>
+__global__ __launch_bounds__(64 * WPB) void k_piecesN(DecodeArgs a) {
+  const int lane = threadIdx.x & 63;
   const uint32_t blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
-  const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(blk);
+  const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(blk * (uint32_t)WPB + (threadIdx.x >> 6));
+  if (WPB > 1 && p >= a.n_pieces) return;  // (a wave of the last workgroup past the grid)
   PieceDesc d[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) d[i] = a.pieces[p + i];
@@ -1229,21 +1230,29 @@ void launch_link(const DecodeArgs& a, hipStream_t s) {
   if (a.validator_only) hipLaunchKernelGGL(k_vlink, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
   else hipLaunchKernelGGL(k_link, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
+#ifndef WSG_DWPB
+#define WSG_DWPB 1  // waves a workgroup of the decode piece kernel (A/B build switch)
+#endif
 void launch_pieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
   // one 64-lane workgroup per two pieces, nontemporal loads/stores, XCD-aware
   // (fastest in tools/ubench_unmask: 2 KiB in flight per wave)
-  hipLaunchKernelGGL((k_piecesN<1, 1, PIECES_PER_WAVE>),
-                     dim3((uint32_t)((n_pieces_bound + PIECES_PER_WAVE - 1) / PIECES_PER_WAVE)), dim3(64), 0, s, a);
+  const uint64_t waves = (n_pieces_bound + PIECES_PER_WAVE - 1) / PIECES_PER_WAVE;
+  hipLaunchKernelGGL((k_piecesN<1, 1, PIECES_PER_WAVE, WSG_DWPB>), dim3((uint32_t)((waves + WSG_DWPB - 1) / WSG_DWPB)),
+                     dim3(64 * WSG_DWPB), 0, s, a);
 }
 void launch_vparse(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_vparse, dim3(a.nblk), dim3(DBLOCK), 0, s, a);
 }
+#ifndef WSG_VWPB
+#define WSG_VWPB 1  // waves a workgroup of the validate-only piece kernel (A/B build switch)
+#endif
 void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
   // validate only: the piece kernel with its stores compiled out (NT bit 2)
   // (read-only streaming wants more bytes in flight per wave than the copy does:
   // VPIECES_PER_WAVE KiB)
-  hipLaunchKernelGGL((k_piecesN<5, 1, VPIECES_PER_WAVE>),
-                     dim3((uint32_t)((n_pieces_bound + VPIECES_PER_WAVE - 1) / VPIECES_PER_WAVE)), dim3(64), 0, s, a);
+  const uint64_t waves = (n_pieces_bound + VPIECES_PER_WAVE - 1) / VPIECES_PER_WAVE;
+  hipLaunchKernelGGL((k_piecesN<5, 1, VPIECES_PER_WAVE, WSG_VWPB>), dim3((uint32_t)((waves + WSG_VWPB - 1) / WSG_VWPB)),
+                     dim3(64 * WSG_VWPB), 0, s, a);
 }
 void launch_final(const DecodeArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_final, dim3((a.n_sessions + 255) / 256), dim3(256), 0, s, a);
