@@ -1107,8 +1107,8 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
   return err;
 }
 
-template <int NT, int XCD, int N, int WPB = 1>
-__global__ __launch_bounds__(64 * WPB) void k_piecesN(DecodeArgs a) {
+template <int NT, int XCD, int N, int WPB = 1, int MINW = 1>
+__global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW))) void k_piecesN(DecodeArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(blk * (uint32_t)WPB + (threadIdx.x >> 6));
@@ -1246,12 +1246,15 @@ void launch_vparse(const DecodeArgs& a, hipStream_t s) {
 #ifndef WSG_VWPB
 #define WSG_VWPB 1  // waves a workgroup of the validate-only piece kernel (A/B build switch)
 #endif
+#ifndef WSG_VMINW
+#define WSG_VMINW 1  // its minimum waves a SIMD (a register budget: 8 -> 64 VGPRs; A/B build switch)
+#endif
 void launch_vpieces(const DecodeArgs& a, hipStream_t s, uint64_t n_pieces_bound) {
   // validate only: the piece kernel with its stores compiled out (NT bit 2)
   // (read-only streaming wants more bytes in flight per wave than the copy does:
   // VPIECES_PER_WAVE KiB)
   const uint64_t waves = (n_pieces_bound + VPIECES_PER_WAVE - 1) / VPIECES_PER_WAVE;
-  hipLaunchKernelGGL((k_piecesN<5, 1, VPIECES_PER_WAVE, WSG_VWPB>), dim3((uint32_t)((waves + WSG_VWPB - 1) / WSG_VWPB)),
+  hipLaunchKernelGGL((k_piecesN<5, 1, VPIECES_PER_WAVE, WSG_VWPB, WSG_VMINW>), dim3((uint32_t)((waves + WSG_VWPB - 1) / WSG_VWPB)),
                      dim3(64 * WSG_VWPB), 0, s, a);
 }
 void launch_final(const DecodeArgs& a, hipStream_t s) {
