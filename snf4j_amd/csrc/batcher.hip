@@ -15,8 +15,11 @@
 // H2D, decode, D2H) without gathering anything; up to two batches are in flight
 // while the next one is fed.  Per-session decoder state (fragmentation, UTF-8
 // carry, closed) chains through the batches on the device.  The stages after the
-// decoder (inflate, validator, aggregator) and the cross-session encode batcher
-// are here too.
+// decoder (inflate, validator, aggregator) run on the device over the decoded
+// payloads, on a context of their own, with their per-session carry device-resident;
+// one gather writes what the handler receives into pinned memory while the next
+// flush's stages run.  The cross-session encode batcher (pipelined the same way)
+// and the loop -> device policy are here too.
 #include <string.h>
 
 #include <algorithm>
