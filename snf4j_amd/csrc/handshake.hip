@@ -29,6 +29,13 @@ struct Span {
 // A lane's view of its request: bytes come from 16-B aligned blocks held in
 // registers, so a forward scan costs one load per 16 bytes instead of one per byte
 // (the batch buffer is 16-B aligned: a block never leaves the allocation's granule).
+// waves a SIMD the kernels are built for (their register budget; A/B build switches)
+#ifndef WSG_HS_WAVES
+#define WSG_HS_WAVES 6  // k_hs_accept: 80 VGPRs (some spill), 6 waves a SIMD: 2.12 -> 1.87 ms (4, 5, 7, 8 measured slower: DESIGN 8b)
+#endif
+#ifndef WSG_HS_VWAVES
+#define WSG_HS_VWAVES 4
+#endif
 struct Req {
   const uint4* base;  // the aligned block holding byte 0
   uint32_t lead;      // byte 0's offset in that block
@@ -627,7 +634,7 @@ __device__ __forceinline__ void accept_one(Req& d, int64_t n, const wsg_hs_confi
   res->resp_len = (uint16_t)rl;
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_hs_accept(wsg_hs_config cfg, const uint8_t* req, const uint64_t* req_off,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WSG_HS_WAVES))) void k_hs_accept(wsg_hs_config cfg, const uint8_t* req, const uint64_t* req_off,
                                                    uint32_t n, uint8_t* resp, wsg_hs_result* result) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -900,7 +907,7 @@ __device__ __forceinline__ void validate_one(Req& d, int64_t n, const wsg_hs_con
   finish(WSG_HS_FINISHED, WSG_HSC_NONE, none);
 }
 
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void k_hs_validate(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WSG_HS_VWAVES))) void k_hs_validate(
     wsg_hs_config cfg, const uint8_t* resp, const uint64_t* resp_off, const uint8_t* keys, uint32_t n,
     uint8_t* expected, wsg_hs_result* result) {
   const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
