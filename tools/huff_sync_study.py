@@ -151,6 +151,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--sessions", type=int, default=16)
     ap.add_argument("--fractions", type=float, nargs="+", default=[0.25, 0.5, 0.75])
+    ap.add_argument("--restart", action="store_true",
+                    help="a speculative decode that hits an invalid code, or an end of block more than "
+                         "--eob-slack bits before the stream's end, restarts one bit after where it "
+                         "started (the lane cannot tell a false end of block otherwise)")
+    ap.add_argument("--eob-slack", type=int, default=48)
+    ap.add_argument("--window", type=int, default=1024, help="bits after the start a sync is looked for in")
     a = ap.parse_args()
     from benchsupport.synth import deflate_batch
     desc, sf, payload, plain = deflate_batch(0x1F1A, a.sessions, 16, 4096, unique=a.sessions)
@@ -188,14 +194,25 @@ def main():
         for f in a.fractions:
             total += 1
             start = p0 + int((end - p0) * f)
-            spec, _, _ = symbols(bits, start, tabs, limit=4096)
-            # (a literal/length boundary: at a distance code the length before it would differ)
-            hit = next((i for i, bnd in enumerate(spec) if bnd[1] == 0 and bnd in true_set), None)
+            wasted = 0  # codes decoded by starts that were abandoned
+            for _ in range(64 if a.restart else 1):
+                spec, _, ok = symbols(bits, start, tabs, limit=4096)
+                # (a literal/length boundary: at a distance code the length before it would differ)
+                hit = next((i for i, bnd in enumerate(spec) if bnd[1] == 0 and bnd in true_set
+                            and bnd[0] - start < a.window), None)
+                if hit is not None or not a.restart:
+                    break
+                # what the lane sees: an invalid code, or an end of block far from the stream's end
+                last = spec[-1][0] if spec else start
+                if ok and bits.n - last <= a.eob_slack:
+                    break  # a plausible end: the lane would stop here (no sync: the head decodes alone)
+                wasted += len(spec)
+                start += 1
             if hit is None:
                 never += 1
             else:
-                sync_syms.append(hit)
-                sync_bits.append(spec[hit][0] - start)
+                sync_syms.append(hit + wasted)
+                sync_bits.append(spec[hit][0] - (p0 + int((end - p0) * f)))
     ss, sb = np.array(sync_syms), np.array(sync_bits)
     print(f"messages {len(desc)}, blocks per message: mean {np.mean(blocks_per_msg):.2f}, max {max(blocks_per_msg)}")
     print(f"speculative starts {total}: synchronised {len(ss)}, never within the block {never}")
