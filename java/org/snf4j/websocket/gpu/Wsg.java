@@ -146,6 +146,12 @@ final class Wsg {
 	/** wsg_enc_batcher_flush: views = {session_first, wire_off, wire} (valid until the next add / flush). */
 	static native int encBatcherFlush(long batcher, ByteBuffer[] views);
 
+	/** wsg_enc_batcher_flush_async: queue the encode of everything added so far (at most two in flight). */
+	static native int encBatcherFlushAsync(long batcher);
+
+	/** wsg_enc_batcher_wait: the oldest in-flight flush's views (null: discard them). */
+	static native int encBatcherWait(long batcher, ByteBuffer[] views);
+
 	static native int encBatcherSessionReset(long batcher, int sid);
 
 	/* ---- encode: wsg_encoded_length / wsg_encode_batch_host ---- */

@@ -11,7 +11,9 @@
  * loop's task phase (InternalSelectorLoop.java:641, 751-758), after every read of
  * the iteration: one device batch per native batcher for every session that read
  * (gather to pinned staging, H2D, decode + UTF-8 kernels and the batched stages
- * after them, D2H), then one encode batch for every session that wrote.  Frames
+ * after them, D2H), then one encode batch for every session that wrote, queued on
+ * the device and written to the sockets by the next iteration's flush (the loop does
+ * not wait for it; a CLOSE frame first writes out everything before it).  Frames
  * go back to each session in order, through the rest of its codec pipeline, as
  * DefaultCodecExecutor.decode (DefaultCodecExecutor.java:557-584) and
  * CodecExecutorAdapter.read (CodecExecutorAdapter.java:228-254) would have passed
@@ -28,6 +30,7 @@ package org.snf4j.websocket.gpu;
 
 import java.nio.ByteBuffer;
 import java.nio.ByteOrder;
+import java.util.ArrayDeque;
 import java.util.ArrayList;
 import java.util.HashMap;
 import java.util.LinkedHashSet;
@@ -117,6 +120,8 @@ public final class WsgBatcher {
 		final GpuFrameEncoder[] slots;
 		int next;
 		final Set<GpuFrameEncoder> dirty = new LinkedHashSet<GpuFrameEncoder>();
+		/** The encoders of each flush on the device (wsg_enc_batcher_flush_async), oldest first. */
+		final ArrayDeque<List<GpuFrameEncoder>> inflight = new ArrayDeque<List<GpuFrameEncoder>>();
 
 		EncNative(boolean clientMode) {
 			handle = Wsg.encBatcherOpen(ctx, clientMode, maxSessions);
@@ -264,11 +269,17 @@ public final class WsgBatcher {
 		schedule();
 	}
 
-	/** True if the encoder's session has frames queued (later frames must queue behind them). */
+	/** True if the encoder's session has frames queued or on the device (later frames must queue behind them). */
 	synchronized boolean hasQueued(GpuFrameEncoder e) {
-		for (EncNative n : encNatives)
-			if (n != null && n.dirty.contains(e))
+		for (EncNative n : encNatives) {
+			if (n == null)
+				continue;
+			if (n.dirty.contains(e))
 				return true;
+			for (List<GpuFrameEncoder> f : n.inflight)
+				if (f.contains(e))
+					return true;
+		}
 		return false;
 	}
 
@@ -283,8 +294,11 @@ public final class WsgBatcher {
 
 	/**
 	 * One device batch per native batcher; frames go back to their sessions, bytes to
-	 * the sockets.  The decode batches are queued first (wsg_batcher_flush_async), the
-	 * encode batch runs while they are on the device, then each decode is collected.
+	 * the sockets.  The decode batches are queued first (wsg_batcher_flush_async); the
+	 * encode batch queued by the previous flush is written out and this iteration's is
+	 * queued (wsg_enc_batcher_flush_async: its bytes go out one loop iteration later,
+	 * so the loop does not wait for its H2D, kernels and D2H); then each decode is
+	 * collected.
 	 */
 	synchronized void flush() {
 		flushScheduled = false;
@@ -297,7 +311,7 @@ public final class WsgBatcher {
 				throw new IllegalStateException("wsg_batcher_flush_async: " + rc);
 			queued.add(n);
 		}
-		flushEncodes();
+		flushEncodesAsync();
 		collectDecodes(queued);
 	}
 
@@ -332,32 +346,74 @@ public final class WsgBatcher {
 		}
 	}
 
-	/** Encode every queued frame (also called by an encoder before it writes a CLOSE frame). */
+	/**
+	 * Encode every queued frame and write it now (an encoder calls this before it writes
+	 * a CLOSE frame, so what was written before the CLOSE goes out first).
+	 */
 	synchronized void flushEncodes() {
 		ByteBuffer[] views = new ByteBuffer[3];
 		for (EncNative n : encNatives) {
-			if (n == null || n.dirty.isEmpty())
+			if (n == null)
+				continue;
+			while (!n.inflight.isEmpty())
+				collectEncode(n, views);
+			if (n.dirty.isEmpty())
 				continue;
 			int rc = Wsg.encBatcherFlush(n.handle, views);
 			if (rc != 0)
 				throw new IllegalStateException("wsg_enc_batcher_flush: " + rc);
-			ByteBuffer sf = views[0].order(ByteOrder.LITTLE_ENDIAN);
-			ByteBuffer off = views[1].order(ByteOrder.LITTLE_ENDIAN);
-			ByteBuffer wire = views[2];
 			List<GpuFrameEncoder> es = new ArrayList<GpuFrameEncoder>(n.dirty);
 			n.dirty.clear();
-			for (GpuFrameEncoder e : es) {
-				long from = off.getLong(8 * sf.getInt(4 * e.sid)), to = off.getLong(8 * sf.getInt(4 * (e.sid + 1)));
-				int len = (int) (to - from);
-				IStreamSession session = e.session();
-				if (len == 0 || session == null)
-					continue;
-				ByteBuffer out = session.allocate(len);  // FrameEncoder.java:78: the session's allocator
-				ByteBuffer src = wire.duplicate();
-				src.position((int) from).limit((int) to);
-				out.put(src).flip();
-				session.writenf(out);  // no Frame encoder takes a ByteBuffer: straight to the socket
-			}
+			write(n, es, views);
+		}
+	}
+
+	/** The flush's step for the encode side: the previous flush's bytes out, this one's queued. */
+	private void flushEncodesAsync() {
+		ByteBuffer[] views = new ByteBuffer[3];
+		for (EncNative n : encNatives) {
+			if (n == null)
+				continue;
+			while (!n.inflight.isEmpty())
+				collectEncode(n, views);
+			if (n.dirty.isEmpty())
+				continue;
+			int rc = Wsg.encBatcherFlushAsync(n.handle);
+			if (rc != 0)
+				throw new IllegalStateException("wsg_enc_batcher_flush_async: " + rc);
+			n.inflight.add(new ArrayList<GpuFrameEncoder>(n.dirty));
+			n.dirty.clear();
+			schedule();  // the next iteration's flush writes it out, whatever else arrives
+		}
+	}
+
+	/** The oldest in-flight encode flush of n: its bytes to their sessions' sockets. */
+	private void collectEncode(EncNative n, ByteBuffer[] views) {
+		int rc = Wsg.encBatcherWait(n.handle, views);
+		if (rc != 0)
+			throw new IllegalStateException("wsg_enc_batcher_wait: " + rc);
+		write(n, n.inflight.poll(), views);
+	}
+
+	/** Each encoder's frames of a flush's views, in one buffer, to its session. */
+	private void write(EncNative n, List<GpuFrameEncoder> es, ByteBuffer[] views) {
+		ByteBuffer sf = views[0].order(ByteOrder.LITTLE_ENDIAN);
+		ByteBuffer off = views[1].order(ByteOrder.LITTLE_ENDIAN);
+		ByteBuffer wire = views[2];
+		for (GpuFrameEncoder e : es) {
+			// a session reset since (unregister, slot reuse) dropped its frames from the view
+			if (e.sid < 0 || n.slots[e.sid] != e)
+				continue;
+			long from = off.getLong(8 * sf.getInt(4 * e.sid)), to = off.getLong(8 * sf.getInt(4 * (e.sid + 1)));
+			int len = (int) (to - from);
+			IStreamSession session = e.session();
+			if (len == 0 || session == null)
+				continue;
+			ByteBuffer out = session.allocate(len);  // FrameEncoder.java:78: the session's allocator
+			ByteBuffer src = wire.duplicate();
+			src.position((int) from).limit((int) to);
+			out.put(src).flip();
+			session.writenf(out);  // no Frame encoder takes a ByteBuffer: straight to the socket
 		}
 	}
 
@@ -393,6 +449,10 @@ public final class WsgBatcher {
 		natives.clear();
 		for (int i = 0; i < encNatives.length; ++i)
 			if (encNatives[i] != null) {
+				while (!encNatives[i].inflight.isEmpty()) {  // the device work ends before the batcher does
+					Wsg.encBatcherWait(encNatives[i].handle, null);
+					encNatives[i].inflight.poll();
+				}
 				Wsg.encBatcherClose(encNatives[i].handle);
 				encNatives[i] = null;
 			}

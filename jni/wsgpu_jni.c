@@ -249,12 +249,8 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherAdd(JNIEnv* en
     return rc;
 }
 
-/* views[0] = session_first, views[1] = wire_off, views[2] = wire (valid until the next add/flush) */
-JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherFlush(JNIEnv* env, jclass c, jlong b,
-                                                                        jobjectArray views) {
-    wsg_enc_view v;
-    int rc = wsg_enc_batcher_flush(ENC_BATCHER(b), &v);
-    if (rc != WSG_API_OK) return rc;
+static void enc_views(JNIEnv* env, jobjectArray views, const wsg_enc_view* pv) {
+    const wsg_enc_view v = *pv;
     (*env)->SetObjectArrayElement(env, views, 0,
                                   (*env)->NewDirectByteBuffer(env, (void*)v.session_first,
                                                               (jlong)(v.n_sessions + 1) * sizeof(uint32_t)));
@@ -263,6 +259,30 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherFlush(JNIEnv* 
                                                               (jlong)(v.n_frames + 1) * sizeof(uint64_t)));
     (*env)->SetObjectArrayElement(env, views, 2,
                                   (*env)->NewDirectByteBuffer(env, (void*)v.wire, (jlong)v.wire_bytes));
+}
+
+/* views[0] = session_first, views[1] = wire_off, views[2] = wire (valid until the next add/flush) */
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherFlush(JNIEnv* env, jclass c, jlong b,
+                                                                        jobjectArray views) {
+    wsg_enc_view v;
+    int rc = wsg_enc_batcher_flush(ENC_BATCHER(b), &v);
+    if (rc != WSG_API_OK) return rc;
+    enc_views(env, views, &v);
+    return WSG_API_OK;
+}
+
+/* pipelined form: flushAsync queues the encode of everything added so far; wait
+ * returns the oldest in-flight flush's views (valid until that slot flushes again) */
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherFlushAsync(JNIEnv* env, jclass c, jlong b) {
+    return wsg_enc_batcher_flush_async(ENC_BATCHER(b));
+}
+
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherWait(JNIEnv* env, jclass c, jlong b,
+                                                                       jobjectArray views) {
+    wsg_enc_view v;
+    int rc = wsg_enc_batcher_wait(ENC_BATCHER(b), &v);
+    if (rc != WSG_API_OK) return rc;
+    if (views) enc_views(env, views, &v);
     return WSG_API_OK;
 }
 

@@ -104,3 +104,20 @@ def test_java_messages_match_the_python_mirror():
             continue
         text = MESSAGES[code].split("{")[0].rstrip(" (")
         assert text in java, (code, text)
+
+
+def test_encode_flush_is_pipelined():
+    """The loop's flush queues the encode batch (wsg_enc_batcher_flush_async) and writes
+    the previous one out (wsg_enc_batcher_wait) one iteration later; a CLOSE frame
+    (flushEncodes) first drains what is in flight, so writes keep their order."""
+    b = _java("WsgBatcher.java")
+    flush = b[b.index("synchronized void flush()"):b.index("private void collectDecodes")]
+    assert "flushEncodesAsync();" in flush and "flushEncodes();" not in flush
+    asy = b[b.index("private void flushEncodesAsync()"):b.index("private void collectEncode")]
+    assert asy.index("collectEncode(n, views)") < asy.index("Wsg.encBatcherFlushAsync(n.handle)")
+    assert "n.inflight.add(" in asy and "schedule();" in asy
+    sync = b[b.index("synchronized void flushEncodes()"):b.index("private void flushEncodesAsync()")]
+    assert sync.index("collectEncode(n, views)") < sync.index("Wsg.encBatcherFlush(n.handle, views)")
+    assert "n.inflight" in b[b.index("synchronized boolean hasQueued"):b.index("private void schedule()")]
+    jni = _read("jni/wsgpu_jni.c")
+    assert "wsg_enc_batcher_flush_async(ENC_BATCHER(b))" in jni and "wsg_enc_batcher_wait(ENC_BATCHER(b), &v)" in jni
