@@ -11,6 +11,8 @@
 // lines the first pass brought in).  No LDS, no cross-lane traffic.  The lane
 // decides every request whose form it can reproduce exactly and defers the rest to
 // the Java Handshaker (wsgpu.h lists the deferred forms).
+#include <type_traits>
+
 #include "wsgpu_internal.h"
 
 namespace ws {
@@ -31,7 +33,7 @@ struct Span {
 // (the batch buffer is 16-B aligned: a block never leaves the allocation's granule).
 // waves a SIMD the kernels are built for (their register budget; A/B build switches)
 #ifndef WSG_HS_WAVES
-#define WSG_HS_WAVES 6  // k_hs_accept: 80 VGPRs (some spill), 6 waves a SIMD: 2.12 -> 1.87 ms (4, 5, 7, 8 measured slower: DESIGN 8b)
+#define WSG_HS_WAVES 6  // k_hs_accept: 79 VGPRs, 6 waves a SIMD: 2.12 -> 1.79 ms with key_words (4, 5, 7, 8 slower: DESIGN 8b)
 #endif
 #ifndef WSG_HS_VWAVES
 #define WSG_HS_VWAVES 4
@@ -168,6 +170,35 @@ __device__ __forceinline__ void sha1_block(uint32_t h[5], const uint32_t w0[16])
   h[0] += a; h[1] += b; h[2] += c; h[3] += dd; h[4] += e;
 }
 
+#ifndef WSG_HS_KEY_BLOCKS
+#define WSG_HS_KEY_BLOCKS 1  // 0: the key bytes one by one through Req (A/B)
+#endif
+// The KL key bytes at request offset kb as big-endian words, from the (at most three)
+// 16-B blocks that hold them: loaded once and funnel-shifted with selects (no
+// dynamically indexed register array), instead of a byte-at-a-time walk whose block
+// reloads the compiler kept as separate spilled copies.  Only blocks holding key
+// bytes are loaded (they hold request bytes, so they stay in the allocation).
+template <int KL>
+__device__ __forceinline__ void key_words(const Req& d, int32_t kb, uint32_t* kw) {
+  const uint32_t a0 = d.lead + (uint32_t)kb, sh = a0 & 15u;
+  const uint4* const blk = d.base + (a0 >> 4);
+  const uint4 b0 = blk[0], b1 = blk[1];  // (sh + KL > 16: KL >= 22)
+  const uint4 b2 = sh + (uint32_t)KL > 32u ? blk[2] : make_uint4(0u, 0u, 0u, 0u);
+  const uint32_t W[12] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w, b2.x, b2.y, b2.z, b2.w};
+  const uint32_t qd = sh >> 2, sb = sh & 3u;
+  uint32_t V[(KL + 3) / 4 + 1];
+#pragma unroll
+  for (int j = 0; j < (KL + 3) / 4 + 1; ++j)
+    V[j] = qd == 0u ? W[j] : (qd == 1u ? W[j + 1] : (qd == 2u ? W[j + 2] : W[j + 3]));
+#pragma unroll
+  for (int j = 0; j < (KL + 3) / 4; ++j) {
+    const uint32_t le = __builtin_amdgcn_alignbyte(V[j + 1], V[j], sb);  // key bytes 4j..4j+3
+    uint32_t be = __builtin_bswap32(le);
+    if (4 * j + 4 > KL) be &= 0xffffffffu << (8 * (4 * j + 4 - KL));  // bytes past the key: zero
+    kw[j] = be;
+  }
+}
+
 // Sec-WebSocket-Accept = Base64(SHA1(key + GUID)) (HandshakeUtils.generateAnswerKey,
 // HandshakeUtils.java:98-111): 28 characters to the response.  Specialised on the key length,
 // so that every message byte's source (key byte, GUID constant, padding) is known at
@@ -176,12 +207,19 @@ template <int KL, class S, class O>
 __device__ __forceinline__ void accept_key_n(S& d, int32_t kb, O& out) {
   constexpr int total = KL + 36;  // <= 60: two blocks after padding
   uint32_t kw[(KL + 3) / 4];      // the key bytes, big-endian words
+#if WSG_HS_KEY_BLOCKS
+  if constexpr (std::is_same<S, Req>::value) {
+    key_words<KL>(d, kb, kw);
+  } else
+#endif
+  {
 #pragma unroll
-  for (int j = 0; j < (KL + 3) / 4; ++j) {
-    uint32_t v = 0;
+    for (int j = 0; j < (KL + 3) / 4; ++j) {
+      uint32_t v = 0;
 #pragma unroll
-    for (int q = 0; q < 4; ++q) v = (v << 8) | (j * 4 + q < KL ? (uint32_t)d[kb + j * 4 + q] : 0u);
-    kw[j] = v;
+      for (int q = 0; q < 4; ++q) v = (v << 8) | (j * 4 + q < KL ? (uint32_t)d[kb + j * 4 + q] : 0u);
+      kw[j] = v;
+    }
   }
   uint32_t h[5] = {0x67452301u, 0xEFCDAB89u, 0x98BADCFEu, 0x10325476u, 0xC3D2E1F0u};
 #pragma unroll
