@@ -1181,9 +1181,52 @@ def e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev, reps=6):
                                     "threaded by session) + wsg_batcher_flush_async (H2D, decode, D2H of the "
                                     "arena, no gather), two flushes in flight"}
     nb.close()
+    out["drop_in_loop"] = e2e_loop_line(pctx, rounds, wire_bytes, F, n_s)
     pctx.close()
     out["path"] = "pinned host wire -> H2D -> decode -> D2H payload region + descriptors + results + state"
     return out
+
+
+def e2e_loop_line(pctx, rounds, wire_bytes, F, n_s):
+    """The drop-in's own call pattern (WsgBatcher.java, restated in snf4j_amd/loop.py):
+    per loop iteration the reads are recorded, the flush task feeds them in one
+    wsg_batcher_feed_many, delivers every earlier flush whose device work finished
+    (waiting only when two are in flight), queues this one and hands its ticket to the
+    completion thread, which re-enters the loop (executenf) when it is done.  The same
+    socket reads as native_batcher (one 64 KiB read per session an iteration), wire
+    bytes of all iterations / the time from the first read to the last delivery."""
+    import numpy as np
+    from snf4j_amd.loop import LoopBatcher, SelectorLoop, run_until_idle
+    got = {"wire": 0, "frames": 0}
+
+    def deliver(_sid, views, _exc):
+        _, desc, _, res, w = views
+        assert int(res["error"].max()) == 0
+        got["wire"] += w
+        got["frames"] += len(desc)
+
+    best = None
+    for rnd in range(3):  # round 0 sizes the pinned buffers; the best of two timed rounds
+        loop = SelectorLoop()
+        lb = LoopBatcher(loop, n_s, deliver, ctx=pctx, raw=True)
+        got["wire"] = got["frames"] = 0
+        t0 = time.perf_counter()
+        for sids, ptrs, lens in rounds:
+            loop.run_iteration([lambda s=sids, p=ptrs, ln=lens: lb.enqueue_many_ptr(s, p, ln)])
+        run_until_idle(loop, lb, timeout=120)
+        t = time.perf_counter() - t0
+        st = dict(lb.stats)
+        lb.close()
+        assert got["wire"] == wire_bytes and got["frames"] == F, (got, wire_bytes, F)
+        if rnd and (best is None or t < best[0]):
+            best = (t, st)
+    t, st = best
+    return {"GiB_per_s": round(wire_bytes / t / 2**30, 3), "total_s": round(t, 4), "iterations": len(rounds),
+            "flushes": st["flushes"], "collected_in_a_later_iteration": st["collected_later"],
+            "collected_blocking": st["collected_blocking"],
+            "api": "WsgBatcher's scheduling (snf4j_amd/loop.py): per iteration one wsg_batcher_feed_many of the "
+                   "recorded reads, finished flushes collected via wsg_batcher_await(0), flush_async + a "
+                   "completion thread re-entering the loop; the rate a Java selector loop gets"}
 
 
 if __name__ == "__main__":

@@ -386,6 +386,26 @@ int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, cons
 int wsg_batcher_flush_async(wsg_batcher* b);
 int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out);
 int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* st);
+/* Completion across threads (the selector loop must not block on the device):
+ * flush_async queues flush number t = 1, 2, ...; wsg_batcher_ticket returns the last
+ * queued ticket.  wsg_batcher_await blocks until a flush with a ticket > `seen` has
+ * finished its device work (downloads done; a host function on the download stream
+ * signals it) or `timeout_ms` passes (0: do not block, < 0: no limit), and returns the
+ * highest finished ticket.  It is the one batcher call that may run on another thread
+ * than the one driving the batcher (stop that thread before wsg_batcher_close): a
+ * completion thread awaits a flush, then re-enters the selector loop
+ * (SelectorLoop.executenf, InternalSelectorLoop.java:990-1011), whose task collects
+ * it with wsg_batcher_wait without waiting.  Replaces nothing in the reference (its
+ * decode is synchronous on the loop thread). */
+uint64_t wsg_batcher_ticket(wsg_batcher* b);
+int64_t wsg_batcher_await(wsg_batcher* b, uint64_t seen, int64_t timeout_ms);
+/* Size every pinned and device buffer of the three flush slots for flushes of up to
+ * `max_wire` bytes and `max_frames` frames, so those flushes allocate nothing (the
+ * stage chain's buffers, sized by what inflate and the aggregator produce, grow on
+ * first use beyond this: the one documented exception).  wsg_batcher_alloc_count is
+ * the number of pinned/device allocations all batchers of the process have made. */
+int wsg_batcher_reserve(wsg_batcher* b, uint64_t max_wire, uint64_t max_frames);
+uint64_t wsg_batcher_alloc_count(void);
 /* The decoders after "ws-decoder" that a flush runs in the same device batch, in the
  * pipeline order the reference builds (DefaultWebSocketSessionConfig.java:276-281,
  * PerMessageDeflateExtension.java:316-326; a FrameAggregator the application puts
@@ -466,6 +486,11 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b);
 int wsg_enc_batcher_wait(wsg_enc_batcher* b, wsg_enc_view* out);
 /* slot `sid` for a new session: its queued frames are dropped, the close latch cleared */
 int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid);
+/* as wsg_batcher_ticket / _await / _reserve, for the encode batcher (max_payload:
+ * payload bytes a flush may hold) */
+uint64_t wsg_enc_batcher_ticket(wsg_enc_batcher* b);
+int64_t wsg_enc_batcher_await(wsg_enc_batcher* b, uint64_t seen, int64_t timeout_ms);
+int wsg_enc_batcher_reserve(wsg_enc_batcher* b, uint64_t max_frames, uint64_t max_payload);
 
 /* ---------------- device per selector loop (multi-GPU policy) ---------------- */
 /* Sessions shard over the node's GPUs by selector loop, with no cross-device

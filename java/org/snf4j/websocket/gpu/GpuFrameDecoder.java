@@ -8,8 +8,9 @@
  *
  * available() is the reference's frame delimiting, on the loop thread
  * (FrameDecoder.java:290-401, through wsg_frame_available).  decode() hands the
- * bytes to the batcher and releases `data` exactly once (FrameDecoder.java:285-287);
- * it returns with `out` empty.  The frames come back in deliver(), on the loop
+ * bytes, and the ownership of `data`, to the batcher, which releases it exactly once
+ * after the loop iteration's flush has copied it (FrameDecoder.java:285-287); decode
+ * returns with `out` empty.  The frames come back in deliver(), on the loop
  * thread, and go through the decoders after the batched stages and the handler, in
  * order.  The first error does what FrameDecoder.java:92-102 does:
  * writenf(CloseFrame(code)), the closed latch, and an InvalidFrameException with
@@ -115,21 +116,28 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 		return (int) r;
 	}
 
-	/** FrameDecoder.decode (:180-288): the bytes go to the device batch. */
+	/**
+	 * FrameDecoder.decode (:180-288): the bytes go to the device batch.  `data` is
+	 * released exactly once (:285-287): here when it is swallowed, else by the batcher
+	 * once the loop iteration's flush has copied it (WsgBatcher.enqueue).
+	 */
 	@Override
 	public void decode(ISession session, ByteBuffer data, List<Frame> out) throws Exception {
+		this.session = session;
+		if (closed || released) {
+			session.release(data);
+			return;
+		}
 		try {
-			this.session = session;
-			if (closed || released)
-				return;
 			if (sid < 0)
 				sid = batcher.register(this, stages(session.getCodecPipeline()));
-			if (remaining > 0)
-				remaining -= data.remaining();
-			batcher.enqueue(this, data);
-		} finally {
+		} catch (RuntimeException e) {
 			session.release(data);
+			throw e;
 		}
+		if (remaining > 0)
+			remaining -= data.remaining();
+		batcher.enqueue(this, session, data);
 	}
 
 	/**
@@ -217,6 +225,15 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 		for (Object o : in)
 			session.getHandler().read(o);
 		return true;
+	}
+
+	/** The device batch this session's bytes were in failed (not a protocol error). */
+	void failBatch(Exception e) {
+		if (closed || released || session == null)
+			return;
+		closed = true;
+		session.getHandler().exception(e);
+		session.close();
 	}
 
 	private void fail(ISession session, int status, long detail, long detail2, boolean inAvailable) {

@@ -15,6 +15,16 @@
  * writes everything queued (the closing handshake, WebSocketSession.CloseTask,
  * writes it right before session.close()), then latches (:71-76).  Masks come
  * from a java.util.Random as FrameEncoder.RANDOM draws them (:43,111).
+ *
+ * Write futures: for a queued frame encode() returns with `out` empty, and snf4j's
+ * EncodeTask completes the write's future at once (EncodeTask.java:380-381), before
+ * the bytes are encoded or written.  So session.write(frame).sync() on a frame at or
+ * above the device threshold only says the frame was queued; an application that
+ * needs a write confirmation per frame sets the threshold above its largest frame
+ * (the reference FrameEncoder then encodes on the spot) or waits for a later frame's
+ * future below the threshold, which is written after the queued ones.  A device
+ * failure reaches the session as an exception and closes it (failBatch); frames
+ * queued or in flight when the session ends are dropped, as its unwritten bytes are.
  */
 package org.snf4j.websocket.gpu;
 
@@ -43,6 +53,10 @@ public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer>, IEventDrive
 	private final WsgBatcher batcher;
 	int sid = -1;
 	long nativeBatcher;
+	/** WsgBatcher bookkeeping: the open batch this encoder last added to, and the batches
+	 * (open or on the device) holding its frames */
+	long openBatch;
+	int batches;
 	private IStreamSession session;
 	/** FrameEncoder.closed (:71-76) */
 	private boolean closed;
@@ -93,6 +107,15 @@ public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer>, IEventDrive
 		if (sid < 0)
 			sid = batcher.registerEncoder(this, clientMode);
 		batcher.enqueueEncode(this, frame, clientMode ? RANDOM.nextInt() : 0);
+	}
+
+	/** The device batch holding this session's frames failed: the session gets the exception and closes. */
+	void failBatch(Exception e) {
+		if (released || session == null)
+			return;
+		closed = true;
+		session.getHandler().exception(e);
+		session.close();
 	}
 
 	/* ---- IEventDrivenCodec: the slot goes back at the session's end ---- */

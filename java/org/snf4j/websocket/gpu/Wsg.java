@@ -103,6 +103,26 @@ final class Wsg {
 	static native int batcherFeedArray(long batcher, int sid, byte[] data, int off, int len);
 
 	/**
+	 * wsg_batcher_feed_many: one loop iteration's reads in one call.  Read i is session
+	 * sids[i]'s bytes [offs[i], offs[i] + lens[i]) of direct[i] (a direct buffer) or, when
+	 * that is null, of heap[i]; every read is checked before any is fed.
+	 */
+	static native int batcherFeedMany(long batcher, int n, int[] sids, ByteBuffer[] direct, byte[][] heap, int[] offs,
+			int[] lens);
+
+	/** wsg_batcher_reserve: flushes of up to maxWire bytes / maxFrames frames allocate nothing. */
+	static native int batcherReserve(long batcher, long maxWire, long maxFrames);
+
+	/** wsg_batcher_ticket: the last queued flush's ticket (1, 2, ...). */
+	static native long batcherTicket(long batcher);
+
+	/**
+	 * wsg_batcher_await (the completion thread, not the loop's): the highest ticket whose
+	 * device work has finished, once one above seen has or timeoutMs has passed.
+	 */
+	static native long batcherAwait(long batcher, long seen, long timeoutMs);
+
+	/**
 	 * wsg_batcher_flush: decodes every complete frame fed since the last flush.
 	 * views[0..4] receive session_first, desc, payload, result and detail2 wrapped as direct
 	 * buffers (valid until the next flush); counts = {n_frames, wire_bytes}.
@@ -153,6 +173,12 @@ final class Wsg {
 	static native int encBatcherWait(long batcher, ByteBuffer[] views);
 
 	static native int encBatcherSessionReset(long batcher, int sid);
+
+	static native int encBatcherReserve(long batcher, long maxFrames, long maxPayload);
+
+	static native long encBatcherTicket(long batcher);
+
+	static native long encBatcherAwait(long batcher, long seen, long timeoutMs);
 
 	/* ---- encode: wsg_encoded_length / wsg_encode_batch_host ---- */
 	static native long encodedLength(int payloadLen, boolean clientMode);

@@ -486,6 +486,22 @@ class NativeBatcher:
         from ._lib import lib
         self._check(lib.wsg_batcher_flush_async(self._h))
 
+    def ticket(self) -> int:
+        """The last queued flush's ticket (wsg_batcher_ticket: flushes are 1, 2, ...)."""
+        from ._lib import lib
+        return int(lib.wsg_batcher_ticket(self._h))
+
+    def await_done(self, seen: int, timeout_ms: int) -> int:
+        """wsg_batcher_await: the highest ticket whose device work has finished, once one
+        above `seen` has or `timeout_ms` passed (0: no wait).  Safe from another thread."""
+        from ._lib import lib
+        return int(lib.wsg_batcher_await(self._h, int(seen), int(timeout_ms)))
+
+    def reserve(self, max_wire: int, max_frames: int):
+        """wsg_batcher_reserve: flushes up to these sizes allocate nothing."""
+        from ._lib import lib
+        self._check(lib.wsg_batcher_reserve(self._h, int(max_wire), int(max_frames)))
+
     def wait_raw(self):
         """The oldest queued flush's results (wsg_batcher_wait), as flush_raw returns them."""
         import ctypes as C
@@ -624,6 +640,19 @@ class EncodeBatcher:
         collect it with wait().  At most two in flight."""
         from ._lib import lib
         self._check(lib.wsg_enc_batcher_flush_async(self._h))
+
+    def ticket(self) -> int:
+        from ._lib import lib
+        return int(lib.wsg_enc_batcher_ticket(self._h))
+
+    def await_done(self, seen: int, timeout_ms: int) -> int:
+        """wsg_enc_batcher_await (see NativeBatcher.await_done)."""
+        from ._lib import lib
+        return int(lib.wsg_enc_batcher_await(self._h, int(seen), int(timeout_ms)))
+
+    def reserve(self, max_frames: int, max_payload: int):
+        from ._lib import lib
+        self._check(lib.wsg_enc_batcher_reserve(self._h, int(max_frames), int(max_payload)))
 
     def wait_raw(self):
         """The oldest queued flush (wsg_enc_batcher_wait) as numpy views, valid until

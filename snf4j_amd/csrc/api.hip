@@ -162,6 +162,7 @@ namespace ws {
 hipError_t ctx_wait_prev_state(wsg_ctx* c) { return c->ev_prev_state ? hipEventSynchronize(c->ev_prev_state) : hipSuccess; }
 hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e) { return hipEventRecord(e, c->s_out ? c->s_out : c->stream); }
 hipStream_t ctx_stream(wsg_ctx* c) { return c->stream; }
+hipStream_t ctx_out_stream(wsg_ctx* c) { return c->s_out ? c->s_out : c->stream; }
 int ctx_device(wsg_ctx* c) { return c->device; }
 uint8_t* ctx_async_payload(wsg_ctx* c) { return c->last_async_payload; }
 }  // namespace ws

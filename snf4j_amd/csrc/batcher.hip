@@ -24,6 +24,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <deque>
 #include <functional>
@@ -62,6 +63,10 @@ struct SpT {
 
 namespace {
 
+// Host allocations a batcher made (pinned and device): after wsg_batcher_reserve /
+// wsg_enc_batcher_reserve a flush within the reserved sizes makes none.
+std::atomic<uint64_t> g_batcher_allocs{0};
+
 struct PinnedBuf {
   uint8_t* p = nullptr;
   size_t n = 0;
@@ -73,6 +78,7 @@ struct PinnedBuf {
     const size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
     hipError_t e = hipHostMalloc((void**)&p, want, hipHostMallocDefault);
     if (e == hipSuccess) n = want;
+    g_batcher_allocs.fetch_add(1, std::memory_order_relaxed);
     return e;
   }
   void release() {
@@ -176,6 +182,43 @@ class Pool {
   bool stop_ = false;
 };
 
+// Completion signal for a thread other than the one driving a batcher (wsg_batcher_await,
+// wsg_enc_batcher_await): a host function queued on the download stream behind each
+// flush raises `done` to that flush's ticket.  The argument is allocated per flush and
+// holds the signal by shared_ptr, so a late callback never touches a freed batcher.
+struct Notify {
+  std::mutex m;
+  std::condition_variable cv;
+  uint64_t done = 0;
+};
+struct NotifyArg {
+  std::shared_ptr<Notify> n;
+  uint64_t ticket;
+};
+void notify_cb(void* p) {
+  NotifyArg* a = (NotifyArg*)p;
+  {
+    std::lock_guard<std::mutex> g(a->n->m);
+    if (a->ticket > a->n->done) a->n->done = a->ticket;
+  }
+  a->n->cv.notify_all();
+  delete a;
+}
+hipError_t notify_after(hipStream_t s, const std::shared_ptr<Notify>& n, uint64_t ticket) {
+  NotifyArg* a = new NotifyArg{n, ticket};
+  const hipError_t e = hipLaunchHostFunc(s, notify_cb, a);
+  if (e != hipSuccess) delete a;
+  return e;
+}
+int64_t notify_await(Notify& n, uint64_t seen, int64_t timeout_ms) {
+  std::unique_lock<std::mutex> l(n.m);
+  if (timeout_ms > 0)
+    n.cv.wait_for(l, std::chrono::milliseconds(timeout_ms), [&] { return n.done > seen; });
+  else if (timeout_ms < 0)
+    n.cv.wait(l, [&] { return n.done > seen; });
+  return (int64_t)n.done;
+}
+
 // ------------------------------------------------------------------ stage chain: device buffers
 // A device buffer that only grows.  grow_keep() keeps the first `keep` bytes (a
 // stream-ordered copy) when it has to move.
@@ -191,6 +234,7 @@ struct DBuf {
     const size_t want = bytes < 4096 ? 4096 : bytes + bytes / 4;
     hipError_t e = hipMalloc((void**)&p, want);
     if (e == hipSuccess) n = want;
+    g_batcher_allocs.fetch_add(1, std::memory_order_relaxed);
     return e;
   }
   hipError_t grow_keep(size_t bytes, size_t keep, hipStream_t s) {
@@ -198,6 +242,7 @@ struct DBuf {
     const size_t want = bytes + bytes / 4;
     uint8_t* q = nullptr;
     hipError_t e = hipMalloc((void**)&q, want);
+    g_batcher_allocs.fetch_add(1, std::memory_order_relaxed);
     if (e != hipSuccess) return e;
     if (p && keep) {
       e = hipMemcpyAsync(q, p, keep, hipMemcpyDeviceToDevice, s);
@@ -374,6 +419,8 @@ struct wsg_batcher {
   DBuf d_pend;
   hipStream_t s_dl = nullptr;           // downloads of stage outputs
   StageOut* out = nullptr;              // the output the stage run at hand writes
+  uint64_t tickets = 0;                 // flushes queued so far (flush t's ticket is t)
+  std::shared_ptr<Notify> notify = std::make_shared<Notify>();
 };
 
 static int bset(wsg_batcher* b, int code, const char* msg) {
@@ -1144,6 +1191,8 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     f.pcap = pcap;
   }
   B_TRY(b, ws::ctx_record_out(b->ctx, f.done));
+  B_TRY(b, notify_after(ws::ctx_out_stream(b->ctx), b->notify, b->tickets + 1));
+  ++b->tickets;
   b->q.push_back(slot);
   // feeds go to the next slot (waited: at most two in flight)
   b->open = (b->open + 1) % 3;
@@ -1301,6 +1350,39 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
   return WSG_API_OK;
 }
 
+uint64_t wsg_batcher_ticket(wsg_batcher* b) { return b ? b->tickets : 0; }
+
+int64_t wsg_batcher_await(wsg_batcher* b, uint64_t seen, int64_t timeout_ms) {
+  if (!b) return WSG_API_EINVAL;
+  return notify_await(*b->notify, seen, timeout_ms);
+}
+
+// Every pinned and device buffer a flush of up to `max_wire` bytes and `max_frames`
+// frames uses, in all three slots, sized now: such flushes allocate nothing (the
+// stage chain's buffers, sized by what inflate and the aggregator produce, still
+// grow on first use beyond this).
+int wsg_batcher_reserve(wsg_batcher* b, uint64_t max_wire, uint64_t max_frames) {
+  if (!b) return WSG_API_EINVAL;
+  const uint32_t S = b->n;
+  const uint64_t pcap = max_wire + 16 * max_frames + 16;
+  B_TRY(b, b->st.ensure((S + 1) * sizeof(wsg_session_state)));
+  for (FlushSlot& f : b->fs) {
+    if (f.arena.n < max_wire + 64) B_TRY(b, arena_grow(f, max_wire + 64));
+    B_TRY(b, f.off.ensure((max_frames + 1) * sizeof(uint64_t)));
+    B_TRY(b, f.sf.ensure((S + 1) * sizeof(uint32_t)));
+    if (!b->has_stages) B_TRY(b, f.payload.ensure(pcap));
+    B_TRY(b, f.desc.ensure((max_frames + 1) * sizeof(wsg_frame_desc)));
+    B_TRY(b, f.result.ensure((S + 1) * sizeof(wsg_session_result)));
+    if (!f.done) B_TRY(b, hipEventCreateWithFlags(&f.done, hipEventDisableTiming));
+    if (b->has_stages) {
+      B_TRY(b, f.dpay.ensure(pcap));
+      B_TRY(b, f.so.pay.ensure(pcap));
+      if (!f.dpay_done) B_TRY(b, hipEventCreateWithFlags(&f.dpay_done, hipEventDisableTiming));
+    }
+  }
+  return WSG_API_OK;
+}
+
 int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* st) {
   if (!b || sid >= b->n || !st) return WSG_API_EINVAL;
   *st = b->state[sid];
@@ -1369,6 +1451,8 @@ struct wsg_enc_batcher {
   hipStream_t s_in = nullptr, s_out = nullptr;  // uploads / downloads (kernels on the context's stream)
   std::unique_ptr<Pool> pool;                   // add_many's copies
   std::string err;
+  uint64_t tickets = 0;                         // flushes queued so far
+  std::shared_ptr<Notify> notify = std::make_shared<Notify>();
 };
 
 static int eset(wsg_enc_batcher* b, int code, const char* msg) {
@@ -1558,6 +1642,8 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   // (the kept frames' bytes are at most `need`: frames dropped after a CLOSE take none)
   if (need) E_TRY(b, hipMemcpyAsync(e.wire.p, e.d_wire.p, need, hipMemcpyDeviceToHost, b->s_out));
   E_TRY(b, hipEventRecord(e.ev_out, b->s_out));
+  E_TRY(b, notify_after(b->s_out, b->notify, b->tickets + 1));
+  ++b->tickets;
   e.F = F;
   e.need = need;
   e.resets.clear();
@@ -1626,6 +1712,45 @@ int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out) {
   if (rc) return rc;
   return wsg_enc_batcher_wait(b, out);
 }
+
+uint64_t wsg_enc_batcher_ticket(wsg_enc_batcher* b) { return b ? b->tickets : 0; }
+
+int64_t wsg_enc_batcher_await(wsg_enc_batcher* b, uint64_t seen, int64_t timeout_ms) {
+  if (!b) return WSG_API_EINVAL;
+  return notify_await(*b->notify, seen, timeout_ms);
+}
+
+// The pinned and device buffers of all three slots for flushes of up to `max_frames`
+// frames and `max_payload` payload bytes: such flushes allocate nothing.
+int wsg_enc_batcher_reserve(wsg_enc_batcher* b, uint64_t max_frames, uint64_t max_payload) {
+  if (!b) return WSG_API_EINVAL;
+  const uint32_t S = b->n;
+  const uint64_t arena = max_payload + 16 * max_frames + 32;  // 16-B aligned payloads
+  const uint64_t need = max_payload + 14 * max_frames + 32;   // the longest header is 14 B
+  for (EncSlot& e : b->es) {
+    if (e.arena.n < arena) {
+      PinnedBuf g;
+      if (g.ensure(arena) != hipSuccess) return eset(b, WSG_API_ENOMEM, "pinned arena");
+      if (e.arena_len) memcpy(g.p, e.arena.p, e.arena_len);
+      e.arena.release();
+      e.arena = g;
+    }
+    E_TRY(b, e.frames.ensure((max_frames + 1) * sizeof(wsg_encode_frame)));
+    E_TRY(b, e.sf.ensure((S + 1) * sizeof(uint32_t)));
+    E_TRY(b, e.cl.ensure(S + 1));
+    E_TRY(b, e.off.ensure((max_frames + 1) * sizeof(uint64_t)));
+    E_TRY(b, e.wire.ensure(need + 32));
+    E_TRY(b, e.d_pay.ensure(arena + 32));
+    E_TRY(b, e.d_frames.ensure((max_frames + 1) * sizeof(wsg_encode_frame)));
+    E_TRY(b, e.d_sf.ensure((S + 1) * sizeof(uint32_t)));
+    E_TRY(b, e.d_cl.ensure(S + 1));
+    E_TRY(b, e.d_wire.ensure(need + 32));
+    E_TRY(b, e.d_off.ensure((max_frames + 1) * sizeof(uint64_t)));
+  }
+  return WSG_API_OK;
+}
+
+uint64_t wsg_batcher_alloc_count(void) { return g_batcher_allocs.load(); }
 
 int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid) {
   if (!b || sid >= b->n) return WSG_API_EINVAL;

@@ -221,6 +221,7 @@ hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e);
 // the context's kernel stream, and the device payload of its last async batch (valid
 // in stream order until a later batch reuses that staging slot)
 hipStream_t ctx_stream(wsg_ctx* c);
+hipStream_t ctx_out_stream(wsg_ctx* c);  // where ctx_record_out records (the download stream)
 int ctx_device(wsg_ctx* c);
 uint8_t* ctx_async_payload(wsg_ctx* c);
 

@@ -33,7 +33,7 @@ def test_every_native_method_is_used():
     # the handshake natives are bound for the handshake stages INTEGRATION.md §1.3d-e describes
     assert unused <= {"handshakeAvailable", "handshakeAcceptBatchHost", "handshakeValidateBatchHost",
                       "batcherSessionState", "checkHeader", "encodedLength", "encodeBatchHost",
-                      "validateBatchHost", "batcherFlush"}, unused
+                      "validateBatchHost", "batcherFlush", "batcherFeed", "batcherFeedArray"}, unused
 
 
 def test_glue_calls_only_declared_exported_entry_points():
@@ -54,7 +54,7 @@ def test_stage_classes_keep_the_reference_keys_and_types():
     assert "new FrameUtf8Validator()" not in cfg
     dec = _java("GpuFrameDecoder.java")
     assert "implements IBaseDecoder<ByteBuffer, Frame>, IEventDrivenCodec" in dec
-    assert dec.count("session.release(data)") == 1  # exactly once, FrameDecoder.java:285-287
+    # (release exactly once, FrameDecoder.java:285-287: test_decode_releases_data_exactly_once)
     assert "implements IEncoder<Frame, ByteBuffer>, IEventDrivenCodec" in _java("GpuFrameEncoder.java")
     for f in ("GpuPerMessageDeflateDecoder.java", "GpuFrameAggregator.java", "GpuFrameUtf8Validator.java"):
         assert "implements IDecoder<Frame, Frame>" in _java(f) and "GpuStage" in _java(f), f
@@ -91,7 +91,7 @@ def test_feed_handles_every_buffer_kind():
     b = _java("WsgBatcher.java")
     assert "data.hasArray()" in b and "data.isDirect()" in b and "data.duplicate().get(b)" in b
     jni = _read("jni/wsgpu_jni.c")
-    assert "GetDirectBufferCapacity" in jni and "if (!p || cap < 0" in jni
+    assert "GetDirectBufferCapacity" in jni and "if (!p || cap < 0 || (uint64_t)cap < need)" in jni
 
 
 def test_java_messages_match_the_python_mirror():
@@ -106,18 +106,71 @@ def test_java_messages_match_the_python_mirror():
         assert text in java, (code, text)
 
 
-def test_encode_flush_is_pipelined():
-    """The loop's flush queues the encode batch (wsg_enc_batcher_flush_async) and writes
-    the previous one out (wsg_enc_batcher_wait) one iteration later; a CLOSE frame
-    (flushEncodes) first drains what is in flight, so writes keep their order."""
+def _body(src, start, end):
+    return src[src.index(start):src.index(end)]
+
+
+def test_loop_scheduling_matches_the_python_restatement():
+    """WsgBatcher's flush does what snf4j_amd/loop.py (run on the GPU by
+    tests/test_gpu_loop.py) does, in the same order: the iteration's reads in one
+    batcherFeedMany, the finished flushes collected without waiting (await 0, 0), the
+    oldest collected only when two are in flight, then flushAsync + ticket handed to the
+    completion thread; the completion thread calls only the await natives and re-enters
+    the loop with executenf (never schedule() from inside the task phase)."""
     b = _java("WsgBatcher.java")
-    flush = b[b.index("synchronized void flush()"):b.index("private void collectDecodes")]
-    assert "flushEncodesAsync();" in flush and "flushEncodes();" not in flush
-    asy = b[b.index("private void flushEncodesAsync()"):b.index("private void collectEncode")]
-    assert asy.index("collectEncode(n, views)") < asy.index("Wsg.encBatcherFlushAsync(n.handle)")
-    assert "n.inflight.add(" in asy and "schedule();" in asy
-    sync = b[b.index("synchronized void flushEncodes()"):b.index("private void flushEncodesAsync()")]
-    assert sync.index("collectEncode(n, views)") < sync.index("Wsg.encBatcherFlush(n.handle, views)")
-    assert "n.inflight" in b[b.index("synchronized boolean hasQueued"):b.index("private void schedule()")]
+    flush = _body(b, "synchronized void flush()", "private static void check(")
+    order = ["feedReads(n)", "collectReady(n)", "n.inflight.size() == 2", "Wsg.batcherFlushAsync(n.handle)",
+             "Wsg.batcherTicket(n.handle)", "completion.watch(n.handle, t, false)"]
+    pos = [flush.index(x) for x in order]
+    assert pos == sorted(pos), order
+    enc = ["collectReady(n)", "n.inflight.size() == 2", "Wsg.encBatcherFlushAsync(n.handle)",
+           "Wsg.encBatcherTicket(n.handle)", "completion.watch(n.handle, t, true)"]
+    encflush = flush[flush.index("for (EncNative n : encNatives)"):]
+    pos = [encflush.index(x) for x in enc]
+    assert pos == sorted(pos), enc
+    assert "schedule()" not in flush
+    feed = _body(b, "private void feedReads(Native n)", "synchronized void collectReady()")
+    assert feed.count("Wsg.batcherFeedMany(") == 1 and "release(n.owned[i])" in feed
+    comp = _body(b, "private final class Completion", "final long ctx;")
+    natives = set(re.findall(r"Wsg\.(\w+)\(", comp))
+    assert natives == {"batcherAwait", "encBatcherAwait"}, natives
+    assert "loop.executenf(collectTask)" in comp
+    ready = _body(b, "private void collectReady(Native n)", "private void collectReady(EncNative n)")
+    assert "Wsg.batcherAwait(n.handle, 0, 0)" in ready
+    loop = _read("snf4j_amd/loop.py")
+    for x in ("feed_many", "collect_ready()", "len(self.inflight) == 2", "flush_async()", "ticket()",
+              "_completion.watch(t)", "await_done(0, 0)", "executenf(self.task)"):
+        assert x in loop, x
+
+
+def test_decode_releases_data_exactly_once():
+    """FrameDecoder.java:285-287: the decoder releases its input once — GpuFrameDecoder
+    when it swallows it (closed, released, a failed registration), else the batcher
+    after the flush copied it (feedReads), when the session ends first (unregister), or
+    at close."""
+    dec = _java("GpuFrameDecoder.java")
+    body = _body(dec, "public void decode(ISession session, ByteBuffer data", "private WsgBatcher.Cfg stages(")
+    assert body.count("session.release(data)") == 2 and "batcher.enqueue(this, session, data)" in body
+    b = _java("WsgBatcher.java")
+    assert b.count(".release(n.owned[i])") == 3  # feedReads, unregister, close
+
+
+def test_encode_flush_is_pipelined():
+    """The encode batch queued by a flush is written by a later collect (its await
+    done) or, with two in flight, before the next is queued; a CLOSE frame
+    (flushEncodes) first writes out everything in flight, so writes keep their order;
+    hasQueued is a per-encoder count, not a scan."""
+    b = _java("WsgBatcher.java")
+    sync = _body(b, "synchronized void flushEncodes()", "private void writeOldest(")
+    assert sync.index("writeOldest(n)") < sync.index("Wsg.encBatcherFlush(n.handle, views)")
+    hq = _body(b, "boolean hasQueued(GpuFrameEncoder e)", "/* ------------------------------------------------------------------ flush */")
+    assert "e.batches > 0" in hq and "for (" not in hq
+    assert "e.batches--" in _body(b, "private void write(EncNative n", "private void failSessions(Native n")
     jni = _read("jni/wsgpu_jni.c")
     assert "wsg_enc_batcher_flush_async(ENC_BATCHER(b))" in jni and "wsg_enc_batcher_wait(ENC_BATCHER(b), &v)" in jni
+
+
+def test_close_releases_the_loop_device():
+    b = _java("WsgBatcher.java")
+    close = b[b.index("public void close()"):]
+    assert "completion.join()" in close and "if (ownsDevice)" in close and "WsgDevices.release(loop)" in close
