@@ -522,9 +522,7 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
     if (nlit >= lit_cap) return false;
     litw |= b << (8 * (nlit & 3u));
     if ((++nlit & 3u) == 0) {
-#ifndef TOK_EXP_NOSTORE
       reinterpret_cast<uint32_t*>(lit)[(nlit >> 2) - 1] = litw;
-#endif
       litw = 0;
     }
     ++run;
@@ -533,11 +531,7 @@ __device__ __forceinline__ void tok_message(const InflArgs& a, LaneTab* T, const
   };
   auto put_tok = [&](uint32_t t) -> bool {
     if (ntok >= tok_cap) return false;
-#ifdef TOK_EXP_NOSTORE
-    ntok++;
-#else
     tok[ntok++] = t;
-#endif
     return true;
   };
   auto end_run = [&]() -> bool {
