@@ -321,7 +321,7 @@ static int ensure_decode_ws(wsg_ctx* c, uint64_t n_frames, uint32_t n_sessions, 
   HIP_TRY(c, c->blk_max.ensure(4 * ((nblk + 3) & ~3ull) * sizeof(int32_t)));  // rows 16-B aligned (decode.hip blk_stride)
   HIP_TRY(c, c->chunk.ensure((nblk / SCAN_CHUNK + 1) * (sizeof(uint64_t) + 4 * sizeof(int32_t))));
   HIP_TRY(c, c->sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t), 0xff, c->stream));
-  HIP_TRY(c, c->total.ensure(2 * sizeof(uint64_t)));  // the total, then the validator's vcanon word
+  HIP_TRY(c, c->total.ensure(sizeof(uint64_t)));
   return WSG_API_OK;
 }
 
@@ -406,7 +406,6 @@ int wsg_decode_batch_device(wsg_ctx* c, const wsg_decoder_cfg* cfg, const uint8_
   a.chunk_max = (int32_t*)(a.chunk_sum + (n_frames + DBLOCK - 1) / DBLOCK / SCAN_CHUNK + 1);
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
-  a.vcanon = nullptr;
   a.pieces = (PieceDesc*)c->pieces.p;
   a.nblk = (uint32_t)((n_frames + DBLOCK - 1) / DBLOCK);
   a.n_pieces = piece_bound(wire_len, n_frames);
@@ -461,7 +460,6 @@ int wsg_validate_batch_device(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n
   a.chunk_max = (int32_t*)(a.chunk_sum + (n_frames + DBLOCK - 1) / DBLOCK / SCAN_CHUNK + 1);
   a.sess_err = (uint64_t*)c->sess_err.p;
   a.total = (uint64_t*)c->total.p;
-  a.vcanon = (uint32_t*)((uint64_t*)c->total.p + 1);
   a.pieces = (PieceDesc*)c->pieces.p;
   a.nblk = (uint32_t)((n_frames + DBLOCK - 1) / DBLOCK);
   a.n_pieces = piece_bound(payload_len, n_frames);

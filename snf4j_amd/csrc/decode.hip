@@ -352,7 +352,6 @@ __device__ __forceinline__ uint32_t plain_word(const DecodeArgs& a, uint64_t i) 
 
 __global__ __launch_bounds__(DBLOCK) void k_vparse(DecodeArgs a) {
   const uint64_t k = (uint64_t)blockIdx.x * DBLOCK + threadIdx.x;
-  if (k == 0) *a.vcanon = 1u;  // (k_vlink clears it at the first payload away from its slot)
   VAgg v = VAGG_ID;
   if (k < a.n_frames) {
     const uint32_t s = wave_session(a, k);
@@ -696,10 +695,6 @@ __global__ __launch_bounds__(DBLOCK) void k_vlink(DecodeArgs a) {
   VAgg tot;
   const VAgg ex = agg_op(bp, block_excl_scan_t(v, &tot, VAGG_ID));
   if (blockIdx.x + 1 == a.nblk && threadIdx.x == 0) *a.total = bp.sum + tot.sum;
-  // the canonical layout (every payload at its slot offset, as the decoder writes them):
-  // then a piece's bytes sit at the piece's own offset and k_piecesN loads them before
-  // its descriptors arrive
-  if (__syncthreads_or(live && r.src != ex.sum) && threadIdx.x == 0) atomicAnd(a.vcanon, 0u);
   bool validate = false, seam = false;
   if (live) {
     const uint32_t s = r.sess;
@@ -1112,71 +1107,12 @@ __device__ __forceinline__ uint32_t piece_fastN(const DecodeArgs& a, const Piece
   return err;
 }
 
-// Validate only, N pieces of one frame whose bytes were loaded at the pieces' own
-// offset before the descriptors arrived (vcanon: the source is 16-B aligned and
-// contiguous, so no funnel): the UTF-8 rule of piece_fastN over A.
-template <int N>
-__device__ __forceinline__ uint32_t piece_validate_pre(const PieceDesc d, const uint64_t info_last, const u32x4* A,
-                                                       uint32_t sprev, int lane) {
-  if (!(d.info & PD_VALIDATE)) return 0u;
-  const uint32_t nb_last = (uint32_t)(info_last >> PD_NB_SHIFT) & 2047u;
-  const bool full = nb_last >= PIECE;
-  const int keep = (int)nb_last - lane * 16;
-  uint32_t err = 0;
-  uint32_t carry = (d.info & PD_FIRST) ? 0u : sprev;
-#pragma unroll
-  for (int i = 0; i < N; ++i) {
-    const uint32_t w0 = A[i].x, w1 = A[i].y, w2 = A[i].z, w3 = A[i].w;
-    const uint32_t pw = dpp_from_prev(w3, carry);
-    U8W up, u0, u1, u2, u3;
-    u8w_one(pw, up);
-    u8w_pair(w0, w1, u0, u1);
-    u8w_pair(w2, w3, u2, u3);
-    uint32_t f0 = u8w_err(u0, up), f1 = u8w_err(u1, u0), f2 = u8w_err(u2, u1), f3 = u8w_err(u3, u2);
-    if (i == 0 && lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT)) f0 &= 0x80000000u;
-    if (i + 1 == N && !full) {
-      f0 &= keep_flags(keep); f1 &= keep_flags(keep - 4); f2 &= keep_flags(keep - 8); f3 &= keep_flags(keep - 12);
-    }
-    if (i + 1 == N && (info_last & PD_LAST) && keep >= 1 && keep <= 16) {
-      const bool ge3 = N > 1 || !(lane == 0 && (d.info & PD_FIRST) && (d.frame & PDF_CONT) && keep < 3);
-      uint32_t v[4] = {w0, w1, w2, w3};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = keep_bytes(v[k], keep - 4 * k);
-      if (tail_error(last3(pw, v[0], v[1], v[2], v[3], keep), ge3 && (info_last & PD_FIN))) err |= 1u;
-    }
-    err |= (f0 | f1 | f2 | f3) & H80;
-    if (i + 1 < N) carry = (uint32_t)__builtin_amdgcn_readlane((int)w3, 63);
-  }
-  return err;
-}
-
-#ifndef WSG_VSPEC
-#define WSG_VSPEC 0  // validate only: speculative loads at the piece's own offset (A/B build switch)
-#endif
-
 template <int NT, int XCD, int N, int WPB = 1, int MINW = 1>
 __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW))) void k_piecesN(DecodeArgs a) {
   const int lane = threadIdx.x & 63;
   const uint32_t blk = XCD ? xcd_remap(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint64_t p = (uint64_t)N * (uint64_t)__builtin_amdgcn_readfirstlane(blk * (uint32_t)WPB + (threadIdx.x >> 6));
   if (WPB > 1 && p >= a.n_pieces) return;  // (a wave of the last workgroup past the grid)
-  // validate only, canonical layout: the pieces' bytes are at their own offset, so they
-  // are loaded now, beside the descriptor loads instead of after them
-  constexpr bool SPEC = (NT & 4) && WSG_VSPEC;
-  u32x4 S[N];
-  uint32_t sprev = 0u;
-  bool spec = false;
-  if (SPEC && p * PIECE + (uint64_t)N * PIECE <= a.wire_len) {
-    const __amdgpu_buffer_rsrc_t rc = __builtin_amdgcn_make_buffer_rsrc((void*)a.vcanon, 0, 4, 0x00020000);
-    spec = __builtin_amdgcn_readfirstlane((int)__builtin_amdgcn_raw_buffer_load_b32(rc, 0, 0, 0)) != 0;
-    if (spec) {
-      const __amdgpu_buffer_rsrc_t rin =
-          __builtin_amdgcn_make_buffer_rsrc((void*)(a.wire + p * PIECE), 0, (int)(N * PIECE), 0x00020000);
-#pragma unroll
-      for (int i = 0; i < N; ++i) S[i] = __builtin_amdgcn_raw_buffer_load_b128(rin, (uint32_t)lane * 16u + i * PIECE, 0, 2);
-      sprev = p ? *(const uint32_t*)(a.wire + p * PIECE - 4) : 0u;
-    }
-  }
   PieceDesc d[N];
 #pragma unroll
   for (int i = 0; i < N; ++i) d[i] = a.pieces[p + i];
@@ -1189,11 +1125,6 @@ __global__ __launch_bounds__(64 * WPB) __attribute__((amdgpu_waves_per_eu(MINW))
   bool fast = pstart + (uint64_t)(N - 1) * PIECE < total && d[0].frame == d[N - 1].frame;
 #pragma unroll
   for (int i = 0; i < N; ++i) fast = fast && !(d[i].info & PD_MULTI);
-  if (SPEC && fast && spec && (d[0].info & PD_SRC_MASK) == pstart) {
-    const uint32_t err = piece_validate_pre<N>(d[0], d[N - 1].info, S, sprev, lane);
-    if (__any(err != 0) && lane == 0) report_utf8(a, d[0].frame & PDF_INDEX);
-    return;
-  }
   if (fast) {
     const uint32_t err = piece_fastN<NT, N>(a, d[0], d[N - 1].info, pstart, lane);
     if (__any(err != 0) && lane == 0) report_utf8(a, d[0].frame & PDF_INDEX);

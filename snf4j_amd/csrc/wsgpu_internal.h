@@ -108,8 +108,6 @@ struct DecodeArgs {
   int32_t* chunk_max;  // [nblk / SCAN_CHUNK + 1][4]
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none)
   uint64_t* total;     // [1] total payload slot bytes
-  uint32_t* vcanon;    // validator-only: 1 when every frame's payload sits at its slot offset (the
-                       // decoder's output layout), so a piece's bytes are at its own offset (k_vlink)
   struct PieceDesc* pieces;  // [piece_bound]: per-piece work descriptor (k_link)
   uint64_t n_pieces;   // pieces the grid covers (piece_bound): slots beyond are a malformed batch
   uint32_t nblk;
