@@ -382,6 +382,16 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_threads": cpu_mt,
         }
+        # the same kernel's mean launch under rocprofv3 in the committed profile of this
+        # workload (another process, maybe another box): its fraction, and the delta
+        prof_ms, prof_src = profiled_launch("north" if args.config == "north" and not args.binary else
+                                            {"1": "configs1", "3": "configs3"}.get(args.config, "north"),
+                                            "k_piecesN<1, 1, 2>")
+        if prof_ms and F == 1 << 20 and P == 4096 and not args.binary:
+            pf = alg_bytes / (prof_ms / 1e3) / 1e9 / HBM_PEAK_GBS
+            out["roofline"].update({"frac_profiles": round(pf, 4), "profiles_launch_ms": round(prof_ms, 4),
+                                    "profiles_source": prof_src,
+                                    "frac_minus_frac_profiles": round(achieved / HBM_PEAK_GBS - pf, 4)})
         if e2e:
             out["e2e_pinned"] = e2e
         if validator:
@@ -393,6 +403,23 @@ def main():
     if dist:
         dist.barrier()  # (the other ranks wait here for rank 0's CPU baseline)
         dist.destroy_process_group()
+
+
+def profiled_launch(line: str, kernel_prefix: str):
+    """The committed rocprofv3 --kernel-trace --stats summary of this bench line
+    (profiles/<round>_<line>_kernel_stats.csv, the newest round): the kernel's mean
+    launch duration (ms) and the file, so the line can print the roofline fraction the
+    profile gives beside the one its own HIP events give (a box-to-box delta otherwise)."""
+    import csv
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r[0-9][0-9]_{line}_kernel_stats.csv")))
+    if not files:
+        return None, None
+    with open(files[-1]) as fh:
+        for row in csv.DictReader(fh):
+            if kernel_prefix in row["Name"]:
+                return float(row["AverageNs"]) / 1e6, os.path.relpath(files[-1], ROOT)
+    return None, None
 
 
 def validator_line(ctx, dev, desc, sf, payload, n_s, F, P, steps):
