@@ -826,7 +826,7 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   HIP_TRY(c, c->a_last.ensure(F * 2 * sizeof(int32_t)));
   HIP_TRY(c, c->a_pl.ensure(F * sizeof(uint64_t)));
   HIP_TRY(c, c->a_cl.ensure(F * sizeof(uint64_t) + sizeof(uint64_t)));
-  HIP_TRY(c, c->a_blk.ensure(nblk * (2 * sizeof(uint64_t) + 2 * sizeof(int32_t))));
+  HIP_TRY(c, c->a_blk.ensure(nblk * (4 * sizeof(uint64_t) + 2 * sizeof(int32_t))));
   HIP_TRY(c, c->a_sess_err.ensure((uint64_t)n_sessions * sizeof(uint64_t), 0xff, c->stream));
   HIP_TRY(c, c->a_pieces.ensure((a.n_pieces + 1) * sizeof(PieceDesc)));
   a.code = (uint32_t*)c->a_code.p;
@@ -837,7 +837,9 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   a.n_units = a.cl + F;
   a.blk_sum = (uint64_t*)c->a_blk.p;
   a.blk_cnt = a.blk_sum + nblk;
-  a.blk_max = (int32_t*)(a.blk_cnt + nblk);
+  a.pre_sum = a.blk_cnt + nblk;
+  a.pre_cnt = a.pre_sum + nblk;
+  a.blk_max = (int32_t*)(a.pre_cnt + nblk);
   a.sess_err = (uint64_t*)c->a_sess_err.p;
   a.pieces = (PieceDesc*)c->a_pieces.p;
   if (!n_frames) HIP_TRY(c, hipMemsetAsync(agg_total, 0, sizeof(uint64_t), c->stream));

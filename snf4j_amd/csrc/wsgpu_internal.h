@@ -162,8 +162,10 @@ struct AggArgs {
   int32_t* last;       // [2][n] last start / last end before k (batch index, -1 = none)
   uint64_t* pl;        // [n] block-local exclusive member bytes
   uint64_t* cl;        // [n] block-local exclusive (emitted frames | gather units << 32)
-  uint64_t* blk_sum;   // [nblk] member bytes -> exclusive prefix
-  uint64_t* blk_cnt;   // [nblk] (emitted frames | gather units << 32) -> exclusive prefix
+  uint64_t* blk_sum;   // [nblk] member bytes of the block (k_agg_b)
+  uint64_t* blk_cnt;   // [nblk] (emitted frames | gather units << 32) of the block (k_agg_b)
+  uint64_t* pre_sum;   // [nblk] exclusive prefix of blk_sum (k_agg_c's fold, or k_agg_scan)
+  uint64_t* pre_cnt;   // [nblk] exclusive prefix of blk_cnt
   int32_t* blk_max;    // [2][nblk] block maxima of start / end -> exclusive prefix
   uint64_t* sess_err;  // [n_sessions] first failing frame (~0 = none), idle between batches
   uint64_t* n_units;   // [1] gather units of the batch (k_agg_scan)
