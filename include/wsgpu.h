@@ -169,6 +169,8 @@ int wsg_close(wsg_ctx* ctx);
  *   WSG_TUNE_INFLATE_LDS     0: the lane pre-decode keeps its tables in HBM
  *   WSG_TUNE_INFLATE_ORDER   0: lanes take frames in batch order (not longest first)
  *   WSG_TUNE_INFLATE_LANES   k_infl_tok lanes at most (multiple of 64)
+ *   WSG_TUNE_INFLATE_SPLIT   the split-lane decode (two lanes a message): 0 never (default), 1 when a
+ *                            lane a frame would leave half the chip's resident lanes idle, 2 always
  *   WSG_TUNE_INFLATE_TABS    HBM table blocks (3,880 B each) for the lanes whose message needs the
  *                            HBM-table decoder (default 32768; beyond, such messages take the
  *                            serial decoder)
@@ -184,7 +186,8 @@ enum {
     WSG_TUNE_FUSED_SCAN = 6,
     WSG_TUNE_AGG_UNITS = 7,
     WSG_TUNE_AGG_GRID = 8,
-    WSG_TUNE_INFLATE_TABS = 9
+    WSG_TUNE_INFLATE_TABS = 9,
+    WSG_TUNE_INFLATE_SPLIT = 10
 };
 int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */
@@ -199,6 +202,11 @@ int wsg_reserve(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions, uint64
  * compressed payload bytes of the largest batch.  Kept apart from wsg_reserve because
  * the inflate workspace is ~7 B per compressed byte (token and literal regions). */
 int wsg_reserve_inflate(wsg_ctx* ctx, uint64_t max_frames, uint32_t max_sessions, uint64_t max_payload_len);
+
+/* Messages the split-lane decode (WSG_TUNE_INFLATE_SPLIT) has decoded on this context since
+ * it was created: a lane pair joined the head's and the tail's halves of each.  Waits for
+ * the context's stream.  (A measurement and test hook; no reference counterpart.) */
+int wsg_inflate_split_count(wsg_ctx* ctx, uint64_t* count);
 int wsg_sync(wsg_ctx* ctx);
 
 /* Kernel timing (hipEvents recorded around each kernel on the ctx stream).
@@ -435,6 +443,10 @@ typedef struct wsg_stage_cfg {
 } wsg_stage_cfg;
 #define WSG_OUT_AGGREGATED 0x02
 int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages);
+/* The context the stages run on (the batcher's own, opened by wsg_batcher_set_stages on the
+ * batcher context's device, with that context's wsg_set_tuning switches), or NULL before
+ * set_stages: for wsg_inflate_split_count and the like.  Owned by the batcher. */
+wsg_ctx* wsg_batcher_stage_context(wsg_batcher* b);
 /* Give slot `sid` to a new session: drops the pending partial frame and any bytes
  * fed since the last flush, and zeroes the carry (fragmentation, UTF-8 context,
  * closed latch), as a freshly constructed FrameDecoder + FrameUtf8Validator

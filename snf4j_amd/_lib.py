@@ -122,6 +122,8 @@ def _load():
         "wsg_last_error": ([p], C.c_char_p),
         "wsg_reserve": ([p, u64, u32, u64], i32),
         "wsg_reserve_inflate": ([p, u64, u32, u64], i32),
+        "wsg_inflate_split_count": ([p, p], i32),
+        "wsg_batcher_stage_context": ([p], p),
         "wsg_sync": ([p], i32),
         "wsg_set_timing": ([p, i32], i32),
         "wsg_set_timing_every": ([p, u32], i32),

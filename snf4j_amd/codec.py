@@ -452,6 +452,19 @@ class NativeBatcher:
         c = StageCfg(int(inflate), int(noContext), int(validate), int(aggregate), 0, int(maxAggregatedLength))
         self._check(lib.wsg_batcher_set_stages(self._h, C.byref(c)))
 
+    def stage_split_count(self) -> int:
+        """Messages the stage chain's inflate took with the split-lane decode
+        (wsg_inflate_split_count on wsg_batcher_stage_context); 0 before set_stages."""
+        import ctypes as C
+        from ._lib import lib
+        h = lib.wsg_batcher_stage_context(self._h)
+        if not h:
+            return 0
+        n = C.c_uint64()
+        if lib.wsg_inflate_split_count(C.c_void_p(h), C.byref(n)) != 0:
+            raise RuntimeError("wsg_inflate_split_count failed")
+        return int(n.value)
+
     def reset_session(self, sid: int):
         """Hand slot `sid` to a new session (wsg_batcher_session_reset): the partial
         frame and the carry are dropped, as a fresh FrameDecoder would start."""

@@ -70,7 +70,7 @@ class Context:
     with wsg_set_stream (wsg_open(NULL) would create a private stream instead)."""
 
     TUNING = {"inflate_tokens": 1, "inflate_fast": 2, "inflate_lds": 3, "inflate_order": 4, "inflate_lanes": 5,
-              "fused_scan": 6, "agg_units": 7, "agg_grid": 8, "inflate_tabs": 9}
+              "fused_scan": 6, "agg_units": 7, "agg_grid": 8, "inflate_tabs": 9, "inflate_split": 10}
 
     def set_tuning(self, name: str, value: int):
         """A measurement / test switch of this context (wsg_set_tuning; wsgpu.h lists them)."""
@@ -126,6 +126,12 @@ class Context:
     def reserve_inflate(self, max_frames: int, max_sessions: int, max_payload_len: int):
         """wsg_reserve_inflate: pre-size the permessage-deflate workspace."""
         check(lib.wsg_reserve_inflate(self._h, int(max_frames), int(max_sessions), int(max_payload_len)), self._h)
+
+    def inflate_split_count(self) -> int:
+        """wsg_inflate_split_count: messages the split-lane decode took on this context."""
+        n = C.c_uint64()
+        check(lib.wsg_inflate_split_count(self._h, C.byref(n)), self._h)
+        return int(n.value)
 
     def set_timing(self, on=True):
         """True: time every kernel; "hot": only the streaming kernels (an event pair

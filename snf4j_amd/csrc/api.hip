@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <string>
 #include <vector>
 
@@ -67,6 +68,8 @@ struct wsg_ctx {
   DevBuf a_code, a_last, a_pl, a_cl, a_blk, a_sess_err, a_pieces;
   DevBuf v_desc;  // validator-only mode: per-frame status scratch
   DevBuf i_tok, i_lit, i_stat, i_tab, i_tabcnt, i_fast, i_ord;  // inflate pre-decode workspace
+  DevBuf i_split;  // [1] u64: messages the split-lane decode took (wsg_inflate_split_count)
+  DevBuf i_tok2, i_lit2;  // the split's tail regions
   // measurement / test switches (wsg_set_tuning; the defaults are the product)
   int infl_tokens = 1;               // WSG_TUNE_INFLATE_TOKENS 0: no lane pre-decode (serial decoder only)
   uint32_t infl_lanes = 262144;      // WSG_TUNE_INFLATE_LANES: k_infl_tok lanes at most
@@ -74,6 +77,8 @@ struct wsg_ctx {
   int infl_fast = 1;                 // WSG_TUNE_INFLATE_FAST 0: no parallel token replay; 2: it alone (tests)
   int infl_lds = 1;                  // WSG_TUNE_INFLATE_LDS 0: the pre-decode keeps its tables in HBM
   int infl_order = 1;                // WSG_TUNE_INFLATE_ORDER 0: lanes take frames in batch order
+  int infl_split = 0;                // WSG_TUNE_INFLATE_SPLIT 0 (default): never, 1: batches that leave lanes idle, 2: always
+                                     //   (measured slower end to end, DESIGN.md §9.1: kept as a switch)
   int fused_scan = 1;                // WSG_TUNE_FUSED_SCAN 0: always launch k_scan
   int agg_units = 2;                 // WSG_TUNE_AGG_UNITS: k_agg_gather units per wave (1, 2 or 4)
   uint32_t agg_grid = 65536;         // WSG_TUNE_AGG_GRID: k_agg_gather waves at most
@@ -163,6 +168,19 @@ hipError_t ctx_wait_prev_state(wsg_ctx* c) { return c->ev_prev_state ? hipEventS
 hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e) { return hipEventRecord(e, c->s_out ? c->s_out : c->stream); }
 hipStream_t ctx_stream(wsg_ctx* c) { return c->stream; }
 hipStream_t ctx_out_stream(wsg_ctx* c) { return c->s_out ? c->s_out : c->stream; }
+// a context's measurement / test switches (wsg_set_tuning) onto another (a batcher's stage context)
+void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src) {
+  dst->infl_tokens = src->infl_tokens;
+  dst->infl_lanes = src->infl_lanes;
+  dst->infl_tabs = src->infl_tabs;
+  dst->infl_fast = src->infl_fast;
+  dst->infl_lds = src->infl_lds;
+  dst->infl_order = src->infl_order;
+  dst->infl_split = src->infl_split;
+  dst->fused_scan = src->fused_scan;
+  dst->agg_units = src->agg_units;
+  dst->agg_grid = src->agg_grid;
+}
 int ctx_device(wsg_ctx* c) { return c->device; }
 uint8_t* ctx_async_payload(wsg_ctx* c) { return c->last_async_payload; }
 }  // namespace ws
@@ -212,7 +230,8 @@ int wsg_close(wsg_ctx* c) {
   for (DevBuf* b : bufs) b->release();
   DevBuf* abufs[] = {&c->a_code, &c->a_last, &c->a_pl, &c->a_cl,
                      &c->a_blk,  &c->a_sess_err, &c->a_pieces, &c->v_desc, &c->i_tok, &c->i_lit,
-                     &c->i_stat, &c->i_tab, &c->i_tabcnt, &c->i_fast, &c->i_ord};
+                     &c->i_stat, &c->i_tab, &c->i_tabcnt, &c->i_fast, &c->i_ord, &c->i_split,
+                     &c->i_tok2, &c->i_lit2};
   for (DevBuf* b : abufs) b->release();
   for (HostSlot& hs : c->slot) {
     DevBuf* sb[] = {&hs.wire, &hs.off, &hs.sf, &hs.state, &hs.payload, &hs.desc, &hs.result};
@@ -236,6 +255,10 @@ int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
     case WSG_TUNE_INFLATE_LDS: c->infl_lds = value != 0; break;
     case WSG_TUNE_INFLATE_ORDER: c->infl_order = value != 0; break;
     case WSG_TUNE_INFLATE_LANES: c->infl_lanes = value < 64 ? 64u : (uint32_t)value & ~63u; break;
+    case WSG_TUNE_INFLATE_SPLIT:
+      if (value < 0 || value > 2) return set_err(c, WSG_API_EINVAL, "INFLATE_SPLIT is 0, 1 or 2");
+      c->infl_split = (int)value;
+      break;
     case WSG_TUNE_INFLATE_TABS: c->infl_tabs = value < 0 ? 0u : (value > (1 << 22) ? (1u << 22) : (uint32_t)value); break;
     case WSG_TUNE_FUSED_SCAN: c->fused_scan = value != 0; break;
     case WSG_TUNE_AGG_UNITS:
@@ -337,8 +360,20 @@ static int ensure_encode_ws(wsg_ctx* c, uint64_t n_frames) {
 
 // the lane pre-decode's workspace for a batch of n_frames frames and payload_len
 // compressed bytes (grow-only, so a batch within a reservation allocates nothing)
+// k_infl_tok's lanes for a batch: a lane a frame, or (the split-lane decode) a pair of
+// lanes a frame when the batch would leave the chip's resident lanes (256 CUs x 4
+// workgroups of 64, what its LDS allows) half idle, or when tuned to always
+static constexpr uint64_t INFL_RESIDENT_LANES = 65536;
+static bool infl_pairs(const wsg_ctx* c, uint64_t n_frames) {
+  return c->infl_lds && (c->infl_split == 2 || (c->infl_split == 1 && 2 * n_frames <= INFL_RESIDENT_LANES));
+}
+static uint64_t infl_lane_count(const wsg_ctx* c, uint64_t n_frames) {
+  const uint64_t want = infl_pairs(c, n_frames) ? 2 * n_frames : n_frames;
+  return want < c->infl_lanes ? ((want + 63) / 64) * 64 : c->infl_lanes;
+}
+
 static int ensure_inflate_ws(wsg_ctx* c, uint64_t n_frames, uint64_t payload_len) {
-  const uint64_t lanes = n_frames < c->infl_lanes ? ((n_frames + 63) / 64) * 64 : c->infl_lanes;
+  const uint64_t lanes = infl_lane_count(c, n_frames);
   const uint64_t n_tab = lanes < c->infl_tabs ? lanes : c->infl_tabs;
   HIP_TRY(c, c->i_tok.ensure(infl_tok_words(payload_len, n_frames) * 4));
   HIP_TRY(c, c->i_lit.ensure(infl_lit_bytes(payload_len, n_frames)));
@@ -346,6 +381,11 @@ static int ensure_inflate_ws(wsg_ctx* c, uint64_t n_frames, uint64_t payload_len
   HIP_TRY(c, c->i_tab.ensure(n_tab * infl_tab_bytes()));
   HIP_TRY(c, c->i_tabcnt.ensure(sizeof(uint32_t)));
   if (c->infl_order) HIP_TRY(c, c->i_ord.ensure(infl_ord_words(n_frames) * 4));
+  HIP_TRY(c, c->i_split.ensure(sizeof(uint64_t), 0, c->stream));
+  if (infl_pairs(c, n_frames)) {
+    HIP_TRY(c, c->i_tok2.ensure(infl_tok_words(payload_len, n_frames) * 4));
+    HIP_TRY(c, c->i_lit2.ensure(infl_lit_bytes(payload_len, n_frames)));
+  }
   return WSG_API_OK;
 }
 
@@ -353,7 +393,26 @@ int wsg_reserve_inflate(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, 
   if (!c) return WSG_API_EINVAL;
   HIP_TRY(c, hipSetDevice(c->device));
   HIP_TRY(c, c->i_fast.ensure(max_sessions ? max_sessions : 1));
-  return ensure_inflate_ws(c, max_frames, max_payload_len);
+  int rc = ensure_inflate_ws(c, max_frames, max_payload_len);
+  if (rc) return rc;
+  // a smaller batch within the reservation may take the split (2 n_frames <= the resident
+  // lanes): its tail regions too
+  const uint64_t split_frames = c->infl_split == 2 ? max_frames : std::min<uint64_t>(max_frames, INFL_RESIDENT_LANES / 2);
+  if (c->infl_split && c->infl_lds && split_frames) {
+    HIP_TRY(c, c->i_tok2.ensure(infl_tok_words(max_payload_len, split_frames) * 4));
+    HIP_TRY(c, c->i_lit2.ensure(infl_lit_bytes(max_payload_len, split_frames)));
+  }
+  return WSG_API_OK;
+}
+
+int wsg_inflate_split_count(wsg_ctx* c, uint64_t* count) {
+  if (!c || !count) return WSG_API_EINVAL;
+  *count = 0;
+  if (!c->i_split.p) return WSG_API_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  HIP_TRY(c, hipMemcpyAsync(count, c->i_split.p, sizeof(uint64_t), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  return WSG_API_OK;
 }
 
 int wsg_reserve(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len) {
@@ -937,8 +996,12 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   a.order = nullptr;
   a.ord_cnt = nullptr;
   a.tok_lds = c->infl_lds;
+  a.split = 0;
+  a.split_cnt = nullptr;
+  a.tok2 = nullptr;
+  a.lit2 = nullptr;
   if (c->infl_tokens && n_frames) {
-    const uint32_t lanes = (uint32_t)(n_frames < c->infl_lanes ? ((n_frames + 63) / 64) * 64 : c->infl_lanes);
+    const uint32_t lanes = (uint32_t)infl_lane_count(c, n_frames);
     const uint64_t lit_len = infl_lit_bytes(payload_len, n_frames);
     const int rc = ensure_inflate_ws(c, n_frames, payload_len);
     if (rc) return rc;
@@ -952,6 +1015,10 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
     a.n_tab = n_tab;
     a.tab_cnt = (uint32_t*)c->i_tabcnt.p;
     a.n_lanes = lanes;
+    a.split = infl_pairs(c, n_frames) ? 1 : 0;
+    a.tok2 = (uint32_t*)c->i_tok2.p;
+    a.lit2 = (uint8_t*)c->i_lit2.p;
+    a.split_cnt = (unsigned long long*)c->i_split.p;
     a.order = nullptr;
     a.ord_cnt = nullptr;
     if (c->infl_order) {

@@ -899,6 +899,8 @@ int wsg_batcher_open(wsg_ctx* ctx, const wsg_decoder_cfg* cfg, uint32_t n_sessio
   return WSG_API_OK;
 }
 
+wsg_ctx* wsg_batcher_stage_context(wsg_batcher* b) { return b ? b->sctx : nullptr; }
+
 int wsg_batcher_close(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
   if (b->sw.joinable()) {  // the stage worker finishes the flushes queued to it, then stops
@@ -1415,6 +1417,7 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
       const int rc = wsg_open(ws::ctx_device(b->ctx), nullptr, &b->sctx);
       if (rc) return bset(b, rc, "wsg_open (stage context)");
     }
+    ws::ctx_copy_tuning(b->sctx, b->ctx);  // (the batcher context's switches hold for its stages)
     hipStream_t st = ws::ctx_stream(b->sctx);
     B_TRY(b, b->d_istate.ensure(((uint64_t)S + 1) * sizeof(wsg_inflate_state)));
     B_TRY(b, b->d_iwin.ensure(((uint64_t)S + 1) * WSG_INFLATE_WINDOW));

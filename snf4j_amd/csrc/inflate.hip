@@ -768,12 +768,14 @@ struct TokLds {
   uint16_t tab[Q_TAB];         // fixed tables, then the lanes' tables
   uint32_t ring[Q_RING * 64];  // input ring: dword slot s of lane i at s * 64 + i
   uint32_t cnt[8 * 64];        // literal/length table build: count, then next code, of length L in
-                               // half L & 1 of dword (L >> 1) * 64 + i (both < 2^16)
+                               // half L & 1 of dword (L >> 1) * 64 + i (both < 2^16); a split's
+                               // window bitmap (split_bm), then the head's hand-over
+  uint32_t mbox[64];           // a split's mailboxes: lane i's position << 2 | state
 };
 static_assert(sizeof(TokLds) <= 160 * 1024 / WSG_TOK_WG_PER_CU || WSG_QL_ROOT != 7 || WSG_QD_ROOT != 6,
               "the default tables fit WSG_TOK_WG_PER_CU workgroups per CU (160 KiB of LDS)");
 
-enum : int { Q_OK = 0, Q_BAD = 1, Q_BAIL = 2 };
+enum : int { Q_OK = 0, Q_BAD = 1, Q_BAIL = 2, Q_SYNC = 3, Q_IDLE = 4 };
 
 // Canonical two-level table of n code lengths into tab (entry j at base + (j << 6)):
 // root entries len | symbol << 4; a prefix of longer codes points at its sub-table
@@ -962,17 +964,60 @@ __device__ void q_fixed_tables(uint16_t* tab, int t) {
   if (t < 32) tab[QF_D + (__builtin_bitreverse32((uint32_t)t) >> 27)] = (uint16_t)(5 | (t << 4));
 }
 
+// Split-lane decode (k_infl_tok<true>; tools/split_decode_proto.py is
+// the CPU model of these rules).  The two lanes of a pair take one message.  Both read
+// its first block's header (same bits, same tables); then the HEAD decodes from the
+// block's first code and the TAIL from a bit near the middle of the payload.  An
+// arbitrary bit is not a code boundary, but a Huffman decode started anywhere falls into
+// step with the true one within a few codes: the tail marks every literal/length code
+// start it meets in a window of SPLIT_WIN bits from its start (a bitmap in the pair's
+// cnt dwords) and keeps its counters there (snapshots at the top of its region).  When
+// the head reaches a marked position with no length pending, both decodes are at the
+// same code of the same block with the same tables, so they agree from there on: the
+// head stops at that point S, and after the loop the tail moves its tokens and literals
+// after S behind the head's (the run it counted before S comes off its first run token)
+// and writes the message's stats.  The tail writes to its own scratch regions (tok2 /
+// lit2, laid out as tok / lit), so the head never has to wait for it or stay in half a
+// region, and the lanes talk only at the window: the tail's mailbox dword (Q.mbox:
+// window start << 2 | state) is read by the head when it reaches the window.  A tail
+// decode that fails (a bad code, an end of block far from the payload's end) while the
+// head cannot have come near the window (the head moves at most 28 bits a step) starts
+// again one bit later; a head that passes the window unmarked, finds the tail still
+// marking or failed, or leaves the first block carries on alone (the tail's output is
+// dropped).  Every step of the loop pays only a compare for the split; the instructions
+// a step issues are what this one-wave-a-SIMD kernel runs on.
+constexpr uint32_t SPLIT_MIN = 1024;   // payload bytes a message needs for a split
+constexpr uint32_t SPLIT_WIN = 512;    // the tail's window, bits
+constexpr uint32_t SPLIT_MARKS = 96;   // snapshots it keeps (the window ends early past them)
+constexpr uint32_t SPLIT_SNAPW = 4 * SPLIT_MARKS + 4;  // tail-region token words they take (16-B aligned inside)
+constexpr uint32_t SPLIT_STEP_BITS = 28;  // the most bits a step consumes (15-bit code + 13 extra)
+constexpr uint32_t SPLIT_RESTARTS = 48;
+enum : uint32_t { TS_MARK = 0, TS_RUN = 1, TS_FAIL = 2 };  // tail states
+enum : uint32_t { HS_WAIT = 0, HS_OFF = 1, HS_SYNC = 2 };  // head states (the head's own)
+
+// bitmap dword q (0..15) of the pair holding `lane`: the pair's cnt dwords
+__device__ __forceinline__ uint32_t split_bm(uint32_t lane, uint32_t q) {
+  return (q >> 1) * 64u + (lane & ~1u) + (q & 1u);
+}
+
 // One single-frame message from LDS.  Q_BAIL: a table needs more sub-table room than
 // the LDS gives a lane; the caller decodes the message with the HBM tables instead.
+// PAIR (split-lane decode above): Q_SYNC, the head stopped where the tail took over;
+// Q_IDLE, the tail had nothing to do (no split, or the head carried on alone).
+template <bool PAIR>
 __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, const wsg_frame_desc& d, uint64_t k,
                                               uint64_t* pf_) {
   (void)pf_;
   const uint32_t lane = threadIdx.x;
+  const uint32_t role = PAIR ? (lane & 1u) : 0u;  // 0: the head (or the only lane), 1: the tail
   const uint32_t plen = d.payload_len, total = plen + 4u;
   const uint64_t off = d.payload_off;
   const uint32_t tok_cap = plen + 68u, lit_cap = lit_cap_of(plen);
   uint32_t* const tok = a.tok + tok_base(off, k);
   uint8_t* const lit = a.lit + lit_base(off, k);
+  uint32_t* tokp = tok;  // this lane's output (a split's tail: its scratch regions)
+  uint8_t* litp = lit;
+  uint32_t tcap = tok_cap, lcap = lit_cap;
   uint16_t* const tab = Q.tab;
   uint32_t* const lw32 = reinterpret_cast<uint32_t*>(Q.tab + Q_DT);  // code length s: nibble s & 7 of dword (s >> 3) * 64 + lane
   const uint32_t lt = Q_LT + lane, dt = Q_DT + lane;
@@ -1060,13 +1105,26 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     hold >>= n;
     bits -= n;
   };
+  // the input from message bit p (a split's tail)
+  auto seek = [&](uint32_t p) {
+    ip = p >> 3;
+    fill = (off + ip) & ~(uint64_t)31;
+    top_up();
+    top_up();
+    avail = (uint32_t)(fill - (off + ip));
+    hold = 0;
+    bits = 0;
+    rw = ring_word(ip);
+    in_step();
+    drop((int)(p & 7u));
+  };
   // --- the output ---
   uint32_t ntok = 0, nlit = 0, run = 0, outlen = 0, litw = 0;
   auto put_lit = [&](uint32_t b) -> bool {
-    if (nlit >= lit_cap) return false;
+    if (nlit >= lcap) return false;
     litw |= b << (8 * (nlit & 3u));
     if ((++nlit & 3u) == 0) {
-      reinterpret_cast<uint32_t*>(lit)[(nlit >> 2) - 1] = litw;
+      reinterpret_cast<uint32_t*>(litp)[(nlit >> 2) - 1] = litw;
       litw = 0;
     }
     ++run;
@@ -1074,8 +1132,8 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     return true;
   };
   auto put_tok = [&](uint32_t t) -> bool {
-    if (ntok >= tok_cap) return false;
-    tok[ntok++] = t;
+    if (ntok >= tcap) return false;
+    tokp[ntok++] = t;
     return true;
   };
   auto end_run = [&]() -> bool {
@@ -1084,6 +1142,15 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     run = 0;
     return r;
   };
+  // --- the split (PAIR) ---
+  bool split = false;  // open for this message (both lanes decide alike)
+  bool blk1 = false;   // in the first block's symbol loop, where the split lives
+  uint32_t ss = 0;     // HS_* (head) / TS_* (tail)
+  uint32_t win0 = 0;   // the tail's window start (the head: as last seen)
+  uint32_t nmarks = 0, restarts = 0, sync_j = 0;
+  uint32_t tsteps = 0, rlimit = 0;  // the tail's steps; it may start again while tsteps < rlimit
+  uint4* snap = nullptr;
+  bool first = true;   // the message's first block
   int st = Q_OK;
   for (;;) {
     in_step();
@@ -1093,6 +1160,8 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     drop(3);
     if (last) { st = Q_BAD; break; }  // a final block: the stream ends (k_inflate handles it)
     if (type == 0) {                  // stored
+      if (PAIR && first && role) { st = Q_IDLE; break; }  // no split: the head decodes it
+      first = false;
       drop(bits & 7);
       in_step();
       if (bits < 32) { st = Q_BAD; break; }
@@ -1203,6 +1272,33 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       TPROF_ACC(2, t_bld);
     }
     TPROF_ACC(1, t_hdr);
+    if (PAIR && first) {  // open a split, or leave the message to the head
+      const uint32_t pos0 = 8u * ip - (uint32_t)bits, endb = 8u * plen;
+      split = a.split != 0 && plen >= SPLIT_MIN && plen < (1u << 26) && endb > pos0 + 4096u;
+      if (!split) {
+        if (role) { st = Q_IDLE; break; }
+      } else {
+        blk1 = true;
+        win0 = pos0 + (uint32_t)(((uint64_t)(endb - pos0) * 15u) >> 5);
+        // the head is at most pos0 + 28 t after t steps: while t < rlimit it is two
+        // windows short of win0, so a restart cannot pull the bitmap from under it
+        rlimit = (win0 - pos0 > 2u * SPLIT_WIN) ? (win0 - pos0 - 2u * SPLIT_WIN) / SPLIT_STEP_BITS : 0u;
+        if (role == 0) {
+          ss = HS_WAIT;
+        } else {
+          tokp = a.tok2 + tok_base(off, k);
+          litp = a.lit2 + lit_base(off, k);
+          tcap = tok_cap - SPLIT_SNAPW;
+          snap = reinterpret_cast<uint4*>((reinterpret_cast<uintptr_t>(tokp + tcap) + 15u) & ~(uintptr_t)15u);
+          ss = TS_MARK;
+#pragma unroll
+          for (uint32_t q = 0; q < 16; ++q) Q.cnt[split_bm(lane, q)] = 0u;
+          seek(win0);
+          Q.mbox[lane] = (win0 << 2) | TS_MARK;
+        }
+      }
+    }
+    first = false;
     TPROF_T(t_sym);
     // the block's symbols, one code a step (literal/length, or the distance of the
     // length before it) through one lookup path
@@ -1210,7 +1306,6 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     const uint32_t lrb = fixed ? QF_LROOT : QL_ROOT, drb = fixed ? QF_DROOT : QD_ROOT;
     const uint32_t tsh = fixed ? 0u : 6u;  // entry j at base + (j << tsh)
     uint32_t mlen = 0;                     // a length waiting for its distance
-    uint32_t* const lit32 = reinterpret_cast<uint32_t*>(lit);
     // Branch-light: one instruction stream for the 64 lanes; the stores are masked to
     // the lanes that complete something (a literal word, a match and the literal run
     // before it), so every output byte is written once.  (Unconditional stores of the
@@ -1228,25 +1323,86 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       const uint32_t e = tok_ent(Q.ents, r >> 4, dist);
       const uint32_t x = e_extra(e), eo = e_op(e);
       const uint32_t v = e_val(e) + ((uint32_t)(hold >> len) & ((1u << x) - 1u));
+      if (PAIR && split) {
+        const uint32_t cur = 8u * ip - (uint32_t)bits;
+        if (role == 0) {
+          if (ss == HS_WAIT && !dist && cur >= win0) {  // at the tail's window: its mailbox
+            const uint32_t pm = Q.mbox[lane ^ 1u];
+            const uint32_t w0 = pm >> 2, ts = pm & 3u;
+            if (w0 > win0) {
+              win0 = w0;  // the tail started again further on: look again there
+            } else if (ts != TS_RUN || cur >= w0 + SPLIT_WIN) {
+              ss = HS_OFF;  // the tail failed or is still marking, or the window passed unmarked
+            } else {
+              const uint32_t b = cur - w0, q = b >> 5;
+              const uint32_t wq = Q.cnt[split_bm(lane, q)];
+              if ((wq >> (b & 31u)) & 1u) {  // S: the tail decoded from here too
+                uint32_t j = (uint32_t)__builtin_popcount(wq & ((1u << (b & 31u)) - 1u));
+                for (uint32_t q2 = 0; q2 < q; ++q2) j += (uint32_t)__builtin_popcount(Q.cnt[split_bm(lane, q2)]);
+                sync_j = j;
+                ss = HS_SYNC;
+                st = Q_SYNC;
+                break;
+              }
+            }
+          }
+        } else {
+          ++tsteps;
+          if (blk1 && ss == TS_MARK && !dist) {
+            if (cur < win0 + SPLIT_WIN && nmarks < SPLIT_MARKS) {
+              const uint32_t b = cur - win0;
+              Q.cnt[split_bm(lane, b >> 5)] |= 1u << (b & 31u);
+              snap[nmarks++] = make_uint4(ntok, nlit, outlen, run);
+            } else {
+              ss = TS_RUN;
+              Q.mbox[lane] = (win0 << 2) | TS_RUN;
+            }
+          }
+        }
+      }
       const bool is_lit = !dist && eo == OP_LIT, is_len = !dist && eo == OP_BASE;
       const uint32_t has_run = (dist && run) ? 1u : 0u;
       // (bitwise: one exit test, no short-circuit branches)
-      const bool bad = ((int)(len + x) > bits) | (eo == OP_BAD) | (is_lit & (nlit >= lit_cap)) |
-                       (dist & (ntok + 1u + has_run > tok_cap));
+      const bool bad = ((int)(len + x) > bits) | (eo == OP_BAD) | (is_lit & (nlit >= lcap)) |
+                       (dist & (ntok + 1u + has_run > tcap));
       const bool eob = !dist & (eo == OP_EOB);
       if (bad | eob) {
+        if (PAIR && split && role && ss != TS_FAIL &&
+            (bad || (blk1 && tsteps < rlimit && 8u * total - (8u * ip - (uint32_t)bits + len) > 48u))) {
+          // the tail off the true stream (an end of block far from the payload's end is
+          // taken for one): again one bit on while the head cannot be near, else give up
+          // (a failure after the head stopped at S is the message's: the serial decoder's)
+          if (blk1 && tsteps < rlimit && restarts < SPLIT_RESTARTS) {
+            ++restarts;
+            ++win0;
+#pragma unroll
+            for (uint32_t q = 0; q < 16; ++q) Q.cnt[split_bm(lane, q)] = 0u;
+            seek(win0);
+            ntok = nlit = run = outlen = litw = 0;
+            mlen = 0;
+            nmarks = 0;
+            ss = TS_MARK;
+            Q.mbox[lane] = (win0 << 2) | TS_MARK;
+            continue;
+          }
+          ss = TS_FAIL;
+          Q.mbox[lane] = (win0 << 2) | TS_FAIL;
+          st = Q_IDLE;
+          break;
+        }
         if (bad) st = Q_BAD;
         else drop((int)len);
         break;
       }
       drop((int)(len + x));
+      uint32_t* const lit32 = reinterpret_cast<uint32_t*>(litp);
       const uint32_t nlit2 = nlit + (is_lit ? 1u : 0u);
       const uint32_t litw2 = is_lit ? (litw | (v << (8u * (nlit & 3u)))) : litw;
       const bool word_done = is_lit && (nlit2 & 3u) == 0u;
       if (word_done) lit32[(nlit2 >> 2) - 1u] = litw2;  // the word just filled
       if (dist) {
-        if (has_run) tok[ntok] = run;
-        tok[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
+        if (has_run) tokp[ntok] = run;
+        tokp[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
       }
       ntok += dist ? 1u + has_run : 0u;
       litw = word_done ? 0u : litw2;
@@ -1256,8 +1412,105 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       mlen = is_len ? v : (dist ? 0u : mlen);
     }
     TPROF_ACC(3, t_sym);
+    if (PAIR && blk1) {  // leaving the first block: the head's split ends, the tail's window closes
+      if (role == 0 && ss == HS_WAIT) ss = HS_OFF;
+      if (role == 1 && ss == TS_MARK) {
+        ss = TS_RUN;
+        Q.mbox[lane] = (win0 << 2) | TS_RUN;
+      }
+      blk1 = false;
+    }
     if (st != Q_OK) break;
   }
+  if (PAIR && split) {
+    // both lanes are past the loop here (the wave leaves it together): the head hands
+    // its counters to the tail through its own cnt dwords
+    if (role == 0) {
+      if (st == Q_SYNC) {
+        end_run();  // (room: checked at S)
+        Q.cnt[0 * 64 + lane] = 1u;
+        Q.cnt[1 * 64 + lane] = sync_j;
+        Q.cnt[2 * 64 + lane] = ntok;
+        Q.cnt[3 * 64 + lane] = nlit;
+        Q.cnt[4 * 64 + lane] = outlen;
+        Q.cnt[5 * 64 + lane] = litw;
+      } else {
+        Q.cnt[0 * 64 + lane] = 0u;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    __asm__ volatile("" ::: "memory");
+    if (role == 1) {
+      const uint32_t hl = lane ^ 1u;
+      if (Q.cnt[0 * 64 + hl] != 1u) return Q_IDLE;  // the head decoded the message alone
+      if (st == Q_BAIL) return Q_BAIL;             // (a later block's tables: the caller's HBM decoder)
+      if (st != Q_OK || !end_run()) {              // the message's own error: the serial decoder's
+        a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
+        return Q_BAD;
+      }
+      if (nlit & 3u) reinterpret_cast<uint32_t*>(litp)[nlit >> 2] = litw;
+      const uint32_t j = Q.cnt[1 * 64 + hl], nth = Q.cnt[2 * 64 + hl], nlh = Q.cnt[3 * 64 + hl],
+                     outh = Q.cnt[4 * 64 + hl], litwh = Q.cnt[5 * 64 + hl];
+      const uint4 sn = snap[j];  // the tail's counters at S: tokens, literals, output, run
+      // its tokens after S behind the head's; the run before S comes off the first run token
+      const uint32_t* src = tokp + sn.x;
+      uint32_t n = ntok - sn.x, nt = nth;
+      const uint32_t m = nlit - sn.y;
+      if (nth + n > tok_cap || nlh + m > lit_cap) {  // (room as the one-lane decode has it)
+        a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
+        return Q_BAD;
+      }
+      if (sn.w && n) {
+        const uint32_t v0 = src[0] - sn.w;
+        if (v0) tok[nt++] = v0;
+        ++src;
+        --n;
+      }
+      uint32_t i = 0;
+      for (; i + 8 <= n; i += 8) {  // (8 loads in flight a lane)
+        uint32_t t[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) t[u] = src[i + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) tok[nt + i + u] = t[u];
+      }
+      for (; i < n; ++i) tok[nt + i] = src[i];
+      nt += n;
+      // its literals after S behind the head's, byte-shifted word by word (the head's
+      // partial last word merged into the first)
+      const uint32_t sb = sn.y, db = nlh;
+      const uint32_t* const s32 = reinterpret_cast<const uint32_t*>(litp);
+      uint32_t* const l32 = reinterpret_cast<uint32_t*>(lit);
+      const uint32_t w0 = db >> 2, we = (db + m + 3u) >> 2;
+      for (uint32_t w = w0; w < we; w += 4) {
+        uint32_t vv[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          // source byte of the word's first byte: below 0 only for the first word, whose
+          // bytes there are the head's (kept below)
+          const int32_t sp = (int32_t)(4u * (w + u) + sb) - (int32_t)db;
+          const int32_t q = sp >> 2;
+          vv[u] = __builtin_amdgcn_alignbyte(s32[q + 1], q >= 0 ? s32[q] : 0u, (uint32_t)sp & 3u);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const uint32_t ww = w + u;
+          if (ww >= we) break;
+          uint32_t x = vv[u];
+          if (ww == w0 && (db & 3u)) {
+            const uint32_t keep = (1u << (8u * (db & 3u))) - 1u;
+            x = (x & ~keep) | (litwh & keep);
+          }
+          l32[ww] = x;
+        }
+      }
+      a.tstat[k] = InflTokStat{1u, nt, nlh + m, outh + (outlen - sn.z)};
+      if (a.split_cnt) atomicAdd(a.split_cnt, 1ull);
+      return Q_SYNC;
+    }
+    if (st == Q_SYNC) return Q_SYNC;
+  }
+  if (PAIR && role) return Q_IDLE;  // (no split: every outcome is the head's)
   if (st == Q_OK) {
     if (!end_run()) st = Q_BAD;
     else {
@@ -1269,6 +1522,9 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   return st;
 }
 
+// PAIR: the two lanes of a pair take the same frames (the split-lane decode above);
+// otherwise a lane takes its own.
+template <bool PAIR>
 __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
   // symbol -> entry (base, extra bits, op) for the 16-bit root entries
   __shared__ TokLds Q;
@@ -1277,15 +1533,17 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
   q_fixed_tables(Q.tab, threadIdx.x);
   __syncthreads();
   const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lane_id >= a.n_lanes) return;
+  if (lane_id >= a.n_lanes) return;  // (n_lanes: whole waves)
 #ifdef WSG_INFLATE_TOK_PROF
   uint64_t pf_[8] = {};
 #define PF_PTR pf_
 #else
 #define PF_PTR nullptr
 #endif
+  const uint32_t unit = PAIR ? lane_id >> 1 : lane_id, n_units = PAIR ? a.n_lanes >> 1 : a.n_lanes;
+  const bool tail = PAIR && (lane_id & 1u);
   LaneTab* T = nullptr;  // the lane's HBM tables, taken from the pool when first needed
-  for (uint64_t i = lane_id; i < a.n_frames; i += a.n_lanes) {
+  for (uint64_t i = unit; i < a.n_frames; i += n_units) {
     const uint64_t k = a.order ? a.order[i] : i;
     const wsg_frame_desc d = a.desc[k];
     const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
@@ -1293,7 +1551,7 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
                        d.payload_off + d.payload_len <= a.payload_len;
     if (!start) {
       // a continuation's stats are its message's (the start frame's lane writes them)
-      if (op != WSG_OP_CONTINUATION) a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
+      if (!tail && op != WSG_OP_CONTINUATION) a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
       continue;
     }
     // The message: frame k and, if it is not FIN, the session's continuation frames up
@@ -1319,16 +1577,18 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
       }
     }
     if (!whole) {
-      a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
+      if (!tail) a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
       continue;
     }
-    if (kend == k) {
+    if (kend == k && a.tok_lds) {
       TPROF_T(t_msg);
-      const int st = a.tok_lds ? tok_single_lds(a, Q, d, k, PF_PTR) : Q_BAIL;
+      const int st = tok_single_lds<PAIR>(a, Q, d, k, PF_PTR);
       TPROF_ACC(0, t_msg);
       TPROF_CNT(6, 1);
       TPROF_CNT(7, st == Q_BAIL);
-      if (st != Q_BAIL) continue;
+      if (st != Q_BAIL) continue;  // (a tail's Q_BAIL: its part of a split needs the HBM tables)
+    } else if (tail) {
+      continue;  // the head takes it alone
     }
     if (!T) {
       const uint32_t slot = atomicAdd(a.tab_cnt, 1u);
@@ -1346,6 +1606,7 @@ __global__ __launch_bounds__(64) void k_infl_tok(InflArgs a) {
 #ifdef WSG_INFLATE_TOK_PROF
   for (int i = 0; i < 8; ++i) atomicAdd(&g_tok_prof[i], (unsigned long long)pf_[i]);
 #endif
+#undef PF_PTR
 }
 
 }  // namespace
@@ -2506,7 +2767,10 @@ void launch_infl_tok(const InflArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(k_ord_scan, dim3(1), dim3(1024), 0, s, a);
     hipLaunchKernelGGL(k_ord_scatter, dim3((uint32_t)((a.n_frames + 255) / 256)), dim3(256), 0, s, a);
   }
-  hipLaunchKernelGGL(k_infl_tok, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+  if (a.split)
+    hipLaunchKernelGGL(k_infl_tok<true>, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL(k_infl_tok<false>, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
 }
 uint64_t infl_ord_words(uint64_t n_frames) { return n_frames + ORD_BUCKETS; }
 

@@ -202,6 +202,10 @@ struct InflArgs {
   int tok_lds;                // k_infl_tok decodes single-frame messages from LDS tables (else HBM tables)
   uint32_t* order;            // [n_frames] frame order for k_infl_tok's lanes (longest first), or null
   uint32_t* ord_cnt;          // [ORD_BUCKETS] its counting-sort buckets
+  int split;                  // k_infl_tok<true>: lane pairs, split-lane decode of each message
+  uint32_t* tok2;             // the split's tail regions (laid out as tok / lit)
+  uint8_t* lit2;
+  unsigned long long* split_cnt;  // [1] messages a split decoded (accumulates), or null
 };
 
 struct InflTokStat {
@@ -223,7 +227,8 @@ hipError_t ctx_record_out(wsg_ctx* c, hipEvent_t e);
 // the context's kernel stream, and the device payload of its last async batch (valid
 // in stream order until a later batch reuses that staging slot)
 hipStream_t ctx_stream(wsg_ctx* c);
-hipStream_t ctx_out_stream(wsg_ctx* c);  // where ctx_record_out records (the download stream)
+hipStream_t ctx_out_stream(wsg_ctx* c);
+void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src);  // where ctx_record_out records (the download stream)
 int ctx_device(wsg_ctx* c);
 uint8_t* ctx_async_payload(wsg_ctx* c);
 

@@ -493,3 +493,109 @@ def test_inflate_lds_table_paths(oracle):
         assert zlib.decompressobj(-15).decompress(comp[i] + b"\x00\x00\xff\xff") == body
         for r in results:
             assert r[i] == body, (i, kind)
+
+
+def _split_ctx(mode):
+    from snf4j_amd import Context
+    c = Context(0)
+    c.set_tuning("inflate_split", mode)
+    return c
+
+
+@pytest.mark.parametrize("msg_bytes", [4096, 16384])
+def test_inflate_split_lanes_match_zlib(oracle, msg_bytes):
+    """The split-lane decode (k_infl_tok<true>: a head lane from the block's first code, a
+    tail lane from the middle, joined where the head meets one of the tail's code starts)
+    on the bench's message shape (context takeover, one FIN frame a message, ~3x
+    compressible text): with it forced (inflate_split 2) every message must equal zlib's
+    and the serial decoder's (inflate_tokens 0), and the split must have taken most
+    messages (wsg_inflate_split_count); with it off (inflate_split 0) the one-lane decode
+    gives the same bytes.  (Only messages whose code tables fit a lane's LDS room split:
+    the others take the HBM-table decoder, tok_message, alone.  At 16 KiB, with more
+    distinct codes, that is most of them.)"""
+    import zlib
+    from snf4j_amd._lib import INFLATE_STATE_DTYPE
+    from benchsupport.synth import deflate_batch
+    n_s, msgs = 64, 6
+    desc, sf, payload, plain = deflate_batch(0x5B1 + msg_bytes, n_s, msgs, msg_bytes, unique=16)
+    n_big = int((desc["payload_len"] >= 1024).sum())
+    assert n_big >= n_s * msgs // 2  # the shape this test is about: messages a split takes
+    outs = []
+    for env in ({"inflate_split": 2}, {"inflate_split": 0}, {"inflate_tokens": 0}):
+        from snf4j_amd import Context
+        c = Context(0)
+        for k, v in env.items():
+            c.set_tuning(k, v)
+        state = np.zeros(n_s, dtype=INFLATE_STATE_DTYPE)
+        window = np.zeros(n_s * 32768, dtype=np.uint8)
+        out_off = (np.arange(n_s + 1) * msgs * (msg_bytes + 4096)).astype(np.uint64)
+        out, od, res, rf = c.inflate_host(False, desc, sf, payload, state, window, out_off)
+        assert (res["error"] == 0).all()
+        outs.append([out[int(o["payload_off"]):int(o["payload_off"]) + int(o["payload_len"])].tobytes() for o in od])
+        n_split = c.inflate_split_count()
+        c.close()
+        if env.get("inflate_split") == 2:
+            assert n_split >= (0.9 if msg_bytes <= 4096 else 0.25) * n_big, (n_split, n_big)
+        else:
+            assert n_split == 0, (env, n_split)
+    assert outs[0] == outs[1] == outs[2]
+    for s in range(n_s):
+        z = zlib.decompressobj(-15)
+        for j in range(msgs):
+            o = desc[s * msgs + j]
+            exp = z.decompress(payload[int(o["payload_off"]):int(o["payload_off"]) + int(o["payload_len"])].tobytes()
+                               + b"\x00\x00\xff\xff")
+            assert outs[0][s * msgs + j] == exp, (s, j)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_inflate_random_batches_split_modes(oracle, seed):
+    """test_inflate_random_batches' sessions (fragments, pings, raw messages, final
+    blocks, damaged bytes) with the split-lane decode forced on every message, and off."""
+    for mode in (2, 0):
+        rng = np.random.default_rng(1300 + seed)
+        no_context = bool(seed & 1)
+        level = [1, 6, 9][seed % 3]
+        n_s = int(rng.integers(1, 48))
+        sessions = [_session(rng, int(rng.integers(0, 10)), level, no_context, big=True, corrupt=seed in (2, 5))
+                    for _ in range(n_s)]
+        c = _split_ctx(mode)
+        try:
+            _run(c, oracle, sessions, no_context, 1 + seed % 3, rng)
+        finally:
+            c.close()
+
+
+def test_inflate_lds_table_paths_split(oracle):
+    """_lds_path_messages (fixed codes, stored blocks, wide and far codes, several blocks a
+    message) with the split-lane decode forced, against zlib: a first block that is
+    stored leaves the message to the head, a split whose window falls past the first
+    block's end is dropped, and the tail's later blocks rebuild its tables."""
+    from snf4j_amd._lib import DESC_DTYPE, INFLATE_STATE_DTYPE
+    rng = np.random.default_rng(0x5D5)
+    kinds = _lds_path_messages(rng)
+    comp = [(c.compress(body) + c.flush(zlib.Z_SYNC_FLUSH))[:-4] for _, body, c in kinds]
+    n = len(kinds)
+    desc = np.zeros(n, dtype=DESC_DTYPE)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    np.cumsum([len(x) for x in comp], out=off[1:])
+    desc["payload_off"] = off[:-1]
+    desc["payload_len"] = [len(x) for x in comp]
+    desc["opcode"] = 1
+    desc["flags"] = 0x80 | (4 << 4)
+    payload = np.frombuffer(b"".join(comp) + bytes(16), dtype=np.uint8)
+    sf = np.arange(n + 1, dtype=np.uint32)
+    cap = max(len(b) for _, b, _ in kinds) + 64
+    out_off = (np.arange(n + 1) * cap).astype(np.uint64)
+    c = _split_ctx(2)
+    try:
+        state = np.zeros(n, dtype=INFLATE_STATE_DTYPE)
+        window = np.zeros(n * 32768, dtype=np.uint8)
+        out, od, res, rf = c.inflate_host(True, desc, sf, payload, state, window, out_off)
+        assert (res["error"] == 0).all(), res["error"]
+        assert c.inflate_split_count() > 0
+    finally:
+        c.close()
+    for i, (kind, body, _) in enumerate(kinds):
+        o = od[i]
+        assert out[int(o["payload_off"]):int(o["payload_off"]) + int(o["payload_len"])].tobytes() == body, (i, kind)

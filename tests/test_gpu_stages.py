@@ -24,7 +24,7 @@ def ctx():
     c.close()
 
 
-def _messages(rng, n_msgs, no_context, bad_utf8):
+def _messages(rng, n_msgs, no_context, bad_utf8, big=False):
     """(opcode, fin, rsv, payload) of one session: compressed text/binary messages cut
     into fragments with pings between them, uncompressed messages, invalid UTF-8 in a
     few compressed text messages, corrupt compressed bytes now and then."""
@@ -42,8 +42,9 @@ def _messages(rng, n_msgs, no_context, bad_utf8):
             out.append((9, True, 0, b"ping"))
             continue
         op = 1 if rng.random() < 0.7 else 2
-        body = wsgen.rand_text(rng, int(rng.integers(0, 3000))) if op == 1 else \
-            rng.integers(0, 256, int(rng.integers(0, 3000)), dtype=np.uint8).tobytes()
+        top = 12000 if big else 3000
+        body = wsgen.rand_text(rng, int(rng.integers(0, top))) if op == 1 else \
+            rng.integers(0, 256, int(rng.integers(0, top)), dtype=np.uint8).tobytes()
         if op == 1 and rng.random() < bad_utf8:
             bad = wsgen.BAD_UTF8[int(rng.integers(0, len(wsgen.BAD_UTF8)))]
             at = int(rng.integers(0, len(body) + 1))
@@ -98,13 +99,33 @@ def _oracle_chain(oracle, stream, no_context, validate, aggregate, max_agg):
 @pytest.mark.parametrize("seed,no_context,aggregate", [(0, False, True), (1, True, True), (2, False, False),
                                                        (3, False, True)])
 def test_batcher_stage_chain_matches_oracle(ctx, oracle, seed, no_context, aggregate):
+    _chain_case(ctx, oracle, seed, no_context, aggregate)
+
+
+def test_batcher_stage_chain_split_lanes(oracle):
+    """The chain with the split-lane inflate forced (set_tuning inflate_split 2 on the
+    batcher's context, which its stage context takes over), with and without context
+    takeover; the split must have taken some messages (a message cut into fragments, or
+    whose tables need the HBM decoder, is decoded by one lane)."""
+    from snf4j_amd import Context
+    c = Context(0)
+    try:
+        c.set_tuning("inflate_split", 2)
+        n_split = sum(_chain_case(c, oracle, seed, no_context, True, big=True)
+                      for seed, no_context in ((0, False), (1, True)))
+        assert n_split > 0
+    finally:
+        c.close()
+
+
+def _chain_case(ctx, oracle, seed, no_context, aggregate, big=False):
     from snf4j_amd import NativeBatcher
     rng = np.random.default_rng(6100 + seed)
     n = 48
     max_agg = 4000 if seed == 3 else 1 << 20
     streams = []
     for s in range(n):
-        msgs = _messages(rng, int(rng.integers(1, 14)), no_context, bad_utf8=0.05)
+        msgs = _messages(rng, int(rng.integers(1, 14)), no_context, bad_utf8=0.05, big=big)
         wire = b"".join(wsgen.build_frame(op, fin, rsv, p, True, tuple(int(x) for x in rng.integers(0, 256, 4)))
                         for (op, fin, rsv, p) in msgs)
         if s % 11 == 5:  # a protocol error after some frames (opcode 3)
@@ -134,7 +155,9 @@ def test_batcher_stage_chain_matches_oracle(ctx, oracle, seed, no_context, aggre
         assert [(int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload()) for f in got[s]] == exp, s
         n_err += eerr is not None
     assert n_err  # the generator produced failures of some kind
+    n_split = b.stage_split_count()
     b.close()
+    return n_split
 
 
 @pytest.mark.parametrize("seed,aggregate", [(10, True), (11, False)])
