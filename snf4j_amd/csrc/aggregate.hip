@@ -43,7 +43,10 @@ constexpr uint32_t AG_CARRY = 64u;   // member of the frame carried in from an e
 
 // grids up to this many blocks fold the block aggregates before their own in k_agg_b /
 // k_agg_c (no k_agg_scan launch); k_agg_c stages the sums' prefixes in LDS (16 B a block)
-constexpr uint32_t AGG_FOLD_MAX = 2048;
+#ifndef WSG_AGG_FOLD_MAX
+#define WSG_AGG_FOLD_MAX 3072  // (configs[2]: 2,128 blocks fold; k_agg_c stages 16 B a block: 48 KiB of LDS at most)
+#endif
+constexpr uint32_t AGG_FOLD_MAX = WSG_AGG_FOLD_MAX;
 __device__ __forceinline__ uint64_t agg_pos(const AggArgs& a, uint64_t j) { return a.pl[j] + a.pre_sum[j / BLOCK]; }
 // cl / blk_cnt pack two counts: emitted frames (bits 0-31) and gather units (32-63)
 __device__ __forceinline__ uint64_t agg_cnt(const AggArgs& a, uint64_t j) {

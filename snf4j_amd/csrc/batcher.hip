@@ -49,7 +49,8 @@
 static double g_sp[16];
 static const char* g_sp_name[16] = {"compute", "inflate.input", "inflate.kernels+sync", "inflate.results",
                                     "validate", "aggregate", "fin.list", "gather.launch", "finish.sync", "wait.total",
-                                    "precompute", "gather.pay_ensure", "gather.upload", "inflate.x", "", ""};
+                                    "precompute", "gather.pay_ensure", "gather.upload", "inflate.x", "inflate.launch",
+                                    "validate.sync"};
 struct SpT {
   int i;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
@@ -60,6 +61,13 @@ struct SpT {
 #else
 #define SP(k) (void)0
 #endif
+
+// The stage worker's events sleep while it waits (hipEventBlockingSync) rather than spin
+// on a core the feed threads use (-DWSG_STAGE_BLOCKING=0: spinning, for A/B).
+#ifndef WSG_STAGE_BLOCKING
+#define WSG_STAGE_BLOCKING 1
+#endif
+#define WSG_STAGE_EVENT_FLAGS (hipEventDisableTiming | (WSG_STAGE_BLOCKING ? hipEventBlockingSync : 0))
 
 namespace {
 
@@ -385,6 +393,7 @@ struct FlushSlot {
   std::vector<uint32_t> resets;   // slots given to a new session while this batch was in flight
   std::vector<int64_t> detail2;   // [n]: the view's detail2
   hipEvent_t done = nullptr;      // after its downloads
+  hipEvent_t done_w = nullptr;    // the same point, for the stage worker (WSG_STAGE_EVENT_FLAGS)
   uint64_t ticket = 0;            // its flush number (wsg_batcher_ticket)
   int st_state = 0;               // stages: 0 none, 1 queued for the stage worker, 2 staged (st_rc)
   int st_rc = 0;
@@ -513,6 +522,8 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     x.sf.assign(S + 1, 0);
     std::vector<uint64_t> oo(S + 1, 0);
     size_t ti = 0;
+    {
+    SP(1);
     for (uint32_t s = 0; s < S; ++s) {
       x.sf[s] = (uint32_t)x.desc.size();
       const bool in = ti < todo.size() && todo[ti] == s;
@@ -532,6 +543,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
         d.flags &= (uint8_t)~WSG_DESC_REPLAY;
         x.desc.push_back(d);
       }
+    }
     }
     x.sf[S] = (uint32_t)x.desc.size();
     const uint64_t F = x.desc.size();
@@ -568,6 +580,8 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
       uint64_t src, dst, len;
     };
     std::vector<Held> hd_copies;
+    {
+    SP(3);
     for (uint32_t s : todo) {
       if (r[s].error == WSG_E_INFLATE_CAPACITY) {
         cap[s] *= 8;
@@ -600,6 +614,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
       }
       h.held_desc.swap(nhd);
       h.held_bytes.assign(nb, 0);
+    }
     }
     for (const Held& c : hd_copies)
       if (c.len)
@@ -645,7 +660,10 @@ static int stage_validate(wsg_batcher* b, StageList& cur, uint64_t used) {
   if (rc) return bset(b, rc, wsg_last_error(b->sctx));
   B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
-  B_TRY(b, hipStreamSynchronize(st));
+  {
+    SP(15);
+    B_TRY(b, hipStreamSynchronize(st));
+  }
   const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
   for (uint32_t s = 0; s < S; ++s) {
     cur.n_ok[s] = std::min(cur.n_ok[s], r[s].n_delivered);
@@ -805,15 +823,18 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   StageList cur;
   cur.sf.assign(S + 1, 0);
   cur.n_ok.assign(S, 0);
-  for (uint32_t s = 0; s < S; ++s) {
-    cur.sf[s] = (uint32_t)cur.desc.size();
-    const uint32_t nd = b->stage_closed[s] ? 0u : res[s].n_delivered;
-    for (uint32_t k = sf[s]; k < sf[s] + nd; ++k) {
-      wsg_frame_desc d = desc[k];
-      d.flags &= 0xf0u | 0x80u;  // FIN, RSV (the "was masked" bit is the decoder's)
-      cur.desc.push_back(d);
+  {
+    SP(10);
+    for (uint32_t s = 0; s < S; ++s) {
+      cur.sf[s] = (uint32_t)cur.desc.size();
+      const uint32_t nd = b->stage_closed[s] ? 0u : res[s].n_delivered;
+      for (uint32_t k = sf[s]; k < sf[s] + nd; ++k) {
+        wsg_frame_desc d = desc[k];
+        d.flags &= 0xf0u | 0x80u;  // FIN, RSV (the "was masked" bit is the decoder's)
+        cur.desc.push_back(d);
+      }
+      cur.n_ok[s] = nd;
     }
-    cur.n_ok[s] = nd;
   }
   cur.sf[S] = (uint32_t)cur.desc.size();
   uint64_t used = al16(f.pcap);
@@ -842,7 +863,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   // stages have the GPU meanwhile (a runtime D2H here is a blit kernel that takes
   // every CU while it waits on PCIe)
   if (!o.gathered) B_TRY(b, hipEventCreateWithFlags(&o.gathered, hipEventDisableTiming));
-  if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, hipEventDisableTiming));
+  if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, WSG_STAGE_EVENT_FLAGS));
   if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
   {
     SP(11);
@@ -923,6 +944,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     if (f.so.gathered) (void)hipEventDestroy(f.so.gathered);
     if (f.so.downloaded) (void)hipEventDestroy(f.so.downloaded);
     if (f.done) (void)hipEventDestroy(f.done);
+    if (f.done_w) (void)hipEventDestroy(f.done_w);
     if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
   }
   b->st.release();
@@ -1213,6 +1235,10 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     f.pcap = pcap;
   }
   B_TRY(b, ws::ctx_record_out(b->ctx, f.done));
+  if (b->has_stages) {
+    if (!f.done_w) B_TRY(b, hipEventCreateWithFlags(&f.done_w, WSG_STAGE_EVENT_FLAGS));
+    B_TRY(b, ws::ctx_record_out(b->ctx, f.done_w));
+  }
   f.ticket = b->tickets + 1;
   if (b->has_stages) {  // the stage worker runs the chain once the decode is done, then signals
     {
@@ -1365,7 +1391,7 @@ static void stage_worker(wsg_batcher* b) {
       slot = b->sw_jobs.front();
     }
     FlushSlot& f = b->fs[slot];
-    int rc = hipEventSynchronize(f.done) == hipSuccess ? WSG_API_OK : WSG_API_EHIP;
+    int rc = hipEventSynchronize(f.done_w) == hipSuccess ? WSG_API_OK : WSG_API_EHIP;
     std::vector<wsg_session_result> res;
     {
       std::lock_guard<std::mutex> g(b->sw_m);
