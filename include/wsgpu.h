@@ -403,7 +403,10 @@ int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* s
  * than the one driving the batcher (stop that thread before wsg_batcher_close): a
  * completion thread awaits a flush, then re-enters the selector loop
  * (SelectorLoop.executenf, InternalSelectorLoop.java:990-1011), whose task collects
- * it with wsg_batcher_wait without waiting.  Replaces nothing in the reference (its
+ * it with wsg_batcher_wait without waiting.  With stages (wsg_batcher_set_stages) the
+ * ticket marks the decode; wsg_batcher_wait then runs the stage chain on the calling
+ * thread (a stage thread that ran it as soon as the decode was done measured 8-20%
+ * slower on the stage lines: DESIGN.md §8c).  Replaces nothing in the reference (its
  * decode is synchronous on the loop thread). */
 uint64_t wsg_batcher_ticket(wsg_batcher* b);
 int64_t wsg_batcher_await(wsg_batcher* b, uint64_t seen, int64_t timeout_ms);

@@ -62,12 +62,6 @@ struct SpT {
 #define SP(k) (void)0
 #endif
 
-// The stage worker's events sleep while it waits (hipEventBlockingSync) rather than spin
-// on a core the feed threads use (-DWSG_STAGE_BLOCKING=0: spinning, for A/B).
-#ifndef WSG_STAGE_BLOCKING
-#define WSG_STAGE_BLOCKING 1
-#endif
-#define WSG_STAGE_EVENT_FLAGS (hipEventDisableTiming | (WSG_STAGE_BLOCKING ? hipEventBlockingSync : 0))
 
 namespace {
 
@@ -393,10 +387,7 @@ struct FlushSlot {
   std::vector<uint32_t> resets;   // slots given to a new session while this batch was in flight
   std::vector<int64_t> detail2;   // [n]: the view's detail2
   hipEvent_t done = nullptr;      // after its downloads
-  hipEvent_t done_w = nullptr;    // the same point, for the stage worker (WSG_STAGE_EVENT_FLAGS)
   uint64_t ticket = 0;            // its flush number (wsg_batcher_ticket)
-  int st_state = 0;               // stages: 0 none, 1 queued for the stage worker, 2 staged (st_rc)
-  int st_rc = 0;
 };
 
 struct wsg_batcher {
@@ -433,16 +424,6 @@ struct wsg_batcher {
   StageOut* out = nullptr;              // the output the stage run at hand writes
   uint64_t tickets = 0;                 // flushes queued so far (flush t's ticket is t)
   std::shared_ptr<Notify> notify = std::make_shared<Notify>();
-  // The stage worker: a flush's stage chain runs on this thread as soon as its decode
-  // is done, so the loop thread's next feeds overlap it (wsg_batcher_wait joins it).
-  // Only the worker touches the stage carry (ss, stage_closed, stage_resets, the stage
-  // buffers, sctx); the loop thread hands it slot resets through sw_resets.
-  std::thread sw;
-  std::mutex sw_m;
-  std::condition_variable sw_cv;
-  std::deque<int> sw_jobs;                              // slots to stage, in flush order
-  std::vector<std::pair<uint32_t, uint64_t>> sw_resets;  // (sid, flushes queued when it was reset)
-  bool sw_stop = false;
 };
 
 static int bset(wsg_batcher* b, int code, const char* msg) {
@@ -863,7 +844,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   // stages have the GPU meanwhile (a runtime D2H here is a blit kernel that takes
   // every CU while it waits on PCIe)
   if (!o.gathered) B_TRY(b, hipEventCreateWithFlags(&o.gathered, hipEventDisableTiming));
-  if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, WSG_STAGE_EVENT_FLAGS));
+  if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, hipEventDisableTiming));
   if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
   {
     SP(11);
@@ -891,7 +872,8 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
 // Wait for a flush's stage output and put in the bytes only the host holds.
 static int stage_finish(wsg_batcher* b, FlushSlot& f) {
   SP(8);
-  StageOut& o = f.so;  // (the stage worker waited for its download)
+  StageOut& o = f.so;
+  B_TRY(b, hipEventSynchronize(o.downloaded));
   for (auto& hp : o.host_parts)
     if (!hp.second.empty()) memcpy(o.pay.p + hp.first, hp.second.data(), hp.second.size());
   o.host_parts.clear();
@@ -924,14 +906,6 @@ wsg_ctx* wsg_batcher_stage_context(wsg_batcher* b) { return b ? b->sctx : nullpt
 
 int wsg_batcher_close(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
-  if (b->sw.joinable()) {  // the stage worker finishes the flushes queued to it, then stops
-    {
-      std::lock_guard<std::mutex> g(b->sw_m);
-      b->sw_stop = true;
-    }
-    b->sw_cv.notify_all();
-    b->sw.join();
-  }
   (void)wsg_sync(b->ctx);
   if (b->sctx) (void)wsg_sync(b->sctx);
   if (b->s_dl) (void)hipStreamSynchronize(b->s_dl);
@@ -944,7 +918,6 @@ int wsg_batcher_close(wsg_batcher* b) {
     if (f.so.gathered) (void)hipEventDestroy(f.so.gathered);
     if (f.so.downloaded) (void)hipEventDestroy(f.so.downloaded);
     if (f.done) (void)hipEventDestroy(f.done);
-    if (f.done_w) (void)hipEventDestroy(f.done_w);
     if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
   }
   b->st.release();
@@ -1235,22 +1208,8 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     f.pcap = pcap;
   }
   B_TRY(b, ws::ctx_record_out(b->ctx, f.done));
-  if (b->has_stages) {
-    if (!f.done_w) B_TRY(b, hipEventCreateWithFlags(&f.done_w, WSG_STAGE_EVENT_FLAGS));
-    B_TRY(b, ws::ctx_record_out(b->ctx, f.done_w));
-  }
   f.ticket = b->tickets + 1;
-  if (b->has_stages) {  // the stage worker runs the chain once the decode is done, then signals
-    {
-      std::lock_guard<std::mutex> g(b->sw_m);
-      f.st_state = 1;
-      f.st_rc = 0;
-      b->sw_jobs.push_back(slot);
-    }
-    b->sw_cv.notify_all();
-  } else {
-    B_TRY(b, notify_after(ws::ctx_out_stream(b->ctx), b->notify, f.ticket));
-  }
+  B_TRY(b, notify_after(ws::ctx_out_stream(b->ctx), b->notify, f.ticket));
   ++b->tickets;
   b->q.push_back(slot);
   // feeds go to the next slot (waited: at most two in flight)
@@ -1288,12 +1247,6 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   b->q.pop_front();
   FlushSlot& f = b->fs[slot];
   B_TRY(b, hipEventSynchronize(f.done));
-  if (f.st_state) {  // the stage worker reads this flush's results: it finishes first
-    std::unique_lock<std::mutex> l(b->sw_m);
-    b->sw_cv.wait(l, [&] { return f.st_state == 2; });
-    f.st_state = 0;
-    if (f.st_rc) return bset(b, f.st_rc, "stage chain failed");
-  }
   const uint32_t S = b->n;
   const wsg_session_state* st = (const wsg_session_state*)b->st.p;
   if (b->q.empty()) {  // the state after the last batch (else the newer batch owns the pinned copy)
@@ -1341,8 +1294,18 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
       x.host_closed = true;
     }
   if (!b->has_stages) return WSG_API_OK;
-  int rc2 = stage_finish(b, f);  // (joined above)
+  int rc2 = f.so.staged ? WSG_API_OK : stage_compute(b, f, res);
   if (rc2) return rc2;
+  // the next flush's stages, while this one's output downloads (its decode done)
+  if (!b->q.empty()) {
+    FlushSlot& g = b->fs[b->q.front()];
+    if (!g.so.staged && hipEventQuery(g.done) == hipSuccess) {
+      std::vector<wsg_session_result> gres;
+      adjusted_results(b, g, gres);
+      if ((rc2 = stage_compute(b, g, gres.data()))) return rc2;
+    }
+  }
+  if ((rc2 = stage_finish(b, f))) return rc2;
   StageOut& o = f.so;
   for (uint32_t sid : f.resets) o.res[sid] = wsg_session_result{};  // (also those reset after its stages ran)
   for (uint32_t i = 0; i < S; ++i) {
@@ -1377,55 +1340,6 @@ int wsg_batcher_flush(wsg_batcher* b, wsg_batch_view* out) {
   return wsg_batcher_wait(b, out);
 }
 
-// The stage worker (see wsg_batcher): per queued flush, in order, wait for its decode,
-// apply the slot resets that came before it was queued, run its stage chain, wait for
-// its output download, then signal wsg_batcher_wait and the completion waiters.
-static void stage_worker(wsg_batcher* b) {
-  (void)hipSetDevice(ws::ctx_device(b->ctx));  // (the current device is per thread)
-  for (;;) {
-    int slot;
-    {
-      std::unique_lock<std::mutex> l(b->sw_m);
-      b->sw_cv.wait(l, [&] { return b->sw_stop || !b->sw_jobs.empty(); });
-      if (b->sw_jobs.empty()) return;  // (stop, nothing left)
-      slot = b->sw_jobs.front();
-    }
-    FlushSlot& f = b->fs[slot];
-    int rc = hipEventSynchronize(f.done_w) == hipSuccess ? WSG_API_OK : WSG_API_EHIP;
-    std::vector<wsg_session_result> res;
-    {
-      std::lock_guard<std::mutex> g(b->sw_m);
-      // resets of slots before this flush was queued: fresh stage decoders
-      std::vector<std::pair<uint32_t, uint64_t>> keep;
-      for (const auto& r : b->sw_resets) {
-        if (r.second < f.ticket) {
-          b->ss[r.first] = StageSess{};
-          b->stage_closed[r.first] = 0;
-          b->stage_resets.push_back(r.first);
-        } else {
-          keep.push_back(r);
-        }
-      }
-      b->sw_resets.swap(keep);
-      adjusted_results(b, f, res);  // (f.resets: slots reset while this flush was in flight)
-    }
-    if (rc == WSG_API_OK) rc = stage_compute(b, f, res.data());
-    if (rc == WSG_API_OK && hipEventSynchronize(f.so.downloaded) != hipSuccess) rc = WSG_API_EHIP;
-    {
-      std::lock_guard<std::mutex> g(b->sw_m);
-      f.st_rc = rc;
-      f.st_state = 2;
-      b->sw_jobs.pop_front();
-    }
-    b->sw_cv.notify_all();
-    {  // the completion waiters (wsg_batcher_await): this flush's output is ready
-      std::lock_guard<std::mutex> g(b->notify->m);
-      if (f.ticket > b->notify->done) b->notify->done = f.ticket;
-    }
-    b->notify->cv.notify_all();
-  }
-}
-
 int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
   if (!b || !stages) return WSG_API_EINVAL;
   if (stages->aggregate && stages->max_aggregated_len < 0) return bset(b, WSG_API_EINVAL, "max_aggregated_len < 0");
@@ -1452,7 +1366,6 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
     DBuf* z[] = {&b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate};
     for (DBuf* d : z) B_TRY(b, hipMemsetAsync(d->p, 0, d->n, st));
     B_TRY(b, hipStreamSynchronize(st));
-    if (!b->sw.joinable()) b->sw = std::thread(stage_worker, b);
   }
   return WSG_API_OK;
 }
@@ -1512,14 +1425,13 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
   x.d1 = x.d2 = 0;
   x.host_closed = false;
   b->state[sid] = wsg_session_state{};
-  {  // (the stage worker reads the in-flight slots' resets)
-    std::lock_guard<std::mutex> g(b->sw_m);
-    for (int slot : b->q) b->fs[slot].resets.push_back(sid);  // the old session's results in flight are dropped
-    // fresh stage decoders too: the worker zeroes the stage carry before staging the
-    // first flush queued after this reset
-    if (b->has_stages) b->sw_resets.push_back({sid, b->tickets});
-  }
+  for (int slot : b->q) b->fs[slot].resets.push_back(sid);  // the old session's results in flight are dropped
   b->patch.push_back({sid, 0});
+  if (b->has_stages) {  // fresh stage decoders too (the device carry is zeroed before the next stage run)
+    b->ss[sid] = StageSess{};
+    b->stage_closed[sid] = 0;
+    b->stage_resets.push_back(sid);
+  }
   return WSG_API_OK;
 }
 
