@@ -1321,6 +1321,10 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         r = tab[base + (((1u << rb) + (r >> 8) + ((uint32_t)(hold >> rb) & ((1u << ((r >> 4) & 15u)) - 1u))) << tsh)];
       const uint32_t len = r & 15u;
       const uint32_t e = tok_ent(Q.ents, r >> 4, dist);
+      // a second literal in the same step (text is mostly literals): the root entry of the
+      // code after this one, read beside the symbol entry, taken when both are literals
+      // whose codes the root resolves
+      const uint32_t r2 = !PAIR ? tab[lbase + ((((uint32_t)(hold >> len)) & ((1u << lrb) - 1u)) << tsh)] : 0u;
       const uint32_t x = e_extra(e), eo = e_op(e);
       const uint32_t v = e_val(e) + ((uint32_t)(hold >> len) & ((1u << x) - 1u));
       if (PAIR && split) {
@@ -1394,21 +1398,24 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         else drop((int)len);
         break;
       }
-      drop((int)(len + x));
+      const uint32_t len2 = r2 & 15u, sym2 = r2 >> 4;
+      const bool two = !PAIR && is_lit && len2 != 0u && sym2 < 256u && (int)(len + len2) <= bits && nlit + 2u <= lcap;
+      drop((int)(len + x + (two ? len2 : 0u)));
       uint32_t* const lit32 = reinterpret_cast<uint32_t*>(litp);
-      const uint32_t nlit2 = nlit + (is_lit ? 1u : 0u);
-      const uint32_t litw2 = is_lit ? (litw | (v << (8u * (nlit & 3u)))) : litw;
-      const bool word_done = is_lit && (nlit2 & 3u) == 0u;
-      if (word_done) lit32[(nlit2 >> 2) - 1u] = litw2;  // the word just filled
+      const uint32_t nadd = is_lit ? (two ? 2u : 1u) : 0u;
+      const uint32_t sh = 8u * (nlit & 3u);
+      const uint64_t acc = (uint64_t)litw | ((uint64_t)(is_lit ? v : 0u) << sh) | ((uint64_t)(two ? sym2 : 0u) << (sh + 8u));
+      const bool word_done = (nlit & 3u) + nadd >= 4u;
+      if (word_done) lit32[nlit >> 2] = (uint32_t)acc;  // the word just filled
       if (dist) {
         if (has_run) tokp[ntok] = run;
         tokp[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
       }
       ntok += dist ? 1u + has_run : 0u;
-      litw = word_done ? 0u : litw2;
-      nlit = nlit2;
-      outlen += is_lit ? 1u : (dist ? mlen : 0u);
-      run = dist ? 0u : run + (is_lit ? 1u : 0u);
+      litw = word_done ? (uint32_t)(acc >> 32) : (uint32_t)acc;
+      nlit += nadd;
+      outlen += is_lit ? nadd : (dist ? mlen : 0u);
+      run = dist ? 0u : run + nadd;
       mlen = is_len ? v : (dist ? 0u : mlen);
     }
     TPROF_ACC(3, t_sym);
