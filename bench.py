@@ -386,7 +386,7 @@ def main():
         # workload (another process, maybe another box): its fraction, and the delta
         prof_ms, prof_src = profiled_launch("north" if args.config == "north" and not args.binary else
                                             {"1": "configs1", "3": "configs3"}.get(args.config, "north"),
-                                            "k_piecesN<1, 1, 2>")
+                                            "k_piecesN<1, 1, 2")  # (rocprof prints the defaulted template arguments too)
         if prof_ms and F == 1 << 20 and P == 4096 and not args.binary:
             pf = alg_bytes / (prof_ms / 1e3) / 1e9 / HBM_PEAK_GBS
             out["roofline"].update({"frac_profiles": round(pf, 4), "profiles_launch_ms": round(prof_ms, 4),
