@@ -47,20 +47,20 @@ constexpr uint32_t AG_CARRY = 64u;   // member of the frame carried in from an e
 #define WSG_AGG_FOLD_MAX 3072  // (configs[2]: 2,128 blocks fold; k_agg_c stages 16 B a block: 48 KiB of LDS at most)
 #endif
 constexpr uint32_t AGG_FOLD_MAX = WSG_AGG_FOLD_MAX;
-__device__ __forceinline__ uint64_t agg_pos(const AggArgs& a, uint64_t j) { return a.pl[j] + a.pre_sum[j / BLOCK]; }
+__device__ __forceinline__ uint64_t agg_pos(const AggArgs& a, uint64_t j) { return a.pl[j] + a.pre_sum[j / ABLOCK]; }
 // cl / blk_cnt pack two counts: emitted frames (bits 0-31) and gather units (32-63)
 __device__ __forceinline__ uint64_t agg_cnt(const AggArgs& a, uint64_t j) {
-  return (a.cl[j] + a.pre_cnt[j / BLOCK]) & 0xffffffffull;
+  return (a.cl[j] + a.pre_cnt[j / ABLOCK]) & 0xffffffffull;
 }
 // A member's bytes go out as gather units: 64 16-B blocks of agg_out each (the first
 // and last block partial), ceil((m + 15) / 1 KiB) of them for m bytes at any
 // alignment (one may come out empty).  A unit copies one source range: no lookups.
 __device__ __forceinline__ uint32_t agg_units(uint64_t m) { return m ? (uint32_t)((m + 15u + PIECE - 1u) / PIECE) : 0u; }
-__device__ __forceinline__ uint64_t agg_mi(const AggArgs& a, uint64_t j) { return (a.cl[j] + a.pre_cnt[j / BLOCK]) >> 32; }
+__device__ __forceinline__ uint64_t agg_mi(const AggArgs& a, uint64_t j) { return (a.cl[j] + a.pre_cnt[j / ABLOCK]) >> 32; }
 
 // ------------------------------------------------------------------ k_agg_a
-__global__ __launch_bounds__(BLOCK) void k_agg_a(AggArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+__global__ __launch_bounds__(ABLOCK) void k_agg_a(AggArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * ABLOCK + threadIdx.x;
   Agg v = AGG_ID;
   if (k < a.n_frames) {
     const uint32_t s = wave_find_session(a.session_first, a.n_sessions, a.n_frames, k);
@@ -147,8 +147,8 @@ __global__ __launch_bounds__(1024) void k_agg_scan(AggArgs a, int sums) {
 }
 
 // ------------------------------------------------------------------ k_agg_b
-__global__ __launch_bounds__(BLOCK) void k_agg_b(AggArgs a) {
-  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+__global__ __launch_bounds__(ABLOCK) void k_agg_b(AggArgs a) {
+  const uint64_t k = (uint64_t)blockIdx.x * ABLOCK + threadIdx.x;
   const bool live = k < a.n_frames;
   uint32_t c = live ? a.code[k] : 0u;
   Agg v = AGG_ID;
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(BLOCK) void k_agg_b(AggArgs a) {
   int32_t bs, be;
   if (a.nblk <= AGG_FOLD_MAX) {
     Agg f = AGG_ID, ft;
-    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += BLOCK) {
+    for (uint32_t b = threadIdx.x; b < blockIdx.x; b += ABLOCK) {
       const int32_t x0 = a.blk_max[b], x1 = a.blk_max[a.nblk + b];
       f.m0 = x0 > f.m0 ? x0 : f.m0;
       f.m1 = x1 > f.m1 ? x1 : f.m1;
@@ -221,21 +221,21 @@ __global__ __launch_bounds__(BLOCK) void k_agg_b(AggArgs a) {
 // block) is an LDS read; the block's own prefix goes to pre_sum / pre_cnt for the
 // gather and the final step, and the last block leaves the totals.
 template <bool FOLD>
-__global__ __launch_bounds__(BLOCK) void k_agg_c(AggArgs a) {
+__global__ __launch_bounds__(ABLOCK) void k_agg_c(AggArgs a) {
   extern __shared__ uint64_t fold[];  // FOLD: [2][blockIdx.x + 1] (sum, cnt) exclusive prefixes
-  const uint64_t k = (uint64_t)blockIdx.x * BLOCK + threadIdx.x;
+  const uint64_t k = (uint64_t)blockIdx.x * ABLOCK + threadIdx.x;
   const int lane = threadIdx.x & 63;
   const bool live = k < a.n_frames;
   const uint32_t B = blockIdx.x;
   if (FOLD) {
     uint64_t* const fs = fold;
     uint64_t* const fc = fold + (B + 1);
-    for (uint32_t b = threadIdx.x; b <= B; b += BLOCK) {
+    for (uint32_t b = threadIdx.x; b <= B; b += ABLOCK) {
       fs[b] = a.blk_sum[b];
       fc[b] = a.blk_cnt[b];
     }
     __syncthreads();
-    const uint32_t n = B + 1, per = (n + BLOCK - 1) / BLOCK;
+    const uint32_t n = B + 1, per = (n + ABLOCK - 1) / ABLOCK;
     const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
     Agg t = AGG_ID;
     uint64_t tc = 0;
@@ -268,12 +268,12 @@ __global__ __launch_bounds__(BLOCK) void k_agg_c(AggArgs a) {
     }
   }
   // the global position / counts of frame j <= this block's last frame
-  auto pos_of = [&](uint64_t j) -> uint64_t { return a.pl[j] + (FOLD ? fold[j / BLOCK] : a.pre_sum[j / BLOCK]); };
+  auto pos_of = [&](uint64_t j) -> uint64_t { return a.pl[j] + (FOLD ? fold[j / ABLOCK] : a.pre_sum[j / ABLOCK]); };
   auto cnt_of = [&](uint64_t j) -> uint64_t {
-    return (a.cl[j] + (FOLD ? fold[(B + 1) + j / BLOCK] : a.pre_cnt[j / BLOCK])) & 0xffffffffull;
+    return (a.cl[j] + (FOLD ? fold[(B + 1) + j / ABLOCK] : a.pre_cnt[j / ABLOCK])) & 0xffffffffull;
   };
   auto mi_of = [&](uint64_t j) -> uint64_t {
-    return (a.cl[j] + (FOLD ? fold[(B + 1) + j / BLOCK] : a.pre_cnt[j / BLOCK])) >> 32;
+    return (a.cl[j] + (FOLD ? fold[(B + 1) + j / ABLOCK] : a.pre_cnt[j / ABLOCK])) >> 32;
   };
   const uint32_t c = live ? a.code[k] : 0u;
   uint64_t pos = live ? pos_of(k) : 0ull, src = 0;
@@ -552,15 +552,15 @@ __global__ __launch_bounds__(64) void k_agg_gather(AggArgs a, uint64_t src_lim) 
 // ------------------------------------------------------------------ launchers
 void launch_agg_plan(const AggArgs& a, hipStream_t s) {
   if (!a.n_frames) return;
-  hipLaunchKernelGGL(k_agg_a, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_agg_a, dim3(a.nblk), dim3(ABLOCK), 0, s, a);
   const bool fold = a.nblk <= AGG_FOLD_MAX;
   if (!fold) hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 0);
-  hipLaunchKernelGGL(k_agg_b, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+  hipLaunchKernelGGL(k_agg_b, dim3(a.nblk), dim3(ABLOCK), 0, s, a);
   if (fold) {
-    hipLaunchKernelGGL(k_agg_c<true>, dim3(a.nblk), dim3(BLOCK), 2 * a.nblk * sizeof(uint64_t), s, a);
+    hipLaunchKernelGGL(k_agg_c<true>, dim3(a.nblk), dim3(ABLOCK), 2 * a.nblk * sizeof(uint64_t), s, a);
   } else {
     hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 1);
-    hipLaunchKernelGGL(k_agg_c<false>, dim3(a.nblk), dim3(BLOCK), 0, s, a);
+    hipLaunchKernelGGL(k_agg_c<false>, dim3(a.nblk), dim3(ABLOCK), 0, s, a);
   }
 }
 void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim, int per_wave, uint32_t grid_cap) {

@@ -862,7 +862,7 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
     return set_err(c, WSG_API_EINVAL, "payload and agg_out must be 16-B aligned");
   HIP_TRY(c, hipSetDevice(c->device));
   const uint64_t F = n_frames ? n_frames : 1;
-  const uint64_t nblk = (F + BLOCK - 1) / BLOCK;
+  const uint64_t nblk = (F + ABLOCK - 1) / ABLOCK;
   AggArgs a;
   a.max_len = max_aggregated_len;
   a.desc = desc;
@@ -877,7 +877,7 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   a.out_desc = out_desc;
   a.out_result = out_result;
   a.agg_total = agg_total;
-  a.nblk = (uint32_t)((n_frames + BLOCK - 1) / BLOCK);
+  a.nblk = (uint32_t)((n_frames + ABLOCK - 1) / ABLOCK);
   // gather units: a member of m bytes has ceil((m + 15) / 1 KiB); those holding bytes below
   // agg_cap number at most agg_cap / 1 KiB + 2 per member before them
   a.n_pieces = agg_cap / PIECE + 2 * F + 2;
