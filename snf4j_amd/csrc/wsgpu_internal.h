@@ -42,7 +42,10 @@ constexpr int BLOCK = 256;    // frames per block in the encode passes
 #define WSG_AGG_BLOCK 512  // (256 and 1024 measured slower: profiles/r04_ab_aggblock.txt)
 #endif
 constexpr int ABLOCK = WSG_AGG_BLOCK;  // frames (threads) per block in the aggregator's plan passes
-constexpr int DBLOCK = 256;   // frames (threads) per block in the decode parse / link passes
+#ifndef WSG_DBLOCK
+#define WSG_DBLOCK 256
+#endif
+constexpr int DBLOCK = WSG_DBLOCK;  // frames (threads) per block in the decode parse / link passes
 constexpr uint32_t PIECE = 1024;  // payload-output bytes per wave in k_pieces (64 lanes x 16 B)
 constexpr int PIECES_PER_WAVE = 2; // pieces one k_piecesN wave takes (tools/ubench_unmask)
 #ifndef WSG_VPIECES
