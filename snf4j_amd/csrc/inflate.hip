@@ -2347,6 +2347,16 @@ constexpr int FNT = 256;  // threads per session (4 waves)
 #ifndef WSG_FAST_RING
 #define WSG_FAST_RING 0
 #endif
+// WSG_FAST_XSCAN=1: the expansion resolves whole 64-byte rows a lane a byte (the byte's
+// token from a max-scan of marks the tokens leave in fd), two tokens a thread a round;
+// 0: a thread a token writes all of its bytes (a wave loops for its longest token)
+#ifndef WSG_FAST_XSCAN
+#define WSG_FAST_XSCAN 1
+#endif
+// WSG_FAST_BGATHER=1: the gather's byte loads without a branch a byte (see there)
+#ifndef WSG_FAST_BGATHER
+#define WSG_FAST_BGATHER 1
+#endif
 #ifndef WSG_FAST_WAVES
 #if WSG_FAST_RING
 #define WSG_FAST_WAVES 3  // waves a SIMD: what the LDS allows (3 sessions of 4 waves a CU)
@@ -2379,8 +2389,11 @@ __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, u
 }
 
 __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WAVES))) void k_infl_fast(InflArgs a) {
-  __shared__ uint32_t fd[FC];
+  __shared__ __attribute__((aligned(16))) uint32_t fd[FC];
   __shared__ uint32_t lbuf[FC / 4 + 2];  // the chunk's literal bytes (at most FC), from a dword boundary
+#if WSG_FAST_XSCAN
+  __shared__ uint2 tokrec[2 * FNT];  // a round's token records (below)
+#endif
 #if WSG_FAST_RING
   __shared__ uint4 ring16[WSG_INFLATE_WINDOW / 16];  // history: position p at byte (p + ph) & WMASK
   uint8_t* const ring = reinterpret_cast<uint8_t*>(ring16);
@@ -2407,6 +2420,9 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
   const uint32_t ph = wl0 ? (uint32_t)st0.window_phase & WMASK : 0u;
   // the session's output so far, read around L1 (bytes this wave stored a chunk ago)
   const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)ocap, 0x00020000);
+#if WSG_FAST_BGATHER
+  const __amdgpu_buffer_rsrc_t rwin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(win), 0, (int)WSG_INFLATE_WINDOW, 0x00020000);
+#endif
   int has_dec = st0.has_decoder;
   int32_t pos = 0, wstart = -wl0;
   bool bad = false;
@@ -2463,8 +2479,118 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       for (uint32_t w = (uint32_t)lane; w < lw_n; w += FNT)
         lbuf[w] = (lw0 + w) * 4 + 4 <= a.lit_len ? reinterpret_cast<const uint32_t*>(a.lit)[lw0 + w] : 0u;
       const uint32_t lsh = (uint32_t)(lg & 3u) - l_first;  // literal index i is byte i + lsh of lbuf
+#if WSG_FAST_XSCAN
+      for (uint32_t w = (uint32_t)lane; w < FC / 4; w += FNT) reinterpret_cast<uint4*>(fd)[w] = make_uint4(0u, 0u, 0u, 0u);
+#endif
       __syncthreads();
       const uint8_t* const lb = reinterpret_cast<const uint8_t*>(lbuf);
+#if WSG_FAST_XSCAN
+      // 1. expand the tokens that overlap [c0, c1) into fd, 2 * FNT tokens a round.  A
+      //    block scan of a thread's two token lengths places its tokens; each token
+      //    leaves a record (below) and its round index at its first byte in the chunk
+      //    and at every 64-byte row start it covers (fd was cleared: the other bytes
+      //    hold 0, the round's first token); then a wave resolves whole rows, a lane a
+      //    byte, the byte's token being the max-scan of the row's marks up to it.  The
+      //    work is the chunk's bytes, not a loop over each token's bytes.
+      //    Record: a match .x = the source of chunk byte jj, minus jj, while the byte is
+      //    less than a distance into the match (P0 + c0 - distance + FD_BIAS), .y = flag
+      //    | distance - 1 | (start - c0 + 512) << 15; a literal run .x = the lb index of
+      //    chunk byte jj's literal, minus jj, .y = 0.
+      const int lw = threadIdx.x & 63, wv = threadIdx.x >> 6;
+      uint32_t t = tt, o = t_off, li = t_li;
+      bool crossed = false;
+      const uint32_t t2 = 2u * (uint32_t)lane;
+      uint32_t nk0 = t + t2 < n_tok ? T[t + t2] : 0u, nk1 = t + t2 + 1u < n_tok ? T[t + t2 + 1u] : 0u;
+      while (t < n_tok && o < c1) {
+        const bool v0 = t + t2 < n_tok, v1 = t + t2 + 1u < n_tok;
+        const uint32_t k0 = v0 ? nk0 : 0u, k1 = v1 ? nk1 : 0u;
+        {  // the next round's tokens, read ahead
+          const uint32_t tn = t + 2u * (uint32_t)FNT + t2;
+          nk0 = tn < n_tok ? T[tn] : 0u;
+          nk1 = tn + 1u < n_tok ? T[tn + 1u] : 0u;
+        }
+        const bool m0 = (k0 & 0x80000000u) != 0, m1 = (k1 & 0x80000000u) != 0;
+        const uint32_t l0 = !v0 ? 0u : (m0 ? ((k0 >> 16) & 255u) + 3u : k0);
+        const uint32_t l1 = !v1 ? 0u : (m1 ? ((k1 >> 16) & 255u) + 3u : k1);
+        if (threadIdx.x == 0) x_first = 0xffffffffu;
+        uint64_t tot;
+        const uint64_t ex = blk_excl_add2(((uint64_t)(l0 + l1) << 32) | ((m0 ? 0u : l0) + (m1 ? 0u : l1)), &tot, wsum);
+        const uint32_t tot_len = uni((uint32_t)(tot >> 32)), tot_lit = uni((uint32_t)tot);
+        const uint32_t to0 = o + (uint32_t)(ex >> 32), tl0 = li + (uint32_t)ex;
+        const uint32_t to1 = to0 + l0, tl1 = tl0 + (m0 ? 0u : l0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const bool v = i ? v1 : v0, ism = i ? m1 : m0;
+          const uint32_t tk = i ? k1 : k0, len = i ? l1 : l0, to = i ? to1 : to0, tli = i ? tl1 : tl0;
+          const uint32_t idx = t2 + (uint32_t)i;
+          const bool here = v && len && to < c1 && to + len > c0;  // has bytes in the chunk
+          const uint32_t toc = to - c0;                      // (mod 2^32: may be "negative")
+          uint2 rec;
+          if (ism) {
+            const uint32_t md = (tk & 0x7fffu) + 1u;
+            if (here && (int32_t)md > P0 + (int32_t)to - wstart) bad = true;  // "invalid distance too far back"
+            rec.x = (uint32_t)(P0 + (int32_t)c0 - (int32_t)md + FD_BIAS);
+            rec.y = 0x80000000u | (md - 1u) | (((toc + 512u) & 0xffffu) << 15);
+          } else {
+            rec.x = tli + lsh - toc;
+            rec.y = 0u;
+          }
+          tokrec[idx] = rec;
+          if (here) {
+            const uint32_t s = to > c0 ? toc : 0u, e = (to + len < c1 ? to + len : c1) - c0;
+            fd[s] = idx;
+            for (uint32_t r = (s + 64u) & ~63u; r < e; r += 64u) fd[r] = idx;
+          }
+          if (v && to <= c1 && to + len > c1) {  // the token holding byte c1 (one at most): the
+            x_first = idx;                         // next chunk starts from it
+            x_off = to;
+            x_li = tli;
+            x_lf = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
+          }
+        }
+        __syncthreads();
+        const uint32_t xf = uni(x_first), xo = uni(x_off), xl = uni(x_li), xlf = uni(x_lf);
+        const uint32_t rs = (o > c0 ? o : c0) - c0;
+        const uint32_t re = (o + tot_len < c1 ? o + tot_len : c1) - c0;
+        for (uint32_t row = (rs >> 6) + (uint32_t)wv; (row << 6) < re; row += FNT / 64) {
+          const uint32_t jj = (row << 6) + (uint32_t)lw;
+          const bool in = jj >= rs && jj < re;
+          uint32_t m = in ? fd[jj] : 0u;
+          m = max(m, dpp_u32<DPP_ROW_SHR1, 0xf>(m, 0u));
+          m = max(m, dpp_u32<DPP_ROW_SHR2, 0xf>(m, 0u));
+          m = max(m, dpp_u32<DPP_ROW_SHR4, 0xf>(m, 0u));
+          m = max(m, dpp_u32<DPP_ROW_SHR8, 0xf>(m, 0u));
+          m = max(m, dpp_u32<DPP_ROW_BCAST15, 0xa>(m, 0u));
+          m = max(m, dpp_u32<DPP_ROW_BCAST31, 0xc>(m, 0u));
+          if (in) {
+            const uint2 rec = tokrec[m];
+            uint32_t v;
+            if (rec.y & 0x80000000u) {
+              v = rec.x + jj;
+              const uint32_t md = (rec.y & 0x7fffu) + 1u;
+              const uint32_t toc = ((rec.y >> 15) & 0xffffu) - 512u;
+              const uint32_t x = jj - toc;  // the byte's index in its match
+              if (x >= md) v = rec.x + toc + x % md;
+            } else {
+              v = FD_LIT | lb[rec.x + jj];
+            }
+            fd[jj] = v;
+          }
+        }
+        if (xf != 0xffffffffu) {  // the chunk ends inside token xf
+          tt = t + xf;
+          t_off = xo;
+          t_li = xl;
+          l_first = xlf;
+          crossed = true;
+          break;
+        }
+        __syncthreads();  // the records are read before the next round writes them
+        t += 2u * (uint32_t)FNT;
+        o += tot_len;
+        li += tot_lit;
+      }
+#else
       // 1. expand the tokens that overlap [c0, c1) into fd
       uint32_t t = tt, o = t_off, li = t_li;
       bool crossed = false;
@@ -2519,6 +2645,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         o += tot_len;
         li += tot_lit;
       }
+#endif
       if (!crossed) {
         tt = t < n_tok ? t : n_tok;
         t_off = o;
@@ -2552,6 +2679,19 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         for (int u = 0; u < GU; ++u) {
           const uint32_t j = (uint32_t)FNT * (u0 + u) + (uint32_t)lane;
           v[u] = j < n && u0 + u < (int)(FC / FNT) ? fd[j] : FD_LIT;
+#if WSG_FAST_BGATHER && !WSG_FAST_RING
+          {  // no branch a byte: both loads issued, the one not wanted out of range (reads 0)
+            const bool isp = !(v[u] & FD_LIT);
+            const int32_t q = (int32_t)v[u] - FD_BIAS;
+            const uint32_t oq = isp && q >= 0 ? (uint32_t)q : 0xffffffffu;
+            uint32_t b = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rout, oq, 0, 1);
+            if (wl0) {  // (wave-uniform) a carried window
+              const uint32_t wq = isp && q < 0 ? (((uint32_t)q + ph) & WMASK) : 0xffffffffu;
+              b |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rwin, wq, 0, 1);
+            }
+            v[u] = isp ? (FD_LIT | b) : v[u];
+          }
+#else
           if (!(v[u] & FD_LIT)) {
             const int32_t q = (int32_t)v[u] - FD_BIAS;
 #if WSG_FAST_RING
@@ -2561,6 +2701,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
                                     : (uint32_t)win[((uint32_t)q + ph) & WMASK]);
 #endif
           }
+#endif
         }
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
