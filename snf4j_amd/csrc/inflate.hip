@@ -2312,12 +2312,15 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
 // Parallel token replay (k_infl_fast).  A session whose compressed messages in this
 // batch k_infl_tok all decoded cleanly (whole messages, one frame or several), met in
 // the clean state (no message open, no final block seen), needs no serial decoder and
-// no LDS window (its other frames pass through): per message, the 64 lanes expand the tokens into one descriptor per output
-// byte (a literal, or the absolute session position it copies: a back-reference byte
-// i of (length, distance) at p copies p - distance + i mod distance), chase the
-// copies that land inside the chunk through LDS, gather the ones that land before it
-// from the session's output in HBM (or the carried window image), and store the
-// chunk.  Every output byte is resolved independently, so nothing serialises on a
+// no LDS window (its other frames pass through): per message, in chunks of FC output
+// bytes, the threads expand the tokens into one descriptor per output byte (a literal,
+// or the absolute session position it copies: a back-reference byte i of (length,
+// distance) at p copies p - distance + i mod distance) — each token marks its first
+// byte and the 64-byte row starts it covers, and a lane a byte finds its token by a
+// max-scan of its row's marks, so the work is the chunk's bytes whatever the match
+// lengths — chase the copies that land inside the chunk through LDS, gather the ones
+// that land before it from the session's output in HBM (or the carried window image)
+// with no branch a byte, and store the chunk.  Every output byte is resolved independently, so nothing serialises on a
 // window round trip; a session is one 256-thread workgroup (4 waves, 16 KiB of LDS).  A
 // session it cannot finish (a distance too far back, capacity, any frame that does
 // not qualify) is left to k_inflate, which runs the serial decoder for exactly the
@@ -2339,30 +2342,12 @@ constexpr uint32_t FD_LIT = 0x80000000u;  // descriptor: a resolved byte (bits 0
 constexpr int32_t FD_BIAS = 32768;        // descriptor: position + FD_BIAS (history positions are >= -32768)
 
 constexpr int FNT = 256;  // threads per session (4 waves)
-// WSG_FAST_RING=1 (A/B build, not the default): the session's last 32 KiB of output in
-// an LDS ring, so a copy's source bytes come from LDS instead of HBM, and the ring is
-// the window image the batch commits.  52 KB of LDS a session allows 3 sessions a CU
-// instead of 6: k_infl_fast 2.27 -> 3.07 ms (same-box), the VALU-bound expansion
-// loses more from the halved occupancy than the gather gains.
-#ifndef WSG_FAST_RING
-#define WSG_FAST_RING 0
+#ifndef WSG_FAST_TPT
+#define WSG_FAST_TPT 2  // tokens a thread a round (records: 8 B a token of LDS; 3 spills, 4 holds 5 sessions a CU)
 #endif
-// WSG_FAST_XSCAN=1: the expansion resolves whole 64-byte rows a lane a byte (the byte's
-// token from a max-scan of marks the tokens leave in fd), two tokens a thread a round;
-// 0: a thread a token writes all of its bytes (a wave loops for its longest token)
-#ifndef WSG_FAST_XSCAN
-#define WSG_FAST_XSCAN 1
-#endif
-// WSG_FAST_BGATHER=1: the gather's byte loads without a branch a byte (see there)
-#ifndef WSG_FAST_BGATHER
-#define WSG_FAST_BGATHER 1
-#endif
+constexpr int FTPT = WSG_FAST_TPT;
 #ifndef WSG_FAST_WAVES
-#if WSG_FAST_RING
-#define WSG_FAST_WAVES 3  // waves a SIMD: what the LDS allows (3 sessions of 4 waves a CU)
-#else
 #define WSG_FAST_WAVES 6  // waves a SIMD: the register budget (80 VGPRs) that keeps 6 sessions a CU
-#endif
 #endif
 
 // block-wide exclusive sum of a packed (hi, lo) pair of 32-bit counts; the totals
@@ -2391,13 +2376,7 @@ __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, u
 __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WAVES))) void k_infl_fast(InflArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t fd[FC];
   __shared__ uint32_t lbuf[FC / 4 + 2];  // the chunk's literal bytes (at most FC), from a dword boundary
-#if WSG_FAST_XSCAN
-  __shared__ uint2 tokrec[2 * FNT];  // a round's token records (below)
-#endif
-#if WSG_FAST_RING
-  __shared__ uint4 ring16[WSG_INFLATE_WINDOW / 16];  // history: position p at byte (p + ph) & WMASK
-  uint8_t* const ring = reinterpret_cast<uint8_t*>(ring16);
-#endif
+  __shared__ uint2 tokrec[FTPT * FNT];  // a round's token records (below)
   __shared__ uint64_t wsum[FNT / 64];
   __shared__ uint32_t x_first, x_off, x_li, x_lf;
   const int lane = threadIdx.x;  // (the block's thread: FNT per session)
@@ -2420,19 +2399,11 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
   const uint32_t ph = wl0 ? (uint32_t)st0.window_phase & WMASK : 0u;
   // the session's output so far, read around L1 (bytes this wave stored a chunk ago)
   const __amdgpu_buffer_rsrc_t rout = __builtin_amdgcn_make_buffer_rsrc(out, 0, (int)ocap, 0x00020000);
-#if WSG_FAST_BGATHER
   const __amdgpu_buffer_rsrc_t rwin = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(win), 0, (int)WSG_INFLATE_WINDOW, 0x00020000);
-#endif
   int has_dec = st0.has_decoder;
   int32_t pos = 0, wstart = -wl0;
   bool bad = false;
   int compressing = 0;
-#if WSG_FAST_RING
-  if (wl0) {  // the carried-in history (a ring image with the same phase)
-    for (uint32_t i = (uint32_t)lane; i < WSG_INFLATE_WINDOW / 16; i += FNT) ring16[i] = reinterpret_cast<const uint4*>(win)[i];
-    __syncthreads();
-  }
-#endif
   for (uint32_t k = f0; k < f1 && !bad; ++k) {
     const wsg_frame_desc d = a.desc[k];
     const uint32_t op = d.opcode & 15u, fin = (d.flags >> 7) & 1u, rsv = (d.flags >> 4) & 7u;
@@ -2479,12 +2450,9 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       for (uint32_t w = (uint32_t)lane; w < lw_n; w += FNT)
         lbuf[w] = (lw0 + w) * 4 + 4 <= a.lit_len ? reinterpret_cast<const uint32_t*>(a.lit)[lw0 + w] : 0u;
       const uint32_t lsh = (uint32_t)(lg & 3u) - l_first;  // literal index i is byte i + lsh of lbuf
-#if WSG_FAST_XSCAN
       for (uint32_t w = (uint32_t)lane; w < FC / 4; w += FNT) reinterpret_cast<uint4*>(fd)[w] = make_uint4(0u, 0u, 0u, 0u);
-#endif
       __syncthreads();
       const uint8_t* const lb = reinterpret_cast<const uint8_t*>(lbuf);
-#if WSG_FAST_XSCAN
       // 1. expand the tokens that overlap [c0, c1) into fd, 2 * FNT tokens a round.  A
       //    block scan of a thread's two token lengths places its tokens; each token
       //    leaves a record (below) and its round index at its first byte in the chunk
@@ -2499,32 +2467,35 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       const int lw = threadIdx.x & 63, wv = threadIdx.x >> 6;
       uint32_t t = tt, o = t_off, li = t_li;
       bool crossed = false;
-      const uint32_t t2 = 2u * (uint32_t)lane;
-      uint32_t nk0 = t + t2 < n_tok ? T[t + t2] : 0u, nk1 = t + t2 + 1u < n_tok ? T[t + t2 + 1u] : 0u;
+      const uint32_t tq = (uint32_t)FTPT * (uint32_t)lane;
+      uint32_t nk[FTPT];
+#pragma unroll
+      for (int i = 0; i < FTPT; ++i) nk[i] = t + tq + i < n_tok ? T[t + tq + i] : 0u;
       while (t < n_tok && o < c1) {
-        const bool v0 = t + t2 < n_tok, v1 = t + t2 + 1u < n_tok;
-        const uint32_t k0 = v0 ? nk0 : 0u, k1 = v1 ? nk1 : 0u;
-        {  // the next round's tokens, read ahead
-          const uint32_t tn = t + 2u * (uint32_t)FNT + t2;
-          nk0 = tn < n_tok ? T[tn] : 0u;
-          nk1 = tn + 1u < n_tok ? T[tn + 1u] : 0u;
+        uint32_t kk[FTPT], ll[FTPT], lsum = 0u, lit_sum = 0u;
+#pragma unroll
+        for (int i = 0; i < FTPT; ++i) {
+          const bool v = t + tq + i < n_tok;
+          kk[i] = v ? nk[i] : 0u;
+          const uint32_t tn = t + (uint32_t)(FTPT * FNT) + tq + i;  // the next round's, read ahead
+          nk[i] = tn < n_tok ? T[tn] : 0u;
+          const bool ism = (kk[i] & 0x80000000u) != 0;
+          ll[i] = !v ? 0u : (ism ? ((kk[i] >> 16) & 255u) + 3u : kk[i]);
+          lsum += ll[i];
+          lit_sum += ism ? 0u : ll[i];
         }
-        const bool m0 = (k0 & 0x80000000u) != 0, m1 = (k1 & 0x80000000u) != 0;
-        const uint32_t l0 = !v0 ? 0u : (m0 ? ((k0 >> 16) & 255u) + 3u : k0);
-        const uint32_t l1 = !v1 ? 0u : (m1 ? ((k1 >> 16) & 255u) + 3u : k1);
         if (threadIdx.x == 0) x_first = 0xffffffffu;
         uint64_t tot;
-        const uint64_t ex = blk_excl_add2(((uint64_t)(l0 + l1) << 32) | ((m0 ? 0u : l0) + (m1 ? 0u : l1)), &tot, wsum);
+        const uint64_t ex = blk_excl_add2(((uint64_t)lsum << 32) | lit_sum, &tot, wsum);
         const uint32_t tot_len = uni((uint32_t)(tot >> 32)), tot_lit = uni((uint32_t)tot);
-        const uint32_t to0 = o + (uint32_t)(ex >> 32), tl0 = li + (uint32_t)ex;
-        const uint32_t to1 = to0 + l0, tl1 = tl0 + (m0 ? 0u : l0);
+        uint32_t to = o + (uint32_t)(ex >> 32), tli = li + (uint32_t)ex;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-          const bool v = i ? v1 : v0, ism = i ? m1 : m0;
-          const uint32_t tk = i ? k1 : k0, len = i ? l1 : l0, to = i ? to1 : to0, tli = i ? tl1 : tl0;
-          const uint32_t idx = t2 + (uint32_t)i;
+        for (int i = 0; i < FTPT; ++i) {
+          const uint32_t tk = kk[i], len = ll[i];
+          const bool v = t + tq + i < n_tok, ism = (tk & 0x80000000u) != 0;
+          const uint32_t idx = tq + (uint32_t)i;
           const bool here = v && len && to < c1 && to + len > c0;  // has bytes in the chunk
-          const uint32_t toc = to - c0;                      // (mod 2^32: may be "negative")
+          const uint32_t toc = to - c0;                             // (mod 2^32: may be "negative")
           uint2 rec;
           if (ism) {
             const uint32_t md = (tk & 0x7fffu) + 1u;
@@ -2547,6 +2518,8 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
             x_li = tli;
             x_lf = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
           }
+          to += len;
+          tli += ism ? 0u : len;
         }
         __syncthreads();
         const uint32_t xf = uni(x_first), xo = uni(x_off), xl = uni(x_li), xlf = uni(x_lf);
@@ -2562,19 +2535,16 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           m = max(m, dpp_u32<DPP_ROW_SHR8, 0xf>(m, 0u));
           m = max(m, dpp_u32<DPP_ROW_BCAST15, 0xa>(m, 0u));
           m = max(m, dpp_u32<DPP_ROW_BCAST31, 0xc>(m, 0u));
-          if (in) {
+          {  // (no branch a byte: literal and match values both formed, one kept)
             const uint2 rec = tokrec[m];
-            uint32_t v;
-            if (rec.y & 0x80000000u) {
-              v = rec.x + jj;
-              const uint32_t md = (rec.y & 0x7fffu) + 1u;
-              const uint32_t toc = ((rec.y >> 15) & 0xffffu) - 512u;
-              const uint32_t x = jj - toc;  // the byte's index in its match
-              if (x >= md) v = rec.x + toc + x % md;
-            } else {
-              v = FD_LIT | lb[rec.x + jj];
-            }
-            fd[jj] = v;
+            const bool ism = (rec.y & 0x80000000u) != 0;
+            const uint32_t md = (rec.y & 0x7fffu) + 1u;
+            const uint32_t toc = ((rec.y >> 15) & 0xffffu) - 512u;
+            const uint32_t x = jj - toc;  // the byte's index in its match
+            const uint32_t lv = FD_LIT | lb[ism || !in ? 0u : rec.x + jj];
+            uint32_t v = ism ? rec.x + jj : lv;
+            if (in && ism && x >= md) v = rec.x + toc + x % md;  // (rare: a match longer than its distance)
+            if (in) fd[jj] = v;
           }
         }
         if (xf != 0xffffffffu) {  // the chunk ends inside token xf
@@ -2586,66 +2556,10 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           break;
         }
         __syncthreads();  // the records are read before the next round writes them
-        t += 2u * (uint32_t)FNT;
+        t += (uint32_t)(FTPT * FNT);
         o += tot_len;
         li += tot_lit;
       }
-#else
-      // 1. expand the tokens that overlap [c0, c1) into fd
-      uint32_t t = tt, o = t_off, li = t_li;
-      bool crossed = false;
-      uint32_t tk_next = t + (uint32_t)lane < n_tok ? T[t + lane] : 0u;  // a round of tokens read ahead
-      while (t < n_tok && o < c1) {
-        const bool valid = t + (uint32_t)lane < n_tok;
-        const uint32_t tk = valid ? tk_next : 0u;
-        tk_next = t + (uint32_t)FNT + (uint32_t)lane < n_tok ? T[t + FNT + lane] : 0u;
-        const bool ism = (tk & 0x80000000u) != 0;
-        const uint32_t len = !valid ? 0u : (ism ? ((tk >> 16) & 255u) + 3u : tk);
-        uint64_t tot;
-        const uint64_t ex = blk_excl_add2(((uint64_t)len << 32) | (ism ? 0u : len), &tot, wsum);
-        const uint32_t tot_len = (uint32_t)(tot >> 32), tot_lit = (uint32_t)tot;
-        const uint32_t to = o + (uint32_t)(ex >> 32);
-        const uint32_t tli = li + (uint32_t)ex;
-        if (valid && to < c1 && to + len > c0) {
-          const uint32_t b0 = to > c0 ? to : c0, b1 = to + len < c1 ? to + len : c1;
-          if (ism) {
-            const uint32_t md = (tk & 0x7fffu) + 1u;
-            if ((int32_t)md > P0 + (int32_t)to - wstart) bad = true;  // "invalid distance too far back"
-            const int32_t src0 = P0 + (int32_t)to - (int32_t)md + FD_BIAS;
-            uint32_t r = (b0 - to) % md;
-            for (uint32_t j = b0; j < b1; ++j) {
-              fd[j - c0] = (uint32_t)(src0 + (int32_t)r);
-              if (++r == md) r = 0;
-            }
-          } else {
-            for (uint32_t j = b0; j < b1; ++j) fd[j - c0] = FD_LIT | lb[tli + (j - to) + lsh];
-          }
-        }
-        // the chunk ends inside a token: the next chunk starts from the first such one
-        if (__syncthreads_or(valid && to + len > c1)) {
-          if (threadIdx.x == 0) x_first = 0xffffffffu;
-          __syncthreads();
-          if (valid && to + len > c1) atomicMin(&x_first, (uint32_t)lane);
-          __syncthreads();
-          const uint32_t f = x_first;
-          if ((uint32_t)lane == f) {
-            x_off = to;
-            x_li = tli;
-            x_lf = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
-          }
-          __syncthreads();
-          tt = t + f;
-          t_off = x_off;
-          t_li = x_li;
-          l_first = x_lf;
-          crossed = true;
-          break;
-        }
-        t += (uint32_t)FNT;
-        o += tot_len;
-        li += tot_lit;
-      }
-#endif
       if (!crossed) {
         tt = t < n_tok ? t : n_tok;
         t_off = o;
@@ -2679,29 +2593,17 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         for (int u = 0; u < GU; ++u) {
           const uint32_t j = (uint32_t)FNT * (u0 + u) + (uint32_t)lane;
           v[u] = j < n && u0 + u < (int)(FC / FNT) ? fd[j] : FD_LIT;
-#if WSG_FAST_BGATHER && !WSG_FAST_RING
-          {  // no branch a byte: both loads issued, the one not wanted out of range (reads 0)
-            const bool isp = !(v[u] & FD_LIT);
-            const int32_t q = (int32_t)v[u] - FD_BIAS;
-            const uint32_t oq = isp && q >= 0 ? (uint32_t)q : 0xffffffffu;
-            uint32_t b = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rout, oq, 0, 1);
-            if (wl0) {  // (wave-uniform) a carried window
-              const uint32_t wq = isp && q < 0 ? (((uint32_t)q + ph) & WMASK) : 0xffffffffu;
-              b |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rwin, wq, 0, 1);
-            }
-            v[u] = isp ? (FD_LIT | b) : v[u];
+          // no branch a byte (a branch each cost more than the loads): both loads are
+          // issued, the one not wanted at an offset out of its buffer's range (reads 0)
+          const bool isp = !(v[u] & FD_LIT);
+          const int32_t q = (int32_t)v[u] - FD_BIAS;
+          const uint32_t oq = isp && q >= 0 ? (uint32_t)q : 0xffffffffu;
+          uint32_t b = (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rout, oq, 0, 1);
+          if (wl0) {  // (session-uniform) a carried window
+            const uint32_t wq = isp && q < 0 ? (((uint32_t)q + ph) & WMASK) : 0xffffffffu;
+            b |= (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rwin, wq, 0, 1);
           }
-#else
-          if (!(v[u] & FD_LIT)) {
-            const int32_t q = (int32_t)v[u] - FD_BIAS;
-#if WSG_FAST_RING
-            v[u] = FD_LIT | (uint32_t)ring[((uint32_t)q + ph) & WMASK];  // (q >= C0 - 32768: still in the ring)
-#else
-            v[u] = FD_LIT | (q >= 0 ? (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(rout, (uint32_t)q, 0, 1)
-                                    : (uint32_t)win[((uint32_t)q + ph) & WMASK]);
-#endif
-          }
-#endif
+          v[u] = isp ? (FD_LIT | b) : v[u];
         }
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
@@ -2725,11 +2627,6 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       }
       const uint32_t tb = head + 4u * nw;
       if ((uint32_t)lane < n - tb) dst[tb + lane] = (uint8_t)fd[tb + lane];
-#if WSG_FAST_RING
-      // into the history ring (the chunk's gathers are done: the slots it overwrites, 32 KiB
-      // back, are no longer read)
-      for (uint32_t j = (uint32_t)lane; j < n; j += FNT) ring[((uint32_t)C0 + j + ph) & WMASK] = (uint8_t)fd[j];
-#endif
       // the stores complete before the next chunk gathers from them
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
       __syncthreads();
@@ -2762,16 +2659,6 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
   st.finished = 0;
   st.window_len = 0;
   st.window_phase = 0;
-#if WSG_FAST_RING
-  if (has_dec) {  // the ring is the new window image (its phase moves with the output)
-    const int32_t P = pos, nh = (P - wstart) < (int32_t)WSG_INFLATE_WINDOW ? (P - wstart) : (int32_t)WSG_INFLATE_WINDOW;
-    __syncthreads();
-    uint4* const wout16 = reinterpret_cast<uint4*>(a.window + (uint64_t)s * WSG_INFLATE_WINDOW);
-    for (uint32_t i = (uint32_t)lane; i < WSG_INFLATE_WINDOW / 16; i += FNT) wout16[i] = ring16[i];
-    st.window_len = (uint16_t)nh;
-    st.window_phase = (uint16_t)(((uint32_t)P + ph) & WMASK);
-  }
-#else
   if (has_dec) {
     const int32_t P = pos, nh = (P - wstart) < (int32_t)WSG_INFLATE_WINDOW ? (P - wstart) : (int32_t)WSG_INFLATE_WINDOW;
     const uint32_t nph = ((uint32_t)P + ph) & WMASK;
@@ -2823,7 +2710,6 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
     st.window_len = (uint16_t)nh;
     st.window_phase = (uint16_t)nph;
   }
-#endif
   if (lane == 0) {
     a.state[s] = st;
     wsg_session_result res = {f1 - f0, 0u, 0u, 0};
