@@ -2350,10 +2350,11 @@ constexpr int FTPT = WSG_FAST_TPT;
 #define WSG_FAST_WAVES 6  // waves a SIMD: the register budget (80 VGPRs) that keeps 6 sessions a CU
 #endif
 
-// block-wide exclusive sum of a packed (hi, lo) pair of 32-bit counts; the totals
+// block-wide exclusive sum of a packed (hi, lo) pair of 32-bit counts, and the totals;
+// no trailing barrier: the caller alternates two wsum buffers
 __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, uint64_t* wsum) {
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  uint64_t inc = v;  // wave scan by DPP row operations (wsgpu_scan.h wave_incl_scan)
+  uint64_t inc = v;
   inc += dpp_u64<DPP_ROW_SHR1, 0xf>(inc, 0ull);
   inc += dpp_u64<DPP_ROW_SHR2, 0xf>(inc, 0ull);
   inc += dpp_u64<DPP_ROW_SHR4, 0xf>(inc, 0ull);
@@ -2368,7 +2369,6 @@ __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, u
     pre += w < wid ? wsum[w] : 0ull;
     tot += wsum[w];
   }
-  __syncthreads();
   *total = tot;
   return pre + inc - v;
 }
@@ -2376,9 +2376,11 @@ __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, u
 __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WAVES))) void k_infl_fast(InflArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t fd[FC];
   __shared__ uint32_t lbuf[FC / 4 + 2];  // the chunk's literal bytes (at most FC), from a dword boundary
-  __shared__ uint2 tokrec[FTPT * FNT];  // a round's token records (below)
-  __shared__ uint64_t wsum[FNT / 64];
-  __shared__ uint32_t x_first, x_off, x_li, x_lf;
+  // a round's token records (below), its wave sums and the token holding byte c1; two of
+  // each, rounds alternating, so a round needs two barriers (sums, records) and not four
+  __shared__ uint32_t tokrec[2][FTPT * FNT];
+  __shared__ uint64_t wsum2[2][FNT / 64];
+  __shared__ uint32_t xs[2][4];
   const int lane = threadIdx.x;  // (the block's thread: FNT per session)
   const uint32_t s = blockIdx.x;
   if (s >= a.n_sessions) return;
@@ -2460,14 +2462,11 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       //    hold 0, the round's first token); then a wave resolves whole rows, a lane a
       //    byte, the byte's token being the max-scan of the row's marks up to it.  The
       //    work is the chunk's bytes, not a loop over each token's bytes.
-      //    Record: a match .x = the source of chunk byte jj, minus jj, while the byte is
-      //    less than a distance into the match (P0 + c0 - distance + FD_BIAS), .y = flag
-      //    | distance - 1 | (start - c0 + 512) << 15; a literal run .x = the lb index of
-      //    chunk byte jj's literal, minus jj, .y = 0.
       const int lw = threadIdx.x & 63, wv = threadIdx.x >> 6;
-      uint32_t t = tt, o = t_off, li = t_li;
+      uint32_t t = tt, o = t_off, li = t_li, rp = 0;
       bool crossed = false;
       const uint32_t tq = (uint32_t)FTPT * (uint32_t)lane;
+      const uint32_t mb = (uint32_t)(P0 + (int32_t)c0 + FD_BIAS);  // a match's source, + jj - distance
       uint32_t nk[FTPT];
 #pragma unroll
       for (int i = 0; i < FTPT; ++i) nk[i] = t + tq + i < n_tok ? T[t + tq + i] : 0u;
@@ -2484,9 +2483,11 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           lsum += ll[i];
           lit_sum += ism ? 0u : ll[i];
         }
-        if (threadIdx.x == 0) x_first = 0xffffffffu;
+        uint32_t* const rec_r = tokrec[rp];
+        uint32_t* const xs_r = xs[rp];
+        if (threadIdx.x == 0) xs_r[0] = 0xffffffffu;
         uint64_t tot;
-        const uint64_t ex = blk_excl_add2(((uint64_t)lsum << 32) | lit_sum, &tot, wsum);
+        const uint64_t ex = blk_excl_add2(((uint64_t)lsum << 32) | lit_sum, &tot, wsum2[rp]);
         const uint32_t tot_len = uni((uint32_t)(tot >> 32)), tot_lit = uni((uint32_t)tot);
         uint32_t to = o + (uint32_t)(ex >> 32), tli = li + (uint32_t)ex;
 #pragma unroll
@@ -2496,33 +2497,34 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           const uint32_t idx = tq + (uint32_t)i;
           const bool here = v && len && to < c1 && to + len > c0;  // has bytes in the chunk
           const uint32_t toc = to - c0;                             // (mod 2^32: may be "negative")
-          uint2 rec;
+          // the record (read only for a token with bytes in the chunk, whose fields fit): a
+          // match: flag | distance - 1 | (start - c0 + 512) << 15; a literal run: the lb
+          // index of chunk byte jj's literal, minus jj, + 8192 (14 bits)
+          uint32_t rec;
           if (ism) {
             const uint32_t md = (tk & 0x7fffu) + 1u;
             if (here && (int32_t)md > P0 + (int32_t)to - wstart) bad = true;  // "invalid distance too far back"
-            rec.x = (uint32_t)(P0 + (int32_t)c0 - (int32_t)md + FD_BIAS);
-            rec.y = 0x80000000u | (md - 1u) | (((toc + 512u) & 0xffffu) << 15);
+            rec = 0x80000000u | (md - 1u) | (((toc + 512u) & 0x1fffu) << 15);
           } else {
-            rec.x = tli + lsh - toc;
-            rec.y = 0u;
+            rec = (tli + lsh - toc + 8192u) & 0x3fffu;
           }
-          tokrec[idx] = rec;
+          rec_r[idx] = rec;
           if (here) {
             const uint32_t s = to > c0 ? toc : 0u, e = (to + len < c1 ? to + len : c1) - c0;
             fd[s] = idx;
             for (uint32_t r = (s + 64u) & ~63u; r < e; r += 64u) fd[r] = idx;
           }
           if (v && to <= c1 && to + len > c1) {  // the token holding byte c1 (one at most): the
-            x_first = idx;                         // next chunk starts from it
-            x_off = to;
-            x_li = tli;
-            x_lf = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
+            xs_r[0] = idx;                         // next chunk starts from it
+            xs_r[1] = to;
+            xs_r[2] = tli;
+            xs_r[3] = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
           }
           to += len;
           tli += ism ? 0u : len;
         }
         __syncthreads();
-        const uint32_t xf = uni(x_first), xo = uni(x_off), xl = uni(x_li), xlf = uni(x_lf);
+        const uint32_t xf = uni(xs_r[0]), xo = uni(xs_r[1]), xl = uni(xs_r[2]), xlf = uni(xs_r[3]);
         const uint32_t rs = (o > c0 ? o : c0) - c0;
         const uint32_t re = (o + tot_len < c1 ? o + tot_len : c1) - c0;
         for (uint32_t row = (rs >> 6) + (uint32_t)wv; (row << 6) < re; row += FNT / 64) {
@@ -2536,14 +2538,15 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           m = max(m, dpp_u32<DPP_ROW_BCAST15, 0xa>(m, 0u));
           m = max(m, dpp_u32<DPP_ROW_BCAST31, 0xc>(m, 0u));
           {  // (no branch a byte: literal and match values both formed, one kept)
-            const uint2 rec = tokrec[m];
-            const bool ism = (rec.y & 0x80000000u) != 0;
-            const uint32_t md = (rec.y & 0x7fffu) + 1u;
-            const uint32_t toc = ((rec.y >> 15) & 0xffffu) - 512u;
+            const uint32_t rec = rec_r[m];
+            const bool ism = (rec & 0x80000000u) != 0;
+            const uint32_t md = (rec & 0x7fffu) + 1u;
+            const uint32_t toc = ((rec >> 15) & 0x1fffu) - 512u;
             const uint32_t x = jj - toc;  // the byte's index in its match
-            const uint32_t lv = FD_LIT | lb[ism || !in ? 0u : rec.x + jj];
-            uint32_t v = ism ? rec.x + jj : lv;
-            if (in && ism && x >= md) v = rec.x + toc + x % md;  // (rare: a match longer than its distance)
+            const uint32_t lv = FD_LIT | lb[ism || !in ? 0u : (rec & 0x3fffu) - 8192u + jj];
+            const uint32_t base = mb - md;
+            uint32_t v = ism ? base + jj : lv;
+            if (in && ism && x >= md) v = base + toc + x % md;  // (rare: a match longer than its distance)
             if (in) fd[jj] = v;
           }
         }
@@ -2555,7 +2558,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           crossed = true;
           break;
         }
-        __syncthreads();  // the records are read before the next round writes them
+        rp ^= 1u;  // (no barrier: the next round writes the other records, sums and xs)
         t += (uint32_t)(FTPT * FNT);
         o += tot_len;
         li += tot_lit;
