@@ -2530,7 +2530,10 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         for (uint32_t row = (rs >> 6) + (uint32_t)wv; (row << 6) < re; row += FNT / 64) {
           const uint32_t jj = (row << 6) + (uint32_t)lw;
           const bool in = jj >= rs && jj < re;
-          uint32_t m = in ? fd[jj] : 0u;
+          // (read and written back by every lane, no exec-mask branch: a lane outside the
+          // round's bytes rewrites what it read — the rounds either side are past a barrier)
+          const uint32_t orig = fd[jj];
+          uint32_t m = in ? orig : 0u;
           m = max(m, dpp_u32<DPP_ROW_SHR1, 0xf>(m, 0u));
           m = max(m, dpp_u32<DPP_ROW_SHR2, 0xf>(m, 0u));
           m = max(m, dpp_u32<DPP_ROW_SHR4, 0xf>(m, 0u));
@@ -2547,7 +2550,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
             const uint32_t base = mb - md;
             uint32_t v = ism ? base + jj : lv;
             if (in && ism && x >= md) v = base + toc + x % md;  // (rare: a match longer than its distance)
-            if (in) fd[jj] = v;
+            fd[jj] = in ? v : orig;
           }
         }
         if (xf != 0xffffffffu) {  // the chunk ends inside token xf
@@ -2595,7 +2598,8 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
           const uint32_t j = (uint32_t)FNT * (u0 + u) + (uint32_t)lane;
-          v[u] = j < n && u0 + u < (int)(FC / FNT) ? fd[j] : FD_LIT;
+          v[u] = u0 + u < (int)(FC / FNT) ? fd[j] : FD_LIT;  // (read unmasked: j < FC)
+          v[u] = j < n ? v[u] : FD_LIT;
           // no branch a byte (a branch each cost more than the loads): both loads are
           // issued, the one not wanted at an offset out of its buffer's range (reads 0)
           const bool isp = !(v[u] & FD_LIT);
@@ -2611,7 +2615,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
 #pragma unroll
         for (int u = 0; u < GU; ++u) {
           const uint32_t j = (uint32_t)FNT * (u0 + u) + (uint32_t)lane;
-          if (j < n && u0 + u < (int)(FC / FNT)) fd[j] = v[u];
+          if (u0 + u < (int)(FC / FNT)) fd[j] = v[u];  // (unmasked: past n it is unused)
         }
       }
       __syncthreads();
