@@ -2374,13 +2374,14 @@ __device__ __forceinline__ uint64_t blk_excl_add2(uint64_t v, uint64_t* total, u
 }
 
 __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WAVES))) void k_infl_fast(InflArgs a) {
-  __shared__ __attribute__((aligned(16))) uint32_t fd[FC];
+  __shared__ __attribute__((aligned(16))) uint32_t fd[FC + 4];  // (+ a slot the marks of tokens outside the chunk go to)
   __shared__ uint32_t lbuf[FC / 4 + 2];  // the chunk's literal bytes (at most FC), from a dword boundary
   // a round's token records (below), its wave sums and the token holding byte c1; two of
   // each, rounds alternating, so a round needs two barriers (sums, records) and not four
   __shared__ uint32_t tokrec[2][FTPT * FNT];
   __shared__ uint64_t wsum2[2][FNT / 64];
   __shared__ uint32_t xs[2][4];
+  __shared__ uint32_t xbad;  // a lane of the chunk's rounds met a distance too far back
   const int lane = threadIdx.x;  // (the block's thread: FNT per session)
   const uint32_t s = blockIdx.x;
   if (s >= a.n_sessions) return;
@@ -2453,6 +2454,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         lbuf[w] = (lw0 + w) * 4 + 4 <= a.lit_len ? reinterpret_cast<const uint32_t*>(a.lit)[lw0 + w] : 0u;
       const uint32_t lsh = (uint32_t)(lg & 3u) - l_first;  // literal index i is byte i + lsh of lbuf
       for (uint32_t w = (uint32_t)lane; w < FC / 4; w += FNT) reinterpret_cast<uint4*>(fd)[w] = make_uint4(0u, 0u, 0u, 0u);
+      if (threadIdx.x == 0) xbad = 0u;
       __syncthreads();
       const uint8_t* const lb = reinterpret_cast<const uint8_t*>(lbuf);
       // 1. expand the tokens that overlap [c0, c1) into fd, 2 * FNT tokens a round.  A
@@ -2503,14 +2505,14 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
           uint32_t rec;
           if (ism) {
             const uint32_t md = (tk & 0x7fffu) + 1u;
-            if (here && (int32_t)md > P0 + (int32_t)to - wstart) bad = true;  // "invalid distance too far back"
+            if (here && (int32_t)md > P0 + (int32_t)to - wstart) xbad = 1u;  // "invalid distance too far back"
             rec = 0x80000000u | (md - 1u) | (((toc + 512u) & 0x1fffu) << 15);
           } else {
             rec = (tli + lsh - toc + 8192u) & 0x3fffu;
           }
           rec_r[idx] = rec;
-          if (here) {
-            const uint32_t s = to > c0 ? toc : 0u, e = (to + len < c1 ? to + len : c1) - c0;
+          {  // (no exec-mask branch: a token outside the chunk marks the spare slot)
+            const uint32_t s = !here ? FC : (to > c0 ? toc : 0u), e = here ? (to + len < c1 ? to + len : c1) - c0 : 0u;
             fd[s] = idx;
             for (uint32_t r = (s + 64u) & ~63u; r < e; r += 64u) fd[r] = idx;
           }
@@ -2572,7 +2574,8 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
         t_li = li;
         l_first = li;
       }
-      if (__syncthreads_or(bad)) {
+      __syncthreads();
+      if (uni(xbad)) {
         bad = true;
         break;
       }
