@@ -2380,7 +2380,7 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
   // each, rounds alternating, so a round needs two barriers (sums, records) and not four
   __shared__ uint32_t tokrec[2][FTPT * FNT];
   __shared__ uint64_t wsum2[2][FNT / 64];
-  __shared__ uint32_t xs[2][4];
+  __shared__ uint32_t xs[3][4];  // (row 2: the spare the other lanes write)
   __shared__ uint32_t xbad;  // a lane of the chunk's rounds met a distance too far back
   const int lane = threadIdx.x;  // (the block's thread: FNT per session)
   const uint32_t s = blockIdx.x;
@@ -2516,11 +2516,13 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
             fd[s] = idx;
             for (uint32_t r = (s + 64u) & ~63u; r < e; r += 64u) fd[r] = idx;
           }
-          if (v && to <= c1 && to + len > c1) {  // the token holding byte c1 (one at most): the
-            xs_r[0] = idx;                         // next chunk starts from it
-            xs_r[1] = to;
-            xs_r[2] = tli;
-            xs_r[3] = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
+          {  // the token holding byte c1 (one at most): the next chunk starts from it (the
+             // others write a spare row: no exec-mask branch)
+            uint32_t* const xw = (v && to <= c1 && to + len > c1) ? xs_r : xs[2];
+            xw[0] = idx;
+            xw[1] = to;
+            xw[2] = tli;
+            xw[3] = ism ? tli : tli + (c1 - to);  // the next chunk's first literal
           }
           to += len;
           tli += ism ? 0u : len;
@@ -2630,10 +2632,11 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       if (head > n) head = n;
       if ((uint32_t)lane < head) dst[lane] = (uint8_t)fd[lane];
       const uint32_t nw = (n - head) >> 2;
-      for (uint32_t w = (uint32_t)lane; w < nw; w += FNT) {
-        const uint32_t b = head + 4u * w;
-        reinterpret_cast<uint32_t*>(dst + head)[w] =
-            (fd[b] & 0xffu) | ((fd[b + 1] & 0xffu) << 8) | ((fd[b + 2] & 0xffu) << 16) | ((fd[b + 3] & 0xffu) << 24);
+#pragma unroll
+      for (int q = 0; q < (int)(FC / 4 / FNT); ++q) {  // (descriptors read unmasked: b + 3 < FC + 4)
+        const uint32_t w = (uint32_t)FNT * q + (uint32_t)lane, b = head + 4u * w;
+        const uint32_t x = (fd[b] & 0xffu) | ((fd[b + 1] & 0xffu) << 8) | ((fd[b + 2] & 0xffu) << 16) | ((fd[b + 3] & 0xffu) << 24);
+        if (w < nw) reinterpret_cast<uint32_t*>(dst + head)[w] = x;
       }
       const uint32_t tb = head + 4u * nw;
       if ((uint32_t)lane < n - tb) dst[tb + lane] = (uint8_t)fd[tb + lane];
