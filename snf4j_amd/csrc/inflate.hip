@@ -2585,8 +2585,16 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
       FPROF_T(f_ch);
       // 2. chase copies inside the chunk: a byte's source precedes it, so a chain
       //    ends at a literal or at a byte before the chunk (kept as a position)
-      for (uint32_t j = (uint32_t)lane; j < n; j += FNT) {
+#pragma unroll
+      for (int u = 0; u < (int)(FC / FNT); ++u) {
+        // the first hop unmasked (a byte with no source in the chunk re-reads itself), the
+        // rest of a chain (rarer) by the loop; fd read and written unmasked (j < FC)
+        const uint32_t j = (uint32_t)FNT * u + (uint32_t)lane;
         uint32_t v = fd[j];
+        v = j < n ? v : FD_LIT;
+        const bool p1 = !(v & FD_LIT) && (int32_t)v - FD_BIAS >= C0;
+        const uint32_t h = fd[p1 ? (uint32_t)((int32_t)v - FD_BIAS - C0) : j];
+        v = p1 ? h : v;
         while (!(v & FD_LIT) && (int32_t)v - FD_BIAS >= C0) v = fd[(int32_t)v - FD_BIAS - C0];
         fd[j] = v;
       }
