@@ -5,4 +5,4 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 bash scripts/gpu_r04_final.sh || exit 1
-bash scripts/gpu_profiles.sh r04y inflate
+bash scripts/gpu_profiles.sh r04z inflate
