@@ -117,15 +117,33 @@ def launch_or_check_world(args) -> int:
     return world
 
 
+def cpu_quota() -> float | None:
+    """CPUs this process's cgroup may use (cgroup v2 cpu.max quota / period), if capped."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as fh:
+            q, p = fh.read().split()[:2]
+        return None if q == "max" else int(q) / int(p)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_threads() -> tuple[int, str]:
-    """Host threads for the N-thread CPU baseline: this process's CPU affinity,
-    capped by OMP_NUM_THREADS when set (the GPU box's CPU share is 16, while the
-    affinity mask may list the whole machine)."""
+    """Host threads for the N-thread CPU baseline: every CPU this process may run on
+    (sched_getaffinity), except that on the GPU box the harness allots one GPU's job a
+    CPU share (OMP_NUM_THREADS / the cgroup quota, 16) and asks worker pools to stay
+    within it — the affinity mask there lists the whole shared machine.  Both counts
+    are stated beside the figure."""
     aff = len(os.sched_getaffinity(0))
+    quota = cpu_quota()
     omp = os.environ.get("OMP_NUM_THREADS")
-    if omp and omp.isdigit() and 0 < int(omp) < aff:
-        return int(omp), f"min(sched_getaffinity={aff}, OMP_NUM_THREADS={omp})"
-    return aff, f"sched_getaffinity={aff}"
+    share = int(omp) if omp and omp.isdigit() and int(omp) > 0 else None
+    if quota is not None:
+        share = min(share or aff, max(1, int(quota)))
+    if share and share < aff:
+        return share, (f"{share} = the job's CPU share (OMP_NUM_THREADS={omp}, cgroup quota "
+                       f"{'none' if quota is None else f'{quota:g} CPUs'}); sched_getaffinity lists {aff} CPUs "
+                       f"of the shared host")
+    return aff, f"sched_getaffinity={aff} (every CPU this process may use)"
 
 
 def config0_line():
@@ -382,16 +400,16 @@ def main():
             "cpu_baseline": cpu,
             "cpu_baseline_threads": cpu_mt,
         }
-        # the same kernel's mean launch under rocprofv3 in the committed profile of this
-        # workload (another process, maybe another box): its fraction, and the delta
+        # NOT measured by this run: the same kernel's mean launch in the committed rocprofv3
+        # profile of this workload (another process, maybe another build or box), kept
+        # apart from the measured roofline block as a cross-reference
         prof_ms, prof_src = profiled_launch("north" if args.config == "north" and not args.binary else
                                             {"1": "configs1", "3": "configs3"}.get(args.config, "north"),
                                             "k_piecesN<1, 1, 2")  # (rocprof prints the defaulted template arguments too)
         if prof_ms and F == 1 << 20 and P == 4096 and not args.binary:
             pf = alg_bytes / (prof_ms / 1e3) / 1e9 / HBM_PEAK_GBS
-            out["roofline"].update({"frac_profiles": round(pf, 4), "profiles_launch_ms": round(prof_ms, 4),
-                                    "profiles_source": prof_src,
-                                    "frac_minus_frac_profiles": round(achieved / HBM_PEAK_GBS - pf, 4)})
+            out["reference_profile"] = {"source": prof_src, "launch_ms": round(prof_ms, 4), "frac": round(pf, 4),
+                                        "note": "committed profile, not this run (compare with roofline.frac)"}
         if e2e:
             out["e2e_pinned"] = e2e
         if validator:

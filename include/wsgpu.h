@@ -176,7 +176,10 @@ int wsg_close(wsg_ctx* ctx);
  *                            serial decoder)
  *   WSG_TUNE_FUSED_SCAN      0: always launch k_scan (k_link does not fold block aggregates)
  *   WSG_TUNE_AGG_UNITS       aggregator gather units per wave: 1, 2 (default) or 4
- *   WSG_TUNE_AGG_GRID        aggregator gather waves at most (default 65536) */
+ *   WSG_TUNE_AGG_GRID        aggregator gather waves at most (default 65536)
+ *   WSG_TUNE_AGG_FOLD_MAX    aggregator plans of up to this many 512-frame blocks fold the block
+ *                            sums in k_agg_b / k_agg_c (default: as many as LDS allows, 3,072);
+ *                            larger ones run k_agg_scan (0 forces it: the tests' way to reach it) */
 enum {
     WSG_TUNE_INFLATE_TOKENS = 1,
     WSG_TUNE_INFLATE_FAST = 2,
@@ -187,7 +190,8 @@ enum {
     WSG_TUNE_AGG_UNITS = 7,
     WSG_TUNE_AGG_GRID = 8,
     WSG_TUNE_INFLATE_TABS = 9,
-    WSG_TUNE_INFLATE_SPLIT = 10
+    WSG_TUNE_INFLATE_SPLIT = 10,
+    WSG_TUNE_AGG_FOLD_MAX = 11
 };
 int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */
@@ -414,7 +418,9 @@ int64_t wsg_batcher_await(wsg_batcher* b, uint64_t seen, int64_t timeout_ms);
  * `max_wire` bytes and `max_frames` frames, so those flushes allocate nothing (the
  * stage chain's buffers, sized by what inflate and the aggregator produce, grow on
  * first use beyond this: the one documented exception).  wsg_batcher_alloc_count is
- * the number of pinned/device allocations all batchers of the process have made. */
+ * the number of pinned/device allocations all batchers of the process have made.
+ * Precondition: no flush in flight (it moves the slots' buffers, which a queued flush
+ * still reads and writes): WSG_API_ERANGE otherwise, nothing changed. */
 int wsg_batcher_reserve(wsg_batcher* b, uint64_t max_wire, uint64_t max_frames);
 uint64_t wsg_batcher_alloc_count(void);
 /* The decoders after "ws-decoder" that a flush runs in the same device batch, in the
@@ -502,7 +508,7 @@ int wsg_enc_batcher_wait(wsg_enc_batcher* b, wsg_enc_view* out);
 /* slot `sid` for a new session: its queued frames are dropped, the close latch cleared */
 int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid);
 /* as wsg_batcher_ticket / _await / _reserve, for the encode batcher (max_payload:
- * payload bytes a flush may hold) */
+ * payload bytes a flush may hold; reserve: WSG_API_ERANGE with a flush in flight) */
 uint64_t wsg_enc_batcher_ticket(wsg_enc_batcher* b);
 int64_t wsg_enc_batcher_await(wsg_enc_batcher* b, uint64_t seen, int64_t timeout_ms);
 int wsg_enc_batcher_reserve(wsg_enc_batcher* b, uint64_t max_frames, uint64_t max_payload);

@@ -16,6 +16,21 @@
  * writenf(CloseFrame(code)), the closed latch, and an InvalidFrameException with
  * the reference's message (GENTLE close, InvalidFrameException.java:75-77).
  *
+ * An exception thrown after the decoder (a decoder behind the batched stages, or
+ * the handler's read) ends the session as the selector loop ends it when the
+ * pipeline throws (InternalSelectorLoop.java:589-601 -> InternalSession.exception
+ * -> controlClose, InternalSession.java:804-848): an ICloseControllingException
+ * GENTLE -> handler.exception(getClosingCause()) + close(); NONE -> the exception
+ * only, the session goes on with its next frame; DEFAULT, or any other exception ->
+ * handler.exception + quickClose().  Not reachable from outside org.snf4j.core:
+ * futuresController.exception (the session futures fail when the session closes
+ * instead) and pipelineItem.cause.
+ *
+ * available() throws the u64 length errors itself, as FrameDecoder.available does
+ * (:388-394), but only after every frame the session read before the bad header
+ * has been delivered (WsgBatcher.drain): the reference delivered those before it
+ * reached the header.
+ *
  * The session slot is taken at the first decode (the pipeline is then complete:
  * the handshake has switched the decoders and the extensions have added theirs)
  * and given back at the session's end (IEventDrivenCodec, as ZlibDecoder does,
@@ -27,11 +42,13 @@ import java.nio.ByteBuffer;
 import java.util.ArrayList;
 import java.util.List;
 
+import org.snf4j.core.ICloseControllingException;
 import org.snf4j.core.codec.IBaseDecoder;
 import org.snf4j.core.codec.ICodec;
 import org.snf4j.core.codec.ICodecPipeline;
 import org.snf4j.core.codec.IDecoder;
 import org.snf4j.core.codec.IEventDrivenCodec;
+import org.snf4j.core.handler.IHandler;
 import org.snf4j.core.handler.SessionEvent;
 import org.snf4j.core.session.ISession;
 import org.snf4j.core.session.IStreamSession;
@@ -81,7 +98,7 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 		if (remaining > 0)
 			return (int) Math.min(len, remaining);
 		long r = Wsg.frameAvailable(buffer, off, len, err);
-		return checked(session, r);
+		return checked(session, r, len);
 	}
 
 	/** FrameDecoder.available(ISession, ByteBuffer, boolean) (:290-332); the buffer is not modified. */
@@ -103,13 +120,21 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 			b.duplicate().get(hdr);  // available() must not move the buffer (IBaseDecoder.java:58-70)
 			r = Wsg.frameAvailable(hdr, 0, len, err);
 		}
-		return checked(session, r);
+		return checked(session, r, len);
 	}
 
 	/** err = {status, detail, detail2, frame length once the header is complete} */
-	private int checked(ISession session, long r) {
+	private int checked(ISession session, long r, int len) {
+		if (r == -2)  // (the JNI call's arguments, never the bytes)
+			throw new IllegalArgumentException("frameAvailable: bad buffer range");
 		if (r < 0) {  // Negative / Extended payload length (FrameDecoder.java:388-394)
-			fail(session, (int) err[0], err[1], err[2], true);
+			long status = err[0], detail = err[1], detail2 = err[2];
+			this.session = session;
+			if (sid >= 0)
+				batcher.drain(this);  // the frames read before this header first
+			if (closed)  // one of them failed first: the reference never reached this header
+				return len;
+			fail(session, (int) status, detail, detail2, true);
 		}
 		if (r > 0 && err[3] > r)  // a partial frame: the rest follows in later reads
 			remaining = err[3];
@@ -204,36 +229,63 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 		return chain;
 	}
 
-	/** One frame through the rest of the pipeline, then the handler (DefaultCodecExecutor.java:557-584). */
+	/**
+	 * One frame through the rest of the pipeline, then the handler
+	 * (DefaultCodecExecutor.java:557-584, CodecExecutorAdapter.java:228-254).  An
+	 * exception from either goes where the selector loop sends it (controlClose);
+	 * false if the session is closed by it.
+	 */
 	private boolean downstream(Frame frame, List<IDecoder<Object, Object>> chain) {
 		List<Object> in = new ArrayList<Object>(1);
 		in.add(frame);
-		for (IDecoder<Object, Object> c : chain) {
-			List<Object> next = new ArrayList<Object>();
-			for (Object o : in) {
-				try {
+		try {
+			for (IDecoder<Object, Object> c : chain) {
+				List<Object> next = new ArrayList<Object>();
+				for (Object o : in)
 					c.decode(session, o, next);
-				} catch (Exception e) {
-					session.getHandler().exception(e);
-					session.close();
-					closed = true;
-					return false;
-				}
+				in = next;
 			}
-			in = next;
+			for (Object o : in)
+				session.getHandler().read(o);
+		} catch (Exception e) {
+			return controlClose(e);
 		}
-		for (Object o : in)
-			session.getHandler().read(o);
 		return true;
+	}
+
+	/**
+	 * InternalSession.exception / controlClose (InternalSession.java:804-848) for an
+	 * exception the pipeline threw: true if the session stays open (close type NONE).
+	 */
+	private boolean controlClose(Throwable t) {
+		IHandler handler = session.getHandler();
+		if (t instanceof ICloseControllingException) {
+			ICloseControllingException c = (ICloseControllingException) t;
+			Throwable cause = c.getClosingCause();
+			switch (c.getCloseType()) {
+			case GENTLE:
+				closed = true;
+				handler.exception(cause);
+				session.close();
+				return false;
+			case NONE:
+				handler.exception(cause);
+				return true;
+			default:
+				t = cause;
+			}
+		}
+		closed = true;
+		handler.exception(t);
+		session.quickClose();
+		return false;
 	}
 
 	/** The device batch this session's bytes were in failed (not a protocol error). */
 	void failBatch(Exception e) {
 		if (closed || released || session == null)
 			return;
-		closed = true;
-		session.getHandler().exception(e);
-		session.close();
+		controlClose(e);
 	}
 
 	private void fail(ISession session, int status, long detail, long detail2, boolean inAvailable) {
@@ -244,9 +296,8 @@ public class GpuFrameDecoder implements IBaseDecoder<ByteBuffer, Frame>, IEventD
 		if (inAvailable)
 			throw e;  // FrameDecoder.available throws here too (:388-394)
 		// a deferred decode error: what the selector loop does with the pipeline's exception
-		// (InternalSelectorLoop.java:589-601), then the GENTLE close (InternalSession.java:804-829)
-		session.getHandler().exception(e);
-		session.close();
+		// (InternalSelectorLoop.java:589-601): InvalidFrameException is GENTLE (:75-77)
+		controlClose(e);
 	}
 
 	/* ---- IEventDrivenCodec (IEventDrivenCodec.java:36-62) ---- */

@@ -386,6 +386,33 @@ public final class WsgBatcher {
 		schedule();
 	}
 
+	/**
+	 * Every frame d's session has read so far delivered now, in order: the iteration's
+	 * reads of d's batcher fed and flushed, and all its flushes collected, waiting for
+	 * the device.  GpuFrameDecoder.available calls it before it throws a header error
+	 * (FrameDecoder.java:388-394), since the reference delivered the frames before that
+	 * header when it reached it.  An error path: the loop blocks here.
+	 */
+	synchronized void drain(GpuFrameDecoder d) {
+		Native n = nativeOf(d);
+		if (n == null)
+			return;
+		try {
+			boolean fed = n.nReads > 0;
+			feedReads(n);
+			if (fed) {
+				if (n.inflight.size() == 2)
+					collectOldest(n);
+				check(Wsg.batcherFlushAsync(n.handle), "wsg_batcher_flush_async");
+				n.inflight.add(Wsg.batcherTicket(n.handle));
+			}
+			while (!n.inflight.isEmpty())
+				collectOldest(n);
+		} catch (RuntimeException ex) {
+			failSessions(n, ex);
+		}
+	}
+
 	/* ------------------------------------------------------------------ encode side */
 
 	synchronized int registerEncoder(GpuFrameEncoder e, boolean clientMode) {

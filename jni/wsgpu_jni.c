@@ -230,27 +230,32 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherFeedMany(JNIEnv* 
         (*env)->GetIntArrayRegion(env, sids, base, m, so);
         (*env)->GetIntArrayRegion(env, offs, base, m, oo);
         (*env)->GetIntArrayRegion(env, lens, base, m, lo);
-        for (jint k = 0; k < m; ++k) {
+        int rc = WSG_API_OK;
+        for (jint k = 0; k < m; ++k) {  /* checked again: pass 1's values are not trusted across the passes */
             gs[k] = (uint32_t)so[k];
             gl[k] = (uint64_t)lo[k];
             gp[k] = NULL;
             pin[k] = NULL;
+            ref[k] = NULL;
+            if (rc != WSG_API_OK) continue;
+            if (so[k] < 0 || oo[k] < 0 || lo[k] < 0) {
+                rc = WSG_API_EINVAL;
+                continue;
+            }
             ref[k] = (*env)->GetObjectArrayElement(env, direct, base + k);
-            if (ref[k]) {
+            if (ref[k]) {  /* a direct buffer: its address, never pinned as an array */
                 gp[k] = span_at(env, ref[k], oo[k], lo[k]);
+                if (!gp[k]) rc = WSG_API_EINVAL;
             } else {
                 ref[k] = (*env)->GetObjectArrayElement(env, heap, base + k);  /* byte[] or null (empty read) */
+                if (ref[k] ? !range_in(env, ref[k], oo[k], lo[k]) : lo[k] != 0) rc = WSG_API_EINVAL;
             }
         }
-        int rc = WSG_API_OK;
-        for (jint k = 0; k < m; ++k)  /* the heap arrays pinned: only critical calls until released */
+        for (jint k = 0; k < m && rc == WSG_API_OK; ++k)  /* the heap arrays pinned: only critical calls until released */
             if (ref[k] && !gp[k]) {
                 pin[k] = (*env)->GetPrimitiveArrayCritical(env, ref[k], NULL);
-                if (!pin[k]) {
-                    rc = WSG_API_ENOMEM;
-                    break;
-                }
-                gp[k] = (const uint8_t*)pin[k] + oo[k];
+                if (pin[k]) gp[k] = (const uint8_t*)pin[k] + oo[k];
+                else rc = WSG_API_ENOMEM;
             }
         if (rc == WSG_API_OK) rc = wsg_batcher_feed_many(BATCHER(b), (uint32_t)m, gs, gp, gl);
         for (jint k = m; k-- > 0;)

@@ -47,6 +47,7 @@ constexpr uint32_t AG_CARRY = 64u;   // member of the frame carried in from an e
 #define WSG_AGG_FOLD_MAX 3072  // (configs[2]: 2,128 blocks fold; k_agg_c stages 16 B a block: 48 KiB of LDS at most)
 #endif
 constexpr uint32_t AGG_FOLD_MAX = WSG_AGG_FOLD_MAX;
+uint32_t agg_fold_bound() { return AGG_FOLD_MAX; }
 __device__ __forceinline__ uint64_t agg_pos(const AggArgs& a, uint64_t j) { return a.pl[j] + a.pre_sum[j / ABLOCK]; }
 // cl / blk_cnt pack two counts: emitted frames (bits 0-31) and gather units (32-63)
 __device__ __forceinline__ uint64_t agg_cnt(const AggArgs& a, uint64_t j) {
@@ -162,7 +163,7 @@ __global__ __launch_bounds__(ABLOCK) void k_agg_b(AggArgs a) {
   // block folds k_agg_a's block maxima itself (coalesced; max commutes), so the
   // first k_agg_scan launch is skipped; beyond, k_agg_scan left the exclusive maxima
   int32_t bs, be;
-  if (a.nblk <= AGG_FOLD_MAX) {
+  if (a.nblk <= a.fold_max) {
     Agg f = AGG_ID, ft;
     for (uint32_t b = threadIdx.x; b < blockIdx.x; b += ABLOCK) {
       const int32_t x0 = a.blk_max[b], x1 = a.blk_max[a.nblk + b];
@@ -553,7 +554,7 @@ __global__ __launch_bounds__(64) void k_agg_gather(AggArgs a, uint64_t src_lim) 
 void launch_agg_plan(const AggArgs& a, hipStream_t s) {
   if (!a.n_frames) return;
   hipLaunchKernelGGL(k_agg_a, dim3(a.nblk), dim3(ABLOCK), 0, s, a);
-  const bool fold = a.nblk <= AGG_FOLD_MAX;
+  const bool fold = a.nblk <= a.fold_max;
   if (!fold) hipLaunchKernelGGL(k_agg_scan, dim3(1), dim3(1024), 0, s, a, 0);
   hipLaunchKernelGGL(k_agg_b, dim3(a.nblk), dim3(ABLOCK), 0, s, a);
   if (fold) {
@@ -575,6 +576,5 @@ void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim, int pe
   else if (per_wave == 4) hipLaunchKernelGGL((k_agg_gather<4>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
   else hipLaunchKernelGGL((k_agg_gather<2>), dim3((uint32_t)g), dim3(64), 0, s, a, src_lim);
 }
-void launch_agg_final(const AggArgs&, hipStream_t) {}  // (done by k_agg_gather's first waves)
 
 }  // namespace ws

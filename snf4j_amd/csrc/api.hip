@@ -17,7 +17,7 @@ namespace {
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_agg_final", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate"};
+                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -82,6 +82,7 @@ struct wsg_ctx {
   int fused_scan = 1;                // WSG_TUNE_FUSED_SCAN 0: always launch k_scan
   int agg_units = 2;                 // WSG_TUNE_AGG_UNITS: k_agg_gather units per wave (1, 2 or 4)
   uint32_t agg_grid = 65536;         // WSG_TUNE_AGG_GRID: k_agg_gather waves at most
+  uint32_t agg_fold = 0xFFFFFFFFu;   // WSG_TUNE_AGG_FOLD_MAX: plan blocks folded at most (tests: 0 forces k_agg_scan)
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -180,6 +181,7 @@ void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src) {
   dst->fused_scan = src->fused_scan;
   dst->agg_units = src->agg_units;
   dst->agg_grid = src->agg_grid;
+  dst->agg_fold = src->agg_fold;
 }
 int ctx_device(wsg_ctx* c) { return c->device; }
 uint8_t* ctx_async_payload(wsg_ctx* c) { return c->last_async_payload; }
@@ -266,6 +268,7 @@ int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
       c->agg_units = (int)value;
       break;
     case WSG_TUNE_AGG_GRID: c->agg_grid = value < 1 ? 1u : (value > (1 << 24) ? (1u << 24) : (uint32_t)value); break;
+    case WSG_TUNE_AGG_FOLD_MAX: c->agg_fold = value < 0 ? 0u : (value > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)value); break;
     default: return set_err(c, WSG_API_EINVAL, "unknown tuning key");
   }
   return WSG_API_OK;
@@ -881,6 +884,7 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   // gather units: a member of m bytes has ceil((m + 15) / 1 KiB); those holding bytes below
   // agg_cap number at most agg_cap / 1 KiB + 2 per member before them
   a.n_pieces = agg_cap / PIECE + 2 * F + 2;
+  a.fold_max = std::min(c->agg_fold, agg_fold_bound());
   HIP_TRY(c, c->a_code.ensure(F * 2 * sizeof(uint32_t)));
   HIP_TRY(c, c->a_last.ensure(F * 2 * sizeof(int32_t)));
   HIP_TRY(c, c->a_pl.ensure(F * sizeof(uint64_t)));
@@ -904,7 +908,6 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   if (!n_frames) HIP_TRY(c, hipMemsetAsync(agg_total, 0, sizeof(uint64_t), c->stream));
   timed(c, K_AGG, [&] { launch_agg_plan(a, c->stream); });
   timed(c, K_AGG_GATHER, [&] { launch_agg_gather(a, c->stream, payload_len, c->agg_units, c->agg_grid); });
-  timed(c, K_AGG_FINAL, [&] { launch_agg_final(a, c->stream); });
   HIP_TRY(c, hipGetLastError());
   return WSG_API_OK;
 }

@@ -1383,6 +1383,9 @@ int64_t wsg_batcher_await(wsg_batcher* b, uint64_t seen, int64_t timeout_ms) {
 // grow on first use beyond this).
 int wsg_batcher_reserve(wsg_batcher* b, uint64_t max_wire, uint64_t max_frames) {
   if (!b) return WSG_API_EINVAL;
+  // growing a slot's buffers moves them: a flush in flight reads or writes them (its
+  // H2D source, its D2H targets), so the batcher must be idle
+  if (!b->q.empty()) return bset(b, WSG_API_ERANGE, "wsg_batcher_reserve: flushes in flight (wait for them first)");
   const uint32_t S = b->n;
   const uint64_t pcap = max_wire + 16 * max_frames + 16;
   B_TRY(b, b->st.ensure((S + 1) * sizeof(wsg_session_state)));
@@ -1744,6 +1747,7 @@ int64_t wsg_enc_batcher_await(wsg_enc_batcher* b, uint64_t seen, int64_t timeout
 // frames and `max_payload` payload bytes: such flushes allocate nothing.
 int wsg_enc_batcher_reserve(wsg_enc_batcher* b, uint64_t max_frames, uint64_t max_payload) {
   if (!b) return WSG_API_EINVAL;
+  if (!b->q.empty()) return eset(b, WSG_API_ERANGE, "wsg_enc_batcher_reserve: flushes in flight (wait for them first)");
   const uint32_t S = b->n;
   const uint64_t arena = max_payload + 16 * max_frames + 32;  // 16-B aligned payloads
   const uint64_t need = max_payload + 14 * max_frames + 32;   // the longest header is 14 B

@@ -2338,6 +2338,10 @@ namespace {
 #define WSG_FAST_CHUNK 4096
 #endif
 constexpr uint32_t FC = WSG_FAST_CHUNK;   // output bytes resolved per chunk (a multiple of FNT)
+// the replay's token records pack (start - c0 + 512) into 13 bits and a literal's lb
+// index - jj + 8192 into 14: both must stay below their field for every chunk size built
+static_assert(FC + 512u + 258u < 8192u, "WSG_FAST_CHUNK too large for the 13-bit match start field");
+static_assert(FC + 4u < 8192u, "WSG_FAST_CHUNK too large for the 14-bit literal offset field");
 constexpr uint32_t FD_LIT = 0x80000000u;  // descriptor: a resolved byte (bits 0-7)
 constexpr int32_t FD_BIAS = 32768;        // descriptor: position + FD_BIAS (history positions are >= -32768)
 

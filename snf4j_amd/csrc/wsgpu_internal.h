@@ -178,6 +178,8 @@ struct AggArgs {
   uint64_t* n_units;   // [1] gather units of the batch (k_agg_scan)
   struct PieceDesc* pieces;  // [n_pieces]: gather units (k_agg_c -> k_agg_gather)
   uint64_t n_pieces;         // bound on the units (agg_units_bound)
+  uint32_t fold_max;         // plans of up to this many blocks fold their block aggregates
+                             // (min(WSG_TUNE_AGG_FOLD_MAX, the LDS bound)); larger: k_agg_scan
   uint32_t nblk;
 };
 
@@ -222,7 +224,7 @@ struct InflTokStat {
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_AGG_FINAL, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -253,9 +255,9 @@ void launch_enc_desc(const EncodeArgs& a, hipStream_t s);
 void launch_enc_pieces(const EncodeArgs& a, hipStream_t s);
 void launch_enc_final(const EncodeArgs& a, hipStream_t s);
 
+uint32_t agg_fold_bound();  // the largest plan (blocks) k_agg_c's LDS can fold
 void launch_agg_plan(const AggArgs& a, hipStream_t s);
 void launch_agg_gather(const AggArgs& a, hipStream_t s, uint64_t src_lim, int per_wave, uint32_t grid_cap);
-void launch_agg_final(const AggArgs& a, hipStream_t s);
 
 void launch_inflate(const InflArgs& a, hipStream_t s);
 void launch_infl_tok(const InflArgs& a, hipStream_t s);

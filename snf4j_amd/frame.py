@@ -198,3 +198,7 @@ class InvalidFrameException(RuntimeError):
 
     def getCloseType(self):
         return self.closeType
+
+    def getClosingCause(self):
+        """ICloseControllingException.getClosingCause (InvalidFrameException.java:112-115)."""
+        return self

@@ -1,0 +1,325 @@
+"""Harness for the drop-in decoder's session behaviour (test infrastructure).
+
+Two runs of the same plan — per session: a byte stream cut into socket reads, a
+decoder behind "ws-decoder" that throws on chosen frames with a chosen close type,
+and a handler whose read() throws on chosen frames — through the restated snf4j read
+loop (snf4j_amd/loop.py StreamSession: StreamSession.java:765-854, controlClose
+InternalSession.java:804-848):
+
+  reference  the oracle's FrameDecoder (oracle/ws_oracle.c, FrameDecoder.java:92-401
+             + FrameUtf8Validator) as "ws-decoder", one session at a time;
+  drop-in    snf4j_amd.loop.GpuFrameDecoder over a batcher, all sessions on one
+             SelectorLoop: the native DecoderBatcher on the GPU, or OracleBatcher
+             below (the same scheduling, the oracle decoding each flush) on the CPU.
+
+Each session's record is what its handler saw and how the session ended:
+("read", opcode, fin, rsv, payload) | ("exception", type, message) | ("close",) |
+("quickClose",) | ("writenf", close status).  The peer sends nothing once the
+reference session closed (the drop-in gets the same reads), and after an exception
+that leaves bytes unread (close type NONE) it sends one more PING so that the
+reference reads them (the drop-in then reads the same PINGs).
+"""
+from __future__ import annotations
+
+import collections
+import threading
+import random
+import struct
+
+import numpy as np
+
+from snf4j_amd.frame import CloseFrame, InvalidFrameException, make_frame
+from snf4j_amd.loop import ByteBuffer, CloseType, SelectorLoop, StreamSession
+from tests import wsgen
+
+PING = wsgen.build_frame(9, True, 0, b"!", True, (1, 2, 3, 4))
+
+
+# ---------------------------------------------------------------- exceptions the chain throws
+class _Controlled(RuntimeError):
+    """An ICloseControllingException whose closing cause is another exception."""
+    KIND = None
+
+    def __init__(self, msg):
+        super().__init__(msg)
+        self.cause = ValueError(f"cause of {msg}")
+
+    def getCloseType(self):
+        return self.KIND
+
+    def getClosingCause(self):
+        return self.cause
+
+
+class GentleError(_Controlled):
+    KIND = CloseType.GENTLE
+
+
+class NoneError(_Controlled):
+    KIND = CloseType.NONE
+
+
+class DefaultError(_Controlled):
+    KIND = CloseType.DEFAULT
+
+
+class PlainError(RuntimeError):
+    pass
+
+
+_RAISE = {"GENTLE": GentleError, "NONE": NoneError, "DEFAULT": DefaultError, "PLAIN": PlainError}
+
+
+class Thrower:
+    """A decoder after "ws-decoder": throws on the k-th data frame it sees if plan[k]."""
+    batched = False
+
+    def __init__(self, plan):
+        self.plan, self.k = plan, 0
+
+    def decode(self, session, frame, out):
+        if int(frame.getOpcode()) <= 2:
+            k, self.k = self.k, self.k + 1
+            kind = self.plan.get(k)
+            if kind:
+                raise _RAISE[kind](f"decoder throws {kind} at data frame {k}")
+        out.append(frame)
+
+
+def handler_thrower(plan):
+    """IHandler.read throwing on the k-th data frame it receives."""
+    n = [0]
+
+    def read(session, frame):
+        if int(frame.getOpcode()) <= 2:
+            k = n[0]
+            n[0] += 1
+            kind = plan.get(k)
+            if kind:
+                raise _RAISE[kind](f"handler throws {kind} at data frame {k}")
+    return read
+
+
+class RefFrameDecoder:
+    """The reference FrameDecoder as "ws-decoder": the oracle, with the reference's
+    writenf(CloseFrame) + InvalidFrameException (FrameDecoder.java:92-102, :388-394)."""
+    batched = False
+
+    def __init__(self, oracle):
+        self.o = oracle
+        self.d = oracle.Decoder(False, False, 65536, True)
+
+    def available(self, session, buf, off, length):
+        try:
+            return self.d.available(bytes(buf), off, length)
+        except self.o.InvalidFrame as e:
+            session.writenf(CloseFrame.of_status(1002))
+            raise InvalidFrameException(str(e))
+
+    def available_buffer(self, session, b: ByteBuffer, flipped):
+        v = b.duplicate() if flipped else b.duplicate().flip()
+        return self.available(session, v.peek(), 0, v.remaining())
+
+    def decode(self, session, data: ByteBuffer, out):
+        try:
+            f = self.d.decode(data.get(data.remaining()))
+        except self.o.InvalidFrame as e:
+            session.writenf(CloseFrame.of_status(e.close_code))
+            raise InvalidFrameException(str(e))
+        finally:
+            session.release(data)
+        if f is not None:
+            out.append(make_frame(f.opcode, f.fin, f.rsv, f.payload))
+
+
+# ---------------------------------------------------------------- plans
+def bad_length_header(rng, negative: bool) -> bytes:
+    """A masked header whose u64 length available() rejects (FrameDecoder.java:388-394)."""
+    n = (1 << 63) | rng.randrange(1 << 40) if negative else 0x7FFFFFF0 + rng.randrange(1 << 20)
+    return bytes([0x82, 0xFF]) + struct.pack(">Q", n) + bytes(4)
+
+
+def make_plan(seed: int, n_sessions: int, big_every: int = 9):
+    rng = random.Random(seed)
+    nrng = np.random.default_rng(seed)
+    sessions = []
+    for s in range(n_sessions):
+        inject = wsgen.INJECT_KINDS[rng.randrange(len(wsgen.INJECT_KINDS))] if rng.random() < 0.2 else None
+        frames = wsgen.session_frames(nrng, rng.randrange(2, 16), big=(s % big_every == 0), inject=inject)
+        if rng.random() < 0.15:  # a u64 length error, somewhere in the stream, garbage after it
+            pos = rng.randrange(len(frames) + 1)
+            frames.insert(pos, bad_length_header(rng, rng.random() < 0.5) + bytes(rng.randrange(0, 40)))
+        stream = b"".join(frames)
+        cuts = sorted(rng.randrange(1, len(stream)) for _ in range(rng.randrange(0, 8))) if len(stream) > 1 else []
+        pts = [0] + cuts + [len(stream)]
+        chunks = [stream[a:b] for a, b in zip(pts, pts[1:]) if b > a]
+        dec = {}
+        hnd = {}
+        r = rng.random()
+        if r < 0.5:
+            for _ in range(rng.randrange(1, 3)):
+                dec[rng.randrange(0, 12)] = rng.choice(["GENTLE", "NONE", "NONE", "DEFAULT", "PLAIN"])
+        if rng.random() < 0.25:
+            hnd[rng.randrange(0, 12)] = rng.choice(["NONE", "PLAIN", "GENTLE"])
+        sessions.append({"chunks": chunks, "dec": dec, "hnd": hnd,
+                         "optimized": rng.random() < 0.5, "direct": rng.random() < 0.3})
+    return sessions
+
+
+def _event(e):
+    if e[0] == "read":
+        f = e[1]
+        return ("read", int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload())
+    if e[0] == "exception":
+        return ("exception", type(e[1]).__name__, str(e[1]))
+    if e[0] == "writenf":
+        return ("writenf", e[1].getStatus())
+    return e
+
+
+def endings(records) -> set:
+    """The kinds of exception and ending the records hold (a plan's coverage)."""
+    tags = set()
+    for rec in records:
+        for e in rec:
+            if e[0] in ("close", "quickClose"):
+                tags.add(e[0])
+            elif e[0] == "exception":
+                tags.add(e[1])
+                tags |= {k for k in _RAISE if f"throws {k} " in e[2]}
+                if "payload length" in e[2] and "Negative" in e[2] or "Extended" in e[2]:
+                    tags.add("length")
+    return tags
+
+
+def _session(sp, base):
+    return StreamSession([("ws-decoder", base), ("thrower", Thrower(sp["dec"]))],
+                         handler_read=handler_thrower(sp["hnd"]), optimized=sp["optimized"], direct=sp["direct"])
+
+
+def run_reference(oracle, plan):
+    """Each session alone; fixes each plan's reads (truncated at the close, PINGs added)."""
+    out = []
+    for sp in plan:
+        s = _session(sp, RefFrameDecoder(oracle))
+        sent = []
+        for c in sp["chunks"]:
+            if s.closing:
+                break
+            s.read_event(c)
+            sent.append(c)
+        for _ in range(64):  # bytes left unread by an exception that kept the session open
+            if s.closing or not s.pending_input():
+                break
+            s.read_event(PING)
+            sent.append(PING)
+        sp["reads"] = sent
+        out.append([_event(e) for e in s.events])
+    return out
+
+
+def run_dropin(plan, batcher, seed: int = 7):
+    """All sessions on one loop, reads interleaved at random, through GpuFrameDecoder."""
+    from snf4j_amd.loop import GpuFrameDecoder, run_until_idle
+    rng = random.Random(seed)
+    loop = batcher.loop
+    sess = [_session(sp, GpuFrameDecoder(False, False, 65536, batcher)) for sp in plan]
+    pos = [0] * len(plan)
+    while any(pos[i] < len(plan[i]["reads"]) for i in range(len(plan))):
+        reads = []
+        for i, sp in enumerate(plan):
+            if pos[i] < len(sp["reads"]) and rng.random() < 0.6:
+                c = sp["reads"][pos[i]]
+                pos[i] += 1
+                reads.append(lambda s=sess[i], c=c: s.read_event(c))
+        loop.run_iteration(reads)
+        if not reads:
+            loop.select(0.02)
+    run_until_idle(loop, batcher)
+    return [[_event(e) for e in s.events] for s in sess]
+
+
+# ---------------------------------------------------------------- a CPU batcher for the host logic
+class OracleBatcher:
+    """DecoderBatcher's interface and scheduling (enqueue records, one flush a loop
+    iteration, a flush delivered in a later iteration, drain) with each session's
+    bytes framed and decoded by the oracle as the native batcher does on the device:
+    test infrastructure, for running GpuFrameDecoder's host logic without a GPU."""
+
+    def __init__(self, oracle, loop: SelectorLoop, n_sessions: int):
+        self.o, self.loop, self.n = oracle, loop, n_sessions
+        self.slots = [None] * n_sessions
+        self.dec = [None] * n_sessions
+        self.buf = [b""] * n_sessions
+        self.failed = [False] * n_sessions
+        self.pending: list = []
+        self.inflight: collections.deque = collections.deque()
+        self.flush_scheduled = False
+        self.drained_reads = 0
+
+    def register(self, d):
+        sid = self.slots.index(None)
+        self.slots[sid] = d
+        self.dec[sid] = self.o.Decoder(False, False, 65536, True)
+        self.buf[sid], self.failed[sid] = b"", False
+        return sid
+
+    def unregister(self, d):
+        if d.sid >= 0 and self.slots[d.sid] is d:
+            self.slots[d.sid] = None
+            self.pending = [p for p in self.pending if p[0] != d.sid]
+
+    def enqueue(self, d, session, data):
+        self.pending.append((d.sid, data.peek()))
+        session.release(data)
+        if not self.flush_scheduled:
+            self.flush_scheduled = True
+            self.loop.executenf(self.flush)
+
+    def _decode_pending(self):
+        out = collections.defaultdict(lambda: ([], None))
+        for sid, b in self.pending:
+            frames, exc = out[sid]
+            if self.failed[sid]:
+                continue
+            self.buf[sid] += b
+            d = self.dec[sid]
+            while True:
+                try:
+                    n = d.available(self.buf[sid])
+                    if n <= 0:
+                        break
+                    f = d.decode(self.buf[sid][:n])
+                    self.buf[sid] = self.buf[sid][n:]
+                    if f is not None:
+                        frames.append(make_frame(f.opcode, f.fin, f.rsv, f.payload))
+                except self.o.InvalidFrame as e:
+                    exc = InvalidFrameException(str(e))
+                    exc.close_code = e.close_code or 1002
+                    self.failed[sid] = True
+                    break
+            out[sid] = (frames, exc)
+        self.pending = []
+        return dict(out)
+
+    def flush(self):
+        self.flush_scheduled = False
+        self.collect()
+        if self.pending:  # delivered in a later iteration: a timer in the completion thread's role
+            self.inflight.append(self._decode_pending())
+            t = threading.Timer(0.002, self.loop.executenf, (self.collect,))
+            t.daemon = True
+            t.start()
+
+    def collect(self):
+        while self.inflight:
+            for sid, (frames, exc) in self.inflight.popleft().items():
+                d = self.slots[sid]
+                if d is not None:
+                    d.deliver(frames, exc)
+
+    def drain(self, d):
+        self.drained_reads += len(self.pending)
+        if self.pending:
+            self.inflight.append(self._decode_pending())
+        self.collect()

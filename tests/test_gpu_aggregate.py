@@ -96,11 +96,23 @@ def _rand_session(rng, n, big):
     return out
 
 
+@pytest.mark.parametrize("fold", [True, False])
 @pytest.mark.parametrize("seed", range(6))
-def test_aggregate_random_batches(ctx, oracle, seed):
+def test_aggregate_random_batches(ctx, oracle, seed, fold):
     """Arbitrary frame sequences (also ones a decoder would reject: continuations
     outside a message pass through, a new start replaces an open message), split
-    over several batches with the carry, vs the oracle fed the same frames."""
+    over several batches with the carry, vs the oracle fed the same frames.  fold=False
+    forces the plan's k_agg_scan path (WSG_TUNE_AGG_FOLD_MAX 0), which the default
+    takes only above 3,072 blocks (1.5 M frames)."""
+    from snf4j_amd import BatchAggregator
+    ctx.set_tuning("agg_fold_max", 1 << 30 if fold else 0)
+    try:
+        _random_batches(ctx, oracle, seed)
+    finally:
+        ctx.set_tuning("agg_fold_max", 1 << 30)
+
+
+def _random_batches(ctx, oracle, seed):
     from snf4j_amd import BatchAggregator
     rng = np.random.default_rng(500 + seed)
     n_s = int(rng.integers(1, 90))
@@ -155,8 +167,9 @@ def test_aggregate_truncated_sessions(ctx, oracle):
 
 
 def test_aggregate_multi_pass_block_scan(ctx, oracle):
-    """More than 4096 blocks of 256 frames (1.1 M tiny frames), so k_agg_scan carries
-    its scans across passes: every session's output against the oracle."""
+    """1.1 M tiny frames: 2,150 plan blocks of 512, folded by k_agg_b / k_agg_c (the
+    default up to 3,072 blocks) and through k_agg_scan, which then carries its scans
+    across passes of 1,024 (forced): every session's output against the oracle."""
     from snf4j_amd import BatchAggregator
     rng = np.random.default_rng(4097)
     n_s, per = 128, 8600
@@ -172,7 +185,16 @@ def test_aggregate_multi_pass_block_scan(ctx, oracle):
         sessions.append(fr)
     desc, sf, res, payload = _batch(sessions)
     assert len(desc) > 4096 * 256
-    out = BatchAggregator(n_s, 1 << 20, ctx=ctx).run(desc, sf, res, payload)
+    for fold in (True, False):  # 2,150 blocks of 512: folded by default, k_agg_scan forced
+        ctx.set_tuning("agg_fold_max", 1 << 30 if fold else 0)
+        try:
+            out = BatchAggregator(n_s, 1 << 20, ctx=ctx).run(desc, sf, res, payload)
+        finally:
+            ctx.set_tuning("agg_fold_max", 1 << 30)
+        _check_multi(oracle, sessions, out)
+
+
+def _check_multi(oracle, sessions, out):
     for s, (frames, exc) in enumerate(out):
         agg = oracle.Aggregator(1 << 20)
         exp = [f for f in (agg.decode(*fr) for fr in sessions[s]) if f is not None]

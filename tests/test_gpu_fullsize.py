@@ -142,3 +142,65 @@ def test_full_size_encode_decode_round_trip():
         assert torch.equal(out[:n * FP], payload)
     finally:
         ctx.close()
+
+
+def test_configs1_full_size_binary_involution_and_no_errors():
+    """configs[1] at full size: 1 M masked BINARY frames of 1 KiB, 256 sessions (the
+    unmask-only line; BINARY frames take no UTF-8 check): zero errors, every frame
+    delivered in order into 1 KiB slots, and every payload XOR its mask is the wire
+    payload, over all 1.07 GB on the device; then planted protocol errors (a reserved
+    opcode, a clear mask bit) fail exactly those sessions at exactly those frames."""
+    import numpy as np
+    import torch
+    from snf4j_amd import Context, decoder_cfg
+    from snf4j_amd._lib import DESC_DTYPE, RESULT_DTYPE
+    F, P1, S1 = 1 << 20, 1024, 256
+    FL = P1 + 8
+    dev = torch.device("cuda", 0)
+    ctx = Context(0)
+    try:
+        wire = torch.empty(F * FL + 64, dtype=torch.uint8, device=dev)
+        off = torch.empty(F + 1, dtype=torch.int64, device=dev)
+        sf = torch.empty(S1 + 1, dtype=torch.int32, device=dev)
+        benchsupport.synth_uniform(ctx, 0xC0F1, F, P1, F // S1, 2, True, 0, wire, off, sf)
+
+        def decode():
+            payload = torch.empty(F * FL + 16 * F + 16, dtype=torch.uint8, device=dev)
+            desc = torch.empty(F * 16, dtype=torch.uint8, device=dev)
+            res = torch.empty(S1 * 16, dtype=torch.uint8, device=dev)
+            state = torch.zeros(S1 * 8, dtype=torch.uint8, device=dev)
+            ctx.decode_device(decoder_cfg(False, False, 65536, True), wire, off, sf, state, payload, desc, res,
+                              wire_len=F * FL)
+            torch.cuda.synchronize(dev)
+            return payload, desc.cpu().numpy().view(DESC_DTYPE), res.cpu().numpy().view(RESULT_DTYPE)
+
+        payload, d, r = decode()
+        assert int(r["error"].max()) == 0 and (r["n_delivered"] == F // S1).all()
+        assert (d["payload_len"] == P1).all() and (d["opcode"] == 2).all() and (d["flags"] & 0x80 == 0x80).all()
+        assert np.array_equal(d["payload_off"], np.arange(F, dtype=np.uint64) * P1)
+        w = wire[:F * FL].view(F, FL)
+        assert (w[:, 0] == 0x82).all() and (w[:, 1] == 0xFE).all()
+        for c0 in range(0, F, 1 << 18):
+            c1 = c0 + (1 << 18)
+            mask = w[c0:c1, 4:8].repeat(1, P1 // 4)
+            assert torch.equal(payload[c0 * P1:c1 * P1].view(c1 - c0, P1) ^ mask, w[c0:c1, 8:]), c0
+        del payload
+        fps = F // S1
+        plant = {7: (100, 0x83), 200: (fps - 1, 0x02)}  # session -> (frame, byte 0 / byte 1 change)
+        k7, k200 = 7 * fps + 100, 200 * fps + fps - 1
+        b0, b1 = int(w[k7, 0].item()), int(w[k200, 1].item())
+        w[k7, 0] = 0x83          # reserved opcode 3: "Invalid opcode", 1002
+        w[k200, 1] = 0x7E        # mask bit clear from a client: "Masking", 1002
+        try:
+            _, _, r = decode()
+        finally:
+            w[k7, 0], w[k200, 1] = b0, b1
+        for s in range(S1):
+            if s in plant:
+                assert int(r["error"][s]) != 0 and int(r["close_code"][s]) == 1002, s
+                assert int(r["n_delivered"][s]) == plant[s][0], s
+            else:
+                assert int(r["error"][s]) == 0 and int(r["n_delivered"][s]) == fps, s
+    finally:
+        ctx.close()
+        torch.cuda.empty_cache()

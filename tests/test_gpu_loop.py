@@ -122,3 +122,49 @@ def test_loop_encode_matches_oracle(ctx, oracle):
     for s in range(n):
         assert written[s] == expect[s], s
     eb.close()
+
+
+def test_reserve_refused_with_flushes_in_flight(ctx, oracle):
+    """wsg_batcher_reserve / wsg_enc_batcher_reserve move the slots' buffers, which a
+    queued flush still reads and writes: with flushes in flight they return
+    WSG_API_ERANGE and change nothing; the queued flushes' results stay exact."""
+    from snf4j_amd import frame as F
+    from snf4j_amd._lib import WsgError
+    from snf4j_amd.codec import EncodeBatcher, NativeBatcher
+    rng = random.Random(5)
+    nrng = np.random.default_rng(5)
+    n = 8
+    nb = NativeBatcher(n, ctx=ctx)
+    nb.reserve(1 << 16, 256)
+    streams = [[b"".join(wsgen.session_frames(nrng, rng.randrange(1, 6))) for _ in range(2)] for _ in range(n)]
+    for k in range(2):
+        for s in range(n):
+            nb.feed(s, streams[s][k])
+        nb.flush_async()
+    with pytest.raises(WsgError):
+        nb.reserve(64 << 20, 1 << 20)  # larger: every buffer would move
+    for k in range(2):
+        got = nb.wait()
+        for s in range(n):
+            frames, e = oracle.stream_decode(streams[s][k])
+            assert [(f.opcode, f.payload) for f in frames] == \
+                   [(int(f.getOpcode()), f.getPayload()) for f in got[s][0]], (k, s)
+    nb.reserve(64 << 20, 1 << 20)  # idle: fine
+    nb.close()
+    eb = EncodeBatcher(n, True, ctx=ctx)
+    eb.reserve(64, 1 << 16)
+    enc = [oracle.Encoder(True) for _ in range(n)]
+    expect = []
+    for k in range(2):
+        exp = []
+        for s in range(n):
+            p = bytes(rng.randrange(256) for _ in range(rng.randrange(0, 3000)))
+            eb.add(s, F.make_frame(2, True, 0, p), (1, 2, 3, 4))
+            exp.append(enc[s].encode(2, True, 0, p, (1, 2, 3, 4)))
+        expect.append(exp)
+        eb.flush_async()
+    with pytest.raises(WsgError):
+        eb.reserve(1 << 16, 64 << 20)
+    for k in range(2):
+        assert list(eb.wait()) == expect[k], k
+    eb.close()

@@ -174,3 +174,43 @@ def test_close_releases_the_loop_device():
     b = _java("WsgBatcher.java")
     close = b[b.index("public void close()"):]
     assert "completion.join()" in close and "if (ownsDevice)" in close and "WsgDevices.release(loop)" in close
+
+
+def test_decoder_close_control_matches_the_restatement():
+    """GpuFrameDecoder ends a session as InternalSession.exception/controlClose does
+    (InternalSession.java:804-848) — GENTLE: exception(closing cause) + close(); NONE:
+    the exception only, the next frame goes on; DEFAULT or any other exception:
+    quickClose() — for exceptions of the decoders behind it and of the handler's read,
+    and delivers the frames before a u64 length error (WsgBatcher.drain) before
+    available() throws it (FrameDecoder.java:388-394).  snf4j_amd/loop.py's
+    GpuFrameDecoder does the same, run against the reference by
+    tests/test_session_model.py (CPU batcher) and tests/test_gpu_session.py (GPU)."""
+    dec = _java("GpuFrameDecoder.java")
+    cc = _body(dec, "private boolean controlClose(Throwable t)", "void failBatch(Exception e)")
+    assert "t instanceof ICloseControllingException" in cc and "c.getClosingCause()" in cc
+    gentle = _body(cc, "case GENTLE:", "case NONE:")
+    assert "handler.exception(cause)" in gentle and "session.close()" in gentle and "return false" in gentle
+    none = _body(cc, "case NONE:", "default:")
+    assert "handler.exception(cause)" in none and "return true" in none and "close" not in none
+    tail = cc[cc.index("default:"):]
+    assert "t = cause" in tail and "handler.exception(t)" in tail and "session.quickClose()" in tail
+    down = _body(dec, "private boolean downstream(Frame frame", "private boolean controlClose(")
+    # the handler's read is inside the try: its exceptions end the session the same way
+    assert down.index("try {") < down.index("session.getHandler().read(o)") < down.index("catch (Exception e)")
+    assert "return controlClose(e)" in down
+    deliver = _body(dec, "void deliver(List<Frame> frames", "/** The decoders after")
+    assert "if (!downstream(f, chain))" in deliver
+    chk = _body(dec, "private int checked(ISession session, long r, int len)", "/**\n\t * FrameDecoder.decode")
+    assert chk.index("batcher.drain(this)") < chk.index("if (closed)") < chk.index("fail(session")
+    fail = _body(dec, "private void fail(ISession session", "/* ---- IEventDrivenCodec")
+    assert fail.index("writenf(new CloseFrame(") < fail.index("if (inAvailable)") < fail.index("controlClose(e)")
+    b = _java("WsgBatcher.java")
+    drain = _body(b, "synchronized void drain(GpuFrameDecoder d)", "/* ------------------------------------------------------------------ encode side */")
+    order = ["feedReads(n)", "Wsg.batcherFlushAsync(n.handle)", "while (!n.inflight.isEmpty())"]
+    pos = [drain.index(x) for x in order]
+    assert pos == sorted(pos), order
+    assert "collectOldest(n)" in drain[pos[-1]:]
+    loop = _read("snf4j_amd/loop.py")
+    for x in ("def _control_close(self, t)", "self.batcher.drain(self)", "kind == CloseType.NONE",
+              "s.quickClose()", "def drain(self, d: GpuFrameDecoder)"):
+        assert x in loop, x
