@@ -415,14 +415,23 @@ int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* s
 uint64_t wsg_batcher_ticket(wsg_batcher* b);
 int64_t wsg_batcher_await(wsg_batcher* b, uint64_t seen, int64_t timeout_ms);
 /* Size every pinned and device buffer of the three flush slots for flushes of up to
- * `max_wire` bytes and `max_frames` frames, so those flushes allocate nothing (the
- * stage chain's buffers, sized by what inflate and the aggregator produce, grow on
- * first use beyond this: the one documented exception).  wsg_batcher_alloc_count is
- * the number of pinned/device allocations all batchers of the process have made.
+ * `max_wire` bytes and `max_frames` frames, so those flushes allocate nothing (with
+ * stages, wsg_batcher_reserve_stages sizes theirs).  wsg_batcher_alloc_count is the
+ * number of pinned/device allocations all batchers and contexts of the process have
+ * made (batcher buffers and device workspaces).
  * Precondition: no flush in flight (it moves the slots' buffers, which a queued flush
  * still reads and writes): WSG_API_ERANGE otherwise, nothing changed. */
 int wsg_batcher_reserve(wsg_batcher* b, uint64_t max_wire, uint64_t max_frames);
 uint64_t wsg_batcher_alloc_count(void);
+/* With stages (call after wsg_batcher_set_stages and wsg_batcher_reserve): every stage
+ * buffer sized for flushes within the reserved wire/frame sizes whose stages deliver up
+ * to `max_out_bytes` bytes in up to `max_out_frames` frames (inflated or aggregated
+ * messages): the stage arena, the pinned output and its copy list, the stage lists
+ * uploaded and downloaded, the stage context's workspace.  Such flushes allocate
+ * nothing.  A flush beyond grows what it needs.  WSG_API_ERANGE with a flush in
+ * flight, WSG_API_EINVAL before set_stages.  Replaces nothing in the reference (its
+ * buffers come from the session allocator, IByteBufferAllocator.java:47-73). */
+int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t max_out_frames);
 /* The decoders after "ws-decoder" that a flush runs in the same device batch, in the
  * pipeline order the reference builds (DefaultWebSocketSessionConfig.java:276-281,
  * PerMessageDeflateExtension.java:316-326; a FrameAggregator the application puts

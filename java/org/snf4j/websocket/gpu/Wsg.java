@@ -112,6 +112,7 @@ final class Wsg {
 
 	/** wsg_batcher_reserve: flushes of up to maxWire bytes / maxFrames frames allocate nothing. */
 	static native int batcherReserve(long batcher, long maxWire, long maxFrames);
+	static native int batcherReserveStages(long batcher, long maxOutBytes, long maxOutFrames);
 
 	/** wsg_batcher_ticket: the last queued flush's ticket (1, 2, ...). */
 	static native long batcherTicket(long batcher);

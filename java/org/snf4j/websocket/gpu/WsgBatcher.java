@@ -138,6 +138,10 @@ public final class WsgBatcher {
 				throw new IllegalStateException("wsg_batcher_set_stages: " + Wsg.lastError(ctx));
 			if (Wsg.batcherReserve(handle, maxWireLen, maxFrames) != 0)
 				throw new IllegalStateException("wsg_batcher_reserve: " + Wsg.lastError(ctx));
+			// the stage chain's buffers too: inflated output up to STAGE_RATIO x the wire (more
+			// grows on demand), within the 2 GiB a flush's payload view may span
+			if (c.hasStages() && Wsg.batcherReserveStages(handle, maxStageLen(), maxFrames) != 0)
+				throw new IllegalStateException("wsg_batcher_reserve_stages: " + Wsg.lastError(ctx));
 			slots = new GpuFrameDecoder[maxSessions];
 		}
 
@@ -291,6 +295,13 @@ public final class WsgBatcher {
 			throw new IllegalStateException("wsg_reserve: " + Wsg.lastError(ctx));
 		completion = new Completion();
 		completion.start();
+	}
+
+	/** Inflated bytes a flush's stages are sized for, per wire byte (permessage-deflate's typical ratio). */
+	static final int STAGE_RATIO = 4;
+
+	private long maxStageLen() {
+		return Math.min(STAGE_RATIO * maxWireLen, Integer.MAX_VALUE - 16L * maxFrames - 32);
 	}
 
 	/* ------------------------------------------------------------------ decode side */

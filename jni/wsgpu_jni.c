@@ -299,6 +299,14 @@ JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherReserve(JNIEnv* e
     return wsg_batcher_reserve(BATCHER(b), (uint64_t)max_wire, (uint64_t)max_frames);
 }
 
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_batcherReserveStages(JNIEnv* env, jclass c, jlong b,
+                                                                             jlong max_out, jlong max_frames) {
+    (void)env;
+    (void)c;
+    if (max_out < 0 || max_frames < 0) return WSG_API_EINVAL;
+    return wsg_batcher_reserve_stages(BATCHER(b), (uint64_t)max_out, (uint64_t)max_frames);
+}
+
 /* the flush view as direct buffers: session_first, desc, payload, result (+ detail2) */
 static int batch_views(JNIEnv* env, const wsg_batch_view* pv, jobjectArray views, jlongArray counts) {
     wsg_batch_view v = *pv;

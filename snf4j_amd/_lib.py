@@ -154,6 +154,7 @@ def _load():
         "wsg_batcher_ticket": ([p], u64),
         "wsg_batcher_await": ([p, u64, i64], i64),
         "wsg_batcher_reserve": ([p, u64, u64], i32),
+        "wsg_batcher_reserve_stages": ([p, u64, u64], i32),
         "wsg_batcher_alloc_count": ([], u64),
         "wsg_enc_batcher_ticket": ([p], u64),
         "wsg_enc_batcher_await": ([p, u64, i64], i64),

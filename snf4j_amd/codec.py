@@ -515,6 +515,12 @@ class NativeBatcher:
         from ._lib import lib
         self._check(lib.wsg_batcher_reserve(self._h, int(max_wire), int(max_frames)))
 
+    def reserve_stages(self, max_out_bytes: int, max_out_frames: int):
+        """wsg_batcher_reserve_stages (after set_stages and reserve): flushes whose stages
+        deliver up to these sizes allocate nothing."""
+        from ._lib import lib
+        self._check(lib.wsg_batcher_reserve_stages(self._h, int(max_out_bytes), int(max_out_frames)))
+
     def wait_raw(self):
         """The oldest queued flush's results (wsg_batcher_wait), as flush_raw returns them."""
         import ctypes as C

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <atomic>
 #include <string>
 #include <vector>
 
@@ -14,6 +15,8 @@
 using namespace ws;
 
 namespace {
+
+std::atomic<uint64_t> g_ctx_allocs{0};  // device workspace allocations of every context
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_final",    "k_enc_len",  "k_enc_scan",
@@ -30,6 +33,7 @@ struct DevBuf {
     n = 0;
     size_t want = bytes < 256 ? 256 : bytes;
     hipError_t e = hipMalloc(&p, want);
+    g_ctx_allocs.fetch_add(1, std::memory_order_relaxed);
     if (e != hipSuccess) return e;
     n = want;
     return fill >= 0 ? hipMemsetAsync(p, fill, want, s) : hipSuccess;
@@ -417,6 +421,30 @@ int wsg_inflate_split_count(wsg_ctx* c, uint64_t* count) {
   HIP_TRY(c, hipStreamSynchronize(c->stream));
   return WSG_API_OK;
 }
+
+static int ensure_agg_ws(wsg_ctx* c, uint64_t F, uint32_t n_sessions, uint64_t agg_cap);
+
+}  // extern "C" (reopened below)
+
+namespace ws {
+uint64_t ctx_alloc_count() { return g_ctx_allocs.load(); }
+
+// The stage context's workspace for a flush's stages (wsg_batcher_reserve_stages):
+// inflate over `payload_len` arena bytes, the validator over the same, the aggregator
+// into `agg_cap` bytes, `max_frames` frames and `max_sessions` sessions each.
+int ctx_reserve_stages(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t payload_len,
+                       uint64_t agg_cap) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  int rc = wsg_reserve_inflate(c, max_frames, max_sessions, payload_len);
+  if (!rc) rc = ensure_decode_ws(c, max_frames, max_sessions, payload_len);
+  if (rc) return rc;
+  HIP_TRY(c, c->v_desc.ensure((max_frames + 1) * sizeof(wsg_frame_desc)));
+  return ensure_agg_ws(c, max_frames ? max_frames : 1, max_sessions, agg_cap);
+}
+}  // namespace ws
+
+extern "C" {
 
 int wsg_reserve(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t max_wire_len) {
   if (!c) return WSG_API_EINVAL;
@@ -853,6 +881,19 @@ int wsg_encode_batch_host(wsg_ctx* c, int client_mode, const uint8_t* payload, u
   return WSG_API_OK;
 }
 
+// the aggregator's workspace for F frames, S sessions and agg_cap output bytes
+static int ensure_agg_ws(wsg_ctx* c, uint64_t F, uint32_t n_sessions, uint64_t agg_cap) {
+  const uint64_t nblk = (F + ABLOCK - 1) / ABLOCK;
+  HIP_TRY(c, c->a_code.ensure(F * 2 * sizeof(uint32_t)));
+  HIP_TRY(c, c->a_last.ensure(F * 2 * sizeof(int32_t)));
+  HIP_TRY(c, c->a_pl.ensure(F * sizeof(uint64_t)));
+  HIP_TRY(c, c->a_cl.ensure(F * sizeof(uint64_t) + sizeof(uint64_t)));
+  HIP_TRY(c, c->a_blk.ensure(nblk * (4 * sizeof(uint64_t) + 2 * sizeof(int32_t))));
+  HIP_TRY(c, c->a_sess_err.ensure((uint64_t)(n_sessions ? n_sessions : 1) * sizeof(uint64_t), 0xff, c->stream));
+  HIP_TRY(c, c->a_pieces.ensure((agg_cap / PIECE + 2 * F + 2 + 1) * sizeof(PieceDesc)));
+  return WSG_API_OK;
+}
+
 int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg_frame_desc* desc,
                                uint64_t n_frames, const uint32_t* session_first, uint32_t n_sessions,
                                const wsg_session_result* dec_result, const uint8_t* payload, uint64_t payload_len,
@@ -885,13 +926,10 @@ int wsg_aggregate_batch_device(wsg_ctx* c, int64_t max_aggregated_len, const wsg
   // agg_cap number at most agg_cap / 1 KiB + 2 per member before them
   a.n_pieces = agg_cap / PIECE + 2 * F + 2;
   a.fold_max = std::min(c->agg_fold, agg_fold_bound());
-  HIP_TRY(c, c->a_code.ensure(F * 2 * sizeof(uint32_t)));
-  HIP_TRY(c, c->a_last.ensure(F * 2 * sizeof(int32_t)));
-  HIP_TRY(c, c->a_pl.ensure(F * sizeof(uint64_t)));
-  HIP_TRY(c, c->a_cl.ensure(F * sizeof(uint64_t) + sizeof(uint64_t)));
-  HIP_TRY(c, c->a_blk.ensure(nblk * (4 * sizeof(uint64_t) + 2 * sizeof(int32_t))));
-  HIP_TRY(c, c->a_sess_err.ensure((uint64_t)n_sessions * sizeof(uint64_t), 0xff, c->stream));
-  HIP_TRY(c, c->a_pieces.ensure((a.n_pieces + 1) * sizeof(PieceDesc)));
+  {
+    const int rc = ensure_agg_ws(c, F, n_sessions, agg_cap);
+    if (rc) return rc;
+  }
   a.code = (uint32_t*)c->a_code.p;
   a.sess = a.code + F;
   a.last = (int32_t*)c->a_last.p;

@@ -33,6 +33,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "wsgpu_internal.h"
@@ -275,7 +276,8 @@ constexpr uint32_t COPY_MAX = 65536;
 
 // One workgroup per copy.  Output slots are 16-B aligned; a source is 16-B aligned when
 // it is a decoder payload slot, byte-aligned when it is inflated output (messages back
-// to back), so the widest access both sides allow is used.
+// to back): either way the host sees 16-B stores (PCIe writes of whole 16-B chunks; the
+// 4-B stores of the unaligned case ran at 31.6 GB/s, profiles/r04_stageprof_final.txt).
 constexpr uint32_t GATHER_GROUPS = 12;  // workgroups of the output gather: enough to fill PCIe, few enough
                                          // that the next flush's small downloads still get a share of it
 
@@ -292,6 +294,31 @@ __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ 
     done = c.len & ~15u;
     for (uint32_t i = 16 * t; i < done; i += 16 * 256)
       __builtin_nontemporal_store(__builtin_nontemporal_load((const ws_u32x4*)(s + i)), (ws_u32x4*)(d + i));
+  } else if ((c.dst & 15) == 0) {
+    // dst aligned, src not (inflated messages lie back to back): each 16-B store is
+    // assembled from the two aligned source words around it (v_alignbyte over the
+    // word pair; the dword shift is uniform over the copy).  The second word may lie
+    // up to 15 B past the source: inside the arena's 64-B tail, and never used.
+    done = c.len & ~15u;
+    const uint32_t sh = (uint32_t)(c.src & 15), q = sh >> 2, r = sh & 3;
+    const ws_u32x4* s16 = (const ws_u32x4*)(s - sh);
+    auto run = [&](auto qc) {
+      constexpr uint32_t Q = decltype(qc)::value;
+      for (uint32_t i = 16 * t; i < done; i += 16 * 256) {
+        const ws_u32x4 x = __builtin_nontemporal_load(s16 + i / 16), y = __builtin_nontemporal_load(s16 + i / 16 + 1);
+        const uint32_t w[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+        ws_u32x4 o;
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) o[j] = __builtin_amdgcn_alignbyte(w[j + Q + 1], w[j + Q], r);
+        __builtin_nontemporal_store(o, (ws_u32x4*)(d + i));
+      }
+    };
+    switch (q) {
+      case 0: run(std::integral_constant<uint32_t, 0>{}); break;
+      case 1: run(std::integral_constant<uint32_t, 1>{}); break;
+      case 2: run(std::integral_constant<uint32_t, 2>{}); break;
+      default: run(std::integral_constant<uint32_t, 3>{}); break;
+    }
   } else if ((al & 3) == 0) {
     done = c.len & ~3u;
     for (uint32_t i = 4 * t; i < done; i += 4 * 256) *(uint32_t*)(d + i) = *(const uint32_t*)(s + i);
@@ -323,6 +350,44 @@ __global__ __launch_bounds__(256) void k_stage_reset(const uint32_t* __restrict_
     vstate[sid] = wsg_session_state{};
     astate[sid] = wsg_agg_state{};
   }
+}
+
+// The validator's input, made from inflate's output on the device (no host hop between
+// the two stages): output slot k of session s holds a frame the validator must see
+// when it is one of the n_delivered frames after the session's replayed ones (which
+// stage_inflate keeps); its payload offset moves into the arena (inflated bytes lie at
+// `ipos`, passed-through ones where the decoder left them).  Every other slot — a
+// replayed frame, a frame after the session's inflate error, every frame of a session
+// whose output region overflowed (run again) — becomes an empty final PING, a frame
+// FrameUtf8Validator passes without touching its context (FrameUtf8Validator.java:
+// 59-98), so the validator's state and its failure index (minus nheld) stay exact.
+__global__ __launch_bounds__(256) void k_stage_vprep(const wsg_frame_desc* __restrict__ odesc,
+                                                     const uint32_t* __restrict__ sf,
+                                                     const uint32_t* __restrict__ nheld,
+                                                     const wsg_session_result* __restrict__ ores, uint64_t ipos,
+                                                     uint32_t S, uint64_t F, wsg_frame_desc* __restrict__ vdesc) {
+  const uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (k >= F) return;
+  uint32_t lo = 0, hi = S;  // the session owning slot k: sf[s] <= k < sf[s + 1]
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) / 2;
+    if (sf[mid] <= k) lo = mid;
+    else hi = mid;
+  }
+  const uint32_t s = lo;
+  const wsg_session_result r = ores[s];
+  const uint64_t first = (uint64_t)sf[s] + nheld[s];
+  wsg_frame_desc d;
+  if (k >= first && k - first < r.n_delivered && r.error != WSG_E_INFLATE_CAPACITY) {
+    d = odesc[k];
+    if (d.flags & WSG_DESC_INFLATED) d.payload_off += ipos;
+    d.flags &= 0xf0u | 0x80u;
+  } else {
+    d = wsg_frame_desc{};
+    d.opcode = WSG_OP_PING;
+    d.flags = 0x80u;
+  }
+  vdesc[k] = d;
 }
 
 }  // namespace
@@ -417,13 +482,15 @@ struct wsg_batcher {
   DBuf* ar = nullptr;  // the stage arena at hand: its flush's dpay (decoded payloads | held frames |
                        // inflated | aggregated)
   DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot;
-  PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot;  // stage results downloaded
+  DBuf d_nheld, d_vdesc, d_vres;        // the validator's input made on the device, its results
+  PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot, h_vres;  // stage results downloaded
   PinnedBuf h_pend;                     // aggregator bytes held for the next flush, downloaded
   DBuf d_pend;
   hipStream_t s_dl = nullptr;           // downloads of stage outputs
   StageOut* out = nullptr;              // the output the stage run at hand writes
   uint64_t tickets = 0;                 // flushes queued so far (flush t's ticket is t)
   std::shared_ptr<Notify> notify = std::make_shared<Notify>();
+  uint64_t res_wire = 0, res_frames = 0;  // the sizes wsg_batcher_reserve was given
 };
 
 static int bset(wsg_batcher* b, int code, const char* msg) {
@@ -497,6 +564,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
   uint64_t ipos = al16(hpos);
   std::vector<uint32_t> nheld(S, 0);
   while (!todo.empty()) {
+    std::fill(nheld.begin(), nheld.end(), 0u);  // (this attempt's sessions set theirs)
     // this attempt's input: the todo sessions' frames; every session takes part (the
     // carry is indexed by session), the others with no frames
     StageList x;
@@ -542,12 +610,35 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
                                       (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
                                       (uint32_t*)b->d_rf.p);
     if (rc) return bset(b, rc, wsg_last_error(b->sctx));
+    // FrameUtf8Validator right behind it on the device (PerMessageDeflateExtension.java:
+    // 316-326): its input made from inflate's output by k_stage_vprep, no host hop
+    const bool validate = b->stages.validate != 0;
+    if (validate) {
+      B_TRY(b, upload(b->d_nheld, nheld, st));
+      B_TRY(b, b->d_vdesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+      B_TRY(b, b->d_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+      if (F) {
+        hipLaunchKernelGGL(k_stage_vprep, dim3((uint32_t)((F + 255) / 256)), dim3(256), 0, st,
+                           (const wsg_frame_desc*)b->d_odesc.p, (const uint32_t*)b->d_sf.p,
+                           (const uint32_t*)b->d_nheld.p, (const wsg_session_result*)b->d_ores.p, ipos, S, F,
+                           (wsg_frame_desc*)b->d_vdesc.p);
+        B_TRY(b, hipGetLastError());
+      }
+      rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_vdesc.p, F, (const uint32_t*)b->d_sf.p, S,
+                                     b->ar->p, ipos + oo[S], (wsg_session_state*)b->d_vstate.p,
+                                     (wsg_session_result*)b->d_vres.p);
+      if (rc) return bset(b, rc, wsg_last_error(b->sctx));
+    }
     B_TRY(b, b->h_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
     B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
     B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
     if (F) B_TRY(b, hipMemcpyAsync(b->h_odesc.p, b->d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, st));
     B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
     B_TRY(b, hipMemcpyAsync(b->h_rf.p, b->d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (validate) {
+      B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+      B_TRY(b, hipMemcpyAsync(b->h_vres.p, b->d_vres.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
+    }
     {
       SP(2);
       B_TRY(b, hipStreamSynchronize(st));
@@ -555,6 +646,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     const wsg_frame_desc* odesc = (const wsg_frame_desc*)b->h_odesc.p;
     const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
     const uint32_t* rf = (const uint32_t*)b->h_rf.p;
+    const wsg_session_result* vr = validate ? (const wsg_session_result*)b->h_vres.p : nullptr;
     std::vector<uint32_t> retry;
     struct Held {
       uint32_t s;
@@ -581,8 +673,14 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
       od_n[s] = j;
       std::vector<wsg_frame_desc> nhd;
       uint64_t nb = 0;
+      if (r[s].error) stage_fail(b, s, r[s]);
+      if (vr && vr[s].error) {  // the validator failed an earlier frame: its result is the session's
+        const uint32_t v = vr[s].n_delivered >= nheld[s] ? vr[s].n_delivered - nheld[s] : 0u;
+        od_n[s] = std::min(od_n[s], v);
+        wsg_session_result e = vr[s];
+        stage_fail(b, s, e);
+      }
       if (r[s].error) {
-        stage_fail(b, s, r[s]);
       } else if (rf[s] != 0xFFFFFFFFu) {  // a message left open: its frames go again with the next batch
         for (uint32_t k = x.sf[s] + rf[s]; k < x.sf[s + 1]; ++k) {
           wsg_frame_desc d = x.desc[k];
@@ -615,7 +713,7 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     k += od_n[s];
   }
   cur.sf[S] = (uint32_t)k;
-  if (in_order) {
+  if (in_order && k == od.size()) {
     cur.desc.swap(od);
   } else {
     cur.desc.resize(k);
@@ -623,33 +721,6 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
       std::copy(od.begin() + od_at[s], od.begin() + od_at[s] + od_n[s], cur.desc.begin() + cur.sf[s]);
   }
   used = ipos;
-  return WSG_API_OK;
-}
-
-// FrameUtf8Validator over `cur` (FrameUtf8Validator.java:59-98), on the device: the
-// frames a session passes before its first failure go on.
-static int stage_validate(wsg_batcher* b, StageList& cur, uint64_t used) {
-  SP(4);
-  const uint32_t S = b->n;
-  hipStream_t st = ws::ctx_stream(b->sctx);
-  B_TRY(b, upload(b->d_desc, cur.desc, st));
-  B_TRY(b, upload(b->d_sf, cur.sf, st));
-  B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
-  int rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_desc.p, cur.desc.size(),
-                                     (const uint32_t*)b->d_sf.p, S, b->ar->p, used,
-                                     (wsg_session_state*)b->d_vstate.p, (wsg_session_result*)b->d_ores.p);
-  if (rc) return bset(b, rc, wsg_last_error(b->sctx));
-  B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
-  B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
-  {
-    SP(15);
-    B_TRY(b, hipStreamSynchronize(st));
-  }
-  const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
-  for (uint32_t s = 0; s < S; ++s) {
-    cur.n_ok[s] = std::min(cur.n_ok[s], r[s].n_delivered);
-    if (r[s].error) stage_fail(b, s, r[s]);
-  }
   return WSG_API_OK;
 }
 
@@ -821,9 +892,8 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   uint64_t used = al16(f.pcap);
   if (f.pcap) B_TRY(b, hipStreamWaitEvent(st, f.dpay_done, 0));
   int rc;
-  if (b->stages.inflate) {
+  if (b->stages.inflate) {  // (the validator runs inside, on the device)
     if ((rc = stage_inflate(b, f, cur, used))) return rc;
-    if (b->stages.validate && (rc = stage_validate(b, cur, used))) return rc;
   } else {
     B_TRY(b, b->ar->grow_keep(used + 64, f.pcap, st));
   }
@@ -922,9 +992,10 @@ int wsg_batcher_close(wsg_batcher* b) {
   }
   b->st.release();
   DBuf* dbufs[] = {&b->d_pend, &b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->d_sf, &b->d_desc,
-                   &b->d_odesc, &b->d_res, &b->d_ores, &b->d_rf, &b->d_ooff, &b->d_tot};
+                   &b->d_odesc, &b->d_res, &b->d_ores, &b->d_rf, &b->d_ooff, &b->d_tot, &b->d_nheld, &b->d_vdesc,
+                   &b->d_vres};
   for (DBuf* d : dbufs) d->release();
-  PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot, &b->h_pend};
+  PinnedBuf* hbufs[] = {&b->h_odesc, &b->h_ores, &b->h_rf, &b->h_astate, &b->h_tot, &b->h_pend, &b->h_vres};
   for (PinnedBuf* p : hbufs) p->release();
   if (b->s_dl) {
     (void)hipStreamSynchronize(b->s_dl);
@@ -1388,6 +1459,8 @@ int wsg_batcher_reserve(wsg_batcher* b, uint64_t max_wire, uint64_t max_frames) 
   if (!b->q.empty()) return bset(b, WSG_API_ERANGE, "wsg_batcher_reserve: flushes in flight (wait for them first)");
   const uint32_t S = b->n;
   const uint64_t pcap = max_wire + 16 * max_frames + 16;
+  b->res_wire = std::max(b->res_wire, max_wire);
+  b->res_frames = std::max(b->res_frames, max_frames);
   B_TRY(b, b->st.ensure((S + 1) * sizeof(wsg_session_state)));
   for (FlushSlot& f : b->fs) {
     if (f.arena.n < max_wire + 64) B_TRY(b, arena_grow(f, max_wire + 64));
@@ -1403,6 +1476,71 @@ int wsg_batcher_reserve(wsg_batcher* b, uint64_t max_wire, uint64_t max_frames) 
       if (!f.dpay_done) B_TRY(b, hipEventCreateWithFlags(&f.dpay_done, hipEventDisableTiming));
     }
   }
+  return WSG_API_OK;
+}
+
+// The stage chain's buffers (wsg_batcher_set_stages) for flushes within the sizes of
+// wsg_batcher_reserve whose stages produce up to max_out_bytes bytes in up to
+// max_out_frames frames: the stage arena of every slot (decoded payloads | held frames |
+// inflate's per-session output regions | aggregated bytes), the pinned output and its
+// copy list, the descriptor and result lists each stage uploads and downloads, and the
+// stage context's workspace.  A flush that stays within them allocates nothing; one
+// beyond grows what it needs (an inflate that overflows its region is run again with a
+// larger one).
+int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t max_out_frames) {
+  if (!b) return WSG_API_EINVAL;
+  if (!b->has_stages || !b->sctx) return bset(b, WSG_API_EINVAL, "wsg_batcher_reserve_stages: set the stages first");
+  if (!b->q.empty()) return bset(b, WSG_API_ERANGE, "wsg_batcher_reserve_stages: flushes in flight (wait for them first)");
+  const uint64_t S = b->n, W = b->res_wire, Fi = b->res_frames;
+  const uint64_t Fo = std::max(max_out_frames, Fi);
+  const uint64_t F = Fi + Fo + S + 1;               // a stage's frames: this flush's, held ones, one a session
+  const uint64_t pcap = W + 16 * Fi + 16;            // the decoded payloads (flush_async's region)
+  const uint64_t held = al16(W) + 16 * S;            // compressed frames of messages left open
+  const uint64_t in_len = al16(pcap) + held;         // inflate's input: payloads and held frames
+  const uint64_t infl = S * (4096 + 16) + 8 * (in_len + 4 * F);  // stage_inflate's per-session regions
+  const uint64_t maxo = std::max(max_out_bytes, pcap);
+  const uint64_t agg = al16(maxo + 16);
+  const uint64_t arena = in_len + infl + agg + 256;
+  const uint64_t out = maxo + 16 * Fo + 32;          // the handler's bytes, a 16-B slot a frame
+  const uint64_t copies = maxo / COPY_MAX + Fo + S + 2;
+  hipStream_t st = ws::ctx_stream(b->sctx);
+  for (FlushSlot& f : b->fs) {
+    B_TRY(b, f.dpay.grow_keep(arena, 0, st));
+    B_TRY(b, f.so.pay.ensure(out));
+    B_TRY(b, f.so.d_copy.ensure((copies + 1) * sizeof(StageCopy)));
+    B_TRY(b, f.so.d_copy.up.ensure((copies + 1) * sizeof(StageCopy)));
+    if (!f.dpay_done) B_TRY(b, hipEventCreateWithFlags(&f.dpay_done, hipEventDisableTiming));
+    if (!f.so.gathered) B_TRY(b, hipEventCreateWithFlags(&f.so.gathered, hipEventDisableTiming));
+    if (!f.so.downloaded) B_TRY(b, hipEventCreateWithFlags(&f.so.downloaded, hipEventDisableTiming));
+  }
+  if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
+  struct Up {
+    DBuf* d;
+    uint64_t bytes;
+  };
+  const Up ups[] = {{&b->d_desc, (F + 1) * sizeof(wsg_frame_desc)}, {&b->d_sf, (S + 2) * sizeof(uint32_t)},
+                    {&b->d_ooff, (S + 2) * sizeof(uint64_t)},      {&b->d_res, (S + 1) * sizeof(wsg_session_result)},
+                    {&b->d_resets, (S + 1) * sizeof(uint32_t)},    {&b->d_pend, (copies + 1) * sizeof(StageCopy)},
+                    {&b->d_nheld, (S + 1) * sizeof(uint32_t)}};
+  for (const Up& u : ups) {
+    B_TRY(b, u.d->ensure(u.bytes));
+    B_TRY(b, u.d->up.ensure(u.bytes));
+  }
+  B_TRY(b, b->d_odesc.ensure((F + S + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
+  B_TRY(b, b->d_tot.ensure(sizeof(uint64_t)));
+  B_TRY(b, b->d_vdesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, b->d_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->h_odesc.ensure((F + S + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
+  B_TRY(b, b->h_astate.ensure((S + 1) * sizeof(wsg_agg_state)));
+  B_TRY(b, b->h_pend.ensure(maxo + 16 * S + 32));
+  const int rc = ws::ctx_reserve_stages(b->sctx, F, (uint32_t)S, in_len + infl, agg);
+  if (rc) return bset(b, rc, wsg_last_error(b->sctx));
+  B_TRY(b, hipStreamSynchronize(st));
   return WSG_API_OK;
 }
 
@@ -1774,7 +1912,7 @@ int wsg_enc_batcher_reserve(wsg_enc_batcher* b, uint64_t max_frames, uint64_t ma
   return WSG_API_OK;
 }
 
-uint64_t wsg_batcher_alloc_count(void) { return g_batcher_allocs.load(); }
+uint64_t wsg_batcher_alloc_count(void) { return g_batcher_allocs.load() + ws::ctx_alloc_count(); }
 
 int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid) {
   if (!b || sid >= b->n) return WSG_API_EINVAL;

@@ -240,6 +240,9 @@ hipStream_t ctx_out_stream(wsg_ctx* c);
 void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src);  // where ctx_record_out records (the download stream)
 int ctx_device(wsg_ctx* c);
 uint8_t* ctx_async_payload(wsg_ctx* c);
+uint64_t ctx_alloc_count();  // device workspace allocations of every context so far
+int ctx_reserve_stages(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t payload_len,
+                       uint64_t agg_cap);
 
 void launch_parse(const DecodeArgs& a, hipStream_t s);
 void launch_scan(const DecodeArgs& a, hipStream_t s);

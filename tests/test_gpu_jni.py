@@ -68,11 +68,15 @@ def _collect(jni, views, counts, sids):
 class JavaDecodeLoop:
     """The decode side of WsgBatcher, call for call through the JNI natives."""
 
-    def __init__(self, jni, ctx, n, max_wire, max_frames):
+    def __init__(self, jni, ctx, n, max_wire, max_frames, inflate=False, max_out=0):
         self.jni, self.n = jni, n
-        self.b = jni.call("batcherOpen", ctx, 0, 0, 65536, 1, n)
+        self.b = jni.call("batcherOpen", ctx, 0, 1 if inflate else 0, 65536, 1, n)
         assert self.b
+        if inflate:  # WsgBatcher.Native: set_stages, reserve, then the stages' reserve
+            assert jni.call("batcherSetStages", self.b, 1, 0, 1, 0, 0) == OK
         assert jni.call("batcherReserve", self.b, max_wire, max_frames) == OK
+        if inflate:
+            assert jni.call("batcherReserveStages", self.b, max_out, max_frames) == OK
         self.views = jni.objs_empty(5)
         self.counts = jni.longs(2)
         self.inflight = []  # tickets, oldest first
@@ -198,6 +202,48 @@ def test_jni_reserved_batcher_flushes_allocate_nothing(jni, ctx):
         res = loop.collect_oldest(range(n))
         assert all(len(fr) == 20 and e is None for fr, e in res.values())
     assert lib.wsg_batcher_alloc_count() == a0
+    loop.close()
+
+
+def test_jni_reserved_stage_batcher_flushes_allocate_nothing(jni, ctx):
+    """The same with the stage chain (permessage-deflate decoder -> ws-utf8-validator,
+    PerMessageDeflateExtension.java:316-326) after batcherReserveStages: flushes within
+    the reserved sizes make no pinned or device allocation — the batcher's buffers and
+    the contexts' workspaces (wsg_batcher_alloc_count counts both) — and every session
+    gets its messages inflated (compared with the plaintext)."""
+    from snf4j_amd._lib import lib
+    n, msgs = 16, 24
+    rng = random.Random(3)
+    nrng = np.random.default_rng(3)
+    plain = [[wsgen.rand_text(nrng, int(nrng.integers(200, 3000))) for _ in range(msgs)] for _ in range(n)]
+    wires = []
+    for s in range(n):
+        fr = wsgen.pm_deflate_encode([(1, True, 0, p) for p in plain[s]])
+        wires.append(b"".join(wsgen.build_frame(op, fin, rsv, p, True, (9, 8, 7, 6)) for op, fin, rsv, p in fr))
+    loop = JavaDecodeLoop(jni, ctx, n, max_wire=1 << 20, max_frames=4096, inflate=True, max_out=8 << 20)
+    got = [[] for _ in range(n)]
+    pos = [0] * n
+    it = 0
+    a0 = None
+    while any(pos[s] < len(wires[s]) for s in range(n)):
+        if it == 2:
+            a0 = lib.wsg_batcher_alloc_count()
+        reads = []
+        for s in range(n):
+            if pos[s] < len(wires[s]):
+                c = rng.randrange(500, 6000)
+                reads.append((s, wires[s][pos[s]:pos[s] + c]))
+                pos[s] += c
+        loop.feed(rng, reads)
+        loop.flush_async()
+        for s, (fr, e) in loop.collect_oldest(range(n)).items():
+            assert e is None, (s, e)
+            got[s] += [f[3] for f in fr]
+        it += 1
+    assert it > 4 and a0 is not None
+    assert lib.wsg_batcher_alloc_count() == a0
+    for s in range(n):
+        assert got[s] == plain[s], s
     loop.close()
 
 
