@@ -925,6 +925,14 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
     apply_tuning(pctx)
     nb = snf4j_amd.NativeBatcher(n_s, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=pctx)
     nb.set_stages(inflate=True, noContext=False, validate=True)
+    # sized once, as WsgBatcher does (wsg_batcher_reserve, then _reserve_stages with its
+    # STAGE_RATIO of 4 inflated bytes a wire byte): a round's reads plus carried partial
+    # frames (messages are <= 4 KiB + header compressed); frames: a generous bound of one
+    # a 64 B of a read (a flush beyond it would grow its buffers, as WsgBatcher's would)
+    max_wire = max(int(lens.sum()) for _, _, lens in rounds) + n_s * (msg_bytes + 64)
+    max_frames = n_s * (chunk // 64 + 2)
+    nb.reserve(max_wire, max_frames)
+    nb.reserve_stages(4 * max_wire, max_frames)
     times = []
     for rep in range(W + K):
         for s in range(n_s):
@@ -1250,10 +1258,16 @@ def e2e_loop_line(pctx, rounds, wire_bytes, F, n_s):
         got["wire"] += w
         got["frames"] += len(desc)
 
+    # WsgBatcher reserves its buffers at construction (wsg_batcher_reserve with its
+    # maxWireLen / maxFrames): a flush's wire is an iteration's reads plus the partial
+    # frames carried into it, its frames at most one a FLEN of that
+    flen = wire_bytes // F
+    max_wire = max(int(lens.sum()) for _, _, lens in rounds) + n_s * flen
+    max_frames = max_wire // flen + n_s
     best = None
-    for rnd in range(3):  # round 0 sizes the pinned buffers; the best of two timed rounds
+    for rnd in range(3):  # round 0 warms up; the best of two timed rounds
         loop = SelectorLoop()
-        lb = LoopBatcher(loop, n_s, deliver, ctx=pctx, raw=True)
+        lb = LoopBatcher(loop, n_s, deliver, ctx=pctx, raw=True, max_wire=max_wire, max_frames=max_frames)
         got["wire"] = got["frames"] = 0
         t0 = time.perf_counter()
         for sids, ptrs, lens in rounds:

@@ -806,8 +806,11 @@ class DecoderBatcher(LoopBatcher):
         super().enqueue(d.sid, data.peek())
         session.release(data)  # (Java releases it once the flush has fed it; the copy is taken here)
 
-    def drain(self, d: GpuFrameDecoder):
-        """WsgBatcher.drain: the iteration's reads fed and flushed, every flush collected."""
+    def drain(self, d: GpuFrameDecoder | None = None):
+        """WsgBatcher.drain: the iteration's reads fed and flushed, every flush collected
+        (with no decoder: LoopBatcher.drain, what close() does)."""
+        if d is None:
+            return super().drain()
         fed = bool(self._sids)
         if fed:
             ids, data = self._sids, self._data

@@ -212,5 +212,5 @@ def test_decoder_close_control_matches_the_restatement():
     assert "collectOldest(n)" in drain[pos[-1]:]
     loop = _read("snf4j_amd/loop.py")
     for x in ("def _control_close(self, t)", "self.batcher.drain(self)", "kind == CloseType.NONE",
-              "s.quickClose()", "def drain(self, d: GpuFrameDecoder)"):
+              "s.quickClose()", "def drain(self, d: GpuFrameDecoder | None = None)"):
         assert x in loop, x
