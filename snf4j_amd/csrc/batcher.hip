@@ -427,6 +427,23 @@ struct StageOut {
   bool staged = false;  // computed, download queued (wsg_batcher_wait collects it)
 };
 
+// A flush's stage chain between its start and its collection (stage_begin ->
+// stage_compute): the stage input, and the inflate attempt in flight.
+struct InflJob {
+  bool active = false;               // begun: the input built (and the inflate launched)
+  StageList cur;                     // the stage input, then (after inflate) its output
+  uint64_t used = 0;                 // the arena's extent so far
+  StageList x;                       // the inflate attempt in flight
+  std::vector<uint32_t> todo, nheld;
+  std::vector<uint64_t> cap, held_at, oo;
+  uint64_t ipos = 0;
+  bool validate = false;
+  std::vector<wsg_frame_desc> od;    // output frames, a session's contiguous at od_at[s]
+  std::vector<uint64_t> od_at;
+  std::vector<uint32_t> od_n;
+  bool in_order = true;              // (a session re-run for capacity comes after the others)
+};
+
 // One flush's pinned staging and results (two alternate: a flush can be in flight
 // while the next one gathers).
 struct HostErr {
@@ -447,6 +464,7 @@ struct FlushSlot {
   uint64_t pcap = 0;                      //   (their region's size)
   hipEvent_t dpay_done = nullptr;         //   after their copy (the stage stream waits for it)
   StageOut so;                            // the stages' output
+  InflJob ij;                             // the stage chain begun (stage_begin)
   uint64_t F = 0, W = 0;
   std::vector<HostErr> host_err;  // header errors found on the host after this batch's frames
   std::vector<uint32_t> resets;   // slots given to a new session while this batch was in flight
@@ -526,127 +544,160 @@ static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
   return hipMemcpyAsync(d.p, d.up.p, bytes, hipMemcpyHostToDevice, s);
 }
 
-// PerMessageDeflateDecoder over `cur` (PerMessageDeflateDecoder.java:68-105), on the
-// device: each session's frames after the frames of a message it left open; the
-// inflated bytes go to the arena after `used`.  A session whose output region
-// overflows is run again with a larger one (nothing of it was committed).
-static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t& used) {
+// PerMessageDeflateDecoder over a flush's frames (PerMessageDeflateDecoder.java:68-105),
+// on the device, with FrameUtf8Validator behind it: each session's frames after the
+// frames of a message it left open; the inflated bytes go to the arena after the
+// decoded payloads and the held frames.  Launched by infl_launch (uploads, kernels,
+// result downloads: no host wait), collected by infl_collect (the wait, the results,
+// and a session whose output region overflowed run again with a larger one — nothing
+// of it was committed).  Between the two the caller feeds the next reads: the inflate
+// runs meanwhile.
+
+// this attempt's input: the todo sessions' frames; every session takes part (the carry
+// is indexed by session), the others with no frames
+static int infl_launch(wsg_batcher* b, FlushSlot& f) {
+  SP(13);
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
-  std::vector<wsg_frame_desc> od;  // the sessions' output frames, a session's contiguous at od_at[s]
-  std::vector<uint64_t> od_at(S, 0);
-  std::vector<uint32_t> od_n(S, 0);
-  bool in_order = true;            // (a session re-run for capacity comes after the others)
-  std::vector<uint32_t> todo;
-  std::vector<uint64_t> cap(S, 0), held_at(S, 0);
-  // the held frames' bytes go after the decoded payloads
-  uint64_t hpos = used;
-  for (uint32_t s = 0; s < S; ++s) {
-    const StageSess& h = b->ss[s];
-    uint64_t c = 0;
-    if (!h.held_desc.empty()) {
-      held_at[s] = hpos;
-      hpos = al16(hpos + h.held_bytes.size());
-      for (const wsg_frame_desc& hd : h.held_desc) c += hd.payload_len + 4;
-    }
-    for (uint32_t k = cur.sf[s]; k < cur.sf[s + 1]; ++k) c += cur.desc[k].payload_len + 4;
-    if (h.held_desc.empty() && cur.sf[s + 1] == cur.sf[s]) continue;
-    todo.push_back(s);
-    cap[s] = al16(4096 + 8 * c);
-  }
-  B_TRY(b, b->ar->grow_keep(hpos + 64, f.pcap, st));
-  for (uint32_t s = 0; s < S; ++s) {
-    const StageSess& h = b->ss[s];
-    if (!h.held_bytes.empty())
-      B_TRY(b, hipMemcpyAsync(b->ar->p + held_at[s], h.held_bytes.data(), h.held_bytes.size(),
-                              hipMemcpyHostToDevice, st));
-  }
-  uint64_t ipos = al16(hpos);
-  std::vector<uint32_t> nheld(S, 0);
-  while (!todo.empty()) {
-    std::fill(nheld.begin(), nheld.end(), 0u);  // (this attempt's sessions set theirs)
-    // this attempt's input: the todo sessions' frames; every session takes part (the
-    // carry is indexed by session), the others with no frames
-    StageList x;
-    x.sf.assign(S + 1, 0);
-    std::vector<uint64_t> oo(S + 1, 0);
-    size_t ti = 0;
-    {
+  InflJob& j = f.ij;
+  StageList& x = j.x;
+  x.sf.assign(S + 1, 0);
+  x.desc.clear();
+  j.oo.assign(S + 1, 0);
+  std::fill(j.nheld.begin(), j.nheld.end(), 0u);  // (this attempt's sessions set theirs)
+  size_t ti = 0;
+  {
     SP(1);
     for (uint32_t s = 0; s < S; ++s) {
       x.sf[s] = (uint32_t)x.desc.size();
-      const bool in = ti < todo.size() && todo[ti] == s;
-      oo[s + 1] = oo[s] + (in ? cap[s] : 0);
+      const bool in = ti < j.todo.size() && j.todo[ti] == s;
+      j.oo[s + 1] = j.oo[s] + (in ? j.cap[s] : 0);
       if (!in) continue;
       ++ti;
       const StageSess& h = b->ss[s];
       for (const wsg_frame_desc& hd : h.held_desc) {
         wsg_frame_desc d = hd;
         d.flags |= WSG_DESC_REPLAY;
-        d.payload_off += held_at[s];
+        d.payload_off += j.held_at[s];
         x.desc.push_back(d);
       }
-      nheld[s] = (uint32_t)h.held_desc.size();
-      for (uint32_t k = cur.sf[s]; k < cur.sf[s + 1]; ++k) {
-        wsg_frame_desc d = cur.desc[k];
+      j.nheld[s] = (uint32_t)h.held_desc.size();
+      for (uint32_t k = j.cur.sf[s]; k < j.cur.sf[s + 1]; ++k) {
+        wsg_frame_desc d = j.cur.desc[k];
         d.flags &= (uint8_t)~WSG_DESC_REPLAY;
         x.desc.push_back(d);
       }
     }
+  }
+  x.sf[S] = (uint32_t)x.desc.size();
+  const uint64_t F = x.desc.size();
+  const uint64_t ipos = j.ipos;
+  DBuf& ar = f.dpay;
+  B_TRY(b, ar.grow_keep(ipos + j.oo[S] + 64, ipos, st));
+  B_TRY(b, upload(b->d_desc, x.desc, st));
+  B_TRY(b, upload(b->d_sf, x.sf, st));
+  B_TRY(b, upload(b->d_ooff, j.oo, st));
+  B_TRY(b, b->d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
+  int rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
+                                    (const uint32_t*)b->d_sf.p, S, ar.p, ipos, (wsg_inflate_state*)b->d_istate.p,
+                                    b->d_iwin.p, ar.p + ipos, (const uint64_t*)b->d_ooff.p,
+                                    (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
+                                    (uint32_t*)b->d_rf.p);
+  if (rc) return bset(b, rc, wsg_last_error(b->sctx));
+  // FrameUtf8Validator right behind it on the device (PerMessageDeflateExtension.java:
+  // 316-326): its input made from inflate's output by k_stage_vprep, no host hop
+  j.validate = b->stages.validate != 0;
+  if (j.validate) {
+    B_TRY(b, upload(b->d_nheld, j.nheld, st));
+    B_TRY(b, b->d_vdesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+    B_TRY(b, b->d_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+    if (F) {
+      hipLaunchKernelGGL(k_stage_vprep, dim3((uint32_t)((F + 255) / 256)), dim3(256), 0, st,
+                         (const wsg_frame_desc*)b->d_odesc.p, (const uint32_t*)b->d_sf.p,
+                         (const uint32_t*)b->d_nheld.p, (const wsg_session_result*)b->d_ores.p, ipos, S, F,
+                         (wsg_frame_desc*)b->d_vdesc.p);
+      B_TRY(b, hipGetLastError());
     }
-    x.sf[S] = (uint32_t)x.desc.size();
-    const uint64_t F = x.desc.size();
-    SP(13);
-    B_TRY(b, b->ar->grow_keep(ipos + oo[S] + 64, ipos, st));
-    B_TRY(b, upload(b->d_desc, x.desc, st));
-    B_TRY(b, upload(b->d_sf, x.sf, st));
-    B_TRY(b, upload(b->d_ooff, oo, st));
-    B_TRY(b, b->d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
-    B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
-    B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
-    int rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
-                                      (const uint32_t*)b->d_sf.p, S, b->ar->p, ipos, (wsg_inflate_state*)b->d_istate.p,
-                                      b->d_iwin.p, b->ar->p + ipos, (const uint64_t*)b->d_ooff.p,
-                                      (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
-                                      (uint32_t*)b->d_rf.p);
+    rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_vdesc.p, F, (const uint32_t*)b->d_sf.p, S,
+                                   ar.p, ipos + j.oo[S], (wsg_session_state*)b->d_vstate.p,
+                                   (wsg_session_result*)b->d_vres.p);
     if (rc) return bset(b, rc, wsg_last_error(b->sctx));
-    // FrameUtf8Validator right behind it on the device (PerMessageDeflateExtension.java:
-    // 316-326): its input made from inflate's output by k_stage_vprep, no host hop
-    const bool validate = b->stages.validate != 0;
-    if (validate) {
-      B_TRY(b, upload(b->d_nheld, nheld, st));
-      B_TRY(b, b->d_vdesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
-      B_TRY(b, b->d_vres.ensure((S + 1) * sizeof(wsg_session_result)));
-      if (F) {
-        hipLaunchKernelGGL(k_stage_vprep, dim3((uint32_t)((F + 255) / 256)), dim3(256), 0, st,
-                           (const wsg_frame_desc*)b->d_odesc.p, (const uint32_t*)b->d_sf.p,
-                           (const uint32_t*)b->d_nheld.p, (const wsg_session_result*)b->d_ores.p, ipos, S, F,
-                           (wsg_frame_desc*)b->d_vdesc.p);
-        B_TRY(b, hipGetLastError());
-      }
-      rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_vdesc.p, F, (const uint32_t*)b->d_sf.p, S,
-                                     b->ar->p, ipos + oo[S], (wsg_session_state*)b->d_vstate.p,
-                                     (wsg_session_result*)b->d_vres.p);
-      if (rc) return bset(b, rc, wsg_last_error(b->sctx));
+  }
+  B_TRY(b, b->h_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
+  B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
+  if (F) B_TRY(b, hipMemcpyAsync(b->h_odesc.p, b->d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, st));
+  B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
+  B_TRY(b, hipMemcpyAsync(b->h_rf.p, b->d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  if (j.validate) {
+    B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+    B_TRY(b, hipMemcpyAsync(b->h_vres.p, b->d_vres.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
+  }
+  return WSG_API_OK;
+}
+
+// The inflate job of flush f: the frames it takes (j.cur, the decoder's delivered frames),
+// per session its output region and its held frames' place in the arena, their bytes
+// uploaded; then the first attempt launched.
+static int infl_begin(wsg_batcher* b, FlushSlot& f) {
+  const uint32_t S = b->n;
+  hipStream_t st = ws::ctx_stream(b->sctx);
+  InflJob& j = f.ij;
+  j.todo.clear();
+  j.cap.assign(S, 0);
+  j.held_at.assign(S, 0);
+  j.nheld.assign(S, 0);
+  j.od.clear();
+  j.od_at.assign(S, 0);
+  j.od_n.assign(S, 0);
+  j.in_order = true;
+  // the held frames' bytes go after the decoded payloads
+  uint64_t hpos = j.used;
+  for (uint32_t s = 0; s < S; ++s) {
+    const StageSess& h = b->ss[s];
+    uint64_t c = 0;
+    if (!h.held_desc.empty()) {
+      j.held_at[s] = hpos;
+      hpos = al16(hpos + h.held_bytes.size());
+      for (const wsg_frame_desc& hd : h.held_desc) c += hd.payload_len + 4;
     }
-    B_TRY(b, b->h_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
-    B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
-    B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
-    if (F) B_TRY(b, hipMemcpyAsync(b->h_odesc.p, b->d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, st));
-    B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
-    B_TRY(b, hipMemcpyAsync(b->h_rf.p, b->d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    if (validate) {
-      B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
-      B_TRY(b, hipMemcpyAsync(b->h_vres.p, b->d_vres.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
-    }
+    for (uint32_t k = j.cur.sf[s]; k < j.cur.sf[s + 1]; ++k) c += j.cur.desc[k].payload_len + 4;
+    if (h.held_desc.empty() && j.cur.sf[s + 1] == j.cur.sf[s]) continue;
+    j.todo.push_back(s);
+    j.cap[s] = al16(4096 + 8 * c);
+  }
+  B_TRY(b, f.dpay.grow_keep(hpos + 64, f.pcap, st));
+  for (uint32_t s = 0; s < S; ++s) {
+    const StageSess& h = b->ss[s];
+    if (!h.held_bytes.empty())
+      B_TRY(b, hipMemcpyAsync(f.dpay.p + j.held_at[s], h.held_bytes.data(), h.held_bytes.size(),
+                              hipMemcpyHostToDevice, st));
+  }
+  j.ipos = al16(hpos);
+  if (j.todo.empty()) return WSG_API_OK;
+  return infl_launch(b, f);
+}
+
+// Wait for the attempt in flight, take its results (runs again what overflowed), and
+// leave in j.cur the inflate stage's output frames (validated), in j.used the arena's
+// extent.  Sessions reset since the flush (f.resets) take nothing from it.
+static int infl_collect(wsg_batcher* b, FlushSlot& f) {
+  const uint32_t S = b->n;
+  hipStream_t st = ws::ctx_stream(b->sctx);
+  InflJob& j = f.ij;
+  while (!j.todo.empty()) {
     {
       SP(2);
       B_TRY(b, hipStreamSynchronize(st));
     }
+    const StageList& x = j.x;
     const wsg_frame_desc* odesc = (const wsg_frame_desc*)b->h_odesc.p;
     const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
     const uint32_t* rf = (const uint32_t*)b->h_rf.p;
-    const wsg_session_result* vr = validate ? (const wsg_session_result*)b->h_vres.p : nullptr;
+    const wsg_session_result* vr = j.validate ? (const wsg_session_result*)b->h_vres.p : nullptr;
+    const uint64_t ipos = j.ipos;
     std::vector<uint32_t> retry;
     struct Held {
       uint32_t s;
@@ -654,73 +705,81 @@ static int stage_inflate(wsg_batcher* b, FlushSlot& f, StageList& cur, uint64_t&
     };
     std::vector<Held> hd_copies;
     {
-    SP(3);
-    for (uint32_t s : todo) {
-      if (r[s].error == WSG_E_INFLATE_CAPACITY) {
-        cap[s] *= 8;
-        retry.push_back(s);
-        continue;
-      }
-      StageSess& h = b->ss[s];
-      uint32_t j = 0;
-      od_at[s] = od.size();
-      for (uint32_t k = x.sf[s] + nheld[s]; k < x.sf[s + 1] && j < r[s].n_delivered; ++k, ++j) {
-        wsg_frame_desc d = odesc[k];
-        if (d.flags & WSG_DESC_INFLATED) d.payload_off += ipos;  // (else the input's arena offset)
-        d.flags &= 0xf0u | 0x80u;
-        od.push_back(d);
-      }
-      od_n[s] = j;
-      std::vector<wsg_frame_desc> nhd;
-      uint64_t nb = 0;
-      if (r[s].error) stage_fail(b, s, r[s]);
-      if (vr && vr[s].error) {  // the validator failed an earlier frame: its result is the session's
-        const uint32_t v = vr[s].n_delivered >= nheld[s] ? vr[s].n_delivered - nheld[s] : 0u;
-        od_n[s] = std::min(od_n[s], v);
-        wsg_session_result e = vr[s];
-        stage_fail(b, s, e);
-      }
-      if (r[s].error) {
-      } else if (rf[s] != 0xFFFFFFFFu) {  // a message left open: its frames go again with the next batch
-        for (uint32_t k = x.sf[s] + rf[s]; k < x.sf[s + 1]; ++k) {
-          wsg_frame_desc d = x.desc[k];
-          d.flags &= (uint8_t)~WSG_DESC_REPLAY;
-          hd_copies.push_back({s, d.payload_off, nb, d.payload_len});
-          d.payload_off = nb;
-          nb += d.payload_len;
-          nhd.push_back(d);
+      SP(3);
+      for (uint32_t s : j.todo) {
+        if (std::find(f.resets.begin(), f.resets.end(), s) != f.resets.end()) {
+          j.od_at[s] = j.od.size();  // the slot has a new session: this flush is not its
+          j.od_n[s] = 0;
+          continue;
         }
+        if (r[s].error == WSG_E_INFLATE_CAPACITY) {
+          j.cap[s] *= 8;
+          retry.push_back(s);
+          continue;
+        }
+        StageSess& h = b->ss[s];
+        uint32_t n = 0;
+        j.od_at[s] = j.od.size();
+        for (uint32_t k = x.sf[s] + j.nheld[s]; k < x.sf[s + 1] && n < r[s].n_delivered; ++k, ++n) {
+          wsg_frame_desc d = odesc[k];
+          if (d.flags & WSG_DESC_INFLATED) d.payload_off += ipos;  // (else the input's arena offset)
+          d.flags &= 0xf0u | 0x80u;
+          j.od.push_back(d);
+        }
+        j.od_n[s] = n;
+        std::vector<wsg_frame_desc> nhd;
+        uint64_t nb = 0;
+        if (r[s].error) stage_fail(b, s, r[s]);
+        if (vr && vr[s].error) {  // the validator failed an earlier frame: its result is the session's
+          const uint32_t v = vr[s].n_delivered >= j.nheld[s] ? vr[s].n_delivered - j.nheld[s] : 0u;
+          j.od_n[s] = std::min(j.od_n[s], v);
+          stage_fail(b, s, vr[s]);
+        }
+        if (!r[s].error && rf[s] != 0xFFFFFFFFu) {  // a message left open: its frames go again with the next batch
+          for (uint32_t k = x.sf[s] + rf[s]; k < x.sf[s + 1]; ++k) {
+            wsg_frame_desc d = x.desc[k];
+            d.flags &= (uint8_t)~WSG_DESC_REPLAY;
+            hd_copies.push_back({s, d.payload_off, nb, d.payload_len});
+            d.payload_off = nb;
+            nb += d.payload_len;
+            nhd.push_back(d);
+          }
+        }
+        h.held_desc.swap(nhd);
+        h.held_bytes.assign(nb, 0);
       }
-      h.held_desc.swap(nhd);
-      h.held_bytes.assign(nb, 0);
-    }
     }
     for (const Held& c : hd_copies)
       if (c.len)
-        B_TRY(b, hipMemcpyAsync(b->ss[c.s].held_bytes.data() + c.dst, b->ar->p + c.src, c.len,
+        B_TRY(b, hipMemcpyAsync(b->ss[c.s].held_bytes.data() + c.dst, f.dpay.p + c.src, c.len,
                                 hipMemcpyDeviceToHost, st));
     if (!hd_copies.empty()) B_TRY(b, hipStreamSynchronize(st));
-    ipos = al16(ipos + oo[S]);
-    if (!retry.empty()) in_order = false;
-    todo.swap(retry);
+    j.ipos = al16(ipos + j.oo[S]);
+    if (!retry.empty()) j.in_order = false;
+    j.todo.swap(retry);
+    if (!j.todo.empty()) {
+      const int rc = infl_launch(b, f);
+      if (rc) return rc;
+    }
   }
+  StageList& cur = j.cur;
   cur.sf.assign(S + 1, 0);
   cur.n_ok.assign(S, 0);
   uint64_t k = 0;
   for (uint32_t s = 0; s < S; ++s) {
     cur.sf[s] = (uint32_t)k;
-    cur.n_ok[s] = od_n[s];
-    k += od_n[s];
+    cur.n_ok[s] = j.od_n[s];
+    k += j.od_n[s];
   }
   cur.sf[S] = (uint32_t)k;
-  if (in_order && k == od.size()) {
-    cur.desc.swap(od);
+  if (j.in_order && k == j.od.size()) {
+    cur.desc.swap(j.od);
   } else {
     cur.desc.resize(k);
     for (uint32_t s = 0; s < S; ++s)
-      std::copy(od.begin() + od_at[s], od.begin() + od_at[s] + od_n[s], cur.desc.begin() + cur.sf[s]);
+      std::copy(j.od.begin() + j.od_at[s], j.od.begin() + j.od_at[s] + j.od_n[s], cur.desc.begin() + cur.sf[s]);
   }
-  used = ipos;
+  j.used = j.ipos;
   return WSG_API_OK;
 }
 
@@ -840,17 +899,16 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
   return WSG_API_OK;
 }
 
-// The stage chain over a flush whose decode is done: the decoder's delivered frames
-// (their payloads still on the device, f.dpay) through inflate -> validator ->
-// aggregator on the device, then one gather, and the download of what the handler
-// receives queued on the download stream (collected by stage_finish).
-static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
+// The stage chain of a flush whose decode is done, begun: the output reset, the stage
+// carry of slots handed to new sessions zeroed, the stage input built from the
+// decoder's delivered frames (their payloads still on the device, f.dpay), and the
+// inflate + validator launched on the stage stream (no wait: stage_compute collects).
+static int stage_begin(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
   SP(0);
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
   StageOut& o = f.so;
   b->out = &o;
-  b->ar = &f.dpay;
   o.res.assign(res, res + S);
   o.sf.assign(S + 1, 0);
   o.desc.clear();
@@ -872,9 +930,10 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
     if (b->stage_closed[s]) o.res[s] = wsg_session_result{};
   const uint32_t* sf = (const uint32_t*)f.sf.p;
   const wsg_frame_desc* desc = (const wsg_frame_desc*)f.desc.p;
-  StageList cur;
+  StageList& cur = f.ij.cur;
   cur.sf.assign(S + 1, 0);
   cur.n_ok.assign(S, 0);
+  cur.desc.clear();
   {
     SP(10);
     for (uint32_t s = 0; s < S; ++s) {
@@ -889,14 +948,31 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
     }
   }
   cur.sf[S] = (uint32_t)cur.desc.size();
-  uint64_t used = al16(f.pcap);
+  f.ij.used = al16(f.pcap);
+  f.ij.todo.clear();
+  f.ij.active = true;
   if (f.pcap) B_TRY(b, hipStreamWaitEvent(st, f.dpay_done, 0));
+  if (b->stages.inflate) return infl_begin(b, f);  // (the validator runs inside, on the device)
+  B_TRY(b, f.dpay.grow_keep(f.ij.used + 64, f.pcap, st));
+  return WSG_API_OK;
+}
+
+// The rest of the chain: the inflate's results collected, the aggregator, then one
+// gather, and the download of what the handler receives queued on the download
+// stream (collected by stage_finish).
+static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
   int rc;
-  if (b->stages.inflate) {  // (the validator runs inside, on the device)
-    if ((rc = stage_inflate(b, f, cur, used))) return rc;
-  } else {
-    B_TRY(b, b->ar->grow_keep(used + 64, f.pcap, st));
-  }
+  if (!f.ij.active && (rc = stage_begin(b, f, res))) return rc;
+  SP(0);
+  const uint32_t S = b->n;
+  hipStream_t st = ws::ctx_stream(b->sctx);
+  StageOut& o = f.so;
+  b->out = &o;
+  b->ar = &f.dpay;
+  if (b->stages.inflate && (rc = infl_collect(b, f))) return rc;
+  f.ij.active = false;
+  StageList& cur = f.ij.cur;
+  const uint64_t used = f.ij.used;
   if (b->stages.aggregate) {
     if ((rc = stage_aggregate(b, cur, used))) return rc;
   } else {
@@ -1367,13 +1443,17 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   if (!b->has_stages) return WSG_API_OK;
   int rc2 = f.so.staged ? WSG_API_OK : stage_compute(b, f, res);
   if (rc2) return rc2;
-  // the next flush's stages, while this one's output downloads (its decode done)
+  // the next flush's chain begun now (its inflate launched, not waited for): it runs
+  // while this flush's output downloads and while the caller feeds the next reads;
+  // its decode results are needed to build its input, so they are waited for (one
+  // flush's decode: short, and needed by its own wait anyway)
   if (!b->q.empty()) {
     FlushSlot& g = b->fs[b->q.front()];
-    if (!g.so.staged && hipEventQuery(g.done) == hipSuccess) {
+    if (!g.so.staged && !g.ij.active) {
+      B_TRY(b, hipEventSynchronize(g.done));
       std::vector<wsg_session_result> gres;
       adjusted_results(b, g, gres);
-      if ((rc2 = stage_compute(b, g, gres.data()))) return rc2;
+      if ((rc2 = stage_begin(b, g, gres.data()))) return rc2;
     }
   }
   if ((rc2 = stage_finish(b, f))) return rc2;

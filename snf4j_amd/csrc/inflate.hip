@@ -247,8 +247,7 @@ __device__ __forceinline__ bool tdec(const uint32_t* root, int rbits, const Huff
 
 namespace {
 
-constexpr uint32_t TOK_SLACK = 96;  // per-frame slack of the token / literal regions (their starts are
-                                    // rounded up to 16 B: the lane decoder stores whole 16-B groups)
+constexpr uint32_t TOK_SLACK = 80;  // per-frame slack of the token / literal regions
 
 // ---------------------------------------------------------------------------------
 // Message-parallel pre-decode (k_infl_tok).  permessage-deflate ends every message
@@ -429,11 +428,9 @@ __device__ __forceinline__ uint32_t lane_sym(const uint16_t* root, int rbits, co
 }
 
 
-__device__ __forceinline__ uint64_t tok_base(uint64_t po, uint64_t k) {
-  return (po + (uint64_t)TOK_SLACK * k + 3) & ~(uint64_t)3;  // (words: 16-B aligned)
-}
+__device__ __forceinline__ uint64_t tok_base(uint64_t po, uint64_t k) { return po + (uint64_t)TOK_SLACK * k; }
 __device__ __forceinline__ uint64_t lit_base(uint64_t po, uint64_t k) {
-  return (3 * po + (uint64_t)TOK_SLACK * k + 15) & ~(uint64_t)15;
+  return (3 * po + (uint64_t)TOK_SLACK * k + 3) & ~(uint64_t)3;
 }
 __device__ __forceinline__ uint32_t lit_cap_of(uint32_t plen) { return 3u * (plen + 4u) + 60u; }
 
@@ -1122,44 +1119,12 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     drop((int)(p & 7u));
   };
   // --- the output ---
-  // Literal words and tokens are staged in registers a 16-B group at a time and stored
-  // when the group is whole: a lane's stores go out as whole 16-B chunks of its own
-  // region (every lane writes a different region, so 4-B stores each became a partial
-  // line write of their own: 3.5x the token + literal bytes written, and more stores
-  // for the ring top-ups' memory waits to drain).  flush_staged() writes a partial group.
   uint32_t ntok = 0, nlit = 0, run = 0, outlen = 0, litw = 0;
-  uint32_t lq0 = 0, lq1 = 0, lq2 = 0, lq3 = 0, tq0 = 0, tq1 = 0, tq2 = 0, tq3 = 0;
-  auto lq_put = [&](uint32_t wi, uint32_t w) {  // literal word wi is complete
-    const uint32_t j = wi & 3u;
-    lq0 = j == 0u ? w : lq0;
-    lq1 = j == 1u ? w : lq1;
-    lq2 = j == 2u ? w : lq2;
-    lq3 = j == 3u ? w : lq3;
-    if (j == 3u) reinterpret_cast<uint4*>(litp)[wi >> 2] = make_uint4(lq0, lq1, lq2, lq3);
-  };
-  auto tq_put = [&](uint32_t ti, uint32_t t) {  // token ti
-    const uint32_t j = ti & 3u;
-    tq0 = j == 0u ? t : tq0;
-    tq1 = j == 1u ? t : tq1;
-    tq2 = j == 2u ? t : tq2;
-    tq3 = j == 3u ? t : tq3;
-    if (j == 3u) reinterpret_cast<uint4*>(tokp)[ti >> 2] = make_uint4(tq0, tq1, tq2, tq3);
-  };
-  auto flush_staged = [&]() {  // the complete words and tokens of the open groups (not litw)
-    uint32_t* const l32 = reinterpret_cast<uint32_t*>(litp);
-    const uint32_t lw = nlit >> 2, lg = lw & ~3u, tg = ntok & ~3u;
-    if (lw - lg > 0u) l32[lg] = lq0;
-    if (lw - lg > 1u) l32[lg + 1u] = lq1;
-    if (lw - lg > 2u) l32[lg + 2u] = lq2;
-    if (ntok - tg > 0u) tokp[tg] = tq0;
-    if (ntok - tg > 1u) tokp[tg + 1u] = tq1;
-    if (ntok - tg > 2u) tokp[tg + 2u] = tq2;
-  };
   auto put_lit = [&](uint32_t b) -> bool {
     if (nlit >= lcap) return false;
     litw |= b << (8 * (nlit & 3u));
     if ((++nlit & 3u) == 0) {
-      lq_put((nlit >> 2) - 1, litw);
+      reinterpret_cast<uint32_t*>(litp)[(nlit >> 2) - 1] = litw;
       litw = 0;
     }
     ++run;
@@ -1168,7 +1133,7 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   };
   auto put_tok = [&](uint32_t t) -> bool {
     if (ntok >= tcap) return false;
-    tq_put(ntok++, t);
+    tokp[ntok++] = t;
     return true;
   };
   auto end_run = [&]() -> bool {
@@ -1436,14 +1401,15 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       const uint32_t len2 = r2 & 15u, sym2 = r2 >> 4;
       const bool two = !PAIR && is_lit && len2 != 0u && sym2 < 256u && (int)(len + len2) <= bits && nlit + 2u <= lcap;
       drop((int)(len + x + (two ? len2 : 0u)));
+      uint32_t* const lit32 = reinterpret_cast<uint32_t*>(litp);
       const uint32_t nadd = is_lit ? (two ? 2u : 1u) : 0u;
       const uint32_t sh = 8u * (nlit & 3u);
       const uint64_t acc = (uint64_t)litw | ((uint64_t)(is_lit ? v : 0u) << sh) | ((uint64_t)(two ? sym2 : 0u) << (sh + 8u));
       const bool word_done = (nlit & 3u) + nadd >= 4u;
-      if (word_done) lq_put(nlit >> 2, (uint32_t)acc);  // the word just filled
+      if (word_done) lit32[nlit >> 2] = (uint32_t)acc;  // the word just filled
       if (dist) {
-        if (has_run) tq_put(ntok, run);
-        tq_put(ntok + has_run, 0x80000000u | ((mlen - 3u) << 16) | (v - 1u));
+        if (has_run) tokp[ntok] = run;
+        tokp[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
       }
       ntok += dist ? 1u + has_run : 0u;
       litw = word_done ? (uint32_t)(acc >> 32) : (uint32_t)acc;
@@ -1469,7 +1435,6 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
     if (role == 0) {
       if (st == Q_SYNC) {
         end_run();  // (room: checked at S)
-        flush_staged();  // (the tail appends behind these in memory)
         Q.cnt[0 * 64 + lane] = 1u;
         Q.cnt[1 * 64 + lane] = sync_j;
         Q.cnt[2 * 64 + lane] = ntok;
@@ -1490,7 +1455,6 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         a.tstat[k] = InflTokStat{0u, 0u, 0u, 0u};
         return Q_BAD;
       }
-      flush_staged();  // (its tokens and literals are read back below)
       if (nlit & 3u) reinterpret_cast<uint32_t*>(litp)[nlit >> 2] = litw;
       const uint32_t j = Q.cnt[1 * 64 + hl], nth = Q.cnt[2 * 64 + hl], nlh = Q.cnt[3 * 64 + hl],
                      outh = Q.cnt[4 * 64 + hl], litwh = Q.cnt[5 * 64 + hl];
@@ -1557,7 +1521,6 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
   if (st == Q_OK) {
     if (!end_run()) st = Q_BAD;
     else {
-      flush_staged();
       if (nlit & 3u) reinterpret_cast<uint32_t*>(lit)[nlit >> 2] = litw;
       a.tstat[k] = InflTokStat{1u, ntok, nlit, outlen};
     }
