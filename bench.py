@@ -45,6 +45,11 @@ CONFIGS = {
 
 
 
+# flushes the bench lines keep in flight: WSG_BATCHER_MAX_INFLIGHT (snf4j_amd._lib; checked
+# equal in tests/test_bench_cli.py); WSG_BENCH_INFLIGHT=2 for A/B runs against older builds
+BATCHER_MAX_INFLIGHT = int(os.environ.get("WSG_BENCH_INFLIGHT", "3"))
+
+
 def apply_tuning(ctx):
     """A/B runs (scripts/ab_env.sh): WSG_TUNE_<NAME>=<value> in the bench's environment
     sets the context switch wsg_set_tuning(<NAME>) — the harness reads it, not the library."""
@@ -905,7 +910,7 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
     FrameUtf8Validator, PerMessageDeflateExtension.java:316-326), end to end from host
     socket reads to host frames: per round one `chunk`-byte read of every session
     (wsg_batcher_feed_many), then wsg_batcher_flush_async (H2D, decode, inflate,
-    validate, D2H), two flushes in flight.  Value: inflated bytes delivered per second."""
+    validate, D2H), three flushes in flight.  Value: inflated bytes delivered per second."""
     import numpy as np
     import torch
     import snf4j_amd
@@ -944,7 +949,7 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
             ta = time.perf_counter()
             nb.feed_many_ptrs(sids, ptrs, lens)
             tf += time.perf_counter() - ta
-            if pending == 2:
+            if pending == BATCHER_MAX_INFLIGHT:
                 ta = time.perf_counter()
                 sfb, descb, _, resb, _ = nb.wait_raw()
                 tw += time.perf_counter() - ta
@@ -1038,7 +1043,7 @@ def e2e_encode_line(ctx, dev, K, W, n_s=64, msg_bytes=16 << 20, frame=65536, per
 def e2e_aggregate_line(ctx, dev, K, W, chunk=65536):
     """The native batcher with FrameAggregator after the decoder (wsg_batcher_set_stages
     aggregate; FrameAggregator.java:72-104) on configs[2]'s 4 GiB mixed batch, host to
-    host: per round one `chunk`-byte read of every session, two flushes in flight;
+    host: per round one `chunk`-byte read of every session, three flushes in flight;
     the decode's UTF-8 check stays fused.  Value: wire bytes fed per second."""
     import numpy as np
     import torch
@@ -1080,7 +1085,7 @@ def e2e_aggregate_line(ctx, dev, K, W, chunk=65536):
         pending, n_out, n_err = 0, 0, 0
         for sids, ptrs, lens in rounds:
             nb.feed_many_ptrs(sids, ptrs, lens)
-            if pending == 2:
+            if pending == BATCHER_MAX_INFLIGHT:
                 sfb, descb, _, resb, _ = nb.wait_raw()
                 n_out += int(resb["n_delivered"].astype(np.int64).sum())
                 n_err += int((resb["error"] != 0).sum())
@@ -1212,7 +1217,7 @@ def e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev, reps=6):
             tf = time.perf_counter()
             nb.feed_many_ptrs(sids, ptrs, lens)
             feed_t += time.perf_counter() - tf
-            if pending == 2:
+            if pending == BATCHER_MAX_INFLIGHT:
                 sfb, descb, _, resb, w = nb.wait_raw()
                 assert int(resb["error"].max()) == 0
                 wb, n_fr, pending = wb + w, n_fr + len(descb), pending - 1
@@ -1232,7 +1237,7 @@ def e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev, reps=6):
                              "api": "per round: wsg_batcher_feed_many (one 64 KiB socket read per session, "
                                     "copied once into the open batch's pinned arena and framed in place, "
                                     "threaded by session) + wsg_batcher_flush_async (H2D, decode, D2H of the "
-                                    "arena, no gather), two flushes in flight"}
+                                    "arena, no gather), three flushes in flight"}
     nb.close()
     out["drop_in_loop"] = e2e_loop_line(pctx, rounds, wire_bytes, F, n_s)
     pctx.close()

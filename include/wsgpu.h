@@ -391,10 +391,16 @@ int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, cons
  * staging and queues H2D, decode and D2H (wsg_decode_batch_host_async) without
  * waiting, so the next feeds and the next gather overlap the device and PCIe
  * work; wsg_batcher_wait returns the oldest queued flush's results (a view valid
- * until the flush after next).  At most two flushes in flight; the carry state
- * chains through them on the device side, and host changes (a slot reset, a
- * header error found on the host) apply to the next batch queued.
+ * until that slot is flushed again, WSG_BATCHER_MAX_INFLIGHT flushes later).  At
+ * most WSG_BATCHER_MAX_INFLIGHT flushes in flight (WSG_API_ERANGE beyond); the
+ * carry state chains through them on the device side, and host changes (a slot
+ * reset, a header error found on the host) apply to the next batch queued.  With
+ * stages, wsg_batcher_wait collects the oldest flush's chain and starts the chains
+ * of the flushes behind it (inflate + validator launched, the output gather of the
+ * next one queued), so they run while the caller feeds: keeping three in flight
+ * gives the chain two flushes of lead.
  * wsg_batcher_flush = wait for the queued ones (results dropped) + flush_async + wait. */
+#define WSG_BATCHER_MAX_INFLIGHT 3
 int wsg_batcher_flush_async(wsg_batcher* b);
 int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out);
 int wsg_batcher_session_state(wsg_batcher* b, uint32_t sid, wsg_session_state* st);

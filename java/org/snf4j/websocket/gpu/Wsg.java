@@ -18,6 +18,9 @@ package org.snf4j.websocket.gpu;
 import java.nio.ByteBuffer;
 
 final class Wsg {
+	/** WSG_BATCHER_MAX_INFLIGHT (wsgpu.h): decode flushes a native batcher keeps in flight. */
+	static final int BATCHER_MAX_INFLIGHT = 3;
+
 
 	static {
 		System.loadLibrary("wsgpu_jni");

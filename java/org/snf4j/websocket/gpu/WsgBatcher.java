@@ -16,7 +16,8 @@
  *      side copies them into the open batch's pinned arena and frames them, several
  *      threads for large iterations), then releases the buffers;
  *   2. delivers every earlier flush whose device work has finished (wsg_batcher_await
- *      with no wait; only when two are already in flight does it wait for the oldest);
+ *      with no wait; only with BATCHER_MAX_INFLIGHT (3) already in flight does it wait
+ *      for the oldest);
  *   3. queues this iteration's batch (wsg_batcher_flush_async: H2D, decode + UTF-8 and
  *      the stages after the decoder, D2H) and hands its ticket to the completion
  *      thread.
@@ -412,7 +413,7 @@ public final class WsgBatcher {
 			boolean fed = n.nReads > 0;
 			feedReads(n);
 			if (fed) {
-				if (n.inflight.size() == 2)
+				if (n.inflight.size() == Wsg.BATCHER_MAX_INFLIGHT)
 					collectOldest(n);
 				check(Wsg.batcherFlushAsync(n.handle), "wsg_batcher_flush_async");
 				n.inflight.add(Wsg.batcherTicket(n.handle));
@@ -499,7 +500,7 @@ public final class WsgBatcher {
 				collectReady(n);
 				if (!fed)
 					continue;
-				if (n.inflight.size() == 2)
+				if (n.inflight.size() == Wsg.BATCHER_MAX_INFLIGHT)
 					collectOldest(n);
 				check(Wsg.batcherFlushAsync(n.handle), "wsg_batcher_flush_async");
 				long t = Wsg.batcherTicket(n.handle);

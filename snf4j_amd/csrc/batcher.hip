@@ -480,7 +480,7 @@ struct wsg_batcher {
   std::vector<SessIn> s;
   std::vector<wsg_session_state> state;  // the carry as of the last waited flush (+ host changes)
   PinnedBuf st;                          // the carry the device batches chain through
-  FlushSlot fs[3];                       // one being fed, up to two in flight
+  FlushSlot fs[WSG_BATCHER_MAX_INFLIGHT + 1];  // one being fed, up to MAX_INFLIGHT in flight
   int open = 0;                          // the slot feeds land in
   std::deque<int> q;                     // flushes in flight, oldest first
   std::vector<std::pair<uint32_t, int>> patch;  // host changes for the next batch's state: 0 reset, 1 closed
@@ -1291,7 +1291,8 @@ static int stage_state(wsg_batcher* b) {
 
 int wsg_batcher_flush_async(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
-  if (b->q.size() >= 2) return bset(b, WSG_API_ERANGE, "two flushes in flight: wsg_batcher_wait first");
+  if (b->q.size() >= WSG_BATCHER_MAX_INFLIGHT)
+    return bset(b, WSG_API_ERANGE, "WSG_BATCHER_MAX_INFLIGHT flushes in flight: wsg_batcher_wait first");
   const uint32_t S = b->n;
   int rc;
   const int slot = b->open;
@@ -1360,7 +1361,7 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
   ++b->tickets;
   b->q.push_back(slot);
   // feeds go to the next slot (waited: at most two in flight)
-  b->open = (b->open + 1) % 3;
+  b->open = (b->open + 1) % (WSG_BATCHER_MAX_INFLIGHT + 1);
   FlushSlot& g = b->fs[b->open];
   g.arena_len = 0;
   for (uint32_t i = 0; i < S; ++i) {
@@ -1443,17 +1444,22 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   if (!b->has_stages) return WSG_API_OK;
   int rc2 = f.so.staged ? WSG_API_OK : stage_compute(b, f, res);
   if (rc2) return rc2;
-  // the next flush's chain begun now (its inflate launched, not waited for): it runs
-  // while this flush's output downloads and while the caller feeds the next reads;
-  // its decode results are needed to build its input, so they are waited for (one
-  // flush's decode: short, and needed by its own wait anyway)
-  if (!b->q.empty()) {
-    FlushSlot& g = b->fs[b->q.front()];
-    if (!g.so.staged && !g.ij.active) {
+  // The chains of the flushes behind this one, so that the device works on them while
+  // this flush's output downloads and while the caller feeds the next reads: the next
+  // one's collected and its output gather queued if its chain was begun in an earlier
+  // wait (its inflate ran meanwhile), else begun; the one after it begun (inflate +
+  // validator launched, not waited for).  A chain is begun from its flush's decode
+  // results, so those are waited for (one flush's decode: short).
+  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
+    FlushSlot& g = b->fs[b->q[qi]];
+    if (g.so.staged) continue;
+    std::vector<wsg_session_result> gres;
+    if (!g.ij.active) {
       B_TRY(b, hipEventSynchronize(g.done));
-      std::vector<wsg_session_result> gres;
       adjusted_results(b, g, gres);
       if ((rc2 = stage_begin(b, g, gres.data()))) return rc2;
+    } else if (qi == 0 && b->q.size() > 1) {
+      if ((rc2 = stage_compute(b, g, nullptr))) return rc2;
     }
   }
   if ((rc2 = stage_finish(b, f))) return rc2;

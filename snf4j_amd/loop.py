@@ -15,7 +15,8 @@ The batching on that loop:
   executenf, which runs after every read of the iteration;
 - flush() feeds the iteration's reads with one wsg_batcher_feed_many, collects every
   earlier flush whose device work has finished (wsg_batcher_await with no wait),
-  collects the oldest one blocking only when two are in flight, then queues this one
+  collects the oldest one blocking only when WSG_BATCHER_MAX_INFLIGHT (3) are in
+  flight, then queues this one
   (wsg_batcher_flush_async) and hands its ticket to the completion thread;
 - the completion thread waits for the ticket (wsg_batcher_await) and re-enters the
   loop with executenf(collect_ready): the loop thread never waits on the device for a
@@ -32,6 +33,7 @@ import collections
 import queue
 import threading
 
+from ._lib import BATCHER_MAX_INFLIGHT
 from .codec import EncodeBatcher, NativeBatcher
 
 
@@ -179,7 +181,7 @@ class LoopBatcher:
         self.collect_ready()
         if not fed:  # (the reads went with a drain)
             return
-        if len(self.inflight) == 2:
+        if len(self.inflight) == BATCHER_MAX_INFLIGHT:
             self._collect_oldest(blocking=True)
         self.nb.flush_async()
         t = self.nb.ticket()

@@ -47,3 +47,9 @@ def test_cpu_threads_from_affinity(monkeypatch):
     if aff > 1:
         monkeypatch.setenv("OMP_NUM_THREADS", "1")
         assert bench.cpu_threads()[0] == 1
+
+
+def test_bench_inflight_limit_is_the_library_one():
+    import bench
+    from snf4j_amd import _lib
+    assert bench.BATCHER_MAX_INFLIGHT == _lib.BATCHER_MAX_INFLIGHT

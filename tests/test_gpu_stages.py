@@ -160,11 +160,14 @@ def _chain_case(ctx, oracle, seed, no_context, aggregate, big=False):
     return n_split
 
 
-@pytest.mark.parametrize("seed,aggregate", [(10, True), (11, False)])
-def test_batcher_stage_chain_pipelined(ctx, oracle, seed, aggregate):
-    """The same chain with two flushes in flight (wsg_batcher_flush_async / wait): a
-    session a stage fails in one flush gets nothing from the flush already in flight
-    behind it (the session is closed), and a reset slot starts from fresh stage decoders."""
+@pytest.mark.parametrize("seed,aggregate,depth", [(10, True, 2), (11, False, 2), (12, True, 3), (13, False, 3)])
+def test_batcher_stage_chain_pipelined(ctx, oracle, seed, aggregate, depth):
+    """The same chain with `depth` flushes in flight (wsg_batcher_flush_async / wait; 3 =
+    WSG_BATCHER_MAX_INFLIGHT: each wait collects the next flush's chain and begins the
+    one after): a session a stage fails in one flush gets nothing from the flushes
+    already in flight behind it (the session is closed), a slot reset while its chains
+    are begun or collected delivers nothing of the old session, and a reset slot starts
+    from fresh stage decoders."""
     from snf4j_amd import NativeBatcher
     rng = np.random.default_rng(6200 + seed)
     n = 40
@@ -191,13 +194,19 @@ def test_batcher_stage_chain_pipelined(ctx, oracle, seed, aggregate):
                     assert err[s] is None, s
                     err[s] = (e.getMessage(), e.close_code)
 
+        it = 0
         while any(pos[s] < len(streams[s]) for s in range(n)):
+            it += 1
+            if rnd == 0 and it == 3:  # slots to new sessions mid-stream, flushes in flight
+                for s in range(0, n, 7):
+                    b.reset_session(s)
+                    got[s], err[s], pos[s] = [], None, 0
             for s in range(n):
                 if pos[s] < len(streams[s]):
                     c = int(rng.integers(1, 1500))
                     b.feed(s, streams[s][pos[s]:pos[s] + c])
                     pos[s] += c
-            if pending == 2:
+            if pending == depth:
                 collect()
                 pending -= 1
             b.flush_async()

@@ -119,7 +119,8 @@ def test_loop_scheduling_matches_the_python_restatement():
     the loop with executenf (never schedule() from inside the task phase)."""
     b = _java("WsgBatcher.java")
     flush = _body(b, "synchronized void flush()", "private static void check(")
-    order = ["feedReads(n)", "collectReady(n)", "n.inflight.size() == 2", "Wsg.batcherFlushAsync(n.handle)",
+    order = ["feedReads(n)", "collectReady(n)", "n.inflight.size() == Wsg.BATCHER_MAX_INFLIGHT",
+             "Wsg.batcherFlushAsync(n.handle)",
              "Wsg.batcherTicket(n.handle)", "completion.watch(n.handle, t, false)"]
     pos = [flush.index(x) for x in order]
     assert pos == sorted(pos), order
@@ -138,7 +139,7 @@ def test_loop_scheduling_matches_the_python_restatement():
     ready = _body(b, "private void collectReady(Native n)", "private void collectReady(EncNative n)")
     assert "Wsg.batcherAwait(n.handle, 0, 0)" in ready
     loop = _read("snf4j_amd/loop.py")
-    for x in ("feed_many", "collect_ready()", "len(self.inflight) == 2", "flush_async()", "ticket()",
+    for x in ("feed_many", "collect_ready()", "len(self.inflight) == BATCHER_MAX_INFLIGHT", "flush_async()", "ticket()",
               "_completion.watch(t)", "await_done(0, 0)", "executenf(self.task)"):
         assert x in loop, x
 
@@ -214,3 +215,11 @@ def test_decoder_close_control_matches_the_restatement():
     for x in ("def _control_close(self, t)", "self.batcher.drain(self)", "kind == CloseType.NONE",
               "s.quickClose()", "def drain(self, d: GpuFrameDecoder | None = None)"):
         assert x in loop, x
+
+
+def test_inflight_limit_agrees():
+    """WSG_BATCHER_MAX_INFLIGHT (wsgpu.h) = Wsg.BATCHER_MAX_INFLIGHT = _lib.BATCHER_MAX_INFLIGHT."""
+    from snf4j_amd import _lib
+    h = re.search(r"#define WSG_BATCHER_MAX_INFLIGHT (\d+)", _read("include/wsgpu.h"))
+    j = re.search(r"static final int BATCHER_MAX_INFLIGHT = (\d+);", _java("Wsg.java"))
+    assert h and j and int(h.group(1)) == int(j.group(1)) == _lib.BATCHER_MAX_INFLIGHT
