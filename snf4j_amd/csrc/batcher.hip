@@ -1445,22 +1445,25 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   int rc2 = f.so.staged ? WSG_API_OK : stage_compute(b, f, res);
   if (rc2) return rc2;
   // The chains of the flushes behind this one, so that the device works on them while
-  // this flush's output downloads and while the caller feeds the next reads: the next
-  // one's collected and its output gather queued if its chain was begun in an earlier
-  // wait (its inflate ran meanwhile), else begun; the one after it begun (inflate +
-  // validator launched, not waited for).  A chain is begun from its flush's decode
-  // results, so those are waited for (one flush's decode: short).
+  // this flush's output downloads and while the caller feeds the next reads.  A chain
+  // starts from the one before it (the frames of a message it left open, the sessions
+  // a stage closed): it is begun only once its predecessor is collected.  So with a
+  // flush behind the next one, the next one is collected and its output gather queued
+  // (its inflate, begun in an earlier wait, ran meanwhile), then the one after it is
+  // begun (inflate + validator launched, not waited for); the last flush in flight is
+  // only begun.  A chain is begun from its flush's decode results, so those are waited
+  // for (one flush's decode: short).
   for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
     FlushSlot& g = b->fs[b->q[qi]];
     if (g.so.staged) continue;
-    std::vector<wsg_session_result> gres;
     if (!g.ij.active) {
       B_TRY(b, hipEventSynchronize(g.done));
+      std::vector<wsg_session_result> gres;
       adjusted_results(b, g, gres);
       if ((rc2 = stage_begin(b, g, gres.data()))) return rc2;
-    } else if (qi == 0 && b->q.size() > 1) {
-      if ((rc2 = stage_compute(b, g, nullptr))) return rc2;
     }
+    if (qi + 1 == b->q.size() || qi == 1) break;  // the last one: begun only
+    if ((rc2 = stage_compute(b, g, nullptr))) return rc2;
   }
   if ((rc2 = stage_finish(b, f))) return rc2;
   StageOut& o = f.so;
