@@ -47,11 +47,11 @@
 #ifdef WSG_STAGE_PROF
 #include <chrono>
 #include <cstdio>
-static double g_sp[16];
-static const char* g_sp_name[16] = {"compute", "inflate.input", "inflate.kernels+sync", "inflate.results",
+static double g_sp[20];
+static const char* g_sp_name[20] = {"compute", "inflate.input", "inflate.kernels+sync", "inflate.results",
                                     "validate", "aggregate", "fin.list", "gather.launch", "finish.sync", "wait.total",
                                     "precompute", "gather.pay_ensure", "gather.upload", "inflate.x", "inflate.launch",
-                                    "validate.sync"};
+                                    "validate.sync", "upload.memcpy", "upload.h2d", "begin", "fin.build"};
 struct SpT {
   int i;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
@@ -540,7 +540,11 @@ static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
   hipError_t e = d.ensure(bytes + sizeof(T));
   if (e == hipSuccess) e = d.up.ensure(bytes + sizeof(T));
   if (e != hipSuccess || v.empty()) return e;
-  memcpy(d.up.p, v.data(), bytes);
+  {
+    SP(16);
+    memcpy(d.up.p, v.data(), bytes);
+  }
+  SP(17);
   return hipMemcpyAsync(d.p, d.up.p, bytes, hipMemcpyHostToDevice, s);
 }
 
@@ -904,7 +908,7 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
 // decoder's delivered frames (their payloads still on the device, f.dpay), and the
 // inflate + validator launched on the stage stream (no wait: stage_compute collects).
 static int stage_begin(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
-  SP(0);
+  SP(18);
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
   StageOut& o = f.so;
@@ -976,6 +980,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   if (b->stages.aggregate) {
     if ((rc = stage_aggregate(b, cur, used))) return rc;
   } else {
+    SP(19);
     for (uint32_t s = 0; s < S; ++s) {
       o.sf[s] = (uint32_t)o.desc.size();
       for (uint32_t k = cur.sf[s]; k < cur.sf[s] + cur.n_ok[s]; ++k)
@@ -1079,7 +1084,7 @@ int wsg_batcher_close(wsg_batcher* b) {
   }
   if (b->sctx) (void)wsg_close(b->sctx);
 #ifdef WSG_STAGE_PROF
-  for (int i = 0; i < 16; ++i)
+  for (int i = 0; i < 20; ++i)
     if (g_sp[i] > 0) fprintf(stderr, "[stage prof] %-22s %9.3f ms\n", g_sp_name[i], g_sp[i]);
 #endif
   delete b;
