@@ -87,6 +87,7 @@ struct wsg_ctx {
   int agg_units = 2;                 // WSG_TUNE_AGG_UNITS: k_agg_gather units per wave (1, 2 or 4)
   uint32_t agg_grid = 65536;         // WSG_TUNE_AGG_GRID: k_agg_gather waves at most
   uint32_t agg_fold = 0xFFFFFFFFu;   // WSG_TUNE_AGG_FOLD_MAX: plan blocks folded at most (tests: 0 forces k_agg_scan)
+  uint64_t tok_frames = 0, tok_payload_len = 0;  // the last ws::inflate_tok_phase's list (its workspace's layout)
   // host-path device buffers
   DevBuf h_wire, h_off, h_sf, h_state, h_payload, h_desc, h_result, h_frames, h_closed, h_wire_off;
   // pipelined host path: copy-in / copy-out streams and two staging slots
@@ -188,6 +189,8 @@ void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src) {
   dst->agg_fold = src->agg_fold;
 }
 int ctx_device(wsg_ctx* c) { return c->device; }
+// the batcher's two-phase inflate applies (the pre-decode on, the split-lane decode off)
+bool ctx_inflate_two_phase(const wsg_ctx* c) { return c->infl_tokens && c->infl_split == 0; }
 uint8_t* ctx_async_payload(wsg_ctx* c) { return c->last_async_payload; }
 }  // namespace ws
 
@@ -1002,14 +1005,14 @@ int wsg_aggregate_batch_host(wsg_ctx* c, int64_t max_aggregated_len, const wsg_f
   return WSG_API_OK;
 }
 
-int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
-                             const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
-                             uint64_t payload_len, wsg_inflate_state* state, uint8_t* window, uint8_t* out,
-                             const uint64_t* out_off, wsg_frame_desc* out_desc, wsg_session_result* out_result,
-                             uint32_t* replay_from) {
-  if (!c) return WSG_API_EINVAL;
-  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
-  HIP_TRY(c, hipSetDevice(c->device));
+}  // extern "C" (reopened below)
+
+// The arguments of an inflate launch sequence with no pre-decode attached.
+static InflArgs infl_args(wsg_ctx* c, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                          const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                          uint64_t payload_len, wsg_inflate_state* state, uint8_t* window, uint8_t* out,
+                          const uint64_t* out_off, wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                          uint32_t* replay_from) {
   InflArgs a;
   a.no_context = no_context != 0;
   a.desc = desc;
@@ -1041,31 +1044,98 @@ int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* d
   a.split_cnt = nullptr;
   a.tok2 = nullptr;
   a.lit2 = nullptr;
-  if (c->infl_tokens && n_frames) {
-    const uint32_t lanes = (uint32_t)infl_lane_count(c, n_frames);
-    const uint64_t lit_len = infl_lit_bytes(payload_len, n_frames);
-    const int rc = ensure_inflate_ws(c, n_frames, payload_len);
-    if (rc) return rc;
-    const uint32_t n_tab = lanes < c->infl_tabs ? lanes : c->infl_tabs;
-    HIP_TRY(c, hipMemsetAsync(c->i_tabcnt.p, 0, sizeof(uint32_t), c->stream));
-    a.tok = (uint32_t*)c->i_tok.p;
-    a.lit = (uint8_t*)c->i_lit.p;
-    a.lit_len = lit_len;
-    a.tstat = (InflTokStat*)c->i_stat.p;
-    a.tab = (uint8_t*)c->i_tab.p;
-    a.n_tab = n_tab;
-    a.tab_cnt = (uint32_t*)c->i_tabcnt.p;
-    a.n_lanes = lanes;
-    a.split = infl_pairs(c, n_frames) ? 1 : 0;
-    a.tok2 = (uint32_t*)c->i_tok2.p;
-    a.lit2 = (uint8_t*)c->i_lit2.p;
-    a.split_cnt = (unsigned long long*)c->i_split.p;
-    a.order = nullptr;
-    a.ord_cnt = nullptr;
-    if (c->infl_order) {
-      a.order = (uint32_t*)c->i_ord.p;
-      a.ord_cnt = a.order + n_frames;
+  a.tmap = nullptr;
+  return a;
+}
+
+// The pre-decode's workspace on c for a list of n_frames frames over payload_len bytes.
+static int infl_tok_args(wsg_ctx* c, InflArgs& a, uint64_t n_frames, uint64_t payload_len) {
+  const uint32_t lanes = (uint32_t)infl_lane_count(c, n_frames);
+  const int rc = ensure_inflate_ws(c, n_frames, payload_len);
+  if (rc) return rc;
+  a.tok = (uint32_t*)c->i_tok.p;
+  a.lit = (uint8_t*)c->i_lit.p;
+  a.lit_len = infl_lit_bytes(payload_len, n_frames);
+  a.tstat = (InflTokStat*)c->i_stat.p;
+  a.tab = (uint8_t*)c->i_tab.p;
+  a.n_tab = lanes < c->infl_tabs ? lanes : c->infl_tabs;
+  a.tab_cnt = (uint32_t*)c->i_tabcnt.p;
+  a.n_lanes = lanes;
+  a.split = infl_pairs(c, n_frames) ? 1 : 0;
+  a.tok2 = (uint32_t*)c->i_tok2.p;
+  a.lit2 = (uint8_t*)c->i_lit2.p;
+  a.split_cnt = (unsigned long long*)c->i_split.p;
+  a.order = nullptr;
+  a.ord_cnt = nullptr;
+  if (c->infl_order) {
+    a.order = (uint32_t*)c->i_ord.p;
+    a.ord_cnt = a.order + n_frames;
+  }
+  return WSG_API_OK;
+}
+
+namespace ws {
+int inflate_tok_phase(wsg_ctx* c, const wsg_frame_desc* desc, uint64_t n_frames, const uint32_t* session_first,
+                      uint32_t n_sessions, const uint8_t* payload, uint64_t payload_len) {
+  if (!c) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  c->tok_frames = n_frames;
+  c->tok_payload_len = payload_len;
+  if (!n_frames || !c->infl_tokens) return WSG_API_OK;
+  InflArgs a = infl_args(c, 0, desc, n_frames, session_first, n_sessions, payload, payload_len, nullptr, nullptr,
+                         nullptr, nullptr, nullptr, nullptr, nullptr);
+  const int rc = infl_tok_args(c, a, n_frames, payload_len);
+  if (rc) return rc;
+  HIP_TRY(c, hipMemsetAsync(c->i_tabcnt.p, 0, sizeof(uint32_t), c->stream));
+  timed(c, K_INFL_TOK, [&] { launch_infl_tok(a, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+
+int inflate_replay_phase(wsg_ctx* c, wsg_ctx* tokc, const uint32_t* tmap, int no_context, const wsg_frame_desc* desc,
+                         uint64_t n_frames, const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                         uint64_t payload_len, wsg_inflate_state* state, uint8_t* window, uint8_t* out,
+                         const uint64_t* out_off, wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                         uint32_t* replay_from) {
+  if (!c || !tokc) return WSG_API_EINVAL;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  InflArgs a = infl_args(c, no_context, desc, n_frames, session_first, n_sessions, payload, payload_len, state, window,
+                         out, out_off, out_desc, out_result, replay_from);
+  if (tokc->infl_tokens && tokc->tok_frames && n_frames) {  // the pre-decode tokc ran (its layout)
+    a.tok = (uint32_t*)tokc->i_tok.p;
+    a.lit = (uint8_t*)tokc->i_lit.p;
+    a.lit_len = infl_lit_bytes(tokc->tok_payload_len, tokc->tok_frames);
+    a.tstat = (InflTokStat*)tokc->i_stat.p;
+    a.tmap = tmap;
+    if (c->infl_fast) {
+      HIP_TRY(c, c->i_fast.ensure(n_sessions));
+      a.fast_done = (uint8_t*)c->i_fast.p;
+      timed(c, K_INFL_FAST, [&] { launch_infl_fast(a, c->stream); });
     }
+  }
+  if (!(c->infl_fast == 2 && a.fast_done)) timed(c, K_INFLATE, [&] { launch_inflate(a, c->stream); });
+  HIP_TRY(c, hipGetLastError());
+  return WSG_API_OK;
+}
+}  // namespace ws
+
+extern "C" {
+
+int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                             uint64_t payload_len, wsg_inflate_state* state, uint8_t* window, uint8_t* out,
+                             const uint64_t* out_off, wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                             uint32_t* replay_from) {
+  if (!c) return WSG_API_EINVAL;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  HIP_TRY(c, hipSetDevice(c->device));
+  InflArgs a = infl_args(c, no_context, desc, n_frames, session_first, n_sessions, payload, payload_len, state, window,
+                         out, out_off, out_desc, out_result, replay_from);
+  if (c->infl_tokens && n_frames) {
+    const int rc = infl_tok_args(c, a, n_frames, payload_len);
+    if (rc) return rc;
+    HIP_TRY(c, hipMemsetAsync(c->i_tabcnt.p, 0, sizeof(uint32_t), c->stream));
     timed(c, K_INFL_TOK, [&] { launch_infl_tok(a, c->stream); });
     if (c->infl_fast) {
       HIP_TRY(c, c->i_fast.ensure(n_sessions));  // (sessions: not covered by wsg_reserve_inflate)

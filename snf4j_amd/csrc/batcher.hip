@@ -430,7 +430,12 @@ struct StageOut {
 // A flush's stage chain between its start and its collection (stage_begin ->
 // stage_compute): the stage input, and the inflate attempt in flight.
 struct InflJob {
-  bool active = false;               // begun: the input built (and the inflate launched)
+  bool prepped = false;              // the input built (and, two-phase, its pre-decode launched)
+  bool active = false;               // begun: the inflate replay launched
+  std::vector<wsg_session_result> res;  // the decode results the input was built from
+  int tc = -1;                       // two-phase: the pre-decode's context (b->tctx[tc])
+  hipEvent_t tok_done = nullptr;     //   after its pre-decode
+  std::vector<uint32_t> tmap;        //   the attempt's frame -> its index in cur (the pre-decode's list)
   StageList cur;                     // the stage input, then (after inflate) its output
   uint64_t used = 0;                 // the arena's extent so far
   StageList x;                       // the inflate attempt in flight
@@ -501,6 +506,12 @@ struct wsg_batcher {
                        // inflated | aggregated)
   DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot;
   DBuf d_nheld, d_vdesc, d_vres;        // the validator's input made on the device, its results
+  // two-phase inflate: a flush's message-parallel pre-decode runs on one of two contexts
+  // of its own (flush t on tctx[t % 2]) as soon as its decode is done, ahead of the
+  // previous flush's replay; the replay reads it through d_tmap
+  bool two_phase = false;
+  wsg_ctx* tctx[2] = {nullptr, nullptr};
+  DBuf d_tdesc[2], d_tsf[2], d_tmap;
   PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot, h_vres;  // stage results downloaded
   PinnedBuf h_pend;                     // aggregator bytes held for the next flush, downloaded
   DBuf d_pend;
@@ -567,6 +578,7 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
   StageList& x = j.x;
   x.sf.assign(S + 1, 0);
   x.desc.clear();
+  j.tmap.clear();
   j.oo.assign(S + 1, 0);
   std::fill(j.nheld.begin(), j.nheld.end(), 0u);  // (this attempt's sessions set theirs)
   size_t ti = 0;
@@ -586,10 +598,12 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
         x.desc.push_back(d);
       }
       j.nheld[s] = (uint32_t)h.held_desc.size();
+      if (b->two_phase) j.tmap.insert(j.tmap.end(), h.held_desc.size(), 0xFFFFFFFFu);  // (not pre-decoded)
       for (uint32_t k = j.cur.sf[s]; k < j.cur.sf[s + 1]; ++k) {
         wsg_frame_desc d = j.cur.desc[k];
         d.flags &= (uint8_t)~WSG_DESC_REPLAY;
         x.desc.push_back(d);
+        if (b->two_phase) j.tmap.push_back((uint32_t)k);
       }
     }
   }
@@ -597,6 +611,8 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
   const uint64_t F = x.desc.size();
   const uint64_t ipos = j.ipos;
   DBuf& ar = f.dpay;
+  // (a move of the arena waits for the pre-decode reading it)
+  if (j.tc >= 0 && ipos + j.oo[S] + 64 > ar.n) B_TRY(b, hipEventSynchronize(j.tok_done));
   B_TRY(b, ar.grow_keep(ipos + j.oo[S] + 64, ipos, st));
   B_TRY(b, upload(b->d_desc, x.desc, st));
   B_TRY(b, upload(b->d_sf, x.sf, st));
@@ -604,11 +620,22 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
   B_TRY(b, b->d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
   B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
-  int rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
-                                    (const uint32_t*)b->d_sf.p, S, ar.p, ipos, (wsg_inflate_state*)b->d_istate.p,
-                                    b->d_iwin.p, ar.p + ipos, (const uint64_t*)b->d_ooff.p,
-                                    (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
-                                    (uint32_t*)b->d_rf.p);
+  int rc;
+  if (j.tc >= 0) {  // the replay of the pre-decode that ran on tctx[tc]
+    B_TRY(b, upload(b->d_tmap, j.tmap, st));
+    B_TRY(b, hipStreamWaitEvent(st, j.tok_done, 0));
+    rc = ws::inflate_replay_phase(b->sctx, b->tctx[j.tc], (const uint32_t*)b->d_tmap.p, b->stages.inflate_no_context,
+                                  (const wsg_frame_desc*)b->d_desc.p, F, (const uint32_t*)b->d_sf.p, S, ar.p, ipos,
+                                  (wsg_inflate_state*)b->d_istate.p, b->d_iwin.p, ar.p + ipos,
+                                  (const uint64_t*)b->d_ooff.p, (wsg_frame_desc*)b->d_odesc.p,
+                                  (wsg_session_result*)b->d_ores.p, (uint32_t*)b->d_rf.p);
+  } else {
+    rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
+                                  (const uint32_t*)b->d_sf.p, S, ar.p, ipos, (wsg_inflate_state*)b->d_istate.p,
+                                  b->d_iwin.p, ar.p + ipos, (const uint64_t*)b->d_ooff.p,
+                                  (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
+                                  (uint32_t*)b->d_rf.p);
+  }
   if (rc) return bset(b, rc, wsg_last_error(b->sctx));
   // FrameUtf8Validator right behind it on the device (PerMessageDeflateExtension.java:
   // 316-326): its input made from inflate's output by k_stage_vprep, no host hop
@@ -657,9 +684,11 @@ static int infl_begin(wsg_batcher* b, FlushSlot& f) {
   j.od_at.assign(S, 0);
   j.od_n.assign(S, 0);
   j.in_order = true;
-  // the held frames' bytes go after the decoded payloads
+  // the held frames' bytes go after the decoded payloads; sessions a stage closed or a
+  // reset gave to a new session since the input was built take no part
   uint64_t hpos = j.used;
   for (uint32_t s = 0; s < S; ++s) {
+    if (b->stage_closed[s] || std::find(f.resets.begin(), f.resets.end(), s) != f.resets.end()) continue;
     const StageSess& h = b->ss[s];
     uint64_t c = 0;
     if (!h.held_desc.empty()) {
@@ -672,8 +701,10 @@ static int infl_begin(wsg_batcher* b, FlushSlot& f) {
     j.todo.push_back(s);
     j.cap[s] = al16(4096 + 8 * c);
   }
+  if (j.tc >= 0 && hpos + 64 > f.dpay.n) B_TRY(b, hipEventSynchronize(j.tok_done));
   B_TRY(b, f.dpay.grow_keep(hpos + 64, f.pcap, st));
   for (uint32_t s = 0; s < S; ++s) {
+    if (b->stage_closed[s] || std::find(f.resets.begin(), f.resets.end(), s) != f.resets.end()) continue;
     const StageSess& h = b->ss[s];
     if (!h.held_bytes.empty())
       B_TRY(b, hipMemcpyAsync(f.dpay.p + j.held_at[s], h.held_bytes.data(), h.held_bytes.size(),
@@ -903,38 +934,17 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
   return WSG_API_OK;
 }
 
-// The stage chain of a flush whose decode is done, begun: the output reset, the stage
-// carry of slots handed to new sessions zeroed, the stage input built from the
-// decoder's delivered frames (their payloads still on the device, f.dpay), and the
-// inflate + validator launched on the stage stream (no wait: stage_compute collects).
-static int stage_begin(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
-  SP(18);
+// A flush's stage input, built once its decode is done: the decoder's delivered frames
+// (their payloads still on the device, f.dpay).  Two-phase inflate: the message-parallel
+// pre-decode of those frames launched on the flush's own context (it needs no inflater
+// state: it runs ahead of the previous flush's replay, while the host collects that one).
+static int stage_prep(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
   const uint32_t S = b->n;
-  hipStream_t st = ws::ctx_stream(b->sctx);
-  StageOut& o = f.so;
-  b->out = &o;
-  o.res.assign(res, res + S);
-  o.sf.assign(S + 1, 0);
-  o.desc.clear();
-  o.copies.clear();
-  o.host_parts.clear();
-  o.len = 0;
-  if (!b->stage_resets.empty()) {  // sessions handed to new sessions since the last run
-    B_TRY(b, upload(b->d_resets, b->stage_resets, st));
-    hipLaunchKernelGGL(k_stage_reset, dim3((uint32_t)b->stage_resets.size()), dim3(256), 0, st,
-                       (const uint32_t*)b->d_resets.p, (wsg_inflate_state*)b->d_istate.p, b->d_iwin.p,
-                       (wsg_session_state*)b->d_vstate.p, (wsg_agg_state*)b->d_astate.p);
-    B_TRY(b, hipGetLastError());
-    B_TRY(b, hipStreamSynchronize(st));  // (d_resets is reused)
-    b->stage_resets.clear();
-  }
-  // a session a stage failed in an earlier flush is closed (InternalSession.controlClose):
-  // the frames decoded for it in flushes already in flight reach no stage and no handler
-  for (uint32_t s = 0; s < S; ++s)
-    if (b->stage_closed[s]) o.res[s] = wsg_session_result{};
+  InflJob& j = f.ij;
+  j.res.assign(res, res + S);
   const uint32_t* sf = (const uint32_t*)f.sf.p;
   const wsg_frame_desc* desc = (const wsg_frame_desc*)f.desc.p;
-  StageList& cur = f.ij.cur;
+  StageList& cur = j.cur;
   cur.sf.assign(S + 1, 0);
   cur.n_ok.assign(S, 0);
   cur.desc.clear();
@@ -952,6 +962,58 @@ static int stage_begin(wsg_batcher* b, FlushSlot& f, const wsg_session_result* r
     }
   }
   cur.sf[S] = (uint32_t)cur.desc.size();
+  j.prepped = true;
+  j.tc = -1;
+  if (!b->two_phase || cur.desc.empty()) return WSG_API_OK;
+  j.tc = (int)(f.ticket & 1u);
+  wsg_ctx* tc = b->tctx[j.tc];
+  hipStream_t ts = ws::ctx_stream(tc);
+  if (!j.tok_done) B_TRY(b, hipEventCreateWithFlags(&j.tok_done, hipEventDisableTiming));
+  B_TRY(b, upload(b->d_tdesc[j.tc], cur.desc, ts));
+  B_TRY(b, upload(b->d_tsf[j.tc], cur.sf, ts));
+  if (f.pcap) B_TRY(b, hipStreamWaitEvent(ts, f.dpay_done, 0));
+  const int rc = ws::inflate_tok_phase(tc, (const wsg_frame_desc*)b->d_tdesc[j.tc].p, cur.desc.size(),
+                                       (const uint32_t*)b->d_tsf[j.tc].p, S, f.dpay.p, al16(f.pcap));
+  if (rc) return bset(b, rc, wsg_last_error(tc));
+  B_TRY(b, hipEventRecord(j.tok_done, ts));
+  return WSG_API_OK;
+}
+
+// The stage chain of a flush begun (its predecessor's chain collected): the output
+// reset, the stage carry of slots handed to new sessions zeroed, and the inflate (the
+// replay of its pre-decode, two-phase) + validator launched on the stage stream (no
+// wait: stage_compute collects).
+static int stage_begin(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
+  int rc;
+  if (!f.ij.prepped && (rc = stage_prep(b, f, res))) return rc;
+  SP(18);
+  const uint32_t S = b->n;
+  hipStream_t st = ws::ctx_stream(b->sctx);
+  StageOut& o = f.so;
+  b->out = &o;
+  o.res = f.ij.res;
+  o.sf.assign(S + 1, 0);
+  o.desc.clear();
+  o.copies.clear();
+  o.host_parts.clear();
+  o.len = 0;
+  if (!b->stage_resets.empty()) {  // sessions handed to new sessions since the last run
+    B_TRY(b, upload(b->d_resets, b->stage_resets, st));
+    hipLaunchKernelGGL(k_stage_reset, dim3((uint32_t)b->stage_resets.size()), dim3(256), 0, st,
+                       (const uint32_t*)b->d_resets.p, (wsg_inflate_state*)b->d_istate.p, b->d_iwin.p,
+                       (wsg_session_state*)b->d_vstate.p, (wsg_agg_state*)b->d_astate.p);
+    B_TRY(b, hipGetLastError());
+    B_TRY(b, hipStreamSynchronize(st));  // (d_resets is reused)
+    b->stage_resets.clear();
+  }
+  // a session a stage failed in an earlier flush is closed (InternalSession.controlClose):
+  // the frames decoded for it in flushes already in flight reach no stage and no handler;
+  // nor do a reset slot's old session's (also when the input was built before)
+  for (uint32_t s = 0; s < S; ++s)
+    if (b->stage_closed[s] || std::find(f.resets.begin(), f.resets.end(), s) != f.resets.end()) {
+      o.res[s] = wsg_session_result{};
+      f.ij.cur.n_ok[s] = 0;
+    }
   f.ij.used = al16(f.pcap);
   f.ij.todo.clear();
   f.ij.active = true;
@@ -975,6 +1037,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   b->ar = &f.dpay;
   if (b->stages.inflate && (rc = infl_collect(b, f))) return rc;
   f.ij.active = false;
+  f.ij.prepped = false;
   StageList& cur = f.ij.cur;
   const uint64_t used = f.ij.used;
   if (b->stages.aggregate) {
@@ -1058,6 +1121,8 @@ wsg_ctx* wsg_batcher_stage_context(wsg_batcher* b) { return b ? b->sctx : nullpt
 int wsg_batcher_close(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
   (void)wsg_sync(b->ctx);
+  for (wsg_ctx* t : b->tctx)
+    if (t) (void)wsg_sync(t);
   if (b->sctx) (void)wsg_sync(b->sctx);
   if (b->s_dl) (void)hipStreamSynchronize(b->s_dl);
   for (FlushSlot& f : b->fs) {
@@ -1070,6 +1135,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     if (f.so.downloaded) (void)hipEventDestroy(f.so.downloaded);
     if (f.done) (void)hipEventDestroy(f.done);
     if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
+    if (f.ij.tok_done) (void)hipEventDestroy(f.ij.tok_done);
   }
   b->st.release();
   DBuf* dbufs[] = {&b->d_pend, &b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->d_sf, &b->d_desc,
@@ -1083,6 +1149,12 @@ int wsg_batcher_close(wsg_batcher* b) {
     (void)hipStreamDestroy(b->s_dl);
   }
   if (b->sctx) (void)wsg_close(b->sctx);
+  for (int i = 0; i < 2; ++i) {
+    if (b->tctx[i]) (void)wsg_close(b->tctx[i]);
+    b->d_tdesc[i].release();
+    b->d_tsf[i].release();
+  }
+  b->d_tmap.release();
 #ifdef WSG_STAGE_PROF
   for (int i = 0; i < 20; ++i)
     if (g_sp[i] > 0) fprintf(stderr, "[stage prof] %-22s %9.3f ms\n", g_sp_name[i], g_sp[i]);
@@ -1458,15 +1530,20 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   // begun (inflate + validator launched, not waited for); the last flush in flight is
   // only begun.  A chain is begun from its flush's decode results, so those are waited
   // for (one flush's decode: short).
+  // (two-phase inflate: every queued flush's pre-decode is launched first — flush t's
+  // context was last used by flush t - 2, collected by now — so it runs meanwhile)
+  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
+    FlushSlot& g = b->fs[b->q[qi]];
+    if (g.so.staged || g.ij.prepped) continue;
+    B_TRY(b, hipEventSynchronize(g.done));
+    std::vector<wsg_session_result> gres;
+    adjusted_results(b, g, gres);
+    if ((rc2 = stage_prep(b, g, gres.data()))) return rc2;
+  }
   for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
     FlushSlot& g = b->fs[b->q[qi]];
     if (g.so.staged) continue;
-    if (!g.ij.active) {
-      B_TRY(b, hipEventSynchronize(g.done));
-      std::vector<wsg_session_result> gres;
-      adjusted_results(b, g, gres);
-      if ((rc2 = stage_begin(b, g, gres.data()))) return rc2;
-    }
+    if (!g.ij.active && (rc2 = stage_begin(b, g, nullptr))) return rc2;
     if (qi + 1 == b->q.size() || qi == 1) break;  // the last one: begun only
     if ((rc2 = stage_compute(b, g, nullptr))) return rc2;
   }
@@ -1523,6 +1600,14 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
       if (rc) return bset(b, rc, "wsg_open (stage context)");
     }
     ws::ctx_copy_tuning(b->sctx, b->ctx);  // (the batcher context's switches hold for its stages)
+    b->two_phase = stages->inflate && ws::ctx_inflate_two_phase(b->ctx);
+    for (int i = 0; b->two_phase && i < 2; ++i) {  // the pre-decode contexts (stream + workspace each)
+      if (!b->tctx[i]) {
+        const int rc = wsg_open(ws::ctx_device(b->ctx), nullptr, &b->tctx[i]);
+        if (rc) return bset(b, rc, "wsg_open (pre-decode context)");
+      }
+      ws::ctx_copy_tuning(b->tctx[i], b->ctx);
+    }
     hipStream_t st = ws::ctx_stream(b->sctx);
     B_TRY(b, b->d_istate.ensure(((uint64_t)S + 1) * sizeof(wsg_inflate_state)));
     B_TRY(b, b->d_iwin.ensure(((uint64_t)S + 1) * WSG_INFLATE_WINDOW));
@@ -1634,6 +1719,18 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
   B_TRY(b, b->h_pend.ensure(maxo + 16 * S + 32));
   const int rc = ws::ctx_reserve_stages(b->sctx, F, (uint32_t)S, in_len + infl, agg);
   if (rc) return bset(b, rc, wsg_last_error(b->sctx));
+  for (int i = 0; b->two_phase && i < 2; ++i) {  // the pre-decodes: a flush's decoded frames and payloads
+    const int rc2 = wsg_reserve_inflate(b->tctx[i], Fi + 1, (uint32_t)S, al16(pcap));
+    if (rc2) return bset(b, rc2, wsg_last_error(b->tctx[i]));
+    B_TRY(b, b->d_tdesc[i].ensure((Fi + 2) * sizeof(wsg_frame_desc)));
+    B_TRY(b, b->d_tdesc[i].up.ensure((Fi + 2) * sizeof(wsg_frame_desc)));
+    B_TRY(b, b->d_tsf[i].ensure((S + 2) * sizeof(uint32_t)));
+    B_TRY(b, b->d_tsf[i].up.ensure((S + 2) * sizeof(uint32_t)));
+  }
+  B_TRY(b, b->d_tmap.ensure((F + 1) * sizeof(uint32_t)));
+  B_TRY(b, b->d_tmap.up.ensure((F + 1) * sizeof(uint32_t)));
+  for (FlushSlot& f : b->fs)
+    if (!f.ij.tok_done) B_TRY(b, hipEventCreateWithFlags(&f.ij.tok_done, hipEventDisableTiming));
   B_TRY(b, hipStreamSynchronize(st));
   return WSG_API_OK;
 }

@@ -1818,15 +1818,16 @@ __global__ __launch_bounds__(64) void k_inflate(InflArgs a) {
       // A single-frame message met in the clean state k_infl_tok assumed: replay its
       // tokens instead of decoding.
       bool tok_use = false;
-      if (a.tstat && !finished && !compressing && fin && !replay && (op == WSG_OP_TEXT || op == WSG_OP_BINARY) &&
-          mode == M_HEAD && bits == 0 && !last)
-        tok_use = uni(a.tstat[k].ok) != 0u;
+      const uint64_t tk = a.tmap ? (uint64_t)a.tmap[k] : k;  // frame k in the pre-decode's list
+      if (a.tstat && tk != 0xFFFFFFFFull && !finished && !compressing && fin && !replay &&
+          (op == WSG_OP_TEXT || op == WSG_OP_BINARY) && mode == M_HEAD && bits == 0 && !last)
+        tok_use = uni(a.tstat[tk].ok) != 0u;
       if (finished) {
         raw_rest();
       } else if (tok_use) {
-        const uint32_t n_tok = uni(a.tstat[k].n_tok), n_lit = uni(a.tstat[k].n_lit);
-        const uint32_t* const T = a.tok + tok_base(d.payload_off, k);
-        const uint64_t lb = lit_base(d.payload_off, k);
+        const uint32_t n_tok = uni(a.tstat[tk].n_tok), n_lit = uni(a.tstat[tk].n_lit);
+        const uint32_t* const T = a.tok + tok_base(d.payload_off, tk);
+        const uint64_t lb = lit_base(d.payload_off, tk);
         uint32_t li = 0, lw_lo = 0, lw_hi = 0, lw_off = 0;  // ibuf holds literal bytes [lw_lo, lw_hi) from lw_off
         auto lit_stage = [&](uint32_t i) {
           const uint64_t g = lb + i;
@@ -2430,7 +2431,9 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
     }
     if (start && compressing) { bad = true; break; }
     // the message's pre-decode (its start frame's lane wrote every frame's stats)
-    const InflTokStat ts = a.tstat[k];
+    const uint64_t tk = a.tmap ? (uint64_t)a.tmap[k] : k;  // frame k in the pre-decode's list
+    if (tk == 0xFFFFFFFFull) { bad = true; break; }
+    const InflTokStat ts = a.tstat[tk];
     if (!ts.ok || !ts.out_len || (int64_t)pos + ts.out_len > ocap) { bad = true; break; }
     if (!has_dec) {  // new ZlibDecoder(RAW): a fresh history (DeflateDecoder.java:80-93)
       has_dec = 1;
@@ -2438,8 +2441,8 @@ __global__ __launch_bounds__(FNT) __attribute__((amdgpu_waves_per_eu(WSG_FAST_WA
     }
     const int32_t P0 = pos;
     const uint32_t L = ts.out_len, n_tok = ts.n_tok;
-    const uint32_t* const T = a.tok + tok_base(d.payload_off, k);
-    const uint8_t* const lit = a.lit + lit_base(d.payload_off, k);
+    const uint32_t* const T = a.tok + tok_base(d.payload_off, tk);
+    const uint8_t* const lit = a.lit + lit_base(d.payload_off, tk);
     uint32_t tt = 0, t_off = 0, t_li = 0;  // the first token not fully emitted: index, output offset, literal index
     uint32_t l_first = 0;                  // the index of the chunk's first literal
     for (uint32_t c0 = 0; c0 < L && !bad; c0 += FC) {

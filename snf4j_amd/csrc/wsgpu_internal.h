@@ -215,6 +215,8 @@ struct InflArgs {
   uint32_t* tok2;             // the split's tail regions (laid out as tok / lit)
   uint8_t* lit2;
   unsigned long long* split_cnt;  // [1] messages a split decoded (accumulates), or null
+  const uint32_t* tmap;       // [n_frames] frame k's index in the pre-decode's own frame list (the
+                              // batcher's two-phase inflate: ~0u = not pre-decoded), or null: k
 };
 
 struct InflTokStat {
@@ -239,10 +241,24 @@ hipStream_t ctx_stream(wsg_ctx* c);
 hipStream_t ctx_out_stream(wsg_ctx* c);
 void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src);  // where ctx_record_out records (the download stream)
 int ctx_device(wsg_ctx* c);
+bool ctx_inflate_two_phase(const wsg_ctx* c);
 uint8_t* ctx_async_payload(wsg_ctx* c);
 uint64_t ctx_alloc_count();  // device workspace allocations of every context so far
 int ctx_reserve_stages(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t payload_len,
                        uint64_t agg_cap);
+// permessage-deflate in two phases (the batcher's pipelined stage chain): the message-
+// parallel pre-decode of a flush's frames on context `tokc` (k_infl_tok; it needs no
+// inflater state, so it runs ahead of the previous flush's replay), then the replay and
+// the serial decoder on context c over a frame list whose frame k is the pre-decode's
+// frame tmap[k] (the list may add replayed frames); tokc's workspace must hold that
+// pre-decode until the replay has run (its stream ordered after tokc's by the caller).
+int inflate_tok_phase(wsg_ctx* tokc, const wsg_frame_desc* desc, uint64_t n_frames, const uint32_t* session_first,
+                      uint32_t n_sessions, const uint8_t* payload, uint64_t payload_len);
+int inflate_replay_phase(wsg_ctx* c, wsg_ctx* tokc, const uint32_t* tmap, int no_context, const wsg_frame_desc* desc,
+                         uint64_t n_frames, const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                         uint64_t payload_len, wsg_inflate_state* state, uint8_t* window, uint8_t* out,
+                         const uint64_t* out_off, wsg_frame_desc* out_desc, wsg_session_result* out_result,
+                         uint32_t* replay_from);
 
 void launch_parse(const DecodeArgs& a, hipStream_t s);
 void launch_scan(const DecodeArgs& a, hipStream_t s);
