@@ -343,6 +343,9 @@ def main():
         extras = [config0_line()] + measure_extras(ctx, dev, args)
         if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
             e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 1)
+            # the same sessions streaming 4x longer: the pipeline's fill and drain (a pass of
+            # 5 flushes spends 2-3 of them filling and draining) amortised over ~20 flushes
+            e2e["native_batcher_stages_steady"] = e2e_stages_line(ctx, dev, 2, 1, msgs=64)
             e2e["native_encode_batcher"] = e2e_encode_line(ctx, dev, 3, 1)
             e2e["native_batcher_aggregate"] = e2e_aggregate_line(ctx, dev, 3, 1)
 
@@ -1113,6 +1116,7 @@ def e2e_aggregate_line(ctx, dev, K, W, chunk=65536):
 
 EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2": line_configs2,
                "encode": line_encode, "validator": line_validator, "e2e_stages": e2e_stages_line,
+               "e2e_stages_steady": lambda ctx, dev, K, W: e2e_stages_line(ctx, dev, K, W, msgs=64),
                "e2e_encode": e2e_encode_line, "e2e_aggregate": e2e_aggregate_line,
                "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
                "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W),
