@@ -1276,7 +1276,8 @@ def e2e_loop_line(pctx, rounds, wire_bytes, F, n_s):
     best = None
     for rnd in range(3):  # round 0 warms up; the best of two timed rounds
         loop = SelectorLoop()
-        lb = LoopBatcher(loop, n_s, deliver, ctx=pctx, raw=True, max_wire=max_wire, max_frames=max_frames)
+        lb = LoopBatcher(loop, n_s, deliver, ctx=pctx, raw=True, max_wire=max_wire, max_frames=max_frames,
+                         max_inflight=BATCHER_MAX_INFLIGHT)
         got["wire"] = got["frames"] = 0
         t0 = time.perf_counter()
         for sids, ptrs, lens in rounds:

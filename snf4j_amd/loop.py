@@ -114,8 +114,10 @@ class LoopBatcher:
 
     def __init__(self, loop: SelectorLoop, n_sessions: int, deliver, ctx=None, clientMode: bool = False,
                  allowExtensions: bool = False, maxPayloadLen: int = 65536, validate_utf8: bool = True,
-                 max_wire: int = 0, max_frames: int = 0, raw: bool = False):
+                 max_wire: int = 0, max_frames: int = 0, raw: bool = False,
+                 max_inflight: int = BATCHER_MAX_INFLIGHT):
         self.loop = loop
+        self.max_inflight = max_inflight  # (WsgBatcher: Wsg.BATCHER_MAX_INFLIGHT)
         self.nb = NativeBatcher(n_sessions, clientMode, allowExtensions, maxPayloadLen, validate_utf8, ctx=ctx)
         if max_wire:
             self.nb.reserve(max_wire, max_frames)
@@ -181,7 +183,7 @@ class LoopBatcher:
         self.collect_ready()
         if not fed:  # (the reads went with a drain)
             return
-        if len(self.inflight) == BATCHER_MAX_INFLIGHT:
+        if len(self.inflight) == self.max_inflight:
             self._collect_oldest(blocking=True)
         self.nb.flush_async()
         t = self.nb.ticket()

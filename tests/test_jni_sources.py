@@ -139,7 +139,7 @@ def test_loop_scheduling_matches_the_python_restatement():
     ready = _body(b, "private void collectReady(Native n)", "private void collectReady(EncNative n)")
     assert "Wsg.batcherAwait(n.handle, 0, 0)" in ready
     loop = _read("snf4j_amd/loop.py")
-    for x in ("feed_many", "collect_ready()", "len(self.inflight) == BATCHER_MAX_INFLIGHT", "flush_async()", "ticket()",
+    for x in ("feed_many", "collect_ready()", "len(self.inflight) == self.max_inflight", "flush_async()", "ticket()",
               "_completion.watch(t)", "await_done(0, 0)", "executenf(self.task)"):
         assert x in loop, x
 
