@@ -510,6 +510,11 @@ struct wsg_batcher {
   // of its own (flush t on tctx[t % 2]) as soon as its decode is done, ahead of the
   // previous flush's replay; the replay reads it through d_tmap
   bool two_phase = false;
+#ifdef WSG_NO_STAGE_EARLY
+  bool stage_early = false;  // (A/B build: the chains start from wsg_batcher_wait only)
+#else
+  bool stage_early = true;   // stage_advance from flush_async
+#endif
   wsg_ctx* tctx[2] = {nullptr, nullptr};
   DBuf d_tdesc[2], d_tsf[2], d_tmap;
   PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot, h_vres;  // stage results downloaded
@@ -1366,6 +1371,39 @@ static int stage_state(wsg_batcher* b) {
   return WSG_API_OK;
 }
 
+// The queued flushes' stage chains started without blocking, from flush_async: the
+// oldest flush whose predecessor is collected is begun once its decode is done (the
+// replay + validator launched), the next one's pre-decode launched, so that the device
+// inflates while the caller feeds the following reads instead of from the first
+// wsg_batcher_wait on (a pipeline WSG_BATCHER_MAX_INFLIGHT flushes deep otherwise
+// starts inflating only when it is full).  A decode not done yet is left to wait.
+static void adjusted_results(wsg_batcher* b, const FlushSlot& g, std::vector<wsg_session_result>& r);
+static int stage_advance(wsg_batcher* b) {
+  bool pred_collected = true;  // (the flush before q[0] is)
+  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
+    FlushSlot& g = b->fs[b->q[qi]];
+    if (g.so.staged) {
+      pred_collected = true;
+      continue;
+    }
+    if (!g.ij.prepped) {
+      const hipError_t e = hipEventQuery(g.done);
+      if (e == hipErrorNotReady) break;
+      B_TRY(b, e);
+      std::vector<wsg_session_result> gres;
+      adjusted_results(b, g, gres);
+      int rc = stage_prep(b, g, gres.data());
+      if (rc) return rc;
+    }
+    if (pred_collected && !g.ij.active) {
+      int rc = stage_begin(b, g, nullptr);
+      if (rc) return rc;
+    }
+    pred_collected = false;
+  }
+  return WSG_API_OK;
+}
+
 int wsg_batcher_flush_async(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
   if (b->q.size() >= WSG_BATCHER_MAX_INFLIGHT)
@@ -1445,6 +1483,7 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     g.fo[i].clear();
     g.fb[i] = 0;
   }
+  if (b->has_stages && b->stage_early) return stage_advance(b);
   return WSG_API_OK;
 }
 
