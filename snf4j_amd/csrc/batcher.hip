@@ -435,6 +435,7 @@ struct InflJob {
   std::vector<wsg_session_result> res;  // the decode results the input was built from
   int tc = -1;                       // two-phase: the pre-decode's context (b->tctx[tc])
   hipEvent_t tok_done = nullptr;     //   after its pre-decode
+  hipEvent_t launched = nullptr;     // after the attempt in flight (its result downloads)
   std::vector<uint32_t> tmap;        //   the attempt's frame -> its index in cur (the pre-decode's list)
   StageList cur;                     // the stage input, then (after inflate) its output
   uint64_t used = 0;                 // the arena's extent so far
@@ -514,6 +515,11 @@ struct wsg_batcher {
   bool stage_early = false;  // (A/B build: the chains start from wsg_batcher_wait only)
 #else
   bool stage_early = true;   // stage_advance from flush_async
+#endif
+#ifdef WSG_STAGE_LAZY
+  bool stage_lazy = true;    // (A/B build) wsg_batcher_wait blocks on its own flush only
+#else
+  bool stage_lazy = false;
 #endif
   wsg_ctx* tctx[2] = {nullptr, nullptr};
   DBuf d_tdesc[2], d_tsf[2], d_tmap;
@@ -671,6 +677,8 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
     B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
     B_TRY(b, hipMemcpyAsync(b->h_vres.p, b->d_vres.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
   }
+  if (!j.launched) B_TRY(b, hipEventCreateWithFlags(&j.launched, hipEventDisableTiming));
+  B_TRY(b, hipEventRecord(j.launched, st));
   return WSG_API_OK;
 }
 
@@ -1141,6 +1149,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     if (f.done) (void)hipEventDestroy(f.done);
     if (f.dpay_done) (void)hipEventDestroy(f.dpay_done);
     if (f.ij.tok_done) (void)hipEventDestroy(f.ij.tok_done);
+    if (f.ij.launched) (void)hipEventDestroy(f.ij.launched);
   }
   b->st.release();
   DBuf* dbufs[] = {&b->d_pend, &b->d_resets, &b->d_istate, &b->d_iwin, &b->d_vstate, &b->d_astate, &b->d_sf, &b->d_desc,
@@ -1377,16 +1386,22 @@ static int stage_state(wsg_batcher* b) {
 // inflates while the caller feeds the following reads instead of from the first
 // wsg_batcher_wait on (a pipeline WSG_BATCHER_MAX_INFLIGHT flushes deep otherwise
 // starts inflating only when it is full).  A decode not done yet is left to wait.
+// Lazy collection (b->stage_lazy): a begun chain whose inflate is done is collected
+// here too (its output gather queued), and the one behind it begun — so wsg_batcher_wait
+// waits for its own flush only, and the caller's feeds overlap the device work.
 static void adjusted_results(wsg_batcher* b, const FlushSlot& g, std::vector<wsg_session_result>& r);
+static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res);
 static int stage_advance(wsg_batcher* b) {
   bool pred_collected = true;  // (the flush before q[0] is)
-  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
+  for (size_t qi = 0; qi < b->q.size() && qi < 3; ++qi) {
     FlushSlot& g = b->fs[b->q[qi]];
     if (g.so.staged) {
       pred_collected = true;
       continue;
     }
     if (!g.ij.prepped) {
+      // (its pre-decode context was flush t - 2's: that one must be collected)
+      if (qi >= 2 && !b->fs[b->q[qi - 2]].so.staged) break;
       const hipError_t e = hipEventQuery(g.done);
       if (e == hipErrorNotReady) break;
       B_TRY(b, e);
@@ -1398,6 +1413,15 @@ static int stage_advance(wsg_batcher* b) {
     if (pred_collected && !g.ij.active) {
       int rc = stage_begin(b, g, nullptr);
       if (rc) return rc;
+    }
+    if (b->stage_lazy && pred_collected && b->stages.inflate && g.ij.active) {
+      const hipError_t e = g.ij.todo.empty() ? hipSuccess : hipEventQuery(g.ij.launched);
+      if (e != hipErrorNotReady) {
+        B_TRY(b, e);
+        int rc = stage_compute(b, g, nullptr);
+        if (rc) return rc;
+        continue;  // (staged: the next one may begin)
+      }
     }
     pred_collected = false;
   }
@@ -1503,6 +1527,38 @@ static void adjusted_results(wsg_batcher* b, const FlushSlot& g, std::vector<wsg
   }
 }
 
+static int stage_advance_blocking(wsg_batcher* b) {
+  int rc;
+  // wsg_batcher_wait (eager mode): the chains of the flushes behind the one it collects,
+  // advanced — blocking — so that the device works on them while
+  // this flush's output downloads and while the caller feeds the next reads.  A chain
+  // starts from the one before it (the frames of a message it left open, the sessions
+  // a stage closed): it is begun only once its predecessor is collected.  So with a
+  // flush behind the next one, the next one is collected and its output gather queued
+  // (its inflate, begun in an earlier wait, ran meanwhile), then the one after it is
+  // begun (inflate + validator launched, not waited for); the last flush in flight is
+  // only begun.  A chain is begun from its flush's decode results, so those are waited
+  // for (one flush's decode: short).
+  // (two-phase inflate: every queued flush's pre-decode is launched first — flush t's
+  // context was last used by flush t - 2, collected by now — so it runs meanwhile)
+  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
+    FlushSlot& g = b->fs[b->q[qi]];
+    if (g.so.staged || g.ij.prepped) continue;
+    B_TRY(b, hipEventSynchronize(g.done));
+    std::vector<wsg_session_result> gres;
+    adjusted_results(b, g, gres);
+    if ((rc = stage_prep(b, g, gres.data()))) return rc;
+  }
+  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
+    FlushSlot& g = b->fs[b->q[qi]];
+    if (g.so.staged) continue;
+    if (!g.ij.active && (rc = stage_begin(b, g, nullptr))) return rc;
+    if (qi + 1 == b->q.size() || qi == 1) break;  // the last one: begun only
+    if ((rc = stage_compute(b, g, nullptr))) return rc;
+  }
+  return WSG_API_OK;
+}
+
 int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   SP(9);
   if (!b || !out) return WSG_API_EINVAL;
@@ -1560,32 +1616,9 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   if (!b->has_stages) return WSG_API_OK;
   int rc2 = f.so.staged ? WSG_API_OK : stage_compute(b, f, res);
   if (rc2) return rc2;
-  // The chains of the flushes behind this one, so that the device works on them while
-  // this flush's output downloads and while the caller feeds the next reads.  A chain
-  // starts from the one before it (the frames of a message it left open, the sessions
-  // a stage closed): it is begun only once its predecessor is collected.  So with a
-  // flush behind the next one, the next one is collected and its output gather queued
-  // (its inflate, begun in an earlier wait, ran meanwhile), then the one after it is
-  // begun (inflate + validator launched, not waited for); the last flush in flight is
-  // only begun.  A chain is begun from its flush's decode results, so those are waited
-  // for (one flush's decode: short).
-  // (two-phase inflate: every queued flush's pre-decode is launched first — flush t's
-  // context was last used by flush t - 2, collected by now — so it runs meanwhile)
-  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
-    FlushSlot& g = b->fs[b->q[qi]];
-    if (g.so.staged || g.ij.prepped) continue;
-    B_TRY(b, hipEventSynchronize(g.done));
-    std::vector<wsg_session_result> gres;
-    adjusted_results(b, g, gres);
-    if ((rc2 = stage_prep(b, g, gres.data()))) return rc2;
-  }
-  for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
-    FlushSlot& g = b->fs[b->q[qi]];
-    if (g.so.staged) continue;
-    if (!g.ij.active && (rc2 = stage_begin(b, g, nullptr))) return rc2;
-    if (qi + 1 == b->q.size() || qi == 1) break;  // the last one: begun only
-    if ((rc2 = stage_compute(b, g, nullptr))) return rc2;
-  }
+  rc2 = b->stage_lazy ? stage_advance(b)  // the chains behind it advanced as far as they are ready
+                      : stage_advance_blocking(b);
+  if (rc2) return rc2;
   if ((rc2 = stage_finish(b, f))) return rc2;
   StageOut& o = f.so;
   for (uint32_t sid : f.resets) o.res[sid] = wsg_session_result{};  // (also those reset after its stages ran)
@@ -1768,8 +1801,10 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
   }
   B_TRY(b, b->d_tmap.ensure((F + 1) * sizeof(uint32_t)));
   B_TRY(b, b->d_tmap.up.ensure((F + 1) * sizeof(uint32_t)));
-  for (FlushSlot& f : b->fs)
+  for (FlushSlot& f : b->fs) {
     if (!f.ij.tok_done) B_TRY(b, hipEventCreateWithFlags(&f.ij.tok_done, hipEventDisableTiming));
+    if (!f.ij.launched) B_TRY(b, hipEventCreateWithFlags(&f.ij.launched, hipEventDisableTiming));
+  }
   B_TRY(b, hipStreamSynchronize(st));
   return WSG_API_OK;
 }
