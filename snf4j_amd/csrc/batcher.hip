@@ -133,8 +133,11 @@ class Pool {
     for (auto& t : w_) t.join();
   }
   uint32_t size() const { return (uint32_t)w_.size() + 1; }
-  void run(uint32_t T, const std::function<void(uint32_t)>& fn) {
+  // fn(0..T-1) over the workers and the caller; `side`, if any, runs on the caller
+  // first, while the workers start on the jobs
+  void run(uint32_t T, const std::function<void(uint32_t)>& fn, const std::function<void()>* side = nullptr) {
     if (T <= 1 || w_.empty()) {
+      if (side) (*side)();
       for (uint32_t t = 0; t < T; ++t) fn(t);
       return;
     }
@@ -147,6 +150,7 @@ class Pool {
       ++gen_;
     }
     cv_.notify_all();
+    if (side) (*side)();
     work();
     std::unique_lock<std::mutex> l(m_);
     done_.wait(l, [this] { return left_ == 0; });
@@ -516,10 +520,10 @@ struct wsg_batcher {
 #else
   bool stage_early = true;   // stage_advance from flush_async
 #endif
-#ifdef WSG_STAGE_LAZY
-  bool stage_lazy = true;    // (A/B build) wsg_batcher_wait blocks on its own flush only
+#ifdef WSG_NO_FEED_ADVANCE
+  bool feed_advance = false;  // (A/B build)
 #else
-  bool stage_lazy = false;
+  bool feed_advance = true;   // stage_advance(collect) beside wsg_batcher_feed_many's copies
 #endif
   wsg_ctx* tctx[2] = {nullptr, nullptr};
   DBuf d_tdesc[2], d_tsf[2], d_tmap;
@@ -1274,6 +1278,8 @@ static void copy_to_arena(uint8_t* d, const uint8_t* s, uint64_t n) { memcpy(d, 
 // carried partial frame then its reads, copied there and framed in place by up to
 // 16 threads (the sessions are independent): the bytes are copied once, into
 // memory the DMA engines read.
+static int stage_advance(wsg_batcher* b, bool collect);
+
 int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, const uint8_t* const* data,
                           const uint64_t* lens) {
   if (!b || (n && (!sids || !data || !lens))) return WSG_API_EINVAL;
@@ -1348,9 +1354,18 @@ int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, cons
       while (i < R && rs[i + 1] <= target) ++i;
       cut[t] = i;
     }
-    b->pool->run(T, [&](uint32_t t) {
-      for (uint32_t i = cut[t]; i < cut[t + 1]; ++i) region(i);
-    });
+    int side_rc = WSG_API_OK;
+    const std::function<void()> side = [&] { side_rc = stage_advance(b, true); };
+    const bool adv = b->has_stages && b->stage_early && b->feed_advance && !b->q.empty();
+    b->pool->run(
+        T, [&](uint32_t t) {
+          for (uint32_t i = cut[t]; i < cut[t + 1]; ++i) region(i);
+        },
+        adv ? &side : nullptr);
+    if (side_rc) {
+      f.arena_len = pos;
+      return side_rc;
+    }
   }
   f.arena_len = pos;
   return WSG_API_OK;
@@ -1386,12 +1401,14 @@ static int stage_state(wsg_batcher* b) {
 // inflates while the caller feeds the following reads instead of from the first
 // wsg_batcher_wait on (a pipeline WSG_BATCHER_MAX_INFLIGHT flushes deep otherwise
 // starts inflating only when it is full).  A decode not done yet is left to wait.
-// Lazy collection (b->stage_lazy): a begun chain whose inflate is done is collected
-// here too (its output gather queued), and the one behind it begun — so wsg_batcher_wait
-// waits for its own flush only, and the caller's feeds overlap the device work.
+// With `collect` (from wsg_batcher_feed_many, on the calling thread while the pool's
+// workers copy the reads): a begun chain whose inflate is done is collected too (its
+// output gather queued), and the one behind it begun, so the chains move on during the
+// feeds instead of only inside wsg_batcher_wait.  (The stage chain touches none of what
+// the feed writes: the open slot, the sessions' carried input and host state.)
 static void adjusted_results(wsg_batcher* b, const FlushSlot& g, std::vector<wsg_session_result>& r);
 static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res);
-static int stage_advance(wsg_batcher* b) {
+static int stage_advance(wsg_batcher* b, bool collect) {
   bool pred_collected = true;  // (the flush before q[0] is)
   for (size_t qi = 0; qi < b->q.size() && qi < 3; ++qi) {
     FlushSlot& g = b->fs[b->q[qi]];
@@ -1414,7 +1431,7 @@ static int stage_advance(wsg_batcher* b) {
       int rc = stage_begin(b, g, nullptr);
       if (rc) return rc;
     }
-    if (b->stage_lazy && pred_collected && b->stages.inflate && g.ij.active) {
+    if (collect && pred_collected && b->stages.inflate && g.ij.active) {
       const hipError_t e = g.ij.todo.empty() ? hipSuccess : hipEventQuery(g.ij.launched);
       if (e != hipErrorNotReady) {
         B_TRY(b, e);
@@ -1507,7 +1524,7 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     g.fo[i].clear();
     g.fb[i] = 0;
   }
-  if (b->has_stages && b->stage_early) return stage_advance(b);
+  if (b->has_stages && b->stage_early) return stage_advance(b, false);
   return WSG_API_OK;
 }
 
@@ -1616,9 +1633,7 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   if (!b->has_stages) return WSG_API_OK;
   int rc2 = f.so.staged ? WSG_API_OK : stage_compute(b, f, res);
   if (rc2) return rc2;
-  rc2 = b->stage_lazy ? stage_advance(b)  // the chains behind it advanced as far as they are ready
-                      : stage_advance_blocking(b);
-  if (rc2) return rc2;
+  if ((rc2 = stage_advance_blocking(b))) return rc2;
   if ((rc2 = stage_finish(b, f))) return rc2;
   StageOut& o = f.so;
   for (uint32_t sid : f.resets) o.res[sid] = wsg_session_result{};  // (also those reset after its stages ran)
