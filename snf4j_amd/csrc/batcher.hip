@@ -119,6 +119,20 @@ uint64_t frame_total(const uint8_t* p) {
 // A persistent pool for the batcher's host work (feeds, the flush gather): creating
 // threads per call cost ~30 us each, per round.  run(T, fn) runs fn(0..T-1) on the
 // pool and the calling thread and returns when all are done.
+// The flushes in flight (the header's WSG_BATCHER_MAX_INFLIGHT; A/B builds may
+// override it, with bench.py's WSG_BENCH_INFLIGHT to match) and the two-phase inflate's
+// pre-decode contexts (flush t pre-decodes on context t % kTokCtx).
+#ifdef WSG_AB_INFLIGHT
+static constexpr int kInflight = WSG_AB_INFLIGHT;
+#else
+static constexpr int kInflight = WSG_BATCHER_MAX_INFLIGHT;
+#endif
+#ifdef WSG_AB_TOKCTX
+static constexpr int kTokCtx = WSG_AB_TOKCTX;
+#else
+static constexpr int kTokCtx = 2;
+#endif
+
 class Pool {
  public:
   explicit Pool(uint32_t n) {
@@ -490,7 +504,7 @@ struct wsg_batcher {
   std::vector<SessIn> s;
   std::vector<wsg_session_state> state;  // the carry as of the last waited flush (+ host changes)
   PinnedBuf st;                          // the carry the device batches chain through
-  FlushSlot fs[WSG_BATCHER_MAX_INFLIGHT + 1];  // one being fed, up to MAX_INFLIGHT in flight
+  FlushSlot fs[kInflight + 1];  // one being fed, up to MAX_INFLIGHT in flight
   int open = 0;                          // the slot feeds land in
   std::deque<int> q;                     // flushes in flight, oldest first
   std::vector<std::pair<uint32_t, int>> patch;  // host changes for the next batch's state: 0 reset, 1 closed
@@ -512,7 +526,7 @@ struct wsg_batcher {
   DBuf d_sf, d_desc, d_odesc, d_res, d_ores, d_rf, d_ooff, d_tot;
   DBuf d_nheld, d_vdesc, d_vres;        // the validator's input made on the device, its results
   // two-phase inflate: a flush's message-parallel pre-decode runs on one of two contexts
-  // of its own (flush t on tctx[t % 2]) as soon as its decode is done, ahead of the
+  // of its own (flush t on tctx[t % kTokCtx]) as soon as its decode is done, ahead of the
   // previous flush's replay; the replay reads it through d_tmap
   bool two_phase = false;
 #ifdef WSG_NO_STAGE_EARLY
@@ -525,8 +539,8 @@ struct wsg_batcher {
 #else
   bool feed_advance = true;   // stage_advance(collect) beside wsg_batcher_feed_many's copies
 #endif
-  wsg_ctx* tctx[2] = {nullptr, nullptr};
-  DBuf d_tdesc[2], d_tsf[2], d_tmap;
+  wsg_ctx* tctx[kTokCtx] = {};
+  DBuf d_tdesc[kTokCtx], d_tsf[kTokCtx], d_tmap;
   PinnedBuf h_odesc, h_ores, h_rf, h_astate, h_tot, h_vres;  // stage results downloaded
   PinnedBuf h_pend;                     // aggregator bytes held for the next flush, downloaded
   DBuf d_pend;
@@ -982,7 +996,7 @@ static int stage_prep(wsg_batcher* b, FlushSlot& f, const wsg_session_result* re
   j.prepped = true;
   j.tc = -1;
   if (!b->two_phase || cur.desc.empty()) return WSG_API_OK;
-  j.tc = (int)(f.ticket & 1u);
+  j.tc = (int)(f.ticket % kTokCtx);
   wsg_ctx* tc = b->tctx[j.tc];
   hipStream_t ts = ws::ctx_stream(tc);
   if (!j.tok_done) B_TRY(b, hipEventCreateWithFlags(&j.tok_done, hipEventDisableTiming));
@@ -1167,7 +1181,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     (void)hipStreamDestroy(b->s_dl);
   }
   if (b->sctx) (void)wsg_close(b->sctx);
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < kTokCtx; ++i) {
     if (b->tctx[i]) (void)wsg_close(b->tctx[i]);
     b->d_tdesc[i].release();
     b->d_tsf[i].release();
@@ -1410,15 +1424,15 @@ static void adjusted_results(wsg_batcher* b, const FlushSlot& g, std::vector<wsg
 static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res);
 static int stage_advance(wsg_batcher* b, bool collect) {
   bool pred_collected = true;  // (the flush before q[0] is)
-  for (size_t qi = 0; qi < b->q.size() && qi < 3; ++qi) {
+  for (size_t qi = 0; qi < b->q.size(); ++qi) {
     FlushSlot& g = b->fs[b->q[qi]];
     if (g.so.staged) {
       pred_collected = true;
       continue;
     }
     if (!g.ij.prepped) {
-      // (its pre-decode context was flush t - 2's: that one must be collected)
-      if (qi >= 2 && !b->fs[b->q[qi - 2]].so.staged) break;
+      // (its pre-decode context was flush t - kTokCtx's: that one must be collected)
+      if (qi >= (size_t)kTokCtx && !b->fs[b->q[qi - kTokCtx]].so.staged) break;
       const hipError_t e = hipEventQuery(g.done);
       if (e == hipErrorNotReady) break;
       B_TRY(b, e);
@@ -1447,7 +1461,7 @@ static int stage_advance(wsg_batcher* b, bool collect) {
 
 int wsg_batcher_flush_async(wsg_batcher* b) {
   if (!b) return WSG_API_EINVAL;
-  if (b->q.size() >= WSG_BATCHER_MAX_INFLIGHT)
+  if (b->q.size() >= (size_t)kInflight)
     return bset(b, WSG_API_ERANGE, "WSG_BATCHER_MAX_INFLIGHT flushes in flight: wsg_batcher_wait first");
   const uint32_t S = b->n;
   int rc;
@@ -1517,7 +1531,7 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
   ++b->tickets;
   b->q.push_back(slot);
   // feeds go to the next slot (waited: at most two in flight)
-  b->open = (b->open + 1) % (WSG_BATCHER_MAX_INFLIGHT + 1);
+  b->open = (b->open + 1) % (kInflight + 1);
   FlushSlot& g = b->fs[b->open];
   g.arena_len = 0;
   for (uint32_t i = 0; i < S; ++i) {
@@ -1573,6 +1587,9 @@ static int stage_advance_blocking(wsg_batcher* b) {
     if (qi + 1 == b->q.size() || qi == 1) break;  // the last one: begun only
     if ((rc = stage_compute(b, g, nullptr))) return rc;
   }
+  // (more pre-decode contexts than two: the pre-decodes of the flushes further back
+  // whose decode is done)
+  if (kTokCtx > 2 && b->stage_early) return stage_advance(b, false);
   return WSG_API_OK;
 }
 
@@ -1688,7 +1705,7 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
     }
     ws::ctx_copy_tuning(b->sctx, b->ctx);  // (the batcher context's switches hold for its stages)
     b->two_phase = stages->inflate && ws::ctx_inflate_two_phase(b->ctx);
-    for (int i = 0; b->two_phase && i < 2; ++i) {  // the pre-decode contexts (stream + workspace each)
+    for (int i = 0; b->two_phase && i < kTokCtx; ++i) {  // the pre-decode contexts (stream + workspace each)
       if (!b->tctx[i]) {
         const int rc = wsg_open(ws::ctx_device(b->ctx), nullptr, &b->tctx[i]);
         if (rc) return bset(b, rc, "wsg_open (pre-decode context)");
@@ -1806,7 +1823,7 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
   B_TRY(b, b->h_pend.ensure(maxo + 16 * S + 32));
   const int rc = ws::ctx_reserve_stages(b->sctx, F, (uint32_t)S, in_len + infl, agg);
   if (rc) return bset(b, rc, wsg_last_error(b->sctx));
-  for (int i = 0; b->two_phase && i < 2; ++i) {  // the pre-decodes: a flush's decoded frames and payloads
+  for (int i = 0; b->two_phase && i < kTokCtx; ++i) {  // the pre-decodes: a flush's decoded frames and payloads
     const int rc2 = wsg_reserve_inflate(b->tctx[i], Fi + 1, (uint32_t)S, al16(pcap));
     if (rc2) return bset(b, rc2, wsg_last_error(b->tctx[i]));
     B_TRY(b, b->d_tdesc[i].ensure((Fi + 2) * sizeof(wsg_frame_desc)));
