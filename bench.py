@@ -45,9 +45,9 @@ CONFIGS = {
 
 
 
-# flushes the bench lines keep in flight: WSG_BATCHER_MAX_INFLIGHT (snf4j_amd._lib; checked
-# equal in tests/test_bench_cli.py); WSG_BENCH_INFLIGHT=2 for A/B runs against older builds
-BATCHER_MAX_INFLIGHT = int(os.environ.get("WSG_BENCH_INFLIGHT", "3"))
+# flushes the bench lines keep in flight: WSG_BATCHER_MAX_INFLIGHT (snf4j_amd._lib, 4; checked
+# equal in tests/test_bench_cli.py); WSG_BENCH_INFLIGHT for A/B runs against builds with another depth
+BATCHER_MAX_INFLIGHT = int(os.environ.get("WSG_BENCH_INFLIGHT", "4"))
 
 
 def apply_tuning(ctx):
@@ -913,7 +913,7 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
     FrameUtf8Validator, PerMessageDeflateExtension.java:316-326), end to end from host
     socket reads to host frames: per round one `chunk`-byte read of every session
     (wsg_batcher_feed_many), then wsg_batcher_flush_async (H2D, decode, inflate,
-    validate, D2H), three flushes in flight.  Value: inflated bytes delivered per second."""
+    validate, D2H), four flushes in flight.  Value: inflated bytes delivered per second."""
     import numpy as np
     import torch
     import snf4j_amd
@@ -1046,7 +1046,7 @@ def e2e_encode_line(ctx, dev, K, W, n_s=64, msg_bytes=16 << 20, frame=65536, per
 def e2e_aggregate_line(ctx, dev, K, W, chunk=65536):
     """The native batcher with FrameAggregator after the decoder (wsg_batcher_set_stages
     aggregate; FrameAggregator.java:72-104) on configs[2]'s 4 GiB mixed batch, host to
-    host: per round one `chunk`-byte read of every session, three flushes in flight;
+    host: per round one `chunk`-byte read of every session, four flushes in flight;
     the decode's UTF-8 check stays fused.  Value: wire bytes fed per second."""
     import numpy as np
     import torch
@@ -1241,7 +1241,7 @@ def e2e_rate(ctx, cfg, wire, off, sf, n_s, wire_bytes, F, dev, reps=6):
                              "api": "per round: wsg_batcher_feed_many (one 64 KiB socket read per session, "
                                     "copied once into the open batch's pinned arena and framed in place, "
                                     "threaded by session) + wsg_batcher_flush_async (H2D, decode, D2H of the "
-                                    "arena, no gather), three flushes in flight"}
+                                    "arena, no gather), four flushes in flight"}
     nb.close()
     out["drop_in_loop"] = e2e_loop_line(pctx, rounds, wire_bytes, F, n_s)
     pctx.close()

@@ -19,7 +19,7 @@ import java.nio.ByteBuffer;
 
 final class Wsg {
 	/** WSG_BATCHER_MAX_INFLIGHT (wsgpu.h): decode flushes a native batcher keeps in flight. */
-	static final int BATCHER_MAX_INFLIGHT = 3;
+	static final int BATCHER_MAX_INFLIGHT = 4;
 
 
 	static {

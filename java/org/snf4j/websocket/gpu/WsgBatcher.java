@@ -16,7 +16,7 @@
  *      side copies them into the open batch's pinned arena and frames them, several
  *      threads for large iterations), then releases the buffers;
  *   2. delivers every earlier flush whose device work has finished (wsg_batcher_await
- *      with no wait; only with BATCHER_MAX_INFLIGHT (3) already in flight does it wait
+ *      with no wait; only with BATCHER_MAX_INFLIGHT (4) already in flight does it wait
  *      for the oldest);
  *   3. queues this iteration's batch (wsg_batcher_flush_async: H2D, decode + UTF-8 and
  *      the stages after the decoder, D2H) and hands its ticket to the completion

@@ -67,7 +67,7 @@ class HsConfig(C.Structure):
                 ("extensions", C.c_uint8), ("host_policy", C.c_uint8)]
 
 
-BATCHER_MAX_INFLIGHT = 3  # WSG_BATCHER_MAX_INFLIGHT: decode flushes a batcher keeps in flight
+BATCHER_MAX_INFLIGHT = 4  # WSG_BATCHER_MAX_INFLIGHT: decode flushes a batcher keeps in flight
 HS_RESP_STRIDE = 160
 HS_EXPECTED_STRIDE = 32   # wsg_handshake_validate_batch_*: expected Sec-WebSocket-Accept per session
 

@@ -130,7 +130,7 @@ static constexpr int kInflight = WSG_BATCHER_MAX_INFLIGHT;
 #ifdef WSG_AB_TOKCTX
 static constexpr int kTokCtx = WSG_AB_TOKCTX;
 #else
-static constexpr int kTokCtx = 2;
+static constexpr int kTokCtx = 3;
 #endif
 
 class Pool {
@@ -296,8 +296,12 @@ constexpr uint32_t COPY_MAX = 65536;
 // it is a decoder payload slot, byte-aligned when it is inflated output (messages back
 // to back): either way the host sees 16-B stores (PCIe writes of whole 16-B chunks; the
 // 4-B stores of the unaligned case ran at 31.6 GB/s, profiles/r04_stageprof_final.txt).
+#ifdef WSG_AB_GATHER
+constexpr uint32_t GATHER_GROUPS = WSG_AB_GATHER;
+#else
 constexpr uint32_t GATHER_GROUPS = 12;  // workgroups of the output gather: enough to fill PCIe, few enough
                                          // that the next flush's small downloads still get a share of it
+#endif
 
 __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                     const StageCopy* __restrict__ cp, uint32_t n) {
@@ -1571,7 +1575,7 @@ static int stage_advance_blocking(wsg_batcher* b) {
   // only begun.  A chain is begun from its flush's decode results, so those are waited
   // for (one flush's decode: short).
   // (two-phase inflate: every queued flush's pre-decode is launched first — flush t's
-  // context was last used by flush t - 2, collected by now — so it runs meanwhile)
+  // context was last used by flush t - kTokCtx, collected by now — so it runs meanwhile)
   for (size_t qi = 0; qi < b->q.size() && qi < 2; ++qi) {
     FlushSlot& g = b->fs[b->q[qi]];
     if (g.so.staged || g.ij.prepped) continue;

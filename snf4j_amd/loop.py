@@ -15,7 +15,7 @@ The batching on that loop:
   executenf, which runs after every read of the iteration;
 - flush() feeds the iteration's reads with one wsg_batcher_feed_many, collects every
   earlier flush whose device work has finished (wsg_batcher_await with no wait),
-  collects the oldest one blocking only when WSG_BATCHER_MAX_INFLIGHT (3) are in
+  collects the oldest one blocking only when WSG_BATCHER_MAX_INFLIGHT (4) are in
   flight, then queues this one
   (wsg_batcher_flush_async) and hands its ticket to the completion thread;
 - the completion thread waits for the ticket (wsg_batcher_await) and re-enters the
