@@ -160,11 +160,12 @@ def _chain_case(ctx, oracle, seed, no_context, aggregate, big=False):
     return n_split
 
 
-@pytest.mark.parametrize("seed,aggregate,depth", [(10, True, 2), (11, False, 2), (12, True, 3), (13, False, 3)])
+@pytest.mark.parametrize("seed,aggregate,depth", [(10, True, 2), (11, False, 2), (12, True, 3), (13, False, 3),
+                                                   (14, True, 4), (15, False, 4)])
 def test_batcher_stage_chain_pipelined(ctx, oracle, seed, aggregate, depth):
-    """The same chain with `depth` flushes in flight (wsg_batcher_flush_async / wait; 3 =
-    WSG_BATCHER_MAX_INFLIGHT: each wait collects the next flush's chain and begins the
-    one after): a session a stage fails in one flush gets nothing from the flushes
+    """The same chain with `depth` flushes in flight (wsg_batcher_flush_async / wait; 4 =
+    WSG_BATCHER_MAX_INFLIGHT: flush_async and feed_many start the queued chains, each
+    wait collects the next flush's chain and begins the one after): a session a stage fails in one flush gets nothing from the flushes
     already in flight behind it (the session is closed), a slot reset while its chains
     are begun or collected delivers nothing of the old session, and a reset slot starts
     from fresh stage decoders."""
@@ -256,3 +257,67 @@ def test_batcher_stage_chain_capacity_rerun(ctx, oracle):
         assert eerr is None
         assert [(int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload()) for f in got[s]] == exp, s
     b.close()
+
+
+def test_batcher_stage_chain_threaded_feeds(ctx, oracle):
+    """Feeds big enough for wsg_batcher_feed_many's thread pool (8 MB a round), so the
+    chains of the flushes in flight advance on the calling thread while the workers
+    copy (stage_advance beside the copies), WSG_BATCHER_MAX_INFLIGHT flushes deep, with
+    slots reset mid-stream; every session's frames and first error equal the oracle
+    chain's."""
+    from snf4j_amd import NativeBatcher
+    from snf4j_amd._lib import BATCHER_MAX_INFLIGHT
+    rng = np.random.default_rng(6400)
+    n, u, chunk = 1024, 32, 8192
+    uniq = []
+    for _ in range(u):
+        msgs = _messages(rng, 20, False, bad_utf8=0.04)
+        uniq.append(b"".join(wsgen.build_frame(op, fin, rsv, p, True, tuple(int(x) for x in rng.integers(0, 256, 4)))
+                             for (op, fin, rsv, p) in msgs))
+    wire = np.frombuffer(b"".join(uniq), dtype=np.uint8).copy()
+    ustart = np.concatenate([[0], np.cumsum([len(x) for x in uniq])])
+    base = wire.ctypes.data
+    b = NativeBatcher(n, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=ctx)
+    b.set_stages(inflate=True, noContext=False, validate=True)
+    got = [[] for _ in range(n)]
+    err = [None] * n
+    pos = np.zeros(n, dtype=np.int64)
+    end = np.array([len(uniq[s % u]) for s in range(n)], dtype=np.int64)
+    off = np.array([ustart[s % u] for s in range(n)], dtype=np.int64)
+
+    def collect():
+        for s, (fr, e) in enumerate(b.wait()):
+            got[s] += fr
+            if e is not None:
+                assert err[s] is None, s
+                err[s] = (e.getMessage(), e.close_code)
+
+    pending, it = 0, 0
+    while (pos < end).any():
+        it += 1
+        if it == 2:  # slots to new sessions mid-stream, flushes in flight
+            for s in range(0, n, 97):
+                b.reset_session(s)
+                got[s], err[s], pos[s] = [], None, 0
+        live = np.nonzero(pos < end)[0]
+        ln = np.minimum(end[live] - pos[live], chunk)
+        assert ln.sum() >= (4 << 20) or it > 2  # (the pool's threshold: the first rounds are threaded)
+        b.feed_many_ptrs(live.astype(np.uint32), (base + off[live] + pos[live]).astype(np.uint64), ln.astype(np.uint64))
+        pos[live] += ln
+        if pending == BATCHER_MAX_INFLIGHT:
+            collect()
+            pending -= 1
+        b.flush_async()
+        pending += 1
+    while pending:
+        collect()
+        pending -= 1
+    b.close()
+    want = [_oracle_chain(oracle, uniq[k], False, True, False, 1 << 20) for k in range(u)]
+    n_err = 0
+    for s in range(n):
+        exp, eerr = want[s % u]
+        assert err[s] == eerr, (s, err[s], eerr)
+        assert [(int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload()) for f in got[s]] == exp, s
+        n_err += eerr is not None
+    assert n_err
