@@ -445,6 +445,7 @@ struct StageOut {
   uint64_t len = 0;
   PinnedBuf pay;
   DBuf d_copy;
+  DBuf dstage;  // (WSG_AB_SDMA_OUT) the output gathered on the device, then one D2H
   hipEvent_t gathered = nullptr, downloaded = nullptr;
   bool staged = false;  // computed, download queued (wsg_batcher_wait collects it)
 };
@@ -1106,12 +1107,20 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
     }
     B_TRY(b, hipEventRecord(o.gathered, st));
     B_TRY(b, hipStreamWaitEvent(b->s_dl, o.gathered, 0));
+    const uint32_t n = (uint32_t)o.copies.size();
+#ifdef WSG_AB_SDMA_OUT
+    B_TRY(b, o.dstage.ensure(o.len + 16));
+    hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, 1024)), dim3(256), 0, b->s_dl, b->ar->p,
+                       o.dstage.p, (const StageCopy*)o.d_copy.p, n);
+    B_TRY(b, hipGetLastError());
+    B_TRY(b, hipMemcpyAsync(o.pay.p, o.dstage.p, o.len, hipMemcpyDeviceToHost, b->s_dl));
+#else
     uint8_t* dst = nullptr;
     B_TRY(b, hipHostGetDevicePointer((void**)&dst, o.pay.p, 0));
-    const uint32_t n = (uint32_t)o.copies.size();
     hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, GATHER_GROUPS)), dim3(256), 0, b->s_dl, b->ar->p,
                        dst, (const StageCopy*)o.d_copy.p, n);
     B_TRY(b, hipGetLastError());
+#endif
   }
   B_TRY(b, hipEventRecord(o.downloaded, b->s_dl));
   o.staged = true;
@@ -1166,6 +1175,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     f.dpay.release();
     f.so.pay.release();
     f.so.d_copy.release();
+    f.so.dstage.release();
     if (f.so.gathered) (void)hipEventDestroy(f.so.gathered);
     if (f.so.downloaded) (void)hipEventDestroy(f.so.downloaded);
     if (f.done) (void)hipEventDestroy(f.done);
@@ -1794,6 +1804,9 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
   for (FlushSlot& f : b->fs) {
     B_TRY(b, f.dpay.grow_keep(arena, 0, st));
     B_TRY(b, f.so.pay.ensure(out));
+#ifdef WSG_AB_SDMA_OUT
+    B_TRY(b, f.so.dstage.ensure(out));
+#endif
     B_TRY(b, f.so.d_copy.ensure((copies + 1) * sizeof(StageCopy)));
     B_TRY(b, f.so.d_copy.up.ensure((copies + 1) * sizeof(StageCopy)));
     if (!f.dpay_done) B_TRY(b, hipEventCreateWithFlags(&f.dpay_done, hipEventDisableTiming));
