@@ -445,7 +445,6 @@ struct StageOut {
   uint64_t len = 0;
   PinnedBuf pay;
   DBuf d_copy;
-  DBuf dstage;  // (WSG_AB_SDMA_OUT) the output gathered on the device, then one D2H
   hipEvent_t gathered = nullptr, downloaded = nullptr;
   bool staged = false;  // computed, download queued (wsg_batcher_wait collects it)
 };
@@ -1092,7 +1091,9 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   // the output: gathered from this flush's arena straight into the pinned host buffer
   // by a few workgroups on the download stream (PCIe writes), so the next flush's
   // stages have the GPU meanwhile (a runtime D2H here is a blit kernel that takes
-  // every CU while it waits on PCIe)
+  // every CU while it waits on PCIe: round 5 measured a device-side gather + one
+  // hipMemcpyAsync D2H, profiles/r05_ab/r05q_*: the blit's 0.9-1.5 ms slowed the
+  // replay and the pre-decode beside it 2-4x)
   if (!o.gathered) B_TRY(b, hipEventCreateWithFlags(&o.gathered, hipEventDisableTiming));
   if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, hipEventDisableTiming));
   if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
@@ -1108,19 +1109,11 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
     B_TRY(b, hipEventRecord(o.gathered, st));
     B_TRY(b, hipStreamWaitEvent(b->s_dl, o.gathered, 0));
     const uint32_t n = (uint32_t)o.copies.size();
-#ifdef WSG_AB_SDMA_OUT
-    B_TRY(b, o.dstage.ensure(o.len + 16));
-    hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, 1024)), dim3(256), 0, b->s_dl, b->ar->p,
-                       o.dstage.p, (const StageCopy*)o.d_copy.p, n);
-    B_TRY(b, hipGetLastError());
-    B_TRY(b, hipMemcpyAsync(o.pay.p, o.dstage.p, o.len, hipMemcpyDeviceToHost, b->s_dl));
-#else
     uint8_t* dst = nullptr;
     B_TRY(b, hipHostGetDevicePointer((void**)&dst, o.pay.p, 0));
     hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, GATHER_GROUPS)), dim3(256), 0, b->s_dl, b->ar->p,
                        dst, (const StageCopy*)o.d_copy.p, n);
     B_TRY(b, hipGetLastError());
-#endif
   }
   B_TRY(b, hipEventRecord(o.downloaded, b->s_dl));
   o.staged = true;
@@ -1175,7 +1168,6 @@ int wsg_batcher_close(wsg_batcher* b) {
     f.dpay.release();
     f.so.pay.release();
     f.so.d_copy.release();
-    f.so.dstage.release();
     if (f.so.gathered) (void)hipEventDestroy(f.so.gathered);
     if (f.so.downloaded) (void)hipEventDestroy(f.so.downloaded);
     if (f.done) (void)hipEventDestroy(f.done);
@@ -1804,9 +1796,6 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
   for (FlushSlot& f : b->fs) {
     B_TRY(b, f.dpay.grow_keep(arena, 0, st));
     B_TRY(b, f.so.pay.ensure(out));
-#ifdef WSG_AB_SDMA_OUT
-    B_TRY(b, f.so.dstage.ensure(out));
-#endif
     B_TRY(b, f.so.d_copy.ensure((copies + 1) * sizeof(StageCopy)));
     B_TRY(b, f.so.d_copy.up.ensure((copies + 1) * sizeof(StageCopy)));
     if (!f.dpay_done) B_TRY(b, hipEventCreateWithFlags(&f.dpay_done, hipEventDisableTiming));
