@@ -578,18 +578,41 @@ static void stage_fail(wsg_batcher* b, uint32_t s, const wsg_session_result& r) 
   b->out->res[s].detail = r.detail;
 }
 
+// A stage list's upload: the host copy into the buffer's pinned staging, then the
+// device pulls it over PCIe (k_pull: 16-B loads from the mapped staging, a few
+// workgroups) in stream order.  The runtime's DMA copy costs ~11 us of engine time a
+// call at these sizes (16-320 KB: 40 x 213 KB drained in 457 us against 166 us pulled,
+// tools/ubench_hostapi.hip, profiles/r05_ab/r05r_hostapi.txt), and a stage flush makes
+// eight of them.
+__global__ __launch_bounds__(256) void k_pull(const ws_u32x4* __restrict__ src, ws_u32x4* __restrict__ dst,
+                                              uint32_t n16) {
+  for (uint32_t i = blockIdx.x * 256 + threadIdx.x; i < n16; i += gridDim.x * 256)
+    dst[i] = __builtin_nontemporal_load(src + i);
+}
+
 template <typename T>
 static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
   const size_t bytes = v.size() * sizeof(T);
-  hipError_t e = d.ensure(bytes + sizeof(T));
-  if (e == hipSuccess) e = d.up.ensure(bytes + sizeof(T));
+  // (both sized to whole 16-B words: the pull reads and writes up to 15 B past `bytes`)
+  hipError_t e = d.ensure(al16(bytes) + sizeof(T));
+  if (e == hipSuccess) e = d.up.ensure(al16(bytes) + sizeof(T));
   if (e != hipSuccess || v.empty()) return e;
   {
     SP(16);
     memcpy(d.up.p, v.data(), bytes);
   }
   SP(17);
+#ifdef WSG_AB_DMA_UPLOAD
   return hipMemcpyAsync(d.p, d.up.p, bytes, hipMemcpyHostToDevice, s);
+#else
+  void* src = nullptr;
+  e = hipHostGetDevicePointer(&src, d.up.p, 0);
+  if (e != hipSuccess) return e;
+  const uint32_t n16 = (uint32_t)(al16(bytes) / 16);
+  hipLaunchKernelGGL(k_pull, dim3(std::min<uint32_t>(256, (n16 + 255) / 256)), dim3(256), 0, s, (const ws_u32x4*)src,
+                     (ws_u32x4*)d.p, n16);
+  return hipGetLastError();
+#endif
 }
 
 // PerMessageDeflateDecoder over a flush's frames (PerMessageDeflateDecoder.java:68-105),
