@@ -1567,7 +1567,11 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     g.fo[i].clear();
     g.fb[i] = 0;
   }
+#ifdef WSG_AB_NO_FLUSH_ADVANCE
+  if (b->has_stages && b->stage_early && !b->feed_advance) return stage_advance(b, false);
+#else
   if (b->has_stages && b->stage_early) return stage_advance(b, false);
+#endif
   return WSG_API_OK;
 }
 
