@@ -305,6 +305,9 @@ constexpr uint32_t GATHER_GROUPS = 12;  // workgroups of the output gather: enou
 
 __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                     const StageCopy* __restrict__ cp, uint32_t n) {
+#ifdef WSG_AB_GATHER_PRIO
+  __builtin_amdgcn_s_setprio(3);  // (A/B) issue ahead of the pre-decode / replay waves sharing the SIMD
+#endif
   for (uint32_t ci = blockIdx.x; ci < n; ci += gridDim.x) {
   const StageCopy c = cp[ci];
   const uint8_t* s = src + c.src;
@@ -876,6 +879,18 @@ static int infl_collect(wsg_batcher* b, FlushSlot& f) {
   return WSG_API_OK;
 }
 
+// the stage outputs' download stream
+static hipError_t dl_stream(wsg_batcher* b) {
+  if (b->s_dl) return hipSuccess;
+#ifdef WSG_AB_DL_PRIO
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  return e != hipSuccess ? e : hipStreamCreateWithPriority(&b->s_dl, hipStreamNonBlocking, hi);
+#else
+  return hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking);
+#endif
+}
+
 // append an output frame: dev_len bytes at arena offset src, after `prefix` (host bytes)
 static void fin_push(wsg_batcher* b, wsg_frame_desc d, uint64_t src, uint32_t dev_len, std::vector<uint8_t>* prefix) {
   StageOut& fp = *b->out;
@@ -1119,7 +1134,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   // replay and the pre-decode beside it 2-4x)
   if (!o.gathered) B_TRY(b, hipEventCreateWithFlags(&o.gathered, hipEventDisableTiming));
   if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, hipEventDisableTiming));
-  if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
+  B_TRY(b, dl_stream(b));
   {
     SP(11);
     B_TRY(b, o.pay.ensure(o.len + 16));
@@ -1567,11 +1582,7 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     g.fo[i].clear();
     g.fb[i] = 0;
   }
-#ifdef WSG_AB_NO_FLUSH_ADVANCE
-  if (b->has_stages && b->stage_early && !b->feed_advance) return stage_advance(b, false);
-#else
   if (b->has_stages && b->stage_early) return stage_advance(b, false);
-#endif
   return WSG_API_OK;
 }
 
@@ -1829,7 +1840,7 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
     if (!f.so.gathered) B_TRY(b, hipEventCreateWithFlags(&f.so.gathered, hipEventDisableTiming));
     if (!f.so.downloaded) B_TRY(b, hipEventCreateWithFlags(&f.so.downloaded, hipEventDisableTiming));
   }
-  if (!b->s_dl) B_TRY(b, hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking));
+  B_TRY(b, dl_stream(b));
   struct Up {
     DBuf* d;
     uint64_t bytes;
