@@ -465,6 +465,7 @@ struct InflJob {
   StageList cur;                     // the stage input, then (after inflate) its output
   uint64_t used = 0;                 // the arena's extent so far
   StageList x;                       // the inflate attempt in flight
+  bool x_cur = false;                //   (its input is cur as it is: x is not built)
   std::vector<uint32_t> todo, nheld;
   std::vector<uint64_t> cap, held_at, oo;
   uint64_t ipos = 0;
@@ -635,13 +636,34 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
   hipStream_t st = ws::ctx_stream(b->sctx);
   InflJob& j = f.ij;
   StageList& x = j.x;
-  x.sf.assign(S + 1, 0);
-  x.desc.clear();
-  j.tmap.clear();
   j.oo.assign(S + 1, 0);
   std::fill(j.nheld.begin(), j.nheld.end(), 0u);  // (this attempt's sessions set theirs)
-  size_t ti = 0;
+  // Two-phase, with no held frames and every session that has frames taking part (the
+  // common case), the attempt's input is the pre-decode's list as it is: its copy on the
+  // device (d_tdesc / d_tsf of the pre-decode context) is the replay's, with the frame
+  // map the identity, so nothing is rebuilt or uploaded for it.
+  bool same = j.tc >= 0;
   {
+    size_t ti = 0;
+    for (uint32_t s = 0; s < S && same; ++s) {
+      const bool in = ti < j.todo.size() && j.todo[ti] == s;
+      ti += in;
+      if (in ? !b->ss[s].held_desc.empty() : j.cur.sf[s + 1] != j.cur.sf[s]) same = false;
+      j.oo[s + 1] = j.oo[s] + (in ? j.cap[s] : 0);
+    }
+  }
+  j.x_cur = same;
+  if (same) {
+    x.sf.clear();
+    x.desc.clear();
+    j.tmap.clear();
+  } else {
+    x.sf.assign(S + 1, 0);
+    x.desc.clear();
+    j.tmap.clear();
+  }
+  size_t ti = 0;
+  if (!same) {
     SP(1);
     for (uint32_t s = 0; s < S; ++s) {
       x.sf[s] = (uint32_t)x.desc.size();
@@ -666,31 +688,35 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
       }
     }
   }
-  x.sf[S] = (uint32_t)x.desc.size();
-  const uint64_t F = x.desc.size();
+  if (!same) x.sf[S] = (uint32_t)x.desc.size();
+  const uint64_t F = same ? j.cur.desc.size() : x.desc.size();
   const uint64_t ipos = j.ipos;
   DBuf& ar = f.dpay;
   // (a move of the arena waits for the pre-decode reading it)
   if (j.tc >= 0 && ipos + j.oo[S] + 64 > ar.n) B_TRY(b, hipEventSynchronize(j.tok_done));
   B_TRY(b, ar.grow_keep(ipos + j.oo[S] + 64, ipos, st));
-  B_TRY(b, upload(b->d_desc, x.desc, st));
-  B_TRY(b, upload(b->d_sf, x.sf, st));
+  if (!same) {
+    B_TRY(b, upload(b->d_desc, x.desc, st));
+    B_TRY(b, upload(b->d_sf, x.sf, st));
+  }
+  const wsg_frame_desc* dx = (const wsg_frame_desc*)(same ? b->d_tdesc[j.tc].p : b->d_desc.p);
+  const uint32_t* dxsf = (const uint32_t*)(same ? b->d_tsf[j.tc].p : b->d_sf.p);
   B_TRY(b, upload(b->d_ooff, j.oo, st));
   B_TRY(b, b->d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
   B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
   int rc;
   if (j.tc >= 0) {  // the replay of the pre-decode that ran on tctx[tc]
-    B_TRY(b, upload(b->d_tmap, j.tmap, st));
+    if (!same) B_TRY(b, upload(b->d_tmap, j.tmap, st));
     B_TRY(b, hipStreamWaitEvent(st, j.tok_done, 0));
-    rc = ws::inflate_replay_phase(b->sctx, b->tctx[j.tc], (const uint32_t*)b->d_tmap.p, b->stages.inflate_no_context,
-                                  (const wsg_frame_desc*)b->d_desc.p, F, (const uint32_t*)b->d_sf.p, S, ar.p, ipos,
+    rc = ws::inflate_replay_phase(b->sctx, b->tctx[j.tc], same ? nullptr : (const uint32_t*)b->d_tmap.p,
+                                  b->stages.inflate_no_context, dx, F, dxsf, S, ar.p, ipos,
                                   (wsg_inflate_state*)b->d_istate.p, b->d_iwin.p, ar.p + ipos,
                                   (const uint64_t*)b->d_ooff.p, (wsg_frame_desc*)b->d_odesc.p,
                                   (wsg_session_result*)b->d_ores.p, (uint32_t*)b->d_rf.p);
   } else {
-    rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, (const wsg_frame_desc*)b->d_desc.p, F,
-                                  (const uint32_t*)b->d_sf.p, S, ar.p, ipos, (wsg_inflate_state*)b->d_istate.p,
+    rc = wsg_inflate_batch_device(b->sctx, b->stages.inflate_no_context, dx, F, dxsf, S, ar.p, ipos,
+                                  (wsg_inflate_state*)b->d_istate.p,
                                   b->d_iwin.p, ar.p + ipos, (const uint64_t*)b->d_ooff.p,
                                   (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
                                   (uint32_t*)b->d_rf.p);
@@ -705,12 +731,11 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
     B_TRY(b, b->d_vres.ensure((S + 1) * sizeof(wsg_session_result)));
     if (F) {
       hipLaunchKernelGGL(k_stage_vprep, dim3((uint32_t)((F + 255) / 256)), dim3(256), 0, st,
-                         (const wsg_frame_desc*)b->d_odesc.p, (const uint32_t*)b->d_sf.p,
-                         (const uint32_t*)b->d_nheld.p, (const wsg_session_result*)b->d_ores.p, ipos, S, F,
+                         (const wsg_frame_desc*)b->d_odesc.p, dxsf, (const uint32_t*)b->d_nheld.p, (const wsg_session_result*)b->d_ores.p, ipos, S, F,
                          (wsg_frame_desc*)b->d_vdesc.p);
       B_TRY(b, hipGetLastError());
     }
-    rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_vdesc.p, F, (const uint32_t*)b->d_sf.p, S,
+    rc = wsg_validate_batch_device(b->sctx, (const wsg_frame_desc*)b->d_vdesc.p, F, dxsf, S,
                                    ar.p, ipos + j.oo[S], (wsg_session_state*)b->d_vstate.p,
                                    (wsg_session_result*)b->d_vres.p);
     if (rc) return bset(b, rc, wsg_last_error(b->sctx));
@@ -788,7 +813,7 @@ static int infl_collect(wsg_batcher* b, FlushSlot& f) {
       SP(2);
       B_TRY(b, hipStreamSynchronize(st));
     }
-    const StageList& x = j.x;
+    const StageList& x = j.x_cur ? j.cur : j.x;
     const wsg_frame_desc* odesc = (const wsg_frame_desc*)b->h_odesc.p;
     const wsg_session_result* r = (const wsg_session_result*)b->h_ores.p;
     const uint32_t* rf = (const uint32_t*)b->h_rf.p;
