@@ -305,9 +305,6 @@ constexpr uint32_t GATHER_GROUPS = 12;  // workgroups of the output gather: enou
 
 __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
                                                     const StageCopy* __restrict__ cp, uint32_t n) {
-#ifdef WSG_AB_GATHER_PRIO
-  __builtin_amdgcn_s_setprio(3);  // (A/B) issue ahead of the pre-decode / replay waves sharing the SIMD
-#endif
   for (uint32_t ci = blockIdx.x; ci < n; ci += gridDim.x) {
   const StageCopy c = cp[ci];
   const uint8_t* s = src + c.src;
@@ -553,6 +550,7 @@ struct wsg_batcher {
   PinnedBuf h_pend;                     // aggregator bytes held for the next flush, downloaded
   DBuf d_pend;
   hipStream_t s_dl = nullptr;           // downloads of stage outputs
+  hipStream_t s_stage = nullptr;        // the stage context's stream when the batcher makes it
   StageOut* out = nullptr;              // the output the stage run at hand writes
   uint64_t tickets = 0;                 // flushes queued so far (flush t's ticket is t)
   std::shared_ptr<Notify> notify = std::make_shared<Notify>();
@@ -904,16 +902,21 @@ static int infl_collect(wsg_batcher* b, FlushSlot& f) {
   return WSG_API_OK;
 }
 
-// the stage outputs' download stream
-static hipError_t dl_stream(wsg_batcher* b) {
-  if (b->s_dl) return hipSuccess;
-#ifdef WSG_AB_DL_PRIO
+// A stream at the device's highest priority: the queue's dispatches go ahead of the
+// other streams' (the pre-decode, the next flushes' decode).
+static hipError_t high_stream(hipStream_t* s) {
   int lo = 0, hi = 0;
   hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-  return e != hipSuccess ? e : hipStreamCreateWithPriority(&b->s_dl, hipStreamNonBlocking, hi);
-#else
-  return hipStreamCreateWithFlags(&b->s_dl, hipStreamNonBlocking);
-#endif
+  return e != hipSuccess ? e : hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
+// The stage outputs' download stream, at high priority: the output gather is what a
+// flush's collection waits for, and its few workgroups were dispatched behind the
+// pre-decode's and replay's (stage lines +7%: burst 18.8-19.0 -> 19.7-20.9, steady
+// 25.1-25.6 -> 26.5-27.7 GiB/s, profiles/r05_ab/r05u_ab_prio.txt; the gather's waves at
+// s_setprio 3 instead: no gain).
+static hipError_t dl_stream(wsg_batcher* b) {
+  return b->s_dl ? hipSuccess : high_stream(&b->s_dl);
 }
 
 // append an output frame: dev_len bytes at arena offset src, after `prefix` (host bytes)
@@ -1250,6 +1253,7 @@ int wsg_batcher_close(wsg_batcher* b) {
     (void)hipStreamDestroy(b->s_dl);
   }
   if (b->sctx) (void)wsg_close(b->sctx);
+  if (b->s_stage) (void)hipStreamDestroy(b->s_stage);
   for (int i = 0; i < kTokCtx; ++i) {
     if (b->tctx[i]) (void)wsg_close(b->tctx[i]);
     b->d_tdesc[i].release();
@@ -1769,7 +1773,10 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
   b->stage_resets.clear();
   if (b->has_stages) {  // the device-resident stage carry, zeroed (fresh stage decoders)
     if (!b->sctx) {
-      const int rc = wsg_open(ws::ctx_device(b->ctx), nullptr, &b->sctx);
+#ifdef WSG_AB_STAGE_PRIO
+      B_TRY(b, high_stream(&b->s_stage));  // (A/B) the replay chain at high priority too
+#endif
+      const int rc = wsg_open(ws::ctx_device(b->ctx), b->s_stage, &b->sctx);
       if (rc) return bset(b, rc, "wsg_open (stage context)");
     }
     ws::ctx_copy_tuning(b->sctx, b->ctx);  // (the batcher context's switches hold for its stages)
