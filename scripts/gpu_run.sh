@@ -18,5 +18,5 @@ if [ "$2" != bench-only ]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" || exit $?
 fi
 [ "$2" = tests-only ] && { echo ALL_DONE; exit 0; }
-step bench 600 python bench.py --e2e || exit $?
+step bench 600 python bench.py || exit $?
 echo ALL_DONE

@@ -550,7 +550,6 @@ struct wsg_batcher {
   PinnedBuf h_pend;                     // aggregator bytes held for the next flush, downloaded
   DBuf d_pend;
   hipStream_t s_dl = nullptr;           // downloads of stage outputs
-  hipStream_t s_stage = nullptr;        // the stage context's stream when the batcher makes it
   StageOut* out = nullptr;              // the output the stage run at hand writes
   uint64_t tickets = 0;                 // flushes queued so far (flush t's ticket is t)
   std::shared_ptr<Notify> notify = std::make_shared<Notify>();
@@ -914,7 +913,8 @@ static hipError_t high_stream(hipStream_t* s) {
 // flush's collection waits for, and its few workgroups were dispatched behind the
 // pre-decode's and replay's (stage lines +7%: burst 18.8-19.0 -> 19.7-20.9, steady
 // 25.1-25.6 -> 26.5-27.7 GiB/s, profiles/r05_ab/r05u_ab_prio.txt; the gather's waves at
-// s_setprio 3 instead: no gain).
+// s_setprio 3 instead: no gain; the stage context's stream at high priority as well: a
+// tie, r05v_ab_stprio.txt).
 static hipError_t dl_stream(wsg_batcher* b) {
   return b->s_dl ? hipSuccess : high_stream(&b->s_dl);
 }
@@ -1253,7 +1253,6 @@ int wsg_batcher_close(wsg_batcher* b) {
     (void)hipStreamDestroy(b->s_dl);
   }
   if (b->sctx) (void)wsg_close(b->sctx);
-  if (b->s_stage) (void)hipStreamDestroy(b->s_stage);
   for (int i = 0; i < kTokCtx; ++i) {
     if (b->tctx[i]) (void)wsg_close(b->tctx[i]);
     b->d_tdesc[i].release();
@@ -1773,10 +1772,7 @@ int wsg_batcher_set_stages(wsg_batcher* b, const wsg_stage_cfg* stages) {
   b->stage_resets.clear();
   if (b->has_stages) {  // the device-resident stage carry, zeroed (fresh stage decoders)
     if (!b->sctx) {
-#ifdef WSG_AB_STAGE_PRIO
-      B_TRY(b, high_stream(&b->s_stage));  // (A/B) the replay chain at high priority too
-#endif
-      const int rc = wsg_open(ws::ctx_device(b->ctx), b->s_stage, &b->sctx);
+      const int rc = wsg_open(ws::ctx_device(b->ctx), nullptr, &b->sctx);
       if (rc) return bset(b, rc, "wsg_open (stage context)");
     }
     ws::ctx_copy_tuning(b->sctx, b->ctx);  // (the batcher context's switches hold for its stages)
