@@ -340,7 +340,10 @@ def main():
     if world == 1 and not args.no_extras:
         del wire, payload, desc, res, state, off, sf
         torch.cuda.empty_cache()
-        extras = [config0_line()] + measure_extras(ctx, dev, args)
+        # the host-to-host batcher lines first, before the secondary configs: configs[3]'s
+        # 34 GB shard and the others leave the host's memory in a state that slows these
+        # lines' feeds and copies by a quarter (round 5: encode batcher 28.7 in the suite
+        # against 40.5-40.8 GiB/s alone, the stage line 17.3 against 22.5)
         if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
             e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 1)
             # the same sessions streaming 4x longer: the pipeline's fill and drain (a pass of
@@ -348,6 +351,7 @@ def main():
             e2e["native_batcher_stages_steady"] = e2e_stages_line(ctx, dev, 2, 1, msgs=64)
             e2e["native_encode_batcher"] = e2e_encode_line(ctx, dev, 3, 1)
             e2e["native_batcher_aggregate"] = e2e_aggregate_line(ctx, dev, 3, 1)
+        extras = [config0_line()] + measure_extras(ctx, dev, args)
 
     # the CPU baseline runs after every timed region, on rank 0 only (at N > 1 the
     # other ranks wait for it at the closing barrier)
