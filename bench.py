@@ -15,6 +15,7 @@ exits with their status; under a launcher, --gpus must equal WORLD_SIZE.
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import shutil
@@ -340,10 +341,13 @@ def main():
     if world == 1 and not args.no_extras:
         del wire, payload, desc, res, state, off, sf
         torch.cuda.empty_cache()
-        # the host-to-host batcher lines first, before the secondary configs: configs[3]'s
-        # 34 GB shard and the others leave the host's memory in a state that slows these
-        # lines' feeds and copies by a quarter (round 5: encode batcher 28.7 in the suite
-        # against 40.5-40.8 GiB/s alone, the stage line 17.3 against 22.5)
+        # the pinned buffers of the lines above (≈ 13 GB, held by torch's pinned-memory
+        # cache) go back before the host-to-host batcher lines (round 5: with them held,
+        # the encode batcher measured 28.7 in the suite against 40.5-40.8 GiB/s alone,
+        # the stage line 17.3 against 22.5)
+        gc.collect()
+        if hasattr(torch._C, "_host_emptyCache"):
+            torch._C._host_emptyCache()
         if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
             e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 1)
             # the same sessions streaming 4x longer: the pipeline's fill and drain (a pass of
