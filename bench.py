@@ -342,19 +342,19 @@ def main():
         del wire, payload, desc, res, state, off, sf
         torch.cuda.empty_cache()
         # the pinned buffers of the lines above (≈ 13 GB, held by torch's pinned-memory
-        # cache) go back before the host-to-host batcher lines (round 5: with them held,
-        # the encode batcher measured 28.7 in the suite against 40.5-40.8 GiB/s alone,
-        # the stage line 17.3 against 22.5)
+        # cache) go back before the host-to-host batcher lines; those lines take two
+        # untimed passes, as with --only (one was not enough: the encode batcher measured
+        # 29.2 GiB/s after one in a fresh process, 40.3 after two; scripts/e2e_probe_w.py)
         gc.collect()
         if hasattr(torch._C, "_host_emptyCache"):
             torch._C._host_emptyCache()
         if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
-            e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 1)
+            e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 2)
             # the same sessions streaming 4x longer: the pipeline's fill and drain (a pass of
             # 5 flushes spends 2-3 of them filling and draining) amortised over ~20 flushes
-            e2e["native_batcher_stages_steady"] = e2e_stages_line(ctx, dev, 2, 1, msgs=64)
-            e2e["native_encode_batcher"] = e2e_encode_line(ctx, dev, 3, 1)
-            e2e["native_batcher_aggregate"] = e2e_aggregate_line(ctx, dev, 3, 1)
+            e2e["native_batcher_stages_steady"] = e2e_stages_line(ctx, dev, 2, 2, msgs=64)
+            e2e["native_encode_batcher"] = e2e_encode_line(ctx, dev, 3, 2)
+            e2e["native_batcher_aggregate"] = e2e_aggregate_line(ctx, dev, 3, 2)
         extras = [config0_line()] + measure_extras(ctx, dev, args)
 
     # the CPU baseline runs after every timed region, on rank 0 only (at N > 1 the
