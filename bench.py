@@ -1002,11 +1002,16 @@ def e2e_encode_line(ctx, dev, K, W, n_s=64, msg_bytes=16 << 20, frame=65536, per
     wsg_enc_batcher_flush_async; two flushes in flight, each waited view's wire bytes
     counted.  Value: wire bytes out per second."""
     import numpy as np
+    import torch
     import snf4j_amd
     rng = np.random.default_rng(0xE4C)
     src = rng.integers(0, 256, msg_bytes, dtype=np.uint8)  # the same message bytes for every session
     nf = msg_bytes // frame
-    eb = snf4j_amd.EncodeBatcher(n_s, True, ctx=ctx)
+    # the batcher on a context of its own, as a selector loop's is (WsgBatcher), not on
+    # the one the device-resident lines used
+    pctx = snf4j_amd.Context(dev.index, stream=torch.cuda.Stream(dev))
+    apply_tuning(pctx)
+    eb = snf4j_amd.EncodeBatcher(n_s, True, ctx=pctx)
     masks = rng.integers(0, 256, (n_s, nf, 4), dtype=np.uint8)
     base = src.ctypes.data
     # a round's writes, session by session: fragments [r, r + per_round) of every session
@@ -1041,6 +1046,7 @@ def e2e_encode_line(ctx, dev, K, W, n_s=64, msg_bytes=16 << 20, frame=65536, per
             times.append(t)
         wire_total = wb
     eb.close()
+    pctx.close()
     exp = n_s * nf * (frame + 14)
     assert wire_total == exp, (wire_total, exp)
     t = float(np.median(times))

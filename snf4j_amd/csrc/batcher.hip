@@ -2125,8 +2125,16 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   const int slot = b->open;
   EncSlot& e = b->es[slot];
   E_TRY(b, hipSetDevice(ws::ctx_device(b->ctx)));
+#if defined(WSG_AB_ENC_PRIO_BOTH)
+  if (!b->s_in) E_TRY(b, high_stream(&b->s_in));
+  if (!b->s_out) E_TRY(b, high_stream(&b->s_out));
+#elif defined(WSG_AB_ENC_PRIO_OUT)
+  if (!b->s_in) E_TRY(b, hipStreamCreateWithFlags(&b->s_in, hipStreamNonBlocking));
+  if (!b->s_out) E_TRY(b, high_stream(&b->s_out));
+#else
   if (!b->s_in) E_TRY(b, hipStreamCreateWithFlags(&b->s_in, hipStreamNonBlocking));
   if (!b->s_out) E_TRY(b, hipStreamCreateWithFlags(&b->s_out, hipStreamNonBlocking));
+#endif
   hipEvent_t* evs[] = {&e.ev_in, &e.ev_k, &e.ev_out};
   for (hipEvent_t* v : evs)
     if (!*v) E_TRY(b, hipEventCreateWithFlags(v, hipEventDisableTiming));
