@@ -2,11 +2,12 @@
 in one process, then after creating and destroying 1-3 more streams, to tell whether
 what slows it is where the runtime puts its new streams (hardware queue sharing)."""
 import json
+import os
 import sys
 
 import torch
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 import snf4j_amd  # noqa: E402
 

@@ -2125,16 +2125,8 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   const int slot = b->open;
   EncSlot& e = b->es[slot];
   E_TRY(b, hipSetDevice(ws::ctx_device(b->ctx)));
-#if defined(WSG_AB_ENC_PRIO_BOTH)
-  if (!b->s_in) E_TRY(b, high_stream(&b->s_in));
-  if (!b->s_out) E_TRY(b, high_stream(&b->s_out));
-#elif defined(WSG_AB_ENC_PRIO_OUT)
-  if (!b->s_in) E_TRY(b, hipStreamCreateWithFlags(&b->s_in, hipStreamNonBlocking));
-  if (!b->s_out) E_TRY(b, high_stream(&b->s_out));
-#else
   if (!b->s_in) E_TRY(b, hipStreamCreateWithFlags(&b->s_in, hipStreamNonBlocking));
   if (!b->s_out) E_TRY(b, hipStreamCreateWithFlags(&b->s_out, hipStreamNonBlocking));
-#endif
   hipEvent_t* evs[] = {&e.ev_in, &e.ev_k, &e.ev_out};
   for (hipEvent_t* v : evs)
     if (!*v) E_TRY(b, hipEventCreateWithFlags(v, hipEventDisableTiming));
@@ -2160,7 +2152,15 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   E_TRY(b, e.d_frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
   E_TRY(b, e.d_sf.ensure((S + 1) * sizeof(uint32_t)));
   E_TRY(b, e.d_cl.ensure(S + 1));
+#ifdef WSG_AB_ENC_DIRECT
+  // the kernels write the wire straight into the pinned host buffer (PCIe writes from the
+  // encode kernel itself: no device copy and no runtime D2H of it)
+  uint8_t* wire_out = nullptr;
+  E_TRY(b, hipHostGetDevicePointer((void**)&wire_out, e.wire.p, 0));
+#else
   E_TRY(b, e.d_wire.ensure(need + 32));
+  uint8_t* wire_out = e.d_wire.p;
+#endif
   E_TRY(b, e.d_off.ensure((F + 1) * sizeof(uint64_t)));
   if (e.arena_len) E_TRY(b, hipMemcpyAsync(e.d_pay.p, e.arena.p, e.arena_len, hipMemcpyHostToDevice, b->s_in));
   if (F) E_TRY(b, hipMemcpyAsync(e.d_frames.p, e.frames.p, F * sizeof(wsg_encode_frame), hipMemcpyHostToDevice, b->s_in));
@@ -2170,7 +2170,7 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   hipStream_t ks = ws::ctx_stream(b->ctx);
   E_TRY(b, hipStreamWaitEvent(ks, e.ev_in, 0));
   int rc = wsg_encode_batch_device(b->ctx, b->client, e.d_pay.p, e.arena_len, (const wsg_encode_frame*)e.d_frames.p,
-                                   F, (const uint32_t*)e.d_sf.p, S, e.d_cl.p, e.d_wire.p, need + 32,
+                                   F, (const uint32_t*)e.d_sf.p, S, e.d_cl.p, wire_out, need + 32,
                                    (uint64_t*)e.d_off.p);
   if (rc) return eset(b, rc, wsg_last_error(b->ctx));
   if (!F) E_TRY(b, hipMemsetAsync(e.d_off.p, 0, sizeof(uint64_t), ks));
@@ -2178,7 +2178,9 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   E_TRY(b, hipStreamWaitEvent(b->s_out, e.ev_k, 0));
   E_TRY(b, hipMemcpyAsync(e.off.p, e.d_off.p, (F + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, b->s_out));
   // (the kept frames' bytes are at most `need`: frames dropped after a CLOSE take none)
+#ifndef WSG_AB_ENC_DIRECT
   if (need) E_TRY(b, hipMemcpyAsync(e.wire.p, e.d_wire.p, need, hipMemcpyDeviceToHost, b->s_out));
+#endif
   E_TRY(b, hipEventRecord(e.ev_out, b->s_out));
   E_TRY(b, notify_after(b->s_out, b->notify, b->tickets + 1));
   ++b->tickets;
