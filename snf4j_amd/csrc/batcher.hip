@@ -1958,7 +1958,7 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
 struct EncSlot {
   PinnedBuf arena, frames, sf, cl, wire, off;
   uint64_t arena_len = 0, F = 0, need = 0;
-  DBuf d_pay, d_frames, d_sf, d_cl, d_wire, d_off;
+  DBuf d_pay, d_frames, d_sf, d_cl, d_off;
   hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_out = nullptr;
   std::vector<uint32_t> resets;  // sessions reset while this flush was in flight: their bytes are dropped
   // the view with those sessions' frames left out (built only when there are some)
@@ -2017,7 +2017,7 @@ int wsg_enc_batcher_close(wsg_enc_batcher* b) {
   for (EncSlot& e : b->es) {
     PinnedBuf* bufs[] = {&e.arena, &e.frames, &e.sf, &e.cl, &e.wire, &e.off};
     for (PinnedBuf* p : bufs) p->release();
-    DBuf* dbufs[] = {&e.d_pay, &e.d_frames, &e.d_sf, &e.d_cl, &e.d_wire, &e.d_off};
+    DBuf* dbufs[] = {&e.d_pay, &e.d_frames, &e.d_sf, &e.d_cl, &e.d_off};
     for (DBuf* d : dbufs) d->release();
     hipEvent_t evs[] = {e.ev_in, e.ev_k, e.ev_out};
     for (hipEvent_t v : evs)
@@ -2152,15 +2152,15 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   E_TRY(b, e.d_frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
   E_TRY(b, e.d_sf.ensure((S + 1) * sizeof(uint32_t)));
   E_TRY(b, e.d_cl.ensure(S + 1));
-#ifdef WSG_AB_ENC_DIRECT
-  // the kernels write the wire straight into the pinned host buffer (PCIe writes from the
-  // encode kernel itself: no device copy and no runtime D2H of it)
+  // The kernels write the wire straight into the pinned host buffer (PCIe writes from
+  // the encode kernel itself), not to the device for a runtime D2H: that D2H is a blit
+  // kernel on the download stream, and where the runtime places the batcher's streams
+  // on the process's hardware queues decided whether it overlapped the next flush's
+  // upload — 26.6-29.5 GiB/s against 39.3-40.5 on the e2e encode line depending on the
+  // streams created before it; written directly, 36.1-37.8 whatever the placement
+  // (profiles/r05_ab/r05ad_ab_encdirect.txt, scripts/seq_probe.py).
   uint8_t* wire_out = nullptr;
   E_TRY(b, hipHostGetDevicePointer((void**)&wire_out, e.wire.p, 0));
-#else
-  E_TRY(b, e.d_wire.ensure(need + 32));
-  uint8_t* wire_out = e.d_wire.p;
-#endif
   E_TRY(b, e.d_off.ensure((F + 1) * sizeof(uint64_t)));
   if (e.arena_len) E_TRY(b, hipMemcpyAsync(e.d_pay.p, e.arena.p, e.arena_len, hipMemcpyHostToDevice, b->s_in));
   if (F) E_TRY(b, hipMemcpyAsync(e.d_frames.p, e.frames.p, F * sizeof(wsg_encode_frame), hipMemcpyHostToDevice, b->s_in));
@@ -2178,9 +2178,6 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   E_TRY(b, hipStreamWaitEvent(b->s_out, e.ev_k, 0));
   E_TRY(b, hipMemcpyAsync(e.off.p, e.d_off.p, (F + 1) * sizeof(uint64_t), hipMemcpyDeviceToHost, b->s_out));
   // (the kept frames' bytes are at most `need`: frames dropped after a CLOSE take none)
-#ifndef WSG_AB_ENC_DIRECT
-  if (need) E_TRY(b, hipMemcpyAsync(e.wire.p, e.d_wire.p, need, hipMemcpyDeviceToHost, b->s_out));
-#endif
   E_TRY(b, hipEventRecord(e.ev_out, b->s_out));
   E_TRY(b, notify_after(b->s_out, b->notify, b->tickets + 1));
   ++b->tickets;
@@ -2285,7 +2282,6 @@ int wsg_enc_batcher_reserve(wsg_enc_batcher* b, uint64_t max_frames, uint64_t ma
     E_TRY(b, e.d_frames.ensure((max_frames + 1) * sizeof(wsg_encode_frame)));
     E_TRY(b, e.d_sf.ensure((S + 1) * sizeof(uint32_t)));
     E_TRY(b, e.d_cl.ensure(S + 1));
-    E_TRY(b, e.d_wire.ensure(need + 32));
     E_TRY(b, e.d_off.ensure((max_frames + 1) * sizeof(uint64_t)));
   }
   return WSG_API_OK;
