@@ -1395,7 +1395,6 @@ int wsg_batcher_close(wsg_batcher* b) {
     f.dpay.release();
     f.so.pay.release();
     f.so.d_copy.release();
-    f.so.d_lay.release();
     if (f.so.gathered) (void)hipEventDestroy(f.so.gathered);
     if (f.so.downloaded) (void)hipEventDestroy(f.so.downloaded);
     if (f.done) (void)hipEventDestroy(f.done);
@@ -2025,7 +2024,6 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
     B_TRY(b, f.dpay.grow_keep(arena, 0, st));
     B_TRY(b, f.so.pay.ensure(out));
     B_TRY(b, f.so.d_copy.ensure((copies + 1) * sizeof(StageCopy)));
-    B_TRY(b, f.so.d_lay.ensure(16));
     B_TRY(b, f.so.d_copy.up.ensure((copies + 1) * sizeof(StageCopy)));
     if (!f.dpay_done) B_TRY(b, hipEventCreateWithFlags(&f.dpay_done, hipEventDisableTiming));
     if (!f.so.gathered) B_TRY(b, hipEventCreateWithFlags(&f.so.gathered, hipEventDisableTiming));
