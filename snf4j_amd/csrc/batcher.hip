@@ -303,11 +303,8 @@ constexpr uint32_t GATHER_GROUPS = 12;  // workgroups of the output gather: enou
                                          // that the next flush's small downloads still get a share of it
 #endif
 
-// (n_dev: the copy count as the device-side layout left it, k_stage_layout)
 __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                    const StageCopy* __restrict__ cp, uint32_t n,
-                                                    const uint32_t* __restrict__ n_dev) {
-  if (n_dev) n = *n_dev;
+                                                    const StageCopy* __restrict__ cp, uint32_t n) {
   for (uint32_t ci = blockIdx.x; ci < n; ci += gridDim.x) {
   const StageCopy c = cp[ci];
   const uint8_t* s = src + c.src;
@@ -361,83 +358,6 @@ __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ 
   }
   for (uint32_t i = done + t; i < c.len; i += 256) d[i] = s[i];
   }
-}
-
-// The output layout of an inflate (+ validator) flush on the device, so that its gather
-// starts when the validator ends instead of after the host's collection (one
-// workgroup).  The rule is the host's (stage_compute / fin_push): sessions in order,
-// each its delivered frames — the n_delivered inflate frames after its replayed ones,
-// cut at the validator's failure — each at the next 16-B aligned offset, split into
-// copies of at most COPY_MAX.  A session whose output region overflowed (re-run by the
-// host) takes nothing here; the host compares its own counts and gathers again when
-// they differ (that, a slot reset since, or an output beyond `cap`: then n_copies = 0).
-constexpr uint32_t LAYOUT_T = 1024;
-__global__ __launch_bounds__(LAYOUT_T) void k_stage_layout(
-    const wsg_frame_desc* __restrict__ od, const uint32_t* __restrict__ xsf, const uint32_t* __restrict__ nheld,
-    const wsg_session_result* __restrict__ ores, const wsg_session_result* __restrict__ vres, uint32_t S, uint32_t F,
-    uint64_t ipos, uint64_t cap, uint32_t max_copies, StageCopy* __restrict__ copies, uint32_t* __restrict__ n_copies) {
-  __shared__ uint64_t sb[LAYOUT_T];
-  __shared__ uint32_t sc[LAYOUT_T];
-  const uint32_t t = threadIdx.x, m = (F + LAYOUT_T - 1) / LAYOUT_T;
-  const uint32_t k0 = min(F, t * m), k1 = min(F, k0 + m);
-  // the session of frame k0: the last s with xsf[s] <= k0
-  uint32_t lo = 0, hi = S;
-  while (lo + 1 < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (xsf[mid] <= k0) lo = mid; else hi = mid;
-  }
-  auto frame = [&](uint32_t k, uint32_t& s, uint32_t& first, uint32_t& n, bool& moved) {
-    while (s + 1 < S && xsf[s + 1] <= k) { ++s; moved = true; }
-    if (moved) {
-      moved = false;
-      const uint32_t nh = nheld[s], fs = xsf[s + 1] - xsf[s];
-      first = xsf[s] + nh;
-      const wsg_session_result r = ores[s];
-      n = r.error == WSG_E_INFLATE_CAPACITY ? 0u : min(r.n_delivered, fs > nh ? fs - nh : 0u);
-      if (vres && vres[s].error) n = min(n, vres[s].n_delivered >= nh ? vres[s].n_delivered - nh : 0u);
-    }
-    return k >= first && k - first < n;
-  };
-  uint64_t bytes = 0;
-  uint32_t ncp = 0;
-  {
-    uint32_t s = lo, first = 0, n = 0;
-    bool moved = true;
-    for (uint32_t k = k0; k < k1; ++k)
-      if (frame(k, s, first, n, moved)) {
-        const uint32_t len = od[k].payload_len;
-        bytes += (len + 15u) & ~15ull;
-        ncp += (len + COPY_MAX - 1) / COPY_MAX;
-      }
-  }
-  sb[t] = bytes;
-  sc[t] = ncp;
-  __syncthreads();
-  for (uint32_t d = 1; d < LAYOUT_T; d <<= 1) {  // inclusive scan (Hillis-Steele)
-    const uint64_t vb = t >= d ? sb[t - d] : 0;
-    const uint32_t vc = t >= d ? sc[t - d] : 0;
-    __syncthreads();
-    sb[t] += vb;
-    sc[t] += vc;
-    __syncthreads();
-  }
-  const uint64_t total = sb[LAYOUT_T - 1];
-  const uint32_t total_cp = sc[LAYOUT_T - 1];
-  const bool fits = total <= cap && total_cp <= max_copies;
-  if (t == 0) n_copies[0] = fits ? total_cp : 0u;
-  if (!fits) return;
-  uint64_t pos = sb[t] - bytes;
-  uint32_t ci = sc[t] - ncp;
-  uint32_t s = lo, first = 0, n = 0;
-  bool moved = true;
-  for (uint32_t k = k0; k < k1; ++k)
-    if (frame(k, s, first, n, moved)) {
-      const wsg_frame_desc d = od[k];
-      const uint64_t src = d.payload_off + ((d.flags & WSG_DESC_INFLATED) ? ipos : 0);
-      for (uint32_t o = 0; o < d.payload_len; o += COPY_MAX)
-        copies[ci++] = StageCopy{src + o, pos + o, min(COPY_MAX, d.payload_len - o), 0u};
-      pos += (d.payload_len + 15u) & ~15ull;
-    }
 }
 
 // Fresh stage decoders for the sessions in sids[0..n): one workgroup per session zeroes
@@ -525,7 +445,6 @@ struct StageOut {
   uint64_t len = 0;
   PinnedBuf pay;
   DBuf d_copy;
-  DBuf d_lay;  // the device-side layout's copy count (k_stage_layout)
   hipEvent_t gathered = nullptr, downloaded = nullptr;
   bool staged = false;  // computed, download queued (wsg_batcher_wait collects it)
 };
@@ -552,10 +471,6 @@ struct InflJob {
   std::vector<uint64_t> od_at;
   std::vector<uint32_t> od_n;
   bool in_order = true;              // (a session re-run for capacity comes after the others)
-  bool dev_gather = false;           // the output gather queued from the device's layout (k_stage_layout)
-  bool dev_match = false;            //   and the host's delivered counts agree with it
-  uint64_t dev_cap = 0;              //   the output bytes it could take
-  uint32_t dev_max_copies = 0;       //   and the copies
 };
 
 // One flush's pinned staging and results (two alternate: a flush can be in flight
@@ -635,13 +550,6 @@ struct wsg_batcher {
   PinnedBuf h_pend;                     // aggregator bytes held for the next flush, downloaded
   DBuf d_pend;
   hipStream_t s_dl = nullptr;           // downloads of stage outputs
-#ifdef WSG_AB_NO_DEV_LAYOUT
-  bool dev_layout = false;              // (A/B build)
-#else
-  bool dev_layout = true;               // inflate-only chains: the output laid out on the device (k_stage_layout)
-#endif
-  bool fin_count_only = false;          // fin_push: count the copies, do not list them
-  uint64_t fin_copies = 0;
   StageOut* out = nullptr;              // the output the stage run at hand writes
   uint64_t tickets = 0;                 // flushes queued so far (flush t's ticket is t)
   std::shared_ptr<Notify> notify = std::make_shared<Notify>();
@@ -708,24 +616,6 @@ static hipError_t upload(DBuf& d, const std::vector<T>& v, hipStream_t s) {
 #endif
 }
 
-// A stream at the device's highest priority: the queue's dispatches go ahead of the
-// other streams' (the pre-decode, the next flushes' decode).
-static hipError_t high_stream(hipStream_t* s) {
-  int lo = 0, hi = 0;
-  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
-  return e != hipSuccess ? e : hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
-}
-
-// The stage outputs' download stream, at high priority: the output gather is what a
-// flush's collection waits for, and its few workgroups were dispatched behind the
-// pre-decode's and replay's (stage lines +7%: burst 18.8-19.0 -> 19.7-20.9, steady
-// 25.1-25.6 -> 26.5-27.7 GiB/s, profiles/r05_ab/r05u_ab_prio.txt; the gather's waves at
-// s_setprio 3 instead: no gain; the stage context's stream at high priority as well: a
-// tie, r05v_ab_stprio.txt).
-static hipError_t dl_stream(wsg_batcher* b) {
-  return b->s_dl ? hipSuccess : high_stream(&b->s_dl);
-}
-
 // PerMessageDeflateDecoder over a flush's frames (PerMessageDeflateDecoder.java:68-105),
 // on the device, with FrameUtf8Validator behind it: each session's frames after the
 // frames of a message it left open; the inflated bytes go to the arena after the
@@ -737,7 +627,7 @@ static hipError_t dl_stream(wsg_batcher* b) {
 
 // this attempt's input: the todo sessions' frames; every session takes part (the carry
 // is indexed by session), the others with no frames
-static int infl_launch(wsg_batcher* b, FlushSlot& f, bool first) {
+static int infl_launch(wsg_batcher* b, FlushSlot& f) {
   SP(13);
   const uint32_t S = b->n;
   hipStream_t st = ws::ctx_stream(b->sctx);
@@ -857,31 +747,6 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f, bool first) {
     B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
     B_TRY(b, hipMemcpyAsync(b->h_vres.p, b->d_vres.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
   }
-  // the output gather queued now, from the device's layout of this attempt's results
-  // (the first attempt of an inflate-only chain; the host checks it at collection)
-  StageOut& o = f.so;
-  const uint32_t max_copies = o.d_copy.n >= 2 * sizeof(StageCopy) ? (uint32_t)(o.d_copy.n / sizeof(StageCopy) - 1) : 0u;
-  if (first && b->dev_layout && !b->stages.aggregate && F && o.pay.n > 16 && max_copies) {
-    if (!j.validate) B_TRY(b, upload(b->d_nheld, j.nheld, st));
-    B_TRY(b, o.d_lay.ensure(16));
-    j.dev_cap = o.pay.n - 16;
-    j.dev_max_copies = max_copies;
-    hipLaunchKernelGGL(k_stage_layout, dim3(1), dim3(LAYOUT_T), 0, st, (const wsg_frame_desc*)b->d_odesc.p, dxsf,
-                       (const uint32_t*)b->d_nheld.p, (const wsg_session_result*)b->d_ores.p,
-                       j.validate ? (const wsg_session_result*)b->d_vres.p : nullptr, S, (uint32_t)F, ipos, j.dev_cap,
-                       max_copies, (StageCopy*)o.d_copy.p, (uint32_t*)o.d_lay.p);
-    B_TRY(b, hipGetLastError());
-    if (!o.gathered) B_TRY(b, hipEventCreateWithFlags(&o.gathered, hipEventDisableTiming));
-    B_TRY(b, hipEventRecord(o.gathered, st));
-    B_TRY(b, dl_stream(b));
-    B_TRY(b, hipStreamWaitEvent(b->s_dl, o.gathered, 0));
-    uint8_t* dst = nullptr;
-    B_TRY(b, hipHostGetDevicePointer((void**)&dst, o.pay.p, 0));
-    hipLaunchKernelGGL(k_stage_copy, dim3(GATHER_GROUPS), dim3(256), 0, b->s_dl, ar.p, dst, (const StageCopy*)o.d_copy.p,
-                       0u, (const uint32_t*)o.d_lay.p);
-    B_TRY(b, hipGetLastError());
-    j.dev_gather = true;
-  }
   if (!j.launched) B_TRY(b, hipEventCreateWithFlags(&j.launched, hipEventDisableTiming));
   B_TRY(b, hipEventRecord(j.launched, st));
   return WSG_API_OK;
@@ -902,7 +767,6 @@ static int infl_begin(wsg_batcher* b, FlushSlot& f) {
   j.od_at.assign(S, 0);
   j.od_n.assign(S, 0);
   j.in_order = true;
-  j.dev_gather = j.dev_match = false;
   // the held frames' bytes go after the decoded payloads; sessions a stage closed or a
   // reset gave to a new session since the input was built take no part
   uint64_t hpos = j.used;
@@ -931,7 +795,7 @@ static int infl_begin(wsg_batcher* b, FlushSlot& f) {
   }
   j.ipos = al16(hpos);
   if (j.todo.empty()) return WSG_API_OK;
-  return infl_launch(b, f, true);
+  return infl_launch(b, f);
 }
 
 // Wait for the attempt in flight, take its results (runs again what overflowed), and
@@ -1009,23 +873,10 @@ static int infl_collect(wsg_batcher* b, FlushSlot& f) {
                                 hipMemcpyDeviceToHost, st));
     if (!hd_copies.empty()) B_TRY(b, hipStreamSynchronize(st));
     j.ipos = al16(ipos + j.oo[S]);
-    if (j.dev_gather && retry.empty() && !j.dev_match) {
-      // the first attempt's results: the device's layout took, per session, the counts
-      // k_stage_layout computes; the host's may be fewer (a slot reset since)
-      bool match = true;
-      for (uint32_t s : j.todo) {
-        const uint32_t nh = j.nheld[s], fs = x.sf[s + 1] - x.sf[s];
-        uint32_t n = r[s].error == WSG_E_INFLATE_CAPACITY ? 0u : std::min(r[s].n_delivered, fs > nh ? fs - nh : 0u);
-        if (vr && vr[s].error) n = std::min(n, vr[s].n_delivered >= nh ? vr[s].n_delivered - nh : 0u);
-        match &= n == j.od_n[s];
-      }
-      j.dev_match = match;
-    }
     if (!retry.empty()) j.in_order = false;
     j.todo.swap(retry);
     if (!j.todo.empty()) {
-      if (j.dev_gather) B_TRY(b, hipStreamSynchronize(b->s_dl));  // (the arena may move: the gather reads it)
-      const int rc = infl_launch(b, f, false);
+      const int rc = infl_launch(b, f);
       if (rc) return rc;
     }
   }
@@ -1050,6 +901,24 @@ static int infl_collect(wsg_batcher* b, FlushSlot& f) {
   return WSG_API_OK;
 }
 
+// A stream at the device's highest priority: the queue's dispatches go ahead of the
+// other streams' (the pre-decode, the next flushes' decode).
+static hipError_t high_stream(hipStream_t* s) {
+  int lo = 0, hi = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&lo, &hi);
+  return e != hipSuccess ? e : hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
+}
+
+// The stage outputs' download stream, at high priority: the output gather is what a
+// flush's collection waits for, and its few workgroups were dispatched behind the
+// pre-decode's and replay's (stage lines +7%: burst 18.8-19.0 -> 19.7-20.9, steady
+// 25.1-25.6 -> 26.5-27.7 GiB/s, profiles/r05_ab/r05u_ab_prio.txt; the gather's waves at
+// s_setprio 3 instead: no gain; the stage context's stream at high priority as well: a
+// tie, r05v_ab_stprio.txt).
+static hipError_t dl_stream(wsg_batcher* b) {
+  return b->s_dl ? hipSuccess : high_stream(&b->s_dl);
+}
+
 // append an output frame: dev_len bytes at arena offset src, after `prefix` (host bytes)
 static void fin_push(wsg_batcher* b, wsg_frame_desc d, uint64_t src, uint32_t dev_len, std::vector<uint8_t>* prefix) {
   StageOut& fp = *b->out;
@@ -1057,13 +926,9 @@ static void fin_push(wsg_batcher* b, wsg_frame_desc d, uint64_t src, uint32_t de
   const uint64_t pre = prefix ? prefix->size() : 0;
   d.payload_off = pos;
   d.payload_len = (uint32_t)(pre + dev_len);
-  if (b->fin_count_only) {  // (the device laid the copies out: only their number)
-    b->fin_copies += (dev_len + COPY_MAX - 1) / COPY_MAX;
-  } else {
-    for (uint64_t o = 0; o < dev_len; o += COPY_MAX) {
-      const uint32_t n = (uint32_t)std::min<uint64_t>(COPY_MAX, dev_len - o);
-      fp.copies.push_back({src + o, pos + pre + o, n, 0});
-    }
+  for (uint64_t o = 0; o < dev_len; o += COPY_MAX) {
+    const uint32_t n = (uint32_t)std::min<uint64_t>(COPY_MAX, dev_len - o);
+    fp.copies.push_back({src + o, pos + pre + o, n, 0});
   }
   if (pre) fp.host_parts.emplace_back(pos, std::move(*prefix));
   fp.len = al16(pos + pre + dev_len);
@@ -1159,7 +1024,7 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
     B_TRY(b, hipHostGetDevicePointer((void**)&dst, b->h_pend.p, 0));
     const uint32_t n = (uint32_t)pc.size();
     hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, GATHER_GROUPS)), dim3(256), 0, st, b->ar->p, dst,
-                       (const StageCopy*)b->d_pend.p, n, nullptr);
+                       (const StageCopy*)b->d_pend.p, n);
     B_TRY(b, hipGetLastError());
     B_TRY(b, hipStreamSynchronize(st));
     for (const auto& pe : pending) {
@@ -1276,44 +1141,18 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
   f.ij.prepped = false;
   StageList& cur = f.ij.cur;
   const uint64_t used = f.ij.used;
-  // the device's layout holds when the host delivers exactly what it laid out (no slot
-  // reset since, no capacity re-run) and it fitted the output buffer and copy list
-  bool dev = false;
   if (b->stages.aggregate) {
     if ((rc = stage_aggregate(b, cur, used))) return rc;
   } else {
     SP(19);
-    const bool try_dev = f.ij.dev_gather && f.ij.dev_match && f.ij.in_order;
-    b->fin_count_only = try_dev;
-    b->fin_copies = 0;
     for (uint32_t s = 0; s < S; ++s) {
       o.sf[s] = (uint32_t)o.desc.size();
       for (uint32_t k = cur.sf[s]; k < cur.sf[s] + cur.n_ok[s]; ++k)
         fin_push(b, cur.desc[k], cur.desc[k].payload_off, cur.desc[k].payload_len, nullptr);
       o.res[s].n_delivered = cur.n_ok[s];
     }
-    b->fin_count_only = false;
-    dev = try_dev && o.len <= f.ij.dev_cap && b->fin_copies <= f.ij.dev_max_copies;
-    if (try_dev && !dev) {  // (the layout did not fit: the copies the host gathers)
-      o.desc.clear();
-      o.len = 0;
-      for (uint32_t s = 0; s < S; ++s) {
-        o.sf[s] = (uint32_t)o.desc.size();
-        for (uint32_t k = cur.sf[s]; k < cur.sf[s] + cur.n_ok[s]; ++k)
-          fin_push(b, cur.desc[k], cur.desc[k].payload_off, cur.desc[k].payload_len, nullptr);
-      }
-    }
   }
   o.sf[S] = (uint32_t)o.desc.size();
-  if (dev) {  // gathered already (queued behind the validator by infl_launch)
-    if (!o.downloaded) B_TRY(b, hipEventCreateWithFlags(&o.downloaded, hipEventDisableTiming));
-    B_TRY(b, hipEventRecord(o.downloaded, b->s_dl));
-    o.staged = true;
-    return WSG_API_OK;
-  }
-  // the device's gather, if one was queued, may still write the output and read the copy
-  // list this one replaces
-  if (f.ij.dev_gather) B_TRY(b, hipStreamSynchronize(b->s_dl));
   SP(7);
   // the output: gathered from this flush's arena straight into the pinned host buffer
   // by a few workgroups on the download stream (PCIe writes), so the next flush's
@@ -1339,7 +1178,7 @@ static int stage_compute(wsg_batcher* b, FlushSlot& f, const wsg_session_result*
     uint8_t* dst = nullptr;
     B_TRY(b, hipHostGetDevicePointer((void**)&dst, o.pay.p, 0));
     hipLaunchKernelGGL(k_stage_copy, dim3(std::min<uint32_t>(n, GATHER_GROUPS)), dim3(256), 0, b->s_dl, b->ar->p,
-                       dst, (const StageCopy*)o.d_copy.p, n, nullptr);
+                       dst, (const StageCopy*)o.d_copy.p, n);
     B_TRY(b, hipGetLastError());
   }
   B_TRY(b, hipEventRecord(o.downloaded, b->s_dl));
