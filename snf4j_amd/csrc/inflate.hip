@@ -753,6 +753,9 @@ constexpr uint32_t QF_L = 0, QF_D = 1u << QF_LROOT;  // their u16 offsets
 constexpr uint32_t Q_LT = QF_D + (1u << QF_DROOT);   // lane tables: entry j of lane i at Q_LT + j * 64 + i
 constexpr uint32_t Q_DT = Q_LT + QL_N * 64;
 constexpr uint32_t Q_TAB = Q_DT + QD_N * 64;
+#ifndef WSG_TOK_MATCH1
+#define WSG_TOK_MATCH1 0  // a match's length and distance in one lane-decoder step (A/B)
+#endif
 #ifndef WSG_TOK_MIRROR
 #define WSG_TOK_MIRROR 1
 #endif
@@ -1365,10 +1368,33 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
         }
       }
       const bool is_lit = !dist && eo == OP_LIT, is_len = !dist && eo == OP_BASE;
-      const uint32_t has_run = (dist && run) ? 1u : 0u;
+#if WSG_TOK_MATCH1
+      // A length's distance in the same step (a match in one step instead of two) when its
+      // code resolves at the distance root, is a valid distance, and all its bits are held
+      // (a step holds 32-63 bits; otherwise the next step decodes it as before).
+      bool m1 = false;
+      uint32_t dv = 0, dbits = 0;
+      if (!PAIR) {
+        const uint32_t sh1 = len + x;
+        const uint64_t h2 = hold >> sh1;
+        const uint32_t rd = tab[dbase + (((uint32_t)h2 & ((1u << drb) - 1u)) << tsh)];
+        const uint32_t dl = rd & 15u;
+        const uint32_t ed = tok_ent(Q.ents, rd >> 4, true);
+        const uint32_t dx = e_extra(ed);
+        dv = e_val(ed) + ((uint32_t)(h2 >> dl) & ((1u << dx) - 1u));
+        dbits = dl + dx;
+        m1 = is_len && dl != 0u && e_op(ed) == OP_BASE && (int)(sh1 + dbits) <= bits;
+      }
+      const bool emit = dist | m1;  // a match token this step
+#else
+      constexpr bool m1 = false;
+      constexpr uint32_t dv = 0, dbits = 0;
+      const bool emit = dist;
+#endif
+      const uint32_t has_run = (emit && run) ? 1u : 0u;
       // (bitwise: one exit test, no short-circuit branches)
       const bool bad = ((int)(len + x) > bits) | (eo == OP_BAD) | (is_lit & (nlit >= lcap)) |
-                       (dist & (ntok + 1u + has_run > tcap));
+                       (emit & (ntok + 1u + has_run > tcap));
       const bool eob = !dist & (eo == OP_EOB);
       if (bad | eob) {
         if (PAIR && split && role && ss != TS_FAIL &&
@@ -1400,23 +1426,24 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       }
       const uint32_t len2 = r2 & 15u, sym2 = r2 >> 4;
       const bool two = !PAIR && is_lit && len2 != 0u && sym2 < 256u && (int)(len + len2) <= bits && nlit + 2u <= lcap;
-      drop((int)(len + x + (two ? len2 : 0u)));
+      drop((int)(len + x + (two ? len2 : 0u) + (m1 ? dbits : 0u)));
       uint32_t* const lit32 = reinterpret_cast<uint32_t*>(litp);
       const uint32_t nadd = is_lit ? (two ? 2u : 1u) : 0u;
       const uint32_t sh = 8u * (nlit & 3u);
       const uint64_t acc = (uint64_t)litw | ((uint64_t)(is_lit ? v : 0u) << sh) | ((uint64_t)(two ? sym2 : 0u) << (sh + 8u));
       const bool word_done = (nlit & 3u) + nadd >= 4u;
       if (word_done) lit32[nlit >> 2] = (uint32_t)acc;  // the word just filled
-      if (dist) {
+      if (emit) {
         if (has_run) tokp[ntok] = run;
-        tokp[ntok + has_run] = 0x80000000u | ((mlen - 3u) << 16) | (v - 1u);
+        const uint32_t ml = dist ? mlen : v, md = dist ? v : dv;
+        tokp[ntok + has_run] = 0x80000000u | ((ml - 3u) << 16) | (md - 1u);
       }
-      ntok += dist ? 1u + has_run : 0u;
+      ntok += emit ? 1u + has_run : 0u;
       litw = word_done ? (uint32_t)(acc >> 32) : (uint32_t)acc;
       nlit += nadd;
-      outlen += is_lit ? nadd : (dist ? mlen : 0u);
-      run = dist ? 0u : run + nadd;
-      mlen = is_len ? v : (dist ? 0u : mlen);
+      outlen += is_lit ? nadd : (dist ? mlen : (m1 ? v : 0u));
+      run = emit ? 0u : run + nadd;
+      mlen = (is_len && !m1) ? v : (dist ? 0u : mlen);
     }
     TPROF_ACC(3, t_sym);
     if (PAIR && blk1) {  // leaving the first block: the head's split ends, the tail's window closes
