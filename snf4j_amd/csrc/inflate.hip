@@ -759,6 +759,9 @@ constexpr uint32_t Q_TAB = Q_DT + QD_N * 64;
 // profiles/r05_ab/r05aj_ab_match1.txt); 0 restores two steps a match (A/B)
 #define WSG_TOK_MATCH1 1
 #endif
+#ifndef WSG_TOK_EAGER
+#define WSG_TOK_EAGER 0  // (A/B) refill the lane's bit buffer to 57-64 bits every step
+#endif
 #ifndef WSG_TOK_MIRROR
 #define WSG_TOK_MIRROR 1
 #endif
@@ -1100,7 +1103,14 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       rw = ring_word(ip);
     }
     const uint32_t rem = total - ip;
+#if WSG_TOK_EAGER
+    // as many whole bytes of the ring word as the 64-bit buffer has room for, so a step
+    // holds 57-64 bits and the one-step match and second literal fire more often
+    const uint32_t room = (uint32_t)(64 - bits) >> 3;
+    const uint32_t nb = min(min(room, 4u), rem);
+#else
     const uint32_t nb = bits < 32 ? (rem < 4u ? rem : 4u) : 0u;
+#endif
     hold |= (uint64_t)(rw & (nb == 4u ? 0xffffffffu : ((1u << (8u * nb)) - 1u))) << bits;
     bits += 8 * (int)nb;
     ip += nb;
