@@ -19,5 +19,5 @@ for round in 1 2 3; do
       python -c "import json;d=json.load(open('gpurun_out/abst.json'));print('$line $lib', d['value'], d.get('ms_per_batch'))"
     done
   done
-done | tee gpurun_out/r05ak_ab_match1.txt
+done | tee gpurun_out/r05ak_ab_eager.txt
 echo R05AJ_DONE
