@@ -97,6 +97,23 @@ def parse():
     return args
 
 
+def child_line(line: str, extra_steps: int = 3, timeout: int = 300) -> dict:
+    """One secondary line measured by `python bench.py --only <line>` in a child process
+    (started, not exec'd: this process has the GPU) — its JSON line, marked as such."""
+    cmd = [sys.executable, os.path.abspath(__file__), "--only", line, "--no-cpu-baseline",
+           "--extra-steps", str(extra_steps)]
+    try:
+        p = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=timeout)
+    except subprocess.TimeoutExpired:
+        return {"error": f"timed out after {timeout} s", "cmd": " ".join(cmd[1:])}
+    rows = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    if p.returncode != 0 or not rows:
+        return {"error": f"exit {p.returncode}: {p.stderr.strip()[-300:]}", "cmd": " ".join(cmd[1:])}
+    out = json.loads(rows[-1])
+    out["process"] = f"own process: python bench.py --only {line}"
+    return out
+
+
 def _free_port() -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
@@ -342,19 +359,25 @@ def main():
         del wire, payload, desc, res, state, off, sf
         torch.cuda.empty_cache()
         # the pinned buffers of the lines above (≈ 13 GB, held by torch's pinned-memory
-        # cache) go back before the host-to-host batcher lines; those lines take two
-        # untimed passes, as with --only (one was not enough: the encode batcher measured
-        # 29.2 GiB/s after one in a fresh process, 40.3 after two; scripts/e2e_probe_w.py)
+        # cache) go back before the host-to-host batcher lines
         gc.collect()
         if hasattr(torch._C, "_host_emptyCache"):
             torch._C._host_emptyCache()
-        if e2e is not None:  # the drop-in with permessage-deflate: batcher -> inflate -> validator, host to host
-            e2e["native_batcher_stages"] = e2e_stages_line(ctx, dev, 3, 2)
-            # the same sessions streaming 4x longer: the pipeline's fill and drain (a pass of
-            # 5 flushes spends 2-3 of them filling and draining) amortised over ~20 flushes
-            e2e["native_batcher_stages_steady"] = e2e_stages_line(ctx, dev, 2, 2, msgs=64)
-            e2e["native_encode_batcher"] = e2e_encode_line(ctx, dev, 3, 2)
-            e2e["native_batcher_aggregate"] = e2e_aggregate_line(ctx, dev, 3, 2)
+        if e2e is not None:
+            # Each host-to-host batcher line in a process of its own (`python bench.py
+            # --only <line>`, started as a child; this one waits): a batcher's streams share
+            # the process's hardware queues with every stream created before them, and in
+            # this process, after the lines above, that alone moved the encode batcher
+            # 27-40 GiB/s and the stage line 17-22 — a server process
+            # runs its loops' batchers, not a benchmark's other lines.  Two untimed passes
+            # each (one was not enough: scripts/e2e_probe_w.py).
+            torch.cuda.synchronize()
+            for key, line in (("native_batcher_stages", "e2e_stages"),  # batcher -> inflate -> validator
+                              # the same sessions streaming 4x longer: the burst line's pipeline
+                              # fill and drain amortised over ~20 flushes
+                              ("native_batcher_stages_steady", "e2e_stages_steady"),
+                              ("native_encode_batcher", "e2e_encode"), ("native_batcher_aggregate", "e2e_aggregate")):
+                e2e[key] = child_line(line)
         extras = [config0_line()] + measure_extras(ctx, dev, args)
 
     # the CPU baseline runs after every timed region, on rank 0 only (at N > 1 the
