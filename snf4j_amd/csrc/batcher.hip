@@ -49,9 +49,9 @@
 #include <cstdio>
 static double g_sp[20];
 static const char* g_sp_name[20] = {"compute", "inflate.input", "inflate.kernels+sync", "inflate.results",
-                                    "validate", "aggregate", "fin.list", "gather.launch", "finish.sync", "wait.total",
-                                    "precompute", "gather.pay_ensure", "gather.upload", "inflate.x", "inflate.launch",
-                                    "validate.sync", "upload.memcpy", "upload.h2d", "begin", "fin.build"};
+                                    "launch.validator", "aggregate", "fin.list", "gather.launch", "finish.sync", "wait.total",
+                                    "precompute", "gather.pay_ensure", "gather.upload", "inflate.x", "launch.replay",
+                                    "launch.downloads", "upload.memcpy", "upload.h2d", "begin", "fin.build"};
 struct SpT {
   int i;
   std::chrono::steady_clock::time_point t = std::chrono::steady_clock::now();
@@ -703,6 +703,8 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
   B_TRY(b, b->d_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, b->d_rf.ensure((S + 1) * sizeof(uint32_t)));
   int rc;
+  {
+  SP(14);
   if (j.tc >= 0) {  // the replay of the pre-decode that ran on tctx[tc]
     if (!same) B_TRY(b, upload(b->d_tmap, j.tmap, st));
     B_TRY(b, hipStreamWaitEvent(st, j.tok_done, 0));
@@ -718,11 +720,13 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
                                   (wsg_frame_desc*)b->d_odesc.p, (wsg_session_result*)b->d_ores.p,
                                   (uint32_t*)b->d_rf.p);
   }
+  }
   if (rc) return bset(b, rc, wsg_last_error(b->sctx));
   // FrameUtf8Validator right behind it on the device (PerMessageDeflateExtension.java:
   // 316-326): its input made from inflate's output by k_stage_vprep, no host hop
   j.validate = b->stages.validate != 0;
   if (j.validate) {
+    SP(4);
     B_TRY(b, upload(b->d_nheld, j.nheld, st));
     B_TRY(b, b->d_vdesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
     B_TRY(b, b->d_vres.ensure((S + 1) * sizeof(wsg_session_result)));
@@ -737,6 +741,7 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
                                    (wsg_session_result*)b->d_vres.p);
     if (rc) return bset(b, rc, wsg_last_error(b->sctx));
   }
+  SP(15);
   B_TRY(b, b->h_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
   B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
