@@ -360,6 +360,29 @@ __global__ __launch_bounds__(256) void k_stage_copy(const uint8_t* __restrict__ 
   }
 }
 
+// Small device results to pinned host memory by a kernel writing the mapped buffers: a
+// runtime D2H of these sizes (16-210 KB) held the calling thread until its stream
+// reached it — ≈ 0.5 ms a stage flush of the host's time, the replay and validator's
+// duration (profiles/r05_ab/r05an_stageprof.txt, launch.downloads).  Segment
+// blockIdx.y, 16-B stores where both ends allow, bytes for the tail.
+struct PushSeg {
+  const uint8_t* src;
+  uint8_t* dst;
+  uint64_t bytes;
+};
+struct PushSegs {
+  PushSeg s[4];
+  int n;
+};
+__global__ __launch_bounds__(256) void k_push(PushSegs a) {
+  const PushSeg g = a.s[blockIdx.y];
+  const uint64_t n16 = g.bytes / 16, stride = (uint64_t)gridDim.x * 256;
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n16; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load((const ws_u32x4*)g.src + i), (ws_u32x4*)g.dst + i);
+  if (blockIdx.x == 0)
+    for (uint64_t i = 16 * n16 + threadIdx.x; i < g.bytes; i += 256) g.dst[i] = g.src[i];
+}
+
 // Fresh stage decoders for the sessions in sids[0..n): one workgroup per session zeroes
 // its inflater state and window, validator context and aggregator state.
 __global__ __launch_bounds__(256) void k_stage_reset(const uint32_t* __restrict__ sids, wsg_inflate_state* istate,
@@ -745,13 +768,34 @@ static int infl_launch(wsg_batcher* b, FlushSlot& f) {
   B_TRY(b, b->h_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
   B_TRY(b, b->h_ores.ensure((S + 1) * sizeof(wsg_session_result)));
   B_TRY(b, b->h_rf.ensure((S + 1) * sizeof(uint32_t)));
+  if (j.validate) B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+#ifdef WSG_AB_RUNTIME_D2H
   if (F) B_TRY(b, hipMemcpyAsync(b->h_odesc.p, b->d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, st));
   B_TRY(b, hipMemcpyAsync(b->h_ores.p, b->d_ores.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
   B_TRY(b, hipMemcpyAsync(b->h_rf.p, b->d_rf.p, S * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-  if (j.validate) {
-    B_TRY(b, b->h_vres.ensure((S + 1) * sizeof(wsg_session_result)));
+  if (j.validate)
     B_TRY(b, hipMemcpyAsync(b->h_vres.p, b->d_vres.p, S * sizeof(wsg_session_result), hipMemcpyDeviceToHost, st));
+#else
+  {  // the results pushed into pinned memory by one kernel (see k_push)
+    PushSegs ps{};
+    int n = 0;
+    auto seg = [&](PinnedBuf& h, const DBuf& d, uint64_t bytes) -> hipError_t {
+      void* hp = nullptr;
+      const hipError_t e = hipHostGetDevicePointer(&hp, h.p, 0);
+      if (e == hipSuccess && bytes) ps.s[n++] = PushSeg{d.p, (uint8_t*)hp, bytes};
+      return e;
+    };
+    B_TRY(b, seg(b->h_odesc, b->d_odesc, F * sizeof(wsg_frame_desc)));
+    B_TRY(b, seg(b->h_ores, b->d_ores, S * sizeof(wsg_session_result)));
+    B_TRY(b, seg(b->h_rf, b->d_rf, S * sizeof(uint32_t)));
+    if (j.validate) B_TRY(b, seg(b->h_vres, b->d_vres, S * sizeof(wsg_session_result)));
+    ps.n = n;
+    if (n) {
+      hipLaunchKernelGGL(k_push, dim3(16, (uint32_t)n), dim3(256), 0, st, ps);
+      B_TRY(b, hipGetLastError());
+    }
   }
+#endif
   if (!j.launched) B_TRY(b, hipEventCreateWithFlags(&j.launched, hipEventDisableTiming));
   B_TRY(b, hipEventRecord(j.launched, st));
   return WSG_API_OK;
