@@ -759,6 +759,9 @@ constexpr uint32_t Q_TAB = Q_DT + QD_N * 64;
 // profiles/r05_ab/r05aj_ab_match1.txt); 0 restores two steps a match (A/B)
 #define WSG_TOK_MATCH1 1
 #endif
+#ifndef WSG_TOK_MATCH1_SUB
+#define WSG_TOK_MATCH1_SUB 0  // (A/B) the one-step match also through the distance sub-tables
+#endif
 #ifndef WSG_TOK_EAGER
 // the lane's bit buffer refilled to 57-64 bits every step (not only below 32): more
 // one-step matches and literal pairs, k_infl_tok 2.168 -> 2.133 ms (same box, 3 rounds,
@@ -1393,7 +1396,11 @@ __device__ __forceinline__ int tok_single_lds(const InflArgs& a, TokLds& Q, cons
       if (!PAIR) {
         const uint32_t sh1 = len + x;
         const uint64_t h2 = hold >> sh1;
-        const uint32_t rd = tab[dbase + (((uint32_t)h2 & ((1u << drb) - 1u)) << tsh)];
+        uint32_t rd = tab[dbase + (((uint32_t)h2 & ((1u << drb) - 1u)) << tsh)];
+#if WSG_TOK_MATCH1_SUB
+        if ((rd & 15u) == 0)  // a longer distance code: its sub-table, as the main lookup does
+          rd = tab[dbase + (((1u << drb) + (rd >> 8) + ((uint32_t)(h2 >> drb) & ((1u << ((rd >> 4) & 15u)) - 1u))) << tsh)];
+#endif
         const uint32_t dl = rd & 15u;
         const uint32_t ed = tok_ent(Q.ents, rd >> 4, true);
         const uint32_t dx = e_extra(ed);
