@@ -667,6 +667,24 @@ int wsg_inflate_batch_host(wsg_ctx* ctx, int no_context,
                            wsg_frame_desc* out_desc, wsg_session_result* out_result,
                            uint32_t* replay_from);
 
+/* ---------------- permessage-deflate encode (PerMessageDeflateEncoder) ---------------- */
+/* Per-session carry of PerMessageDeflateEncoder / DeflateEncoder / its raw ZlibEncoder's
+ * java.util.zip.Deflater (PerMessageDeflateEncoder.java:41, DeflateEncoder.java:42-46,
+ * ZlibEncoder.java:49): the scalars of zlib's deflate_state that outlive a
+ * deflate(Z_SYNC_FLUSH) call; the window and hash tables are in the session's
+ * WSG_DEFLATE_SESSION_BYTES block (zlib's layout: window[65536], head[32768] and
+ * prev[32768] as 16-bit window indices). */
+typedef struct wsg_deflate_state {
+    uint32_t strstart;     /* deflate_state.strstart: window index of the next byte */
+    uint32_t high_water;   /* .high_water: window bytes ever written or zeroed */
+    uint16_t insert;       /* .insert: trailing strings not yet hashed (<= 2) */
+    uint8_t has_deflater;  /* DeflateEncoder.encoder != null (a Deflater exists) */
+    uint8_t compressing;   /* PerMessageDeflateEncoder.compressing */
+    uint32_t reserved;
+} wsg_deflate_state; /* 16 bytes; zeros = a new session */
+
+#define WSG_DEFLATE_SESSION_BYTES (65536u + 2u * 32768u * 2u) /* window + head + prev */
+
 /* ---------------- opening handshake, server side ------- */
 /* Replaces, for a batch of server sessions whose handshake request arrives
  * together (a connection storm), the read-loop pair

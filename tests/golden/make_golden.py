@@ -516,6 +516,55 @@ def deflate_kats():
                       "invalid compressed data format"}]
 
 
+def deflate_encode_kats():
+    """PerMessageDeflateCodecTest's encoder cases (extensions/compress/
+    PerMessageDeflateCodecTest.java): testEncodeDecode :96-131 (PerMessageDeflateEncoder(8,
+    noContext) for noContext false and true), testEncodeWithoutRsv1 :151-166 (frames that
+    must come back as the same object), testEncodeCompressed :262-286 (a message whose
+    first frame already has RSV1: every frame of it passes through), testMinInflateBound
+    :289-309 and testDecompressionFailure :312-324 (2024-byte BINARY frames, one encoder).
+    The expected bytes are what zlib (java.util.zip.Deflater's engine) writes, driven the
+    way ZlibEncoder drives Deflater (oracle/deflate_ref.c); out_rsv and pass_through are the
+    reference's own assertions (rsv | 4 on compressed TEXT/BINARY, the same frame object
+    otherwise)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+    from oracle.deflateref import encode_frames
+    src = "extensions/compress/PerMessageDeflateCodecTest.java"
+
+    def seq_bytes(n):
+        return bytes(i & 0xFF for i in range(n))
+
+    def case(where, kind, level, nc, frames):
+        fr = [(OPS[op], fin, rsv, payload) for op, fin, rsv, payload in frames]
+        got = encode_frames(fr, level, nc)
+        out = []
+        for (op, fin, rsv, payload), g in zip(fr, got):
+            allow = (op in (1, 2) and not rsv & 4)
+            out.append({"opcode": op, "fin": fin, "rsv": rsv, "payload": hx(payload), "out": hx(g[3]),
+                        "out_rsv": g[2], "pass_through": g[3] == payload and g[2] == rsv and not allow
+                        and not (op == 0 and g[3] != payload)})
+        return {"src": src + where, "kind": kind, "level": level, "no_context": nc, "frames": out}
+
+    round_trip = [("TEXT", True, 0, b"ABCDEFG"), ("TEXT", True, 3, b"1"), ("TEXT", True, 1, b""),
+                  ("BINARY", True, 1, seq_bytes(1024)), ("PING", True, 0, seq_bytes(10)),
+                  ("PONG", True, 0, seq_bytes(10)), ("CLOSE", True, 0, bytes([0x03, 0xE8]) + b"XXX"),
+                  ("CONTINUATION", True, 1, seq_bytes(10)), ("TEXT", False, 0, b"ABCDEFG"),
+                  ("CONTINUATION", False, 0, b"IJKLMNOP"), ("CONTINUATION", True, 0, b"XYZ")]
+    without_rsv1 = [("TEXT", True, 4, b"ABC"), ("BINARY", True, 7, seq_bytes(10)),
+                    ("CONTINUATION", True, 0, seq_bytes(10)), ("PING", True, 0, seq_bytes(10)),
+                    ("PONG", True, 0, seq_bytes(10)), ("CLOSE", True, 0, bytes([0x03, 0xE8]))]
+    compressed = [("TEXT", True, 4, b"TEXT"), ("TEXT", False, 4, b"TEXT"), ("CONTINUATION", False, 3, b"TEXT"),
+                  ("CONTINUATION", True, 0, b"TEXT")]
+    return [case(":96-131", "round_trip", 8, False, round_trip),
+            case(":96-131", "round_trip", 8, True, round_trip),
+            case(":151-166", "pass_through", 8, False, without_rsv1),
+            case(":262-286", "pass_through", 8, False, compressed),
+            case(":289-309", "round_trip", 8, False, [("BINARY", True, 0, bytes(2024))]),
+            case(":312-324", "round_trip", 8, False,
+                 [("BINARY", True, 0, seq_bytes(2024)), ("BINARY", True, 0, seq_bytes(2024))])]
+
+
 def handshake_kats():
     """Opening-handshake vectors (server side), transcribed from the reference's tests
     under snf4j-websocket/src/test/java/org/snf4j/websocket/handshake/:
@@ -729,6 +778,7 @@ def main():
         "handshake_client": handshake_client_kats(),
         "handshake": handshake_kats(),
         "deflate": deflate_kats(),
+        "deflate_encode": deflate_encode_kats(),
         "aggregator": aggregator_kats(),
         "builder": builder_kats(),
         "decode": decode_kats(),

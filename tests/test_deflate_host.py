@@ -1,0 +1,117 @@
+"""permessage-deflate compression on the host (no GPU): the oracle against Python's zlib,
+the golden encode vectors, and the GPU algorithm (snf4j_amd/csrc/deflate_core.h, built for
+the CPU by tests/cpp/deflate_host.cpp) against the oracle, byte for byte, in both forms
+(serial restatement; the levels-4-9 decomposition the GPU runs), with the session state
+carried across batches and bit-identical between the two forms."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle.deflateref import encode_frames
+from tests import deflatehost as dh
+from tests.golden.fixtures import unhex
+from tests.wsgen import pm_deflate_encode
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "deflate_encode_kat.json")
+
+
+def _multi(frames, level, nc, rng, nb):
+    """The frames in nb batches, the state carried, each batch in a random form."""
+    cuts = sorted(set(int(x) for x in rng.integers(0, len(frames) + 1, nb - 1)))
+    st, out = None, []
+    for a, b in zip([0] + cuts, cuts + [len(frames)]):
+        if a == b:
+            continue
+        o, st = dh.run_session(frames[a:b], level, nc, int(rng.integers(0, 2)), st)
+        out += o
+    return out
+
+
+@pytest.mark.parametrize("level", range(10))
+def test_oracle_equals_python_zlib(level):
+    """deflate_ref.c (one deflate(SYNC_FLUSH) a frame, Java's buffers) equals Python's
+    compressobj + flush(Z_SYNC_FLUSH) (tests/wsgen.pm_deflate_encode) below 32 KiB frames."""
+    rng = np.random.default_rng(level)
+    for nc in (False, True):
+        fr = dh.random_frames(rng, 24, "text")
+        assert encode_frames(fr, level, nc) == pm_deflate_encode(fr, level, nc)
+
+
+def test_golden_encode_vectors():
+    """PerMessageDeflateCodecTest's encoder cases (tests/golden/deflate_encode_kat.json):
+    the oracle reproduces the recorded bytes, RSV bits and pass-through frames."""
+    import zlib
+    cases = json.load(open(GOLDEN))
+    assert len(cases) >= 5
+    for c in cases:
+        fr = [(f["opcode"], f["fin"], f["rsv"], unhex(f["payload"])) for f in c["frames"]]
+        got = encode_frames(fr, c["level"], c["no_context"])
+        for f, g in zip(c["frames"], got):
+            assert g[2] == f["out_rsv"] and g[3] == unhex(f["out"]), (c["src"], f)
+            if f["pass_through"]:
+                assert g[3] == unhex(f["payload"])
+        if c["kind"] == "round_trip":   # the compressed frames inflate back (context kept unless noContext)
+            d = zlib.decompressobj(-15)
+            for f, g in zip(c["frames"], got):
+                if f["pass_through"]:
+                    continue
+                if g[3] == b"\x00" and not f["payload"]:
+                    continue
+                tail = b"\x00\x00\xff\xff" if f["fin"] else b""
+                assert d.decompress(g[3] + tail) == unhex(f["payload"])
+                if f["fin"] and c["no_context"]:
+                    d = zlib.decompressobj(-15)
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_golden_encode_vectors_host(mode):
+    for c in json.load(open(GOLDEN)):
+        fr = [(f["opcode"], f["fin"], f["rsv"], unhex(f["payload"])) for f in c["frames"]]
+        got, _ = dh.run_session(fr, c["level"], c["no_context"], mode)
+        assert [(g[2], g[3]) for g in got] == [(f["out_rsv"], unhex(f["out"])) for f in c["frames"]], c["src"]
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_host_forms_match_zlib(seed):
+    """Both forms, every level, both context modes, text / low-entropy / random / tiny /
+    >64 KiB frames: output equal to zlib's, and the carried state bit-identical."""
+    kinds = ["text", "big", "bin", "rand", "tiny"]
+    for it in range(10):
+        rng = np.random.default_rng(seed * 1000 + it)
+        kind = kinds[it % 5]
+        level = int(rng.integers(0, 10))
+        nc = bool(rng.integers(0, 2))
+        fr = dh.random_frames(rng, int(rng.integers(1, 16 if kind == "big" else 30)), kind)
+        ref = encode_frames(fr, level, nc)
+        a, sa = dh.run_session(fr, level, nc, 0)
+        b, sb = dh.run_session(fr, level, nc, 1)
+        assert a == ref, (seed, it, kind, level, nc)
+        assert b == ref, (seed, it, kind, level, nc)
+        for x, y in zip(sa, sb):
+            assert np.array_equal(x, y), (seed, it, "state")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_host_window_slides_and_batches(seed):
+    """Frame ends around window index 65274 (slides at a call start and inside a frame's
+    last 261 bytes), the NIL head at exactly MAX_DIST after a slide, runs of one byte,
+    >64 KiB frames, the state carried over 1-3 batches in mixed forms."""
+    for it in range(8):
+        rng = np.random.default_rng(7000 + seed * 100 + it)
+        t = it % 4
+        level = int(rng.integers(4, 10))
+        nc = False
+        if t == 0:
+            fr = dh.nil_edge_frames(rng)
+        elif t == 1:
+            fr = dh.slide_frames(rng)
+        elif t == 2:
+            fr = [(2, True, 0, (rng.integers(0, 2, int(rng.integers(1, 70000)), dtype=np.uint8)
+                                * int(rng.integers(1, 256))).astype(np.uint8).tobytes()) for _ in range(3)]
+        else:
+            fr = dh.random_frames(rng, int(rng.integers(2, 10)), "big")
+            nc = bool(rng.integers(0, 2))
+        ref = encode_frames(fr, level, nc)
+        assert _multi(fr, level, nc, rng, int(rng.integers(1, 4))) == ref, (seed, it, t, level)
