@@ -98,6 +98,31 @@ def mixed_plan(seed: int, n_sessions: int, target_wire_bytes: int, min_len: int 
     return t, off, sf, int(off[-1]), info
 
 
+def deflate_plain(seed: int, n_sessions: int, msgs_per_session: int, msg_bytes: int, unique: int = 64):
+    """The plain TEXT messages deflate_batch compresses: word-salad ASCII (a 3,000-word
+    random vocabulary plus JSON-ish tokens and numbers, ~3x compressible by zlib level 6).
+    `unique` distinct sessions are generated and tiled over n_sessions (shared objects).
+    Returns [session][message] -> bytes."""
+    rng = np.random.default_rng(seed)
+    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
+    vocab = [bytes(letters[rng.integers(0, 26, int(rng.integers(2, 10)))]) for _ in range(3000)]
+    vocab += [b'{"id":', b'"name":', b'"value":', b'},', b'"ts":', b'true', b'false', b'null']
+    u = min(unique, n_sessions)
+    out = []
+    for _ in range(u):
+        msgs = []
+        for _ in range(msgs_per_session):
+            words, n = [], 0
+            while n < msg_bytes:
+                w = vocab[int(rng.integers(0, len(vocab)))] if rng.random() < 0.9 else str(
+                    int(rng.integers(0, 100000))).encode()
+                words.append(w)
+                n += len(w) + 1
+            msgs.append(b" ".join(words)[:msg_bytes])
+        out.append(msgs)
+    return [out[s % u] for s in range(n_sessions)]
+
+
 def deflate_batch(seed: int, n_sessions: int, msgs_per_session: int, msg_bytes: int, level: int = 6,
                   unique: int = 64):
     """A decoded batch of permessage-deflate TEXT messages (one FIN frame each, RSV1) as
@@ -109,23 +134,13 @@ def deflate_batch(seed: int, n_sessions: int, msgs_per_session: int, msg_bytes: 
     Returns (desc[n], session_first[n_s+1], payload, plain_bytes_per_batch)."""
     import zlib
     from snf4j_amd._lib import DESC_DTYPE
-    rng = np.random.default_rng(seed)
-    letters = np.frombuffer(b"abcdefghijklmnopqrstuvwxyz", np.uint8)
-    vocab = [bytes(letters[rng.integers(0, 26, int(rng.integers(2, 10)))]) for _ in range(3000)]
-    vocab += [b'{"id":', b'"name":', b'"value":', b'},', b'"ts":', b'true', b'false', b'null']
     u = min(unique, n_sessions)
+    bodies = deflate_plain(seed, u, msgs_per_session, msg_bytes, unique=u)
     streams, plain = [], []
-    for _ in range(u):
+    for s in range(u):
         comp = zlib.compressobj(level, zlib.DEFLATED, -15)
         msgs, tot = [], 0
-        for _ in range(msgs_per_session):
-            words, n = [], 0
-            while n < msg_bytes:
-                w = vocab[int(rng.integers(0, len(vocab)))] if rng.random() < 0.9 else str(
-                    int(rng.integers(0, 100000))).encode()
-                words.append(w)
-                n += len(w) + 1
-            body = b" ".join(words)[:msg_bytes]
+        for body in bodies[s]:
             tot += len(body)
             msgs.append((comp.compress(body) + comp.flush(zlib.Z_SYNC_FLUSH))[:-4])
         streams.append(msgs)

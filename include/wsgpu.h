@@ -177,6 +177,8 @@ int wsg_close(wsg_ctx* ctx);
  *   WSG_TUNE_FUSED_SCAN      0: always launch k_scan (k_link does not fold block aggregates)
  *   WSG_TUNE_AGG_UNITS       aggregator gather units per wave: 1, 2 (default) or 4
  *   WSG_TUNE_AGG_GRID        aggregator gather waves at most (default 65536)
+ *   WSG_TUNE_DEFLATE_SERIAL  1: permessage-deflate compression runs zlib's loop one lane a session at
+ *                            every level (the parallel form for levels 4-9 is the default; tests)
  *   WSG_TUNE_AGG_FOLD_MAX    aggregator plans of up to this many 512-frame blocks fold the block
  *                            sums in k_agg_b / k_agg_c (default: as many as LDS allows, 3,072);
  *                            larger ones run k_agg_scan (0 forces it: the tests' way to reach it) */
@@ -191,7 +193,8 @@ enum {
     WSG_TUNE_AGG_GRID = 8,
     WSG_TUNE_INFLATE_TABS = 9,
     WSG_TUNE_INFLATE_SPLIT = 10,
-    WSG_TUNE_AGG_FOLD_MAX = 11
+    WSG_TUNE_AGG_FOLD_MAX = 11,
+    WSG_TUNE_DEFLATE_SERIAL = 12
 };
 int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */
@@ -684,6 +687,44 @@ typedef struct wsg_deflate_state {
 } wsg_deflate_state; /* 16 bytes; zeros = a new session */
 
 #define WSG_DEFLATE_SESSION_BYTES (65536u + 2u * 32768u * 2u) /* window + head + prev */
+#define WSG_DESC_DEFLATED 0x02 /* output desc.flags: payload in `out` (else the input payload) */
+
+/* Device-resident PerMessageDeflateEncoder over a batch of outgoing frames: its encode()
+ * once per frame per session in order (PerMessageDeflateEncoder.java:81-99 over
+ * DeflateEncoder.java:62-104 and ZlibEncoder.encode, ZlibEncoder.java:223-287).  A
+ * TEXT/BINARY frame without RSV1, and the continuations of such a message, are compressed:
+ * one zlib deflate(Z_SYNC_FLUSH) of the payload on the session's raw deflater (windowBits
+ * -15, memLevel 8, `level`), byte-identical to java.util.zip.Deflater's; the 00 00 FF FF
+ * tail is removed from a final fragment, an empty payload becomes one 00 byte, RSV1 is set
+ * on TEXT/BINARY.  Other frames pass through.  no_context: PerMessageDeflateEncoder(level,
+ * true) — the deflater is dropped after every final fragment.
+ *   desc[n_frames], payload      the frames to send (payload_off / payload_len / opcode /
+ *                                flags: bit 7 FIN, bits 4-6 RSV)
+ *   session_first[0..n_sessions] session s owns frames [session_first[s], session_first[s+1])
+ *   state[n_sessions], session_mem[n_sessions * WSG_DEFLATE_SESSION_BYTES]   carry in / out
+ *   out[out_cap]                 compressed payloads (a 16-B aligned slot per frame, up to
+ *                                ZlibEncoder.deflateBound(len) bytes)
+ *   out_desc[n_frames]           per frame: the payload to send — in `out` (WSG_DESC_DEFLATED)
+ *                                or the input payload — and its opcode, FIN and RSV bits
+ *   *out_total (host)            bytes of `out` the batch's slots span
+ * Synchronises once (the slot sizes are planned on the device and read back).  Returns
+ * WSG_API_ERANGE when out_cap is too small (nothing compressed, the state unchanged). */
+int wsg_deflate_batch_device(wsg_ctx* ctx, int level, int no_context,
+                             const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions,
+                             const uint8_t* payload, uint64_t payload_len,
+                             wsg_deflate_state* state, uint8_t* session_mem,
+                             uint8_t* out, uint64_t out_cap, wsg_frame_desc* out_desc,
+                             uint64_t* out_total);
+/* Same contract with host pointers: H2D, compress, D2H of the used out bytes, descriptors,
+ * state and session_mem; synchronises. */
+int wsg_deflate_batch_host(wsg_ctx* ctx, int level, int no_context,
+                           const wsg_frame_desc* desc, uint64_t n_frames,
+                           const uint32_t* session_first, uint32_t n_sessions,
+                           const uint8_t* payload, uint64_t payload_len,
+                           wsg_deflate_state* state, uint8_t* session_mem,
+                           uint8_t* out, uint64_t out_cap, wsg_frame_desc* out_desc,
+                           uint64_t* out_total);
 
 /* ---------------- opening handshake, server side ------- */
 /* Replaces, for a batch of server sessions whose handshake request arrives

@@ -92,6 +92,8 @@ try:
                                 ("length", "<u4")])
     INFLATE_STATE_DTYPE = np.dtype([("compressing", "u1"), ("has_decoder", "u1"), ("finished", "u1"),
                                     ("reserved", "u1"), ("window_len", "<u2"), ("window_phase", "<u2")])
+    DEFLATE_STATE_DTYPE = np.dtype([("strstart", "<u4"), ("high_water", "<u4"), ("insert", "<u2"),
+                                    ("has_deflater", "u1"), ("compressing", "u1"), ("reserved", "<u4")])
     HS_RESULT_DTYPE = np.dtype([("frame_len", "<u4"), ("http_status", "<u2"), ("kind", "u1"), ("cause", "u1"),
                                 ("resp_len", "<u2"), ("detail_len", "<u2"), ("detail_off", "<u4")])
     assert HS_RESULT_DTYPE.itemsize == 16
@@ -180,6 +182,8 @@ def _load():
         "wsg_host_trim": ([], i32),
         "wsg_inflate_batch_device": ([p, i32, p, u64, p, u32, p, u64, p, p, p, p, p, p, p], i32),
         "wsg_inflate_batch_host": ([p, i32, p, u64, p, u32, p, u64, p, p, p, p, p, p, p], i32),
+        "wsg_deflate_batch_device": ([p, i32, i32, p, u64, p, u32, p, u64, p, p, p, u64, p, P(u64)], i32),
+        "wsg_deflate_batch_host": ([p, i32, i32, p, u64, p, u32, p, u64, p, p, p, u64, p, P(u64)], i32),
         "wsg_validate_batch_device": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_validate_batch_host": ([p, p, u64, p, u32, p, u64, p, p], i32),
         "wsg_aggregate_batch_device": ([p, i64, p, u64, p, u32, p, p, u64, p, p, u64, p, p, p], i32),

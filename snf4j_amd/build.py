@@ -11,8 +11,8 @@ from concurrent.futures import ThreadPoolExecutor
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 OUT = os.path.join(HERE, "libwsgpu.so")
-SOURCES = ["decode.hip", "encode.hip", "aggregate.hip", "api.hip", "batcher.hip", "inflate.hip", "handshake.hip"]
-HEADERS = ["ws_rules.h", "wsgpu_internal.h", "wsgpu_scan.h", "../../include/wsgpu.h"]
+SOURCES = ["decode.hip", "encode.hip", "aggregate.hip", "api.hip", "batcher.hip", "inflate.hip", "handshake.hip", "deflate.hip"]
+HEADERS = ["ws_rules.h", "wsgpu_internal.h", "wsgpu_scan.h", "deflate_core.h", "deflate_pmd.h", "../../include/wsgpu.h"]
 BENCH_DIR = os.path.join(os.path.dirname(HERE), "benchsupport")
 BENCH_SRC = os.path.join(BENCH_DIR, "csrc", "synth.hip")
 BENCH_OUT = os.path.join(BENCH_DIR, "libwsbench.so")

@@ -823,6 +823,85 @@ class BatchInflater:
         return results
 
 
+class BatchDeflater:
+    """PerMessageDeflateEncoder(compressionLevel, noContext) (PerMessageDeflateEncoder.java:
+    39-100) for every session of a batch flow, run on the GPU over each batch of outgoing
+    frames (wsg_deflate_batch_host): zlib's raw deflate with a Z_SYNC_FLUSH per frame,
+    byte-identical to java.util.zip.Deflater's.  The per-session deflater state (zlib's
+    strstart / high_water / insert and its window, head and prev arrays) stays in `state` /
+    `session_mem` between batches (context takeover)."""
+
+    def __init__(self, n_sessions: int, compressionLevel: int = 6, noContext: bool = False,
+                 ctx: Context | None = None):
+        from ._lib import DEFLATE_STATE_DTYPE
+        from .context import DEFLATE_SESSION_BYTES
+        if compressionLevel < 0 or compressionLevel > 9:
+            raise ValueError("compression level is out of range")   # ZlibEncoder.java:102-104
+        self.level = int(compressionLevel)
+        self.no_context = bool(noContext)
+        self.ctx = ctx
+        self.n = n_sessions
+        self.state = np.zeros(n_sessions, dtype=DEFLATE_STATE_DTYPE)
+        self.session_mem = np.zeros(n_sessions * DEFLATE_SESSION_BYTES, dtype=np.uint8)
+
+    def run(self, frames, with_flags: bool = False):
+        """frames[s] = [(opcode, fin, rsv, payload)] of session s, in order.  Returns the
+        encoded frames of every session, [(opcode, fin, rsv, payload)] (with_flags: a fifth
+        element, True when the payload was produced by the deflater)."""
+        ctx = self.ctx or default_context()
+        rows, chunks, sf, pos = [], [], [0], 0
+        for s in range(self.n):
+            for op, fin, rsv, p in frames[s]:
+                r = np.zeros((), dtype=DESC_DTYPE)
+                r["payload_off"] = pos
+                r["payload_len"] = len(p)
+                r["opcode"] = int(op)
+                r["flags"] = (0x80 if fin else 0) | ((int(rsv) & 7) << 4)
+                rows.append(r)
+                chunks.append(bytes(p))
+                pos += len(p)
+            sf.append(len(rows))
+        desc = np.array(rows, dtype=DESC_DTYPE) if rows else np.zeros(0, DESC_DTYPE)
+        payload = np.frombuffer(b"".join(chunks) + bytes(16), dtype=np.uint8)
+        out, odesc = ctx.deflate_host(self.level, self.no_context, desc, np.array(sf, np.uint32), payload,
+                                      self.state, self.session_mem)
+        res = []
+        for s in range(self.n):
+            fs = []
+            for k in range(sf[s], sf[s + 1]):
+                d = odesc[k]
+                o, ln = int(d["payload_off"]), int(d["payload_len"])
+                deflated = bool(int(d["flags"]) & 0x02)
+                data = out[o:o + ln].tobytes() if deflated else chunks[k]
+                t = (int(d["opcode"]), bool(int(d["flags"]) & 0x80), (int(d["flags"]) >> 4) & 7, data)
+                fs.append(t + (deflated,) if with_flags else t)
+            res.append(fs)
+        return res
+
+
+class PerMessageDeflateEncoder:
+    """GPU-backed PerMessageDeflateEncoder(compressionLevel, noContext): IEncoder<Frame,Frame>
+    (PerMessageDeflateEncoder.java:39-100).  encode() of one frame runs a one-frame batch;
+    BatchDeflater compresses whole batches of every session's outgoing frames."""
+
+    def __init__(self, compressionLevel: int, noContext: bool, ctx: Context | None = None):
+        self._b = BatchDeflater(1, compressionLevel, noContext, ctx)
+
+    def getInboundType(self):
+        return Frame
+
+    def getOutboundType(self):
+        return Frame
+
+    def encode(self, session, frame: Frame, out: list):
+        src = (int(frame.getOpcode()), frame.isFinalFragment(), frame.getRsvBits(), bytes(frame.getPayload()))
+        op, fin, rsv, data, deflated = self._b.run([[src]], with_flags=True)[0][0]
+        if not deflated:
+            out.append(frame)   # allowEncoding false: the same frame object (DeflateEncoder.java:103)
+        else:
+            out.append(make_frame(op, fin, rsv, data))
+
+
 class PerMessageDeflateDecoder:
     """GPU-backed PerMessageDeflateDecoder(noContext): IDecoder<Frame,Frame>
     (PerMessageDeflateDecoder.java:33-107).  decode() of one frame runs a one-frame

@@ -12,6 +12,8 @@ import numpy as np
 from . import _lib
 from ._lib import AGG_STATE_DTYPE, DESC_DTYPE, ENCODE_DTYPE, RESULT_DTYPE, STATE_DTYPE, DecoderCfg, check, lib
 
+DEFLATE_SESSION_BYTES = 65536 + 2 * 32768 * 2   # WSG_DEFLATE_SESSION_BYTES: window + head + prev
+
 MESSAGES = {
     1: "Unexpected opcode value ({d})",
     2: "Unexpected non-zero RSV bits ({d})",
@@ -71,7 +73,7 @@ class Context:
 
     TUNING = {"inflate_tokens": 1, "inflate_fast": 2, "inflate_lds": 3, "inflate_order": 4, "inflate_lanes": 5,
               "fused_scan": 6, "agg_units": 7, "agg_grid": 8, "inflate_tabs": 9, "inflate_split": 10,
-              "agg_fold_max": 11}
+              "agg_fold_max": 11, "deflate_serial": 12}
 
     def set_tuning(self, name: str, value: int):
         """A measurement / test switch of this context (wsg_set_tuning; wsgpu.h lists them)."""
@@ -257,6 +259,47 @@ class Context:
                                          out.ctypes.data, out_off.ctypes.data, odesc.ctypes.data, res.ctypes.data,
                                          rf.ctypes.data), self._h)
         return out, odesc[:n], res[:n_s], rf[:n_s]
+
+    # -------------------------------------------------------------- deflate (permessage-deflate encode)
+    def deflate_device(self, level: int, no_context: bool, desc, session_first, payload, state, session_mem, out,
+                       out_desc, n_frames: int | None = None) -> int:
+        """PerMessageDeflateEncoder over a device batch of outgoing frames (wsg_deflate_batch_device);
+        all arguments cuda tensors (desc / state as uint8 byte views, session_mem uint8 of
+        n_sessions x SESSION_BYTES).  Synchronises once; returns the out bytes used."""
+        n = desc.numel() // DESC_DTYPE.itemsize if n_frames is None else int(n_frames)
+        n_s = session_first.numel() - 1
+        assert session_mem.numel() >= n_s * DEFLATE_SESSION_BYTES and state.numel() >= n_s * 16
+        tot = C.c_uint64(0)
+        check(lib.wsg_deflate_batch_device(self._h, int(level), int(bool(no_context)), _p(desc), n, _p(session_first),
+                                           n_s, _p(payload), payload.numel(), _p(state), _p(session_mem), _p(out),
+                                           out.numel(), _p(out_desc), C.byref(tot)), self._h)
+        return int(tot.value)
+
+    def deflate_host(self, level: int, no_context: bool, desc: np.ndarray, session_first: np.ndarray,
+                     payload: np.ndarray, state: np.ndarray, session_mem: np.ndarray):
+        """PerMessageDeflateEncoder over a host batch (wsg_deflate_batch_host).  `state`
+        (DEFLATE_STATE_DTYPE) and `session_mem` (uint8, n_sessions x SESSION_BYTES) are updated
+        in place.  Returns (out, out_desc)."""
+        from ._lib import DEFLATE_STATE_DTYPE
+        desc = np.ascontiguousarray(desc, dtype=DESC_DTYPE)
+        session_first = np.ascontiguousarray(session_first, dtype=np.uint32)
+        payload = np.ascontiguousarray(payload, dtype=np.uint8)
+        assert state.dtype == DEFLATE_STATE_DTYPE and state.flags.c_contiguous
+        assert session_mem.dtype == np.uint8 and session_mem.flags.c_contiguous
+        n, n_s = len(desc), len(session_first) - 1
+        assert session_mem.size >= n_s * DEFLATE_SESSION_BYTES
+        lens = desc["payload_len"].astype(np.uint64)
+        cap = int((((lens + ((lens + 7) >> 3) + ((lens + 63) >> 6) + 15 + 15) >> 4) << 4).sum()) + 16 * n + 16
+        out = np.zeros(cap, dtype=np.uint8)
+        odesc = np.zeros(max(1, n), dtype=DESC_DTYPE)
+        d = desc if n else np.zeros(1, DESC_DTYPE)
+        pl = payload if payload.size else np.zeros(16, np.uint8)
+        tot = C.c_uint64(0)
+        check(lib.wsg_deflate_batch_host(self._h, int(level), int(bool(no_context)), d.ctypes.data, n,
+                                         session_first.ctypes.data, n_s, pl.ctypes.data, payload.size,
+                                         state.ctypes.data, session_mem.ctypes.data, out.ctypes.data, cap,
+                                         odesc.ctypes.data, C.byref(tot)), self._h)
+        return out[:int(tot.value)], odesc[:n]
 
     # -------------------------------------------------------------- handshake
     def handshake_accept_device(self, cfg, req, req_off, resp, result, n: int | None = None):

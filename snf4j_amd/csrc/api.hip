@@ -20,7 +20,8 @@ std::atomic<uint64_t> g_ctx_allocs{0};  // device workspace allocations of every
 
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_final",    "k_enc_len",  "k_enc_scan",
-                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate"};
+                                           "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate",
+                                           "k_defl_plan", "k_defl_prep", "k_defl_match", "k_defl_parse", "k_defl_final", "k_defl_serial"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -74,6 +75,9 @@ struct wsg_ctx {
   DevBuf i_tok, i_lit, i_stat, i_tab, i_tabcnt, i_fast, i_ord;  // inflate pre-decode workspace
   DevBuf i_split;  // [1] u64: messages the split-lane decode took (wsg_inflate_split_count)
   DevBuf i_tok2, i_lit2;  // the split's tail regions
+  // permessage-deflate compression workspace (deflate.hip, DeflArgs)
+  DevBuf d_flags, d_fout, d_fsym, d_ff, d_fs, d_sums, d_S, d_link, d_res, d_tres, d_strips, d_ftail, d_chunks, d_sym, d_tw, d_ssym;
+  int defl_serial = 0;               // WSG_TUNE_DEFLATE_SERIAL 1: zlib's loop per session at every level (tests)
   // measurement / test switches (wsg_set_tuning; the defaults are the product)
   int infl_tokens = 1;               // WSG_TUNE_INFLATE_TOKENS 0: no lane pre-decode (serial decoder only)
   uint32_t infl_lanes = 262144;      // WSG_TUNE_INFLATE_LANES: k_infl_tok lanes at most
@@ -153,7 +157,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST)) {
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL)) {
     f();
     return;
   }
@@ -187,6 +191,7 @@ void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src) {
   dst->agg_units = src->agg_units;
   dst->agg_grid = src->agg_grid;
   dst->agg_fold = src->agg_fold;
+  dst->defl_serial = src->defl_serial;
 }
 int ctx_device(wsg_ctx* c) { return c->device; }
 // the batcher's two-phase inflate applies (the pre-decode on, the split-lane decode off)
@@ -275,6 +280,7 @@ int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
       c->agg_units = (int)value;
       break;
     case WSG_TUNE_AGG_GRID: c->agg_grid = value < 1 ? 1u : (value > (1 << 24) ? (1u << 24) : (uint32_t)value); break;
+    case WSG_TUNE_DEFLATE_SERIAL: c->defl_serial = value != 0; break;
     case WSG_TUNE_AGG_FOLD_MAX: c->agg_fold = value < 0 ? 0u : (value > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)value); break;
     default: return set_err(c, WSG_API_EINVAL, "unknown tuning key");
   }
@@ -1121,6 +1127,136 @@ int inflate_replay_phase(wsg_ctx* c, wsg_ctx* tokc, const uint32_t* tmap, int no
 }  // namespace ws
 
 extern "C" {
+
+// ---------------------------------------------------------------- permessage-deflate encode
+int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                             uint64_t payload_len, wsg_deflate_state* state, uint8_t* session_mem, uint8_t* out,
+                             uint64_t out_cap, wsg_frame_desc* out_desc, uint64_t* out_total) {
+  if (!c || !out_total) return WSG_API_EINVAL;
+  if (level < 0 || level > 9) return set_err(c, WSG_API_EINVAL, "compression level is out of range");
+  *out_total = 0;
+  if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
+  if (n_frames >= (1ull << 31)) return set_err(c, WSG_API_ERANGE, "too many frames in one batch (max 2^31 - 1)");
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t S = n_sessions, F = n_frames ? n_frames : 1;
+  HIP_TRY(c, c->d_flags.ensure(F * sizeof(uint32_t)));
+  HIP_TRY(c, c->d_fout.ensure(F * sizeof(uint64_t)));
+  HIP_TRY(c, c->d_fsym.ensure(F * sizeof(uint64_t)));
+  HIP_TRY(c, c->d_ff.ensure(F * sizeof(DeflFrame)));
+  HIP_TRY(c, c->d_fs.ensure(S * sizeof(DeflSess)));
+  HIP_TRY(c, c->d_sums.ensure(4 * (S + 1) * sizeof(uint64_t)));
+  HIP_TRY(c, c->d_ftail.ensure(F));
+  DeflArgs a{};
+  a.level = level;
+  a.no_context = no_context ? 1 : 0;
+  a.serial = (level >= 1 && level <= 3) || (level >= 4 && c->defl_serial) ? 1 : 0;
+  a.desc = desc;
+  a.n_frames = n_frames;
+  a.session_first = session_first;
+  a.n_sessions = n_sessions;
+  a.payload = payload;
+  a.state = state;
+  a.smem = session_mem;
+  a.out = out;
+  a.out_cap = out_cap;
+  a.out_desc = out_desc;
+  a.fflags = (uint32_t*)c->d_flags.p;
+  a.fout = (uint64_t*)c->d_fout.p;
+  a.fsym = (uint64_t*)c->d_fsym.p;
+  a.ff = (DeflFrame*)c->d_ff.p;
+  a.fs = (DeflSess*)c->d_fs.p;
+  a.sums = (uint64_t*)c->d_sums.p;
+  a.ftail = (uint8_t*)c->d_ftail.p;
+  (void)payload_len;
+  timed(c, K_DEFL_PLAN, [&] { launch_defl_plan(a, c->stream); });
+  // the regions' totals decide the workspace: read them back
+  uint64_t tot[4];
+  for (int i = 0; i < 4; i++)
+    HIP_TRY(c, hipMemcpyAsync(&tot[i], a.sums + (uint64_t)i * (S + 1) + S, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                              c->stream));
+  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (tot[1] > out_cap)
+    return set_err(c, WSG_API_ERANGE, "out_cap %llu below the batch's %llu slot bytes", (unsigned long long)out_cap,
+                   (unsigned long long)tot[1]);
+  *out_total = tot[1];
+  const size_t twb = defl_treework_bytes();
+  if (a.serial) {
+    HIP_TRY(c, c->d_ssym.ensure(S * zd_lit_bufsize() * sizeof(uint32_t)));
+    HIP_TRY(c, c->d_tw.ensure(S * twb));
+    a.ssym = (uint32_t*)c->d_ssym.p;
+    a.tw = c->d_tw.p;
+    timed(c, K_DEFL_SERIAL, [&] { launch_defl_serial(a, c->stream); });
+    return WSG_API_OK;
+  }
+  a.n_lanes = (uint32_t)(F < 65536 ? F : 65536);
+  HIP_TRY(c, c->d_tw.ensure(a.n_lanes * twb));
+  a.tw = c->d_tw.p;
+  if (level >= 4) {
+    HIP_TRY(c, c->d_S.ensure(tot[0] + 64));
+    HIP_TRY(c, c->d_link.ensure((tot[0] + 64) * sizeof(uint16_t)));
+    HIP_TRY(c, c->d_res.ensure((tot[0] + 64) * 2 * sizeof(uint32_t)));
+    HIP_TRY(c, c->d_tres.ensure(F * DEFL_TAILN * 2 * sizeof(uint32_t)));
+    HIP_TRY(c, c->d_strips.ensure(F * 2 * zd_strip()));
+    HIP_TRY(c, c->d_chunks.ensure((tot[3] + 1) * sizeof(uint64_t)));
+    HIP_TRY(c, c->d_sym.ensure((tot[2] + 4) * sizeof(uint32_t)));
+    a.S = (uint8_t*)c->d_S.p;
+    a.link = (uint16_t*)c->d_link.p;
+    a.res = (uint32_t*)c->d_res.p;
+    a.tres = (uint32_t*)c->d_tres.p;
+    a.strips = (uint8_t*)c->d_strips.p;
+    a.chunks = (uint64_t*)c->d_chunks.p;
+    a.chunk_cap = tot[3];
+    a.sym = (uint32_t*)c->d_sym.p;
+    timed(c, K_DEFL_PREP, [&] { launch_defl_prep(a, c->stream); });
+    if (tot[3]) timed(c, K_DEFL_MATCH, [&] { launch_defl_match(a, c->stream); });
+  }
+  timed(c, K_DEFL_PARSE, [&] { launch_defl_parse(a, c->stream); });
+  timed(c, K_DEFL_FINAL, [&] { launch_defl_final(a, c->stream); });
+  return WSG_API_OK;
+}
+
+int wsg_deflate_batch_host(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                           const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                           uint64_t payload_len, wsg_deflate_state* state, uint8_t* session_mem, uint8_t* out,
+                           uint64_t out_cap, wsg_frame_desc* out_desc, uint64_t* out_total) {
+  if (!c || !out_total) return WSG_API_EINVAL;
+  HIP_TRY(c, hipSetDevice(c->device));
+  const uint64_t S = n_sessions, F = n_frames;
+  DevBuf d_desc, d_sf, d_pay, d_state, d_mem, d_out, d_odesc;
+  struct Guard {
+    DevBuf* b[7];
+    ~Guard() { for (DevBuf* x : b) x->release(); }
+  } g{{&d_desc, &d_sf, &d_pay, &d_state, &d_mem, &d_out, &d_odesc}};
+  HIP_TRY(c, d_desc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  HIP_TRY(c, d_sf.ensure((S + 1) * sizeof(uint32_t)));
+  HIP_TRY(c, d_pay.ensure(payload_len + 32));
+  HIP_TRY(c, d_state.ensure((S + 1) * sizeof(wsg_deflate_state)));
+  HIP_TRY(c, d_mem.ensure((S + 1) * (uint64_t)WSG_DEFLATE_SESSION_BYTES));
+  HIP_TRY(c, d_out.ensure(out_cap + 32));
+  HIP_TRY(c, d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+  hipStream_t s = c->stream;
+  if (F) HIP_TRY(c, hipMemcpyAsync(d_desc.p, desc, F * sizeof(wsg_frame_desc), hipMemcpyHostToDevice, s));
+  HIP_TRY(c, hipMemcpyAsync(d_sf.p, session_first, (S + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, s));
+  if (payload_len) HIP_TRY(c, hipMemcpyAsync(d_pay.p, payload, payload_len, hipMemcpyHostToDevice, s));
+  if (S) {
+    HIP_TRY(c, hipMemcpyAsync(d_state.p, state, S * sizeof(wsg_deflate_state), hipMemcpyHostToDevice, s));
+    HIP_TRY(c, hipMemcpyAsync(d_mem.p, session_mem, S * (uint64_t)WSG_DEFLATE_SESSION_BYTES, hipMemcpyHostToDevice, s));
+  }
+  int rc = wsg_deflate_batch_device(c, level, no_context, (const wsg_frame_desc*)d_desc.p, F, (const uint32_t*)d_sf.p,
+                                    n_sessions, (const uint8_t*)d_pay.p, payload_len, (wsg_deflate_state*)d_state.p,
+                                    (uint8_t*)d_mem.p, (uint8_t*)d_out.p, out_cap, (wsg_frame_desc*)d_odesc.p,
+                                    out_total);
+  if (rc) return rc;
+  if (*out_total) HIP_TRY(c, hipMemcpyAsync(out, d_out.p, *out_total, hipMemcpyDeviceToHost, s));
+  if (F) HIP_TRY(c, hipMemcpyAsync(out_desc, d_odesc.p, F * sizeof(wsg_frame_desc), hipMemcpyDeviceToHost, s));
+  if (S) {
+    HIP_TRY(c, hipMemcpyAsync(state, d_state.p, S * sizeof(wsg_deflate_state), hipMemcpyDeviceToHost, s));
+    HIP_TRY(c, hipMemcpyAsync(session_mem, d_mem.p, S * (uint64_t)WSG_DEFLATE_SESSION_BYTES, hipMemcpyDeviceToHost, s));
+  }
+  HIP_TRY(c, hipStreamSynchronize(s));
+  return WSG_API_OK;
+}
 
 int wsg_inflate_batch_device(wsg_ctx* c, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
                              const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,

@@ -1,0 +1,634 @@
+// deflate.hip — permessage-deflate compression on the GPU: PerMessageDeflateEncoder
+// (PerMessageDeflateEncoder.java:55-99) over DeflateEncoder (DeflateEncoder.java:62-104) over
+// ZlibEncoder's java.util.zip.Deflater (ZlibEncoder.java:223-287), i.e. zlib's raw deflate
+// with one deflate(Z_SYNC_FLUSH) per frame, byte-identical (deflate_core.h).
+//
+// Levels 4-9 (deflate_slow), per batch:
+//   k_defl_plan   thread per session: PerMessageDeflateEncoder's frame rules (pmd_step), the
+//                 window geometry of every deflate call (where zlib's fill_window slides), and
+//                 the sizes of the session's regions;  k_defl_scan: their bases.
+//   k_defl_prep   workgroup per session: the stream S (32 KiB of history + the frames' bytes),
+//                 hash links in position order (an LDS table of the last position of each of
+//                 the 32 K hashes), the window image zlib keeps — the bytes past every frame's
+//                 end before and after a slide there — and zlib's head/prev arrays for the
+//                 next batch; the match-chunk list.
+//   k_defl_match  one wave per 256 positions of a frame: longest_match at every position for
+//                 both chain budgets (match_at).
+//   k_defl_parse  lane per frame: deflate_slow's lazy evaluation over those results
+//                 (parse_call), Huffman trees and the bits of every block, the sync marker.
+//   k_defl_final  workgroup per session: a slide inside the last frame's tail, the state.
+// Levels 1-3 (deflate_fast, whose hash chains depend on its matches) run zlib's own loop
+// one lane a session (k_defl_serial); level 0 is stored blocks (k_defl_parse).
+#include <hip/hip_runtime.h>
+
+#include "deflate_core.h"
+#include "deflate_pmd.h"
+#include "wsgpu_internal.h"
+
+namespace ws {
+
+namespace {
+
+constexpr int32_t HNONE = INT32_MIN;
+
+__device__ inline uint32_t java_bound(uint32_t len) { return len + ((len + 7) >> 3) + ((len + 63) >> 6) + 15; }
+__device__ inline uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
+
+__device__ inline void wave_mem_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+struct Sums {
+  uint64_t *S, *O, *Y, *C;
+  __device__ Sums(const DeflArgs& a) {
+    const uint64_t n = (uint64_t)a.n_sessions + 1;
+    S = a.sums;
+    O = a.sums + n;
+    Y = a.sums + 2 * n;
+    C = a.sums + 3 * n;
+  }
+};
+
+// ------------------------------------------------------------------ k_defl_plan
+__global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  Sums sm(a);
+  if (s >= a.n_sessions) {
+    if (s == a.n_sessions) sm.S[s] = sm.O[s] = sm.Y[s] = sm.C[s] = 0;
+    return;
+  }
+  const wsg_deflate_state st = a.state[s];
+  uint8_t comp = st.compressing;
+  bool hasd = st.has_deflater != 0;
+  uint32_t sw = hasd ? st.strstart : 0;
+  const bool parallel = a.level >= 4 && !a.serial;
+  const uint32_t k0 = a.session_first[s], k1 = a.session_first[s + 1];
+  uint64_t orel = 0, yrel = 0, chunks = 0;
+  uint32_t srel = DEFL_HIST, last = ~0u;
+  bool any_call = false, first_fresh = false;
+  for (uint32_t k = k0; k < k1; k++) {
+    const wsg_frame_desc d = a.desc[k];
+    const int fin = d.flags >> 7, rsv = (d.flags >> 4) & 7;
+    const uint32_t len = d.payload_len;
+    uint8_t rsv_out, drop;
+    const int kind = pmd_step(&comp, d.opcode, fin, rsv, len, a.no_context, &rsv_out, &drop);
+    uint32_t fl = (uint32_t)kind | (drop ? DF_DROP : 0u) | ((uint32_t)rsv_out << DF_RSV_SHIFT) | (fin ? DF_FIN : 0u);
+    DeflFrame f{0, 0, len, s};
+    if (kind == PMD_CALL) {
+      if (!hasd) {
+        fl |= DF_SEG;
+        if (!any_call) first_fresh = true;
+        hasd = true;
+        sw = 0;
+      }
+      any_call = true;
+      if (sw >= (uint32_t)(zd::WSIZE + zd::MAX_DIST)) {   // fill_window's slide at the call's first loop top
+        if (sw == (uint32_t)(zd::WSIZE + zd::MAX_DIST)) fl |= DF_START_SLID;
+        sw -= zd::WSIZE;
+      }
+      f.start_w = sw;
+      uint32_t n = len < (uint32_t)zd::WINDOW_SIZE - sw ? len : (uint32_t)zd::WINDOW_SIZE - sw;
+      uint32_t loaded = sw + n, rem = len - n;
+      while (rem) {   // frames longer than the free window: slide + read again
+        loaded -= zd::WSIZE;
+        uint32_t m = rem < (uint32_t)zd::WINDOW_SIZE - loaded ? rem : (uint32_t)zd::WINDOW_SIZE - loaded;
+        loaded += m;
+        rem -= m;
+      }
+      if (loaded > (uint32_t)(zd::WSIZE + zd::MAX_DIST)) fl |= DF_TAIL_OK;
+      sw = loaded;
+      a.fout[k] = orel;
+      orel += r16(java_bound(len));
+      if (parallel) {
+        f.s_rel = srel;
+        a.fsym[k] = yrel;
+        yrel += ((len < (uint32_t)zd::SYM_END ? len : (uint32_t)zd::SYM_END) + 4) & ~3u;
+        chunks += (len > 2 ? (len - 2 + DEFL_CH - 1) / DEFL_CH : 0) + ((fl & DF_TAIL_OK) ? 1 : 0);
+        srel += len;
+      }
+      last = k;
+    } else if (kind == PMD_EMPTY) {
+      a.fout[k] = orel;
+      orel += 16;
+    } else {
+      a.fout[k] = 0;
+    }
+    if (drop) hasd = false;
+    a.fflags[k] = fl;
+    a.ff[k] = f;
+  }
+  const bool persist = hasd && last != ~0u;
+  if (persist) {   // the calls of the segment that outlives the batch
+    for (uint32_t k = last + 1; k-- > k0;) {
+      const uint32_t fl = a.fflags[k];
+      if ((fl & DF_KIND) != PMD_CALL) continue;
+      a.fflags[k] = fl | DF_PERSIST;
+      if (fl & DF_SEG) break;
+    }
+  }
+  sm.S[s] = parallel && any_call ? (uint64_t)srel + DEFL_PAD : 0;
+  sm.O[s] = orel;
+  sm.Y[s] = yrel;
+  sm.C[s] = chunks;
+  DeflSess fs;
+  fs.sw_final = sw;
+  fs.hw_final = st.high_water;
+  fs.last_call = last;
+  fs.has_deflater = hasd;
+  fs.compressing = comp;
+  fs.first_fresh = first_fresh;
+  fs.persist = persist;
+  a.fs[s] = fs;
+}
+
+// exclusive scan of the four per-session size arrays (one workgroup)
+__global__ __launch_bounds__(1024) void k_defl_scan(DeflArgs a) {
+  __shared__ uint64_t part[1024];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t n = a.n_sessions;
+  for (int arr = 0; arr < 4; arr++) {
+    uint64_t* v = a.sums + (uint64_t)arr * (n + 1);
+    uint64_t carry = 0;
+    for (uint64_t b = 0; b < n; b += 1024) {
+      const uint64_t i = b + tid;
+      const uint64_t x = i < n ? v[i] : 0;
+      part[tid] = x;
+      __syncthreads();
+      for (uint32_t o = 1; o < 1024; o <<= 1) {
+        const uint64_t y = tid >= o ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += y;
+        __syncthreads();
+      }
+      if (i < n) v[i] = carry + part[tid] - x;
+      carry += part[1023];
+      __syncthreads();
+    }
+    if (tid == 0) v[n] = carry;
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------------ k_defl_prep
+// link pass of one segment, wave 0: strings [p_begin, p_last] in position order.  Each
+// group of 64 consecutive strings reads the last position of its hash (hpos), then atomicMax
+// leaves the group's last occurrence there; a string whose hash repeats inside the group
+// takes its predecessor from the group (peeled by rank), all others the value read.
+__device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint16_t* prev, int32_t p_begin,
+                          int32_t p_last, int32_t nil_pos, bool persist, int32_t base_final) {
+  const int lane = threadIdx.x & 63;
+  for (int32_t g = p_begin; g <= p_last; g += 64) {
+    const int32_t p = g + lane;
+    const bool valid = p <= p_last;
+    const bool part = valid && p != nil_pos;   // window index 0 of a new deflater is NIL
+    uint32_t h = 0;
+    if (valid) h = zd::hash3(S[p], S[p + 1], S[p + 2]);
+    const int32_t old = part ? hpos[h] : HNONE;
+    if (part) atomicMax(&hpos[h], p);
+    int32_t M = part ? hpos[h] : 0;
+    int32_t pred = old;
+    const uint64_t dup = __ballot(part && M != p);
+    if (dup) {
+      const uint64_t pm = __ballot(part);
+      const uint32_t h0 = __shfl(h, __builtin_ctzll(pm));
+      if (__ballot(part && h == h0) == pm) {   // one hash for the whole group (a run)
+        const bool prev_part = lane > 0 && ((pm >> (lane - 1)) & 1);
+        pred = prev_part ? p - 1 : old;
+      } else {
+        const bool top0 = part && M == p;
+        bool act = part;
+        while (__ballot(act)) {
+          const bool is_top = act && M == p;
+          const bool rem = act && !is_top;
+          if (act) hpos[h] = old;
+          if (rem) atomicMax(&hpos[h], p);
+          const int32_t M2 = act ? hpos[h] : 0;
+          if (is_top) pred = M2;
+          act = rem;
+          M = M2;
+        }
+        if (top0) hpos[h] = p;
+      }
+    }
+    if (valid) {
+      link[p] = (uint16_t)((pred != HNONE && p - pred < zd::WSIZE) ? p - pred : 0);
+      if (persist) {
+        const int32_t v = pred != HNONE ? pred - base_final : 0;
+        prev[(uint32_t)(p - base_final) & zd::WMASK] = (uint16_t)(v > 0 ? v : 0);
+      }
+    }
+  }
+}
+
+// zlib's high_water zeroing after a read into the window (fill_window's tail)
+__device__ void zero_hw(uint8_t* W, uint32_t& hw, uint32_t curr) {
+  const int lane = threadIdx.x & 63;
+  if (hw >= (uint32_t)zd::WINDOW_SIZE) return;
+  uint32_t from, init;
+  if (hw < curr) {
+    init = (uint32_t)zd::WINDOW_SIZE - curr < (uint32_t)zd::WIN_INIT ? (uint32_t)zd::WINDOW_SIZE - curr : (uint32_t)zd::WIN_INIT;
+    from = curr;
+    hw = curr + init;
+  } else if (hw < curr + zd::WIN_INIT) {
+    init = curr + zd::WIN_INIT - hw;
+    if (init > (uint32_t)zd::WINDOW_SIZE - hw) init = (uint32_t)zd::WINDOW_SIZE - hw;
+    from = hw;
+    hw += init;
+  } else {
+    return;
+  }
+  for (uint32_t i = lane; i < init; i += 64) W[from + i] = 0;
+  wave_mem_sync();
+}
+
+__device__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+  wave_mem_sync();
+}
+
+// window walk of one segment, wave 1: zlib's window image through the segment's calls
+// (slides, reads, zeroing) and each frame's strips (window bytes after its end, before and
+// after a slide there)
+__device__ uint32_t window_walk(const DeflArgs& a, uint8_t* W, const uint8_t* S, uint32_t c0, uint32_t c_end,
+                                uint32_t sw, uint32_t hw) {
+  const int lane = threadIdx.x & 63;
+  for (uint32_t k = c0; k < c_end; k++) {
+    if ((a.fflags[k] & DF_KIND) != PMD_CALL) continue;
+    const DeflFrame f = a.ff[k];
+    if (sw >= (uint32_t)(zd::WSIZE + zd::MAX_DIST)) {
+      wave_copy(W, W + zd::WSIZE, sw - zd::WSIZE);
+      sw -= zd::WSIZE;
+    }
+    const uint32_t L = f.len;
+    uint32_t n = L < (uint32_t)zd::WINDOW_SIZE - sw ? L : (uint32_t)zd::WINDOW_SIZE - sw;
+    wave_copy(W + sw, S + f.s_rel, n);
+    uint32_t loaded = sw + n, rem = L - n;
+    zero_hw(W, hw, loaded);
+    while (rem) {
+      wave_copy(W, W + zd::WSIZE, loaded - zd::WSIZE);
+      loaded -= zd::WSIZE;
+      uint32_t m = rem < (uint32_t)zd::WINDOW_SIZE - loaded ? rem : (uint32_t)zd::WINDOW_SIZE - loaded;
+      wave_copy(W + loaded, S + f.s_rel + (L - rem), m);
+      loaded += m;
+      rem -= m;
+      zero_hw(W, hw, loaded);
+    }
+    uint8_t* st0 = a.strips + (uint64_t)k * 2 * zd::STRIP;
+    for (uint32_t j = lane; j < (uint32_t)zd::STRIP; j += 64) {
+      st0[j] = loaded + j < (uint32_t)zd::WINDOW_SIZE ? W[loaded + j] : 0;
+      const uint32_t q = loaded - zd::WSIZE + j;
+      st0[zd::STRIP + j] = (loaded >= (uint32_t)zd::WSIZE && q < (uint32_t)zd::WINDOW_SIZE) ? W[q] : 0;
+    }
+    sw = loaded;
+  }
+  return hw;
+}
+
+__global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
+  __shared__ int32_t hpos[zd::WSIZE];   // 128 KiB: last position of each hash (S coordinates)
+  const uint32_t s = blockIdx.x, tid = threadIdx.x, wv = tid >> 6;
+  const DeflSess fs = a.fs[s];
+  if (fs.last_call == ~0u) return;
+  Sums sm(a);
+  const uint64_t soff = sm.S[s];
+  uint8_t* S = a.S + soff;
+  uint16_t* link = a.link + soff;
+  uint8_t* W = a.smem + (uint64_t)s * WSG_DEFLATE_SESSION_BYTES;
+  uint16_t* head = (uint16_t*)(W + zd::WINDOW_SIZE);
+  uint16_t* prev = head + zd::WSIZE;
+  const wsg_deflate_state st = a.state[s];
+  const uint32_t k0 = a.session_first[s], k1 = a.session_first[s + 1];
+  // the match-chunk list of the session's calls
+  if (tid == 0) {
+    uint64_t c = sm.C[s];
+    for (uint32_t k = k0; k < k1; k++) {
+      const uint32_t fl = a.fflags[k];
+      if ((fl & DF_KIND) != PMD_CALL) continue;
+      const uint32_t len = a.ff[k].len;
+      const uint32_t nch = len > 2 ? (len - 2 + DEFL_CH - 1) / DEFL_CH : 0;
+      for (uint32_t i = 0; i < nch; i++) a.chunks[c++] = (uint64_t)k | (uint64_t)i << 32;
+      if (fl & DF_TAIL_OK) a.chunks[c++] = (uint64_t)k | 1ull << 63;
+    }
+  }
+  uint32_t k = k0;
+  for (;;) {
+    while (k < k1 && (a.fflags[k] & DF_KIND) != PMD_CALL) k++;
+    if (k >= k1) break;
+    const uint32_t c0 = k;
+    uint32_t c_last = c0, c_end = c0 + 1;
+    for (uint32_t j = c0 + 1; j < k1; j++) {
+      const uint32_t fl = a.fflags[j];
+      if ((fl & DF_KIND) != PMD_CALL) continue;
+      if (fl & DF_SEG) break;
+      c_last = j;
+      c_end = j + 1;
+    }
+    const uint32_t fl0 = a.fflags[c0];
+    const bool fresh = (fl0 & DF_SEG) != 0, persist = (fl0 & DF_PERSIST) != 0;
+    const uint32_t strstart0 = fresh ? 0 : st.strstart, ins0 = fresh ? 0 : st.insert;
+    const uint32_t H = fresh ? 0 : (strstart0 < (uint32_t)zd::WSIZE ? strstart0 : (uint32_t)zd::WSIZE);
+    const DeflFrame f0 = a.ff[c0], fl_ = a.ff[c_last];
+    const int32_t seg_begin = fresh ? (int32_t)f0.s_rel : (int32_t)(DEFL_HIST - H);
+    const int32_t base0 = fresh ? (int32_t)f0.s_rel : (int32_t)DEFL_HIST - (int32_t)strstart0;
+    const int32_t seg_end = (int32_t)(fl_.s_rel + fl_.len);
+    const int32_t base_final = seg_end - (int32_t)fs.sw_final;
+    // 1. the stream: history, then the frames' bytes
+    if (!fresh)
+      for (uint32_t i = tid; i < H; i += blockDim.x) S[DEFL_HIST - H + i] = W[strstart0 - H + i];
+    for (uint32_t j = c0; j < c_end; j++) {
+      if ((a.fflags[j] & DF_KIND) != PMD_CALL) continue;
+      const DeflFrame f = a.ff[j];
+      const uint8_t* src = a.payload + a.desc[j].payload_off;
+      for (uint32_t i = tid; i < f.len; i += blockDim.x) S[f.s_rel + i] = src[i];
+    }
+    // 2. links of the hashed history strings (zlib's prev[]); the hash heads
+    if (!fresh)
+      for (uint32_t p = DEFL_HIST - H + tid; p < DEFL_HIST - ins0; p += blockDim.x) {
+        const uint32_t w = (uint32_t)((int32_t)p - base0);
+        const uint32_t pv = prev[w & zd::WMASK];
+        link[p] = (uint16_t)((pv != 0 && w - pv < (uint32_t)zd::WSIZE) ? w - pv : 0);
+      }
+    for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x)
+      hpos[h] = (fresh || head[h] == 0) ? HNONE : (int32_t)head[h] + base0;
+    __syncthreads();
+    // 3. the slides of this batch applied to the prev entries no string of it replaces
+    if (persist && !fresh && base_final != base0)
+      for (uint32_t j = tid; j < (uint32_t)zd::WSIZE; j += blockDim.x) {
+        const uint32_t v = prev[j];
+        const int32_t nv = v ? (int32_t)v + base0 - base_final : 0;
+        prev[j] = (uint16_t)(nv > 0 ? nv : 0);
+      }
+    __syncthreads();
+    // 4. links (wave 0) beside the window walk (wave 1)
+    if (wv == 0) {
+      const int32_t p_begin = fresh ? seg_begin : (int32_t)(DEFL_HIST - ins0);
+      // window index 0 is NIL: a deflater's first string, also when it is still pending (strstart <= 2)
+      link_pass(hpos, S, link, prev, p_begin, seg_end - 3, base0, persist, base_final);
+    } else if (wv == 1) {
+      const uint32_t hw = window_walk(a, W, S, c0, c_end, strstart0, fresh ? 0 : st.high_water);
+      if (persist && (tid & 63) == 0) a.fs[s].hw_final = hw;
+    }
+    __syncthreads();
+    // 5. zlib's head[] for the next batch
+    if (persist)
+      for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x) {
+        const int32_t v = hpos[h];
+        const int32_t nv = v != HNONE ? v - base_final : 0;
+        head[h] = (uint16_t)(nv > 0 ? nv : 0);
+      }
+    __syncthreads();
+    k = c_end;
+  }
+}
+
+// ------------------------------------------------------------------ k_defl_match
+struct StripBytes {
+  const uint8_t* S;
+  uint32_t end;
+  const uint8_t* strip;
+  __device__ uint32_t operator()(uint32_t p) const { return p < end ? S[p] : strip[p - end]; }
+};
+struct LinkAcc {
+  const uint16_t* l;
+  __device__ uint32_t operator()(uint32_t p) const { return l[p]; }
+};
+
+__global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
+  Sums sm(a);
+  const uint64_t total = sm.C[a.n_sessions];
+  const zd::Cfg cfg = zd::level_cfg(a.level);
+  const uint32_t lane = threadIdx.x;
+  for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
+    const uint64_t e = a.chunks[c];
+    const uint32_t k = (uint32_t)e, ci = (uint32_t)(e >> 32) & 0x7fffffffu;
+    const bool var = (e >> 63) != 0;
+    const DeflFrame f = a.ff[k];
+    const uint64_t soff = sm.S[f.sess];
+    const uint8_t* S = a.S + soff;
+    const uint16_t* link = a.link + soff;
+    uint32_t* res = a.res + 2 * soff;
+    const uint32_t start = f.s_rel, end = start + f.len;
+    const uint32_t tstart = end - start > DEFL_TAILN ? end - DEFL_TAILN : start;
+    const uint32_t p0 = var ? tstart : start + ci * DEFL_CH;
+    const uint32_t p1 = var ? end - 2 : (p0 + DEFL_CH < end - 2 ? p0 + DEFL_CH : end - 2);
+    StripBytes by{S, end, a.strips + ((uint64_t)k * 2 + (var ? 1 : 0)) * zd::STRIP};
+    for (uint32_t p = p0 + lane; p < p1; p += 64) {
+      uint32_t full, quarter;
+      zd::match_at(by, LinkAcc{link}, p, end, cfg, &full, &quarter);
+      if (var) {
+        uint32_t* t = a.tres + ((uint64_t)k * DEFL_TAILN + (p - tstart)) * 2;
+        t[0] = full;
+        t[1] = quarter;
+      } else {
+        res[2 * (uint64_t)p] = full;
+        res[2 * (uint64_t)p + 1] = quarter;
+      }
+    }
+  }
+}
+
+// ------------------------------------------------------------------ k_defl_parse
+struct ResAcc {
+  const uint32_t* res;   // session base, indexed by stream position
+  const uint32_t* tres;  // the frame's tail results
+  uint32_t tstart;
+  __device__ void operator()(uint32_t p, int variant, uint32_t* f, uint32_t* q) const {
+    if (variant && p >= tstart) {
+      const uint32_t* t = tres + 2 * (p - tstart);
+      *f = t[0];
+      *q = t[1];
+    } else {
+      const uint32_t* r = res + 2 * (uint64_t)p;
+      *f = r[0];
+      *q = r[1];
+    }
+  }
+};
+struct SBytes {
+  const uint8_t* S;
+  __device__ uint32_t operator()(uint32_t p) const { return S[p]; }
+  __device__ const uint8_t* ptr(uint32_t p) const { return S + p; }
+};
+
+__device__ void pass_or_empty(const DeflArgs& a, uint32_t k, uint32_t fl, uint64_t obase) {
+  const wsg_frame_desc d = a.desc[k];
+  wsg_frame_desc o;
+  o.opcode = d.opcode;
+  o.flags = (uint8_t)(((fl & DF_FIN) ? 0x80 : 0) | (((fl >> DF_RSV_SHIFT) & 7) << 4));
+  o.status = 0;
+  if ((fl & DF_KIND) == PMD_PASS) {
+    o.payload_off = d.payload_off;
+    o.payload_len = d.payload_len;
+  } else {
+    o.payload_off = obase + a.fout[k];
+    o.payload_len = 1;
+    o.flags |= WSG_DESC_DEFLATED;
+    a.out[o.payload_off] = 0;
+  }
+  a.out_desc[k] = o;
+}
+
+__global__ __launch_bounds__(64) void k_defl_parse(DeflArgs a) {
+  Sums sm(a);
+  const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
+  if (tid >= a.n_lanes) return;   // one TreeWork a lane
+  const uint32_t stride = a.n_lanes;
+  zd::TreeWork* tw = (zd::TreeWork*)a.tw + tid;
+  const zd::Cfg cfg = zd::level_cfg(a.level);
+  for (uint64_t k = tid; k < a.n_frames; k += stride) {
+    const uint32_t fl = a.fflags[k];
+    const DeflFrame f = a.ff[k];
+    const uint64_t obase = sm.O[f.sess];
+    if ((fl & DF_KIND) != PMD_CALL) {
+      pass_or_empty(a, (uint32_t)k, fl, obase);
+      continue;
+    }
+    const wsg_frame_desc d = a.desc[k];
+    zd::BitWriter bw{a.out + obase + a.fout[k], 0, 0, 0};
+    if (a.level == 0) {
+      zd::stored_call(&bw, a.payload + d.payload_off, f.len);
+    } else {
+      const uint64_t soff = sm.S[f.sess];
+      const uint32_t end = f.s_rel + f.len;
+      ResAcc ra{a.res + 2 * soff, a.tres + (uint64_t)k * DEFL_TAILN * 2,
+                end - f.s_rel > DEFL_TAILN ? end - DEFL_TAILN : f.s_rel};
+      zd::CallGeom g{f.start_w, (uint8_t)((fl & DF_START_SLID) ? 1 : 0)};
+      const bool tail = zd::parse_call(ra, SBytes{a.S + soff}, f.s_rel, f.len, g, cfg, tw,
+                                       a.sym + sm.Y[f.sess] + a.fsym[k], &bw);
+      a.ftail[k] = tail ? 1 : 0;
+    }
+    wsg_frame_desc o;
+    o.payload_off = obase + a.fout[k];
+    o.payload_len = (uint32_t)bw.pos - ((fl & DF_FIN) ? 4u : 0u);
+    o.opcode = d.opcode;
+    o.flags = (uint8_t)(((fl & DF_FIN) ? 0x80 : 0) | (((fl >> DF_RSV_SHIFT) & 7) << 4) | WSG_DESC_DEFLATED);
+    o.status = 0;
+    a.out_desc[k] = o;
+  }
+}
+
+// ------------------------------------------------------------------ k_defl_final
+__global__ __launch_bounds__(256) void k_defl_final(DeflArgs a) {
+  const uint32_t s = blockIdx.x, tid = threadIdx.x;
+  const DeflSess fs = a.fs[s];
+  wsg_deflate_state st = a.state[s];
+  st.compressing = fs.compressing;
+  if (!fs.has_deflater) {
+    st.strstart = st.high_water = 0;
+    st.insert = 0;
+    st.has_deflater = 0;
+  } else if (fs.last_call != ~0u && a.level > 0) {
+    uint32_t sw = fs.sw_final;
+    if (a.ftail[fs.last_call]) {   // the window slid inside the last frame's tail
+      uint8_t* W = a.smem + (uint64_t)s * WSG_DEFLATE_SESSION_BYTES;
+      uint16_t* hp = (uint16_t*)(W + zd::WINDOW_SIZE);
+      for (uint32_t i = tid; i < sw - zd::WSIZE; i += blockDim.x) W[i] = W[i + zd::WSIZE];
+      for (uint32_t j = tid; j < 2u * zd::WSIZE; j += blockDim.x) {
+        const uint32_t v = hp[j];
+        hp[j] = (uint16_t)(v >= (uint32_t)zd::WSIZE ? v - zd::WSIZE : 0);
+      }
+      sw -= zd::WSIZE;
+    }
+    st.strstart = sw;
+    st.high_water = fs.hw_final;
+    st.insert = (uint16_t)(sw < 2 ? sw : 2);
+    st.has_deflater = 1;
+  } else if (fs.last_call != ~0u) {   // level 0: stored blocks, the window is never read
+    st.has_deflater = 1;
+  }
+  if (tid == 0) a.state[s] = st;
+}
+
+// ------------------------------------------------------------------ k_defl_serial
+// zlib's loop, one lane a session (levels 1-3, or any level with WSG_TUNE_DEFLATE_SERIAL)
+__global__ __launch_bounds__(64) void k_defl_serial(DeflArgs a) {
+  const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= a.n_sessions) return;
+  Sums sm(a);
+  const DeflSess fs = a.fs[s];
+  wsg_deflate_state st = a.state[s];
+  uint8_t* W = a.smem + (uint64_t)s * WSG_DEFLATE_SESSION_BYTES;
+  zd::SerialState ss;
+  ss.window = W;
+  ss.head = (uint16_t*)(W + zd::WINDOW_SIZE);
+  ss.prev = ss.head + zd::WSIZE;
+  ss.strstart = st.strstart;
+  ss.insert = st.insert;
+  ss.high_water = st.high_water;
+  ss.ins_h = 0;
+  ss.match_start = ss.prev_match = 0;
+  ss.cfg = zd::level_cfg(a.level);
+  ss.sym = a.ssym + (uint64_t)s * zd::LIT_BUFSIZE;
+  ss.tw = (zd::TreeWork*)a.tw + s;
+  const uint64_t obase = sm.O[s];
+  for (uint32_t k = a.session_first[s]; k < a.session_first[s + 1]; k++) {
+    const uint32_t fl = a.fflags[k];
+    if ((fl & DF_KIND) != PMD_CALL) {
+      pass_or_empty(a, k, fl, obase);
+      continue;
+    }
+    const wsg_frame_desc d = a.desc[k];
+    ss.bw = zd::BitWriter{a.out + obase + a.fout[k], 0, 0, 0};
+    if (a.level == 0) {
+      zd::stored_call(&ss.bw, a.payload + d.payload_off, d.payload_len);
+    } else {
+      if (fl & DF_SEG) {   // a new Deflater: deflateInit2's CLEAR_HASH, strstart 0
+        for (uint32_t h = 0; h < (uint32_t)zd::WSIZE; h++) ss.head[h] = 0;
+        ss.strstart = 0;
+        ss.insert = 0;
+        ss.high_water = 0;
+      }
+      zd::serial_call(&ss, a.payload + d.payload_off, d.payload_len, a.level);
+    }
+    wsg_frame_desc o;
+    o.payload_off = obase + a.fout[k];
+    o.payload_len = (uint32_t)ss.bw.pos - ((fl & DF_FIN) ? 4u : 0u);
+    o.opcode = d.opcode;
+    o.flags = (uint8_t)(((fl & DF_FIN) ? 0x80 : 0) | (((fl >> DF_RSV_SHIFT) & 7) << 4) | WSG_DESC_DEFLATED);
+    o.status = 0;
+    a.out_desc[k] = o;
+  }
+  st.compressing = fs.compressing;
+  if (!fs.has_deflater) {
+    st.strstart = st.high_water = 0;
+    st.insert = 0;
+    st.has_deflater = 0;
+  } else {
+    st.has_deflater = 1;
+    if (a.level > 0) {
+      st.strstart = ss.strstart;
+      st.high_water = ss.high_water;
+      st.insert = (uint16_t)ss.insert;
+    }
+  }
+  a.state[s] = st;
+}
+
+}  // namespace
+
+size_t defl_treework_bytes() { return sizeof(zd::TreeWork); }
+
+void launch_defl_plan(const DeflArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_defl_plan, dim3((a.n_sessions + 1 + 63) / 64), dim3(64), 0, s, a);
+  hipLaunchKernelGGL(k_defl_scan, dim3(1), dim3(1024), 0, s, a);
+}
+void launch_defl_prep(const DeflArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_defl_prep, dim3(a.n_sessions), dim3(256), 0, s, a);
+}
+void launch_defl_match(const DeflArgs& a, hipStream_t s) {
+  uint64_t g = a.chunk_cap < 262144 ? a.chunk_cap : 262144;
+  hipLaunchKernelGGL(k_defl_match, dim3((uint32_t)(g ? g : 1)), dim3(64), 0, s, a);
+}
+void launch_defl_parse(const DeflArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_defl_parse, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_defl_final(const DeflArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_defl_final, dim3(a.n_sessions), dim3(256), 0, s, a);
+}
+void launch_defl_serial(const DeflArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_defl_serial, dim3((a.n_sessions + 63) / 64), dim3(64), 0, s, a);
+}
+
+}  // namespace ws

@@ -223,10 +223,73 @@ struct InflTokStat {
   uint32_t ok, n_tok, n_lit, out_len;
 };
 
+// permessage-deflate compression (deflate.hip).  Per frame: DF_* flags; per session the
+// planned sizes of its regions (S stream, output, symbols, match chunks), scanned into bases.
+constexpr uint32_t DF_KIND = 3u;          // PMD_PASS / PMD_CALL / PMD_EMPTY
+constexpr uint32_t DF_DROP = 1u << 2;     // the deflater is discarded after this frame (noContext, FIN)
+constexpr uint32_t DF_SEG = 1u << 3;      // a CALL that starts a new deflater (fresh window)
+constexpr uint32_t DF_RSV_SHIFT = 4;      // 3 bits: RSV after encoding
+constexpr uint32_t DF_FIN = 1u << 9;
+constexpr uint32_t DF_START_SLID = 1u << 10;  // geometry: the call-start slide put strstart at MAX_DIST
+constexpr uint32_t DF_TAIL_OK = 1u << 11;     // geometry: a slide can fall inside the frame's last bytes
+constexpr uint32_t DF_PERSIST = 1u << 12;     // the call's deflater outlives the batch
+constexpr uint32_t DEFL_CH = 256;         // positions a k_defl_match wave takes
+constexpr uint32_t DEFL_TAILN = 264;      // positions whose match reads pass the frame's end
+constexpr uint32_t DEFL_HIST = 32768;     // S-region bytes before the first call (the history)
+constexpr uint32_t DEFL_PAD = 288;        // S-region bytes after the last call
+
+struct DeflFrame {   // per CALL frame (k_defl_plan)
+  uint32_t s_rel;    // S-region offset of the frame's first byte (stream position)
+  uint32_t start_w;  // strstart after the call-start fill_window
+  uint32_t len;
+  uint32_t sess;
+};
+
+struct DeflSess {    // per session (k_defl_plan; k_defl_prep fills hw)
+  uint32_t sw_final;    // strstart after the batch's last call (before a slide in its tail)
+  uint32_t hw_final;    // high_water after it (k_defl_prep)
+  uint32_t last_call;   // frame index of the last call, ~0u none
+  uint8_t has_deflater, compressing, first_fresh, persist;
+};
+
+struct DeflArgs {
+  int32_t level, no_context, serial;
+  const wsg_frame_desc* desc;
+  uint64_t n_frames;
+  const uint32_t* session_first;
+  uint32_t n_sessions;
+  const uint8_t* payload;
+  wsg_deflate_state* state;
+  uint8_t* smem;            // n_sessions * WSG_DEFLATE_SESSION_BYTES: window | head | prev
+  uint8_t* out;
+  uint64_t out_cap;
+  wsg_frame_desc* out_desc;
+  // workspace
+  uint32_t* fflags;         // [n_frames] DF_*
+  uint64_t* fout;           // [n_frames] output offset within the session's output region
+  uint64_t* fsym;           // [n_frames] symbol-buffer offset within the session's region (words)
+  DeflFrame* ff;            // [n_frames]
+  DeflSess* fs;             // [n_sessions]
+  uint64_t* sums;           // [4][n_sessions + 1]: S bytes, output bytes, symbol words, chunks -> exclusive
+  uint8_t* S;               // stream regions
+  uint16_t* link;           // [S]: distance to the previous string of its hash (0: none / >= 32 KiB)
+  uint32_t* res;            // [2 x S]: match_at results at the calls' positions (full, quarter)
+  uint32_t* tres;           // [n_frames][DEFL_TAILN][2]: the same after a slide in the frame's tail
+  uint8_t* strips;          // [n_frames][2][zd::STRIP]: window bytes after the frame's end (before/after)
+  uint8_t* ftail;           // [n_frames]: the parse saw a slide in the frame's tail
+  uint64_t* chunks;         // [chunk bound]: frame | chunk << 32 | tail variant << 63
+  uint64_t chunk_cap;
+  uint32_t* sym;            // symbol buffers
+  void* tw;                 // zd::TreeWork per parse lane
+  uint32_t n_lanes;         // parse lanes (grid-stride over frames)
+  uint32_t* ssym;           // serial path: [n_sessions][zd::LIT_BUFSIZE]
+};
+
 // kernel ids for timing
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
-  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE, K_COUNT
+  K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE,
+  K_DEFL_PLAN, K_DEFL_PREP, K_DEFL_MATCH, K_DEFL_PARSE, K_DEFL_FINAL, K_DEFL_SERIAL, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -285,6 +348,16 @@ uint64_t infl_tok_words(uint64_t payload_len, uint64_t n_frames);
 uint64_t infl_lit_bytes(uint64_t payload_len, uint64_t n_frames);
 uint64_t infl_ord_words(uint64_t n_frames);  // order + bucket counts
 uint64_t infl_tab_bytes();
+
+void launch_defl_plan(const DeflArgs& a, hipStream_t s);    // k_defl_plan + k_defl_scan
+void launch_defl_prep(const DeflArgs& a, hipStream_t s);
+void launch_defl_match(const DeflArgs& a, hipStream_t s);
+void launch_defl_parse(const DeflArgs& a, hipStream_t s);
+void launch_defl_final(const DeflArgs& a, hipStream_t s);
+void launch_defl_serial(const DeflArgs& a, hipStream_t s);
+size_t defl_treework_bytes();
+constexpr uint64_t zd_lit_bufsize() { return 16384; }   // zd::LIT_BUFSIZE
+constexpr uint64_t zd_strip() { return 260; }         // zd::STRIP
 
 void launch_hs_accept(const wsg_hs_config& cfg, const uint8_t* req, const uint64_t* req_off, uint32_t n,
                       uint8_t* resp, wsg_hs_result* result, hipStream_t s);

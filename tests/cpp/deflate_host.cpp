@@ -136,7 +136,7 @@ void decomp_segment(Session& S, int level, std::vector<Call>& calls) {
         int64_t q = hpos[h];
         pred[p] = q;
         if (q >= 0 && (int64_t)p - q < WSIZE) link[p] = (uint16_t)(p - q);
-        if (!(strstart0 == 0 && p == 0)) hpos[h] = p;   // window index 0 is NIL
+        if ((int64_t)p != base0) hpos[h] = p;   // window index 0 is NIL (a deflater's first string)
     }
     // the window walk: strips after each frame's end, call geometry
     std::vector<uint8_t> W(S.win, S.win + WINDOW_SIZE);

@@ -115,3 +115,22 @@ def test_host_window_slides_and_batches(seed):
             nc = bool(rng.integers(0, 2))
         ref = encode_frames(fr, level, nc)
         assert _multi(fr, level, nc, rng, int(rng.integers(1, 4))) == ref, (seed, it, t, level)
+
+
+@pytest.mark.parametrize("level", range(4, 10))
+def test_host_pending_strings_across_batches(level):
+    """A deflater that has seen fewer than 3 bytes when a batch ends keeps its first strings
+    pending (zlib's insert): the first of them is window index 0, NIL once hashed, so it
+    never becomes a match candidate in the next batch."""
+    rng = np.random.default_rng(9000 + level)
+    for it in range(12):
+        first = [(1, False, 0, rng.integers(97, 100, int(rng.integers(1, 3)), dtype=np.uint8).tobytes())]
+        rest = dh.random_frames(rng, int(rng.integers(2, 9)), "tiny" if it % 2 else "bin")
+        rest = [(0, f[1], 0, f[3]) for f in rest]
+        fr = first + rest
+        ref = encode_frames(fr, level, False)
+        st, out = None, []
+        for part in (fr[:1], fr[1:]):
+            o, st = dh.run_session(part, level, False, 1, st)
+            out += o
+        assert out == ref, (level, it)

@@ -1,0 +1,171 @@
+"""permessage-deflate compression on the GPU (wsg_deflate_batch_*, deflate.hip) against zlib
+driven as java.util.zip.Deflater is (oracle/deflate_ref.c): every output byte, the RSV bits,
+the pass-through frames and the carried state, at levels 0-9, with and without context
+takeover, over many sessions a batch and several batches; the parallel form (levels 4-9)
+and zlib's loop per session (levels 1-3, and forced for 4-9) both."""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+from oracle.deflateref import encode_frames
+from tests import deflatehost as dh
+from tests.golden.fixtures import unhex
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "deflate_encode_kat.json")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    from snf4j_amd.context import Context
+    return Context(0, stream="own")
+
+
+def _deflater(ctx, n, level, nc, serial=False):
+    from snf4j_amd.codec import BatchDeflater
+    ctx.set_tuning("deflate_serial", 1 if serial else 0)
+    return BatchDeflater(n, level, nc, ctx)
+
+
+def _check_batches(ctx, sessions, level, nc, n_batches, rng, serial=False):
+    """sessions[s] = frame list; runs them over n_batches batches (random cut per session)
+    and compares every session with the oracle."""
+    n = len(sessions)
+    bd = _deflater(ctx, n, level, nc, serial)
+    cuts = []
+    for fr in sessions:
+        c = sorted(int(x) for x in rng.integers(0, len(fr) + 1, n_batches - 1))
+        cuts.append([0] + c + [len(fr)])
+    got = [[] for _ in range(n)]
+    for b in range(n_batches):
+        batch = [fr[cuts[s][b]:cuts[s][b + 1]] for s, fr in enumerate(sessions)]
+        for s, o in enumerate(bd.run(batch)):
+            got[s] += o
+    for s, fr in enumerate(sessions):
+        ref = encode_frames(fr, level, nc)
+        assert got[s] == ref, ("session", s, "level", level, "nc", nc, "serial", serial)
+    return bd
+
+
+def test_golden_encode_vectors(ctx):
+    """PerMessageDeflateCodecTest's encoder cases (tests/golden/deflate_encode_kat.json), one
+    session a case, all in one batch, both forms."""
+    cases = json.load(open(GOLDEN))
+    for serial in (False, True):
+        for c in cases:
+            fr = [(f["opcode"], f["fin"], f["rsv"], unhex(f["payload"])) for f in c["frames"]]
+            bd = _deflater(ctx, 1, c["level"], c["no_context"], serial)
+            got = bd.run([fr])[0]
+            assert [(g[2], g[3]) for g in got] == [(f["out_rsv"], unhex(f["out"])) for f in c["frames"]], c["src"]
+
+
+def test_encoder_mirror_pass_through_identity(ctx):
+    """PerMessageDeflateEncoder.encode hands frames it does not compress on as the same object
+    (PerMessageDeflateCodecTest.testEncodeWithoutRsv1 :151-166)."""
+    from snf4j_amd.codec import PerMessageDeflateEncoder
+    from snf4j_amd.frame import make_frame
+    e = PerMessageDeflateEncoder(8, False, ctx)
+    for f in [make_frame(1, True, 4, b"ABC"), make_frame(2, True, 7, bytes(range(10))),
+              make_frame(0, True, 0, bytes(range(10))), make_frame(9, True, 0, bytes(range(10)))]:
+        out = []
+        e.encode(None, f, out)
+        assert len(out) == 1 and out[0] is f
+    out = []
+    f = make_frame(1, True, 0, b"ABCDEFG")
+    e.encode(None, f, out)
+    assert out[0] is not f and out[0].getRsvBits() == 4
+    assert zlib.decompressobj(-15).decompress(out[0].getPayload() + b"\x00\x00\xff\xff") == b"ABCDEFG"
+
+
+@pytest.mark.parametrize("level", range(10))
+def test_random_sessions_all_levels(ctx, level):
+    rng = np.random.default_rng(100 + level)
+    kinds = ["text", "bin", "rand", "tiny", "text"]
+    for nc in (False, True):
+        sessions = [dh.random_frames(rng, int(rng.integers(1, 24)), kinds[s % 5]) for s in range(40)]
+        _check_batches(ctx, sessions, level, nc, 3, rng)
+
+
+@pytest.mark.parametrize("level", [4, 6, 9])
+def test_serial_form_forced(ctx, level):
+    """zlib's own loop per session (the form levels 1-3 take) at the parallel levels."""
+    rng = np.random.default_rng(200 + level)
+    sessions = [dh.random_frames(rng, int(rng.integers(1, 16)), "text") for _ in range(24)]
+    _check_batches(ctx, sessions, level, False, 2, rng, serial=True)
+
+
+@pytest.mark.parametrize("level", [4, 6, 8, 9])
+def test_window_slides_nil_edge_runs_big(ctx, level):
+    """Window slides at a call start and inside a frame's last bytes, the NIL head exactly
+    MAX_DIST back after a slide, one-byte runs, frames longer than the window."""
+    rng = np.random.default_rng(300 + level)
+    sessions = []
+    for s in range(16):
+        t = s % 4
+        if t == 0:
+            sessions.append(dh.nil_edge_frames(rng))
+        elif t == 1:
+            sessions.append(dh.slide_frames(rng))
+        elif t == 2:
+            sessions.append([(2, True, 0, (rng.integers(0, 2, int(rng.integers(1, 70000)), dtype=np.uint8)
+                                           * int(rng.integers(1, 256))).astype(np.uint8).tobytes())
+                             for _ in range(3)])
+        else:
+            sessions.append(dh.random_frames(rng, 6, "big"))
+    _check_batches(ctx, sessions, level, False, 2, rng)
+
+
+def test_parallel_state_equals_serial(ctx):
+    """After the same batches the parallel form leaves the state zlib's loop leaves: the
+    scalars, the window up to high_water, the hash heads."""
+    rng = np.random.default_rng(400)
+    sessions = [dh.random_frames(rng, 12, "text") + dh.slide_frames(rng) for _ in range(8)]
+    a = _check_batches(ctx, sessions, 6, False, 1, rng)
+    b = _check_batches(ctx, sessions, 6, False, 1, rng, serial=True)
+    assert np.array_equal(a.state, b.state)
+    ma = a.session_mem.reshape(len(sessions), -1)
+    mb = b.session_mem.reshape(len(sessions), -1)
+    for s in range(len(sessions)):
+        hw = int(a.state[s]["high_water"])
+        assert np.array_equal(ma[s, :hw], mb[s, :hw])
+        assert np.array_equal(ma[s, 65536:131072], mb[s, 65536:131072])   # head
+
+
+def test_round_trip_through_gpu_inflater(ctx):
+    """Frames compressed on the GPU inflate back on the GPU (BatchInflater, context kept)."""
+    from snf4j_amd._lib import DESC_DTYPE
+    from snf4j_amd.codec import BatchInflater
+    rng = np.random.default_rng(500)
+    sessions = [[(1, True, 0, dh.text(rng, int(rng.integers(1, 5000)))) for _ in range(10)] for _ in range(16)]
+    enc = _deflater(ctx, 16, 6, False).run(sessions)
+    inf = BatchInflater(16, False, ctx)
+    rows, chunks, sf, pos = [], [], [0], 0
+    for s in range(16):
+        for op, fin, rsv, p in enc[s]:
+            r = np.zeros((), DESC_DTYPE)
+            r["payload_off"], r["payload_len"], r["opcode"] = pos, len(p), op
+            r["flags"] = (0x80 if fin else 0) | (rsv << 4)
+            rows.append(r)
+            chunks.append(p)
+            pos += len(p)
+        sf.append(len(rows))
+    res = inf.run(np.array(rows, DESC_DTYPE), np.array(sf, np.uint32), np.frombuffer(b"".join(chunks), np.uint8))
+    for s in range(16):
+        frames, exc = res[s]
+        assert exc is None
+        assert [bytes(f.getPayload()) for f in frames] == [p for (_, _, _, p) in sessions[s]]
+
+
+def test_bench_shaped_batch(ctx):
+    """The bench's shape (word-salad TEXT messages of 4 KiB, level 6, context takeover) over
+    256 sessions x 16 messages in one batch."""
+    from benchsupport.synth import deflate_plain
+    msgs = deflate_plain(0xDEF1, 256, 16, 4096)
+    sessions = [[(1, True, 0, m) for m in msgs[s]] for s in range(256)]
+    got = _deflater(ctx, 256, 6, False).run(sessions)
+    for s in range(0, 256, 5):
+        assert got[s] == encode_frames(sessions[s], 6, False), s
