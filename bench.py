@@ -87,7 +87,8 @@ def parse():
     ap.add_argument("--handshake-only", action="store_true", help="only the server handshake line")
     ap.add_argument("--inflate-sessions", type=int, nargs="+", default=[8192])
     ap.add_argument("--only", default=None,
-                    help="print only one secondary line: configs1|configs2|configs3|encode|validator|inflate|handshake|hs_client")
+                    help="print only one secondary line: configs1|configs2|configs3|encode|validator|inflate|deflate|"
+                         "handshake|hs_client")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     for k in ("frames", "payload", "sessions"):
@@ -660,6 +661,117 @@ def inflate_line(ctx, dev, steps, warmup, n_s=8192, msgs=16, msg_bytes=4096, cpu
             "pipeline_ms": pipe}
 
 
+def deflate_line(ctx, dev, steps, warmup, n_s=8192, msgs=16, msg_bytes=4096, level=6, cpu_seconds=3.0):
+    """PerMessageDeflateEncoder (wsg_deflate_batch_device) over a device-resident batch of
+    TEXT messages, context takeover, level 6 (the compressing side):
+    every byte identical to zlib's (java.util.zip.Deflater's engine).  A step compresses
+    every session's messages from a new deflater.  The bound is the per-position match
+    search and the per-frame lazy parse (latency and issue), not HBM; the roofline figure
+    is reported against HBM for scale.  cpu_baseline: zlib level 6 driven as ZlibEncoder
+    drives Deflater (oracle/deflate_ref.c) on 1 host thread and on the job's threads."""
+    import threading
+    import numpy as np
+    import torch
+    from benchsupport.synth import deflate_plain
+    from oracle import deflateref
+    from snf4j_amd._lib import DESC_DTYPE
+    from snf4j_amd.context import DEFLATE_SESSION_BYTES
+    bodies = deflate_plain(0xDEF1, n_s, msgs, msg_bytes)
+    n = n_s * msgs
+    lens = np.array([len(m) for ms in bodies for m in ms], dtype=np.uint64)
+    desc_h = np.zeros(n, dtype=DESC_DTYPE)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)[:-1]
+    desc_h["payload_off"], desc_h["payload_len"], desc_h["opcode"], desc_h["flags"] = off, lens, 1, 0x80
+    plain = int(lens.sum())
+    pl_h = np.frombuffer(b"".join(m for ms in bodies for m in ms) + bytes(16), dtype=np.uint8)
+    sf_h = (np.arange(n_s + 1) * msgs).astype(np.uint32)
+    desc = torch.from_numpy(desc_h.view(np.uint8).copy()).to(dev)
+    sf = torch.from_numpy(sf_h.view(np.int32).copy()).to(dev)
+    payload = torch.from_numpy(pl_h.copy()).to(dev)
+    state = torch.zeros(n_s * 16, dtype=torch.uint8, device=dev)
+    smem = torch.empty(n_s * DEFLATE_SESSION_BYTES, dtype=torch.uint8, device=dev)
+    bound = int(((lens + ((lens + 7) >> 3) + ((lens + 63) >> 6) + 15 + 15) >> 4 << 4).sum())
+    out = torch.empty(bound + 16, dtype=torch.uint8, device=dev)
+    odesc = torch.empty(n * 16, dtype=torch.uint8, device=dev)
+
+    def step():
+        state.zero_()   # new deflaters: every step compresses the same streams from the start
+        ctx.deflate_device(level, False, desc, sf, payload, state, smem, out, odesc, n_frames=n)
+
+    step()
+    torch.cuda.synchronize(dev)
+    od = odesc.cpu().numpy().view(DESC_DTYPE)
+    comp = int(od["payload_len"].astype(np.int64).sum())
+    oh = None
+    for s in (0, n_s - 1):   # spot check against zlib driven as Deflater is
+        ref = deflateref.encode_frames([(1, True, 0, m) for m in bodies[s]], level, False)
+        if oh is None:
+            oh = out.cpu().numpy()
+        for i, k in enumerate(range(s * msgs, (s + 1) * msgs)):
+            o, ln = int(od[k]["payload_off"]), int(od[k]["payload_len"])
+            assert oh[o:o + ln].tobytes() == ref[i][3] and int(od[k]["flags"]) == 0x80 | 0x40 | 0x02, \
+                ("deflate mismatch", s, i)
+    del oh
+    kernels = ["k_defl_prep", "k_defl_match", "k_defl_parse"]
+    el, kms, pipe = _timed(ctx, step, steps, warmup, dev, kernels)
+    alg = plain + comp
+    ach = alg / (kms / 1e3) / 1e9
+    # CPU: zlib level 6 over whole session streams (16 x 4 KiB each), 1 thread then N threads
+    slens = np.array([len(m) for m in bodies[0]], dtype=np.uint32)
+
+    def sess_data(s):
+        return np.frombuffer(b"".join(bodies[s]), dtype=np.uint8)
+
+    data = [sess_data(s) for s in range(64)]
+    done, t = 0, 0.0
+    while t < cpu_seconds:
+        t0 = time.perf_counter()
+        deflateref.stream_bytes(level, slens, data[done % 64])
+        t += time.perf_counter() - t0
+        done += 1
+    cpu1 = done * int(slens.sum()) / t / 2**30
+    threads, how = cpu_threads()
+    counts = [0] * threads
+    stop = time.perf_counter() + cpu_seconds
+
+    def work(i):
+        j = i
+        while time.perf_counter() < stop:
+            deflateref.stream_bytes(level, slens, data[j % 64])
+            counts[i] += 1
+            j += threads
+
+    ts = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    t0 = time.perf_counter()
+    for th in ts:
+        th.start()
+    for th in ts:
+        th.join()
+    elt = time.perf_counter() - t0
+    cpun = sum(counts) * int(slens.sum()) / elt / 2**30
+    return {"config": f"permessage-deflate compress: {n_s} sessions x {msgs} TEXT messages x {msg_bytes} B, "
+                      f"context takeover, level {level} ({plain / 1e6:.0f} MB -> {comp / 1e6:.0f} MB, "
+                      f"byte-identical to zlib)",
+            "value": round(plain * steps / el / 2**30, 3), "unit": "GiB/s (uncompressed bytes)",
+            "ms_per_step": round(el / steps * 1e3, 4),
+            "roofline": {"kernel": "k_defl_prep + k_defl_match + k_defl_parse (the compress launches of a step)",
+                         "bound": "per-position hash-chain match search and per-frame lazy parse (latency, issue), "
+                                  "not hbm",
+                         "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
+                         "avg_launch_ms": round(kms, 4)},
+            "cpu_baseline": {"value": round(cpu1, 4), "unit": "GiB/s (uncompressed bytes)", "cores": 1,
+                             "kind": "zlib",
+                             "sample": f"{done} session streams ({msgs} x {msg_bytes} B) deflated at level {level} "
+                                       f"by zlib driven as ZlibEncoder drives java.util.zip.Deflater "
+                                       f"(oracle/deflate_ref.c) in {t:.1f} s, 1 thread"},
+            "cpu_baseline_threads": {"value": round(cpun, 4), "unit": "GiB/s (uncompressed bytes)",
+                                     "cores": threads, "kind": "zlib", "cores_from": how,
+                                     "sample": f"{sum(counts)} session streams on {threads} threads in {elt:.1f} s"},
+            "pipeline_ms": pipe}
+
+
 def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps, warmup, expect_errors=None,
                  aggregate=False):
     """Decode GiB/s (wire) + k_piecesN roofline of one device-resident batch."""
@@ -1156,6 +1268,7 @@ EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2":
                "e2e_stages_steady": lambda ctx, dev, K, W: e2e_stages_line(ctx, dev, K, W, msgs=64),
                "e2e_encode": e2e_encode_line, "e2e_aggregate": e2e_aggregate_line,
                "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
+               "deflate": lambda ctx, dev, K, W: deflate_line(ctx, dev, K, W),
                "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W),
                "hs_client": lambda ctx, dev, K, W: handshake_client_line(ctx, dev, K, W)}
 
@@ -1164,7 +1277,7 @@ def measure_extras(ctx, dev, args):
     """The other 1-GPU configurations of BASELINE.json, each a device-resident batch."""
     import torch
     out = []
-    for name in ("configs1", "configs3", "configs2", "encode", "inflate", "handshake", "hs_client"):
+    for name in ("configs1", "configs3", "configs2", "encode", "inflate", "deflate", "handshake", "hs_client"):
         out.append(EXTRA_LINES[name](ctx, dev, args.extra_steps, 2))
         torch.cuda.empty_cache()
     return out

@@ -21,7 +21,8 @@ std::atomic<uint64_t> g_ctx_allocs{0};  // device workspace allocations of every
 const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link",     "k_piecesN",
                                            "k_final",    "k_enc_len",  "k_enc_scan",
                                            "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate",
-                                           "k_defl_plan", "k_defl_prep", "k_defl_match", "k_defl_parse", "k_defl_final", "k_defl_serial"};
+                                           "k_defl_plan", "k_defl_prep", "k_defl_match", "k_defl_parse", "k_defl_final", "k_defl_serial",
+                                           "k_defl_trees", "k_defl_emit"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -76,7 +77,8 @@ struct wsg_ctx {
   DevBuf i_split;  // [1] u64: messages the split-lane decode took (wsg_inflate_split_count)
   DevBuf i_tok2, i_lit2;  // the split's tail regions
   // permessage-deflate compression workspace (deflate.hip, DeflArgs)
-  DevBuf d_flags, d_fout, d_fsym, d_ff, d_fs, d_sums, d_S, d_link, d_res, d_tres, d_strips, d_ftail, d_chunks, d_sym, d_tw, d_ssym;
+  DevBuf d_flags, d_fout, d_fsym, d_ff, d_fs, d_sums, d_S, d_link, d_res, d_tres, d_strips, d_ftail, d_chunks, d_sym, d_tw, d_ssym,
+      d_blocks;
   int defl_serial = 0;               // WSG_TUNE_DEFLATE_SERIAL 1: zlib's loop per session at every level (tests)
   // measurement / test switches (wsg_set_tuning; the defaults are the product)
   int infl_tokens = 1;               // WSG_TUNE_INFLATE_TOKENS 0: no lane pre-decode (serial decoder only)
@@ -157,7 +159,8 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL)) {
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL && kid != K_DEFL_TREES &&
+                                 kid != K_DEFL_EMIT)) {
     f();
     return;
   }
@@ -1145,7 +1148,7 @@ int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_fr
   HIP_TRY(c, c->d_fsym.ensure(F * sizeof(uint64_t)));
   HIP_TRY(c, c->d_ff.ensure(F * sizeof(DeflFrame)));
   HIP_TRY(c, c->d_fs.ensure(S * sizeof(DeflSess)));
-  HIP_TRY(c, c->d_sums.ensure(4 * (S + 1) * sizeof(uint64_t)));
+  HIP_TRY(c, c->d_sums.ensure(5 * (S + 1) * sizeof(uint64_t)));
   HIP_TRY(c, c->d_ftail.ensure(F));
   DeflArgs a{};
   a.level = level;
@@ -1171,8 +1174,8 @@ int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_fr
   (void)payload_len;
   timed(c, K_DEFL_PLAN, [&] { launch_defl_plan(a, c->stream); });
   // the regions' totals decide the workspace: read them back
-  uint64_t tot[4];
-  for (int i = 0; i < 4; i++)
+  uint64_t tot[5];
+  for (int i = 0; i < 5; i++)
     HIP_TRY(c, hipMemcpyAsync(&tot[i], a.sums + (uint64_t)i * (S + 1) + S, sizeof(uint64_t), hipMemcpyDeviceToHost,
                               c->stream));
   HIP_TRY(c, hipStreamSynchronize(c->stream));
@@ -1200,6 +1203,7 @@ int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_fr
     HIP_TRY(c, c->d_strips.ensure(F * 2 * zd_strip()));
     HIP_TRY(c, c->d_chunks.ensure((tot[3] + 1) * sizeof(uint64_t)));
     HIP_TRY(c, c->d_sym.ensure((tot[2] + 4) * sizeof(uint32_t)));
+    HIP_TRY(c, c->d_blocks.ensure((tot[4] + 1) * sizeof(DeflBlock)));
     a.S = (uint8_t*)c->d_S.p;
     a.link = (uint16_t*)c->d_link.p;
     a.res = (uint32_t*)c->d_res.p;
@@ -1208,10 +1212,13 @@ int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_fr
     a.chunks = (uint64_t*)c->d_chunks.p;
     a.chunk_cap = tot[3];
     a.sym = (uint32_t*)c->d_sym.p;
+    a.blocks = (DeflBlock*)c->d_blocks.p;
     timed(c, K_DEFL_PREP, [&] { launch_defl_prep(a, c->stream); });
     if (tot[3]) timed(c, K_DEFL_MATCH, [&] { launch_defl_match(a, c->stream); });
   }
   timed(c, K_DEFL_PARSE, [&] { launch_defl_parse(a, c->stream); });
+  if (level >= 4) timed(c, K_DEFL_TREES, [&] { launch_defl_trees(a, c->stream, tot[4]); });
+  timed(c, K_DEFL_EMIT, [&] { launch_defl_emit(a, c->stream); });
   timed(c, K_DEFL_FINAL, [&] { launch_defl_final(a, c->stream); });
   return WSG_API_OK;
 }

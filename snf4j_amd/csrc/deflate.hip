@@ -40,13 +40,14 @@ __device__ inline void wave_mem_sync() {
 }
 
 struct Sums {
-  uint64_t *S, *O, *Y, *C;
+  uint64_t *S, *O, *Y, *C, *B;
   __device__ Sums(const DeflArgs& a) {
     const uint64_t n = (uint64_t)a.n_sessions + 1;
     S = a.sums;
     O = a.sums + n;
     Y = a.sums + 2 * n;
     C = a.sums + 3 * n;
+    B = a.sums + 4 * n;
   }
 };
 
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   Sums sm(a);
   if (s >= a.n_sessions) {
-    if (s == a.n_sessions) sm.S[s] = sm.O[s] = sm.Y[s] = sm.C[s] = 0;
+    if (s == a.n_sessions) sm.S[s] = sm.O[s] = sm.Y[s] = sm.C[s] = sm.B[s] = 0;
     return;
   }
   const wsg_deflate_state st = a.state[s];
@@ -65,7 +66,7 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
   const bool parallel = a.level >= 4 && !a.serial;
   const uint32_t k0 = a.session_first[s], k1 = a.session_first[s + 1];
   uint64_t orel = 0, yrel = 0, chunks = 0;
-  uint32_t srel = DEFL_HIST, last = ~0u;
+  uint32_t srel = DEFL_HIST, last = ~0u, brel = 0;
   bool any_call = false, first_fresh = false;
   for (uint32_t k = k0; k < k1; k++) {
     const wsg_frame_desc d = a.desc[k];
@@ -74,7 +75,7 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
     uint8_t rsv_out, drop;
     const int kind = pmd_step(&comp, d.opcode, fin, rsv, len, a.no_context, &rsv_out, &drop);
     uint32_t fl = (uint32_t)kind | (drop ? DF_DROP : 0u) | ((uint32_t)rsv_out << DF_RSV_SHIFT) | (fin ? DF_FIN : 0u);
-    DeflFrame f{0, 0, len, s};
+    DeflFrame f{0, 0, len, s, 0, 0};
     if (kind == PMD_CALL) {
       if (!hasd) {
         fl |= DF_SEG;
@@ -103,7 +104,9 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
       if (parallel) {
         f.s_rel = srel;
         a.fsym[k] = yrel;
-        yrel += ((len < (uint32_t)zd::SYM_END ? len : (uint32_t)zd::SYM_END) + 4) & ~3u;
+        yrel += (len + 3) & ~3u;   // every block's symbols, back to back (a symbol covers >= 1 byte)
+        f.blk_rel = brel;
+        brel += defl_blk_cap(len);
         chunks += (len > 2 ? (len - 2 + DEFL_CH - 1) / DEFL_CH : 0) + ((fl & DF_TAIL_OK) ? 1 : 0);
         srel += len;
       }
@@ -131,6 +134,7 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
   sm.O[s] = orel;
   sm.Y[s] = yrel;
   sm.C[s] = chunks;
+  sm.B[s] = brel;
   DeflSess fs;
   fs.sw_final = sw;
   fs.hw_final = st.high_water;
@@ -142,12 +146,12 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
   a.fs[s] = fs;
 }
 
-// exclusive scan of the four per-session size arrays (one workgroup)
+// exclusive scan of the five per-session size arrays (one workgroup)
 __global__ __launch_bounds__(1024) void k_defl_scan(DeflArgs a) {
   __shared__ uint64_t part[1024];
   const uint32_t tid = threadIdx.x;
   const uint64_t n = a.n_sessions;
-  for (int arr = 0; arr < 4; arr++) {
+  for (int arr = 0; arr < 5; arr++) {
     uint64_t* v = a.sums + (uint64_t)arr * (n + 1);
     uint64_t carry = 0;
     for (uint64_t b = 0; b < n; b += 1024) {
@@ -395,11 +399,90 @@ struct LinkAcc {
   __device__ uint32_t operator()(uint32_t p) const { return l[p]; }
 };
 
+__device__ inline uint64_t load_u64(const uint8_t* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);   // unaligned global load
+  return v;
+}
+
+// longest_match at a position whose scan never reaches the frame's end (p + 266 <= end):
+// one candidate a call, 8 bytes a compare; the same walk as zd::match_at
+struct FastWalk {
+  uint32_t q, dist, k, best, best_d, qres;
+  uint64_t b;
+  bool done;
+};
+
+__device__ inline void fast_init(FastWalk& w, const uint8_t* S, const uint16_t* link, uint32_t p) {
+  const uint32_t d = link[p];
+  w.k = 1;
+  w.best = 2;
+  w.best_d = 0;
+  w.qres = 0;
+  w.dist = d;
+  w.q = p - d;
+  w.done = d == 0 || d > (uint32_t)zd::MAX_DIST;
+  w.b = load_u64(S + p);
+}
+
+// evaluates candidate w.q; returns true when the walk is over
+__device__ inline bool fast_step(FastWalk& w, const uint8_t* S, const uint16_t* link, uint32_t p, const zd::Cfg& c) {
+  const uint32_t qbudget = c.chain >> 2;
+  const uint8_t* mq = S + w.q;
+  const uint64_t x = load_u64(mq) ^ w.b;
+  if ((x & 0xFFFF) == 0) {
+    const bool cand = w.best < 8 ? ((x >> (8 * w.best)) & 0xFF) == 0 : mq[w.best] == S[p + w.best];
+    if (cand) {
+      uint32_t len;
+      if (x) {
+        len = (uint32_t)__builtin_ctzll(x) >> 3;
+      } else {
+        len = 8;
+        for (;;) {
+          const uint64_t y = load_u64(mq + len) ^ load_u64(S + p + len);
+          if (y) {
+            len += (uint32_t)__builtin_ctzll(y) >> 3;
+            break;
+          }
+          len += 8;
+          if (len >= (uint32_t)zd::MAX_MATCH) break;
+        }
+        if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
+      }
+      if (len > w.best) {
+        w.best = len;
+        w.best_d = w.dist;
+        if (len >= c.nice) return true;
+      }
+    }
+  }
+  if (w.k == qbudget) w.qres = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
+  if (w.k >= c.chain) return true;
+  const uint32_t l = link[w.q];
+  if (l == 0) return true;
+  w.dist += l;
+  if (w.dist >= (uint32_t)zd::MAX_DIST) return true;
+  w.q -= l;
+  w.k++;
+  return false;
+}
+
+__device__ inline void fast_result(const FastWalk& w, const zd::Cfg& c, uint32_t p0d, uint32_t* full, uint32_t* quarter) {
+  if (p0d == 0 || p0d > (uint32_t)zd::MAX_DIST) {
+    *full = *quarter = 0;
+    return;
+  }
+  const uint32_t f = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
+  *full = f | (p0d == (uint32_t)zd::MAX_DIST ? (uint32_t)zd::MR_HEAD_AT_MAX : 0u);
+  *quarter = w.k <= (uint32_t)(c.chain >> 2) ? f : w.qres;
+}
+
 __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
   Sums sm(a);
   const uint64_t total = sm.C[a.n_sessions];
   const zd::Cfg cfg = zd::level_cfg(a.level);
   const uint32_t lane = threadIdx.x;
+  const uint64_t lt_mask = (1ull << lane) - 1;
   for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
     const uint64_t e = a.chunks[c];
     const uint32_t k = (uint32_t)e, ci = (uint32_t)(e >> 32) & 0x7fffffffu;
@@ -413,8 +496,44 @@ __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
     const uint32_t tstart = end - start > DEFL_TAILN ? end - DEFL_TAILN : start;
     const uint32_t p0 = var ? tstart : start + ci * DEFL_CH;
     const uint32_t p1 = var ? end - 2 : (p0 + DEFL_CH < end - 2 ? p0 + DEFL_CH : end - 2);
+    // positions whose scan stays inside the frame: the fast walk, lanes refilled as they finish
+    const uint32_t pf = var ? p0 : (end >= 266 && end - 266 > p0 ? (end - 266 < p1 ? end - 266 : p1) : p0);
+    if (pf > p0) {
+      uint32_t next = p0 + 64;
+      uint32_t p = p0 + lane;
+      bool act = p < pf;
+      FastWalk w;
+      uint32_t d0 = 0;
+      if (act) {
+        fast_init(w, S, link, p);
+        d0 = w.dist;
+      }
+      while (__ballot(act)) {
+        bool fin = false;
+        if (act) fin = w.done || fast_step(w, S, link, p, cfg);
+        if (fin) {
+          uint32_t full, quarter;
+          fast_result(w, cfg, d0, &full, &quarter);
+          res[2 * (uint64_t)p] = full;
+          res[2 * (uint64_t)p + 1] = quarter;
+        }
+        const uint64_t m = __ballot(fin);
+        if (m) {
+          if (fin) {
+            p = next + (uint32_t)__builtin_popcountll(m & lt_mask);
+            act = p < pf;
+            if (act) {
+              fast_init(w, S, link, p);
+              d0 = w.dist;
+            }
+          }
+          next += (uint32_t)__builtin_popcountll(m);
+        }
+      }
+    }
+    // the frame's last bytes (and the tail variant): the scan may pass the end
     StripBytes by{S, end, a.strips + ((uint64_t)k * 2 + (var ? 1 : 0)) * zd::STRIP};
-    for (uint32_t p = p0 + lane; p < p1; p += 64) {
+    for (uint32_t p = (pf > p0 ? pf : p0) + lane; p < p1; p += 64) {
       uint32_t full, quarter;
       zd::match_at(by, LinkAcc{link}, p, end, cfg, &full, &quarter);
       if (var) {
@@ -470,42 +589,345 @@ __device__ void pass_or_empty(const DeflArgs& a, uint32_t k, uint32_t fl, uint64
   a.out_desc[k] = o;
 }
 
+// the parse's block sink: one DeflBlock slot a block zlib flushes
+struct BlockSink {
+  DeflBlock* blk;
+  const uint32_t* sym_base;
+  uint32_t nb;
+  __device__ void operator()(const uint32_t* sym, uint32_t nsym, uint32_t stored_s, uint32_t stored_len,
+                             bool stored_ok) {
+    DeflBlock* b = blk + nb++;
+    b->sym0 = (uint64_t)(sym - sym_base);
+    b->nsym = nsym;
+    b->stored_s = stored_s;
+    b->stored_len = stored_len;
+    b->stored_ok = stored_ok ? 1 : 0;
+  }
+};
+
+// lane per frame: deflate_slow's control flow over the match results; the symbols of
+// every block and its stored range go to the frame's block slots (k_defl_trees, k_defl_emit)
 __global__ __launch_bounds__(64) void k_defl_parse(DeflArgs a) {
   Sums sm(a);
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (tid >= a.n_lanes) return;   // one TreeWork a lane
-  const uint32_t stride = a.n_lanes;
-  zd::TreeWork* tw = (zd::TreeWork*)a.tw + tid;
+  if (tid >= a.n_lanes) return;
   const zd::Cfg cfg = zd::level_cfg(a.level);
-  for (uint64_t k = tid; k < a.n_frames; k += stride) {
+  for (uint64_t k = tid; k < a.n_frames; k += a.n_lanes) {
     const uint32_t fl = a.fflags[k];
     const DeflFrame f = a.ff[k];
-    const uint64_t obase = sm.O[f.sess];
     if ((fl & DF_KIND) != PMD_CALL) {
-      pass_or_empty(a, (uint32_t)k, fl, obase);
+      pass_or_empty(a, (uint32_t)k, fl, sm.O[f.sess]);
       continue;
     }
-    const wsg_frame_desc d = a.desc[k];
-    zd::BitWriter bw{a.out + obase + a.fout[k], 0, 0, 0};
-    if (a.level == 0) {
-      zd::stored_call(&bw, a.payload + d.payload_off, f.len);
-    } else {
-      const uint64_t soff = sm.S[f.sess];
-      const uint32_t end = f.s_rel + f.len;
-      ResAcc ra{a.res + 2 * soff, a.tres + (uint64_t)k * DEFL_TAILN * 2,
-                end - f.s_rel > DEFL_TAILN ? end - DEFL_TAILN : f.s_rel};
-      zd::CallGeom g{f.start_w, (uint8_t)((fl & DF_START_SLID) ? 1 : 0)};
-      const bool tail = zd::parse_call(ra, SBytes{a.S + soff}, f.s_rel, f.len, g, cfg, tw,
-                                       a.sym + sm.Y[f.sess] + a.fsym[k], &bw);
-      a.ftail[k] = tail ? 1 : 0;
+    if (a.level == 0) continue;   // stored framing: k_defl_emit
+    const uint64_t soff = sm.S[f.sess];
+    const uint32_t end = f.s_rel + f.len;
+    ResAcc ra{a.res + 2 * soff, a.tres + (uint64_t)k * DEFL_TAILN * 2,
+              end - f.s_rel > DEFL_TAILN ? end - DEFL_TAILN : f.s_rel};
+    zd::CallGeom g{f.start_w, (uint8_t)((fl & DF_START_SLID) ? 1 : 0)};
+    DeflBlock* blk = a.blocks + sm.B[f.sess] + f.blk_rel;
+    BlockSink sink{blk, a.sym, 0};
+    const bool tail = zd::parse_call(ra, SBytes{a.S + soff}, f.s_rel, f.len, g, cfg,
+                                     a.sym + sm.Y[f.sess] + a.fsym[k], true, sink);
+    for (uint32_t b = sink.nb; b < defl_blk_cap(f.len); b++) blk[b].nsym = 0;
+    a.ftail[k] = tail ? 1 : 0;
+    a.ff[k].nblk = sink.nb;
+  }
+}
+
+// lane per block, the block's TreeWork in LDS (32 lanes a workgroup): frequencies, the
+// three Huffman trees exactly as zlib's heap builds them, the block type and its size
+__global__ __launch_bounds__(32) void k_defl_trees(DeflArgs a) {
+  __shared__ zd::TreeWork tws[32];
+  Sums sm(a);
+  const uint64_t total = sm.B[a.n_sessions];
+  zd::TreeWork* t = &tws[threadIdx.x];
+  for (uint64_t i = (uint64_t)blockIdx.x * 32 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 32) {
+    DeflBlock* b = a.blocks + i;
+    const uint32_t nsym = b->nsym;
+    if (nsym == 0) continue;
+    zd::init_block(t);
+    const uint32_t* sy = a.sym + b->sym0;
+    for (uint32_t j = 0; j < nsym; j++) zd::tally(t, sy[j]);
+    uint32_t bits;
+    int max_blindex;
+    const int type = zd::plan_block(t, b->stored_ok != 0, b->stored_len, &bits, &max_blindex);
+    b->type = (uint8_t)type;
+    b->bits = bits;
+    if (type == 2) {
+      b->lcodes = (uint16_t)(t->l_max + 1);
+      b->dcodes = (uint8_t)(t->d_max + 1);
+      b->blcodes = (uint8_t)(max_blindex + 1);
+      for (int n = 0; n <= t->l_max; n++) b->ltab[n] = t->lfc[n] | (uint32_t)t->ldl[n] << 16;
+      for (int n = 0; n <= t->d_max; n++) b->dtab[n] = t->dfc[n] | (uint32_t)t->ddl[n] << 16;
+      for (int n = 0; n < zd::BL_CODES; n++) b->btab[n] = t->bfc[n] | (uint32_t)t->bdl[n] << 16;
     }
-    wsg_frame_desc o;
-    o.payload_off = obase + a.fout[k];
-    o.payload_len = (uint32_t)bw.pos - ((fl & DF_FIN) ? 4u : 0u);
-    o.opcode = d.opcode;
-    o.flags = (uint8_t)(((fl & DF_FIN) ? 0x80 : 0) | (((fl >> DF_RSV_SHIFT) & 7) << 4) | WSG_DESC_DEFLATED);
-    o.status = 0;
-    a.out_desc[k] = o;
+  }
+}
+
+// bit output of one thread into the zeroed output words: the first and last words of the
+// thread's run may be shared with a neighbour's (atomicOr), the rest are its own
+struct WordSink {
+  uint32_t* w;        // the frame's output as words
+  uint64_t acc;
+  uint32_t n;         // bits in acc
+  uint32_t idx;       // word the low bits of acc go to
+  bool first;
+  __device__ WordSink(uint32_t* words, uint32_t bitpos) : w(words), acc(0), n(bitpos & 31), idx(bitpos >> 5),
+                                                         first(true) {}
+  __device__ void put(uint32_t v, uint32_t len) {
+    acc |= (uint64_t)v << n;
+    n += len;
+    if (n >= 32) {
+      if (first) {
+        atomicOr(&w[idx], (uint32_t)acc);
+        first = false;
+      } else {
+        w[idx] = (uint32_t)acc;
+      }
+      idx++;
+      acc >>= 32;
+      n -= 32;
+    }
+  }
+  __device__ void done() {
+    if (n > 0) atomicOr(&w[idx], (uint32_t)acc);
+  }
+};
+
+__device__ inline void sym_code(uint32_t sy, const uint32_t* ltab, const uint32_t* dtab, bool is_static, uint32_t* c1,
+                                uint32_t* l1, uint32_t* c2, uint32_t* l2) {
+  // one symbol as at most two (code, length) pairs: (literal) or (length code + extra bits,
+  // distance code + extra bits); at most 15 + 5 and 15 + 13 bits
+  const uint32_t dist = sy >> 8;
+  const int lc = (int)(sy & 255);
+  if (dist == 0) {
+    if (is_static) {
+      *c1 = zd::static_lcode(lc);
+      *l1 = (uint32_t)zd::static_llen(lc);
+    } else {
+      *c1 = ltab[lc] & 0xffff;
+      *l1 = ltab[lc] >> 16;
+    }
+    *l2 = 0;
+    *c2 = 0;
+    return;
+  }
+  const int code = zd::len_code(lc);
+  uint32_t c, l;
+  if (is_static) {
+    c = zd::static_lcode(code + 257);
+    l = (uint32_t)zd::static_llen(code + 257);
+  } else {
+    c = ltab[code + 257] & 0xffff;
+    l = ltab[code + 257] >> 16;
+  }
+  const int ex = zd::len_extra(code);
+  *c1 = c | (ex ? (uint32_t)(lc - zd::len_base(code)) << l : 0u);
+  *l1 = l + (uint32_t)ex;
+  const int d = (int)dist - 1;
+  const int dc = zd::dist_code(d);
+  if (is_static) {
+    c = zd::static_dcode(dc);
+    l = 5;
+  } else {
+    c = dtab[dc] & 0xffff;
+    l = dtab[dc] >> 16;
+  }
+  const int dx = zd::dist_extra(dc);
+  *c2 = c | (dx ? (uint32_t)(d - zd::dist_base(dc)) << l : 0u);
+  *l2 = l + (uint32_t)dx;
+}
+
+// send_tree into a WordSink (thread 0 of k_defl_emit): zlib's run-length coding of a
+// tree's code lengths with the bit-length codes
+__device__ void send_tree_w(WordSink& o, const uint32_t* tab, int max_code, const uint32_t* btab) {
+  auto len_of = [&](int n) -> int { return n <= max_code ? (int)(tab[n] >> 16) : 0xffff; };
+  auto bl = [&](int sym) { o.put(btab[sym] & 0xffff, btab[sym] >> 16); };
+  int prevlen = -1, curlen, nextlen = len_of(0), count = 0, max_count = 7, min_count = 4;
+  if (nextlen == 0) max_count = 138, min_count = 3;
+  for (int n = 0; n <= max_code; n++) {
+    curlen = nextlen;
+    nextlen = len_of(n + 1);
+    if (++count < max_count && curlen == nextlen) {
+      continue;
+    } else if (count < min_count) {
+      do { bl(curlen); } while (--count != 0);
+    } else if (curlen != 0) {
+      if (curlen != prevlen) {
+        bl(curlen);
+        count--;
+      }
+      bl(zd::REP_3_6);
+      o.put((uint32_t)(count - 3), 2);
+    } else if (count <= 10) {
+      bl(zd::REPZ_3_10);
+      o.put((uint32_t)(count - 3), 3);
+    } else {
+      bl(zd::REPZ_11_138);
+      o.put((uint32_t)(count - 11), 7);
+    }
+    count = 0;
+    prevlen = curlen;
+    if (nextlen == 0) max_count = 138, min_count = 3;
+    else if (curlen == nextlen) max_count = 6, min_count = 3;
+    else max_count = 7, min_count = 4;
+  }
+}
+
+// workgroup per frame: the bits of its blocks (stored copies, static or dynamic codes: the
+// trees by thread 0, the symbols by every thread at offsets from a block-wide scan) and the
+// sync marker, into the frame's zeroed output slot
+constexpr int EMIT_T = 256;
+__global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
+  __shared__ uint32_t s_ltab[286], s_dtab[30];
+  __shared__ uint32_t s_scan[EMIT_T];
+  __shared__ uint32_t s_off;   // running bit offset of the frame
+  Sums sm(a);
+  const uint32_t tid = threadIdx.x;
+  for (uint64_t k = blockIdx.x; k < a.n_frames; k += gridDim.x) {
+    const uint32_t fl = a.fflags[k];
+    if ((fl & DF_KIND) != PMD_CALL) continue;
+    const DeflFrame f = a.ff[k];
+    const uint64_t obase = sm.O[f.sess] + a.fout[k];
+    uint8_t* ob = a.out + obase;
+    uint32_t* ow = (uint32_t*)ob;
+    const DeflBlock* blk = a.blocks + sm.B[f.sess] + f.blk_rel;
+    const uint32_t nb = a.level == 0 ? 0 : f.nblk;
+    // the frame's size: blocks in order, then the sync marker (3 bits, pad, 00 00 FF FF)
+    uint64_t bitsz = 0;
+    if (a.level == 0) {
+      const uint32_t nst = (f.len + 65534) / 65535;
+      bitsz = 8ull * (f.len + 5ull * nst);
+    } else {
+      for (uint32_t b = 0; b < nb; b++)
+        bitsz = blk[b].type == 0 ? ((bitsz + 3 + 7) & ~7ull) + 32 + 8ull * blk[b].stored_len : bitsz + 3 + blk[b].bits;
+    }
+    const uint64_t bytes = (((bitsz + 3 + 7) & ~7ull) + 32) >> 3;
+    for (uint64_t i = tid; i < (bytes + 3) >> 2; i += EMIT_T) ow[i] = 0;
+    if (tid == 0) s_off = 0;
+    __syncthreads();
+    if (a.level == 0) {   // deflate_stored with Java's output buffer: 65535-byte stored blocks
+      const uint8_t* src = a.payload + a.desc[k].payload_off;
+      for (uint32_t o = 0, i = 0; o < f.len; o += 65535, i++) {
+        const uint32_t n = f.len - o < 65535u ? f.len - o : 65535u;
+        uint8_t* h = ob + (uint64_t)o + 5ull * i;
+        if (tid == 0) {
+          h[0] = 0;
+          h[1] = (uint8_t)n;
+          h[2] = (uint8_t)(n >> 8);
+          h[3] = (uint8_t)~n;
+          h[4] = (uint8_t)(~n >> 8);
+        }
+        for (uint32_t j = tid; j < n; j += EMIT_T) h[5 + j] = src[o + j];
+      }
+      __syncthreads();
+      if (tid == 0) s_off = (uint32_t)(8ull * (f.len + 5ull * ((f.len + 65534) / 65535)));
+    }
+    const uint8_t* S = a.S + sm.S[f.sess];
+    for (uint32_t b = 0; b < nb; b++) {
+      const DeflBlock* B = blk + b;
+      const uint32_t o = s_off;
+      const int type = B->type;
+      if (type == 0) {   // stored: 000, pad, LEN, NLEN, the bytes (as whole words, OR'ed in)
+        const uint32_t pos = ((o + 3 + 7) & ~7u) >> 3;
+        const uint32_t L = B->stored_len;
+        const uint8_t* src = S + B->stored_s;
+        const uint32_t w0 = pos >> 2, w1 = (pos + 4 + L + 3) >> 2;
+        for (uint32_t w = w0 + tid; w < w1; w += EMIT_T) {
+          uint32_t v = 0;
+          for (uint32_t j = 0; j < 4; j++) {
+            const uint32_t bp = w * 4 + j;   // byte of the frame
+            uint32_t x = 0;
+            if (bp >= pos && bp < pos + 4 + L) {
+              const uint32_t r = bp - pos;
+              x = r == 0 ? (L & 0xff) : r == 1 ? (L >> 8) & 0xff : r == 2 ? (~L) & 0xff : r == 3 ? (~L >> 8) & 0xff
+                                                                                                 : src[r - 4];
+            }
+            v |= x << (8 * j);
+          }
+          if (w == w0 || w == w1 - 1) atomicOr(&ow[w], v);
+          else ow[w] = v;
+        }
+        __syncthreads();
+        if (tid == 0) s_off = (pos + 4 + L) * 8;
+        __syncthreads();
+        continue;
+      }
+      const bool is_static = type == 1;
+      if (!is_static) {
+        for (uint32_t i = tid; i < B->lcodes; i += EMIT_T) s_ltab[i] = B->ltab[i];
+        for (uint32_t i = tid; i < B->dcodes; i += EMIT_T) s_dtab[i] = B->dtab[i];
+      }
+      __syncthreads();
+      // the symbols: a contiguous run a thread; bit offsets from a block-wide scan
+      const uint32_t nsym = B->nsym;
+      const uint32_t per = (nsym + EMIT_T - 1) / EMIT_T;
+      const uint32_t i0 = tid * per < nsym ? tid * per : nsym;
+      const uint32_t i1 = i0 + per < nsym ? i0 + per : nsym;
+      const uint32_t* sy = a.sym + B->sym0;
+      uint32_t mybits = 0;
+      for (uint32_t i = i0; i < i1; i++) {
+        uint32_t c1, l1, c2, l2;
+        sym_code(sy[i], s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
+        mybits += l1 + l2;
+      }
+      s_scan[tid] = mybits;
+      __syncthreads();
+      for (uint32_t st = 1; st < EMIT_T; st <<= 1) {
+        const uint32_t y = tid >= st ? s_scan[tid - st] : 0;
+        __syncthreads();
+        s_scan[tid] += y;
+        __syncthreads();
+      }
+      const uint32_t sym_bits = s_scan[EMIT_T - 1];
+      const uint32_t eob_c = is_static ? zd::static_lcode(zd::END_BLOCK) : s_ltab[zd::END_BLOCK] & 0xffff;
+      const uint32_t eob_l = is_static ? 7u : s_ltab[zd::END_BLOCK] >> 16;
+      const uint32_t blk_end = o + 3 + B->bits;
+      const uint32_t sym_start = blk_end - eob_l - sym_bits;
+      {
+        WordSink ws(ow, sym_start + s_scan[tid] - mybits);
+        for (uint32_t i = i0; i < i1; i++) {
+          uint32_t c1, l1, c2, l2;
+          sym_code(sy[i], s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
+          ws.put(c1, l1);
+          if (l2) ws.put(c2, l2);
+        }
+        if (tid == EMIT_T - 1) ws.put(eob_c, eob_l);
+        ws.done();
+      }
+      if (tid == 0) {   // the block header, then (dynamic) send_all_trees
+        WordSink ws(ow, o);
+        ws.put(is_static ? 2u : 4u, 3);
+        if (!is_static) {
+          const int lcodes = B->lcodes, dcodes = B->dcodes, blcodes = B->blcodes;
+          ws.put((uint32_t)(lcodes - 257), 5);
+          ws.put((uint32_t)(dcodes - 1), 5);
+          ws.put((uint32_t)(blcodes - 4), 4);
+          for (int r = 0; r < blcodes; r++) ws.put(B->btab[zd::bl_order(r)] >> 16, 3);
+          send_tree_w(ws, s_ltab, lcodes - 1, B->btab);
+          send_tree_w(ws, s_dtab, dcodes - 1, B->btab);
+        }
+        ws.done();
+      }
+      __syncthreads();
+      if (tid == 0) s_off = blk_end;
+      __syncthreads();
+    }
+    // the sync marker: 000, pad, 00 00 FF FF
+    if (tid == 0) {
+      const uint32_t pos = ((s_off + 3 + 7) & ~7u) >> 3;
+      ob[pos + 2] = 0xff;   // (bytes past the last block are zero, and only thread 0 writes here now)
+      ob[pos + 3] = 0xff;
+      wsg_frame_desc o;
+      o.payload_off = obase;
+      o.payload_len = (uint32_t)(pos + 4) - ((fl & DF_FIN) ? 4u : 0u);
+      o.opcode = a.desc[k].opcode;
+      o.flags = (uint8_t)(((fl & DF_FIN) ? 0x80 : 0) | (((fl >> DF_RSV_SHIFT) & 7) << 4) | WSG_DESC_DEFLATED);
+      o.status = 0;
+      a.out_desc[k] = o;
+    }
+    __syncthreads();
   }
 }
 
@@ -623,6 +1045,14 @@ void launch_defl_match(const DeflArgs& a, hipStream_t s) {
 }
 void launch_defl_parse(const DeflArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_defl_parse, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_defl_trees(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
+  uint64_t g = (n_blocks + 31) / 32;
+  hipLaunchKernelGGL(k_defl_trees, dim3((uint32_t)(g < 65536 ? (g ? g : 1) : 65536)), dim3(32), 0, s, a);
+}
+void launch_defl_emit(const DeflArgs& a, hipStream_t s) {
+  uint64_t g = a.n_frames < 262144 ? a.n_frames : 262144;
+  hipLaunchKernelGGL(k_defl_emit, dim3((uint32_t)(g ? g : 1)), dim3(EMIT_T), 0, s, a);
 }
 void launch_defl_final(const DeflArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_defl_final, dim3(a.n_sessions), dim3(256), 0, s, a);

@@ -384,27 +384,48 @@ ZD_FN void compress_block(BitWriter* bw, const TreeWork* t, const SYMS& syms, ui
     else bw->put(t->lfc[END_BLOCK], t->ldl[END_BLOCK]);
 }
 
-// _tr_flush_block (last = 0) over a block whose frequencies t holds (init_block + tally);
-// stored = the block's bytes (window + block_start) or null when block_start < 0
-template <class SYMS>
-ZD_FN void flush_block(TreeWork* t, BitWriter* bw, const SYMS& syms, uint32_t nsym, const uint8_t* stored,
-                       uint32_t stored_len) {
+// The decision half of _tr_flush_block over a block whose frequencies t holds (init_block
+// + tally): the trees (codes in fc, lengths in dl), max_blindex, and the block type zlib
+// picks — 0 stored (only when `stored_ok`, zlib's block_start >= 0), 1 static, 2 dynamic.
+// *bits: the block's size after its 3-bit header (static_len or opt_len; stored blocks are
+// byte-aligned: 5 bytes + the data).
+ZD_FN int plan_block(TreeWork* t, bool stored_ok, uint32_t stored_len, uint32_t* bits, int* max_blindex_out) {
     t->l_max = (int16_t)build_tree<0>(t, t->lfc, t->ldl);
     t->d_max = (int16_t)build_tree<1>(t, t->dfc, t->ddl);
-    // build_bl_tree
-    scan_tree(t->bfc, t->ldl, t->l_max);
+    scan_tree(t->bfc, t->ldl, t->l_max);   // build_bl_tree
     scan_tree(t->bfc, t->ddl, t->d_max);
     build_tree<2>(t, t->bfc, t->bdl);
     int max_blindex;
     for (max_blindex = BL_CODES - 1; max_blindex >= 3; max_blindex--)
         if (t->bdl[bl_order(max_blindex)] != 0) break;
     t->opt_len += 3u * ((uint32_t)max_blindex + 1) + 5 + 5 + 4;
+    *max_blindex_out = max_blindex;
     uint32_t opt_lenb = (t->opt_len + 3 + 7) >> 3;
     uint32_t static_lenb = (t->static_len + 3 + 7) >> 3;
     if (static_lenb <= opt_lenb) opt_lenb = static_lenb;
-    if (stored_len + 4 <= opt_lenb && stored != nullptr) {
+    if (stored_len + 4 <= opt_lenb && stored_ok) {
+        *bits = 0;
+        return 0;
+    }
+    if (static_lenb == opt_lenb) {
+        *bits = t->static_len;
+        return 1;
+    }
+    *bits = t->opt_len;
+    return 2;
+}
+
+// _tr_flush_block (last = 0) over a block whose frequencies t holds (init_block + tally);
+// stored = the block's bytes (window + block_start) or null when block_start < 0
+template <class SYMS>
+ZD_FN void flush_block(TreeWork* t, BitWriter* bw, const SYMS& syms, uint32_t nsym, const uint8_t* stored,
+                       uint32_t stored_len) {
+    uint32_t bits;
+    int max_blindex;
+    const int type = plan_block(t, stored != nullptr, stored_len, &bits, &max_blindex);
+    if (type == 0) {
         stored_block(bw, stored, stored_len);
-    } else if (static_lenb == opt_lenb) {
+    } else if (type == 1) {
         bw->put(2, 3);   // (STATIC_TREES << 1) + last
         compress_block<true>(bw, t, syms, nsym);
     } else {
@@ -730,15 +751,17 @@ struct CallGeom {
     uint8_t start_slid;   // that fill slid the window with strstart exactly WSIZE + MAX_DIST
 };
 
-// deflate_slow over one frame from the per-position results.  res(s, variant) gives the
-// packed (full, quarter) pair at stream position s; variant 1 = after the frame's tail
-// slide (the window bytes past the end differ).  byte(p) is the stream byte (literals and
-// stored blocks).  Emits blocks (and the sync marker) to bw; returns whether the window
-// slid inside the frame's tail (the next call then starts without a slide).
-template <class RES, class BYTE>
+// deflate_slow over one frame from the per-position results.  res(s, variant, &full,
+// &quarter) gives the packed pair at stream position s; variant 1 = after a slide in the
+// frame's tail (the window bytes past the end differ).  byte(p) is the stream byte (the
+// literals).  Every block zlib would flush goes to sink(sym, nsym, stored_s, stored_len,
+// stored_ok): its symbols, and for the stored choice the stream range it covers (stored_ok:
+// zlib's block_start >= 0).  With sym_advance the next block's symbols follow (sym +=
+// nsym), else the buffer is reused.  The caller adds the sync marker.  Returns whether the
+// window slid inside the frame's tail (the next call then starts without a slide).
+template <class RES, class BYTE, class SINK>
 ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t len, CallGeom g, Cfg c,
-                      TreeWork* t, uint32_t* sym, BitWriter* bw, uint8_t* stored_scratch_unused = nullptr) {
-    (void)stored_scratch_unused;
+                      uint32_t* sym, bool sym_advance, SINK& sink) {
     uint32_t sw = g.start_w;                 // strstart, window index
     uint32_t s = start;                      // strstart, stream position
     uint32_t more = WINDOW_SIZE - sw;
@@ -746,28 +769,18 @@ ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t
     uint32_t n0 = rem < more ? rem : more;
     uint32_t loaded = sw + n0;               // window index of the loaded end
     rem -= n0;
-    const uint32_t end = start + len;
     int32_t block_start_w = (int32_t)sw;
     uint32_t block_start_s = s;
     uint32_t match_length = MIN_MATCH - 1, prev_length, match_start = 0, prev_match;
     bool match_available = false, tail_slid = false;
     bool slid_here = g.start_slid != 0;      // a slide put strstart at MAX_DIST at this loop top
     uint32_t nsym = 0;
-    init_block(t);
     auto flush = [&](uint32_t cur_s, int32_t cur_w) {
-        (void)cur_w;
-        uint32_t stored_len = cur_s - block_start_s;
-        // stored blocks copy window + block_start: the stream bytes of the block
-        const uint8_t* sp = block_start_w >= 0 ? byte.ptr(block_start_s) : nullptr;
-        flush_block(t, bw, ArraySyms{sym}, nsym, sp, stored_len);
+        sink(sym, nsym, block_start_s, cur_s - block_start_s, block_start_w >= 0);
+        if (sym_advance) sym += nsym;
         block_start_s = cur_s;
         block_start_w = cur_w;
         nsym = 0;
-    };
-    auto tally_sym = [&](uint32_t v) {
-        sym[nsym++] = v;
-        tally(t, v);
-        return nsym == (uint32_t)SYM_END;
     };
     for (;;) {
         uint32_t lookahead = loaded - sw;
@@ -814,16 +827,16 @@ ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t
         }
         slid_here = false;
         if (prev_length >= (uint32_t)MIN_MATCH && match_length <= prev_length) {
-            bool bflush = tally_sym(sym_match(s - 1 - prev_match, prev_length - MIN_MATCH));
+            sym[nsym++] = sym_match(s - 1 - prev_match, prev_length - MIN_MATCH);
             uint32_t adv = prev_length - 1;   // strstart moves to the match end
             s += adv;
             sw += adv;
             match_available = false;
             match_length = MIN_MATCH - 1;
-            if (bflush) flush(s, (int32_t)sw);
+            if (nsym == (uint32_t)SYM_END) flush(s, (int32_t)sw);
         } else if (match_available) {
-            bool bflush = tally_sym(sym_lit(byte(s - 1)));
-            if (bflush) flush(s, (int32_t)sw);
+            sym[nsym++] = sym_lit(byte(s - 1));
+            if (nsym == (uint32_t)SYM_END) flush(s, (int32_t)sw);
             s++;
             sw++;
         } else {
@@ -832,11 +845,22 @@ ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t
             sw++;
         }
     }
-    if (match_available) tally_sym(sym_lit(byte(s - 1)));
+    if (match_available) sym[nsym++] = sym_lit(byte(s - 1));
     if (nsym) flush(s, (int32_t)sw);
-    sync_marker(bw);
-    (void)end;
     return tail_slid;
 }
+
+// The host form of the sink: _tr_flush_block right away (trees, bits), as zlib does.
+struct FlushNow {
+    TreeWork* t;
+    BitWriter* bw;
+    const uint8_t* S;   // stream bytes (stored blocks)
+    ZD_MFN void operator()(const uint32_t* sym, uint32_t nsym, uint32_t stored_s, uint32_t stored_len,
+                           bool stored_ok) {
+        init_block(t);
+        for (uint32_t i = 0; i < nsym; i++) tally(t, sym[i]);
+        flush_block(t, bw, ArraySyms{sym}, nsym, stored_ok ? S + stored_s : nullptr, stored_len);
+    }
+};
 
 }  // namespace zd

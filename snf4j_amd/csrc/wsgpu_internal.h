@@ -243,7 +243,26 @@ struct DeflFrame {   // per CALL frame (k_defl_plan)
   uint32_t start_w;  // strstart after the call-start fill_window
   uint32_t len;
   uint32_t sess;
+  uint32_t blk_rel;  // first block slot within the session's (k_defl_plan)
+  uint32_t nblk;     // blocks zlib flushes for the frame (k_defl_parse)
 };
+
+// One deflate block (k_defl_parse -> k_defl_trees -> k_defl_emit).
+struct DeflBlock {
+  uint64_t sym0;        // first symbol (index into the symbol buffers)
+  uint32_t nsym;        // 0: an unused slot
+  uint32_t stored_s;    // the block's bytes: session-local stream position, length
+  uint32_t stored_len;
+  uint32_t bits;        // static / dynamic: bits after the 3-bit header (k_defl_trees)
+  uint8_t stored_ok;    // zlib's block_start >= 0 (a stored block is possible)
+  uint8_t type;         // 0 stored, 1 static trees, 2 dynamic trees
+  uint8_t dcodes, blcodes;
+  uint16_t lcodes, pad;
+  uint32_t ltab[286];   // dynamic: literal/length code | length << 16
+  uint32_t dtab[30];    // distance codes
+  uint32_t btab[19];    // bit-length codes, by bit-length symbol
+};
+constexpr uint32_t defl_blk_cap(uint32_t len) { return len / 16383u + 1u; }   // blocks a frame can need
 
 struct DeflSess {    // per session (k_defl_plan; k_defl_prep fills hw)
   uint32_t sw_final;    // strstart after the batch's last call (before a slide in its tail)
@@ -270,7 +289,8 @@ struct DeflArgs {
   uint64_t* fsym;           // [n_frames] symbol-buffer offset within the session's region (words)
   DeflFrame* ff;            // [n_frames]
   DeflSess* fs;             // [n_sessions]
-  uint64_t* sums;           // [4][n_sessions + 1]: S bytes, output bytes, symbol words, chunks -> exclusive
+  uint64_t* sums;           // [5][n_sessions + 1]: S bytes, output bytes, symbol words, chunks, block slots
+                            // -> exclusive
   uint8_t* S;               // stream regions
   uint16_t* link;           // [S]: distance to the previous string of its hash (0: none / >= 32 KiB)
   uint32_t* res;            // [2 x S]: match_at results at the calls' positions (full, quarter)
@@ -280,6 +300,7 @@ struct DeflArgs {
   uint64_t* chunks;         // [chunk bound]: frame | chunk << 32 | tail variant << 63
   uint64_t chunk_cap;
   uint32_t* sym;            // symbol buffers
+  DeflBlock* blocks;        // block slots
   void* tw;                 // zd::TreeWork per parse lane
   uint32_t n_lanes;         // parse lanes (grid-stride over frames)
   uint32_t* ssym;           // serial path: [n_sessions][zd::LIT_BUFSIZE]
@@ -289,7 +310,8 @@ struct DeflArgs {
 enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
   K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE,
-  K_DEFL_PLAN, K_DEFL_PREP, K_DEFL_MATCH, K_DEFL_PARSE, K_DEFL_FINAL, K_DEFL_SERIAL, K_COUNT
+  K_DEFL_PLAN, K_DEFL_PREP, K_DEFL_MATCH, K_DEFL_PARSE, K_DEFL_FINAL, K_DEFL_SERIAL, K_DEFL_TREES, K_DEFL_EMIT,
+  K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -353,6 +375,8 @@ void launch_defl_plan(const DeflArgs& a, hipStream_t s);    // k_defl_plan + k_d
 void launch_defl_prep(const DeflArgs& a, hipStream_t s);
 void launch_defl_match(const DeflArgs& a, hipStream_t s);
 void launch_defl_parse(const DeflArgs& a, hipStream_t s);
+void launch_defl_trees(const DeflArgs& a, hipStream_t s, uint64_t n_blocks);
+void launch_defl_emit(const DeflArgs& a, hipStream_t s);
 void launch_defl_final(const DeflArgs& a, hipStream_t s);
 void launch_defl_serial(const DeflArgs& a, hipStream_t s);
 size_t defl_treework_bytes();

@@ -204,7 +204,9 @@ void decomp_segment(Session& S, int level, std::vector<Call>& calls) {
             }
         };
         BitWriter bw{calls[k].out, 0, 0, 0};
-        last_tail = parse_call(res, PlainBytes{Sb.data()}, start, calls[k].len, geom[k], c, &tw, sym.data(), &bw);
+        FlushNow sink{&tw, &bw, Sb.data()};
+        last_tail = parse_call(res, PlainBytes{Sb.data()}, start, calls[k].len, geom[k], c, sym.data(), false, sink);
+        sync_marker(&bw);
         calls[k].out_len = bw.pos;
     }
     if (nc && last_tail) {
