@@ -371,7 +371,7 @@ def main():
             # this process, after the lines above, that alone moved the encode batcher
             # 27-40 GiB/s and the stage line 17-22 — a server process
             # runs its loops' batchers, not a benchmark's other lines.  Two untimed passes
-            # each (one was not enough: scripts/e2e_probe_w.py).
+            # each (one was not enough: a round-5 probe, profiles/r05_ab).
             torch.cuda.synchronize()
             for key, line in (("native_batcher_stages", "e2e_stages"),  # batcher -> inflate -> validator
                               # the same sessions streaming 4x longer: the burst line's pipeline

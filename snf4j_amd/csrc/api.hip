@@ -22,7 +22,7 @@ const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link", 
                                            "k_final",    "k_enc_len",  "k_enc_scan",
                                            "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate",
                                            "k_defl_plan", "k_defl_prep", "k_defl_match", "k_defl_parse", "k_defl_final", "k_defl_serial",
-                                           "k_defl_trees", "k_defl_emit"};
+                                           "k_defl_trees", "k_defl_emit", "k_defl_hist"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -160,7 +160,7 @@ static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
   if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL && kid != K_DEFL_TREES &&
-                                 kid != K_DEFL_EMIT)) {
+                                 kid != K_DEFL_EMIT && kid != K_DEFL_HIST)) {
     f();
     return;
   }
@@ -1217,7 +1217,10 @@ int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_fr
     if (tot[3]) timed(c, K_DEFL_MATCH, [&] { launch_defl_match(a, c->stream); });
   }
   timed(c, K_DEFL_PARSE, [&] { launch_defl_parse(a, c->stream); });
-  if (level >= 4) timed(c, K_DEFL_TREES, [&] { launch_defl_trees(a, c->stream, tot[4]); });
+  if (level >= 4) {
+    timed(c, K_DEFL_HIST, [&] { launch_defl_hist(a, c->stream, tot[4]); });
+    timed(c, K_DEFL_TREES, [&] { launch_defl_trees(a, c->stream, tot[4]); });
+  }
   timed(c, K_DEFL_EMIT, [&] { launch_defl_emit(a, c->stream); });
   timed(c, K_DEFL_FINAL, [&] { launch_defl_final(a, c->stream); });
   return WSG_API_OK;

@@ -2207,7 +2207,7 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   // on the process's hardware queues decided whether it overlapped the next flush's
   // upload — 26.6-29.5 GiB/s against 39.3-40.5 on the e2e encode line depending on the
   // streams created before it; written directly, 36.1-37.8 whatever the placement
-  // (profiles/r05_ab/r05ad_ab_encdirect.txt, scripts/seq_probe.py).
+  // (profiles/r05_ab/r05ad_ab_encdirect.txt).
   uint8_t* wire_out = nullptr;
   E_TRY(b, hipHostGetDevicePointer((void**)&wire_out, e.wire.p, 0));
   E_TRY(b, e.d_off.ensure((F + 1) * sizeof(uint64_t)));

@@ -130,7 +130,7 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
       if (fl & DF_SEG) break;
     }
   }
-  sm.S[s] = parallel && any_call ? (uint64_t)srel + DEFL_PAD : 0;
+  sm.S[s] = parallel && any_call ? r16((uint64_t)srel + DEFL_PAD) : 0;
   sm.O[s] = orel;
   sm.Y[s] = yrel;
   sm.C[s] = chunks;
@@ -175,51 +175,84 @@ __global__ __launch_bounds__(1024) void k_defl_scan(DeflArgs a) {
 }
 
 // ------------------------------------------------------------------ k_defl_prep
-// link pass of one segment, wave 0: strings [p_begin, p_last] in position order.  Each
-// group of 64 consecutive strings reads the last position of its hash (hpos), then atomicMax
-// leaves the group's last occurrence there; a string whose hash repeats inside the group
-// takes its predecessor from the group (peeled by rank), all others the value read.
+__device__ inline uint32_t load_u32u(const uint8_t* p) {
+  uint32_t v;
+  __builtin_memcpy(&v, p, 4);   // unaligned global load
+  return v;
+}
+
+// link pass of one segment, wave 0: strings [p_begin, p_last] in position order, 64 a
+// group, 8 groups a batch (the batch's stream words are loaded first and its links stored
+// last: a store before a load would hold the load, loads and stores sharing vmcnt).
+// A group's lanes atomicMax their position into the hash's LDS entry (hpos) and take the
+// value returned, the last position of the hash before them; a lane that sees a position
+// of its own group shares its hash inside the group, and such groups take their
+// predecessors by rank (peeled), or from the lane before for a run of one hash.
+constexpr int LINK_BATCH = 8;
+
+// a group with a hash that repeats inside it (kept out of line: rare): predecessors by rank
+__device__ __noinline__ int32_t link_repeats(int32_t* hpos, uint32_t h, int32_t p, bool part, int32_t g, int32_t r) {
+  const int lane = threadIdx.x & 63;
+  if (part && r < g) hpos[h] = r;   // the first lane of each hash saw the value before the group
+  const int32_t old = part ? hpos[h] : HNONE;
+  if (part) atomicMax(&hpos[h], p);
+  int32_t M = part ? hpos[h] : 0;
+  int32_t pr = old;
+  const uint64_t pm = __ballot(part);
+  const uint32_t h0 = __shfl(h, __builtin_ctzll(pm));
+  if (__ballot(part && h == h0) == pm) {   // one hash for the whole group (a run)
+    const bool prev_part = lane > 0 && ((pm >> (lane - 1)) & 1);
+    return prev_part ? p - 1 : old;
+  }
+  const bool top0 = part && M == p;
+  bool act = part;
+  while (__ballot(act)) {
+    const bool is_top = act && M == p;
+    const bool rem = act && !is_top;
+    if (act) hpos[h] = old;
+    if (rem) atomicMax(&hpos[h], p);
+    const int32_t M2 = act ? hpos[h] : 0;
+    if (is_top) pr = M2;
+    act = rem;
+    M = M2;
+  }
+  if (top0) hpos[h] = p;
+  return pr;
+}
 __device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint16_t* prev, int32_t p_begin,
                           int32_t p_last, int32_t nil_pos, bool persist, int32_t base_final) {
   const int lane = threadIdx.x & 63;
-  for (int32_t g = p_begin; g <= p_last; g += 64) {
-    const int32_t p = g + lane;
-    const bool valid = p <= p_last;
-    const bool part = valid && p != nil_pos;   // window index 0 of a new deflater is NIL
-    uint32_t h = 0;
-    if (valid) h = zd::hash3(S[p], S[p + 1], S[p + 2]);
-    const int32_t old = part ? hpos[h] : HNONE;
-    if (part) atomicMax(&hpos[h], p);
-    int32_t M = part ? hpos[h] : 0;
-    int32_t pred = old;
-    const uint64_t dup = __ballot(part && M != p);
-    if (dup) {
-      const uint64_t pm = __ballot(part);
-      const uint32_t h0 = __shfl(h, __builtin_ctzll(pm));
-      if (__ballot(part && h == h0) == pm) {   // one hash for the whole group (a run)
-        const bool prev_part = lane > 0 && ((pm >> (lane - 1)) & 1);
-        pred = prev_part ? p - 1 : old;
-      } else {
-        const bool top0 = part && M == p;
-        bool act = part;
-        while (__ballot(act)) {
-          const bool is_top = act && M == p;
-          const bool rem = act && !is_top;
-          if (act) hpos[h] = old;
-          if (rem) atomicMax(&hpos[h], p);
-          const int32_t M2 = act ? hpos[h] : 0;
-          if (is_top) pred = M2;
-          act = rem;
-          M = M2;
-        }
-        if (top0) hpos[h] = p;
-      }
+  for (int32_t g0 = p_begin; g0 <= p_last; g0 += 64 * LINK_BATCH) {
+    uint32_t wv[LINK_BATCH];
+    int32_t pred[LINK_BATCH];
+#pragma unroll
+    for (int j = 0; j < LINK_BATCH; j++) {
+      const int32_t p = g0 + 64 * j + lane;
+      wv[j] = p <= p_last ? load_u32u(S + p) : 0;
     }
-    if (valid) {
-      link[p] = (uint16_t)((pred != HNONE && p - pred < zd::WSIZE) ? p - pred : 0);
-      if (persist) {
-        const int32_t v = pred != HNONE ? pred - base_final : 0;
-        prev[(uint32_t)(p - base_final) & zd::WMASK] = (uint16_t)(v > 0 ? v : 0);
+#pragma unroll
+    for (int j = 0; j < LINK_BATCH; j++) {
+      const int32_t g = g0 + 64 * j;
+      const int32_t p = g + lane;
+      const bool valid = p <= p_last;
+      const bool part = valid && p != nil_pos;   // window index 0 of a deflater is NIL
+      const uint32_t h = zd::hash3(wv[j] & 0xff, (wv[j] >> 8) & 0xff, (wv[j] >> 16) & 0xff);
+      int32_t r = HNONE;
+      if (part) r = atomicMax(&hpos[h], p);
+      int32_t pr = part ? r : HNONE;
+      if (__ballot(part && r >= g)) pr = link_repeats(hpos, h, p, part, g, r);   // a hash repeats in the group
+      pred[j] = pr;
+    }
+#pragma unroll
+    for (int j = 0; j < LINK_BATCH; j++) {
+      const int32_t p = g0 + 64 * j + lane;
+      if (p <= p_last) {
+        const int32_t pr = pred[j];
+        link[p] = (uint16_t)((pr != HNONE && p - pr < zd::WSIZE) ? p - pr : 0);
+        if (persist) {
+          const int32_t v = pr != HNONE ? pr - base_final : 0;
+          prev[(uint32_t)(p - base_final) & zd::WMASK] = (uint16_t)(v > 0 ? v : 0);
+        }
       }
     }
   }
@@ -246,10 +279,37 @@ __device__ void zero_hw(uint8_t* W, uint32_t& hw, uint32_t curr) {
   wave_mem_sync();
 }
 
+__device__ inline uint4 load16(const uint8_t* p) {
+  uint4 v;
+  __builtin_memcpy(&v, p, 16);   // unaligned global load
+  return v;
+}
+__device__ inline void store16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
+
+// dst[0, n) = src[0, n) by T threads from thread t (disjoint ranges): 16-B pieces, four
+// loads in flight before their stores
+__device__ void copy_pieces(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t t, uint32_t T) {
+  const uint32_t np = n >> 4;
+  for (uint32_t i0 = 0; i0 < np; i0 += T * 4) {
+    const uint32_t i_0 = i0 + t, i_1 = i_0 + T, i_2 = i_1 + T, i_3 = i_2 + T;
+    uint4 v0, v1, v2, v3;
+    if (i_0 < np) v0 = load16(src + 16 * (uint64_t)i_0);
+    if (i_1 < np) v1 = load16(src + 16 * (uint64_t)i_1);
+    if (i_2 < np) v2 = load16(src + 16 * (uint64_t)i_2);
+    if (i_3 < np) v3 = load16(src + 16 * (uint64_t)i_3);
+    if (i_0 < np) store16(dst + 16 * (uint64_t)i_0, v0);
+    if (i_1 < np) store16(dst + 16 * (uint64_t)i_1, v1);
+    if (i_2 < np) store16(dst + 16 * (uint64_t)i_2, v2);
+    if (i_3 < np) store16(dst + 16 * (uint64_t)i_3, v3);
+  }
+  for (uint32_t i = (np << 4) + t; i < n; i += T) dst[i] = src[i];
+}
 __device__ void wave_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
-  const int lane = threadIdx.x & 63;
-  for (uint32_t i = lane; i < n; i += 64) dst[i] = src[i];
+  copy_pieces(dst, src, n, threadIdx.x & 63, 64);
   wave_mem_sync();
+}
+__device__ void block_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
+  copy_pieces(dst, src, n, threadIdx.x, blockDim.x);
 }
 
 // window walk of one segment, wave 1: zlib's window image through the segment's calls
@@ -339,14 +399,13 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
     const int32_t seg_end = (int32_t)(fl_.s_rel + fl_.len);
     const int32_t base_final = seg_end - (int32_t)fs.sw_final;
     // 1. the stream: history, then the frames' bytes
-    if (!fresh)
-      for (uint32_t i = tid; i < H; i += blockDim.x) S[DEFL_HIST - H + i] = W[strstart0 - H + i];
+    if (!fresh) block_copy(S + DEFL_HIST - H, W + strstart0 - H, H);
     for (uint32_t j = c0; j < c_end; j++) {
       if ((a.fflags[j] & DF_KIND) != PMD_CALL) continue;
       const DeflFrame f = a.ff[j];
-      const uint8_t* src = a.payload + a.desc[j].payload_off;
-      for (uint32_t i = tid; i < f.len; i += blockDim.x) S[f.s_rel + i] = src[i];
+      block_copy(S + f.s_rel, a.payload + a.desc[j].payload_off, f.len);
     }
+    __syncthreads();
     // 2. links of the hashed history strings (zlib's prev[]); the hash heads
     if (!fresh)
       for (uint32_t p = DEFL_HIST - H + tid; p < DEFL_HIST - ins0; p += blockDim.x) {
@@ -478,12 +537,22 @@ __device__ inline void fast_result(const FastWalk& w, const zd::Cfg& c, uint32_t
 }
 
 __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
+  // a chunk's results are kept in LDS and written at its end: a global store would make
+  // every later load of the wave wait for it (loads and stores share vmcnt)
+  __shared__ uint2 rs[DEFL_CH > DEFL_TAILN ? DEFL_CH : DEFL_TAILN];
   Sums sm(a);
   const uint64_t total = sm.C[a.n_sessions];
   const zd::Cfg cfg = zd::level_cfg(a.level);
   const uint32_t lane = threadIdx.x;
   const uint64_t lt_mask = (1ull << lane) - 1;
-  for (uint64_t c = blockIdx.x; c < total; c += gridDim.x) {
+  // XCD-aware order: workgroups are dealt round-robin to the 8 XCDs; XCD x takes the x-th
+  // eighth of the chunk list (a run of whole sessions), so the waves sharing an L2 walk the
+  // same sessions' streams and links
+  const uint32_t xcd = blockIdx.x & 7, g8 = gridDim.x >> 3;
+  const uint64_t per_xcd = (total + 7) >> 3;
+  for (uint64_t L = blockIdx.x >> 3; L < per_xcd; L += g8) {
+    const uint64_t c = xcd * per_xcd + L;
+    if (c >= total) break;
     const uint64_t e = a.chunks[c];
     const uint32_t k = (uint32_t)e, ci = (uint32_t)(e >> 32) & 0x7fffffffu;
     const bool var = (e >> 63) != 0;
@@ -514,8 +583,7 @@ __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
         if (fin) {
           uint32_t full, quarter;
           fast_result(w, cfg, d0, &full, &quarter);
-          res[2 * (uint64_t)p] = full;
-          res[2 * (uint64_t)p + 1] = quarter;
+          rs[p - p0] = make_uint2(full, quarter);
         }
         const uint64_t m = __ballot(fin);
         if (m) {
@@ -536,33 +604,101 @@ __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
     for (uint32_t p = (pf > p0 ? pf : p0) + lane; p < p1; p += 64) {
       uint32_t full, quarter;
       zd::match_at(by, LinkAcc{link}, p, end, cfg, &full, &quarter);
-      if (var) {
-        uint32_t* t = a.tres + ((uint64_t)k * DEFL_TAILN + (p - tstart)) * 2;
-        t[0] = full;
-        t[1] = quarter;
-      } else {
-        res[2 * (uint64_t)p] = full;
-        res[2 * (uint64_t)p + 1] = quarter;
-      }
+      rs[p - p0] = make_uint2(full, quarter);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    uint2* dst = var ? (uint2*)(a.tres + ((uint64_t)k * DEFL_TAILN + (p0 - tstart)) * 2) : (uint2*)(res + 2 * (uint64_t)p0);
+    for (uint32_t i = lane; i < p1 - p0; i += 64) dst[i] = rs[i];
+    __builtin_amdgcn_wave_barrier();
   }
 }
 
 // ------------------------------------------------------------------ k_defl_parse
-struct ResAcc {
-  const uint32_t* res;   // session base, indexed by stream position
+// The parse lane's reads come through register windows (8 positions of results, 16 stream
+// bytes) and its symbols through a 32-word LDS ring flushed in bursts: a global store in
+// the loop would hold every later load of the wave until it completed (shared vmcnt).
+struct ResWin {
+  const uint4* res;      // session base: 2 positions a uint4
   const uint32_t* tres;  // the frame's tail results
   uint32_t tstart;
-  __device__ void operator()(uint32_t p, int variant, uint32_t* f, uint32_t* q) const {
+  uint32_t wbase;
+  uint4 w0, w1, w2, w3;  // positions wbase .. wbase + 7
+  __device__ void operator()(uint32_t p, int variant, uint32_t* f, uint32_t* q) {
     if (variant && p >= tstart) {
       const uint32_t* t = tres + 2 * (p - tstart);
       *f = t[0];
       *q = t[1];
-    } else {
-      const uint32_t* r = res + 2 * (uint64_t)p;
-      *f = r[0];
-      *q = r[1];
+      return;
     }
+    const uint32_t b = p & ~7u;
+    if (b != wbase) {
+      wbase = b;
+      const uint4* r = res + (b >> 1);
+      w0 = r[0];
+      w1 = r[1];
+      w2 = r[2];
+      w3 = r[3];
+    }
+    const uint32_t i = p & 7;   // component selects only: an aggregate select would live in scratch
+    const bool o = i & 1, b1 = i & 2, b2 = i & 4;
+    const uint32_t ax = o ? w0.z : w0.x, ay = o ? w0.w : w0.y;
+    const uint32_t bx = o ? w1.z : w1.x, by_ = o ? w1.w : w1.y;
+    const uint32_t cx = o ? w2.z : w2.x, cy = o ? w2.w : w2.y;
+    const uint32_t dx = o ? w3.z : w3.x, dy = o ? w3.w : w3.y;
+    const uint32_t lx = b1 ? bx : ax, ly = b1 ? by_ : ay, hx = b1 ? dx : cx, hy = b1 ? dy : cy;
+    *f = b2 ? hx : lx;
+    *q = b2 ? hy : ly;
+  }
+};
+struct ByteWin {
+  const uint8_t* S;
+  uint32_t wbase;
+  uint4 w;
+  __device__ uint32_t operator()(uint32_t p) {
+    const uint32_t b = p & ~15u;
+    if (b != wbase) {
+      wbase = b;
+      w = *(const uint4*)(S + b);
+    }
+    const uint32_t i = p & 15;
+    const uint32_t lo = (i & 4) ? w.y : w.x, hi = (i & 4) ? w.w : w.z;
+    const uint32_t x = (i & 8) ? hi : lo;
+    return (x >> (8 * (i & 3))) & 0xff;
+  }
+};
+constexpr uint32_t SYM_RING = 32;
+struct SymStage {
+  uint32_t* ring;   // LDS: word j of this lane at ring[j * 64]
+  uint32_t* dst;    // the frame's symbol region
+  uint32_t n;       // symbols of the frame so far
+  uint32_t staged;
+  __device__ void flush() {
+    uint32_t* d = dst + (n - staged);
+    for (uint32_t j = 0; j < staged; j++) d[j] = ring[j * 64];
+    staged = 0;
+  }
+  __device__ void put(uint32_t v) {
+    ring[staged * 64] = v;
+    staged++;
+    n++;
+    if (staged == SYM_RING) flush();
+  }
+  __device__ void block_done() { flush(); }
+};
+// the parse's block sink: one DeflBlock slot a block zlib flushes
+struct BlockSink {
+  DeflBlock* blk;
+  uint64_t sym_at;   // index of the frame's first symbol in the symbol buffers
+  uint32_t nb, done;
+  __device__ void operator()(uint32_t nsym, uint32_t stored_s, uint32_t stored_len, bool stored_ok) {
+    DeflBlock* b = blk + nb++;
+    b->sym0 = sym_at + done;
+    b->nsym = nsym;
+    b->stored_s = stored_s;
+    b->stored_len = stored_len;
+    b->stored_ok = stored_ok ? 1 : 0;
+    done += nsym;
   }
 };
 struct SBytes {
@@ -589,25 +725,10 @@ __device__ void pass_or_empty(const DeflArgs& a, uint32_t k, uint32_t fl, uint64
   a.out_desc[k] = o;
 }
 
-// the parse's block sink: one DeflBlock slot a block zlib flushes
-struct BlockSink {
-  DeflBlock* blk;
-  const uint32_t* sym_base;
-  uint32_t nb;
-  __device__ void operator()(const uint32_t* sym, uint32_t nsym, uint32_t stored_s, uint32_t stored_len,
-                             bool stored_ok) {
-    DeflBlock* b = blk + nb++;
-    b->sym0 = (uint64_t)(sym - sym_base);
-    b->nsym = nsym;
-    b->stored_s = stored_s;
-    b->stored_len = stored_len;
-    b->stored_ok = stored_ok ? 1 : 0;
-  }
-};
-
 // lane per frame: deflate_slow's control flow over the match results; the symbols of
-// every block and its stored range go to the frame's block slots (k_defl_trees, k_defl_emit)
+// every block and its stored range go to the frame's block slots (k_defl_hist/trees/emit)
 __global__ __launch_bounds__(64) void k_defl_parse(DeflArgs a) {
+  __shared__ uint32_t ring[SYM_RING * 64];
   Sums sm(a);
   const uint32_t tid = blockIdx.x * blockDim.x + threadIdx.x;
   if (tid >= a.n_lanes) return;
@@ -622,21 +743,50 @@ __global__ __launch_bounds__(64) void k_defl_parse(DeflArgs a) {
     if (a.level == 0) continue;   // stored framing: k_defl_emit
     const uint64_t soff = sm.S[f.sess];
     const uint32_t end = f.s_rel + f.len;
-    ResAcc ra{a.res + 2 * soff, a.tres + (uint64_t)k * DEFL_TAILN * 2,
-              end - f.s_rel > DEFL_TAILN ? end - DEFL_TAILN : f.s_rel};
+    ResWin ra{(const uint4*)(a.res + 2 * soff), a.tres + (uint64_t)k * DEFL_TAILN * 2,
+              end - f.s_rel > DEFL_TAILN ? end - DEFL_TAILN : f.s_rel, ~0u, {}, {}, {}, {}};
+    ByteWin by{a.S + soff, ~0u, {}};
     zd::CallGeom g{f.start_w, (uint8_t)((fl & DF_START_SLID) ? 1 : 0)};
     DeflBlock* blk = a.blocks + sm.B[f.sess] + f.blk_rel;
-    BlockSink sink{blk, a.sym, 0};
-    const bool tail = zd::parse_call(ra, SBytes{a.S + soff}, f.s_rel, f.len, g, cfg,
-                                     a.sym + sm.Y[f.sess] + a.fsym[k], true, sink);
+    const uint64_t sym_at = sm.Y[f.sess] + a.fsym[k];
+    SymStage sw{ring + threadIdx.x, a.sym + sym_at, 0, 0};
+    BlockSink sink{blk, sym_at, 0, 0};
+    const bool tail = zd::parse_call(ra, by, f.s_rel, f.len, g, cfg, sw, sink);
     for (uint32_t b = sink.nb; b < defl_blk_cap(f.len); b++) blk[b].nsym = 0;
     a.ftail[k] = tail ? 1 : 0;
     a.ff[k].nblk = sink.nb;
   }
 }
 
-// lane per block, the block's TreeWork in LDS (32 lanes a workgroup): frequencies, the
-// three Huffman trees exactly as zlib's heap builds them, the block type and its size
+// workgroup per block slot: the block's symbol frequencies (LDS atomics)
+__global__ __launch_bounds__(256) void k_defl_hist(DeflArgs a) {
+  __shared__ uint32_t cnt[zd::L_CODES + zd::D_CODES];
+  Sums sm(a);
+  const uint64_t total = sm.B[a.n_sessions];
+  for (uint64_t i = blockIdx.x; i < total; i += gridDim.x) {
+    DeflBlock* b = a.blocks + i;
+    const uint32_t nsym = b->nsym;
+    if (nsym == 0) continue;
+    for (uint32_t j = threadIdx.x; j < (uint32_t)(zd::L_CODES + zd::D_CODES); j += 256) cnt[j] = 0;
+    __syncthreads();
+    const uint32_t* sy = a.sym + b->sym0;
+    for (uint32_t j = threadIdx.x; j < nsym; j += 256) {
+      const uint32_t v = sy[j], dist = v >> 8, lc = v & 255;
+      if (dist == 0) {
+        atomicAdd(&cnt[lc], 1u);
+      } else {
+        atomicAdd(&cnt[zd::len_code((int)lc) + 257], 1u);
+        atomicAdd(&cnt[zd::L_CODES + zd::dist_code((int)dist - 1)], 1u);
+      }
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < (uint32_t)(zd::L_CODES + zd::D_CODES); j += 256) b->freq[j] = (uint16_t)cnt[j];
+    __syncthreads();
+  }
+}
+
+// lane per block, the block's TreeWork in LDS (32 lanes a workgroup): the three Huffman
+// trees exactly as zlib's heap builds them, the block type and its size
 __global__ __launch_bounds__(32) void k_defl_trees(DeflArgs a) {
   __shared__ zd::TreeWork tws[32];
   Sums sm(a);
@@ -647,8 +797,8 @@ __global__ __launch_bounds__(32) void k_defl_trees(DeflArgs a) {
     const uint32_t nsym = b->nsym;
     if (nsym == 0) continue;
     zd::init_block(t);
-    const uint32_t* sy = a.sym + b->sym0;
-    for (uint32_t j = 0; j < nsym; j++) zd::tally(t, sy[j]);
+    for (int n = 0; n < zd::L_CODES; n++) t->lfc[n] = (uint16_t)(b->freq[n] + (n == zd::END_BLOCK ? 1 : 0));
+    for (int n = 0; n < zd::D_CODES; n++) t->dfc[n] = b->freq[zd::L_CODES + n];
     uint32_t bits;
     int max_blindex;
     const int type = zd::plan_block(t, b->stored_ok != 0, b->stored_len, &bits, &max_blindex);
@@ -1041,10 +1191,15 @@ void launch_defl_prep(const DeflArgs& a, hipStream_t s) {
 }
 void launch_defl_match(const DeflArgs& a, hipStream_t s) {
   uint64_t g = a.chunk_cap < 262144 ? a.chunk_cap : 262144;
-  hipLaunchKernelGGL(k_defl_match, dim3((uint32_t)(g ? g : 1)), dim3(64), 0, s, a);
+  g = (g + 7) & ~7ull;   // a multiple of the 8 XCDs (k_defl_match's chunk order)
+  hipLaunchKernelGGL(k_defl_match, dim3((uint32_t)(g ? g : 8)), dim3(64), 0, s, a);
 }
 void launch_defl_parse(const DeflArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_defl_parse, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+}
+void launch_defl_hist(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
+  hipLaunchKernelGGL(k_defl_hist, dim3((uint32_t)(n_blocks < 262144 ? (n_blocks ? n_blocks : 1) : 262144)), dim3(256), 0,
+                     s, a);
 }
 void launch_defl_trees(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
   uint64_t g = (n_blocks + 31) / 32;

@@ -754,14 +754,14 @@ struct CallGeom {
 // deflate_slow over one frame from the per-position results.  res(s, variant, &full,
 // &quarter) gives the packed pair at stream position s; variant 1 = after a slide in the
 // frame's tail (the window bytes past the end differ).  byte(p) is the stream byte (the
-// literals).  Every block zlib would flush goes to sink(sym, nsym, stored_s, stored_len,
-// stored_ok): its symbols, and for the stored choice the stream range it covers (stored_ok:
-// zlib's block_start >= 0).  With sym_advance the next block's symbols follow (sym +=
-// nsym), else the buffer is reused.  The caller adds the sync marker.  Returns whether the
-// window slid inside the frame's tail (the next call then starts without a slide).
-template <class RES, class BYTE, class SINK>
-ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t len, CallGeom g, Cfg c,
-                      uint32_t* sym, bool sym_advance, SINK& sink) {
+// literals).  Symbols go to symw.put(v); every block zlib would flush is closed by
+// symw.block_done() and handed to sink(nsym, stored_s, stored_len, stored_ok): its symbol
+// count, and for the stored choice the stream range it covers (stored_ok: zlib's
+// block_start >= 0).  The caller adds the sync marker.  Returns whether the window slid
+// inside the frame's tail (the next call then starts without a slide).
+template <class RES, class BYTE, class SYMW, class SINK>
+ZD_FN bool parse_call(RES&& res, BYTE&& byte, uint32_t start, uint32_t len, CallGeom g, Cfg c, SYMW& symw,
+                      SINK& sink) {
     uint32_t sw = g.start_w;                 // strstart, window index
     uint32_t s = start;                      // strstart, stream position
     uint32_t more = WINDOW_SIZE - sw;
@@ -776,8 +776,8 @@ ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t
     bool slid_here = g.start_slid != 0;      // a slide put strstart at MAX_DIST at this loop top
     uint32_t nsym = 0;
     auto flush = [&](uint32_t cur_s, int32_t cur_w) {
-        sink(sym, nsym, block_start_s, cur_s - block_start_s, block_start_w >= 0);
-        if (sym_advance) sym += nsym;
+        symw.block_done();
+        sink(nsym, block_start_s, cur_s - block_start_s, block_start_w >= 0);
         block_start_s = cur_s;
         block_start_w = cur_w;
         nsym = 0;
@@ -827,7 +827,8 @@ ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t
         }
         slid_here = false;
         if (prev_length >= (uint32_t)MIN_MATCH && match_length <= prev_length) {
-            sym[nsym++] = sym_match(s - 1 - prev_match, prev_length - MIN_MATCH);
+            symw.put(sym_match(s - 1 - prev_match, prev_length - MIN_MATCH));
+            nsym++;
             uint32_t adv = prev_length - 1;   // strstart moves to the match end
             s += adv;
             sw += adv;
@@ -835,7 +836,8 @@ ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t
             match_length = MIN_MATCH - 1;
             if (nsym == (uint32_t)SYM_END) flush(s, (int32_t)sw);
         } else if (match_available) {
-            sym[nsym++] = sym_lit(byte(s - 1));
+            symw.put(sym_lit(byte(s - 1)));
+            nsym++;
             if (nsym == (uint32_t)SYM_END) flush(s, (int32_t)sw);
             s++;
             sw++;
@@ -845,21 +847,32 @@ ZD_FN bool parse_call(const RES& res, const BYTE& byte, uint32_t start, uint32_t
             sw++;
         }
     }
-    if (match_available) sym[nsym++] = sym_lit(byte(s - 1));
+    if (match_available) {
+        symw.put(sym_lit(byte(s - 1)));
+        nsym++;
+    }
     if (nsym) flush(s, (int32_t)sw);
     return tail_slid;
 }
 
-// The host form of the sink: _tr_flush_block right away (trees, bits), as zlib does.
+// The host forms: a symbol buffer reused per block, and a sink that runs _tr_flush_block
+// right away (trees, bits), as zlib does.
+struct SymBuf {
+    uint32_t* buf;
+    uint32_t n;
+    ZD_MFN void put(uint32_t v) { buf[n++] = v; }
+    ZD_MFN void block_done() {}
+};
 struct FlushNow {
     TreeWork* t;
     BitWriter* bw;
     const uint8_t* S;   // stream bytes (stored blocks)
-    ZD_MFN void operator()(const uint32_t* sym, uint32_t nsym, uint32_t stored_s, uint32_t stored_len,
-                           bool stored_ok) {
+    SymBuf* sb;
+    ZD_MFN void operator()(uint32_t nsym, uint32_t stored_s, uint32_t stored_len, bool stored_ok) {
         init_block(t);
-        for (uint32_t i = 0; i < nsym; i++) tally(t, sym[i]);
-        flush_block(t, bw, ArraySyms{sym}, nsym, stored_ok ? S + stored_s : nullptr, stored_len);
+        for (uint32_t i = 0; i < nsym; i++) tally(t, sb->buf[i]);
+        flush_block(t, bw, ArraySyms{sb->buf}, nsym, stored_ok ? S + stored_s : nullptr, stored_len);
+        sb->n = 0;
     }
 };
 

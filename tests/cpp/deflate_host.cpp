@@ -204,8 +204,9 @@ void decomp_segment(Session& S, int level, std::vector<Call>& calls) {
             }
         };
         BitWriter bw{calls[k].out, 0, 0, 0};
-        FlushNow sink{&tw, &bw, Sb.data()};
-        last_tail = parse_call(res, PlainBytes{Sb.data()}, start, calls[k].len, geom[k], c, sym.data(), false, sink);
+        SymBuf sbuf{sym.data(), 0};
+        FlushNow sink{&tw, &bw, Sb.data(), &sbuf};
+        last_tail = parse_call(res, PlainBytes{Sb.data()}, start, calls[k].len, geom[k], c, sbuf, sink);
         sync_marker(&bw);
         calls[k].out_len = bw.pos;
     }
