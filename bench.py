@@ -1408,7 +1408,8 @@ def e2e_loop_line(pctx, rounds, wire_bytes, F, n_s):
     socket reads as native_batcher (one 64 KiB read per session an iteration), wire
     bytes of all iterations / the time from the first read to the last delivery."""
     import numpy as np
-    from snf4j_amd.loop import LoopBatcher, SelectorLoop, run_until_idle
+    from benchsupport.selector import SelectorLoop, run_until_idle
+    from snf4j_amd.loop import LoopBatcher
     got = {"wire": 0, "frames": 0}
 
     def deliver(_sid, views, _exc):

@@ -181,7 +181,9 @@ int wsg_close(wsg_ctx* ctx);
  *                            every level (the parallel form for levels 4-9 is the default; tests)
  *   WSG_TUNE_AGG_FOLD_MAX    aggregator plans of up to this many 512-frame blocks fold the block
  *                            sums in k_agg_b / k_agg_c (default: as many as LDS allows, 3,072);
- *                            larger ones run k_agg_scan (0 forces it: the tests' way to reach it) */
+ *                            larger ones run k_agg_scan (0 forces it: the tests' way to reach it)
+ *   WSG_TUNE_STAGE_FAIL      n > 0: the n-th stage-chain step a batcher on this context begins from now
+ *                            fails as a device error would (tests of the error path) */
 enum {
     WSG_TUNE_INFLATE_TOKENS = 1,
     WSG_TUNE_INFLATE_FAST = 2,
@@ -194,7 +196,8 @@ enum {
     WSG_TUNE_INFLATE_TABS = 9,
     WSG_TUNE_INFLATE_SPLIT = 10,
     WSG_TUNE_AGG_FOLD_MAX = 11,
-    WSG_TUNE_DEFLATE_SERIAL = 12
+    WSG_TUNE_DEFLATE_SERIAL = 12,
+    WSG_TUNE_STAGE_FAIL = 13
 };
 int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */
@@ -525,8 +528,18 @@ int wsg_enc_batcher_flush(wsg_enc_batcher* b, wsg_enc_view* out);
  * flight.  A session reset while its frames are in flight drops them from the view. */
 int wsg_enc_batcher_flush_async(wsg_enc_batcher* b);
 int wsg_enc_batcher_wait(wsg_enc_batcher* b, wsg_enc_view* out);
-/* slot `sid` for a new session: its queued frames are dropped, the close latch cleared */
+/* slot `sid` for a new session: its queued frames are dropped, the close latch cleared
+ * (and, with deflate on, a new deflater) */
 int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid);
+/* The "permessage-deflate-encoder" stage in front of the encoder for every session of the
+ * batcher: PerMessageDeflateEncoder(level, noContext) as PerMessageDeflateExtension.
+ * updateEncoders installs it (PerMessageDeflateExtension.java:303-313).  Each flush then
+ * compresses its frames on the device first — wsg_deflate_batch_device's rules and bytes
+ * (byte-identical to java.util.zip.Deflater), the deflater state and its window | head | prev
+ * kept per session on the device (WSG_DEFLATE_SESSION_BYTES each: n_sessions x 192 KiB of
+ * HBM) — and frames what it hands on, still without a host synchronisation (the workspace is
+ * sized from the frames' lengths).  Once, before the first add; level 0-9. */
+int wsg_enc_batcher_set_deflate(wsg_enc_batcher* b, int level, int no_context);
 /* as wsg_batcher_ticket / _await / _reserve, for the encode batcher (max_payload:
  * payload bytes a flush may hold; reserve: WSG_API_ERANGE with a flush in flight) */
 uint64_t wsg_enc_batcher_ticket(wsg_enc_batcher* b);

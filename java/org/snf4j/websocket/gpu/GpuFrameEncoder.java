@@ -16,6 +16,14 @@
  * writes it right before session.close()), then latches (:71-76).  Masks come
  * from a java.util.Random as FrameEncoder.RANDOM draws them (:43,111).
  *
+ * With a GPU permessage-deflate-encoder in front (GpuPerMessageDeflateExtension puts a
+ * GpuPerMessageDeflateEncoder under "permessage-deflate-encoder" and attaches it here),
+ * compression is a stage of the same device batch (wsg_enc_batcher_set_deflate): the
+ * marker hands frames on unchanged and every data frame (TEXT / BINARY / CONTINUATION,
+ * whatever its size: each one moves the session's deflater or its compressing flag,
+ * PerMessageDeflateEncoder.java:83-99) is queued; control frames, which the deflate
+ * encoder passes through, keep the threshold rule above.
+ *
  * Write futures: for a queued frame encode() returns with `out` empty, and snf4j's
  * EncodeTask completes the write's future at once (EncodeTask.java:380-381), before
  * the bytes are encoded or written.  So session.write(frame).sync() on a frame at or
@@ -60,6 +68,8 @@ public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer>, IEventDrive
 	private IStreamSession session;
 	/** FrameEncoder.closed (:71-76) */
 	private boolean closed;
+	/** the batched permessage-deflate-encoder in front of this encoder, or null */
+	private GpuPerMessageDeflateEncoder deflate;
 	private boolean released;
 
 	public GpuFrameEncoder(boolean clientMode, WsgBatcher batcher, int deviceThreshold) {
@@ -87,6 +97,17 @@ public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer>, IEventDrive
 		return session;
 	}
 
+	/**
+	 * The session's permessage-deflate-encoder runs in this encoder's device batch (called
+	 * when the extension installs it, before any frame of the session is encoded).
+	 */
+	void attachDeflate(GpuPerMessageDeflateEncoder d) {
+		if (sid >= 0 || deflate != null)
+			return;  // frames already went out without it: the marker keeps its reference encoder
+		deflate = d;
+		d.setBatched();
+	}
+
 	@Override
 	public void encode(ISession session, Frame frame, List<ByteBuffer> out) throws Exception {
 		this.session = (IStreamSession) session;
@@ -100,12 +121,13 @@ public class GpuFrameEncoder implements IEncoder<Frame, ByteBuffer>, IEventDrive
 			return;
 		}
 		boolean queued = sid >= 0 && batcher.hasQueued(this);
-		if (frame.getPayloadLength() < deviceThreshold && !queued) {
+		boolean data = !frame.getOpcode().isControl();
+		if (frame.getPayloadLength() < deviceThreshold && !queued && !(deflate != null && data)) {
 			small.encode(session, frame, out);
 			return;
 		}
 		if (sid < 0)
-			sid = batcher.registerEncoder(this, clientMode);
+			sid = batcher.registerEncoder(this, clientMode, deflate);
 		batcher.enqueueEncode(this, frame, clientMode ? RANDOM.nextInt() : 0);
 	}
 

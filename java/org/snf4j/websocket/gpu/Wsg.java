@@ -180,6 +180,9 @@ final class Wsg {
 
 	static native int encBatcherReserve(long batcher, long maxFrames, long maxPayload);
 
+	/** wsg_enc_batcher_set_deflate: PerMessageDeflateEncoder(level, noContext) in front of the encoder, on the device. */
+	static native int encBatcherSetDeflate(long batcher, int level, boolean noContext);
+
 	static native long encBatcherTicket(long batcher);
 
 	static native long encBatcherAwait(long batcher, long seen, long timeoutMs);

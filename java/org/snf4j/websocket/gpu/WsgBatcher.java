@@ -169,7 +169,11 @@ public final class WsgBatcher {
 		}
 	}
 
-	/** One native encode batcher (wsg_enc_batcher_open takes the client mode). */
+	/**
+	 * One native encode batcher: wsg_enc_batcher_open takes the client mode, and a batcher
+	 * with the permessage-deflate-encoder stage (wsg_enc_batcher_set_deflate) one
+	 * PerMessageDeflateEncoder(level, noContext) configuration.
+	 */
 	private final class EncNative {
 		final long handle;
 		final GpuFrameEncoder[] slots;
@@ -179,10 +183,12 @@ public final class WsgBatcher {
 		long serial = 1;  // the open batch's number
 		final ArrayDeque<EncFlush> inflight = new ArrayDeque<EncFlush>();
 
-		EncNative(boolean clientMode) {
+		EncNative(boolean clientMode, GpuPerMessageDeflateEncoder deflate) {
 			handle = Wsg.encBatcherOpen(ctx, clientMode, maxSessions);
 			if (handle == 0)
 				throw new IllegalStateException("wsg_enc_batcher_open: " + Wsg.lastError(ctx));
+			if (deflate != null && Wsg.encBatcherSetDeflate(handle, deflate.level, deflate.noContext) != 0)
+				throw new IllegalStateException("wsg_enc_batcher_set_deflate: " + Wsg.lastError(ctx));
 			if (Wsg.encBatcherReserve(handle, maxFrames, maxWireLen) != 0)
 				throw new IllegalStateException("wsg_enc_batcher_reserve: " + Wsg.lastError(ctx));
 			slots = new GpuFrameEncoder[maxSessions];
@@ -241,7 +247,8 @@ public final class WsgBatcher {
 	private final int maxSessions;
 	private final long maxFrames, maxWireLen;
 	private final Map<Cfg, Native> natives = new HashMap<Cfg, Native>();
-	private final EncNative[] encNatives = new EncNative[2];
+	/* by encNativeIndex: client mode, then no deflate stage or its level and noContext */
+	private final EncNative[] encNatives = new EncNative[2 * 21];
 	private boolean flushScheduled;
 	private final Completion completion;
 	private final ByteBuffer[] views = new ByteBuffer[5];
@@ -427,10 +434,20 @@ public final class WsgBatcher {
 
 	/* ------------------------------------------------------------------ encode side */
 
-	synchronized int registerEncoder(GpuFrameEncoder e, boolean clientMode) {
-		int m = clientMode ? 1 : 0;
+	private static int encNativeIndex(boolean clientMode, GpuPerMessageDeflateEncoder deflate) {
+		int d = deflate == null ? 0 : 1 + 2 * deflate.level + (deflate.noContext ? 1 : 0);
+		return 2 * d + (clientMode ? 1 : 0);
+	}
+
+	/**
+	 * A session slot for an encoder (at its first queued frame), in a fresh state; with
+	 * deflate (the session's GPU permessage-deflate-encoder) a slot of the batcher running
+	 * that configuration, with a new deflater.
+	 */
+	synchronized int registerEncoder(GpuFrameEncoder e, boolean clientMode, GpuPerMessageDeflateEncoder deflate) {
+		int m = encNativeIndex(clientMode, deflate);
 		if (encNatives[m] == null)
-			encNatives[m] = new EncNative(clientMode);
+			encNatives[m] = new EncNative(clientMode, deflate);
 		EncNative n = encNatives[m];
 		for (int i = 0; i < maxSessions; ++i) {
 			int sid = (n.next + i) % maxSessions;

@@ -496,6 +496,13 @@ JNIEXPORT jlong JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherAwait(JNIEnv*
     return (jlong)wsg_enc_batcher_await(ENC_BATCHER(b), (uint64_t)seen, (int64_t)timeout_ms);
 }
 
+JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherSetDeflate(JNIEnv* env, jclass c, jlong b,
+                                                                             jint level, jboolean no_context) {
+    (void)env;
+    (void)c;
+    return wsg_enc_batcher_set_deflate(ENC_BATCHER(b), (int)level, no_context ? 1 : 0);
+}
+
 JNIEXPORT jint JNICALL Java_org_snf4j_websocket_gpu_Wsg_encBatcherReserve(JNIEnv* env, jclass c, jlong b,
                                                                           jlong max_frames, jlong max_payload) {
     (void)env;

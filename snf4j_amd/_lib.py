@@ -162,6 +162,7 @@ def _load():
         "wsg_enc_batcher_ticket": ([p], u64),
         "wsg_enc_batcher_await": ([p, u64, i64], i64),
         "wsg_enc_batcher_reserve": ([p, u64, u64], i32),
+        "wsg_enc_batcher_set_deflate": ([p, i32, i32], i32),
         "wsg_set_tuning": ([p, i32, C.c_int64], i32),
         "wsg_device_policy_init": ([i32], i32),
         "wsg_device_for_loop": ([u64], i32),

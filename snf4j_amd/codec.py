@@ -642,6 +642,12 @@ class EncodeBatcher:
                                                  flags.ctypes.data, m.ctypes.data if m is not None else None,
                                                  ptrs.ctypes.data, lens.ctypes.data))
 
+    def set_deflate(self, compressionLevel: int, noContext: bool):
+        """PerMessageDeflateEncoder(compressionLevel, noContext) in front of the encoder for
+        every session (wsg_enc_batcher_set_deflate): each flush compresses on the device first."""
+        from ._lib import lib
+        self._check(lib.wsg_enc_batcher_set_deflate(self._h, int(compressionLevel), int(bool(noContext))))
+
     def reset_session(self, sid: int):
         from ._lib import lib
         self._check(lib.wsg_enc_batcher_session_reset(self._h, int(sid)))

@@ -80,6 +80,7 @@ struct wsg_ctx {
   DevBuf d_flags, d_fout, d_fsym, d_ff, d_fs, d_sums, d_S, d_link, d_res, d_tres, d_strips, d_ftail, d_chunks, d_sym, d_tw, d_ssym,
       d_blocks;
   int defl_serial = 0;               // WSG_TUNE_DEFLATE_SERIAL 1: zlib's loop per session at every level (tests)
+  int64_t stage_fail = 0;            // WSG_TUNE_STAGE_FAIL n: the n-th stage step from now fails (tests)
   // measurement / test switches (wsg_set_tuning; the defaults are the product)
   int infl_tokens = 1;               // WSG_TUNE_INFLATE_TOKENS 0: no lane pre-decode (serial decoder only)
   uint32_t infl_lanes = 262144;      // WSG_TUNE_INFLATE_LANES: k_infl_tok lanes at most
@@ -200,6 +201,7 @@ int ctx_device(wsg_ctx* c) { return c->device; }
 // the batcher's two-phase inflate applies (the pre-decode on, the split-lane decode off)
 bool ctx_inflate_two_phase(const wsg_ctx* c) { return c->infl_tokens && c->infl_split == 0; }
 uint8_t* ctx_async_payload(wsg_ctx* c) { return c->last_async_payload; }
+bool ctx_stage_fail(wsg_ctx* c) { return c->stage_fail > 0 && --c->stage_fail == 0; }
 }  // namespace ws
 
 extern "C" {
@@ -284,6 +286,7 @@ int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
       break;
     case WSG_TUNE_AGG_GRID: c->agg_grid = value < 1 ? 1u : (value > (1 << 24) ? (1u << 24) : (uint32_t)value); break;
     case WSG_TUNE_DEFLATE_SERIAL: c->defl_serial = value != 0; break;
+    case WSG_TUNE_STAGE_FAIL: c->stage_fail = value < 0 ? 0 : value; break;
     case WSG_TUNE_AGG_FOLD_MAX: c->agg_fold = value < 0 ? 0u : (value > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)value); break;
     default: return set_err(c, WSG_API_EINVAL, "unknown tuning key");
   }
@@ -1129,16 +1132,28 @@ int inflate_replay_phase(wsg_ctx* c, wsg_ctx* tokc, const uint32_t* tmap, int no
 }
 }  // namespace ws
 
-extern "C" {
-
+namespace ws {
 // ---------------------------------------------------------------- permessage-deflate encode
-int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
-                             const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
-                             uint64_t payload_len, wsg_deflate_state* state, uint8_t* session_mem, uint8_t* out,
-                             uint64_t out_cap, wsg_frame_desc* out_desc, uint64_t* out_total) {
-  if (!c || !out_total) return WSG_API_EINVAL;
+static inline uint64_t r16h(uint64_t x) { return (x + 15) & ~15ull; }
+
+void deflate_bounds_add(DeflBounds& b, uint32_t len) {
+  b.tot[0] += len;
+  b.tot[1] += r16h(len + ((len + 7) >> 3) + ((len + 63) >> 6) + 15);   // ZlibEncoder.deflateBound (java_bound)
+  b.tot[2] += (len + 3) & ~3u;
+  b.tot[3] += (len > 2 ? (len - 2 + DEFL_CH - 1) / DEFL_CH : 0) + 1;
+  b.tot[4] += defl_blk_cap(len);
+}
+void deflate_bounds_session(DeflBounds& b) { b.tot[0] += r16h(DEFL_HIST + DEFL_PAD) + 16; }
+
+// wsg_deflate_batch_device; with `bounds` the workspace is sized from them and nothing is read
+// back (the launches stay asynchronous), else from the plan's totals (one synchronisation)
+int deflate_launch(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                   const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                   wsg_deflate_state* state, uint8_t* session_mem, uint8_t* out, uint64_t out_cap,
+                   wsg_frame_desc* out_desc, const DeflBounds* bounds, uint64_t* out_total) {
+  if (!c) return WSG_API_EINVAL;
   if (level < 0 || level > 9) return set_err(c, WSG_API_EINVAL, "compression level is out of range");
-  *out_total = 0;
+  if (out_total) *out_total = 0;
   if (n_sessions == 0) return n_frames ? set_err(c, WSG_API_EINVAL, "frames without sessions") : WSG_API_OK;
   if (n_frames >= (1ull << 31)) return set_err(c, WSG_API_ERANGE, "too many frames in one batch (max 2^31 - 1)");
   HIP_TRY(c, hipSetDevice(c->device));
@@ -1171,18 +1186,20 @@ int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_fr
   a.fs = (DeflSess*)c->d_fs.p;
   a.sums = (uint64_t*)c->d_sums.p;
   a.ftail = (uint8_t*)c->d_ftail.p;
-  (void)payload_len;
   timed(c, K_DEFL_PLAN, [&] { launch_defl_plan(a, c->stream); });
-  // the regions' totals decide the workspace: read them back
   uint64_t tot[5];
-  for (int i = 0; i < 5; i++)
-    HIP_TRY(c, hipMemcpyAsync(&tot[i], a.sums + (uint64_t)i * (S + 1) + S, sizeof(uint64_t), hipMemcpyDeviceToHost,
-                              c->stream));
-  HIP_TRY(c, hipStreamSynchronize(c->stream));
+  if (bounds) {
+    for (int i = 0; i < 5; i++) tot[i] = bounds->tot[i];
+  } else {  // the regions' totals decide the workspace: read them back
+    for (int i = 0; i < 5; i++)
+      HIP_TRY(c, hipMemcpyAsync(&tot[i], a.sums + (uint64_t)i * (S + 1) + S, sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                c->stream));
+    HIP_TRY(c, hipStreamSynchronize(c->stream));
+  }
   if (tot[1] > out_cap)
     return set_err(c, WSG_API_ERANGE, "out_cap %llu below the batch's %llu slot bytes", (unsigned long long)out_cap,
                    (unsigned long long)tot[1]);
-  *out_total = tot[1];
+  if (out_total) *out_total = tot[1];
   const size_t twb = defl_treework_bytes();
   if (a.serial) {
     HIP_TRY(c, c->d_ssym.ensure(S * zd_lit_bufsize() * sizeof(uint32_t)));
@@ -1223,7 +1240,21 @@ int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_fr
   }
   timed(c, K_DEFL_EMIT, [&] { launch_defl_emit(a, c->stream); });
   timed(c, K_DEFL_FINAL, [&] { launch_defl_final(a, c->stream); });
+  HIP_TRY(c, hipGetLastError());
   return WSG_API_OK;
+}
+}  // namespace ws
+
+extern "C" {
+
+int wsg_deflate_batch_device(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                             const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                             uint64_t payload_len, wsg_deflate_state* state, uint8_t* session_mem, uint8_t* out,
+                             uint64_t out_cap, wsg_frame_desc* out_desc, uint64_t* out_total) {
+  if (!c || !out_total) return WSG_API_EINVAL;
+  (void)payload_len;
+  return ws::deflate_launch(c, level, no_context, desc, n_frames, session_first, n_sessions, payload, state,
+                            session_mem, out, out_cap, out_desc, nullptr, out_total);
 }
 
 int wsg_deflate_batch_host(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,

@@ -539,6 +539,8 @@ struct wsg_batcher {
   uint32_t threads = 8;
   std::unique_ptr<Pool> pool;           // threads - 1 workers (the caller is the last one)
   std::string err;
+  int stage_rc = 0;        // a deferred stage-chain error (stage_defer), reported by the next wait
+  std::string stage_msg;
   // stages after the decoder (wsg_batcher_set_stages), run on the device at wait()
   wsg_stage_cfg stages{};
   bool has_stages = false;
@@ -577,11 +579,25 @@ struct wsg_batcher {
   uint64_t tickets = 0;                 // flushes queued so far (flush t's ticket is t)
   std::shared_ptr<Notify> notify = std::make_shared<Notify>();
   uint64_t res_wire = 0, res_frames = 0;  // the sizes wsg_batcher_reserve was given
+  // inflate's first output region per session: 4 KiB + infl_ratio x its compressed bytes (a
+  // session that overflows runs again with a larger one); wsg_batcher_reserve_stages sets it
+  // from the caller's max_out_bytes (its expected expansion), 2..8
+  uint32_t infl_ratio = 8;
 };
 
 static int bset(wsg_batcher* b, int code, const char* msg) {
   if (b) b->err = msg ? msg : "";
   return code;
+}
+
+// A stage-chain step that flush_async or a feed runs on the side (advancing the chains of
+// flushes already queued) failed: that call did its own job, so it returns OK and the
+// error is kept for the next wsg_batcher_wait, which reports it.
+static void stage_defer(wsg_batcher* b, int rc) {
+  if (rc && !b->stage_rc) {
+    b->stage_rc = rc;
+    b->stage_msg = b->err;
+  }
 }
 
 #define B_TRY(b, expr)                                                           \
@@ -831,7 +847,7 @@ static int infl_begin(wsg_batcher* b, FlushSlot& f) {
     for (uint32_t k = j.cur.sf[s]; k < j.cur.sf[s + 1]; ++k) c += j.cur.desc[k].payload_len + 4;
     if (h.held_desc.empty() && j.cur.sf[s + 1] == j.cur.sf[s]) continue;
     j.todo.push_back(s);
-    j.cap[s] = al16(4096 + 8 * c);
+    j.cap[s] = al16(4096 + (uint64_t)b->infl_ratio * c);
   }
   if (j.tc >= 0 && hpos + 64 > f.dpay.n) B_TRY(b, hipEventSynchronize(j.tok_done));
   B_TRY(b, f.dpay.grow_keep(hpos + 64, f.pcap, st));
@@ -1089,6 +1105,7 @@ static int stage_aggregate(wsg_batcher* b, StageList& cur, uint64_t used) {
 // pre-decode of those frames launched on the flush's own context (it needs no inflater
 // state: it runs ahead of the previous flush's replay, while the host collects that one).
 static int stage_prep(wsg_batcher* b, FlushSlot& f, const wsg_session_result* res) {
+  if (ws::ctx_stage_fail(b->ctx)) return bset(b, WSG_API_EHIP, "injected stage failure (WSG_TUNE_STAGE_FAIL)");
   const uint32_t S = b->n;
   InflJob& j = f.ij;
   j.res.assign(res, res + S);
@@ -1490,17 +1507,22 @@ int wsg_batcher_feed_many(wsg_batcher* b, uint32_t n, const uint32_t* sids, cons
       cut[t] = i;
     }
     int side_rc = WSG_API_OK;
-    const std::function<void()> side = [&] { side_rc = stage_advance(b, true); };
+    const std::function<void()> side = [&] {  // (the only writer of b->err while the copies run)
+      try {
+        side_rc = stage_advance(b, true);
+      } catch (const std::exception& ex) {  // never unwind past the pool's run: the workers use these frames
+        side_rc = bset(b, WSG_API_ENOMEM, ex.what());
+      } catch (...) {
+        side_rc = bset(b, WSG_API_ENOMEM, "stage chain: unknown exception");
+      }
+    };
     const bool adv = b->has_stages && b->stage_early && b->feed_advance && !b->q.empty();
     b->pool->run(
         T, [&](uint32_t t) {
           for (uint32_t i = cut[t]; i < cut[t + 1]; ++i) region(i);
         },
         adv ? &side : nullptr);
-    if (side_rc) {
-      f.arena_len = pos;
-      return side_rc;
-    }
+    stage_defer(b, side_rc);
   }
   f.arena_len = pos;
   return WSG_API_OK;
@@ -1659,7 +1681,7 @@ int wsg_batcher_flush_async(wsg_batcher* b) {
     g.fo[i].clear();
     g.fb[i] = 0;
   }
-  if (b->has_stages && b->stage_early) return stage_advance(b, false);
+  if (b->has_stages && b->stage_early) stage_defer(b, stage_advance(b, false));  // (queued: OK from here on)
   return WSG_API_OK;
 }
 
@@ -1722,6 +1744,12 @@ int wsg_batcher_wait(wsg_batcher* b, wsg_batch_view* out) {
   b->q.pop_front();
   FlushSlot& f = b->fs[slot];
   B_TRY(b, hipEventSynchronize(f.done));
+  if (b->stage_rc) {  // a stage step run on the side failed since the last wait
+    const int rc = b->stage_rc;
+    b->stage_rc = 0;
+    b->err = b->stage_msg;
+    return rc;
+  }
   const uint32_t S = b->n;
   const wsg_session_state* st = (const wsg_session_state*)b->st.p;
   if (b->q.empty()) {  // the state after the last batch (else the newer batch owns the pinned copy)
@@ -1901,9 +1929,14 @@ int wsg_batcher_reserve_stages(wsg_batcher* b, uint64_t max_out_bytes, uint64_t 
   const uint64_t pcap = W + 16 * Fi + 16;            // the decoded payloads (flush_async's region)
   const uint64_t held = al16(W) + 16 * S;            // compressed frames of messages left open
   const uint64_t in_len = al16(pcap) + held;         // inflate's input: payloads and held frames
-  const uint64_t infl = S * (4096 + 16) + 8 * (in_len + 4 * F);  // stage_inflate's per-session regions
+  // the inflate regions follow the expansion the caller sized its output for (max_out_bytes
+  // over the wire bytes), not a fixed 8x: 8x of a 256 MB flush in each of the five slots
+  // was tens of GB of HBM reserved for output the caller never expects
+  const uint64_t ratio = std::min<uint64_t>(8, std::max<uint64_t>(2, (max_out_bytes + pcap - 1) / pcap));
+  b->infl_ratio = (uint32_t)ratio;
+  const uint64_t infl = b->stages.inflate ? S * (4096 + 16) + ratio * (in_len + 4 * F) : 0;
   const uint64_t maxo = std::max(max_out_bytes, pcap);
-  const uint64_t agg = al16(maxo + 16);
+  const uint64_t agg = b->stages.aggregate ? al16(maxo + 16) : 0;  // (the aggregator's output only)
   const uint64_t arena = in_len + infl + agg + 256;
   const uint64_t out = maxo + 16 * Fo + 32;          // the handler's bytes, a 16-B slot a frame
   const uint64_t copies = maxo / COPY_MAX + Fo + S + 2;
@@ -2005,9 +2038,9 @@ int wsg_batcher_session_reset(wsg_batcher* b, uint32_t sid) {
 // One encode flush's pinned staging and device buffers (three: one being filled by
 // add(), up to two in flight).
 struct EncSlot {
-  PinnedBuf arena, frames, sf, cl, wire, off;
+  PinnedBuf arena, frames, sf, cl, wire, off, ddesc;
   uint64_t arena_len = 0, F = 0, need = 0;
-  DBuf d_pay, d_frames, d_sf, d_cl, d_off;
+  DBuf d_pay, d_frames, d_sf, d_cl, d_off, d_ddesc, d_odesc;
   hipEvent_t ev_in = nullptr, ev_k = nullptr, ev_out = nullptr;
   std::vector<uint32_t> resets;  // sessions reset while this flush was in flight: their bytes are dropped
   // the view with those sessions' frames left out (built only when there are some)
@@ -2032,7 +2065,30 @@ struct wsg_enc_batcher {
   std::string err;
   uint64_t tickets = 0;                         // flushes queued so far
   std::shared_ptr<Notify> notify = std::make_shared<Notify>();
+  // permessage-deflate before the encoder (wsg_enc_batcher_set_deflate): level < 0 off;
+  // the deflater state and window | head | prev of every session, on the device
+  int defl_level = -1, defl_nc = 0;
+  DBuf d_dstate, d_dmem;
 };
+
+// Frame k's encode record from the deflate stage's output descriptor: the payload to frame
+// is the compressed one (in the out region, `out_base` bytes into the payload buffer) or the
+// frame's own, with the RSV bits the PerMessageDeflateEncoder gave it; the mask stays.
+__global__ __launch_bounds__(256) void k_enc_from_defl(const wsg_frame_desc* __restrict__ od,
+                                                       wsg_encode_frame* __restrict__ fr, uint64_t n,
+                                                       uint64_t out_base) {
+  const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const wsg_frame_desc d = od[k];
+  wsg_encode_frame f = fr[k];
+  f.payload_off = (d.flags & WSG_DESC_DEFLATED) ? out_base + d.payload_off : d.payload_off;
+  f.payload_len = d.payload_len;
+  f.opcode = d.opcode;
+  f.flags = d.flags & 0xF0;
+  fr[k] = f;
+}
+
+static inline uint64_t java_bound_h(uint64_t len) { return len + ((len + 7) >> 3) + ((len + 63) >> 6) + 15; }
 
 static int eset(wsg_enc_batcher* b, int code, const char* msg) {
   if (b) b->err = msg ? msg : "";
@@ -2064,17 +2120,37 @@ int wsg_enc_batcher_close(wsg_enc_batcher* b) {
   if (b->s_in) (void)hipStreamSynchronize(b->s_in);
   if (b->s_out) (void)hipStreamSynchronize(b->s_out);
   for (EncSlot& e : b->es) {
-    PinnedBuf* bufs[] = {&e.arena, &e.frames, &e.sf, &e.cl, &e.wire, &e.off};
+    PinnedBuf* bufs[] = {&e.arena, &e.frames, &e.sf, &e.cl, &e.wire, &e.off, &e.ddesc};
     for (PinnedBuf* p : bufs) p->release();
-    DBuf* dbufs[] = {&e.d_pay, &e.d_frames, &e.d_sf, &e.d_cl, &e.d_off};
+    DBuf* dbufs[] = {&e.d_pay, &e.d_frames, &e.d_sf, &e.d_cl, &e.d_off, &e.d_ddesc, &e.d_odesc};
     for (DBuf* d : dbufs) d->release();
     hipEvent_t evs[] = {e.ev_in, e.ev_k, e.ev_out};
     for (hipEvent_t v : evs)
       if (v) (void)hipEventDestroy(v);
   }
+  b->d_dstate.release();
+  b->d_dmem.release();
   if (b->s_in) (void)hipStreamDestroy(b->s_in);
   if (b->s_out) (void)hipStreamDestroy(b->s_out);
   delete b;
+  return WSG_API_OK;
+}
+
+// PerMessageDeflateEncoder(level, noContext) in front of the encoder for every session
+// (PerMessageDeflateExtension.updateEncoders, PerMessageDeflateExtension.java:303-313): the
+// state of a new deflater per session (zeros), its window and hash arrays on the device.
+int wsg_enc_batcher_set_deflate(wsg_enc_batcher* b, int level, int no_context) {
+  if (!b) return WSG_API_EINVAL;
+  if (level < 0 || level > 9) return eset(b, WSG_API_EINVAL, "compression level is out of range");
+  if (!b->q.empty() || !b->rec.empty() || b->defl_level >= 0)
+    return eset(b, WSG_API_ERANGE, "wsg_enc_batcher_set_deflate: once, before the first add");
+  E_TRY(b, hipSetDevice(ws::ctx_device(b->ctx)));
+  const uint64_t S = b->n ? b->n : 1;
+  E_TRY(b, b->d_dstate.ensure(S * sizeof(wsg_deflate_state)));
+  E_TRY(b, b->d_dmem.ensure(S * (uint64_t)WSG_DEFLATE_SESSION_BYTES));
+  E_TRY(b, hipMemsetAsync(b->d_dstate.p, 0, S * sizeof(wsg_deflate_state), ws::ctx_stream(b->ctx)));
+  b->defl_level = level;
+  b->defl_nc = no_context ? 1 : 0;
   return WSG_API_OK;
 }
 
@@ -2191,13 +2267,30 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
     wsg_encode_frame* fr = (wsg_encode_frame*)e.frames.p;
     for (uint64_t k = 0; k < F; ++k) fr[pos[b->rec_sid[k]]++] = b->rec[k];
   }
+  const bool defl = b->defl_level >= 0;
+  ws::DeflBounds bounds;
   uint64_t need = 0;
-  for (uint64_t k = 0; k < F; ++k) need += wsg_encoded_length(b->rec[k].payload_len, b->client);
+  if (!defl) {
+    for (uint64_t k = 0; k < F; ++k) need += wsg_encoded_length(b->rec[k].payload_len, b->client);
+  } else {  // a compressed payload is at most ZlibEncoder.deflateBound(len) bytes
+    E_TRY(b, e.ddesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+    const wsg_encode_frame* fr = (const wsg_encode_frame*)e.frames.p;
+    wsg_frame_desc* dd = (wsg_frame_desc*)e.ddesc.p;
+    for (uint64_t k = 0; k < F; ++k) {
+      dd[k] = wsg_frame_desc{fr[k].payload_off, fr[k].payload_len, fr[k].opcode, fr[k].flags, 0};
+      need += wsg_encoded_length(java_bound_h(fr[k].payload_len), b->client);
+      ws::deflate_bounds_add(bounds, fr[k].payload_len);
+    }
+    for (uint32_t i = 0; i < S; ++i)
+      if (b->count[i]) ws::deflate_bounds_session(bounds);
+  }
   E_TRY(b, e.wire.ensure(need + 32));
   if (S) memcpy(e.cl.p, b->closed.data(), S);
   for (uint64_t k = 0; k < F; ++k)  // the latch the next batch starts from
     if (b->rec[k].opcode == WSG_OP_CLOSE) b->closed[b->rec_sid[k]] = 1;
-  E_TRY(b, e.d_pay.ensure(e.arena_len + 32));
+  // with deflate the compressed payloads follow the arena in the same device buffer
+  const uint64_t out_base = (e.arena_len + 255) & ~255ull, out_cap = defl ? bounds.tot[1] : 0;
+  E_TRY(b, e.d_pay.ensure(defl ? out_base + out_cap + 64 : e.arena_len + 32));
   E_TRY(b, e.d_frames.ensure((F + 1) * sizeof(wsg_encode_frame)));
   E_TRY(b, e.d_sf.ensure((S + 1) * sizeof(uint32_t)));
   E_TRY(b, e.d_cl.ensure(S + 1));
@@ -2215,12 +2308,28 @@ int wsg_enc_batcher_flush_async(wsg_enc_batcher* b) {
   if (F) E_TRY(b, hipMemcpyAsync(e.d_frames.p, e.frames.p, F * sizeof(wsg_encode_frame), hipMemcpyHostToDevice, b->s_in));
   E_TRY(b, hipMemcpyAsync(e.d_sf.p, e.sf.p, (S + 1) * sizeof(uint32_t), hipMemcpyHostToDevice, b->s_in));
   if (S) E_TRY(b, hipMemcpyAsync(e.d_cl.p, e.cl.p, S, hipMemcpyHostToDevice, b->s_in));
+  if (defl) {
+    E_TRY(b, e.d_ddesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+    E_TRY(b, e.d_odesc.ensure((F + 1) * sizeof(wsg_frame_desc)));
+    if (F) E_TRY(b, hipMemcpyAsync(e.d_ddesc.p, e.ddesc.p, F * sizeof(wsg_frame_desc), hipMemcpyHostToDevice, b->s_in));
+  }
   E_TRY(b, hipEventRecord(e.ev_in, b->s_in));
   hipStream_t ks = ws::ctx_stream(b->ctx);
   E_TRY(b, hipStreamWaitEvent(ks, e.ev_in, 0));
-  int rc = wsg_encode_batch_device(b->ctx, b->client, e.d_pay.p, e.arena_len, (const wsg_encode_frame*)e.d_frames.p,
-                                   F, (const uint32_t*)e.d_sf.p, S, e.d_cl.p, wire_out, need + 32,
-                                   (uint64_t*)e.d_off.p);
+  int rc;
+  if (defl && F) {  // the permessage-deflate-encoder stage, then the frames it hands on
+    rc = ws::deflate_launch(b->ctx, b->defl_level, b->defl_nc, (const wsg_frame_desc*)e.d_ddesc.p, F,
+                            (const uint32_t*)e.d_sf.p, S, e.d_pay.p, (wsg_deflate_state*)b->d_dstate.p,
+                            b->d_dmem.p, e.d_pay.p + out_base, out_cap, (wsg_frame_desc*)e.d_odesc.p, &bounds,
+                            nullptr);
+    if (rc) return eset(b, rc, wsg_last_error(b->ctx));
+    hipLaunchKernelGGL(k_enc_from_defl, dim3((uint32_t)((F + 255) / 256)), dim3(256), 0, ks,
+                       (const wsg_frame_desc*)e.d_odesc.p, (wsg_encode_frame*)e.d_frames.p, F, out_base);
+    E_TRY(b, hipGetLastError());
+  }
+  rc = wsg_encode_batch_device(b->ctx, b->client, e.d_pay.p, defl ? out_base + out_cap : e.arena_len,
+                               (const wsg_encode_frame*)e.d_frames.p, F, (const uint32_t*)e.d_sf.p, S, e.d_cl.p,
+                               wire_out, need + 32, (uint64_t*)e.d_off.p);
   if (rc) return eset(b, rc, wsg_last_error(b->ctx));
   if (!F) E_TRY(b, hipMemsetAsync(e.d_off.p, 0, sizeof(uint64_t), ks));
   E_TRY(b, hipEventRecord(e.ev_k, ks));
@@ -2327,6 +2436,14 @@ int wsg_enc_batcher_reserve(wsg_enc_batcher* b, uint64_t max_frames, uint64_t ma
     E_TRY(b, e.cl.ensure(S + 1));
     E_TRY(b, e.off.ensure((max_frames + 1) * sizeof(uint64_t)));
     E_TRY(b, e.wire.ensure(need + 32));
+    if (b->defl_level >= 0) {  // the compressed payloads after the arena, their descriptors
+      const uint64_t out = java_bound_h(max_payload) + 32 * max_frames;
+      E_TRY(b, e.d_pay.ensure(((arena + 255) & ~255ull) + out + 64));
+      E_TRY(b, e.wire.ensure(out + 14 * max_frames + 32));
+      E_TRY(b, e.ddesc.ensure((max_frames + 1) * sizeof(wsg_frame_desc)));
+      E_TRY(b, e.d_ddesc.ensure((max_frames + 1) * sizeof(wsg_frame_desc)));
+      E_TRY(b, e.d_odesc.ensure((max_frames + 1) * sizeof(wsg_frame_desc)));
+    }
     E_TRY(b, e.d_pay.ensure(arena + 32));
     E_TRY(b, e.d_frames.ensure((max_frames + 1) * sizeof(wsg_encode_frame)));
     E_TRY(b, e.d_sf.ensure((S + 1) * sizeof(uint32_t)));
@@ -2353,6 +2470,9 @@ int wsg_enc_batcher_session_reset(wsg_enc_batcher* b, uint32_t sid) {
   }
   b->closed[sid] = 0;
   for (int slot : b->q) b->es[slot].resets.push_back(sid);
+  if (b->defl_level >= 0)  // a new deflater (in stream order: after the flushes in flight)
+    E_TRY(b, hipMemsetAsync((wsg_deflate_state*)b->d_dstate.p + sid, 0, sizeof(wsg_deflate_state),
+                            ws::ctx_stream(b->ctx)));
   return WSG_API_OK;
 }
 

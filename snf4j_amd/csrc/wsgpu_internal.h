@@ -329,6 +329,7 @@ void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src);  // where ctx_record_out
 int ctx_device(wsg_ctx* c);
 bool ctx_inflate_two_phase(const wsg_ctx* c);
 uint8_t* ctx_async_payload(wsg_ctx* c);
+bool ctx_stage_fail(wsg_ctx* c);  // WSG_TUNE_STAGE_FAIL: this stage step is the one to fail
 uint64_t ctx_alloc_count();  // device workspace allocations of every context so far
 int ctx_reserve_stages(wsg_ctx* c, uint64_t max_frames, uint32_t max_sessions, uint64_t payload_len,
                        uint64_t agg_cap);
@@ -371,6 +372,19 @@ uint64_t infl_tok_words(uint64_t payload_len, uint64_t n_frames);
 uint64_t infl_lit_bytes(uint64_t payload_len, uint64_t n_frames);
 uint64_t infl_ord_words(uint64_t n_frames);  // order + bucket counts
 uint64_t infl_tab_bytes();
+
+// Upper bounds of the plan's five region totals (S bytes, output bytes, symbol words, match
+// chunks, block slots) from the frames' lengths alone: _add per frame, _session per session
+// with frames.  deflate_launch with bounds sizes its workspace from them and reads nothing back.
+struct DeflBounds {
+  uint64_t tot[5] = {0, 0, 0, 0, 0};
+};
+void deflate_bounds_add(DeflBounds& b, uint32_t len);
+void deflate_bounds_session(DeflBounds& b);
+int deflate_launch(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* desc, uint64_t n_frames,
+                   const uint32_t* session_first, uint32_t n_sessions, const uint8_t* payload,
+                   wsg_deflate_state* state, uint8_t* session_mem, uint8_t* out, uint64_t out_cap,
+                   wsg_frame_desc* out_desc, const DeflBounds* bounds, uint64_t* out_total);
 
 void launch_defl_plan(const DeflArgs& a, hipStream_t s);    // k_defl_plan + k_defl_scan
 void launch_defl_prep(const DeflArgs& a, hipStream_t s);

@@ -3,6 +3,11 @@ java/org/snf4j/websocket/gpu/WsgBatcher.java over the native batchers, restated 
 Python so that it runs here (there is no JDK in this image) — the same calls in the
 same order, driven by the same kind of loop.
 
+The loop object these classes take is anything with snf4j's task-queue calls
+(executenf, iteration): the SelectorLoop model the tests and the bench drive them with
+is benchsupport/selector.py; the session around the decoder stage (snf4j-core's read
+loop and exception path) is modelled in tests/harness/session.py.
+
 snf4j's loop (InternalSelectorLoop.java): one thread repeats select() -> the reads
 of the ready sessions, each going through its decoder (StreamSession.java:798-854 ->
 GpuFrameDecoder.decode -> LoopBatcher.enqueue) -> handleTasks (:641, :751-758),
@@ -37,53 +42,11 @@ from ._lib import BATCHER_MAX_INFLIGHT
 from .codec import EncodeBatcher, NativeBatcher
 
 
-class SelectorLoop:
-    """The task side of InternalSelectorLoop: executenf queues (any thread) and wakes
-    the selector; handle_tasks runs tasks until the queue is empty."""
-
-    def __init__(self):
-        self._tasks = collections.deque()
-        self._lock = threading.Lock()
-        self._wake = threading.Event()
-        self.iteration = 0
-
-    def executenf(self, task):
-        with self._lock:
-            self._tasks.append(task)
-        self._wake.set()
-
-    def handle_tasks(self):
-        while True:
-            with self._lock:
-                if not self._tasks:
-                    return
-                task = self._tasks.popleft()
-            task()
-
-    def select(self, timeout: float | None) -> bool:
-        """Block until woken (executenf) or the timeout; True if woken."""
-        woke = self._wake.wait(timeout)
-        self._wake.clear()
-        return woke
-
-    def run_iteration(self, reads):
-        """One loop iteration: the reads (callables, each a session's read -> decode),
-        then the task phase."""
-        self.iteration += 1
-        for r in reads:
-            r()
-        self.handle_tasks()
-
-    def has_tasks(self) -> bool:
-        with self._lock:
-            return bool(self._tasks)
-
-
 class _Completion(threading.Thread):
     """Waits for the tickets it is given (await on the native batcher) and re-enters
     the loop with executenf(task) for each one that finished."""
 
-    def __init__(self, loop: SelectorLoop, await_fn, task, name: str):
+    def __init__(self, loop, await_fn, task, name: str):
         super().__init__(name=name, daemon=True)
         self.loop, self.await_fn, self.task = loop, await_fn, task
         self.q: queue.Queue = queue.Queue()
@@ -112,7 +75,7 @@ class LoopBatcher:
     """WsgBatcher's decode side.  deliver(sid, frames, exc) is called on the loop
     thread, per session in flush order (frames as NativeBatcher returns them)."""
 
-    def __init__(self, loop: SelectorLoop, n_sessions: int, deliver, ctx=None, clientMode: bool = False,
+    def __init__(self, loop, n_sessions: int, deliver, ctx=None, clientMode: bool = False,
                  allowExtensions: bool = False, maxPayloadLen: int = 65536, validate_utf8: bool = True,
                  max_wire: int = 0, max_frames: int = 0, raw: bool = False,
                  max_inflight: int = BATCHER_MAX_INFLIGHT):
@@ -226,7 +189,7 @@ class LoopBatcher:
 class LoopEncodeBatcher:
     """WsgBatcher's encode side: write(sid, wire bytes) on the loop thread."""
 
-    def __init__(self, loop: SelectorLoop, n_sessions: int, write, clientMode: bool = True, ctx=None,
+    def __init__(self, loop, n_sessions: int, write, clientMode: bool = True, ctx=None,
                  max_frames: int = 0, max_payload: int = 0):
         self.loop = loop
         self.eb = EncodeBatcher(n_sessions, clientMode, ctx=ctx)
@@ -296,318 +259,10 @@ class LoopEncodeBatcher:
         self.eb.close()
 
 
-def run_until_idle(loop: SelectorLoop, *batchers, timeout: float = 60.0):
-    """Loop iterations without reads until every batcher's flushes are delivered
-    (woken by the completion threads)."""
-    import time
-    end = time.monotonic() + timeout
-    while any(b.inflight or b.flush_scheduled for b in batchers) or loop.has_tasks():
-        if time.monotonic() > end:
-            raise TimeoutError("flushes still in flight")
-        loop.select(0.05)
-        loop.run_iteration([])
-
-
-
-
-# ====================================================================== the session side
-# What the decoder stage sits in: snf4j-core's stream session read loop and its
-# exception path, restated so that GpuFrameDecoder (below) runs in the same calls the
-# reference makes — and the reference's own FrameDecoder in the same harness (the
-# parity test puts the oracle's decoder there).
-#
-#   StreamSession.consumeBuffer, copy path      StreamSession.java:798-854
-#   StreamSession.consumeBuffer, optimized path StreamSession.java:765-796
-#   the pipeline's decode                       CodecExecutorAdapter.java:100-156
-#   an exception out of the read                InternalSelectorLoop.java:589-624
-#   InternalSession.exception / controlClose    InternalSession.java:804-848
-#
-# One choice where the reference leaves it open: an exception that does not close
-# the session (close type NONE) leaves the rest of the input buffer unconsumed, and
-# the plain stream session does not compact it (SelectorLoop.java:600-611); the
-# engine session does (EngineStreamHandler.java:179-183), which is what the model
-# does: the bytes stay for the next read event.
-
 class CloseType:
     """ICloseControllingException.CloseType (ICloseControllingException.java:40-60)."""
     GENTLE, DEFAULT, NONE = "GENTLE", "DEFAULT", "NONE"
 
-
-class PipelineDecodeException(RuntimeError):
-    """PipelineDecodeException (PipelineDecodeException.java:28-42): a decoder threw."""
-
-    def __init__(self, cause):
-        super().__init__(str(cause))
-        self.cause = cause
-
-
-class ByteBuffer:
-    """The java.nio.ByteBuffer state the read loop relies on: position, limit,
-    capacity over a shared backing array (duplicate() shares it)."""
-
-    def __init__(self, capacity: int = 0, direct: bool = False, _buf=None):
-        self.buf = bytearray(capacity) if _buf is None else _buf
-        self.pos, self.lim, self.direct = 0, len(self.buf), direct
-        self.reading = False  # flipped (read mode) since the last clear / compact
-
-    @staticmethod
-    def wrap(data) -> "ByteBuffer":
-        return ByteBuffer(_buf=bytearray(data))
-
-    def capacity(self): return len(self.buf)
-    def position(self): return self.pos
-    def limit(self): return self.lim
-    def remaining(self): return self.lim - self.pos
-    def hasRemaining(self): return self.lim > self.pos
-    def hasArray(self): return not self.direct
-    def array(self): return self.buf
-    def arrayOffset(self): return 0
-
-    def set_position(self, p):
-        self.pos = p
-        return self
-
-    def set_limit(self, n):
-        self.lim = n
-        self.pos = min(self.pos, n)
-        return self
-
-    def flip(self):
-        self.lim, self.pos = self.pos, 0
-        self.reading = True
-        return self
-
-    def clear(self):
-        self.pos, self.lim = 0, len(self.buf)
-        self.reading = False
-        return self
-
-    def compact(self):
-        n = self.lim - self.pos
-        self.buf[0:n] = self.buf[self.pos:self.lim]
-        self.pos, self.lim = n, len(self.buf)
-        self.reading = False
-        return self
-
-    def duplicate(self) -> "ByteBuffer":
-        d = ByteBuffer(_buf=self.buf, direct=self.direct)
-        d.pos, d.lim, d.reading = self.pos, self.lim, self.reading
-        return d
-
-    def get(self, n: int) -> bytes:
-        if n > self.remaining():
-            raise ValueError("BufferUnderflowException")
-        b = bytes(self.buf[self.pos:self.pos + n])
-        self.pos += n
-        return b
-
-    def put(self, src) -> "ByteBuffer":
-        b = src.get(src.remaining()) if isinstance(src, ByteBuffer) else bytes(src)
-        if len(b) > self.lim - self.pos:
-            raise ValueError("BufferOverflowException")
-        self.buf[self.pos:self.pos + len(b)] = b
-        self.pos += len(b)
-        return self
-
-    def peek(self) -> bytes:
-        """The bytes between position and limit (no state change)."""
-        return bytes(self.buf[self.pos:self.lim])
-
-
-def consume_buffer(in_buffer: ByteBuffer, reader, skip_consuming) -> None:
-    """StreamSession.consumeBuffer(ByteBuffer, IStreamReader, IConsumeController), the
-    copy path (StreamSession.java:798-854): in_buffer is in write mode; each frame the
-    decoder delimits is copied out and read."""
-    has_array = in_buffer.hasArray()
-    if has_array:
-        array, arr_off = in_buffer.array(), in_buffer.arrayOffset()
-        available = reader.available_array(array, arr_off, in_buffer.position())
-    else:
-        array, arr_off = None, 0
-        available = reader.available_buffer(in_buffer, False)
-    if available > 0:
-        in_buffer.flip()
-        data = in_buffer.get(available)
-        reader.read(data)
-        if in_buffer.hasRemaining():
-            while True:
-                if has_array:
-                    available = reader.available_array(array, arr_off + in_buffer.position(), in_buffer.remaining())
-                else:
-                    available = reader.available_buffer(in_buffer, True)
-                if available <= 0:
-                    break
-                if skip_consuming():
-                    break
-                reader.read(in_buffer.get(available))
-            if in_buffer.hasRemaining():
-                in_buffer.compact()
-            else:
-                in_buffer.clear()
-        else:
-            in_buffer.clear()
-
-
-def consume_buffer_optimized(in_buffer: ByteBuffer, reader, allocate, skip_consuming):
-    """StreamSession.consumeBuffer(ByteBuffer, IStreamReader, IByteBufferAllocator,
-    IConsumeController), the optimized path (StreamSession.java:765-796): a frame that
-    fills the buffer is handed over as the buffer itself (None returned: the session
-    allocates a new one), else each frame goes out in a buffer of its own."""
-    available = reader.available_buffer(in_buffer, False)
-    if available > 0:
-        in_buffer.flip()
-        if available == in_buffer.remaining():
-            reader.read(in_buffer)
-            return None
-        dup = in_buffer.duplicate()
-        while True:
-            data = allocate(available)
-            dup.set_limit(dup.position() + available)
-            data.put(dup)
-            data.flip()
-            in_buffer.set_position(dup.position())
-            reader.read(data)
-            if skip_consuming():
-                break
-            available = reader.available_buffer(in_buffer, True)
-            if available == in_buffer.remaining():
-                reader.read(in_buffer)
-                return None
-            if available <= 0:
-                break
-        in_buffer.compact()
-    return in_buffer
-
-
-class StreamSession:
-    """The session around a decoder pipeline: a socket read (read_event) appends to the
-    input buffer and consumes it; the pipeline is [("ws-decoder", base decoder),
-    (key, decoder), ...]; what reaches the handler and how the session ends is recorded
-    in `events`:
-      ("read", frame) | ("exception", cause) | ("close",) | ("quickClose",) | ("writenf", frame)."""
-
-    def __init__(self, pipeline, handler_read=None, optimized: bool = False, direct: bool = False,
-                 min_in: int = 2048):
-        self.pipeline = list(pipeline)
-        self.handler_read = handler_read
-        self.optimized, self.direct, self.min_in = optimized, direct, min_in
-        self.in_buffer = None if optimized else ByteBuffer(min_in, direct=direct)
-        self.events: list = []
-        self.close_called = False  # InternalSession.closeCalled
-        self.closing = None        # "close" | "quickClose"
-        self.released = 0
-
-    # ---- ISession
-    def getCodecPipeline(self):
-        return self.pipeline
-
-    def writenf(self, frame):
-        self.events.append(("writenf", frame))
-
-    def release(self, data):
-        self.released += 1
-
-    def close(self):
-        self.close_called = True
-        if self.closing is None:
-            self.closing = "close"
-            self.events.append(("close",))
-
-    def quickClose(self):
-        self.close_called = True
-        if self.closing != "quickClose":
-            self.closing = "quickClose"
-            self.events.append(("quickClose",))
-
-    # ---- IHandler
-    def handler_exception(self, t):
-        self.events.append(("exception", t))
-
-    def read_object(self, o):
-        self.events.append(("read", o))
-        if self.handler_read is not None:
-            self.handler_read(self, o)
-
-    # ---- InternalSession.exception / controlClose (InternalSession.java:804-848)
-    def exception(self, t):
-        if isinstance(t, PipelineDecodeException):  # InternalSelectorLoop.java:589-597: its cause
-            t = t.cause
-        ct = getattr(t, "getCloseType", None)
-        if ct is not None:
-            kind, cause = ct(), t.getClosingCause()
-            if kind == CloseType.GENTLE:
-                self.handler_exception(cause)
-                self.close()
-                return
-            if kind == CloseType.NONE:
-                self.handler_exception(cause)
-                return
-            t = cause
-        self.handler_exception(t)
-        self.quickClose()
-
-    # ---- the codec adapter (CodecExecutorAdapter.java:100-156) as the IStreamReader
-    def available_array(self, array, off, length):
-        return self.pipeline[0][1].available(self, bytes(array[off:off + length]), 0, length)
-
-    def available_buffer(self, buf, flipped):
-        return self.pipeline[0][1].available_buffer(self, buf, flipped)
-
-    def read(self, data):
-        out = []
-        try:
-            base = self.pipeline[0][1]
-            base.decode(self, data if isinstance(data, ByteBuffer) else ByteBuffer.wrap(data), out)
-            for _, c in self.pipeline[1:]:
-                if getattr(c, "batched", False):
-                    continue
-                nxt = []
-                for o in out:
-                    c.decode(self, o, nxt)
-                out = nxt
-        except Exception as e:  # noqa: BLE001 - any decoder exception is the pipeline's
-            raise PipelineDecodeException(e)
-        for o in out:
-            self.read_object(o)
-
-    # ---- SelectorLoop.handleReading (SelectorLoop.java:600-611) + the catch of
-    # InternalSelectorLoop.java:589-624
-    def read_event(self, chunk: bytes):
-        if self.closing == "quickClose":  # the channel is closed
-            return
-        if self.optimized:
-            need = len(chunk)
-            if self.in_buffer is None:
-                self.in_buffer = ByteBuffer(max(self.min_in, need), direct=self.direct)
-            elif self.in_buffer.capacity() - self.in_buffer.position() < need:  # allocator.ensureSome
-                grown = ByteBuffer(self.in_buffer.position() + need, direct=self.direct)
-                grown.put(self.in_buffer.duplicate().flip())
-                self.in_buffer = grown
-        elif self.in_buffer.capacity() - self.in_buffer.position() < len(chunk):
-            grown = ByteBuffer(self.in_buffer.position() + len(chunk), direct=self.direct)
-            grown.put(self.in_buffer.duplicate().flip())
-            self.in_buffer = grown
-        self.in_buffer.put(chunk)
-        try:
-            if self.optimized:
-                self.in_buffer = consume_buffer_optimized(self.in_buffer, self, lambda n: ByteBuffer(n, self.direct),
-                                                          lambda: self.close_called)
-            else:
-                consume_buffer(self.in_buffer, self, lambda: self.close_called)
-        except Exception as e:  # noqa: BLE001
-            self._keep_unconsumed()
-            self.exception(e)
-
-    def _keep_unconsumed(self):
-        """An exception left the input buffer in read mode: what is unread stays for the
-        next read event (EngineStreamHandler.java:179-183 compacts it)."""
-        b = self.in_buffer
-        if b is not None and b.reading:
-            b.compact()
-
-    def pending_input(self) -> int:
-        b = self.in_buffer
-        return 0 if b is None else b.position()
 
 
 class GpuFrameDecoder:
@@ -780,7 +435,7 @@ class DecoderBatcher(LoopBatcher):
     """WsgBatcher's decode side with its session slots (register / unregister /
     enqueue / drain, WsgBatcher.java): deliveries go to the decoder holding the slot."""
 
-    def __init__(self, loop: SelectorLoop, n_sessions: int, **kw):
+    def __init__(self, loop, n_sessions: int, **kw):
         self.slots: list = [None] * n_sessions
         self.next = 0
         super().__init__(loop, n_sessions, self._route, **kw)
@@ -820,7 +475,7 @@ class DecoderBatcher(LoopBatcher):
             ids, data = self._sids, self._data
             self._sids, self._data = [], []
             self.nb.feed_many(ids, data)
-            if len(self.inflight) == 2:
+            if len(self.inflight) == self.max_inflight:
                 self._collect_oldest(blocking=True)
             self.nb.flush_async()
             self.inflight.append((self.nb.ticket(), self.loop.iteration))
@@ -828,6 +483,4 @@ class DecoderBatcher(LoopBatcher):
             self._collect_oldest(blocking=True)
 
 
-__all__ = ["SelectorLoop", "LoopBatcher", "LoopEncodeBatcher", "run_until_idle", "CloseType", "ByteBuffer",
-           "consume_buffer", "consume_buffer_optimized", "StreamSession", "GpuFrameDecoder", "DecoderBatcher",
-           "PipelineDecodeException"]
+__all__ = ["LoopBatcher", "LoopEncodeBatcher", "CloseType", "GpuFrameDecoder", "DecoderBatcher"]

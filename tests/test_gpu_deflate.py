@@ -169,3 +169,83 @@ def test_bench_shaped_batch(ctx):
     got = _deflater(ctx, 256, 6, False).run(sessions)
     for s in range(0, 256, 5):
         assert got[s] == encode_frames(sessions[s], 6, False), s
+
+
+def _pmd_stream(rng, n_frames):
+    """A session's outgoing frames: messages of 1-3 fragments (TEXT / BINARY then
+    continuations), PINGs between fragments, now and then a message already carrying RSV1
+    (passed through, PerMessageDeflateEncoder.allowEncoding) and empty payloads."""
+    fr, i = [], 0
+    while i < n_frames:
+        nfrag = int(rng.integers(1, 4))
+        op = int(rng.choice([1, 2]))
+        rsv = 4 if rng.random() < 0.08 else 0
+        for j in range(nfrag):
+            n = 0 if rng.random() < 0.05 else int(rng.integers(1, 9000))
+            fr.append((op if j == 0 else 0, j == nfrag - 1, rsv if j == 0 else 0, dh.text(rng, n)))
+            if rng.random() < 0.1:
+                fr.append((9, True, 0, bytes(rng.integers(0, 256, int(rng.integers(0, 60)), dtype=np.uint8))))
+            i += 1
+    return fr
+
+
+@pytest.mark.parametrize("level,nc", [(6, False), (6, True), (1, False), (9, False), (0, True)])
+def test_encode_batcher_deflate(ctx, oracle, level, nc):
+    """The permessage-deflate-encoder stage inside the encode batcher
+    (wsg_enc_batcher_set_deflate): frames of many sessions added interleaved over several
+    pipelined flushes (two in flight), compressed and framed on the device; every session's
+    wire bytes equal the reference chain's — PerMessageDeflateEncoder (zlib as Deflater,
+    oracle/deflate_ref.c) then FrameEncoder (the oracle's) — with the deflater kept across
+    flushes, a CLOSE latching its session, and a slot reset giving a new session a new
+    deflater while its old frames are in flight."""
+    from snf4j_amd import EncodeBatcher
+    from snf4j_amd.frame import make_frame
+    for cm in (False, True):
+        rng = np.random.default_rng(1000 + 10 * level + nc + 2 * cm)
+        n = 24
+        b = EncodeBatcher(n, cm, ctx=ctx)
+        b.set_deflate(level, nc)
+        streams = [_pmd_stream(rng, 40) for _ in range(n)]
+        streams[7] = streams[7][:5] + [(8, True, 0, b"\x03\xe8")] + streams[7][5:]   # CLOSE mid-stream
+        hist = [[] for _ in range(n)]       # frames since the slot's last reset
+        enc = [oracle.Encoder(cm) for _ in range(n)]
+        pos = [0] * n
+        pending = []
+        for flush in range(6):
+            want = [b""] * n
+            adds = []
+            for s in range(n):
+                k = int(rng.integers(0, 10))
+                for f in streams[s][pos[s]:pos[s] + k]:
+                    adds.append((s, f))
+                pos[s] += k
+            rng.shuffle(adds)
+            per = [[] for _ in range(n)]
+            for s, f in adds:   # a session's frames keep their order (the shuffle mixes sessions only)
+                per[s].append(f)
+            order = sorted(range(len(adds)), key=lambda i: rng.random())
+            qs = [list(p) for p in per]
+            for i in order:
+                s = adds[i][0]
+                if not qs[s]:
+                    continue
+                op, fin, rsv, p = qs[s].pop(0)
+                mask = tuple(int(x) for x in rng.integers(0, 256, 4))
+                b.add(s, make_frame(op, fin, rsv, p), mask)
+                h0 = len(hist[s])
+                hist[s].append((op, fin, rsv, p))
+                out = encode_frames(hist[s], level, nc)[h0]
+                want[s] += enc[s].encode(out[0], out[1], out[2], out[3], mask if cm else (0, 0, 0, 0))
+            b.flush_async()
+            pending.append(want)
+            if flush == 3:   # slot 11 to a new session while its frames are in flight
+                b.reset_session(11)
+                hist[11] = []
+                enc[11] = oracle.Encoder(cm)
+                for w in pending:
+                    w[11] = b""
+            if len(pending) == 2:
+                assert b.wait() == pending.pop(0), (level, nc, cm, flush)
+        while pending:
+            assert b.wait() == pending.pop(0), (level, nc, cm)
+        b.close()

@@ -25,7 +25,8 @@ def ctx():
 
 
 def test_loop_decode_matches_oracle(ctx, oracle):
-    from snf4j_amd.loop import LoopBatcher, SelectorLoop, run_until_idle
+    from benchsupport.selector import SelectorLoop, run_until_idle
+    from snf4j_amd.loop import LoopBatcher
     rng = random.Random(2024)
     nrng = np.random.default_rng(2024)
     n = 64
@@ -88,7 +89,8 @@ def test_loop_decode_matches_oracle(ctx, oracle):
 
 def test_loop_encode_matches_oracle(ctx, oracle):
     from snf4j_amd import frame as F
-    from snf4j_amd.loop import LoopEncodeBatcher, SelectorLoop, run_until_idle
+    from benchsupport.selector import SelectorLoop, run_until_idle
+    from snf4j_amd.loop import LoopEncodeBatcher
     rng = random.Random(77)
     n = 24
     written = [b"" for _ in range(n)]

@@ -29,7 +29,8 @@ def ctx():
 
 @pytest.mark.parametrize("seed", [1, 2, 3, 4])
 def test_gpu_frame_decoder_sessions_match_reference(ctx, oracle, seed):
-    from snf4j_amd.loop import DecoderBatcher, SelectorLoop
+    from benchsupport.selector import SelectorLoop
+    from snf4j_amd.loop import DecoderBatcher
     plan = M.make_plan(seed, 64)
     want = M.run_reference(oracle, plan)
     loop = SelectorLoop()

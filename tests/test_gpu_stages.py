@@ -321,3 +321,45 @@ def test_batcher_stage_chain_threaded_feeds(ctx, oracle):
         assert [(int(f.getOpcode()), f.isFinalFragment(), f.getRsvBits(), f.getPayload()) for f in got[s]] == exp, s
         n_err += eerr is not None
     assert n_err
+
+
+def test_stage_failure_reported_by_wait_not_by_flush():
+    """A stage-chain step that fails while flush_async or a feed advances the chains of
+    flushes already queued (WSG_TUNE_STAGE_FAIL injects it, as a device error would come):
+    those calls still return OK — the flush is queued, the reads copied — and a later
+    wsg_batcher_wait reports the error; the batcher goes on with the flushes after it."""
+    from snf4j_amd import Context, NativeBatcher
+    from snf4j_amd._lib import WsgError
+    rng = np.random.default_rng(6500)
+    n = 16
+    c = Context(0)
+    try:
+        b = NativeBatcher(n, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=c)
+        b.set_stages(inflate=True, noContext=False, validate=True)
+        streams = [b"".join(wsgen.build_frame(op, fin, rsv, p, True, (1, 2, 3, 4))
+                            for (op, fin, rsv, p) in _messages(rng, 12, False, bad_utf8=0.0)) for _ in range(n)]
+        c.set_tuning("stage_fail", 2)
+        errors, pending, pos = [], 0, [0] * n
+        for it in range(8):
+            for s in range(n):
+                if pos[s] < len(streams[s]):
+                    b.feed(s, streams[s][pos[s]:pos[s] + 700])   # never raises for the side step
+                    pos[s] += 700
+            if pending == 3:
+                try:
+                    b.wait()
+                except WsgError as e:
+                    errors.append(str(e))
+                pending -= 1
+            b.flush_async()   # queued: OK whatever the stage step it ran on the side did
+            pending += 1
+        while pending:
+            try:
+                b.wait()
+            except WsgError as e:
+                errors.append(str(e))
+            pending -= 1
+        assert len(errors) == 1 and "injected stage failure" in errors[0], errors
+        b.close()
+    finally:
+        c.close()

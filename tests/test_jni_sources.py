@@ -60,11 +60,41 @@ def test_stage_classes_keep_the_reference_keys_and_types():
         assert "implements IDecoder<Frame, Frame>" in _java(f) and "GpuStage" in _java(f), f
     ext = _java("GpuPerMessageDeflateExtension.java")
     assert "implements IExtension" in ext and "PERMESSAGE_DEFLATE_DECODER" in ext
+    assert "implements IEncoder<Frame, Frame>" in _java("GpuPerMessageDeflateEncoder.java")
     files = sorted(os.listdir(JAVA))
     assert files == ["GpuFrameAggregator.java", "GpuFrameDecoder.java", "GpuFrameEncoder.java",
                      "GpuFrameUtf8Validator.java", "GpuPerMessageDeflateDecoder.java",
-                     "GpuPerMessageDeflateExtension.java", "GpuStage.java", "GpuWebSocketSessionConfig.java",
-                     "PinnedByteBufferAllocator.java", "Wsg.java", "WsgBatcher.java", "WsgDevices.java"]
+                     "GpuPerMessageDeflateEncoder.java", "GpuPerMessageDeflateExtension.java", "GpuStage.java",
+                     "GpuWebSocketSessionConfig.java", "PinnedByteBufferAllocator.java", "Wsg.java",
+                     "WsgBatcher.java", "WsgDevices.java"]
+
+
+def test_deflate_encoder_marker_is_installed_and_batched():
+    """PerMessageDeflateExtension.updateEncoders (PerMessageDeflateExtension.java:303-313)
+    puts PerMessageDeflateEncoder under "permessage-deflate-encoder"; the GPU extension
+    wraps it there in GpuPerMessageDeflateEncoder with the negotiated noContext (the
+    server's parameter for a server, :310) and attaches it to the GpuFrameEncoder, whose
+    encode batcher then runs the deflate stage (wsg_enc_batcher_set_deflate) for every data
+    frame of the session, whatever its size."""
+    ext = _java("GpuPerMessageDeflateExtension.java")
+    up = _body(ext, "public void updateEncoders(ICodecPipeline pipeline)", "public void updateDecoders(")
+    order = ["delegate.updateEncoders(pipeline)", "pipeline.get(PerMessageDeflateExtension.PERMESSAGE_DEFLATE_ENCODER)",
+             "SERVER_NO_CONTEXT : CLIENT_NO_CONTEXT", "pipeline.replace(PerMessageDeflateExtension.PERMESSAGE_DEFLATE_ENCODER",
+             "pipeline.get(IWebSocketSessionConfig.WEBSOCKET_ENCODER)", ".attachDeflate(g)"]
+    pos = [up.index(x) for x in order]
+    assert pos == sorted(pos), order
+    marker = _java("GpuPerMessageDeflateEncoder.java")
+    enc = _body(marker, "public void encode(ISession session, Frame frame", "public void added(")
+    assert "if (batched)" in enc and "out.add(frame)" in enc and "fallback.encode(session, frame, out)" in enc
+    fe = _java("GpuFrameEncoder.java")
+    att = fe[fe.index("void attachDeflate(GpuPerMessageDeflateEncoder d)"):fe.index("public void encode(ISession")]
+    assert "if (sid >= 0 || deflate != null)" in att and "d.setBatched()" in att
+    assert "!(deflate != null && data)" in fe and "batcher.registerEncoder(this, clientMode, deflate)" in fe
+    b = _java("WsgBatcher.java")
+    en = b[b.index("EncNative(boolean clientMode, GpuPerMessageDeflateEncoder deflate)"):]
+    assert en.index("Wsg.encBatcherSetDeflate(handle, deflate.level, deflate.noContext)") < \
+        en.index("Wsg.encBatcherReserve(handle")
+    assert "wsg_enc_batcher_set_deflate(ENC_BATCHER(b)" in _read("jni/wsgpu_jni.c")
 
 
 def test_session_lifecycle_reaches_the_native_reset():

@@ -16,7 +16,9 @@ import random
 import numpy as np
 import pytest
 
-from snf4j_amd.loop import CloseType, SelectorLoop, StreamSession
+from benchsupport.selector import SelectorLoop
+from snf4j_amd.loop import CloseType
+from tests.harness.session import StreamSession
 from tests import sessionmodel as M
 from tests import wsgen
 
