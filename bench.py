@@ -811,12 +811,36 @@ def _decode_line(ctx, dev, name, wire, wl, off, sf, n, n_s, payload_bytes, steps
             "pipeline_ms": pipe, **({"aggregate": agg} if agg else {})}
 
 
+def _hs_port_baselines(buf, n, L, keys=None, seconds=3.0):
+    """The compiled handshake port (oracle/handshake_port.c: parse + SHA-1 + Base64 a
+    request, kind "port") over a bounded sample of the line's requests (or responses), on
+    one host core and on the job's cores (cpu_threads)."""
+    import numpy as np
+    from oracle import handshake_port as HP
+    m = min(n, 65536)
+    flat = np.ascontiguousarray(buf[:m]).reshape(-1)
+    off = (np.arange(m + 1, dtype=np.uint64) * L)
+    k = np.ascontiguousarray(keys[:m]).reshape(-1) if keys is not None else None
+    what = "responses validated" if keys is not None else "requests accepted"
+    r1, d1 = HP.rate(flat, off, k, 1, seconds)
+    threads, how = cpu_threads()
+    rn, dn = HP.rate(flat, off, k, threads, max(1.0, seconds / 2))
+    one = {"value": round(r1 / 1e6, 4), "unit": "M handshakes/s", "cores": 1, "kind": "port",
+           "sample": f"{d1} {what} by the compiled C port (oracle/handshake_port.c: HttpUtils framing, "
+                     f"HandshakeFactory.parse, Handshaker checks, SHA-1 + Base64, response format) over {m} "
+                     f"distinct {L}-B buffers, 1 thread; no JDK on the box"}
+    mt = {"value": round(rn / 1e6, 4), "unit": "M handshakes/s", "cores": threads, "kind": "port", "cores_from": how,
+          "sample": f"{dn} {what} by the same port on {threads} threads"}
+    return one, mt
+
+
 def handshake_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
     """Server opening handshakes (wsg_handshake_accept_batch_device)
     over a device-resident connection storm: n browser-like upgrade requests, random keys.
     One lane per request: the bound is per-lane serial parsing + SHA-1, reported against
-    HBM for scale.  cpu_baseline: the Python restatement (oracle/handshake_oracle.py) on
-    one host core (no JDK on the box)."""
+    HBM for scale.  cpu_baseline: the compiled C port (oracle/handshake_port.c) on one host
+    core, beside it on the job's cores and the Python restatement (oracle/handshake_oracle.py)
+    on one core (no JDK on the box)."""
     import base64
     import numpy as np
     import torch
@@ -861,6 +885,7 @@ def handshake_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
         H.accept(buf[done % n].tobytes())
         done += 1
     t = time.perf_counter() - t0
+    port1, portn = _hs_port_baselines(buf, n, L)
     return {"config": f"server handshake: {n} upgrade requests of {L} B (browser-like, random keys), "
                       "HandshakeDecoder + Handshaker.accept + 101 response with Sec-WebSocket-Accept",
             "value": round(n * steps / el / 1e6, 3), "unit": "M handshakes/s",
@@ -869,9 +894,11 @@ def handshake_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
                          "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
                          "avg_launch_ms": round(kms, 4)},
-            "cpu_baseline": {"value": round(done / t / 1e6, 5), "unit": "M handshakes/s", "cores": 1, "kind": "port",
-                             "sample": f"{done} requests through the Python restatement "
-                                       f"(oracle/handshake_oracle.py) in {t:.1f} s, 1 thread; no JDK on the box"},
+            "cpu_baseline": port1, "cpu_baseline_threads": portn,
+            "cpu_baseline_python": {"value": round(done / t / 1e6, 5), "unit": "M handshakes/s", "cores": 1,
+                                    "kind": "port",
+                                    "sample": f"{done} requests through the Python restatement "
+                                              f"(oracle/handshake_oracle.py) in {t:.1f} s, 1 thread"},
             "pipeline_ms": pipe}
 
 
@@ -994,7 +1021,8 @@ def handshake_client_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
     """Client opening handshakes (wsg_handshake_validate_batch_device): n servers'
     101 responses, each validated against the key its session sent (HandshakeDecoder
     in client mode + Handshaker.validate).  One lane per response.  cpu_baseline: the
-    Python restatement on one host core (no JDK on the box)."""
+    compiled C port on one host core, beside it on the job's cores and the Python
+    restatement on one core (no JDK on the box)."""
     import base64
     import numpy as np
     import torch
@@ -1036,6 +1064,7 @@ def handshake_client_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
         H.validate(buf[done % n].tobytes(), keys[done % n].decode())
         done += 1
     t = time.perf_counter() - t0
+    port1, portn = _hs_port_baselines(buf, n, L, keys=k24)
     return {"config": f"client handshake: {n} server responses of {L} B (101, random keys), "
                       "HandshakeDecoder(clientMode) + Handshaker.validate (key challenge, basic fields)",
             "value": round(n * steps / el / 1e6, 3), "unit": "M handshakes/s",
@@ -1044,9 +1073,11 @@ def handshake_client_line(ctx, dev, steps, warmup, n=1 << 20, cpu_seconds=2.0):
                          "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(ach / HBM_PEAK_GBS, 4), "alg_bytes_per_launch": alg,
                          "avg_launch_ms": round(kms, 4)},
-            "cpu_baseline": {"value": round(done / t / 1e6, 5), "unit": "M handshakes/s", "cores": 1, "kind": "port",
-                             "sample": f"{done} responses through the Python restatement "
-                                       f"(oracle/handshake_oracle.py) in {t:.1f} s, 1 thread; no JDK on the box"},
+            "cpu_baseline": port1, "cpu_baseline_threads": portn,
+            "cpu_baseline_python": {"value": round(done / t / 1e6, 5), "unit": "M handshakes/s", "cores": 1,
+                                    "kind": "port",
+                                    "sample": f"{done} responses through the Python restatement "
+                                              f"(oracle/handshake_oracle.py) in {t:.1f} s, 1 thread"},
             "pipeline_ms": pipe}
 
 
