@@ -377,7 +377,9 @@ def main():
                               # the same sessions streaming 4x longer: the burst line's pipeline
                               # fill and drain amortised over ~20 flushes
                               ("native_batcher_stages_steady", "e2e_stages_steady"),
-                              ("native_encode_batcher", "e2e_encode"), ("native_batcher_aggregate", "e2e_aggregate")):
+                              ("native_encode_batcher", "e2e_encode"), ("native_batcher_aggregate", "e2e_aggregate"),
+                              # 1, 2 and 4 loops of one process on one device (the JVM's shape)
+                              ("native_batcher_stages_multi_loop", "e2e_stages_multi")):
                 e2e[key] = child_line(line)
         extras = [config0_line()] + measure_extras(ctx, dev, args)
 
@@ -1160,6 +1162,92 @@ def e2e_stages_line(ctx, dev, K, W, n_s=4096, msgs=16, msg_bytes=4096, chunk=819
             "api": "wsg_batcher_feed_many + wsg_batcher_flush_async/wait with wsg_batcher_set_stages"}
 
 
+def e2e_stages_multi_line(ctx, dev, K, W, loops=(1, 2, 4), n_s=4096, msgs=16, msg_bytes=4096, chunk=8192):
+    """The deployment shape the single-batcher lines avoid: L selector loops of one process on
+    one device (WsgDevices puts them there when the node has fewer GPUs than loops), each with
+    its own batcher, stage chain and context streams, driven from its own thread, the sessions
+    split over the loops.  Each loop runs e2e_stages' round pattern over its sessions; value:
+    inflated bytes of all loops / the wall time from the common start to the last loop's end,
+    at the default GPU_MAX_HW_QUEUES."""
+    import threading
+    import numpy as np
+    import torch
+    import snf4j_amd
+    from benchsupport.synth import deflate_wire
+    wire_np, starts, plain = deflate_wire(0x1F1A, n_s, msgs, msg_bytes)
+    h_wire = torch.from_numpy(wire_np).pin_memory()
+    base = h_wire.numpy().ctypes.data
+    out = {}
+    for L in loops:
+        per = n_s // L
+        loops_state = []
+        for li in range(L):
+            s0, s1 = li * per, (li + 1) * per
+            pos, endv = starts[s0:s1].copy(), starts[s0 + 1:s1 + 1].copy()
+            rounds = []
+            while (pos < endv).any():
+                live = np.nonzero(pos < endv)[0]
+                ln = np.minimum(endv[live] - pos[live], chunk)
+                rounds.append((live.astype(np.uint32), (base + pos[live]).astype(np.uint64), ln.astype(np.uint64)))
+                pos[live] += chunk
+            pctx = snf4j_amd.Context(dev.index, stream=torch.cuda.Stream(dev))
+            apply_tuning(pctx)
+            nb = snf4j_amd.NativeBatcher(per, clientMode=False, allowExtensions=True, maxPayloadLen=1 << 20, ctx=pctx)
+            nb.set_stages(inflate=True, noContext=False, validate=True)
+            max_wire = max(int(lens.sum()) for _, _, lens in rounds) + per * (msg_bytes + 64)
+            max_frames = per * (chunk // 64 + 2)
+            nb.reserve(max_wire, max_frames)
+            nb.reserve_stages(4 * max_wire, max_frames)
+            loops_state.append((pctx, nb, rounds))
+
+        def run(li, res):
+            _, nb, rounds = loops_state[li]
+            pending, ob = 0, 0
+            for sids, ptrs, lens in rounds:
+                nb.feed_many_ptrs(sids, ptrs, lens)
+                if pending == BATCHER_MAX_INFLIGHT:
+                    _, descb, _, resb, _ = nb.wait_raw()
+                    assert int(resb["error"].max()) == 0
+                    ob += int(descb["payload_len"].astype(np.int64).sum())
+                    pending -= 1
+                nb.flush_async()
+                pending += 1
+            while pending:
+                _, descb, _, resb, _ = nb.wait_raw()
+                assert int(resb["error"].max()) == 0
+                ob += int(descb["payload_len"].astype(np.int64).sum())
+                pending -= 1
+            res[li] = ob
+
+        times = []
+        for rep in range(W + K):
+            for _, nb, _ in loops_state:
+                for s in range(per):
+                    nb.reset_session(s)
+            res = [0] * L
+            ts = [threading.Thread(target=run, args=(li, res)) for li in range(L)]
+            t0 = time.perf_counter()
+            for t in ts:
+                t.start()
+            for t in ts:
+                t.join()
+            t = time.perf_counter() - t0
+            assert sum(res) == plain, (sum(res), plain)
+            if rep >= W:
+                times.append(t)
+        for pctx, nb, _ in loops_state:
+            nb.close()
+            pctx.close()
+        t = sorted(times)[len(times) // 2]
+        out[str(L)] = {"GiB_per_s": round(plain / t / 2**30, 3), "ms_per_batch": round(t * 1e3, 3),
+                       "sessions_per_loop": per}
+    return {"config": f"native batcher + stages (inflate -> validator) on L loops of one process on one device, "
+                      f"{n_s} sessions split over the loops, {msgs} compressed TEXT messages x {msg_bytes} B each, "
+                      f"{chunk} B reads, each loop its own thread / batcher / stage chain / streams",
+            "unit": "GiB/s (inflated bytes, host to host)", "loops": out,
+            "gpu_max_hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default")}
+
+
 def e2e_encode_line(ctx, dev, K, W, n_s=64, msg_bytes=16 << 20, frame=65536, per_round=16):
     """The native encode batcher host to host on configs[4]'s shape (64 client sessions,
     a 16 MiB message each in 64 KiB fragments, FrameEncoder.java:69-120): per round
@@ -1298,6 +1386,7 @@ EXTRA_LINES = {"configs1": line_configs1, "configs3": line_configs3, "configs2":
                "encode": line_encode, "validator": line_validator, "e2e_stages": e2e_stages_line,
                "e2e_stages_steady": lambda ctx, dev, K, W: e2e_stages_line(ctx, dev, K, W, msgs=64),
                "e2e_encode": e2e_encode_line, "e2e_aggregate": e2e_aggregate_line,
+               "e2e_stages_multi": e2e_stages_multi_line,
                "inflate": lambda ctx, dev, K, W: inflate_line(ctx, dev, K, W),
                "deflate": lambda ctx, dev, K, W: deflate_line(ctx, dev, K, W),
                "handshake": lambda ctx, dev, K, W: handshake_line(ctx, dev, K, W),
