@@ -190,9 +190,11 @@ class LoopEncodeBatcher:
     """WsgBatcher's encode side: write(sid, wire bytes) on the loop thread."""
 
     def __init__(self, loop, n_sessions: int, write, clientMode: bool = True, ctx=None,
-                 max_frames: int = 0, max_payload: int = 0):
+                 max_frames: int = 0, max_payload: int = 0, deflate: tuple | None = None):
         self.loop = loop
         self.eb = EncodeBatcher(n_sessions, clientMode, ctx=ctx)
+        if deflate is not None:  # (level, noContext): WsgBatcher.EncNative's wsg_enc_batcher_set_deflate
+            self.eb.set_deflate(*deflate)
         if max_frames:
             self.eb.reserve(max_frames, max_payload)
         self.write = write
