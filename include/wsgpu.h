@@ -183,7 +183,9 @@ int wsg_close(wsg_ctx* ctx);
  *                            sums in k_agg_b / k_agg_c (default: as many as LDS allows, 3,072);
  *                            larger ones run k_agg_scan (0 forces it: the tests' way to reach it)
  *   WSG_TUNE_STAGE_FAIL      n > 0: the n-th stage-chain step a batcher on this context begins from now
- *                            fails as a device error would (tests of the error path) */
+ *                            fails as a device error would (tests of the error path)
+ *   WSG_TUNE_DEFLATE_LDS     0: the deflate match search walks every chain in global memory (the
+ *                            LDS-resident walk of a session's window is the default; tests, A/B) */
 enum {
     WSG_TUNE_INFLATE_TOKENS = 1,
     WSG_TUNE_INFLATE_FAST = 2,
@@ -197,7 +199,8 @@ enum {
     WSG_TUNE_INFLATE_SPLIT = 10,
     WSG_TUNE_AGG_FOLD_MAX = 11,
     WSG_TUNE_DEFLATE_SERIAL = 12,
-    WSG_TUNE_STAGE_FAIL = 13
+    WSG_TUNE_STAGE_FAIL = 13,
+    WSG_TUNE_DEFLATE_LDS = 14
 };
 int wsg_set_tuning(wsg_ctx* ctx, int key, int64_t value);
 /* Use `stream` for all later work (NULL = the null stream); a private stream is synchronised and destroyed. */

@@ -73,7 +73,8 @@ class Context:
 
     TUNING = {"inflate_tokens": 1, "inflate_fast": 2, "inflate_lds": 3, "inflate_order": 4, "inflate_lanes": 5,
               "fused_scan": 6, "agg_units": 7, "agg_grid": 8, "inflate_tabs": 9, "inflate_split": 10,
-              "agg_fold_max": 11, "deflate_serial": 12, "stage_fail": 13}
+              "agg_fold_max": 11, "deflate_serial": 12, "stage_fail": 13,
+              "deflate_lds": 14}
 
     def set_tuning(self, name: str, value: int):
         """A measurement / test switch of this context (wsg_set_tuning; wsgpu.h lists them)."""

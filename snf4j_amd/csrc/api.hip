@@ -22,7 +22,7 @@ const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link", 
                                            "k_final",    "k_enc_len",  "k_enc_scan",
                                            "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate",
                                            "k_defl_plan", "k_defl_prep", "k_defl_match", "k_defl_parse", "k_defl_final", "k_defl_serial",
-                                           "k_defl_trees", "k_defl_emit", "k_defl_hist"};
+                                           "k_defl_trees", "k_defl_emit", "k_defl_hist", "k_defl_match_lds"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -81,6 +81,7 @@ struct wsg_ctx {
       d_blocks;
   int defl_serial = 0;               // WSG_TUNE_DEFLATE_SERIAL 1: zlib's loop per session at every level (tests)
   int64_t stage_fail = 0;            // WSG_TUNE_STAGE_FAIL n: the n-th stage step from now fails (tests)
+  int defl_lds = 1;                  // WSG_TUNE_DEFLATE_LDS 0: the match search in global memory only
   // measurement / test switches (wsg_set_tuning; the defaults are the product)
   int infl_tokens = 1;               // WSG_TUNE_INFLATE_TOKENS 0: no lane pre-decode (serial decoder only)
   uint32_t infl_lanes = 262144;      // WSG_TUNE_INFLATE_LANES: k_infl_tok lanes at most
@@ -160,7 +161,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL && kid != K_DEFL_TREES &&
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL && kid != K_DEFL_TREES && kid != K_DEFL_MATCH_LDS &&
                                  kid != K_DEFL_EMIT && kid != K_DEFL_HIST)) {
     f();
     return;
@@ -196,6 +197,7 @@ void ctx_copy_tuning(wsg_ctx* dst, const wsg_ctx* src) {
   dst->agg_grid = src->agg_grid;
   dst->agg_fold = src->agg_fold;
   dst->defl_serial = src->defl_serial;
+  dst->defl_lds = src->defl_lds;
 }
 int ctx_device(wsg_ctx* c) { return c->device; }
 // the batcher's two-phase inflate applies (the pre-decode on, the split-lane decode off)
@@ -287,6 +289,7 @@ int wsg_set_tuning(wsg_ctx* c, int key, int64_t value) {
     case WSG_TUNE_AGG_GRID: c->agg_grid = value < 1 ? 1u : (value > (1 << 24) ? (1u << 24) : (uint32_t)value); break;
     case WSG_TUNE_DEFLATE_SERIAL: c->defl_serial = value != 0; break;
     case WSG_TUNE_STAGE_FAIL: c->stage_fail = value < 0 ? 0 : value; break;
+    case WSG_TUNE_DEFLATE_LDS: c->defl_lds = value != 0; break;
     case WSG_TUNE_AGG_FOLD_MAX: c->agg_fold = value < 0 ? 0u : (value > 0xFFFFFFFFll ? 0xFFFFFFFFu : (uint32_t)value); break;
     default: return set_err(c, WSG_API_EINVAL, "unknown tuning key");
   }
@@ -1169,6 +1172,7 @@ int deflate_launch(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* 
   a.level = level;
   a.no_context = no_context ? 1 : 0;
   a.serial = (level >= 1 && level <= 3) || (level >= 4 && c->defl_serial) ? 1 : 0;
+  a.match_lds = c->defl_lds;
   a.desc = desc;
   a.n_frames = n_frames;
   a.session_first = session_first;
@@ -1209,9 +1213,8 @@ int deflate_launch(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* 
     timed(c, K_DEFL_SERIAL, [&] { launch_defl_serial(a, c->stream); });
     return WSG_API_OK;
   }
-  a.n_lanes = (uint32_t)(F < 65536 ? F : 65536);
-  HIP_TRY(c, c->d_tw.ensure(a.n_lanes * twb));
-  a.tw = c->d_tw.p;
+  // a parse lane a frame (the lanes are latency-bound: 65536 of them were one wave a SIMD)
+  a.n_lanes = (uint32_t)(F < (1u << 22) ? F : (1u << 22));
   if (level >= 4) {
     HIP_TRY(c, c->d_S.ensure(tot[0] + 64));
     HIP_TRY(c, c->d_link.ensure((tot[0] + 64) * sizeof(uint16_t)));
@@ -1231,7 +1234,10 @@ int deflate_launch(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* 
     a.sym = (uint32_t*)c->d_sym.p;
     a.blocks = (DeflBlock*)c->d_blocks.p;
     timed(c, K_DEFL_PREP, [&] { launch_defl_prep(a, c->stream); });
-    if (tot[3]) timed(c, K_DEFL_MATCH, [&] { launch_defl_match(a, c->stream); });
+    if (tot[3]) {
+      if (a.match_lds) timed(c, K_DEFL_MATCH_LDS, [&] { launch_defl_match_lds(a, c->stream); });
+      timed(c, K_DEFL_MATCH, [&] { launch_defl_match(a, c->stream); });
+    }
   }
   timed(c, K_DEFL_PARSE, [&] { launch_defl_parse(a, c->stream); });
   if (level >= 4) {

@@ -34,6 +34,15 @@ constexpr int32_t HNONE = INT32_MIN;
 __device__ inline uint32_t java_bound(uint32_t len) { return len + ((len + 7) >> 3) + ((len + 63) >> 6) + 15; }
 __device__ inline uint64_t r16(uint64_t x) { return (x + 15) & ~15ull; }
 
+// the match chunks of a frame k_defl_match takes: all of them, or with the LDS walk
+// (k_defl_match_lds) on and the frame short enough for its ring, those from the first one
+// holding a position of the frame's last 266 (the fast range [0, len - 266) is the ring's)
+__device__ inline uint32_t chunk_first(const DeflArgs& a, uint32_t len) {
+  if (!a.match_lds || len > DEFL_LDS_MAXLEN || len < 267) return 0;
+  return (len - 266) / DEFL_CH;
+}
+__device__ inline uint32_t chunk_count(uint32_t len) { return len > 2 ? (len - 2 + DEFL_CH - 1) / DEFL_CH : 0; }
+
 __device__ inline void wave_mem_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
@@ -107,7 +116,7 @@ __global__ __launch_bounds__(64) void k_defl_plan(DeflArgs a) {
         yrel += (len + 3) & ~3u;   // every block's symbols, back to back (a symbol covers >= 1 byte)
         f.blk_rel = brel;
         brel += defl_blk_cap(len);
-        chunks += (len > 2 ? (len - 2 + DEFL_CH - 1) / DEFL_CH : 0) + ((fl & DF_TAIL_OK) ? 1 : 0);
+        chunks += chunk_count(len) - chunk_first(a, len) + ((fl & DF_TAIL_OK) ? 1 : 0);
         srel += len;
       }
       last = k;
@@ -312,6 +321,27 @@ __device__ void block_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
   copy_pieces(dst, src, n, threadIdx.x, blockDim.x);
 }
 
+// for i in [lo, hi) by the workgroup: v = ld(i) for eight of a thread's indices, then
+// st(i, v) for them — the loads in flight together instead of one load, its wait and its
+// store an index (the session-sized loops of k_defl_prep were a global load latency each)
+template <class LD, class ST>
+__device__ void batched_for(uint32_t lo, uint32_t hi, LD ld, ST st) {
+  const uint32_t T = blockDim.x;
+  for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * T) {
+    uint32_t v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t i = i0 + j * T;
+      v[j] = i < hi ? ld(i) : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t i = i0 + j * T;
+      if (i < hi) st(i, v[j]);
+    }
+  }
+}
+
 // window walk of one segment, wave 1: zlib's window image through the segment's calls
 // (slides, reads, zeroing) and each frame's strips (window bytes after its end, before and
 // after a slide there)
@@ -371,8 +401,8 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
       const uint32_t fl = a.fflags[k];
       if ((fl & DF_KIND) != PMD_CALL) continue;
       const uint32_t len = a.ff[k].len;
-      const uint32_t nch = len > 2 ? (len - 2 + DEFL_CH - 1) / DEFL_CH : 0;
-      for (uint32_t i = 0; i < nch; i++) a.chunks[c++] = (uint64_t)k | (uint64_t)i << 32;
+      const uint32_t nch = chunk_count(len);
+      for (uint32_t i = chunk_first(a, len); i < nch; i++) a.chunks[c++] = (uint64_t)k | (uint64_t)i << 32;
       if (fl & DF_TAIL_OK) a.chunks[c++] = (uint64_t)k | 1ull << 63;
     }
   }
@@ -408,21 +438,27 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
     __syncthreads();
     // 2. links of the hashed history strings (zlib's prev[]); the hash heads
     if (!fresh)
-      for (uint32_t p = DEFL_HIST - H + tid; p < DEFL_HIST - ins0; p += blockDim.x) {
-        const uint32_t w = (uint32_t)((int32_t)p - base0);
-        const uint32_t pv = prev[w & zd::WMASK];
-        link[p] = (uint16_t)((pv != 0 && w - pv < (uint32_t)zd::WSIZE) ? w - pv : 0);
-      }
-    for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x)
-      hpos[h] = (fresh || head[h] == 0) ? HNONE : (int32_t)head[h] + base0;
+      batched_for(
+          DEFL_HIST - H, DEFL_HIST - ins0,
+          [&](uint32_t p) { return (uint32_t)prev[(uint32_t)((int32_t)p - base0) & zd::WMASK]; },
+          [&](uint32_t p, uint32_t pv) {
+            const uint32_t w = (uint32_t)((int32_t)p - base0);
+            link[p] = (uint16_t)((pv != 0 && w - pv < (uint32_t)zd::WSIZE) ? w - pv : 0);
+          });
+    if (fresh) {
+      for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x) hpos[h] = HNONE;
+    } else {
+      batched_for(0, zd::WSIZE, [&](uint32_t h) { return (uint32_t)head[h]; },
+                  [&](uint32_t h, uint32_t v) { hpos[h] = v == 0 ? HNONE : (int32_t)v + base0; });
+    }
     __syncthreads();
     // 3. the slides of this batch applied to the prev entries no string of it replaces
     if (persist && !fresh && base_final != base0)
-      for (uint32_t j = tid; j < (uint32_t)zd::WSIZE; j += blockDim.x) {
-        const uint32_t v = prev[j];
-        const int32_t nv = v ? (int32_t)v + base0 - base_final : 0;
-        prev[j] = (uint16_t)(nv > 0 ? nv : 0);
-      }
+      batched_for(0, zd::WSIZE, [&](uint32_t j) { return (uint32_t)prev[j]; },
+                  [&](uint32_t j, uint32_t v) {
+                    const int32_t nv = v ? (int32_t)v + base0 - base_final : 0;
+                    prev[j] = (uint16_t)(nv > 0 ? nv : 0);
+                  });
     __syncthreads();
     // 4. links (wave 0) beside the window walk (wave 1)
     if (wv == 0) {
@@ -447,17 +483,6 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
 }
 
 // ------------------------------------------------------------------ k_defl_match
-struct StripBytes {
-  const uint8_t* S;
-  uint32_t end;
-  const uint8_t* strip;
-  __device__ uint32_t operator()(uint32_t p) const { return p < end ? S[p] : strip[p - end]; }
-};
-struct LinkAcc {
-  const uint16_t* l;
-  __device__ uint32_t operator()(uint32_t p) const { return l[p]; }
-};
-
 __device__ inline uint64_t load_u64(const uint8_t* p) {
   uint64_t v;
   __builtin_memcpy(&v, p, 8);   // unaligned global load
@@ -536,6 +561,294 @@ __device__ inline void fast_result(const FastWalk& w, const zd::Cfg& c, uint32_t
   *quarter = w.k <= (uint32_t)(c.chain >> 2) ? f : w.qres;
 }
 
+// ------------------------------------------------------------------ k_defl_match_lds
+// The match search of a session's frames out of LDS (round 6): k_defl_match's chain walks
+// are random 8-B and 2-B gathers from L2, one request a lane a candidate, and the texture
+// path's gather rate bounds them (PMC: 97% L2 hits, the waves waiting 61% of their
+// cycles).  Here one 1024-thread workgroup a session holds a ring of DEFL_RING stream
+// positions (bytes and links, 144 KiB) and walks every chain in LDS.  A phase loads the
+// window of a run of consecutive frames (from MAX_DIST before the first one's start to the
+// last one's end, DEFL_RING at most), then the lanes take the run's fast positions (a scan
+// that stays inside its frame: p + 266 <= end) from an LDS counter, two at a time a lane,
+// and write the results of each straight to the result array (no global load follows:
+// the walk's loads are LDS).  Positions nearer a frame's end, the tail variants, and frames
+// longer than DEFL_LDS_MAXLEN stay with k_defl_match.
+struct LdsRing {
+  uint32_t bytes[(DEFL_RING + 16) / 4];   // position x at byte x % DEFL_RING; words 0..3 mirrored past the end
+  uint16_t link[DEFL_RING];
+  uint32_t next;                           // the run's position dispenser
+  uint32_t nfr;                            // frames of the run with a fast range
+  uint32_t fr_lo[8], fr_pre[9];            // their first fast position, prefix of fast-range lengths
+};
+static_assert(sizeof(LdsRing) <= 160 * 1024, "the ring fits the LDS");
+
+__device__ inline uint64_t ring8(const LdsRing& R, uint32_t x) {   // stream bytes x .. x + 7
+  const uint32_t r = x % DEFL_RING, w = r >> 2, sh = r & 3;
+  const uint32_t w0 = R.bytes[w], w1 = R.bytes[w + 1], w2 = R.bytes[w + 2];
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  return (uint64_t)hi << 32 | lo;
+}
+__device__ inline uint32_t ring1(const LdsRing& R, uint32_t x) {
+  const uint32_t r = x % DEFL_RING;
+  return (R.bytes[r >> 2] >> (8 * (r & 3))) & 0xff;
+}
+
+// one candidate of the walk at position p (FastWalk over the ring); true when the walk is over
+__device__ inline bool ring_step(FastWalk& w, const LdsRing& R, uint32_t p, const zd::Cfg& c) {
+  const uint32_t qbudget = c.chain >> 2;
+  const uint64_t x = ring8(R, w.q) ^ w.b;
+  const uint32_t l = R.link[w.q % DEFL_RING];
+  if ((x & 0xFFFF) == 0) {
+    const bool cand = w.best < 8 ? ((x >> (8 * w.best)) & 0xFF) == 0 : ring1(R, w.q + w.best) == ring1(R, p + w.best);
+    if (cand) {
+      uint32_t len;
+      if (x) {
+        len = (uint32_t)__builtin_ctzll(x) >> 3;
+      } else {
+        len = 8;
+        for (;;) {
+          const uint64_t y = ring8(R, w.q + len) ^ ring8(R, p + len);
+          if (y) {
+            len += (uint32_t)__builtin_ctzll(y) >> 3;
+            break;
+          }
+          len += 8;
+          if (len >= (uint32_t)zd::MAX_MATCH) break;
+        }
+        if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
+      }
+      if (len > w.best) {
+        w.best = len;
+        w.best_d = w.dist;
+        if (len >= c.nice) return true;
+      }
+    }
+  }
+  if (w.k == qbudget) w.qres = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
+  if (w.k >= c.chain) return true;
+  if (l == 0) return true;
+  w.dist += l;
+  if (w.dist >= (uint32_t)zd::MAX_DIST) return true;
+  w.q -= l;
+  w.k++;
+  return false;
+}
+
+__device__ inline void ring_init(FastWalk& w, const LdsRing& R, uint32_t p) {
+  const uint32_t d = R.link[p % DEFL_RING];
+  w.k = 1;
+  w.best = 2;
+  w.best_d = 0;
+  w.qres = 0;
+  w.dist = d;
+  w.q = p - d;
+  w.done = d == 0 || d > (uint32_t)zd::MAX_DIST;
+  w.b = ring8(R, p);
+}
+
+// a frame's fast range: [start, end - 266) when the frame takes the LDS walk
+__device__ inline bool lds_frame(const DeflFrame& f) { return f.len <= DEFL_LDS_MAXLEN; }
+
+__global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
+  __shared__ LdsRing R;
+  const uint32_t s = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const DeflSess fs = a.fs[s];
+  if (fs.last_call == ~0u) return;
+  Sums sm(a);
+  const uint64_t soff = sm.S[s];
+  const uint32_t* Sw = (const uint32_t*)(a.S + soff);   // (S regions are 16-B aligned)
+  const uint16_t* link = a.link + soff;
+  uint32_t* res = a.res + 2 * soff;
+  const zd::Cfg cfg = zd::level_cfg(a.level);
+  const uint32_t k0 = a.session_first[s], k1 = a.session_first[s + 1];
+  uint32_t lo_loaded = 0, hi_loaded = 0;   // stream positions the ring holds: [lo, hi)
+  uint32_t k = k0;
+  for (;;) {
+    // the run: consecutive LDS frames whose window fits the ring
+    while (k < k1 && ((a.fflags[k] & DF_KIND) != PMD_CALL || !lds_frame(a.ff[k]))) k++;
+    if (k >= k1) break;
+    const DeflFrame f0 = a.ff[k];
+    const uint32_t need_lo = f0.s_rel > (uint32_t)zd::MAX_DIST ? f0.s_rel - zd::MAX_DIST : 0;
+    uint32_t run_end = f0.s_rel + f0.len, kn = k + 1, nfr = 0;
+    uint32_t lo8[8], pre8[9];
+    pre8[0] = 0;
+    {
+      const uint32_t e0 = f0.s_rel + f0.len;
+      if (e0 >= f0.s_rel + 267) {
+        lo8[0] = f0.s_rel;
+        pre8[1] = f0.len - 266;
+        nfr = 1;
+      }
+    }
+    while (kn < k1 && nfr < 8) {
+      const uint32_t fl = a.fflags[kn];
+      if ((fl & DF_KIND) != PMD_CALL) {
+        kn++;
+        continue;
+      }
+      const DeflFrame f = a.ff[kn];
+      if (!lds_frame(f) || f.s_rel != run_end || f.s_rel + f.len - need_lo > DEFL_RING - 16) break;
+      if (f.len >= 267) {
+        lo8[nfr] = f.s_rel;
+        pre8[nfr + 1] = pre8[nfr] + f.len - 266;
+        nfr++;
+      }
+      run_end = f.s_rel + f.len;
+      kn++;
+    }
+    // load the window [need_lo, run_end): what the ring does not hold yet
+    const uint32_t from = (need_lo >= lo_loaded && need_lo <= hi_loaded) ? hi_loaded : need_lo;
+    __syncthreads();   // (the previous run's walks read the ring)
+    for (uint32_t wd = (from >> 2) + tid; wd < (run_end + 3) >> 2; wd += blockDim.x) {
+      const uint32_t v = Sw[wd];
+      const uint32_t r = (wd << 2) % DEFL_RING >> 2;
+      R.bytes[r] = v;
+      if (r < 4) R.bytes[DEFL_RING / 4 + r] = v;
+    }
+    for (uint32_t x = from + tid; x < run_end; x += blockDim.x) R.link[x % DEFL_RING] = link[x];
+    if (tid == 0) {
+      R.next = 0;
+      R.nfr = nfr;
+      for (uint32_t i = 0; i < nfr; i++) R.fr_lo[i] = lo8[i];
+      for (uint32_t i = 0; i <= nfr; i++) R.fr_pre[i] = pre8[i];
+    }
+    lo_loaded = need_lo;
+    hi_loaded = run_end;
+    k = kn;
+    __syncthreads();
+    const uint32_t total = pre8[nfr];
+    if (total == 0) continue;
+    // the walks: two a lane, refilled from the dispenser a wave at a time
+    auto pos_of = [&](uint32_t v) -> uint32_t {
+      uint32_t j = 0;
+      while (j + 1 < nfr && R.fr_pre[j + 1] <= v) j++;
+      return R.fr_lo[j] + (v - R.fr_pre[j]);
+    };
+    uint32_t base = 0;
+    if (lane == 0) base = atomicAdd(&R.next, 128u);
+    base = __shfl(base, 0);
+    uint32_t va = base + lane, vb = base + 64 + lane;
+    bool acta = va < total, actb = vb < total;
+    uint32_t pa = acta ? pos_of(va) : 0, pb = actb ? pos_of(vb) : 0;
+    FastWalk wa, wb;
+    uint32_t da = 0, db = 0;
+    if (acta) {
+      ring_init(wa, R, pa);
+      da = wa.dist;
+    }
+    if (actb) {
+      ring_init(wb, R, pb);
+      db = wb.dist;
+    }
+    while (__ballot(acta || actb)) {
+      bool fina = false, finb = false;
+      if (acta) fina = wa.done || ring_step(wa, R, pa, cfg);
+      if (actb) finb = wb.done || ring_step(wb, R, pb, cfg);
+      if (fina) {
+        uint32_t full, quarter;
+        fast_result(wa, cfg, da, &full, &quarter);
+        *(uint2*)(res + 2 * (uint64_t)pa) = make_uint2(full, quarter);
+      }
+      if (finb) {
+        uint32_t full, quarter;
+        fast_result(wb, cfg, db, &full, &quarter);
+        *(uint2*)(res + 2 * (uint64_t)pb) = make_uint2(full, quarter);
+      }
+      const uint64_t ma = __ballot(fina), mb = __ballot(finb);
+      const uint32_t na = (uint32_t)__builtin_popcountll(ma), nb = (uint32_t)__builtin_popcountll(mb);
+      if (na + nb) {
+        uint32_t b2 = 0;
+        if (lane == 0) b2 = atomicAdd(&R.next, na + nb);
+        b2 = __shfl(b2, 0);
+        if (fina) {
+          va = b2 + (uint32_t)__builtin_popcountll(ma & ((1ull << lane) - 1));
+          acta = va < total;
+          if (acta) {
+            pa = pos_of(va);
+            ring_init(wa, R, pa);
+            da = wa.dist;
+          }
+        }
+        if (finb) {
+          vb = b2 + na + (uint32_t)__builtin_popcountll(mb & ((1ull << lane) - 1));
+          actb = vb < total;
+          if (actb) {
+            pb = pos_of(vb);
+            ring_init(wb, R, pb);
+            db = wb.dist;
+          }
+        }
+      }
+    }
+  }
+}
+
+// longest_match at a position of a frame's last bytes, whose compares may pass the frame's
+// end into its strip (zd::match_at's walk, 8 bytes a compare where they lie before the end)
+__device__ inline uint64_t tail8(const uint8_t* S, const uint8_t* strip, uint32_t end, uint32_t x) {
+  if (x + 8 <= end) return load_u64(S + x);
+  uint64_t v = 0;
+  for (uint32_t i = 0; i < 8; i++) {
+    const uint32_t y = x + i;
+    const uint64_t b = y < end ? S[y] : (y - end < (uint32_t)zd::STRIP ? strip[y - end] : 0u);
+    v |= b << (8 * i);
+  }
+  return v;
+}
+__device__ void tail_match_at(const uint8_t* S, const uint8_t* strip, const uint16_t* link, uint32_t s, uint32_t end,
+                              const zd::Cfg& c, uint32_t* out_full, uint32_t* out_quarter) {
+  const uint32_t d = link[s];
+  if (d == 0 || d > (uint32_t)zd::MAX_DIST) {
+    *out_full = *out_quarter = 0;
+    return;
+  }
+  const uint32_t flags = d == (uint32_t)zd::MAX_DIST ? (uint32_t)zd::MR_HEAD_AT_MAX : 0u;
+  const uint32_t nice = c.nice < end - s ? c.nice : end - s;
+  const uint32_t qbudget = c.chain >> 2;
+  const uint64_t b = tail8(S, strip, end, s);
+  uint32_t best = 2, best_d = 0, qres = 0, q = s - d, dist = d, k = 1;
+  for (;; k++) {
+    const uint64_t x = tail8(S, strip, end, q) ^ b;
+    if ((x & 0xFFFF) == 0) {
+      const bool cand = best < 8 ? ((x >> (8 * best)) & 0xFF) == 0
+                                 : (tail8(S, strip, end, q + best) & 0xFF) == (tail8(S, strip, end, s + best) & 0xFF);
+      if (cand) {
+        uint32_t len;
+        if (x) {
+          len = (uint32_t)__builtin_ctzll(x) >> 3;
+        } else {
+          len = 8;
+          for (;;) {
+            const uint64_t y = tail8(S, strip, end, q + len) ^ tail8(S, strip, end, s + len);
+            if (y) {
+              len += (uint32_t)__builtin_ctzll(y) >> 3;
+              break;
+            }
+            len += 8;
+            if (len >= (uint32_t)zd::MAX_MATCH) break;
+          }
+          if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
+        }
+        if (len > best) {
+          best = len;
+          best_d = dist;
+          if (len >= nice) break;
+        }
+      }
+    }
+    if (k == qbudget) qres = best > 2 ? ((best - 2) | best_d << 9) : 0;
+    if (k >= c.chain) break;
+    const uint32_t l = link[q];
+    if (l == 0) break;
+    dist += l;
+    if (dist >= (uint32_t)zd::MAX_DIST) break;
+    q -= l;
+  }
+  const uint32_t full = best > 2 ? ((best - 2) | best_d << 9) : 0;
+  *out_full = full | flags;
+  *out_quarter = k <= qbudget ? full : qres;
+}
+
 __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
   // a chunk's results are kept in LDS and written at its end: a global store would make
   // every later load of the wave wait for it (loads and stores share vmcnt)
@@ -567,7 +880,8 @@ __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
     const uint32_t p1 = var ? end - 2 : (p0 + DEFL_CH < end - 2 ? p0 + DEFL_CH : end - 2);
     // positions whose scan stays inside the frame: the fast walk, lanes refilled as they finish
     const uint32_t pf = var ? p0 : (end >= 266 && end - 266 > p0 ? (end - 266 < p1 ? end - 266 : p1) : p0);
-    if (pf > p0) {
+    const bool in_lds = a.match_lds && !var && lds_frame(f);   // (its fast range: k_defl_match_lds)
+    if (pf > p0 && !in_lds) {
       uint32_t next = p0 + 64;
       uint32_t p = p0 + lane;
       bool act = p < pf;
@@ -600,16 +914,16 @@ __global__ __launch_bounds__(64) void k_defl_match(DeflArgs a) {
       }
     }
     // the frame's last bytes (and the tail variant): the scan may pass the end
-    StripBytes by{S, end, a.strips + ((uint64_t)k * 2 + (var ? 1 : 0)) * zd::STRIP};
+    const uint8_t* strip = a.strips + ((uint64_t)k * 2 + (var ? 1 : 0)) * zd::STRIP;
     for (uint32_t p = (pf > p0 ? pf : p0) + lane; p < p1; p += 64) {
       uint32_t full, quarter;
-      zd::match_at(by, LinkAcc{link}, p, end, cfg, &full, &quarter);
+      tail_match_at(S, strip, link, p, end, cfg, &full, &quarter);
       rs[p - p0] = make_uint2(full, quarter);
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     uint2* dst = var ? (uint2*)(a.tres + ((uint64_t)k * DEFL_TAILN + (p0 - tstart)) * 2) : (uint2*)(res + 2 * (uint64_t)p0);
-    for (uint32_t i = lane; i < p1 - p0; i += 64) dst[i] = rs[i];
+    for (uint32_t i = (in_lds ? pf - p0 : 0) + lane; i < p1 - p0; i += 64) dst[i] = rs[i];
     __builtin_amdgcn_wave_barrier();
   }
 }
@@ -930,7 +1244,7 @@ __device__ void send_tree_w(WordSink& o, const uint32_t* tab, int max_code, cons
 // sync marker, into the frame's zeroed output slot
 constexpr int EMIT_T = 256;
 __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
-  __shared__ uint32_t s_ltab[286], s_dtab[30];
+  __shared__ uint32_t s_ltab[286], s_dtab[30], s_btab[19];
   __shared__ uint32_t s_scan[EMIT_T];
   __shared__ uint32_t s_off;   // running bit offset of the frame
   Sums sm(a);
@@ -1005,9 +1319,10 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
         continue;
       }
       const bool is_static = type == 1;
-      if (!is_static) {
+      if (!is_static) {   // (thread 0's send_all_trees reads the three tables in turn: LDS, not global loads)
         for (uint32_t i = tid; i < B->lcodes; i += EMIT_T) s_ltab[i] = B->ltab[i];
         for (uint32_t i = tid; i < B->dcodes; i += EMIT_T) s_dtab[i] = B->dtab[i];
+        if (tid < 19) s_btab[tid] = B->btab[tid];
       }
       __syncthreads();
       // the symbols: a contiguous run a thread; bit offsets from a block-wide scan
@@ -1054,9 +1369,9 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
           ws.put((uint32_t)(lcodes - 257), 5);
           ws.put((uint32_t)(dcodes - 1), 5);
           ws.put((uint32_t)(blcodes - 4), 4);
-          for (int r = 0; r < blcodes; r++) ws.put(B->btab[zd::bl_order(r)] >> 16, 3);
-          send_tree_w(ws, s_ltab, lcodes - 1, B->btab);
-          send_tree_w(ws, s_dtab, dcodes - 1, B->btab);
+          for (int r = 0; r < blcodes; r++) ws.put(s_btab[zd::bl_order(r)] >> 16, 3);
+          send_tree_w(ws, s_ltab, lcodes - 1, s_btab);
+          send_tree_w(ws, s_dtab, dcodes - 1, s_btab);
         }
         ws.done();
       }
@@ -1193,6 +1508,9 @@ void launch_defl_match(const DeflArgs& a, hipStream_t s) {
   uint64_t g = a.chunk_cap < 262144 ? a.chunk_cap : 262144;
   g = (g + 7) & ~7ull;   // a multiple of the 8 XCDs (k_defl_match's chunk order)
   hipLaunchKernelGGL(k_defl_match, dim3((uint32_t)(g ? g : 8)), dim3(64), 0, s, a);
+}
+void launch_defl_match_lds(const DeflArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_defl_match_lds, dim3(a.n_sessions), dim3(1024), 0, s, a);
 }
 void launch_defl_parse(const DeflArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_defl_parse, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);

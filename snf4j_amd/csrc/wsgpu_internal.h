@@ -237,6 +237,8 @@ constexpr uint32_t DEFL_CH = 256;         // positions a k_defl_match wave takes
 constexpr uint32_t DEFL_TAILN = 264;      // positions whose match reads pass the frame's end
 constexpr uint32_t DEFL_HIST = 32768;     // S-region bytes before the first call (the history)
 constexpr uint32_t DEFL_PAD = 288;        // S-region bytes after the last call
+constexpr uint32_t DEFL_RING = 49152;     // k_defl_match_lds: stream positions its LDS ring holds
+constexpr uint32_t DEFL_LDS_MAXLEN = DEFL_RING - 32506 - 16;   // frames up to this long take the LDS walk
 
 struct DeflFrame {   // per CALL frame (k_defl_plan)
   uint32_t s_rel;    // S-region offset of the frame's first byte (stream position)
@@ -274,6 +276,7 @@ struct DeflSess {    // per session (k_defl_plan; k_defl_prep fills hw)
 
 struct DeflArgs {
   int32_t level, no_context, serial;
+  int32_t match_lds;        // k_defl_match_lds walks the frames up to DEFL_LDS_MAXLEN (their fast range)
   const wsg_frame_desc* desc;
   uint64_t n_frames;
   const uint32_t* session_first;
@@ -312,7 +315,7 @@ enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
   K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE,
   K_DEFL_PLAN, K_DEFL_PREP, K_DEFL_MATCH, K_DEFL_PARSE, K_DEFL_FINAL, K_DEFL_SERIAL, K_DEFL_TREES, K_DEFL_EMIT,
-  K_DEFL_HIST, K_COUNT
+  K_DEFL_HIST, K_DEFL_MATCH_LDS, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -389,6 +392,7 @@ int deflate_launch(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* 
 void launch_defl_plan(const DeflArgs& a, hipStream_t s);    // k_defl_plan + k_defl_scan
 void launch_defl_prep(const DeflArgs& a, hipStream_t s);
 void launch_defl_match(const DeflArgs& a, hipStream_t s);
+void launch_defl_match_lds(const DeflArgs& a, hipStream_t s);
 void launch_defl_parse(const DeflArgs& a, hipStream_t s);
 void launch_defl_hist(const DeflArgs& a, hipStream_t s, uint64_t n_blocks);
 void launch_defl_trees(const DeflArgs& a, hipStream_t s, uint64_t n_blocks);

@@ -249,3 +249,27 @@ def test_encode_batcher_deflate(ctx, oracle, level, nc):
         while pending:
             assert b.wait() == pending.pop(0), (level, nc, cm)
         b.close()
+
+
+@pytest.mark.parametrize("level", [5, 9])
+def test_match_paths_agree(level):
+    """The chain walks out of the LDS ring (k_defl_match_lds, the default) and all in global
+    memory (WSG_TUNE_DEFLATE_LDS 0): both byte-identical to zlib, over frames short enough for
+    the ring, ones too long for it (> DEFL_LDS_MAXLEN) between them, and runs the ring must
+    reload after a long frame."""
+    from snf4j_amd.context import Context
+    rng = np.random.default_rng(600 + level)
+    sessions = []
+    for s in range(12):
+        fr = []
+        for i in range(int(rng.integers(3, 12))):
+            n = int(rng.integers(17000, 40000)) if rng.random() < 0.2 else int(rng.integers(0, 9000))
+            fr.append((1 if i % 3 == 0 else 0, i % 3 == 2, 0, dh.text(rng, n)))
+        sessions.append(fr)
+    for lds in (1, 0):
+        c = Context(0, stream="own")
+        try:
+            c.set_tuning("deflate_lds", lds)
+            _check_batches(c, sessions, level, False, 2, rng)
+        finally:
+            c.close()
