@@ -191,48 +191,36 @@ __device__ inline uint32_t load_u32u(const uint8_t* p) {
 }
 
 // link pass of one segment, wave 0: strings [p_begin, p_last] in position order, 64 a
-// group, 8 groups a batch (the batch's stream words are loaded first and its links stored
-// last: a store before a load would hold the load, loads and stores sharing vmcnt).
-// A group's lanes atomicMax their position into the hash's LDS entry (hpos) and take the
-// value returned, the last position of the hash before them; a lane that sees a position
-// of its own group shares its hash inside the group, and such groups take their
-// predecessors by rank (peeled), or from the lane before for a run of one hash.
+// group, 8 groups a batch.  A group's lanes atomicMax their position into the hash's LDS
+// entry (hpos) and take the value returned: the last position of the hash before them,
+// or, for a hash that repeats inside the group, a position of the group, which the lane
+// then replaces by the nearest lane below with its hash (wave-local: hpos already holds the
+// group's last position of every hash, what the groups after it must see).  So a batch's
+// eight atomics go out back to back, nothing waiting on another's return; its stream words
+// are loaded first and its links stored last (a store before a load would hold the load,
+// loads and stores sharing vmcnt).
 constexpr int LINK_BATCH = 8;
 
-// a group with a hash that repeats inside it (kept out of line: rare): predecessors by rank
-__device__ __noinline__ int32_t link_repeats(int32_t* hpos, uint32_t h, int32_t p, bool part, int32_t g, int32_t r) {
+// the lanes of a group whose hash an earlier lane of the group has (r >= g): predecessor =
+// the nearest such lane below (positions are g + lane)
+__device__ __noinline__ int32_t link_repeats(uint32_t h, bool part, int32_t g, int32_t r) {
   const int lane = threadIdx.x & 63;
-  if (part && r < g) hpos[h] = r;   // the first lane of each hash saw the value before the group
-  const int32_t old = part ? hpos[h] : HNONE;
-  if (part) atomicMax(&hpos[h], p);
-  int32_t M = part ? hpos[h] : 0;
-  int32_t pr = old;
-  const uint64_t pm = __ballot(part);
-  const uint32_t h0 = __shfl(h, __builtin_ctzll(pm));
-  if (__ballot(part && h == h0) == pm) {   // one hash for the whole group (a run)
-    const bool prev_part = lane > 0 && ((pm >> (lane - 1)) & 1);
-    return prev_part ? p - 1 : old;
+  const uint64_t lt = (1ull << lane) - 1;
+  int32_t pr = r;
+  uint64_t todo = __ballot(part && r >= g);
+  while (todo) {
+    const uint32_t h0 = __shfl(h, __builtin_ctzll(todo));
+    const uint64_t set = __ballot(part && h == h0);
+    if (part && r >= g && h == h0) pr = g + (63 - __builtin_clzll(set & lt));
+    todo &= ~set;
   }
-  const bool top0 = part && M == p;
-  bool act = part;
-  while (__ballot(act)) {
-    const bool is_top = act && M == p;
-    const bool rem = act && !is_top;
-    if (act) hpos[h] = old;
-    if (rem) atomicMax(&hpos[h], p);
-    const int32_t M2 = act ? hpos[h] : 0;
-    if (is_top) pr = M2;
-    act = rem;
-    M = M2;
-  }
-  if (top0) hpos[h] = p;
   return pr;
 }
 __device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint16_t* prev, int32_t p_begin,
                           int32_t p_last, int32_t nil_pos, bool persist, int32_t base_final) {
   const int lane = threadIdx.x & 63;
   for (int32_t g0 = p_begin; g0 <= p_last; g0 += 64 * LINK_BATCH) {
-    uint32_t wv[LINK_BATCH];
+    uint32_t wv[LINK_BATCH], hh[LINK_BATCH];
     int32_t pred[LINK_BATCH];
 #pragma unroll
     for (int j = 0; j < LINK_BATCH; j++) {
@@ -240,17 +228,17 @@ __device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint1
       wv[j] = p <= p_last ? load_u32u(S + p) : 0;
     }
 #pragma unroll
+    for (int j = 0; j < LINK_BATCH; j++) {   // the batch's atomics, in position order
+      const int32_t p = g0 + 64 * j + lane;
+      const bool part = p <= p_last && p != nil_pos;   // window index 0 of a deflater is NIL
+      hh[j] = zd::hash3(wv[j] & 0xff, (wv[j] >> 8) & 0xff, (wv[j] >> 16) & 0xff);
+      pred[j] = part ? atomicMax(&hpos[hh[j]], p) : HNONE;
+    }
+#pragma unroll
     for (int j = 0; j < LINK_BATCH; j++) {
-      const int32_t g = g0 + 64 * j;
-      const int32_t p = g + lane;
-      const bool valid = p <= p_last;
-      const bool part = valid && p != nil_pos;   // window index 0 of a deflater is NIL
-      const uint32_t h = zd::hash3(wv[j] & 0xff, (wv[j] >> 8) & 0xff, (wv[j] >> 16) & 0xff);
-      int32_t r = HNONE;
-      if (part) r = atomicMax(&hpos[h], p);
-      int32_t pr = part ? r : HNONE;
-      if (__ballot(part && r >= g)) pr = link_repeats(hpos, h, p, part, g, r);   // a hash repeats in the group
-      pred[j] = pr;
+      const int32_t g = g0 + 64 * j, p = g + lane;
+      const bool part = p <= p_last && p != nil_pos;
+      if (__ballot(part && pred[j] >= g)) pred[j] = link_repeats(hh[j], part, g, pred[j]);
     }
 #pragma unroll
     for (int j = 0; j < LINK_BATCH; j++) {
@@ -569,12 +557,15 @@ __device__ inline void fast_result(const FastWalk& w, const zd::Cfg& c, uint32_t
 // positions (bytes and links, 144 KiB) and walks every chain in LDS.  A phase loads the
 // window of a run of consecutive frames (from MAX_DIST before the first one's start to the
 // last one's end, DEFL_RING at most), then the lanes take the run's fast positions (a scan
-// that stays inside its frame: p + 266 <= end) from an LDS counter, two at a time a lane,
-// and write the results of each straight to the result array (no global load follows:
-// the walk's loads are LDS).  Positions nearer a frame's end, the tail variants, and frames
-// longer than DEFL_LDS_MAXLEN stay with k_defl_match.
+// that stays inside its frame: p + 266 <= end), a wave 256 at a time from an LDS counter,
+// refilled lane by lane as walks end, and write each result straight to the result array
+// (no global load follows: the walk's loads are LDS).  A walk keeps ring indices, not
+// stream positions (the ring's first 272 bytes are mirrored past its end, so a compare
+// never wraps).  Positions nearer a frame's end, the tail variants, and frames longer than
+// DEFL_LDS_MAXLEN stay with k_defl_match.
+constexpr uint32_t RING_MIRROR = 272;   // bytes: the longest compare (258 + an 8-B read + 3) past a ring index
 struct LdsRing {
-  uint32_t bytes[(DEFL_RING + 16) / 4];   // position x at byte x % DEFL_RING; words 0..3 mirrored past the end
+  uint32_t bytes[(DEFL_RING + RING_MIRROR) / 4];   // position x at byte x % DEFL_RING
   uint16_t link[DEFL_RING];
   uint32_t next;                           // the run's position dispenser
   uint32_t nfr;                            // frames of the run with a fast range
@@ -582,24 +573,41 @@ struct LdsRing {
 };
 static_assert(sizeof(LdsRing) <= 160 * 1024, "the ring fits the LDS");
 
-__device__ inline uint64_t ring8(const LdsRing& R, uint32_t x) {   // stream bytes x .. x + 7
-  const uint32_t r = x % DEFL_RING, w = r >> 2, sh = r & 3;
+__device__ inline uint64_t ring8(const LdsRing& R, uint32_t r) {   // bytes at ring index r .. r + 7
+  const uint32_t w = r >> 2, sh = r & 3;
   const uint32_t w0 = R.bytes[w], w1 = R.bytes[w + 1], w2 = R.bytes[w + 2];
   const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, sh), hi = __builtin_amdgcn_alignbyte(w2, w1, sh);
   return (uint64_t)hi << 32 | lo;
 }
-__device__ inline uint32_t ring1(const LdsRing& R, uint32_t x) {
-  const uint32_t r = x % DEFL_RING;
-  return (R.bytes[r >> 2] >> (8 * (r & 3))) & 0xff;
+__device__ inline uint32_t ring1(const LdsRing& R, uint32_t r) { return (R.bytes[r >> 2] >> (8 * (r & 3))) & 0xff; }
+
+// a walk over the ring: FastWalk's fields with q and the position as ring indices
+struct RingWalk {
+  uint32_t q, pr, dist, k, best, best_d, qres;
+  uint64_t b;
+  bool done;
+};
+
+__device__ inline void ring_init(RingWalk& w, const LdsRing& R, uint32_t p) {
+  const uint32_t pr = p % DEFL_RING;
+  const uint32_t d = R.link[pr];
+  w.pr = pr;
+  w.k = 1;
+  w.best = 2;
+  w.best_d = 0;
+  w.qres = 0;
+  w.dist = d;
+  w.q = pr >= d ? pr - d : pr + DEFL_RING - d;
+  w.done = d == 0 || d > (uint32_t)zd::MAX_DIST;
+  w.b = ring8(R, pr);
 }
 
-// one candidate of the walk at position p (FastWalk over the ring); true when the walk is over
-__device__ inline bool ring_step(FastWalk& w, const LdsRing& R, uint32_t p, const zd::Cfg& c) {
-  const uint32_t qbudget = c.chain >> 2;
+// one candidate; true when the walk is over
+__device__ inline bool ring_step(RingWalk& w, const LdsRing& R, const zd::Cfg& c) {
   const uint64_t x = ring8(R, w.q) ^ w.b;
-  const uint32_t l = R.link[w.q % DEFL_RING];
+  const uint32_t l = R.link[w.q];
   if ((x & 0xFFFF) == 0) {
-    const bool cand = w.best < 8 ? ((x >> (8 * w.best)) & 0xFF) == 0 : ring1(R, w.q + w.best) == ring1(R, p + w.best);
+    const bool cand = w.best < 8 ? ((x >> (8 * w.best)) & 0xFF) == 0 : ring1(R, w.q + w.best) == ring1(R, w.pr + w.best);
     if (cand) {
       uint32_t len;
       if (x) {
@@ -607,7 +615,7 @@ __device__ inline bool ring_step(FastWalk& w, const LdsRing& R, uint32_t p, cons
       } else {
         len = 8;
         for (;;) {
-          const uint64_t y = ring8(R, w.q + len) ^ ring8(R, p + len);
+          const uint64_t y = ring8(R, w.q + len) ^ ring8(R, w.pr + len);
           if (y) {
             len += (uint32_t)__builtin_ctzll(y) >> 3;
             break;
@@ -624,26 +632,24 @@ __device__ inline bool ring_step(FastWalk& w, const LdsRing& R, uint32_t p, cons
       }
     }
   }
-  if (w.k == qbudget) w.qres = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
+  if (w.k == (uint32_t)(c.chain >> 2)) w.qres = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
   if (w.k >= c.chain) return true;
   if (l == 0) return true;
   w.dist += l;
   if (w.dist >= (uint32_t)zd::MAX_DIST) return true;
-  w.q -= l;
+  w.q = w.q >= l ? w.q - l : w.q + DEFL_RING - l;
   w.k++;
   return false;
 }
 
-__device__ inline void ring_init(FastWalk& w, const LdsRing& R, uint32_t p) {
-  const uint32_t d = R.link[p % DEFL_RING];
-  w.k = 1;
-  w.best = 2;
-  w.best_d = 0;
-  w.qres = 0;
-  w.dist = d;
-  w.q = p - d;
-  w.done = d == 0 || d > (uint32_t)zd::MAX_DIST;
-  w.b = ring8(R, p);
+__device__ inline void ring_result(const RingWalk& w, const zd::Cfg& c, uint32_t p0d, uint32_t* full, uint32_t* quarter) {
+  if (p0d == 0 || p0d > (uint32_t)zd::MAX_DIST) {
+    *full = *quarter = 0;
+    return;
+  }
+  const uint32_t f = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
+  *full = f | (p0d == (uint32_t)zd::MAX_DIST ? (uint32_t)zd::MR_HEAD_AT_MAX : 0u);
+  *quarter = w.k <= (uint32_t)(c.chain >> 2) ? f : w.qres;
 }
 
 // a frame's fast range: [start, end - 266) when the frame takes the LDS walk
@@ -652,6 +658,7 @@ __device__ inline bool lds_frame(const DeflFrame& f) { return f.len <= DEFL_LDS_
 __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
   __shared__ LdsRing R;
   const uint32_t s = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const uint64_t lt_mask = (1ull << lane) - 1;
   const DeflSess fs = a.fs[s];
   if (fs.last_call == ~0u) return;
   Sums sm(a);
@@ -672,13 +679,10 @@ __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
     uint32_t run_end = f0.s_rel + f0.len, kn = k + 1, nfr = 0;
     uint32_t lo8[8], pre8[9];
     pre8[0] = 0;
-    {
-      const uint32_t e0 = f0.s_rel + f0.len;
-      if (e0 >= f0.s_rel + 267) {
-        lo8[0] = f0.s_rel;
-        pre8[1] = f0.len - 266;
-        nfr = 1;
-      }
+    if (f0.len >= 267) {
+      lo8[0] = f0.s_rel;
+      pre8[1] = f0.len - 266;
+      nfr = 1;
     }
     while (kn < k1 && nfr < 8) {
       const uint32_t fl = a.fflags[kn];
@@ -699,13 +703,15 @@ __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
     // load the window [need_lo, run_end): what the ring does not hold yet
     const uint32_t from = (need_lo >= lo_loaded && need_lo <= hi_loaded) ? hi_loaded : need_lo;
     __syncthreads();   // (the previous run's walks read the ring)
-    for (uint32_t wd = (from >> 2) + tid; wd < (run_end + 3) >> 2; wd += blockDim.x) {
-      const uint32_t v = Sw[wd];
-      const uint32_t r = (wd << 2) % DEFL_RING >> 2;
-      R.bytes[r] = v;
-      if (r < 4) R.bytes[DEFL_RING / 4 + r] = v;
-    }
-    for (uint32_t x = from + tid; x < run_end; x += blockDim.x) R.link[x % DEFL_RING] = link[x];
+    // (eight global loads of a thread in flight before their LDS stores)
+    batched_for((from >> 2), (run_end + 3) >> 2, [&](uint32_t wd) { return Sw[wd]; },
+                [&](uint32_t wd, uint32_t v) {
+                  const uint32_t r = (wd << 2) % DEFL_RING >> 2;
+                  R.bytes[r] = v;
+                  if (r < RING_MIRROR / 4) R.bytes[DEFL_RING / 4 + r] = v;
+                });
+    batched_for(from, run_end, [&](uint32_t x) { return (uint32_t)link[x]; },
+                [&](uint32_t x, uint32_t v) { R.link[x % DEFL_RING] = (uint16_t)v; });
     if (tid == 0) {
       R.next = 0;
       R.nfr = nfr;
@@ -718,65 +724,74 @@ __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
     __syncthreads();
     const uint32_t total = pre8[nfr];
     if (total == 0) continue;
-    // the walks: two a lane, refilled from the dispenser a wave at a time
     auto pos_of = [&](uint32_t v) -> uint32_t {
       uint32_t j = 0;
       while (j + 1 < nfr && R.fr_pre[j + 1] <= v) j++;
       return R.fr_lo[j] + (v - R.fr_pre[j]);
     };
-    uint32_t base = 0;
-    if (lane == 0) base = atomicAdd(&R.next, 128u);
-    base = __shfl(base, 0);
-    uint32_t va = base + lane, vb = base + 64 + lane;
-    bool acta = va < total, actb = vb < total;
-    uint32_t pa = acta ? pos_of(va) : 0, pb = actb ? pos_of(vb) : 0;
-    FastWalk wa, wb;
-    uint32_t da = 0, db = 0;
-    if (acta) {
-      ring_init(wa, R, pa);
-      da = wa.dist;
+    // the wave's range of virtual indices [next, cend), 256 at a time from the dispenser
+    auto grab = [&](uint32_t& nx, uint32_t& ce) {
+      uint32_t b = 0;
+      if (lane == 0) b = atomicAdd(&R.next, 256u);
+      b = __shfl(b, 0);
+      nx = b < total ? b : total;
+      ce = b + 256 < total ? b + 256 : total;
+    };
+    uint32_t next, cend;
+    grab(next, cend);
+    uint32_t p = next + lane;
+    bool act = p < cend;
+    next = next + 64 < cend ? next + 64 : cend;
+    RingWalk w;
+    uint32_t d0 = 0;
+    if (act) {
+      p = pos_of(p);
+      ring_init(w, R, p);
+      d0 = w.dist;
     }
-    if (actb) {
-      ring_init(wb, R, pb);
-      db = wb.dist;
-    }
-    while (__ballot(acta || actb)) {
-      bool fina = false, finb = false;
-      if (acta) fina = wa.done || ring_step(wa, R, pa, cfg);
-      if (actb) finb = wb.done || ring_step(wb, R, pb, cfg);
-      if (fina) {
-        uint32_t full, quarter;
-        fast_result(wa, cfg, da, &full, &quarter);
-        *(uint2*)(res + 2 * (uint64_t)pa) = make_uint2(full, quarter);
+    for (;;) {
+      if (!__ballot(act)) {   // every walk ended and the range is used up: another one
+        if (next >= cend) {
+          grab(next, cend);
+          if (next >= cend) break;
+        }
+        const uint32_t v = next + lane;
+        act = v < cend;
+        next = next + 64 < cend ? next + 64 : cend;
+        if (act) {
+          p = pos_of(v);
+          ring_init(w, R, p);
+          d0 = w.dist;
+        }
+        continue;
       }
-      if (finb) {
+      const bool fin = act && (w.done || ring_step(w, R, cfg));
+      if (fin) {
         uint32_t full, quarter;
-        fast_result(wb, cfg, db, &full, &quarter);
-        *(uint2*)(res + 2 * (uint64_t)pb) = make_uint2(full, quarter);
+        ring_result(w, cfg, d0, &full, &quarter);
+        *(uint2*)(res + 2 * (uint64_t)p) = make_uint2(full, quarter);
       }
-      const uint64_t ma = __ballot(fina), mb = __ballot(finb);
-      const uint32_t na = (uint32_t)__builtin_popcountll(ma), nb = (uint32_t)__builtin_popcountll(mb);
-      if (na + nb) {
-        uint32_t b2 = 0;
-        if (lane == 0) b2 = atomicAdd(&R.next, na + nb);
-        b2 = __shfl(b2, 0);
-        if (fina) {
-          va = b2 + (uint32_t)__builtin_popcountll(ma & ((1ull << lane) - 1));
-          acta = va < total;
-          if (acta) {
-            pa = pos_of(va);
-            ring_init(wa, R, pa);
-            da = wa.dist;
+      const uint64_t m = __ballot(fin);
+      if (m) {   // lanes whose walk ended take the next positions: the range's, then a new range's
+        const uint32_t need = (uint32_t)__builtin_popcountll(m), avail = cend - next;
+        uint32_t n2 = cend, c2 = cend;
+        if (need > avail) grab(n2, c2);
+        if (fin) {
+          const uint32_t r = (uint32_t)__builtin_popcountll(m & lt_mask);
+          const uint32_t v = r < avail ? next + r : n2 + (r - avail);
+          act = r < avail || v < c2;
+          if (act) {
+            p = pos_of(v);
+            ring_init(w, R, p);
+            d0 = w.dist;
           }
         }
-        if (finb) {
-          vb = b2 + na + (uint32_t)__builtin_popcountll(mb & ((1ull << lane) - 1));
-          actb = vb < total;
-          if (actb) {
-            pb = pos_of(vb);
-            ring_init(wb, R, pb);
-            db = wb.dist;
-          }
+        if (need > avail) {
+          const uint32_t n = n2 + (need - avail);
+          next = n < c2 ? n : c2;
+          cend = c2;
+        } else {
+          next += need;
         }
       }
     }
