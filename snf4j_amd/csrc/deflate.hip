@@ -191,15 +191,15 @@ __device__ inline uint32_t load_u32u(const uint8_t* p) {
 }
 
 // link pass of one segment, wave 0: strings [p_begin, p_last] in position order, 64 a
-// group, 8 groups a batch.  A group's lanes atomicMax their position into the hash's LDS
+// group, 16 groups a batch.  A group's lanes atomicMax their position into the hash's LDS
 // entry (hpos) and take the value returned: the last position of the hash before them,
 // or, for a hash that repeats inside the group, a position of the group, which the lane
 // then replaces by the nearest lane below with its hash (wave-local: hpos already holds the
 // group's last position of every hash, what the groups after it must see).  So a batch's
-// eight atomics go out back to back, nothing waiting on another's return; its stream words
+// sixteen atomics go out back to back, nothing waiting on another's return; its stream words
 // are loaded first and its links stored last (a store before a load would hold the load,
 // loads and stores sharing vmcnt).
-constexpr int LINK_BATCH = 8;
+constexpr int LINK_BATCH = 16;
 
 // the lanes of a group whose hash an earlier lane of the group has (r >= g): predecessor =
 // the nearest such lane below (positions are g + lane)
@@ -283,21 +283,30 @@ __device__ inline uint4 load16(const uint8_t* p) {
 }
 __device__ inline void store16(uint8_t* p, uint4 v) { __builtin_memcpy(p, &v, 16); }
 
-// dst[0, n) = src[0, n) by T threads from thread t (disjoint ranges): 16-B pieces, four
+// dst[0, n) = src[0, n) by T threads from thread t (disjoint ranges): 16-B pieces, eight
 // loads in flight before their stores
 __device__ void copy_pieces(uint8_t* dst, const uint8_t* src, uint32_t n, uint32_t t, uint32_t T) {
   const uint32_t np = n >> 4;
-  for (uint32_t i0 = 0; i0 < np; i0 += T * 4) {
+  for (uint32_t i0 = 0; i0 < np; i0 += T * 8) {
     const uint32_t i_0 = i0 + t, i_1 = i_0 + T, i_2 = i_1 + T, i_3 = i_2 + T;
-    uint4 v0, v1, v2, v3;
+    const uint32_t i_4 = i_3 + T, i_5 = i_4 + T, i_6 = i_5 + T, i_7 = i_6 + T;
+    uint4 v0, v1, v2, v3, v4, v5, v6, v7;
     if (i_0 < np) v0 = load16(src + 16 * (uint64_t)i_0);
     if (i_1 < np) v1 = load16(src + 16 * (uint64_t)i_1);
     if (i_2 < np) v2 = load16(src + 16 * (uint64_t)i_2);
     if (i_3 < np) v3 = load16(src + 16 * (uint64_t)i_3);
+    if (i_4 < np) v4 = load16(src + 16 * (uint64_t)i_4);
+    if (i_5 < np) v5 = load16(src + 16 * (uint64_t)i_5);
+    if (i_6 < np) v6 = load16(src + 16 * (uint64_t)i_6);
+    if (i_7 < np) v7 = load16(src + 16 * (uint64_t)i_7);
     if (i_0 < np) store16(dst + 16 * (uint64_t)i_0, v0);
     if (i_1 < np) store16(dst + 16 * (uint64_t)i_1, v1);
     if (i_2 < np) store16(dst + 16 * (uint64_t)i_2, v2);
     if (i_3 < np) store16(dst + 16 * (uint64_t)i_3, v3);
+    if (i_4 < np) store16(dst + 16 * (uint64_t)i_4, v4);
+    if (i_5 < np) store16(dst + 16 * (uint64_t)i_5, v5);
+    if (i_6 < np) store16(dst + 16 * (uint64_t)i_6, v6);
+    if (i_7 < np) store16(dst + 16 * (uint64_t)i_7, v7);
   }
   for (uint32_t i = (np << 4) + t; i < n; i += T) dst[i] = src[i];
 }
@@ -1258,8 +1267,10 @@ __device__ void send_tree_w(WordSink& o, const uint32_t* tab, int max_code, cons
 // trees by thread 0, the symbols by every thread at offsets from a block-wide scan) and the
 // sync marker, into the frame's zeroed output slot
 constexpr int EMIT_T = 256;
+constexpr uint32_t EMIT_SYM = 4096;
 __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
   __shared__ uint32_t s_ltab[286], s_dtab[30], s_btab[19];
+  __shared__ uint32_t s_sym[EMIT_SYM];   // a block's symbols, loaded once, coalesced (blocks up to EMIT_SYM)
   __shared__ uint32_t s_scan[EMIT_T];
   __shared__ uint32_t s_off;   // running bit offset of the frame
   Sums sm(a);
@@ -1346,10 +1357,16 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
       const uint32_t i0 = tid * per < nsym ? tid * per : nsym;
       const uint32_t i1 = i0 + per < nsym ? i0 + per : nsym;
       const uint32_t* sy = a.sym + B->sym0;
+      const bool staged = nsym <= EMIT_SYM;   // both passes read the symbols from LDS (one coalesced load)
+      if (staged) {
+        batched_for(0, nsym, [&](uint32_t i) { return sy[i]; }, [&](uint32_t i, uint32_t v) { s_sym[i] = v; });
+        __syncthreads();
+      }
+      auto sym_at = [&](uint32_t i) { return staged ? s_sym[i] : sy[i]; };
       uint32_t mybits = 0;
       for (uint32_t i = i0; i < i1; i++) {
         uint32_t c1, l1, c2, l2;
-        sym_code(sy[i], s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
+        sym_code(sym_at(i), s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
         mybits += l1 + l2;
       }
       s_scan[tid] = mybits;
@@ -1369,7 +1386,7 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
         WordSink ws(ow, sym_start + s_scan[tid] - mybits);
         for (uint32_t i = i0; i < i1; i++) {
           uint32_t c1, l1, c2, l2;
-          sym_code(sy[i], s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
+          sym_code(sym_at(i), s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
           ws.put(c1, l1);
           if (l2) ws.put(c2, l2);
         }

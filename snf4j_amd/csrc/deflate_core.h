@@ -146,12 +146,18 @@ ZD_FN void stored_block(BitWriter* bw, const uint8_t* buf, uint32_t len) {
 
 // ------------------------------------------------------------------ trees.c
 // ct_data split into fc (Freq, then Code) and dl (Dad, then Len), as zlib's unions are used
+// The heap proper holds keys freq << 15 | depth << 10 | node: zlib's smaller() (freq, then
+// depth; equal keys count as smaller) is a compare of key >> 10, with no lookup of the two
+// nodes' freq and depth a heap step.  (A block has at most 16384 symbols with its end code,
+// so a freq fits 15 bits; a Huffman tree over weights >= 1 totalling at most 16384 is at
+// most 19 levels high, so a depth fits 5.)  heap[] keeps zlib's node order from heap_max
+// up (gen_bitlen's walk).  fc / dl: leaves' freqs then codes; dads then lengths.
 struct TreeWork {
-    uint16_t lfc[HEAP_SIZE], ldl[HEAP_SIZE];
-    uint16_t dfc[2 * D_CODES + 1], ddl[2 * D_CODES + 1];
-    uint16_t bfc[2 * BL_CODES + 1], bdl[2 * BL_CODES + 1];
+    uint16_t lfc[L_CODES], ldl[HEAP_SIZE];
+    uint16_t dfc[D_CODES], ddl[2 * D_CODES + 1];
+    uint16_t bfc[BL_CODES], bdl[2 * BL_CODES + 1];
     int16_t heap[2 * L_CODES + 1];
-    uint8_t depth[2 * L_CODES + 1];
+    uint32_t kheap[L_CODES + 1];
     uint16_t bl_count[MAX_BITS + 1];
     uint32_t opt_len, static_len;
     int16_t l_max, d_max;
@@ -184,20 +190,26 @@ template <int KIND> ZD_FN int tree_xbits(int n) {
     return KIND == 0 ? (n >= 257 ? len_extra(n - 257) : 0) : KIND == 1 ? dist_extra(n) : bl_extra(n);
 }
 
-ZD_FN bool smaller(const uint16_t* fc, const uint8_t* depth, int n, int m) {
-    return fc[n] < fc[m] || (fc[n] == fc[m] && depth[n] <= depth[m]);
-}
-ZD_FN void pqdownheap(TreeWork* t, const uint16_t* fc, int k, int heap_len) {
-    int v = t->heap[k];
+ZD_FN uint32_t heap_key(uint32_t freq, uint32_t depth, uint32_t node) { return freq << 15 | depth << 10 | node; }
+// pqdownheap over the keys (zlib's smaller(a, b): key(a) >> 10 <= key(b) >> 10)
+ZD_FN void pqdownheap(uint32_t* kh, int k, int heap_len) {
+    const uint32_t v = kh[k];
     int j = k << 1;
     while (j <= heap_len) {
-        if (j < heap_len && smaller(fc, t->depth, t->heap[j + 1], t->heap[j])) j++;
-        if (smaller(fc, t->depth, v, t->heap[j])) break;
-        t->heap[k] = t->heap[j];
+        uint32_t kj = kh[j];
+        if (j < heap_len) {
+            const uint32_t kj1 = kh[j + 1];
+            if ((kj1 >> 10) <= (kj >> 10)) {
+                j++;
+                kj = kj1;
+            }
+        }
+        if ((v >> 10) <= (kj >> 10)) break;
+        kh[k] = kj;
         k = j;
         j <<= 1;
     }
-    t->heap[k] = (int16_t)v;
+    kh[k] = v;
 }
 
 template <int KIND> ZD_FN void gen_bitlen(TreeWork* t, const uint16_t* fc, uint16_t* dl, int max_code, int heap_max) {
@@ -258,39 +270,39 @@ ZD_FN void gen_codes(uint16_t* fc, const uint16_t* dl, int max_code, const uint1
 // build_tree: Huffman code lengths (fc = freqs in, codes out; dl = lengths out); returns max_code
 template <int KIND> ZD_FN int build_tree(TreeWork* t, uint16_t* fc, uint16_t* dl) {
     const int elems = tree_elems<KIND>();
+    uint32_t* kh = t->kheap;
     int n, m, max_code = -1, node, heap_len = 0, heap_max = HEAP_SIZE;
     for (n = 0; n < elems; n++) {
         if (fc[n] != 0) {
-            t->heap[++heap_len] = (int16_t)(max_code = n);
-            t->depth[n] = 0;
+            kh[++heap_len] = heap_key(fc[n], 0, (uint32_t)(max_code = n));
         } else {
             dl[n] = 0;
         }
     }
     while (heap_len < 2) {   // at least two codes of non-zero frequency
         node = max_code < 2 ? ++max_code : 0;
-        t->heap[++heap_len] = (int16_t)node;
+        kh[++heap_len] = heap_key(1, 0, (uint32_t)node);
         fc[node] = 1;
-        t->depth[node] = 0;
         t->opt_len--;
         if (KIND != 2) t->static_len -= (uint32_t)tree_stree_len<KIND>(node);
     }
-    for (n = heap_len / 2; n >= 1; n--) pqdownheap(t, fc, n, heap_len);
+    for (n = heap_len / 2; n >= 1; n--) pqdownheap(kh, n, heap_len);
     node = elems;
     do {
-        n = t->heap[1];   // pqremove
-        t->heap[1] = t->heap[heap_len--];
-        pqdownheap(t, fc, 1, heap_len);
-        m = t->heap[1];
+        const uint32_t kn = kh[1];   // pqremove
+        kh[1] = kh[heap_len--];
+        pqdownheap(kh, 1, heap_len);
+        const uint32_t km = kh[1];
+        n = (int)(kn & 1023);
+        m = (int)(km & 1023);
         t->heap[--heap_max] = (int16_t)n;
         t->heap[--heap_max] = (int16_t)m;
-        fc[node] = (uint16_t)(fc[n] + fc[m]);
-        t->depth[node] = (uint8_t)((t->depth[n] >= t->depth[m] ? t->depth[n] : t->depth[m]) + 1);
+        const uint32_t dn = (kn >> 10) & 31, dm = (km >> 10) & 31;
         dl[n] = dl[m] = (uint16_t)node;
-        t->heap[1] = (int16_t)node++;
-        pqdownheap(t, fc, 1, heap_len);
+        kh[1] = heap_key((kn >> 15) + (km >> 15), (dn >= dm ? dn : dm) + 1, (uint32_t)node++);
+        pqdownheap(kh, 1, heap_len);
     } while (heap_len >= 2);
-    t->heap[--heap_max] = t->heap[1];
+    t->heap[--heap_max] = (int16_t)(kh[1] & 1023);
     gen_bitlen<KIND>(t, fc, dl, max_code, heap_max);
     gen_codes(fc, dl, max_code, t->bl_count);
     return max_code;
