@@ -1123,14 +1123,17 @@ __global__ __launch_bounds__(256) void k_defl_hist(DeflArgs a) {
   }
 }
 
-// lane per block, the block's TreeWork in LDS (32 lanes a workgroup): the three Huffman
+// lane per block, the block's TreeWork in LDS (TREE_LANES a workgroup, as many as the LDS
+// holds: 48 of 3.2 KiB since the heap keys share their storage with the node order): the three Huffman
 // trees exactly as zlib's heap builds them, the block type and its size
-__global__ __launch_bounds__(32) void k_defl_trees(DeflArgs a) {
-  __shared__ zd::TreeWork tws[32];
+constexpr uint32_t TREE_LANES = 48;
+static_assert(TREE_LANES * sizeof(zd::TreeWork) <= 160 * 1024, "the tree lanes' work fits the LDS");
+__global__ __launch_bounds__(TREE_LANES) void k_defl_trees(DeflArgs a) {
+  __shared__ zd::TreeWork tws[TREE_LANES];
   Sums sm(a);
   const uint64_t total = sm.B[a.n_sessions];
   zd::TreeWork* t = &tws[threadIdx.x];
-  for (uint64_t i = (uint64_t)blockIdx.x * 32 + threadIdx.x; i < total; i += (uint64_t)gridDim.x * 32) {
+  for (uint64_t i = (uint64_t)blockIdx.x * TREE_LANES + threadIdx.x; i < total; i += (uint64_t)gridDim.x * TREE_LANES) {
     DeflBlock* b = a.blocks + i;
     const uint32_t nsym = b->nsym;
     if (nsym == 0) continue;
@@ -1552,8 +1555,8 @@ void launch_defl_hist(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
                      s, a);
 }
 void launch_defl_trees(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
-  uint64_t g = (n_blocks + 31) / 32;
-  hipLaunchKernelGGL(k_defl_trees, dim3((uint32_t)(g < 65536 ? (g ? g : 1) : 65536)), dim3(32), 0, s, a);
+  uint64_t g = (n_blocks + TREE_LANES - 1) / TREE_LANES;
+  hipLaunchKernelGGL(k_defl_trees, dim3((uint32_t)(g < 65536 ? (g ? g : 1) : 65536)), dim3(TREE_LANES), 0, s, a);
 }
 void launch_defl_emit(const DeflArgs& a, hipStream_t s) {
   uint64_t g = a.n_frames < 262144 ? a.n_frames : 262144;

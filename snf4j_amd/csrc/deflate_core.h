@@ -150,18 +150,23 @@ ZD_FN void stored_block(BitWriter* bw, const uint8_t* buf, uint32_t len) {
 // depth; equal keys count as smaller) is a compare of key >> 10, with no lookup of the two
 // nodes' freq and depth a heap step.  (A block has at most 16384 symbols with its end code,
 // so a freq fits 15 bits; a Huffman tree over weights >= 1 totalling at most 16384 is at
-// most 19 levels high, so a depth fits 5.)  heap[] keeps zlib's node order from heap_max
-// up (gen_bitlen's walk).  fc / dl: leaves' freqs then codes; dads then lengths.
+// most 19 levels high, so a depth fits 5.)  zlib's heap[heap_max..HEAP_SIZE) (the node
+// order gen_bitlen walks) shares the keys' storage from its far end: a merge frees one key
+// (4 B) as it adds two nodes (2 B each), so the two never meet (node h at u16 slot h + 1).
+// fc / dl: leaves' freqs then codes; dads then lengths.
 struct TreeWork {
     uint16_t lfc[L_CODES], ldl[HEAP_SIZE];
     uint16_t dfc[D_CODES], ddl[2 * D_CODES + 1];
     uint16_t bfc[BL_CODES], bdl[2 * BL_CODES + 1];
-    int16_t heap[2 * L_CODES + 1];
-    uint32_t kheap[L_CODES + 1];
+    union {
+        uint32_t kheap[L_CODES + 1];
+        int16_t hsort[2 * L_CODES + 2];
+    };
     uint16_t bl_count[MAX_BITS + 1];
     uint32_t opt_len, static_len;
     int16_t l_max, d_max;
 };
+ZD_FN int16_t& heap_node(TreeWork* t, int h) { return t->hsort[h + 1]; }   // zlib's heap[h], h >= heap_max
 
 ZD_FN void init_block(TreeWork* t) {
     for (int n = 0; n < L_CODES; n++) t->lfc[n] = 0;
@@ -216,9 +221,9 @@ template <int KIND> ZD_FN void gen_bitlen(TreeWork* t, const uint16_t* fc, uint1
     const int max_length = KIND == 2 ? MAX_BL_BITS : MAX_BITS;
     int h, n, m, bits, overflow = 0;
     for (bits = 0; bits <= MAX_BITS; bits++) t->bl_count[bits] = 0;
-    dl[t->heap[heap_max]] = 0;   // root
+    dl[heap_node(t, heap_max)] = 0;   // root
     for (h = heap_max + 1; h < HEAP_SIZE; h++) {
-        n = t->heap[h];
+        n = heap_node(t, h);
         bits = dl[dl[n]] + 1;
         if (bits > max_length) bits = max_length, overflow++;
         dl[n] = (uint16_t)bits;
@@ -241,7 +246,7 @@ template <int KIND> ZD_FN void gen_bitlen(TreeWork* t, const uint16_t* fc, uint1
     for (bits = max_length; bits != 0; bits--) {
         n = t->bl_count[bits];
         while (n != 0) {
-            m = t->heap[--h];
+            m = heap_node(t, --h);
             if (m > max_code) continue;
             if (dl[m] != (uint32_t)bits) {
                 t->opt_len += ((uint32_t)bits - dl[m]) * fc[m];
@@ -295,14 +300,15 @@ template <int KIND> ZD_FN int build_tree(TreeWork* t, uint16_t* fc, uint16_t* dl
         const uint32_t km = kh[1];
         n = (int)(kn & 1023);
         m = (int)(km & 1023);
-        t->heap[--heap_max] = (int16_t)n;
-        t->heap[--heap_max] = (int16_t)m;
+        heap_node(t, --heap_max) = (int16_t)n;
+        heap_node(t, --heap_max) = (int16_t)m;
         const uint32_t dn = (kn >> 10) & 31, dm = (km >> 10) & 31;
         dl[n] = dl[m] = (uint16_t)node;
         kh[1] = heap_key((kn >> 15) + (km >> 15), (dn >= dm ? dn : dm) + 1, (uint32_t)node++);
         pqdownheap(kh, 1, heap_len);
     } while (heap_len >= 2);
-    t->heap[--heap_max] = (int16_t)(kh[1] & 1023);
+    const int16_t root = (int16_t)(kh[1] & 1023);
+    heap_node(t, --heap_max) = root;
     gen_bitlen<KIND>(t, fc, dl, max_code, heap_max);
     gen_codes(fc, dl, max_code, t->bl_count);
     return max_code;
