@@ -318,6 +318,25 @@ __device__ void block_copy(uint8_t* dst, const uint8_t* src, uint32_t n) {
   copy_pieces(dst, src, n, threadIdx.x, blockDim.x);
 }
 
+// batched_for over 16-B values
+template <class LD, class ST>
+__device__ void batched_for16(uint32_t lo, uint32_t hi, LD ld, ST st) {
+  const uint32_t T = blockDim.x;
+  for (uint32_t i0 = lo + threadIdx.x; i0 < hi; i0 += 8 * T) {
+    uint4 v[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t i = i0 + j * T;
+      v[j] = i < hi ? ld(i) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const uint32_t i = i0 + j * T;
+      if (i < hi) st(i, v[j]);
+    }
+  }
+}
+
 // for i in [lo, hi) by the workgroup: v = ld(i) for eight of a thread's indices, then
 // st(i, v) for them — the loads in flight together instead of one load, its wait and its
 // store an index (the session-sized loops of k_defl_prep were a global load latency each)
@@ -366,11 +385,25 @@ __device__ uint32_t window_walk(const DeflArgs& a, uint8_t* W, const uint8_t* S,
       rem -= m;
       zero_hw(W, hw, loaded);
     }
+    // the strips: every lane's loads first, then its stores (a store between them would
+    // make each next load wait for it: five round trips a frame instead of one)
     uint8_t* st0 = a.strips + (uint64_t)k * 2 * zd::STRIP;
-    for (uint32_t j = lane; j < (uint32_t)zd::STRIP; j += 64) {
-      st0[j] = loaded + j < (uint32_t)zd::WINDOW_SIZE ? W[loaded + j] : 0;
+    constexpr int SJ = (zd::STRIP + 63) / 64;
+    uint8_t v0[SJ], v1[SJ];
+#pragma unroll
+    for (int i = 0; i < SJ; i++) {
+      const uint32_t j = lane + 64 * i;
       const uint32_t q = loaded - zd::WSIZE + j;
-      st0[zd::STRIP + j] = (loaded >= (uint32_t)zd::WSIZE && q < (uint32_t)zd::WINDOW_SIZE) ? W[q] : 0;
+      v0[i] = (j < (uint32_t)zd::STRIP && loaded + j < (uint32_t)zd::WINDOW_SIZE) ? W[loaded + j] : 0;
+      v1[i] = (j < (uint32_t)zd::STRIP && loaded >= (uint32_t)zd::WSIZE && q < (uint32_t)zd::WINDOW_SIZE) ? W[q] : 0;
+    }
+#pragma unroll
+    for (int i = 0; i < SJ; i++) {
+      const uint32_t j = lane + 64 * i;
+      if (j < (uint32_t)zd::STRIP) {
+        st0[j] = v0[i];
+        st0[zd::STRIP + j] = v1[i];
+      }
     }
     sw = loaded;
   }
@@ -444,18 +477,38 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
           });
     if (fresh) {
       for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x) hpos[h] = HNONE;
-    } else {
-      batched_for(0, zd::WSIZE, [&](uint32_t h) { return (uint32_t)head[h]; },
-                  [&](uint32_t h, uint32_t v) { hpos[h] = v == 0 ? HNONE : (int32_t)v + base0; });
+    } else {   // (head as 16-B pieces, eight entries each, eight pieces of a thread in flight)
+      const uint4* head16 = (const uint4*)head;
+      batched_for16(0, zd::WSIZE / 8, [&](uint32_t i) { return head16[i]; }, [&](uint32_t i, uint4 v) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const uint32_t hv = (w[e >> 1] >> (16 * (e & 1))) & 0xffff;
+          hpos[8 * i + e] = hv == 0 ? HNONE : (int32_t)hv + base0;
+        }
+      });
     }
     __syncthreads();
     // 3. the slides of this batch applied to the prev entries no string of it replaces
-    if (persist && !fresh && base_final != base0)
-      batched_for(0, zd::WSIZE, [&](uint32_t j) { return (uint32_t)prev[j]; },
-                  [&](uint32_t j, uint32_t v) {
-                    const int32_t nv = v ? (int32_t)v + base0 - base_final : 0;
-                    prev[j] = (uint16_t)(nv > 0 ? nv : 0);
-                  });
+    if (persist && !fresh && base_final != base0) {
+      uint4* prev16 = (uint4*)prev;
+      const int32_t shift = base0 - base_final;
+      batched_for16(0, zd::WSIZE / 8, [&](uint32_t i) { return prev16[i]; }, [&](uint32_t i, uint4 v) {
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          uint32_t o = 0;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const uint32_t pv = (w[e] >> (16 * h)) & 0xffff;
+            const int32_t nv = pv ? (int32_t)pv + shift : 0;
+            o |= (uint32_t)(nv > 0 ? nv : 0) << (16 * h);
+          }
+          w[e] = o;
+        }
+        prev16[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      });
+    }
     __syncthreads();
     // 4. links (wave 0) beside the window walk (wave 1)
     if (wv == 0) {
@@ -468,11 +521,21 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
     }
     __syncthreads();
     // 5. zlib's head[] for the next batch
-    if (persist)
-      for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x) {
-        const int32_t v = hpos[h];
-        const int32_t nv = v != HNONE ? v - base_final : 0;
-        head[h] = (uint16_t)(nv > 0 ? nv : 0);
+    if (persist)   // (eight entries a 16-B store)
+      for (uint32_t i = tid; i < (uint32_t)zd::WSIZE / 8; i += blockDim.x) {
+        uint32_t w[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          uint32_t o = 0;
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const int32_t v = hpos[8 * i + 2 * e + h];
+            const int32_t nv = v != HNONE ? v - base_final : 0;
+            o |= (uint32_t)(nv > 0 ? nv : 0) << (16 * h);
+          }
+          w[e] = o;
+        }
+        ((uint4*)head)[i] = make_uint4(w[0], w[1], w[2], w[3]);
       }
     __syncthreads();
     k = c_end;
