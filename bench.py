@@ -715,7 +715,7 @@ def deflate_line(ctx, dev, steps, warmup, n_s=8192, msgs=16, msg_bytes=4096, lev
             assert oh[o:o + ln].tobytes() == ref[i][3] and int(od[k]["flags"]) == 0x80 | 0x40 | 0x02, \
                 ("deflate mismatch", s, i)
     del oh
-    kernels = ["k_defl_prep", "k_defl_match_lds", "k_defl_match", "k_defl_parse"]
+    kernels = ["k_defl_prep", "k_defl_links", "k_defl_match_lds", "k_defl_match", "k_defl_parse"]
     el, kms, pipe = _timed(ctx, step, steps, warmup, dev, kernels)
     alg = plain + comp
     ach = alg / (kms / 1e3) / 1e9
@@ -757,7 +757,7 @@ def deflate_line(ctx, dev, steps, warmup, n_s=8192, msgs=16, msg_bytes=4096, lev
                       f"byte-identical to zlib)",
             "value": round(plain * steps / el / 2**30, 3), "unit": "GiB/s (uncompressed bytes)",
             "ms_per_step": round(el / steps * 1e3, 4),
-            "roofline": {"kernel": "k_defl_prep + k_defl_match_lds + k_defl_match + k_defl_parse (the compress launches of a step)",
+            "roofline": {"kernel": "k_defl_prep + k_defl_links + k_defl_match_lds + k_defl_match + k_defl_parse (the compress launches of a step)",
                          "bound": "per-position hash-chain match search and per-frame lazy parse (latency, issue), "
                                   "not hbm",
                          "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -22,7 +22,7 @@ const char* const kKernelNames[K_COUNT] = {"k_parse",   "k_scan",     "k_link", 
                                            "k_final",    "k_enc_len",  "k_enc_scan",
                                            "k_enc_piecesN", "k_enc_final", "k_enc_desc", "k_agg_plan", "k_agg_gather", "k_inflate", "k_hs_accept", "k_infl_tok", "k_infl_fast", "k_hs_validate",
                                            "k_defl_plan", "k_defl_prep", "k_defl_match", "k_defl_parse", "k_defl_final", "k_defl_serial",
-                                           "k_defl_trees", "k_defl_emit", "k_defl_hist", "k_defl_match_lds"};
+                                           "k_defl_trees", "k_defl_emit", "k_defl_hist", "k_defl_match_lds", "k_defl_links"};
 
 struct DevBuf {
   void* p = nullptr;
@@ -161,7 +161,7 @@ template <typename F>
 static void timed(wsg_ctx* c, int kid, F&& f) {
   // an event pair costs a few microseconds of queue time: mode 2 brackets only the
   // streaming kernels, so a timed step keeps the side kernels back to back
-  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL && kid != K_DEFL_TREES && kid != K_DEFL_MATCH_LDS &&
+  if (!c->timing || (c->timing == 2 && kid != K_UNMASK && kid != K_ENC_EMIT && kid != K_AGG_GATHER && kid != K_INFLATE && kid != K_HS_ACCEPT && kid != K_HS_VALIDATE && kid != K_INFL_TOK && kid != K_INFL_FAST && kid != K_DEFL_MATCH && kid != K_DEFL_PARSE && kid != K_DEFL_PREP && kid != K_DEFL_SERIAL && kid != K_DEFL_TREES && kid != K_DEFL_MATCH_LDS && kid != K_DEFL_LINKS &&
                                  kid != K_DEFL_EMIT && kid != K_DEFL_HIST)) {
     f();
     return;
@@ -1234,6 +1234,7 @@ int deflate_launch(wsg_ctx* c, int level, int no_context, const wsg_frame_desc* 
     a.sym = (uint32_t*)c->d_sym.p;
     a.blocks = (DeflBlock*)c->d_blocks.p;
     timed(c, K_DEFL_PREP, [&] { launch_defl_prep(a, c->stream); });
+    timed(c, K_DEFL_LINKS, [&] { launch_defl_links(a, c->stream); });
     if (tot[3]) {
       if (a.match_lds) timed(c, K_DEFL_MATCH_LDS, [&] { launch_defl_match_lds(a, c->stream); });
       timed(c, K_DEFL_MATCH, [&] { launch_defl_match(a, c->stream); });

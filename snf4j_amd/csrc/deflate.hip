@@ -216,10 +216,15 @@ __device__ __noinline__ int32_t link_repeats(uint32_t h, bool part, int32_t g, i
   }
   return pr;
 }
+// All the workgroup's waves (LINK_WAVES), batch b of a round to wave b: the waves load and
+// hash their batches together, issue their atomics in turn (a barrier after each wave's
+// turn, so batch order is position order), then resolve repeats and store together.
+constexpr int LINK_WAVES = 4;
 __device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint16_t* prev, int32_t p_begin,
                           int32_t p_last, int32_t nil_pos, bool persist, int32_t base_final) {
-  const int lane = threadIdx.x & 63;
-  for (int32_t g0 = p_begin; g0 <= p_last; g0 += 64 * LINK_BATCH) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int32_t r0 = p_begin; r0 <= p_last; r0 += 64 * LINK_BATCH * LINK_WAVES) {
+    const int32_t g0 = r0 + 64 * LINK_BATCH * wave;
     uint32_t wv[LINK_BATCH], hh[LINK_BATCH];
     int32_t pred[LINK_BATCH];
 #pragma unroll
@@ -228,11 +233,17 @@ __device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint1
       wv[j] = p <= p_last ? load_u32u(S + p) : 0;
     }
 #pragma unroll
-    for (int j = 0; j < LINK_BATCH; j++) {   // the batch's atomics, in position order
-      const int32_t p = g0 + 64 * j + lane;
-      const bool part = p <= p_last && p != nil_pos;   // window index 0 of a deflater is NIL
-      hh[j] = zd::hash3(wv[j] & 0xff, (wv[j] >> 8) & 0xff, (wv[j] >> 16) & 0xff);
-      pred[j] = part ? atomicMax(&hpos[hh[j]], p) : HNONE;
+    for (int j = 0; j < LINK_BATCH; j++) hh[j] = zd::hash3(wv[j] & 0xff, (wv[j] >> 8) & 0xff, (wv[j] >> 16) & 0xff);
+    for (int t = 0; t < LINK_WAVES; t++) {
+      if (t == wave) {
+#pragma unroll
+        for (int j = 0; j < LINK_BATCH; j++) {   // the batch's atomics, in position order
+          const int32_t p = g0 + 64 * j + lane;
+          const bool part = p <= p_last && p != nil_pos;   // window index 0 of a deflater is NIL
+          pred[j] = part ? atomicMax(&hpos[hh[j]], p) : HNONE;
+        }
+      }
+      __syncthreads();
     }
 #pragma unroll
     for (int j = 0; j < LINK_BATCH; j++) {
@@ -410,8 +421,48 @@ __device__ uint32_t window_walk(const DeflArgs& a, uint8_t* W, const uint8_t* S,
   return hw;
 }
 
+// Segments of a session: runs of calls on one deflater (a DF_SEG call starts a new one)
+struct SegInfo {
+  uint32_t c0, c_end, c_last;
+  bool fresh, persist;
+  uint32_t strstart0, ins0, H;
+  int32_t seg_begin, base0, seg_end, base_final;
+};
+__device__ inline bool next_segment(const DeflArgs& a, const DeflSess& fs, const wsg_deflate_state& st, uint32_t& k,
+                                    uint32_t k1, SegInfo& g) {
+  while (k < k1 && (a.fflags[k] & DF_KIND) != PMD_CALL) k++;
+  if (k >= k1) return false;
+  g.c0 = k;
+  g.c_last = k;
+  g.c_end = k + 1;
+  for (uint32_t j = k + 1; j < k1; j++) {
+    const uint32_t fl = a.fflags[j];
+    if ((fl & DF_KIND) != PMD_CALL) continue;
+    if (fl & DF_SEG) break;
+    g.c_last = j;
+    g.c_end = j + 1;
+  }
+  const uint32_t fl0 = a.fflags[g.c0];
+  g.fresh = (fl0 & DF_SEG) != 0;
+  g.persist = (fl0 & DF_PERSIST) != 0;
+  g.strstart0 = g.fresh ? 0 : st.strstart;
+  g.ins0 = g.fresh ? 0 : st.insert;
+  g.H = g.fresh ? 0 : (g.strstart0 < (uint32_t)zd::WSIZE ? g.strstart0 : (uint32_t)zd::WSIZE);
+  const DeflFrame f0 = a.ff[g.c0], fl_ = a.ff[g.c_last];
+  g.seg_begin = g.fresh ? (int32_t)f0.s_rel : (int32_t)(DEFL_HIST - g.H);
+  g.base0 = g.fresh ? (int32_t)f0.s_rel : (int32_t)DEFL_HIST - (int32_t)g.strstart0;
+  g.seg_end = (int32_t)(fl_.s_rel + fl_.len);
+  g.base_final = g.seg_end - (int32_t)fs.sw_final;
+  k = g.c_end;
+  return true;
+}
+
+// The stream and the window (no LDS table: many sessions a CU): per segment the stream S
+// (history, then the frames' bytes), the history strings' links from zlib's prev[], the
+// slides applied to the prev entries no string of the batch replaces, and the window walk
+// (zlib's window image, the strips); the match-chunk list.  k_defl_links then hashes the
+// segment's strings.
 __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
-  __shared__ int32_t hpos[zd::WSIZE];   // 128 KiB: last position of each hash (S coordinates)
   const uint32_t s = blockIdx.x, tid = threadIdx.x, wv = tid >> 6;
   const DeflSess fs = a.fs[s];
   if (fs.last_call == ~0u) return;
@@ -437,60 +488,29 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
     }
   }
   uint32_t k = k0;
-  for (;;) {
-    while (k < k1 && (a.fflags[k] & DF_KIND) != PMD_CALL) k++;
-    if (k >= k1) break;
-    const uint32_t c0 = k;
-    uint32_t c_last = c0, c_end = c0 + 1;
-    for (uint32_t j = c0 + 1; j < k1; j++) {
-      const uint32_t fl = a.fflags[j];
-      if ((fl & DF_KIND) != PMD_CALL) continue;
-      if (fl & DF_SEG) break;
-      c_last = j;
-      c_end = j + 1;
-    }
-    const uint32_t fl0 = a.fflags[c0];
-    const bool fresh = (fl0 & DF_SEG) != 0, persist = (fl0 & DF_PERSIST) != 0;
-    const uint32_t strstart0 = fresh ? 0 : st.strstart, ins0 = fresh ? 0 : st.insert;
-    const uint32_t H = fresh ? 0 : (strstart0 < (uint32_t)zd::WSIZE ? strstart0 : (uint32_t)zd::WSIZE);
-    const DeflFrame f0 = a.ff[c0], fl_ = a.ff[c_last];
-    const int32_t seg_begin = fresh ? (int32_t)f0.s_rel : (int32_t)(DEFL_HIST - H);
-    const int32_t base0 = fresh ? (int32_t)f0.s_rel : (int32_t)DEFL_HIST - (int32_t)strstart0;
-    const int32_t seg_end = (int32_t)(fl_.s_rel + fl_.len);
-    const int32_t base_final = seg_end - (int32_t)fs.sw_final;
+  SegInfo g;
+  while (next_segment(a, fs, st, k, k1, g)) {
     // 1. the stream: history, then the frames' bytes
-    if (!fresh) block_copy(S + DEFL_HIST - H, W + strstart0 - H, H);
-    for (uint32_t j = c0; j < c_end; j++) {
+    if (!g.fresh) block_copy(S + DEFL_HIST - g.H, W + g.strstart0 - g.H, g.H);
+    for (uint32_t j = g.c0; j < g.c_end; j++) {
       if ((a.fflags[j] & DF_KIND) != PMD_CALL) continue;
       const DeflFrame f = a.ff[j];
       block_copy(S + f.s_rel, a.payload + a.desc[j].payload_off, f.len);
     }
     __syncthreads();
-    // 2. links of the hashed history strings (zlib's prev[]); the hash heads
-    if (!fresh)
+    // 2. links of the hashed history strings (zlib's prev[])
+    const int32_t base0 = g.base0, base_final = g.base_final;
+    if (!g.fresh)
       batched_for(
-          DEFL_HIST - H, DEFL_HIST - ins0,
+          DEFL_HIST - g.H, DEFL_HIST - g.ins0,
           [&](uint32_t p) { return (uint32_t)prev[(uint32_t)((int32_t)p - base0) & zd::WMASK]; },
           [&](uint32_t p, uint32_t pv) {
             const uint32_t w = (uint32_t)((int32_t)p - base0);
             link[p] = (uint16_t)((pv != 0 && w - pv < (uint32_t)zd::WSIZE) ? w - pv : 0);
           });
-    if (fresh) {
-      for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x) hpos[h] = HNONE;
-    } else {   // (head as 16-B pieces, eight entries each, eight pieces of a thread in flight)
-      const uint4* head16 = (const uint4*)head;
-      batched_for16(0, zd::WSIZE / 8, [&](uint32_t i) { return head16[i]; }, [&](uint32_t i, uint4 v) {
-        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-        for (int e = 0; e < 8; e++) {
-          const uint32_t hv = (w[e >> 1] >> (16 * (e & 1))) & 0xffff;
-          hpos[8 * i + e] = hv == 0 ? HNONE : (int32_t)hv + base0;
-        }
-      });
-    }
     __syncthreads();
     // 3. the slides of this batch applied to the prev entries no string of it replaces
-    if (persist && !fresh && base_final != base0) {
+    if (g.persist && !g.fresh && base_final != base0) {
       uint4* prev16 = (uint4*)prev;
       const int32_t shift = base0 - base_final;
       batched_for16(0, zd::WSIZE / 8, [&](uint32_t i) { return prev16[i]; }, [&](uint32_t i, uint4 v) {
@@ -509,19 +529,58 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
         prev16[i] = make_uint4(w[0], w[1], w[2], w[3]);
       });
     }
-    __syncthreads();
-    // 4. links (wave 0) beside the window walk (wave 1)
+    // 4. the window walk (wave 0)
     if (wv == 0) {
-      const int32_t p_begin = fresh ? seg_begin : (int32_t)(DEFL_HIST - ins0);
-      // window index 0 is NIL: a deflater's first string, also when it is still pending (strstart <= 2)
-      link_pass(hpos, S, link, prev, p_begin, seg_end - 3, base0, persist, base_final);
-    } else if (wv == 1) {
-      const uint32_t hw = window_walk(a, W, S, c0, c_end, strstart0, fresh ? 0 : st.high_water);
-      if (persist && (tid & 63) == 0) a.fs[s].hw_final = hw;
+      const uint32_t hw = window_walk(a, W, S, g.c0, g.c_end, g.strstart0, g.fresh ? 0 : st.high_water);
+      if (g.persist && (tid & 63) == 0) a.fs[s].hw_final = hw;
     }
     __syncthreads();
-    // 5. zlib's head[] for the next batch
-    if (persist)   // (eight entries a 16-B store)
+  }
+}
+
+// The segments' strings hashed in position order (an LDS table of the last position of
+// each of the 32 K hashes: one session a CU), their links, zlib's prev[] entries for them,
+// and head[] for the next batch.
+__global__ __launch_bounds__(64 * LINK_WAVES) void k_defl_links(DeflArgs a) {
+  __shared__ int32_t hpos[zd::WSIZE];   // 128 KiB: last position of each hash (S coordinates)
+  const uint32_t s = blockIdx.x, tid = threadIdx.x, wv = tid >> 6;
+  const DeflSess fs = a.fs[s];
+  if (fs.last_call == ~0u) return;
+  Sums sm(a);
+  const uint64_t soff = sm.S[s];
+  const uint8_t* S = a.S + soff;
+  uint16_t* link = a.link + soff;
+  uint8_t* W = a.smem + (uint64_t)s * WSG_DEFLATE_SESSION_BYTES;
+  uint16_t* head = (uint16_t*)(W + zd::WINDOW_SIZE);
+  uint16_t* prev = head + zd::WSIZE;
+  const wsg_deflate_state st = a.state[s];
+  const uint32_t k0 = a.session_first[s], k1 = a.session_first[s + 1];
+  uint32_t k = k0;
+  SegInfo g;
+  while (next_segment(a, fs, st, k, k1, g)) {
+    const int32_t base0 = g.base0, base_final = g.base_final;
+    if (g.fresh) {
+      for (uint32_t h = tid; h < (uint32_t)zd::WSIZE; h += blockDim.x) hpos[h] = HNONE;
+    } else {   // (head as 16-B pieces, eight entries each, eight pieces of a thread in flight)
+      const uint4* head16 = (const uint4*)head;
+      batched_for16(0, zd::WSIZE / 8, [&](uint32_t i) { return head16[i]; }, [&](uint32_t i, uint4 v) {
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 8; e++) {
+          const uint32_t hv = (w[e >> 1] >> (16 * (e & 1))) & 0xffff;
+          hpos[8 * i + e] = hv == 0 ? HNONE : (int32_t)hv + base0;
+        }
+      });
+    }
+    __syncthreads();
+    {
+      const int32_t p_begin = g.fresh ? g.seg_begin : (int32_t)(DEFL_HIST - g.ins0);
+      // window index 0 is NIL: a deflater's first string, also when it is still pending (strstart <= 2)
+      link_pass(hpos, S, link, prev, p_begin, g.seg_end - 3, base0, g.persist, base_final);
+    }
+    __syncthreads();
+    // zlib's head[] for the next batch
+    if (g.persist)   // (eight entries a 16-B store)
       for (uint32_t i = tid; i < (uint32_t)zd::WSIZE / 8; i += blockDim.x) {
         uint32_t w[4];
 #pragma unroll
@@ -538,7 +597,6 @@ __global__ __launch_bounds__(256) void k_defl_prep(DeflArgs a) {
         ((uint4*)head)[i] = make_uint4(w[0], w[1], w[2], w[3]);
       }
     __syncthreads();
-    k = c_end;
   }
 }
 
@@ -1601,6 +1659,9 @@ void launch_defl_plan(const DeflArgs& a, hipStream_t s) {
 }
 void launch_defl_prep(const DeflArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_defl_prep, dim3(a.n_sessions), dim3(256), 0, s, a);
+}
+void launch_defl_links(const DeflArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(k_defl_links, dim3(a.n_sessions), dim3(64 * LINK_WAVES), 0, s, a);
 }
 void launch_defl_match(const DeflArgs& a, hipStream_t s) {
   uint64_t g = a.chunk_cap < 262144 ? a.chunk_cap : 262144;

@@ -315,7 +315,7 @@ enum KernelId {
   K_PARSE = 0, K_SCAN, K_LINK, K_UNMASK, K_FINAL,
   K_ENC_LEN, K_ENC_SCAN, K_ENC_EMIT, K_ENC_FINAL, K_ENC_DESC, K_AGG, K_AGG_GATHER, K_INFLATE, K_HS_ACCEPT, K_INFL_TOK, K_INFL_FAST, K_HS_VALIDATE,
   K_DEFL_PLAN, K_DEFL_PREP, K_DEFL_MATCH, K_DEFL_PARSE, K_DEFL_FINAL, K_DEFL_SERIAL, K_DEFL_TREES, K_DEFL_EMIT,
-  K_DEFL_HIST, K_DEFL_MATCH_LDS, K_COUNT
+  K_DEFL_HIST, K_DEFL_MATCH_LDS, K_DEFL_LINKS, K_COUNT
 };
 
 // launchers (enqueue on `s`; the timing hook wraps each one)
@@ -393,6 +393,7 @@ void launch_defl_plan(const DeflArgs& a, hipStream_t s);    // k_defl_plan + k_d
 void launch_defl_prep(const DeflArgs& a, hipStream_t s);
 void launch_defl_match(const DeflArgs& a, hipStream_t s);
 void launch_defl_match_lds(const DeflArgs& a, hipStream_t s);
+void launch_defl_links(const DeflArgs& a, hipStream_t s);
 void launch_defl_parse(const DeflArgs& a, hipStream_t s);
 void launch_defl_hist(const DeflArgs& a, hipStream_t s, uint64_t n_blocks);
 void launch_defl_trees(const DeflArgs& a, hipStream_t s, uint64_t n_blocks);
