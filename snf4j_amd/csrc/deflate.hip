@@ -199,7 +199,7 @@ __device__ inline uint32_t load_u32u(const uint8_t* p) {
 // sixteen atomics go out back to back, nothing waiting on another's return; its stream words
 // are loaded first and its links stored last (a store before a load would hold the load,
 // loads and stores sharing vmcnt).
-constexpr int LINK_BATCH = 16;
+constexpr int LINK_BATCH = 8;
 
 // the lanes of a group whose hash an earlier lane of the group has (r >= g): predecessor =
 // the nearest such lane below (positions are g + lane)
@@ -219,7 +219,7 @@ __device__ __noinline__ int32_t link_repeats(uint32_t h, bool part, int32_t g, i
 // All the workgroup's waves (LINK_WAVES), batch b of a round to wave b: the waves load and
 // hash their batches together, issue their atomics in turn (a barrier after each wave's
 // turn, so batch order is position order), then resolve repeats and store together.
-constexpr int LINK_WAVES = 4;
+constexpr int LINK_WAVES = 16;
 __device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint16_t* prev, int32_t p_begin,
                           int32_t p_last, int32_t nil_pos, bool persist, int32_t base_final) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1351,40 +1351,93 @@ __device__ inline void sym_code(uint32_t sy, const uint32_t* ltab, const uint32_
   *l2 = l + (uint32_t)dx;
 }
 
-// send_tree into a WordSink (thread 0 of k_defl_emit): zlib's run-length coding of a
-// tree's code lengths with the bit-length codes
-__device__ void send_tree_w(WordSink& o, const uint32_t* tab, int max_code, const uint32_t* btab) {
-  auto len_of = [&](int n) -> int { return n <= max_code ? (int)(tab[n] >> 16) : 0xffff; };
-  auto bl = [&](int sym) { o.put(btab[sym] & 0xffff, btab[sym] >> 16); };
-  int prevlen = -1, curlen, nextlen = len_of(0), count = 0, max_count = 7, min_count = 4;
-  if (nextlen == 0) max_count = 138, min_count = 3;
-  for (int n = 0; n <= max_code; n++) {
-    curlen = nextlen;
-    nextlen = len_of(n + 1);
-    if (++count < max_count && curlen == nextlen) {
-      continue;
-    } else if (count < min_count) {
-      do { bl(curlen); } while (--count != 0);
-    } else if (curlen != 0) {
-      if (curlen != prevlen) {
-        bl(curlen);
-        count--;
-      }
-      bl(zd::REP_3_6);
-      o.put((uint32_t)(count - 3), 2);
-    } else if (count <= 10) {
-      bl(zd::REPZ_3_10);
-      o.put((uint32_t)(count - 3), 3);
-    } else {
-      bl(zd::REPZ_11_138);
-      o.put((uint32_t)(count - 11), 7);
-    }
-    count = 0;
-    prevlen = curlen;
-    if (nextlen == 0) max_count = 138, min_count = 3;
-    else if (curlen == nextlen) max_count = 6, min_count = 3;
-    else max_count = 7, min_count = 4;
+// inclusive sum over the wave's lanes
+__device__ inline uint32_t wave_incl_sum(uint32_t x) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d);
+    if (lane >= d) x += y;
   }
+  return x;
+}
+
+// bits v (len <= 32) at bit offset off of the LDS words hb (zeroed)
+__device__ inline void lds_or_bits(uint32_t* hb, uint32_t off, uint32_t v, uint32_t len) {
+  if (!len) return;
+  const uint32_t sh = off & 31;
+  atomicOr(&hb[off >> 5], v << sh);
+  if (sh + len > 32) atomicOr(&hb[(off >> 5) + 1], v >> (32 - sh));
+}
+
+// zlib's send_tree (the run-length coding of a tree's code lengths with the bit-length
+// codes) by one wave, 64 code lengths a round, into the LDS words hb from bit pos on;
+// returns the bit position after it.  zlib's loop cuts each run of equal lengths into
+// chunks (at most 7, then 6, entries of a non-zero length; 138 of zeros) whose coding
+// depends only on the chunk (its length, count, and whether it continues the run), so
+// each chunk's first lane codes it: (count < min) the length count times; (non-zero) the
+// length unless continued, REP_3_6 + 2 bits; (zeros) REPZ_3_10 + 3 bits or REPZ_11_138 + 7
+// bits.  run_end: LDS scratch of max_code + 1 entries.
+__device__ uint32_t send_tree_wave(uint32_t* hb, uint32_t pos, const uint32_t* tab, int max_code, const uint32_t* btab,
+                                   uint16_t* run_end) {
+  const int lane = (int)(threadIdx.x & 63);
+  auto len_of = [&](int n) -> uint32_t { return n < 0 ? 0x1ffffu : (n <= max_code ? tab[n] >> 16 : 0xffffu); };
+  // the last index of each index's run (a backward sweep, the carry from the window above)
+  uint32_t carry = (uint32_t)max_code;
+  for (int base = max_code & ~63; base >= 0; base -= 64) {
+    const int n = base + lane;
+    const bool valid = n <= max_code;
+    const uint64_t m = __ballot(valid && len_of(n) != len_of(n + 1));
+    const uint64_t hi = m & (~0ull << lane);
+    if (valid) run_end[n] = (uint16_t)(hi ? (uint32_t)base + (uint32_t)__builtin_ctzll(hi) : carry);
+    carry = m ? (uint32_t)base + (uint32_t)__builtin_ctzll(m) : carry;
+  }
+  wave_mem_sync();
+  uint32_t r0c = 0;   // the first index of the run the window above ended in
+  for (int base = 0; base <= max_code; base += 64) {
+    const int n = base + lane;
+    const bool valid = n <= max_code;
+    const uint32_t v = valid ? len_of(n) : 0u;
+    const uint64_t sm = __ballot(valid && v != len_of(n - 1));
+    const uint64_t lo = sm & ((2ull << lane) - 1);   // (lane 63: all bits)
+    const uint32_t r0 = lo ? (uint32_t)base + 63u - (uint32_t)__builtin_clzll(lo) : r0c;
+    r0c = sm ? (uint32_t)base + 63u - (uint32_t)__builtin_clzll(sm) : r0c;
+    const uint32_t o = (uint32_t)n - r0;
+    const bool cs = valid && (v == 0 ? o % 138 == 0 : (o == 0 || (o >= 7 && (o - 7) % 6 == 0)));
+    uint32_t code = 0, len = 0;
+    if (cs) {
+      const bool cont = o != 0;   // a chunk after the run's first: the previous length is its own
+      const uint32_t rem = (uint32_t)run_end[n] - (uint32_t)n + 1;
+      const uint32_t mx = v == 0 ? 138u : (cont ? 6u : 7u), mn = (v == 0 || cont) ? 3u : 4u;
+      const uint32_t c = rem < mx ? rem : mx;
+      auto put = [&](uint32_t cv, uint32_t cl) {
+        code |= cv << len;
+        len += cl;
+      };
+      auto bl = [&](uint32_t sym) { put(btab[sym] & 0xffff, btab[sym] >> 16); };
+      if (c < mn) {
+        for (uint32_t i = 0; i < c; i++) bl(v);
+      } else if (v != 0) {
+        uint32_t cc = c;
+        if (!cont) {
+          bl(v);
+          cc--;
+        }
+        bl(zd::REP_3_6);
+        put(cc - 3, 2);
+      } else if (c <= 10) {
+        bl(zd::REPZ_3_10);
+        put(c - 3, 3);
+      } else {
+        bl(zd::REPZ_11_138);
+        put(c - 11, 7);
+      }
+    }
+    const uint32_t incl = wave_incl_sum(len);
+    lds_or_bits(hb, pos + incl - len, code, len);
+    pos += __shfl(incl, 63);
+  }
+  return pos;
 }
 
 // workgroup per frame: the bits of its blocks (stored copies, static or dynamic codes: the
@@ -1392,10 +1445,13 @@ __device__ void send_tree_w(WordSink& o, const uint32_t* tab, int max_code, cons
 // sync marker, into the frame's zeroed output slot
 constexpr int EMIT_T = 256;
 constexpr uint32_t EMIT_SYM = 4096;
+constexpr uint32_t EMIT_HDR_W = 80;   // 31 + 17 + 57 + 7 x (286 + 30) bits at most
 __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
   __shared__ uint32_t s_ltab[286], s_dtab[30], s_btab[19];
   __shared__ uint32_t s_sym[EMIT_SYM];   // a block's symbols, loaded once, coalesced (blocks up to EMIT_SYM)
-  __shared__ uint32_t s_scan[EMIT_T];
+  __shared__ uint32_t s_wsum[EMIT_T / 64];
+  __shared__ uint32_t s_hdr[EMIT_HDR_W];   // a dynamic block's header bits
+  __shared__ uint16_t s_run[zd::L_CODES];  // send_tree_wave's run ends
   __shared__ uint32_t s_off;   // running bit offset of the frame
   Sums sm(a);
   const uint32_t tid = threadIdx.x;
@@ -1493,21 +1549,23 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
         sym_code(sym_at(i), s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
         mybits += l1 + l2;
       }
-      s_scan[tid] = mybits;
+      // bit offsets: wave sums, then the waves' totals (one barrier)
+      const uint32_t incl = wave_incl_sum(mybits);
+      if ((tid & 63) == 63) s_wsum[tid >> 6] = incl;
       __syncthreads();
-      for (uint32_t st = 1; st < EMIT_T; st <<= 1) {
-        const uint32_t y = tid >= st ? s_scan[tid - st] : 0;
-        __syncthreads();
-        s_scan[tid] += y;
-        __syncthreads();
+      uint32_t before = 0, sym_bits = 0;
+#pragma unroll
+      for (uint32_t w = 0; w < EMIT_T / 64; w++) {
+        const uint32_t x = s_wsum[w];
+        before += w < (tid >> 6) ? x : 0u;
+        sym_bits += x;
       }
-      const uint32_t sym_bits = s_scan[EMIT_T - 1];
       const uint32_t eob_c = is_static ? zd::static_lcode(zd::END_BLOCK) : s_ltab[zd::END_BLOCK] & 0xffff;
       const uint32_t eob_l = is_static ? 7u : s_ltab[zd::END_BLOCK] >> 16;
       const uint32_t blk_end = o + 3 + B->bits;
       const uint32_t sym_start = blk_end - eob_l - sym_bits;
       {
-        WordSink ws(ow, sym_start + s_scan[tid] - mybits);
+        WordSink ws(ow, sym_start + before + incl - mybits);
         for (uint32_t i = i0; i < i1; i++) {
           uint32_t c1, l1, c2, l2;
           sym_code(sym_at(i), s_ltab, s_dtab, is_static, &c1, &l1, &c2, &l2);
@@ -1517,19 +1575,31 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
         if (tid == EMIT_T - 1) ws.put(eob_c, eob_l);
         ws.done();
       }
-      if (tid == 0) {   // the block header, then (dynamic) send_all_trees
-        WordSink ws(ow, o);
-        ws.put(is_static ? 2u : 4u, 3);
-        if (!is_static) {
-          const int lcodes = B->lcodes, dcodes = B->dcodes, blcodes = B->blcodes;
-          ws.put((uint32_t)(lcodes - 257), 5);
-          ws.put((uint32_t)(dcodes - 1), 5);
-          ws.put((uint32_t)(blcodes - 4), 4);
-          for (int r = 0; r < blcodes; r++) ws.put(s_btab[zd::bl_order(r)] >> 16, 3);
-          send_tree_w(ws, s_ltab, lcodes - 1, s_btab);
-          send_tree_w(ws, s_dtab, dcodes - 1, s_btab);
+      if (is_static) {   // the block header
+        if (tid == 0) {
+          WordSink ws(ow, o);
+          ws.put(2u, 3);
+          ws.done();
         }
-        ws.done();
+      } else if (tid < 64) {   // the header and send_all_trees by wave 0, into LDS words, then out
+        const uint32_t lane = tid, sh = o & 31;
+        for (uint32_t i = lane; i < EMIT_HDR_W; i += 64) s_hdr[i] = 0;
+        wave_mem_sync();
+        const int lcodes = B->lcodes, dcodes = B->dcodes, blcodes = B->blcodes;
+        if (lane == 0)
+          lds_or_bits(s_hdr, sh, 4u | (uint32_t)(lcodes - 257) << 3 | (uint32_t)(dcodes - 1) << 8 | (uint32_t)(blcodes - 4) << 13,
+                      17);
+        if ((int)lane < blcodes) lds_or_bits(s_hdr, sh + 17 + 3 * lane, s_btab[zd::bl_order((int)lane)] >> 16, 3);
+        uint32_t pos = sh + 17 + 3 * (uint32_t)blcodes;
+        pos = send_tree_wave(s_hdr, pos, s_ltab, lcodes - 1, s_btab, s_run);
+        wave_mem_sync();
+        pos = send_tree_wave(s_hdr, pos, s_dtab, dcodes - 1, s_btab, s_run);
+        wave_mem_sync();
+        const uint32_t nw = (pos + 31) >> 5, w0 = o >> 5;   // (the first and last words shared)
+        for (uint32_t i = lane; i < nw; i += 64) {
+          if (i == 0 || i == nw - 1) atomicOr(&ow[w0 + i], s_hdr[i]);
+          else ow[w0 + i] = s_hdr[i];
+        }
       }
       __syncthreads();
       if (tid == 0) s_off = blk_end;
