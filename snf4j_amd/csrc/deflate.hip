@@ -732,44 +732,40 @@ __device__ inline void ring_init(RingWalk& w, const LdsRing& R, uint32_t p) {
   w.b = ring8(R, pr);
 }
 
-// one candidate; true when the walk is over
+// one candidate; true when the walk is over.  Branch-light: the common prefix of the first
+// 8 bytes comes from the compare word (a chain joins strings of one hash, so two equal
+// bytes mean three), and a candidate takes the lead when that prefix is longer than the
+// best: zlib's scan_end pre-checks only skip candidates that cannot.  Only a prefix of all 8
+// bytes goes on comparing.
 __device__ inline bool ring_step(RingWalk& w, const LdsRing& R, const zd::Cfg& c) {
   const uint64_t x = ring8(R, w.q) ^ w.b;
   const uint32_t l = R.link[w.q];
-  if ((x & 0xFFFF) == 0) {
-    const bool cand = w.best < 8 ? ((x >> (8 * w.best)) & 0xFF) == 0 : ring1(R, w.q + w.best) == ring1(R, w.pr + w.best);
-    if (cand) {
-      uint32_t len;
-      if (x) {
-        len = (uint32_t)__builtin_ctzll(x) >> 3;
-      } else {
-        len = 8;
-        for (;;) {
-          const uint64_t y = ring8(R, w.q + len) ^ ring8(R, w.pr + len);
-          if (y) {
-            len += (uint32_t)__builtin_ctzll(y) >> 3;
-            break;
-          }
-          len += 8;
-          if (len >= (uint32_t)zd::MAX_MATCH) break;
-        }
-        if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
+  uint32_t len = (uint32_t)__builtin_ctzll(x | (1ull << 63)) >> 3;   // (7 for x == 0 and x's top byte)
+  if (x == 0) {
+    len = 8;
+    for (;;) {
+      const uint64_t y = ring8(R, w.q + len) ^ ring8(R, w.pr + len);
+      if (y) {
+        len += (uint32_t)__builtin_ctzll(y) >> 3;
+        break;
       }
-      if (len > w.best) {
-        w.best = len;
-        w.best_d = w.dist;
-        if (len >= c.nice) return true;
-      }
+      len += 8;
+      if (len >= (uint32_t)zd::MAX_MATCH) break;
     }
+    if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
   }
+  const bool upd = len > w.best;
+  w.best = upd ? len : w.best;
+  w.best_d = upd ? w.dist : w.best_d;
   if (w.k == (uint32_t)(c.chain >> 2)) w.qres = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
-  if (w.k >= c.chain) return true;
-  if (l == 0) return true;
-  w.dist += l;
-  if (w.dist >= (uint32_t)zd::MAX_DIST) return true;
-  w.q = w.q >= l ? w.q - l : w.q + DEFL_RING - l;
-  w.k++;
-  return false;
+  const uint32_t nd = w.dist + l;
+  const bool end = (upd && len >= c.nice) || w.k >= c.chain || l == 0 || nd >= (uint32_t)zd::MAX_DIST;
+  if (!end) {
+    w.dist = nd;
+    w.q = w.q >= l ? w.q - l : w.q + DEFL_RING - l;
+    w.k++;
+  }
+  return end;
 }
 
 __device__ inline void ring_result(const RingWalk& w, const zd::Cfg& c, uint32_t p0d, uint32_t* full, uint32_t* quarter) {
