@@ -631,33 +631,26 @@ __device__ inline void fast_init(FastWalk& w, const uint8_t* S, const uint16_t* 
 __device__ inline bool fast_step(FastWalk& w, const uint8_t* S, const uint16_t* link, uint32_t p, const zd::Cfg& c) {
   const uint32_t qbudget = c.chain >> 2;
   const uint8_t* mq = S + w.q;
+  // (branch-light, as ring_step)
   const uint64_t x = load_u64(mq) ^ w.b;
-  if ((x & 0xFFFF) == 0) {
-    const bool cand = w.best < 8 ? ((x >> (8 * w.best)) & 0xFF) == 0 : mq[w.best] == S[p + w.best];
-    if (cand) {
-      uint32_t len;
-      if (x) {
-        len = (uint32_t)__builtin_ctzll(x) >> 3;
-      } else {
-        len = 8;
-        for (;;) {
-          const uint64_t y = load_u64(mq + len) ^ load_u64(S + p + len);
-          if (y) {
-            len += (uint32_t)__builtin_ctzll(y) >> 3;
-            break;
-          }
-          len += 8;
-          if (len >= (uint32_t)zd::MAX_MATCH) break;
-        }
-        if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
+  uint32_t len = (uint32_t)__builtin_ctzll(x | (1ull << 63)) >> 3;
+  if (x == 0) {
+    len = 8;
+    for (;;) {
+      const uint64_t y = load_u64(mq + len) ^ load_u64(S + p + len);
+      if (y) {
+        len += (uint32_t)__builtin_ctzll(y) >> 3;
+        break;
       }
-      if (len > w.best) {
-        w.best = len;
-        w.best_d = w.dist;
-        if (len >= c.nice) return true;
-      }
+      len += 8;
+      if (len >= (uint32_t)zd::MAX_MATCH) break;
     }
+    if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
   }
+  const bool upd = len > w.best;
+  w.best = upd ? len : w.best;
+  w.best_d = upd ? w.dist : w.best_d;
+  if (upd && len >= c.nice) return true;
   if (w.k == qbudget) w.qres = w.best > 2 ? ((w.best - 2) | w.best_d << 9) : 0;
   if (w.k >= c.chain) return true;
   const uint32_t l = link[w.q];
@@ -949,34 +942,26 @@ __device__ void tail_match_at(const uint8_t* S, const uint8_t* strip, const uint
   const uint64_t b = tail8(S, strip, end, s);
   uint32_t best = 2, best_d = 0, qres = 0, q = s - d, dist = d, k = 1;
   for (;; k++) {
+    // (branch-light, as ring_step)
     const uint64_t x = tail8(S, strip, end, q) ^ b;
-    if ((x & 0xFFFF) == 0) {
-      const bool cand = best < 8 ? ((x >> (8 * best)) & 0xFF) == 0
-                                 : (tail8(S, strip, end, q + best) & 0xFF) == (tail8(S, strip, end, s + best) & 0xFF);
-      if (cand) {
-        uint32_t len;
-        if (x) {
-          len = (uint32_t)__builtin_ctzll(x) >> 3;
-        } else {
-          len = 8;
-          for (;;) {
-            const uint64_t y = tail8(S, strip, end, q + len) ^ tail8(S, strip, end, s + len);
-            if (y) {
-              len += (uint32_t)__builtin_ctzll(y) >> 3;
-              break;
-            }
-            len += 8;
-            if (len >= (uint32_t)zd::MAX_MATCH) break;
-          }
-          if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
+    uint32_t len = (uint32_t)__builtin_ctzll(x | (1ull << 63)) >> 3;
+    if (x == 0) {
+      len = 8;
+      for (;;) {
+        const uint64_t y = tail8(S, strip, end, q + len) ^ tail8(S, strip, end, s + len);
+        if (y) {
+          len += (uint32_t)__builtin_ctzll(y) >> 3;
+          break;
         }
-        if (len > best) {
-          best = len;
-          best_d = dist;
-          if (len >= nice) break;
-        }
+        len += 8;
+        if (len >= (uint32_t)zd::MAX_MATCH) break;
       }
+      if (len > (uint32_t)zd::MAX_MATCH) len = zd::MAX_MATCH;
     }
+    const bool upd = len > best;
+    best = upd ? len : best;
+    best_d = upd ? dist : best_d;
+    if (upd && len >= nice) break;
     if (k == qbudget) qres = best > 2 ? ((best - 2) | best_d << 9) : 0;
     if (k >= c.chain) break;
     const uint32_t l = link[q];
