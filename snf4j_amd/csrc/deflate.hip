@@ -1064,6 +1064,9 @@ struct ResWin {
   uint32_t tstart;
   uint32_t wbase;
   uint4 w0, w1, w2, w3;  // positions wbase .. wbase + 7
+  const uint8_t* S;      // session stream
+  uint64_t blo, bhi;     // its bytes wbase - 8 .. wbase + 7, loaded with the results: the
+                         // literal a step may take is the byte before its position
   __device__ void operator()(uint32_t p, int variant, uint32_t* f, uint32_t* q) {
     if (variant && p >= tstart) {
       const uint32_t* t = tres + 2 * (p - tstart);
@@ -1079,6 +1082,8 @@ struct ResWin {
       w1 = r[1];
       w2 = r[2];
       w3 = r[3];
+      blo = b >= 8 ? *(const uint64_t*)(S + b - 8) : 0ull;
+      bhi = *(const uint64_t*)(S + b);
     }
     const uint32_t i = p & 7;   // component selects only: an aggregate select would live in scratch
     const bool o = i & 1, b1 = i & 2, b2 = i & 4;
@@ -1091,20 +1096,14 @@ struct ResWin {
     *q = b2 ? hy : ly;
   }
 };
+// the parse's byte(p): from the results window's bytes (a byte outside them, at a frame's
+// last positions where no lookup ran, from the stream)
 struct ByteWin {
-  const uint8_t* S;
-  uint32_t wbase;
-  uint4 w;
-  __device__ uint32_t operator()(uint32_t p) {
-    const uint32_t b = p & ~15u;
-    if (b != wbase) {
-      wbase = b;
-      w = *(const uint4*)(S + b);
-    }
-    const uint32_t i = p & 15;
-    const uint32_t lo = (i & 4) ? w.y : w.x, hi = (i & 4) ? w.w : w.z;
-    const uint32_t x = (i & 8) ? hi : lo;
-    return (x >> (8 * (i & 3))) & 0xff;
+  const ResWin* r;
+  __device__ uint32_t operator()(uint32_t p) const {
+    const uint32_t o = p + 8 - r->wbase;
+    if (o >= 16 || r->wbase == ~0u) return r->S[p];
+    return (uint32_t)(((o < 8 ? r->blo : r->bhi) >> (8 * (o & 7))) & 0xff);
   }
 };
 constexpr uint32_t SYM_RING = 32;
@@ -1184,8 +1183,8 @@ __global__ __launch_bounds__(64) void k_defl_parse(DeflArgs a) {
     const uint64_t soff = sm.S[f.sess];
     const uint32_t end = f.s_rel + f.len;
     ResWin ra{(const uint4*)(a.res + 2 * soff), a.tres + (uint64_t)k * DEFL_TAILN * 2,
-              end - f.s_rel > DEFL_TAILN ? end - DEFL_TAILN : f.s_rel, ~0u, {}, {}, {}, {}};
-    ByteWin by{a.S + soff, ~0u, {}};
+              end - f.s_rel > DEFL_TAILN ? end - DEFL_TAILN : f.s_rel, ~0u, {}, {}, {}, {}, a.S + soff, 0ull, 0ull};
+    ByteWin by{&ra};
     zd::CallGeom g{f.start_w, (uint8_t)((fl & DF_START_SLID) ? 1 : 0)};
     DeflBlock* blk = a.blocks + sm.B[f.sess] + f.blk_rel;
     const uint64_t sym_at = sm.Y[f.sess] + a.fsym[k];
@@ -1618,11 +1617,21 @@ __global__ __launch_bounds__(256) void k_defl_final(DeflArgs a) {
     if (a.ftail[fs.last_call]) {   // the window slid inside the last frame's tail
       uint8_t* W = a.smem + (uint64_t)s * WSG_DEFLATE_SESSION_BYTES;
       uint16_t* hp = (uint16_t*)(W + zd::WINDOW_SIZE);
-      for (uint32_t i = tid; i < sw - zd::WSIZE; i += blockDim.x) W[i] = W[i + zd::WSIZE];
-      for (uint32_t j = tid; j < 2u * zd::WSIZE; j += blockDim.x) {
-        const uint32_t v = hp[j];
-        hp[j] = (uint16_t)(v >= (uint32_t)zd::WSIZE ? v - zd::WSIZE : 0);
-      }
+      // (the two ranges are disjoint: sw <= 2 WSIZE; 16-B pieces, eight in flight a thread)
+      const uint32_t n = sw - zd::WSIZE, n16 = n >> 4;
+      uint4* W16 = (uint4*)W;
+      batched_for16(0, n16, [&](uint32_t i) { return W16[i + zd::WSIZE / 16]; }, [&](uint32_t i, uint4 v) { W16[i] = v; });
+      for (uint32_t i = 16 * n16 + tid; i < n; i += blockDim.x) W[i] = W[i + zd::WSIZE];
+      uint4* hp16 = (uint4*)hp;
+      batched_for16(0, 2u * zd::WSIZE / 8, [&](uint32_t i) { return hp16[i]; }, [&](uint32_t i, uint4 v) {
+        uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+          const uint32_t lo = w[e] & 0xffff, hi = w[e] >> 16;
+          w[e] = (lo >= (uint32_t)zd::WSIZE ? lo - zd::WSIZE : 0) | (hi >= (uint32_t)zd::WSIZE ? hi - zd::WSIZE : 0) << 16;
+        }
+        hp16[i] = make_uint4(w[0], w[1], w[2], w[3]);
+      });
       sw -= zd::WSIZE;
     }
     st.strstart = sw;
