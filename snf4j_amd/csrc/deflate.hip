@@ -1425,6 +1425,7 @@ __device__ uint32_t send_tree_wave(uint32_t* hb, uint32_t pos, const uint32_t* t
 // sync marker, into the frame's zeroed output slot
 constexpr int EMIT_T = 256;
 constexpr uint32_t EMIT_SYM = 4096;
+constexpr uint32_t EMIT_OUT_W = 2048;   // 8 KiB
 constexpr uint32_t EMIT_HDR_W = 80;   // 31 + 17 + 57 + 7 x (286 + 30) bits at most
 __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
   __shared__ uint32_t s_ltab[286], s_dtab[30], s_btab[19];
@@ -1432,6 +1433,7 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
   __shared__ uint32_t s_wsum[EMIT_T / 64];
   __shared__ uint32_t s_hdr[EMIT_HDR_W];   // a dynamic block's header bits
   __shared__ uint16_t s_run[zd::L_CODES];  // send_tree_wave's run ends
+  __shared__ uint32_t s_out[EMIT_OUT_W];   // the frame's output (frames up to EMIT_OUT_W words)
   __shared__ uint32_t s_off;   // running bit offset of the frame
   Sums sm(a);
   const uint32_t tid = threadIdx.x;
@@ -1440,8 +1442,7 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
     if ((fl & DF_KIND) != PMD_CALL) continue;
     const DeflFrame f = a.ff[k];
     const uint64_t obase = sm.O[f.sess] + a.fout[k];
-    uint8_t* ob = a.out + obase;
-    uint32_t* ow = (uint32_t*)ob;
+    uint8_t* const ob_g = a.out + obase;
     const DeflBlock* blk = a.blocks + sm.B[f.sess] + f.blk_rel;
     const uint32_t nb = a.level == 0 ? 0 : f.nblk;
     // the frame's size: blocks in order, then the sync marker (3 bits, pad, 00 00 FF FF)
@@ -1454,6 +1455,12 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
         bitsz = blk[b].type == 0 ? ((bitsz + 3 + 7) & ~7ull) + 32 + 8ull * blk[b].stored_len : bitsz + 3 + blk[b].bits;
     }
     const uint64_t bytes = (((bitsz + 3 + 7) & ~7ull) + 32) >> 3;
+    // a frame's output up to EMIT_OUT_W words is put together in LDS and stored once, in
+    // order (the global form's zeroing, atomics and barrier waits on stores cost more than
+    // the bits); larger frames write their slot directly
+    const bool lds_out = ((bytes + 3) >> 2) <= EMIT_OUT_W;
+    uint8_t* const ob = lds_out ? (uint8_t*)s_out : ob_g;
+    uint32_t* const ow = (uint32_t*)ob;
     for (uint64_t i = tid; i < (bytes + 3) >> 2; i += EMIT_T) ow[i] = 0;
     if (tid == 0) s_off = 0;
     __syncthreads();
@@ -1599,6 +1606,10 @@ __global__ __launch_bounds__(EMIT_T) void k_defl_emit(DeflArgs a) {
       a.out_desc[k] = o;
     }
     __syncthreads();
+    if (lds_out) {
+      uint32_t* const og = (uint32_t*)ob_g;
+      for (uint32_t i = tid; i < (uint32_t)((bytes + 3) >> 2); i += EMIT_T) og[i] = s_out[i];
+    }
   }
 }
 
