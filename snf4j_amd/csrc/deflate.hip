@@ -720,8 +720,8 @@ __device__ inline void ring_init(RingWalk& w, const LdsRing& R, uint32_t p) {
   w.best_d = 0;
   w.qres = 0;
   w.dist = d;
-  w.q = pr >= d ? pr - d : pr + DEFL_RING - d;
   w.done = d == 0 || d > (uint32_t)zd::MAX_DIST;
+  w.q = w.done ? pr : (pr >= d ? pr - d : pr + DEFL_RING - d);   // (a done walk still steps: in the ring)
   w.b = ring8(R, pr);
 }
 
@@ -730,11 +730,11 @@ __device__ inline void ring_init(RingWalk& w, const LdsRing& R, uint32_t p) {
 // bytes mean three), and a candidate takes the lead when that prefix is longer than the
 // best: zlib's scan_end pre-checks only skip candidates that cannot.  Only a prefix of all 8
 // bytes goes on comparing.
-__device__ inline bool ring_step(RingWalk& w, const LdsRing& R, const zd::Cfg& c) {
+__device__ inline bool ring_step(RingWalk& w, const LdsRing& R, const zd::Cfg& c, bool live) {
   const uint64_t x = ring8(R, w.q) ^ w.b;
   const uint32_t l = R.link[w.q];
   uint32_t len = (uint32_t)__builtin_ctzll(x | (1ull << 63)) >> 3;   // (7 for x == 0 and x's top byte)
-  if (x == 0) {
+  if (x == 0 && live) {   // (a lane not walking must not compare on: its string may be itself)
     len = 8;
     for (;;) {
       const uint64_t y = ring8(R, w.q + len) ^ ring8(R, w.pr + len);
@@ -862,6 +862,7 @@ __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
     bool act = p < cend;
     next = next + 64 < cend ? next + 64 : cend;
     RingWalk w;
+    w.q = w.pr = 0;   // (every lane steps, active or not: its indices stay in the ring)
     uint32_t d0 = 0;
     if (act) {
       p = pos_of(p);
@@ -884,7 +885,10 @@ __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
         }
         continue;
       }
-      const bool fin = act && (w.done || ring_step(w, R, cfg));
+      // every lane takes the step (no branch round it, no state merges): an inactive lane's
+      // walk is never read, and a done lane's result is 0 whatever its walk holds
+      const bool stepped = ring_step(w, R, cfg, act && !w.done);
+      const bool fin = act && (w.done || stepped);
       if (fin) {
         uint32_t full, quarter;
         ring_result(w, cfg, d0, &full, &quarter);
