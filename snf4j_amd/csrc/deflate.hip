@@ -199,7 +199,10 @@ __device__ inline uint32_t load_u32u(const uint8_t* p) {
 // sixteen atomics go out back to back, nothing waiting on another's return; its stream words
 // are loaded first and its links stored last (a store before a load would hold the load,
 // loads and stores sharing vmcnt).
-constexpr int LINK_BATCH = 8;
+#ifndef WSG_LINK_BATCH
+#define WSG_LINK_BATCH 8
+#endif
+constexpr int LINK_BATCH = WSG_LINK_BATCH;   // (build override for A/B)
 
 // the lanes of a group whose hash an earlier lane of the group has (r >= g): predecessor =
 // the nearest such lane below (positions are g + lane)
@@ -219,7 +222,10 @@ __device__ __noinline__ int32_t link_repeats(uint32_t h, bool part, int32_t g, i
 // All the workgroup's waves (LINK_WAVES), batch b of a round to wave b: the waves load and
 // hash their batches together, issue their atomics in turn (a barrier after each wave's
 // turn, so batch order is position order), then resolve repeats and store together.
-constexpr int LINK_WAVES = 16;
+#ifndef WSG_LINK_WAVES
+#define WSG_LINK_WAVES 16
+#endif
+constexpr int LINK_WAVES = WSG_LINK_WAVES;
 __device__ void link_pass(int32_t* hpos, const uint8_t* S, uint16_t* link, uint16_t* prev, int32_t p_begin,
                           int32_t p_last, int32_t nil_pos, bool persist, int32_t base_final) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -1110,7 +1116,10 @@ struct ByteWin {
     return (uint32_t)(((o < 8 ? r->blo : r->bhi) >> (8 * (o & 7))) & 0xff);
   }
 };
-constexpr uint32_t SYM_RING = 32;
+#ifndef WSG_SYM_RING
+#define WSG_SYM_RING 32
+#endif
+constexpr uint32_t SYM_RING = WSG_SYM_RING;
 struct SymStage {
   uint32_t* ring;   // LDS: word j of this lane at ring[j * 64]
   uint32_t* dst;    // the frame's symbol region
@@ -1427,7 +1436,10 @@ __device__ uint32_t send_tree_wave(uint32_t* hb, uint32_t pos, const uint32_t* t
 // workgroup per frame: the bits of its blocks (stored copies, static or dynamic codes: the
 // trees by thread 0, the symbols by every thread at offsets from a block-wide scan) and the
 // sync marker, into the frame's zeroed output slot
-constexpr int EMIT_T = 256;
+#ifndef WSG_EMIT_T
+#define WSG_EMIT_T 256
+#endif
+constexpr int EMIT_T = WSG_EMIT_T;
 constexpr uint32_t EMIT_SYM = 4096;
 constexpr uint32_t EMIT_OUT_W = 2048;   // 8 KiB
 constexpr uint32_t EMIT_HDR_W = 80;   // 31 + 17 + 57 + 7 x (286 + 30) bits at most
@@ -1747,7 +1759,10 @@ void launch_defl_match_lds(const DeflArgs& a, hipStream_t s) {
   hipLaunchKernelGGL(k_defl_match_lds, dim3(a.n_sessions), dim3(1024), 0, s, a);
 }
 void launch_defl_parse(const DeflArgs& a, hipStream_t s) {
-  hipLaunchKernelGGL(k_defl_parse, dim3((a.n_lanes + 63) / 64), dim3(64), 0, s, a);
+#ifndef WSG_PARSE_T
+#define WSG_PARSE_T 64   // (A/B: 32 = half-full waves, twice as many)
+#endif
+  hipLaunchKernelGGL(k_defl_parse, dim3((a.n_lanes + WSG_PARSE_T - 1) / WSG_PARSE_T), dim3(WSG_PARSE_T), 0, s, a);
 }
 void launch_defl_hist(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
   hipLaunchKernelGGL(k_defl_hist, dim3((uint32_t)(n_blocks < 262144 ? (n_blocks ? n_blocks : 1) : 262144)), dim3(256), 0,
