@@ -1240,14 +1240,25 @@ __global__ __launch_bounds__(256) void k_defl_hist(DeflArgs a) {
 // lane per block, the block's TreeWork in LDS (TREE_LANES a workgroup, as many as the LDS
 // holds: 48 of 3.2 KiB since the heap keys share their storage with the node order): the three Huffman
 // trees exactly as zlib's heap builds them, the block type and its size
+// The lanes are spread over TREE_WAVES waves (TREE_LANES / TREE_WAVES a wave).  Not much
+// rides on it: 1, 2, 3, 4 waves ran 2.90, 2.88, 3.12, 3.06 ms (same box, 3 rounds,
+// profiles/r06/r06zb_ab_tree_waves.txt) — the 48 lanes' LDS heap traffic, not one SIMD's
+// issue, bounds the kernel.
+#ifndef WSG_TREE_WAVES
+#define WSG_TREE_WAVES 2
+#endif
 constexpr uint32_t TREE_LANES = 48;
+constexpr uint32_t TREE_WAVES = WSG_TREE_WAVES, TREE_PER_WAVE = TREE_LANES / TREE_WAVES;
+static_assert(TREE_LANES % TREE_WAVES == 0 && TREE_PER_WAVE <= 64, "whole tree lanes a wave");
 static_assert(TREE_LANES * sizeof(zd::TreeWork) <= 160 * 1024, "the tree lanes' work fits the LDS");
-__global__ __launch_bounds__(TREE_LANES) void k_defl_trees(DeflArgs a) {
+__global__ __launch_bounds__(64 * TREE_WAVES) void k_defl_trees(DeflArgs a) {
   __shared__ zd::TreeWork tws[TREE_LANES];
   Sums sm(a);
   const uint64_t total = sm.B[a.n_sessions];
-  zd::TreeWork* t = &tws[threadIdx.x];
-  for (uint64_t i = (uint64_t)blockIdx.x * TREE_LANES + threadIdx.x; i < total; i += (uint64_t)gridDim.x * TREE_LANES) {
+  const uint32_t lane = threadIdx.x & 63, slot = (threadIdx.x >> 6) * TREE_PER_WAVE + lane;
+  if (lane >= TREE_PER_WAVE) return;
+  zd::TreeWork* t = &tws[slot];
+  for (uint64_t i = (uint64_t)blockIdx.x * TREE_LANES + slot; i < total; i += (uint64_t)gridDim.x * TREE_LANES) {
     DeflBlock* b = a.blocks + i;
     const uint32_t nsym = b->nsym;
     if (nsym == 0) continue;
@@ -1770,7 +1781,7 @@ void launch_defl_hist(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
 }
 void launch_defl_trees(const DeflArgs& a, hipStream_t s, uint64_t n_blocks) {
   uint64_t g = (n_blocks + TREE_LANES - 1) / TREE_LANES;
-  hipLaunchKernelGGL(k_defl_trees, dim3((uint32_t)(g < 65536 ? (g ? g : 1) : 65536)), dim3(TREE_LANES), 0, s, a);
+  hipLaunchKernelGGL(k_defl_trees, dim3((uint32_t)(g < 65536 ? (g ? g : 1) : 65536)), dim3(64 * TREE_WAVES), 0, s, a);
 }
 void launch_defl_emit(const DeflArgs& a, hipStream_t s) {
   uint64_t g = a.n_frames < 262144 ? a.n_frames : 262144;
