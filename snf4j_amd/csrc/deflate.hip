@@ -697,8 +697,6 @@ struct LdsRing {
   uint32_t bytes[(DEFL_RING + RING_MIRROR) / 4];   // position x at byte x % DEFL_RING
   uint16_t link[DEFL_RING];
   uint32_t next;                           // the run's position dispenser
-  uint32_t nfr;                            // frames of the run with a fast range
-  uint32_t fr_lo[8], fr_pre[9];            // their first fast position, prefix of fast-range lengths
 };
 static_assert(sizeof(LdsRing) <= 160 * 1024, "the ring fits the LDS");
 
@@ -839,9 +837,6 @@ __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
                 [&](uint32_t x, uint32_t v) { R.link[x % DEFL_RING] = (uint16_t)v; });
     if (tid == 0) {
       R.next = 0;
-      R.nfr = nfr;
-      for (uint32_t i = 0; i < nfr; i++) R.fr_lo[i] = lo8[i];
-      for (uint32_t i = 0; i <= nfr; i++) R.fr_pre[i] = pre8[i];
     }
     lo_loaded = need_lo;
     hi_loaded = run_end;
@@ -849,10 +844,17 @@ __global__ __launch_bounds__(1024) void k_defl_match_lds(DeflArgs a) {
     __syncthreads();
     const uint32_t total = pre8[nfr];
     if (total == 0) continue;
+    // (the run's frames from the registers every thread computed: a select a frame, no
+    // dependent LDS reads when a lane takes its next position)
     auto pos_of = [&](uint32_t v) -> uint32_t {
-      uint32_t j = 0;
-      while (j + 1 < nfr && R.fr_pre[j + 1] <= v) j++;
-      return R.fr_lo[j] + (v - R.fr_pre[j]);
+      uint32_t lo = lo8[0], pre = 0;
+#pragma unroll
+      for (uint32_t j = 1; j < 8; j++) {
+        const bool c = j < nfr && pre8[j] <= v;
+        lo = c ? lo8[j] : lo;
+        pre = c ? pre8[j] : pre;
+      }
+      return lo + (v - pre);
     };
     // the wave's range of virtual indices [next, cend), 256 at a time from the dispenser
     auto grab = [&](uint32_t& nx, uint32_t& ce) {
