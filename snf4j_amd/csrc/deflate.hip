@@ -1119,7 +1119,7 @@ struct ByteWin {
   }
 };
 #ifndef WSG_SYM_RING
-#define WSG_SYM_RING 32
+#define WSG_SYM_RING 64
 #endif
 constexpr uint32_t SYM_RING = WSG_SYM_RING;
 struct SymStage {
